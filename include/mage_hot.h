@@ -1,0 +1,208 @@
+/*
+ * mage_hot.h — C-ABI of the MI355X-native MAGE-SLAM hot path.
+ *
+ * This is the drop-in boundary described in SURVEY.md §8(b).  Every entry point takes
+ * plain pointers and sizes (no torch, OpenCV, Eigen or g2o types) and replaces one
+ * reference interface, cited per function.  Reference paths are relative to the
+ * marwie/mageslam tree; `Core/.../Source` = `Core/MAGESLAM/Source`.
+ *
+ * Status codes replace the reference's CV_Assert / assert failures; the C++ facades
+ * (include/mage/mage.hpp) turn them back into exceptions so callers keep the reference
+ * behaviour.
+ */
+#ifndef MAGE_HOT_H
+#define MAGE_HOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum mage_status {
+    MAGE_OK = 0,
+    MAGE_EINVAL = 1,        /* bad argument (reference: CV_Assert / assert) */
+    MAGE_EDEVICE = 2,       /* HIP runtime error or no usable gfx950 device */
+    MAGE_ENOMEM = 3,        /* device allocation failed */
+    MAGE_EUNSUPPORTED = 4,  /* valid reference input this build does not handle yet */
+    MAGE_ECAPACITY = 5      /* output capacity too small (outputs are truncated) */
+} mage_status;
+
+/* Layout-identical to cv::KeyPoint {Point2f pt; float size, angle, response; int octave, class_id}
+ * as stored in ImageData (Core/.../Source/Image/ImageData.h:186-205). 28 bytes. */
+typedef struct mage_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} mage_keypoint;
+
+/* Layout-identical to cv::DMatch {int queryIdx, trainIdx, imgIdx; float distance}. 16 bytes. */
+typedef struct mage_dmatch {
+    int32_t query_idx, train_idx, img_idx;
+    float distance;
+} mage_dmatch;
+
+/* The 14 constructor scalars of OrbDetector (Core/.../Source/Image/OpenCVModified.h:68-82),
+ * same order and meaning; defaults in FeatureExtractorSettings (MageSettings.h:151-167). */
+typedef struct mage_orb_settings {
+    uint32_t gaussian_kernel_size; /* 7 */
+    uint32_t nfeatures;            /* 440 (2000 in the 720p benchmark) */
+    float scale_factor;            /* 1.5 */
+    uint32_t nlevels;              /* 1 */
+    uint32_t patch_size;           /* 15 */
+    uint32_t fast_threshold;       /* 4 */
+    int32_t use_orientation;       /* 0 */
+    float feature_factor;          /* 1.5 (ANMS) */
+    float feature_strength;        /* 0.9 (ANMS) */
+    int32_t strong_response;       /* 20 (ANMS) */
+    float min_robust_factor;       /* 1.1 */
+    float max_robust_factor;       /* 2.0 */
+    int32_t num_cells_x;           /* 32 */
+    int32_t num_cells_y;           /* 32 */
+} mage_orb_settings;
+
+typedef void* mage_stream; /* a hipStream_t; NULL = the default stream */
+
+/* ------------------------------------------------------------------------------------------ */
+/* Library                                                                                      */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Version string and the gfx target the device code was compiled for ("gfx950"). */
+const char* mage_version(void);
+/* Last error message of the calling thread (empty string if none). */
+const char* mage_last_error(void);
+
+/* ------------------------------------------------------------------------------------------ */
+/* ORB extraction — replaces OrbDetector (Core/.../Source/Image/OpenCVModified.h:64-173)        */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct mage_orb mage_orb;
+
+/* OrbDetector::OrbDetector (OpenCVModified.cpp:362-393).  Also binds the HIP device. */
+mage_status mage_orb_create(const mage_orb_settings* settings, int device, mage_orb** out);
+mage_status mage_orb_destroy(mage_orb* orb);
+
+/* OrbDetector::DetectAndCompute (OpenCVModified.cpp:771-886) on one 8-bit gray frame in host
+ * memory; synchronous.  Writes up to `cap` keypoints (the ImageData capacity,
+ * ImageData.h:65-70 truncates silently) and cap*32 descriptor bytes; *n = count.
+ * Keypoint order is the canonical order of DESIGN.md §ORB (ANMS rank, else raster). */
+mage_status mage_orb_detect_and_compute(mage_orb* orb, const uint8_t* img, int32_t width,
+                                        int32_t height, int32_t stride, mage_keypoint* kp,
+                                        uint8_t* desc, uint32_t cap, uint32_t* n);
+
+/* Batched, device-resident form: `batch` frames at d_frames + f*frame_pitch (device memory),
+ * outputs at d_kp + f*cap, d_desc + f*cap*32, d_n[f].  Asynchronous on `stream`. */
+mage_status mage_orb_detect_and_compute_batch_device(mage_orb* orb, const uint8_t* d_frames,
+                                                     uint32_t batch, int32_t width,
+                                                     int32_t height, int32_t stride,
+                                                     int64_t frame_pitch, mage_keypoint* d_kp,
+                                                     uint8_t* d_desc, uint32_t cap,
+                                                     uint32_t* d_n, mage_stream stream);
+
+/* Sticky device-side status of the batched path (capacity overflow etc.): synchronises
+ * `stream` and returns MAGE_OK, MAGE_ECAPACITY or MAGE_EUNSUPPORTED; reset clears it. */
+mage_status mage_orb_status(mage_orb* orb, mage_stream stream);
+mage_status mage_orb_reset_status(mage_orb* orb, mage_stream stream);
+
+/* Benchmark/test input generator: writes frames t0..t0+count-1 of the seeded
+ * panning texture sequence, each width*height bytes at d_out + i*frame_pitch.  Identical to
+ * mageslam_amd/synth.py frame(). */
+mage_status mage_synth_frames_device(uint8_t* d_out, uint32_t count, int32_t width,
+                                     int32_t height, int64_t frame_pitch, uint32_t t0,
+                                     uint64_t seed, mage_stream stream);
+
+/* FAST-9/16 score map of FAST_t<16> with NMS disabled-equivalent view: score[y*W+x] =
+ * cornerScore if (x,y) passes the segment test, else 0 (OpenCVModified.cpp:1225-1512,
+ * 927-1071).  Host buffers, synchronous.  Used for the VERIFY_SIMD-style parity check. */
+mage_status mage_orb_fast_score_map(const uint8_t* img, int32_t width, int32_t height,
+                                    int32_t stride, int32_t threshold, uint8_t* score_map,
+                                    int device);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Hamming matching — replaces FeatureMatcher (Core/.../Source/Tracking/FeatureMatcher.h)        */
+/* ------------------------------------------------------------------------------------------ */
+
+/* GetDescriptorDistance (FeatureMatcher.cpp:453-504): popcount(a ^ b) over 32 bytes. */
+int32_t mage_hamming_distance(const uint8_t* a32, const uint8_t* b32);
+
+/* Match (FeatureMatcher.cpp:61-190): masked two-way brute force with the ratio-delta test.
+ * Masks may be NULL (= all true).  Host buffers, synchronous.  Output in ascending A index. */
+mage_status mage_hamming_match(const uint8_t* desc_a, uint32_t n_a, const uint8_t* mask_a,
+                               const uint8_t* desc_b, uint32_t n_b, const uint8_t* mask_b,
+                               int32_t max_distance, int32_t min_difference, mage_dmatch* out,
+                               uint32_t cap, uint32_t* n);
+
+/* Batched device form: pair p matches A = d_desc_a + p*a_pitch (n_a[p] rows) against
+ * B = d_desc_b + p*b_pitch (n_b[p] rows); no masks.  Results per pair at d_out + p*cap,
+ * count in d_n[p].  d_n_a / d_n_b are device arrays.  Asynchronous on `stream`. */
+mage_status mage_hamming_match_batch_device(const uint8_t* d_desc_a, int64_t a_pitch,
+                                            const uint32_t* d_n_a, const uint8_t* d_desc_b,
+                                            int64_t b_pitch, const uint32_t* d_n_b,
+                                            uint32_t pairs, int32_t max_distance,
+                                            int32_t min_difference, mage_dmatch* d_out,
+                                            uint32_t cap, uint32_t* d_n, mage_stream stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Local bundle adjustment — replaces BundlerLib (Dependencies/BundlerLib/Include/BundlerLib.h) */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct mage_ba mage_ba;
+
+/* BundlerLib::BundlerLib(BundlerParameters{ArePointsFixed}) (BundlerLib.cpp:184-196). */
+mage_status mage_ba_create(int32_t points_fixed, int device, mage_ba** out);
+mage_status mage_ba_destroy(mage_ba* ba);
+
+/* AllocateCameras + SetCameraPose for all cameras (BundlerLib.cpp:198-207, 261-278).
+ * pos3: view-space position t (3 floats/camera); R9: rotation, Eigen column-major
+ * (9 floats/camera); intr4: {cx, cy, fx, fy}; fixed: 0/1.  Only fx is used as the focal
+ * length, as in the reference (CameraParameters(intr[2], (intr[0], intr[1]), 0)). */
+mage_status mage_ba_set_cameras(mage_ba* ba, uint32_t n, const float* pos3, const float* r9,
+                                const float* intr4, const uint8_t* fixed);
+/* FixCameraPose (BundlerLib.cpp:280-283). */
+mage_status mage_ba_fix_camera(mage_ba* ba, uint32_t idx, int32_t fixed);
+/* AllocateMapPoints + SetMapPoint (BundlerLib.cpp:209-217, 285-292). */
+mage_status mage_ba_set_points(mage_ba* ba, uint32_t n, const float* xyz);
+/* AllocateObservations + SetObservation (BundlerLib.cpp:219-229, 294-309). */
+mage_status mage_ba_set_observations(mage_ba* ba, uint32_t n, const float* uv,
+                                     const uint32_t* cam, const uint32_t* pt,
+                                     const float* info);
+/* SetCurrentLambda / GetCurrentLambda (BundlerLib.cpp:354-362). */
+mage_status mage_ba_set_lambda(mage_ba* ba, float lambda);
+mage_status mage_ba_get_lambda(mage_ba* ba, float* lambda);
+/* Tether constraints (SetFixedDistance/RelativeRotation/RelativeTransformConstraint,
+ * BundlerLib.cpp:311-350).  Not implemented yet: returns MAGE_EUNSUPPORTED. */
+mage_status mage_ba_set_tethers(mage_ba* ba, uint32_t kind, uint32_t n, const uint32_t* cam1,
+                                const uint32_t* cam2, const float* params, const float* weight);
+
+/* StepBundleAdjustment (BundlerLib.cpp:364-447): one LM iteration per entry of huber[],
+ * stopping early if an iteration fails; then the outlier / cheirality pass.  Outlier
+ * observation indices are appended in ascending order (g2o active-edge order) to
+ * outliers[0..cap); *n_out = number reported.  *mean_sq = Σ‖e‖²/count over kept edges
+ * (NaN if none, as the reference's 0/0). */
+mage_status mage_ba_step(mage_ba* ba, const float* huber, uint32_t nsteps,
+                         float max_error_square, uint32_t* outliers, uint32_t cap,
+                         uint32_t* n_out, float* mean_sq);
+
+/* GetPose / GetPoint (BundlerLib.cpp:457-471), all at once. */
+mage_status mage_ba_get_poses(mage_ba* ba, float* pos3, float* r9);
+mage_status mage_ba_get_points(mage_ba* ba, float* xyz);
+
+/* The fp64 estimate itself: qt7 = {qx, qy, qz, qw, tx, ty, tz} per camera, xyz per point
+ * (either may be NULL).  Used by the parity tests; the reference exposes only the float casts. */
+mage_status mage_ba_get_state_f64(mage_ba* ba, double* qt7, double* xyz);
+
+/* Instrumentation: counters since creation. */
+typedef struct mage_ba_stats {
+    uint64_t iterations;      /* LM solve() calls */
+    uint64_t trials;          /* LM inner trials (linear solves) */
+    uint64_t rejected_trials; /* trials that popped the state */
+    double last_chi2;         /* robust chi2 after the last iteration */
+    double lambda;            /* current LM lambda */
+} mage_ba_stats;
+mage_status mage_ba_get_stats(mage_ba* ba, mage_ba_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MAGE_HOT_H */

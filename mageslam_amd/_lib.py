@@ -1,0 +1,133 @@
+"""ctypes binding of libmage_hot.so (the C-ABI in include/mage_hot.h).
+
+The product path has no CPU fallback: if the HIP library is missing this module raises at
+import, and every call that needs a GPU fails with MageError(MAGE_EDEVICE).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libmage_hot.so"
+
+MAGE_OK, MAGE_EINVAL, MAGE_EDEVICE, MAGE_ENOMEM, MAGE_EUNSUPPORTED, MAGE_ECAPACITY = range(6)
+STATUS_NAMES = {0: "MAGE_OK", 1: "MAGE_EINVAL", 2: "MAGE_EDEVICE", 3: "MAGE_ENOMEM",
+                4: "MAGE_EUNSUPPORTED", 5: "MAGE_ECAPACITY"}
+
+# Every entry point declared in include/mage_hot.h (checked by tests/test_capi.py).
+EXPORTS = [
+    "mage_version", "mage_last_error",
+    "mage_orb_create", "mage_orb_destroy", "mage_orb_detect_and_compute",
+    "mage_orb_detect_and_compute_batch_device", "mage_orb_status", "mage_orb_reset_status",
+    "mage_synth_frames_device", "mage_orb_fast_score_map",
+    "mage_hamming_distance", "mage_hamming_match", "mage_hamming_match_batch_device",
+    "mage_ba_create", "mage_ba_destroy", "mage_ba_set_cameras", "mage_ba_fix_camera",
+    "mage_ba_set_points", "mage_ba_set_observations", "mage_ba_set_lambda", "mage_ba_get_lambda",
+    "mage_ba_set_tethers", "mage_ba_step", "mage_ba_get_poses", "mage_ba_get_points",
+    "mage_ba_get_stats", "mage_ba_get_state_f64",
+]
+
+
+class MageError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class KeyPoint(C.Structure):
+    """cv::KeyPoint layout (28 B)."""
+
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+class OrbSettingsC(C.Structure):
+    _fields_ = [("gaussian_kernel_size", C.c_uint32), ("nfeatures", C.c_uint32),
+                ("scale_factor", C.c_float), ("nlevels", C.c_uint32), ("patch_size", C.c_uint32),
+                ("fast_threshold", C.c_uint32), ("use_orientation", C.c_int32),
+                ("feature_factor", C.c_float), ("feature_strength", C.c_float),
+                ("strong_response", C.c_int32), ("min_robust_factor", C.c_float),
+                ("max_robust_factor", C.c_float), ("num_cells_x", C.c_int32),
+                ("num_cells_y", C.c_int32)]
+
+
+class BAStats(C.Structure):
+    _fields_ = [("iterations", C.c_uint64), ("trials", C.c_uint64), ("rejected_trials", C.c_uint64),
+                ("last_chi2", C.c_double), ("lambda_", C.c_double)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+DM_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", "<i4"),
+                     ("distance", "<f4")])
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libmage_hot.so (raises ImportError if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python -m mageslam_amd.build`")
+        lib = C.CDLL(str(LIB_PATH))
+        _declare(lib)
+        _lib = lib
+    return _lib
+
+
+def ptr(a):
+    """Host pointer of a numpy array, or raw device pointer of a torch tensor / int."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return C.c_void_p(a)
+    if hasattr(a, "data_ptr"):
+        return C.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def check(status: int) -> None:
+    if status != MAGE_OK:
+        msg = load().mage_last_error().decode(errors="replace")
+        raise MageError(status, msg)
+
+
+def _declare(L: C.CDLL) -> None:
+    vp, i32, u32, f32, i64, u64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_float, C.c_int64, C.c_uint64
+    st = C.c_int
+
+    def sig(name, res, *args):
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = list(args)
+
+    sig("mage_version", C.c_char_p)
+    sig("mage_last_error", C.c_char_p)
+    sig("mage_orb_create", st, vp, C.c_int, C.POINTER(vp))
+    sig("mage_orb_destroy", st, vp)
+    sig("mage_orb_detect_and_compute", st, vp, vp, i32, i32, i32, vp, vp, u32, C.POINTER(u32))
+    sig("mage_orb_detect_and_compute_batch_device", st, vp, vp, u32, i32, i32, i32, i64, vp, vp, u32, vp, vp)
+    sig("mage_orb_status", st, vp, vp)
+    sig("mage_orb_reset_status", st, vp, vp)
+    sig("mage_synth_frames_device", st, vp, u32, i32, i32, i64, u32, u64, vp)
+    sig("mage_orb_fast_score_map", st, vp, i32, i32, i32, i32, vp, C.c_int)
+    sig("mage_hamming_distance", i32, vp, vp)
+    sig("mage_hamming_match", st, vp, u32, vp, vp, u32, vp, i32, i32, vp, u32, C.POINTER(u32))
+    sig("mage_hamming_match_batch_device", st, vp, i64, vp, vp, i64, vp, u32, i32, i32, vp, u32, vp, vp)
+    sig("mage_ba_create", st, i32, C.c_int, C.POINTER(vp))
+    sig("mage_ba_destroy", st, vp)
+    sig("mage_ba_set_cameras", st, vp, u32, vp, vp, vp, vp)
+    sig("mage_ba_fix_camera", st, vp, u32, i32)
+    sig("mage_ba_set_points", st, vp, u32, vp)
+    sig("mage_ba_set_observations", st, vp, u32, vp, vp, vp, vp)
+    sig("mage_ba_set_lambda", st, vp, f32)
+    sig("mage_ba_get_lambda", st, vp, C.POINTER(f32))
+    sig("mage_ba_set_tethers", st, vp, u32, u32, vp, vp, vp, vp)
+    sig("mage_ba_step", st, vp, vp, u32, f32, vp, u32, C.POINTER(u32), C.POINTER(f32))
+    sig("mage_ba_get_poses", st, vp, vp, vp)
+    sig("mage_ba_get_points", st, vp, vp)
+    sig("mage_ba_get_state_f64", st, vp, vp, vp)
+    sig("mage_ba_get_stats", st, vp, C.POINTER(BAStats))

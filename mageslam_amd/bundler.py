@@ -1,0 +1,185 @@
+"""BundlerLib — host mirror of the reference bundle adjuster interface.
+
+Mirrors `class BundlerLib` (Dependencies/BundlerLib/Include/BundlerLib.h:20-66) method for
+method; the Eigen::Map arguments become numpy arrays (orientation is the logical 3x3 matrix;
+the column-major Eigen layout is produced here).  Setters buffer on the host and the problem
+is handed to libmage_hot.so (gfx950) at the first StepBundleAdjustment.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import BAStats, check, ptr
+
+
+@dataclass
+class BundlerParameters:
+    ArePointsFixed: bool = False
+
+
+class BundlerLib:
+    def __init__(self, params: BundlerParameters | None = None, device: int = 0):
+        self.params = params or BundlerParameters()
+        self._h = C.c_void_p()
+        check(_lib.load().mage_ba_create(int(self.params.ArePointsFixed), device, C.byref(self._h)))
+        self._cams = None
+        self._pts = None
+        self._obs = None
+        self._uploaded = {"cams": False, "pts": False, "obs": False}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.load().mage_ba_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- allocation / setters (BundlerLib.cpp:198-309) ---
+    def AllocateCameras(self, count: int) -> None:
+        if self._cams is not None:
+            raise RuntimeError("can only allocate once")
+        self._cams = dict(pos=np.zeros((count, 3), np.float32), r9=np.zeros((count, 9), np.float32),
+                          intr=np.zeros((count, 4), np.float32), fixed=np.zeros(count, np.uint8))
+
+    def SetCameraPose(self, idx: int, position, orientation, intrinsics, isFixed: bool) -> None:
+        c = self._cams
+        c["pos"][idx] = np.asarray(position, np.float32).reshape(3)
+        c["r9"][idx] = np.asarray(orientation, np.float32).reshape(3, 3).T.reshape(9)  # column-major
+        c["intr"][idx] = np.asarray(intrinsics, np.float32).reshape(4)
+        c["fixed"][idx] = 1 if isFixed else 0
+        self._uploaded["cams"] = False
+
+    def FixCameraPose(self, idx: int, value: bool) -> None:
+        self._cams["fixed"][idx] = 1 if value else 0
+        if self._uploaded["cams"]:
+            check(_lib.load().mage_ba_fix_camera(self._h, idx, int(value)))
+
+    def AllocateMapPoints(self, count: int) -> None:
+        self._pts = np.zeros((count, 3), np.float32)
+        self._uploaded["pts"] = False
+
+    def SetMapPoint(self, idx: int, point) -> None:
+        self._pts[idx] = np.asarray(point, np.float32).reshape(3)
+        self._uploaded["pts"] = False
+
+    def AllocateObservations(self, count: int) -> None:
+        self._obs = dict(uv=np.zeros((count, 2), np.float32), cam=np.zeros(count, np.uint32),
+                         pt=np.zeros(count, np.uint32), info=np.zeros(count, np.float32))
+        self._uploaded["obs"] = False
+
+    def SetObservation(self, idx: int, position, cameraIndex: int, mapPointIndex: int,
+                       informationMatrixScalar: float) -> None:
+        o = self._obs
+        o["uv"][idx] = np.asarray(position, np.float32).reshape(2)
+        o["cam"][idx] = cameraIndex
+        o["pt"][idx] = mapPointIndex
+        o["info"][idx] = informationMatrixScalar
+        self._uploaded["obs"] = False
+
+    def set_graph(self, g) -> None:
+        """Bulk form of the setters for a synth.BAGraph-like object."""
+        n = len(g.pos)
+        self._cams = dict(pos=np.ascontiguousarray(g.pos, np.float32), r9=g.rot_colmajor.astype(np.float32),
+                          intr=np.ascontiguousarray(g.intr, np.float32),
+                          fixed=np.ascontiguousarray(g.fixed, np.uint8))
+        assert len(self._cams["r9"]) == n
+        self._pts = np.ascontiguousarray(g.points, np.float32)
+        self._obs = dict(uv=np.ascontiguousarray(g.uv, np.float32), cam=np.ascontiguousarray(g.cam, np.uint32),
+                         pt=np.ascontiguousarray(g.pt, np.uint32), info=np.ascontiguousarray(g.info, np.float32))
+        self._uploaded = {"cams": False, "pts": False, "obs": False}
+
+    def AllocateFixedDistanceConstraints(self, count: int) -> None:
+        if count:
+            raise NotImplementedError("tether constraints are not implemented in this build")
+
+    AllocateRelativeRotationConstraints = AllocateFixedDistanceConstraints
+    AllocateRelativeTransformConstraints = AllocateFixedDistanceConstraints
+
+    def SetCurrentLambda(self, userLambda: float) -> None:
+        check(_lib.load().mage_ba_set_lambda(self._h, float(userLambda)))
+
+    def GetCurrentLambda(self) -> float:
+        v = C.c_float()
+        check(_lib.load().mage_ba_get_lambda(self._h, C.byref(v)))
+        return float(v.value)
+
+    def _upload(self) -> None:
+        L = _lib.load()
+        if not self._uploaded["cams"] and self._cams is not None:
+            c = self._cams
+            check(L.mage_ba_set_cameras(self._h, len(c["pos"]), ptr(c["pos"]), ptr(c["r9"]), ptr(c["intr"]),
+                                        ptr(c["fixed"])))
+            self._uploaded["cams"] = True
+        if not self._uploaded["pts"] and self._pts is not None:
+            check(L.mage_ba_set_points(self._h, len(self._pts), ptr(self._pts)))
+            self._uploaded["pts"] = True
+        if not self._uploaded["obs"] and self._obs is not None:
+            o = self._obs
+            check(L.mage_ba_set_observations(self._h, len(o["cam"]), ptr(o["uv"]), ptr(o["cam"]), ptr(o["pt"]),
+                                             ptr(o["info"])))
+            self._uploaded["obs"] = True
+
+    def StepBundleAdjustment(self, huberWidthPerIteration, maxErrorSquare: float, outliers: list | None = None) -> float:
+        """BundlerLib::StepBundleAdjustment (BundlerLib.cpp:364-447): returns the mean squared
+        error of the kept edges and appends outlier observation indices to `outliers`."""
+        self._upload()
+        hw = np.ascontiguousarray(np.asarray(huberWidthPerIteration, np.float32).reshape(-1))
+        cap = max(len(self._obs["cam"]) if self._obs is not None else 0, 1)
+        out = np.zeros(cap, np.uint32)
+        n = C.c_uint32(0)
+        ms = C.c_float(0)
+        check(_lib.load().mage_ba_step(self._h, ptr(hw), len(hw), float(maxErrorSquare), ptr(out), cap,
+                                       C.byref(n), C.byref(ms)))
+        if outliers is not None:
+            outliers.extend(int(v) for v in out[: n.value])
+        return float(ms.value)
+
+    def step(self, huber_widths, max_error_square):
+        """Convenience form: returns (mean_sq, outliers ndarray)."""
+        outl: list = []
+        ms = self.StepBundleAdjustment(huber_widths, max_error_square, outl)
+        return ms, np.asarray(outl, np.uint32)
+
+    def poses(self):
+        n = len(self._cams["pos"])
+        pos = np.zeros((n, 3), np.float32)
+        r9 = np.zeros((n, 9), np.float32)
+        self._upload()
+        check(_lib.load().mage_ba_get_poses(self._h, ptr(pos), ptr(r9)))
+        return pos, r9
+
+    def points(self):
+        xyz = np.zeros((len(self._pts), 3), np.float32)
+        self._upload()
+        check(_lib.load().mage_ba_get_points(self._h, ptr(xyz)))
+        return xyz
+
+    def state(self):
+        """fp64 state: (C,7) [qx,qy,qz,qw,tx,ty,tz] and (P,3) points."""
+        self._upload()
+        qt = np.zeros((len(self._cams["pos"]), 7), np.float64)
+        xyz = np.zeros((len(self._pts), 3), np.float64)
+        check(_lib.load().mage_ba_get_state_f64(self._h, ptr(qt), ptr(xyz)))
+        return qt, xyz
+
+    def GetPose(self, idx: int):
+        """(position (3,), orientation (3,3)) of camera idx (BundlerLib.cpp:457-465)."""
+        pos, r9 = self.poses()
+        return pos[idx], r9[idx].reshape(3, 3).T
+
+    def GetPoint(self, idx: int):
+        return self.points()[idx]
+
+    def stats(self) -> dict:
+        s = BAStats()
+        check(_lib.load().mage_ba_get_stats(self._h, C.byref(s)))
+        return dict(iterations=s.iterations, trials=s.trials, rejected=s.rejected_trials, chi2=s.last_chi2,
+                    lambda_=s.lambda_)

@@ -1,0 +1,1336 @@
+// ba.hip — local bundle adjustment on MI355X (gfx950).  Replaces BundlerLib
+// (Dependencies/BundlerLib/Source/BundlerLib.cpp) and the g2o machinery it drives
+// (OptimizationAlgorithmLevenberg + BlockSolver_6_3 Schur + LinearSolverDense +
+// EdgeProjectXYZ2UV / VertexSE3Expmap / VertexSBAPointXYZ / RobustKernelHuber), in fp64.
+//
+// Device-resident problem, CSR by point and by camera (active edges, insertion order).
+// One LM iteration (g2o solve(iteration)) =
+//   point_linearize   thread/point: errors of all its edges (kept per edge, as g2o keeps
+//                     _error), robust chi2, Hll, bl, Hpl_e = J_pose^T w J_point per edge
+//   cam_linearize     workgroup/camera: Hpp, bp (recomputes J_pose; no per-edge 6x6 in HBM)
+//   reduce            chi2, max diagonal (lambda init)
+//   trial loop (<= 10, host decides from one 3-double readback per trial):
+//     point_schur     Dinv = (Hll + lambda I)^-1, db = Dinv bl
+//     build_schur     workgroup/camera row: S_c1,c2 = Hpp + lambda I - sum_p Hpl Dinv Hpl^T in
+//                     LDS (fp64 LDS atomics), rhs = bp - sum Hpl db
+//     cholesky_solve  one workgroup, blocked right-looking Cholesky (16-wide panels, wave-
+//                     register diagonal factor) + blocked triangular solves
+//     point_backsub   xl = Dinv (bl - Hpl^T xp)
+//     update          trial state = exp(xp) * T, p + xl  (double-buffered: pop = no copy)
+//     point_errors    errors + robust chi2 of the trial state
+//     reduce          trial chi2 and g2o computeScale
+// then the outlier / cheirality post-pass of StepBundleAdjustment (BundlerLib.cpp:385-446).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "common.hpp"
+
+namespace mage {
+namespace {
+
+constexpr int BA_THREADS = 256;
+
+// ---------------- SE3Quat / Eigen primitives (device) ----------------
+
+__device__ __forceinline__ void d_cross(const double a[3], const double b[3], double c[3])
+{
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Quaternion * Vector3 (Eigen _transformVector); q = (x, y, z, w)
+__device__ __forceinline__ void d_qrot(const double q[4], const double v[3], double o[3])
+{
+    double uv[3], uv2[3];
+    d_cross(q, v, uv);
+    uv[0] += uv[0];
+    uv[1] += uv[1];
+    uv[2] += uv[2];
+    d_cross(q, uv, uv2);
+    for (int i = 0; i < 3; i++) o[i] = v[i] + q[3] * uv[i] + uv2[i];
+}
+
+__device__ __forceinline__ void d_qmat(const double q[4], double r[9])
+{
+    double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    r[0] = 1 - (tyy + tzz);
+    r[1] = txy - twz;
+    r[2] = txz + twy;
+    r[3] = txy + twz;
+    r[4] = 1 - (txx + tzz);
+    r[5] = tyz - twx;
+    r[6] = txz - twy;
+    r[7] = tyz + twx;
+    r[8] = 1 - (txx + tyy);
+}
+
+__device__ __forceinline__ void d_quat_from_matrix(const double* m, double q[4])
+{
+    double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[7] - m[5]) * t;
+        q[1] = (m[2] - m[6]) * t;
+        q[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 4]) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * t;
+        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
+        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+    }
+}
+
+__device__ __forceinline__ void d_se3_normalize(double q[4])
+{
+    if (q[3] < 0)
+        for (int i = 0; i < 4; i++) q[i] = -q[i];
+    double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; i++) q[i] /= n;
+}
+
+// T <- exp(u) * T  (VertexSE3Expmap::oplusImpl with SE3Quat::exp, g2o se3quat.h)
+__device__ void d_oplus(double q[4], double t[3], const double u[6])
+{
+    const double w0 = u[0], w1 = u[1], w2 = u[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) O2[r * 3 + c] = O[r * 3] * O[c] + O[r * 3 + 1] * O[3 + c] + O[r * 3 + 2] * O[6 + c];
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+        const double c = (theta - sin(theta)) / (theta * theta * theta);
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4 == 0 ? 1.0 : 0.0);
+            R[i] = I + a * O[i] + b * O2[i];
+            V[i] = I + b * O[i] + c * O2[i];
+        }
+    }
+    double eq[4], et[3];
+    d_quat_from_matrix(R, eq);
+    for (int r = 0; r < 3; r++) et[r] = V[r * 3] * u[3] + V[r * 3 + 1] * u[4] + V[r * 3 + 2] * u[5];
+    d_se3_normalize(eq);
+    // result = e * T: t' = e.t + e.q * T.t ; q' = e.q * T.q
+    double rt[3];
+    d_qrot(eq, t, rt);
+    double nq[4];
+    nq[3] = eq[3] * q[3] - eq[0] * q[0] - eq[1] * q[1] - eq[2] * q[2];
+    nq[0] = eq[3] * q[0] + eq[0] * q[3] + eq[1] * q[2] - eq[2] * q[1];
+    nq[1] = eq[3] * q[1] + eq[1] * q[3] + eq[2] * q[0] - eq[0] * q[2];
+    nq[2] = eq[3] * q[2] + eq[2] * q[3] + eq[0] * q[1] - eq[1] * q[0];
+    d_se3_normalize(nq);
+    for (int i = 0; i < 4; i++) q[i] = nq[i];
+    for (int i = 0; i < 3; i++) t[i] = et[i] + rt[i];
+}
+
+__device__ __forceinline__ void d_huber(double delta, double e2, double& rho0, double& rho1)
+{
+    const double dsqr = delta * delta;
+    if (e2 <= dsqr) {
+        rho0 = e2;
+        rho1 = 1.0;
+    } else {
+        const double sq = sqrt(e2);
+        rho0 = 2 * sq * delta - dsqr;
+        rho1 = delta / sq;
+    }
+}
+
+struct State {  // one copy of the optimisable state
+    double* q;  // C x 4
+    double* t;  // C x 3
+    double* p;  // P x 3
+};
+
+struct Problem {
+    int C, P;
+    const double* camk;   // C x 3: f, cx, cy
+    const int* camh;      // C: Hessian block index or -1
+    const int* ptfree;    // P: 1 if the point is in the system
+    const double* uv;     // E x 2
+    const int* ecam;      // E
+    const int* ept;       // E
+    const double* info;   // E
+    const int* pstart;    // P+1
+    const int* pedges;    // active edges by point
+    const int* cstart;    // C+1
+    const int* cedges;    // active edges by camera
+    double huber;
+};
+
+// computeError + chi2 + robustify for one edge at state s; returns rho0, writes err, xc
+__device__ __forceinline__ void edge_eval(const Problem& pb, const State& s, int e, double err[2],
+                                          double xc[3], double& rho0, double& rho1)
+{
+    const int c = pb.ecam[e], p = pb.ept[e];
+    const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
+    const double X[3] = {s.p[3 * p], s.p[3 * p + 1], s.p[3 * p + 2]};
+    d_qrot(q, X, xc);
+    xc[0] += s.t[3 * c];
+    xc[1] += s.t[3 * c + 1];
+    xc[2] += s.t[3 * c + 2];
+    const double f = pb.camk[3 * c], cx = pb.camk[3 * c + 1], cy = pb.camk[3 * c + 2];
+    err[0] = pb.uv[2 * e] - (xc[0] / xc[2] * f + cx);
+    err[1] = pb.uv[2 * e + 1] - (xc[1] / xc[2] * f + cy);
+    const double inf = pb.info[e];
+    const double chi2 = inf * (err[0] * err[0] + err[1] * err[1]);
+    d_huber(pb.huber, chi2, rho0, rho1);
+}
+
+// EdgeProjectXYZ2UV::linearizeOplus pose block (2x6, row-major)
+__device__ __forceinline__ void jac_pose(const double xc[3], double f, double Jp[12])
+{
+    const double x = xc[0], y = xc[1], z = xc[2], z2 = z * z;
+    Jp[0] = x * y / z2 * f;
+    Jp[1] = -(1 + (x * x / z2)) * f;
+    Jp[2] = y / z * f;
+    Jp[3] = -1. / z * f;
+    Jp[4] = 0;
+    Jp[5] = x / z2 * f;
+    Jp[6] = (1 + y * y / z2) * f;
+    Jp[7] = -x * y / z2 * f;
+    Jp[8] = -x / z * f;
+    Jp[9] = 0;
+    Jp[10] = -1. / z * f;
+    Jp[11] = y / z2 * f;
+}
+
+// ---------------- kernels ----------------
+
+// Per point: edge errors, robust chi2, Hll, bl, Hpl per edge (BlockSolver::buildSystem with
+// BaseBinaryEdge::constructQuadraticForm, robust first-order weighting).
+__global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State s, int linearize,
+                                                              double* __restrict__ err,
+                                                              double* __restrict__ Hll,
+                                                              double* __restrict__ bl,
+                                                              double* __restrict__ Hpl,
+                                                              double* __restrict__ chi_part,
+                                                              double* __restrict__ maxd_part)
+{
+    const int p = blockIdx.x * BA_THREADS + threadIdx.x;
+    if (p >= pb.P) return;
+    const int free_p = linearize && pb.ptfree[p];
+    double H[6] = {0, 0, 0, 0, 0, 0};  // 00 01 02 11 12 22
+    double g[3] = {0, 0, 0};
+    double chi = 0;
+    const int e0 = pb.pstart[p], e1 = pb.pstart[p + 1];
+    for (int a = e0; a < e1; a++) {
+        const int e = pb.pedges[a];
+        double ev[2], xc[3], rho0, rho1;
+        edge_eval(pb, s, e, ev, xc, rho0, rho1);
+        err[2 * e] = ev[0];
+        err[2 * e + 1] = ev[1];
+        chi += rho0;
+        if (!free_p) continue;
+        const int c = pb.ecam[e];
+        const double f = pb.camk[3 * c];
+        const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
+        double R[9];
+        d_qmat(q, R);
+        const double x = xc[0], y = xc[1], z = xc[2];
+        const double tmp0[3] = {f, 0, -x / z * f}, tmp1[3] = {0, f, -y / z * f};
+        double J[6];
+        for (int k = 0; k < 3; k++) {
+            J[k] = -1. / z * (tmp0[0] * R[k] + tmp0[1] * R[3 + k] + tmp0[2] * R[6 + k]);
+            J[3 + k] = -1. / z * (tmp1[0] * R[k] + tmp1[1] * R[3 + k] + tmp1[2] * R[6 + k]);
+        }
+        const double inf = pb.info[e];
+        const double w = rho1 * inf;
+        const double or0 = -inf * ev[0] * rho1, or1 = -inf * ev[1] * rho1;
+        g[0] += J[0] * or0 + J[3] * or1;
+        g[1] += J[1] * or0 + J[4] * or1;
+        g[2] += J[2] * or0 + J[5] * or1;
+        H[0] += (J[0] * J[0] + J[3] * J[3]) * w;
+        H[1] += (J[0] * J[1] + J[3] * J[4]) * w;
+        H[2] += (J[0] * J[2] + J[3] * J[5]) * w;
+        H[3] += (J[1] * J[1] + J[4] * J[4]) * w;
+        H[4] += (J[1] * J[2] + J[4] * J[5]) * w;
+        H[5] += (J[2] * J[2] + J[5] * J[5]) * w;
+        if (pb.camh[c] >= 0) {
+            double Jp[12];
+            jac_pose(xc, f, Jp);
+            double* o = Hpl + 18 * (long long)e;
+            for (int r = 0; r < 6; r++)
+                for (int k = 0; k < 3; k++) o[r * 3 + k] = (Jp[r] * J[k] + Jp[6 + r] * J[3 + k]) * w;
+        }
+    }
+    chi_part[p] = chi;
+    if (!linearize) return;
+    double* Ho = Hll + 9 * (long long)p;
+    Ho[0] = H[0];
+    Ho[1] = H[1];
+    Ho[2] = H[2];
+    Ho[3] = H[1];
+    Ho[4] = H[3];
+    Ho[5] = H[4];
+    Ho[6] = H[2];
+    Ho[7] = H[4];
+    Ho[8] = H[5];
+    bl[3 * p] = g[0];
+    bl[3 * p + 1] = g[1];
+    bl[3 * p + 2] = g[2];
+    maxd_part[p] = free_p ? fmax(fabs(H[0]), fmax(fabs(H[3]), fabs(H[5]))) : 0.0;
+}
+
+// Per camera: Hpp (6x6) and bp (6) from its active edges; errors come from point_linearize.
+__global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s,
+                                                            const double* __restrict__ err,
+                                                            double* __restrict__ Hpp,
+                                                            double* __restrict__ bp,
+                                                            double* __restrict__ maxd_part)
+{
+    const int c = blockIdx.x;
+    __shared__ double red[BA_THREADS / kWave][27];
+    double acc[27];
+    for (int k = 0; k < 27; k++) acc[k] = 0;
+    const bool inSys = pb.camh[c] >= 0;
+    if (inSys) {
+        const double f = pb.camk[3 * c];
+        for (int a = pb.cstart[c] + threadIdx.x; a < pb.cstart[c + 1]; a += BA_THREADS) {
+            const int e = pb.cedges[a];
+            double ev[2], xc[3], rho0, rho1;
+            edge_eval(pb, s, e, ev, xc, rho0, rho1);
+            double Jp[12];
+            jac_pose(xc, f, Jp);
+            const double inf = pb.info[e];
+            const double w = rho1 * inf;
+            const double e0 = err[2 * e], e1v = err[2 * e + 1];
+            const double or0 = -inf * e0 * rho1, or1 = -inf * e1v * rho1;
+            int k = 0;
+            for (int r = 0; r < 6; r++)
+                for (int cc = r; cc < 6; cc++) acc[k++] += (Jp[r] * Jp[cc] + Jp[6 + r] * Jp[6 + cc]) * w;
+            for (int r = 0; r < 6; r++) acc[21 + r] += Jp[r] * or0 + Jp[6 + r] * or1;
+        }
+    }
+    // block reduction: waves via shuffles, then LDS
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int k = 0; k < 27; k++) {
+        double v = acc[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[wave][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 27) {
+        double v = 0;
+        for (int w = 0; w < BA_THREADS / kWave; w++) v += red[w][threadIdx.x];
+        red[0][threadIdx.x] = v;  // only wave 0 writes row 0 after all reads of row 0 by this thread
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double* H = Hpp + 36 * (long long)c;
+        int k = 0;
+        double md = 0;
+        for (int r = 0; r < 6; r++)
+            for (int cc = r; cc < 6; cc++) {
+                H[r * 6 + cc] = red[0][k];
+                H[cc * 6 + r] = red[0][k];
+                k++;
+            }
+        for (int r = 0; r < 6; r++) {
+            bp[6 * c + r] = red[0][21 + r];
+            md = fmax(md, fabs(H[r * 7]));
+        }
+        maxd_part[c] = inSys ? md : 0.0;
+    }
+}
+
+// Fixed-order reduction of up to three partial arrays into out[0..2] (sum, sum, max).
+__global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, int na,
+                                                const double* __restrict__ b, int nb,
+                                                const double* __restrict__ m, int nm,
+                                                double* __restrict__ out)
+{
+    __shared__ double sa[1024], sb[1024], sm[1024];
+    double va = 0, vb = 0, vm = 0;
+    for (int i = threadIdx.x; i < na; i += 1024) va += a[i];
+    for (int i = threadIdx.x; i < nb; i += 1024) vb += b[i];
+    for (int i = threadIdx.x; i < nm; i += 1024) vm = fmax(vm, m[i]);
+    sa[threadIdx.x] = va;
+    sb[threadIdx.x] = vb;
+    sm[threadIdx.x] = vm;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            sa[threadIdx.x] += sa[threadIdx.x + s];
+            sb[threadIdx.x] += sb[threadIdx.x + s];
+            sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + s]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = sa[0];
+        out[1] = sb[0];
+        out[2] = sm[0];
+    }
+}
+
+// Eigen Matrix3d::inverse (cofactors)
+__device__ __forceinline__ void d_inv3(const double m[9], double o[9])
+{
+    const double c0 = m[4] * m[8] - m[5] * m[7];
+    const double c1 = m[5] * m[6] - m[3] * m[8];
+    const double c2 = m[3] * m[7] - m[4] * m[6];
+    const double det = m[0] * c0 + m[1] * c1 + m[2] * c2;
+    const double id = 1.0 / det;
+    o[0] = c0 * id;
+    o[1] = (m[2] * m[7] - m[1] * m[8]) * id;
+    o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    o[3] = c1 * id;
+    o[4] = (m[0] * m[8] - m[2] * m[6]) * id;
+    o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    o[6] = c2 * id;
+    o[7] = (m[1] * m[6] - m[0] * m[7]) * id;
+    o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+__global__ __launch_bounds__(BA_THREADS) void point_schur(int P, const int* __restrict__ ptfree,
+                                                          const double* __restrict__ Hll,
+                                                          const double* __restrict__ bl, double lambda,
+                                                          double* __restrict__ Dinv,
+                                                          double* __restrict__ db)
+{
+    const int p = blockIdx.x * BA_THREADS + threadIdx.x;
+    if (p >= P || !ptfree[p]) return;
+    double D[9], Di[9];
+    for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
+    D[0] += lambda;
+    D[4] += lambda;
+    D[8] += lambda;
+    d_inv3(D, Di);
+    for (int k = 0; k < 9; k++) Dinv[9 * (long long)p + k] = Di[k];
+    const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
+    for (int r = 0; r < 3; r++) db[3 * p + r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
+}
+
+constexpr int SCHUR_MAX_BLOCKS = 96;  // free cameras handled by the LDS row accumulator
+
+// Row block h1 (camera c1) of the reduced camera system:
+//   S[h1][h2] = delta(h1,h2) (Hpp_c1 + lambda I) - sum_p Hpl_{c1 p} Dinv_p Hpl_{c2 p}^T  (h2 >= h1)
+//   rhs[h1]   = bp_c1 - sum_p Hpl_{c1 p} Dinv_p bl_p
+// (BlockSolver::solve Schur loop).  Lower blocks are mirrored for the dense factorisation.
+__global__ __launch_bounds__(BA_THREADS) void build_schur(Problem pb, int n, const int* __restrict__ cam_of_block,
+                                                          const double* __restrict__ Hpp,
+                                                          const double* __restrict__ bp,
+                                                          const double* __restrict__ Hpl,
+                                                          const double* __restrict__ Dinv,
+                                                          const double* __restrict__ db, double lambda,
+                                                          double* __restrict__ S, double* __restrict__ rhs)
+{
+    __shared__ double acc[SCHUR_MAX_BLOCKS * 36];
+    __shared__ double racc[BA_THREADS / kWave][6];
+    const int h1 = blockIdx.x;
+    const int c1 = cam_of_block[h1];
+    const int nb = n / 6;
+    for (int i = threadIdx.x; i < nb * 36; i += BA_THREADS) acc[i] = 0;
+    __syncthreads();
+    double r6[6] = {0, 0, 0, 0, 0, 0};
+    for (int a = pb.cstart[c1] + threadIdx.x; a < pb.cstart[c1 + 1]; a += BA_THREADS) {
+        const int e1 = pb.cedges[a];
+        const int p = pb.ept[e1];
+        if (!pb.ptfree[p]) continue;
+        const double* W1 = Hpl + 18 * (long long)e1;
+        const double* Di = Dinv + 9 * (long long)p;
+        double Z[18];  // W1 * Dinv (6x3)
+        for (int r = 0; r < 6; r++)
+            for (int k = 0; k < 3; k++) Z[r * 3 + k] = W1[r * 3] * Di[k] + W1[r * 3 + 1] * Di[3 + k] + W1[r * 3 + 2] * Di[6 + k];
+        const double g0 = db[3 * p], g1 = db[3 * p + 1], g2 = db[3 * p + 2];
+        for (int r = 0; r < 6; r++) r6[r] += W1[r * 3] * g0 + W1[r * 3 + 1] * g1 + W1[r * 3 + 2] * g2;
+        for (int b = pb.pstart[p]; b < pb.pstart[p + 1]; b++) {
+            const int e2 = pb.pedges[b];
+            const int h2 = pb.camh[pb.ecam[e2]];
+            if (h2 < h1) continue;
+            const double* W2 = Hpl + 18 * (long long)e2;
+            double* A = acc + 36 * h2;
+            for (int r = 0; r < 6; r++)
+                for (int k = 0; k < 6; k++)
+                    atomicAdd(&A[r * 6 + k], Z[r * 3] * W2[k * 3] + Z[r * 3 + 1] * W2[k * 3 + 1] + Z[r * 3 + 2] * W2[k * 3 + 2]);
+        }
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int r = 0; r < 6; r++) {
+        double v = r6[r];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) racc[wave][r] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        double v = 0;
+        for (int w = 0; w < BA_THREADS / kWave; w++) v += racc[w][threadIdx.x];
+        rhs[6 * h1 + threadIdx.x] = bp[6 * c1 + threadIdx.x] - v;
+    }
+    for (int i = threadIdx.x; i < (nb - h1) * 36; i += BA_THREADS) {
+        const int h2 = h1 + i / 36, rc = i % 36, r = rc / 6, k = rc % 6;
+        double v = -acc[36 * h2 + rc];
+        if (h2 == h1) v += Hpp[36 * (long long)c1 + rc] + (r == k ? lambda : 0.0);
+        S[(long long)(6 * h1 + r) * n + 6 * h2 + k] = v;
+        S[(long long)(6 * h2 + k) * n + 6 * h1 + r] = v;
+    }
+}
+
+// Dense SPD solve S x = b in one workgroup: blocked right-looking Cholesky (NB = 16), the
+// diagonal 16x16 factor in one wave's registers (shuffles, no workgroup barriers), panel TRSM
+// one row per thread, trailing update from an LDS copy of the panel; then blocked forward /
+// backward substitution.  S (row-major, full) is overwritten by L in its lower triangle.
+constexpr int CH_THREADS = 1024;
+constexpr int NB = 16;
+constexpr int CH_PANEL_ROWS = 1024;
+
+__global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict__ S, int n,
+                                                             const double* __restrict__ b,
+                                                             double* __restrict__ x,
+                                                             int* __restrict__ fail)
+{
+    __shared__ double L11[NB][NB + 1];
+    __shared__ double panel[CH_PANEL_ROWS][NB + 1];
+    __shared__ int s_fail;
+    __shared__ double ytile[NB];
+    const int tid = threadIdx.x;
+    if (tid == 0) s_fail = 0;
+    __syncthreads();
+    for (int kb = 0; kb < n; kb += NB) {
+        const int nbk = min(NB, n - kb);
+        // (1) diagonal block by wave 0
+        if (tid < kWave) {
+            const int l = tid;
+            double a[NB];
+#pragma unroll
+            for (int k = 0; k < NB; k++) a[k] = (l < nbk && k < nbk) ? S[(long long)(kb + l) * n + kb + k] : 0.0;
+            int bad = 0;
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                if (j < nbk) {
+                    const double djj = __shfl(a[j], j);
+                    if (!(djj > 0)) bad = 1;
+                    const double d = sqrt(djj);
+                    if (l == j) a[j] = d;
+                    if (l > j) a[j] = a[j] / d;
+#pragma unroll
+                    for (int k = j + 1; k < NB; k++) {
+                        const double lkj = __shfl(a[j], k);
+                        if (l >= k && k < nbk) a[k] -= a[j] * lkj;
+                    }
+                }
+            }
+            if (l < nbk) {
+#pragma unroll
+                for (int k = 0; k < NB; k++) {
+                    if (k <= l && k < nbk) {
+                        L11[l][k] = a[k];
+                        S[(long long)(kb + l) * n + kb + k] = a[k];
+                    }
+                }
+            }
+            if (l == 0 && bad) s_fail = 1;
+        }
+        __syncthreads();
+        if (s_fail) break;
+        // (2) panel TRSM: rows below the block, L21 = A21 L11^-T
+        const int r0 = kb + nbk;
+        for (int i = r0 + tid; i < n; i += CH_THREADS) {
+            double v[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j++) v[j] = j < nbk ? S[(long long)i * n + kb + j] : 0.0;
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                if (j < nbk) {
+                    double s = v[j];
+#pragma unroll
+                    for (int k = 0; k < j; k++) s -= v[k] * L11[j][k];
+                    v[j] = s / L11[j][j];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                if (j < nbk) {
+                    S[(long long)i * n + kb + j] = v[j];
+                    if (i - r0 < CH_PANEL_ROWS) panel[i - r0][j] = v[j];
+                }
+            }
+        }
+        __syncthreads();
+        // (3) trailing update of the lower triangle: A22 -= L21 L21^T
+        const int m = n - r0;
+        const long long tri = (long long)m * (m + 1) / 2;
+        for (long long t = tid; t < tri; t += CH_THREADS) {
+            // t -> (i, k) with k <= i, row-major lower triangle
+            int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+            while ((long long)(i + 1) * (i + 2) / 2 <= t) i++;
+            while ((long long)i * (i + 1) / 2 > t) i--;
+            const int k = (int)(t - (long long)i * (i + 1) / 2);
+            double s = 0;
+            if (i < CH_PANEL_ROWS) {
+#pragma unroll
+                for (int j = 0; j < NB; j++)
+                    if (j < nbk) s += panel[i][j] * panel[k][j];
+            } else {
+                for (int j = 0; j < nbk; j++) s += S[(long long)(r0 + i) * n + kb + j] * S[(long long)(r0 + k) * n + kb + j];
+            }
+            S[(long long)(r0 + i) * n + r0 + k] -= s;
+        }
+        __syncthreads();
+    }
+    if (s_fail) {
+        if (tid == 0) *fail = 1;
+        return;
+    }
+    // forward: L y = b (y stored in x)
+    for (int i = tid; i < n; i += CH_THREADS) x[i] = b[i];
+    __syncthreads();
+    for (int kb = 0; kb < n; kb += NB) {
+        const int nbk = min(NB, n - kb);
+        if (tid < kWave) {
+            // one wave solves the 16x16 triangle sequentially (lane 0), broadcast via LDS
+            if (tid == 0) {
+                for (int j = 0; j < nbk; j++) {
+                    double s = x[kb + j];
+                    for (int k = 0; k < j; k++) s -= S[(long long)(kb + j) * n + kb + k] * ytile[k];
+                    ytile[j] = s / S[(long long)(kb + j) * n + kb + j];
+                    x[kb + j] = ytile[j];
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = kb + nbk + tid; i < n; i += CH_THREADS) {
+            double s = 0;
+            for (int j = 0; j < nbk; j++) s += S[(long long)i * n + kb + j] * ytile[j];
+            x[i] -= s;
+        }
+        __syncthreads();
+    }
+    // backward: L^T x = y
+    for (int kb = ((n - 1) / NB) * NB; kb >= 0; kb -= NB) {
+        const int nbk = min(NB, n - kb);
+        if (tid == 0) {
+            for (int j = nbk - 1; j >= 0; j--) {
+                double s = x[kb + j];
+                for (int k = j + 1; k < nbk; k++) s -= S[(long long)(kb + k) * n + kb + j] * ytile[k];
+                ytile[j] = s / S[(long long)(kb + j) * n + kb + j];
+                x[kb + j] = ytile[j];
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < kb; i += CH_THREADS) {
+            double s = 0;
+            for (int j = 0; j < nbk; j++) s += S[(long long)(kb + j) * n + i] * ytile[j];
+            x[i] -= s;
+        }
+        __syncthreads();
+    }
+}
+
+// xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]); also the point part of computeScale.
+__global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const double* __restrict__ Hpl,
+                                                            const double* __restrict__ Dinv,
+                                                            const double* __restrict__ bl,
+                                                            const double* __restrict__ xp, double lambda,
+                                                            double* __restrict__ xl,
+                                                            double* __restrict__ scale_part)
+{
+    const int p = blockIdx.x * BA_THREADS + threadIdx.x;
+    if (p >= pb.P) return;
+    if (!pb.ptfree[p]) {
+        scale_part[p] = 0;
+        return;
+    }
+    double cl[3] = {bl[3 * p], bl[3 * p + 1], bl[3 * p + 2]};
+    for (int a = pb.pstart[p]; a < pb.pstart[p + 1]; a++) {
+        const int e = pb.pedges[a];
+        const int h = pb.camh[pb.ecam[e]];
+        if (h < 0) continue;
+        const double* W = Hpl + 18 * (long long)e;
+        const double* X = xp + 6 * h;
+        for (int k = 0; k < 3; k++)
+            for (int r = 0; r < 6; r++) cl[k] -= W[r * 3 + k] * X[r];
+    }
+    const double* Di = Dinv + 9 * (long long)p;
+    double sc = 0;
+    for (int r = 0; r < 3; r++) {
+        const double v = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
+        xl[3 * p + r] = v;
+        sc += v * (lambda * v + bl[3 * p + r]);
+    }
+    scale_part[p] = sc;
+}
+
+// Trial state B from A: cameras exp(xp) * T (free) or copy; points p + xl (free) or copy.
+// Also the camera part of computeScale.
+__global__ __launch_bounds__(BA_THREADS) void update_state(Problem pb, State A, State B,
+                                                           const double* __restrict__ xp,
+                                                           const double* __restrict__ xl,
+                                                           const double* __restrict__ bp, double lambda,
+                                                           double* __restrict__ scale_part_cam)
+{
+    const int i = blockIdx.x * BA_THREADS + threadIdx.x;
+    if (i < pb.C) {
+        double q[4] = {A.q[4 * i], A.q[4 * i + 1], A.q[4 * i + 2], A.q[4 * i + 3]};
+        double t[3] = {A.t[3 * i], A.t[3 * i + 1], A.t[3 * i + 2]};
+        const int h = pb.camh[i];
+        double sc = 0;
+        if (h >= 0) {
+            double u[6];
+            for (int k = 0; k < 6; k++) {
+                u[k] = xp[6 * h + k];
+                sc += u[k] * (lambda * u[k] + bp[6 * i + k]);
+            }
+            d_oplus(q, t, u);
+        }
+        for (int k = 0; k < 4; k++) B.q[4 * i + k] = q[k];
+        for (int k = 0; k < 3; k++) B.t[3 * i + k] = t[k];
+        scale_part_cam[i] = sc;
+    }
+    if (i < pb.P) {
+        const bool fr = pb.ptfree[i];
+        for (int k = 0; k < 3; k++) B.p[3 * i + k] = A.p[3 * i + k] + (fr ? xl[3 * i + k] : 0.0);
+    }
+}
+
+// StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) per active edge at state s using the
+// stored errors: flag[e] = 1 if behind the camera or |e|^2 > maxErrorSquare.
+__global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s, int E,
+                                                           const unsigned char* __restrict__ active,
+                                                           const double* __restrict__ err,
+                                                           double maxErrSq,
+                                                           unsigned char* __restrict__ flag,
+                                                           double* __restrict__ sum_part,
+                                                           double* __restrict__ cnt_part)
+{
+    __shared__ double ssum[BA_THREADS], scnt[BA_THREADS];
+    const int e = blockIdx.x * BA_THREADS + threadIdx.x;
+    double vs = 0, vc = 0;
+    if (e < E) {
+        unsigned char fl = 0;
+        if (active[e]) {
+            const double e0 = err[2 * e], e1 = err[2 * e + 1];
+            const double sumSquares = e0 * e0 + e1 * e1;
+            const int c = pb.ecam[e], p = pb.ept[e];
+            // SE3Quat::inverse: q* , -(q* t); forward = q* (0,0,1)
+            const double qc[4] = {-s.q[4 * c], -s.q[4 * c + 1], -s.q[4 * c + 2], s.q[4 * c + 3]};
+            const double tt[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
+            double it[3], fwd[3];
+            d_qrot(qc, tt, it);
+            const double z[3] = {0, 0, 1};
+            d_qrot(qc, z, fwd);
+            const double dot = (s.p[3 * p] + it[0]) * fwd[0] + (s.p[3 * p + 1] + it[1]) * fwd[1] +
+                               (s.p[3 * p + 2] + it[2]) * fwd[2];
+            if (dot <= 0 || sumSquares > maxErrSq) {
+                fl = 1;
+            } else {
+                vs = sumSquares;
+                vc = 1;
+            }
+        }
+        flag[e] = fl;
+    }
+    ssum[threadIdx.x] = vs;
+    scnt[threadIdx.x] = vc;
+    __syncthreads();
+    for (int st = BA_THREADS / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) {
+            ssum[threadIdx.x] += ssum[threadIdx.x + st];
+            scnt[threadIdx.x] += scnt[threadIdx.x + st];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        sum_part[blockIdx.x] = ssum[0];
+        cnt_part[blockIdx.x] = scnt[0];
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Host: the StepOptimizer / OptimizationAlgorithmLevenberg control flow
+// ------------------------------------------------------------------------------------------
+
+struct BundleAdjuster {
+    int device = 0;
+    bool points_fixed = false;
+    // host copies of the problem
+    int C = 0, P = 0, E = 0;
+    std::vector<double> q, t, camk, p, uv, info;
+    std::vector<int> fixed, ecam, ept;
+    std::vector<unsigned char> removed;
+    bool dirty = true, useless = false, state_on_device = false, host_state_stale = false;
+    int iteration = 0;
+    double user_lambda = 0, lambda = 0, ni = 2, huber = 0;
+    int n = 0;  // 6 * cameras in the system
+    std::vector<int> camh, ptfree, cam_of_block;
+    hipStream_t st = nullptr;
+    int cur = 0;  // which state buffer holds the current estimate
+    // device buffers
+    DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
+        d_pstart, d_pedges, d_cstart, d_cedges, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp, d_bp,
+        d_Dinv, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_flag, d_osum, d_ocnt,
+        d_camblk, d_fail;
+    mage_ba_stats stats{};
+
+    Problem problem() const
+    {
+        Problem pb;
+        pb.C = C;
+        pb.P = P;
+        pb.camk = d_camk.as<double>();
+        pb.camh = d_camh.as<int>();
+        pb.ptfree = d_ptfree.as<int>();
+        pb.uv = d_uv.as<double>();
+        pb.ecam = d_ecam.as<int>();
+        pb.ept = d_ept.as<int>();
+        pb.info = d_info.as<double>();
+        pb.pstart = d_pstart.as<int>();
+        pb.pedges = d_pedges.as<int>();
+        pb.cstart = d_cstart.as<int>();
+        pb.cedges = d_cedges.as<int>();
+        pb.huber = huber;
+        return pb;
+    }
+    State state(int i) const { return State{d_q[i].as<double>(), d_t[i].as<double>(), d_p[i].as<double>()}; }
+
+    void release()
+    {
+        for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh,
+                        &d_ptfree, &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart,
+                        &d_cedges, &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_Dinv,
+                        &d_db, &d_S, &d_rhs, &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_flag,
+                        &d_osum, &d_ocnt, &d_camblk, &d_fail})
+            b->release();
+        if (st) (void)hipStreamDestroy(st);
+        st = nullptr;
+    }
+
+    template <typename T>
+    mage_status upload(DeviceBuffer& b, const std::vector<T>& v)
+    {
+        mage_status r = b.reserve(std::max<size_t>(v.size() * sizeof(T), 16));
+        if (r != MAGE_OK) return r;
+        if (!v.empty()) MAGE_HIP(hipMemcpyAsync(b.ptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
+        return MAGE_OK;
+    }
+
+    // Pull the current estimate back to the host vectors (before re-initialisation).
+    mage_status sync_host_state()
+    {
+        if (!state_on_device || !host_state_stale) return MAGE_OK;
+        MAGE_HIP(hipMemcpyAsync(q.data(), d_q[cur].ptr, sizeof(double) * 4 * C, hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipMemcpyAsync(t.data(), d_t[cur].ptr, sizeof(double) * 3 * C, hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipMemcpyAsync(p.data(), d_p[cur].ptr, sizeof(double) * 3 * P, hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        host_state_stale = false;
+        return MAGE_OK;
+    }
+
+    // SparseOptimizer::initializeOptimization (+ StepOptimizer::InitializeOptimization):
+    // active edges, vertices in the system, CSR structures; iteration reset to 0.
+    mage_status initialize()
+    {
+        mage_status r = sync_host_state();
+        if (r != MAGE_OK) return r;
+        std::vector<unsigned char> active(E);
+        std::vector<int> camHas(C, 0), ptHas(P, 0);
+        for (int e = 0; e < E; e++) {
+            const bool a = !removed[e] && !(fixed[ecam[e]] && points_fixed);
+            active[e] = a;
+            if (a) {
+                camHas[ecam[e]] = 1;
+                ptHas[ept[e]] = 1;
+            }
+        }
+        camh.assign(C, -1);
+        cam_of_block.clear();
+        for (int c = 0; c < C; c++)
+            if (!fixed[c] && camHas[c]) {
+                camh[c] = (int)cam_of_block.size();
+                cam_of_block.push_back(c);
+            }
+        ptfree.assign(P, 0);
+        int nfp = 0;
+        for (int i = 0; i < P; i++)
+            if (!points_fixed && ptHas[i]) {
+                ptfree[i] = 1;
+                nfp++;
+            }
+        n = 6 * (int)cam_of_block.size();
+        useless = (cam_of_block.empty() && nfp == 0);
+        MAGE_REQUIRE((int)cam_of_block.size() <= SCHUR_MAX_BLOCKS, MAGE_EUNSUPPORTED,
+                     "more than 96 free cameras in one bundle adjustment");
+        std::vector<int> pstart(P + 1, 0), cstart(C + 1, 0);
+        for (int e = 0; e < E; e++)
+            if (active[e]) {
+                pstart[ept[e] + 1]++;
+                cstart[ecam[e] + 1]++;
+            }
+        for (int i = 0; i < P; i++) pstart[i + 1] += pstart[i];
+        for (int c = 0; c < C; c++) cstart[c + 1] += cstart[c];
+        std::vector<int> pedges(std::max(pstart[P], 1)), cedges(std::max(cstart[C], 1));
+        {
+            std::vector<int> pf(pstart.begin(), pstart.end() - 1), cf(cstart.begin(), cstart.end() - 1);
+            for (int e = 0; e < E; e++)
+                if (active[e]) {
+                    pedges[pf[ept[e]]++] = e;
+                    cedges[cf[ecam[e]]++] = e;
+                }
+        }
+        if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
+        if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
+        if ((r = upload(d_active, active)) != MAGE_OK) return r;
+        if ((r = upload(d_pstart, pstart)) != MAGE_OK) return r;
+        if ((r = upload(d_pedges, pedges)) != MAGE_OK) return r;
+        if ((r = upload(d_cstart, cstart)) != MAGE_OK) return r;
+        if ((r = upload(d_cedges, cedges)) != MAGE_OK) return r;
+        if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
+        if (!state_on_device) {
+            if ((r = upload(d_q[0], q)) != MAGE_OK) return r;
+            if ((r = upload(d_t[0], t)) != MAGE_OK) return r;
+            if ((r = upload(d_p[0], p)) != MAGE_OK) return r;
+            if ((r = d_q[1].reserve(d_q[0].bytes)) != MAGE_OK) return r;
+            if ((r = d_t[1].reserve(d_t[0].bytes)) != MAGE_OK) return r;
+            if ((r = d_p[1].reserve(d_p[0].bytes)) != MAGE_OK) return r;
+            cur = 0;
+            state_on_device = true;
+        }
+        const size_t Pm = std::max(P, 1), Cm = std::max(C, 1), Em = std::max(E, 1);
+        for (auto pr : {std::make_pair(&d_err, Em * 2 * 8), std::make_pair(&d_Hll, Pm * 9 * 8),
+                        std::make_pair(&d_bl, Pm * 3 * 8), std::make_pair(&d_Hpl, Em * 18 * 8),
+                        std::make_pair(&d_Hpp, Cm * 36 * 8), std::make_pair(&d_bp, Cm * 6 * 8),
+                        std::make_pair(&d_Dinv, Pm * 9 * 8), std::make_pair(&d_db, Pm * 3 * 8),
+                        std::make_pair(&d_S, (size_t)std::max(n, 1) * std::max(n, 1) * 8),
+                        std::make_pair(&d_rhs, (size_t)std::max(n, 1) * 8),
+                        std::make_pair(&d_x, ((size_t)n + 3 * Pm + 1) * 8),
+                        std::make_pair(&d_chi, Pm * 8), std::make_pair(&d_maxd, (Pm + Cm) * 8),
+                        std::make_pair(&d_scale, (Pm + Cm) * 8), std::make_pair(&d_red, (size_t)64),
+                        std::make_pair(&d_flag, Em), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 8),
+                        std::make_pair(&d_ocnt, (Em / BA_THREADS + 2) * 8), std::make_pair(&d_fail, (size_t)16)})
+            if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
+        MAGE_HIP(hipMemsetAsync(d_maxd.ptr, 0, (Pm + Cm) * 8, st));
+        MAGE_HIP(hipMemsetAsync(d_scale.ptr, 0, (Pm + Cm) * 8, st));
+        iteration = 0;
+        dirty = false;
+        return MAGE_OK;
+    }
+
+    // errors (+ linearisation) of the current state; returns chi2 (and max diagonal)
+    mage_status linearize(bool lin, double* chi, double* maxd)
+    {
+        Problem pb = problem();
+        const int gp = (P + BA_THREADS - 1) / BA_THREADS;
+        if (P > 0)
+            hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(cur), lin ? 1 : 0,
+                               d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
+                               d_chi.as<double>(), d_maxd.as<double>());
+        MAGE_HIP(hipGetLastError());
+        if (lin && C > 0) {
+            hipLaunchKernelGGL(cam_linearize, dim3(C), dim3(BA_THREADS), 0, st, pb, state(cur), d_err.as<double>(),
+                               d_Hpp.as<double>(), d_bp.as<double>(), d_maxd.as<double>() + P);
+            MAGE_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_chi.as<double>(), 0,
+                           d_maxd.as<double>(), lin ? P + C : 0, d_red.as<double>());
+        MAGE_HIP(hipGetLastError());
+        double h[3];
+        MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        *chi = h[0];
+        if (maxd) *maxd = h[2];
+        return MAGE_OK;
+    }
+
+    // One trial: solve with lambda, build the trial state in the other buffer, evaluate it.
+    mage_status trial(double lam, bool* ok, double* tempChi, double* scale)
+    {
+        Problem pb = problem();
+        const int gp = (P + BA_THREADS - 1) / BA_THREADS;
+        const int gmax = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
+        double* xp = d_x.as<double>();
+        double* xl = d_x.as<double>() + n;
+        MAGE_HIP(hipMemsetAsync(d_fail.ptr, 0, 4, st));
+        if (P > 0 && !points_fixed)
+            hipLaunchKernelGGL(point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
+                               d_Hll.as<double>(), d_bl.as<double>(), lam, d_Dinv.as<double>(), d_db.as<double>());
+        if (n > 0) {
+            hipLaunchKernelGGL(build_schur, dim3(n / 6), dim3(BA_THREADS), 0, st, pb, n, d_camblk.as<int>(),
+                               d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(), d_Dinv.as<double>(),
+                               d_db.as<double>(), lam, d_S.as<double>(), d_rhs.as<double>());
+            hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), n,
+                               d_rhs.as<double>(), xp, d_fail.as<int>());
+        }
+        if (P > 0)
+            hipLaunchKernelGGL(point_backsub, dim3(gp), dim3(BA_THREADS), 0, st, pb, d_Hpl.as<double>(),
+                               d_Dinv.as<double>(), d_bl.as<double>(), xp, lam, xl, d_scale.as<double>());
+        if (std::max(P, C) > 0)
+            hipLaunchKernelGGL(update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur), xp, xl,
+                               d_bp.as<double>(), lam, d_scale.as<double>() + P);
+        if (P > 0)
+            hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
+                               d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
+                               d_chi.as<double>(), d_maxd.as<double>());
+        hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_scale.as<double>(), P + C,
+                           d_maxd.as<double>(), 0, d_red.as<double>());
+        MAGE_HIP(hipGetLastError());
+        double h[3];
+        int fail = 0;
+        MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipMemcpyAsync(&fail, d_fail.ptr, 4, hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        *ok = fail == 0;
+        *tempChi = h[0];
+        *scale = h[1];
+        return MAGE_OK;
+    }
+
+    // OptimizationAlgorithmLevenberg::solve (g2o); result 1 = OK, 0 = Terminate
+    mage_status lm_solve(int* result)
+    {
+        double currentChi = 0, maxd = 0;
+        mage_status r = linearize(true, &currentChi, &maxd);
+        if (r != MAGE_OK) return r;
+        if (iteration == 0) {
+            lambda = user_lambda > 0 ? user_lambda : 1e-5 * maxd;  // computeLambdaInit, tau = 1e-5
+            ni = 2;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            bool ok2 = true;
+            double tempChi = 0, scale = 0;
+            if ((r = trial(lambda, &ok2, &tempChi, &scale)) != MAGE_OK) return r;
+            if (!ok2) tempChi = std::numeric_limits<double>::max();
+            rho = currentChi - tempChi;
+            scale += 1e-3;
+            rho /= scale;
+            stats.trials++;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+                cur = 1 - cur;  // discardTop: the trial state becomes current
+                host_state_stale = true;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                stats.rejected_trials++;  // pop: current buffer unchanged
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10);
+        stats.iterations++;
+        stats.last_chi2 = currentChi;
+        stats.lambda = lambda;
+        *result = (qmax == 10 || rho == 0 || !std::isfinite(lambda)) ? 0 : 1;
+        return MAGE_OK;
+    }
+
+    mage_status step_once(bool* ok)
+    {
+        mage_status r;
+        if (dirty && (r = initialize()) != MAGE_OK) return r;
+        if (useless) {
+            *ok = false;
+            return MAGE_OK;
+        }
+        int res = 0;
+        if ((r = lm_solve(&res)) != MAGE_OK) return r;
+        iteration++;
+        *ok = res == 1;
+        return MAGE_OK;
+    }
+
+    mage_status step(const float* hw, uint32_t nsteps, float maxErrSq, uint32_t* outliers, uint32_t cap,
+                     uint32_t* nOut, float* meanSq)
+    {
+        mage_status r;
+        MAGE_HIP(hipSetDevice(device));
+        float prior = -1.f;
+        for (uint32_t s = 0; s < nsteps; s++) {
+            if (hw[s] != prior) {
+                huber = (double)hw[s];
+                prior = hw[s];
+            }
+            bool ok = false;
+            if ((r = step_once(&ok)) != MAGE_OK) return r;
+            if (!ok) break;
+        }
+        if (dirty && (r = initialize()) != MAGE_OK) return r;
+        if (E == 0) {
+            *nOut = 0;
+            *meanSq = std::numeric_limits<float>::quiet_NaN();
+            return MAGE_OK;
+        }
+        const int ge = (E + BA_THREADS - 1) / BA_THREADS;
+        hipLaunchKernelGGL(outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), state(cur), E,
+                           d_active.as<unsigned char>(), d_err.as<double>(), (double)maxErrSq,
+                           d_flag.as<unsigned char>(), d_osum.as<double>(), d_ocnt.as<double>());
+        hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_osum.as<double>(), ge, d_ocnt.as<double>(), ge,
+                           d_osum.as<double>(), 0, d_red.as<double>());
+        MAGE_HIP(hipGetLastError());
+        std::vector<unsigned char> flag(E);
+        double h[3];
+        MAGE_HIP(hipMemcpyAsync(flag.data(), d_flag.ptr, E, hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        uint32_t no = 0;
+        for (int e = 0; e < E; e++)
+            if (flag[e]) {
+                removed[e] = 1;
+                dirty = true;
+                if (no < cap) outliers[no] = (uint32_t)e;
+                no++;
+            }
+        *nOut = std::min(no, cap);
+        *meanSq = (float)(h[0] / h[1]);
+        return no > cap ? MAGE_ECAPACITY : MAGE_OK;
+    }
+};
+
+}  // namespace mage
+
+struct mage_ba : mage::BundleAdjuster {};
+
+extern "C" {
+
+mage_status mage_ba_create(int32_t points_fixed, int device, mage_ba** out)
+{
+    MAGE_REQUIRE(out, MAGE_EINVAL, "null output");
+    *out = nullptr;
+    mage_status r = mage::bind_device(device);
+    if (r != MAGE_OK) return r;
+    auto* b = new mage_ba();
+    b->device = device;
+    b->points_fixed = points_fixed != 0;
+    if (hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess) {
+        delete b;
+        mage::set_error("hipStreamCreate failed");
+        return MAGE_EDEVICE;
+    }
+    *out = b;
+    return MAGE_OK;
+}
+
+mage_status mage_ba_destroy(mage_ba* ba)
+{
+    if (!ba) return MAGE_OK;
+    (void)hipSetDevice(ba->device);
+    ba->release();
+    delete ba;
+    return MAGE_OK;
+}
+
+mage_status mage_ba_set_cameras(mage_ba* b, uint32_t n, const float* pos3, const float* r9, const float* intr4,
+                                const uint8_t* fixed)
+{
+    MAGE_REQUIRE(b && (n == 0 || (pos3 && r9 && intr4)), MAGE_EINVAL, "null argument");
+    MAGE_REQUIRE(!b->state_on_device || (int)n == b->C, MAGE_EINVAL, "cameras can only be allocated once");
+    b->C = (int)n;
+    b->q.assign(4 * n, 0);
+    b->t.assign(3 * n, 0);
+    b->camk.assign(3 * n, 0);
+    b->fixed.assign(n, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        // Eigen::Quaternionf{Map<const Matrix3f>}.normalized() in float (BundlerLib.cpp:271-273),
+        // the column-major map read as m(r,c) = r9[c*3+r]
+        float m[9];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) m[r * 3 + c] = r9[9 * i + c * 3 + r];
+        float qf[4];
+        float tr = m[0] + m[4] + m[8];
+        if (tr > 0.f) {
+            float s = std::sqrt(tr + 1.0f);
+            qf[3] = 0.5f * s;
+            s = 0.5f / s;
+            qf[0] = (m[7] - m[5]) * s;
+            qf[1] = (m[2] - m[6]) * s;
+            qf[2] = (m[3] - m[1]) * s;
+        } else {
+            int a = 0;
+            if (m[4] > m[0]) a = 1;
+            if (m[8] > m[a * 4]) a = 2;
+            int j = (a + 1) % 3, k = (j + 1) % 3;
+            float s = std::sqrt(m[a * 4] - m[j * 4] - m[k * 4] + 1.0f);
+            qf[a] = 0.5f * s;
+            s = 0.5f / s;
+            qf[3] = (m[k * 3 + j] - m[j * 3 + k]) * s;
+            qf[j] = (m[j * 3 + a] + m[a * 3 + j]) * s;
+            qf[k] = (m[k * 3 + a] + m[a * 3 + k]) * s;
+        }
+        float nrm = std::sqrt(qf[0] * qf[0] + qf[1] * qf[1] + qf[2] * qf[2] + qf[3] * qf[3]);
+        double qd[4];
+        for (int k = 0; k < 4; k++) qd[k] = (double)(qf[k] / nrm);
+        // SE3Quat(q, t) normalizeRotation
+        if (qd[3] < 0)
+            for (int k = 0; k < 4; k++) qd[k] = -qd[k];
+        double dn = std::sqrt(qd[0] * qd[0] + qd[1] * qd[1] + qd[2] * qd[2] + qd[3] * qd[3]);
+        for (int k = 0; k < 4; k++) b->q[4 * i + k] = qd[k] / dn;
+        for (int k = 0; k < 3; k++) b->t[3 * i + k] = (double)pos3[3 * i + k];
+        // CameraParameters(intrinsics[2], (intrinsics[0], intrinsics[1]), 0) (BundlerLib.cpp:266)
+        b->camk[3 * i] = (double)intr4[4 * i + 2];
+        b->camk[3 * i + 1] = (double)intr4[4 * i + 0];
+        b->camk[3 * i + 2] = (double)intr4[4 * i + 1];
+        b->fixed[i] = fixed ? (fixed[i] != 0) : 0;
+    }
+    b->dirty = true;
+    b->state_on_device = false;
+    (void)hipSetDevice(b->device);
+    return b->upload(b->d_camk, b->camk);
+}
+
+mage_status mage_ba_fix_camera(mage_ba* b, uint32_t idx, int32_t fixed)
+{
+    MAGE_REQUIRE(b && (int)idx < b->C, MAGE_EINVAL, "bad camera index");
+    b->fixed[idx] = fixed != 0;  // setFixed does not dirty the optimizer (BundlerLib.cpp:280-283)
+    return MAGE_OK;
+}
+
+mage_status mage_ba_set_points(mage_ba* b, uint32_t n, const float* xyz)
+{
+    MAGE_REQUIRE(b && (n == 0 || xyz), MAGE_EINVAL, "null argument");
+    mage_status r = b->sync_host_state();
+    if (r != MAGE_OK) return r;
+    b->P = (int)n;
+    b->p.assign(3 * n, 0);
+    for (uint32_t i = 0; i < 3 * n; i++) b->p[i] = (double)xyz[i];
+    b->dirty = true;
+    b->state_on_device = false;
+    return MAGE_OK;
+}
+
+mage_status mage_ba_set_observations(mage_ba* b, uint32_t n, const float* uv, const uint32_t* cam,
+                                     const uint32_t* pt, const float* info)
+{
+    MAGE_REQUIRE(b && (n == 0 || (uv && cam && pt && info)), MAGE_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; i++)
+        MAGE_REQUIRE((int)cam[i] < b->C && (int)pt[i] < b->P, MAGE_EINVAL, "observation index out of range");
+    b->E = (int)n;
+    b->uv.assign(2 * n, 0);
+    b->info.assign(n, 0);
+    b->ecam.assign(n, 0);
+    b->ept.assign(n, 0);
+    b->removed.assign(n, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        b->uv[2 * i] = uv[2 * i];
+        b->uv[2 * i + 1] = uv[2 * i + 1];
+        b->ecam[i] = (int)cam[i];
+        b->ept[i] = (int)pt[i];
+        b->info[i] = info[i];
+    }
+    b->dirty = true;
+    (void)hipSetDevice(b->device);
+    mage_status r;
+    if ((r = b->upload(b->d_uv, b->uv)) != MAGE_OK) return r;
+    if ((r = b->upload(b->d_info, b->info)) != MAGE_OK) return r;
+    if ((r = b->upload(b->d_ecam, b->ecam)) != MAGE_OK) return r;
+    return b->upload(b->d_ept, b->ept);
+}
+
+mage_status mage_ba_set_lambda(mage_ba* b, float lambda)
+{
+    MAGE_REQUIRE(b, MAGE_EINVAL, "null handle");
+    b->iteration = 0;  // StepOptimizer::SetCurrentLambda (BundlerLib.cpp:123-130)
+    b->user_lambda = (double)lambda;
+    return MAGE_OK;
+}
+
+mage_status mage_ba_get_lambda(mage_ba* b, float* lambda)
+{
+    MAGE_REQUIRE(b && lambda, MAGE_EINVAL, "null argument");
+    *lambda = (float)b->lambda;
+    return MAGE_OK;
+}
+
+mage_status mage_ba_set_tethers(mage_ba* b, uint32_t, uint32_t n, const uint32_t*, const uint32_t*, const float*,
+                                const float*)
+{
+    MAGE_REQUIRE(b, MAGE_EINVAL, "null handle");
+    if (n == 0) return MAGE_OK;
+    mage::set_error("tether constraints are not implemented in this build");
+    return MAGE_EUNSUPPORTED;
+}
+
+mage_status mage_ba_step(mage_ba* b, const float* huber, uint32_t nsteps, float max_error_square, uint32_t* outliers,
+                         uint32_t cap, uint32_t* n_out, float* mean_sq)
+{
+    MAGE_REQUIRE(b && n_out && mean_sq && (nsteps == 0 || huber) && (cap == 0 || outliers), MAGE_EINVAL,
+                 "null argument");
+    for (uint32_t s = 0; s < nsteps; s++) MAGE_REQUIRE(huber[s] >= 0.f, MAGE_EINVAL, "Huber widths must be nonnegative");
+    return b->step(huber, nsteps, max_error_square, outliers, cap, n_out, mean_sq);
+}
+
+mage_status mage_ba_get_poses(mage_ba* b, float* pos3, float* r9)
+{
+    MAGE_REQUIRE(b && pos3 && r9, MAGE_EINVAL, "null argument");
+    (void)hipSetDevice(b->device);
+    mage_status r = b->sync_host_state();
+    if (r != MAGE_OK) return r;
+    for (int c = 0; c < b->C; c++) {
+        // GetPose (BundlerLib.cpp:457-465): t, R of the normalised quaternion, cast to float
+        double q[4] = {b->q[4 * c], b->q[4 * c + 1], b->q[4 * c + 2], b->q[4 * c + 3]};
+        double nn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        for (double& v : q) v /= nn;
+        double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+        double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+        double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+        double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+        const double R[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz),
+                             tyz - twx,       txz - twy, tyz + twx, 1 - (txx + tyy)};
+        for (int k = 0; k < 3; k++) pos3[3 * c + k] = (float)b->t[3 * c + k];
+        for (int rr = 0; rr < 3; rr++)
+            for (int cc = 0; cc < 3; cc++) r9[9 * c + cc * 3 + rr] = (float)R[rr * 3 + cc];
+    }
+    return MAGE_OK;
+}
+
+mage_status mage_ba_get_points(mage_ba* b, float* xyz)
+{
+    MAGE_REQUIRE(b && xyz, MAGE_EINVAL, "null argument");
+    (void)hipSetDevice(b->device);
+    mage_status r = b->sync_host_state();
+    if (r != MAGE_OK) return r;
+    for (int i = 0; i < 3 * b->P; i++) xyz[i] = (float)b->p[i];
+    return MAGE_OK;
+}
+
+mage_status mage_ba_get_state_f64(mage_ba* b, double* qt7, double* xyz)
+{
+    MAGE_REQUIRE(b, MAGE_EINVAL, "null handle");
+    (void)hipSetDevice(b->device);
+    mage_status r = b->sync_host_state();
+    if (r != MAGE_OK) return r;
+    if (qt7)
+        for (int c = 0; c < b->C; c++) {
+            for (int k = 0; k < 4; k++) qt7[7 * c + k] = b->q[4 * c + k];
+            for (int k = 0; k < 3; k++) qt7[7 * c + 4 + k] = b->t[3 * c + k];
+        }
+    if (xyz)
+        for (int i = 0; i < 3 * b->P; i++) xyz[i] = b->p[i];
+    return MAGE_OK;
+}
+
+mage_status mage_ba_get_stats(mage_ba* b, mage_ba_stats* s)
+{
+    MAGE_REQUIRE(b && s, MAGE_EINVAL, "null argument");
+    *s = b->stats;
+    return MAGE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,68 @@
+// common.hpp — shared host/device helpers for the MI355X hot-path library (libmage_hot.so).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/mage_hot.h"
+
+namespace mage {
+
+// Thread-local last error (mage_last_error()).
+void set_error(const std::string& msg);
+const char* last_error();
+
+#define MAGE_HIP(expr)                                                                      \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) {                                                             \
+            ::mage::set_error(std::string(#expr " failed: ") + hipGetErrorString(_e) +     \
+                              " at " + __FILE__ + ":" + std::to_string(__LINE__));          \
+            return MAGE_EDEVICE;                                                            \
+        }                                                                                   \
+    } while (0)
+
+#define MAGE_REQUIRE(cond, code, msg)                                                       \
+    do {                                                                                    \
+        if (!(cond)) {                                                                      \
+            ::mage::set_error(msg);                                                         \
+            return code;                                                                    \
+        }                                                                                   \
+    } while (0)
+
+// Selects `device` and verifies it is a gfx950 part; returns MAGE_OK or MAGE_EDEVICE.
+mage_status bind_device(int device);
+
+// Grow-only device buffer.
+struct DeviceBuffer {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    mage_status reserve(size_t n) {
+        if (n <= bytes) return MAGE_OK;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        if (hipMalloc(&ptr, n) != hipSuccess) {
+            set_error("hipMalloc of " + std::to_string(n) + " bytes failed");
+            return MAGE_ENOMEM;
+        }
+        bytes = n;
+        return MAGE_OK;
+    }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as() const {
+        return static_cast<T*>(ptr);
+    }
+};
+
+constexpr int kWave = 64;
+
+}  // namespace mage

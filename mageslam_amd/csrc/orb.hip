@@ -1,0 +1,875 @@
+// orb.hip — ORB extraction on MI355X (gfx950): FAST-9/16 + NMS, retain + grid ANMS, fused
+// Gaussian blur + pre-rotated BRIEF.  Replaces OrbDetector::DetectAndCompute
+// (Core/MAGESLAM/Source/Image/OpenCVModified.cpp:771-886).
+//
+// Pipeline for a batch of B frames (all device resident), three launches:
+//   1. fast_nms_kernel  grid (W/64, H/16, B): 64x16 tile + 4-px halo staged in LDS, FAST score
+//      for a 66x18 region, strict 3x3 NMS, border filter, per-tile LDS compaction, one global
+//      atomic per tile.  Candidates are packed u32 (y<<20 | x<<8 | score).
+//   2. select_kernel    grid (B), 1024 threads: 256-bin histogram -> RetainBestFeatures cut,
+//      bbox, 32x32 cell counting sort, per-item ANMS ring search, 64-bit key bitonic sort in LDS,
+//      emits keypoints in canonical order (ANMS rank r desc, strength desc, raster asc).
+//   3. describe_kernel  grid (cap/4, B), one wave per keypoint: raw window -> separable 8U
+//      Gaussian (OpenCV Q8 taps) in LDS -> 256 tests -> four 64-bit ballots = the descriptor.
+// The whole-frame blur of the reference (OpenCVModified.cpp:853-865) is replaced by blurring
+// only the windows the descriptors sample: same values, no full-frame write/read.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+#include "orb_tables.hpp"
+
+namespace mage {
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// 1. FAST-9/16 + NMS
+// ------------------------------------------------------------------------------------------
+constexpr int TW = 64, TH = 16, HALO = 4;
+constexpr int LW = TW + 2 * HALO;  // 72
+constexpr int LH = TH + 2 * HALO;  // 24
+constexpr int SW = TW + 2, SH = TH + 2;
+constexpr int FAST_THREADS = 256;
+
+struct FastParams {
+    int w, h, stride;
+    long long pitch;
+    int threshold;
+    int xlo, xhi, ylo, yhi;  // emission window (FAST range ∩ RunByImageBorder)
+    unsigned cand_cap;
+};
+
+// Ring of FAST_t<16> (makeOffsets, OpenCVModified.cpp:890-921) as (dx, dy).
+__device__ __constant__ signed char c_ring[16][2] = {
+    {0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+    {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+// True if the cyclic 16-bit mask has >= 9 consecutive set bits (count > K=8, :1429-1478).
+__device__ __forceinline__ bool has_run9(unsigned m16)
+{
+    unsigned m = m16 | (m16 << 16);
+    unsigned a = m & (m >> 1);
+    a &= a >> 2;
+    a &= a >> 4;
+    a &= m >> 8;
+    return (a & 0xFFFFu) != 0u;
+}
+
+// FAST score of the pixel at p (LDS, row stride LW): cornerScore<16> if it passes the segment
+// test, else 0.  cornerScore = max over the 16 cyclic 9-arcs of min(v - x) and of min(x - v),
+// minus one (OpenCVModified.cpp:927-1071: the scalar and SSE2 branches agree on corners).
+__device__ __forceinline__ int fast_score(const uint8_t* p, int t)
+{
+    const int v = p[0];
+    int d[16];
+    unsigned bright = 0, dark = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int x = p[c_ring[k][1] * LW + c_ring[k][0]];
+        d[k] = v - x;
+        dark |= (unsigned)(x < v - t) << k;
+        bright |= (unsigned)(x > v + t) << k;
+    }
+    if (!has_run9(dark) && !has_run9(bright)) return 0;
+    int m2[16], m4[16], x2[16], x4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m2[k] = min(d[k], d[(k + 1) & 15]);
+        x2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m4[k] = min(m2[k], m2[(k + 2) & 15]);
+        x4[k] = max(x2[k], x2[(k + 2) & 15]);
+    }
+    int a = -1000, b = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int m8 = min(m4[k], m4[(k + 4) & 15]);
+        int x8 = max(x4[k], x4[(k + 4) & 15]);
+        a = max(a, min(m8, d[(k + 8) & 15]));
+        b = min(b, max(x8, d[(k + 8) & 15]));
+    }
+    return max(a, -b) - 1;
+}
+
+__device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const FastParams& p,
+                                          uint8_t (*img)[LW])
+{
+    const int gx0 = blockIdx.x * TW - HALO, gy0 = blockIdx.y * TH - HALO;
+    for (int i = threadIdx.x; i < LH * LW; i += FAST_THREADS) {
+        int r = i / LW, c = i - r * LW;
+        int gx = gx0 + c, gy = gy0 + r;
+        uint8_t v = 0;
+        if (gx >= 0 && gx < p.w && gy >= 0 && gy < p.h) v = src[(long long)gy * p.stride + gx];
+        img[r][c] = v;
+    }
+}
+
+__global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* __restrict__ frames,
+                                                                FastParams p,
+                                                                uint32_t* __restrict__ cand,
+                                                                uint32_t* __restrict__ counts)
+{
+    __shared__ uint8_t img[LH][LW];
+    __shared__ uint8_t sc[SH][SW + 2];
+    __shared__ uint32_t list[TW * TH / 2];
+    __shared__ uint32_t s_cnt, s_base;
+    const int f = blockIdx.z;
+    load_tile(frames + (long long)f * p.pitch, p, img);
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < SH * SW; i += FAST_THREADS) {
+        int sy = i / SW, sx = i - sy * SW;
+        int X = blockIdx.x * TW - 1 + sx, Y = blockIdx.y * TH - 1 + sy;
+        int s = 0;
+        if (X >= 3 && X <= p.w - 4 && Y >= 3 && Y <= p.h - 4) s = fast_score(&img[sy + 3][sx + 3], p.threshold);
+        sc[sy][sx] = (uint8_t)s;
+    }
+    __syncthreads();
+    // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter
+    for (int i = threadIdx.x; i < TW * TH; i += FAST_THREADS) {
+        int oy = i / TW, ox = i - oy * TW;
+        int X = blockIdx.x * TW + ox, Y = blockIdx.y * TH + oy;
+        int s = sc[oy + 1][ox + 1];
+        bool keep = s > 0 && X >= p.xlo && X <= p.xhi && Y >= p.ylo && Y <= p.yhi &&
+                    s > sc[oy][ox] && s > sc[oy][ox + 1] && s > sc[oy][ox + 2] &&
+                    s > sc[oy + 1][ox] && s > sc[oy + 1][ox + 2] && s > sc[oy + 2][ox] &&
+                    s > sc[oy + 2][ox + 1] && s > sc[oy + 2][ox + 2];
+        if (keep) {
+            uint32_t slot = atomicAdd(&s_cnt, 1u);
+            list[slot] = ((uint32_t)Y << 20) | ((uint32_t)X << 8) | (uint32_t)s;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&counts[f], s_cnt) : 0u;
+    __syncthreads();
+    uint32_t* out = cand + (long long)f * p.cand_cap;
+    for (uint32_t k = threadIdx.x; k < s_cnt; k += FAST_THREADS) {
+        uint32_t idx = s_base + k;
+        if (idx < p.cand_cap) out[idx] = list[k];
+    }
+}
+
+__global__ __launch_bounds__(FAST_THREADS) void fast_score_map_kernel(const uint8_t* __restrict__ src,
+                                                                      FastParams p,
+                                                                      uint8_t* __restrict__ score)
+{
+    __shared__ uint8_t img[LH][LW];
+    load_tile(src, p, img);
+    __syncthreads();
+    for (int i = threadIdx.x; i < TW * TH; i += FAST_THREADS) {
+        int oy = i / TW, ox = i - oy * TW;
+        int X = blockIdx.x * TW + ox, Y = blockIdx.y * TH + oy;
+        if (X >= p.w || Y >= p.h) continue;
+        int s = 0;
+        if (X >= 3 && X <= p.w - 4 && Y >= 3 && Y <= p.h - 4) s = fast_score(&img[oy + HALO][ox + HALO], p.threshold);
+        score[(long long)Y * p.w + X] = (uint8_t)s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 2. Retain + ANMS + canonical ordering
+// ------------------------------------------------------------------------------------------
+constexpr int SEL_THREADS = 1024;
+constexpr int KMAX = 8192;     // retained items handled in LDS
+constexpr int CELLMAX = 4096;  // grid cells (NumCellsX * NumCellsY)
+
+struct SelectParams {
+    int w, h;
+    unsigned cand_cap;
+    int nfeatures;
+    int max_num;  // (int)(nfeatures * FeatureFactor)  (ComputeKeyPoints :723)
+    unsigned out_cap;
+    int fast_threshold;
+    float feature_strength;
+    int strong;
+    float min_r, max_r;
+    int cells_x, cells_y;
+    float kp_size;
+};
+
+enum : uint32_t { ST_KMAX = 1u, ST_CELLS = 2u };
+
+__device__ __forceinline__ int cand_x(uint32_t c) { return (int)((c >> 8) & 0xFFFu); }
+__device__ __forceinline__ int cand_y(uint32_t c) { return (int)(c >> 20); }
+__device__ __forceinline__ int cand_s(uint32_t c) { return (int)(c & 0xFFu); }
+
+// Descending bitonic sort of keys[0..P), P a power of two.
+__device__ void bitonic_desc(unsigned long long* keys, int P)
+{
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += SEL_THREADS) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    unsigned long long a = keys[i], b = keys[ixj];
+                    bool desc = (i & k) == 0;
+                    if (desc ? (a < b) : (a > b)) {
+                        keys[i] = b;
+                        keys[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __restrict__ cand,
+                                                             const uint32_t* __restrict__ counts,
+                                                             SelectParams p,
+                                                             mage_keypoint* __restrict__ kp_out,
+                                                             uint32_t* __restrict__ xy_out,
+                                                             uint32_t* __restrict__ n_out,
+                                                             uint32_t* __restrict__ status)
+{
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t items[KMAX];
+    __shared__ uint32_t sorted[KMAX];
+    __shared__ uint32_t cellStart[CELLMAX + 1];
+    __shared__ unsigned long long keys[KMAX];
+    __shared__ int s_cut, s_K, s_minX, s_maxX, s_minY, s_maxY, s_minS, s_gmax, s_mcd2, s_mode;
+    __shared__ float s_rob, s_robInv;
+
+    const int f = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint32_t* C = cand + (long long)f * p.cand_cap;
+    const int n0 = (int)min(counts[f], p.cand_cap);
+    for (int i = tid; i < 256; i += SEL_THREADS) hist[i] = 0;
+    if (tid == 0) {
+        s_K = 0;
+        s_minX = s_minY = s_minS = 0x7FFFFFFF;
+        s_maxX = s_maxY = -1;
+    }
+    __syncthreads();
+    for (int i = tid; i < n0; i += SEL_THREADS) atomicAdd(&hist[cand_s(C[i])], 1u);
+    __syncthreads();
+
+    const int N = p.nfeatures;
+    if (tid == 0) {
+        if (n0 <= N) {
+            s_mode = 0;  // no retain / ANMS: keep all, raster order
+            s_cut = 0;
+        } else {
+            // RetainBestFeatures (OpenCVModified.cpp:571-617)
+            int minThreshold = p.fast_threshold;
+            int minNumThreshold = minThreshold;
+            int num = 0;
+            for (int i = 255; i >= minThreshold; i--) {
+                num += (int)hist[i];
+                if (num >= N) {
+                    minNumThreshold = i;
+                    break;
+                }
+            }
+            int lower = max((int)__fmul_rn((float)minNumThreshold, p.feature_strength), minThreshold);
+            num = 0;
+            int i;
+            for (i = 255; i >= lower; i--) {
+                num += (int)hist[i];
+                if (num >= p.max_num) break;
+            }
+            s_cut = i < lower ? lower : i;
+            s_mode = 1;
+        }
+    }
+    __syncthreads();
+    const int cut = s_cut;
+    for (int i = tid; i < n0; i += SEL_THREADS) {
+        uint32_t c = C[i];
+        if (cand_s(c) >= cut) {
+            int pos = atomicAdd(&s_K, 1);
+            if (pos < KMAX) items[pos] = c;
+        }
+    }
+    __syncthreads();
+    int K = s_K;
+    if (K > KMAX) {
+        if (tid == 0) atomicOr(status, ST_KMAX);
+        K = KMAX;
+    }
+    int P = 1;
+    while (P < K) P <<= 1;
+    const bool anms = s_mode == 1 && N <= K;  // AdaptiveNonMaximalSuppresion early return :177-180
+
+    if (!anms) {
+        for (int i = tid; i < P; i += SEL_THREADS) {
+            unsigned long long key = 0;
+            if (i < K) {
+                uint32_t c = items[i];
+                uint32_t raster = (uint32_t)cand_y(c) * (uint32_t)p.w + (uint32_t)cand_x(c);
+                key = ((unsigned long long)(0xFFFFFFFFu - raster) << 8) | (unsigned long long)cand_s(c);
+            }
+            keys[i] = key;
+        }
+        __syncthreads();
+        bitonic_desc(keys, P);
+    } else {
+        const int numX = p.cells_x, numY = p.cells_y, ncell = numX * numY;
+        if (ncell > CELLMAX) {
+            if (tid == 0) {
+                atomicOr(status, ST_CELLS);
+                n_out[f] = 0;
+            }
+            return;
+        }
+        for (int i = tid; i < K; i += SEL_THREADS) {
+            uint32_t c = items[i];
+            atomicMin(&s_minX, cand_x(c));
+            atomicMax(&s_maxX, cand_x(c));
+            atomicMin(&s_minY, cand_y(c));
+            atomicMax(&s_maxY, cand_y(c));
+            atomicMin(&s_minS, cand_s(c));
+        }
+        for (int i = tid; i <= ncell; i += SEL_THREADS) cellStart[i] = 0;
+        __syncthreads();
+        const int minX = s_minX, maxX = s_maxX, minY = s_minY, maxY = s_maxY;
+        if (tid == 0) {
+            // robustness factor (OpenCVModified.cpp:205-214), float arithmetic as written
+            const int t = p.fast_threshold;
+            float hi = __fsub_rn((float)p.strong, (float)t);
+            float val = fminf(hi, fmaxf(0.0f, __fsub_rn((float)s_minS, (float)t)));
+            float range = fmaxf(0.0f, __fsub_rn(p.max_r, p.min_r));
+            float rob = __fsub_rn(p.max_r, __fmul_rn(__fdiv_rn(val, (float)(p.strong - t)), range));
+            s_rob = rob;
+            s_robInv = __fdiv_rn(1.0f, rob);
+            s_gmax = (int)(((double)(maxX - minX)) * ((double)(maxY - minY)) / (double)N);
+            int dx = max((maxX - minX) / numX, 1), dy = max((maxY - minY) / numY, 1);
+            s_mcd2 = min(dx, dy) * min(dx, dy);
+        }
+        // counting sort by cell
+        for (int i = tid; i < K; i += SEL_THREADS) {
+            uint32_t c = items[i];
+            int cx = (cand_x(c) - minX) * numX / (maxX + 1 - minX);
+            int cy = (cand_y(c) - minY) * numY / (maxY + 1 - minY);
+            atomicAdd(&cellStart[cy * numX + cx + 1], 1u);
+        }
+        __syncthreads();
+        if (tid < kWave) {  // exclusive scan of ncell+1 entries by one wave
+            const int per = (ncell + 1 + kWave - 1) / kWave;
+            const int b0 = tid * per, b1 = min(b0 + per, ncell + 1);
+            uint32_t s = 0;
+            for (int i = b0; i < b1; i++) s += cellStart[i];
+            uint32_t incl = s;
+            for (int off = 1; off < kWave; off <<= 1) {
+                uint32_t o = __shfl_up(incl, off);
+                if (tid >= off) incl += o;
+            }
+            uint32_t run = incl - s;
+            for (int i = b0; i < b1; i++) {
+                run += cellStart[i];
+                cellStart[i] = run;
+            }
+        }
+        __syncthreads();
+        uint32_t* fill = reinterpret_cast<uint32_t*>(keys);  // cell fill cursors (keys unused yet)
+        for (int i = tid; i < ncell; i += SEL_THREADS) fill[i] = cellStart[i];
+        __syncthreads();
+        for (int i = tid; i < K; i += SEL_THREADS) {
+            uint32_t c = items[i];
+            int cx = (cand_x(c) - minX) * numX / (maxX + 1 - minX);
+            int cy = (cand_y(c) - minY) * numY / (maxY + 1 - minY);
+            uint32_t pos = atomicAdd(&fill[cy * numX + cx], 1u);
+            sorted[pos] = c;
+        }
+        __syncthreads();
+        const float rob = s_rob, robInv = s_robInv;
+        const int gmax = s_gmax, mcd2 = s_mcd2;
+        unsigned long long mykeys[KMAX / SEL_THREADS];
+#pragma unroll
+        for (int q = 0; q < KMAX / SEL_THREADS; q++) {
+            int i = tid + q * SEL_THREADS;
+            unsigned long long key = 0;
+            if (i < K) {
+                uint32_t c = items[i];
+                const int x = cand_x(c), y = cand_y(c), s = cand_s(c);
+                const int cx = (x - minX) * numX / (maxX + 1 - minX);
+                const int cy = (y - minY) * numY / (maxY + 1 - minY);
+                const float strength = (float)s;
+                const float sth = strength >= 0 ? __fadd_rn(__fmul_rn(strength, rob), 0.002f)
+                                                 : __fadd_rn(__fmul_rn(strength, robInv), 0.002f);
+                int minR2 = gmax;
+                // ring search (OpenCVModified.cpp:266-326)
+                for (int d = 0; max(0, d - 1) * max(0, d - 1) * mcd2 < minR2; d++) {
+                    for (int yy = -d; yy <= d; yy++) {
+                        const int cYY = cy + yy;
+                        if (cYY < 0 || cYY >= numY) continue;
+                        const bool edgeRow = (yy == -d || yy == d);
+                        const int step = edgeRow ? 1 : max(2 * d, 1);
+                        for (int xx = -d; xx <= d; xx += step) {
+                            const int cXX = cx + xx;
+                            if (cXX < 0 || cXX >= numX) continue;
+                            const int cell = cYY * numX + cXX;
+                            const uint32_t e = cellStart[cell + 1];
+                            for (uint32_t qq = cellStart[cell]; qq < e; qq++) {
+                                uint32_t o = sorted[qq];
+                                if ((float)cand_s(o) > sth) {
+                                    int ddx = x - cand_x(o), ddy = y - cand_y(o);
+                                    minR2 = min(minR2, ddx * ddx + ddy * ddy);
+                                }
+                            }
+                        }
+                    }
+                }
+                uint32_t raster = (uint32_t)y * (uint32_t)p.w + (uint32_t)x;
+                key = ((unsigned long long)(uint32_t)minR2 << 40) | ((unsigned long long)s << 32) |
+                      (unsigned long long)(0xFFFFFFFFu - raster);
+            }
+            mykeys[q] = key;
+        }
+        __syncthreads();  // fill cursors (aliasing keys) are dead now
+#pragma unroll
+        for (int q = 0; q < KMAX / SEL_THREADS; q++) {
+            int i = tid + q * SEL_THREADS;
+            if (i < P) keys[i] = mykeys[q];
+        }
+        __syncthreads();
+        bitonic_desc(keys, P);
+    }
+
+    int nout = anms ? min(N, K) : K;
+    nout = min(nout, (int)p.out_cap);  // ImageData::Insert truncation (ImageData.h:65-70)
+    mage_keypoint* kp = kp_out + (long long)f * p.out_cap;
+    uint32_t* xy = xy_out + (long long)f * p.out_cap;
+    for (int i = tid; i < nout; i += SEL_THREADS) {
+        unsigned long long key = keys[i];
+        uint32_t raster, s;
+        if (anms) {
+            raster = 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull);
+            s = (uint32_t)((key >> 32) & 0xFFu);
+        } else {
+            raster = 0xFFFFFFFFu - (uint32_t)(key >> 8);
+            s = (uint32_t)(key & 0xFFu);
+        }
+        uint32_t y = raster / (uint32_t)p.w, x = raster - y * (uint32_t)p.w;
+        mage_keypoint k;
+        k.x = (float)x;
+        k.y = (float)y;
+        k.size = p.kp_size;
+        k.angle = 0.0f;
+        k.response = (float)s;
+        k.octave = 0;
+        k.class_id = -1;
+        kp[i] = k;
+        xy[i] = (y << 16) | x;
+    }
+    if (tid == 0) n_out[f] = (uint32_t)nout;
+}
+
+// ------------------------------------------------------------------------------------------
+// 3. Blur-in-window + pre-rotated BRIEF
+// ------------------------------------------------------------------------------------------
+constexpr int DESC_WAVES = 4;
+constexpr int RMAX = 18;  // max |pattern offset| over both tables and all rotations
+constexpr int KHMAX = 7;  // max Gaussian half-size (ksize <= 15)
+constexpr int RAWD = 2 * (RMAX + KHMAX) + 1;
+constexpr int BD_MAX = 2 * RMAX + 1;
+
+struct DescParams {
+    int w, h, stride;
+    long long pitch;
+    unsigned out_cap;
+    int R;      // sampling radius of the pattern rotations in use
+    int ksize;  // Gaussian taps (<= 1: no blur)
+    int taps[2 * KHMAX + 1];
+};
+
+__device__ __forceinline__ int reflect101(int i, int n)
+{
+    if (n == 1) return 0;
+    while ((unsigned)i >= (unsigned)n) i = i < 0 ? -i : 2 * n - 2 - i;
+    return i;
+}
+
+__global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
+    const uint8_t* __restrict__ frames, DescParams p, const uint32_t* __restrict__ xy_in,
+    const uint32_t* __restrict__ n_in, const int8_t* __restrict__ pattern,
+    uint8_t* __restrict__ desc_out)
+{
+    __shared__ uint8_t raw[DESC_WAVES][RAWD * RAWD];
+    __shared__ int rowp[DESC_WAVES][RAWD * BD_MAX];
+    __shared__ uint8_t blur[DESC_WAVES][BD_MAX * BD_MAX];
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int k = blockIdx.x * DESC_WAVES + wave;
+    const bool live = k < (int)n_in[f];
+    const int kh = p.ksize > 1 ? p.ksize / 2 : 0;
+    const int R = p.R, Rr = R + kh, rawDim = 2 * Rr + 1, bd = 2 * R + 1;
+    int cx = 0, cy = 0;
+    if (live) {
+        uint32_t v = xy_in[(long long)f * p.out_cap + k];
+        cx = (int)(v & 0xFFFFu);
+        cy = (int)(v >> 16);
+        const uint8_t* src = frames + (long long)f * p.pitch;
+        for (int i = lane; i < rawDim * rawDim; i += kWave) {
+            int r = i / rawDim, c = i - r * rawDim;
+            int gy = reflect101(cy - Rr + r, p.h), gx = reflect101(cx - Rr + c, p.w);
+            raw[wave][i] = src[(long long)gy * p.stride + gx];
+        }
+    }
+    __syncthreads();
+    if (live && kh > 0) {
+        for (int i = lane; i < rawDim * bd; i += kWave) {
+            int r = i / bd, c = i - r * bd;
+            const uint8_t* q = &raw[wave][r * rawDim + c];
+            int s = 0;
+            for (int t = 0; t < p.ksize; t++) s += p.taps[t] * q[t];
+            rowp[wave][i] = s;
+        }
+    }
+    __syncthreads();
+    if (live) {
+        for (int i = lane; i < bd * bd; i += kWave) {
+            int r = i / bd, c = i - r * bd;
+            int v;
+            if (kh > 0) {
+                int s = 0;
+                for (int t = 0; t < p.ksize; t++) s += p.taps[t] * rowp[wave][(r + t) * bd + c];
+                v = (s + (1 << 15)) >> 16;
+                v = v < 0 ? 0 : (v > 255 ? 255 : v);
+            } else {
+                v = raw[wave][r * rawDim + c];
+            }
+            blur[wave][i] = (uint8_t)v;
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    // rotation 0: angle = 0 without orientation (OpenCVModified.cpp:748-754, :522)
+    const char4* pat = reinterpret_cast<const char4*>(pattern);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
+#pragma unroll
+    for (int chunk = 0; chunk < 4; chunk++) {
+        char4 e = pat[chunk * kWave + lane];  // (x0, y0, x1, y1) of bit 64*chunk + lane
+        int t0 = blur[wave][(R + e.y) * bd + R + e.x];
+        int t1 = blur[wave][(R + e.w) * bd + R + e.z];
+        unsigned long long m = __ballot(t0 < t1);
+        if (lane == 0) dst[chunk] = m;
+    }
+}
+
+__global__ void synth_frames_kernel(uint8_t* __restrict__ out, int w, int h, long long pitch,
+                                    unsigned t0, unsigned long long seed)
+{
+    const int f = blockIdx.z;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= w) return;
+    const unsigned long long t = (unsigned long long)(t0 + f);
+    const unsigned long long u = (unsigned long long)x + 3ull * t, v = (unsigned long long)y + 2ull * t;
+    auto mix = [](unsigned long long z) {
+        z += 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    const unsigned long long K1 = 0x9E3779B97F4A7C15ull, K2 = 0xC2B2AE3D27D4EB4Full;
+    unsigned long long base = mix(seed ^ ((u >> 3) * K1) ^ ((v >> 3) * K2));
+    unsigned long long fine = mix(seed ^ 0xA5A5A5A5ull ^ ((u / 3) * K1) ^ ((v / 3) * K2));
+    int g = (int)(base >> 56) + (int)((fine >> 56) % 49ull) - 24;
+    out[(long long)f * pitch + (long long)y * w + x] = (uint8_t)(g < 0 ? 0 : (g > 255 ? 255 : g));
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------
+
+struct OrbDetector {
+    mage_orb_settings s{};
+    int device = 0;
+    int taps[2 * KHMAX + 1] = {0};
+    int R = 7;
+    DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n;
+};
+
+namespace {
+
+// cv::getGaussianKernel(ksize, 2, CV_32F) -> convertTo(CV_32S, 1<<8) (OpenCV 3.4.0
+// createSeparableLinearFilter, 8U smoothing path; see DESIGN.md §Blur for why this path).
+void gaussian_taps(int ksize, double sigma, int* taps)
+{
+    std::vector<float> cf(ksize);
+    double sum = 0;
+    double sg = sigma > 0 ? sigma : ((ksize - 1) * 0.5 - 1) * 0.3 + 0.8;
+    double scale2 = -0.5 / (sg * sg);
+    for (int i = 0; i < ksize; i++) {
+        double x = i - (ksize - 1) * 0.5;
+        cf[i] = (float)std::exp(scale2 * x * x);
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < ksize; i++) {
+        cf[i] = (float)(cf[i] * sum);
+        taps[i] = (int)std::lrint((double)cf[i] * 256.0);
+    }
+}
+
+mage_status validate(const OrbDetector* o, int w, int h, int stride)
+{
+    MAGE_REQUIRE(o != nullptr, MAGE_EINVAL, "null detector");
+    MAGE_REQUIRE(w > 0 && h > 0 && stride >= w, MAGE_EINVAL, "bad image geometry");
+    MAGE_REQUIRE(w <= 4095 && h <= 4095, MAGE_EUNSUPPORTED, "frames up to 4095x4095 supported");
+    return MAGE_OK;
+}
+
+mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, int w, int h,
+                      int stride, long long pitch, mage_keypoint* d_kp, uint8_t* d_desc,
+                      uint32_t cap, uint32_t* d_n, hipStream_t st)
+{
+    const mage_orb_settings& s = o->s;
+    const unsigned candCap = (unsigned)(((w + 1) / 2) * ((h + 1) / 2));
+    mage_status r;
+    if ((r = o->cand.reserve((size_t)batch * candCap * 4)) != MAGE_OK) return r;
+    if ((r = o->counts.reserve((size_t)batch * 4)) != MAGE_OK) return r;
+    if ((r = o->xy.reserve((size_t)batch * std::max(cap, 1u) * 4)) != MAGE_OK) return r;
+    if ((r = o->status.reserve(4)) != MAGE_OK) return r;
+    MAGE_HIP(hipMemsetAsync(o->counts.ptr, 0, (size_t)batch * 4, st));
+
+    const int half = (int)s.patch_size / 2;
+    const int border = half;  // RunByImageBorder(halfPatchSize) without orientation (:712)
+    FastParams fp{};
+    fp.w = w;
+    fp.h = h;
+    fp.stride = stride;
+    fp.pitch = pitch;
+    fp.threshold = std::min(std::max((int)s.fast_threshold, 0), 255);
+    fp.xlo = std::max(3, border);
+    fp.xhi = std::min(w - 4, w - border - 1);
+    fp.ylo = std::max(3, border);
+    fp.yhi = std::min(h - 4, h - border - 1);
+    if (h <= 2 * border || w <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
+    fp.cand_cap = candCap;
+    dim3 g1((w + TW - 1) / TW, (h + TH - 1) / TH, batch);
+    hipLaunchKernelGGL(fast_nms_kernel, g1, dim3(FAST_THREADS), 0, st, d_frames, fp,
+                       o->cand.as<uint32_t>(), o->counts.as<uint32_t>());
+    MAGE_HIP(hipGetLastError());
+
+    SelectParams sp{};
+    sp.w = w;
+    sp.h = h;
+    sp.cand_cap = candCap;
+    sp.nfeatures = (int)s.nfeatures;  // nfeaturesPerLevel[0] for one level (:659-672)
+    sp.max_num = (int)((float)s.nfeatures * s.feature_factor);
+    sp.out_cap = cap;
+    sp.fast_threshold = (int)s.fast_threshold;
+    sp.feature_strength = s.feature_strength;
+    sp.strong = s.strong_response;
+    sp.min_r = s.min_robust_factor;
+    sp.max_r = s.max_robust_factor;
+    sp.cells_x = s.num_cells_x;
+    sp.cells_y = s.num_cells_y;
+    sp.kp_size = (float)s.patch_size * 1.0f;
+    hipLaunchKernelGGL(select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, o->cand.as<uint32_t>(),
+                       o->counts.as<uint32_t>(), sp, d_kp, o->xy.as<uint32_t>(), d_n,
+                       o->status.as<uint32_t>());
+    MAGE_HIP(hipGetLastError());
+
+    if (cap > 0) {
+        DescParams dp{};
+        dp.w = w;
+        dp.h = h;
+        dp.stride = stride;
+        dp.pitch = pitch;
+        dp.out_cap = cap;
+        dp.R = o->R;
+        dp.ksize = (int)s.gaussian_kernel_size;
+        for (int i = 0; i < 2 * KHMAX + 1; i++) dp.taps[i] = o->taps[i];
+        dim3 g3((cap + DESC_WAVES - 1) / DESC_WAVES, batch);
+        hipLaunchKernelGGL(describe_kernel, g3, dim3(DESC_WAVES * kWave), 0, st, d_frames, dp,
+                           o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
+        MAGE_HIP(hipGetLastError());
+    }
+    return MAGE_OK;
+}
+
+mage_status check_status(OrbDetector* o, hipStream_t st)
+{
+    uint32_t flags = 0;
+    MAGE_HIP(hipMemcpyAsync(&flags, o->status.ptr, 4, hipMemcpyDeviceToHost, st));
+    MAGE_HIP(hipStreamSynchronize(st));
+    MAGE_REQUIRE(!(flags & ST_KMAX), MAGE_ECAPACITY, "retained keypoints exceed the LDS capacity (8192)");
+    MAGE_REQUIRE(!(flags & ST_CELLS), MAGE_EUNSUPPORTED, "NumCellsX*NumCellsY > 4096");
+    return MAGE_OK;
+}
+
+}  // namespace
+}  // namespace mage
+
+using mage::OrbDetector;
+
+struct mage_orb : OrbDetector {};
+
+extern "C" {
+
+mage_status mage_orb_create(const mage_orb_settings* settings, int device, mage_orb** out)
+{
+    MAGE_REQUIRE(settings && out, MAGE_EINVAL, "null argument");
+    *out = nullptr;
+    const mage_orb_settings& s = *settings;
+    // CV_Assert(m_patchSize >= 2) (OpenCVModified.cpp:776)
+    MAGE_REQUIRE(s.patch_size >= 2, MAGE_EINVAL, "patchSize must be >= 2");
+    MAGE_REQUIRE(s.gaussian_kernel_size <= 1 || (s.gaussian_kernel_size % 2 == 1 && s.gaussian_kernel_size <= 15),
+                 MAGE_EINVAL, "GaussianKernelSize must be odd and <= 15");
+    MAGE_REQUIRE(s.num_cells_x >= 1 && s.num_cells_y >= 1, MAGE_EINVAL, "NumCells must be >= 1");
+    MAGE_REQUIRE(s.nlevels == 1, MAGE_EUNSUPPORTED, "NumLevels > 1 not implemented yet");
+    MAGE_REQUIRE(!s.use_orientation, MAGE_EUNSUPPORTED, "UseOrientation not implemented yet");
+    MAGE_REQUIRE(s.patch_size == 15 || s.patch_size == 31, MAGE_EUNSUPPORTED,
+                 "only the pre-rotated patterns (PatchSize 15 / 31) are implemented");
+    mage_status r = mage::bind_device(device);
+    if (r != MAGE_OK) return r;
+    auto* o = new mage_orb();
+    o->s = s;
+    o->device = device;
+    if (s.gaussian_kernel_size > 1) mage::gaussian_taps((int)s.gaussian_kernel_size, 2.0, o->taps);
+    const int8_t* table = s.patch_size == 31 ? mage_bit_pattern_31_rotated : mage_bit_pattern_15_rotated;
+    int R = 0;
+    for (int i = 0; i < 1024; i++) R = std::max(R, std::abs((int)table[i]));  // rotation 0
+    o->R = R;
+    if ((r = o->pattern.reserve(30 * 1024)) != MAGE_OK) {
+        delete o;
+        return r;
+    }
+    if (hipMemcpy(o->pattern.ptr, table, 30 * 1024, hipMemcpyHostToDevice) != hipSuccess) {
+        delete o;
+        mage::set_error("pattern upload failed");
+        return MAGE_EDEVICE;
+    }
+    *out = o;
+    return MAGE_OK;
+}
+
+mage_status mage_orb_destroy(mage_orb* orb)
+{
+    if (!orb) return MAGE_OK;
+    for (auto* b : {&orb->pattern, &orb->cand, &orb->counts, &orb->xy, &orb->status, &orb->img,
+                    &orb->kp, &orb->desc, &orb->n})
+        b->release();
+    delete orb;
+    return MAGE_OK;
+}
+
+mage_status mage_orb_detect_and_compute_batch_device(mage_orb* orb, const uint8_t* d_frames,
+                                                     uint32_t batch, int32_t width,
+                                                     int32_t height, int32_t stride,
+                                                     int64_t frame_pitch, mage_keypoint* d_kp,
+                                                     uint8_t* d_desc, uint32_t cap,
+                                                     uint32_t* d_n, mage_stream stream)
+{
+    mage_status r = mage::validate(orb, width, height, stride);
+    if (r != MAGE_OK) return r;
+    if (batch == 0) return MAGE_OK;
+    MAGE_REQUIRE(d_frames && d_kp && d_n && (d_desc || cap == 0), MAGE_EINVAL, "null buffer");
+    MAGE_HIP(hipSetDevice(orb->device));
+    return mage::run_batch(orb, d_frames, batch, width, height, stride, frame_pitch, d_kp, d_desc,
+                           cap, d_n, (hipStream_t)stream);
+}
+
+mage_status mage_orb_detect_and_compute(mage_orb* orb, const uint8_t* img, int32_t width,
+                                        int32_t height, int32_t stride, mage_keypoint* kp,
+                                        uint8_t* desc, uint32_t cap, uint32_t* n)
+{
+    mage_status r = mage::validate(orb, width, height, stride);
+    if (r != MAGE_OK) return r;
+    MAGE_REQUIRE(img && n && (cap == 0 || (kp && desc)), MAGE_EINVAL, "null buffer");
+    MAGE_HIP(hipSetDevice(orb->device));
+    *n = 0;
+    const size_t bytes = (size_t)stride * height;
+    if ((r = orb->img.reserve(bytes)) != MAGE_OK) return r;
+    if ((r = orb->kp.reserve(sizeof(mage_keypoint) * std::max(cap, 1u))) != MAGE_OK) return r;
+    if ((r = orb->desc.reserve(32 * (size_t)std::max(cap, 1u))) != MAGE_OK) return r;
+    if ((r = orb->n.reserve(4)) != MAGE_OK) return r;
+    if ((r = orb->status.reserve(4)) != MAGE_OK) return r;
+    hipStream_t st = nullptr;
+    MAGE_HIP(hipMemsetAsync(orb->status.ptr, 0, 4, st));
+    MAGE_HIP(hipMemcpyAsync(orb->img.ptr, img, bytes, hipMemcpyHostToDevice, st));
+    r = mage::run_batch(orb, orb->img.as<uint8_t>(), 1, width, height, stride, (long long)bytes,
+                        orb->kp.as<mage_keypoint>(), orb->desc.as<uint8_t>(), cap,
+                        orb->n.as<uint32_t>(), st);
+    if (r != MAGE_OK) return r;
+    if ((r = mage::check_status(orb, st)) != MAGE_OK) return r;
+    uint32_t count = 0;
+    MAGE_HIP(hipMemcpy(&count, orb->n.ptr, 4, hipMemcpyDeviceToHost));
+    if (count) {
+        MAGE_HIP(hipMemcpy(kp, orb->kp.ptr, sizeof(mage_keypoint) * count, hipMemcpyDeviceToHost));
+        MAGE_HIP(hipMemcpy(desc, orb->desc.ptr, 32 * (size_t)count, hipMemcpyDeviceToHost));
+    }
+    *n = count;
+    return MAGE_OK;
+}
+
+mage_status mage_orb_status(mage_orb* orb, mage_stream stream)
+{
+    MAGE_REQUIRE(orb, MAGE_EINVAL, "null detector");
+    MAGE_HIP(hipSetDevice(orb->device));
+    if (!orb->status.ptr) return MAGE_OK;
+    return mage::check_status(orb, (hipStream_t)stream);
+}
+
+mage_status mage_orb_reset_status(mage_orb* orb, mage_stream stream)
+{
+    MAGE_REQUIRE(orb, MAGE_EINVAL, "null detector");
+    MAGE_HIP(hipSetDevice(orb->device));
+    mage_status r = orb->status.reserve(4);
+    if (r != MAGE_OK) return r;
+    MAGE_HIP(hipMemsetAsync(orb->status.ptr, 0, 4, (hipStream_t)stream));
+    return MAGE_OK;
+}
+
+mage_status mage_orb_fast_score_map(const uint8_t* img, int32_t width, int32_t height,
+                                    int32_t stride, int32_t threshold, uint8_t* score_map,
+                                    int device)
+{
+    MAGE_REQUIRE(img && score_map && width > 0 && height > 0 && stride >= width, MAGE_EINVAL, "bad arguments");
+    mage_status r = mage::bind_device(device);
+    if (r != MAGE_OK) return r;
+    mage::DeviceBuffer dimg, dscore;
+    if ((r = dimg.reserve((size_t)stride * height)) != MAGE_OK) return r;
+    if ((r = dscore.reserve((size_t)width * height)) != MAGE_OK) {
+        dimg.release();
+        return r;
+    }
+    mage::FastParams fp{};
+    fp.w = width;
+    fp.h = height;
+    fp.stride = stride;
+    fp.threshold = std::min(std::max((int)threshold, 0), 255);
+    hipError_t e = hipMemcpy(dimg.ptr, img, (size_t)stride * height, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        dim3 g((width + mage::TW - 1) / mage::TW, (height + mage::TH - 1) / mage::TH);
+        hipLaunchKernelGGL(mage::fast_score_map_kernel, g, dim3(mage::FAST_THREADS), 0, nullptr,
+                           dimg.as<uint8_t>(), fp, dscore.as<uint8_t>());
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(score_map, dscore.ptr, (size_t)width * height, hipMemcpyDeviceToHost);
+    dimg.release();
+    dscore.release();
+    if (e != hipSuccess) {
+        mage::set_error(std::string("fast score map: ") + hipGetErrorString(e));
+        return MAGE_EDEVICE;
+    }
+    return MAGE_OK;
+}
+
+mage_status mage_synth_frames_device(uint8_t* d_out, uint32_t count, int32_t width,
+                                     int32_t height, int64_t frame_pitch, uint32_t t0,
+                                     uint64_t seed, mage_stream stream)
+{
+    MAGE_REQUIRE(d_out && width > 0 && height > 0 && frame_pitch >= (int64_t)width * height,
+                 MAGE_EINVAL, "bad arguments");
+    if (count == 0) return MAGE_OK;
+    dim3 g((width + 255) / 256, height, count);
+    hipLaunchKernelGGL(mage::synth_frames_kernel, g, dim3(256), 0, (hipStream_t)stream, d_out,
+                       width, height, (long long)frame_pitch, t0, (unsigned long long)seed);
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}
+
+}  // extern "C"

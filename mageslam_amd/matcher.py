@@ -1,0 +1,56 @@
+"""Hamming matching — host mirror of FeatureMatcher's brute-force entry points.
+
+`Match` mirrors `unsigned Match(imageA, imageB, maskA, maskB, countA, countB, maxHammingDist,
+minHammingDifference, goodMatches)` (Core/MAGESLAM/Source/Tracking/FeatureMatcher.h:68-77):
+descriptors are passed directly instead of AnalyzedImage, masks are boolean arrays, and the
+result is an array of cv::DMatch-layout records.  `GetDescriptorDistance` mirrors
+FeatureMatcher.cpp:453-504.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import DM_DTYPE, check, ptr
+
+
+def GetDescriptorDistance(d0: np.ndarray, d1: np.ndarray) -> int:
+    a = np.ascontiguousarray(d0, np.uint8)
+    b = np.ascontiguousarray(d1, np.uint8)
+    if a.size != 32 or b.size != 32:
+        raise ValueError("ORB descriptors are 32 bytes")
+    return int(_lib.load().mage_hamming_distance(ptr(a), ptr(b)))
+
+
+def Match(descA: np.ndarray, descB: np.ndarray, maskA=None, maskB=None, maxHammingDist: int = 30,
+          minHammingDifference: int = 1) -> np.ndarray:
+    """Two-way brute-force match on the GPU; returns DMatch records in ascending A index.
+
+    Returns an empty array (and 0 matches) when either mask selects nothing
+    (FeatureMatcher.cpp:72-77)."""
+    da = np.ascontiguousarray(descA, np.uint8).reshape(-1, 32)
+    db = np.ascontiguousarray(descB, np.uint8).reshape(-1, 32)
+    ma = None if maskA is None else np.ascontiguousarray(np.asarray(maskA, bool), np.uint8)
+    mb = None if maskB is None else np.ascontiguousarray(np.asarray(maskB, bool), np.uint8)
+    if ma is not None and len(ma) != len(da):
+        raise ValueError("maskA length must equal the number of A descriptors")
+    if mb is not None and len(mb) != len(db):
+        raise ValueError("maskB length must equal the number of B descriptors")
+    cap = max(len(da), 1)
+    out = np.zeros(cap, DM_DTYPE)
+    n = C.c_uint32(0)
+    check(_lib.load().mage_hamming_match(ptr(da), len(da), ptr(ma), ptr(db), len(db), ptr(mb),
+                                         int(maxHammingDist), int(minHammingDifference), ptr(out),
+                                         cap, C.byref(n)))
+    return out[: n.value].copy()
+
+
+def match_batch_device(desc_a, a_pitch: int, n_a, desc_b, b_pitch: int, n_b, pairs: int,
+                       max_distance: int, min_difference: int, out, capacity: int, n_out,
+                       stream=None) -> None:
+    """Batched device path over `pairs` (A_p, B_p) descriptor sets (torch device tensors)."""
+    check(_lib.load().mage_hamming_match_batch_device(
+        ptr(desc_a), a_pitch, ptr(n_a), ptr(desc_b), b_pitch, ptr(n_b), pairs, max_distance,
+        min_difference, ptr(out), capacity, ptr(n_out), C.c_void_p(stream) if stream else None))

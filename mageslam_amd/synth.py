@@ -1,0 +1,159 @@
+"""Seeded synthetic inputs for the hot path.
+
+Frames: a world texture T(u, v) of 8x8-px cells with a uniform gray level from a splitmix64
+hash, plus a 3x3-px layer of +-24, clamped to [0, 255]; frame t = T(x + 3t, y + 2t), an
+integer pan so consecutive frames overlap and have true matches.  The same function is
+implemented on the GPU (`mage_synth_frames` in csrc/synth.hip) so the benchmark's frames are
+generated in HBM; tests check both agree byte for byte.
+
+BA graph (C3): 50 pinhole cameras on a line looking +z, 5000 points each seen by 20
+consecutive cameras (100k observations), 0.5 px noise, 1% outliers, cameras 0-9 fixed.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+FRAME_SEED = 0x5EEDF00D
+BA_SEED = 0xBA5EBA11
+K1 = np.uint64(0x9E3779B97F4A7C15)
+K2 = np.uint64(0xC2B2AE3D27D4EB4F)
+FINE_SALT = np.uint64(0xA5A5A5A5)
+
+
+def splitmix64(z: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser on uint64 arrays (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        z = (z + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def texture(u: np.ndarray, v: np.ndarray, seed: int = FRAME_SEED) -> np.ndarray:
+    """World texture T(u, v) for non-negative integer coordinates (uint8)."""
+    s = np.uint64(seed)
+    u = u.astype(np.uint64)
+    v = v.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        base = splitmix64(s ^ ((u >> np.uint64(3)) * K1) ^ ((v >> np.uint64(3)) * K2))
+        fine = splitmix64(s ^ FINE_SALT ^ ((u // np.uint64(3)) * K1) ^ ((v // np.uint64(3)) * K2))
+    g = (base >> np.uint64(56)).astype(np.int32)
+    f = ((fine >> np.uint64(56)) % np.uint64(49)).astype(np.int32) - 24
+    return np.clip(g + f, 0, 255).astype(np.uint8)
+
+
+def frame(t: int, width: int, height: int, seed: int = FRAME_SEED) -> np.ndarray:
+    """Frame t of the panning sequence, shape (height, width), uint8."""
+    y, x = np.mgrid[0:height, 0:width]
+    return texture(x + 3 * t, y + 2 * t, seed)
+
+
+def frames(t0: int, count: int, width: int, height: int, seed: int = FRAME_SEED) -> np.ndarray:
+    return np.stack([frame(t0 + i, width, height, seed) for i in range(count)])
+
+
+@dataclass
+class BAGraph:
+    """Inputs of one BundlerLib problem in the reference's boundary layout."""
+
+    pos: np.ndarray  # (C,3) float32 view-space translation t (X_cam = R X + t)
+    rot: np.ndarray  # (C,3,3) float32 rotation R (row-major here; C-ABI takes column-major)
+    intr: np.ndarray  # (C,4) float32 {cx, cy, fx, fy}
+    fixed: np.ndarray  # (C,) uint8
+    points: np.ndarray  # (P,3) float32 initial (perturbed) positions
+    uv: np.ndarray  # (E,2) float32 observations
+    cam: np.ndarray  # (E,) uint32
+    pt: np.ndarray  # (E,) uint32
+    info: np.ndarray  # (E,) float32
+    true_points: np.ndarray
+    true_pos: np.ndarray
+    true_rot: np.ndarray
+
+    @property
+    def rot_colmajor(self) -> np.ndarray:
+        """(C,9) Eigen column-major layout used by SetCameraPose (BundleAdjust.cpp:46-55)."""
+        return np.ascontiguousarray(np.transpose(self.rot, (0, 2, 1)).reshape(-1, 9))
+
+
+def _rot(yaw: float, pitch: float = 0.0, roll: float = 0.0) -> np.ndarray:
+    cy, sy = np.cos(yaw), np.sin(yaw)
+    cp, sp = np.cos(pitch), np.sin(pitch)
+    cr, sr = np.cos(roll), np.sin(roll)
+    ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+    rz = np.array([[cr, -sr, 0], [sr, cr, 0], [0, 0, 1]])
+    return rz @ rx @ ry
+
+
+def refinement_confidence(count: np.ndarray) -> np.ndarray:
+    """MapPointRefinementConfidence (Core/.../Source/Map/MappingMath.h:42-49), float32."""
+    c = count.astype(np.float32)
+    return (np.float32(1.0) - np.float32(1.0) / np.power(np.float32(1.5) + c, np.float32(2.0))).astype(np.float32)
+
+
+def ba_graph(
+    cameras: int = 50,
+    points: int = 5000,
+    obs_per_point: int = 20,
+    fixed_cameras: int = 10,
+    seed: int = BA_SEED,
+    noise_px: float = 0.5,
+    outlier_frac: float = 0.01,
+) -> BAGraph:
+    """Synthetic local-BA window (SURVEY.md §8(d) 'BA graph (C3)')."""
+    rng = np.random.default_rng(seed)
+    f, cx, cy = 900.0, 640.0, 360.0
+    obs_per_point = min(obs_per_point, cameras)
+    # true cameras: centres at x = 0.1 i, looking +z, yaw ~ U(-5, 5) deg
+    true_rot = np.zeros((cameras, 3, 3))
+    true_pos = np.zeros((cameras, 3))
+    for i in range(cameras):
+        R = _rot(np.deg2rad(rng.uniform(-5, 5)))
+        centre = np.array([0.1 * i, 0.0, 0.0])
+        true_rot[i] = R
+        true_pos[i] = -R @ centre  # t = -R c
+    span = max(cameras - obs_per_point + 1, 1)
+    xs = rng.uniform(-1, 6, points) if cameras >= 50 else rng.uniform(-1, 0.1 * cameras + 1, points)
+    true_pts = np.stack([xs, rng.uniform(-1.5, 1.5, points), rng.uniform(4, 8, points)], axis=1)
+    starts = rng.integers(0, span, points)
+    cam = (starts[:, None] + np.arange(obs_per_point)[None, :]).reshape(-1).astype(np.uint32)
+    pt = np.repeat(np.arange(points), obs_per_point).astype(np.uint32)
+    Xc = np.einsum("eij,ej->ei", true_rot[cam], true_pts[pt]) + true_pos[cam]
+    uv = np.stack([f * Xc[:, 0] / Xc[:, 2] + cx, f * Xc[:, 1] / Xc[:, 2] + cy], axis=1)
+    uv += rng.normal(0, noise_px, uv.shape)
+    n_out = int(round(outlier_frac * len(cam)))
+    out_idx = rng.choice(len(cam), n_out, replace=False)
+    ang = rng.uniform(0, 2 * np.pi, n_out)
+    mag = rng.uniform(15, 30, n_out)
+    uv[out_idx] += np.stack([mag * np.cos(ang), mag * np.sin(ang)], axis=1)
+    # initial estimates: rotation N(0, 0.3 deg) per axis, translation N(0, 0.01); points N(0, 0.02)
+    rot0 = np.zeros_like(true_rot)
+    pos0 = np.zeros_like(true_pos)
+    for i in range(cameras):
+        if i < fixed_cameras:
+            rot0[i], pos0[i] = true_rot[i], true_pos[i]
+        else:
+            d = np.deg2rad(rng.normal(0, 0.3, 3))
+            rot0[i] = _rot(d[0], d[1], d[2]) @ true_rot[i]
+            pos0[i] = true_pos[i] + rng.normal(0, 0.01, 3)
+    pts0 = true_pts + rng.normal(0, 0.02, true_pts.shape)
+    fixed = np.zeros(cameras, np.uint8)
+    fixed[:fixed_cameras] = 1
+    info = refinement_confidence(np.arange(points)[pt] % 6)
+    intr = np.tile(np.array([cx, cy, f, f], np.float32), (cameras, 1))
+    return BAGraph(
+        pos=pos0.astype(np.float32),
+        rot=rot0.astype(np.float32),
+        intr=intr,
+        fixed=fixed,
+        points=pts0.astype(np.float32),
+        uv=uv.astype(np.float32),
+        cam=cam,
+        pt=pt,
+        info=info,
+        true_points=true_pts,
+        true_pos=true_pos,
+        true_rot=true_rot,
+    )

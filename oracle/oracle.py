@@ -1,0 +1,261 @@
+"""ctypes binding of the CPU oracle (oracle/_build/libmage_oracle.so).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker; the product (mageslam_amd) never imports it.
+Parity unpinned: see the headers of orb_oracle.c / ba_oracle.c and DESIGN.md §Parity.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "libmage_oracle.so"
+DATA = HERE.parent / "mageslam_amd" / "data"
+
+
+class KeyPoint(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+class DMatch(C.Structure):
+    _fields_ = [("query_idx", C.c_int32), ("train_idx", C.c_int32), ("img_idx", C.c_int32),
+                ("distance", C.c_float)]
+
+
+class OrbSettings(C.Structure):
+    _fields_ = [("gaussian_kernel_size", C.c_uint32), ("nfeatures", C.c_uint32),
+                ("scale_factor", C.c_float), ("nlevels", C.c_uint32), ("patch_size", C.c_uint32),
+                ("fast_threshold", C.c_uint32), ("use_orientation", C.c_int32),
+                ("feature_factor", C.c_float), ("feature_strength", C.c_float),
+                ("strong_response", C.c_int32), ("min_robust_factor", C.c_float),
+                ("max_robust_factor", C.c_float), ("num_cells_x", C.c_int32),
+                ("num_cells_y", C.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+DM_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", "<i4"),
+                     ("distance", "<f4")])
+
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        _lib = C.CDLL(str(LIB_PATH))
+        _declare(_lib)
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def _declare(L):
+    vp, i32, u32, f32 = C.c_void_p, C.c_int, C.c_uint32, C.c_float
+    L.oracle_fast_score_map.argtypes = [vp, i32, i32, i32, i32, vp]
+    L.oracle_gaussian_blur.argtypes = [vp, i32, i32, i32, i32, vp]
+    L.oracle_gaussian_taps.argtypes = [i32, C.c_double, vp]
+    L.oracle_orb_detect.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, u32, C.POINTER(u32)]
+    L.oracle_orb_detect.restype = i32
+    L.oracle_hamming.argtypes = [vp, vp]
+    L.oracle_hamming.restype = i32
+    L.oracle_match.argtypes = [vp, u32, vp, vp, u32, vp, i32, i32, vp, u32]
+    L.oracle_match.restype = u32
+    L.oracle_ba_create.argtypes = [i32]
+    L.oracle_ba_create.restype = vp
+    L.oracle_ba_destroy.argtypes = [vp]
+    L.oracle_ba_set_cameras.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.oracle_ba_fix_camera.argtypes = [vp, i32, i32]
+    L.oracle_ba_set_points.argtypes = [vp, i32, vp]
+    L.oracle_ba_set_observations.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.oracle_ba_set_lambda.argtypes = [vp, f32]
+    L.oracle_ba_get_lambda.argtypes = [vp]
+    L.oracle_ba_get_lambda.restype = f32
+    L.oracle_ba_step.argtypes = [vp, vp, i32, f32, vp, u32, C.POINTER(u32), C.POINTER(f32)]
+    L.oracle_ba_step.restype = i32
+    L.oracle_ba_get_poses.argtypes = [vp, vp, vp]
+    L.oracle_ba_get_points.argtypes = [vp, vp]
+    L.oracle_ba_get_state.argtypes = [vp, vp, vp]
+    L.oracle_ba_get_stats.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.oracle_ba_edge_linearization.argtypes = [vp, i32, vp, vp, vp]
+    L.oracle_ba_perturb_camera.argtypes = [vp, i32, vp]
+    L.oracle_ba_perturb_point.argtypes = [vp, i32, vp]
+
+
+def default_settings(nfeatures: int = 440, **kw) -> OrbSettings:
+    """FeatureExtractorSettings defaults (MageSettings.h:151-167)."""
+    s = OrbSettings(7, nfeatures, 1.5, 1, 15, 4, 0, 1.5, 0.9, 20, 1.1, 2.0, 32, 32)
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+def pattern_table(patch: int) -> np.ndarray:
+    return np.fromfile(DATA / f"bit_pattern_{patch}_rotated.bin", dtype=np.int8)
+
+
+def fast_score_map(img: np.ndarray, threshold: int = 4) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((h, w), np.uint8)
+    lib().oracle_fast_score_map(_p(img), w, h, w, threshold, _p(out))
+    return out
+
+
+def gaussian_blur(img: np.ndarray, ksize: int = 7) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((h, w), np.uint8)
+    lib().oracle_gaussian_blur(_p(img), w, h, w, ksize, _p(out))
+    return out
+
+
+def gaussian_taps(ksize: int = 7, sigma: float = 2.0) -> np.ndarray:
+    out = np.zeros(ksize, np.int32)
+    lib().oracle_gaussian_taps(ksize, sigma, _p(out))
+    return out
+
+
+def orb_detect(img: np.ndarray, settings: OrbSettings | None = None, cap: int | None = None):
+    """Returns (status, keypoints structured array, descriptors (n,32) uint8)."""
+    s = settings or default_settings()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = int(cap if cap is not None else s.nfeatures)
+    kp = np.zeros(max(cap, 1), KP_DTYPE)
+    desc = np.zeros((max(cap, 1), 32), np.uint8)
+    n = C.c_uint32(0)
+    table = pattern_table(s.patch_size if s.patch_size in (15, 31) else 15)
+    st = lib().oracle_orb_detect(C.byref(s), _p(table), _p(img), w, h, w, _p(kp), _p(desc), cap,
+                                 C.byref(n))
+    return st, kp[: n.value].copy(), desc[: n.value].copy()
+
+
+def hamming(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return int(lib().oracle_hamming(_p(a), _p(b)))
+
+
+def match(desc_a, desc_b, mask_a=None, mask_b=None, max_distance=30, min_difference=1):
+    da = np.ascontiguousarray(desc_a, np.uint8).reshape(-1, 32)
+    db = np.ascontiguousarray(desc_b, np.uint8).reshape(-1, 32)
+    ma = None if mask_a is None else np.ascontiguousarray(mask_a, np.uint8)
+    mb = None if mask_b is None else np.ascontiguousarray(mask_b, np.uint8)
+    cap = max(len(da), 1)
+    out = np.zeros(cap, DM_DTYPE)
+    n = lib().oracle_match(_p(da), len(da), _p(ma), _p(db), len(db), _p(mb), max_distance,
+                           min_difference, _p(out), cap)
+    return out[:n].copy()
+
+
+class BundlerOracle:
+    """BundlerLib restated on the CPU (same call sequence as the product's BundlerLib)."""
+
+    def __init__(self, points_fixed: bool = False):
+        self.h = lib().oracle_ba_create(int(points_fixed))
+        self.nc = self.np_ = self.ne = 0
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_ba_destroy(self.h)
+            self.h = None
+
+    def set_graph(self, g):
+        self.set_cameras(g.pos, g.rot_colmajor, g.intr, g.fixed)
+        self.set_points(g.points)
+        self.set_observations(g.uv, g.cam, g.pt, g.info)
+
+    def set_cameras(self, pos, r9_colmajor, intr, fixed):
+        pos = np.ascontiguousarray(pos, np.float32)
+        r9 = np.ascontiguousarray(r9_colmajor, np.float32)
+        intr = np.ascontiguousarray(intr, np.float32)
+        fixed = np.ascontiguousarray(fixed, np.uint8)
+        self.nc = len(pos)
+        lib().oracle_ba_set_cameras(self.h, self.nc, _p(pos), _p(r9), _p(intr), _p(fixed))
+
+    def fix_camera(self, idx, fixed=True):
+        lib().oracle_ba_fix_camera(self.h, idx, int(fixed))
+
+    def set_points(self, xyz):
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        self.np_ = len(xyz)
+        lib().oracle_ba_set_points(self.h, self.np_, _p(xyz))
+
+    def set_observations(self, uv, cam, pt, info):
+        uv = np.ascontiguousarray(uv, np.float32)
+        cam = np.ascontiguousarray(cam, np.uint32)
+        pt = np.ascontiguousarray(pt, np.uint32)
+        info = np.ascontiguousarray(info, np.float32)
+        self.ne = len(cam)
+        lib().oracle_ba_set_observations(self.h, self.ne, _p(uv), _p(cam), _p(pt), _p(info))
+
+    def set_lambda(self, lam):
+        lib().oracle_ba_set_lambda(self.h, lam)
+
+    def get_lambda(self):
+        return float(lib().oracle_ba_get_lambda(self.h))
+
+    def step(self, huber_widths, max_error_square):
+        hw = np.ascontiguousarray(huber_widths, np.float32)
+        cap = max(self.ne, 1)
+        outl = np.zeros(cap, np.uint32)
+        n = C.c_uint32(0)
+        ms = C.c_float(0)
+        lib().oracle_ba_step(self.h, _p(hw), len(hw), max_error_square, _p(outl), cap, C.byref(n),
+                             C.byref(ms))
+        return float(ms.value), outl[: min(n.value, cap)].copy()
+
+    def poses(self):
+        pos = np.zeros((self.nc, 3), np.float32)
+        r9 = np.zeros((self.nc, 9), np.float32)
+        lib().oracle_ba_get_poses(self.h, _p(pos), _p(r9))
+        return pos, r9
+
+    def points(self):
+        xyz = np.zeros((self.np_, 3), np.float32)
+        lib().oracle_ba_get_points(self.h, _p(xyz))
+        return xyz
+
+    def state(self):
+        qt = np.zeros((self.nc, 7), np.float64)
+        xyz = np.zeros((self.np_, 3), np.float64)
+        lib().oracle_ba_get_state(self.h, _p(qt), _p(xyz))
+        return qt, xyz
+
+    def stats(self):
+        it, tr, rj = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        chi, lam = C.c_double(), C.c_double()
+        lib().oracle_ba_get_stats(self.h, C.byref(it), C.byref(tr), C.byref(rj), C.byref(chi),
+                                  C.byref(lam))
+        return dict(iterations=it.value, trials=tr.value, rejected=rj.value, chi2=chi.value,
+                    lambda_=lam.value)
+
+    def edge_linearization(self, i):
+        err = np.zeros(2)
+        jpt = np.zeros(6)
+        jp = np.zeros(12)
+        lib().oracle_ba_edge_linearization(self.h, i, _p(err), _p(jpt), _p(jp))
+        return err, jpt.reshape(2, 3), jp.reshape(2, 6)
+
+    def perturb_camera(self, c, u):
+        u = np.ascontiguousarray(u, np.float64)
+        lib().oracle_ba_perturb_camera(self.h, c, _p(u))
+
+    def perturb_point(self, p, u):
+        u = np.ascontiguousarray(u, np.float64)
+        lib().oracle_ba_perturb_point(self.h, p, _p(u))

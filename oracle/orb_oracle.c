@@ -1,0 +1,537 @@
+/*
+ * orb_oracle.c — CPU restatement of MAGE-SLAM's ORB extractor (TEST INFRASTRUCTURE ONLY).
+ *
+ * This file is the parity oracle and the timed CPU baseline for the ORB hot path.  It is
+ * linked only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by
+ * the product library under mageslam_amd/.
+ *
+ * PARITY UNPINNED: the reference cannot be built here (OpenCV 3.4.0 / g2o / Eigen absent,
+ * MSVC-only sources) and ships no fixtures, golden vectors or tests for this
+ * path.  This restatement follows the reference line by line as cited below;
+ * the only data taken from the reference are the pre-rotated BRIEF tables
+ * (OpenCVModified.cpp:74-138, extracted by tools/extract_patterns.py).  Third-party steps are
+ * restated from their published algorithms:
+ *   - OpenCV 3.4.0 GaussianBlur 8U (separable, kernel quantised to Q8, (s+2^15)>>16), and
+ *   - the canonical keypoint order (the reference's order depends on MSVC std::nth_element).
+ * Build with -ffp-contract=off: the ANMS comparisons are float-exact.
+ *
+ * Reference paths: Core/MAGESLAM/Source/Image/OpenCVModified.cpp unless noted.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/mage_hot.h"
+
+/* Ring offsets of FAST 9/16, makeOffsets (OpenCVModified.cpp:890-921). */
+static const int kRing16[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1},
+                                   {2, -2}, {1, -3},  {0, -3},  {-1, -3}, {-2, -2}, {-3, -1},
+                                   {-3, 0}, {-3, 1},  {-2, 2},  {-1, 3}};
+
+static int imin(int a, int b) { return a < b ? a : b; }
+static int imax(int a, int b) { return a > b ? a : b; }
+
+/* cornerScore<16>, scalar branch (OpenCVModified.cpp:1030-1064); equals the SSE2 branch for
+ * every detected corner (VERIFY_SIMD, :1265-1271). */
+static int corner_score16(const uint8_t* p, const int pixel[25], int threshold)
+{
+    int d[25];
+    int v = p[0];
+    for (int k = 0; k < 25; k++) d[k] = (short)(v - p[pixel[k]]);
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = imin(d[k + 1], d[k + 2]);
+        a = imin(a, d[k + 3]);
+        if (a <= a0) continue;
+        a = imin(a, d[k + 4]);
+        a = imin(a, d[k + 5]);
+        a = imin(a, d[k + 6]);
+        a = imin(a, d[k + 7]);
+        a = imin(a, d[k + 8]);
+        a0 = imax(a0, imin(a, d[k]));
+        a0 = imax(a0, imin(a, d[k + 9]));
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = imax(d[k + 1], d[k + 2]);
+        b = imax(b, d[k + 3]);
+        b = imax(b, d[k + 4]);
+        b = imax(b, d[k + 5]);
+        if (b >= b0) continue;
+        b = imax(b, d[k + 6]);
+        b = imax(b, d[k + 7]);
+        b = imax(b, d[k + 8]);
+        b0 = imin(b0, imax(b, d[k]));
+        b0 = imin(b0, imax(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+/* Segment test of FAST_t<16>, scalar path (OpenCVModified.cpp:1415-1479): some cyclic run of
+ * more than K=8 ring pixels all darker than v-t or all brighter than v+t. */
+static int is_corner16(const uint8_t* p, const int pixel[25], int t)
+{
+    int v = p[0];
+    int vt = v - t, count = 0;
+    for (int k = 0; k < 25; k++) {
+        if (p[pixel[k]] < vt) {
+            if (++count > 8) return 1;
+        } else
+            count = 0;
+    }
+    vt = v + t;
+    count = 0;
+    for (int k = 0; k < 25; k++) {
+        if (p[pixel[k]] > vt) {
+            if (++count > 8) return 1;
+        } else
+            count = 0;
+    }
+    return 0;
+}
+
+static void make_offsets(int pixel[25], int stride)
+{
+    for (int k = 0; k < 16; k++) pixel[k] = kRing16[k][0] + kRing16[k][1] * stride;
+    for (int k = 16; k < 25; k++) pixel[k] = pixel[k - 16];
+}
+
+/* Score map: rows 3..H-4, cols 3..W-4 are tested (FAST_t loop bounds :1248, :1269, :1415);
+ * everything else is 0. */
+void oracle_fast_score_map(const uint8_t* img, int w, int h, int stride, int threshold,
+                           uint8_t* score)
+{
+    int pixel[25];
+    make_offsets(pixel, stride);
+    threshold = imin(imax(threshold, 0), 255);
+    memset(score, 0, (size_t)w * h);
+    for (int y = 3; y < h - 3; y++) {
+        for (int x = 3; x < w - 3; x++) {
+            const uint8_t* p = img + (size_t)y * stride + x;
+            if (is_corner16(p, pixel, threshold))
+                score[(size_t)y * w + x] = (uint8_t)corner_score16(p, pixel, threshold);
+        }
+    }
+}
+
+typedef struct {
+    int x, y;
+    int score;
+} cand_t;
+
+/* FAST with strict 3x3 NMS, emission in raster order (OpenCVModified.cpp:1489-1509).
+ * Returns the candidate count; `out` must hold w*h/4+w+h entries. */
+static int fast_nms(const uint8_t* img, int w, int h, int stride, int t, uint8_t* score,
+                    cand_t* out)
+{
+    oracle_fast_score_map(img, w, h, stride, t, score);
+    int n = 0;
+    for (int y = 3; y < h - 3; y++) {
+        for (int x = 3; x < w - 3; x++) {
+            int s = score[(size_t)y * w + x];
+            if (!s) continue;
+            const uint8_t* c = score + (size_t)y * w + x;
+            if (s > c[-1] && s > c[1] && s > c[-w - 1] && s > c[-w] && s > c[-w + 1] &&
+                s > c[w - 1] && s > c[w] && s > c[w + 1]) {
+                out[n].x = x;
+                out[n].y = y;
+                out[n].score = s;
+                n++;
+            }
+        }
+    }
+    return n;
+}
+
+/* OpenCV cvRound: round half to even (used by cvRound(double) on x64). */
+static int cv_round(double v) { return (int)lrint(v); }
+
+/* Gaussian taps of cv::getGaussianKernel(ksize, sigma, CV_32F) quantised by convertTo(CV_32S,
+ * 256) in createSeparableLinearFilter (OpenCV 3.4.0 filter.cpp, the 8U smoothing path). */
+void oracle_gaussian_taps(int ksize, double sigma, int* taps)
+{
+    float cf[64];
+    double sum = 0;
+    double s = sigma > 0 ? sigma : ((ksize - 1) * 0.5 - 1) * 0.3 + 0.8;
+    double scale2 = -0.5 / (s * s);
+    for (int i = 0; i < ksize; i++) {
+        double x = i - (ksize - 1) * 0.5;
+        cf[i] = (float)exp(scale2 * x * x);
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < ksize; i++) {
+        cf[i] = (float)(cf[i] * sum);
+        taps[i] = cv_round((double)cf[i] * 256.0);
+    }
+}
+
+static int reflect101(int i, int n)
+{
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+/* GaussianBlur(ksize, sigma=2, BORDER_REFLECT_101) on an 8-bit image (OpenCVModified.cpp:853-865):
+ * int32 row pass, int32 column pass, (sum + 2^15) >> 16, saturate to u8. */
+void oracle_gaussian_blur(const uint8_t* src, int w, int h, int stride, int ksize, uint8_t* dst)
+{
+    int taps[64];
+    oracle_gaussian_taps(ksize, 2.0, taps);
+    int r = ksize / 2;
+    int32_t* rows = (int32_t*)malloc(sizeof(int32_t) * (size_t)w * h);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int32_t s = 0;
+            for (int k = -r; k <= r; k++) s += taps[k + r] * src[(size_t)y * stride + reflect101(x + k, w)];
+            rows[(size_t)y * w + x] = s;
+        }
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int32_t s = 0;
+            for (int k = -r; k <= r; k++) s += taps[k + r] * rows[(size_t)reflect101(y + k, h) * w + x];
+            int v = (s + (1 << 15)) >> 16;
+            dst[(size_t)y * w + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+        }
+    free(rows);
+}
+
+typedef struct {
+    int x, y;
+    float strength;
+    int r;
+    int idx; /* canonical: raster rank within the retained set */
+} anms_item;
+
+static int cmp_item_rank(const void* pa, const void* pb)
+{
+    const anms_item* a = (const anms_item*)pa;
+    const anms_item* b = (const anms_item*)pb;
+    if (a->r != b->r) return a->r > b->r ? -1 : 1;
+    if (a->strength != b->strength) return a->strength > b->strength ? -1 : 1;
+    return a->idx < b->idx ? -1 : (a->idx > b->idx ? 1 : 0);
+}
+
+/* RetainBestFeatures (OpenCVModified.cpp:571-617).  Returns the lowest response kept; the
+ * kept set {response >= cut} is exactly what nth_element keeps because the count stops on a
+ * histogram-bin boundary. */
+static int retain_cut(const cand_t* c, int n, int minThreshold, int maxNum, int minNum,
+                      float responseFactor)
+{
+    unsigned hist[256];
+    memset(hist, 0, sizeof(hist));
+    for (int i = 0; i < n; i++) hist[imin(imax(c[i].score, 0), 255)]++;
+    size_t minNumThreshold = (size_t)minThreshold;
+    int num = 0;
+    for (int i = 255; i >= minThreshold; i--) {
+        num += (int)hist[i];
+        if (num >= minNum) {
+            minNumThreshold = (size_t)i;
+            break;
+        }
+    }
+    int lower = imax((int)((float)minNumThreshold * responseFactor), minThreshold);
+    num = 0;
+    int i;
+    for (i = 255; i >= lower; i--) {
+        num += (int)hist[i];
+        if (num >= maxNum) break;
+    }
+    return i < lower ? lower : i;
+}
+
+/* AdaptiveNonMaximalSuppresion (OpenCVModified.cpp:144-360) on items[0..n) (raster order);
+ * writes the kept items to `kept` in canonical order (r desc, strength desc, idx asc) and
+ * returns their count. */
+static int anms(anms_item* items, int n, int numToKeep, int threshold, const mage_orb_settings* s,
+                anms_item* kept)
+{
+    const int numX = s->num_cells_x, numY = s->num_cells_y;
+    const float ROBUST_EPS = 0.002f;
+    if (n == 0) return 0;
+    if ((unsigned)numToKeep > (unsigned)n) {
+        memcpy(kept, items, sizeof(anms_item) * n);
+        return n;
+    }
+    int minX = items[0].x, maxX = items[0].x, minY = items[0].y, maxY = items[0].y;
+    float minStrength = items[0].strength;
+    for (int i = 0; i < n; i++) {
+        minX = imin(minX, items[i].x);
+        minY = imin(minY, items[i].y);
+        maxX = imax(maxX, items[i].x);
+        maxY = imax(maxY, items[i].y);
+        if (items[i].strength < minStrength) minStrength = items[i].strength;
+    }
+    float robust;
+    {
+        /* mira::clamp<float> = fmin(hi, fmax(lo, v)) (arcana/math.h:57-67) */
+        float hi = (float)s->strong_response - (float)threshold;
+        float val = fminf(hi, fmaxf(0.0f, minStrength - (float)threshold));
+        float range = fmaxf(0.0f, s->max_robust_factor - s->min_robust_factor);
+        robust = s->max_robust_factor - (val / (float)(s->strong_response - threshold)) * range;
+    }
+    float robustInv = 1.0f / robust;
+
+    /* bucket: cell lists (order inside a cell does not change r: every item stronger than s
+     * is visited, OpenCVModified.cpp:268-326) */
+    int ncell = numX * numY;
+    int* cellStart = (int*)calloc((size_t)ncell + 1, sizeof(int));
+    int* cellOf = (int*)malloc(sizeof(int) * n);
+    int* order = (int*)malloc(sizeof(int) * n);
+    for (int i = 0; i < n; i++) {
+        int cx = (items[i].x - minX) * numX / (maxX + 1 - minX);
+        int cy = (items[i].y - minY) * numY / (maxY + 1 - minY);
+        cellOf[i] = cy * numX + cx;
+        cellStart[cellOf[i] + 1]++;
+    }
+    for (int c = 0; c < ncell; c++) cellStart[c + 1] += cellStart[c];
+    {
+        int* fill = (int*)malloc(sizeof(int) * ncell);
+        memcpy(fill, cellStart, sizeof(int) * ncell);
+        for (int i = 0; i < n; i++) order[fill[cellOf[i]]++] = i;
+        free(fill);
+    }
+    int globalMaxR2 = (int)(((double)(maxX - minX)) * ((double)(maxY - minY)) / (double)numToKeep);
+    int minCellDelta2;
+    {
+        int dx = imax((maxX - minX) / numX, 1);
+        int dy = imax((maxY - minY) / numY, 1);
+        minCellDelta2 = imin(dx, dy) * imin(dx, dy);
+    }
+    for (int i = 0; i < n; i++) {
+        anms_item* it = &items[i];
+        int cx = cellOf[i] % numX, cy = cellOf[i] / numX;
+        int minR2 = globalMaxR2;
+        float sth = (it->strength >= 0) ? (it->strength * robust + ROBUST_EPS)
+                                        : (it->strength * robustInv + ROBUST_EPS);
+        for (int d = 0; imax(0, d - 1) * imax(0, d - 1) * minCellDelta2 < minR2; d++) {
+            for (int yy = -d; yy <= d; yy++) {
+                int cYY = yy + cy;
+                if (cYY < 0 || cYY >= numY) continue;
+                for (int xx = -d; xx <= d; xx++) {
+                    int cXX = xx + cx;
+                    if (cXX < 0 || cXX >= numX || imax(abs(xx), abs(yy)) != d) continue;
+                    int cell = cYY * numX + cXX;
+                    for (int q = cellStart[cell]; q < cellStart[cell + 1]; q++) {
+                        const anms_item* o = &items[order[q]];
+                        if (o->strength > sth) {
+                            int ddx = it->x - o->x, ddy = it->y - o->y;
+                            int rr = ddx * ddx + ddy * ddy;
+                            if (rr < minR2) minR2 = rr;
+                        }
+                    }
+                }
+            }
+        }
+        it->r = minR2;
+    }
+    free(cellStart);
+    free(cellOf);
+    free(order);
+    memcpy(kept, items, sizeof(anms_item) * n);
+    qsort(kept, n, sizeof(anms_item), cmp_item_rank);
+    return numToKeep;
+}
+
+/* ComputeOrbDescriptorsPrerotated (OpenCVModified.cpp:502-549) on the blurred level. */
+static void describe(const uint8_t* blurred, int stride, const signed char* pattern_table,
+                     int cx, int cy, int rot, uint8_t* desc)
+{
+    const uint8_t* center = blurred + (ptrdiff_t)cy * stride + cx;
+    const signed char* pattern = pattern_table + rot * 1024;
+    for (int i = 0; i < 32; i++, pattern += 32) {
+        int val = 0;
+        for (int bit = 0; bit < 8; bit++) {
+            const signed char* q = pattern + 4 * bit;
+            int t0 = center[q[1] * stride + q[0]];
+            int t1 = center[q[3] * stride + q[2]];
+            val |= (t0 < t1) << bit;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+/* OrbDetector::DetectAndCompute (OpenCVModified.cpp:771-886) for nlevels == 1 and patch 15/31.
+ * Returns MAGE_OK and the count in *n_out. */
+int oracle_orb_detect(const mage_orb_settings* s, const signed char* pattern_table,
+                      const uint8_t* img, int w, int h, int stride, mage_keypoint* kp,
+                      uint8_t* desc, uint32_t cap, uint32_t* n_out)
+{
+    *n_out = 0;
+    if (s->patch_size < 2) return MAGE_EINVAL;
+    if (s->nlevels != 1 || s->use_orientation) return MAGE_EUNSUPPORTED;
+    if (s->patch_size != 15 && s->patch_size != 31) return MAGE_EUNSUPPORTED;
+    if (s->gaussian_kernel_size > 1 && (s->gaussian_kernel_size % 2) == 0) return MAGE_EINVAL;
+
+    const int nfeatures = (int)s->nfeatures;
+    const int fastThreshold = (int)s->fast_threshold;
+    const int halfPatch = (int)s->patch_size / 2;
+    const int border = halfPatch; /* no orientation: RunByImageBorder(halfPatchSize) :712 */
+
+    uint8_t* score = (uint8_t*)malloc((size_t)w * h);
+    int capc = (w / 2 + 2) * (h / 2 + 2);
+    cand_t* cand = (cand_t*)malloc(sizeof(cand_t) * capc);
+    int nc = fast_nms(img, w, h, stride, fastThreshold, score, cand);
+
+    /* RunByImageBorder (:619-639): keep b <= x < W-b, b <= y < H-b */
+    int m = 0;
+    if (h > border * 2 && w > border * 2) {
+        for (int i = 0; i < nc; i++)
+            if (cand[i].x >= border && cand[i].x < w - border && cand[i].y >= border && cand[i].y < h - border)
+                cand[m++] = cand[i];
+    }
+    nc = m;
+
+    anms_item* items = (anms_item*)malloc(sizeof(anms_item) * (nc + 1));
+    anms_item* kept = (anms_item*)malloc(sizeof(anms_item) * (nc + 1));
+    int nk;
+    if (nc > nfeatures) {
+        int maxNum = (int)((float)nfeatures * s->feature_factor);
+        int cut = retain_cut(cand, nc, fastThreshold, maxNum, nfeatures, s->feature_strength);
+        int ni = 0;
+        for (int i = 0; i < nc; i++)
+            if (cand[i].score >= cut) {
+                items[ni].x = cand[i].x;
+                items[ni].y = cand[i].y;
+                items[ni].strength = (float)cand[i].score;
+                items[ni].r = 0;
+                items[ni].idx = ni;
+                ni++;
+            }
+        nk = anms(items, ni, nfeatures, fastThreshold, s, kept);
+    } else {
+        for (int i = 0; i < nc; i++) {
+            kept[i].x = cand[i].x;
+            kept[i].y = cand[i].y;
+            kept[i].strength = (float)cand[i].score;
+            kept[i].r = 0;
+            kept[i].idx = i;
+        }
+        nk = nc;
+    }
+    if ((uint32_t)nk > cap) nk = (int)cap; /* ImageData::Insert truncation (ImageData.h:65-70) */
+
+    /* keypoint fields: FAST emits KeyPoint(x, y, 7, -1, score) (:1508); ComputeKeyPoints sets
+     * octave/size (:713-717), angle = 0 without orientation (:748-754), pt *= 1 (:756-760). */
+    for (int i = 0; i < nk; i++) {
+        kp[i].x = (float)kept[i].x;
+        kp[i].y = (float)kept[i].y;
+        kp[i].size = (float)s->patch_size * 1.0f;
+        kp[i].angle = 0.0f;
+        kp[i].response = kept[i].strength;
+        kp[i].octave = 0;
+        kp[i].class_id = -1;
+    }
+    *n_out = (uint32_t)nk;
+
+    if (nk > 0) {
+        uint8_t* blurred = (uint8_t*)malloc((size_t)w * h);
+        if (s->gaussian_kernel_size > 1)
+            oracle_gaussian_blur(img, w, h, stride, (int)s->gaussian_kernel_size, blurred);
+        else
+            for (int y = 0; y < h; y++) memcpy(blurred + (size_t)y * w, img + (size_t)y * stride, w);
+        for (int i = 0; i < nk; i++) {
+            /* rot = cvRound(angle/12) % 30 with angle = 0 (:522) */
+            describe(blurred, w, pattern_table, kept[i].x, kept[i].y, 0, desc + 32 * (size_t)i);
+        }
+        free(blurred);
+    }
+    free(score);
+    free(cand);
+    free(items);
+    free(kept);
+    return MAGE_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Matching (Core/MAGESLAM/Source/Tracking/FeatureMatcher.cpp)                                  */
+/* ------------------------------------------------------------------------------------------ */
+
+/* GetDescriptorDistance, SWAR branch (FeatureMatcher.cpp:488-500). */
+int oracle_hamming(const uint8_t* a, const uint8_t* b)
+{
+    int result = 0;
+    for (int k = 0; k < 8; k++) {
+        uint32_t x, y;
+        memcpy(&x, a + 4 * k, 4);
+        memcpy(&y, b + 4 * k, 4);
+        uint32_t bits = x ^ y;
+        bits = bits - ((bits >> 1) & 0x55555555u);
+        bits = (bits & 0x33333333u) + ((bits >> 2) & 0x33333333u);
+        result += (int)((((bits + (bits >> 4)) & 0x0F0F0F0Fu) * 0x01010101u) >> 24);
+    }
+    return result;
+}
+
+/* One direction of BFMatcher::radiusMatch (OpenCV 3.4.0, inclusive radius) reduced to what
+ * Match reads: the best candidate (lowest distance, lowest index on ties) and whether the
+ * row passes the delta test (FeatureMatcher.cpp:125-137, 144-156).  best[i] = -1 if rejected. */
+static void best_rows(const uint8_t* q, const int* qi, int nq, const uint8_t* t, const int* ti,
+                      int nt, int maxDist, int minDiff, int* best, int* bestDist)
+{
+    for (int i = 0; i < nq; i++) {
+        int d0 = 1 << 30, d1 = 1 << 30, j0 = -1, cnt = 0;
+        for (int j = 0; j < nt; j++) {
+            int d = oracle_hamming(q + 32 * (size_t)qi[i], t + 32 * (size_t)ti[j]);
+            if (d > maxDist) continue;
+            cnt++;
+            if (d < d0) {
+                d1 = d0;
+                d0 = d;
+                j0 = j;
+            } else if (d < d1)
+                d1 = d;
+        }
+        best[i] = -1;
+        bestDist[i] = d0;
+        if (cnt == 0) continue;
+        if (cnt > 1 && (float)(d1 - d0) < (float)minDiff) continue;
+        best[i] = j0;
+    }
+}
+
+/* Match (FeatureMatcher.cpp:61-190).  Returns the number of matches written. */
+uint32_t oracle_match(const uint8_t* da, uint32_t na, const uint8_t* ma, const uint8_t* db,
+                      uint32_t nb, const uint8_t* mb, int maxDist, int minDiff, mage_dmatch* out,
+                      uint32_t cap)
+{
+    int* ia = (int*)malloc(sizeof(int) * (na + 1));
+    int* ib = (int*)malloc(sizeof(int) * (nb + 1));
+    int ca = 0, cb = 0;
+    for (uint32_t i = 0; i < na; i++)
+        if (!ma || ma[i]) ia[ca++] = (int)i;
+    for (uint32_t i = 0; i < nb; i++)
+        if (!mb || mb[i]) ib[cb++] = (int)i;
+    uint32_t n = 0;
+    if (ca && cb) {
+        int* fwd = (int*)malloc(sizeof(int) * ca);
+        int* fwdD = (int*)malloc(sizeof(int) * ca);
+        int* bwd = (int*)malloc(sizeof(int) * cb);
+        int* bwdD = (int*)malloc(sizeof(int) * cb);
+        best_rows(da, ia, ca, db, ib, cb, maxDist, minDiff, fwd, fwdD);
+        best_rows(db, ib, cb, da, ia, ca, maxDist, minDiff, bwd, bwdD);
+        for (int i = 0; i < ca; i++) {
+            int j = fwd[i];
+            if (j < 0 || bwd[j] != i) continue;
+            if (n < cap) {
+                out[n].query_idx = ia[i];
+                out[n].train_idx = ib[j];
+                out[n].img_idx = 0;
+                out[n].distance = (float)fwdD[i];
+            }
+            n++;
+        }
+        free(fwd);
+        free(fwdD);
+        free(bwd);
+        free(bwdD);
+    }
+    free(ia);
+    free(ib);
+    return n;
+}
