@@ -1,0 +1,300 @@
+#!/usr/bin/env python3
+"""bench.py — MAGE-SLAM hot path on MI355X: ORB extract + match @720p (headline) and local-BA
+iterations (50 KF x 5000 pts), with roofline and CPU-baseline fields.
+
+Step = one batch of B synthetic 1280x720 frames (resident in HBM before timing): ORB extraction
+(FAST/NMS -> retain/ANMS -> blur+rBRIEF) of every frame and the two-way Hamming match of each
+frame against its predecessor (SURVEY.md §8(d) unit of work).  Multi-GPU (C5): one independent
+sequence per rank (seed + rank), no collective in the data path ("scaling": "weak"); after the
+timed region rank 0 gathers each rank's per-frame (keypoints, matches) summary over RCCL.
+
+Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 via torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+
+METRIC = "frames/sec ORB extract+match @720p; local-BA iters/sec (50 KF, 5k pts)"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured)
+FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 (vector = matrix), SURVEY.md §8(d)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=256, help="frames per step")
+    p.add_argument("--frames", type=int, default=1024, help="resident sequence length per rank")
+    p.add_argument("--width", type=int, default=1280)
+    p.add_argument("--height", type=int, default=720)
+    p.add_argument("--features", type=int, default=2000)
+    p.add_argument("--ba-iters", type=int, default=30)
+    p.add_argument("--ba-warmup", type=int, default=3)
+    p.add_argument("--no-ba", action="store_true")
+    p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
+    return p.parse_args()
+
+
+def orb_bytes_per_frame(w, h, n):
+    # frame read + keypoint/descriptor write + two descriptor-set reads + matches
+    return w * h + n * (28 + 32) + 2 * n * 32 + n * 16
+
+
+def ba_flops(g, trials_per_iter):
+    """F = 330 E + trials * (sum_p [40 + 144 f_p + 108 f_p (f_p + 1)] + n^3/3 + 2 n^2)."""
+    free = g.fixed[g.cam] == 0
+    f_p = np.bincount(g.pt[free], minlength=len(g.points)).astype(np.float64)
+    n = 6 * int((g.fixed == 0).sum())
+    schur = float(np.sum(40 + 144 * f_p + 108 * f_p * (f_p + 1)))
+    return 330.0 * len(g.cam) + trials_per_iter * (schur + n ** 3 / 3 + 2 * n ** 2)
+
+
+def load_pmc(kernel):
+    """HBM bytes per launch for `kernel` from the committed rocprofv3 PMC summary, if any."""
+    f = ROOT / "profiles" / "pmc_summary.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_orb_baseline(args, budget_s):
+    from mageslam_amd import synth
+    from oracle import oracle as O
+
+    s = O.default_settings(args.features)
+    _, _, prev = O.orb_detect(synth.frame(0, args.width, args.height), s)  # untimed warm-up
+    n_timed, el = 0, 0.0
+    while el < budget_s or n_timed < 2:
+        img = synth.frame(n_timed + 1, args.width, args.height)  # frame synthesis is not timed
+        t0 = time.perf_counter()
+        _, _, d = O.orb_detect(img, s)
+        O.match(d, prev, max_distance=30, min_difference=1)
+        el += time.perf_counter() - t0
+        prev = d
+        n_timed += 1
+    return {"value": n_timed / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n_timed} consecutive {args.width}x{args.height} synthetic frames, oracle "
+                      f"extract ({args.features} features) + match vs previous frame, single thread, "
+                      f"{el:.1f} s"}
+
+
+def run_orb(args, rank, world, local_rank, torch, dist):
+    from mageslam_amd import _lib, matcher, orb, synth
+
+    W, H, N, B = args.width, args.height, args.features, args.batch
+    F = max(B, (args.frames // B) * B)
+    dev = torch.device("cuda", local_rank)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    det = orb.OrbDetector(nfeatures=N, device=local_rank)
+    frames = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
+    orb.synth_frames_device(frames, F, W, H, 0, synth.FRAME_SEED + rank, stream=stream)
+    kp = torch.zeros((B + 1, N * 28), dtype=torch.uint8, device=dev)
+    desc = torch.zeros((B + 1, N, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+    mt = torch.zeros((B, N * 16), dtype=torch.uint8, device=dev)
+    nm = torch.zeros(B, dtype=torch.int32, device=dev)
+
+    def step(s):
+        start = (s * B) % F
+        fr = frames[start:start + B]
+        det.detect_and_compute_batch_device(fr, W, H, kp[1:], desc[1:], cnt[1:], N, stream=stream)
+        matcher.match_batch_device(desc[1:], N * 32, cnt[1:], desc[:-1], N * 32, cnt[:-1], B, 30, 1,
+                                   mt, N, nm, stream=stream)
+        # the batch's last frame becomes the predecessor of the next batch's first frame
+        kp[0].copy_(kp[B])
+        desc[0].copy_(desc[B])
+        cnt[0:1].copy_(cnt[B:B + 1])
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize(dev)
+    det.device_status()
+    lib = _lib.load()
+    if args.profile:
+        lib.mage_profile_reset()
+        lib.mage_profile_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.warmup, args.warmup + args.steps):
+        step(s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    lib.mage_profile_enable(0)
+    kern = _lib.profile_report() if args.profile else {}
+    det.device_status()
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el_max = float(el_t.item())
+    # end-of-run exchange: per-frame (keypoints, matches) of the last batch from every rank
+    summary = torch.stack([cnt[1:].to(torch.int64), nm.to(torch.int64)], 1)
+    gathered = [torch.zeros_like(summary) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(gathered, summary)
+    else:
+        gathered = [summary]
+    frames_total = world * args.steps * B
+    res = {
+        "value": frames_total / el_max,
+        "ms_per_step": 1000.0 * el_max / args.steps,
+        "frames_per_step": B,
+        "kernels": {k: {"launches": c, "avg_ms": ms / max(c, 1)} for k, (c, ms) in kern.items()},
+        "mean_keypoints": float(torch.cat(gathered)[:, 0].float().mean().item()),
+        "mean_matches": float(torch.cat(gathered)[:, 1].float().mean().item()),
+    }
+    orb_k = {k: v for k, v in res["kernels"].items() if k.startswith(("orb.", "match."))}
+    if orb_k:
+        dom = max(orb_k, key=lambda k: orb_k[k]["avg_ms"] * orb_k[k]["launches"])
+        per_frame = orb_bytes_per_frame(W, H, N)
+        avg_s = orb_k[dom]["avg_ms"] / 1000.0
+        achieved = per_frame * B / avg_s / 1e9
+        traffic = load_pmc(dom)
+        res["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                           "algorithmic_bytes_per_launch": per_frame * B,
+                           "avg_launch_ms": orb_k[dom]["avg_ms"]}
+    return res
+
+
+def run_ba(args, local_rank, torch):
+    from mageslam_amd import _lib, bundler, synth
+
+    g = synth.ba_graph()
+    b = bundler.BundlerLib(device=local_rank)
+    b.set_graph(g)
+    me = 7.25
+    scale2 = 0.95 * 0.95
+    for _ in range(args.ba_warmup):  # the first run removes the planted outliers (re-init)
+        b.step([1.8], me)
+        me *= scale2
+    s0 = b.stats()
+    lib = _lib.load()
+    lib.mage_profile_reset()
+    lib.mage_profile_enable(1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.ba_iters):
+        b.step([1.8], me)
+        me *= scale2
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    lib.mage_profile_enable(0)
+    kern = _lib.profile_report()
+    s1 = b.stats()
+    iters = s1["iterations"] - s0["iterations"]
+    trials = (s1["trials"] - s0["trials"]) / max(iters, 1)
+    res = {"metric": "local-BA iters/sec (50 KF, 5k pts)", "value": args.ba_iters / el, "unit": "iters/s",
+           "lm_iterations": iters, "trials_per_iteration": trials, "dtype": "f64",
+           "config": {"workload": "C3: 50 keyframes (10 fixed) x 5000 points x 20 obs = 100k observations",
+                      "iteration": "BundlerLib::StepBundleAdjustment with one LM step + outlier pass"},
+           "kernels": {k: {"launches": c, "avg_ms": ms / max(c, 1), "total_ms": ms} for k, (c, ms) in kern.items()}}
+    flops_iter = ba_flops(g, trials)
+    achieved = flops_iter * res["value"] / 1e12
+    dom = max(kern, key=lambda k: kern[k][1]) if kern else None
+    res["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                       "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "flops_per_iteration": flops_iter,
+                       "dominant_kernel": dom}
+    return res, g
+
+
+def cpu_ba_baseline(g, budget_s):
+    from oracle import oracle as O
+
+    b = O.BundlerOracle()
+    b.set_graph(g)
+    me = 7.25
+    for _ in range(3):
+        b.step([1.8], me)
+        me *= 0.9025
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and n < 200:
+        b.step([1.8], me)
+        me *= 0.9025
+        n += 1
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "iters/s", "cores": 1, "kind": "port",
+            "sample": f"{n} StepBundleAdjustment iterations of the C3 graph after 3 warm-up, oracle, "
+                      f"single thread, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    orb_res = run_orb(args, rank, world, local_rank, torch, dist)
+    ba_res, g = (None, None) if args.no_ba else run_ba(args, local_rank, torch)
+    if world > 1:
+        dist.barrier()
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": orb_res["value"],
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": orb_res["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"C2: {args.width}x{args.height} synthetic pan sequence, {args.features} "
+                                   f"features/frame, ORB extract + two-way match vs previous frame"
+                                   + (f"; C5: {world} independent sequences, one per GPU" if world > 1 else ""),
+                       "frames_per_step": args.batch, "resident_frames_per_rank": max(args.batch, (args.frames // args.batch) * args.batch),
+                       "parallelism": f"sequence-sharded x{world}"},
+            "roofline": orb_res.get("roofline"),
+            "kernels": orb_res["kernels"],
+            "mean_keypoints": orb_res["mean_keypoints"],
+            "mean_matches": orb_res["mean_matches"],
+        }
+        if ba_res is not None:
+            out["ba"] = ba_res
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_orb_baseline(args, args.cpu_sample_s)
+            if ba_res is not None:
+                cb = cpu_ba_baseline(g, args.cpu_sample_s)
+                ba_res["cpu_baseline"] = cb
+                ba_res["vs_cpu"] = ba_res["value"] / cb["value"]
+            out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

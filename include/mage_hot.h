@@ -72,6 +72,12 @@ const char* mage_version(void);
 /* Last error message of the calling thread (empty string if none). */
 const char* mage_last_error(void);
 
+/* Per-kernel timing: when enabled, every launch is bracketed by HIP events recorded on the
+ * stream it is launched on.  The report is one line per kernel: "<name> <launches> <total_ms>". */
+void mage_profile_enable(int32_t enable);
+void mage_profile_reset(void);
+const char* mage_profile_report(void);
+
 /* ------------------------------------------------------------------------------------------ */
 /* ORB extraction — replaces OrbDetector (Core/.../Source/Image/OpenCVModified.h:64-173)        */
 /* ------------------------------------------------------------------------------------------ */

@@ -18,8 +18,8 @@ STATUS_NAMES = {0: "MAGE_OK", 1: "MAGE_EINVAL", 2: "MAGE_EDEVICE", 3: "MAGE_ENOM
 
 # Every entry point declared in include/mage_hot.h (checked by tests/test_capi.py).
 EXPORTS = [
-    "mage_version", "mage_last_error",
-    "mage_orb_create", "mage_orb_destroy", "mage_orb_detect_and_compute",
+    "mage_version", "mage_last_error", "mage_profile_enable", "mage_profile_reset",
+    "mage_profile_report", "mage_orb_create", "mage_orb_destroy", "mage_orb_detect_and_compute",
     "mage_orb_detect_and_compute_batch_device", "mage_orb_status", "mage_orb_reset_status",
     "mage_synth_frames_device", "mage_orb_fast_score_map",
     "mage_hamming_distance", "mage_hamming_match", "mage_hamming_match_batch_device",
@@ -95,6 +95,15 @@ def check(status: int) -> None:
         raise MageError(status, msg)
 
 
+def profile_report() -> dict:
+    """{kernel: (launches, total_ms)} from the library's event timers."""
+    out = {}
+    for line in load().mage_profile_report().decode().splitlines():
+        name, cnt, ms = line.split()
+        out[name] = (int(cnt), float(ms))
+    return out
+
+
 def _declare(L: C.CDLL) -> None:
     vp, i32, u32, f32, i64, u64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_float, C.c_int64, C.c_uint64
     st = C.c_int
@@ -106,6 +115,9 @@ def _declare(L: C.CDLL) -> None:
 
     sig("mage_version", C.c_char_p)
     sig("mage_last_error", C.c_char_p)
+    sig("mage_profile_enable", None, i32)
+    sig("mage_profile_reset", None)
+    sig("mage_profile_report", C.c_char_p)
     sig("mage_orb_create", st, vp, C.c_int, C.POINTER(vp))
     sig("mage_orb_destroy", st, vp)
     sig("mage_orb_detect_and_compute", st, vp, vp, i32, i32, i32, vp, vp, u32, C.POINTER(u32))

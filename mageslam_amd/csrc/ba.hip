@@ -935,17 +935,26 @@ struct BundleAdjuster {
         Problem pb = problem();
         const int gp = (P + BA_THREADS - 1) / BA_THREADS;
         if (P > 0)
-            hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(cur), lin ? 1 : 0,
-                               d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
-                               d_chi.as<double>(), d_maxd.as<double>());
+            {
+                KernelTimer _kt("ba.point_linearize", st);
+                hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(cur), lin ? 1 : 0,
+                                   d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
+                                   d_chi.as<double>(), d_maxd.as<double>());
+            }
         MAGE_HIP(hipGetLastError());
         if (lin && C > 0) {
-            hipLaunchKernelGGL(cam_linearize, dim3(C), dim3(BA_THREADS), 0, st, pb, state(cur), d_err.as<double>(),
-                               d_Hpp.as<double>(), d_bp.as<double>(), d_maxd.as<double>() + P);
+            {
+                KernelTimer _kt("ba.cam_linearize", st);
+                hipLaunchKernelGGL(cam_linearize, dim3(C), dim3(BA_THREADS), 0, st, pb, state(cur), d_err.as<double>(),
+                                   d_Hpp.as<double>(), d_bp.as<double>(), d_maxd.as<double>() + P);
+            }
             MAGE_HIP(hipGetLastError());
         }
-        hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_chi.as<double>(), 0,
-                           d_maxd.as<double>(), lin ? P + C : 0, d_red.as<double>());
+        {
+            KernelTimer _kt("ba.reduce", st);
+            hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_chi.as<double>(), 0,
+                               d_maxd.as<double>(), lin ? P + C : 0, d_red.as<double>());
+        }
         MAGE_HIP(hipGetLastError());
         double h[3];
         MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
@@ -965,27 +974,48 @@ struct BundleAdjuster {
         double* xl = d_x.as<double>() + n;
         MAGE_HIP(hipMemsetAsync(d_fail.ptr, 0, 4, st));
         if (P > 0 && !points_fixed)
-            hipLaunchKernelGGL(point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
-                               d_Hll.as<double>(), d_bl.as<double>(), lam, d_Dinv.as<double>(), d_db.as<double>());
+            {
+                KernelTimer _kt("ba.point_schur", st);
+                hipLaunchKernelGGL(point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
+                                   d_Hll.as<double>(), d_bl.as<double>(), lam, d_Dinv.as<double>(), d_db.as<double>());
+            }
         if (n > 0) {
-            hipLaunchKernelGGL(build_schur, dim3(n / 6), dim3(BA_THREADS), 0, st, pb, n, d_camblk.as<int>(),
-                               d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(), d_Dinv.as<double>(),
-                               d_db.as<double>(), lam, d_S.as<double>(), d_rhs.as<double>());
-            hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), n,
-                               d_rhs.as<double>(), xp, d_fail.as<int>());
+            {
+                KernelTimer _kt("ba.build_schur", st);
+                hipLaunchKernelGGL(build_schur, dim3(n / 6), dim3(BA_THREADS), 0, st, pb, n, d_camblk.as<int>(),
+                                   d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(), d_Dinv.as<double>(),
+                                   d_db.as<double>(), lam, d_S.as<double>(), d_rhs.as<double>());
+            }
+            {
+                KernelTimer _kt("ba.cholesky_solve", st);
+                hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), n,
+                                   d_rhs.as<double>(), xp, d_fail.as<int>());
+            }
         }
         if (P > 0)
-            hipLaunchKernelGGL(point_backsub, dim3(gp), dim3(BA_THREADS), 0, st, pb, d_Hpl.as<double>(),
-                               d_Dinv.as<double>(), d_bl.as<double>(), xp, lam, xl, d_scale.as<double>());
+            {
+                KernelTimer _kt("ba.point_backsub", st);
+                hipLaunchKernelGGL(point_backsub, dim3(gp), dim3(BA_THREADS), 0, st, pb, d_Hpl.as<double>(),
+                                   d_Dinv.as<double>(), d_bl.as<double>(), xp, lam, xl, d_scale.as<double>());
+            }
         if (std::max(P, C) > 0)
-            hipLaunchKernelGGL(update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur), xp, xl,
-                               d_bp.as<double>(), lam, d_scale.as<double>() + P);
+            {
+                KernelTimer _kt("ba.update_state", st);
+                hipLaunchKernelGGL(update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur), xp, xl,
+                                   d_bp.as<double>(), lam, d_scale.as<double>() + P);
+            }
         if (P > 0)
-            hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
-                               d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
-                               d_chi.as<double>(), d_maxd.as<double>());
-        hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_scale.as<double>(), P + C,
-                           d_maxd.as<double>(), 0, d_red.as<double>());
+            {
+                KernelTimer _kt("ba.point_linearize", st);
+                hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
+                                   d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
+                                   d_chi.as<double>(), d_maxd.as<double>());
+            }
+        {
+            KernelTimer _kt("ba.reduce", st);
+            hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_scale.as<double>(), P + C,
+                               d_maxd.as<double>(), 0, d_red.as<double>());
+        }
         MAGE_HIP(hipGetLastError());
         double h[3];
         int fail = 0;
@@ -1079,11 +1109,17 @@ struct BundleAdjuster {
             return MAGE_OK;
         }
         const int ge = (E + BA_THREADS - 1) / BA_THREADS;
-        hipLaunchKernelGGL(outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), state(cur), E,
-                           d_active.as<unsigned char>(), d_err.as<double>(), (double)maxErrSq,
-                           d_flag.as<unsigned char>(), d_osum.as<double>(), d_ocnt.as<double>());
-        hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_osum.as<double>(), ge, d_ocnt.as<double>(), ge,
-                           d_osum.as<double>(), 0, d_red.as<double>());
+        {
+            KernelTimer _kt("ba.outlier_pass", st);
+            hipLaunchKernelGGL(outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), state(cur), E,
+                               d_active.as<unsigned char>(), d_err.as<double>(), (double)maxErrSq,
+                               d_flag.as<unsigned char>(), d_osum.as<double>(), d_ocnt.as<double>());
+        }
+        {
+            KernelTimer _kt("ba.reduce", st);
+            hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_osum.as<double>(), ge, d_ocnt.as<double>(), ge,
+                               d_osum.as<double>(), 0, d_red.as<double>());
+        }
         MAGE_HIP(hipGetLastError());
         std::vector<unsigned char> flag(E);
         double h[3];

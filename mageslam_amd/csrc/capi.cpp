@@ -1,8 +1,12 @@
 // capi.cpp — library-level C-ABI entry points: version, last error, device binding.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "common.hpp"
 
@@ -36,11 +40,87 @@ mage_status bind_device(int device)
     return MAGE_OK;
 }
 
+namespace {
+struct TimedLaunch {
+    std::string name;
+    hipEvent_t start, stop;
+};
+std::atomic<bool> g_profiling{false};
+std::mutex g_prof_mu;
+std::vector<TimedLaunch> g_prof_pending;
+struct Totals {
+    uint64_t count = 0;
+    double ms = 0;
+};
+std::map<std::string, Totals> g_prof_totals;
+std::string g_prof_text;
+
+void drain_locked()
+{
+    for (auto& t : g_prof_pending) {
+        float ms = 0;
+        if (hipEventSynchronize(t.stop) == hipSuccess && hipEventElapsedTime(&ms, t.start, t.stop) == hipSuccess) {
+            auto& tot = g_prof_totals[t.name];
+            tot.count++;
+            tot.ms += ms;
+        }
+        (void)hipEventDestroy(t.start);
+        (void)hipEventDestroy(t.stop);
+    }
+    g_prof_pending.clear();
+}
+}  // namespace
+
+bool profiling_enabled() { return g_profiling.load(std::memory_order_relaxed); }
+
+KernelTimer::KernelTimer(const char* kernel, hipStream_t st) : stream(st), name(kernel)
+{
+    if (!profiling_enabled()) return;
+    if (hipEventCreate(&start) != hipSuccess || hipEventCreate(&stop) != hipSuccess) {
+        start = stop = nullptr;
+        return;
+    }
+    (void)hipEventRecord(start, stream);
+}
+
+KernelTimer::~KernelTimer()
+{
+    if (!start) return;
+    (void)hipEventRecord(stop, stream);
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_pending.push_back({name, start, stop});
+    if (g_prof_pending.size() > 4096) drain_locked();
+}
+
 }  // namespace mage
 
 extern "C" {
 
 const char* mage_version(void) { return "mageslam_amd 0.1.0 (gfx950)"; }
 const char* mage_last_error(void) { return mage::last_error(); }
+
+void mage_profile_enable(int32_t enable) { mage::g_profiling.store(enable != 0); }
+
+void mage_profile_reset(void)
+{
+    std::lock_guard<std::mutex> lk(mage::g_prof_mu);
+    mage::drain_locked();
+    mage::g_prof_totals.clear();
+}
+
+const char* mage_profile_report(void)
+{
+    std::lock_guard<std::mutex> lk(mage::g_prof_mu);
+    mage::drain_locked();
+    std::string s;
+    for (auto& kv : mage::g_prof_totals) {
+        char buf[256];
+        std::snprintf(buf, sizeof(buf), "%s %llu %.6f\n", kv.first.c_str(), (unsigned long long)kv.second.count,
+                      kv.second.ms);
+        s += buf;
+    }
+    mage::g_prof_text = s;
+    return mage::g_prof_text.c_str();
+}
 
 }

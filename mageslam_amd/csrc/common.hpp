@@ -65,4 +65,17 @@ struct DeviceBuffer {
 
 constexpr int kWave = 64;
 
+// Optional per-kernel timing with HIP events recorded on the launch stream (mage_profile_*).
+// When disabled (the default) a KernelTimer costs one relaxed flag check.
+bool profiling_enabled();
+struct KernelTimer {
+    hipEvent_t start = nullptr, stop = nullptr;
+    hipStream_t stream = nullptr;
+    const char* name = nullptr;
+    KernelTimer(const char* kernel, hipStream_t st);
+    ~KernelTimer();
+    KernelTimer(const KernelTimer&) = delete;
+    KernelTimer& operator=(const KernelTimer&) = delete;
+};
+
 }  // namespace mage

@@ -207,7 +207,10 @@ mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA
     mp.out_cap = cap;
     mp.a_pitch = aPitch;
     mp.b_pitch = bPitch;
-    hipLaunchKernelGGL(match_kernel, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
+    {
+        KernelTimer _kt("match.two_way", st);
+        hipLaunchKernelGGL(match_kernel, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
+    }
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;
 }

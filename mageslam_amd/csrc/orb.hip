@@ -648,8 +648,11 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
     if (h <= 2 * border || w <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
     fp.cand_cap = candCap;
     dim3 g1((w + TW - 1) / TW, (h + TH - 1) / TH, batch);
-    hipLaunchKernelGGL(fast_nms_kernel, g1, dim3(FAST_THREADS), 0, st, d_frames, fp,
-                       o->cand.as<uint32_t>(), o->counts.as<uint32_t>());
+    {
+        KernelTimer _kt("orb.fast_nms", st);
+        hipLaunchKernelGGL(fast_nms_kernel, g1, dim3(FAST_THREADS), 0, st, d_frames, fp,
+                           o->cand.as<uint32_t>(), o->counts.as<uint32_t>());
+    }
     MAGE_HIP(hipGetLastError());
 
     SelectParams sp{};
@@ -667,9 +670,12 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
     sp.cells_x = s.num_cells_x;
     sp.cells_y = s.num_cells_y;
     sp.kp_size = (float)s.patch_size * 1.0f;
-    hipLaunchKernelGGL(select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, o->cand.as<uint32_t>(),
-                       o->counts.as<uint32_t>(), sp, d_kp, o->xy.as<uint32_t>(), d_n,
-                       o->status.as<uint32_t>());
+    {
+        KernelTimer _kt("orb.select", st);
+        hipLaunchKernelGGL(select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, o->cand.as<uint32_t>(),
+                           o->counts.as<uint32_t>(), sp, d_kp, o->xy.as<uint32_t>(), d_n,
+                           o->status.as<uint32_t>());
+    }
     MAGE_HIP(hipGetLastError());
 
     if (cap > 0) {
@@ -683,8 +689,11 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         dp.ksize = (int)s.gaussian_kernel_size;
         for (int i = 0; i < 2 * KHMAX + 1; i++) dp.taps[i] = o->taps[i];
         dim3 g3((cap + DESC_WAVES - 1) / DESC_WAVES, batch);
-        hipLaunchKernelGGL(describe_kernel, g3, dim3(DESC_WAVES * kWave), 0, st, d_frames, dp,
-                           o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
+        {
+            KernelTimer _kt("orb.describe", st);
+            hipLaunchKernelGGL(describe_kernel, g3, dim3(DESC_WAVES * kWave), 0, st, d_frames, dp,
+                               o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
+        }
         MAGE_HIP(hipGetLastError());
     }
     return MAGE_OK;

@@ -76,8 +76,9 @@ def test_detect_settings_variants(gpu, oracle, kw):
 def test_raster_path_and_capacity(gpu, oracle):
     # few corners: no retain/ANMS, raster order; capacity smaller than the count truncates
     img = np.full((120, 160), 100, np.uint8)
-    img[20:40, 30:60] = 200
-    img[70:90, 100:140] = 20
+    rng = np.random.default_rng(4)
+    ys, xs = rng.integers(10, 110, 40), rng.integers(10, 150, 40)
+    img[ys, xs] = rng.integers(130, 250, 40)  # isolated dots: strict local maxima
     det = orb.OrbDetector(nfeatures=440)
     kp, d = det.DetectAndCompute(img)
     _, okp, od = oracle.orb_detect(img, oracle.default_settings(440))
