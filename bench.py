@@ -183,11 +183,13 @@ def run_ba(args, local_rank, torch):
     g = synth.ba_graph()
     b = bundler.BundlerLib(device=local_rank)
     b.set_graph(g)
+    # warm-up removes the planted outliers (first pass) with the reference schedule; the timed
+    # iterations then hold maxErrorSquare at MaxOutlierError (7.25, BundleAdjust.cpp:375) so every
+    # timed iteration does the same work on GPU and CPU (a shrinking threshold would eventually
+    # empty the graph).
     me = 7.25
-    scale2 = 0.95 * 0.95
-    for _ in range(args.ba_warmup):  # the first run removes the planted outliers (re-init)
+    for _ in range(args.ba_warmup):
         b.step([1.8], me)
-        me *= scale2
     s0 = b.stats()
     lib = _lib.load()
     lib.mage_profile_reset()
@@ -196,7 +198,6 @@ def run_ba(args, local_rank, torch):
     t0 = time.perf_counter()
     for _ in range(args.ba_iters):
         b.step([1.8], me)
-        me *= scale2
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     lib.mage_profile_enable(0)
@@ -223,15 +224,13 @@ def cpu_ba_baseline(g, budget_s):
 
     b = O.BundlerOracle()
     b.set_graph(g)
-    me = 7.25
+    me = 7.25  # same schedule as the GPU leg (run_ba)
     for _ in range(3):
         b.step([1.8], me)
-        me *= 0.9025
     n = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and n < 200:
+    while (time.perf_counter() - t0 < budget_s and n < 200) or n < 3:
         b.step([1.8], me)
-        me *= 0.9025
         n += 1
     el = time.perf_counter() - t0
     return {"value": n / el, "unit": "iters/s", "cores": 1, "kind": "port",

@@ -3,23 +3,26 @@
 // (OptimizationAlgorithmLevenberg + BlockSolver_6_3 Schur + LinearSolverDense +
 // EdgeProjectXYZ2UV / VertexSE3Expmap / VertexSBAPointXYZ / RobustKernelHuber), in fp64.
 //
-// Device-resident problem, CSR by point and by camera (active edges, insertion order).
-// One LM iteration (g2o solve(iteration)) =
-//   point_linearize   thread/point: errors of all its edges (kept per edge, as g2o keeps
-//                     _error), robust chi2, Hll, bl, Hpl_e = J_pose^T w J_point per edge
+// Device-resident problem with CSR by point (edge order) and by camera (sorted by point id),
+// filtered by a per-edge `active` byte so that outlier removal never rebuilds structure.
+// One LM iteration (g2o solve(iteration)):
+//   point_linearize   thread/point: errors of its edges (kept per edge, as g2o keeps _error),
+//                     robust chi2, Hll, bl and Hpl_e = J_pose^T w J_point per edge
 //   cam_linearize     workgroup/camera: Hpp, bp (recomputes J_pose; no per-edge 6x6 in HBM)
-//   reduce            chi2, max diagonal (lambda init)
-//   trial loop (<= 10, host decides from one 3-double readback per trial):
+//   trial loop (<= 10; one 48-byte readback per trial decides accept / reject on the host):
 //     point_schur     Dinv = (Hll + lambda I)^-1, db = Dinv bl
-//     build_schur     workgroup/camera row: S_c1,c2 = Hpp + lambda I - sum_p Hpl Dinv Hpl^T in
-//                     LDS (fp64 LDS atomics), rhs = bp - sum Hpl db
-//     cholesky_solve  one workgroup, blocked right-looking Cholesky (16-wide panels, wave-
-//                     register diagonal factor) + blocked triangular solves
+//     schur_pairs     workgroup per covisible camera pair (h1 <= h2): intersect the two
+//                     point-sorted edge lists by binary search, accumulate
+//                     sum_p Hpl_{c1 p} Dinv_p Hpl_{c2 p}^T in registers, one deterministic
+//                     workgroup reduction, write the 6x6 block (+ Hpp + lambda I, rhs on h1 = h2)
+//     cholesky_solve  one workgroup: 16-wide right-looking Cholesky, diagonal block factored in
+//                     one wave's registers, panel TRSM one row per thread, trailing SYRK on f64
+//                     MFMA (v_mfma_f64_16x16x4f64) tiles; triangular solves by wave shuffles
 //     point_backsub   xl = Dinv (bl - Hpl^T xp)
-//     update          trial state = exp(xp) * T, p + xl  (double-buffered: pop = no copy)
-//     point_errors    errors + robust chi2 of the trial state
-//     reduce          trial chi2 and g2o computeScale
-// then the outlier / cheirality post-pass of StepBundleAdjustment (BundlerLib.cpp:385-446).
+//     update_state    trial state = exp(xp) * T, p + xl  (double-buffered: pop = no copy)
+//     point_linearize errors + robust chi2 of the trial state;  reduce: chi2 and computeScale
+// then the StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) on the device, appending
+// outlier indices and clearing their `active` byte.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,195 +31,15 @@
 #include <limits>
 #include <vector>
 
+#include "ba_math.hpp"
 #include "common.hpp"
 
 namespace mage {
 namespace {
 
+using namespace ba;
+
 constexpr int BA_THREADS = 256;
-
-// ---------------- SE3Quat / Eigen primitives (device) ----------------
-
-__device__ __forceinline__ void d_cross(const double a[3], const double b[3], double c[3])
-{
-    c[0] = a[1] * b[2] - a[2] * b[1];
-    c[1] = a[2] * b[0] - a[0] * b[2];
-    c[2] = a[0] * b[1] - a[1] * b[0];
-}
-
-// Quaternion * Vector3 (Eigen _transformVector); q = (x, y, z, w)
-__device__ __forceinline__ void d_qrot(const double q[4], const double v[3], double o[3])
-{
-    double uv[3], uv2[3];
-    d_cross(q, v, uv);
-    uv[0] += uv[0];
-    uv[1] += uv[1];
-    uv[2] += uv[2];
-    d_cross(q, uv, uv2);
-    for (int i = 0; i < 3; i++) o[i] = v[i] + q[3] * uv[i] + uv2[i];
-}
-
-__device__ __forceinline__ void d_qmat(const double q[4], double r[9])
-{
-    double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
-    double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
-    double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
-    double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
-    r[0] = 1 - (tyy + tzz);
-    r[1] = txy - twz;
-    r[2] = txz + twy;
-    r[3] = txy + twz;
-    r[4] = 1 - (txx + tzz);
-    r[5] = tyz - twx;
-    r[6] = txz - twy;
-    r[7] = tyz + twx;
-    r[8] = 1 - (txx + tyy);
-}
-
-__device__ __forceinline__ void d_quat_from_matrix(const double* m, double q[4])
-{
-    double t = m[0] + m[4] + m[8];
-    if (t > 0) {
-        t = sqrt(t + 1.0);
-        q[3] = 0.5 * t;
-        t = 0.5 / t;
-        q[0] = (m[7] - m[5]) * t;
-        q[1] = (m[2] - m[6]) * t;
-        q[2] = (m[3] - m[1]) * t;
-    } else {
-        int i = 0;
-        if (m[4] > m[0]) i = 1;
-        if (m[8] > m[i * 4]) i = 2;
-        int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
-        q[i] = 0.5 * t;
-        t = 0.5 / t;
-        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * t;
-        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
-        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
-    }
-}
-
-__device__ __forceinline__ void d_se3_normalize(double q[4])
-{
-    if (q[3] < 0)
-        for (int i = 0; i < 4; i++) q[i] = -q[i];
-    double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    for (int i = 0; i < 4; i++) q[i] /= n;
-}
-
-// T <- exp(u) * T  (VertexSE3Expmap::oplusImpl with SE3Quat::exp, g2o se3quat.h)
-__device__ void d_oplus(double q[4], double t[3], const double u[6])
-{
-    const double w0 = u[0], w1 = u[1], w2 = u[2];
-    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
-    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
-    double O2[9];
-    for (int r = 0; r < 3; r++)
-        for (int c = 0; c < 3; c++) O2[r * 3 + c] = O[r * 3] * O[c] + O[r * 3 + 1] * O[3 + c] + O[r * 3 + 2] * O[6 + c];
-    double R[9], V[9];
-    if (theta < 0.00001) {
-        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
-        for (int i = 0; i < 9; i++) V[i] = R[i];
-    } else {
-        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-        const double c = (theta - sin(theta)) / (theta * theta * theta);
-        for (int i = 0; i < 9; i++) {
-            const double I = (i % 4 == 0 ? 1.0 : 0.0);
-            R[i] = I + a * O[i] + b * O2[i];
-            V[i] = I + b * O[i] + c * O2[i];
-        }
-    }
-    double eq[4], et[3];
-    d_quat_from_matrix(R, eq);
-    for (int r = 0; r < 3; r++) et[r] = V[r * 3] * u[3] + V[r * 3 + 1] * u[4] + V[r * 3 + 2] * u[5];
-    d_se3_normalize(eq);
-    // result = e * T: t' = e.t + e.q * T.t ; q' = e.q * T.q
-    double rt[3];
-    d_qrot(eq, t, rt);
-    double nq[4];
-    nq[3] = eq[3] * q[3] - eq[0] * q[0] - eq[1] * q[1] - eq[2] * q[2];
-    nq[0] = eq[3] * q[0] + eq[0] * q[3] + eq[1] * q[2] - eq[2] * q[1];
-    nq[1] = eq[3] * q[1] + eq[1] * q[3] + eq[2] * q[0] - eq[0] * q[2];
-    nq[2] = eq[3] * q[2] + eq[2] * q[3] + eq[0] * q[1] - eq[1] * q[0];
-    d_se3_normalize(nq);
-    for (int i = 0; i < 4; i++) q[i] = nq[i];
-    for (int i = 0; i < 3; i++) t[i] = et[i] + rt[i];
-}
-
-__device__ __forceinline__ void d_huber(double delta, double e2, double& rho0, double& rho1)
-{
-    const double dsqr = delta * delta;
-    if (e2 <= dsqr) {
-        rho0 = e2;
-        rho1 = 1.0;
-    } else {
-        const double sq = sqrt(e2);
-        rho0 = 2 * sq * delta - dsqr;
-        rho1 = delta / sq;
-    }
-}
-
-struct State {  // one copy of the optimisable state
-    double* q;  // C x 4
-    double* t;  // C x 3
-    double* p;  // P x 3
-};
-
-struct Problem {
-    int C, P;
-    const double* camk;   // C x 3: f, cx, cy
-    const int* camh;      // C: Hessian block index or -1
-    const int* ptfree;    // P: 1 if the point is in the system
-    const double* uv;     // E x 2
-    const int* ecam;      // E
-    const int* ept;       // E
-    const double* info;   // E
-    const int* pstart;    // P+1
-    const int* pedges;    // active edges by point
-    const int* cstart;    // C+1
-    const int* cedges;    // active edges by camera
-    double huber;
-};
-
-// computeError + chi2 + robustify for one edge at state s; returns rho0, writes err, xc
-__device__ __forceinline__ void edge_eval(const Problem& pb, const State& s, int e, double err[2],
-                                          double xc[3], double& rho0, double& rho1)
-{
-    const int c = pb.ecam[e], p = pb.ept[e];
-    const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
-    const double X[3] = {s.p[3 * p], s.p[3 * p + 1], s.p[3 * p + 2]};
-    d_qrot(q, X, xc);
-    xc[0] += s.t[3 * c];
-    xc[1] += s.t[3 * c + 1];
-    xc[2] += s.t[3 * c + 2];
-    const double f = pb.camk[3 * c], cx = pb.camk[3 * c + 1], cy = pb.camk[3 * c + 2];
-    err[0] = pb.uv[2 * e] - (xc[0] / xc[2] * f + cx);
-    err[1] = pb.uv[2 * e + 1] - (xc[1] / xc[2] * f + cy);
-    const double inf = pb.info[e];
-    const double chi2 = inf * (err[0] * err[0] + err[1] * err[1]);
-    d_huber(pb.huber, chi2, rho0, rho1);
-}
-
-// EdgeProjectXYZ2UV::linearizeOplus pose block (2x6, row-major)
-__device__ __forceinline__ void jac_pose(const double xc[3], double f, double Jp[12])
-{
-    const double x = xc[0], y = xc[1], z = xc[2], z2 = z * z;
-    Jp[0] = x * y / z2 * f;
-    Jp[1] = -(1 + (x * x / z2)) * f;
-    Jp[2] = y / z * f;
-    Jp[3] = -1. / z * f;
-    Jp[4] = 0;
-    Jp[5] = x / z2 * f;
-    Jp[6] = (1 + y * y / z2) * f;
-    Jp[7] = -x * y / z2 * f;
-    Jp[8] = -x / z * f;
-    Jp[9] = 0;
-    Jp[10] = -1. / z * f;
-    Jp[11] = y / z2 * f;
-}
-
-// ---------------- kernels ----------------
 
 // Per point: edge errors, robust chi2, Hll, bl, Hpl per edge (BlockSolver::buildSystem with
 // BaseBinaryEdge::constructQuadraticForm, robust first-order weighting).
@@ -237,6 +60,7 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
     const int e0 = pb.pstart[p], e1 = pb.pstart[p + 1];
     for (int a = e0; a < e1; a++) {
         const int e = pb.pedges[a];
+        if (!pb.active[e]) continue;
         double ev[2], xc[3], rho0, rho1;
         edge_eval(pb, s, e, ev, xc, rho0, rho1);
         err[2 * e] = ev[0];
@@ -293,6 +117,28 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
     maxd_part[p] = free_p ? fmax(fabs(H[0]), fmax(fabs(H[3]), fabs(H[5]))) : 0.0;
 }
 
+// Block sum of `acc[N]` over the workgroup; the result lands in red[0][0..N).
+template <int N>
+__device__ __forceinline__ void block_sum(double (&acc)[N], double (*red)[N])
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        double v = acc[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[wave][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < N) {
+        double v = 0;
+        for (int w = 0; w < BA_THREADS / kWave; w++) v += red[w][threadIdx.x];
+        acc[0] = v;  // thread k keeps the total of entry k in acc[0]
+    }
+    __syncthreads();
+    if (threadIdx.x < N) red[0][threadIdx.x] = acc[0];
+    __syncthreads();
+}
+
 // Per camera: Hpp (6x6) and bp (6) from its active edges; errors come from point_linearize.
 __global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s,
                                                             const double* __restrict__ err,
@@ -309,34 +155,21 @@ __global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s,
         const double f = pb.camk[3 * c];
         for (int a = pb.cstart[c] + threadIdx.x; a < pb.cstart[c + 1]; a += BA_THREADS) {
             const int e = pb.cedges[a];
+            if (!pb.active[e]) continue;
             double ev[2], xc[3], rho0, rho1;
             edge_eval(pb, s, e, ev, xc, rho0, rho1);
             double Jp[12];
             jac_pose(xc, f, Jp);
             const double inf = pb.info[e];
             const double w = rho1 * inf;
-            const double e0 = err[2 * e], e1v = err[2 * e + 1];
-            const double or0 = -inf * e0 * rho1, or1 = -inf * e1v * rho1;
+            const double or0 = -inf * err[2 * e] * rho1, or1 = -inf * err[2 * e + 1] * rho1;
             int k = 0;
             for (int r = 0; r < 6; r++)
                 for (int cc = r; cc < 6; cc++) acc[k++] += (Jp[r] * Jp[cc] + Jp[6 + r] * Jp[6 + cc]) * w;
             for (int r = 0; r < 6; r++) acc[21 + r] += Jp[r] * or0 + Jp[6 + r] * or1;
         }
     }
-    // block reduction: waves via shuffles, then LDS
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int k = 0; k < 27; k++) {
-        double v = acc[k];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) red[wave][k] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < 27) {
-        double v = 0;
-        for (int w = 0; w < BA_THREADS / kWave; w++) v += red[w][threadIdx.x];
-        red[0][threadIdx.x] = v;  // only wave 0 writes row 0 after all reads of row 0 by this thread
-    }
-    __syncthreads();
+    block_sum<27>(acc, red);
     if (threadIdx.x == 0) {
         double* H = Hpp + 36 * (long long)c;
         int k = 0;
@@ -355,7 +188,7 @@ __global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s,
     }
 }
 
-// Fixed-order reduction of up to three partial arrays into out[0..2] (sum, sum, max).
+// Fixed-order reduction of two sum arrays and one max array into out[0..2].
 __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, int na,
                                                 const double* __restrict__ b, int nb,
                                                 const double* __restrict__ m, int nm,
@@ -423,170 +256,181 @@ __global__ __launch_bounds__(BA_THREADS) void point_schur(int P, const int* __re
     for (int r = 0; r < 3; r++) db[3 * p + r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
 }
 
-constexpr int SCHUR_MAX_BLOCKS = 96;  // free cameras handled by the LDS row accumulator
-
-// Row block h1 (camera c1) of the reduced camera system:
-//   S[h1][h2] = delta(h1,h2) (Hpp_c1 + lambda I) - sum_p Hpl_{c1 p} Dinv_p Hpl_{c2 p}^T  (h2 >= h1)
-//   rhs[h1]   = bp_c1 - sum_p Hpl_{c1 p} Dinv_p bl_p
-// (BlockSolver::solve Schur loop).  Lower blocks are mirrored for the dense factorisation.
-__global__ __launch_bounds__(BA_THREADS) void build_schur(Problem pb, int n, const int* __restrict__ cam_of_block,
+// One covisible camera pair (h1 <= h2) per workgroup (BlockSolver::solve Schur loop):
+//   S[h1][h2] = delta(h1,h2) (Hpp_c1 + lambda I) - sum_p Hpl_{c1 p} Dinv_p Hpl_{c2 p}^T
+//   rhs[h1]   = bp_c1 - sum_p Hpl_{c1 p} Dinv_p bl_p                          (h1 == h2 only)
+// The shared points come from intersecting c1's point-sorted edges with c2's by binary
+// search; each thread accumulates its 6x6 partial in registers (no atomics, deterministic).
+__global__ __launch_bounds__(BA_THREADS) void schur_pairs(Problem pb, const int2* __restrict__ pairs,
+                                                          const int* __restrict__ cam_of_block,
                                                           const double* __restrict__ Hpp,
                                                           const double* __restrict__ bp,
                                                           const double* __restrict__ Hpl,
                                                           const double* __restrict__ Dinv,
                                                           const double* __restrict__ db, double lambda,
-                                                          double* __restrict__ S, double* __restrict__ rhs)
+                                                          int np, double* __restrict__ S,
+                                                          double* __restrict__ rhs)
 {
-    __shared__ double acc[SCHUR_MAX_BLOCKS * 36];
-    __shared__ double racc[BA_THREADS / kWave][6];
-    const int h1 = blockIdx.x;
-    const int c1 = cam_of_block[h1];
-    const int nb = n / 6;
-    for (int i = threadIdx.x; i < nb * 36; i += BA_THREADS) acc[i] = 0;
-    __syncthreads();
-    double r6[6] = {0, 0, 0, 0, 0, 0};
+    __shared__ double red[BA_THREADS / kWave][42];
+    const int2 hp = pairs[blockIdx.x];
+    const int h1 = hp.x, h2 = hp.y;
+    const int c1 = cam_of_block[h1], c2 = cam_of_block[h2];
+    const bool diag = h1 == h2;
+    double acc[42];
+#pragma unroll
+    for (int k = 0; k < 42; k++) acc[k] = 0;
+    const int b0 = pb.cstart[c2], b1 = pb.cstart[c2 + 1];
     for (int a = pb.cstart[c1] + threadIdx.x; a < pb.cstart[c1 + 1]; a += BA_THREADS) {
         const int e1 = pb.cedges[a];
-        const int p = pb.ept[e1];
-        if (!pb.ptfree[p]) continue;
+        const int p = pb.cpt[a];
+        if (!pb.active[e1] || !pb.ptfree[p]) continue;
+        // first index in c2's list with point >= p
+        int lo = b0, hi = b1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (pb.cpt[mid] < p) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo >= b1 || pb.cpt[lo] != p) continue;
         const double* W1 = Hpl + 18 * (long long)e1;
         const double* Di = Dinv + 9 * (long long)p;
         double Z[18];  // W1 * Dinv (6x3)
+#pragma unroll
         for (int r = 0; r < 6; r++)
+#pragma unroll
             for (int k = 0; k < 3; k++) Z[r * 3 + k] = W1[r * 3] * Di[k] + W1[r * 3 + 1] * Di[3 + k] + W1[r * 3 + 2] * Di[6 + k];
-        const double g0 = db[3 * p], g1 = db[3 * p + 1], g2 = db[3 * p + 2];
-        for (int r = 0; r < 6; r++) r6[r] += W1[r * 3] * g0 + W1[r * 3 + 1] * g1 + W1[r * 3 + 2] * g2;
-        for (int b = pb.pstart[p]; b < pb.pstart[p + 1]; b++) {
-            const int e2 = pb.pedges[b];
-            const int h2 = pb.camh[pb.ecam[e2]];
-            if (h2 < h1) continue;
+        if (diag) {
+            const double g0 = db[3 * p], g1 = db[3 * p + 1], g2 = db[3 * p + 2];
+#pragma unroll
+            for (int r = 0; r < 6; r++) acc[36 + r] += W1[r * 3] * g0 + W1[r * 3 + 1] * g1 + W1[r * 3 + 2] * g2;
+        }
+        for (int q = lo; q < b1 && pb.cpt[q] == p; q++) {
+            const int e2 = pb.cedges[q];
+            if (!pb.active[e2]) continue;
             const double* W2 = Hpl + 18 * (long long)e2;
-            double* A = acc + 36 * h2;
+            double w2[18];
+#pragma unroll
+            for (int k = 0; k < 18; k++) w2[k] = W2[k];
+#pragma unroll
             for (int r = 0; r < 6; r++)
+#pragma unroll
                 for (int k = 0; k < 6; k++)
-                    atomicAdd(&A[r * 6 + k], Z[r * 3] * W2[k * 3] + Z[r * 3 + 1] * W2[k * 3 + 1] + Z[r * 3 + 2] * W2[k * 3 + 2]);
+                    acc[r * 6 + k] += Z[r * 3] * w2[k * 3] + Z[r * 3 + 1] * w2[k * 3 + 1] + Z[r * 3 + 2] * w2[k * 3 + 2];
         }
     }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int r = 0; r < 6; r++) {
-        double v = r6[r];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) racc[wave][r] = v;
+    block_sum<42>(acc, red);
+    for (int i = threadIdx.x; i < 36; i += BA_THREADS) {
+        const int r = i / 6, k = i % 6;
+        double v = -red[0][i];
+        if (diag) v += Hpp[36 * (long long)c1 + i] + (r == k ? lambda : 0.0);
+        S[(long long)(6 * h1 + r) * np + 6 * h2 + k] = v;
+        S[(long long)(6 * h2 + k) * np + 6 * h1 + r] = v;
     }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        double v = 0;
-        for (int w = 0; w < BA_THREADS / kWave; w++) v += racc[w][threadIdx.x];
-        rhs[6 * h1 + threadIdx.x] = bp[6 * c1 + threadIdx.x] - v;
-    }
-    for (int i = threadIdx.x; i < (nb - h1) * 36; i += BA_THREADS) {
-        const int h2 = h1 + i / 36, rc = i % 36, r = rc / 6, k = rc % 6;
-        double v = -acc[36 * h2 + rc];
-        if (h2 == h1) v += Hpp[36 * (long long)c1 + rc] + (r == k ? lambda : 0.0);
-        S[(long long)(6 * h1 + r) * n + 6 * h2 + k] = v;
-        S[(long long)(6 * h2 + k) * n + 6 * h1 + r] = v;
-    }
+    if (diag && threadIdx.x < 6) rhs[6 * h1 + threadIdx.x] = bp[6 * c1 + threadIdx.x] - red[0][36 + threadIdx.x];
 }
 
-// Dense SPD solve S x = b in one workgroup: blocked right-looking Cholesky (NB = 16), the
-// diagonal 16x16 factor in one wave's registers (shuffles, no workgroup barriers), panel TRSM
-// one row per thread, trailing update from an LDS copy of the panel; then blocked forward /
-// backward substitution.  S (row-major, full) is overwritten by L in its lower triangle.
+// Dense SPD solve S x = b in one workgroup, S of padded order np (multiple of 16, rows n..np-1
+// set to identity here).  Right-looking Cholesky with 16-wide panels:
+//   (1) the 16x16 diagonal block is factored in one wave's registers (shuffles, no barriers),
+//   (2) panel TRSM one row per thread into an LDS copy of the panel,
+//   (3) trailing update A22 -= L21 L21^T on f64 MFMA 16x16x4 tiles (lower triangle only).
+// Then forward / backward substitution, each 16-block solved by one wave with shuffles.
 constexpr int CH_THREADS = 1024;
+constexpr int CH_WAVES = CH_THREADS / kWave;
 constexpr int NB = 16;
-constexpr int CH_PANEL_ROWS = 1024;
+constexpr int CH_PANEL_ROWS = 576;  // 96 free cameras
 
-__global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict__ S, int n,
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict__ S, int np, int n,
                                                              const double* __restrict__ b,
                                                              double* __restrict__ x,
                                                              int* __restrict__ fail)
 {
     __shared__ double L11[NB][NB + 1];
     __shared__ double panel[CH_PANEL_ROWS][NB + 1];
+    __shared__ double yv[NB];
     __shared__ int s_fail;
-    __shared__ double ytile[NB];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (long long idx = tid; idx < (long long)(np - n) * np; idx += CH_THREADS) {
+        const int i = n + (int)(idx / np), k = (int)(idx % np);
+        S[(long long)i * np + k] = (i == k) ? 1.0 : 0.0;
+    }
     if (tid == 0) s_fail = 0;
     __syncthreads();
-    for (int kb = 0; kb < n; kb += NB) {
-        const int nbk = min(NB, n - kb);
-        // (1) diagonal block by wave 0
-        if (tid < kWave) {
-            const int l = tid;
+    for (int kb = 0; kb < np; kb += NB) {
+        if (wave == 0) {
+            const int l = lane;
             double a[NB];
 #pragma unroll
-            for (int k = 0; k < NB; k++) a[k] = (l < nbk && k < nbk) ? S[(long long)(kb + l) * n + kb + k] : 0.0;
-            int bad = 0;
+            for (int k = 0; k < NB; k++) a[k] = (l < NB && k <= l) ? S[(long long)(kb + l) * np + kb + k] : 0.0;
+            bool bad = false;
 #pragma unroll
             for (int j = 0; j < NB; j++) {
-                if (j < nbk) {
-                    const double djj = __shfl(a[j], j);
-                    if (!(djj > 0)) bad = 1;
-                    const double d = sqrt(djj);
-                    if (l == j) a[j] = d;
-                    if (l > j) a[j] = a[j] / d;
+                const double djj = __shfl(a[j], j);
+                if (!(djj > 0)) bad = true;
+                const double d = sqrt(djj);
+                if (l == j) a[j] = d;
+                if (l > j) a[j] = a[j] / d;
 #pragma unroll
-                    for (int k = j + 1; k < NB; k++) {
-                        const double lkj = __shfl(a[j], k);
-                        if (l >= k && k < nbk) a[k] -= a[j] * lkj;
-                    }
+                for (int k = j + 1; k < NB; k++) {
+                    const double lkj = __shfl(a[j], k);
+                    if (l >= k) a[k] -= a[j] * lkj;
                 }
             }
-            if (l < nbk) {
+            if (l < NB) {
 #pragma unroll
                 for (int k = 0; k < NB; k++) {
-                    if (k <= l && k < nbk) {
-                        L11[l][k] = a[k];
-                        S[(long long)(kb + l) * n + kb + k] = a[k];
-                    }
+                    L11[l][k] = k <= l ? a[k] : 0.0;
+                    if (k <= l) S[(long long)(kb + l) * np + kb + k] = a[k];
                 }
             }
             if (l == 0 && bad) s_fail = 1;
         }
         __syncthreads();
         if (s_fail) break;
-        // (2) panel TRSM: rows below the block, L21 = A21 L11^-T
-        const int r0 = kb + nbk;
-        for (int i = r0 + tid; i < n; i += CH_THREADS) {
+        const int r0 = kb + NB, m = np - r0;
+        for (int i = r0 + tid; i < np; i += CH_THREADS) {
+            // keeps hipcc from hoisting the 136 loop-invariant L11 reads into registers (spills)
+            asm volatile("" ::: "memory");
             double v[NB];
 #pragma unroll
-            for (int j = 0; j < NB; j++) v[j] = j < nbk ? S[(long long)i * n + kb + j] : 0.0;
+            for (int j = 0; j < NB; j++) v[j] = S[(long long)i * np + kb + j];
 #pragma unroll
             for (int j = 0; j < NB; j++) {
-                if (j < nbk) {
-                    double s = v[j];
+                double s = v[j];
 #pragma unroll
-                    for (int k = 0; k < j; k++) s -= v[k] * L11[j][k];
-                    v[j] = s / L11[j][j];
-                }
+                for (int k = 0; k < j; k++) s -= v[k] * L11[j][k];
+                v[j] = s / L11[j][j];
             }
 #pragma unroll
             for (int j = 0; j < NB; j++) {
-                if (j < nbk) {
-                    S[(long long)i * n + kb + j] = v[j];
-                    if (i - r0 < CH_PANEL_ROWS) panel[i - r0][j] = v[j];
-                }
+                S[(long long)i * np + kb + j] = v[j];
+                panel[i - r0][j] = v[j];
             }
         }
         __syncthreads();
-        // (3) trailing update of the lower triangle: A22 -= L21 L21^T
-        const int m = n - r0;
-        const long long tri = (long long)m * (m + 1) / 2;
-        for (long long t = tid; t < tri; t += CH_THREADS) {
-            // t -> (i, k) with k <= i, row-major lower triangle
-            int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-            while ((long long)(i + 1) * (i + 2) / 2 <= t) i++;
-            while ((long long)i * (i + 1) / 2 > t) i--;
-            const int k = (int)(t - (long long)i * (i + 1) / 2);
-            double s = 0;
-            if (i < CH_PANEL_ROWS) {
-#pragma unroll
-                for (int j = 0; j < NB; j++)
-                    if (j < nbk) s += panel[i][j] * panel[k][j];
-            } else {
-                for (int j = 0; j < nbk; j++) s += S[(long long)(r0 + i) * n + kb + j] * S[(long long)(r0 + k) * n + kb + j];
+        const int mt = m / NB;
+        const int ntiles = mt * (mt + 1) / 2;
+        for (int t = wave; t < ntiles; t += CH_WAVES) {
+            int ti = 0, rem = t;
+            while (rem > ti) {
+                rem -= ti + 1;
+                ti++;
             }
-            S[(long long)(r0 + i) * n + r0 + k] -= s;
+            const int tk = rem;
+            const int col = lane & 15, rb = lane >> 4;
+            dbl4 c;
+#pragma unroll
+            for (int r = 0; r < 4; r++) c[r] = S[(long long)(r0 + ti * NB + rb + 4 * r) * np + r0 + tk * NB + col];
+#pragma unroll
+            for (int kk = 0; kk < NB / 4; kk++) {
+                const double av = -panel[ti * NB + (lane & 15)][kk * 4 + (lane >> 4)];
+                const double bv = panel[tk * NB + (lane & 15)][kk * 4 + (lane >> 4)];
+                c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) S[(long long)(r0 + ti * NB + rb + 4 * r) * np + r0 + tk * NB + col] = c[r];
         }
         __syncthreads();
     }
@@ -594,45 +438,60 @@ __global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict_
         if (tid == 0) *fail = 1;
         return;
     }
-    // forward: L y = b (y stored in x)
-    for (int i = tid; i < n; i += CH_THREADS) x[i] = b[i];
+    for (int i = tid; i < np; i += CH_THREADS) x[i] = i < n ? b[i] : 0.0;
     __syncthreads();
-    for (int kb = 0; kb < n; kb += NB) {
-        const int nbk = min(NB, n - kb);
-        if (tid < kWave) {
-            // one wave solves the 16x16 triangle sequentially (lane 0), broadcast via LDS
-            if (tid == 0) {
-                for (int j = 0; j < nbk; j++) {
-                    double s = x[kb + j];
-                    for (int k = 0; k < j; k++) s -= S[(long long)(kb + j) * n + kb + k] * ytile[k];
-                    ytile[j] = s / S[(long long)(kb + j) * n + kb + j];
-                    x[kb + j] = ytile[j];
-                }
+    // forward: L y = b
+    for (int kb = 0; kb < np; kb += NB) {
+        if (wave == 0) {
+            const int l = lane & 15;
+            double Lrow[NB];
+#pragma unroll
+            for (int k = 0; k < NB; k++) Lrow[k] = S[(long long)(kb + l) * np + kb + k];
+            double s = x[kb + l], y = 0;
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const double yj = __shfl(s / Lrow[j], j);
+                if (l == j) y = yj;
+                if (l > j) s -= Lrow[j] * yj;
+            }
+            if (lane < NB) {
+                x[kb + l] = y;
+                yv[l] = y;
             }
         }
         __syncthreads();
-        for (int i = kb + nbk + tid; i < n; i += CH_THREADS) {
+        for (int i = kb + NB + tid; i < np; i += CH_THREADS) {
             double s = 0;
-            for (int j = 0; j < nbk; j++) s += S[(long long)i * n + kb + j] * ytile[j];
+#pragma unroll
+            for (int j = 0; j < NB; j++) s += S[(long long)i * np + kb + j] * yv[j];
             x[i] -= s;
         }
         __syncthreads();
     }
     // backward: L^T x = y
-    for (int kb = ((n - 1) / NB) * NB; kb >= 0; kb -= NB) {
-        const int nbk = min(NB, n - kb);
-        if (tid == 0) {
-            for (int j = nbk - 1; j >= 0; j--) {
-                double s = x[kb + j];
-                for (int k = j + 1; k < nbk; k++) s -= S[(long long)(kb + k) * n + kb + j] * ytile[k];
-                ytile[j] = s / S[(long long)(kb + j) * n + kb + j];
-                x[kb + j] = ytile[j];
+    for (int kb = np - NB; kb >= 0; kb -= NB) {
+        if (wave == 0) {
+            const int l = lane & 15;
+            double Lcol[NB];  // Lcol[k] = L[kb+k][kb+l]
+#pragma unroll
+            for (int k = 0; k < NB; k++) Lcol[k] = S[(long long)(kb + k) * np + kb + l];
+            double s = x[kb + l], y = 0;
+#pragma unroll
+            for (int j = NB - 1; j >= 0; j--) {
+                const double yj = __shfl(s / Lcol[j], j);
+                if (l == j) y = yj;
+                if (l < j) s -= Lcol[j] * yj;
+            }
+            if (lane < NB) {
+                x[kb + l] = y;
+                yv[l] = y;
             }
         }
         __syncthreads();
         for (int i = tid; i < kb; i += CH_THREADS) {
             double s = 0;
-            for (int j = 0; j < nbk; j++) s += S[(long long)(kb + j) * n + i] * ytile[j];
+#pragma unroll
+            for (int j = 0; j < NB; j++) s += S[(long long)(kb + j) * np + i] * yv[j];
             x[i] -= s;
         }
         __syncthreads();
@@ -656,6 +515,7 @@ __global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const do
     double cl[3] = {bl[3 * p], bl[3 * p + 1], bl[3 * p + 2]};
     for (int a = pb.pstart[p]; a < pb.pstart[p + 1]; a++) {
         const int e = pb.pedges[a];
+        if (!pb.active[e]) continue;
         const int h = pb.camh[pb.ecam[e]];
         if (h < 0) continue;
         const double* W = Hpl + 18 * (long long)e;
@@ -706,41 +566,40 @@ __global__ __launch_bounds__(BA_THREADS) void update_state(Problem pb, State A, 
 }
 
 // StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) per active edge at state s using the
-// stored errors: flag[e] = 1 if behind the camera or |e|^2 > maxErrorSquare.
+// stored errors: an edge behind the camera or with |e|^2 > maxErrorSquare is removed (active
+// byte cleared, index appended; the host sorts the short list into g2o's active-edge order).
 __global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s, int E,
-                                                           const unsigned char* __restrict__ active,
+                                                           unsigned char* __restrict__ active,
                                                            const double* __restrict__ err,
                                                            double maxErrSq,
-                                                           unsigned char* __restrict__ flag,
+                                                           uint32_t* __restrict__ out_list,
+                                                           uint32_t* __restrict__ out_count,
                                                            double* __restrict__ sum_part,
                                                            double* __restrict__ cnt_part)
 {
     __shared__ double ssum[BA_THREADS], scnt[BA_THREADS];
     const int e = blockIdx.x * BA_THREADS + threadIdx.x;
     double vs = 0, vc = 0;
-    if (e < E) {
-        unsigned char fl = 0;
-        if (active[e]) {
-            const double e0 = err[2 * e], e1 = err[2 * e + 1];
-            const double sumSquares = e0 * e0 + e1 * e1;
-            const int c = pb.ecam[e], p = pb.ept[e];
-            // SE3Quat::inverse: q* , -(q* t); forward = q* (0,0,1)
-            const double qc[4] = {-s.q[4 * c], -s.q[4 * c + 1], -s.q[4 * c + 2], s.q[4 * c + 3]};
-            const double tt[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
-            double it[3], fwd[3];
-            d_qrot(qc, tt, it);
-            const double z[3] = {0, 0, 1};
-            d_qrot(qc, z, fwd);
-            const double dot = (s.p[3 * p] + it[0]) * fwd[0] + (s.p[3 * p + 1] + it[1]) * fwd[1] +
-                               (s.p[3 * p + 2] + it[2]) * fwd[2];
-            if (dot <= 0 || sumSquares > maxErrSq) {
-                fl = 1;
-            } else {
-                vs = sumSquares;
-                vc = 1;
-            }
+    if (e < E && active[e]) {
+        const double e0 = err[2 * e], e1 = err[2 * e + 1];
+        const double sumSquares = e0 * e0 + e1 * e1;
+        const int c = pb.ecam[e], p = pb.ept[e];
+        // SE3Quat::inverse: q*, -(q* t); forward = q* (0,0,1)
+        const double qc[4] = {-s.q[4 * c], -s.q[4 * c + 1], -s.q[4 * c + 2], s.q[4 * c + 3]};
+        const double tt[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
+        double it[3], fwd[3];
+        d_qrot(qc, tt, it);
+        const double z[3] = {0, 0, 1};
+        d_qrot(qc, z, fwd);
+        const double dot = (s.p[3 * p] + it[0]) * fwd[0] + (s.p[3 * p + 1] + it[1]) * fwd[1] +
+                           (s.p[3 * p + 2] + it[2]) * fwd[2];
+        if (dot <= 0 || sumSquares > maxErrSq) {
+            active[e] = 0;
+            out_list[atomicAdd(out_count, 1u)] = (uint32_t)e;
+        } else {
+            vs = sumSquares;
+            vc = 1;
         }
-        flag[e] = fl;
     }
     ssum[threadIdx.x] = vs;
     scnt[threadIdx.x] = vc;
@@ -758,6 +617,26 @@ __global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s, 
     }
 }
 
+// After removals: points keep their system membership only while they have an active edge
+// (SparseOptimizer::initializeOptimization); cameras' active-edge counts tell the host whether
+// the block numbering must be rebuilt.
+__global__ __launch_bounds__(BA_THREADS) void refresh_membership(Problem pb, int points_fixed,
+                                                                 int* __restrict__ ptfree,
+                                                                 int* __restrict__ cam_active)
+{
+    const int i = blockIdx.x * BA_THREADS + threadIdx.x;
+    if (i < pb.P) {
+        int any = 0;
+        for (int a = pb.pstart[i]; a < pb.pstart[i + 1] && !any; a++) any = pb.active[pb.pedges[a]];
+        ptfree[i] = !points_fixed && any;
+    }
+    if (i < pb.C) {
+        int cnt = 0;
+        for (int a = pb.cstart[i]; a < pb.cstart[i + 1]; a++) cnt += pb.active[pb.cedges[a]];
+        cam_active[i] = cnt;
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -772,18 +651,20 @@ struct BundleAdjuster {
     std::vector<double> q, t, camk, p, uv, info;
     std::vector<int> fixed, ecam, ept;
     std::vector<unsigned char> removed;
-    bool dirty = true, useless = false, state_on_device = false, host_state_stale = false;
+    bool dirty = true;  // full (re)initialisation needed: setters or a camera left the system
+    bool useless = false, state_on_device = false, host_state_stale = false, err_initialized = false;
     int iteration = 0;
     double user_lambda = 0, lambda = 0, ni = 2, huber = 0;
-    int n = 0;  // 6 * cameras in the system
+    int n = 0, np = 0;  // 6 * cameras in the system, padded to a multiple of 16
+    int npairs = 0;
     std::vector<int> camh, ptfree, cam_of_block;
     hipStream_t st = nullptr;
     int cur = 0;  // which state buffer holds the current estimate
     // device buffers
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
-        d_pstart, d_pedges, d_cstart, d_cedges, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp, d_bp,
-        d_Dinv, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_flag, d_osum, d_ocnt,
-        d_camblk, d_fail;
+        d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
+        d_bp, d_Dinv, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_ocnt, d_camblk,
+        d_pairs, d_fail, d_olist, d_camcnt;
     mage_ba_stats stats{};
 
     Problem problem() const
@@ -798,10 +679,12 @@ struct BundleAdjuster {
         pb.ecam = d_ecam.as<int>();
         pb.ept = d_ept.as<int>();
         pb.info = d_info.as<double>();
+        pb.active = d_active.as<unsigned char>();
         pb.pstart = d_pstart.as<int>();
         pb.pedges = d_pedges.as<int>();
         pb.cstart = d_cstart.as<int>();
         pb.cedges = d_cedges.as<int>();
+        pb.cpt = d_cpt.as<int>();
         pb.huber = huber;
         return pb;
     }
@@ -809,11 +692,11 @@ struct BundleAdjuster {
 
     void release()
     {
-        for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh,
-                        &d_ptfree, &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart,
-                        &d_cedges, &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_Dinv,
-                        &d_db, &d_S, &d_rhs, &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_flag,
-                        &d_osum, &d_ocnt, &d_camblk, &d_fail})
+        for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
+                        &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
+                        &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_Dinv, &d_db, &d_S, &d_rhs,
+                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_ocnt, &d_camblk, &d_pairs,
+                        &d_fail, &d_olist, &d_camcnt})
             b->release();
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
@@ -828,7 +711,7 @@ struct BundleAdjuster {
         return MAGE_OK;
     }
 
-    // Pull the current estimate back to the host vectors (before re-initialisation).
+    // Pull the current estimate back to the host vectors.
     mage_status sync_host_state()
     {
         if (!state_on_device || !host_state_stale) return MAGE_OK;
@@ -841,7 +724,7 @@ struct BundleAdjuster {
     }
 
     // SparseOptimizer::initializeOptimization (+ StepOptimizer::InitializeOptimization):
-    // active edges, vertices in the system, CSR structures; iteration reset to 0.
+    // active edges, vertices in the system, CSR structures, covisible camera pairs; iteration 0.
     mage_status initialize()
     {
         mage_status r = sync_host_state();
@@ -870,10 +753,12 @@ struct BundleAdjuster {
                 ptfree[i] = 1;
                 nfp++;
             }
-        n = 6 * (int)cam_of_block.size();
-        useless = (cam_of_block.empty() && nfp == 0);
-        MAGE_REQUIRE((int)cam_of_block.size() <= SCHUR_MAX_BLOCKS, MAGE_EUNSUPPORTED,
-                     "more than 96 free cameras in one bundle adjustment");
+        const int nb = (int)cam_of_block.size();
+        n = 6 * nb;
+        np = (n + 15) / 16 * 16;
+        useless = (nb == 0 && nfp == 0);
+        MAGE_REQUIRE(nb <= CH_PANEL_ROWS / 6, MAGE_EUNSUPPORTED, "more than 96 free cameras in one bundle adjustment");
+        // CSR by point (edge order) and by camera (point order, then edge order)
         std::vector<int> pstart(P + 1, 0), cstart(C + 1, 0);
         for (int e = 0; e < E; e++)
             if (active[e]) {
@@ -882,15 +767,41 @@ struct BundleAdjuster {
             }
         for (int i = 0; i < P; i++) pstart[i + 1] += pstart[i];
         for (int c = 0; c < C; c++) cstart[c + 1] += cstart[c];
-        std::vector<int> pedges(std::max(pstart[P], 1)), cedges(std::max(cstart[C], 1));
+        std::vector<int> pedges(std::max(pstart[P], 1)), cedges(std::max(cstart[C], 1)), cpt(std::max(cstart[C], 1));
         {
             std::vector<int> pf(pstart.begin(), pstart.end() - 1), cf(cstart.begin(), cstart.end() - 1);
             for (int e = 0; e < E; e++)
-                if (active[e]) {
-                    pedges[pf[ept[e]]++] = e;
-                    cedges[cf[ecam[e]]++] = e;
+                if (active[e]) pedges[pf[ept[e]]++] = e;
+            // walking points in order makes each camera's list sorted by point id
+            for (int i = 0; i < P; i++)
+                for (int a = pstart[i]; a < pstart[i + 1]; a++) {
+                    const int e = pedges[a];
+                    cedges[cf[ecam[e]]] = e;
+                    cpt[cf[ecam[e]]++] = i;
                 }
         }
+        // covisible camera pairs (h1 <= h2) of the reduced system
+        std::vector<int2> pairs;
+        if (nb > 0) {
+            std::vector<unsigned char> mark((size_t)nb * nb, 0);
+            std::vector<int> hs;
+            for (int i = 0; i < P; i++) {
+                if (!ptfree[i]) continue;
+                hs.clear();
+                for (int a = pstart[i]; a < pstart[i + 1]; a++) {
+                    const int h = camh[ecam[pedges[a]]];
+                    if (h >= 0) hs.push_back(h);
+                }
+                for (int x : hs)
+                    for (int y : hs)
+                        if (x <= y) mark[(size_t)x * nb + y] = 1;
+            }
+            for (int h = 0; h < nb; h++) mark[(size_t)h * nb + h] = 1;
+            for (int x = 0; x < nb; x++)
+                for (int y = x; y < nb; y++)
+                    if (mark[(size_t)x * nb + y]) pairs.push_back(make_int2(x, y));
+        }
+        npairs = (int)pairs.size();
         if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
         if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
         if ((r = upload(d_active, active)) != MAGE_OK) return r;
@@ -898,7 +809,9 @@ struct BundleAdjuster {
         if ((r = upload(d_pedges, pedges)) != MAGE_OK) return r;
         if ((r = upload(d_cstart, cstart)) != MAGE_OK) return r;
         if ((r = upload(d_cedges, cedges)) != MAGE_OK) return r;
+        if ((r = upload(d_cpt, cpt)) != MAGE_OK) return r;
         if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
+        if ((r = upload(d_pairs, pairs)) != MAGE_OK) return r;
         if (!state_on_device) {
             if ((r = upload(d_q[0], q)) != MAGE_OK) return r;
             if ((r = upload(d_t[0], t)) != MAGE_OK) return r;
@@ -910,143 +823,148 @@ struct BundleAdjuster {
             state_on_device = true;
         }
         const size_t Pm = std::max(P, 1), Cm = std::max(C, 1), Em = std::max(E, 1);
+        const size_t npm = std::max(np, 16);
         for (auto pr : {std::make_pair(&d_err, Em * 2 * 8), std::make_pair(&d_Hll, Pm * 9 * 8),
                         std::make_pair(&d_bl, Pm * 3 * 8), std::make_pair(&d_Hpl, Em * 18 * 8),
                         std::make_pair(&d_Hpp, Cm * 36 * 8), std::make_pair(&d_bp, Cm * 6 * 8),
                         std::make_pair(&d_Dinv, Pm * 9 * 8), std::make_pair(&d_db, Pm * 3 * 8),
-                        std::make_pair(&d_S, (size_t)std::max(n, 1) * std::max(n, 1) * 8),
-                        std::make_pair(&d_rhs, (size_t)std::max(n, 1) * 8),
-                        std::make_pair(&d_x, ((size_t)n + 3 * Pm + 1) * 8),
-                        std::make_pair(&d_chi, Pm * 8), std::make_pair(&d_maxd, (Pm + Cm) * 8),
-                        std::make_pair(&d_scale, (Pm + Cm) * 8), std::make_pair(&d_red, (size_t)64),
-                        std::make_pair(&d_flag, Em), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 8),
-                        std::make_pair(&d_ocnt, (Em / BA_THREADS + 2) * 8), std::make_pair(&d_fail, (size_t)16)})
+                        std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
+                        std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, Pm * 8),
+                        std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
+                        std::make_pair(&d_red, (size_t)128), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 8),
+                        std::make_pair(&d_ocnt, (Em / BA_THREADS + 2) * 8), std::make_pair(&d_fail, (size_t)16),
+                        std::make_pair(&d_olist, Em * 4 + 16), std::make_pair(&d_camcnt, Cm * 4)})
             if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
         MAGE_HIP(hipMemsetAsync(d_maxd.ptr, 0, (Pm + Cm) * 8, st));
         MAGE_HIP(hipMemsetAsync(d_scale.ptr, 0, (Pm + Cm) * 8, st));
+        if (!err_initialized) {
+            MAGE_HIP(hipMemsetAsync(d_err.ptr, 0, Em * 2 * 8, st));
+            err_initialized = true;
+        }
         iteration = 0;
         dirty = false;
         return MAGE_OK;
     }
 
-    // errors (+ linearisation) of the current state; returns chi2 (and max diagonal)
-    mage_status linearize(bool lin, double* chi, double* maxd)
+    // Linearise the current state (errors, Hll/bl/Hpl, Hpp/bp) and reduce chi2 / max diagonal
+    // into d_red[0..2]; no host synchronisation.
+    mage_status linearize()
     {
         Problem pb = problem();
         const int gp = (P + BA_THREADS - 1) / BA_THREADS;
-        if (P > 0)
-            {
-                KernelTimer _kt("ba.point_linearize", st);
-                hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(cur), lin ? 1 : 0,
-                                   d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
-                                   d_chi.as<double>(), d_maxd.as<double>());
-            }
-        MAGE_HIP(hipGetLastError());
-        if (lin && C > 0) {
-            {
-                KernelTimer _kt("ba.cam_linearize", st);
-                hipLaunchKernelGGL(cam_linearize, dim3(C), dim3(BA_THREADS), 0, st, pb, state(cur), d_err.as<double>(),
-                                   d_Hpp.as<double>(), d_bp.as<double>(), d_maxd.as<double>() + P);
-            }
-            MAGE_HIP(hipGetLastError());
+        if (P > 0) {
+            KernelTimer _kt("ba.point_linearize", st);
+            hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(cur), 1,
+                               d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
+                               d_chi.as<double>(), d_maxd.as<double>());
+        }
+        if (C > 0) {
+            KernelTimer _kt("ba.cam_linearize", st);
+            hipLaunchKernelGGL(cam_linearize, dim3(C), dim3(BA_THREADS), 0, st, pb, state(cur), d_err.as<double>(),
+                               d_Hpp.as<double>(), d_bp.as<double>(), d_maxd.as<double>() + P);
         }
         {
             KernelTimer _kt("ba.reduce", st);
             hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_chi.as<double>(), 0,
-                               d_maxd.as<double>(), lin ? P + C : 0, d_red.as<double>());
+                               d_maxd.as<double>(), P + C, d_red.as<double>());
         }
         MAGE_HIP(hipGetLastError());
-        double h[3];
-        MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
-        MAGE_HIP(hipStreamSynchronize(st));
-        *chi = h[0];
-        if (maxd) *maxd = h[2];
         return MAGE_OK;
     }
 
     // One trial: solve with lambda, build the trial state in the other buffer, evaluate it.
-    mage_status trial(double lam, bool* ok, double* tempChi, double* scale)
+    // Reads back red[0..5] = {chi(current), -, maxdiag, chi(trial), scale, -} and the fail flag.
+    mage_status trial(double lam, bool* ok, double red[6])
     {
         Problem pb = problem();
         const int gp = (P + BA_THREADS - 1) / BA_THREADS;
         const int gmax = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
         double* xp = d_x.as<double>();
-        double* xl = d_x.as<double>() + n;
+        double* xl = d_x.as<double>() + np;
         MAGE_HIP(hipMemsetAsync(d_fail.ptr, 0, 4, st));
-        if (P > 0 && !points_fixed)
-            {
-                KernelTimer _kt("ba.point_schur", st);
-                hipLaunchKernelGGL(point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
-                                   d_Hll.as<double>(), d_bl.as<double>(), lam, d_Dinv.as<double>(), d_db.as<double>());
-            }
+        if (P > 0 && !points_fixed) {
+            KernelTimer _kt("ba.point_schur", st);
+            hipLaunchKernelGGL(point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
+                               d_Hll.as<double>(), d_bl.as<double>(), lam, d_Dinv.as<double>(), d_db.as<double>());
+        }
         if (n > 0) {
+            MAGE_HIP(hipMemsetAsync(d_S.ptr, 0, (size_t)np * np * 8, st));
             {
-                KernelTimer _kt("ba.build_schur", st);
-                hipLaunchKernelGGL(build_schur, dim3(n / 6), dim3(BA_THREADS), 0, st, pb, n, d_camblk.as<int>(),
-                                   d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(), d_Dinv.as<double>(),
-                                   d_db.as<double>(), lam, d_S.as<double>(), d_rhs.as<double>());
+                KernelTimer _kt("ba.schur_pairs", st);
+                hipLaunchKernelGGL(schur_pairs, dim3(npairs), dim3(BA_THREADS), 0, st, pb, d_pairs.as<int2>(),
+                                   d_camblk.as<int>(), d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(),
+                                   d_Dinv.as<double>(), d_db.as<double>(), lam, np, d_S.as<double>(),
+                                   d_rhs.as<double>());
             }
             {
                 KernelTimer _kt("ba.cholesky_solve", st);
-                hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), n,
+                hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np, n,
                                    d_rhs.as<double>(), xp, d_fail.as<int>());
             }
         }
-        if (P > 0)
-            {
-                KernelTimer _kt("ba.point_backsub", st);
-                hipLaunchKernelGGL(point_backsub, dim3(gp), dim3(BA_THREADS), 0, st, pb, d_Hpl.as<double>(),
-                                   d_Dinv.as<double>(), d_bl.as<double>(), xp, lam, xl, d_scale.as<double>());
-            }
-        if (std::max(P, C) > 0)
-            {
-                KernelTimer _kt("ba.update_state", st);
-                hipLaunchKernelGGL(update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur), xp, xl,
-                                   d_bp.as<double>(), lam, d_scale.as<double>() + P);
-            }
-        if (P > 0)
-            {
-                KernelTimer _kt("ba.point_linearize", st);
-                hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
-                                   d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
-                                   d_chi.as<double>(), d_maxd.as<double>());
-            }
+        if (P > 0) {
+            KernelTimer _kt("ba.point_backsub", st);
+            hipLaunchKernelGGL(point_backsub, dim3(gp), dim3(BA_THREADS), 0, st, pb, d_Hpl.as<double>(),
+                               d_Dinv.as<double>(), d_bl.as<double>(), xp, lam, xl, d_scale.as<double>());
+        }
+        if (std::max(P, C) > 0) {
+            KernelTimer _kt("ba.update_state", st);
+            hipLaunchKernelGGL(update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur),
+                               xp, xl, d_bp.as<double>(), lam, d_scale.as<double>() + P);
+        }
+        if (P > 0) {
+            KernelTimer _kt("ba.point_linearize", st);
+            hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
+                               d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
+                               d_chi.as<double>(), d_maxd.as<double>());
+        }
         {
             KernelTimer _kt("ba.reduce", st);
-            hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_scale.as<double>(), P + C,
-                               d_maxd.as<double>(), 0, d_red.as<double>());
+            hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_scale.as<double>(),
+                               P + C, d_maxd.as<double>(), 0, d_red.as<double>() + 3);
         }
         MAGE_HIP(hipGetLastError());
-        double h[3];
         int fail = 0;
-        MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipMemcpyAsync(red, d_red.ptr, 6 * sizeof(double), hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipMemcpyAsync(&fail, d_fail.ptr, 4, hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipStreamSynchronize(st));
         *ok = fail == 0;
-        *tempChi = h[0];
-        *scale = h[1];
         return MAGE_OK;
     }
 
     // OptimizationAlgorithmLevenberg::solve (g2o); result 1 = OK, 0 = Terminate
     mage_status lm_solve(int* result)
     {
-        double currentChi = 0, maxd = 0;
-        mage_status r = linearize(true, &currentChi, &maxd);
+        mage_status r = linearize();
         if (r != MAGE_OK) return r;
-        if (iteration == 0) {
-            lambda = user_lambda > 0 ? user_lambda : 1e-5 * maxd;  // computeLambdaInit, tau = 1e-5
+        double currentChi = 0;
+        bool haveChi = false;
+        if (iteration == 0 && user_lambda <= 0) {
+            double h[3];
+            MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
+            MAGE_HIP(hipStreamSynchronize(st));
+            currentChi = h[0];
+            haveChi = true;
+            lambda = 1e-5 * h[2];  // computeLambdaInit, tau = 1e-5
+            ni = 2;
+        } else if (iteration == 0) {
+            lambda = user_lambda;
             ni = 2;
         }
         double rho = 0;
         int qmax = 0;
         do {
             bool ok2 = true;
-            double tempChi = 0, scale = 0;
-            if ((r = trial(lambda, &ok2, &tempChi, &scale)) != MAGE_OK) return r;
+            double red[6];
+            if ((r = trial(lambda, &ok2, red)) != MAGE_OK) return r;
+            if (!haveChi) {
+                currentChi = red[0];
+                haveChi = true;
+            }
+            double tempChi = red[3];
             if (!ok2) tempChi = std::numeric_limits<double>::max();
             rho = currentChi - tempChi;
-            scale += 1e-3;
+            double scale = red[4] + 1e-3;
             rho /= scale;
             stats.trials++;
             if (rho > 0 && std::isfinite(tempChi)) {
@@ -1061,7 +979,7 @@ struct BundleAdjuster {
             } else {
                 lambda *= ni;
                 ni *= 2;
-                stats.rejected_trials++;  // pop: current buffer unchanged
+                stats.rejected_trials++;  // pop: the current buffer is unchanged
             }
             qmax++;
         } while (rho < 0 && qmax < 10);
@@ -1109,31 +1027,48 @@ struct BundleAdjuster {
             return MAGE_OK;
         }
         const int ge = (E + BA_THREADS - 1) / BA_THREADS;
+        uint32_t* d_count = d_olist.as<uint32_t>() + E;
+        MAGE_HIP(hipMemsetAsync(d_count, 0, 4, st));
         {
             KernelTimer _kt("ba.outlier_pass", st);
             hipLaunchKernelGGL(outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), state(cur), E,
                                d_active.as<unsigned char>(), d_err.as<double>(), (double)maxErrSq,
-                               d_flag.as<unsigned char>(), d_osum.as<double>(), d_ocnt.as<double>());
+                               d_olist.as<uint32_t>(), d_count, d_osum.as<double>(), d_ocnt.as<double>());
         }
         {
             KernelTimer _kt("ba.reduce", st);
             hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_osum.as<double>(), ge, d_ocnt.as<double>(), ge,
-                               d_osum.as<double>(), 0, d_red.as<double>());
+                               d_osum.as<double>(), 0, d_red.as<double>() + 6);
         }
         MAGE_HIP(hipGetLastError());
-        std::vector<unsigned char> flag(E);
         double h[3];
-        MAGE_HIP(hipMemcpyAsync(flag.data(), d_flag.ptr, E, hipMemcpyDeviceToHost, st));
-        MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
-        MAGE_HIP(hipStreamSynchronize(st));
         uint32_t no = 0;
-        for (int e = 0; e < E; e++)
-            if (flag[e]) {
-                removed[e] = 1;
-                dirty = true;
-                if (no < cap) outliers[no] = (uint32_t)e;
-                no++;
+        MAGE_HIP(hipMemcpyAsync(h, d_red.as<double>() + 6, sizeof(h), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipMemcpyAsync(&no, d_count, 4, hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        if (no > 0) {
+            std::vector<uint32_t> list(no);
+            MAGE_HIP(hipMemcpyAsync(list.data(), d_olist.ptr, 4 * (size_t)no, hipMemcpyDeviceToHost, st));
+            // membership after the removal (points drop out with their last edge; a free camera
+            // without edges changes the block numbering -> full re-initialisation)
+            const int gm = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
+            {
+                KernelTimer _kt("ba.refresh_membership", st);
+                hipLaunchKernelGGL(refresh_membership, dim3(gm), dim3(BA_THREADS), 0, st, problem(),
+                                   points_fixed ? 1 : 0, d_ptfree.as<int>(), d_camcnt.as<int>());
             }
+            std::vector<int> camcnt(C);
+            MAGE_HIP(hipMemcpyAsync(camcnt.data(), d_camcnt.ptr, 4 * (size_t)C, hipMemcpyDeviceToHost, st));
+            MAGE_HIP(hipStreamSynchronize(st));
+            std::sort(list.begin(), list.end());  // g2o active-edge order = insertion order
+            for (uint32_t k = 0; k < no; k++) {
+                removed[list[k]] = 1;
+                if (k < cap) outliers[k] = list[k];
+            }
+            for (int c = 0; c < C; c++)
+                if (camh[c] >= 0 && camcnt[c] == 0) dirty = true;
+            iteration = 0;  // removeEdge dirties the optimizer: next Step re-initialises (lambda init)
+        }
         *nOut = std::min(no, cap);
         *meanSq = (float)(h[0] / h[1]);
         return no > cap ? MAGE_ECAPACITY : MAGE_OK;

@@ -1,0 +1,195 @@
+// ba_math.hpp — fp64 SE3Quat / Eigen / g2o primitives shared by the BA kernels (device code).
+// Restates g2o se3quat.h (exp, map, normalizeRotation), Eigen Quaternion (transformVector,
+// toRotationMatrix, from-matrix) and EdgeProjectXYZ2UV / RobustKernelHuber as used by BundlerLib.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mage {
+namespace ba {
+
+// ---------------- SE3Quat / Eigen primitives (device) ----------------
+
+__device__ __forceinline__ void d_cross(const double a[3], const double b[3], double c[3])
+{
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Quaternion * Vector3 (Eigen _transformVector); q = (x, y, z, w)
+__device__ __forceinline__ void d_qrot(const double q[4], const double v[3], double o[3])
+{
+    double uv[3], uv2[3];
+    d_cross(q, v, uv);
+    uv[0] += uv[0];
+    uv[1] += uv[1];
+    uv[2] += uv[2];
+    d_cross(q, uv, uv2);
+    for (int i = 0; i < 3; i++) o[i] = v[i] + q[3] * uv[i] + uv2[i];
+}
+
+__device__ __forceinline__ void d_qmat(const double q[4], double r[9])
+{
+    double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    r[0] = 1 - (tyy + tzz);
+    r[1] = txy - twz;
+    r[2] = txz + twy;
+    r[3] = txy + twz;
+    r[4] = 1 - (txx + tzz);
+    r[5] = tyz - twx;
+    r[6] = txz - twy;
+    r[7] = tyz + twx;
+    r[8] = 1 - (txx + tyy);
+}
+
+__device__ __forceinline__ void d_quat_from_matrix(const double* m, double q[4])
+{
+    double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[7] - m[5]) * t;
+        q[1] = (m[2] - m[6]) * t;
+        q[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 4]) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * t;
+        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
+        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+    }
+}
+
+__device__ __forceinline__ void d_se3_normalize(double q[4])
+{
+    if (q[3] < 0)
+        for (int i = 0; i < 4; i++) q[i] = -q[i];
+    double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; i++) q[i] /= n;
+}
+
+// T <- exp(u) * T  (VertexSE3Expmap::oplusImpl with SE3Quat::exp, g2o se3quat.h)
+__device__ void d_oplus(double q[4], double t[3], const double u[6])
+{
+    const double w0 = u[0], w1 = u[1], w2 = u[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) O2[r * 3 + c] = O[r * 3] * O[c] + O[r * 3 + 1] * O[3 + c] + O[r * 3 + 2] * O[6 + c];
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+        const double c = (theta - sin(theta)) / (theta * theta * theta);
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4 == 0 ? 1.0 : 0.0);
+            R[i] = I + a * O[i] + b * O2[i];
+            V[i] = I + b * O[i] + c * O2[i];
+        }
+    }
+    double eq[4], et[3];
+    d_quat_from_matrix(R, eq);
+    for (int r = 0; r < 3; r++) et[r] = V[r * 3] * u[3] + V[r * 3 + 1] * u[4] + V[r * 3 + 2] * u[5];
+    d_se3_normalize(eq);
+    // result = e * T: t' = e.t + e.q * T.t ; q' = e.q * T.q
+    double rt[3];
+    d_qrot(eq, t, rt);
+    double nq[4];
+    nq[3] = eq[3] * q[3] - eq[0] * q[0] - eq[1] * q[1] - eq[2] * q[2];
+    nq[0] = eq[3] * q[0] + eq[0] * q[3] + eq[1] * q[2] - eq[2] * q[1];
+    nq[1] = eq[3] * q[1] + eq[1] * q[3] + eq[2] * q[0] - eq[0] * q[2];
+    nq[2] = eq[3] * q[2] + eq[2] * q[3] + eq[0] * q[1] - eq[1] * q[0];
+    d_se3_normalize(nq);
+    for (int i = 0; i < 4; i++) q[i] = nq[i];
+    for (int i = 0; i < 3; i++) t[i] = et[i] + rt[i];
+}
+
+__device__ __forceinline__ void d_huber(double delta, double e2, double& rho0, double& rho1)
+{
+    const double dsqr = delta * delta;
+    if (e2 <= dsqr) {
+        rho0 = e2;
+        rho1 = 1.0;
+    } else {
+        const double sq = sqrt(e2);
+        rho0 = 2 * sq * delta - dsqr;
+        rho1 = delta / sq;
+    }
+}
+
+struct State {  // one copy of the optimisable state
+    double* q;  // C x 4
+    double* t;  // C x 3
+    double* p;  // P x 3
+};
+
+struct Problem {
+    int C, P;
+    const double* camk;           // C x 3: f, cx, cy
+    const int* camh;              // C: Hessian block index or -1
+    const int* ptfree;            // P: 1 if the point is in the system
+    const double* uv;             // E x 2
+    const int* ecam;              // E
+    const int* ept;               // E
+    const double* info;           // E
+    const unsigned char* active;  // E: edge in the optimizer's active set
+    const int* pstart;            // P+1
+    const int* pedges;            // edges by point (edge order), filtered by `active`
+    const int* cstart;            // C+1
+    const int* cedges;            // edges by camera, sorted by point id, filtered by `active`
+    const int* cpt;               // point id of each cedges entry (binary search key)
+    double huber;
+};
+
+// computeError + chi2 + robustify for one edge at state s; returns rho0, writes err, xc
+__device__ __forceinline__ void edge_eval(const Problem& pb, const State& s, int e, double err[2],
+                                          double xc[3], double& rho0, double& rho1)
+{
+    const int c = pb.ecam[e], p = pb.ept[e];
+    const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
+    const double X[3] = {s.p[3 * p], s.p[3 * p + 1], s.p[3 * p + 2]};
+    d_qrot(q, X, xc);
+    xc[0] += s.t[3 * c];
+    xc[1] += s.t[3 * c + 1];
+    xc[2] += s.t[3 * c + 2];
+    const double f = pb.camk[3 * c], cx = pb.camk[3 * c + 1], cy = pb.camk[3 * c + 2];
+    err[0] = pb.uv[2 * e] - (xc[0] / xc[2] * f + cx);
+    err[1] = pb.uv[2 * e + 1] - (xc[1] / xc[2] * f + cy);
+    const double inf = pb.info[e];
+    const double chi2 = inf * (err[0] * err[0] + err[1] * err[1]);
+    d_huber(pb.huber, chi2, rho0, rho1);
+}
+
+// EdgeProjectXYZ2UV::linearizeOplus pose block (2x6, row-major)
+__device__ __forceinline__ void jac_pose(const double xc[3], double f, double Jp[12])
+{
+    const double x = xc[0], y = xc[1], z = xc[2], z2 = z * z;
+    Jp[0] = x * y / z2 * f;
+    Jp[1] = -(1 + (x * x / z2)) * f;
+    Jp[2] = y / z * f;
+    Jp[3] = -1. / z * f;
+    Jp[4] = 0;
+    Jp[5] = x / z2 * f;
+    Jp[6] = (1 + y * y / z2) * f;
+    Jp[7] = -x * y / z2 * f;
+    Jp[8] = -x / z * f;
+    Jp[9] = 0;
+    Jp[10] = -1. / z * f;
+    Jp[11] = y / z2 * f;
+}
+
+
+}  // namespace ba
+}  // namespace mage

@@ -1,0 +1,102 @@
+"""Summarise rocprofv3 outputs into profiles/ (committed evidence).
+
+Usage: python tools/rocprof_summary.py <prof_dir> <round_tag>
+  <prof_dir>/trace/run_kernel_stats.csv          (--kernel-trace --stats)
+  <prof_dir>/pmc_fetch/run_counter_collection.csv (--pmc FETCH_SIZE, its own pass)
+  <prof_dir>/pmc_write/run_counter_collection.csv (--pmc WRITE_SIZE, its own pass)
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB; on gfx950
+FETCH_SIZE reads half the bytes of a wide (16 B/lane) coalesced stream, so the corrected read
+side is 2 x FETCH_SIZE for such kernels.  Our kernels mix widths, so both the raw and the x2
+figures are kept; `hbm_bytes_per_launch` uses the raw FETCH (lower bound) + WRITE.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def short(name: str) -> str:
+    m = re.search(r"::([A-Za-z0-9_]+)\(", name)
+    base = m.group(1) if m else name.split("(")[0]
+    return base
+
+
+KERNEL_TAG = {
+    "fast_nms_kernel": "orb.fast_nms", "select_kernel": "orb.select", "describe_kernel": "orb.describe",
+    "match_kernel": "match.two_way", "build_schur": "ba.build_schur", "cholesky_solve": "ba.cholesky_solve",
+    "point_linearize": "ba.point_linearize", "cam_linearize": "ba.cam_linearize",
+    "point_backsub": "ba.point_backsub", "point_schur": "ba.point_schur", "update_state": "ba.update_state",
+    "outlier_pass": "ba.outlier_pass", "reduce3": "ba.reduce",
+}
+
+
+def read_stats(path: Path):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append({"kernel": short(r["Name"]), "calls": int(r["Calls"]),
+                         "avg_us": float(r["AverageNs"]) / 1e3, "total_ms": float(r["TotalDurationNs"]) / 1e6,
+                         "pct": float(r["Percentage"])})
+    return rows
+
+
+def read_pmc(path: Path, counter: str):
+    acc = defaultdict(lambda: [0.0, 0])
+    if not path.exists():
+        return {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            k = short(r["Kernel_Name"])
+            acc[k][0] += float(r["Counter_Value"])
+            acc[k][1] += 1
+    return {k: v[0] / v[1] for k, v in acc.items()}
+
+
+def main():
+    prof = Path(sys.argv[1])
+    tag = sys.argv[2]
+    out_dir = ROOT / "profiles"
+    out_dir.mkdir(exist_ok=True)
+    stats = read_stats(prof / "trace" / "run_kernel_stats.csv")
+    fetch = read_pmc(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
+    write = read_pmc(prof / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
+    lines = [f"# rocprofv3 summary — {tag}", "",
+             "`rocprofv3 --kernel-trace --stats` (durations) and separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` "
+             "passes of `python bench.py` on one MI355X.  KiB counters converted to bytes; FETCH x2 is the "
+             "gfx950 wide-stream correction (MI355X_MICROARCH.md §HBM).", "",
+             "| kernel | calls | avg µs | total ms | % | FETCH MB/launch (raw) | FETCH x2 | WRITE MB/launch |",
+             "|---|---|---|---|---|---|---|---|"]
+    summary = {}
+    for r in stats:
+        k = r["kernel"]
+        f = fetch.get(k)
+        w = write.get(k)
+        fmb = f * 1024 / 1e6 if f is not None else None
+        wmb = w * 1024 / 1e6 if w is not None else None
+        lines.append(f"| {k} | {r['calls']} | {r['avg_us']:.1f} | {r['total_ms']:.2f} | {r['pct']:.1f} | "
+                     f"{'' if fmb is None else f'{fmb:.3f}'} | {'' if fmb is None else f'{2 * fmb:.3f}'} | "
+                     f"{'' if wmb is None else f'{wmb:.3f}'} |")
+        tagname = KERNEL_TAG.get(k)
+        if tagname:
+            summary[tagname] = {"avg_us": r["avg_us"], "calls": r["calls"],
+                                "fetch_bytes_per_launch": None if f is None else f * 1024,
+                                "write_bytes_per_launch": None if w is None else w * 1024,
+                                "hbm_bytes_per_launch": None if (f is None or w is None) else (f + w) * 1024,
+                                "hbm_bytes_per_launch_fetch_x2": None if (f is None or w is None) else (2 * f + w) * 1024}
+    (out_dir / f"{tag}_rocprof.md").write_text("\n".join(lines) + "\n")
+    (out_dir / f"{tag}_pmc_summary.json").write_text(json.dumps(summary, indent=1))
+    (out_dir / "pmc_summary.json").write_text(json.dumps(summary, indent=1))
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
