@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
+    p.add_argument("--cpu-dry-run", action="store_true", help="gloo rehearsal of the multi-rank flow (tests)")
     return p.parse_args()
 
 
@@ -96,7 +97,7 @@ def cpu_orb_baseline(args, budget_s):
 
 
 def run_orb(args, rank, world, local_rank, torch, dist):
-    from mageslam_amd import _lib, matcher, orb, synth
+    from mageslam_amd import _lib, matcher, multigpu, orb, synth
 
     W, H, N, B = args.width, args.height, args.features, args.batch
     F = max(B, (args.frames // B) * B)
@@ -104,7 +105,7 @@ def run_orb(args, rank, world, local_rank, torch, dist):
     stream = torch.cuda.current_stream(dev).cuda_stream
     det = orb.OrbDetector(nfeatures=N, device=local_rank)
     frames = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
-    orb.synth_frames_device(frames, F, W, H, 0, synth.FRAME_SEED + rank, stream=stream)
+    orb.synth_frames_device(frames, F, W, H, 0, multigpu.sequence_seed(synth.FRAME_SEED, rank), stream=stream)
     kp = torch.zeros((B + 1, N * 28), dtype=torch.uint8, device=dev)
     desc = torch.zeros((B + 1, N, 32), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(B + 1, dtype=torch.int32, device=dev)
@@ -130,30 +131,21 @@ def run_orb(args, rank, world, local_rank, torch, dist):
     if args.profile:
         lib.mage_profile_reset()
         lib.mage_profile_enable(1)
-    if world > 1:
-        dist.barrier()
+    multigpu.barrier(dist)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.warmup, args.warmup + args.steps):
         step(s)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    multigpu.barrier(dist)
     el = time.perf_counter() - t0
     lib.mage_profile_enable(0)
     kern = _lib.profile_report() if args.profile else {}
     det.device_status()
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el_max = float(el_t.item())
-    # end-of-run exchange: per-frame (keypoints, matches) of the last batch from every rank
+    el_max = multigpu.max_over_ranks(el, dev, dist)
+    # end-of-run exchange (RCCL over xGMI): per-frame (keypoints, matches) of the last batch
     summary = torch.stack([cnt[1:].to(torch.int64), nm.to(torch.int64)], 1)
-    gathered = [torch.zeros_like(summary) for _ in range(world)]
-    if world > 1:
-        dist.all_gather(gathered, summary)
-    else:
-        gathered = [summary]
+    gathered = multigpu.gather_rows(summary, dist)
     frames_total = world * args.steps * B
     res = {
         "value": frames_total / el_max,
@@ -238,19 +230,52 @@ def cpu_ba_baseline(g, budget_s):
                       f"single thread, {el:.1f} s"}
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+def run_dry(args, rank, world, dist):
+    """CPU rehearsal of the multi-rank control flow (gloo): per-rank sequences, timed loop,
+    max-reduce and the end-of-run gather, with the GPU kernels replaced by frame synthesis."""
     import torch
 
-    torch.cuda.set_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
+    from mageslam_amd import multigpu, synth
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    seed = multigpu.sequence_seed(synth.FRAME_SEED, rank)
+    w, h, B = 64, 48, 4
+    multigpu.barrier(dist)
+    t0 = time.perf_counter()
+    sums = []
+    for s in range(args.steps):
+        fr = synth.frames(s * B, B, w, h, seed)
+        sums.append(fr.reshape(B, -1).sum(1))
+    el = time.perf_counter() - t0
+    el_max = multigpu.max_over_ranks(el, "cpu", dist)
+    summary = torch.tensor(np.stack([np.full(B, rank), sums[-1]], 1), dtype=torch.int64)
+    gathered = multigpu.gather_rows(summary, dist)
+    return {"value": world * args.steps * B / el_max, "ms_per_step": 1000 * el_max / args.steps, "kernels": {},
+            "mean_keypoints": 0.0, "mean_matches": 0.0, "frames_per_step": B,
+            "gathered_ranks": [int(g[0, 0]) for g in gathered],
+            "gathered_checksums": [int(g[:, 1].sum()) for g in gathered]}
+
+
+def main():
+    args = parse()
+    from mageslam_amd import multigpu
+
+    rank, world, local_rank = multigpu.rank_env()
+    import torch
+
+    if args.cpu_dry_run:
+        dist = multigpu.init("gloo", local_rank)
+        res = run_dry(args, rank, world, dist)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": res["value"], "unit": "frames/s", "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+                              "dry_run": True, "scaling": "weak", "gathered_ranks": res["gathered_ranks"],
+                              "gathered_checksums": res["gathered_checksums"]}))
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    torch.cuda.set_device(local_rank)
+    dist = multigpu.init("nccl", local_rank)
 
     orb_res = run_orb(args, rank, world, local_rank, torch, dist)
     ba_res, g = (None, None) if args.no_ba else run_ba(args, local_rank, torch)

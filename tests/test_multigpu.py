@@ -1,0 +1,62 @@
+"""N>1 path rehearsed on CPU with gloo (world_size 2): per-rank sequences, max-over-ranks timing,
+end-of-run gather, and bench.py's JSON contract under torch.distributed.run."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch
+
+    from mageslam_amd import multigpu, synth
+
+    dist = multigpu.init("gloo", rank)
+    seed = multigpu.sequence_seed(synth.FRAME_SEED, rank)
+    fr = synth.frame(0, 32, 24, seed)
+    row = torch.tensor([[rank, int(fr.sum())]], dtype=torch.int64)
+    g = multigpu.gather_rows(row, dist)
+    m = multigpu.max_over_ranks(float(rank + 1), "cpu", dist)
+    q.put((rank, [r.tolist() for r in g], m))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_gather_and_max():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29511
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, gathered, m in res:
+        assert [g[0][0] for g in gathered] == [0, 1]  # ordered by rank
+        assert gathered[0][0][1] != gathered[1][0][1]  # independent sequences (seed + rank)
+        assert m == 2.0
+
+
+def test_bench_cpu_dry_run_world2():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29513", str(ROOT / "bench.py"), "--gpus", "2",
+           "--steps", "3", "--warmup", "1", "--cpu-dry-run"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["gathered_ranks"] == [0, 1] and d["value"] > 0
+    assert d["gathered_checksums"][0] != d["gathered_checksums"][1]
