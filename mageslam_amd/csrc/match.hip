@@ -2,17 +2,21 @@
 // GetDescriptorDistance (Core/MAGESLAM/Source/Tracking/FeatureMatcher.cpp:61-190, 453-504); the
 // reference builds two N x N float distance matrices with cv::BFMatcher::radiusMatch twice.
 //
-// One workgroup (8 waves) per (A, B) frame pair, nothing materialised in HBM:
-//   * each lane owns one A row (32 B in 8 VGPRs) and walks 64-column B tiles staged in LDS,
-//     d = sum popc(a ^ b) (v_xor + v_bcnt with accumulate), keeping the row's best and second
-//     best as packed keys (d << 16 | j) with two min and one max per pair;
-//   * the 64x64 distance tile is transposed through LDS (2 distances per dword, 65-dword row
-//     pitch: conflict-free) so that lane c then owns column c and reduces it in registers;
-//   * wave column partials merge in LDS; the final cross-check (best(a) = b and best(b) = a,
+// One workgroup (8 waves) per (A, B) frame pair, nothing materialised in HBM.
+//   * Each lane owns RPL = 4 A rows (32 B each, in VGPRs); B is staged in LDS in 1024-row
+//     tiles, split into first and second 16-byte halves.
+//   * Only pairs with d <= maxDist can change "best and second best within the radius"
+//     (radiusMatch keeps d <= maxDist; FeatureMatcher.cpp:117-156), so the reductions are a rare
+//     branch instead of per-pair work.  The first-half popcount (4 x v_xor + v_bcnt) is a lower
+//     bound of d: if it exceeds maxDist for every lane and row of the wave (one ballot), the
+//     second half is never read.  For random 256-bit descriptors and maxDist = 30 the branch is
+//     taken only around true matches.
+//   * Row best / second live in registers as packed keys (d << 16 | j); column best / second
+//     live in LDS and are updated by 64-bit compare-and-swap (order-independent: the two
+//     smallest keys of a set).  The cross-check (best(a) = b and best(b) = a,
 //     FeatureMatcher.cpp:158) and the ordered DMatch compaction run in the same launch.
-// Radius semantics follow OpenCV radiusMatch (distance <= maxDist); ties at the best distance
-// are rejected by the delta test for minDifference >= 1, and otherwise resolve to the lowest
-// index (canonical).
+// Ties at the best distance are rejected by the delta test for minDifference >= 1 and
+// otherwise resolve to the lowest index (canonical).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,15 +27,19 @@
 namespace mage {
 namespace {
 
-constexpr int MW = 8;               // waves per workgroup
-constexpr int MT = MW * kWave;      // rows per pass
-constexpr int NMAX = 4096;          // max descriptors per side (row/column state in LDS)
+constexpr int MW = 8;              // waves per workgroup
+constexpr int MT = MW * kWave;     // threads per workgroup
+constexpr int RPL = 4;             // A rows per lane
+constexpr int ROWS = MT * RPL;     // A rows per pass
+constexpr int BT = 1024;           // B rows per LDS tile
+constexpr int NMAX = 4096;         // max descriptors per side (column state in LDS)
 constexpr uint32_t INF = 0xFFFFFFFFu;
 
 struct MatchParams {
     int max_dist, min_diff;
     unsigned out_cap;
     long long a_pitch, b_pitch;  // bytes between pairs
+    uint32_t* row_scratch;       // per pair NMAX x 2 u32 (row states between passes)
 };
 
 __device__ __forceinline__ void push2(uint32_t& m1, uint32_t& m2, uint32_t key)
@@ -40,37 +48,35 @@ __device__ __forceinline__ void push2(uint32_t& m1, uint32_t& m2, uint32_t key)
     m1 = min(m1, key);
 }
 
-__device__ __forceinline__ void merge2(uint32_t& a1, uint32_t& a2, uint32_t b1, uint32_t b2)
-{
-    uint32_t n1 = min(a1, b1);
-    a2 = min(max(a1, b1), min(a2, b2));
-    a1 = n1;
-}
-
 // Row/column acceptance of FeatureMatcher.cpp:125-137 on (best, second) keys.
 __device__ __forceinline__ bool accept(uint32_t m1, uint32_t m2, int maxDist, int minDiff)
 {
     if (m1 == INF) return false;
-    int d0 = (int)(m1 >> 16);
+    const int d0 = (int)(m1 >> 16);
     if (d0 > maxDist) return false;
     if (m2 != INF) {
-        int d1 = (int)(m2 >> 16);
+        const int d1 = (int)(m2 >> 16);
         if (d1 <= maxDist && d1 - d0 < minDiff) return false;
     }
     return true;
 }
 
-__device__ __forceinline__ uint32_t hamming(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1)
+__device__ __forceinline__ uint32_t popc4(const uint4& a, const uint4& b)
 {
-    uint32_t d = __popc(a0.x ^ b0.x);
-    d += __popc(a0.y ^ b0.y);
-    d += __popc(a0.z ^ b0.z);
-    d += __popc(a0.w ^ b0.w);
-    d += __popc(a1.x ^ b1.x);
-    d += __popc(a1.y ^ b1.y);
-    d += __popc(a1.z ^ b1.z);
-    d += __popc(a1.w ^ b1.w);
-    return d;
+    return __popc(a.x ^ b.x) + __popc(a.y ^ b.y) + __popc(a.z ^ b.z) + __popc(a.w ^ b.w);
+}
+
+__device__ __forceinline__ void col_push(unsigned long long* cell, uint32_t key)
+{
+    unsigned long long old = *cell, assumed;
+    do {
+        assumed = old;
+        uint32_t m1 = (uint32_t)assumed, m2 = (uint32_t)(assumed >> 32);
+        push2(m1, m2, key);
+        const unsigned long long nw = (unsigned long long)m1 | ((unsigned long long)m2 << 32);
+        if (nw == assumed) return;
+        old = atomicCAS(cell, assumed, nw);
+    } while (old != assumed);
 }
 
 __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A,
@@ -81,16 +87,13 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
                                                    uint32_t* __restrict__ n_out,
                                                    uint32_t* __restrict__ status)
 {
-    __shared__ uint4 Bt[64][2];
-    __shared__ uint32_t T[MW][32][65];
-    __shared__ uint2 colpart[MW][64];
-    __shared__ uint2 colstate[NMAX];
-    __shared__ uint2 rowstate[NMAX];
+    __shared__ uint4 Blo[BT], Bhi[BT];
+    __shared__ unsigned long long colstate[NMAX];
     __shared__ uint32_t wsum[MW];
 
     const int pair = blockIdx.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    int na = (int)nA[pair], nb = (int)nB[pair];
+    const int na = (int)nA[pair], nb = (int)nB[pair];
     if (na > NMAX || nb > NMAX) {
         if (tid == 0) {
             atomicOr(status, 1u);
@@ -98,101 +101,125 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
         }
         return;
     }
+    const int maxDist = p.max_dist;
     const uint4* Ap = reinterpret_cast<const uint4*>(A + pair * p.a_pitch);
     const uint4* Bp = reinterpret_cast<const uint4*>(B + pair * p.b_pitch);
-    for (int j = tid; j < nb; j += MT) colstate[j] = make_uint2(INF, INF);
+    uint32_t* rows = p.row_scratch + (long long)pair * NMAX * 2;
+    for (int j = tid; j < nb; j += MT) colstate[j] = ~0ull;
 
-    for (int rb = 0; rb < na; rb += MT) {
-        const int i = rb + tid;
-        const bool valid = i < na;
-        uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
-        if (valid) {
-            a0 = Ap[2 * i];
-            a1 = Ap[2 * i + 1];
+    uint32_t m1[RPL], m2[RPL];
+    for (int rb = 0; rb < na; rb += ROWS) {
+        uint4 alo[RPL], ahi[RPL];
+        bool valid[RPL];
+#pragma unroll
+        for (int r = 0; r < RPL; r++) {
+            const int i = rb + r * MT + tid;
+            valid[r] = i < na;
+            alo[r] = valid[r] ? Ap[2 * i] : make_uint4(0, 0, 0, 0);
+            ahi[r] = valid[r] ? Ap[2 * i + 1] : make_uint4(0, 0, 0, 0);
+            m1[r] = INF;
+            m2[r] = INF;
         }
-        uint32_t rm1 = INF, rm2 = INF;
-        const int waveRow0 = rb + wave * kWave;
-        const int rowsValid = min(kWave, na - waveRow0);
-        for (int cb = 0; cb < nb; cb += 64) {
-            __syncthreads();  // previous tile fully consumed
-            if (tid < 128) {
-                int j = cb + (tid >> 1);
-                Bt[tid >> 1][tid & 1] = j < nb ? Bp[2 * j + (tid & 1)] : make_uint4(0, 0, 0, 0);
+        for (int cb = 0; cb < nb; cb += BT) {
+            const int ncol = min(BT, nb - cb);
+            __syncthreads();  // previous tile consumed (and colstate initialised)
+            for (int j = tid; j < ncol; j += MT) {
+                Blo[j] = Bp[2 * (cb + j)];
+                Bhi[j] = Bp[2 * (cb + j) + 1];
             }
             __syncthreads();
-            const int ncol = min(64, nb - cb);
-#pragma unroll 4
-            for (int c = 0; c < 64; c += 2) {
-                const uint32_t d0 = hamming(a0, a1, Bt[c][0], Bt[c][1]);
-                const uint32_t d1 = hamming(a0, a1, Bt[c + 1][0], Bt[c + 1][1]);
-                if (valid && c < ncol) push2(rm1, rm2, (d0 << 16) | (uint32_t)(cb + c));
-                if (valid && c + 1 < ncol) push2(rm1, rm2, (d1 << 16) | (uint32_t)(cb + c + 1));
-                T[wave][c >> 1][lane] = d0 | (d1 << 16);
-            }
-            __syncthreads();
-            // lane = column: reduce the wave's 64 rows of this column
-            uint32_t cm1 = INF, cm2 = INF;
-            if (rowsValid > 0) {
-                const int cp = lane >> 1, sh = (lane & 1) * 16;
-                for (int r = 0; r < rowsValid; r++) {
-                    uint32_t d = (T[wave][cp][r] >> sh) & 0xFFFFu;
-                    push2(cm1, cm2, (d << 16) | (uint32_t)(waveRow0 + r));
+            for (int c = 0; c < ncol; c++) {
+                const uint4 b0 = Blo[c];
+                uint32_t h[RPL];
+                bool close = false;
+#pragma unroll
+                for (int r = 0; r < RPL; r++) {
+                    h[r] = valid[r] ? popc4(alo[r], b0) : 1024u;
+                    close |= h[r] <= (uint32_t)maxDist;
+                }
+                if (__any(close)) {
+                    const uint4 b1 = Bhi[c];
+                    const int j = cb + c;
+#pragma unroll
+                    for (int r = 0; r < RPL; r++) {
+                        if (h[r] <= (uint32_t)maxDist) {
+                            const uint32_t d = h[r] + popc4(ahi[r], b1);
+                            if (d <= (uint32_t)maxDist) {
+                                push2(m1[r], m2[r], (d << 16) | (uint32_t)j);
+                                col_push(&colstate[j], (d << 16) | (uint32_t)(rb + r * MT + tid));
+                            }
+                        }
+                    }
                 }
             }
-            colpart[wave][lane] = make_uint2(cm1, cm2);
-            __syncthreads();
-            if (tid < 64 && cb + tid < nb) {
-                uint2 s = colstate[cb + tid];
+        }
+        if (na > ROWS) {  // more passes follow: park this pass's rows (read back by this thread)
 #pragma unroll
-                for (int w = 0; w < MW; w++) merge2(s.x, s.y, colpart[w][tid].x, colpart[w][tid].y);
-                colstate[cb + tid] = s;
+            for (int r = 0; r < RPL; r++) {
+                const int i = rb + r * MT + tid;
+                if (i < na) {
+                    rows[2 * i] = m1[r];
+                    rows[2 * i + 1] = m2[r];
+                }
             }
         }
-        if (valid) rowstate[i] = make_uint2(rm1, rm2);
     }
     __syncthreads();
 
     // cross-check + ordered compaction (ascending A index, FeatureMatcher.cpp:142-167)
     uint32_t base = 0;
     mage_dmatch* o = out + (long long)pair * p.out_cap;
-    for (int rb = 0; rb < na; rb += MT) {
-        const int i = rb + tid;
-        bool ok = false;
-        uint32_t j = 0, d = 0;
-        if (i < na) {
-            uint2 r = rowstate[i];
-            if (accept(r.x, r.y, p.max_dist, p.min_diff)) {
-                j = r.x & 0xFFFFu;
-                d = r.x >> 16;
-                uint2 c = colstate[j];
-                ok = accept(c.x, c.y, p.max_dist, p.min_diff) && (c.x & 0xFFFFu) == (uint32_t)i;
+    for (int rb = 0; rb < na; rb += ROWS) {
+#pragma unroll
+        for (int r = 0; r < RPL; r++) {
+            const int i = rb + r * MT + tid;
+            bool ok = false;
+            uint32_t j = 0, d = 0;
+            if (i < na) {
+                uint32_t r1 = m1[r], r2 = m2[r];
+                if (na > ROWS) {
+                    r1 = rows[2 * i];
+                    r2 = rows[2 * i + 1];
+                }
+                if (accept(r1, r2, maxDist, p.min_diff)) {
+                    j = r1 & 0xFFFFu;
+                    d = r1 >> 16;
+                    const unsigned long long c = colstate[j];
+                    ok = accept((uint32_t)c, (uint32_t)(c >> 32), maxDist, p.min_diff) &&
+                         ((uint32_t)c & 0xFFFFu) == (uint32_t)i;
+                }
             }
-        }
-        const unsigned long long m = __ballot(ok);
-        const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t woff = 0, total = 0;
-        for (int w = 0; w < MW; w++) {
-            if (w < wave) woff += wsum[w];
-            total += wsum[w];
-        }
-        if (ok) {
-            uint32_t pos = base + woff + before;
-            if (pos < p.out_cap) {
-                mage_dmatch mm;
-                mm.query_idx = i;
-                mm.train_idx = (int32_t)j;
-                mm.img_idx = 0;
-                mm.distance = (float)d;
-                o[pos] = mm;
+            const unsigned long long m = __ballot(ok);
+            const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t woff = 0, total = 0;
+            for (int w = 0; w < MW; w++) {
+                if (w < wave) woff += wsum[w];
+                total += wsum[w];
             }
+            if (ok) {
+                const uint32_t pos = base + woff + before;
+                if (pos < p.out_cap) {
+                    mage_dmatch mm;
+                    mm.query_idx = i;
+                    mm.train_idx = (int32_t)j;
+                    mm.img_idx = 0;
+                    mm.distance = (float)d;
+                    o[pos] = mm;
+                }
+            }
+            base += total;
+            __syncthreads();
         }
-        base += total;
-        __syncthreads();
     }
     if (tid == 0) n_out[pair] = base;
 }
+
+struct MatchScratch {
+    DeviceBuffer a, b, n, out, status, rows;
+};
+thread_local MatchScratch g_match;
 
 }  // namespace
 
@@ -201,12 +228,15 @@ mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA
                         int minDiff, mage_dmatch* dOut, uint32_t cap, uint32_t* dN,
                         uint32_t* dStatus, hipStream_t st)
 {
+    mage_status r = g_match.rows.reserve((size_t)pairs * NMAX * 2 * 4);
+    if (r != MAGE_OK) return r;
     MatchParams mp{};
     mp.max_dist = maxDist;
     mp.min_diff = minDiff;
     mp.out_cap = cap;
     mp.a_pitch = aPitch;
     mp.b_pitch = bPitch;
+    mp.row_scratch = g_match.rows.as<uint32_t>();
     {
         KernelTimer _kt("match.two_way", st);
         hipLaunchKernelGGL(match_kernel, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
@@ -214,13 +244,6 @@ mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;
 }
-
-namespace {
-struct MatchScratch {
-    DeviceBuffer a, b, n, out, status;
-};
-thread_local MatchScratch g_match;
-}  // namespace
 
 }  // namespace mage
 

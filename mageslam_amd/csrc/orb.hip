@@ -29,9 +29,9 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // 1. FAST-9/16 + NMS
 // ------------------------------------------------------------------------------------------
-constexpr int TW = 64, TH = 16, HALO = 4;
-constexpr int LW = TW + 2 * HALO;  // 72
-constexpr int LH = TH + 2 * HALO;  // 24
+constexpr int TW = 64, TH = 32, HALO = 4;
+constexpr int LW = TW + 2 * HALO;  // 72 bytes: 18 dwords per LDS row
+constexpr int LH = TH + 2 * HALO;  // 40
 constexpr int SW = TW + 2, SH = TH + 2;
 constexpr int FAST_THREADS = 256;
 
@@ -41,6 +41,7 @@ struct FastParams {
     int threshold;
     int xlo, xhi, ylo, yhi;  // emission window (FAST range ∩ RunByImageBorder)
     unsigned cand_cap;
+    int dword_ok;  // frames 4-byte aligned with width, stride and pitch multiples of 4
 };
 
 // Ring of FAST_t<16> (makeOffsets, OpenCVModified.cpp:890-921) as (dx, dy).
@@ -48,59 +49,54 @@ __device__ __constant__ signed char c_ring[16][2] = {
     {0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
     {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
 
-// True if the cyclic 16-bit mask has >= 9 consecutive set bits (count > K=8, :1429-1478).
-__device__ __forceinline__ bool has_run9(unsigned m16)
-{
-    unsigned m = m16 | (m16 << 16);
-    unsigned a = m & (m >> 1);
-    a &= a >> 2;
-    a &= a >> 4;
-    a &= m >> 8;
-    return (a & 0xFFFFu) != 0u;
-}
-
-// FAST score of the pixel at p (LDS, row stride LW): cornerScore<16> if it passes the segment
-// test, else 0.  cornerScore = max over the 16 cyclic 9-arcs of min(v - x) and of min(x - v),
-// minus one (OpenCVModified.cpp:927-1071: the scalar and SSE2 branches agree on corners).
+// FAST-9/16 score of the pixel at p (LDS, row stride LW), branch-free.
+// With d_k = v - x_k over the 16-pixel ring, let A = max over the 16 cyclic 9-arcs of
+// min(d) and B = max over the arcs of min(-d).  "Some 9 contiguous ring pixels are all darker
+// than v - t" (the segment test of FAST_t<16>, OpenCVModified.cpp:1415-1479) is exactly A > t,
+// "all brighter than v + t" is B > t, and cornerScore<16> (:927-1071; its scalar and SSE2
+// branches agree on corners) is max(A, B) - 1.  So one min3/max3 ladder gives both: 9-arc
+// minima as min3 of three 3-arc minima.  Returns 0 for non-corners.
 __device__ __forceinline__ int fast_score(const uint8_t* p, int t)
 {
     const int v = p[0];
     int d[16];
-    unsigned bright = 0, dark = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - (int)p[c_ring[k][1] * LW + c_ring[k][0]];
+    int m3[16], x3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        int x = p[c_ring[k][1] * LW + c_ring[k][0]];
-        d[k] = v - x;
-        dark |= (unsigned)(x < v - t) << k;
-        bright |= (unsigned)(x > v + t) << k;
-    }
-    if (!has_run9(dark) && !has_run9(bright)) return 0;
-    int m2[16], m4[16], x2[16], x4[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        m2[k] = min(d[k], d[(k + 1) & 15]);
-        x2[k] = max(d[k], d[(k + 1) & 15]);
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        m4[k] = min(m2[k], m2[(k + 2) & 15]);
-        x4[k] = max(x2[k], x2[(k + 2) & 15]);
+        m3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+        x3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
     }
     int a = -1000, b = 1000;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        int m8 = min(m4[k], m4[(k + 4) & 15]);
-        int x8 = max(x4[k], x4[(k + 4) & 15]);
-        a = max(a, min(m8, d[(k + 8) & 15]));
-        b = min(b, max(x8, d[(k + 8) & 15]));
+        a = max(a, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
+        b = min(b, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15]));
     }
-    return max(a, -b) - 1;
+    const int raw = max(a, -b);
+    return raw > t ? raw - 1 : 0;
 }
 
+// Stage the (TW + 8) x (TH + 8) window into LDS; zeros outside the image.  When the row pitch
+// and the width are multiples of 4 every dword is wholly inside or outside the frame (the
+// window origin is 4-aligned), so it is moved with 4-byte loads.
 __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const FastParams& p,
                                           uint8_t (*img)[LW])
 {
     const int gx0 = blockIdx.x * TW - HALO, gy0 = blockIdx.y * TH - HALO;
+    if (p.dword_ok) {
+        constexpr int DW = LW / 4;
+        for (int i = threadIdx.x; i < LH * DW; i += FAST_THREADS) {
+            const int r = i / DW, c = i - r * DW;
+            const int gx = gx0 + 4 * c, gy = gy0 + r;
+            uint32_t v = 0;
+            if (gx >= 0 && gx < p.w && gy >= 0 && gy < p.h)
+                v = *reinterpret_cast<const uint32_t*>(src + (long long)gy * p.stride + gx);
+            *reinterpret_cast<uint32_t*>(&img[r][4 * c]) = v;
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < LH * LW; i += FAST_THREADS) {
         int r = i / LW, c = i - r * LW;
         int gx = gx0 + c, gy = gy0 + r;
@@ -115,9 +111,9 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* _
                                                                 uint32_t* __restrict__ cand,
                                                                 uint32_t* __restrict__ counts)
 {
-    __shared__ uint8_t img[LH][LW];
+    __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
     __shared__ uint8_t sc[SH][SW + 2];
-    __shared__ uint32_t list[TW * TH / 2];
+    __shared__ uint32_t list[(TW / 2) * (TH / 2)];  // strict 3x3 maxima are never 8-adjacent
     __shared__ uint32_t s_cnt, s_base;
     const int f = blockIdx.z;
     load_tile(frames + (long long)f * p.pitch, p, img);
@@ -159,7 +155,7 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_score_map_kernel(const uint
                                                                       FastParams p,
                                                                       uint8_t* __restrict__ score)
 {
-    __shared__ uint8_t img[LH][LW];
+    __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
     load_tile(src, p, img);
     __syncthreads();
     for (int i = threadIdx.x; i < TW * TH; i += FAST_THREADS) {
@@ -467,8 +463,6 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
 constexpr int DESC_WAVES = 4;
 constexpr int RMAX = 18;  // max |pattern offset| over both tables and all rotations
 constexpr int KHMAX = 7;  // max Gaussian half-size (ksize <= 15)
-constexpr int RAWD = 2 * (RMAX + KHMAX) + 1;
-constexpr int BD_MAX = 2 * RMAX + 1;
 
 struct DescParams {
     int w, h, stride;
@@ -477,6 +471,7 @@ struct DescParams {
     int R;      // sampling radius of the pattern rotations in use
     int ksize;  // Gaussian taps (<= 1: no blur)
     int taps[2 * KHMAX + 1];
+    int dword_ok;
 };
 
 __device__ __forceinline__ int reflect101(int i, int n)
@@ -486,70 +481,93 @@ __device__ __forceinline__ int reflect101(int i, int n)
     return i;
 }
 
+// Orders one wave's LDS writes before its other lanes' reads (waves of a workgroup work on
+// different keypoints, so no workgroup barrier is needed).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per keypoint.  RB bounds the pattern radius (7: patch 15, 13: patch 31, rotation 0;
+// 18: any rotation) and sizes the per-wave LDS, so the default configuration keeps 8 waves per
+// SIMD resident.  Interior windows are fetched with aligned dword loads (row segments kept at
+// their byte phase `s`); windows touching the border use reflect-101 byte loads.
+template <int RB>
 __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
     const uint8_t* __restrict__ frames, DescParams p, const uint32_t* __restrict__ xy_in,
     const uint32_t* __restrict__ n_in, const int8_t* __restrict__ pattern,
     uint8_t* __restrict__ desc_out)
 {
-    __shared__ uint8_t raw[DESC_WAVES][RAWD * RAWD];
-    __shared__ int rowp[DESC_WAVES][RAWD * BD_MAX];
-    __shared__ uint8_t blur[DESC_WAVES][BD_MAX * BD_MAX];
+    constexpr int RAWMAX = 2 * (RB + KHMAX) + 1;    // raw window side
+    constexpr int RAWP = ((RAWMAX + 3 + 3) / 4) * 4;  // row pitch: covers any byte phase
+    constexpr int BDMAX = 2 * RB + 1;
+    __shared__ __attribute__((aligned(16))) uint8_t raw[DESC_WAVES][RAWMAX * RAWP];
+    __shared__ int rowp[DESC_WAVES][RAWMAX * BDMAX];
+    __shared__ uint8_t blur[DESC_WAVES][BDMAX * BDMAX];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int k = blockIdx.x * DESC_WAVES + wave;
-    const bool live = k < (int)n_in[f];
+    if (k >= (int)n_in[f]) return;
     const int kh = p.ksize > 1 ? p.ksize / 2 : 0;
     const int R = p.R, Rr = R + kh, rawDim = 2 * Rr + 1, bd = 2 * R + 1;
-    int cx = 0, cy = 0;
-    if (live) {
-        uint32_t v = xy_in[(long long)f * p.out_cap + k];
-        cx = (int)(v & 0xFFFFu);
-        cy = (int)(v >> 16);
-        const uint8_t* src = frames + (long long)f * p.pitch;
+    const uint32_t v = xy_in[(long long)f * p.out_cap + k];
+    const int cx = (int)(v & 0xFFFFu), cy = (int)(v >> 16);
+    const uint8_t* src = frames + (long long)f * p.pitch;
+    uint8_t* rw = raw[wave];
+    const int x0 = cx - Rr, y0 = cy - Rr;
+    const int xa = x0 & ~3, s = x0 - xa;
+    const int nd = (s + rawDim + 3) >> 2;  // dwords per row
+    if (p.dword_ok && x0 >= 0 && y0 >= 0 && y0 + rawDim <= p.h && xa + 4 * nd <= p.w) {
+        for (int i = lane; i < rawDim * nd; i += kWave) {
+            const int r = i / nd, c = i - r * nd;
+            *reinterpret_cast<uint32_t*>(rw + r * RAWP + 4 * c) =
+                *reinterpret_cast<const uint32_t*>(src + (long long)(y0 + r) * p.stride + xa + 4 * c);
+        }
+    } else {
         for (int i = lane; i < rawDim * rawDim; i += kWave) {
-            int r = i / rawDim, c = i - r * rawDim;
-            int gy = reflect101(cy - Rr + r, p.h), gx = reflect101(cx - Rr + c, p.w);
-            raw[wave][i] = src[(long long)gy * p.stride + gx];
+            const int r = i / rawDim, c = i - r * rawDim;
+            const int gy = reflect101(y0 + r, p.h), gx = reflect101(x0 + c, p.w);
+            rw[r * RAWP + s + c] = src[(long long)gy * p.stride + gx];
         }
     }
-    __syncthreads();
-    if (live && kh > 0) {
+    wave_lds_sync();
+    const uint8_t* rb = rw + s;  // raw(r, c) = rb[r * RAWP + c]
+    if (kh > 0) {
         for (int i = lane; i < rawDim * bd; i += kWave) {
-            int r = i / bd, c = i - r * bd;
-            const uint8_t* q = &raw[wave][r * rawDim + c];
-            int s = 0;
-            for (int t = 0; t < p.ksize; t++) s += p.taps[t] * q[t];
-            rowp[wave][i] = s;
+            const int r = i / bd, c = i - r * bd;
+            const uint8_t* q = rb + r * RAWP + c;
+            int acc = 0;
+            for (int t = 0; t < p.ksize; t++) acc += p.taps[t] * q[t];
+            rowp[wave][i] = acc;
         }
+        wave_lds_sync();
     }
-    __syncthreads();
-    if (live) {
-        for (int i = lane; i < bd * bd; i += kWave) {
-            int r = i / bd, c = i - r * bd;
-            int v;
-            if (kh > 0) {
-                int s = 0;
-                for (int t = 0; t < p.ksize; t++) s += p.taps[t] * rowp[wave][(r + t) * bd + c];
-                v = (s + (1 << 15)) >> 16;
-                v = v < 0 ? 0 : (v > 255 ? 255 : v);
-            } else {
-                v = raw[wave][r * rawDim + c];
-            }
-            blur[wave][i] = (uint8_t)v;
+    for (int i = lane; i < bd * bd; i += kWave) {
+        const int r = i / bd, c = i - r * bd;
+        int o;
+        if (kh > 0) {
+            int acc = 0;
+            for (int t = 0; t < p.ksize; t++) acc += p.taps[t] * rowp[wave][(r + t) * bd + c];
+            o = (acc + (1 << 15)) >> 16;
+            o = o < 0 ? 0 : (o > 255 ? 255 : o);
+        } else {
+            o = rb[r * RAWP + c];
         }
+        blur[wave][i] = (uint8_t)o;
     }
-    __syncthreads();
-    if (!live) return;
+    wave_lds_sync();
     // rotation 0: angle = 0 without orientation (OpenCVModified.cpp:748-754, :522)
     const char4* pat = reinterpret_cast<const char4*>(pattern);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
 #pragma unroll
     for (int chunk = 0; chunk < 4; chunk++) {
-        char4 e = pat[chunk * kWave + lane];  // (x0, y0, x1, y1) of bit 64*chunk + lane
-        int t0 = blur[wave][(R + e.y) * bd + R + e.x];
-        int t1 = blur[wave][(R + e.w) * bd + R + e.z];
-        unsigned long long m = __ballot(t0 < t1);
+        const char4 e = pat[chunk * kWave + lane];  // (x0, y0, x1, y1) of bit 64*chunk + lane
+        const int t0 = blur[wave][(R + e.y) * bd + R + e.x];
+        const int t1 = blur[wave][(R + e.w) * bd + R + e.z];
+        const unsigned long long m = __ballot(t0 < t1);
         if (lane == 0) dst[chunk] = m;
     }
 }
@@ -647,6 +665,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
     fp.yhi = std::min(h - 4, h - border - 1);
     if (h <= 2 * border || w <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
     fp.cand_cap = candCap;
+    fp.dword_ok = (w % 4 == 0) && (stride % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)d_frames % 4 == 0);
     dim3 g1((w + TW - 1) / TW, (h + TH - 1) / TH, batch);
     {
         KernelTimer _kt("orb.fast_nms", st);
@@ -688,10 +707,12 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         dp.R = o->R;
         dp.ksize = (int)s.gaussian_kernel_size;
         for (int i = 0; i < 2 * KHMAX + 1; i++) dp.taps[i] = o->taps[i];
+        dp.dword_ok = (stride % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)d_frames % 4 == 0);
         dim3 g3((cap + DESC_WAVES - 1) / DESC_WAVES, batch);
         {
             KernelTimer _kt("orb.describe", st);
-            hipLaunchKernelGGL(describe_kernel, g3, dim3(DESC_WAVES * kWave), 0, st, d_frames, dp,
+            auto kern = dp.R <= 7 ? describe_kernel<7> : (dp.R <= 13 ? describe_kernel<13> : describe_kernel<RMAX>);
+            hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, d_frames, dp,
                                o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
         }
         MAGE_HIP(hipGetLastError());
@@ -850,6 +871,7 @@ mage_status mage_orb_fast_score_map(const uint8_t* img, int32_t width, int32_t h
     fp.h = height;
     fp.stride = stride;
     fp.threshold = std::min(std::max((int)threshold, 0), 255);
+    fp.dword_ok = (width % 4 == 0) && (stride % 4 == 0);
     hipError_t e = hipMemcpy(dimg.ptr, img, (size_t)stride * height, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
         dim3 g((width + mage::TW - 1) / mage::TW, (height + mage::TH - 1) / mage::TH);
