@@ -2,24 +2,28 @@
 // GetDescriptorDistance (Core/MAGESLAM/Source/Tracking/FeatureMatcher.cpp:61-190, 453-504); the
 // reference builds two N x N float distance matrices with cv::BFMatcher::radiusMatch twice.
 //
-// One workgroup (8 waves) per (A, B) frame pair, nothing materialised in HBM.
-//   * Each lane owns RPL = 4 A rows (32 B each, in VGPRs); B is staged in LDS in 1024-row
-//     tiles, split into first and second 16-byte halves.
-//   * Only pairs with d <= maxDist can change "best and second best within the radius"
-//     (radiusMatch keeps d <= maxDist; FeatureMatcher.cpp:117-156), so the reductions are a rare
-//     branch instead of per-pair work.  The first-half popcount (4 x v_xor + v_bcnt) is a lower
-//     bound of d: if it exceeds maxDist for every lane and row of the wave (one ballot), the
-//     second half is never read.  For random 256-bit descriptors and maxDist = 30 the branch is
-//     taken only around true matches.
-//   * Row best / second live in registers as packed keys (d << 16 | j); column best / second
-//     live in LDS and are updated by 64-bit compare-and-swap (order-independent: the two
-//     smallest keys of a set).  The cross-check (best(a) = b and best(b) = a,
-//     FeatureMatcher.cpp:158) and the ordered DMatch compaction run in the same launch.
-// Ties at the best distance are rejected by the delta test for minDifference >= 1 and
-// otherwise resolve to the lowest index (canonical).
+// The distance matrix is a GEMM: with s(x) = 1 - 2x per bit, sum_k s(a_k) s(b_k) = 256 - 2 d(a, b).
+// Descriptors are expanded to +-1 int8 and multiplied with v_mfma_i32_32x32x32_i8 (8 MFMAs per
+// 32 x 32 block of pairs, K = 256); the VALU only turns each result into packed keys and keeps
+// the two best per row and per column.  One workgroup (8 waves) per (A, B) frame pair, nothing
+// materialised in HBM:
+//   * each wave owns RT = 2 row tiles (64 A rows) per pass; their +-1 operands stay in VGPRs;
+//   * B is expanded in 64-column stages into LDS (double buffered, one barrier per stage) in the
+//     exact per-lane operand order, so every wave reads it with conflict-free ds_read_b128;
+//   * keys are (D << 15 | 0x7FFF - index) with D = 256 - 2d, so "larger key" = smaller distance,
+//     then lower index (the canonical tie order); the two largest keys over ALL
+//     columns give radiusMatch's best and second best whenever they lie within the radius
+//     (FeatureMatcher.cpp:117-137), so no per-pair radius mask is needed;
+//   * row (best, second) live per lane and register and are reduce-scattered across the 32
+//     lanes of a half-wave once per pass; column (best, second) are reduced over the lane's 16
+//     rows and its partner half, then merged across waves with two LDS atomicMax (no CAS loop:
+//     every key that loses or is displaced in the best slot is pushed into the second slot).
+// The cross-check (best(a) = b and best(b) = a, FeatureMatcher.cpp:158) and the ordered DMatch
+// compaction run in the same launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <vector>
 
 #include "common.hpp"
@@ -27,56 +31,121 @@
 namespace mage {
 namespace {
 
-constexpr int MW = 8;              // waves per workgroup
-constexpr int MT = MW * kWave;     // threads per workgroup
-constexpr int RPL = 4;             // A rows per lane
-constexpr int ROWS = MT * RPL;     // A rows per pass
-constexpr int BT = 1024;           // B rows per LDS tile
-constexpr int NMAX = 4096;         // max descriptors per side (column state in LDS)
-constexpr uint32_t INF = 0xFFFFFFFFu;
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int MW = 8;               // waves per workgroup
+constexpr int MT = MW * kWave;      // threads per workgroup
+constexpr int RT = 2;               // 32-row tiles per wave per pass
+constexpr int ROWS = MW * RT * 32;  // A rows per pass
+constexpr int SC = 64;              // B columns per LDS stage (two 32-column tiles)
+constexpr int NMAX = 4096;          // max descriptors per side (states in LDS)
+constexpr int NONE = INT_MIN;       // empty key
+static_assert(SC * 8 == MT, "one stage-fill item per thread");
 
 struct MatchParams {
     int max_dist, min_diff;
     unsigned out_cap;
     long long a_pitch, b_pitch;  // bytes between pairs
-    uint32_t* row_scratch;       // per pair NMAX x 2 u32 (row states between passes)
 };
 
-__device__ __forceinline__ void push2(uint32_t& m1, uint32_t& m2, uint32_t key)
+__device__ __forceinline__ int med3(int a, int b, int c)
 {
-    m2 = min(m2, max(m1, key));
-    m1 = min(m1, key);
+    int r;
+    asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
 
-// Row/column acceptance of FeatureMatcher.cpp:125-137 on (best, second) keys.
-__device__ __forceinline__ bool accept(uint32_t m1, uint32_t m2, int maxDist, int minDiff)
+// (m1, m2) = the two largest keys seen; m1 >= m2 always.
+__device__ __forceinline__ void push2(int& m1, int& m2, int k)
 {
-    if (m1 == INF) return false;
-    const int d0 = (int)(m1 >> 16);
+    m2 = med3(m1, m2, k);
+    m1 = max(m1, k);
+}
+
+__device__ __forceinline__ void merge2(int& m1, int& m2, int o1, int o2)
+{
+    const int lo = min(m1, o1);
+    m1 = max(m1, o1);
+    m2 = max(max(lo, m2), o2);
+}
+
+__device__ __forceinline__ int key_dist(int k) { return (256 - (k >> 15)) >> 1; }
+__device__ __forceinline__ int key_index(int k) { return 0x7FFF - (k & 0x7FFF); }
+
+// Row/column acceptance of FeatureMatcher.cpp:125-137 on (best, second) keys.
+__device__ __forceinline__ bool accept(int m1, int m2, int maxDist, int minDiff)
+{
+    if (m1 == NONE) return false;
+    const int d0 = key_dist(m1);
     if (d0 > maxDist) return false;
-    if (m2 != INF) {
-        const int d1 = (int)(m2 >> 16);
+    if (m2 != NONE) {
+        const int d1 = key_dist(m2);
         if (d1 <= maxDist && d1 - d0 < minDiff) return false;
     }
     return true;
 }
 
-__device__ __forceinline__ uint32_t popc4(const uint4& a, const uint4& b)
+// 16 descriptor bits -> 16 bytes of s(bit) = +1 (0x01) / -1 (0xFF); byte b <-> bit b.
+__device__ __forceinline__ v4i expand16(uint32_t w)
 {
-    return __popc(a.x ^ b.x) + __popc(a.y ^ b.y) + __popc(a.z ^ b.z) + __popc(a.w ^ b.w);
+    v4i r;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t t = (w >> (4 * q)) & 0xFu;
+        const uint32_t x = (t * 0x00204081u) & 0x01010101u;  // bit i -> byte i
+        r[q] = (int)__builtin_amdgcn_perm(0u, 0x0000FF01u, x);
+    }
+    return r;
 }
 
-__device__ __forceinline__ void col_push(unsigned long long* cell, uint32_t key)
+// Row offset (within a 32-row tile, lane half 0) of accumulator register g of a 32x32 MFMA.
+__host__ __device__ constexpr int acc_row(int g) { return (g & 3) + 8 * (g >> 2); }
+
+// One 32-column B tile against the wave's RT row tiles.  MASK: some rows or columns are padding.
+template <bool MASK>
+__device__ __forceinline__ void tile_pass(const v4i (&a)[RT][8], const v4i* __restrict__ bt, int lane,
+                                          int colbase, int nb, int rowbase, int na, int (&r1)[RT][16],
+                                          int (&r2)[RT][16], int* colM1, int* colM2)
 {
-    unsigned long long old = *cell, assumed;
-    do {
-        assumed = old;
-        uint32_t m1 = (uint32_t)assumed, m2 = (uint32_t)(assumed >> 32);
-        push2(m1, m2, key);
-        const unsigned long long nw = (unsigned long long)m1 | ((unsigned long long)m2 << 32);
-        if (nw == assumed) return;
-        old = atomicCAS(cell, assumed, nw);
-    } while (old != assumed);
+    v16i acc[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) acc[rt] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const v4i b = bt[s * kWave + lane];
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++) acc[rt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[rt][s], b, acc[rt], 0, 0, 0);
+    }
+    const int h = lane >> 5;
+    const int j = colbase + (lane & 31);
+    const bool jvalid = j < nb;
+    const int jc = 0x7FFF - j;
+    int c1 = NONE, c2 = NONE;
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) {
+#pragma unroll
+        for (int g = 0; g < 16; g++) {
+            const int D = acc[rt][g];  // 256 - 2d
+            int kr = (D << 15) | jc;
+            int kc = (D << 6) | (63 - (rt * 32 + acc_row(g)));  // local row key, 6-bit row
+            if (MASK) {
+                if (!jvalid) kr = NONE;
+                if (rowbase + rt * 32 + acc_row(g) + 4 * h >= na) kc = NONE;
+            }
+            push2(r1[rt][g], r2[rt][g], kr);
+            push2(c1, c2, kc);
+        }
+    }
+    // local column keys -> global (D << 15 | 0x7FFF - i), then merge with the partner half
+    const int ib = rowbase + 4 * h;
+    if (c1 != NONE) c1 = ((c1 >> 6) << 15) | (0x7FFF - (ib + 63 - (c1 & 63)));
+    if (c2 != NONE) c2 = ((c2 >> 6) << 15) | (0x7FFF - (ib + 63 - (c2 & 63)));
+    merge2(c1, c2, __shfl_xor(c1, 32), __shfl_xor(c2, 32));
+    if (h == 0 && jvalid && c1 != NONE) {
+        const int old = atomicMax(&colM1[j], c1);
+        atomicMax(&colM2[j], old > c1 ? c1 : max(old, c2));
+    }
 }
 
 __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A,
@@ -87,8 +156,9 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
                                                    uint32_t* __restrict__ n_out,
                                                    uint32_t* __restrict__ status)
 {
-    __shared__ uint4 Blo[BT], Bhi[BT];
-    __shared__ unsigned long long colstate[NMAX];
+    __shared__ v4i stage[2][SC / 32][8][kWave];  // [buffer][tile][k-step][lane] operands
+    __shared__ int colM1[NMAX], colM2[NMAX];
+    __shared__ int rowM1[NMAX], rowM2[NMAX];
     __shared__ uint32_t wsum[MW];
 
     const int pair = blockIdx.x;
@@ -102,65 +172,96 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
         return;
     }
     const int maxDist = p.max_dist;
-    const uint4* Ap = reinterpret_cast<const uint4*>(A + pair * p.a_pitch);
-    const uint4* Bp = reinterpret_cast<const uint4*>(B + pair * p.b_pitch);
-    uint32_t* rows = p.row_scratch + (long long)pair * NMAX * 2;
-    for (int j = tid; j < nb; j += MT) colstate[j] = ~0ull;
+    const uint32_t* Aw = reinterpret_cast<const uint32_t*>(A + pair * p.a_pitch);
+    const uint32_t* Bw = reinterpret_cast<const uint32_t*>(B + pair * p.b_pitch);
+    for (int j = tid; j < nb; j += MT) {
+        colM1[j] = NONE;
+        colM2[j] = NONE;
+    }
+    const int nstages = (nb + SC - 1) / SC;
+    // stage-fill item of this thread: k-step s, column c of the stage
+    const int fs = tid >> 6, fc = tid & 63;
+    auto fetch = [&](int st) -> uint32_t {
+        const int j = st * SC + fc;
+        return j < nb ? Bw[8 * j + fs] : 0u;
+    };
+    auto fill = [&](int buf, uint32_t dw) {
+        stage[buf][fc >> 5][fs][fc & 31] = expand16(dw & 0xFFFFu);
+        stage[buf][fc >> 5][fs][32 + (fc & 31)] = expand16(dw >> 16);
+    };
 
-    uint32_t m1[RPL], m2[RPL];
-    for (int rb = 0; rb < na; rb += ROWS) {
-        uint4 alo[RPL], ahi[RPL];
-        bool valid[RPL];
+    for (int pb = 0; pb < na; pb += ROWS) {
+        const int rowbase = pb + wave * (RT * 32);
+        const bool active = rowbase < na;
+        v4i a[RT][8];
+        int r1[RT][16], r2[RT][16];
 #pragma unroll
-        for (int r = 0; r < RPL; r++) {
-            const int i = rb + r * MT + tid;
-            valid[r] = i < na;
-            alo[r] = valid[r] ? Ap[2 * i] : make_uint4(0, 0, 0, 0);
-            ahi[r] = valid[r] ? Ap[2 * i + 1] : make_uint4(0, 0, 0, 0);
-            m1[r] = INF;
-            m2[r] = INF;
-        }
-        for (int cb = 0; cb < nb; cb += BT) {
-            const int ncol = min(BT, nb - cb);
-            __syncthreads();  // previous tile consumed (and colstate initialised)
-            for (int j = tid; j < ncol; j += MT) {
-                Blo[j] = Bp[2 * (cb + j)];
-                Bhi[j] = Bp[2 * (cb + j) + 1];
+        for (int rt = 0; rt < RT; rt++) {
+            const int i = rowbase + rt * 32 + (lane & 31);
+            uint32_t dw[8];
+#pragma unroll
+            for (int s = 0; s < 8; s++) dw[s] = i < na ? Aw[8 * i + s] : 0u;
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                a[rt][s] = expand16((lane >> 5) ? (dw[s] >> 16) : (dw[s] & 0xFFFFu));
+                if (i >= na) a[rt][s] = v4i{0, 0, 0, 0};
             }
+#pragma unroll
+            for (int g = 0; g < 16; g++) {
+                r1[rt][g] = NONE;
+                r2[rt][g] = NONE;
+            }
+        }
+        __syncthreads();  // column states initialised / previous pass done with the stages
+        fill(0, fetch(0));
+        __syncthreads();
+        for (int st = 0; st < nstages; st++) {
+            const int buf = st & 1;
+            uint32_t nxt = 0;
+            if (st + 1 < nstages) nxt = fetch(st + 1);
+            if (active) {
+#pragma unroll
+                for (int ct = 0; ct < SC / 32; ct++) {
+                    const int colbase = st * SC + ct * 32;
+                    if (colbase >= nb) break;
+                    const v4i* bt = &stage[buf][ct][0][0];
+                    if (colbase + 32 > nb || rowbase + RT * 32 > na)
+                        tile_pass<true>(a, bt, lane, colbase, nb, rowbase, na, r1, r2, colM1, colM2);
+                    else
+                        tile_pass<false>(a, bt, lane, colbase, nb, rowbase, na, r1, r2, colM1, colM2);
+                }
+            }
+            if (st + 1 < nstages) fill(buf ^ 1, nxt);
             __syncthreads();
-            for (int c = 0; c < ncol; c++) {
-                const uint4 b0 = Blo[c];
-                uint32_t h[RPL];
-                bool close = false;
+        }
+        if (active) {
+            // reduce-scatter the row states over the 32 lanes of each half: lane c ends with
+            // state q = c, i.e. row tile c >> 4, register c & 15.
+            int s1[RT * 16], s2[RT * 16];
 #pragma unroll
-                for (int r = 0; r < RPL; r++) {
-                    h[r] = valid[r] ? popc4(alo[r], b0) : 1024u;
-                    close |= h[r] <= (uint32_t)maxDist;
-                }
-                if (__any(close)) {
-                    const uint4 b1 = Bhi[c];
-                    const int j = cb + c;
+            for (int q = 0; q < RT * 16; q++) {
+                s1[q] = r1[q >> 4][q & 15];
+                s2[q] = r2[q >> 4][q & 15];
+            }
 #pragma unroll
-                    for (int r = 0; r < RPL; r++) {
-                        if (h[r] <= (uint32_t)maxDist) {
-                            const uint32_t d = h[r] + popc4(ahi[r], b1);
-                            if (d <= (uint32_t)maxDist) {
-                                push2(m1[r], m2[r], (d << 16) | (uint32_t)j);
-                                col_push(&colstate[j], (d << 16) | (uint32_t)(rb + r * MT + tid));
-                            }
-                        }
-                    }
+            for (int m = 16, n = 32; m >= 1; m >>= 1, n >>= 1) {
+                const bool up = (lane & m) != 0;
+                const int hf = n / 2;
+#pragma unroll
+                for (int k = 0; k < hf; k++) {
+                    const int send1 = up ? s1[k] : s1[k + hf], send2 = up ? s2[k] : s2[k + hf];
+                    const int keep1 = up ? s1[k + hf] : s1[k], keep2 = up ? s2[k + hf] : s2[k];
+                    int m1 = keep1, m2 = keep2;
+                    merge2(m1, m2, __shfl_xor(send1, m), __shfl_xor(send2, m));
+                    s1[k] = m1;
+                    s2[k] = m2;
                 }
             }
-        }
-        if (na > ROWS) {  // more passes follow: park this pass's rows (read back by this thread)
-#pragma unroll
-            for (int r = 0; r < RPL; r++) {
-                const int i = rb + r * MT + tid;
-                if (i < na) {
-                    rows[2 * i] = m1[r];
-                    rows[2 * i + 1] = m2[r];
-                }
+            const int c = lane & 31;
+            const int i = rowbase + (c >> 4) * 32 + acc_row(c & 15) + 4 * (lane >> 5);
+            if (i < na) {
+                rowM1[i] = s1[0];
+                rowM2[i] = s2[0];
             }
         }
     }
@@ -169,55 +270,43 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
     // cross-check + ordered compaction (ascending A index, FeatureMatcher.cpp:142-167)
     uint32_t base = 0;
     mage_dmatch* o = out + (long long)pair * p.out_cap;
-    for (int rb = 0; rb < na; rb += ROWS) {
-#pragma unroll
-        for (int r = 0; r < RPL; r++) {
-            const int i = rb + r * MT + tid;
-            bool ok = false;
-            uint32_t j = 0, d = 0;
-            if (i < na) {
-                uint32_t r1 = m1[r], r2 = m2[r];
-                if (na > ROWS) {
-                    r1 = rows[2 * i];
-                    r2 = rows[2 * i + 1];
-                }
-                if (accept(r1, r2, maxDist, p.min_diff)) {
-                    j = r1 & 0xFFFFu;
-                    d = r1 >> 16;
-                    const unsigned long long c = colstate[j];
-                    ok = accept((uint32_t)c, (uint32_t)(c >> 32), maxDist, p.min_diff) &&
-                         ((uint32_t)c & 0xFFFFu) == (uint32_t)i;
-                }
-            }
-            const unsigned long long m = __ballot(ok);
-            const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
-            __syncthreads();
-            uint32_t woff = 0, total = 0;
-            for (int w = 0; w < MW; w++) {
-                if (w < wave) woff += wsum[w];
-                total += wsum[w];
-            }
-            if (ok) {
-                const uint32_t pos = base + woff + before;
-                if (pos < p.out_cap) {
-                    mage_dmatch mm;
-                    mm.query_idx = i;
-                    mm.train_idx = (int32_t)j;
-                    mm.img_idx = 0;
-                    mm.distance = (float)d;
-                    o[pos] = mm;
-                }
-            }
-            base += total;
-            __syncthreads();
+    for (int rb = 0; rb < na; rb += MT) {
+        const int i = rb + tid;
+        bool ok = false;
+        int j = 0, d = 0;
+        if (i < na && accept(rowM1[i], rowM2[i], maxDist, p.min_diff)) {
+            j = key_index(rowM1[i]);
+            d = key_dist(rowM1[i]);
+            ok = accept(colM1[j], colM2[j], maxDist, p.min_diff) && key_index(colM1[j]) == i;
         }
+        const unsigned long long m = __ballot(ok);
+        const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t woff = 0, total = 0;
+        for (int w = 0; w < MW; w++) {
+            if (w < wave) woff += wsum[w];
+            total += wsum[w];
+        }
+        if (ok) {
+            const uint32_t pos = base + woff + before;
+            if (pos < p.out_cap) {
+                mage_dmatch mm;
+                mm.query_idx = i;
+                mm.train_idx = j;
+                mm.img_idx = 0;
+                mm.distance = (float)d;
+                o[pos] = mm;
+            }
+        }
+        base += total;
+        __syncthreads();
     }
     if (tid == 0) n_out[pair] = base;
 }
 
 struct MatchScratch {
-    DeviceBuffer a, b, n, out, status, rows;
+    DeviceBuffer a, b, n, out, status;
 };
 thread_local MatchScratch g_match;
 
@@ -228,15 +317,12 @@ mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA
                         int minDiff, mage_dmatch* dOut, uint32_t cap, uint32_t* dN,
                         uint32_t* dStatus, hipStream_t st)
 {
-    mage_status r = g_match.rows.reserve((size_t)pairs * NMAX * 2 * 4);
-    if (r != MAGE_OK) return r;
     MatchParams mp{};
     mp.max_dist = maxDist;
     mp.min_diff = minDiff;
     mp.out_cap = cap;
     mp.a_pitch = aPitch;
     mp.b_pitch = bPitch;
-    mp.row_scratch = g_match.rows.as<uint32_t>();
     {
         KernelTimer _kt("match.two_way", st);
         hipLaunchKernelGGL(match_kernel, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
