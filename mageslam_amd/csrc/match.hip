@@ -7,7 +7,8 @@
 // 32 x 32 block of pairs, K = 256); the VALU only turns each result into packed keys and keeps
 // the two best per row and per column.  One workgroup (8 waves) per (A, B) frame pair, nothing
 // materialised in HBM:
-//   * each wave owns RT = 2 row tiles (64 A rows) per pass; their +-1 operands stay in VGPRs;
+//   * 8 waves; each owns two 32-row tiles per pass, their +-1 operands stay in VGPRs; the MFMAs
+//     of one row tile are in flight while the VALU folds the other (software pipeline);
 //   * B is expanded in 64-column stages into LDS (double buffered, one barrier per stage) in the
 //     exact per-lane operand order, so every wave reads it with conflict-free ds_read_b128;
 //   * keys are (D << 15 | 0x7FFF - index) with D = 256 - 2d, so "larger key" = smaller distance,
@@ -34,19 +35,24 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int MW = 8;               // waves per workgroup
-constexpr int MT = MW * kWave;      // threads per workgroup
-constexpr int RT = 2;               // 32-row tiles per wave per pass
+constexpr int MW = 8;          // waves per workgroup (2 per SIMD)
+constexpr int MT = MW * kWave; // threads per workgroup
+constexpr int RT = 2;          // 32-row tiles per wave per pass
 constexpr int ROWS = MW * RT * 32;  // A rows per pass
-constexpr int SC = 64;              // B columns per LDS stage (two 32-column tiles)
-constexpr int NMAX = 4096;          // max descriptors per side (states in LDS)
-constexpr int NONE = INT_MIN;       // empty key
+constexpr int SC = MT / 8;     // B columns per LDS stage (32-column tiles, one fill item per thread)
+constexpr int NMAX = 4096;     // max descriptors per side (states in LDS)
+constexpr int NBUF = 3;        // B stage buffers
+constexpr int NONE = INT_MIN;  // empty key
 static_assert(SC * 8 == MT, "one stage-fill item per thread");
+#ifndef MAGE_MATCH_ABLATE  // timing experiments only (tools/ablate_match.py); 0 in the product
+#define MAGE_MATCH_ABLATE 0
+#endif
 
 struct MatchParams {
     int max_dist, min_diff;
     unsigned out_cap;
     long long a_pitch, b_pitch;  // bytes between pairs
+    int2* rows;                  // per pair NMAX (best, second) row keys
 };
 
 __device__ __forceinline__ int med3(int a, int b, int c)
@@ -102,52 +108,207 @@ __device__ __forceinline__ v4i expand16(uint32_t w)
 // Row offset (within a 32-row tile, lane half 0) of accumulator register g of a 32x32 MFMA.
 __host__ __device__ constexpr int acc_row(int g) { return (g & 3) + 8 * (g >> 2); }
 
-// One 32-column B tile against the wave's RT row tiles.  MASK: some rows or columns are padding.
-template <bool MASK>
-__device__ __forceinline__ void tile_pass(const v4i (&a)[RT][8], const v4i* __restrict__ bt, int lane,
-                                          int colbase, int nb, int rowbase, int na, int (&r1)[RT][16],
-                                          int (&r2)[RT][16], int* colM1, int* colM2)
+// D = 256 - 2d for the wave's 32 rows x one 32-column B tile: 8 chained MFMAs over K = 256.
+__device__ __forceinline__ v16i tile_mfma(const v4i (&a)[8], const v4i (&b)[8])
 {
-    v16i acc[RT];
+    v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int rt = 0; rt < RT; rt++) acc[rt] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < 8; s++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], b[s], acc, 0, 0, 0);
+    return acc;
+}
+
+__device__ __forceinline__ void load_frags(v4i (&b)[8], const v4i* __restrict__ bt, int lane)
+{
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-        const v4i b = bt[s * kWave + lane];
-#pragma unroll
-        for (int rt = 0; rt < RT; rt++) acc[rt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[rt][s], b, acc[rt], 0, 0, 0);
-    }
+    for (int s = 0; s < 8; s++) b[s] = bt[s * kWave + lane];
+}
+
+// Fold the D block of row tile rt (of the wave's RT) x one 32-column B tile into the row top-2
+// and into the column partial (c1, c2), which holds local keys (D << 6 | 63 - wave row).
+// MASK: some rows or columns are padding.
+template <bool MASK>
+__device__ __forceinline__ void fold(const v16i& acc, int rt, int lane, int colbase, int nb, int rowbase, int na,
+                                     int (&r1)[16], int (&r2)[16], int& c1, int& c2)
+{
     const int h = lane >> 5;
     const int j = colbase + (lane & 31);
-    const bool jvalid = j < nb;
     const int jc = 0x7FFF - j;
-    int c1 = NONE, c2 = NONE;
 #pragma unroll
-    for (int rt = 0; rt < RT; rt++) {
-#pragma unroll
-        for (int g = 0; g < 16; g++) {
-            const int D = acc[rt][g];  // 256 - 2d
-            int kr = (D << 15) | jc;
-            int kc = (D << 6) | (63 - (rt * 32 + acc_row(g)));  // local row key, 6-bit row
-            if (MASK) {
-                if (!jvalid) kr = NONE;
-                if (rowbase + rt * 32 + acc_row(g) + 4 * h >= na) kc = NONE;
-            }
-            push2(r1[rt][g], r2[rt][g], kr);
-            push2(c1, c2, kc);
+    for (int g = 0; g < 16; g++) {
+        const int D = acc[g];
+        if (MAGE_MATCH_ABLATE == 4) {
+            r1[g] = max(r1[g], D);
+            continue;
         }
+        int kr = (D << 15) | jc;
+        int kc = (D << 6) | (63 - (rt * 32 + acc_row(g)));
+        if (MASK) {
+            if (j >= nb) kr = NONE;
+            if (rowbase + rt * 32 + acc_row(g) + 4 * h >= na) kc = NONE;
+        }
+        if (MAGE_MATCH_ABLATE != 2) push2(r1[g], r2[g], kr);
+        if (MAGE_MATCH_ABLATE != 1) push2(c1, c2, kc);
     }
-    // local column keys -> global (D << 15 | 0x7FFF - i), then merge with the partner half
-    const int ib = rowbase + 4 * h;
-    if (c1 != NONE) c1 = ((c1 >> 6) << 15) | (0x7FFF - (ib + 63 - (c1 & 63)));
-    if (c2 != NONE) c2 = ((c2 >> 6) << 15) | (0x7FFF - (ib + 63 - (c2 & 63)));
+}
+
+// Column partial of one B tile -> global keys (D << 15 | 0x7FFF - i), merged with the partner
+// half-wave, then into the workgroup's column top-2 with two LDS atomicMax (no CAS loop: a key
+// that loses, or is displaced from, the best slot is pushed into the second slot).
+__device__ __forceinline__ void flush_cols(int c1, int c2, int lane, int colbase, int nb, int rowbase,
+                                           int* colM1, int* colM2)
+{
+    if (MAGE_MATCH_ABLATE == 1 || MAGE_MATCH_ABLATE == 4) return;
+    const int h = lane >> 5;
+    const int j = colbase + (lane & 31);
+    const int ib = rowbase + 4 * h + 63;
+    if (c1 != NONE) c1 = ((c1 >> 6) << 15) | (0x7FFF - (ib - (c1 & 63)));
+    if (c2 != NONE) c2 = ((c2 >> 6) << 15) | (0x7FFF - (ib - (c2 & 63)));
     merge2(c1, c2, __shfl_xor(c1, 32), __shfl_xor(c2, 32));
-    if (h == 0 && jvalid && c1 != NONE) {
+    if (h == 0 && j < nb && c1 != NONE) {
         const int old = atomicMax(&colM1[j], c1);
         atomicMax(&colM2[j], old > c1 ? c1 : max(old, c2));
     }
 }
 
+// Padding rows and columns have zero operands, so D = 0 (d = 128) there: such a key can neither
+// be accepted (d0 <= maxDist) nor hide an in-radius second best while maxDist < 128, so the
+// kernel for those radii (every practical one) folds without masks; PADMASK covers the rest.
+template <bool PADMASK>
+__device__ __forceinline__ void fold_any(const v16i& acc, int rt, int lane, int colbase, int nb, int rowbase,
+                                         int na, int (&r1)[16], int (&r2)[16], int& c1, int& c2)
+{
+    if (PADMASK && (colbase + 32 > nb || rowbase + RT * 32 > na))
+        fold<true>(acc, rt, lane, colbase, nb, rowbase, na, r1, r2, c1, c2);
+    else
+        fold<false>(acc, rt, lane, colbase, nb, rowbase, na, r1, r2, c1, c2);
+}
+
+// All row passes of one (A, B) pair.  RES: the packed B descriptors are resident in LDS (Bres),
+// so the stage loop issues no global loads (hipcc drains vmcnt(0) at the first use of any
+// global-load result, which would expose a full L2/HBM round trip per stage); otherwise each
+// stage's B words are fetched from global one stage ahead (nb > NRES only).
+template <bool PADMASK, bool RES>
+__device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, const uint32_t* __restrict__ Bw,
+                                           const uint32_t* Bres, int na, int nb,
+                                           v4i (*stage)[SC / 32][8][kWave], int* colM1, int* colM2,
+                                           int2* __restrict__ rows)
+{
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nstages = (nb + SC - 1) / SC;
+    // stage-fill item of this thread: k-step s, column c of the stage
+    const int fs = tid / SC, fc = tid % SC;
+    auto fetch = [&](int st) -> uint32_t {
+        const int j = min(st * SC + fc, nb - 1);
+        return RES ? Bres[8 * j + fs] : Bw[8 * j + fs];
+    };
+    auto fill = [&](int buf, int st, uint32_t dw) {
+        const bool ok = st * SC + fc < nb;  // padding columns: zero operands
+        const v4i zero = {0, 0, 0, 0};
+        stage[buf][fc >> 5][fs][fc & 31] = ok ? expand16(dw & 0xFFFFu) : zero;
+        stage[buf][fc >> 5][fs][32 + (fc & 31)] = ok ? expand16(dw >> 16) : zero;
+    };
+
+    for (int pb = 0; pb < na; pb += ROWS) {
+        const int rowbase = pb + wave * (RT * 32);
+        const bool active = rowbase < na;
+        v4i a[RT][8];
+        int r1[RT][16], r2[RT][16];
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++) {
+            const int i = rowbase + rt * 32 + (lane & 31);
+            const int ic = min(i, na - 1);
+            uint32_t dw[8];
+#pragma unroll
+            for (int s = 0; s < 8; s++) dw[s] = Aw[8 * ic + s];
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                a[rt][s] = expand16((lane >> 5) ? (dw[s] >> 16) : (dw[s] & 0xFFFFu));
+                if (i >= na) a[rt][s] = v4i{0, 0, 0, 0};  // padding rows: zero operands
+            }
+#pragma unroll
+            for (int g = 0; g < 16; g++) {
+                r1[rt][g] = NONE;
+                r2[rt][g] = NONE;
+            }
+        }
+        {
+            const uint32_t w0 = fetch(0), w1 = nstages > 1 ? fetch(1) : 0u;
+            __syncthreads();  // column states / Bres ready; previous pass done with the stages
+            fill(0, 0, w0);
+            if (nstages > 1) fill(1, 1, w1);
+            __syncthreads();
+        }
+        // Software pipeline over the pass's B tiles t (stage st + 2 is filled during stage st,
+        // three buffers):  MFMA(t, rows 0-31) | fold(t-1, rows 32-63) + column flush(t-1) |
+        // MFMA(t, rows 32-63) | fragments of t+1 | fold(t, rows 0-31).
+        v4i bf[8];
+        load_frags(bf, &stage[0][0][0][0], lane);
+        v16i acc1;
+        int cbp = -1, p1 = NONE, p2 = NONE;
+        for (int st = 0; st < nstages; st++) {
+            const int buf = st % NBUF;
+            uint32_t nxt = 0;
+            if (st + 2 < nstages) nxt = fetch(st + 2);
+            if (active) {
+#pragma unroll
+                for (int ct = 0; ct < SC / 32; ct++) {
+                    const int colbase = st * SC + ct * 32;
+                    if (colbase >= nb) break;
+                    const v16i acc0 = tile_mfma(a[0], bf);
+                    if (cbp >= 0) {
+                        fold_any<PADMASK>(acc1, 1, lane, cbp, nb, rowbase, na, r1[1], r2[1], p1, p2);
+                        flush_cols(p1, p2, lane, cbp, nb, rowbase, colM1, colM2);
+                    }
+                    acc1 = tile_mfma(a[1], bf);
+                    if (ct + 1 < SC / 32 && colbase + 32 < nb)
+                        load_frags(bf, &stage[buf][ct + 1][0][0], lane);
+                    else if (st + 1 < nstages)
+                        load_frags(bf, &stage[(st + 1) % NBUF][0][0][0], lane);
+                    p1 = NONE;
+                    p2 = NONE;
+                    fold_any<PADMASK>(acc0, 0, lane, colbase, nb, rowbase, na, r1[0], r2[0], p1, p2);
+                    cbp = colbase;
+                }
+            }
+            if (MAGE_MATCH_ABLATE < 5 && st + 2 < nstages) fill((st + 2) % NBUF, st + 2, nxt);
+            if (MAGE_MATCH_ABLATE != 6) __syncthreads();
+        }
+        if (active) {
+            if (cbp >= 0) {
+                fold_any<PADMASK>(acc1, 1, lane, cbp, nb, rowbase, na, r1[1], r2[1], p1, p2);
+                flush_cols(p1, p2, lane, cbp, nb, rowbase, colM1, colM2);
+            }
+            // reduce-scatter the 32 row states (row tile q >> 4, register q & 15) over the 32
+            // lanes of each half: lane c ends with state q = c.
+            int s1[RT * 16], s2[RT * 16];
+#pragma unroll
+            for (int q = 0; q < RT * 16; q++) {
+                s1[q] = r1[q >> 4][q & 15];
+                s2[q] = r2[q >> 4][q & 15];
+            }
+#pragma unroll
+            for (int m = 16, n = 32; m >= 1; m >>= 1, n >>= 1) {
+                const bool up = (lane & m) != 0;
+                const int hf = n / 2;
+#pragma unroll
+                for (int k = 0; k < hf; k++) {
+                    const int send1 = up ? s1[k] : s1[k + hf], send2 = up ? s2[k] : s2[k + hf];
+                    int m1 = up ? s1[k + hf] : s1[k], m2 = up ? s2[k + hf] : s2[k];
+                    merge2(m1, m2, __shfl_xor(send1, m), __shfl_xor(send2, m));
+                    s1[k] = m1;
+                    s2[k] = m2;
+                }
+            }
+            const int c = lane & 31;
+            const int i = rowbase + (c >> 4) * 32 + acc_row(c & 15) + 4 * (lane >> 5);
+            if (i < na) rows[i] = make_int2(s1[0], s2[0]);
+        }
+    }
+}
+
+constexpr int NRES = 2560;  // B descriptors kept resident in LDS up to this count
+
+template <bool PADMASK>
 __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A,
                                                    const uint32_t* __restrict__ nA,
                                                    const uint8_t* __restrict__ B,
@@ -156,10 +317,12 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
                                                    uint32_t* __restrict__ n_out,
                                                    uint32_t* __restrict__ status)
 {
-    __shared__ v4i stage[2][SC / 32][8][kWave];  // [buffer][tile][k-step][lane] operands
-    __shared__ int colM1[NMAX], colM2[NMAX];
-    __shared__ int rowM1[NMAX], rowM2[NMAX];
+    __shared__ v4i stage[NBUF][SC / 32][8][kWave];  // [buffer][tile][k-step][lane] operands
+    // resident path: packed B (8 words per descriptor) then the column states; streaming path:
+    // the column states only
+    __shared__ __attribute__((aligned(16))) uint32_t pool[NRES * 10];
     __shared__ uint32_t wsum[MW];
+    static_assert(NRES * 10 >= 2 * NMAX, "column states of the streaming path fit the pool");
 
     const int pair = blockIdx.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -174,95 +337,22 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
     const int maxDist = p.max_dist;
     const uint32_t* Aw = reinterpret_cast<const uint32_t*>(A + pair * p.a_pitch);
     const uint32_t* Bw = reinterpret_cast<const uint32_t*>(B + pair * p.b_pitch);
+    int2* rows = p.rows + (long long)pair * NMAX;
+    const bool res = nb <= NRES;
+    int* colM1 = reinterpret_cast<int*>(pool) + (res ? 8 * nb : 0);
+    int* colM2 = colM1 + nb;
     for (int j = tid; j < nb; j += MT) {
         colM1[j] = NONE;
         colM2[j] = NONE;
     }
-    const int nstages = (nb + SC - 1) / SC;
-    // stage-fill item of this thread: k-step s, column c of the stage
-    const int fs = tid >> 6, fc = tid & 63;
-    auto fetch = [&](int st) -> uint32_t {
-        const int j = st * SC + fc;
-        return j < nb ? Bw[8 * j + fs] : 0u;
-    };
-    auto fill = [&](int buf, uint32_t dw) {
-        stage[buf][fc >> 5][fs][fc & 31] = expand16(dw & 0xFFFFu);
-        stage[buf][fc >> 5][fs][32 + (fc & 31)] = expand16(dw >> 16);
-    };
-
-    for (int pb = 0; pb < na; pb += ROWS) {
-        const int rowbase = pb + wave * (RT * 32);
-        const bool active = rowbase < na;
-        v4i a[RT][8];
-        int r1[RT][16], r2[RT][16];
-#pragma unroll
-        for (int rt = 0; rt < RT; rt++) {
-            const int i = rowbase + rt * 32 + (lane & 31);
-            uint32_t dw[8];
-#pragma unroll
-            for (int s = 0; s < 8; s++) dw[s] = i < na ? Aw[8 * i + s] : 0u;
-#pragma unroll
-            for (int s = 0; s < 8; s++) {
-                a[rt][s] = expand16((lane >> 5) ? (dw[s] >> 16) : (dw[s] & 0xFFFFu));
-                if (i >= na) a[rt][s] = v4i{0, 0, 0, 0};
-            }
-#pragma unroll
-            for (int g = 0; g < 16; g++) {
-                r1[rt][g] = NONE;
-                r2[rt][g] = NONE;
-            }
-        }
-        __syncthreads();  // column states initialised / previous pass done with the stages
-        fill(0, fetch(0));
-        __syncthreads();
-        for (int st = 0; st < nstages; st++) {
-            const int buf = st & 1;
-            uint32_t nxt = 0;
-            if (st + 1 < nstages) nxt = fetch(st + 1);
-            if (active) {
-#pragma unroll
-                for (int ct = 0; ct < SC / 32; ct++) {
-                    const int colbase = st * SC + ct * 32;
-                    if (colbase >= nb) break;
-                    const v4i* bt = &stage[buf][ct][0][0];
-                    if (colbase + 32 > nb || rowbase + RT * 32 > na)
-                        tile_pass<true>(a, bt, lane, colbase, nb, rowbase, na, r1, r2, colM1, colM2);
-                    else
-                        tile_pass<false>(a, bt, lane, colbase, nb, rowbase, na, r1, r2, colM1, colM2);
-                }
-            }
-            if (st + 1 < nstages) fill(buf ^ 1, nxt);
+    if (na > 0 && nb > 0) {
+        if (res) {
+            const uint4* src = reinterpret_cast<const uint4*>(Bw);
+            for (int k = tid; k < 2 * nb; k += MT) reinterpret_cast<uint4*>(pool)[k] = src[k];
             __syncthreads();
-        }
-        if (active) {
-            // reduce-scatter the row states over the 32 lanes of each half: lane c ends with
-            // state q = c, i.e. row tile c >> 4, register c & 15.
-            int s1[RT * 16], s2[RT * 16];
-#pragma unroll
-            for (int q = 0; q < RT * 16; q++) {
-                s1[q] = r1[q >> 4][q & 15];
-                s2[q] = r2[q >> 4][q & 15];
-            }
-#pragma unroll
-            for (int m = 16, n = 32; m >= 1; m >>= 1, n >>= 1) {
-                const bool up = (lane & m) != 0;
-                const int hf = n / 2;
-#pragma unroll
-                for (int k = 0; k < hf; k++) {
-                    const int send1 = up ? s1[k] : s1[k + hf], send2 = up ? s2[k] : s2[k + hf];
-                    const int keep1 = up ? s1[k + hf] : s1[k], keep2 = up ? s2[k + hf] : s2[k];
-                    int m1 = keep1, m2 = keep2;
-                    merge2(m1, m2, __shfl_xor(send1, m), __shfl_xor(send2, m));
-                    s1[k] = m1;
-                    s2[k] = m2;
-                }
-            }
-            const int c = lane & 31;
-            const int i = rowbase + (c >> 4) * 32 + acc_row(c & 15) + 4 * (lane >> 5);
-            if (i < na) {
-                rowM1[i] = s1[0];
-                rowM2[i] = s2[0];
-            }
+            row_passes<PADMASK, true>(Aw, Bw, pool, na, nb, stage, colM1, colM2, rows);
+        } else {
+            row_passes<PADMASK, false>(Aw, Bw, pool, na, nb, stage, colM1, colM2, rows);
         }
     }
     __syncthreads();
@@ -270,14 +360,17 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
     // cross-check + ordered compaction (ascending A index, FeatureMatcher.cpp:142-167)
     uint32_t base = 0;
     mage_dmatch* o = out + (long long)pair * p.out_cap;
-    for (int rb = 0; rb < na; rb += MT) {
+    for (int rb = 0; rb < (nb > 0 ? na : 0); rb += MT) {
         const int i = rb + tid;
         bool ok = false;
         int j = 0, d = 0;
-        if (i < na && accept(rowM1[i], rowM2[i], maxDist, p.min_diff)) {
-            j = key_index(rowM1[i]);
-            d = key_dist(rowM1[i]);
-            ok = accept(colM1[j], colM2[j], maxDist, p.min_diff) && key_index(colM1[j]) == i;
+        if (i < na) {
+            const int2 r = rows[i];
+            if (accept(r.x, r.y, maxDist, p.min_diff)) {
+                j = key_index(r.x);
+                d = key_dist(r.x);
+                ok = accept(colM1[j], colM2[j], maxDist, p.min_diff) && key_index(colM1[j]) == i;
+            }
         }
         const unsigned long long m = __ballot(ok);
         const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
@@ -306,7 +399,7 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
 }
 
 struct MatchScratch {
-    DeviceBuffer a, b, n, out, status;
+    DeviceBuffer a, b, n, out, status, rows;
 };
 thread_local MatchScratch g_match;
 
@@ -317,7 +410,10 @@ mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA
                         int minDiff, mage_dmatch* dOut, uint32_t cap, uint32_t* dN,
                         uint32_t* dStatus, hipStream_t st)
 {
+    mage_status r = g_match.rows.reserve((size_t)pairs * NMAX * sizeof(int2));
+    if (r != MAGE_OK) return r;
     MatchParams mp{};
+    mp.rows = g_match.rows.as<int2>();
     mp.max_dist = maxDist;
     mp.min_diff = minDiff;
     mp.out_cap = cap;
@@ -325,7 +421,10 @@ mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA
     mp.b_pitch = bPitch;
     {
         KernelTimer _kt("match.two_way", st);
-        hipLaunchKernelGGL(match_kernel, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
+        if (maxDist < 128)
+            hipLaunchKernelGGL(match_kernel<false>, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
+        else
+            hipLaunchKernelGGL(match_kernel<true>, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
     }
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;
