@@ -3,9 +3,10 @@
 // (Core/MAGESLAM/Source/Image/OpenCVModified.cpp:771-886).
 //
 // Pipeline for a batch of B frames (all device resident), three launches:
-//   1. fast_nms_kernel  grid (W/64, H/16, B): 64x16 tile + 4-px halo staged in LDS, FAST score
-//      for a 66x18 region, strict 3x3 NMS, border filter, per-tile LDS compaction, one global
-//      atomic per tile.  Candidates are packed u32 (y<<20 | x<<8 | score).
+//   1. fast_nms_kernel  grid (W/120, H/30, B): tile + halo staged in LDS; each thread scores a
+//      4-px x 8-row strip from a register window with packed-f16 min3/max3 ladders (two pixels
+//      per instruction), then a dword-vectorised strict 3x3 NMS, border filter, per-tile LDS
+//      compaction, one global atomic per tile.  Candidates are packed u32 (y<<20 | x<<8 | score).
 //   2. select_kernel    grid (B), 1024 threads: 256-bin histogram -> RetainBestFeatures cut,
 //      bbox, 32x32 cell counting sort, per-item ANMS ring search, 64-bit key bitonic sort in LDS,
 //      emits keypoints in canonical order (ANMS rank r desc, strength desc, raster asc).
@@ -29,11 +30,18 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // 1. FAST-9/16 + NMS
 // ------------------------------------------------------------------------------------------
-constexpr int TW = 64, TH = 32, HALO = 4;
-constexpr int LW = TW + 2 * HALO;  // 72 bytes: 18 dwords per LDS row
-constexpr int LH = TH + 2 * HALO;  // 40
-constexpr int SW = TW + 2, SH = TH + 2;
-constexpr int FAST_THREADS = 256;
+// Output tile TW x TH.  Scores are computed for the (TW + 8) x (TH + 2) region starting at
+// (tx0 - 4, ty0 - 1): whole 4-pixel groups plus the 1-pixel NMS ring.  The image region staged
+// in LDS starts at (tx0 - 8, ty0 - 4) so every group's 12-byte window row is three aligned dwords.
+constexpr int TW = 120, TH = 30;
+constexpr int GX = (TW + 8) / 4;       // 32 score groups per row
+constexpr int SR = 8;                  // score rows per thread strip
+constexpr int SROWS = TH + 2;          // 32 score rows
+constexpr int LW = TW + 16;            // 136 image bytes per LDS row (34 dwords)
+constexpr int LH = TH + 8;             // 38 image rows
+constexpr int FAST_THREADS = GX * (SROWS / SR);  // 128
+static_assert(SROWS % SR == 0, "strips tile the score rows");
+static_assert(TW % 4 == 0, "tile origin stays dword aligned");
 
 struct FastParams {
     int w, h, stride;
@@ -44,47 +52,110 @@ struct FastParams {
     int dword_ok;  // frames 4-byte aligned with width, stride and pitch multiples of 4
 };
 
-// Ring of FAST_t<16> (makeOffsets, OpenCVModified.cpp:890-921) as (dx, dy).
-__device__ __constant__ signed char c_ring[16][2] = {
-    {0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
-    {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
-
-// FAST-9/16 score of the pixel at p (LDS, row stride LW), branch-free.
-// With d_k = v - x_k over the 16-pixel ring, let A = max over the 16 cyclic 9-arcs of
-// min(d) and B = max over the arcs of min(-d).  "Some 9 contiguous ring pixels are all darker
-// than v - t" (the segment test of FAST_t<16>, OpenCVModified.cpp:1415-1479) is exactly A > t,
-// "all brighter than v + t" is B > t, and cornerScore<16> (:927-1071; its scalar and SSE2
-// branches agree on corners) is max(A, B) - 1.  So one min3/max3 ladder gives both: 9-arc
-// minima as min3 of three 3-arc minima.  Returns 0 for non-corners.
-__device__ __forceinline__ int fast_score(const uint8_t* p, int t)
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ uint32_t as_u32(h2 h) { return __builtin_bit_cast(uint32_t, h); }
+// v_pk_minimum3_f16 / v_pk_maximum3_f16 (gfx950)
+__device__ __forceinline__ h2 min3h(h2 a, h2 b, h2 c)
 {
-    const int v = p[0];
-    int d[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)p[c_ring[k][1] * LW + c_ring[k][0]];
-    int m3[16], x3[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        m3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-        x3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-    }
-    int a = -1000, b = 1000;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        a = max(a, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
-        b = min(b, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15]));
-    }
-    const int raw = max(a, -b);
-    return raw > t ? raw - 1 : 0;
+    return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ __forceinline__ h2 max3h(h2 a, h2 b, h2 c)
+{
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 
-// Stage the (TW + 8) x (TH + 8) window into LDS; zeros outside the image.  When the row pitch
-// and the width are multiples of 4 every dword is wholly inside or outside the frame (the
-// window origin is 4-aligned), so it is moved with 4-byte loads.
+// Bytes (k, k+1) of dword d as two f16 lanes holding 1024 + byte: [b_k, 0x64, b_k+1, 0x64].
+// The 1024 offset is exact in f16 and cancels in every difference.
+__device__ __forceinline__ h2 pair_in(uint32_t d, int k)
+{
+    return as_h2(__builtin_amdgcn_perm(d, 0x64646464u, (uint32_t)((4 + k) | ((5 + k) << 16))));
+}
+__device__ __forceinline__ h2 pair_cross(uint32_t lo, uint32_t hi)  // (lo.b3, hi.b0)
+{
+    return as_h2(__builtin_amdgcn_perm(hi, lo, 0x0C040C03u) | 0x64006400u);
+}
+
+// The 9 adjacent byte pairs (i, i+1), i = 1..9, of a 12-byte window row; q[i - 1].
+__device__ __forceinline__ void window_row(uint32_t d0, uint32_t d1, uint32_t d2, h2 (&q)[9])
+{
+    q[0] = pair_in(d0, 1);
+    q[1] = pair_in(d0, 2);
+    q[2] = pair_cross(d0, d1);
+    q[3] = pair_in(d1, 0);
+    q[4] = pair_in(d1, 1);
+    q[5] = pair_in(d1, 2);
+    q[6] = pair_cross(d1, d2);
+    q[7] = pair_in(d2, 0);
+    q[8] = pair_in(d2, 1);
+}
+
+// Ring of FAST_t<16> (makeOffsets, OpenCVModified.cpp:890-921) as (dx, dy).
+__host__ __device__ constexpr int ring_dx(int k)
+{
+    constexpr int v[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    return v[k];
+}
+__host__ __device__ constexpr int ring_dy(int k)
+{
+    constexpr int v[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    return v[k];
+}
+
+// FAST-9/16 raw score for two horizontally adjacent pixels (group pixels 2p, 2p + 1) from the
+// 7 window rows w[dy + 3], branch-free.  With d_k = v - x_k over the 16-pixel ring, let
+// A = max over the 16 cyclic 9-arcs of min(d) and B = min over the arcs of max(d).  "Some 9
+// contiguous ring pixels are all darker than v - t" (the segment test of FAST_t<16>,
+// OpenCVModified.cpp:1415-1479) is exactly A > t, "all brighter than v + t" is -B > t, and
+// cornerScore<16> (:927-1071; its scalar and SSE2 branches agree on corners) is max(A, -B) - 1.
+// 9-arc extrema are min3/max3 of three 3-arc extrema; every value is an integer in [-255, 255],
+// exact in f16, so the packed f16 min3/max3 give the integer result.
+template <int P>
+__device__ __forceinline__ h2 fast_raw2(const h2 (&w)[7][9])
+{
+    const h2 v = w[3][4 + 2 * P - 1];
+    h2 d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - w[ring_dy(k) + 3][4 + 2 * P + ring_dx(k) - 1];
+    h2 m3[16], x3[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m3[k] = min3h(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+        x3[k] = max3h(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+    }
+    h2 m9[16], x9[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m9[k] = min3h(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]);
+        x9[k] = max3h(x3[k], x3[(k + 3) & 15], x3[(k + 6) & 15]);
+    }
+    h2 a = max3h(m9[0], m9[1], m9[2]), b = min3h(x9[0], x9[1], x9[2]);
+#pragma unroll
+    for (int k = 3; k < 15; k += 2) {
+        a = max3h(a, m9[k], m9[k + 1]);
+        b = min3h(b, x9[k], x9[k + 1]);
+    }
+    a = __builtin_elementwise_maximum(a, m9[15]);
+    b = __builtin_elementwise_minimum(b, x9[15]);
+    return __builtin_elementwise_maximum(a, -b);
+}
+
+// Score bytes of two pixels from their raw scores: raw > t ? raw - 1 : 0, as 1024 + score.
+__device__ __forceinline__ uint32_t score2(h2 raw, h2 tf)
+{
+    const h2 zero = {(_Float16)0.0f, (_Float16)0.0f}, one = {(_Float16)1.0f, (_Float16)1.0f};
+    const h2 step = __builtin_elementwise_minimum(__builtin_elementwise_maximum(raw - tf, zero), one);
+    const h2 k1024 = {(_Float16)1024.0f, (_Float16)1024.0f};
+    return as_u32(raw * step - step + k1024);
+}
+
+// Stage the LW x LH image window into LDS; zeros outside the frame.  When the row pitch and the
+// width are multiples of 4 every dword is wholly inside or outside the frame (the window origin
+// is 4-aligned), so it is moved with 4-byte loads.
 __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const FastParams& p,
                                           uint8_t (*img)[LW])
 {
-    const int gx0 = blockIdx.x * TW - HALO, gy0 = blockIdx.y * TH - HALO;
+    const int gx0 = blockIdx.x * TW - 8, gy0 = blockIdx.y * TH - 4;
     if (p.dword_ok) {
         constexpr int DW = LW / 4;
         for (int i = threadIdx.x; i < LH * DW; i += FAST_THREADS) {
@@ -98,11 +169,48 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const
         return;
     }
     for (int i = threadIdx.x; i < LH * LW; i += FAST_THREADS) {
-        int r = i / LW, c = i - r * LW;
-        int gx = gx0 + c, gy = gy0 + r;
+        const int r = i / LW, c = i - r * LW;
+        const int gx = gx0 + c, gy = gy0 + r;
         uint8_t v = 0;
         if (gx >= 0 && gx < p.w && gy >= 0 && gy < p.h) v = src[(long long)gy * p.stride + gx];
         img[r][c] = v;
+    }
+}
+
+// Scores of the thread's strip: group gx (4 columns), score rows [SR * chunk, SR * chunk + SR),
+// written as one dword per row into sc.  Pixels outside the FAST range [3, w-4] x [3, h-4]
+// score 0.
+__device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], const FastParams& p)
+{
+    const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
+    const int X0 = blockIdx.x * TW - 4 + 4 * gx;     // image column of the group's first pixel
+    const int Y0 = blockIdx.y * TH - 1 + SR * chunk;  // image row of the strip's first score row
+    uint32_t colmask = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (X0 + q >= 3 && X0 + q <= p.w - 4) colmask |= 0xFFu << (8 * q);
+    const _Float16 t = (_Float16)(float)p.threshold;
+    const h2 tf = {t, t};
+    // window rows: LDS row (score row) + dy + 3; the strip needs LDS rows SR*chunk .. +SR+5
+    h2 w[SR + 6][9];
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(&img[SR * chunk][0]) + gx;
+#pragma unroll
+    for (int r = 0; r < SR + 6; r++) {
+        const uint32_t* rp = base + r * (LW / 4);
+        window_row(rp[0], rp[1], rp[2], w[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < SR; r++) {
+        h2 win[7][9];
+#pragma unroll
+        for (int k = 0; k < 7; k++)
+#pragma unroll
+            for (int i = 0; i < 9; i++) win[k][i] = w[r + k][i];
+        const uint32_t s0 = score2(fast_raw2<0>(win), tf), s1 = score2(fast_raw2<1>(win), tf);
+        uint32_t bytes = __builtin_amdgcn_perm(s1, s0, 0x06040200u);  // low bytes of the 4 lanes
+        const int Y = Y0 + r;
+        if (Y < 3 || Y > p.h - 4) bytes = 0;
+        sc[SR * chunk + r][gx] = bytes & colmask;
     }
 }
 
@@ -112,33 +220,66 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* _
                                                                 uint32_t* __restrict__ counts)
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
-    __shared__ uint8_t sc[SH][SW + 2];
+    __shared__ uint32_t sc[SROWS][GX];
     __shared__ uint32_t list[(TW / 2) * (TH / 2)];  // strict 3x3 maxima are never 8-adjacent
     __shared__ uint32_t s_cnt, s_base;
     const int f = blockIdx.z;
     load_tile(frames + (long long)f * p.pitch, p, img);
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < SH * SW; i += FAST_THREADS) {
-        int sy = i / SW, sx = i - sy * SW;
-        int X = blockIdx.x * TW - 1 + sx, Y = blockIdx.y * TH - 1 + sy;
-        int s = 0;
-        if (X >= 3 && X <= p.w - 4 && Y >= 3 && Y <= p.h - 4) s = fast_score(&img[sy + 3][sx + 3], p.threshold);
-        sc[sy][sx] = (uint8_t)s;
-    }
+    score_strip(img, sc, p);
     __syncthreads();
-    // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter
-    for (int i = threadIdx.x; i < TW * TH; i += FAST_THREADS) {
-        int oy = i / TW, ox = i - oy * TW;
-        int X = blockIdx.x * TW + ox, Y = blockIdx.y * TH + oy;
-        int s = sc[oy + 1][ox + 1];
-        bool keep = s > 0 && X >= p.xlo && X <= p.xhi && Y >= p.ylo && Y <= p.yhi &&
-                    s > sc[oy][ox] && s > sc[oy][ox + 1] && s > sc[oy][ox + 2] &&
-                    s > sc[oy + 1][ox] && s > sc[oy + 1][ox + 2] && s > sc[oy + 2][ox] &&
-                    s > sc[oy + 2][ox + 1] && s > sc[oy + 2][ox + 2];
-        if (keep) {
-            uint32_t slot = atomicAdd(&s_cnt, 1u);
-            list[slot] = ((uint32_t)Y << 20) | ((uint32_t)X << 8) | (uint32_t)s;
+    // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter, four
+    // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8)
+    {
+        constexpr int OG = TW / 4;  // 30 output groups per row
+        const int og = threadIdx.x % 32, chunk = threadIdx.x / 32;
+        if (og < OG) {
+            const int X0 = blockIdx.x * TW + 4 * og;
+            const int oy0 = 8 * chunk, oy1 = min(oy0 + 8, TH);
+            auto load3 = [&](int srow, uint32_t& l, uint32_t& c, uint32_t& r) {
+                l = sc[srow][og];
+                c = sc[srow][og + 1];
+                r = sc[srow][og + 2];
+            };
+            uint32_t ul, uc, ur, ml, mc, mr;
+            load3(oy0, ul, uc, ur);
+            load3(oy0 + 1, ml, mc, mr);
+            for (int oy = oy0; oy < oy1; oy++) {
+                uint32_t dl, dc, dr;
+                load3(oy + 2, dl, dc, dr);
+                if (mc != 0) {
+                    // neighbour bytes aligned to the four centre pixels
+                    const uint32_t nb[8] = {__builtin_amdgcn_alignbyte(uc, ul, 3), uc, __builtin_amdgcn_alignbyte(ur, uc, 1),
+                                            __builtin_amdgcn_alignbyte(mc, ml, 3), __builtin_amdgcn_alignbyte(mr, mc, 1),
+                                            __builtin_amdgcn_alignbyte(dc, dl, 3), dc, __builtin_amdgcn_alignbyte(dr, dc, 1)};
+                    // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) as f16 lanes
+                    auto even = [](uint32_t d) { return as_h2(__builtin_amdgcn_perm(d, 0x64646464u, 0x00060004u)); };
+                    auto odd = [](uint32_t d) { return as_h2(__builtin_amdgcn_perm(d, 0x64646464u, 0x00070005u)); };
+                    const h2 ev = max3h(max3h(even(nb[0]), even(nb[1]), even(nb[2])), max3h(even(nb[3]), even(nb[4]), even(nb[5])),
+                               __builtin_elementwise_maximum(even(nb[6]), even(nb[7])));
+                    const h2 od = max3h(max3h(odd(nb[0]), odd(nb[1]), odd(nb[2])), max3h(odd(nb[3]), odd(nb[4]), odd(nb[5])),
+                               __builtin_elementwise_maximum(odd(nb[6]), odd(nb[7])));
+                    const h2 ge = even(mc) - ev, go = odd(mc) - od;  // > 0: strict maximum
+                    const int Y = blockIdx.y * TH + oy;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const float g = (float)((q & 1) ? go[q >> 1] : ge[q >> 1]);
+                        const int X = X0 + q;
+                        if (g > 0.0f && X >= p.xlo && X <= p.xhi && Y >= p.ylo && Y <= p.yhi) {
+                            const uint32_t s = (mc >> (8 * q)) & 0xFFu;
+                            const uint32_t slot = atomicAdd(&s_cnt, 1u);
+                            list[slot] = ((uint32_t)Y << 20) | ((uint32_t)X << 8) | s;
+                        }
+                    }
+                }
+                ul = ml;
+                uc = mc;
+                ur = mr;
+                ml = dl;
+                mc = dc;
+                mr = dr;
+            }
         }
     }
     __syncthreads();
@@ -146,7 +287,7 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* _
     __syncthreads();
     uint32_t* out = cand + (long long)f * p.cand_cap;
     for (uint32_t k = threadIdx.x; k < s_cnt; k += FAST_THREADS) {
-        uint32_t idx = s_base + k;
+        const uint32_t idx = s_base + k;
         if (idx < p.cand_cap) out[idx] = list[k];
     }
 }
@@ -156,15 +297,17 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_score_map_kernel(const uint
                                                                       uint8_t* __restrict__ score)
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
+    __shared__ uint32_t sc[SROWS][GX];
     load_tile(src, p, img);
     __syncthreads();
+    score_strip(img, sc, p);
+    __syncthreads();
+    const uint8_t* scb = reinterpret_cast<const uint8_t*>(&sc[0][0]);
     for (int i = threadIdx.x; i < TW * TH; i += FAST_THREADS) {
-        int oy = i / TW, ox = i - oy * TW;
-        int X = blockIdx.x * TW + ox, Y = blockIdx.y * TH + oy;
+        const int oy = i / TW, ox = i - oy * TW;
+        const int X = blockIdx.x * TW + ox, Y = blockIdx.y * TH + oy;
         if (X >= p.w || Y >= p.h) continue;
-        int s = 0;
-        if (X >= 3 && X <= p.w - 4 && Y >= 3 && Y <= p.h - 4) s = fast_score(&img[oy + HALO][ox + HALO], p.threshold);
-        score[(long long)Y * p.w + X] = (uint8_t)s;
+        score[(long long)Y * p.w + X] = scb[(oy + 1) * (4 * GX) + ox + 4];
     }
 }
 
