@@ -50,6 +50,12 @@ struct FastParams {
     int xlo, xhi, ylo, yhi;  // emission window (FAST range ∩ RunByImageBorder)
     unsigned cand_cap;
     int dword_ok;  // frames 4-byte aligned with width, stride and pitch multiples of 4
+    // fused 7-tap Gaussian (8U fixed point) of the tile into `blur` (null: no blur)
+    uint8_t* blur;
+    int blur_stride;           // multiple of 4, >= w
+    long long blur_pitch;      // bytes between blurred frames
+    uint32_t t0, t1;           // taps 0-3 and 4-6 (+0) as bytes, for v_dot4_u32_u8
+    uint32_t t01, t23, t45, t6;  // tap pairs as u16, for v_dot2_u32_u16
 };
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -149,31 +155,35 @@ __device__ __forceinline__ uint32_t score2(h2 raw, h2 tf)
     return as_u32(raw * step - step + k1024);
 }
 
-// Stage the LW x LH image window into LDS; zeros outside the frame.  When the row pitch and the
-// width are multiples of 4 every dword is wholly inside or outside the frame (the window origin
-// is 4-aligned), so it is moved with 4-byte loads.
+__device__ __forceinline__ int reflect101(int i, int n)
+{
+    if (n == 1) return 0;
+    while ((unsigned)i >= (unsigned)n) i = i < 0 ? -i : 2 * n - 2 - i;
+    return i;
+}
+
+// Stage the LW x LH image window into LDS, reflect-101 outside the frame (BORDER_DEFAULT of the
+// reference's GaussianBlur; FAST never reads outside the frame, its range is [3, w-4]).  When
+// the row pitch and the width are multiples of 4, dwords wholly inside the frame are moved with
+// 4-byte loads.
 __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const FastParams& p,
                                           uint8_t (*img)[LW])
 {
     const int gx0 = blockIdx.x * TW - 8, gy0 = blockIdx.y * TH - 4;
-    if (p.dword_ok) {
-        constexpr int DW = LW / 4;
-        for (int i = threadIdx.x; i < LH * DW; i += FAST_THREADS) {
-            const int r = i / DW, c = i - r * DW;
-            const int gx = gx0 + 4 * c, gy = gy0 + r;
-            uint32_t v = 0;
-            if (gx >= 0 && gx < p.w && gy >= 0 && gy < p.h)
-                v = *reinterpret_cast<const uint32_t*>(src + (long long)gy * p.stride + gx);
-            *reinterpret_cast<uint32_t*>(&img[r][4 * c]) = v;
+    constexpr int DW = LW / 4;
+    for (int i = threadIdx.x; i < LH * DW; i += FAST_THREADS) {
+        const int r = i / DW, c = i - r * DW;
+        const int gx = gx0 + 4 * c, gy = reflect101(gy0 + r, p.h);
+        const uint8_t* row = src + (long long)gy * p.stride;
+        uint32_t v;
+        if (p.dword_ok && gx >= 0 && gx + 3 < p.w) {
+            v = *reinterpret_cast<const uint32_t*>(row + gx);
+        } else {
+            v = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) v |= (uint32_t)row[reflect101(gx + q, p.w)] << (8 * q);
         }
-        return;
-    }
-    for (int i = threadIdx.x; i < LH * LW; i += FAST_THREADS) {
-        const int r = i / LW, c = i - r * LW;
-        const int gx = gx0 + c, gy = gy0 + r;
-        uint8_t v = 0;
-        if (gx >= 0 && gx < p.w && gy >= 0 && gy < p.h) v = src[(long long)gy * p.stride + gx];
-        img[r][c] = v;
+        *reinterpret_cast<uint32_t*>(&img[r][4 * c]) = v;
     }
 }
 
@@ -214,20 +224,74 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
     }
 }
 
+// Fused Gaussian 7x7 (OpenCV 3.4.0 8U fixed point: taps k_t = round(256 g_t); row pass
+// h = sum k_t x, column pass (sum k_t h + 2^15) >> 16, saturated; OpenCVModified.cpp:853-865)
+// of the tile's TW x TH pixels.  Row pass: two v_dot4_u32_u8 per output from the LDS image
+// (h <= 257 * 255 fits u16), stored transposed as row pairs; column pass: four v_dot2_u32_u16.
+constexpr int HR = TH + 6;      // 36 row-pass rows (output rows -3 .. TH+2)
+constexpr int HP = HR / 2 + 1;  // 19 row pairs per column (padded: odd pitch)
+
+__device__ __forceinline__ void blur_rows(const uint8_t (*img)[LW], uint32_t (*hT)[HP], const FastParams& p)
+{
+    // item: 4 output columns (group g) x 2 rows (pair rp): image rows ty0 - 3 + 2 rp + q are
+    // LDS rows 2 rp + q + 1; output column tx0 + 4g + j needs LDS columns 4g + j + 5 .. + 11.
+    for (int it = threadIdx.x; it < (TW / 4) * (HR / 2); it += FAST_THREADS) {
+        const int rp = it % (HR / 2), g = it / (HR / 2);
+        uint32_t o[2][4];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint32_t* row = reinterpret_cast<const uint32_t*>(&img[2 * rp + q + 1][0]);
+            const uint32_t d0 = row[g + 1], d1 = row[g + 2], d2 = row[g + 3];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t w0 = j < 3 ? __builtin_amdgcn_alignbyte(d1, d0, 1 + j) : d1;
+                const uint32_t w1 = j < 3 ? __builtin_amdgcn_alignbyte(d2, d1, 1 + j) : d2;
+                o[q][j] = __builtin_amdgcn_udot4(w1, p.t1, __builtin_amdgcn_udot4(w0, p.t0, 0u, false), false);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) hT[4 * g + j][rp] = o[0][j] | (o[1][j] << 16);
+    }
+}
+
+__device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), c, false);
+}
+
+__device__ __forceinline__ void blur_cols(const uint32_t (*hT)[HP], uint8_t* bt, const FastParams& p)
+{
+    // item: column x, output rows 2m, 2m + 1 (row-pass rows 2m .. 2m + 7)
+    for (int it = threadIdx.x; it < TW * (TH / 2); it += FAST_THREADS) {
+        const int m = it % (TH / 2), x = it / (TH / 2);
+        const uint32_t* c = &hT[x][m];
+        const uint32_t P0 = c[0], P1 = c[1], P2 = c[2], P3 = c[3], P4 = c[4];
+        const uint32_t e = dot2u(P3, p.t6, dot2u(P2, p.t45, dot2u(P1, p.t23, dot2u(P0, p.t01, 32768u))));
+        const uint32_t Q0 = __builtin_amdgcn_alignbyte(P1, P0, 2), Q1 = __builtin_amdgcn_alignbyte(P2, P1, 2);
+        const uint32_t Q2 = __builtin_amdgcn_alignbyte(P3, P2, 2), Q3 = __builtin_amdgcn_alignbyte(P4, P3, 2);
+        const uint32_t o = dot2u(Q3, p.t6, dot2u(Q2, p.t45, dot2u(Q1, p.t23, dot2u(Q0, p.t01, 32768u))));
+        bt[(2 * m) * TW + x] = (uint8_t)min(e >> 16, 255u);
+        bt[(2 * m + 1) * TW + x] = (uint8_t)min(o >> 16, 255u);
+    }
+}
+
 __global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* __restrict__ frames,
                                                                 FastParams p,
                                                                 uint32_t* __restrict__ cand,
                                                                 uint32_t* __restrict__ counts)
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
-    __shared__ uint32_t sc[SROWS][GX];
+    __shared__ uint32_t sc[SROWS][GX];  // scores; then the blurred tile
     __shared__ uint32_t list[(TW / 2) * (TH / 2)];  // strict 3x3 maxima are never 8-adjacent
+    __shared__ uint32_t hT[TW][HP];     // horizontal blur pass, transposed, row pairs as u16
     __shared__ uint32_t s_cnt, s_base;
     const int f = blockIdx.z;
     load_tile(frames + (long long)f * p.pitch, p, img);
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     score_strip(img, sc, p);
+    if (p.blur) blur_rows(img, hT, p);
     __syncthreads();
     // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter, four
     // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8)
@@ -283,6 +347,20 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* _
         }
     }
     __syncthreads();
+    if (p.blur) {
+        uint8_t* bt = reinterpret_cast<uint8_t*>(&sc[0][0]);
+        blur_cols(hT, bt, p);
+        __syncthreads();
+        // blurred tile -> frame (rows < h, dword columns < blur_stride)
+        uint8_t* dst = p.blur + (long long)f * p.blur_pitch;
+        for (int i = threadIdx.x; i < TH * (TW / 4); i += FAST_THREADS) {
+            const int r = i / (TW / 4), c = i - r * (TW / 4);
+            const int Y = blockIdx.y * TH + r, X = blockIdx.x * TW + 4 * c;
+            if (Y < p.h && X < p.blur_stride)
+                *reinterpret_cast<uint32_t*>(dst + (long long)Y * p.blur_stride + X) =
+                    *reinterpret_cast<const uint32_t*>(bt + r * TW + 4 * c);
+        }
+    }
     if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&counts[f], s_cnt) : 0u;
     __syncthreads();
     uint32_t* out = cand + (long long)f * p.cand_cap;
@@ -615,14 +693,9 @@ struct DescParams {
     int ksize;  // Gaussian taps (<= 1: no blur)
     int taps[2 * KHMAX + 1];
     int dword_ok;
+    int bstride;         // blurred frames (describe_blurred_kernel)
+    long long bpitch;
 };
-
-__device__ __forceinline__ int reflect101(int i, int n)
-{
-    if (n == 1) return 0;
-    while ((unsigned)i >= (unsigned)n) i = i < 0 ? -i : 2 * n - 2 - i;
-    return i;
-}
 
 // Orders one wave's LDS writes before its other lanes' reads (waves of a workgroup work on
 // different keypoints, so no workgroup barrier is needed).
@@ -715,6 +788,50 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
     }
 }
 
+// Descriptor from the frame blurred by fast_nms_kernel: the wave gathers the (2R+1)^2 window
+// with aligned dword loads (kept at byte phase s) into LDS and runs the 256 tests.
+template <int RB>
+__global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
+    const uint8_t* __restrict__ blurred, DescParams p, const uint32_t* __restrict__ xy_in,
+    const uint32_t* __restrict__ n_in, const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
+{
+    constexpr int BDMAX = 2 * RB + 1;
+    constexpr int WP = ((BDMAX + 3 + 3) / 4) * 4;  // row pitch: covers any byte phase
+    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][BDMAX * WP];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int k = blockIdx.x * DESC_WAVES + wave;
+    if (k >= (int)n_in[f]) return;
+    const int R = p.R, bd = 2 * R + 1;
+    const uint32_t v = xy_in[(long long)f * p.out_cap + k];
+    const int cx = (int)(v & 0xFFFFu), cy = (int)(v >> 16);
+    const uint8_t* src = blurred + (long long)f * p.bpitch;
+    uint8_t* w = win[wave];
+    const int x0 = cx - R, y0 = cy - R;
+    const int xa = x0 & ~3, s = x0 - xa;
+    const int nd = (s + bd + 3) >> 2;  // dwords per row
+    for (int i = lane; i < bd * nd; i += kWave) {
+        const int r = i / nd, c = i - r * nd;
+        // keypoints keep the pattern radius from the border (RunByImageBorder), so the clamps
+        // are inert; they only keep reads inside the frame
+        const int gy = min(max(y0 + r, 0), p.h - 1), gx = min(max(xa + 4 * c, 0), p.bstride - 4);
+        *reinterpret_cast<uint32_t*>(w + r * WP + 4 * c) =
+            *reinterpret_cast<const uint32_t*>(src + (long long)gy * p.bstride + gx);
+    }
+    wave_lds_sync();
+    const uint8_t* wb = w + s;
+    const char4* pat = reinterpret_cast<const char4*>(pattern);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
+#pragma unroll
+    for (int chunk = 0; chunk < 4; chunk++) {
+        const char4 e = pat[chunk * kWave + lane];  // (x0, y0, x1, y1) of bit 64*chunk + lane
+        const int t0 = wb[(R + e.y) * WP + R + e.x];
+        const int t1 = wb[(R + e.w) * WP + R + e.z];
+        const unsigned long long m = __ballot(t0 < t1);
+        if (lane == 0) dst[chunk] = m;
+    }
+}
+
 __global__ void synth_frames_kernel(uint8_t* __restrict__ out, int w, int h, long long pitch,
                                     unsigned t0, unsigned long long seed)
 {
@@ -748,7 +865,7 @@ struct OrbDetector {
     int device = 0;
     int taps[2 * KHMAX + 1] = {0};
     int R = 7;
-    DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n;
+    DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n, blurred;
 };
 
 namespace {
@@ -809,6 +926,24 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
     if (h <= 2 * border || w <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
     fp.cand_cap = candCap;
     fp.dword_ok = (w % 4 == 0) && (stride % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)d_frames % 4 == 0);
+    // the default 7-tap Gaussian is fused into the FAST pass (the tile is already in LDS);
+    // other kernel sizes blur inside the descriptor windows instead
+    const bool fused_blur = cap > 0 && s.gaussian_kernel_size == 7;
+    const int bstride = (w + 3) & ~3;
+    const long long bpitch = (long long)bstride * h;
+    if (fused_blur) {
+        if ((r = o->blurred.reserve((size_t)batch * bpitch)) != MAGE_OK) return r;
+        const int* k = o->taps;
+        fp.blur = o->blurred.as<uint8_t>();
+        fp.blur_stride = bstride;
+        fp.blur_pitch = bpitch;
+        fp.t0 = (uint32_t)k[0] | ((uint32_t)k[1] << 8) | ((uint32_t)k[2] << 16) | ((uint32_t)k[3] << 24);
+        fp.t1 = (uint32_t)k[4] | ((uint32_t)k[5] << 8) | ((uint32_t)k[6] << 16);
+        fp.t01 = (uint32_t)k[0] | ((uint32_t)k[1] << 16);
+        fp.t23 = (uint32_t)k[2] | ((uint32_t)k[3] << 16);
+        fp.t45 = (uint32_t)k[4] | ((uint32_t)k[5] << 16);
+        fp.t6 = (uint32_t)k[6];
+    }
     dim3 g1((w + TW - 1) / TW, (h + TH - 1) / TH, batch);
     {
         KernelTimer _kt("orb.fast_nms", st);
@@ -851,12 +986,21 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         dp.ksize = (int)s.gaussian_kernel_size;
         for (int i = 0; i < 2 * KHMAX + 1; i++) dp.taps[i] = o->taps[i];
         dp.dword_ok = (stride % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)d_frames % 4 == 0);
+        dp.bstride = bstride;
+        dp.bpitch = bpitch;
         dim3 g3((cap + DESC_WAVES - 1) / DESC_WAVES, batch);
         {
             KernelTimer _kt("orb.describe", st);
-            auto kern = dp.R <= 7 ? describe_kernel<7> : (dp.R <= 13 ? describe_kernel<13> : describe_kernel<RMAX>);
-            hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, d_frames, dp,
-                               o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
+            if (fused_blur) {
+                auto kern = dp.R <= 7 ? describe_blurred_kernel<7>
+                                      : (dp.R <= 13 ? describe_blurred_kernel<13> : describe_blurred_kernel<RMAX>);
+                hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, o->blurred.as<uint8_t>(), dp,
+                                   o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
+            } else {
+                auto kern = dp.R <= 7 ? describe_kernel<7> : (dp.R <= 13 ? describe_kernel<13> : describe_kernel<RMAX>);
+                hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, d_frames, dp,
+                                   o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
+            }
         }
         MAGE_HIP(hipGetLastError());
     }
