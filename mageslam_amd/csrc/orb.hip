@@ -114,36 +114,38 @@ __host__ __device__ constexpr int ring_dy(int k)
 // contiguous ring pixels are all darker than v - t" (the segment test of FAST_t<16>,
 // OpenCVModified.cpp:1415-1479) is exactly A > t, "all brighter than v + t" is -B > t, and
 // cornerScore<16> (:927-1071; its scalar and SSE2 branches agree on corners) is max(A, -B) - 1.
-// 9-arc extrema are min3/max3 of three 3-arc extrema; every value is an integer in [-255, 255],
-// exact in f16, so the packed f16 min3/max3 give the integer result.
+// Since min over an arc of (v - x) = v - max over the arc of x, A = v - min_k X9[k] and
+// B = v - max_k N9[k] with X9 / N9 the 9-arc max / min of the ring values themselves: 9-arc
+// extrema are min3/max3 of three 3-arc extrema.  Every value is an integer (offset 1024), exact
+// in f16, so the packed f16 min3/max3 give the integer result.
 template <int P>
 __device__ __forceinline__ h2 fast_raw2(const h2 (&w)[7][9])
 {
     const h2 v = w[3][4 + 2 * P - 1];
-    h2 d[16];
+    h2 x[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - w[ring_dy(k) + 3][4 + 2 * P + ring_dx(k) - 1];
-    h2 m3[16], x3[16];
+    for (int k = 0; k < 16; k++) x[k] = w[ring_dy(k) + 3][4 + 2 * P + ring_dx(k) - 1];
+    h2 n3[16], x3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        m3[k] = min3h(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
-        x3[k] = max3h(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+        n3[k] = min3h(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
+        x3[k] = max3h(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
     }
-    h2 m9[16], x9[16];
+    h2 n9[16], x9[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        m9[k] = min3h(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]);
+        n9[k] = min3h(n3[k], n3[(k + 3) & 15], n3[(k + 6) & 15]);
         x9[k] = max3h(x3[k], x3[(k + 3) & 15], x3[(k + 6) & 15]);
     }
-    h2 a = max3h(m9[0], m9[1], m9[2]), b = min3h(x9[0], x9[1], x9[2]);
+    h2 lo = min3h(x9[0], x9[1], x9[2]), hi = max3h(n9[0], n9[1], n9[2]);
 #pragma unroll
     for (int k = 3; k < 15; k += 2) {
-        a = max3h(a, m9[k], m9[k + 1]);
-        b = min3h(b, x9[k], x9[k + 1]);
+        lo = min3h(lo, x9[k], x9[k + 1]);
+        hi = max3h(hi, n9[k], n9[k + 1]);
     }
-    a = __builtin_elementwise_maximum(a, m9[15]);
-    b = __builtin_elementwise_minimum(b, x9[15]);
-    return __builtin_elementwise_maximum(a, -b);
+    lo = __builtin_elementwise_minimum(lo, x9[15]);  // A = v - lo
+    hi = __builtin_elementwise_maximum(hi, n9[15]);  // -B = hi - v
+    return __builtin_elementwise_maximum(v - lo, hi - v);
 }
 
 // Score bytes of two pixels from their raw scores: raw > t ? raw - 1 : 0, as 1024 + score.
@@ -260,19 +262,26 @@ __device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c)
     return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), c, false);
 }
 
-__device__ __forceinline__ void blur_cols(const uint32_t (*hT)[HP], uint8_t* bt, const FastParams& p)
+__device__ __forceinline__ void blur_cols(const uint32_t (*hT)[HP], uint32_t* bt, const FastParams& p)
 {
-    // item: column x, output rows 2m, 2m + 1 (row-pass rows 2m .. 2m + 7)
-    for (int it = threadIdx.x; it < TW * (TH / 2); it += FAST_THREADS) {
-        const int m = it % (TH / 2), x = it / (TH / 2);
-        const uint32_t* c = &hT[x][m];
-        const uint32_t P0 = c[0], P1 = c[1], P2 = c[2], P3 = c[3], P4 = c[4];
-        const uint32_t e = dot2u(P3, p.t6, dot2u(P2, p.t45, dot2u(P1, p.t23, dot2u(P0, p.t01, 32768u))));
-        const uint32_t Q0 = __builtin_amdgcn_alignbyte(P1, P0, 2), Q1 = __builtin_amdgcn_alignbyte(P2, P1, 2);
-        const uint32_t Q2 = __builtin_amdgcn_alignbyte(P3, P2, 2), Q3 = __builtin_amdgcn_alignbyte(P4, P3, 2);
-        const uint32_t o = dot2u(Q3, p.t6, dot2u(Q2, p.t45, dot2u(Q1, p.t23, dot2u(Q0, p.t01, 32768u))));
-        bt[(2 * m) * TW + x] = (uint8_t)min(e >> 16, 255u);
-        bt[(2 * m + 1) * TW + x] = (uint8_t)min(o >> 16, 255u);
+    // item: columns 4g .. 4g + 3, output rows 2m, 2m + 1 (row-pass rows 2m .. 2m + 7); the four
+    // columns' bytes of each row are stored as one dword
+    for (int it = threadIdx.x; it < (TW / 4) * (TH / 2); it += FAST_THREADS) {
+        const int m = it % (TH / 2), g = it / (TH / 2);
+        uint32_t ev = 0, od = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t* c = &hT[4 * g + j][m];
+            const uint32_t P0 = c[0], P1 = c[1], P2 = c[2], P3 = c[3], P4 = c[4];
+            const uint32_t e = dot2u(P3, p.t6, dot2u(P2, p.t45, dot2u(P1, p.t23, dot2u(P0, p.t01, 32768u))));
+            const uint32_t Q0 = __builtin_amdgcn_alignbyte(P1, P0, 2), Q1 = __builtin_amdgcn_alignbyte(P2, P1, 2);
+            const uint32_t Q2 = __builtin_amdgcn_alignbyte(P3, P2, 2), Q3 = __builtin_amdgcn_alignbyte(P4, P3, 2);
+            const uint32_t o = dot2u(Q3, p.t6, dot2u(Q2, p.t45, dot2u(Q1, p.t23, dot2u(Q0, p.t01, 32768u))));
+            ev |= min(e >> 16, 255u) << (8 * j);
+            od |= min(o >> 16, 255u) << (8 * j);
+        }
+        bt[(2 * m) * (TW / 4) + g] = ev;
+        bt[(2 * m + 1) * (TW / 4) + g] = od;
     }
 }
 
@@ -294,61 +303,65 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* _
     if (p.blur) blur_rows(img, hT, p);
     __syncthreads();
     // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter, four
-    // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8)
+    // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8).  Scores
+    // are split into even / odd pixels as f16 lanes (1024 + s); per score row the left / right
+    // neighbour-aligned copies and the 3-wide maximum are formed once and rolled down, so a
+    // pixel's 8-neighbour maximum is max(H3(up), H3(down), left, right).
     {
         constexpr int OG = TW / 4;  // 30 output groups per row
         const int og = threadIdx.x % 32, chunk = threadIdx.x / 32;
         if (og < OG) {
             const int X0 = blockIdx.x * TW + 4 * og;
             const int oy0 = 8 * chunk, oy1 = min(oy0 + 8, TH);
-            auto load3 = [&](int srow, uint32_t& l, uint32_t& c, uint32_t& r) {
-                l = sc[srow][og];
-                c = sc[srow][og + 1];
-                r = sc[srow][og + 2];
+            auto even = [](uint32_t d) { return as_h2(__builtin_amdgcn_perm(d, 0x64646464u, 0x00060004u)); };
+            auto odd = [](uint32_t d) { return as_h2(__builtin_amdgcn_perm(d, 0x64646464u, 0x00070005u)); };
+            struct RowV {
+                h2 ce, co, le, lo, re, ro, he, ho;  // centre, left, right, 3-wide max (even, odd)
+                uint32_t c;
             };
-            uint32_t ul, uc, ur, ml, mc, mr;
-            load3(oy0, ul, uc, ur);
-            load3(oy0 + 1, ml, mc, mr);
+            auto load_row = [&](int srow) {
+                RowV v;
+                const uint32_t l = sc[srow][og], c = sc[srow][og + 1], r = sc[srow][og + 2];
+                const uint32_t L = __builtin_amdgcn_alignbyte(c, l, 3), R = __builtin_amdgcn_alignbyte(r, c, 1);
+                v.c = c;
+                v.ce = even(c);
+                v.co = odd(c);
+                v.le = even(L);
+                v.lo = odd(L);
+                v.re = even(R);
+                v.ro = odd(R);
+                v.he = max3h(v.le, v.ce, v.re);
+                v.ho = max3h(v.lo, v.co, v.ro);
+                return v;
+            };
+            RowV U = load_row(oy0), M = load_row(oy0 + 1);
             for (int oy = oy0; oy < oy1; oy++) {
-                uint32_t dl, dc, dr;
-                load3(oy + 2, dl, dc, dr);
-                if (mc != 0) {
-                    // neighbour bytes aligned to the four centre pixels
-                    const uint32_t nb[8] = {__builtin_amdgcn_alignbyte(uc, ul, 3), uc, __builtin_amdgcn_alignbyte(ur, uc, 1),
-                                            __builtin_amdgcn_alignbyte(mc, ml, 3), __builtin_amdgcn_alignbyte(mr, mc, 1),
-                                            __builtin_amdgcn_alignbyte(dc, dl, 3), dc, __builtin_amdgcn_alignbyte(dr, dc, 1)};
-                    // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) as f16 lanes
-                    auto even = [](uint32_t d) { return as_h2(__builtin_amdgcn_perm(d, 0x64646464u, 0x00060004u)); };
-                    auto odd = [](uint32_t d) { return as_h2(__builtin_amdgcn_perm(d, 0x64646464u, 0x00070005u)); };
-                    const h2 ev = max3h(max3h(even(nb[0]), even(nb[1]), even(nb[2])), max3h(even(nb[3]), even(nb[4]), even(nb[5])),
-                               __builtin_elementwise_maximum(even(nb[6]), even(nb[7])));
-                    const h2 od = max3h(max3h(odd(nb[0]), odd(nb[1]), odd(nb[2])), max3h(odd(nb[3]), odd(nb[4]), odd(nb[5])),
-                               __builtin_elementwise_maximum(odd(nb[6]), odd(nb[7])));
-                    const h2 ge = even(mc) - ev, go = odd(mc) - od;  // > 0: strict maximum
+                const RowV D = load_row(oy + 2);
+                const h2 ge = M.ce - __builtin_elementwise_maximum(max3h(U.he, D.he, M.le), M.re);
+                const h2 go = M.co - __builtin_elementwise_maximum(max3h(U.ho, D.ho, M.lo), M.ro);
+                const h2 zero = {(_Float16)0.0f, (_Float16)0.0f};
+                // > 0: strict maximum (a zero score never is: its neighbours are >= 0)
+                if ((as_u32(__builtin_elementwise_maximum(ge, zero)) | as_u32(__builtin_elementwise_maximum(go, zero))) != 0u) {
                     const int Y = blockIdx.y * TH + oy;
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         const float g = (float)((q & 1) ? go[q >> 1] : ge[q >> 1]);
                         const int X = X0 + q;
                         if (g > 0.0f && X >= p.xlo && X <= p.xhi && Y >= p.ylo && Y <= p.yhi) {
-                            const uint32_t s = (mc >> (8 * q)) & 0xFFu;
+                            const uint32_t sv = (M.c >> (8 * q)) & 0xFFu;
                             const uint32_t slot = atomicAdd(&s_cnt, 1u);
-                            list[slot] = ((uint32_t)Y << 20) | ((uint32_t)X << 8) | s;
+                            list[slot] = ((uint32_t)Y << 20) | ((uint32_t)X << 8) | sv;
                         }
                     }
                 }
-                ul = ml;
-                uc = mc;
-                ur = mr;
-                ml = dl;
-                mc = dc;
-                mr = dr;
+                U = M;
+                M = D;
             }
         }
     }
     __syncthreads();
     if (p.blur) {
-        uint8_t* bt = reinterpret_cast<uint8_t*>(&sc[0][0]);
+        uint32_t* bt = &sc[0][0];
         blur_cols(hT, bt, p);
         __syncthreads();
         // blurred tile -> frame (rows < h, dword columns < blur_stride)
@@ -357,8 +370,7 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* _
             const int r = i / (TW / 4), c = i - r * (TW / 4);
             const int Y = blockIdx.y * TH + r, X = blockIdx.x * TW + 4 * c;
             if (Y < p.h && X < p.blur_stride)
-                *reinterpret_cast<uint32_t*>(dst + (long long)Y * p.blur_stride + X) =
-                    *reinterpret_cast<const uint32_t*>(bt + r * TW + 4 * c);
+                *reinterpret_cast<uint32_t*>(dst + (long long)Y * p.blur_stride + X) = bt[r * (TW / 4) + c];
         }
     }
     if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&counts[f], s_cnt) : 0u;
