@@ -92,7 +92,9 @@ __device__ __forceinline__ bool accept(int m1, int m2, int maxDist, int minDiff)
     return true;
 }
 
-// 16 descriptor bits -> 16 bytes of s(bit) = +1 (0x01) / -1 (0xFF); byte b <-> bit b.
+// 16 descriptor bits -> 16 bytes of c * s(bit), s = +1 / -1; byte b <-> bit b.  TAB holds the
+// two byte values (+c in byte 0, -c in byte 1) that v_perm_b32 selects from.
+template <uint32_t TAB>
 __device__ __forceinline__ v4i expand16(uint32_t w)
 {
     v4i r;
@@ -100,7 +102,7 @@ __device__ __forceinline__ v4i expand16(uint32_t w)
     for (int q = 0; q < 4; q++) {
         const uint32_t t = (w >> (4 * q)) & 0xFu;
         const uint32_t x = (t * 0x00204081u) & 0x01010101u;  // bit i -> byte i
-        r[q] = (int)__builtin_amdgcn_perm(0u, 0x0000FF01u, x);
+        r[q] = (int)__builtin_amdgcn_perm(0u, TAB, x);
     }
     return r;
 }
@@ -123,71 +125,181 @@ __device__ __forceinline__ void load_frags(v4i (&b)[8], const v4i* __restrict__ 
     for (int s = 0; s < 8; s++) b[s] = bt[s * kWave + lane];
 }
 
-// Fold the D block of row tile rt (of the wave's RT) x one 32-column B tile into the row top-2
-// and into the column partial (c1, c2), which holds local keys (D << 6 | 63 - wave row).
-// MASK: some rows or columns are padding.
-template <bool MASK>
-__device__ __forceinline__ void fold(const v16i& acc, int rt, int lane, int colbase, int nb, int rowbase, int na,
-                                     int (&r1)[16], int (&r2)[16], int& c1, int& c2)
-{
-    const int h = lane >> 5;
-    const int j = colbase + (lane & 31);
-    const int jc = 0x7FFF - j;
-#pragma unroll
-    for (int g = 0; g < 16; g++) {
-        const int D = acc[g];
-        if (MAGE_MATCH_ABLATE == 4) {
-            r1[g] = max(r1[g], D);
-            continue;
-        }
-        int kr = (D << 15) | jc;
-        int kc = (D << 6) | (63 - (rt * 32 + acc_row(g)));
-        if (MASK) {
-            if (j >= nb) kr = NONE;
-            if (rowbase + rt * 32 + acc_row(g) + 4 * h >= na) kc = NONE;
-        }
-        if (MAGE_MATCH_ABLATE != 2) push2(r1[g], r2[g], kr);
-        if (MAGE_MATCH_ABLATE != 1) push2(c1, c2, kc);
-    }
-}
-
-// Column partial of one B tile -> global keys (D << 15 | 0x7FFF - i), merged with the partner
+// Column partial of one B tile, as global keys (D << 15 | 0x7FFF - i), merged with the partner
 // half-wave, then into the workgroup's column top-2 with two LDS atomicMax (no CAS loop: a key
 // that loses, or is displaced from, the best slot is pushed into the second slot).
-__device__ __forceinline__ void flush_cols(int c1, int c2, int lane, int colbase, int nb, int rowbase,
-                                           int* colM1, int* colM2)
+__device__ __forceinline__ void flush_global(int c1, int c2, int lane, int colbase, int nb, int* colM1, int* colM2)
 {
-    if (MAGE_MATCH_ABLATE == 1 || MAGE_MATCH_ABLATE == 4) return;
-    const int h = lane >> 5;
-    const int j = colbase + (lane & 31);
-    const int ib = rowbase + 4 * h + 63;
-    if (c1 != NONE) c1 = ((c1 >> 6) << 15) | (0x7FFF - (ib - (c1 & 63)));
-    if (c2 != NONE) c2 = ((c2 >> 6) << 15) | (0x7FFF - (ib - (c2 & 63)));
     merge2(c1, c2, __shfl_xor(c1, 32), __shfl_xor(c2, 32));
-    if (h == 0 && j < nb && c1 != NONE) {
+    const int j = colbase + (lane & 31);
+    if ((lane >> 5) == 0 && j < nb && c1 != NONE) {
         const int old = atomicMax(&colM1[j], c1);
         atomicMax(&colM2[j], old > c1 ? c1 : max(old, c2));
     }
 }
 
-// Padding rows and columns have zero operands, so D = 0 (d = 128) there: such a key can neither
-// be accepted (d0 <= maxDist) nor hide an in-radius second best while maxDist < 128, so the
-// kernel for those radii (every practical one) folds without masks; PADMASK covers the rest.
+// 32-bit keys: operands s = +-1, D = 256 - 2d.  Row keys (D << 15 | 0x7FFF - j); column
+// partials hold local keys (D << 6 | 63 - wave row).  Any nb <= NMAX.  PADMASK: padding rows and
+// columns are masked (needed only when maxDist >= 128, see fold_any).
 template <bool PADMASK>
-__device__ __forceinline__ void fold_any(const v16i& acc, int rt, int lane, int colbase, int nb, int rowbase,
-                                         int na, int (&r1)[16], int (&r2)[16], int& c1, int& c2)
-{
-    if (PADMASK && (colbase + 32 > nb || rowbase + RT * 32 > na))
-        fold<true>(acc, rt, lane, colbase, nb, rowbase, na, r1, r2, c1, c2);
-    else
-        fold<false>(acc, rt, lane, colbase, nb, rowbase, na, r1, r2, c1, c2);
-}
+struct Keys32 {
+    static constexpr uint32_t ATAB = 0x0000FF01u, BTAB = 0x0000FF01u;
+    struct Rows {
+        int r1[RT][16], r2[RT][16];
+    };
+    struct Part {
+        int c1, c2;
+    };
+    static __device__ __forceinline__ void init(Rows& r)
+    {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int g = 0; g < 16; g++) r.r1[rt][g] = r.r2[rt][g] = NONE;
+    }
+    static __device__ __forceinline__ void reset(Part& c) { c.c1 = c.c2 = NONE; }
+
+    template <bool MASK>
+    static __device__ __forceinline__ void fold_m(const v16i& acc, int rt, int lane, int colbase, int nb, int rowbase,
+                                                  int na, Rows& R, Part& C)
+    {
+        const int h = lane >> 5;
+        const int j = colbase + (lane & 31);
+        const int jc = 0x7FFF - j;
+#pragma unroll
+        for (int g = 0; g < 16; g++) {
+            const int D = acc[g];
+            if (MAGE_MATCH_ABLATE == 4) {
+                R.r1[rt][g] = max(R.r1[rt][g], D);
+                continue;
+            }
+            int kr = (D << 15) | jc;
+            int kc = (D << 6) | (63 - (rt * 32 + acc_row(g)));
+            if (MASK) {
+                if (j >= nb) kr = NONE;
+                if (rowbase + rt * 32 + acc_row(g) + 4 * h >= na) kc = NONE;
+            }
+            if (MAGE_MATCH_ABLATE != 2) push2(R.r1[rt][g], R.r2[rt][g], kr);
+            if (MAGE_MATCH_ABLATE != 1) push2(C.c1, C.c2, kc);
+        }
+    }
+    // Padding rows and columns have zero operands, so D = 0 (d = 128) there: such a key can
+    // neither be accepted (d0 <= maxDist) nor hide an in-radius second best while maxDist <
+    // 128, so for those radii (every practical one) the fold needs no masks.
+    static __device__ __forceinline__ void fold(const v16i& acc, int rt, int lane, int colbase, int nb, int rowbase,
+                                                int na, Rows& R, Part& C)
+    {
+        if (PADMASK && (colbase + 32 > nb || rowbase + RT * 32 > na))
+            fold_m<true>(acc, rt, lane, colbase, nb, rowbase, na, R, C);
+        else
+            fold_m<false>(acc, rt, lane, colbase, nb, rowbase, na, R, C);
+    }
+    static __device__ __forceinline__ void flush(const Part& C, int lane, int colbase, int nb, int rowbase,
+                                                 int* colM1, int* colM2)
+    {
+        if (MAGE_MATCH_ABLATE == 1 || MAGE_MATCH_ABLATE == 4) return;
+        const int ib = rowbase + 4 * (lane >> 5) + 63;
+        int c1 = C.c1, c2 = C.c2;
+        if (c1 != NONE) c1 = ((c1 >> 6) << 15) | (0x7FFF - (ib - (c1 & 63)));
+        if (c2 != NONE) c2 = ((c2 >> 6) << 15) | (0x7FFF - (ib - (c2 & 63)));
+        flush_global(c1, c2, lane, colbase, nb, colM1, colM2);
+    }
+    // row state q = rt * 16 + g as global keys
+    static __device__ __forceinline__ void export_rows(const Rows& R, int lane, int (&s1)[RT * 16], int (&s2)[RT * 16])
+    {
+#pragma unroll
+        for (int q = 0; q < RT * 16; q++) {
+            s1[q] = R.r1[q >> 4][q & 15];
+            s2[q] = R.r2[q >> 4][q & 15];
+        }
+    }
+};
+
+// Packed 16-bit keys, two accumulator registers per VGPR: operands +-8 (A) and +-4 (B), so the
+// MFMA yields 64 (128 - d) with six zero low bits.  Row keys ((128 - d) << 6 | 63 - tile),
+// column keys ((128 - d) << 6 | 63 - wave row); both top-2 updates are v_pk_max_i16 /
+// v_pk_min_i16 on two elements at once.  Requires nb <= 2048 (64 tiles) and maxDist < 128.
+struct Keys16 {
+    static constexpr uint32_t ATAB = 0x0000F808u, BTAB = 0x0000FC04u;
+    static constexpr uint32_t NONE2 = 0x80008000u;
+    struct Rows {
+        uint32_t r1[RT][8], r2[RT][8];
+    };
+    struct Part {
+        uint32_t c1, c2;
+    };
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    static __device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b)
+    {
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
+    }
+    static __device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b)
+    {
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
+    }
+    static __device__ __forceinline__ void init(Rows& r)
+    {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r.r1[rt][q] = r.r2[rt][q] = NONE2;
+    }
+    static __device__ __forceinline__ void reset(Part& c) { c.c1 = c.c2 = NONE2; }
+    static __device__ __forceinline__ void fold(const v16i& acc, int rt, int lane, int colbase, int nb, int rowbase,
+                                                int na, Rows& R, Part& C)
+    {
+        const uint32_t tpair = (uint32_t)(63 - (colbase >> 5)) * 0x00010001u;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t P = __builtin_amdgcn_perm((uint32_t)acc[2 * q + 1], (uint32_t)acc[2 * q], 0x05040100u);
+            const uint32_t kr = P | tpair;
+            R.r2[rt][q] = pmax(R.r2[rt][q], pmin(R.r1[rt][q], kr));
+            R.r1[rt][q] = pmax(R.r1[rt][q], kr);
+            const uint32_t rc = (uint32_t)(63 - (rt * 32 + acc_row(2 * q))) |
+                                ((uint32_t)(63 - (rt * 32 + acc_row(2 * q + 1))) << 16);
+            const uint32_t kc = P | rc;
+            C.c2 = pmax(C.c2, pmin(C.c1, kc));
+            C.c1 = pmax(C.c1, kc);
+        }
+    }
+    static __device__ __forceinline__ int lo16(uint32_t v) { return (int)(short)(v & 0xFFFFu); }
+    static __device__ __forceinline__ int hi16(uint32_t v) { return (int)v >> 16; }
+    static __device__ __forceinline__ void flush(const Part& C, int lane, int colbase, int nb, int rowbase,
+                                                 int* colM1, int* colM2)
+    {
+        // merge the even / odd register halves, then local -> global keys
+        int m1 = lo16(C.c1), m2 = lo16(C.c2);
+        merge2(m1, m2, hi16(C.c1), hi16(C.c2));
+        const int ib = rowbase + 4 * (lane >> 5) + 63;
+        int c1 = m1 == -32768 ? NONE : ((m1 >> 6) << 16) | (0x7FFF - (ib - (m1 & 63)));
+        int c2 = m2 == -32768 ? NONE : ((m2 >> 6) << 16) | (0x7FFF - (ib - (m2 & 63)));
+        flush_global(c1, c2, lane, colbase, nb, colM1, colM2);
+    }
+    static __device__ __forceinline__ int row_global(int k, int lane)
+    {
+        if (k == -32768) return NONE;
+        const int j = (63 - (k & 63)) * 32 + (lane & 31);
+        return ((k >> 6) << 16) | (0x7FFF - j);
+    }
+    static __device__ __forceinline__ void export_rows(const Rows& R, int lane, int (&s1)[RT * 16], int (&s2)[RT * 16])
+    {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                s1[rt * 16 + 2 * q] = row_global(lo16(R.r1[rt][q]), lane);
+                s1[rt * 16 + 2 * q + 1] = row_global(hi16(R.r1[rt][q]), lane);
+                s2[rt * 16 + 2 * q] = row_global(lo16(R.r2[rt][q]), lane);
+                s2[rt * 16 + 2 * q + 1] = row_global(hi16(R.r2[rt][q]), lane);
+            }
+    }
+};
 
 // All row passes of one (A, B) pair.  RES: the packed B descriptors are resident in LDS (Bres),
 // so the stage loop issues no global loads (hipcc drains vmcnt(0) at the first use of any
 // global-load result, which would expose a full L2/HBM round trip per stage); otherwise each
 // stage's B words are fetched from global one stage ahead (nb > NRES only).
-template <bool PADMASK, bool RES>
+template <class K, bool RES>
 __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, const uint32_t* __restrict__ Bw,
                                            const uint32_t* Bres, int na, int nb,
                                            v4i (*stage)[SC / 32][8][kWave], int* colM1, int* colM2,
@@ -204,15 +316,16 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
     auto fill = [&](int buf, int st, uint32_t dw) {
         const bool ok = st * SC + fc < nb;  // padding columns: zero operands
         const v4i zero = {0, 0, 0, 0};
-        stage[buf][fc >> 5][fs][fc & 31] = ok ? expand16(dw & 0xFFFFu) : zero;
-        stage[buf][fc >> 5][fs][32 + (fc & 31)] = ok ? expand16(dw >> 16) : zero;
+        stage[buf][fc >> 5][fs][fc & 31] = ok ? expand16<K::BTAB>(dw & 0xFFFFu) : zero;
+        stage[buf][fc >> 5][fs][32 + (fc & 31)] = ok ? expand16<K::BTAB>(dw >> 16) : zero;
     };
 
     for (int pb = 0; pb < na; pb += ROWS) {
         const int rowbase = pb + wave * (RT * 32);
         const bool active = rowbase < na;
         v4i a[RT][8];
-        int r1[RT][16], r2[RT][16];
+        typename K::Rows R;
+        K::init(R);
 #pragma unroll
         for (int rt = 0; rt < RT; rt++) {
             const int i = rowbase + rt * 32 + (lane & 31);
@@ -222,13 +335,8 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
             for (int s = 0; s < 8; s++) dw[s] = Aw[8 * ic + s];
 #pragma unroll
             for (int s = 0; s < 8; s++) {
-                a[rt][s] = expand16((lane >> 5) ? (dw[s] >> 16) : (dw[s] & 0xFFFFu));
+                a[rt][s] = expand16<K::ATAB>((lane >> 5) ? (dw[s] >> 16) : (dw[s] & 0xFFFFu));
                 if (i >= na) a[rt][s] = v4i{0, 0, 0, 0};  // padding rows: zero operands
-            }
-#pragma unroll
-            for (int g = 0; g < 16; g++) {
-                r1[rt][g] = NONE;
-                r2[rt][g] = NONE;
             }
         }
         {
@@ -244,7 +352,9 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
         v4i bf[8];
         load_frags(bf, &stage[0][0][0][0], lane);
         v16i acc1;
-        int cbp = -1, p1 = NONE, p2 = NONE;
+        int cbp = -1;
+        typename K::Part C;
+        K::reset(C);
         for (int st = 0; st < nstages; st++) {
             const int buf = st % NBUF;
             uint32_t nxt = 0;
@@ -256,17 +366,16 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
                     if (colbase >= nb) break;
                     const v16i acc0 = tile_mfma(a[0], bf);
                     if (cbp >= 0) {
-                        fold_any<PADMASK>(acc1, 1, lane, cbp, nb, rowbase, na, r1[1], r2[1], p1, p2);
-                        flush_cols(p1, p2, lane, cbp, nb, rowbase, colM1, colM2);
+                        K::fold(acc1, 1, lane, cbp, nb, rowbase, na, R, C);
+                        K::flush(C, lane, cbp, nb, rowbase, colM1, colM2);
                     }
                     acc1 = tile_mfma(a[1], bf);
                     if (ct + 1 < SC / 32 && colbase + 32 < nb)
                         load_frags(bf, &stage[buf][ct + 1][0][0], lane);
                     else if (st + 1 < nstages)
                         load_frags(bf, &stage[(st + 1) % NBUF][0][0][0], lane);
-                    p1 = NONE;
-                    p2 = NONE;
-                    fold_any<PADMASK>(acc0, 0, lane, colbase, nb, rowbase, na, r1[0], r2[0], p1, p2);
+                    K::reset(C);
+                    K::fold(acc0, 0, lane, colbase, nb, rowbase, na, R, C);
                     cbp = colbase;
                 }
             }
@@ -275,17 +384,13 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
         }
         if (active) {
             if (cbp >= 0) {
-                fold_any<PADMASK>(acc1, 1, lane, cbp, nb, rowbase, na, r1[1], r2[1], p1, p2);
-                flush_cols(p1, p2, lane, cbp, nb, rowbase, colM1, colM2);
+                K::fold(acc1, 1, lane, cbp, nb, rowbase, na, R, C);
+                K::flush(C, lane, cbp, nb, rowbase, colM1, colM2);
             }
             // reduce-scatter the 32 row states (row tile q >> 4, register q & 15) over the 32
             // lanes of each half: lane c ends with state q = c.
             int s1[RT * 16], s2[RT * 16];
-#pragma unroll
-            for (int q = 0; q < RT * 16; q++) {
-                s1[q] = r1[q >> 4][q & 15];
-                s2[q] = r2[q >> 4][q & 15];
-            }
+            K::export_rows(R, lane, s1, s2);
 #pragma unroll
             for (int m = 16, n = 32; m >= 1; m >>= 1, n >>= 1) {
                 const bool up = (lane & m) != 0;
@@ -350,9 +455,12 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
             const uint4* src = reinterpret_cast<const uint4*>(Bw);
             for (int k = tid; k < 2 * nb; k += MT) reinterpret_cast<uint4*>(pool)[k] = src[k];
             __syncthreads();
-            row_passes<PADMASK, true>(Aw, Bw, pool, na, nb, stage, colM1, colM2, rows);
+            if (!PADMASK && nb <= 64 * 32)
+                row_passes<Keys16, true>(Aw, Bw, pool, na, nb, stage, colM1, colM2, rows);
+            else
+                row_passes<Keys32<PADMASK>, true>(Aw, Bw, pool, na, nb, stage, colM1, colM2, rows);
         } else {
-            row_passes<PADMASK, false>(Aw, Bw, pool, na, nb, stage, colM1, colM2, rows);
+            row_passes<Keys32<PADMASK>, false>(Aw, Bw, pool, na, nb, stage, colM1, colM2, rows);
         }
     }
     __syncthreads();

@@ -808,8 +808,10 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     const uint32_t* __restrict__ n_in, const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
 {
     constexpr int BDMAX = 2 * RB + 1;
-    constexpr int WP = ((BDMAX + 3 + 3) / 4) * 4;  // row pitch: covers any byte phase
-    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][BDMAX * WP];
+    constexpr int ND = (BDMAX + 3 + 3) / 4;  // dwords per window row: covers any byte phase
+    constexpr int WP = 4 * ND;
+    constexpr int RPI = kWave / ND;          // window rows per load instruction
+    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][(BDMAX + RPI) * WP];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int k = blockIdx.x * DESC_WAVES + wave;
@@ -821,14 +823,20 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     uint8_t* w = win[wave];
     const int x0 = cx - R, y0 = cy - R;
     const int xa = x0 & ~3, s = x0 - xa;
-    const int nd = (s + bd + 3) >> 2;  // dwords per row
-    for (int i = lane; i < bd * nd; i += kWave) {
-        const int r = i / nd, c = i - r * nd;
-        // keypoints keep the pattern radius from the border (RunByImageBorder), so the clamps
-        // are inert; they only keep reads inside the frame
-        const int gy = min(max(y0 + r, 0), p.h - 1), gx = min(max(xa + 4 * c, 0), p.bstride - 4);
-        *reinterpret_cast<uint32_t*>(w + r * WP + 4 * c) =
-            *reinterpret_cast<const uint32_t*>(src + (long long)gy * p.bstride + gx);
+    // lane -> (row lane / ND, dword lane % ND); keypoints keep the pattern radius from the
+    // border (RunByImageBorder), so the clamps are inert: they only keep reads inside the frame
+    const int lr = lane / ND, lc = lane - lr * ND;
+    const int gx = min(max(xa + 4 * lc, 0), p.bstride - 4);
+    if (lr < RPI) {
+#pragma unroll
+        for (int r0 = 0; r0 < BDMAX; r0 += RPI) {
+            const int r = r0 + lr;
+            if (r < bd) {
+                const int gy = min(max(y0 + r, 0), p.h - 1);
+                *reinterpret_cast<uint32_t*>(w + r * WP + 4 * lc) =
+                    *reinterpret_cast<const uint32_t*>(src + (long long)gy * p.bstride + gx);
+            }
+        }
     }
     wave_lds_sync();
     const uint8_t* wb = w + s;
