@@ -800,8 +800,11 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
     }
 }
 
-// Descriptor from the frame blurred by fast_nms_kernel: the wave gathers the (2R+1)^2 window
-// with aligned dword loads (kept at byte phase s) into LDS and runs the 256 tests.
+// Descriptors from the frame blurred by fast_nms_kernel: each wave handles KPW keypoints; it
+// issues the window loads of all of them (aligned dwords, rows kept at byte phase s) before
+// the first LDS write, so the L2 round trips overlap, then runs the 256 tests per keypoint.
+constexpr int KPW = 4;
+
 template <int RB>
 __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     const uint8_t* __restrict__ blurred, DescParams p, const uint32_t* __restrict__ xy_in,
@@ -811,45 +814,61 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     constexpr int ND = (BDMAX + 3 + 3) / 4;  // dwords per window row: covers any byte phase
     constexpr int WP = 4 * ND;
     constexpr int RPI = kWave / ND;          // window rows per load instruction
-    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][(BDMAX + RPI) * WP];
+    constexpr int NLD = (BDMAX + RPI - 1) / RPI;
+    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KPW][NLD * RPI * WP];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
-    const int k = blockIdx.x * DESC_WAVES + wave;
-    if (k >= (int)n_in[f]) return;
+    const int k0 = (blockIdx.x * DESC_WAVES + wave) * KPW;
+    const int n = (int)n_in[f];
+    if (k0 >= n) return;
     const int R = p.R, bd = 2 * R + 1;
-    const uint32_t v = xy_in[(long long)f * p.out_cap + k];
-    const int cx = (int)(v & 0xFFFFu), cy = (int)(v >> 16);
     const uint8_t* src = blurred + (long long)f * p.bpitch;
-    uint8_t* w = win[wave];
-    const int x0 = cx - R, y0 = cy - R;
-    const int xa = x0 & ~3, s = x0 - xa;
     // lane -> (row lane / ND, dword lane % ND); keypoints keep the pattern radius from the
     // border (RunByImageBorder), so the clamps are inert: they only keep reads inside the frame
     const int lr = lane / ND, lc = lane - lr * ND;
-    const int gx = min(max(xa + 4 * lc, 0), p.bstride - 4);
-    if (lr < RPI) {
+    uint32_t v[KPW][NLD];
+    int sh[KPW];
 #pragma unroll
-        for (int r0 = 0; r0 < BDMAX; r0 += RPI) {
-            const int r = r0 + lr;
-            if (r < bd) {
-                const int gy = min(max(y0 + r, 0), p.h - 1);
-                *reinterpret_cast<uint32_t*>(w + r * WP + 4 * lc) =
-                    *reinterpret_cast<const uint32_t*>(src + (long long)gy * p.bstride + gx);
-            }
+    for (int q = 0; q < KPW; q++) {
+        const int k = min(k0 + q, n - 1);
+        const uint32_t xy = xy_in[(long long)f * p.out_cap + k];
+        const int x0 = (int)(xy & 0xFFFFu) - R, y0 = (int)(xy >> 16) - R;
+        const int xa = x0 & ~3;
+        sh[q] = x0 - xa;
+        const int gx = min(max(xa + 4 * lc, 0), p.bstride - 4);
+#pragma unroll
+        for (int l = 0; l < NLD; l++) {
+            const int gy = min(max(y0 + l * RPI + lr, 0), p.h - 1);
+            v[q][l] = *reinterpret_cast<const uint32_t*>(src + (long long)gy * p.bstride + gx);
         }
     }
-    wave_lds_sync();
-    const uint8_t* wb = w + s;
-    const char4* pat = reinterpret_cast<const char4*>(pattern);
-    unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
+    if (lr < RPI) {
 #pragma unroll
-    for (int chunk = 0; chunk < 4; chunk++) {
-        const char4 e = pat[chunk * kWave + lane];  // (x0, y0, x1, y1) of bit 64*chunk + lane
-        const int t0 = wb[(R + e.y) * WP + R + e.x];
-        const int t1 = wb[(R + e.w) * WP + R + e.z];
-        const unsigned long long m = __ballot(t0 < t1);
-        if (lane == 0) dst[chunk] = m;
+        for (int q = 0; q < KPW; q++)
+#pragma unroll
+            for (int l = 0; l < NLD; l++)
+                *reinterpret_cast<uint32_t*>(&win[wave][q][(l * RPI + lr) * WP + 4 * lc]) = v[q][l];
     }
+    wave_lds_sync();
+    const char4* pat = reinterpret_cast<const char4*>(pattern);
+    char4 e[4];
+#pragma unroll
+    for (int chunk = 0; chunk < 4; chunk++) e[chunk] = pat[chunk * kWave + lane];  // bit 64*chunk + lane
+#pragma unroll
+    for (int q = 0; q < KPW; q++) {
+        const int k = k0 + q;
+        if (k >= n) break;
+        const uint8_t* wb = &win[wave][q][sh[q]];
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
+#pragma unroll
+        for (int chunk = 0; chunk < 4; chunk++) {
+            const int t0 = wb[(R + e[chunk].y) * WP + R + e[chunk].x];
+            const int t1 = wb[(R + e[chunk].w) * WP + R + e[chunk].z];
+            const unsigned long long m = __ballot(t0 < t1);
+            if (lane == 0) dst[chunk] = m;
+        }
+    }
+    (void)bd;
 }
 
 __global__ void synth_frames_kernel(uint8_t* __restrict__ out, int w, int h, long long pitch,
@@ -1012,6 +1031,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         {
             KernelTimer _kt("orb.describe", st);
             if (fused_blur) {
+                g3.x = (cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW);
                 auto kern = dp.R <= 7 ? describe_blurred_kernel<7>
                                       : (dp.R <= 13 ? describe_blurred_kernel<13> : describe_blurred_kernel<RMAX>);
                 hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, o->blurred.as<uint8_t>(), dp,
