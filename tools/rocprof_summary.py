@@ -23,13 +23,15 @@ ROOT = Path(__file__).resolve().parent.parent
 
 
 def short(name: str) -> str:
-    m = re.search(r"::([A-Za-z0-9_]+)\(", name)
+    m = re.search(r"::([A-Za-z0-9_]+)(?:<[^(]*>)?\(", name)
     base = m.group(1) if m else name.split("(")[0]
     return base
 
 
+VALU_PEAK_G = 1024 * 2.4 / 4.0  # G wave64 VALU instructions / s
+
 KERNEL_TAG = {
-    "fast_nms_kernel": "orb.fast_nms", "select_kernel": "orb.select", "describe_kernel": "orb.describe",
+    "fast_nms_kernel": "orb.fast_nms", "select_kernel": "orb.select", "describe_kernel": "orb.describe", "describe_blurred_kernel": "orb.describe",
     "match_kernel": "match.two_way", "build_schur": "ba.build_schur", "cholesky_solve": "ba.cholesky_solve",
     "point_linearize": "ba.point_linearize", "cam_linearize": "ba.cam_linearize",
     "point_backsub": "ba.point_backsub", "point_schur": "ba.point_schur", "update_state": "ba.update_state",
@@ -69,12 +71,17 @@ def main():
     stats = read_stats(prof / "trace" / "run_kernel_stats.csv")
     fetch = read_pmc(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
     write = read_pmc(prof / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
+    valu = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_INSTS_VALU")
+    mfma = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_VALU_MFMA_BUSY_CYCLES")
     lines = [f"# rocprofv3 summary — {tag}", "",
              "`rocprofv3 --kernel-trace --stats` (durations) and separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` "
              "passes of `python bench.py` on one MI355X.  KiB counters converted to bytes; FETCH x2 is the "
              "gfx950 wide-stream correction (MI355X_MICROARCH.md §HBM).", "",
-             "| kernel | calls | avg µs | total ms | % | FETCH MB/launch (raw) | FETCH x2 | WRITE MB/launch |",
-             "|---|---|---|---|---|---|---|---|"]
+             "VALU issue: SQ_INSTS_VALU wave-instructions per launch (own pass) over the launch time, against "
+             "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction (614 G/s; tools/valu_probe.hip measures "
+             "~4.6-4.8 cycles per instruction per SIMD for every form used here).", "",
+             "| kernel | calls | avg µs | total ms | % | FETCH MB/launch (raw) | FETCH x2 | WRITE MB/launch | VALU G inst/s | VALU issue frac |",
+             "|---|---|---|---|---|---|---|---|---|---|"]
     summary = {}
     for r in stats:
         k = r["kernel"]
@@ -82,16 +89,22 @@ def main():
         w = write.get(k)
         fmb = f * 1024 / 1e6 if f is not None else None
         wmb = w * 1024 / 1e6 if w is not None else None
+        v = valu.get(k)
+        vrate = v / (r["avg_us"] * 1e-6) / 1e9 if v is not None and r["avg_us"] > 0 else None
+        vfrac = vrate / VALU_PEAK_G if vrate is not None else None
         lines.append(f"| {k} | {r['calls']} | {r['avg_us']:.1f} | {r['total_ms']:.2f} | {r['pct']:.1f} | "
                      f"{'' if fmb is None else f'{fmb:.3f}'} | {'' if fmb is None else f'{2 * fmb:.3f}'} | "
-                     f"{'' if wmb is None else f'{wmb:.3f}'} |")
+                     f"{'' if wmb is None else f'{wmb:.3f}'} | {'' if vrate is None else f'{vrate:.0f}'} | "
+                     f"{'' if vfrac is None else f'{vfrac:.2f}'} |")
         tagname = KERNEL_TAG.get(k)
         if tagname:
             summary[tagname] = {"avg_us": r["avg_us"], "calls": r["calls"],
                                 "fetch_bytes_per_launch": None if f is None else f * 1024,
                                 "write_bytes_per_launch": None if w is None else w * 1024,
                                 "hbm_bytes_per_launch": None if (f is None or w is None) else (f + w) * 1024,
-                                "hbm_bytes_per_launch_fetch_x2": None if (f is None or w is None) else (2 * f + w) * 1024}
+                                "hbm_bytes_per_launch_fetch_x2": None if (f is None or w is None) else (2 * f + w) * 1024,
+                                "valu_insts_per_launch": v, "valu_issue_frac": vfrac,
+                                "mfma_busy_cycles_per_launch": mfma.get(k)}
     (out_dir / f"{tag}_rocprof.md").write_text("\n".join(lines) + "\n")
     (out_dir / f"{tag}_pmc_summary.json").write_text(json.dumps(summary, indent=1))
     (out_dir / "pmc_summary.json").write_text(json.dumps(summary, indent=1))
