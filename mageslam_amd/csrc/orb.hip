@@ -765,6 +765,7 @@ struct DescParams {
     int dword_ok;
     int bstride;         // blurred frames (describe_blurred_kernel)
     long long bpitch;
+    int chunks, frames;  // describe_blurred_kernel grid decomposition
 };
 
 // Orders one wave's LDS writes before its other lanes' reads (waves of a workgroup work on
@@ -875,8 +876,13 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     constexpr int NLD = (BDMAX + RPI - 1) / RPI;
     __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KPW][NLD * RPI * WP];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int f = blockIdx.y;
-    const int k0 = (blockIdx.x * DESC_WAVES + wave) * KPW;
+    // XCD-aware 1-D grid: workgroups are dispatched round-robin over the 8 XCDs, so block b runs
+    // on XCD b % 8; all keypoint chunks of frame f get blocks = f (mod 8) and consecutive slots,
+    // so the frame's blurred image is fetched into one XCD's L2 once (placement affects speed only)
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int chunk = slot % p.chunks, f = (slot / p.chunks) * 8 + xcd;
+    if (f >= p.frames) return;
+    const int k0 = (chunk * DESC_WAVES + wave) * KPW;
     const int n = (int)n_in[f];
     if (k0 >= n) return;
     const int R = p.R, bd = 2 * R + 1;
@@ -1089,7 +1095,9 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         {
             KernelTimer _kt("orb.describe", st);
             if (fused_blur) {
-                g3.x = (cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW);
+                dp.chunks = (int)((cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW));
+                dp.frames = (int)batch;
+                g3 = dim3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
                 auto kern = dp.R <= 7 ? describe_blurred_kernel<7>
                                       : (dp.R <= 13 ? describe_blurred_kernel<13> : describe_blurred_kernel<RMAX>);
                 hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, o->blurred.as<uint8_t>(), dp,
