@@ -61,6 +61,9 @@ typedef struct mage_orb_settings {
     int32_t num_cells_y;           /* 32 */
 } mage_orb_settings;
 
+/* Pyramid levels supported (nlevels in 1..MAGE_MAX_LEVELS). */
+#define MAGE_MAX_LEVELS 8
+
 typedef void* mage_stream; /* a hipStream_t; NULL = the default stream */
 
 /* ------------------------------------------------------------------------------------------ */

@@ -420,7 +420,11 @@ struct SelectParams {
     int strong;
     float min_r, max_r;
     int cells_x, cells_y;
-    float kp_size;
+    float kp_size;   // PatchSize * layerScale (:716)
+    int level;       // octave
+    float scale;     // layerScale: pt *= scale (:756-760)
+    int accumulate;  // append after the n_out[f] keypoints of the previous levels (Insert)
+    uint16_t* lvl;   // per keypoint (level << 8 | rotation); rotation filled by orient_kernel
 };
 
 enum : uint32_t { ST_KMAX = 1u, ST_CELLS = 2u };
@@ -527,6 +531,7 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
     const int tid = threadIdx.x;
     const uint32_t* C = cand + (long long)f * p.cand_cap;
     const int n0 = (int)min(counts[f], p.cand_cap);
+    const int base = p.accumulate ? (int)n_out[f] : 0;  // read before any barrier; updated at the end
     for (int i = tid; i < 256; i += SEL_THREADS) hist[i] = 0;
     if (tid == 0) {
         s_K = 0;
@@ -601,7 +606,7 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
         if (ncell > CELLMAX) {
             if (tid == 0) {
                 atomicOr(status, ST_CELLS);
-                n_out[f] = 0;
+                n_out[f] = (uint32_t)base;
             }
             return;
         }
@@ -720,9 +725,11 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
     }
 
     int nout = anms ? min(N, K) : K;
-    nout = min(nout, (int)p.out_cap);  // ImageData::Insert truncation (ImageData.h:65-70)
-    mage_keypoint* kp = kp_out + (long long)f * p.out_cap;
-    uint32_t* xy = xy_out + (long long)f * p.out_cap;
+    // ImageData::Insert copies what still fits after the previous levels (ImageData.h:65-70)
+    nout = max(min(nout, (int)p.out_cap - base), 0);
+    mage_keypoint* kp = kp_out + (long long)f * p.out_cap + base;
+    uint32_t* xy = xy_out + (long long)f * p.out_cap + base;
+    uint16_t* lv = p.lvl ? p.lvl + (long long)f * p.out_cap + base : nullptr;
     for (int i = tid; i < nout; i += SEL_THREADS) {
         unsigned long long key = keys[i];
         uint32_t raster, s;
@@ -735,17 +742,18 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
         }
         uint32_t y = raster / (uint32_t)p.w, x = raster - y * (uint32_t)p.w;
         mage_keypoint k;
-        k.x = (float)x;
-        k.y = (float)y;
+        k.x = __fmul_rn((float)x, p.scale);
+        k.y = __fmul_rn((float)y, p.scale);
         k.size = p.kp_size;
         k.angle = 0.0f;
         k.response = (float)s;
-        k.octave = 0;
+        k.octave = p.level;
         k.class_id = -1;
         kp[i] = k;
-        xy[i] = (y << 16) | x;
+        xy[i] = (y << 16) | x;  // level coordinates = the descriptor centre cvRound(pt / layerScale)
+        if (lv) lv[i] = (uint16_t)(p.level << 8);
     }
-    if (tid == 0) n_out[f] = (uint32_t)nout;
+    if (tid == 0) n_out[f] = (uint32_t)(base + nout);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -755,16 +763,21 @@ constexpr int DESC_WAVES = 4;
 constexpr int RMAX = 18;  // max |pattern offset| over both tables and all rotations
 constexpr int KHMAX = 7;  // max Gaussian half-size (ksize <= 15)
 
+struct LevelImages {
+    const uint8_t* base[MAGE_MAX_LEVELS];
+    long long pitch[MAGE_MAX_LEVELS];
+    int stride[MAGE_MAX_LEVELS];
+};
+
 struct DescParams {
-    int w, h, stride;
-    long long pitch;
+    LevelImages lev;  // per level: blurred images (describe_blurred_kernel) or raw (describe_kernel)
+    int lw[MAGE_MAX_LEVELS], lh[MAGE_MAX_LEVELS];
+    const uint16_t* lvl;  // per keypoint (level << 8 | rotation), null: level 0, rotation 0
     unsigned out_cap;
     int R;      // sampling radius of the pattern rotations in use
     int ksize;  // Gaussian taps (<= 1: no blur)
     int taps[2 * KHMAX + 1];
     int dword_ok;
-    int bstride;         // blurred frames (describe_blurred_kernel)
-    long long bpitch;
     int chunks, frames;  // describe_blurred_kernel grid decomposition
 };
 
@@ -783,7 +796,7 @@ __device__ __forceinline__ void wave_lds_sync()
 // their byte phase `s`); windows touching the border use reflect-101 byte loads.
 template <int RB>
 __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
-    const uint8_t* __restrict__ frames, DescParams p, const uint32_t* __restrict__ xy_in,
+    DescParams p, const uint32_t* __restrict__ xy_in,
     const uint32_t* __restrict__ n_in, const int8_t* __restrict__ pattern,
     uint8_t* __restrict__ desc_out)
 {
@@ -802,22 +815,24 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
     const int R = p.R, Rr = R + kh, rawDim = 2 * Rr + 1, bd = 2 * R + 1;
     const uint32_t v = xy_in[(long long)f * p.out_cap + k];
     const int cx = (int)(v & 0xFFFFu), cy = (int)(v >> 16);
-    const uint8_t* src = frames + (long long)f * p.pitch;
+    const int lr = p.lvl ? p.lvl[(long long)f * p.out_cap + k] : 0, l = lr >> 8, rot = lr & 0xFF;
+    const uint8_t* src = p.lev.base[l] + (long long)f * p.lev.pitch[l];
+    const int W = p.lw[l], H = p.lh[l], stride = p.lev.stride[l];
     uint8_t* rw = raw[wave];
     const int x0 = cx - Rr, y0 = cy - Rr;
     const int xa = x0 & ~3, s = x0 - xa;
     const int nd = (s + rawDim + 3) >> 2;  // dwords per row
-    if (p.dword_ok && x0 >= 0 && y0 >= 0 && y0 + rawDim <= p.h && xa + 4 * nd <= p.w) {
+    if (p.dword_ok && x0 >= 0 && y0 >= 0 && y0 + rawDim <= H && xa + 4 * nd <= W) {
         for (int i = lane; i < rawDim * nd; i += kWave) {
             const int r = i / nd, c = i - r * nd;
             *reinterpret_cast<uint32_t*>(rw + r * RAWP + 4 * c) =
-                *reinterpret_cast<const uint32_t*>(src + (long long)(y0 + r) * p.stride + xa + 4 * c);
+                *reinterpret_cast<const uint32_t*>(src + (long long)(y0 + r) * stride + xa + 4 * c);
         }
     } else {
         for (int i = lane; i < rawDim * rawDim; i += kWave) {
             const int r = i / rawDim, c = i - r * rawDim;
-            const int gy = reflect101(y0 + r, p.h), gx = reflect101(x0 + c, p.w);
-            rw[r * RAWP + s + c] = src[(long long)gy * p.stride + gx];
+            const int gy = reflect101(y0 + r, H), gx = reflect101(x0 + c, W);
+            rw[r * RAWP + s + c] = src[(long long)gy * stride + gx];
         }
     }
     wave_lds_sync();
@@ -846,8 +861,8 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
         blur[wave][i] = (uint8_t)o;
     }
     wave_lds_sync();
-    // rotation 0: angle = 0 without orientation (OpenCVModified.cpp:748-754, :522)
-    const char4* pat = reinterpret_cast<const char4*>(pattern);
+    // rotation: cvRound(angle / 12) % 30 (0 without orientation, OpenCVModified.cpp:748-754, :526)
+    const char4* pat = reinterpret_cast<const char4*>(pattern) + rot * 256;
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
 #pragma unroll
     for (int chunk = 0; chunk < 4; chunk++) {
@@ -866,8 +881,8 @@ constexpr int KPW = 4;
 
 template <int RB>
 __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
-    const uint8_t* __restrict__ blurred, DescParams p, const uint32_t* __restrict__ xy_in,
-    const uint32_t* __restrict__ n_in, const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
+    DescParams p, const uint32_t* __restrict__ xy_in, const uint32_t* __restrict__ n_in,
+    const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
 {
     constexpr int BDMAX = 2 * RB + 1;
     constexpr int ND = (BDMAX + 3 + 3) / 4;  // dwords per window row: covers any byte phase
@@ -885,54 +900,179 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     const int k0 = (chunk * DESC_WAVES + wave) * KPW;
     const int n = (int)n_in[f];
     if (k0 >= n) return;
-    const int R = p.R, bd = 2 * R + 1;
-    const uint8_t* src = blurred + (long long)f * p.bpitch;
+    const int R = p.R;
     // lane -> (row lane / ND, dword lane % ND); keypoints keep the pattern radius from the
-    // border (RunByImageBorder), so the clamps are inert: they only keep reads inside the frame
+    // border (RunByImageBorder), so the clamps are inert: they only keep reads inside the level
     const int lr = lane / ND, lc = lane - lr * ND;
     uint32_t v[KPW][NLD];
-    int sh[KPW];
+    int sh[KPW], rot[KPW];
 #pragma unroll
     for (int q = 0; q < KPW; q++) {
-        const int k = min(k0 + q, n - 1);
-        const uint32_t xy = xy_in[(long long)f * p.out_cap + k];
+        const long long ki = (long long)f * p.out_cap + min(k0 + q, n - 1);
+        const uint32_t xy = xy_in[ki];
+        const int lv = p.lvl ? p.lvl[ki] : 0, l = lv >> 8;
+        rot[q] = lv & 0xFF;
+        const uint8_t* src = p.lev.base[l] + (long long)f * p.lev.pitch[l];
+        const int stride = p.lev.stride[l];
         const int x0 = (int)(xy & 0xFFFFu) - R, y0 = (int)(xy >> 16) - R;
         const int xa = x0 & ~3;
         sh[q] = x0 - xa;
-        const int gx = min(max(xa + 4 * lc, 0), p.bstride - 4);
+        const int gx = min(max(xa + 4 * lc, 0), stride - 4);
 #pragma unroll
-        for (int l = 0; l < NLD; l++) {
-            const int gy = min(max(y0 + l * RPI + lr, 0), p.h - 1);
-            v[q][l] = *reinterpret_cast<const uint32_t*>(src + (long long)gy * p.bstride + gx);
+        for (int ld = 0; ld < NLD; ld++) {
+            const int gy = min(max(y0 + ld * RPI + lr, 0), p.lh[l] - 1);
+            v[q][ld] = *reinterpret_cast<const uint32_t*>(src + (long long)gy * stride + gx);
         }
     }
     if (lr < RPI) {
 #pragma unroll
         for (int q = 0; q < KPW; q++)
 #pragma unroll
-            for (int l = 0; l < NLD; l++)
-                *reinterpret_cast<uint32_t*>(&win[wave][q][(l * RPI + lr) * WP + 4 * lc]) = v[q][l];
+            for (int ld = 0; ld < NLD; ld++)
+                *reinterpret_cast<uint32_t*>(&win[wave][q][(ld * RPI + lr) * WP + 4 * lc]) = v[q][ld];
     }
     wave_lds_sync();
     const char4* pat = reinterpret_cast<const char4*>(pattern);
-    char4 e[4];
-#pragma unroll
-    for (int chunk = 0; chunk < 4; chunk++) e[chunk] = pat[chunk * kWave + lane];  // bit 64*chunk + lane
 #pragma unroll
     for (int q = 0; q < KPW; q++) {
         const int k = k0 + q;
         if (k >= n) break;
         const uint8_t* wb = &win[wave][q][sh[q]];
+        const char4* pr = pat + rot[q] * 256;  // cvRound(angle / 12) % 30 (:526)
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
 #pragma unroll
-        for (int chunk = 0; chunk < 4; chunk++) {
-            const int t0 = wb[(R + e[chunk].y) * WP + R + e[chunk].x];
-            const int t1 = wb[(R + e[chunk].w) * WP + R + e[chunk].z];
+        for (int c = 0; c < 4; c++) {
+            const char4 e = pr[c * kWave + lane];  // (x0, y0, x1, y1) of bit 64*c + lane
+            const int t0 = wb[(R + e.y) * WP + R + e.x];
+            const int t1 = wb[(R + e.w) * WP + R + e.z];
             const unsigned long long m = __ballot(t0 < t1);
-            if (lane == 0) dst[chunk] = m;
+            if (lane == 0) dst[c] = m;
         }
     }
-    (void)bd;
+}
+
+// ------------------------------------------------------------------------------------------
+// 4. Pyramid levels > 0: resize(INTER_LINEAR) of the previous level (OpenCVModified.cpp:833)
+// ------------------------------------------------------------------------------------------
+// OpenCV 3.4.0 8U linear resize (imgproc/src/resize.cpp, non-IPP build): per output column
+// xofs / (a0, a1) and per output row yofs / (b0, b1) are the host-computed fixed-point tables
+// (saturate_cast<short>(w * 2048)); the horizontal pass is exact in int32; the vertical pass is
+// the SSE2 VResizeLinearVec_32s8u formula below the last 16/4-wide block boundary `xv`, the
+// scalar FixedPtCast<int, uchar, 22> after it.
+struct ResizeParams {
+    int sw, sh, sstride;
+    long long spitch;
+    int dw, dh, dstride;
+    long long dpitch;
+    int xmax, xv;
+    const int* xofs;
+    const uint32_t* alpha;  // a0 | a1 << 16
+    const int* yofs;
+    const uint32_t* beta;   // b0 | b1 << 16
+};
+
+__global__ __launch_bounds__(256) void resize_linear_kernel(const uint8_t* __restrict__ src,
+                                                           uint8_t* __restrict__ dst, ResizeParams p)
+{
+    const int f = blockIdx.z, dy = blockIdx.y;
+    const int dx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (dx >= p.dw) return;
+    const uint8_t* S = src + (long long)f * p.spitch;
+    const int sy = p.yofs[dy];
+    const uint8_t* r0 = S + (long long)min(max(sy, 0), p.sh - 1) * p.sstride;
+    const uint8_t* r1 = S + (long long)min(max(sy + 1, 0), p.sh - 1) * p.sstride;
+    const int sx = p.xofs[dx];
+    const uint32_t a = p.alpha[dx], b = p.beta[dy];
+    const int a0 = (short)(a & 0xFFFFu), a1 = (short)(a >> 16), b0 = (short)(b & 0xFFFFu), b1 = (short)(b >> 16);
+    int h0, h1;
+    if (dx < p.xmax) {
+        h0 = r0[sx] * a0 + r0[sx + 1] * a1;
+        h1 = r1[sx] * a0 + r1[sx + 1] * a1;
+    } else {
+        h0 = r0[sx] * 2048;
+        h1 = r1[sx] * 2048;
+    }
+    int v;
+    if (dx < p.xv)
+        v = (((((int)(short)(h0 >> 4)) * b0) >> 16) + ((((int)(short)(h1 >> 4)) * b1) >> 16) + 2) >> 2;
+    else
+        v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+    dst[(long long)f * p.dpitch + (long long)dy * p.dstride + dx] = (uint8_t)min(max(v, 0), 255);
+}
+
+// ------------------------------------------------------------------------------------------
+// 5. ICAngles (UseOrientation, OpenCVModified.cpp:399-437) + rotation index (:526)
+// ------------------------------------------------------------------------------------------
+struct OrientParams {
+    LevelImages lev;  // unblurred levels
+    unsigned out_cap;
+    int half_k;
+    int umax[32];
+};
+
+// cv::fastAtan2 (OpenCV 3.4.0 core mathfuncs_core, polynomial atan in degrees), each float
+// operation rounded as the scalar host code does.
+__device__ __forceinline__ float fast_atan2_deg(float y, float x)
+{
+    const float k = (float)(180 / 3.141592653589793);
+    const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+    const float eps = (float)2.2204460492503131e-16;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = __fdiv_rn(ay, __fadd_rn(ax, eps));
+        c2 = __fmul_rn(c, c);
+        a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+    } else {
+        c = __fdiv_rn(ax, __fadd_rn(ay, eps));
+        c2 = __fmul_rn(c, c);
+        a = __fsub_rn(90.f, __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c));
+    }
+    if (x < 0) a = __fsub_rn(180.f, a);
+    if (y < 0) a = __fsub_rn(360.f, a);
+    return a;
+}
+
+// One wave per keypoint: lane u + half_k sums column u of the circular patch (|u| <= umax[|v|])
+// of the unblurred level around the keypoint; integer moments m_10 = sum u I, m_01 = sum v I
+// are order independent, so the wave reduction equals the reference's loops.
+__global__ __launch_bounds__(256) void orient_kernel(mage_keypoint* __restrict__ kp, const uint32_t* __restrict__ xy,
+                                                    uint16_t* __restrict__ lvl, const uint32_t* __restrict__ n_in,
+                                                    OrientParams p)
+{
+    const int f = blockIdx.y;
+    const int k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (k >= (int)n_in[f]) return;
+    const long long i = (long long)f * p.out_cap + k;
+    const int l = lvl[i] >> 8;
+    const uint32_t c = xy[i];
+    const int cx = (int)(c & 0xFFFFu), cy = (int)(c >> 16);
+    const int u = lane - p.half_k;
+    int m10 = 0, m01 = 0;
+    if (lane <= 2 * p.half_k) {
+        const uint8_t* col = p.lev.base[l] + (long long)f * p.lev.pitch[l] + cx + u;
+        const int au = abs(u);
+        for (int v = -p.half_k; v <= p.half_k; v++) {
+            if (au <= p.umax[abs(v)]) {
+                const int val = col[(long long)(cy + v) * p.lev.stride[l]];
+                m10 += u * val;
+                m01 += v * val;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        m10 += __shfl_xor(m10, off);
+        m01 += __shfl_xor(m01, off);
+    }
+    if (lane == 0) {
+        const float angle = fast_atan2_deg((float)m01, (float)m10);
+        kp[i].angle = angle;
+        // rot = cvRound(angle / ROTATION_INCREMENT_DEGREES) % ROTATION_INCREMENT_COUNT (:526)
+        const int rot = ((int)rintf(__fdiv_rn(angle, 12.0f))) % 30;
+        lvl[i] = (uint16_t)((l << 8) | rot);
+    }
 }
 
 __global__ void synth_frames_kernel(uint8_t* __restrict__ out, int w, int h, long long pitch,
@@ -963,12 +1103,33 @@ __global__ void synth_frames_kernel(uint8_t* __restrict__ out, int w, int h, lon
 // Host side
 // ------------------------------------------------------------------------------------------
 
+struct LevelGeom {
+    int w = 0, h = 0, stride = 0;
+    long long pitch = 0;
+    float scale = 1.f;
+    int nfeatures = 0;
+    size_t off = 0, boff = 0, coff = 0;  // pyramid / blurred / candidate offsets (per frame)
+    unsigned cand_cap = 0;
+    int xmax = 0, xv = 0;                 // resize tables (levels > 0)
+    size_t xofs = 0, yofs = 0, alpha = 0, beta = 0;
+};
+
+struct Geometry {
+    int w = -1, h = -1, L = 0;
+    LevelGeom lv[MAGE_MAX_LEVELS];
+    size_t pyr_bytes = 0, blur_bytes = 0, cand_total = 0;
+    std::vector<int> tab_ints;
+    std::vector<uint32_t> tab_words;
+    bool tab_valid = false;
+};
+
 struct OrbDetector {
     mage_orb_settings s{};
     int device = 0;
     int taps[2 * KHMAX + 1] = {0};
     int R = 7;
-    DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n, blurred;
+    Geometry geo;
+    DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n, blurred, pyr, rtab, lvl;
 };
 
 namespace {
@@ -1001,111 +1162,275 @@ mage_status validate(const OrbDetector* o, int w, int h, int stride)
     return MAGE_OK;
 }
 
+// Pyramid geometry (DetectAndCompute :785-804): layerScale = (float)pow(f, l) (getScale :564-567),
+// level size (cvRound(cols / scale), cvRound(rows / scale)); per-level budget (ComputeKeyPoints
+// :659-669) in float as written.  Levels > 0 live in one device buffer, rows padded to 4 bytes.
+void level_geometry(OrbDetector* o, int w, int h)
+{
+    const mage_orb_settings& s = o->s;
+    Geometry& g = o->geo;
+    g.w = w;
+    g.h = h;
+    g.L = (int)s.nlevels;
+    const float factor = 1.0f / s.scale_factor;
+    float nd = (int)s.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)g.L));
+    int sum = 0;
+    size_t off = 0, boff = 0, coff = 0;
+    for (int l = 0; l < g.L; l++) {
+        LevelGeom& v = g.lv[l];
+        v.scale = (float)std::pow((double)s.scale_factor, (double)l);
+        v.w = l == 0 ? w : (int)std::lrint((float)w / v.scale);
+        v.h = l == 0 ? h : (int)std::lrint((float)h / v.scale);
+        v.stride = (v.w + 3) & ~3;
+        v.pitch = (long long)v.stride * v.h;
+        v.off = l == 0 ? 0 : off;
+        if (l > 0) off += (size_t)v.pitch;
+        v.boff = boff;
+        boff += (size_t)v.pitch;
+        v.cand_cap = (unsigned)(((v.w + 1) / 2) * ((v.h + 1) / 2));
+        v.coff = coff;
+        coff += v.cand_cap;
+        if (l < g.L - 1) {
+            v.nfeatures = (int)std::lrint(nd);
+            sum += v.nfeatures;
+            nd *= factor;
+        } else {
+            v.nfeatures = std::max((int)s.nfeatures - sum, 0);
+        }
+    }
+    g.pyr_bytes = off;
+    g.blur_bytes = boff;
+    g.cand_total = coff;
+    // resize(INTER_LINEAR) tables of levels > 0 (OpenCV 3.4.0 resize.cpp, see resize_linear_kernel)
+    std::vector<int> ints;
+    std::vector<uint32_t> words;
+    for (int l = 1; l < g.L; l++) {
+        const LevelGeom &src = g.lv[l - 1], &dst = g.lv[l];
+        LevelGeom& v = g.lv[l];
+        const double scale_x = 1. / ((double)dst.w / src.w), scale_y = 1. / ((double)dst.h / src.h);
+        v.xmax = dst.w;
+        v.xofs = ints.size();
+        v.alpha = words.size();
+        for (int dx = 0; dx < dst.w; dx++) {
+            float fx = (float)((dx + 0.5) * scale_x - 0.5);
+            int sx = (int)std::floor(fx);
+            fx -= sx;
+            if (sx < 0) fx = 0, sx = 0;
+            if (sx + 1 >= src.w) {
+                v.xmax = std::min(v.xmax, dx);
+                if (sx >= src.w - 1) fx = 0, sx = src.w - 1;
+            }
+            ints.push_back(sx);
+            const int a0 = (int)std::lrint((1.f - fx) * 2048), a1 = (int)std::lrint(fx * 2048);
+            words.push_back((uint32_t)(uint16_t)a0 | ((uint32_t)(uint16_t)a1 << 16));
+        }
+        v.yofs = ints.size();
+        v.beta = words.size();
+        for (int dy = 0; dy < dst.h; dy++) {
+            float fy = (float)((dy + 0.5) * scale_y - 0.5);
+            int sy = (int)std::floor(fy);
+            fy -= sy;
+            ints.push_back(sy);
+            const int b0 = (int)std::lrint((1.f - fy) * 2048), b1 = (int)std::lrint(fy * 2048);
+            words.push_back((uint32_t)(uint16_t)b0 | ((uint32_t)(uint16_t)b1 << 16));
+        }
+        int xv = 0;
+        while (xv <= dst.w - 16) xv += 16;
+        while (xv < dst.w - 4) xv += 4;
+        v.xv = xv;
+    }
+    g.tab_ints = ints;
+    g.tab_words = words;
+    g.tab_valid = false;
+}
+
 mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, int w, int h,
                       int stride, long long pitch, mage_keypoint* d_kp, uint8_t* d_desc,
                       uint32_t cap, uint32_t* d_n, hipStream_t st)
 {
     const mage_orb_settings& s = o->s;
-    const unsigned candCap = (unsigned)(((w + 1) / 2) * ((h + 1) / 2));
+    Geometry& g = o->geo;
+    if (g.w != w || g.h != h || g.L != (int)s.nlevels) level_geometry(o, w, h);
+    const int L = g.L;
+    const bool multi = L > 1 || s.use_orientation;
     mage_status r;
-    if ((r = o->cand.reserve((size_t)batch * candCap * 4)) != MAGE_OK) return r;
-    if ((r = o->counts.reserve((size_t)batch * 4)) != MAGE_OK) return r;
+    if ((r = o->cand.reserve((size_t)batch * g.cand_total * 4)) != MAGE_OK) return r;
+    if ((r = o->counts.reserve((size_t)batch * L * 4)) != MAGE_OK) return r;
     if ((r = o->xy.reserve((size_t)batch * std::max(cap, 1u) * 4)) != MAGE_OK) return r;
     if ((r = o->status.reserve(4)) != MAGE_OK) return r;
-    MAGE_HIP(hipMemsetAsync(o->counts.ptr, 0, (size_t)batch * 4, st));
+    if (multi && (r = o->lvl.reserve((size_t)batch * std::max(cap, 1u) * 2)) != MAGE_OK) return r;
+    if (L > 1 && (r = o->pyr.reserve((size_t)batch * g.pyr_bytes)) != MAGE_OK) return r;
+    if (!g.tab_valid && L > 1) {
+        const size_t ib = g.tab_ints.size() * 4, wb = g.tab_words.size() * 4;
+        if ((r = o->rtab.reserve(ib + wb)) != MAGE_OK) return r;
+        MAGE_HIP(hipMemcpy(o->rtab.ptr, g.tab_ints.data(), ib, hipMemcpyHostToDevice));
+        MAGE_HIP(hipMemcpy(o->rtab.as<uint8_t>() + ib, g.tab_words.data(), wb, hipMemcpyHostToDevice));
+        g.tab_valid = true;
+    }
+    MAGE_HIP(hipMemsetAsync(o->counts.ptr, 0, (size_t)batch * L * 4, st));
 
-    const int half = (int)s.patch_size / 2;
-    const int border = half;  // RunByImageBorder(halfPatchSize) without orientation (:712)
-    FastParams fp{};
-    fp.w = w;
-    fp.h = h;
-    fp.stride = stride;
-    fp.pitch = pitch;
-    fp.threshold = std::min(std::max((int)s.fast_threshold, 0), 255);
-    fp.xlo = std::max(3, border);
-    fp.xhi = std::min(w - 4, w - border - 1);
-    fp.ylo = std::max(3, border);
-    fp.yhi = std::min(h - 4, h - border - 1);
-    if (h <= 2 * border || w <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
-    fp.cand_cap = candCap;
-    fp.dword_ok = (w % 4 == 0) && (stride % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)d_frames % 4 == 0);
+    // level images: 0 = the caller's frames, > 0 = the pyramid buffer (batch-major per level)
+    LevelImages raw{};
+    for (int l = 0; l < L; l++) {
+        if (l == 0) {
+            raw.base[0] = d_frames;
+            raw.pitch[0] = pitch;
+            raw.stride[0] = stride;
+        } else {
+            raw.base[l] = o->pyr.as<uint8_t>() + (size_t)batch * g.lv[l].off;
+            raw.pitch[l] = g.lv[l].pitch;
+            raw.stride[l] = g.lv[l].stride;
+        }
+    }
+    if (L > 1) {
+        const int* ints = o->rtab.as<int>();
+        const uint32_t* words = reinterpret_cast<const uint32_t*>(o->rtab.as<uint8_t>() + g.tab_ints.size() * 4);
+        KernelTimer _kt("orb.pyramid", st);
+        for (int l = 1; l < L; l++) {
+            const LevelGeom &src = g.lv[l - 1], &dst = g.lv[l];
+            ResizeParams rp{};
+            rp.sw = src.w;
+            rp.sh = src.h;
+            rp.sstride = raw.stride[l - 1];
+            rp.spitch = raw.pitch[l - 1];
+            rp.dw = dst.w;
+            rp.dh = dst.h;
+            rp.dstride = dst.stride;
+            rp.dpitch = dst.pitch;
+            rp.xmax = dst.xmax;
+            rp.xv = dst.xv;
+            rp.xofs = ints + dst.xofs;
+            rp.yofs = ints + dst.yofs;
+            rp.alpha = words + dst.alpha;
+            rp.beta = words + dst.beta;
+            hipLaunchKernelGGL(resize_linear_kernel, dim3((dst.w + 255) / 256, dst.h, batch), dim3(256), 0, st,
+                               raw.base[l - 1], const_cast<uint8_t*>(raw.base[l]), rp);
+        }
+    }
+    MAGE_HIP(hipGetLastError());
+
     // the default 7-tap Gaussian is fused into the FAST pass (the tile is already in LDS);
     // other kernel sizes blur inside the descriptor windows instead
     const bool fused_blur = cap > 0 && s.gaussian_kernel_size == 7;
-    const int bstride = (w + 3) & ~3;
-    const long long bpitch = (long long)bstride * h;
-    if (fused_blur) {
-        if ((r = o->blurred.reserve((size_t)batch * bpitch)) != MAGE_OK) return r;
-        const int* k = o->taps;
-        fp.blur = o->blurred.as<uint8_t>();
-        fp.blur_stride = bstride;
-        fp.blur_pitch = bpitch;
-        fp.t0 = (uint32_t)k[0] | ((uint32_t)k[1] << 8) | ((uint32_t)k[2] << 16) | ((uint32_t)k[3] << 24);
-        fp.t1 = (uint32_t)k[4] | ((uint32_t)k[5] << 8) | ((uint32_t)k[6] << 16);
-        fp.t01 = (uint32_t)k[0] | ((uint32_t)k[1] << 16);
-        fp.t23 = (uint32_t)k[2] | ((uint32_t)k[3] << 16);
-        fp.t45 = (uint32_t)k[4] | ((uint32_t)k[5] << 16);
-        fp.t6 = (uint32_t)k[6];
-    }
-    dim3 g1((w + TW - 1) / TW, (h + TH - 1) / TH, batch);
-    {
-        KernelTimer _kt("orb.fast_nms", st);
-        hipLaunchKernelGGL(fast_nms_kernel, g1, dim3(FAST_THREADS), 0, st, d_frames, fp,
-                           o->cand.as<uint32_t>(), o->counts.as<uint32_t>());
-    }
-    MAGE_HIP(hipGetLastError());
+    if (fused_blur && (r = o->blurred.reserve((size_t)batch * g.blur_bytes)) != MAGE_OK) return r;
+    LevelImages blurred{};
+    const int half = (int)s.patch_size / 2;
+    // RunByImageBorder(halfPatchSize), or cvCeil(halfPatchSize * sqrt(2.f)) when orienting (:711-712)
+    const int border = s.use_orientation ? (int)std::ceil(half * std::sqrt(2.0f)) : half;
+    for (int l = 0; l < L; l++) {
+        const LevelGeom& v = g.lv[l];
+        const int W = v.w, H = v.h;
+        FastParams fp{};
+        fp.w = W;
+        fp.h = H;
+        fp.stride = raw.stride[l];
+        fp.pitch = raw.pitch[l];
+        fp.threshold = std::min(std::max((int)s.fast_threshold, 0), 255);
+        fp.xlo = std::max(3, border);
+        fp.xhi = std::min(W - 4, W - border - 1);
+        fp.ylo = std::max(3, border);
+        fp.yhi = std::min(H - 4, H - border - 1);
+        if (H <= 2 * border || W <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
+        fp.cand_cap = v.cand_cap;
+        fp.dword_ok = (fp.stride % 4 == 0) && (fp.pitch % 4 == 0) && ((uintptr_t)raw.base[l] % 4 == 0);
+        if (fused_blur) {
+            const int* k = o->taps;
+            blurred.base[l] = o->blurred.as<uint8_t>() + (size_t)batch * v.boff;
+            blurred.pitch[l] = v.pitch;
+            blurred.stride[l] = v.stride;
+            fp.blur = const_cast<uint8_t*>(blurred.base[l]);
+            fp.blur_stride = v.stride;
+            fp.blur_pitch = v.pitch;
+            fp.t0 = (uint32_t)k[0] | ((uint32_t)k[1] << 8) | ((uint32_t)k[2] << 16) | ((uint32_t)k[3] << 24);
+            fp.t1 = (uint32_t)k[4] | ((uint32_t)k[5] << 8) | ((uint32_t)k[6] << 16);
+            fp.t01 = (uint32_t)k[0] | ((uint32_t)k[1] << 16);
+            fp.t23 = (uint32_t)k[2] | ((uint32_t)k[3] << 16);
+            fp.t45 = (uint32_t)k[4] | ((uint32_t)k[5] << 16);
+            fp.t6 = (uint32_t)k[6];
+        }
+        uint32_t* cand = o->cand.as<uint32_t>() + (size_t)batch * v.coff;
+        uint32_t* counts = o->counts.as<uint32_t>() + (size_t)batch * l;
+        {
+            KernelTimer _kt("orb.fast_nms", st);
+            hipLaunchKernelGGL(fast_nms_kernel, dim3((W + TW - 1) / TW, (H + TH - 1) / TH, batch), dim3(FAST_THREADS), 0,
+                               st, raw.base[l], fp, cand, counts);
+        }
+        MAGE_HIP(hipGetLastError());
 
-    SelectParams sp{};
-    sp.w = w;
-    sp.h = h;
-    sp.cand_cap = candCap;
-    sp.nfeatures = (int)s.nfeatures;  // nfeaturesPerLevel[0] for one level (:659-672)
-    sp.max_num = (int)((float)s.nfeatures * s.feature_factor);
-    sp.out_cap = cap;
-    sp.fast_threshold = (int)s.fast_threshold;
-    sp.feature_strength = s.feature_strength;
-    sp.strong = s.strong_response;
-    sp.min_r = s.min_robust_factor;
-    sp.max_r = s.max_robust_factor;
-    sp.cells_x = s.num_cells_x;
-    sp.cells_y = s.num_cells_y;
-    sp.kp_size = (float)s.patch_size * 1.0f;
-    {
-        KernelTimer _kt("orb.select", st);
-        hipLaunchKernelGGL(select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, o->cand.as<uint32_t>(),
-                           o->counts.as<uint32_t>(), sp, d_kp, o->xy.as<uint32_t>(), d_n,
-                           o->status.as<uint32_t>());
+        SelectParams sp{};
+        sp.w = W;
+        sp.h = H;
+        sp.cand_cap = v.cand_cap;
+        sp.nfeatures = v.nfeatures;  // nfeaturesPerLevel[level] (:659-669)
+        sp.max_num = (int)((float)v.nfeatures * s.feature_factor);
+        sp.out_cap = cap;
+        sp.fast_threshold = (int)s.fast_threshold;
+        sp.feature_strength = s.feature_strength;
+        sp.strong = s.strong_response;
+        sp.min_r = s.min_robust_factor;
+        sp.max_r = s.max_robust_factor;
+        sp.cells_x = s.num_cells_x;
+        sp.cells_y = s.num_cells_y;
+        sp.kp_size = (float)s.patch_size * v.scale;
+        sp.level = l;
+        sp.scale = v.scale;
+        sp.accumulate = l > 0;
+        sp.lvl = multi ? o->lvl.as<uint16_t>() : nullptr;
+        {
+            KernelTimer _kt("orb.select", st);
+            hipLaunchKernelGGL(select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, cand, counts, sp, d_kp,
+                               o->xy.as<uint32_t>(), d_n, o->status.as<uint32_t>());
+        }
+        MAGE_HIP(hipGetLastError());
     }
-    MAGE_HIP(hipGetLastError());
+
+    if (cap > 0 && s.use_orientation) {
+        OrientParams op{};
+        op.lev = raw;
+        op.out_cap = cap;
+        op.half_k = half;
+        // u_max (ComputeKeyPoints :671-686)
+        int vmax = (int)std::floor(half * std::sqrt(2.f) / 2 + 1), vmin = (int)std::ceil(half * std::sqrt(2.f) / 2);
+        for (int v = 0; v <= vmax; ++v) op.umax[v] = (int)std::lrint(std::sqrt((double)half * half - v * v));
+        for (int v = half, v0 = 0; v >= vmin; --v) {
+            while (op.umax[v0] == op.umax[v0 + 1]) ++v0;
+            op.umax[v] = v0;
+            ++v0;
+        }
+        KernelTimer _kt("orb.orient", st);
+        hipLaunchKernelGGL(orient_kernel, dim3((cap + 3) / 4, batch), dim3(256), 0, st, d_kp, o->xy.as<uint32_t>(),
+                           o->lvl.as<uint16_t>(), d_n, op);
+        MAGE_HIP(hipGetLastError());
+    }
 
     if (cap > 0) {
         DescParams dp{};
-        dp.w = w;
-        dp.h = h;
-        dp.stride = stride;
-        dp.pitch = pitch;
+        dp.lev = fused_blur ? blurred : raw;
+        for (int l = 0; l < L; l++) {
+            dp.lw[l] = g.lv[l].w;
+            dp.lh[l] = g.lv[l].h;
+        }
+        dp.lvl = multi ? o->lvl.as<uint16_t>() : nullptr;
         dp.out_cap = cap;
         dp.R = o->R;
         dp.ksize = (int)s.gaussian_kernel_size;
         for (int i = 0; i < 2 * KHMAX + 1; i++) dp.taps[i] = o->taps[i];
         dp.dword_ok = (stride % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)d_frames % 4 == 0);
-        dp.bstride = bstride;
-        dp.bpitch = bpitch;
-        dim3 g3((cap + DESC_WAVES - 1) / DESC_WAVES, batch);
         {
             KernelTimer _kt("orb.describe", st);
             if (fused_blur) {
                 dp.chunks = (int)((cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW));
                 dp.frames = (int)batch;
-                g3 = dim3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
+                const dim3 g3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
                 auto kern = dp.R <= 7 ? describe_blurred_kernel<7>
                                       : (dp.R <= 13 ? describe_blurred_kernel<13> : describe_blurred_kernel<RMAX>);
-                hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, o->blurred.as<uint8_t>(), dp,
-                                   o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
+                hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, o->xy.as<uint32_t>(), d_n,
+                                   o->pattern.as<int8_t>(), d_desc);
             } else {
+                const dim3 g3((cap + DESC_WAVES - 1) / DESC_WAVES, batch);
                 auto kern = dp.R <= 7 ? describe_kernel<7> : (dp.R <= 13 ? describe_kernel<13> : describe_kernel<RMAX>);
-                hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, d_frames, dp,
-                                   o->xy.as<uint32_t>(), d_n, o->pattern.as<int8_t>(), d_desc);
+                hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, o->xy.as<uint32_t>(), d_n,
+                                   o->pattern.as<int8_t>(), d_desc);
             }
         }
         MAGE_HIP(hipGetLastError());
@@ -1142,8 +1467,9 @@ mage_status mage_orb_create(const mage_orb_settings* settings, int device, mage_
     MAGE_REQUIRE(s.gaussian_kernel_size <= 1 || (s.gaussian_kernel_size % 2 == 1 && s.gaussian_kernel_size <= 15),
                  MAGE_EINVAL, "GaussianKernelSize must be odd and <= 15");
     MAGE_REQUIRE(s.num_cells_x >= 1 && s.num_cells_y >= 1, MAGE_EINVAL, "NumCells must be >= 1");
-    MAGE_REQUIRE(s.nlevels == 1, MAGE_EUNSUPPORTED, "NumLevels > 1 not implemented yet");
-    MAGE_REQUIRE(!s.use_orientation, MAGE_EUNSUPPORTED, "UseOrientation not implemented yet");
+    MAGE_REQUIRE(s.nlevels >= 1 && s.nlevels <= MAGE_MAX_LEVELS, MAGE_EUNSUPPORTED, "NumLevels must be 1..8");
+    MAGE_REQUIRE(s.nlevels == 1 || (s.scale_factor > 1.0f && std::isfinite(s.scale_factor)), MAGE_EINVAL,
+                 "ScaleFactor must be > 1");
     MAGE_REQUIRE(s.patch_size == 15 || s.patch_size == 31, MAGE_EUNSUPPORTED,
                  "only the pre-rotated patterns (PatchSize 15 / 31) are implemented");
     mage_status r = mage::bind_device(device);
@@ -1153,8 +1479,9 @@ mage_status mage_orb_create(const mage_orb_settings* settings, int device, mage_
     o->device = device;
     if (s.gaussian_kernel_size > 1) mage::gaussian_taps((int)s.gaussian_kernel_size, 2.0, o->taps);
     const int8_t* table = s.patch_size == 31 ? mage_bit_pattern_31_rotated : mage_bit_pattern_15_rotated;
+    // sampling radius: rotation 0 only, or all 30 rotations when orienting
     int R = 0;
-    for (int i = 0; i < 1024; i++) R = std::max(R, std::abs((int)table[i]));  // rotation 0
+    for (int i = 0; i < (s.use_orientation ? 30 : 1) * 1024; i++) R = std::max(R, std::abs((int)table[i]));
     o->R = R;
     if ((r = o->pattern.reserve(30 * 1024)) != MAGE_OK) {
         delete o;
@@ -1172,8 +1499,8 @@ mage_status mage_orb_create(const mage_orb_settings* settings, int device, mage_
 mage_status mage_orb_destroy(mage_orb* orb)
 {
     if (!orb) return MAGE_OK;
-    for (auto* b : {&orb->pattern, &orb->cand, &orb->counts, &orb->xy, &orb->status, &orb->img,
-                    &orb->kp, &orb->desc, &orb->n})
+    for (auto* b : {&orb->pattern, &orb->cand, &orb->counts, &orb->xy, &orb->status, &orb->img, &orb->kp,
+                    &orb->desc, &orb->n, &orb->blurred, &orb->pyr, &orb->rtab, &orb->lvl})
         b->release();
     delete orb;
     return MAGE_OK;

@@ -70,6 +70,14 @@ def _declare(L):
     L.oracle_gaussian_blur.argtypes = [vp, i32, i32, i32, i32, vp]
     L.oracle_gaussian_taps.argtypes = [i32, C.c_double, vp]
     L.oracle_orb_detect.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, u32, C.POINTER(u32)]
+    L.oracle_resize_linear.argtypes = [vp, i32, i32, i32, vp, i32, i32, i32]
+    L.oracle_fast_atan2.argtypes = [f32, f32]
+    L.oracle_fast_atan2.restype = f32
+    L.oracle_umax.argtypes = [i32, vp]
+    L.oracle_ic_angle.argtypes = [vp, i32, i32, i32, vp, i32]
+    L.oracle_ic_angle.restype = f32
+    L.oracle_level_geometry.argtypes = [i32, i32, i32, f32, vp, vp, vp]
+    L.oracle_features_per_level.argtypes = [i32, f32, i32, vp]
     L.oracle_orb_detect.restype = i32
     L.oracle_hamming.argtypes = [vp, vp]
     L.oracle_hamming.restype = i32
@@ -106,6 +114,45 @@ def default_settings(nfeatures: int = 440, **kw) -> OrbSettings:
 
 def pattern_table(patch: int) -> np.ndarray:
     return np.fromfile(DATA / f"bit_pattern_{patch}_rotated.bin", dtype=np.int8)
+
+
+def resize_linear(img: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    """OpenCV 3.4.0 resize(INTER_LINEAR) 8UC1 restatement (pyramid levels > 0)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_linear(_p(img), w, h, w, _p(out), dw, dh, dw)
+    return out
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return float(lib().oracle_fast_atan2(y, x))
+
+
+def umax(half_patch: int) -> np.ndarray:
+    out = np.zeros(half_patch + 2, np.int32)
+    lib().oracle_umax(half_patch, _p(out))
+    return out
+
+
+def ic_angle(img: np.ndarray, x: int, y: int, half_patch: int) -> float:
+    img = np.ascontiguousarray(img, np.uint8)
+    u = umax(half_patch)
+    return float(lib().oracle_ic_angle(_p(img), img.shape[1], x, y, _p(u), half_patch))
+
+
+def level_geometry(w: int, h: int, nlevels: int, scale_factor: float):
+    sc = np.zeros(nlevels, np.float32)
+    lw = np.zeros(nlevels, np.int32)
+    lh = np.zeros(nlevels, np.int32)
+    lib().oracle_level_geometry(w, h, nlevels, scale_factor, _p(sc), _p(lw), _p(lh))
+    return sc, lw, lh
+
+
+def features_per_level(nfeatures: int, scale_factor: float, nlevels: int) -> np.ndarray:
+    out = np.zeros(nlevels, np.int32)
+    lib().oracle_features_per_level(nfeatures, scale_factor, nlevels, _p(out))
+    return out
 
 
 def fast_score_map(img: np.ndarray, threshold: int = 4) -> np.ndarray:

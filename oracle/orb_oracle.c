@@ -11,7 +11,13 @@
  * the only data taken from the reference are the pre-rotated BRIEF tables
  * (OpenCVModified.cpp:74-138, extracted by tools/extract_patterns.py).  Third-party steps are
  * restated from their published algorithms:
- *   - OpenCV 3.4.0 GaussianBlur 8U (separable, kernel quantised to Q8, (s+2^15)>>16), and
+ *   - OpenCV 3.4.0 GaussianBlur 8U (separable, kernel quantised to Q8, (s+2^15)>>16),
+ *   - OpenCV 3.4.0 resize INTER_LINEAR 8U (fixed-point coefficients, SSE2 vertical pass; non-IPP
+ *     build) and fastAtan2 (polynomial atan in degrees), for NumLevels > 1 / UseOrientation,
+ *   - each pyramid level blurred as an isolated image (reflect-101 at its own borders; the
+ *     reference blurs ROIs of one packed buffer, so pixels within 3 px of an inner level edge
+ *     there depend on neighbouring levels or unwritten memory — never sampled when the border
+ *     exceeds the pattern radius by 4, as in the oriented rBRIEF-31 configuration), and
  *   - the canonical keypoint order (the reference's order depends on MSVC std::nth_element).
  * Build with -ffp-contract=off: the ANMS comparisons are float-exact.
  *
@@ -356,95 +362,284 @@ static void describe(const uint8_t* blurred, int stride, const signed char* patt
     }
 }
 
-/* OrbDetector::DetectAndCompute (OpenCVModified.cpp:771-886) for nlevels == 1 and patch 15/31.
- * Returns MAGE_OK and the count in *n_out. */
+static int cv_roundf(float v) { return (int)lrintf(v); }
+static int cv_floorf(float v) { int i = (int)v; return i - (i > v); }
+static int cv_ceilf(float v) { int i = (int)v; return i + (i < v); }
+
+/* cv::resize(src, dst, dsize, 0, 0, INTER_LINEAR) for CV_8UC1, OpenCV 3.4.0 resizeGeneric_ with
+ * HResizeLinear<uchar,int,short,2048> and VResizeLinear<uchar,int,short,FixedPtCast<..,22>> plus
+ * the SSE2 VResizeLinearVec_32s8u (imgproc/src/resize.cpp): coefficients are
+ * saturate_cast<short>(w * 2048); the horizontal pass is exact in int; the vector part of the
+ * vertical pass computes ((((S0>>4)*b0)>>16) + (((S1>>4)*b1)>>16) + 2) >> 2 for x below the
+ * last 16-wide / 4-wide block boundary, the scalar tail (S0*b0 + S1*b1 + 2^21) >> 22. */
+void oracle_resize_linear(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh,
+                          int dstride)
+{
+    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    int* xofs = (int*)malloc(sizeof(int) * dw);
+    short* ialpha = (short*)malloc(sizeof(short) * 2 * dw);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floorf(fx);
+        fx -= sx;
+        if (sx < 0) fx = 0, sx = 0;
+        if (sx + 1 >= sw) {
+            xmax = imin(xmax, dx);
+            if (sx >= sw - 1) fx = 0, sx = sw - 1;
+        }
+        xofs[dx] = sx;
+        ialpha[2 * dx] = (short)cv_roundf((1.f - fx) * 2048);
+        ialpha[2 * dx + 1] = (short)cv_roundf(fx * 2048);
+    }
+    int xv = 0;
+    while (xv <= dw - 16) xv += 16;
+    while (xv < dw - 4) xv += 4;
+    int* rows = (int*)malloc(sizeof(int) * 2 * dw);
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floorf(fy);
+        fy -= sy;
+        const int b0 = (short)cv_roundf((1.f - fy) * 2048), b1 = (short)cv_roundf(fy * 2048);
+        for (int k = 0; k < 2; k++) {
+            const uint8_t* S = src + (size_t)imin(imax(sy + k, 0), sh - 1) * sstride;
+            int* D = rows + k * dw;
+            for (int dx = 0; dx < dw; dx++) {
+                const int sx = xofs[dx];
+                D[dx] = dx < xmax ? S[sx] * ialpha[2 * dx] + S[sx + 1] * ialpha[2 * dx + 1] : S[sx] * 2048;
+            }
+        }
+        uint8_t* out = dst + (size_t)dy * dstride;
+        for (int x = 0; x < dw; x++) {
+            int v;
+            if (x < xv) {
+                const int s0 = (int)(short)(rows[x] >> 4), s1 = (int)(short)(rows[dw + x] >> 4);
+                v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+            } else {
+                v = (rows[x] * b0 + rows[dw + x] * b1 + (1 << 21)) >> 22;
+            }
+            out[x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+        }
+    }
+    free(xofs);
+    free(ialpha);
+    free(rows);
+}
+
+/* cv::fastAtan2 (OpenCV 3.4.0 core/src/mathfuncs_core: polynomial atan in degrees). */
+float oracle_fast_atan2(float y, float x)
+{
+    const float k = (float)(180 / 3.141592653589793);
+    const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+    const float eps = (float)2.2204460492503131e-16;
+    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+/* u_max of ComputeKeyPoints (OpenCVModified.cpp:671-686); umax must hold halfPatch + 2. */
+void oracle_umax(int halfPatchSize, int* umax)
+{
+    int v, v0, vmax = cv_floorf(halfPatchSize * sqrtf(2.f) / 2 + 1);
+    int vmin = cv_ceilf(halfPatchSize * sqrtf(2.f) / 2);
+    for (v = 0; v <= vmax; ++v) umax[v] = cv_round(sqrt((double)halfPatchSize * halfPatchSize - v * v));
+    for (v = halfPatchSize, v0 = 0; v >= vmin; --v) {
+        while (umax[v0] == umax[v0 + 1]) ++v0;
+        umax[v] = v0;
+        ++v0;
+    }
+}
+
+/* ICAngles (OpenCVModified.cpp:399-437) for one keypoint at integer level coordinates. */
+float oracle_ic_angle(const uint8_t* img, int stride, int x, int y, const int* umax, int half_k)
+{
+    const uint8_t* center = img + (ptrdiff_t)y * stride + x;
+    int m_01 = 0, m_10 = 0;
+    for (int u = -half_k; u <= half_k; ++u) m_10 += u * center[u];
+    for (int v = 1; v <= half_k; ++v) {
+        int v_sum = 0;
+        int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            int val_plus = center[u + v * stride], val_minus = center[u - v * stride];
+            v_sum += (val_plus - val_minus);
+            m_10 += u * (val_plus + val_minus);
+        }
+        m_01 += v * v_sum;
+    }
+    return oracle_fast_atan2((float)m_01, (float)m_10);
+}
+
+/* Pyramid geometry of DetectAndCompute (:785-804): layerScale = (float)pow(f, l) (getScale
+ * :564-567), level size (cvRound(cols/scale), cvRound(rows/scale)). */
+void oracle_level_geometry(int w, int h, int nlevels, float scale_factor, float* layer_scale, int* lw, int* lh)
+{
+    for (int l = 0; l < nlevels; l++) {
+        layer_scale[l] = (float)pow((double)scale_factor, (double)l);
+        lw[l] = cv_roundf((float)w / layer_scale[l]);
+        lh[l] = cv_roundf((float)h / layer_scale[l]);
+    }
+}
+
+/* nfeaturesPerLevel (ComputeKeyPoints :659-669), float arithmetic as written. */
+void oracle_features_per_level(int nfeatures, float scale_factor, int nlevels, int* per_level)
+{
+    float factor = 1.0f / scale_factor;
+    float nd = nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {
+        per_level[l] = cv_roundf(nd);
+        sum += per_level[l];
+        nd *= factor;
+    }
+    per_level[nlevels - 1] = imax(nfeatures - sum, 0);
+}
+
+typedef struct {
+    int x, y, level;
+    float strength;
+} level_kp;
+
+/* OrbDetector::DetectAndCompute (OpenCVModified.cpp:771-886) for patch 15/31: pyramid
+ * (resize INTER_LINEAR), per-level FAST + border + Retain + ANMS with the per-level budget,
+ * Insert truncation, ICAngles (UseOrientation), pt *= layerScale, per-level blur and the
+ * pre-rotated descriptors.  Returns MAGE_OK and the count in *n_out. */
 int oracle_orb_detect(const mage_orb_settings* s, const signed char* pattern_table,
                       const uint8_t* img, int w, int h, int stride, mage_keypoint* kp,
                       uint8_t* desc, uint32_t cap, uint32_t* n_out)
 {
     *n_out = 0;
     if (s->patch_size < 2) return MAGE_EINVAL;
-    if (s->nlevels != 1 || s->use_orientation) return MAGE_EUNSUPPORTED;
+    if (s->nlevels < 1 || s->nlevels > MAGE_MAX_LEVELS) return MAGE_EUNSUPPORTED;
     if (s->patch_size != 15 && s->patch_size != 31) return MAGE_EUNSUPPORTED;
     if (s->gaussian_kernel_size > 1 && (s->gaussian_kernel_size % 2) == 0) return MAGE_EINVAL;
 
+    const int L = (int)s->nlevels;
     const int nfeatures = (int)s->nfeatures;
     const int fastThreshold = (int)s->fast_threshold;
     const int halfPatch = (int)s->patch_size / 2;
-    const int border = halfPatch; /* no orientation: RunByImageBorder(halfPatchSize) :712 */
+    /* RunByImageBorder(halfPatchSize), or the hypotenuse when orienting (:711-712) */
+    const int border = s->use_orientation ? cv_ceilf(halfPatch * sqrtf(2.0f)) : halfPatch;
 
-    uint8_t* score = (uint8_t*)malloc((size_t)w * h);
-    int capc = (w / 2 + 2) * (h / 2 + 2);
-    cand_t* cand = (cand_t*)malloc(sizeof(cand_t) * capc);
-    int nc = fast_nms(img, w, h, stride, fastThreshold, score, cand);
-
-    /* RunByImageBorder (:619-639): keep b <= x < W-b, b <= y < H-b */
-    int m = 0;
-    if (h > border * 2 && w > border * 2) {
-        for (int i = 0; i < nc; i++)
-            if (cand[i].x >= border && cand[i].x < w - border && cand[i].y >= border && cand[i].y < h - border)
-                cand[m++] = cand[i];
+    float layerScale[MAGE_MAX_LEVELS];
+    int lw[MAGE_MAX_LEVELS], lh[MAGE_MAX_LEVELS], perLevel[MAGE_MAX_LEVELS];
+    uint8_t* lev[MAGE_MAX_LEVELS];
+    oracle_level_geometry(w, h, L, s->scale_factor, layerScale, lw, lh);
+    oracle_features_per_level(nfeatures, s->scale_factor, L, perLevel);
+    for (int l = 0; l < L; l++) {
+        lev[l] = (uint8_t*)malloc((size_t)lw[l] * lh[l] + 1);
+        if (l == 0)
+            for (int y = 0; y < h; y++) memcpy(lev[0] + (size_t)y * w, img + (size_t)y * stride, w);
+        else
+            oracle_resize_linear(lev[l - 1], lw[l - 1], lh[l - 1], lw[l - 1], lev[l], lw[l], lh[l], lw[l]);
     }
-    nc = m;
 
-    anms_item* items = (anms_item*)malloc(sizeof(anms_item) * (nc + 1));
-    anms_item* kept = (anms_item*)malloc(sizeof(anms_item) * (nc + 1));
-    int nk;
-    if (nc > nfeatures) {
-        int maxNum = (int)((float)nfeatures * s->feature_factor);
-        int cut = retain_cut(cand, nc, fastThreshold, maxNum, nfeatures, s->feature_strength);
-        int ni = 0;
-        for (int i = 0; i < nc; i++)
-            if (cand[i].score >= cut) {
-                items[ni].x = cand[i].x;
-                items[ni].y = cand[i].y;
-                items[ni].strength = (float)cand[i].score;
-                items[ni].r = 0;
-                items[ni].idx = ni;
-                ni++;
-            }
-        nk = anms(items, ni, nfeatures, fastThreshold, s, kept);
-    } else {
-        for (int i = 0; i < nc; i++) {
-            kept[i].x = cand[i].x;
-            kept[i].y = cand[i].y;
-            kept[i].strength = (float)cand[i].score;
-            kept[i].r = 0;
-            kept[i].idx = i;
+    level_kp* all = (level_kp*)malloc(sizeof(level_kp) * (cap + 1));
+    uint32_t nall = 0;
+    for (int l = 0; l < L && nall < cap; l++) {
+        const int W = lw[l], H = lh[l], N = perLevel[l];
+        uint8_t* score = (uint8_t*)malloc((size_t)W * H + 1);
+        int capc = (W / 2 + 2) * (H / 2 + 2);
+        cand_t* cand = (cand_t*)malloc(sizeof(cand_t) * capc);
+        int nc = fast_nms(lev[l], W, H, W, fastThreshold, score, cand);
+        /* RunByImageBorder (:619-639): keep b <= x < W-b, b <= y < H-b */
+        int m = 0;
+        if (H > border * 2 && W > border * 2) {
+            for (int i = 0; i < nc; i++)
+                if (cand[i].x >= border && cand[i].x < W - border && cand[i].y >= border && cand[i].y < H - border)
+                    cand[m++] = cand[i];
         }
-        nk = nc;
+        nc = m;
+        anms_item* items = (anms_item*)malloc(sizeof(anms_item) * (nc + 1));
+        anms_item* kept = (anms_item*)malloc(sizeof(anms_item) * (nc + 1));
+        int nk;
+        if (nc > N) {
+            int maxNum = (int)((float)N * s->feature_factor);
+            int cut = retain_cut(cand, nc, fastThreshold, maxNum, N, s->feature_strength);
+            int ni = 0;
+            for (int i = 0; i < nc; i++)
+                if (cand[i].score >= cut) {
+                    items[ni].x = cand[i].x;
+                    items[ni].y = cand[i].y;
+                    items[ni].strength = (float)cand[i].score;
+                    items[ni].r = 0;
+                    items[ni].idx = ni;
+                    ni++;
+                }
+            nk = anms(items, ni, N, fastThreshold, s, kept);
+        } else {
+            for (int i = 0; i < nc; i++) {
+                kept[i].x = cand[i].x;
+                kept[i].y = cand[i].y;
+                kept[i].strength = (float)cand[i].score;
+                kept[i].r = 0;
+                kept[i].idx = i;
+            }
+            nk = nc;
+        }
+        /* ImageData::Insert copies what still fits (ImageData.h:65-70) */
+        for (int i = 0; i < nk && nall < cap; i++, nall++) {
+            all[nall].x = kept[i].x;
+            all[nall].y = kept[i].y;
+            all[nall].level = l;
+            all[nall].strength = kept[i].strength;
+        }
+        free(score);
+        free(cand);
+        free(items);
+        free(kept);
     }
-    if ((uint32_t)nk > cap) nk = (int)cap; /* ImageData::Insert truncation (ImageData.h:65-70) */
 
-    /* keypoint fields: FAST emits KeyPoint(x, y, 7, -1, score) (:1508); ComputeKeyPoints sets
-     * octave/size (:713-717), angle = 0 without orientation (:748-754), pt *= 1 (:756-760). */
-    for (int i = 0; i < nk; i++) {
-        kp[i].x = (float)kept[i].x;
-        kp[i].y = (float)kept[i].y;
-        kp[i].size = (float)s->patch_size * 1.0f;
-        kp[i].angle = 0.0f;
-        kp[i].response = kept[i].strength;
-        kp[i].octave = 0;
+    /* keypoint fields: FAST emits KeyPoint(x, y, 7, -1, score) (:1508); octave / size
+     * (:713-717); angle by ICAngles on the unblurred level or 0 (:748-754); pt *= layerScale
+     * (:756-760). */
+    int umax[64];
+    if (s->use_orientation) oracle_umax(halfPatch, umax);
+    for (uint32_t i = 0; i < nall; i++) {
+        const level_kp* q = &all[i];
+        const float sc = layerScale[q->level];
+        kp[i].x = (float)q->x * sc;
+        kp[i].y = (float)q->y * sc;
+        kp[i].size = (float)s->patch_size * sc;
+        kp[i].angle = s->use_orientation ? oracle_ic_angle(lev[q->level], lw[q->level], q->x, q->y, umax, halfPatch) : 0.0f;
+        kp[i].response = q->strength;
+        kp[i].octave = q->level;
         kp[i].class_id = -1;
     }
-    *n_out = (uint32_t)nk;
+    *n_out = nall;
 
-    if (nk > 0) {
-        uint8_t* blurred = (uint8_t*)malloc((size_t)w * h);
-        if (s->gaussian_kernel_size > 1)
-            oracle_gaussian_blur(img, w, h, stride, (int)s->gaussian_kernel_size, blurred);
-        else
-            for (int y = 0; y < h; y++) memcpy(blurred + (size_t)y * w, img + (size_t)y * stride, w);
-        for (int i = 0; i < nk; i++) {
-            /* rot = cvRound(angle/12) % 30 with angle = 0 (:522) */
-            describe(blurred, w, pattern_table, kept[i].x, kept[i].y, 0, desc + 32 * (size_t)i);
+    if (nall > 0) {
+        uint8_t* blurred[MAGE_MAX_LEVELS];
+        for (int l = 0; l < L; l++) {
+            blurred[l] = (uint8_t*)malloc((size_t)lw[l] * lh[l] + 1);
+            if (s->gaussian_kernel_size > 1)
+                oracle_gaussian_blur(lev[l], lw[l], lh[l], lw[l], (int)s->gaussian_kernel_size, blurred[l]);
+            else
+                memcpy(blurred[l], lev[l], (size_t)lw[l] * lh[l]);
         }
-        free(blurred);
+        for (uint32_t i = 0; i < nall; i++) {
+            /* ComputeOrbDescriptorsPrerotated (:516-530): centre = cvRound(pt * (1.f/layerScale)),
+             * rot = cvRound(angle / 12) % 30 */
+            const int l = all[i].level;
+            const float sc = 1.f / layerScale[l];
+            const int cx = cv_roundf(kp[i].x * sc), cy = cv_roundf(kp[i].y * sc);
+            const int rot = cv_roundf(kp[i].angle / 12.0f) % 30;
+            describe(blurred[l], lw[l], pattern_table, cx, cy, rot, desc + 32 * (size_t)i);
+        }
+        for (int l = 0; l < L; l++) free(blurred[l]);
     }
-    free(score);
-    free(cand);
-    free(items);
-    free(kept);
+    for (int l = 0; l < L; l++) free(lev[l]);
+    free(all);
     return MAGE_OK;
 }
 

@@ -105,7 +105,9 @@ def test_rejects_bad_input(gpu):
     with pytest.raises(MageError):
         orb.OrbDetector(patchSize=1)
     with pytest.raises(MageError):
-        orb.OrbDetector(nlevels=4)
+        orb.OrbDetector(nlevels=9)
+    with pytest.raises(MageError):
+        orb.OrbDetector(nlevels=2, scaleFactor=1.0)
 
 
 def test_batch_device_equals_single(gpu):
@@ -146,3 +148,51 @@ def test_720p_properties(gpu):
     assert (kp["size"] == 15).all() and (kp["angle"] == 0).all() and (kp["class_id"] == -1).all()
     kp2, d2 = det.DetectAndCompute(img)
     assert np.array_equal(kp_bytes(kp), kp_bytes(kp2)) and np.array_equal(d, d2)  # deterministic
+
+
+# ------------------------- pyramid + orientation (the rBRIEF-31 variant) -------------
+
+
+@pytest.mark.parametrize("kw", [dict(nlevels=4, patchSize=31, useOrientation=True),
+                                dict(nlevels=4, patchSize=31, useOrientation=True, gaussianKernelSize=5),
+                                dict(nlevels=3, patchSize=31),
+                                dict(nlevels=2, patchSize=15, useOrientation=True, scaleFactor=1.2),
+                                dict(nlevels=1, patchSize=31, useOrientation=True),
+                                dict(nlevels=8, patchSize=31, useOrientation=True, scaleFactor=1.3)])
+@pytest.mark.parametrize("size", [(640, 480), (1280, 720), (333, 211)])
+def test_pyramid_orientation_matches_oracle(gpu, oracle, kw, size):
+    w, h = size
+    nfeat = 2000
+    det = orb.OrbDetector(nfeatures=nfeat, **kw)
+    m = {"nlevels": "nlevels", "patchSize": "patch_size", "useOrientation": "use_orientation",
+         "gaussianKernelSize": "gaussian_kernel_size", "scaleFactor": "scale_factor"}
+    s = oracle.default_settings(nfeat, **{m[k]: v for k, v in kw.items()})
+    for t in (0, 5):
+        img = synth.frame(t, w, h)
+        kp, d = det.DetectAndCompute(img)
+        st, okp, od = oracle.orb_detect(img, s)
+        assert st == 0
+        assert len(kp) == len(okp), (kw, size, t)
+        assert np.array_equal(kp_bytes(kp), kp_bytes(okp)), (kw, size, t)
+        assert np.array_equal(d, od), (kw, size, t)
+
+
+def test_pyramid_batch_device_equals_single(gpu):
+    import torch
+
+    w, h, B, cap = 640, 480, 5, 2000
+    frames = torch.empty((B, h, w), dtype=torch.uint8, device="cuda")
+    orb.synth_frames_device(frames, B, w, h, 3, synth.FRAME_SEED)
+    det = orb.OrbDetector(nfeatures=cap, nlevels=4, patchSize=31, useOrientation=True)
+    kp = torch.zeros((B, cap * 28), dtype=torch.uint8, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    det.detect_and_compute_batch_device(frames, w, h, kp, desc, n, cap)
+    torch.cuda.synchronize()
+    host = frames.cpu().numpy()
+    for i in range(B):
+        k1, d1 = det.DetectAndCompute(host[i])
+        ni = int(n[i])
+        assert ni == len(k1)
+        assert np.array_equal(kp[i, : ni * 28].cpu().numpy(), kp_bytes(k1))
+        assert np.array_equal(desc[i, :ni].cpu().numpy(), d1)

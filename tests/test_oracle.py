@@ -118,8 +118,68 @@ def test_orb_invariants(oracle):
     # retained responses are bounded below by the fast threshold
     assert (kp["response"] >= 4).all()
     # oracle status codes: unsupported variants are reported, not approximated
-    assert oracle.orb_detect(img, oracle.default_settings(440, nlevels=3))[0] == 4
+    assert oracle.orb_detect(img, oracle.default_settings(440, nlevels=9))[0] == 4
     assert oracle.orb_detect(img, oracle.default_settings(440, patch_size=1))[0] == 1
+
+
+def test_pyramid_known_answers(oracle):
+    # level geometry and budgets of the rBRIEF-31 variant at 720p (ComputeKeyPoints :659-669)
+    sc, lw, lh = oracle.level_geometry(1280, 720, 4, 1.5)
+    assert sc.tolist() == [1.0, 1.5, 2.25, 3.375]
+    assert lw.tolist() == [1280, 853, 569, 379] and lh.tolist() == [720, 480, 320, 213]
+    assert oracle.features_per_level(2000, 1.5, 4).tolist() == [831, 554, 369, 246]
+    assert oracle.features_per_level(440, 1.5, 1).tolist() == [440]
+    # u_max of OpenCV ORB for halfPatchSize 15 (the circular patch of ICAngles)
+    assert oracle.umax(15)[:16].tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+
+
+def test_resize_linear_properties(oracle):
+    rng = np.random.default_rng(11)
+    img = rng.integers(0, 256, (37, 53), dtype=np.uint8)
+    # same size: coefficients (2048, 0) reproduce the input through both fixed-point passes
+    assert np.array_equal(oracle.resize_linear(img, 53, 37), img)
+    # a constant image stays constant at any scale
+    flat = np.full((40, 60), 173, np.uint8)
+    assert (oracle.resize_linear(flat, 27, 17) == 173).all()
+    # exact 2x downscale of a 2x2-block image returns the blocks
+    blocks = rng.integers(0, 256, (20, 30), dtype=np.uint8)
+    big = np.repeat(np.repeat(blocks, 2, 0), 2, 1)
+    assert np.array_equal(oracle.resize_linear(big, 30, 20), blocks)
+
+
+def test_fast_atan2_accuracy(oracle):
+    rng = np.random.default_rng(5)
+    for y, x in rng.integers(-5000, 5000, (200, 2)):
+        a = oracle.fast_atan2(float(y), float(x))
+        ref = np.degrees(np.arctan2(y, x)) % 360
+        d = abs(a - ref)
+        assert min(d, 360 - d) < 0.02
+        assert 0.0 <= a <= 360.0
+    assert oracle.fast_atan2(0.0, 1.0) == 0.0 and oracle.fast_atan2(1.0, 0.0) == 90.0
+
+
+def test_ic_angle_direction(oracle):
+    # a brightness ramp along +x has its intensity centroid at angle ~0, along +y at ~90
+    x = np.arange(64, dtype=np.float64)
+    ramp = np.tile(x * 3, (64, 1)).astype(np.uint8)
+    assert abs(oracle.ic_angle(ramp, 32, 32, 15)) < 0.5 or abs(oracle.ic_angle(ramp, 32, 32, 15) - 360) < 0.5
+    assert abs(oracle.ic_angle(ramp.T.copy(), 32, 32, 15) - 90) < 0.5
+
+
+def test_orb_pyramid_invariants(oracle):
+    img = synth.frame(2, 640, 480)
+    s = oracle.default_settings(2000, nlevels=4, patch_size=31, use_orientation=1)
+    st, kp, d = oracle.orb_detect(img, s)
+    assert st == 0 and len(kp) == 2000
+    per = oracle.features_per_level(2000, 1.5, 4)
+    assert np.bincount(kp["octave"], minlength=4).tolist() == per.tolist()
+    # level order, sizes and the oriented border (cvCeil(15 sqrt 2) = 22 in level coordinates)
+    assert (np.diff(kp["octave"]) >= 0).all()
+    sc = np.array([1.0, 1.5, 2.25, 3.375], np.float32)
+    assert np.array_equal(kp["size"], np.float32(31) * sc[kp["octave"]])
+    lx = np.rint(kp["x"] / sc[kp["octave"]])
+    assert (lx >= 22).all()
+    assert ((kp["angle"] >= 0) & (kp["angle"] <= 360)).all()
 
 
 def test_blur_flat_and_border(oracle):
