@@ -498,6 +498,286 @@ __global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict_
     }
 }
 
+// Register-resident tiled Cholesky + solve for np <= 240 (the usual local-BA window: 40 free
+// keyframes -> n = 240; larger systems use cholesky_solve).  S = U^T U in upper form: the upper 16x16 tiles (i <= j) of S live in
+// the f64 MFMA accumulator layout of 8 waves (tile t = row-major upper index, wave t % 8, slot
+// t / 8; lane l holds rows (l >> 4) + 4r, column l & 15).  Every product then sums over a
+// tile's row index, which is exactly the B operand of v_mfma_f64_16x16x4f64 taken from those
+// registers (k-step q = register q):
+//   TRSM  U_kj = inv(L_kk) A_kj            (A operand inv(L_kk) from LDS; L = U^T)
+//   SYRK  A_ij -= U_ki^T U_kj, k < i <= j  (both operands from the LDS panel of row-block k)
+// Step k: the owner of tile (k, k) factors it (Cholesky + triangular inverse in one wave) ->
+// barrier -> TRSM of row-block k into the double-buffered panel -> barrier -> SYRK.  Nothing
+// of S leaves the chip between steps; the solves use the per-block inverses kept in LDS.
+#ifndef MAGE_CHOL_ABLATE  // timing experiments only (tools/ablate_ba.py); 0 in the product
+#define MAGE_CHOL_ABLATE 0
+#endif
+constexpr int CT_WAVES = 8;   // 2 per SIMD: 256 VGPRs hold 18 resident tiles + the block factor
+constexpr int CT_THREADS = CT_WAVES * kWave;
+constexpr int CT_TPW = 15;    // tiles per wave: 8 x 15 = 120 upper tiles of np = 240
+constexpr int CT_MAXT = 15;
+
+// Broadcast of lane l's double (two v_readlane_b32: scalar result, no LDS crossbar).
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(u & 0xFFFFFFFFull), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ int upper_tile_index(int i, int j, int mt) { return i * mt - i * (i - 1) / 2 + (j - i); }
+
+__global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restrict__ S, int np, int n,
+                                                         const double* __restrict__ b, double* __restrict__ x,
+                                                         int* __restrict__ fail)
+{
+    __shared__ double invL[CT_MAXT][16][17];      // inverse of L_kk = U_kk^T per diagonal block
+    __shared__ double pan[2][CT_MAXT][16][17];    // U row-block k tiles (k, j); [.][k] = scratch
+    __shared__ double vb[CT_MAXT * 16];           // b -> y -> x
+    __shared__ double yk[16];                     // y_k of the current block
+    __shared__ double red[CT_WAVES][16][17];      // per-wave row-reduction scratch (backward solve)
+    __shared__ int s_fail;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: tile bookkeeping on the SALU
+    const int mt = np >> 4, T = mt * (mt + 1) / 2;
+    const int lr = lane >> 4, lc = lane & 15;  // accumulator layout: rows lr + 4r, column lc
+
+    // tile coordinates of each slot (wave uniform, scalar registers)
+    int tI[CT_TPW], tJ[CT_TPW];
+    {
+        int i = 0, rowend = mt;  // tiles [rowend - (mt - i), rowend) are row i
+        for (int sl = 0; sl < CT_TPW; sl++) {
+            const int t = wave + CT_WAVES * sl;
+            while (i < mt && t >= rowend) {
+                i++;
+                rowend += mt - i;
+            }
+            tI[sl] = t < T ? i : mt;  // mt: no tile
+            tJ[sl] = t < T ? i + (t - (rowend - (mt - i))) : mt;
+        }
+    }
+    auto tile_of = [&](int sl, int& ti, int& tj) {
+        ti = tI[sl];
+        tj = tJ[sl];
+    };
+    dbl4 C[CT_TPW];
+#pragma unroll
+    for (int sl = 0; sl < CT_TPW; sl++) {
+        int ti, tj;
+        tile_of(sl, ti, tj);
+        if (ti < mt) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = 16 * ti + lr + 4 * r, col = 16 * tj + lc;
+                C[sl][r] = (row < n && col < n) ? S[(long long)row * np + col] : (row == col ? 1.0 : 0.0);
+            }
+        } else {
+            C[sl] = dbl4{0, 0, 0, 0};
+        }
+    }
+    if (tid == 0) s_fail = 0;
+    for (int i = tid; i < np; i += CT_THREADS) vb[i] = i < n ? b[i] : 0.0;
+    long long tm[6] = {0, 0, 0, 0, 0, 0}, t0 = 0;  // MAGE_CHOL_ABLATE == 3: phase cycles of wave 0
+    auto tick = [&](int ph) {
+        if (MAGE_CHOL_ABLATE == 3) {
+            const long long t = __builtin_amdgcn_s_memtime();
+            if (ph >= 0) tm[ph] += t - t0;
+            t0 = t;
+        }
+    };
+    tick(-1);
+    __syncthreads();
+    tick(0);
+
+    for (int k = 0; k < mt; k++) {
+        const int buf = k & 1;
+        // --- diagonal block: Cholesky of A_kk and inv(L_kk), by its owner wave ---
+        const int tkk = upper_tile_index(k, k, mt);
+        if (wave == tkk % CT_WAVES) {
+            const int slot = tkk / CT_WAVES;
+            double(*D)[17] = pan[buf][k];
+#pragma unroll
+            for (int sl = 0; sl < CT_TPW; sl++)
+                if (sl == slot)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) D[lr + 4 * r][lc] = C[sl][r];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // lanes 0-15: row l of L (lower), right-looking Cholesky of the 16x16 block; column
+            // values are broadcast with v_readlane (scalar), one reciprocal per column
+            const int l = lane;
+            if (MAGE_CHOL_ABLATE == 2) {
+                if (l < 16)
+                    for (int q = 0; q < 16; q++) invL[k][l][q] = (q == l) ? 1.0 / sqrt(D[l][l]) : 0.0;
+            } else {
+                double a[16], rd[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) a[q] = (l < 16 && q <= l) ? D[q][l] : 0.0;  // A[l][q] = A[q][l]
+                bool bad = false;
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const double djj = readlane_f64(a[j], j);
+                    if (!(djj > 0)) bad = true;
+                    // 1/sqrt by v_rsq_f64 + two Newton steps (no f64 sqrt / division sequence on
+                    // the column's critical path); d = djj / sqrt(djj)
+                    double r = __builtin_amdgcn_rsq(djj);
+                    r = r * (1.5 - 0.5 * djj * r * r);
+                    r = r * (1.5 - 0.5 * djj * r * r);
+                    rd[j] = r;
+                    const double d = djj * r;
+                    a[j] = (l == j) ? d : a[j] * r;
+#pragma unroll
+                    for (int q = j + 1; q < 16; q++) {
+                        const double lqj = readlane_f64(a[j], q);
+                        if (l >= q) a[q] -= a[j] * lqj;
+                    }
+                }
+                if (l == 0 && bad) s_fail = 1;
+                if (l < 16)
+#pragma unroll
+                    for (int q = 0; q < 16; q++) D[l][q] = q <= l ? a[q] : 0.0;  // D := L_kk
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // inv(L_kk), column c = lane & 15: right-looking forward substitution L X = I
+                // (L[m][q] are wave-uniform LDS broadcasts; critical path one FMA + one multiply
+                // per column)
+                const int c = lane & 15;
+                double xc[16];
+#pragma unroll
+                for (int m = 0; m < 16; m++) xc[m] = (m == c) ? 1.0 : 0.0;
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    xc[q] *= rd[q];
+#pragma unroll
+                    for (int m = q + 1; m < 16; m++) xc[m] -= D[m][q] * xc[q];
+                }
+                if (lane < 16)
+#pragma unroll
+                    for (int m = 0; m < 16; m++) invL[k][m][c] = xc[m];
+                // forward substitution fused into the factorisation: vb_k has received every
+                // update from the blocks above, so y_k = inv(L_kk) vb_k (lane c: sum over m of
+                // X[c][m]... computed as column sums of X^T by the 16-lane reduction below)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < 16) {
+                    double y = 0;
+#pragma unroll
+                    for (int m = 0; m < 16; m++) y += invL[k][lane][m] * vb[16 * k + m];
+                    yk[lane] = y;
+                }
+            }
+            // U_kk = L_kk^T into the owner's register tile (kept for nothing but symmetry)
+#pragma unroll
+            for (int sl = 0; sl < CT_TPW; sl++)
+                if (sl == slot)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) C[sl][r] = D[lc][lr + 4 * r];
+        }
+        tick(1);
+        __syncthreads();
+        tick(2);
+        if (s_fail) break;
+        // --- TRSM: U_kj = inv(L_kk) A_kj for the owned tiles of row-block k ---
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++) {
+            int ti, tj;
+            tile_of(sl, ti, tj);
+            if (ti == k && tj > k) {
+                dbl4 acc = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(invL[k][lc][4 * q + lr], C[sl][q], acc, 0, 0, 0);
+                C[sl] = acc;
+#pragma unroll
+                for (int r = 0; r < 4; r++) pan[buf][tj][lr + 4 * r][lc] = acc[r];
+                // forward substitution: vb_j -= U_kj^T y_k (tile (k, j) is the only writer of vb_j
+                // in this step)
+                double pacc = 0;
+#pragma unroll
+                for (int r = 0; r < 4; r++) pacc += acc[r] * yk[lr + 4 * r];
+                pacc += __shfl_xor(pacc, 16);
+                pacc += __shfl_xor(pacc, 32);
+                if (lr == 0) vb[16 * tj + lc] -= pacc;
+            }
+        }
+        if (tid < 16) vb[16 * k + tid] = yk[tid];
+        tick(3);
+        __syncthreads();
+        tick(2);
+        // --- SYRK: A_ij -= U_ki^T U_kj for the owned tiles with k < i <= j ---
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++) {
+            int i, j;
+            tile_of(sl, i, j);
+            if (i > k && i < mt) {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pan[buf][i][4 * q + lr][lc], pan[buf][j][4 * q + lr][lc],
+                                                                C[sl], 0, 0, 0);
+            }
+        }
+        tick(4);
+    }
+    if (s_fail) {
+        if (tid == 0) *fail = 1;
+        return;
+    }
+    // --- backward: U x = y, x_k = inv(U_kk) (y_k - sum_{j>k} U_kj x_j), right-looking with
+    // one barrier per block: the owner of tile (k-1, k) applies the last update of y_{k-1} and
+    // then solves block k-1 itself ---
+    auto solve_block = [&](int k) {  // by one wave: vb_k := inv(U_kk) vb_k, inv(U) = inv(L)^T
+        double xv = 0;
+        if (lane < 16) {
+#pragma unroll
+            for (int c = 0; c < 16; c++) xv += invL[k][c][lane] * vb[16 * k + c];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 16) vb[16 * k + lane] = xv;
+    };
+    if (mt > 0 && wave == 0) solve_block(mt - 1);
+    __syncthreads();
+    for (int k = mt - 1; k >= 1; k--) {
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++) {
+            int ti, tj;
+            tile_of(sl, ti, tj);
+            if (tj == k && ti < k) {
+                // (U_ik x_k)[r] = sum_c U_ik[r][c] x_k[c]: products through the wave's LDS
+                // scratch, row sums by lanes 0-15
+                const double xk = vb[16 * k + lc];
+                double(*P)[17] = red[wave];
+#pragma unroll
+                for (int r = 0; r < 4; r++) P[lr + 4 * r][lc] = C[sl][r] * xk;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < 16) {
+                    double sum = 0;
+#pragma unroll
+                    for (int c = 0; c < 16; c++) sum += P[lane][c];
+                    vb[16 * ti + lane] -= sum;
+                }
+                if (ti == k - 1) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    solve_block(k - 1);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    tick(5);
+    for (int i = tid; i < np; i += CT_THREADS) x[i] = i < n ? vb[i] : 0.0;
+    if (MAGE_CHOL_ABLATE == 3 && tid == 0)
+        printf("chol_tiles np=%d cycles: load %lld diag %lld barrier %lld trsm %lld syrk %lld backward %lld\n", np, tm[0],
+               tm[1], tm[2], tm[3], tm[4], tm[5]);
+}
+
 // xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]); also the point part of computeScale.
 __global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const double* __restrict__ Hpl,
                                                             const double* __restrict__ Dinv,
@@ -898,8 +1178,12 @@ struct BundleAdjuster {
             }
             {
                 KernelTimer _kt("ba.cholesky_solve", st);
-                hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np, n,
-                                   d_rhs.as<double>(), xp, d_fail.as<int>());
+                if (np <= 16 * CT_MAXT)
+                    hipLaunchKernelGGL(chol_tiles, dim3(1), dim3(CT_THREADS), 0, st, d_S.as<double>(), np, n,
+                                       d_rhs.as<double>(), xp, d_fail.as<int>());
+                else
+                    hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np, n,
+                                       d_rhs.as<double>(), xp, d_fail.as<int>());
             }
         }
         if (P > 0) {
