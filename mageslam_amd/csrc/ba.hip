@@ -259,10 +259,13 @@ __global__ __launch_bounds__(BA_THREADS) void point_schur(int P, const int* __re
 // One covisible camera pair (h1 <= h2) per workgroup (BlockSolver::solve Schur loop):
 //   S[h1][h2] = delta(h1,h2) (Hpp_c1 + lambda I) - sum_p Hpl_{c1 p} Dinv_p Hpl_{c2 p}^T
 //   rhs[h1]   = bp_c1 - sum_p Hpl_{c1 p} Dinv_p bl_p                          (h1 == h2 only)
-// The shared points come from intersecting c1's point-sorted edges with c2's by binary
-// search; each thread accumulates its 6x6 partial in registers (no atomics, deterministic).
+// The shared points come from walking c1's point-sorted edges and looking each point up in
+// c2's row of the block x point index (first position of the point in c2's list, -1 if c2 does
+// not see it): one dependent load instead of a binary search.  Each thread accumulates its 6x6
+// partial in registers (no atomics, deterministic).
 __global__ __launch_bounds__(BA_THREADS) void schur_pairs(Problem pb, const int2* __restrict__ pairs,
                                                           const int* __restrict__ cam_of_block,
+                                                          const int* __restrict__ blkidx,
                                                           const double* __restrict__ Hpp,
                                                           const double* __restrict__ bp,
                                                           const double* __restrict__ Hpl,
@@ -279,19 +282,13 @@ __global__ __launch_bounds__(BA_THREADS) void schur_pairs(Problem pb, const int2
     double acc[42];
 #pragma unroll
     for (int k = 0; k < 42; k++) acc[k] = 0;
-    const int b0 = pb.cstart[c2], b1 = pb.cstart[c2 + 1];
+    const int b1 = pb.cstart[c2 + 1];
+    const int* __restrict__ idx2 = blkidx + (long long)h2 * pb.P;
     for (int a = pb.cstart[c1] + threadIdx.x; a < pb.cstart[c1 + 1]; a += BA_THREADS) {
         const int e1 = pb.cedges[a];
         const int p = pb.cpt[a];
-        if (!pb.active[e1] || !pb.ptfree[p]) continue;
-        // first index in c2's list with point >= p
-        int lo = b0, hi = b1;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pb.cpt[mid] < p) lo = mid + 1;
-            else hi = mid;
-        }
-        if (lo >= b1 || pb.cpt[lo] != p) continue;
+        const int lo = idx2[p];
+        if (lo < 0 || !pb.active[e1] || !pb.ptfree[p]) continue;
         const double* W1 = Hpl + 18 * (long long)e1;
         const double* Di = Dinv + 9 * (long long)p;
         double Z[18];  // W1 * Dinv (6x3)
@@ -535,7 +532,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     __shared__ double invL[CT_MAXT][16][17];      // inverse of L_kk = U_kk^T per diagonal block
     __shared__ double pan[2][CT_MAXT][16][17];    // U row-block k tiles (k, j); [.][k] = scratch
     __shared__ double vb[CT_MAXT * 16];           // b -> y -> x
-    __shared__ double yk[16];                     // y_k of the current block
+    __shared__ double yk[2][16];                  // y_k, double-buffered (look-ahead factor)
     __shared__ double red[CT_WAVES][16][17];      // per-wave row-reduction scratch (backward solve)
     __shared__ int s_fail;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -590,96 +587,98 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     __syncthreads();
     tick(0);
 
-    for (int k = 0; k < mt; k++) {
-        const int buf = k & 1;
-        // --- diagonal block: Cholesky of A_kk and inv(L_kk), by its owner wave ---
-        const int tkk = upper_tile_index(k, k, mt);
-        if (wave == tkk % CT_WAVES) {
-            const int slot = tkk / CT_WAVES;
-            double(*D)[17] = pan[buf][k];
+    // --- diagonal block: Cholesky of A_kk and inv(L_kk) by its owner wave (slot `slot`), with
+    // D = pan[dbuf][k] as scratch (row-block k's panel never uses its own column k) ---
+    auto factor_diag = [&](int k, int slot, int dbuf) {
+        double(*D)[17] = pan[dbuf][k];
 #pragma unroll
-            for (int sl = 0; sl < CT_TPW; sl++)
-                if (sl == slot)
+        for (int sl = 0; sl < CT_TPW; sl++)
+            if (sl == slot)
 #pragma unroll
-                    for (int r = 0; r < 4; r++) D[lr + 4 * r][lc] = C[sl][r];
+                for (int r = 0; r < 4; r++) D[lr + 4 * r][lc] = C[sl][r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int l = lane;
+        double* y_out = yk[k & 1];
+        if (MAGE_CHOL_ABLATE == 2) {
+            if (l < 16)
+                for (int q = 0; q < 16; q++) invL[k][l][q] = (q == l) ? 1.0 / sqrt(D[l][l]) : 0.0;
+            if (l < 16) y_out[l] = 0;
+        } else {
+            // lanes 0-15: row l of L (lower), right-looking Cholesky of the 16x16 block; column
+            // values are broadcast with v_readlane (scalar).  Entries above the diagonal and the
+            // lanes >= 16 hold zeros, which every update keeps at zero, so no lane masks.
+            double a[16], rd[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) a[q] = (l < 16 && q <= l) ? D[q][l] : 0.0;  // A[l][q] = A[q][l]
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const double djj = readlane_f64(a[j], j);
+                if (!(djj > 0)) bad = true;
+                // 1/sqrt by v_rsq_f64 + two Newton steps (no f64 sqrt / division sequence on
+                // the column's critical path); d = djj / sqrt(djj)
+                const double h = 0.5 * djj;
+                double r = __builtin_amdgcn_rsq(djj);
+                r *= __builtin_fma(-h * r, r, 1.5);
+                r *= __builtin_fma(-h * r, r, 1.5);
+                rd[j] = r;
+                a[j] = (l == j) ? djj * r : a[j] * r;
+#pragma unroll
+                for (int q = j + 1; q < 16; q++) a[q] = __builtin_fma(-a[j], readlane_f64(a[j], q), a[q]);
+            }
+            if (l == 0 && bad) s_fail = 1;
+            if (l < 16)
+#pragma unroll
+                for (int q = 0; q < 16; q++) D[l][q] = a[q];  // D := L_kk
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // lanes 0-15: row l of L (lower), right-looking Cholesky of the 16x16 block; column
-            // values are broadcast with v_readlane (scalar), one reciprocal per column
-            const int l = lane;
-            if (MAGE_CHOL_ABLATE == 2) {
-                if (l < 16)
-                    for (int q = 0; q < 16; q++) invL[k][l][q] = (q == l) ? 1.0 / sqrt(D[l][l]) : 0.0;
-            } else {
-                double a[16], rd[16];
+            // inv(L_kk), column c = lane & 15: right-looking forward substitution L X = I
+            // (L[m][q] are wave-uniform LDS broadcasts)
+            const int c = lane & 15;
+            double xc[16];
 #pragma unroll
-                for (int q = 0; q < 16; q++) a[q] = (l < 16 && q <= l) ? D[q][l] : 0.0;  // A[l][q] = A[q][l]
-                bool bad = false;
+            for (int m = 0; m < 16; m++) xc[m] = (m == c) ? 1.0 : 0.0;
 #pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    const double djj = readlane_f64(a[j], j);
-                    if (!(djj > 0)) bad = true;
-                    // 1/sqrt by v_rsq_f64 + two Newton steps (no f64 sqrt / division sequence on
-                    // the column's critical path); d = djj / sqrt(djj)
-                    double r = __builtin_amdgcn_rsq(djj);
-                    r = r * (1.5 - 0.5 * djj * r * r);
-                    r = r * (1.5 - 0.5 * djj * r * r);
-                    rd[j] = r;
-                    const double d = djj * r;
-                    a[j] = (l == j) ? d : a[j] * r;
+            for (int q = 0; q < 16; q++) {
+                xc[q] *= rd[q];
 #pragma unroll
-                    for (int q = j + 1; q < 16; q++) {
-                        const double lqj = readlane_f64(a[j], q);
-                        if (l >= q) a[q] -= a[j] * lqj;
-                    }
-                }
-                if (l == 0 && bad) s_fail = 1;
-                if (l < 16)
-#pragma unroll
-                    for (int q = 0; q < 16; q++) D[l][q] = q <= l ? a[q] : 0.0;  // D := L_kk
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                // inv(L_kk), column c = lane & 15: right-looking forward substitution L X = I
-                // (L[m][q] are wave-uniform LDS broadcasts; critical path one FMA + one multiply
-                // per column)
-                const int c = lane & 15;
-                double xc[16];
-#pragma unroll
-                for (int m = 0; m < 16; m++) xc[m] = (m == c) ? 1.0 : 0.0;
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    xc[q] *= rd[q];
-#pragma unroll
-                    for (int m = q + 1; m < 16; m++) xc[m] -= D[m][q] * xc[q];
-                }
-                if (lane < 16)
-#pragma unroll
-                    for (int m = 0; m < 16; m++) invL[k][m][c] = xc[m];
-                // forward substitution fused into the factorisation: vb_k has received every
-                // update from the blocks above, so y_k = inv(L_kk) vb_k (lane c: sum over m of
-                // X[c][m]... computed as column sums of X^T by the 16-lane reduction below)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (lane < 16) {
-                    double y = 0;
-#pragma unroll
-                    for (int m = 0; m < 16; m++) y += invL[k][lane][m] * vb[16 * k + m];
-                    yk[lane] = y;
-                }
+                for (int m = q + 1; m < 16; m++) xc[m] = __builtin_fma(-D[m][q], xc[q], xc[m]);
             }
-            // U_kk = L_kk^T into the owner's register tile (kept for nothing but symmetry)
+            if (lane < 16)
 #pragma unroll
-            for (int sl = 0; sl < CT_TPW; sl++)
-                if (sl == slot)
+                for (int m = 0; m < 16; m++) invL[k][m][c] = xc[m];
+            // forward substitution fused into the factorisation: vb_k has received every update
+            // from the blocks above, so y_k = inv(L_kk) vb_k
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < 16) {
+                double y = 0;
 #pragma unroll
-                    for (int r = 0; r < 4; r++) C[sl][r] = D[lc][lr + 4 * r];
+                for (int m = 0; m < 16; m++) y = __builtin_fma(invL[k][lane][m], vb[16 * k + m], y);
+                y_out[lane] = y;
+            }
         }
-        tick(1);
-        __syncthreads();
-        tick(2);
+        // U_kk = L_kk^T into the owner's register tile
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++)
+            if (sl == slot)
+#pragma unroll
+                for (int r = 0; r < 4; r++) C[sl][r] = D[lc][lr + 4 * r];
+    };
+    if (mt > 0 && wave == 0) factor_diag(0, 0, 0);  // tile (0, 0) is tile 0: wave 0, slot 0
+    tick(1);
+    __syncthreads();
+    tick(2);
+
+    // Step k: TRSM of row-block k -> barrier -> SYRK, during which the owner of tile (k+1, k+1)
+    // updates that tile first and factors it (look-ahead: the serial block factor overlaps the
+    // other waves' SYRK) -> barrier.
+    for (int k = 0; k < mt; k++) {
+        const int buf = k & 1;
         if (s_fail) break;
         // --- TRSM: U_kj = inv(L_kk) A_kj for the owned tiles of row-block k ---
 #pragma unroll
@@ -698,29 +697,41 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 // in this step)
                 double pacc = 0;
 #pragma unroll
-                for (int r = 0; r < 4; r++) pacc += acc[r] * yk[lr + 4 * r];
+                for (int r = 0; r < 4; r++) pacc = __builtin_fma(acc[r], yk[buf][lr + 4 * r], pacc);
                 pacc += __shfl_xor(pacc, 16);
                 pacc += __shfl_xor(pacc, 32);
                 if (lr == 0) vb[16 * tj + lc] -= pacc;
             }
         }
-        if (tid < 16) vb[16 * k + tid] = yk[tid];
+        if (tid < 16) vb[16 * k + tid] = yk[buf][tid];
         tick(3);
         __syncthreads();
         tick(2);
         // --- SYRK: A_ij -= U_ki^T U_kj for the owned tiles with k < i <= j ---
+        auto syrk = [&](int sl) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pan[buf][tI[sl]][4 * q + lr][lc], pan[buf][tJ[sl]][4 * q + lr][lc],
+                                                            C[sl], 0, 0, 0);
+        };
+        const int kn = k + 1, tnn = upper_tile_index(kn, kn, mt);
+        if (kn < mt && wave == tnn % CT_WAVES) {
+            const int slot = tnn / CT_WAVES;
+#pragma unroll
+            for (int sl = 0; sl < CT_TPW; sl++)
+                if (sl == slot) syrk(sl);
+            tick(4);
+            factor_diag(kn, slot, buf ^ 1);
+            tick(1);
+        }
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++) {
-            int i, j;
-            tile_of(sl, i, j);
-            if (i > k && i < mt) {
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pan[buf][i][4 * q + lr][lc], pan[buf][j][4 * q + lr][lc],
-                                                                C[sl], 0, 0, 0);
-            }
+            const int i = tI[sl], j = tJ[sl];
+            if (i > k && i < mt && !(i == kn && j == kn)) syrk(sl);
         }
         tick(4);
+        __syncthreads();
+        tick(2);
     }
     if (s_fail) {
         if (tid == 0) *fail = 1;
@@ -939,12 +950,27 @@ struct BundleAdjuster {
     int npairs = 0;
     std::vector<int> camh, ptfree, cam_of_block;
     hipStream_t st = nullptr;
+    // Control block read back at every host decision (one pinned copy per synchronisation):
+    // doubles [0,3) linearisation chi2 / max diag, [3,6) trial, [6,9) outlier pass, then the
+    // Cholesky failure flag and the outlier count as 32-bit words.
+    static constexpr int CTL_DOUBLES = 16, CTL_FAIL = 10, CTL_COUNT = 11;
+    double* h_ctl = nullptr;
+    int* d_failp() const { return reinterpret_cast<int*>(d_red.as<double>() + CTL_FAIL); }
+    uint32_t* d_countp() const { return reinterpret_cast<uint32_t*>(d_red.as<double>() + CTL_COUNT); }
+    mage_status read_ctl()
+    {
+        MAGE_HIP(hipMemcpyAsync(h_ctl, d_red.ptr, CTL_DOUBLES * sizeof(double), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        return MAGE_OK;
+    }
+    int ctl_fail() const { return *reinterpret_cast<const int*>(h_ctl + CTL_FAIL); }
+    uint32_t ctl_count() const { return *reinterpret_cast<const uint32_t*>(h_ctl + CTL_COUNT); }
     int cur = 0;  // which state buffer holds the current estimate
     // device buffers
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_Dinv, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_ocnt, d_camblk,
-        d_pairs, d_fail, d_olist, d_camcnt;
+        d_pairs, d_olist, d_camcnt, d_blkidx;
     mage_ba_stats stats{};
 
     Problem problem() const
@@ -976,10 +1002,12 @@ struct BundleAdjuster {
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_Dinv, &d_db, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_ocnt, &d_camblk, &d_pairs,
-                        &d_fail, &d_olist, &d_camcnt})
+                        &d_olist, &d_camcnt, &d_blkidx})
             b->release();
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
+        if (h_ctl) (void)hipHostFree(h_ctl);
+        h_ctl = nullptr;
     }
 
     template <typename T>
@@ -1082,6 +1110,14 @@ struct BundleAdjuster {
                     if (mark[(size_t)x * nb + y]) pairs.push_back(make_int2(x, y));
         }
         npairs = (int)pairs.size();
+        // block x point index for the Schur pairs: first position of point i in the list of the
+        // camera of block h (-1: not observed)
+        std::vector<int> blkidx(std::max((size_t)nb * P, (size_t)1), -1);
+        for (int h = 0; h < nb; h++) {
+            const int c = cam_of_block[h];
+            for (int a = cstart[c + 1] - 1; a >= cstart[c]; a--) blkidx[(size_t)h * P + cpt[a]] = a;
+        }
+        if ((r = upload(d_blkidx, blkidx)) != MAGE_OK) return r;
         if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
         if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
         if ((r = upload(d_active, active)) != MAGE_OK) return r;
@@ -1111,8 +1147,8 @@ struct BundleAdjuster {
                         std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
                         std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, Pm * 8),
                         std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
-                        std::make_pair(&d_red, (size_t)128), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 8),
-                        std::make_pair(&d_ocnt, (Em / BA_THREADS + 2) * 8), std::make_pair(&d_fail, (size_t)16),
+                        std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 8),
+                        std::make_pair(&d_ocnt, (Em / BA_THREADS + 2) * 8), 
                         std::make_pair(&d_olist, Em * 4 + 16), std::make_pair(&d_camcnt, Cm * 4)})
             if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
         MAGE_HIP(hipMemsetAsync(d_maxd.ptr, 0, (Pm + Cm) * 8, st));
@@ -1161,7 +1197,7 @@ struct BundleAdjuster {
         const int gmax = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
         double* xp = d_x.as<double>();
         double* xl = d_x.as<double>() + np;
-        MAGE_HIP(hipMemsetAsync(d_fail.ptr, 0, 4, st));
+        MAGE_HIP(hipMemsetAsync(d_failp(), 0, 4, st));
         if (P > 0 && !points_fixed) {
             KernelTimer _kt("ba.point_schur", st);
             hipLaunchKernelGGL(point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
@@ -1172,7 +1208,7 @@ struct BundleAdjuster {
             {
                 KernelTimer _kt("ba.schur_pairs", st);
                 hipLaunchKernelGGL(schur_pairs, dim3(npairs), dim3(BA_THREADS), 0, st, pb, d_pairs.as<int2>(),
-                                   d_camblk.as<int>(), d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(),
+                                   d_camblk.as<int>(), d_blkidx.as<int>(), d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(),
                                    d_Dinv.as<double>(), d_db.as<double>(), lam, np, d_S.as<double>(),
                                    d_rhs.as<double>());
             }
@@ -1180,10 +1216,10 @@ struct BundleAdjuster {
                 KernelTimer _kt("ba.cholesky_solve", st);
                 if (np <= 16 * CT_MAXT)
                     hipLaunchKernelGGL(chol_tiles, dim3(1), dim3(CT_THREADS), 0, st, d_S.as<double>(), np, n,
-                                       d_rhs.as<double>(), xp, d_fail.as<int>());
+                                       d_rhs.as<double>(), xp, d_failp());
                 else
                     hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np, n,
-                                       d_rhs.as<double>(), xp, d_fail.as<int>());
+                                       d_rhs.as<double>(), xp, d_failp());
             }
         }
         if (P > 0) {
@@ -1208,11 +1244,10 @@ struct BundleAdjuster {
                                P + C, d_maxd.as<double>(), 0, d_red.as<double>() + 3);
         }
         MAGE_HIP(hipGetLastError());
-        int fail = 0;
-        MAGE_HIP(hipMemcpyAsync(red, d_red.ptr, 6 * sizeof(double), hipMemcpyDeviceToHost, st));
-        MAGE_HIP(hipMemcpyAsync(&fail, d_fail.ptr, 4, hipMemcpyDeviceToHost, st));
-        MAGE_HIP(hipStreamSynchronize(st));
-        *ok = fail == 0;
+        mage_status r = read_ctl();
+        if (r != MAGE_OK) return r;
+        for (int k = 0; k < 6; k++) red[k] = h_ctl[k];
+        *ok = ctl_fail() == 0;
         return MAGE_OK;
     }
 
@@ -1224,12 +1259,10 @@ struct BundleAdjuster {
         double currentChi = 0;
         bool haveChi = false;
         if (iteration == 0 && user_lambda <= 0) {
-            double h[3];
-            MAGE_HIP(hipMemcpyAsync(h, d_red.ptr, sizeof(h), hipMemcpyDeviceToHost, st));
-            MAGE_HIP(hipStreamSynchronize(st));
-            currentChi = h[0];
+            if ((r = read_ctl()) != MAGE_OK) return r;
+            currentChi = h_ctl[0];
             haveChi = true;
-            lambda = 1e-5 * h[2];  // computeLambdaInit, tau = 1e-5
+            lambda = 1e-5 * h_ctl[2];  // computeLambdaInit, tau = 1e-5
             ni = 2;
         } else if (iteration == 0) {
             lambda = user_lambda;
@@ -1311,7 +1344,7 @@ struct BundleAdjuster {
             return MAGE_OK;
         }
         const int ge = (E + BA_THREADS - 1) / BA_THREADS;
-        uint32_t* d_count = d_olist.as<uint32_t>() + E;
+        uint32_t* d_count = d_countp();
         MAGE_HIP(hipMemsetAsync(d_count, 0, 4, st));
         {
             KernelTimer _kt("ba.outlier_pass", st);
@@ -1325,11 +1358,9 @@ struct BundleAdjuster {
                                d_osum.as<double>(), 0, d_red.as<double>() + 6);
         }
         MAGE_HIP(hipGetLastError());
-        double h[3];
-        uint32_t no = 0;
-        MAGE_HIP(hipMemcpyAsync(h, d_red.as<double>() + 6, sizeof(h), hipMemcpyDeviceToHost, st));
-        MAGE_HIP(hipMemcpyAsync(&no, d_count, 4, hipMemcpyDeviceToHost, st));
-        MAGE_HIP(hipStreamSynchronize(st));
+        if ((r = read_ctl()) != MAGE_OK) return r;
+        const double h[3] = {h_ctl[6], h_ctl[7], h_ctl[8]};
+        const uint32_t no = ctl_count();
         if (no > 0) {
             std::vector<uint32_t> list(no);
             MAGE_HIP(hipMemcpyAsync(list.data(), d_olist.ptr, 4 * (size_t)no, hipMemcpyDeviceToHost, st));
@@ -1374,9 +1405,12 @@ mage_status mage_ba_create(int32_t points_fixed, int device, mage_ba** out)
     auto* b = new mage_ba();
     b->device = device;
     b->points_fixed = points_fixed != 0;
-    if (hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), mage::BundleAdjuster::CTL_DOUBLES * sizeof(double),
+                      hipHostMallocDefault) != hipSuccess) {
+        b->release();
         delete b;
-        mage::set_error("hipStreamCreate failed");
+        mage::set_error("hipStreamCreate / hipHostMalloc failed");
         return MAGE_EDEVICE;
     }
     *out = b;

@@ -42,7 +42,8 @@ mage_status bind_device(int device)
 
 namespace {
 struct TimedLaunch {
-    std::string name;
+    const char* name;  // string literal of the launch site
+    int device;
     hipEvent_t start, stop;
 };
 std::atomic<bool> g_profiling{false};
@@ -54,6 +55,21 @@ struct Totals {
 };
 std::map<std::string, Totals> g_prof_totals;
 std::string g_prof_text;
+// Recycled events per device: a timed launch costs two hipEventRecord calls, not two event
+// creations (which cost more than the short BA kernels they time).
+std::map<int, std::vector<hipEvent_t>> g_event_pool;
+
+hipEvent_t pooled_event_locked(int device)
+{
+    auto& pool = g_event_pool[device];
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
 
 void drain_locked()
 {
@@ -64,8 +80,8 @@ void drain_locked()
             tot.count++;
             tot.ms += ms;
         }
-        (void)hipEventDestroy(t.start);
-        (void)hipEventDestroy(t.stop);
+        g_event_pool[t.device].push_back(t.start);
+        g_event_pool[t.device].push_back(t.stop);
     }
     g_prof_pending.clear();
 }
@@ -76,8 +92,15 @@ bool profiling_enabled() { return g_profiling.load(std::memory_order_relaxed); }
 KernelTimer::KernelTimer(const char* kernel, hipStream_t st) : stream(st), name(kernel)
 {
     if (!profiling_enabled()) return;
-    if (hipEventCreate(&start) != hipSuccess || hipEventCreate(&stop) != hipSuccess) {
-        start = stop = nullptr;
+    if (hipGetDevice(&device) != hipSuccess) return;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        start = pooled_event_locked(device);
+        stop = start ? pooled_event_locked(device) : nullptr;
+        if (start && !stop) g_event_pool[device].push_back(start);
+    }
+    if (!stop) {
+        start = nullptr;
         return;
     }
     (void)hipEventRecord(start, stream);
@@ -88,7 +111,7 @@ KernelTimer::~KernelTimer()
     if (!start) return;
     (void)hipEventRecord(stop, stream);
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    g_prof_pending.push_back({name, start, stop});
+    g_prof_pending.push_back({name, device, start, stop});
     if (g_prof_pending.size() > 4096) drain_locked();
 }
 

@@ -72,6 +72,7 @@ struct KernelTimer {
     hipEvent_t start = nullptr, stop = nullptr;
     hipStream_t stream = nullptr;
     const char* name = nullptr;
+    int device = 0;
     KernelTimer(const char* kernel, hipStream_t st);
     ~KernelTimer();
     KernelTimer(const KernelTimer&) = delete;
