@@ -541,7 +541,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     const int lr = lane >> 4, lc = lane & 15;  // accumulator layout: rows lr + 4r, column lc
 
     // tile coordinates of each slot (wave uniform, scalar registers)
-    int tI[CT_TPW], tJ[CT_TPW];
+    int tIJ[CT_TPW];  // ti | tj << 8, one scalar register per slot
     {
         int i = 0, rowend = mt;  // tiles [rowend - (mt - i), rowend) are row i
         for (int sl = 0; sl < CT_TPW; sl++) {
@@ -550,13 +550,12 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 i++;
                 rowend += mt - i;
             }
-            tI[sl] = t < T ? i : mt;  // mt: no tile
-            tJ[sl] = t < T ? i + (t - (rowend - (mt - i))) : mt;
+            tIJ[sl] = t < T ? i | (i + (t - (rowend - (mt - i)))) << 8 : mt | mt << 8;  // mt: no tile
         }
     }
     auto tile_of = [&](int sl, int& ti, int& tj) {
-        ti = tI[sl];
-        tj = tJ[sl];
+        ti = tIJ[sl] & 0xFF;
+        tj = tIJ[sl] >> 8;
     };
     dbl4 C[CT_TPW];
 #pragma unroll
@@ -575,7 +574,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     }
     if (tid == 0) s_fail = 0;
     for (int i = tid; i < np; i += CT_THREADS) vb[i] = i < n ? b[i] : 0.0;
-    long long tm[6] = {0, 0, 0, 0, 0, 0}, t0 = 0;  // MAGE_CHOL_ABLATE == 3: phase cycles of wave 0
+    long long tm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0;  // MAGE_CHOL_ABLATE == 3: phase cycles of wave 0
     auto tick = [&](int ph) {
         if (MAGE_CHOL_ABLATE == 3) {
             const long long t = __builtin_amdgcn_s_memtime();
@@ -606,68 +605,58 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 for (int q = 0; q < 16; q++) invL[k][l][q] = (q == l) ? 1.0 / sqrt(D[l][l]) : 0.0;
             if (l < 16) y_out[l] = 0;
         } else {
-            // lanes 0-15: row l of L (lower), right-looking Cholesky of the 16x16 block; column
-            // values are broadcast with v_readlane (scalar).  Entries above the diagonal and the
-            // lanes >= 16 hold zeros, which every update keeps at zero, so no lane masks.
-            double a[16], rd[16];
+            // Right-looking Cholesky of the 16x16 block with the triangular inverse and the
+            // forward substitution fused into the same column loop, one register array v[] over
+            // three lane groups that all take the same update v[q] -= v[j] L[q][j]:
+            //   lanes 0-15:  row l of A -> row l of L (entries above the diagonal are never read)
+            //   lanes 16-31: column l-16 of I -> column l-16 of inv(L)
+            //   lane 32:     vb_k (final: every block above has updated it) -> y_k
+            // Column j's L[q][j] are broadcast once with v_readlane (scalar registers).  Lane j's
+            // own v[j] is the pivot d, so v[j] *= 1/sqrt(d) yields sqrt(d) there with no select.
+            // (An LDS column broadcast instead measured 2x slower.)
+            double v[16];
+            const double* vbk = &vb[16 * k];
+            const int c = l - 16;
+            // unconditional loads (one batch, one wait), then per-lane selects
+            double dq[16], bq[16];
 #pragma unroll
-            for (int q = 0; q < 16; q++) a[q] = (l < 16 && q <= l) ? D[q][l] : 0.0;  // A[l][q] = A[q][l]
+            for (int q = 0; q < 16; q++) {
+                dq[q] = D[q][l & 15];
+                bq[q] = vbk[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+                v[q] = l < 16 ? (q <= l ? dq[q] : 0.0) : (l < 32 ? (q == c ? 1.0 : 0.0) : (l == 32 ? bq[q] : 0.0));
             bool bad = false;
+            if (k == 0) tick(6);
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                const double djj = readlane_f64(a[j], j);
+                const double djj = readlane_f64(v[j], j);
                 if (!(djj > 0)) bad = true;
-                // 1/sqrt by v_rsq_f64 + two Newton steps (no f64 sqrt / division sequence on
-                // the column's critical path); d = djj / sqrt(djj)
+                // 1/sqrt by v_rsq_f64 + one Newton step (~1e-14 relative, no f64 sqrt / division
+                // sequence on the column's critical path)
                 const double h = 0.5 * djj;
                 double r = __builtin_amdgcn_rsq(djj);
                 r *= __builtin_fma(-h * r, r, 1.5);
-                r *= __builtin_fma(-h * r, r, 1.5);
-                rd[j] = r;
-                a[j] = (l == j) ? djj * r : a[j] * r;
+                v[j] *= r;
+                // all broadcasts of the column first (distinct scalar registers: the readlane ->
+                // VALU hazard is covered by the batch instead of an s_nop per element)
+                double lq[16];
 #pragma unroll
-                for (int q = j + 1; q < 16; q++) a[q] = __builtin_fma(-a[j], readlane_f64(a[j], q), a[q]);
+                for (int q = j + 1; q < 16; q++) lq[q] = readlane_f64(v[j], q);
+#pragma unroll
+                for (int q = j + 1; q < 16; q++) v[q] = __builtin_fma(-v[j], lq[q], v[q]);
+                __builtin_amdgcn_sched_barrier(0);  // keep each column's broadcasts in its own window
             }
+            if (k == 0) tick(7);
             if (l == 0 && bad) s_fail = 1;
-            if (l < 16)
+            if (l >= 16 && l < 32)
 #pragma unroll
-                for (int q = 0; q < 16; q++) D[l][q] = a[q];  // D := L_kk
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // inv(L_kk), column c = lane & 15: right-looking forward substitution L X = I
-            // (L[m][q] are wave-uniform LDS broadcasts)
-            const int c = lane & 15;
-            double xc[16];
+                for (int m = 0; m < 16; m++) invL[k][m][c] = v[m];
+            if (l == 32)
 #pragma unroll
-            for (int m = 0; m < 16; m++) xc[m] = (m == c) ? 1.0 : 0.0;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                xc[q] *= rd[q];
-#pragma unroll
-                for (int m = q + 1; m < 16; m++) xc[m] = __builtin_fma(-D[m][q], xc[q], xc[m]);
-            }
-            if (lane < 16)
-#pragma unroll
-                for (int m = 0; m < 16; m++) invL[k][m][c] = xc[m];
-            // forward substitution fused into the factorisation: vb_k has received every update
-            // from the blocks above, so y_k = inv(L_kk) vb_k
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < 16) {
-                double y = 0;
-#pragma unroll
-                for (int m = 0; m < 16; m++) y = __builtin_fma(invL[k][lane][m], vb[16 * k + m], y);
-                y_out[lane] = y;
-            }
+                for (int m = 0; m < 16; m++) y_out[m] = v[m];
         }
-        // U_kk = L_kk^T into the owner's register tile
-#pragma unroll
-        for (int sl = 0; sl < CT_TPW; sl++)
-            if (sl == slot)
-#pragma unroll
-                for (int r = 0; r < 4; r++) C[sl][r] = D[lc][lr + 4 * r];
     };
     if (mt > 0 && wave == 0) factor_diag(0, 0, 0);  // tile (0, 0) is tile 0: wave 0, slot 0
     tick(1);
@@ -711,7 +700,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         auto syrk = [&](int sl) {
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pan[buf][tI[sl]][4 * q + lr][lc], pan[buf][tJ[sl]][4 * q + lr][lc],
+                C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pan[buf][tIJ[sl] & 0xFF][4 * q + lr][lc], pan[buf][tIJ[sl] >> 8][4 * q + lr][lc],
                                                             C[sl], 0, 0, 0);
         };
         const int kn = k + 1, tnn = upper_tile_index(kn, kn, mt);
@@ -726,7 +715,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         }
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++) {
-            const int i = tI[sl], j = tJ[sl];
+            const int i = tIJ[sl] & 0xFF, j = tIJ[sl] >> 8;
             if (i > k && i < mt && !(i == kn && j == kn)) syrk(sl);
         }
         tick(4);
@@ -785,8 +774,8 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     tick(5);
     for (int i = tid; i < np; i += CT_THREADS) x[i] = i < n ? vb[i] : 0.0;
     if (MAGE_CHOL_ABLATE == 3 && tid == 0)
-        printf("chol_tiles np=%d cycles: load %lld diag %lld barrier %lld trsm %lld syrk %lld backward %lld\n", np, tm[0],
-               tm[1], tm[2], tm[3], tm[4], tm[5]);
+        printf("chol_tiles np=%d cycles: load %lld diag %lld barrier %lld trsm %lld syrk %lld backward %lld | factor0 stage %lld columns %lld\n", np, tm[0],
+               tm[1], tm[2], tm[3], tm[4], tm[5], tm[6], tm[7]);
 }
 
 // xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]); also the point part of computeScale.
@@ -856,56 +845,112 @@ __global__ __launch_bounds__(BA_THREADS) void update_state(Problem pb, State A, 
     }
 }
 
-// StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) per active edge at state s using the
-// stored errors: an edge behind the camera or with |e|^2 > maxErrorSquare is removed (active
-// byte cleared, index appended; the host sorts the short list into g2o's active-edge order).
-__global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s, int E,
-                                                           unsigned char* __restrict__ active,
+// StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) per active edge using the stored
+// errors: an edge behind the camera or with |e|^2 > maxErrorSquare is an outlier (index appended;
+// the host sorts the short list into g2o's active-edge order and drop_edges removes them).
+// Read-only on the graph, so it runs speculatively with the last trial for NS candidate states
+// at once (ns = 2: the trial state if accepted, the current state if rejected); list k lives at
+// out_list + k E.  Block partials are reduced in fixed order by the last block to finish, which
+// writes ctl->osum[k] = (sum of inlier |e|^2, inlier count) and resets the ticket.
+struct OutlierCtl {
+    double osum[2][2];
+    int fail;
+    uint32_t count[2];
+    uint32_t ticket;
+};
+
+__global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s0, State s1, int ns, int E,
+                                                           const unsigned char* __restrict__ active,
                                                            const double* __restrict__ err,
                                                            double maxErrSq,
                                                            uint32_t* __restrict__ out_list,
-                                                           uint32_t* __restrict__ out_count,
-                                                           double* __restrict__ sum_part,
-                                                           double* __restrict__ cnt_part)
+                                                           double* __restrict__ part,  // [ns][2][gridDim.x]
+                                                           OutlierCtl* __restrict__ ctl)
 {
-    __shared__ double ssum[BA_THREADS], scnt[BA_THREADS];
+    __shared__ double ssum[2][BA_THREADS / kWave], scnt[2][BA_THREADS / kWave];
+    __shared__ int s_last;
     const int e = blockIdx.x * BA_THREADS + threadIdx.x;
-    double vs = 0, vc = 0;
+    double vs[2] = {0, 0}, vc[2] = {0, 0};
     if (e < E && active[e]) {
         const double e0 = err[2 * e], e1 = err[2 * e + 1];
         const double sumSquares = e0 * e0 + e1 * e1;
         const int c = pb.ecam[e], p = pb.ept[e];
-        // SE3Quat::inverse: q*, -(q* t); forward = q* (0,0,1)
-        const double qc[4] = {-s.q[4 * c], -s.q[4 * c + 1], -s.q[4 * c + 2], s.q[4 * c + 3]};
-        const double tt[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
-        double it[3], fwd[3];
-        d_qrot(qc, tt, it);
-        const double z[3] = {0, 0, 1};
-        d_qrot(qc, z, fwd);
-        const double dot = (s.p[3 * p] + it[0]) * fwd[0] + (s.p[3 * p + 1] + it[1]) * fwd[1] +
-                           (s.p[3 * p + 2] + it[2]) * fwd[2];
-        if (dot <= 0 || sumSquares > maxErrSq) {
-            active[e] = 0;
-            out_list[atomicAdd(out_count, 1u)] = (uint32_t)e;
-        } else {
-            vs = sumSquares;
-            vc = 1;
+        for (int k = 0; k < ns; k++) {
+            const State& s = k == 0 ? s0 : s1;
+            // SE3Quat::inverse: q*, -(q* t); forward = q* (0,0,1)
+            const double qc[4] = {-s.q[4 * c], -s.q[4 * c + 1], -s.q[4 * c + 2], s.q[4 * c + 3]};
+            const double tt[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
+            double it[3], fwd[3];
+            d_qrot(qc, tt, it);
+            const double z[3] = {0, 0, 1};
+            d_qrot(qc, z, fwd);
+            const double dot = (s.p[3 * p] + it[0]) * fwd[0] + (s.p[3 * p + 1] + it[1]) * fwd[1] +
+                               (s.p[3 * p + 2] + it[2]) * fwd[2];
+            if (dot <= 0 || sumSquares > maxErrSq) {
+                out_list[(long long)k * E + atomicAdd(&ctl->count[k], 1u)] = (uint32_t)e;
+            } else {
+                vs[k] = sumSquares;
+                vc[k] = 1;
+            }
         }
     }
-    ssum[threadIdx.x] = vs;
-    scnt[threadIdx.x] = vc;
+    // block partials: wave sums by shuffles, then the waves in order
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    for (int k = 0; k < ns; k++) {
+        double a = vs[k], b = vc[k];
+        for (int o = kWave / 2; o > 0; o >>= 1) {
+            a += __shfl_xor(a, o);
+            b += __shfl_xor(b, o);
+        }
+        if (lane == 0) {
+            ssum[k][w] = a;
+            scnt[k][w] = b;
+        }
+    }
     __syncthreads();
-    for (int st = BA_THREADS / 2; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) {
-            ssum[threadIdx.x] += ssum[threadIdx.x + st];
-            scnt[threadIdx.x] += scnt[threadIdx.x + st];
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < ns; k++) {
+            double a = 0, b = 0;
+            for (int i = 0; i < BA_THREADS / kWave; i++) {
+                a += ssum[k][i];
+                b += scnt[k][i];
+            }
+            part[(2 * k) * gridDim.x + blockIdx.x] = a;
+            part[(2 * k + 1) * gridDim.x + blockIdx.x] = b;
+        }
+        __threadfence();
+        s_last = atomicAdd(&ctl->ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    for (int k = 0; k < ns; k++) {
+        for (int h = 0; h < 2; h++) {
+            double v = 0;
+            for (int i = threadIdx.x; i < (int)gridDim.x; i += BA_THREADS) v += part[(2 * k + h) * gridDim.x + i];
+            for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            if (lane == 0) ssum[h][w] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double a = 0, b = 0;
+            for (int i = 0; i < BA_THREADS / kWave; i++) {
+                a += ssum[0][i];
+                b += ssum[1][i];
+            }
+            ctl->osum[k][0] = a;
+            ctl->osum[k][1] = b;
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        sum_part[blockIdx.x] = ssum[0];
-        cnt_part[blockIdx.x] = scnt[0];
-    }
+    if (threadIdx.x == 0) ctl->ticket = 0;
+}
+
+__global__ __launch_bounds__(BA_THREADS) void drop_edges(unsigned char* __restrict__ active,
+                                                         const uint32_t* __restrict__ list, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * BA_THREADS + threadIdx.x;
+    if (i < n) active[list[i]] = 0;
 }
 
 // After removals: points keep their system membership only while they have an active edge
@@ -951,25 +996,31 @@ struct BundleAdjuster {
     std::vector<int> camh, ptfree, cam_of_block;
     hipStream_t st = nullptr;
     // Control block read back at every host decision (one pinned copy per synchronisation):
-    // doubles [0,3) linearisation chi2 / max diag, [3,6) trial, [6,9) outlier pass, then the
-    // Cholesky failure flag and the outlier count as 32-bit words.
-    static constexpr int CTL_DOUBLES = 16, CTL_FAIL = 10, CTL_COUNT = 11;
+    // doubles [0,3) linearisation chi2 / max diag, [3,6) trial, then the outlier pass's
+    // OutlierCtl (sums, Cholesky failure flag, counts, ticket).
+    static constexpr int CTL_DOUBLES = 16, CTL_OUTLIER = 6;
     double* h_ctl = nullptr;
-    int* d_failp() const { return reinterpret_cast<int*>(d_red.as<double>() + CTL_FAIL); }
-    uint32_t* d_countp() const { return reinterpret_cast<uint32_t*>(d_red.as<double>() + CTL_COUNT); }
+    OutlierCtl* d_octl() const { return reinterpret_cast<OutlierCtl*>(d_red.as<double>() + CTL_OUTLIER); }
+    const OutlierCtl& h_octl() const { return *reinterpret_cast<const OutlierCtl*>(h_ctl + CTL_OUTLIER); }
+    int* d_failp() const { return &d_octl()->fail; }
+    // zero the failure flag, counts and ticket (the sums are written, not accumulated)
+    mage_status reset_ctl_words()
+    {
+        MAGE_HIP(hipMemsetAsync(&d_octl()->fail, 0, sizeof(OutlierCtl) - offsetof(OutlierCtl, fail), st));
+        return MAGE_OK;
+    }
     mage_status read_ctl()
     {
         MAGE_HIP(hipMemcpyAsync(h_ctl, d_red.ptr, CTL_DOUBLES * sizeof(double), hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipStreamSynchronize(st));
         return MAGE_OK;
     }
-    int ctl_fail() const { return *reinterpret_cast<const int*>(h_ctl + CTL_FAIL); }
-    uint32_t ctl_count() const { return *reinterpret_cast<const uint32_t*>(h_ctl + CTL_COUNT); }
+    int ctl_fail() const { return h_octl().fail; }
     int cur = 0;  // which state buffer holds the current estimate
     // device buffers
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
-        d_bp, d_Dinv, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_ocnt, d_camblk,
+        d_bp, d_Dinv, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
         d_pairs, d_olist, d_camcnt, d_blkidx;
     mage_ba_stats stats{};
 
@@ -1001,7 +1052,7 @@ struct BundleAdjuster {
         for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_Dinv, &d_db, &d_S, &d_rhs,
-                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_ocnt, &d_camblk, &d_pairs,
+                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk, &d_pairs,
                         &d_olist, &d_camcnt, &d_blkidx})
             b->release();
         if (st) (void)hipStreamDestroy(st);
@@ -1147,12 +1198,14 @@ struct BundleAdjuster {
                         std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
                         std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, Pm * 8),
                         std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
-                        std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 8),
-                        std::make_pair(&d_ocnt, (Em / BA_THREADS + 2) * 8), 
-                        std::make_pair(&d_olist, Em * 4 + 16), std::make_pair(&d_camcnt, Cm * 4)})
+                        std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 4 * 8),
+                        std::make_pair(&d_olist, Em * 2 * 4 + 16), std::make_pair(&d_camcnt, Cm * 4)})
             if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
         MAGE_HIP(hipMemsetAsync(d_maxd.ptr, 0, (Pm + Cm) * 8, st));
         MAGE_HIP(hipMemsetAsync(d_scale.ptr, 0, (Pm + Cm) * 8, st));
+        // chol_tiles reads S without writing it and every trial rewrites the same covisible pair
+        // blocks, so the zero blocks are set once here (cholesky_solve factors in place: per trial)
+        MAGE_HIP(hipMemsetAsync(d_S.ptr, 0, npm * npm * 8, st));
         if (!err_initialized) {
             MAGE_HIP(hipMemsetAsync(d_err.ptr, 0, Em * 2 * 8, st));
             err_initialized = true;
@@ -1169,19 +1222,16 @@ struct BundleAdjuster {
         Problem pb = problem();
         const int gp = (P + BA_THREADS - 1) / BA_THREADS;
         if (P > 0) {
-            KernelTimer _kt("ba.point_linearize", st);
-            hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(cur), 1,
+            launch("ba.point_linearize", point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(cur), 1,
                                d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
                                d_chi.as<double>(), d_maxd.as<double>());
         }
         if (C > 0) {
-            KernelTimer _kt("ba.cam_linearize", st);
-            hipLaunchKernelGGL(cam_linearize, dim3(C), dim3(BA_THREADS), 0, st, pb, state(cur), d_err.as<double>(),
+            launch("ba.cam_linearize", cam_linearize, dim3(C), dim3(BA_THREADS), 0, st, pb, state(cur), d_err.as<double>(),
                                d_Hpp.as<double>(), d_bp.as<double>(), d_maxd.as<double>() + P);
         }
         {
-            KernelTimer _kt("ba.reduce", st);
-            hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_chi.as<double>(), 0,
+            launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_chi.as<double>(), 0,
                                d_maxd.as<double>(), P + C, d_red.as<double>());
         }
         MAGE_HIP(hipGetLastError());
@@ -1190,59 +1240,54 @@ struct BundleAdjuster {
 
     // One trial: solve with lambda, build the trial state in the other buffer, evaluate it.
     // Reads back red[0..5] = {chi(current), -, maxdiag, chi(trial), scale, -} and the fail flag.
-    mage_status trial(double lam, bool* ok, double red[6])
+    mage_status trial(double lam, bool* ok, double red[6], bool speculate)
     {
+        mage_status r0;
         Problem pb = problem();
         const int gp = (P + BA_THREADS - 1) / BA_THREADS;
         const int gmax = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
         double* xp = d_x.as<double>();
         double* xl = d_x.as<double>() + np;
-        MAGE_HIP(hipMemsetAsync(d_failp(), 0, 4, st));
+        if ((r0 = reset_ctl_words()) != MAGE_OK) return r0;
         if (P > 0 && !points_fixed) {
-            KernelTimer _kt("ba.point_schur", st);
-            hipLaunchKernelGGL(point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
+            launch("ba.point_schur", point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
                                d_Hll.as<double>(), d_bl.as<double>(), lam, d_Dinv.as<double>(), d_db.as<double>());
         }
         if (n > 0) {
-            MAGE_HIP(hipMemsetAsync(d_S.ptr, 0, (size_t)np * np * 8, st));
+            if (np > 16 * CT_MAXT) MAGE_HIP(hipMemsetAsync(d_S.ptr, 0, (size_t)np * np * 8, st));
             {
-                KernelTimer _kt("ba.schur_pairs", st);
-                hipLaunchKernelGGL(schur_pairs, dim3(npairs), dim3(BA_THREADS), 0, st, pb, d_pairs.as<int2>(),
+                launch("ba.schur_pairs", schur_pairs, dim3(npairs), dim3(BA_THREADS), 0, st, pb, d_pairs.as<int2>(),
                                    d_camblk.as<int>(), d_blkidx.as<int>(), d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(),
                                    d_Dinv.as<double>(), d_db.as<double>(), lam, np, d_S.as<double>(),
                                    d_rhs.as<double>());
             }
             {
-                KernelTimer _kt("ba.cholesky_solve", st);
                 if (np <= 16 * CT_MAXT)
-                    hipLaunchKernelGGL(chol_tiles, dim3(1), dim3(CT_THREADS), 0, st, d_S.as<double>(), np, n,
-                                       d_rhs.as<double>(), xp, d_failp());
+                    launch("ba.cholesky_solve", chol_tiles, dim3(1), dim3(CT_THREADS), 0, st,
+                           (const double*)d_S.as<double>(), np, n, (const double*)d_rhs.as<double>(), xp, d_failp());
                 else
-                    hipLaunchKernelGGL(cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np, n,
-                                       d_rhs.as<double>(), xp, d_failp());
+                    launch("ba.cholesky_solve", cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np,
+                           n, (const double*)d_rhs.as<double>(), xp, d_failp());
             }
         }
         if (P > 0) {
-            KernelTimer _kt("ba.point_backsub", st);
-            hipLaunchKernelGGL(point_backsub, dim3(gp), dim3(BA_THREADS), 0, st, pb, d_Hpl.as<double>(),
+            launch("ba.point_backsub", point_backsub, dim3(gp), dim3(BA_THREADS), 0, st, pb, d_Hpl.as<double>(),
                                d_Dinv.as<double>(), d_bl.as<double>(), xp, lam, xl, d_scale.as<double>());
         }
         if (std::max(P, C) > 0) {
-            KernelTimer _kt("ba.update_state", st);
-            hipLaunchKernelGGL(update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur),
+            launch("ba.update_state", update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur),
                                xp, xl, d_bp.as<double>(), lam, d_scale.as<double>() + P);
         }
         if (P > 0) {
-            KernelTimer _kt("ba.point_linearize", st);
-            hipLaunchKernelGGL(point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
+            launch("ba.point_linearize", point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
                                d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
                                d_chi.as<double>(), d_maxd.as<double>());
         }
         {
-            KernelTimer _kt("ba.reduce", st);
-            hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_scale.as<double>(),
+            launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_scale.as<double>(),
                                P + C, d_maxd.as<double>(), 0, d_red.as<double>() + 3);
         }
+        if (speculate && E > 0) launch_outlier_pass(state(1 - cur), state(cur), 2);  // read back with this sync
         MAGE_HIP(hipGetLastError());
         mage_status r = read_ctl();
         if (r != MAGE_OK) return r;
@@ -1252,7 +1297,7 @@ struct BundleAdjuster {
     }
 
     // OptimizationAlgorithmLevenberg::solve (g2o); result 1 = OK, 0 = Terminate
-    mage_status lm_solve(int* result)
+    mage_status lm_solve(int* result, bool speculate, int* spec_valid)
     {
         mage_status r = linearize();
         if (r != MAGE_OK) return r;
@@ -1273,7 +1318,8 @@ struct BundleAdjuster {
         do {
             bool ok2 = true;
             double red[6];
-            if ((r = trial(lambda, &ok2, red)) != MAGE_OK) return r;
+            if ((r = trial(lambda, &ok2, red, speculate)) != MAGE_OK) return r;
+            *spec_valid = speculate ? 1 : -1;  // rejected: the current state's result (list 1)
             if (!haveChi) {
                 currentChi = red[0];
                 haveChi = true;
@@ -1293,6 +1339,7 @@ struct BundleAdjuster {
                 currentChi = tempChi;
                 cur = 1 - cur;  // discardTop: the trial state becomes current
                 host_state_stale = true;
+                *spec_valid = speculate ? 0 : -1;  // accepted (the loop ends): the trial state's list 0
             } else {
                 lambda *= ni;
                 ni *= 2;
@@ -1307,7 +1354,7 @@ struct BundleAdjuster {
         return MAGE_OK;
     }
 
-    mage_status step_once(bool* ok)
+    mage_status step_once(bool* ok, bool speculate, int* spec_valid)
     {
         mage_status r;
         if (dirty && (r = initialize()) != MAGE_OK) return r;
@@ -1316,10 +1363,21 @@ struct BundleAdjuster {
             return MAGE_OK;
         }
         int res = 0;
-        if ((r = lm_solve(&res)) != MAGE_OK) return r;
+        if ((r = lm_solve(&res, speculate, spec_valid)) != MAGE_OK) return r;
         iteration++;
         *ok = res == 1;
         return MAGE_OK;
+    }
+
+    double outlier_max_err_sq = 0;
+    // outlier lists, counts and inlier (sum, count) of ns states into the control block (counts
+    // and ticket zeroed by reset_ctl_words beforehand)
+    void launch_outlier_pass(State s0, State s1, int ns)
+    {
+        const int ge = (E + BA_THREADS - 1) / BA_THREADS;
+        launch("ba.outlier_pass", outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), s0, s1, ns, E,
+                           d_active.as<unsigned char>(), d_err.as<double>(), outlier_max_err_sq,
+                           d_olist.as<uint32_t>(), d_osum.as<double>(), d_octl());
     }
 
     mage_status step(const float* hw, uint32_t nsteps, float maxErrSq, uint32_t* outliers, uint32_t cap,
@@ -1328,48 +1386,50 @@ struct BundleAdjuster {
         mage_status r;
         MAGE_HIP(hipSetDevice(device));
         float prior = -1.f;
+        // The outlier pass of the final state runs speculatively with the last step's trials
+        // (launched before their synchronisation): when the last trial is accepted its result is
+        // the pass of the final state and the host skips one round trip.
+        outlier_max_err_sq = (double)maxErrSq;
+        int spec_valid = -1;  // which speculative outlier result holds for the final state (-1 none)
         for (uint32_t s = 0; s < nsteps; s++) {
             if (hw[s] != prior) {
                 huber = (double)hw[s];
                 prior = hw[s];
             }
             bool ok = false;
-            if ((r = step_once(&ok)) != MAGE_OK) return r;
+            if ((r = step_once(&ok, s + 1 == nsteps, &spec_valid)) != MAGE_OK) return r;
             if (!ok) break;
         }
-        if (dirty && (r = initialize()) != MAGE_OK) return r;
+        if (dirty) {
+            spec_valid = -1;
+            if ((r = initialize()) != MAGE_OK) return r;
+        }
         if (E == 0) {
             *nOut = 0;
             *meanSq = std::numeric_limits<float>::quiet_NaN();
             return MAGE_OK;
         }
-        const int ge = (E + BA_THREADS - 1) / BA_THREADS;
-        uint32_t* d_count = d_countp();
-        MAGE_HIP(hipMemsetAsync(d_count, 0, 4, st));
-        {
-            KernelTimer _kt("ba.outlier_pass", st);
-            hipLaunchKernelGGL(outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), state(cur), E,
-                               d_active.as<unsigned char>(), d_err.as<double>(), (double)maxErrSq,
-                               d_olist.as<uint32_t>(), d_count, d_osum.as<double>(), d_ocnt.as<double>());
+        int k = spec_valid;
+        if (k < 0) {
+            if ((r = reset_ctl_words()) != MAGE_OK) return r;
+            launch_outlier_pass(state(cur), state(cur), 1);
+            MAGE_HIP(hipGetLastError());
+            if ((r = read_ctl()) != MAGE_OK) return r;
+            k = 0;
         }
-        {
-            KernelTimer _kt("ba.reduce", st);
-            hipLaunchKernelGGL(reduce3, dim3(1), dim3(1024), 0, st, d_osum.as<double>(), ge, d_ocnt.as<double>(), ge,
-                               d_osum.as<double>(), 0, d_red.as<double>() + 6);
-        }
-        MAGE_HIP(hipGetLastError());
-        if ((r = read_ctl()) != MAGE_OK) return r;
-        const double h[3] = {h_ctl[6], h_ctl[7], h_ctl[8]};
-        const uint32_t no = ctl_count();
+        const double h[2] = {h_octl().osum[k][0], h_octl().osum[k][1]};
+        const uint32_t no = h_octl().count[k];
         if (no > 0) {
             std::vector<uint32_t> list(no);
-            MAGE_HIP(hipMemcpyAsync(list.data(), d_olist.ptr, 4 * (size_t)no, hipMemcpyDeviceToHost, st));
+            const uint32_t* d_list = d_olist.as<uint32_t>() + (size_t)k * E;
+            MAGE_HIP(hipMemcpyAsync(list.data(), d_list, 4 * (size_t)no, hipMemcpyDeviceToHost, st));
+            hipLaunchKernelGGL(drop_edges, dim3((no + BA_THREADS - 1) / BA_THREADS), dim3(BA_THREADS), 0, st,
+                               d_active.as<unsigned char>(), d_list, no);
             // membership after the removal (points drop out with their last edge; a free camera
             // without edges changes the block numbering -> full re-initialisation)
             const int gm = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
             {
-                KernelTimer _kt("ba.refresh_membership", st);
-                hipLaunchKernelGGL(refresh_membership, dim3(gm), dim3(BA_THREADS), 0, st, problem(),
+                launch("ba.refresh_membership", refresh_membership, dim3(gm), dim3(BA_THREADS), 0, st, problem(),
                                    points_fixed ? 1 : 0, d_ptfree.as<int>(), d_camcnt.as<int>());
             }
             std::vector<int> camcnt(C);

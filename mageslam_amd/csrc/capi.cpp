@@ -89,6 +89,27 @@ void drain_locked()
 
 bool profiling_enabled() { return g_profiling.load(std::memory_order_relaxed); }
 
+bool timed_event_pair(hipEvent_t* start, hipEvent_t* stop, int* device)
+{
+    if (hipGetDevice(device) != hipSuccess) return false;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    *start = pooled_event_locked(*device);
+    if (!*start) return false;
+    *stop = pooled_event_locked(*device);
+    if (!*stop) {
+        g_event_pool[*device].push_back(*start);
+        return false;
+    }
+    return true;
+}
+
+void timed_commit(const char* tag, int device, hipEvent_t start, hipEvent_t stop)
+{
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_pending.push_back({tag, device, start, stop});
+    if (g_prof_pending.size() > 4096) drain_locked();
+}
+
 KernelTimer::KernelTimer(const char* kernel, hipStream_t st) : stream(st), name(kernel)
 {
     if (!profiling_enabled()) return;

@@ -1,6 +1,7 @@
 // common.hpp — shared host/device helpers for the MI355X hot-path library (libmage_hot.so).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -68,6 +69,26 @@ constexpr int kWave = 64;
 // Optional per-kernel timing with HIP events recorded on the launch stream (mage_profile_*).
 // When disabled (the default) a KernelTimer costs one relaxed flag check.
 bool profiling_enabled();
+// Timed single launches: the dispatch packet itself carries the start/stop events
+// (hipExtLaunchKernel), so timing adds no marker packets to the stream — the BA step launches
+// ~12 short kernels per trial, where two hipEventRecord calls per launch cost ~20% throughput.
+bool timed_event_pair(hipEvent_t* start, hipEvent_t* stop, int* device);  // pooled; false if off
+void timed_commit(const char* tag, int device, hipEvent_t start, hipEvent_t stop);
+
+template <typename F, typename... Args>
+inline void launch(const char* tag, F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t st, Args... args)
+{
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int dev = 0;
+    if (profiling_enabled() && timed_event_pair(&e0, &e1, &dev)) {
+        hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, e0, e1, 0, args...);
+        timed_commit(tag, dev, e0, e1);
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, shmem, st, args...);
+    }
+}
+
+// Scope timer for multi-launch phases (two hipEventRecord calls around the scope).
 struct KernelTimer {
     hipEvent_t start = nullptr, stop = nullptr;
     hipStream_t stream = nullptr;

@@ -528,11 +528,8 @@ mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA
     mp.a_pitch = aPitch;
     mp.b_pitch = bPitch;
     {
-        KernelTimer _kt("match.two_way", st);
-        if (maxDist < 128)
-            hipLaunchKernelGGL(match_kernel<false>, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
-        else
-            hipLaunchKernelGGL(match_kernel<true>, dim3(pairs), dim3(MT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
+        launch("match.two_way", maxDist < 128 ? match_kernel<false> : match_kernel<true>, dim3(pairs), dim3(MT), 0, st,
+               dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
     }
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;

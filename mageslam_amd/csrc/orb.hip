@@ -1351,8 +1351,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         uint32_t* cand = o->cand.as<uint32_t>() + (size_t)batch * v.coff;
         uint32_t* counts = o->counts.as<uint32_t>() + (size_t)batch * l;
         {
-            KernelTimer _kt("orb.fast_nms", st);
-            hipLaunchKernelGGL(fast_nms_kernel, dim3((W + TW - 1) / TW, (H + TH - 1) / TH, batch), dim3(FAST_THREADS), 0,
+            launch("orb.fast_nms", fast_nms_kernel, dim3((W + TW - 1) / TW, (H + TH - 1) / TH, batch), dim3(FAST_THREADS), 0,
                                st, raw.base[l], fp, cand, counts);
         }
         MAGE_HIP(hipGetLastError());
@@ -1377,8 +1376,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         sp.accumulate = l > 0;
         sp.lvl = multi ? o->lvl.as<uint16_t>() : nullptr;
         {
-            KernelTimer _kt("orb.select", st);
-            hipLaunchKernelGGL(select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, cand, counts, sp, d_kp,
+            launch("orb.select", select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, cand, counts, sp, d_kp,
                                o->xy.as<uint32_t>(), d_n, o->status.as<uint32_t>());
         }
         MAGE_HIP(hipGetLastError());
@@ -1397,8 +1395,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             op.umax[v] = v0;
             ++v0;
         }
-        KernelTimer _kt("orb.orient", st);
-        hipLaunchKernelGGL(orient_kernel, dim3((cap + 3) / 4, batch), dim3(256), 0, st, d_kp, o->xy.as<uint32_t>(),
+        launch("orb.orient", orient_kernel, dim3((cap + 3) / 4, batch), dim3(256), 0, st, d_kp, o->xy.as<uint32_t>(),
                            o->lvl.as<uint16_t>(), d_n, op);
         MAGE_HIP(hipGetLastError());
     }
@@ -1417,20 +1414,19 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         for (int i = 0; i < 2 * KHMAX + 1; i++) dp.taps[i] = o->taps[i];
         dp.dword_ok = (stride % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)d_frames % 4 == 0);
         {
-            KernelTimer _kt("orb.describe", st);
             if (fused_blur) {
                 dp.chunks = (int)((cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW));
                 dp.frames = (int)batch;
                 const dim3 g3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
                 auto kern = dp.R <= 7 ? describe_blurred_kernel<7>
                                       : (dp.R <= 13 ? describe_blurred_kernel<13> : describe_blurred_kernel<RMAX>);
-                hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, o->xy.as<uint32_t>(), d_n,
-                                   o->pattern.as<int8_t>(), d_desc);
+                launch("orb.describe", kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, (const uint32_t*)o->xy.as<uint32_t>(),
+                       d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
             } else {
                 const dim3 g3((cap + DESC_WAVES - 1) / DESC_WAVES, batch);
                 auto kern = dp.R <= 7 ? describe_kernel<7> : (dp.R <= 13 ? describe_kernel<13> : describe_kernel<RMAX>);
-                hipLaunchKernelGGL(kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, o->xy.as<uint32_t>(), d_n,
-                                   o->pattern.as<int8_t>(), d_desc);
+                launch("orb.describe", kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, (const uint32_t*)o->xy.as<uint32_t>(),
+                       d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
             }
         }
         MAGE_HIP(hipGetLastError());
