@@ -9,20 +9,27 @@
 //   point_linearize   thread/point: errors of its edges (kept per edge, as g2o keeps _error),
 //                     robust chi2, Hll, bl and Hpl_e = J_pose^T w J_point per edge
 //   cam_linearize     workgroup/camera: Hpp, bp (recomputes J_pose; no per-edge 6x6 in HBM)
-//   trial loop (<= 10; one 48-byte readback per trial decides accept / reject on the host):
-//     point_schur     Dinv = (Hll + lambda I)^-1, db = Dinv bl
-//     schur_pairs     workgroup per covisible camera pair (h1 <= h2): intersect the two
-//                     point-sorted edge lists by binary search, accumulate
-//                     sum_p Hpl_{c1 p} Dinv_p Hpl_{c2 p}^T in registers, one deterministic
+//   trial loop (<= 10; one pinned 128-byte control-block readback per trial decides accept /
+//   reject on the host):
+//     edge_schur      thread/point-edge: Dinv_p = (Hll + lambda I)^-1, db = Dinv bl (first edge
+//                     of each point), Z_e = Hpl_e Dinv_p (6x3) for every edge
+//     schur_pairs     workgroup per covisible camera pair (h1 <= h2): walk c1's point-sorted
+//                     edges, find c2's edge on the same point in the block x point index,
+//                     accumulate sum_p Z_{c1 p} Hpl_{c2 p}^T in registers, one deterministic
 //                     workgroup reduction, write the 6x6 block (+ Hpp + lambda I, rhs on h1 = h2)
-//     cholesky_solve  one workgroup: 16-wide right-looking Cholesky, diagonal block factored in
-//                     one wave's registers, panel TRSM one row per thread, trailing SYRK on f64
-//                     MFMA (v_mfma_f64_16x16x4f64) tiles; triangular solves by wave shuffles
+//     chol_tiles      one workgroup, np <= 240: register-resident 16x16 upper tiles over 8
+//                     waves; per step the owner factors the diagonal block (Cholesky, inverse
+//                     and forward substitution in one column loop, look-ahead under the
+//                     previous SYRK), TRSM and SYRK on f64 MFMA (v_mfma_f64_16x16x4f64), then a
+//                     one-barrier-per-block backward solve.  cholesky_solve: np > 240 (LDS
+//                     panels, in-place)
 //     point_backsub   xl = Dinv (bl - Hpl^T xp)
 //     update_state    trial state = exp(xp) * T, p + xl  (double-buffered: pop = no copy)
 //     point_linearize errors + robust chi2 of the trial state;  reduce: chi2 and computeScale
-// then the StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) on the device, appending
-// outlier indices and clearing their `active` byte.
+//     outlier_pass    (last step of a StepBundleAdjustment only) speculatively on the trial
+//                     and the current state, so the post-pass result is already on the host
+// then the StepBundleAdjustment post-pass (BundlerLib.cpp:385-446): outlier indices from the
+// speculative (or a fresh) outlier_pass, drop_edges clears their `active` byte.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,6 +48,19 @@ using namespace ba;
 
 constexpr int BA_THREADS = 256;
 
+// A group of PG lanes per point (one edge per lane, strided): the edges' load chains run in
+// parallel and the point sums close with a fixed shuffle tree (deterministic).
+constexpr int PG = 32;
+
+template <int N>
+__device__ __forceinline__ void group_sum(double (&v)[N])
+{
+#pragma unroll
+    for (int off = PG / 2; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < N; k++) v[k] += __shfl_xor(v[k], off);
+}
+
 // Per point: edge errors, robust chi2, Hll, bl, Hpl per edge (BlockSolver::buildSystem with
 // BaseBinaryEdge::constructQuadraticForm, robust first-order weighting).
 __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State s, int linearize,
@@ -51,14 +71,16 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
                                                               double* __restrict__ chi_part,
                                                               double* __restrict__ maxd_part)
 {
-    const int p = blockIdx.x * BA_THREADS + threadIdx.x;
-    if (p >= pb.P) return;
+    const int gid = blockIdx.x * BA_THREADS + threadIdx.x;
+    const int p = gid / PG, sub = gid % PG;
+    if (p >= pb.P) return;  // whole groups: P * PG threads
     const int free_p = linearize && pb.ptfree[p];
-    double H[6] = {0, 0, 0, 0, 0, 0};  // 00 01 02 11 12 22
-    double g[3] = {0, 0, 0};
-    double chi = 0;
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // H 00 01 02 11 12 22, g 0 1 2, chi
+    double* H = acc;
+    double* g = acc + 6;
+    double& chi = acc[9];
     const int e0 = pb.pstart[p], e1 = pb.pstart[p + 1];
-    for (int a = e0; a < e1; a++) {
+    for (int a = e0 + sub; a < e1; a += PG) {
         const int e = pb.pedges[a];
         if (!pb.active[e]) continue;
         double ev[2], xc[3], rho0, rho1;
@@ -72,12 +94,12 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
         const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
         double R[9];
         d_qmat(q, R);
-        const double x = xc[0], y = xc[1], z = xc[2];
-        const double tmp0[3] = {f, 0, -x / z * f}, tmp1[3] = {0, f, -y / z * f};
+        const double iz = 1.0 / xc[2], xi = xc[0] * iz, yi = xc[1] * iz;  // one reciprocal (see jac_pose)
+        const double tmp0[3] = {f, 0, -xi * f}, tmp1[3] = {0, f, -yi * f};
         double J[6];
         for (int k = 0; k < 3; k++) {
-            J[k] = -1. / z * (tmp0[0] * R[k] + tmp0[1] * R[3 + k] + tmp0[2] * R[6 + k]);
-            J[3 + k] = -1. / z * (tmp1[0] * R[k] + tmp1[1] * R[3 + k] + tmp1[2] * R[6 + k]);
+            J[k] = -iz * (tmp0[0] * R[k] + tmp0[1] * R[3 + k] + tmp0[2] * R[6 + k]);
+            J[3 + k] = -iz * (tmp1[0] * R[k] + tmp1[1] * R[3 + k] + tmp1[2] * R[6 + k]);
         }
         const double inf = pb.info[e];
         const double w = rho1 * inf;
@@ -99,6 +121,8 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
                 for (int k = 0; k < 3; k++) o[r * 3 + k] = (Jp[r] * J[k] + Jp[6 + r] * J[3 + k]) * w;
         }
     }
+    group_sum(acc);
+    if (sub != 0) return;
     chi_part[p] = chi;
     if (!linearize) return;
     double* Ho = Hll + 9 * (long long)p;
@@ -117,8 +141,8 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
     maxd_part[p] = free_p ? fmax(fabs(H[0]), fmax(fabs(H[3]), fabs(H[5]))) : 0.0;
 }
 
-// Block sum of `acc[N]` over the workgroup; the result lands in red[0][0..N).
-template <int N>
+// Block sum of `acc[N]` over a workgroup of T threads; the result lands in red[0][0..N).
+template <int N, int T = BA_THREADS>
 __device__ __forceinline__ void block_sum(double (&acc)[N], double (*red)[N])
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -131,7 +155,7 @@ __device__ __forceinline__ void block_sum(double (&acc)[N], double (*red)[N])
     __syncthreads();
     if (threadIdx.x < N) {
         double v = 0;
-        for (int w = 0; w < BA_THREADS / kWave; w++) v += red[w][threadIdx.x];
+        for (int w = 0; w < T / kWave; w++) v += red[w][threadIdx.x];
         acc[0] = v;  // thread k keeps the total of entry k in acc[0]
     }
     __syncthreads();
@@ -139,52 +163,97 @@ __device__ __forceinline__ void block_sum(double (&acc)[N], double (*red)[N])
     __syncthreads();
 }
 
-// Per camera: Hpp (6x6) and bp (6) from its active edges; errors come from point_linearize.
-__global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s,
+// Per free camera: Hpp (6x6, packed upper 21) and bp (6) partial sums from its active edges;
+// errors come from point_linearize.  CAM_CHUNKS workgroups per camera (block = h * CAM_CHUNKS +
+// chunk) take interleaved slices of its edge list and write their partials; linearize_finish
+// adds them in chunk order (no cross-workgroup hand-off inside the kernel).
+constexpr int CAM_CHUNKS = 8;
+constexpr int MAX_FREE_CAMS = 96;  // = CH_PANEL_ROWS / 6, the system-size limit checked at initialisation
+
+__global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s, const int* __restrict__ cam_of_block,
                                                             const double* __restrict__ err,
-                                                            double* __restrict__ Hpp,
-                                                            double* __restrict__ bp,
-                                                            double* __restrict__ maxd_part)
+                                                            double* __restrict__ part)  // [nb][CAM_CHUNKS][27]
 {
-    const int c = blockIdx.x;
+    const int h = blockIdx.x / CAM_CHUNKS, chunk = blockIdx.x % CAM_CHUNKS;
+    const int c = cam_of_block[h];
     __shared__ double red[BA_THREADS / kWave][27];
     double acc[27];
     for (int k = 0; k < 27; k++) acc[k] = 0;
-    const bool inSys = pb.camh[c] >= 0;
-    if (inSys) {
-        const double f = pb.camk[3 * c];
-        for (int a = pb.cstart[c] + threadIdx.x; a < pb.cstart[c + 1]; a += BA_THREADS) {
-            const int e = pb.cedges[a];
-            if (!pb.active[e]) continue;
-            double ev[2], xc[3], rho0, rho1;
-            edge_eval(pb, s, e, ev, xc, rho0, rho1);
-            double Jp[12];
-            jac_pose(xc, f, Jp);
-            const double inf = pb.info[e];
-            const double w = rho1 * inf;
-            const double or0 = -inf * err[2 * e] * rho1, or1 = -inf * err[2 * e + 1] * rho1;
-            int k = 0;
-            for (int r = 0; r < 6; r++)
-                for (int cc = r; cc < 6; cc++) acc[k++] += (Jp[r] * Jp[cc] + Jp[6 + r] * Jp[6 + cc]) * w;
-            for (int r = 0; r < 6; r++) acc[21 + r] += Jp[r] * or0 + Jp[6 + r] * or1;
-        }
+    const double f = pb.camk[3 * c];
+    for (int a = pb.cstart[c] + chunk * BA_THREADS + threadIdx.x; a < pb.cstart[c + 1]; a += CAM_CHUNKS * BA_THREADS) {
+        const int e = pb.cedges[a];
+        if (!pb.active[e]) continue;
+        double ev[2], xc[3], rho0, rho1;
+        edge_eval(pb, s, e, ev, xc, rho0, rho1);
+        double Jp[12];
+        jac_pose(xc, f, Jp);
+        const double inf = pb.info[e];
+        const double w = rho1 * inf;
+        const double or0 = -inf * err[2 * e] * rho1, or1 = -inf * err[2 * e + 1] * rho1;
+        int k = 0;
+        for (int r = 0; r < 6; r++)
+            for (int cc = r; cc < 6; cc++) acc[k++] += (Jp[r] * Jp[cc] + Jp[6 + r] * Jp[6 + cc]) * w;
+        for (int r = 0; r < 6; r++) acc[21 + r] += Jp[r] * or0 + Jp[6 + r] * or1;
     }
     block_sum<27>(acc, red);
-    if (threadIdx.x == 0) {
-        double* H = Hpp + 36 * (long long)c;
-        int k = 0;
-        double md = 0;
-        for (int r = 0; r < 6; r++)
-            for (int cc = r; cc < 6; cc++) {
-                H[r * 6 + cc] = red[0][k];
-                H[cc * 6 + r] = red[0][k];
-                k++;
+    if (threadIdx.x < 27) part[((long long)h * CAM_CHUNKS + chunk) * 27 + threadIdx.x] = red[0][threadIdx.x];
+}
+
+// After the linearisation (one workgroup): Hpp / bp of every free camera from its chunk partials,
+// and out[0] = sum of the points' robust chi2, out[2] = max diagonal entry over Hll and Hpp
+// (computeLambdaInit), with the fixed-order tree of reduce3.
+__global__ __launch_bounds__(1024) void linearize_finish(int nb, const int* __restrict__ cam_of_block,
+                                                         const double* __restrict__ part,
+                                                         const double* __restrict__ chi, int P,
+                                                         const double* __restrict__ maxd_pts,
+                                                         double* __restrict__ Hpp, double* __restrict__ bp,
+                                                         double* __restrict__ out)
+{
+    __shared__ double cams[MAX_FREE_CAMS][27];
+    __shared__ double sa[1024], sm[1024];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < nb * 27; i += 1024) {
+        const int h = i / 27, k = i % 27;
+        double v = 0;
+        for (int q = 0; q < CAM_CHUNKS; q++) v += part[((long long)h * CAM_CHUNKS + q) * 27 + k];
+        cams[h][k] = v;
+    }
+    __syncthreads();
+    for (int i = tid; i < nb * 42; i += 1024) {
+        const int h = i / 42, k = i % 42, c = cam_of_block[h];
+        if (k < 36) {
+            int r = k / 6, cc = k % 6;
+            if (r > cc) {
+                const int t = r;
+                r = cc;
+                cc = t;
             }
-        for (int r = 0; r < 6; r++) {
-            bp[6 * c + r] = red[0][21 + r];
-            md = fmax(md, fabs(H[r * 7]));
+            Hpp[36 * (long long)c + k] = cams[h][r * 6 - r * (r - 1) / 2 + (cc - r)];
+        } else {
+            bp[6 * c + (k - 36)] = cams[h][21 + (k - 36)];
         }
-        maxd_part[c] = inSys ? md : 0.0;
+    }
+    double va = 0, vm = 0;
+    for (int i = tid; i < P; i += 1024) {
+        va += chi[i];
+        vm = fmax(vm, maxd_pts[i]);
+    }
+    for (int h = tid; h < nb; h += 1024)
+        for (int r = 0; r < 6; r++) vm = fmax(vm, fabs(cams[h][r * 6 - r * (r - 1) / 2]));
+    sa[tid] = va;
+    sm[tid] = vm;
+    __syncthreads();
+    for (int st = 512; st > 0; st >>= 1) {
+        if (tid < st) {
+            sa[tid] += sa[tid + st];
+            sm[tid] = fmax(sm[tid], sm[tid + st]);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        out[0] = sa[0];
+        out[1] = 0;
+        out[2] = sm[0];
     }
 }
 
@@ -237,23 +306,43 @@ __device__ __forceinline__ void d_inv3(const double m[9], double o[9])
     o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
 }
 
-__global__ __launch_bounds__(BA_THREADS) void point_schur(int P, const int* __restrict__ ptfree,
-                                                          const double* __restrict__ Hll,
-                                                          const double* __restrict__ bl, double lambda,
-                                                          double* __restrict__ Dinv,
-                                                          double* __restrict__ db)
+// Per point-edge entry a (point-CSR order, so a point's entries are adjacent): D_p = Hll_p +
+// lambda I, Dinv_p by cofactors (each entry of the point recomputes it; the first one stores
+// db_p = Dinv_p bl_p) and Z_e = Hpl_e Dinv_p (6x3), the factor every Schur product and the
+// point back-substitution of edge e reuse.
+__global__ __launch_bounds__(BA_THREADS) void edge_schur(Problem pb, int nentries, const double* __restrict__ Hll,
+                                                         const double* __restrict__ bl,
+                                                         const double* __restrict__ Hpl, double lambda,
+                                                         double* __restrict__ db,
+                                                         double* __restrict__ Z)
 {
-    const int p = blockIdx.x * BA_THREADS + threadIdx.x;
-    if (p >= P || !ptfree[p]) return;
+    const int a = blockIdx.x * BA_THREADS + threadIdx.x;
+    if (a >= nentries) return;
+    const int e = pb.pedges[a];
+    const int p = pb.ept[e];
+    if (!pb.ptfree[p]) return;
     double D[9], Di[9];
+#pragma unroll
     for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
     D[0] += lambda;
     D[4] += lambda;
     D[8] += lambda;
     d_inv3(D, Di);
-    for (int k = 0; k < 9; k++) Dinv[9 * (long long)p + k] = Di[k];
-    const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
-    for (int r = 0; r < 3; r++) db[3 * p + r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
+    if (a == pb.pstart[p]) {
+        const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
+#pragma unroll
+        for (int r = 0; r < 3; r++) db[3 * p + r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
+    }
+    const double* W = Hpl + 18 * (long long)e;
+    double w[18];
+#pragma unroll
+    for (int k = 0; k < 18; k++) w[k] = W[k];
+    double* Ze = Z + 18 * (long long)e;
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            Ze[r * 3 + k] = w[r * 3] * Di[k] + w[r * 3 + 1] * Di[3 + k] + w[r * 3 + 2] * Di[6 + k];
 }
 
 // One covisible camera pair (h1 <= h2) per workgroup (BlockSolver::solve Schur loop):
@@ -269,13 +358,18 @@ __global__ __launch_bounds__(BA_THREADS) void schur_pairs(Problem pb, const int2
                                                           const double* __restrict__ Hpp,
                                                           const double* __restrict__ bp,
                                                           const double* __restrict__ Hpl,
-                                                          const double* __restrict__ Dinv,
-                                                          const double* __restrict__ db, double lambda,
-                                                          int np, double* __restrict__ S,
+                                                          const double* __restrict__ Z,
+                                                          const double* __restrict__ bl, double lambda,
+                                                          int np, int npairs, double* __restrict__ S,
                                                           double* __restrict__ rhs)
 {
     __shared__ double red[BA_THREADS / kWave][42];
-    const int2 hp = pairs[blockIdx.x];
+    // XCD-aware order: block b runs on XCD b % 8; each XCD takes a contiguous run of the
+    // row-major pair list, so a row's Z_{c1 .} stays in that XCD's L2 across its pairs
+    const int chunk = (npairs + 7) >> 3;
+    const int pi = (blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
+    if (pi >= npairs) return;
+    const int2 hp = pairs[pi];
     const int h1 = hp.x, h2 = hp.y;
     const int c1 = cam_of_block[h1], c2 = cam_of_block[h2];
     const bool diag = h1 == h2;
@@ -284,35 +378,38 @@ __global__ __launch_bounds__(BA_THREADS) void schur_pairs(Problem pb, const int2
     for (int k = 0; k < 42; k++) acc[k] = 0;
     const int b1 = pb.cstart[c2 + 1];
     const int* __restrict__ idx2 = blkidx + (long long)h2 * pb.P;
-    for (int a = pb.cstart[c1] + threadIdx.x; a < pb.cstart[c1 + 1]; a += BA_THREADS) {
-        const int e1 = pb.cedges[a];
-        const int p = pb.cpt[a];
-        const int lo = idx2[p];
-        if (lo < 0 || !pb.active[e1] || !pb.ptfree[p]) continue;
-        const double* W1 = Hpl + 18 * (long long)e1;
-        const double* Di = Dinv + 9 * (long long)p;
-        double Z[18];  // W1 * Dinv (6x3)
+    auto add = [&](const double* z, int e2) {
+        const double* W2 = Hpl + 18 * (long long)e2;
+        double w2[18];
+#pragma unroll
+        for (int k = 0; k < 18; k++) w2[k] = W2[k];
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int k = 0; k < 3; k++) Z[r * 3 + k] = W1[r * 3] * Di[k] + W1[r * 3 + 1] * Di[3 + k] + W1[r * 3 + 2] * Di[6 + k];
+            for (int k = 0; k < 6; k++)
+                acc[r * 6 + k] += z[r * 3] * w2[k * 3] + z[r * 3 + 1] * w2[k * 3 + 1] + z[r * 3 + 2] * w2[k * 3 + 2];
+    };
+    for (int a = pb.cstart[c1] + threadIdx.x; a < pb.cstart[c1 + 1]; a += BA_THREADS) {
+        const int e1 = pb.cedges[a];
+        const int p = pb.cpt[a];
+        const int x = idx2[p];  // edge of c2 on p, or -2 - list position (several), -1 none
+        if (x == -1 || !pb.active[e1] || !pb.ptfree[p]) continue;
+        const double* Z1 = Z + 18 * (long long)e1;
+        double z[18];  // Hpl_e1 Dinv_p (6x3)
+#pragma unroll
+        for (int k = 0; k < 18; k++) z[k] = Z1[k];
         if (diag) {
-            const double g0 = db[3 * p], g1 = db[3 * p + 1], g2 = db[3 * p + 2];
+            const double g0 = bl[3 * p], g1 = bl[3 * p + 1], g2 = bl[3 * p + 2];
 #pragma unroll
-            for (int r = 0; r < 6; r++) acc[36 + r] += W1[r * 3] * g0 + W1[r * 3 + 1] * g1 + W1[r * 3 + 2] * g2;
+            for (int r = 0; r < 6; r++) acc[36 + r] += z[r * 3] * g0 + z[r * 3 + 1] * g1 + z[r * 3 + 2] * g2;
         }
-        for (int q = lo; q < b1 && pb.cpt[q] == p; q++) {
-            const int e2 = pb.cedges[q];
-            if (!pb.active[e2]) continue;
-            const double* W2 = Hpl + 18 * (long long)e2;
-            double w2[18];
-#pragma unroll
-            for (int k = 0; k < 18; k++) w2[k] = W2[k];
-#pragma unroll
-            for (int r = 0; r < 6; r++)
-#pragma unroll
-                for (int k = 0; k < 6; k++)
-                    acc[r * 6 + k] += Z[r * 3] * w2[k * 3] + Z[r * 3 + 1] * w2[k * 3 + 1] + Z[r * 3 + 2] * w2[k * 3 + 2];
+        if (x >= 0) {
+            if (pb.active[x]) add(z, x);
+        } else {
+            for (int q = -2 - x; q < b1 && pb.cpt[q] == p; q++) {
+                const int e2 = pb.cedges[q];
+                if (pb.active[e2]) add(z, e2);
+            }
         }
     }
     block_sum<42>(acc, red);
@@ -336,6 +433,7 @@ constexpr int CH_THREADS = 1024;
 constexpr int CH_WAVES = CH_THREADS / kWave;
 constexpr int NB = 16;
 constexpr int CH_PANEL_ROWS = 576;  // 96 free cameras
+static_assert(CH_PANEL_ROWS / 6 == MAX_FREE_CAMS, "free-camera limit");
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
@@ -778,35 +876,41 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                tm[1], tm[2], tm[3], tm[4], tm[5], tm[6], tm[7]);
 }
 
-// xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]); also the point part of computeScale.
-__global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const double* __restrict__ Hpl,
-                                                            const double* __restrict__ Dinv,
+// xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]) = db - sum_e Z_e^T xp[h(e)] (Dinv symmetric,
+// Z_e = Hpl_e Dinv from edge_schur); a PG-lane group per point, one edge per lane.  Also the
+// point part of computeScale.
+__global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const double* __restrict__ Z,
+                                                            const double* __restrict__ db,
                                                             const double* __restrict__ bl,
                                                             const double* __restrict__ xp, double lambda,
                                                             double* __restrict__ xl,
                                                             double* __restrict__ scale_part)
 {
-    const int p = blockIdx.x * BA_THREADS + threadIdx.x;
+    const int gid = blockIdx.x * BA_THREADS + threadIdx.x;
+    const int p = gid / PG, sub = gid % PG;
     if (p >= pb.P) return;
     if (!pb.ptfree[p]) {
-        scale_part[p] = 0;
+        if (sub == 0) scale_part[p] = 0;
         return;
     }
-    double cl[3] = {bl[3 * p], bl[3 * p + 1], bl[3 * p + 2]};
-    for (int a = pb.pstart[p]; a < pb.pstart[p + 1]; a++) {
+    double cl[3] = {0, 0, 0};
+    for (int a = pb.pstart[p] + sub; a < pb.pstart[p + 1]; a += PG) {
         const int e = pb.pedges[a];
         if (!pb.active[e]) continue;
         const int h = pb.camh[pb.ecam[e]];
         if (h < 0) continue;
-        const double* W = Hpl + 18 * (long long)e;
+        const double* Ze = Z + 18 * (long long)e;
         const double* X = xp + 6 * h;
+#pragma unroll
         for (int k = 0; k < 3; k++)
-            for (int r = 0; r < 6; r++) cl[k] -= W[r * 3 + k] * X[r];
+#pragma unroll
+            for (int r = 0; r < 6; r++) cl[k] += Ze[r * 3 + k] * X[r];
     }
-    const double* Di = Dinv + 9 * (long long)p;
+    group_sum(cl);
+    if (sub != 0) return;
     double sc = 0;
     for (int r = 0; r < 3; r++) {
-        const double v = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
+        const double v = db[3 * p + r] - cl[r];
         xl[3 * p + r] = v;
         sc += v * (lambda * v + bl[3 * p + r]);
     }
@@ -1020,9 +1124,13 @@ struct BundleAdjuster {
     // device buffers
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
-        d_bp, d_Dinv, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
-        d_pairs, d_olist, d_camcnt, d_blkidx;
+        d_bp, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
+        d_pairs, d_olist, d_camcnt, d_blkidx, d_Z, d_campart;
+    int n_entries = 0;  // point-CSR entries (active edges at initialisation)
+    int nb_free = 0;    // cameras in the reduced system
     mage_ba_stats stats{};
+
+    static int group_grid(int items) { return (int)(((long long)items * PG + BA_THREADS - 1) / BA_THREADS); }
 
     Problem problem() const
     {
@@ -1051,9 +1159,9 @@ struct BundleAdjuster {
     {
         for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
-                        &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_Dinv, &d_db, &d_S, &d_rhs,
+                        &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_db, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk, &d_pairs,
-                        &d_olist, &d_camcnt, &d_blkidx})
+                        &d_olist, &d_camcnt, &d_blkidx, &d_Z, &d_campart})
             b->release();
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
@@ -1113,6 +1221,7 @@ struct BundleAdjuster {
                 nfp++;
             }
         const int nb = (int)cam_of_block.size();
+        nb_free = nb;
         n = 6 * nb;
         np = (n + 15) / 16 * 16;
         useless = (nb == 0 && nfp == 0);
@@ -1161,13 +1270,17 @@ struct BundleAdjuster {
                     if (mark[(size_t)x * nb + y]) pairs.push_back(make_int2(x, y));
         }
         npairs = (int)pairs.size();
-        // block x point index for the Schur pairs: first position of point i in the list of the
-        // camera of block h (-1: not observed)
+        // block x point index for the Schur pairs: the edge of the camera of block h on point i,
+        // -2 - (first list position) when that camera observes i more than once, -1 if never
         std::vector<int> blkidx(std::max((size_t)nb * P, (size_t)1), -1);
         for (int h = 0; h < nb; h++) {
             const int c = cam_of_block[h];
-            for (int a = cstart[c + 1] - 1; a >= cstart[c]; a--) blkidx[(size_t)h * P + cpt[a]] = a;
+            for (int a = cstart[c]; a < cstart[c + 1]; a++) {
+                int& x = blkidx[(size_t)h * P + cpt[a]];
+                x = x == -1 ? cedges[a] : -2 - (x >= 0 ? a - 1 : -2 - x);
+            }
         }
+        n_entries = pstart[P];
         if ((r = upload(d_blkidx, blkidx)) != MAGE_OK) return r;
         if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
         if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
@@ -1194,7 +1307,9 @@ struct BundleAdjuster {
         for (auto pr : {std::make_pair(&d_err, Em * 2 * 8), std::make_pair(&d_Hll, Pm * 9 * 8),
                         std::make_pair(&d_bl, Pm * 3 * 8), std::make_pair(&d_Hpl, Em * 18 * 8),
                         std::make_pair(&d_Hpp, Cm * 36 * 8), std::make_pair(&d_bp, Cm * 6 * 8),
-                        std::make_pair(&d_Dinv, Pm * 9 * 8), std::make_pair(&d_db, Pm * 3 * 8),
+                        std::make_pair(&d_db, Pm * 3 * 8),
+                        std::make_pair(&d_Z, Em * 18 * 8),
+                        std::make_pair(&d_campart, Cm * CAM_CHUNKS * 27 * 8),
                         std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
                         std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, Pm * 8),
                         std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
@@ -1220,20 +1335,18 @@ struct BundleAdjuster {
     mage_status linearize()
     {
         Problem pb = problem();
-        const int gp = (P + BA_THREADS - 1) / BA_THREADS;
         if (P > 0) {
-            launch("ba.point_linearize", point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(cur), 1,
+            launch("ba.point_linearize", point_linearize, dim3(group_grid(P)), dim3(BA_THREADS), 0, st, pb, state(cur), 1,
                                d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
                                d_chi.as<double>(), d_maxd.as<double>());
         }
-        if (C > 0) {
-            launch("ba.cam_linearize", cam_linearize, dim3(C), dim3(BA_THREADS), 0, st, pb, state(cur), d_err.as<double>(),
-                               d_Hpp.as<double>(), d_bp.as<double>(), d_maxd.as<double>() + P);
+        if (nb_free > 0) {
+            launch("ba.cam_linearize", cam_linearize, dim3(nb_free * CAM_CHUNKS), dim3(BA_THREADS), 0, st, pb, state(cur),
+                   (const int*)d_camblk.as<int>(), (const double*)d_err.as<double>(), d_campart.as<double>());
         }
-        {
-            launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_chi.as<double>(), 0,
-                               d_maxd.as<double>(), P + C, d_red.as<double>());
-        }
+        launch("ba.reduce", linearize_finish, dim3(1), dim3(1024), 0, st, nb_free, (const int*)d_camblk.as<int>(),
+               (const double*)d_campart.as<double>(), (const double*)d_chi.as<double>(), P,
+               (const double*)d_maxd.as<double>(), d_Hpp.as<double>(), d_bp.as<double>(), d_red.as<double>());
         MAGE_HIP(hipGetLastError());
         return MAGE_OK;
     }
@@ -1244,21 +1357,21 @@ struct BundleAdjuster {
     {
         mage_status r0;
         Problem pb = problem();
-        const int gp = (P + BA_THREADS - 1) / BA_THREADS;
         const int gmax = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
         double* xp = d_x.as<double>();
         double* xl = d_x.as<double>() + np;
         if ((r0 = reset_ctl_words()) != MAGE_OK) return r0;
-        if (P > 0 && !points_fixed) {
-            launch("ba.point_schur", point_schur, dim3(gp), dim3(BA_THREADS), 0, st, P, d_ptfree.as<int>(),
-                               d_Hll.as<double>(), d_bl.as<double>(), lam, d_Dinv.as<double>(), d_db.as<double>());
+        if (n_entries > 0 && !points_fixed) {
+            launch("ba.edge_schur", edge_schur, dim3((n_entries + BA_THREADS - 1) / BA_THREADS), dim3(BA_THREADS), 0, st,
+                   pb, n_entries, (const double*)d_Hll.as<double>(), (const double*)d_bl.as<double>(),
+                   (const double*)d_Hpl.as<double>(), lam, d_db.as<double>(), d_Z.as<double>());
         }
         if (n > 0) {
             if (np > 16 * CT_MAXT) MAGE_HIP(hipMemsetAsync(d_S.ptr, 0, (size_t)np * np * 8, st));
             {
-                launch("ba.schur_pairs", schur_pairs, dim3(npairs), dim3(BA_THREADS), 0, st, pb, d_pairs.as<int2>(),
+                launch("ba.schur_pairs", schur_pairs, dim3(8 * ((npairs + 7) / 8)), dim3(BA_THREADS), 0, st, pb, d_pairs.as<int2>(),
                                    d_camblk.as<int>(), d_blkidx.as<int>(), d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(),
-                                   d_Dinv.as<double>(), d_db.as<double>(), lam, np, d_S.as<double>(),
+                                   d_Z.as<double>(), d_bl.as<double>(), lam, np, npairs, d_S.as<double>(),
                                    d_rhs.as<double>());
             }
             {
@@ -1271,15 +1384,16 @@ struct BundleAdjuster {
             }
         }
         if (P > 0) {
-            launch("ba.point_backsub", point_backsub, dim3(gp), dim3(BA_THREADS), 0, st, pb, d_Hpl.as<double>(),
-                               d_Dinv.as<double>(), d_bl.as<double>(), xp, lam, xl, d_scale.as<double>());
+            launch("ba.point_backsub", point_backsub, dim3(group_grid(P)), dim3(BA_THREADS), 0, st, pb,
+                   (const double*)d_Z.as<double>(), (const double*)d_db.as<double>(), (const double*)d_bl.as<double>(),
+                   (const double*)xp, lam, xl, d_scale.as<double>());
         }
         if (std::max(P, C) > 0) {
             launch("ba.update_state", update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur),
                                xp, xl, d_bp.as<double>(), lam, d_scale.as<double>() + P);
         }
         if (P > 0) {
-            launch("ba.point_linearize", point_linearize, dim3(gp), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
+            launch("ba.point_linearize", point_linearize, dim3(group_grid(P)), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
                                d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
                                d_chi.as<double>(), d_maxd.as<double>());
         }

@@ -172,22 +172,25 @@ __device__ __forceinline__ void edge_eval(const Problem& pb, const State& s, int
     d_huber(pb.huber, chi2, rho0, rho1);
 }
 
-// EdgeProjectXYZ2UV::linearizeOplus pose block (2x6, row-major)
+// EdgeProjectXYZ2UV::linearizeOplus pose block (2x6, row-major).  One reciprocal of z instead of
+// g2o's per-entry divisions (the Jacobians feed H and b only, compared to tolerance; the
+// reprojection errors keep the exact divisions).
 __device__ __forceinline__ void jac_pose(const double xc[3], double f, double Jp[12])
 {
-    const double x = xc[0], y = xc[1], z = xc[2], z2 = z * z;
-    Jp[0] = x * y / z2 * f;
-    Jp[1] = -(1 + (x * x / z2)) * f;
-    Jp[2] = y / z * f;
-    Jp[3] = -1. / z * f;
+    const double x = xc[0], y = xc[1], iz = 1.0 / xc[2];
+    const double xi = x * iz, yi = y * iz, fi = f * iz;
+    Jp[0] = xi * yi * f;
+    Jp[1] = -(1 + xi * xi) * f;
+    Jp[2] = yi * f;
+    Jp[3] = -fi;
     Jp[4] = 0;
-    Jp[5] = x / z2 * f;
-    Jp[6] = (1 + y * y / z2) * f;
-    Jp[7] = -x * y / z2 * f;
-    Jp[8] = -x / z * f;
+    Jp[5] = xi * fi;
+    Jp[6] = (1 + yi * yi) * f;
+    Jp[7] = -xi * yi * f;
+    Jp[8] = -xi * f;
     Jp[9] = 0;
-    Jp[10] = -1. / z * f;
-    Jp[11] = y / z2 * f;
+    Jp[10] = -fi;
+    Jp[11] = yi * fi;
 }
 
 

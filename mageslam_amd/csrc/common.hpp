@@ -1,7 +1,10 @@
 // common.hpp — shared host/device helpers for the MI355X hot-path library (libmage_hot.so).
 #pragma once
 
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wc++20-extensions"  // inside the ROCm header's templates
 #include <hip/hip_ext.h>
+#pragma clang diagnostic pop
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

@@ -34,7 +34,7 @@ KERNEL_TAG = {
     "fast_nms_kernel": "orb.fast_nms", "select_kernel": "orb.select", "describe_kernel": "orb.describe", "describe_blurred_kernel": "orb.describe",
     "match_kernel": "match.two_way", "build_schur": "ba.build_schur", "cholesky_solve": "ba.cholesky_solve",
     "point_linearize": "ba.point_linearize", "cam_linearize": "ba.cam_linearize",
-    "point_backsub": "ba.point_backsub", "point_schur": "ba.point_schur", "update_state": "ba.update_state",
+    "point_backsub": "ba.point_backsub", "edge_schur": "ba.edge_schur", "chol_tiles": "ba.cholesky_solve", "drop_edges": "ba.drop_edges", "update_state": "ba.update_state",
     "outlier_pass": "ba.outlier_pass", "reduce3": "ba.reduce",
 }
 
