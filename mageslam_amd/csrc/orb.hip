@@ -779,7 +779,32 @@ struct DescParams {
     int taps[2 * KHMAX + 1];
     int dword_ok;
     int chunks, frames;  // describe_blurred_kernel grid decomposition
+    // random pattern (patch sizes other than 15 / 31): rotation-0 table rotated per keypoint by
+    // its angle (ComputeOrbDescriptors); kp_angle[7 * index] is the keypoint's angle field
+    int random;
+    const float* kp_angle;
 };
+
+// GetComputeOrbDescriptorsValue (OpenCVModified.cpp:442-448): the pattern point rotated in f32
+// (x a - y b, x b + y a; no contraction) and rounded half-to-even like cvRound.
+__device__ __forceinline__ char4 rotate_test(char4 e, float a, float b)
+{
+    const float x0 = __fsub_rn(__fmul_rn((float)e.x, a), __fmul_rn((float)e.y, b));
+    const float y0 = __fadd_rn(__fmul_rn((float)e.x, b), __fmul_rn((float)e.y, a));
+    const float x1 = __fsub_rn(__fmul_rn((float)e.z, a), __fmul_rn((float)e.w, b));
+    const float y1 = __fadd_rn(__fmul_rn((float)e.z, b), __fmul_rn((float)e.w, a));
+    return make_char4((signed char)__float2int_rn(x0), (signed char)__float2int_rn(y0),
+                      (signed char)__float2int_rn(x1), (signed char)__float2int_rn(y1));
+}
+
+// (a, b) = ((float)cos, (float)sin) of the angle in radians, angle *= (float)(CV_PI / 180) in
+// f32 (ComputeOrbDescriptors :466-467); the f64 cos / sin rounded to f32.
+__device__ __forceinline__ void pattern_rotation(float angle_deg, float& a, float& b)
+{
+    const float ang = __fmul_rn(angle_deg, (float)(3.1415926535897932384626433832795 / 180.0f));
+    a = (float)cos((double)ang);
+    b = (float)sin((double)ang);
+}
 
 // Orders one wave's LDS writes before its other lanes' reads (waves of a workgroup work on
 // different keypoints, so no workgroup barrier is needed).
@@ -862,11 +887,15 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
     }
     wave_lds_sync();
     // rotation: cvRound(angle / 12) % 30 (0 without orientation, OpenCVModified.cpp:748-754, :526)
-    const char4* pat = reinterpret_cast<const char4*>(pattern) + rot * 256;
+    // or, for the random pattern, the keypoint angle itself
+    const char4* pat = reinterpret_cast<const char4*>(pattern) + (p.random ? 0 : rot * 256);
+    float ra = 1.f, rb_ = 0.f;
+    if (p.random) pattern_rotation(p.kp_angle[7 * ((long long)f * p.out_cap + k)], ra, rb_);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
 #pragma unroll
     for (int chunk = 0; chunk < 4; chunk++) {
-        const char4 e = pat[chunk * kWave + lane];  // (x0, y0, x1, y1) of bit 64*chunk + lane
+        char4 e = pat[chunk * kWave + lane];  // (x0, y0, x1, y1) of bit 64*chunk + lane
+        if (p.random) e = rotate_test(e, ra, rb_);
         const int t0 = blur[wave][(R + e.y) * bd + R + e.x];
         const int t1 = blur[wave][(R + e.w) * bd + R + e.z];
         const unsigned long long m = __ballot(t0 < t1);
@@ -938,11 +967,14 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
         const int k = k0 + q;
         if (k >= n) break;
         const uint8_t* wb = &win[wave][q][sh[q]];
-        const char4* pr = pat + rot[q] * 256;  // cvRound(angle / 12) % 30 (:526)
+        const char4* pr = pat + (p.random ? 0 : rot[q] * 256);  // cvRound(angle / 12) % 30 (:526)
+        float ra = 1.f, rb_ = 0.f;  // random pattern: rotation by the keypoint angle
+        if (p.random) pattern_rotation(p.kp_angle[7 * ((long long)f * p.out_cap + k)], ra, rb_);
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            const char4 e = pr[c * kWave + lane];  // (x0, y0, x1, y1) of bit 64*c + lane
+            char4 e = pr[c * kWave + lane];  // (x0, y0, x1, y1) of bit 64*c + lane
+            if (p.random) e = rotate_test(e, ra, rb_);
             const int t0 = wb[(R + e.y) * WP + R + e.x];
             const int t1 = wb[(R + e.w) * WP + R + e.z];
             const unsigned long long m = __ballot(t0 < t1);
@@ -1128,11 +1160,28 @@ struct OrbDetector {
     int device = 0;
     int taps[2 * KHMAX + 1] = {0};
     int R = 7;
+    bool random_pattern = false;  // PatchSize not 15 / 31: MakeRandomPattern + per-keypoint rotation
     Geometry geo;
     DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n, blurred, pyr, rtab, lvl;
 };
 
 namespace {
+
+// MakeRandomPattern (OpenCVModified.cpp:551-560) with OpenCV 3.4.0's cv::RNG (multiply-with-carry:
+// state = (unsigned)state * 4164903690 + (state >> 32); uniform(a, b) = a + next() % (b - a)),
+// seed 0x34985739; stored as (x0, y0, x1, y1) per test like the pre-rotated tables.
+void make_random_pattern(int patch, int8_t out[1024])
+{
+    uint64_t st = 0x34985739u;
+    auto uniform = [&](int a, int b) {
+        st = (uint64_t)(uint32_t)st * 4164903690ull + (st >> 32);
+        return a == b ? a : (int)((uint32_t)st % (uint32_t)(b - a) + (uint32_t)a);
+    };
+    for (int i = 0; i < 512; i++) {
+        out[2 * i] = (int8_t)uniform(-patch / 2, patch / 2 + 1);
+        out[2 * i + 1] = (int8_t)uniform(-patch / 2, patch / 2 + 1);
+    }
+}
 
 // cv::getGaussianKernel(ksize, 2, CV_32F) -> convertTo(CV_32S, 1<<8) (OpenCV 3.4.0
 // createSeparableLinearFilter, 8U smoothing path; see DESIGN.md §Blur for why this path).
@@ -1413,6 +1462,8 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         dp.ksize = (int)s.gaussian_kernel_size;
         for (int i = 0; i < 2 * KHMAX + 1; i++) dp.taps[i] = o->taps[i];
         dp.dword_ok = (stride % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)d_frames % 4 == 0);
+        dp.random = o->random_pattern;
+        dp.kp_angle = reinterpret_cast<const float*>(d_kp) + 3;  // mage_keypoint.angle
         {
             if (fused_blur) {
                 dp.chunks = (int)((cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW));
@@ -1466,24 +1517,41 @@ mage_status mage_orb_create(const mage_orb_settings* settings, int device, mage_
     MAGE_REQUIRE(s.nlevels >= 1 && s.nlevels <= MAGE_MAX_LEVELS, MAGE_EUNSUPPORTED, "NumLevels must be 1..8");
     MAGE_REQUIRE(s.nlevels == 1 || (s.scale_factor > 1.0f && std::isfinite(s.scale_factor)), MAGE_EINVAL,
                  "ScaleFactor must be > 1");
-    MAGE_REQUIRE(s.patch_size == 15 || s.patch_size == 31, MAGE_EUNSUPPORTED,
-                 "only the pre-rotated patterns (PatchSize 15 / 31) are implemented");
     mage_status r = mage::bind_device(device);
     if (r != MAGE_OK) return r;
     auto* o = new mage_orb();
     o->s = s;
     o->device = device;
     if (s.gaussian_kernel_size > 1) mage::gaussian_taps((int)s.gaussian_kernel_size, 2.0, o->taps);
-    const int8_t* table = s.patch_size == 31 ? mage_bit_pattern_31_rotated : mage_bit_pattern_15_rotated;
-    // sampling radius: rotation 0 only, or all 30 rotations when orienting
+    // patch 15 / 31: the pre-rotated tables (30 rotations); any other size: MakeRandomPattern
+    // (OpenCVModified.cpp:877-884) in the rotation-0 slot, rotated per keypoint in the kernel
+    o->random_pattern = !(s.patch_size == 15 || s.patch_size == 31);
+    int8_t random_table[1024];
+    if (o->random_pattern) mage::make_random_pattern((int)s.patch_size, random_table);
+    const int8_t* table = o->random_pattern ? random_table
+                                            : (s.patch_size == 31 ? mage_bit_pattern_31_rotated : mage_bit_pattern_15_rotated);
+    // sampling radius: rotation 0 only, all 30 rotations when orienting, or for the random
+    // pattern rotated by any angle: ceil(|p|) bounds |cvRound| of the rotated point
     int R = 0;
-    for (int i = 0; i < (s.use_orientation ? 30 : 1) * 1024; i++) R = std::max(R, std::abs((int)table[i]));
+    if (o->random_pattern) {
+        for (int i = 0; i < 512; i++) {
+            const int x = table[2 * i], y = table[2 * i + 1];
+            R = std::max(R, s.use_orientation ? (int)std::ceil(std::sqrt((double)(x * x + y * y))) : std::max(std::abs(x), std::abs(y)));
+        }
+    } else {
+        for (int i = 0; i < (s.use_orientation ? 30 : 1) * 1024; i++) R = std::max(R, std::abs((int)table[i]));
+    }
+    if (R > mage::RMAX) {
+        delete o;
+        mage::set_error("pattern radius exceeds 18 (PatchSize too large for this build)");
+        return MAGE_EUNSUPPORTED;
+    }
     o->R = R;
     if ((r = o->pattern.reserve(30 * 1024)) != MAGE_OK) {
         delete o;
         return r;
     }
-    if (hipMemcpy(o->pattern.ptr, table, 30 * 1024, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(o->pattern.ptr, table, (o->random_pattern ? 1 : 30) * 1024, hipMemcpyHostToDevice) != hipSuccess) {
         delete o;
         mage::set_error("pattern upload failed");
         return MAGE_EDEVICE;

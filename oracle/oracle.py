@@ -74,6 +74,7 @@ def _declare(L):
     L.oracle_fast_atan2.argtypes = [f32, f32]
     L.oracle_fast_atan2.restype = f32
     L.oracle_umax.argtypes = [i32, vp]
+    L.oracle_random_pattern.argtypes = [i32, vp]
     L.oracle_ic_angle.argtypes = [vp, i32, i32, i32, vp, i32]
     L.oracle_ic_angle.restype = f32
     L.oracle_level_geometry.argtypes = [i32, i32, i32, f32, vp, vp, vp]
@@ -127,6 +128,13 @@ def resize_linear(img: np.ndarray, dw: int, dh: int) -> np.ndarray:
 
 def fast_atan2(y: float, x: float) -> float:
     return float(lib().oracle_fast_atan2(y, x))
+
+
+def random_pattern(patch_size: int) -> np.ndarray:
+    """MakeRandomPattern (OpenCVModified.cpp:551-560) as (x0, y0, x1, y1) int8 per test (256 x 4)."""
+    out = np.zeros(1024, np.int8)
+    lib().oracle_random_pattern(int(patch_size), _p(out))
+    return out
 
 
 def umax(half_patch: int) -> np.ndarray:

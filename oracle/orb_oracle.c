@@ -363,6 +363,55 @@ static void describe(const uint8_t* blurred, int stride, const signed char* patt
 }
 
 static int cv_roundf(float v) { return (int)lrintf(v); }
+
+/* cv::RNG (OpenCV 3.4.0 core/operations.hpp): multiply-with-carry, state = (unsigned)state *
+ * 4164903690 + (state >> 32); uniform(a, b) = a == b ? a : (int)(next() % (b - a) + a). */
+static uint32_t cv_rng_next(uint64_t* st)
+{
+    *st = (uint64_t)(uint32_t)*st * 4164903690ULL + (*st >> 32);
+    return (uint32_t)*st;
+}
+
+static int cv_rng_uniform(uint64_t* st, int a, int b)
+{
+    return a == b ? a : (int)(cv_rng_next(st) % (uint32_t)(b - a) + (uint32_t)a);
+}
+
+/* MakeRandomPattern (OpenCVModified.cpp:551-560): 512 points from RNG(0x34985739), x then y in
+ * [-patch/2, patch/2]; out holds them as (x0, y0, x1, y1) per test, the layout of the
+ * pre-rotated tables (test t compares points 2t and 2t+1, ComputeOrbDescriptors :475-486). */
+void oracle_random_pattern(int patch_size, signed char out[1024])
+{
+    uint64_t st = 0x34985739u;
+    for (int i = 0; i < 512; i++) {
+        out[2 * i] = (signed char)cv_rng_uniform(&st, -patch_size / 2, patch_size / 2 + 1);
+        out[2 * i + 1] = (signed char)cv_rng_uniform(&st, -patch_size / 2, patch_size / 2 + 1);
+    }
+}
+
+/* ComputeOrbDescriptors (OpenCVModified.cpp:452-492) for the random pattern: the keypoint angle
+ * (degrees) times (float)(CV_PI / 180) in f32, a = (float)cos, b = (float)sin, every point
+ * rotated in f32 (x a - y b, x b + y a) and rounded with cvRound (GetComputeOrbDescriptorsValue
+ * :442-448). */
+static void describe_random(const uint8_t* blurred, int stride, const signed char* pts, int cx, int cy,
+                            float angle_deg, uint8_t* desc)
+{
+    const uint8_t* center = blurred + (ptrdiff_t)cy * stride + cx;
+    const float angle = angle_deg * (float)(3.1415926535897932384626433832795 / 180.0f);  /* CV_PI */
+    const float a = (float)cos(angle), b = (float)sin(angle);
+    for (int i = 0; i < 32; i++) {
+        int val = 0;
+        for (int bit = 0; bit < 8; bit++) {
+            const signed char* q = pts + 4 * (8 * i + bit);
+            const float x0 = (float)q[0] * a - (float)q[1] * b, y0 = (float)q[0] * b + (float)q[1] * a;
+            const float x1 = (float)q[2] * a - (float)q[3] * b, y1 = (float)q[2] * b + (float)q[3] * a;
+            const int t0 = center[cv_roundf(y0) * stride + cv_roundf(x0)];
+            const int t1 = center[cv_roundf(y1) * stride + cv_roundf(x1)];
+            val |= (t0 < t1) << bit;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
 static int cv_floorf(float v) { int i = (int)v; return i - (i > v); }
 static int cv_ceilf(float v) { int i = (int)v; return i + (i < v); }
 
@@ -510,10 +559,11 @@ typedef struct {
     float strength;
 } level_kp;
 
-/* OrbDetector::DetectAndCompute (OpenCVModified.cpp:771-886) for patch 15/31: pyramid
+/* OrbDetector::DetectAndCompute (OpenCVModified.cpp:771-886): pyramid
  * (resize INTER_LINEAR), per-level FAST + border + Retain + ANMS with the per-level budget,
  * Insert truncation, ICAngles (UseOrientation), pt *= layerScale, per-level blur and the
- * pre-rotated descriptors.  Returns MAGE_OK and the count in *n_out. */
+ * descriptors: pre-rotated tables for patch 15 / 31, the random pattern (MakeRandomPattern +
+ * ComputeOrbDescriptors, :877-884) otherwise.  Returns MAGE_OK and the count in *n_out. */
 int oracle_orb_detect(const mage_orb_settings* s, const signed char* pattern_table,
                       const uint8_t* img, int w, int h, int stride, mage_keypoint* kp,
                       uint8_t* desc, uint32_t cap, uint32_t* n_out)
@@ -521,7 +571,9 @@ int oracle_orb_detect(const mage_orb_settings* s, const signed char* pattern_tab
     *n_out = 0;
     if (s->patch_size < 2) return MAGE_EINVAL;
     if (s->nlevels < 1 || s->nlevels > MAGE_MAX_LEVELS) return MAGE_EUNSUPPORTED;
-    if (s->patch_size != 15 && s->patch_size != 31) return MAGE_EUNSUPPORTED;
+    const int prerotated = s->patch_size == 15 || s->patch_size == 31;
+    signed char random_pts[1024];
+    if (!prerotated) oracle_random_pattern((int)s->patch_size, random_pts);
     if (s->gaussian_kernel_size > 1 && (s->gaussian_kernel_size % 2) == 0) return MAGE_EINVAL;
 
     const int L = (int)s->nlevels;
@@ -633,8 +685,12 @@ int oracle_orb_detect(const mage_orb_settings* s, const signed char* pattern_tab
             const int l = all[i].level;
             const float sc = 1.f / layerScale[l];
             const int cx = cv_roundf(kp[i].x * sc), cy = cv_roundf(kp[i].y * sc);
-            const int rot = cv_roundf(kp[i].angle / 12.0f) % 30;
-            describe(blurred[l], lw[l], pattern_table, cx, cy, rot, desc + 32 * (size_t)i);
+            if (prerotated) {
+                const int rot = cv_roundf(kp[i].angle / 12.0f) % 30;
+                describe(blurred[l], lw[l], pattern_table, cx, cy, rot, desc + 32 * (size_t)i);
+            } else {
+                describe_random(blurred[l], lw[l], random_pts, cx, cy, kp[i].angle, desc + 32 * (size_t)i);
+            }
         }
         for (int l = 0; l < L; l++) free(blurred[l]);
     }

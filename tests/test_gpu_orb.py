@@ -108,6 +108,8 @@ def test_rejects_bad_input(gpu):
         orb.OrbDetector(nlevels=9)
     with pytest.raises(MageError):
         orb.OrbDetector(nlevels=2, scaleFactor=1.0)
+    with pytest.raises(MageError):  # random-pattern radius 20 > 18
+        orb.OrbDetector(patchSize=41)
 
 
 def test_batch_device_equals_single(gpu):
@@ -173,6 +175,30 @@ def test_pyramid_orientation_matches_oracle(gpu, oracle, kw, size):
         st, okp, od = oracle.orb_detect(img, s)
         assert st == 0
         assert len(kp) == len(okp), (kw, size, t)
+        assert np.array_equal(kp_bytes(kp), kp_bytes(okp)), (kw, size, t)
+        assert np.array_equal(d, od), (kw, size, t)
+
+
+@pytest.mark.parametrize("kw", [dict(patchSize=21),
+                                dict(patchSize=9, useOrientation=True, nlevels=3),
+                                dict(patchSize=25, useOrientation=True),
+                                dict(patchSize=21, gaussianKernelSize=5, useOrientation=True, nlevels=2),
+                                dict(patchSize=35)])
+@pytest.mark.parametrize("size", [(640, 480), (333, 211)])
+def test_random_pattern_matches_oracle(gpu, oracle, kw, size):
+    # patch sizes other than 15 / 31: MakeRandomPattern + ComputeOrbDescriptors (per-keypoint
+    # f32 rotation of the pattern), OpenCVModified.cpp:877-884
+    w, h = size
+    nfeat = 1500
+    det = orb.OrbDetector(nfeatures=nfeat, **kw)
+    m = {"nlevels": "nlevels", "patchSize": "patch_size", "useOrientation": "use_orientation",
+         "gaussianKernelSize": "gaussian_kernel_size", "scaleFactor": "scale_factor"}
+    s = oracle.default_settings(nfeat, **{m[k]: v for k, v in kw.items()})
+    for t in (0, 3):
+        img = synth.frame(t, w, h)
+        kp, d = det.DetectAndCompute(img)
+        st, okp, od = oracle.orb_detect(img, s)
+        assert st == 0 and len(kp) == len(okp) > 0, (kw, size, t)
         assert np.array_equal(kp_bytes(kp), kp_bytes(okp)), (kw, size, t)
         assert np.array_equal(d, od), (kw, size, t)
 

@@ -277,3 +277,36 @@ def test_ba_golden(oracle):
     qt, xyz = b.state()
     assert np.allclose(qt, gold["qt"], atol=1e-9)
     assert np.array_equal(np.concatenate(outs), gold["outliers"])
+
+
+# ------------------------- random pattern (patch sizes other than 15 / 31) -------------------------
+
+
+def _cv_rng_pattern(patch):
+    """Independent restatement of MakeRandomPattern with OpenCV 3.4.0's cv::RNG (multiply-with-carry,
+    core/operations.hpp): state = (uint32)state * 4164903690 + (state >> 32); uniform(a, b) =
+    a + next() % (b - a)."""
+    st = 0x34985739
+    out = []
+    for _ in range(1024):
+        st = ((st & 0xFFFFFFFF) * 4164903690 + (st >> 32)) & 0xFFFFFFFFFFFFFFFF
+        a, b = -(patch // 2), patch // 2 + 1
+        out.append(a + (st & 0xFFFFFFFF) % (b - a))
+    return np.array(out, np.int8)
+
+
+@pytest.mark.parametrize("patch", [2, 9, 21, 25, 35])
+def test_random_pattern_known_answer(oracle, patch):
+    p = oracle.random_pattern(patch)
+    assert np.array_equal(p, _cv_rng_pattern(patch))
+    assert p.min() >= -(patch // 2) and p.max() <= patch // 2
+
+
+def test_random_pattern_detect_runs(oracle):
+    img = synth.frame(0, 320, 240)
+    s = oracle.default_settings(500, patch_size=21, use_orientation=True)
+    st, kp, d = oracle.orb_detect(img, s)
+    assert st == 0 and len(kp) > 0
+    assert d.any(axis=1).mean() > 0.9  # descriptors are not empty
+    st2, kp2, d2 = oracle.orb_detect(img, s)
+    assert np.array_equal(d, d2)
