@@ -832,7 +832,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
     __shared__ int rowp[DESC_WAVES][RAWMAX * BDMAX];
     __shared__ uint8_t blur[DESC_WAVES][BDMAX * BDMAX];
 
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave: scalar
     const int f = blockIdx.y;
     const int k = blockIdx.x * DESC_WAVES + wave;
     if (k >= (int)n_in[f]) return;
@@ -908,7 +908,9 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
 // the first LDS write, so the L2 round trips overlap, then runs the 256 tests per keypoint.
 constexpr int KPW = 4;
 
-template <int RB>
+// MULTI = false (one level, no orientation: the default configuration): level 0 and rotation 0
+// without the per-keypoint level lookups.
+template <int RB, bool MULTI>
 __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     DescParams p, const uint32_t* __restrict__ xy_in, const uint32_t* __restrict__ n_in,
     const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
@@ -919,7 +921,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     constexpr int RPI = kWave / ND;          // window rows per load instruction
     constexpr int NLD = (BDMAX + RPI - 1) / RPI;
     __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KPW][NLD * RPI * WP];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave: scalar
     // XCD-aware 1-D grid: workgroups are dispatched round-robin over the 8 XCDs, so block b runs
     // on XCD b % 8; all keypoint chunks of frame f get blocks = f (mod 8) and consecutive slots,
     // so the frame's blurred image is fetched into one XCD's L2 once (placement affects speed only)
@@ -939,7 +941,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     for (int q = 0; q < KPW; q++) {
         const long long ki = (long long)f * p.out_cap + min(k0 + q, n - 1);
         const uint32_t xy = xy_in[ki];
-        const int lv = p.lvl ? p.lvl[ki] : 0, l = lv >> 8;
+        const int lv = MULTI ? __builtin_amdgcn_readfirstlane(p.lvl[ki]) : 0, l = lv >> 8;  // wave-uniform
         rot[q] = lv & 0xFF;
         const uint8_t* src = p.lev.base[l] + (long long)f * p.lev.pitch[l];
         const int stride = p.lev.stride[l];
@@ -949,7 +951,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
         const int gx = min(max(xa + 4 * lc, 0), stride - 4);
 #pragma unroll
         for (int ld = 0; ld < NLD; ld++) {
-            const int gy = min(max(y0 + ld * RPI + lr, 0), p.lh[l] - 1);
+            const int gy = min(max(y0 + ld * RPI + lr, 0), p.lh[MULTI ? l : 0] - 1);
             v[q][ld] = *reinterpret_cast<const uint32_t*>(src + (long long)gy * stride + gx);
         }
     }
@@ -1469,8 +1471,10 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
                 dp.chunks = (int)((cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW));
                 dp.frames = (int)batch;
                 const dim3 g3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
-                auto kern = dp.R <= 7 ? describe_blurred_kernel<7>
-                                      : (dp.R <= 13 ? describe_blurred_kernel<13> : describe_blurred_kernel<RMAX>);
+                auto kern = multi ? (dp.R <= 7 ? describe_blurred_kernel<7, true>
+                                               : (dp.R <= 13 ? describe_blurred_kernel<13, true> : describe_blurred_kernel<RMAX, true>))
+                                  : (dp.R <= 7 ? describe_blurred_kernel<7, false>
+                                               : (dp.R <= 13 ? describe_blurred_kernel<13, false> : describe_blurred_kernel<RMAX, false>));
                 launch("orb.describe", kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, (const uint32_t*)o->xy.as<uint32_t>(),
                        d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
             } else {
