@@ -97,6 +97,31 @@ inline unsigned Match(const std::vector<Descriptor>& a, const std::vector<Descri
     return n;
 }
 
+// RadiusMatch (FeatureMatcher.cpp:294-378): the target KeypointSpatialIndex is built on the device
+// from targetKeypoints, so callers pass the keypoints instead of the index.  Optional position
+// overrides and masks (nullptr = none).  Clears and fills goodMatches (query order).
+inline unsigned RadiusMatch(const std::vector<KeyPoint>& queryKeypoints, const std::vector<float>* queryPositionOverrides,
+                            const std::vector<bool>* queryKeypointsMask, const std::vector<Descriptor>& queryDescriptors,
+                            const std::vector<KeyPoint>& targetKeypoints, const std::vector<bool>* targetKeypointsMask,
+                            const std::vector<Descriptor>& targetDescriptors, float radius, int maxHammingDist,
+                            int minHammingDifference, std::vector<DMatch>& goodMatches)
+{
+    std::vector<uint8_t> qm, tm;
+    if (queryKeypointsMask) qm.assign(queryKeypointsMask->begin(), queryKeypointsMask->end());
+    if (targetKeypointsMask) tm.assign(targetKeypointsMask->begin(), targetKeypointsMask->end());
+    goodMatches.resize(queryKeypoints.size());
+    uint32_t n = 0;
+    check(mage_radius_match(queryKeypoints.data(), queryPositionOverrides ? queryPositionOverrides->data() : nullptr,
+                            queryKeypointsMask ? qm.data() : nullptr,
+                            queryDescriptors.empty() ? nullptr : queryDescriptors.front().data(), (uint32_t)queryKeypoints.size(),
+                            targetKeypoints.data(), targetKeypointsMask ? tm.data() : nullptr,
+                            targetDescriptors.empty() ? nullptr : targetDescriptors.front().data(),
+                            (uint32_t)targetKeypoints.size(), radius, maxHammingDist, minHammingDifference,
+                            goodMatches.data(), (uint32_t)goodMatches.size(), &n));
+    goodMatches.resize(n);
+    return n;
+}
+
 struct BundlerParameters {
     bool ArePointsFixed{false};
 };

@@ -151,6 +151,35 @@ mage_status mage_hamming_match_batch_device(const uint8_t* d_desc_a, int64_t a_p
                                             int32_t min_difference, mage_dmatch* d_out,
                                             uint32_t cap, uint32_t* d_n, mage_stream stream);
 
+/* RadiusMatch (FeatureMatcher.cpp:294-378, per query :386-446) against the target set's
+ * KeypointSpatialIndex (KeypointSpatialIndex.cpp:46-106, replaced by an on-device band index):
+ * a query matches targets with |x - qx| <= radius, |y - qy| <= radius and the same octave; best /
+ * "second best" as the reference's loop visits candidates in ascending target index; accepted
+ * when second - best > min_difference; then only matches whose distance is the unique minimum
+ * among the matches to their target survive.  query_pos (n_query x 2 floats) overrides the query
+ * positions (queryKeypointPositionOverrides); masks and query_pos may be NULL.  At most 4096
+ * targets.  Host buffers, synchronous; output in query order (train_idx = target index). */
+mage_status mage_radius_match(const mage_keypoint* query_kp, const float* query_pos,
+                              const uint8_t* query_mask, const uint8_t* query_desc, uint32_t n_query,
+                              const mage_keypoint* target_kp, const uint8_t* target_mask,
+                              const uint8_t* target_desc, uint32_t n_target, float radius,
+                              int32_t max_distance, int32_t min_difference, mage_dmatch* out,
+                              uint32_t cap, uint32_t* n);
+
+/* Batched device form, one (query set, target set) pair per workgroup: pair p reads
+ * query_pitch / target_pitch entries further on (keypoints, positions, 32-byte descriptors),
+ * counts from d_n_query[p] / d_n_target[p]; no masks.  d_scratch: pairs x query_pitch int32.
+ * Results at d_out + p*cap, count in d_n[p]; bit 0 of *d_status is set when a target set exceeds
+ * 4096 (that pair reports 0 matches).  Asynchronous on `stream`. */
+mage_status mage_radius_match_batch_device(const mage_keypoint* d_query_kp, const float* d_query_pos,
+                                           const uint8_t* d_query_desc, int64_t query_pitch,
+                                           const uint32_t* d_n_query, const mage_keypoint* d_target_kp,
+                                           const uint8_t* d_target_desc, int64_t target_pitch,
+                                           const uint32_t* d_n_target, uint32_t pairs, float radius,
+                                           int32_t max_distance, int32_t min_difference,
+                                           int32_t* d_scratch, mage_dmatch* d_out, uint32_t cap,
+                                           uint32_t* d_n, uint32_t* d_status, mage_stream stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Local bundle adjustment — replaces BundlerLib (Dependencies/BundlerLib/Include/BundlerLib.h) */
 /* ------------------------------------------------------------------------------------------ */

@@ -1,0 +1,346 @@
+// radius.hip — RadiusMatch on MI355X (gfx950): spatially gated Hamming matching of a query keypoint
+// set against a target set (Core/MAGESLAM/Source/Tracking/FeatureMatcher.cpp:294-446) with the
+// target KeypointSpatialIndex (Image/KeypointSpatialIndex.cpp:46-106) replaced by an LDS-sorted
+// band index.
+//
+// One 1024-thread workgroup per (query set, target set) pair:
+//   1. targets -> 64-bit keys (octave, orderable f32 y, index), sorted ascending in LDS (the
+//      shared hybrid bitonic sort); the R-tree box query |x - qx| <= r, |y - qy| <= r, same
+//      octave becomes a binary search for the y band of the query's octave plus an exact f32
+//      box test on each band entry;
+//   2. one wave per query: lanes scan the band, mask, 32-byte Hamming distance.  The reference
+//      visits candidates in R-tree order and keeps "second best" = the previous best at the last
+//      improvement (:425-437).  With the deterministic ascending-index order
+//      that is order-free: best = min d (lowest index on ties, only if d <= maxDist) and
+//      second = min(maxDist + 1, min d over candidates with a lower index) — two wave reductions;
+//      accepted when second - best > minDiff (:441);
+//   3. batch post-pass (:342-371): a match survives when its distance is the unique minimum among
+//      the matches to its target (LDS atomicMin, then a count of the minima), ordered compaction in
+//      query order.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstring>
+
+#include "common.hpp"
+#include "lds_sort.hpp"
+
+namespace mage {
+namespace {
+
+constexpr int RM_MAXT = 4096;  // targets per pair held in LDS (NumFeatures-sized sets)
+
+struct RadiusParams {
+    const mage_keypoint* qkp;
+    const float* qpos;  // optional query positions (queryKeypointPositionOverrides), 2 floats each
+    const uint8_t* qmask;
+    const uint8_t* qdesc;
+    const uint32_t* nq;
+    long long q_pitch;  // query entries between pairs
+    const mage_keypoint* tkp;
+    const uint8_t* tmask;
+    const uint8_t* tdesc;
+    const uint32_t* nt;
+    long long t_pitch;
+    float radius;
+    int max_dist, min_diff;
+    unsigned cap;
+    int* res;  // per query: target << 9 | distance, or -1 (pairs x q_pitch)
+    mage_dmatch* out;
+    uint32_t* n_out;
+    uint32_t* status;  // bit 0: a target set exceeded RM_MAXT
+};
+
+__device__ __forceinline__ unsigned orderable(float v)
+{
+    const unsigned u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ unsigned long long band_key(int octave, float y, unsigned idx)
+{
+    return ((unsigned long long)(octave & 0xFF) << 56) | ((unsigned long long)orderable(y) << 24) | idx;
+}
+
+// first position in keys[0, n) (ascending) with keys[pos] >= k
+__device__ __forceinline__ int lower_bound_keys(const unsigned long long* keys, int n, unsigned long long k)
+{
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ unsigned wave_min(unsigned v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, off));
+    return v;
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams p)
+{
+    __shared__ unsigned long long keys[RM_MAXT];
+    __shared__ int bestD[RM_MAXT];
+    __shared__ int cnt[RM_MAXT];
+    __shared__ int wsum[SORT_THREADS / kWave];
+    __shared__ int s_base;
+    const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nq = (int)p.nq[pr], ntr = (int)p.nt[pr];
+    const mage_keypoint* qkp = p.qkp + pr * p.q_pitch;
+    const mage_keypoint* tkp = p.tkp + pr * p.t_pitch;
+    const uint8_t* qdesc = p.qdesc + pr * p.q_pitch * 32;
+    const uint8_t* tdesc = p.tdesc + pr * p.t_pitch * 32;
+    const uint8_t* qmask = p.qmask ? p.qmask + pr * p.q_pitch : nullptr;
+    const uint8_t* tmask = p.tmask ? p.tmask + pr * p.t_pitch : nullptr;
+    const float* qpos = p.qpos ? p.qpos + 2 * pr * p.q_pitch : nullptr;
+    int* res = p.res + pr * p.q_pitch;
+    if (ntr > RM_MAXT) {
+        if (tid == 0) {
+            p.n_out[pr] = 0;
+            atomicOr(p.status, 1u);
+        }
+        return;
+    }
+    // 1. band index: ascending keys via the descending sort of their complements (zero padding
+    //    sorts last)
+    int P = 1;
+    while (P < ntr) P <<= 1;
+    for (int i = tid; i < max(P, SORT_THREADS); i += SORT_THREADS)
+        keys[i] = i < ntr ? ~band_key(tkp[i].octave, tkp[i].y, (unsigned)i) : 0ull;
+    __syncthreads();
+    sort_desc(keys, P);
+    for (int i = tid; i < ntr; i += SORT_THREADS) keys[i] = ~keys[i];
+    for (int i = tid; i < ntr; i += SORT_THREADS) {
+        bestD[i] = INT_MAX;
+        cnt[i] = 0;
+    }
+    __syncthreads();
+
+    // 2. one wave per query
+    const float r = p.radius;
+    for (int q = wave; q < nq; q += SORT_THREADS / kWave) {
+        if (qmask && !qmask[q]) {
+            if (lane == 0) res[q] = -1;
+            continue;
+        }
+        const float px = qpos ? qpos[2 * q] : qkp[q].x, py = qpos ? qpos[2 * q + 1] : qkp[q].y;
+        const int oq = qkp[q].octave;
+        const float x0 = px - r, x1 = px + r, y0 = py - r, y1 = py + r;
+        const int lo = lower_bound_keys(keys, ntr, band_key(oq, y0, 0u));
+        const int hi = lower_bound_keys(keys, ntr, band_key(oq, y1, 0xFFFFFFu) + 1ull);
+        uint4 qa = *reinterpret_cast<const uint4*>(qdesc + 32 * (long long)q);
+        uint4 qb = *reinterpret_cast<const uint4*>(qdesc + 32 * (long long)q + 16);
+        // pass 1: best = min (d << 12 | t) over the box candidates
+        unsigned bestk = 0xFFFFFFFFu;
+        for (int i = lo + lane; i < hi; i += kWave) {
+            const int t = (int)(keys[i] & 0xFFFFFFu);
+            const float tx = tkp[t].x, ty = tkp[t].y;
+            if (!(tx >= x0 && tx <= x1 && ty >= y0 && ty <= y1)) continue;
+            if (tmask && !tmask[t]) continue;
+            const uint4 ta = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t);
+            const uint4 tb = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t + 16);
+            const unsigned d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w) +
+                               __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
+            bestk = min(bestk, d << 12 | (unsigned)t);
+        }
+        bestk = wave_min(bestk);
+        const int best = bestk == 0xFFFFFFFFu ? INT_MAX : (int)(bestk >> 12), tbest = (int)(bestk & 0xFFFu);
+        if (best > p.max_dist) {
+            if (lane == 0) res[q] = -1;
+            continue;
+        }
+        // pass 2: second = min(maxDist + 1, min d over candidates with a lower target index)
+        unsigned sec = (unsigned)(p.max_dist + 1);
+        for (int i = lo + lane; i < hi; i += kWave) {
+            const int t = (int)(keys[i] & 0xFFFFFFu);
+            if (t >= tbest) continue;
+            const float tx = tkp[t].x, ty = tkp[t].y;
+            if (!(tx >= x0 && tx <= x1 && ty >= y0 && ty <= y1)) continue;
+            if (tmask && !tmask[t]) continue;
+            const uint4 ta = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t);
+            const uint4 tb = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t + 16);
+            const unsigned d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w) +
+                               __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
+            sec = min(sec, d);
+        }
+        sec = wave_min(sec);
+        if (lane == 0) res[q] = ((int)sec - best > p.min_diff) ? (tbest << 9 | best) : -1;
+    }
+    __syncthreads();
+
+    // 3. unique minimum per target, then ordered compaction in query order
+    for (int q = tid; q < nq; q += SORT_THREADS) {
+        const int v = res[q];
+        if (v >= 0) atomicMin(&bestD[v >> 9], v & 0x1FF);
+    }
+    __syncthreads();
+    for (int q = tid; q < nq; q += SORT_THREADS) {
+        const int v = res[q];
+        if (v >= 0 && (v & 0x1FF) == bestD[v >> 9]) atomicAdd(&cnt[v >> 9], 1);
+    }
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    for (int q0 = 0; q0 < nq; q0 += SORT_THREADS) {
+        const int q = q0 + tid;
+        const int v = q < nq ? res[q] : -1;
+        const bool keep = v >= 0 && (v & 0x1FF) == bestD[v >> 9] && cnt[v >> 9] == 1;
+        const unsigned long long b = __ballot(keep);
+        const int before = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = __popcll(b);
+        __syncthreads();
+        int off = s_base;
+        for (int w = 0; w < wave; w++) off += wsum[w];
+        if (keep) {
+            const int pos = off + before;
+            if (pos < (int)p.cap) {
+                mage_dmatch m;
+                m.query_idx = q;
+                m.train_idx = v >> 9;
+                m.img_idx = 0;
+                m.distance = (float)(v & 0x1FF);
+                p.out[(long long)pr * p.cap + pos] = m;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int w = 0; w < SORT_THREADS / kWave; w++) tot += wsum[w];
+            s_base += tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) p.n_out[pr] = (uint32_t)s_base;
+}
+
+// host-side scratch for the synchronous single-pair entry point (one per device)
+struct RadiusScratch {
+    DeviceBuffer buf;
+    hipStream_t st = nullptr;
+};
+RadiusScratch g_radius[16];
+
+}  // namespace
+
+mage_status radius_match_launch(const RadiusParams& p, uint32_t pairs, hipStream_t st)
+{
+    launch("match.radius", radius_match_kernel, dim3(pairs), dim3(SORT_THREADS), 0, st, p);
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}
+
+}  // namespace mage
+
+extern "C" {
+
+mage_status mage_radius_match(const mage_keypoint* query_kp, const float* query_pos, const uint8_t* query_mask,
+                              const uint8_t* query_desc, uint32_t n_query, const mage_keypoint* target_kp,
+                              const uint8_t* target_mask, const uint8_t* target_desc, uint32_t n_target,
+                              float radius, int32_t max_distance, int32_t min_difference, mage_dmatch* out,
+                              uint32_t cap, uint32_t* n)
+{
+    using namespace mage;
+    MAGE_REQUIRE(n && (cap == 0 || out), MAGE_EINVAL, "null output");
+    *n = 0;
+    MAGE_REQUIRE((n_query == 0 || (query_kp && query_desc)) && (n_target == 0 || (target_kp && target_desc)),
+                 MAGE_EINVAL, "null input");
+    MAGE_REQUIRE(n_target <= (uint32_t)RM_MAXT, MAGE_EUNSUPPORTED, "more than 4096 target keypoints");
+    MAGE_REQUIRE(max_distance >= -1 && max_distance <= 256, MAGE_EINVAL, "maxHammingDist must be in [-1, 256]");
+    if (n_query == 0 || n_target == 0) return MAGE_OK;
+    int dev = 0;
+    MAGE_HIP(hipGetDevice(&dev));
+    mage_status r = bind_device(dev);
+    if (r != MAGE_OK) return r;
+    RadiusScratch& S = g_radius[dev & 15];
+    if (!S.st) MAGE_HIP(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+    // device layout: [qkp][tkp][qdesc][tdesc][qpos][qmask][tmask][res][out][counts]
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t oqk = 0, otk = al(oqk + 28ull * n_query), oqd = al(otk + 28ull * n_target),
+                 otd = al(oqd + 32ull * n_query), oqp = al(otd + 32ull * n_target), oqm = al(oqp + 8ull * n_query),
+                 otm = al(oqm + n_query), ores = al(otm + n_target), oout = al(ores + 4ull * n_query),
+                 ocnt = al(oout + 16ull * n_query), total = ocnt + 16;
+    if ((r = S.buf.reserve(total)) != MAGE_OK) return r;
+    char* b = S.buf.as<char>();
+    MAGE_HIP(hipMemcpyAsync(b + oqk, query_kp, 28ull * n_query, hipMemcpyHostToDevice, S.st));
+    MAGE_HIP(hipMemcpyAsync(b + otk, target_kp, 28ull * n_target, hipMemcpyHostToDevice, S.st));
+    MAGE_HIP(hipMemcpyAsync(b + oqd, query_desc, 32ull * n_query, hipMemcpyHostToDevice, S.st));
+    MAGE_HIP(hipMemcpyAsync(b + otd, target_desc, 32ull * n_target, hipMemcpyHostToDevice, S.st));
+    if (query_pos) MAGE_HIP(hipMemcpyAsync(b + oqp, query_pos, 8ull * n_query, hipMemcpyHostToDevice, S.st));
+    if (query_mask) MAGE_HIP(hipMemcpyAsync(b + oqm, query_mask, n_query, hipMemcpyHostToDevice, S.st));
+    if (target_mask) MAGE_HIP(hipMemcpyAsync(b + otm, target_mask, n_target, hipMemcpyHostToDevice, S.st));
+    const uint32_t counts[4] = {n_query, n_target, 0, 0};
+    MAGE_HIP(hipMemcpyAsync(b + ocnt, counts, 16, hipMemcpyHostToDevice, S.st));
+    RadiusParams p{};
+    p.qkp = reinterpret_cast<const mage_keypoint*>(b + oqk);
+    p.qpos = query_pos ? reinterpret_cast<const float*>(b + oqp) : nullptr;
+    p.qmask = query_mask ? reinterpret_cast<const uint8_t*>(b + oqm) : nullptr;
+    p.qdesc = reinterpret_cast<const uint8_t*>(b + oqd);
+    p.nq = reinterpret_cast<const uint32_t*>(b + ocnt);
+    p.q_pitch = n_query;
+    p.tkp = reinterpret_cast<const mage_keypoint*>(b + otk);
+    p.tmask = target_mask ? reinterpret_cast<const uint8_t*>(b + otm) : nullptr;
+    p.tdesc = reinterpret_cast<const uint8_t*>(b + otd);
+    p.nt = reinterpret_cast<const uint32_t*>(b + ocnt) + 1;
+    p.t_pitch = n_target;
+    p.radius = radius;
+    p.max_dist = max_distance;
+    p.min_diff = min_difference;
+    p.cap = n_query;
+    p.res = reinterpret_cast<int*>(b + ores);
+    p.out = reinterpret_cast<mage_dmatch*>(b + oout);
+    p.n_out = reinterpret_cast<uint32_t*>(b + ocnt) + 2;
+    p.status = reinterpret_cast<uint32_t*>(b + ocnt) + 3;
+    if ((r = radius_match_launch(p, 1, S.st)) != MAGE_OK) return r;
+    uint32_t got[2] = {0, 0};
+    MAGE_HIP(hipMemcpyAsync(got, b + ocnt + 8, 8, hipMemcpyDeviceToHost, S.st));
+    MAGE_HIP(hipStreamSynchronize(S.st));
+    const uint32_t m = got[0];
+    if (m > 0 && cap > 0)
+        MAGE_HIP(hipMemcpy(out, b + oout, 16ull * (m < cap ? m : cap), hipMemcpyDeviceToHost));
+    *n = m < cap ? m : cap;
+    MAGE_REQUIRE(m <= cap, MAGE_ECAPACITY, "output capacity too small");
+    return MAGE_OK;
+}
+
+mage_status mage_radius_match_batch_device(const mage_keypoint* d_query_kp, const float* d_query_pos,
+                                           const uint8_t* d_query_desc, int64_t query_pitch,
+                                           const uint32_t* d_n_query, const mage_keypoint* d_target_kp,
+                                           const uint8_t* d_target_desc, int64_t target_pitch,
+                                           const uint32_t* d_n_target, uint32_t pairs, float radius,
+                                           int32_t max_distance, int32_t min_difference, int32_t* d_scratch,
+                                           mage_dmatch* d_out, uint32_t cap, uint32_t* d_n, uint32_t* d_status,
+                                           mage_stream stream)
+{
+    using namespace mage;
+    if (pairs == 0) return MAGE_OK;
+    MAGE_REQUIRE(d_query_kp && d_query_desc && d_n_query && d_target_kp && d_target_desc && d_n_target &&
+                     d_scratch && d_out && d_n && d_status,
+                 MAGE_EINVAL, "null buffer");
+    MAGE_REQUIRE(query_pitch > 0 && target_pitch > 0, MAGE_EINVAL, "pitches must be positive");
+    MAGE_REQUIRE(max_distance >= -1 && max_distance <= 256, MAGE_EINVAL, "maxHammingDist must be in [-1, 256]");
+    RadiusParams p{};
+    p.qkp = d_query_kp;
+    p.qpos = d_query_pos;
+    p.qdesc = d_query_desc;
+    p.nq = d_n_query;
+    p.q_pitch = query_pitch;
+    p.tkp = d_target_kp;
+    p.tdesc = d_target_desc;
+    p.nt = d_n_target;
+    p.t_pitch = target_pitch;
+    p.radius = radius;
+    p.max_dist = max_distance;
+    p.min_diff = min_difference;
+    p.cap = cap;
+    p.res = d_scratch;
+    p.out = d_out;
+    p.n_out = d_n;
+    p.status = d_status;
+    return radius_match_launch(p, pairs, (hipStream_t)stream);
+}
+
+}  // extern "C"

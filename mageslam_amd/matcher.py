@@ -4,7 +4,8 @@
 minHammingDifference, goodMatches)` (Core/MAGESLAM/Source/Tracking/FeatureMatcher.h:68-77):
 descriptors are passed directly instead of AnalyzedImage, masks are boolean arrays, and the
 result is an array of cv::DMatch-layout records.  `GetDescriptorDistance` mirrors
-FeatureMatcher.cpp:453-504.
+FeatureMatcher.cpp:453-504.  `RadiusMatch` mirrors the batch RadiusMatch (FeatureMatcher.cpp:294-378)
+over a target KeypointSpatialIndex (built on the device from the target keypoints).
 """
 from __future__ import annotations
 
@@ -54,3 +55,43 @@ def match_batch_device(desc_a, a_pitch: int, n_a, desc_b, b_pitch: int, n_b, pai
     check(_lib.load().mage_hamming_match_batch_device(
         ptr(desc_a), a_pitch, ptr(n_a), ptr(desc_b), b_pitch, ptr(n_b), pairs, max_distance,
         min_difference, ptr(out), capacity, ptr(n_out), C.c_void_p(stream) if stream else None))
+
+
+def RadiusMatch(queryKeypoints, queryDescriptors, targetKeypoints, targetDescriptors, radius: float,
+                maxHammingDist: int = 30, minHammingDifference: int = 1, queryKeypointPositionOverrides=None,
+                queryKeypointsMask=None, targetKeypointsMask=None) -> np.ndarray:
+    """RadiusMatch on the GPU (FeatureMatcher.cpp:294-446): keypoints are cv::KeyPoint-layout
+    records (KP_DTYPE), descriptors (n, 32) uint8; returns DMatch records in query order
+    (queryIdx = query index, trainIdx = target index)."""
+    from ._lib import KP_DTYPE
+
+    qk = np.ascontiguousarray(queryKeypoints, KP_DTYPE)
+    tk = np.ascontiguousarray(targetKeypoints, KP_DTYPE)
+    qd = np.ascontiguousarray(queryDescriptors, np.uint8).reshape(-1, 32)
+    td = np.ascontiguousarray(targetDescriptors, np.uint8).reshape(-1, 32)
+    if len(qd) != len(qk) or len(td) != len(tk):
+        raise ValueError("one descriptor per keypoint")
+    qp = None
+    if queryKeypointPositionOverrides is not None:
+        qp = np.ascontiguousarray(queryKeypointPositionOverrides, np.float32).reshape(-1, 2)
+        if len(qp) != len(qk):
+            raise ValueError("one position override per query keypoint")
+    qm = None if queryKeypointsMask is None else np.ascontiguousarray(np.asarray(queryKeypointsMask, bool), np.uint8)
+    tm = None if targetKeypointsMask is None else np.ascontiguousarray(np.asarray(targetKeypointsMask, bool), np.uint8)
+    cap = max(len(qk), 1)
+    out = np.zeros(cap, DM_DTYPE)
+    n = C.c_uint32(0)
+    check(_lib.load().mage_radius_match(ptr(qk), ptr(qp), ptr(qm), ptr(qd), len(qk), ptr(tk), ptr(tm), ptr(td),
+                                        len(tk), float(radius), int(maxHammingDist), int(minHammingDifference),
+                                        ptr(out), cap, C.byref(n)))
+    return out[: n.value].copy()
+
+
+def radius_match_batch_device(query_kp, query_pos, query_desc, query_pitch: int, n_query, target_kp, target_desc,
+                              target_pitch: int, n_target, pairs: int, radius: float, max_distance: int,
+                              min_difference: int, scratch, out, capacity: int, n_out, status, stream=None) -> None:
+    """Batched device RadiusMatch over `pairs` (query set, target set) pairs (torch device tensors)."""
+    check(_lib.load().mage_radius_match_batch_device(
+        ptr(query_kp), ptr(query_pos), ptr(query_desc), query_pitch, ptr(n_query), ptr(target_kp), ptr(target_desc),
+        target_pitch, ptr(n_target), pairs, float(radius), max_distance, min_difference, ptr(scratch), ptr(out),
+        capacity, ptr(n_out), ptr(status), C.c_void_p(stream) if stream else None))

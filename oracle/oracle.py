@@ -75,6 +75,8 @@ def _declare(L):
     L.oracle_fast_atan2.restype = f32
     L.oracle_umax.argtypes = [i32, vp]
     L.oracle_random_pattern.argtypes = [i32, vp]
+    L.oracle_radius_match.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, u32, f32, i32, i32, vp, u32]
+    L.oracle_radius_match.restype = u32
     L.oracle_ic_angle.argtypes = [vp, i32, i32, i32, vp, i32]
     L.oracle_ic_angle.restype = f32
     L.oracle_level_geometry.argtypes = [i32, i32, i32, f32, vp, vp, vp]
@@ -204,6 +206,24 @@ def hamming(a: np.ndarray, b: np.ndarray) -> int:
     a = np.ascontiguousarray(a, np.uint8)
     b = np.ascontiguousarray(b, np.uint8)
     return int(lib().oracle_hamming(_p(a), _p(b)))
+
+
+def radius_match(qkp, qdesc, tkp, tdesc, radius, qpos=None, qmask=None, tmask=None, max_distance=30,
+                 min_difference=1):
+    """RadiusMatch (FeatureMatcher.cpp:294-446) over a target KeypointSpatialIndex; returns an
+    (n,) DM_DTYPE array in query order."""
+    qkp = np.ascontiguousarray(qkp, KP_DTYPE)
+    tkp = np.ascontiguousarray(tkp, KP_DTYPE)
+    qd = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+    td = np.ascontiguousarray(tdesc, np.uint8).reshape(-1, 32)
+    qp = None if qpos is None else np.ascontiguousarray(qpos, np.float32).reshape(-1, 2)
+    qm = None if qmask is None else np.ascontiguousarray(qmask, np.uint8)
+    tm = None if tmask is None else np.ascontiguousarray(tmask, np.uint8)
+    cap = max(len(qkp), 1)
+    out = np.zeros(cap, DM_DTYPE)
+    n = lib().oracle_radius_match(_p(qkp), _p(qp), _p(qm), _p(qd), len(qkp), _p(tkp), _p(tm), _p(td), len(tkp),
+                                  float(radius), int(max_distance), int(min_difference), _p(out), cap)
+    return out[:n].copy()
 
 
 def match(desc_a, desc_b, mask_a=None, mask_b=None, max_distance=30, min_difference=1):

@@ -746,6 +746,81 @@ static void best_rows(const uint8_t* q, const int* qi, int nq, const uint8_t* t,
     }
 }
 
+/* RadiusMatch (FeatureMatcher.cpp:294-378 batch, :386-446 per query) with the target
+ * KeypointSpatialIndex (KeypointSpatialIndex.cpp:46-106): the R-tree box query keeps targets with
+ * |x - qx| <= radius, |y - qy| <= radius (boundary inclusive) and the query's octave (octave
+ * coordinate 100 * octave, query range +-1).  Candidates are visited in ascending target index
+ * (the R-tree's visiting order is unspecified; SURVEY.md §8(f) 1 fixes this order).  Per query:
+ * best starts at maxDist + 1, second at INT_MAX; a strictly smaller distance moves best into
+ * second (:425-437); accepted when (second - best) > minDiff (:441).  Batch: when more than one
+ * query matched, a match survives only if its distance is the strict minimum among the matches
+ * to its target (:342-371).  Output in query order; returns the number of matches. */
+uint32_t oracle_radius_match(const mage_keypoint* qkp, const float* qpos, const uint8_t* qmask,
+                             const uint8_t* qdesc, uint32_t nq, const mage_keypoint* tkp,
+                             const uint8_t* tmask, const uint8_t* tdesc, uint32_t nt, float radius,
+                             int maxDist, int minDiff, mage_dmatch* out, uint32_t cap)
+{
+    mage_dmatch* almost = (mage_dmatch*)malloc(sizeof(mage_dmatch) * (nq + 1));
+    uint32_t na = 0;
+    for (uint32_t q = 0; q < nq; q++) {
+        if (qmask && !qmask[q]) continue;
+        const float px = qpos ? qpos[2 * q] : qkp[q].x, py = qpos ? qpos[2 * q + 1] : qkp[q].y;
+        const float oq = (float)qkp[q].octave * 100.0f;
+        int best = maxDist + 1, second = 2147483647, train = -1;
+        for (uint32_t t = 0; t < nt; t++) {
+            const float ot = (float)tkp[t].octave * 100.0f;
+            if (!(tkp[t].x >= px - radius && tkp[t].x <= px + radius && tkp[t].y >= py - radius &&
+                  tkp[t].y <= py + radius && ot >= oq - 1.0f && ot <= oq + 1.0f))
+                continue;
+            if (tmask && !tmask[t]) continue;
+            const int d = oracle_hamming(qdesc + 32 * (size_t)q, tdesc + 32 * (size_t)t);
+            if (d < best) {
+                train = (int)t;
+                second = best;
+                best = d;
+            }
+        }
+        if (train != -1 && (second - best) > minDiff) {
+            almost[na].query_idx = (int)q;
+            almost[na].train_idx = train;
+            almost[na].img_idx = 0;
+            almost[na].distance = (float)best;
+            na++;
+        }
+    }
+    uint32_t n = 0;
+    if (na > 1) {
+        float* bd = (float*)malloc(sizeof(float) * (nt + 1));
+        float* sd = (float*)malloc(sizeof(float) * (nt + 1));
+        for (uint32_t t = 0; t < nt; t++) bd[t] = sd[t] = 3.402823466e+38f;
+        for (uint32_t i = 0; i < na; i++) {
+            const int t = almost[i].train_idx;
+            if (almost[i].distance < bd[t]) {
+                sd[t] = bd[t];
+                bd[t] = almost[i].distance;
+            } else if (almost[i].distance < sd[t]) {
+                sd[t] = almost[i].distance;
+            }
+        }
+        for (uint32_t i = 0; i < na; i++) {
+            const int t = almost[i].train_idx;
+            if (almost[i].distance == bd[t] && bd[t] < sd[t]) {
+                if (n < cap) out[n] = almost[i];
+                n++;
+            }
+        }
+        free(bd);
+        free(sd);
+    } else {
+        for (uint32_t i = 0; i < na; i++) {
+            if (n < cap) out[n] = almost[i];
+            n++;
+        }
+    }
+    free(almost);
+    return n;
+}
+
 /* Match (FeatureMatcher.cpp:61-190).  Returns the number of matches written. */
 uint32_t oracle_match(const uint8_t* da, uint32_t na, const uint8_t* ma, const uint8_t* db,
                       uint32_t nb, const uint8_t* mb, int maxDist, int minDiff, mage_dmatch* out,

@@ -1,6 +1,7 @@
 // facade_demo.cpp — drives the C++ facades (include/mage/mage.hpp) the way the reference's
 // callers drive OrbDetector / Match / BundlerLib.  Usage: facade_demo <gray.raw> <w> <h> <out.bin>
-// Writes: u32 n, n keypoints (28 B), n descriptors (32 B), u32 self-matches, float BA mean_sq.
+// Writes: u32 n, n keypoints (28 B), n descriptors (32 B), u32 self-matches, float BA mean_sq,
+// u32 radius self-matches (radius 2 px).
 // Exits 3 if no GPU is usable (MAGE_EDEVICE), so the CPU test suite can still run it.
 #include <cstdio>
 #include <fstream>
@@ -44,6 +45,8 @@ int main(int argc, char** argv)
                 ba.SetObservation(3 * p + c, uv, c, p, 1.0f);
             }
         }
+        std::vector<mage::hot::DMatch> rmatches;
+        const unsigned nr = mage::hot::RadiusMatch(kps, nullptr, nullptr, desc, kps, nullptr, desc, 2.0f, 30, 1, rmatches);
         std::vector<unsigned> outliers;
         float ms = 0;
         for (int it = 0; it < 5; it++) ms = ba.StepBundleAdjustment({1.8f}, 1e6f, outliers);
@@ -54,6 +57,7 @@ int main(int argc, char** argv)
         o.write((const char*)desc.data(), (std::streamsize)(32 * n));
         o.write((const char*)&nm, 4);
         o.write((const char*)&ms, 4);
+        o.write((const char*)&nr, 4);
         std::cout << "keypoints " << n << " self-matches " << nm << " ba_mean_sq " << ms << "\n";
     } catch (const mage::hot::Error& e) {
         std::cerr << "mage error: " << e.what() << "\n";

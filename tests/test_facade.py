@@ -60,3 +60,7 @@ def test_facade_matches_python_api(gpu, tmp_path):
     assert n == len(pk) and np.array_equal(kp, pk.view(np.uint8).reshape(-1)) and np.array_equal(desc, pd)
     assert nm == n  # self-match keeps every distinct descriptor
     assert ms < 1e-3  # noiseless observations converge
+    nr = int(np.frombuffer(data[12 + 60 * n:16 + 60 * n], np.uint32)[0])
+    from mageslam_amd import matcher
+
+    assert nr == len(matcher.RadiusMatch(pk, pd, pk, pd, 2.0))

@@ -97,3 +97,109 @@ def test_batch_device(gpu, oracle):
         o = oracle.match(A[p, : na[p]], B[p, : nb[p]])
         assert n_h[p] == len(o)
         assert np.array_equal(out_h[p, : 16 * n_h[p]], dm_bytes(o).reshape(-1))
+
+
+# ------------------------- RadiusMatch (FeatureMatcher.cpp:294-446) -------------
+
+
+def _radius_pair(oracle, **kw):
+    s = oracle.default_settings(2000, **kw)
+    _, k0, d0 = oracle.orb_detect(synth.frame(0, 1280, 720), s)
+    _, k1, d1 = oracle.orb_detect(synth.frame(1, 1280, 720), s)
+    return k1, d1, k0, d0
+
+
+@pytest.mark.parametrize("radius,md,mdiff", [(15.0, 30, 1), (4.0, 30, 1), (40.0, 64, 3), (2.5, 0, 0)])
+def test_radius_match_frames(gpu, oracle, radius, md, mdiff):
+    qk, qd, tk, td = _radius_pair(oracle)
+    g = matcher.RadiusMatch(qk, qd, tk, td, radius, maxHammingDist=md, minHammingDifference=mdiff)
+    o = oracle.radius_match(qk, qd, tk, td, radius, max_distance=md, min_difference=mdiff)
+    assert len(o) > 0 or md == 0
+    assert np.array_equal(dm_bytes(g), dm_bytes(o))
+
+
+def test_radius_match_overrides_masks_octaves(gpu, oracle):
+    qk, qd, tk, td = _radius_pair(oracle, nlevels=3, patch_size=31, use_orientation=True)
+    rng = np.random.default_rng(5)
+    pos = np.stack([qk["x"] + 3.0, qk["y"] + 2.0], 1).astype(np.float32)  # predicted positions (pan)
+    qm = rng.random(len(qk)) < 0.8
+    tm = rng.random(len(tk)) < 0.9
+    for kw in (dict(), dict(qpos=pos), dict(qpos=pos, qmask=qm, tmask=tm)):
+        g = matcher.RadiusMatch(qk, qd, tk, td, 3.0, queryKeypointPositionOverrides=kw.get("qpos"),
+                                queryKeypointsMask=kw.get("qmask"), targetKeypointsMask=kw.get("tmask"))
+        o = oracle.radius_match(qk, qd, tk, td, 3.0, **kw)
+        assert np.array_equal(dm_bytes(g), dm_bytes(o)), kw
+    assert len(o) > 100
+    assert np.all(qk["octave"][o["query_idx"]] == tk["octave"][o["train_idx"]])
+
+
+def test_radius_match_ties(gpu, oracle):
+    # few distinct descriptors on a dense grid: exact ties everywhere exercise the "second best =
+    # previous best" rule and the unique-minimum-per-target pass
+    rng = np.random.default_rng(11)
+    from mageslam_amd._lib import KP_DTYPE
+
+    for nq, nt in ((500, 800), (1, 1), (3000, 4096)):
+        tk = np.zeros(nt, KP_DTYPE)
+        tk["x"] = rng.integers(0, 60, nt).astype(np.float32)
+        tk["y"] = rng.integers(0, 40, nt).astype(np.float32)
+        tk["octave"] = rng.integers(0, 2, nt)
+        qk = np.zeros(nq, KP_DTYPE)
+        qk["x"] = rng.integers(0, 60, nq).astype(np.float32) + 0.5
+        qk["y"] = rng.integers(0, 40, nq).astype(np.float32)
+        qk["octave"] = rng.integers(0, 2, nq)
+        pal = rng.integers(0, 256, (6, 32), dtype=np.uint8)
+        td = pal[rng.integers(0, 6, nt)] ^ (rng.random((nt, 32)) < 0.02).astype(np.uint8)
+        qd = pal[rng.integers(0, 6, nq)]
+        for r, md, mdiff in ((1.5, 30, 1), (3.0, 256, 0), (0.5, 8, 2)):
+            g = matcher.RadiusMatch(qk, qd, tk, td, r, maxHammingDist=md, minHammingDifference=mdiff)
+            o = oracle.radius_match(qk, qd, tk, td, r, max_distance=md, min_difference=mdiff)
+            assert np.array_equal(dm_bytes(g), dm_bytes(o)), (nq, nt, r, md, mdiff)
+
+
+def test_radius_match_edges(gpu, oracle):
+    from mageslam_amd._lib import KP_DTYPE, MageError
+
+    qk, qd, tk, td = _radius_pair(oracle)
+    assert len(matcher.RadiusMatch(qk[:0], qd[:0], tk, td, 10.0)) == 0
+    assert len(matcher.RadiusMatch(qk, qd, tk[:0], td[:0], 10.0)) == 0
+    big = np.zeros(4097, KP_DTYPE)
+    with pytest.raises(MageError):
+        matcher.RadiusMatch(qk, qd, big, np.zeros((4097, 32), np.uint8), 10.0)
+
+
+def test_radius_match_batch_device(gpu, oracle):
+    import torch
+
+    from mageslam_amd._lib import KP_DTYPE
+
+    pairs, pitch = 3, 2000
+    sets = []
+    for t in range(pairs + 1):
+        _, k, d = oracle.orb_detect(synth.frame(t, 640, 480), oracle.default_settings(pitch))
+        sets.append((k, d))
+    kp = np.zeros((pairs + 1, pitch), KP_DTYPE)
+    de = np.zeros((pairs + 1, pitch, 32), np.uint8)
+    nn = np.zeros(pairs + 1, np.uint32)
+    for i, (k, d) in enumerate(sets):
+        kp[i, : len(k)] = k
+        de[i, : len(k)] = d
+        nn[i] = len(k)
+    dev = "cuda"
+    kpt = torch.from_numpy(kp.view(np.uint8).reshape(pairs + 1, -1)).to(dev)
+    det = torch.from_numpy(de).to(dev)
+    nt = torch.from_numpy(nn.astype(np.int32)).to(dev)
+    scratch = torch.zeros(pairs * pitch, dtype=torch.int32, device=dev)
+    out = torch.zeros((pairs, pitch * 16), dtype=torch.uint8, device=dev)
+    nout = torch.zeros(pairs, dtype=torch.int32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    # query set p + 1 against target set p
+    matcher.radius_match_batch_device(kpt[1:], None, det[1:], pitch, nt[1:], kpt[:-1], det[:-1], pitch, nt[:-1],
+                                      pairs, 12.0, 30, 1, scratch, out, pitch, nout, status)
+    torch.cuda.synchronize()
+    assert int(status[0]) == 0
+    for p in range(pairs):
+        o = oracle.radius_match(sets[p + 1][0], sets[p + 1][1], sets[p][0], sets[p][1], 12.0)
+        n = int(nout[p])
+        assert n == len(o)
+        assert np.array_equal(out[p, : 16 * n].cpu().numpy(), dm_bytes(o))

@@ -310,3 +310,55 @@ def test_random_pattern_detect_runs(oracle):
     assert d.any(axis=1).mean() > 0.9  # descriptors are not empty
     st2, kp2, d2 = oracle.orb_detect(img, s)
     assert np.array_equal(d, d2)
+
+
+# ------------------------- RadiusMatch known answers (FeatureMatcher.cpp:294-446) ----------------
+
+
+def _kp(xs, ys, octs=None):
+    from mageslam_amd._lib import KP_DTYPE
+
+    k = np.zeros(len(xs), KP_DTYPE)
+    k["x"], k["y"] = xs, ys
+    if octs is not None:
+        k["octave"] = octs
+    return k
+
+
+def _desc_at_distance(base, d):
+    out = base.copy()
+    bits = np.unpackbits(out)
+    bits[:d] ^= 1
+    return np.packbits(bits)
+
+
+def test_radius_match_known_answers(oracle):
+    base = np.zeros(32, np.uint8)
+    q = _kp([10.0], [10.0])
+    qd = base[None]
+    # candidates in index order with distances 10, 5, 7: best 5 (index 1), second = 10 (the best
+    # before it) -> 10 - 5 > 1 accepted
+    t = _kp([10.0, 11.0, 12.0], [10.0, 10.0, 10.0])
+    td = np.stack([_desc_at_distance(base, d) for d in (10, 5, 7)])
+    m = oracle.radius_match(q, qd, t, td, 5.0)
+    assert len(m) == 1 and m[0]["train_idx"] == 1 and m[0]["distance"] == 5
+    # distances 5, 6 in index order: best 5 found first, second = maxDist + 1 = 31 (the "second" is
+    # only ever the previous best) -> accepted although 6 - 5 = 1 is not > 1
+    td2 = np.stack([_desc_at_distance(base, d) for d in (5, 6, 40)])
+    m = oracle.radius_match(q, qd, t, td2, 5.0)
+    assert len(m) == 1 and m[0]["train_idx"] == 0
+    # distances 6, 5: second = 6 -> 6 - 5 = 1 is not > minDiff = 1 -> rejected
+    td3 = np.stack([_desc_at_distance(base, d) for d in (6, 5, 40)])
+    assert len(oracle.radius_match(q, qd, t, td3, 5.0)) == 0
+    # box is inclusive; other octaves never match
+    t4 = _kp([15.0, 10.0], [15.0, 10.0], [0, 1])
+    td4 = np.stack([_desc_at_distance(base, 3), base])
+    m = oracle.radius_match(q, qd, t4, td4, 5.0)
+    assert len(m) == 1 and m[0]["train_idx"] == 0
+    # two queries with the same best distance to one target: neither survives the batch pass
+    q2 = _kp([10.0, 10.5], [10.0, 10.0])
+    t5 = _kp([10.0], [10.0])
+    td5 = _desc_at_distance(base, 4)[None]
+    assert len(oracle.radius_match(q2, np.stack([base, base]), t5, td5, 5.0)) == 0
+    # ... but a single query keeps its match
+    assert len(oracle.radius_match(q2[:1], base[None], t5, td5, 5.0)) == 1
