@@ -127,6 +127,29 @@ mage_status mage_orb_fast_score_map(const uint8_t* img, int32_t width, int32_t h
                                     int32_t stride, int32_t threshold, uint8_t* score_map,
                                     int device);
 
+/* Camera calibration as OrbFeatureDetector::Process receives it (Device/CameraCalibration.h):
+ * the linear intrinsics of GetCameraMatrix() and the OpenCV-ordered distortion coefficients of
+ * GetCVDistortionCoeffs() — K1 K2 P1 P2 K3 (Poly3k, ndist = 5) [K4 K5 K6] (Rational6k, ndist = 8);
+ * ndist = 0 for DistortionType::None. */
+typedef struct mage_calibration {
+    float fx, fy, cx, cy;
+    float dist[8];
+    int32_t ndist;
+} mage_calibration;
+
+/* OrbFeatureDetector::UndistortKeypoints (OrbFeatureDetector.cpp:30-62): keypoint positions
+ * through cv::undistortPoints(pts, distorted.K, distorted.dist, noArray(), undistorted.K),
+ * in place.  Process() calls it only when the two calibrations differ.  Host buffers. */
+mage_status mage_undistort_keypoints(const mage_calibration* distorted, const mage_calibration* undistorted,
+                                     mage_keypoint* kp, uint32_t n, int device);
+
+/* Batched device form: frame f's keypoints at d_kp + f*pitch (pitch in keypoints), d_n[f] of
+ * them (e.g. the outputs of mage_orb_detect_and_compute_batch_device).  Asynchronous. */
+mage_status mage_undistort_keypoints_batch_device(const mage_calibration* distorted,
+                                                  const mage_calibration* undistorted, mage_keypoint* d_kp,
+                                                  int64_t pitch, const uint32_t* d_n, uint32_t batch,
+                                                  mage_stream stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Hamming matching — replaces FeatureMatcher (Core/.../Source/Tracking/FeatureMatcher.h)        */
 /* ------------------------------------------------------------------------------------------ */

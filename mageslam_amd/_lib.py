@@ -22,6 +22,7 @@ EXPORTS = [
     "mage_profile_report", "mage_orb_create", "mage_orb_destroy", "mage_orb_detect_and_compute",
     "mage_orb_detect_and_compute_batch_device", "mage_orb_status", "mage_orb_reset_status",
     "mage_synth_frames_device", "mage_orb_fast_score_map",
+    "mage_undistort_keypoints", "mage_undistort_keypoints_batch_device",
     "mage_hamming_distance", "mage_hamming_match", "mage_hamming_match_batch_device",
     "mage_radius_match", "mage_radius_match_batch_device",
     "mage_ba_create", "mage_ba_destroy", "mage_ba_set_cameras", "mage_ba_fix_camera",
@@ -35,6 +36,19 @@ class MageError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
         self.status = status
+
+
+class Calibration(C.Structure):
+    """mage_calibration: CameraCalibration's linear intrinsics + OpenCV-ordered distortion."""
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("dist", C.c_float * 8), ("ndist", C.c_int32)]
+
+    @classmethod
+    def make(cls, fx, fy, cx, cy, dist=()):
+        d = list(dist)
+        if len(d) not in (0, 5, 8):
+            raise ValueError("distortion: 0 (None), 5 (Poly3k) or 8 (Rational6k) coefficients")
+        return cls(fx, fy, cx, cy, (C.c_float * 8)(*(d + [0.0] * (8 - len(d)))), len(d))
 
 
 class KeyPoint(C.Structure):
@@ -127,6 +141,8 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_orb_reset_status", st, vp, vp)
     sig("mage_synth_frames_device", st, vp, u32, i32, i32, i64, u32, u64, vp)
     sig("mage_orb_fast_score_map", st, vp, i32, i32, i32, i32, vp, C.c_int)
+    sig("mage_undistort_keypoints", st, vp, vp, vp, u32, C.c_int)
+    sig("mage_undistort_keypoints_batch_device", st, vp, vp, vp, i64, vp, u32, vp)
     sig("mage_hamming_distance", i32, vp, vp)
     sig("mage_hamming_match", st, vp, u32, vp, vp, u32, vp, i32, i32, vp, u32, C.POINTER(u32))
     sig("mage_hamming_match_batch_device", st, vp, i64, vp, vp, i64, vp, u32, i32, i32, vp, u32, vp, vp)

@@ -1424,6 +1424,85 @@ mage_status check_status(OrbDetector* o, hipStream_t st)
     return MAGE_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// 6. UndistortKeypoints (OrbFeatureDetector.cpp:30-62): cv::undistortPoints of OpenCV 3.4.0
+//    (imgproc/undistort.cpp, cvUndistortPoints) with R = noArray(), P = the undistorted camera
+//    matrix, in f64: normalise, 5 fixed-point iterations x = (x0 - delta(x)) * icdist(x) (the
+//    tilt compensation is the identity for zero tilt terms), then RR = P * I applied in
+//    homogeneous form, stored as float.  Same expressions, same order as the C source.
+// ------------------------------------------------------------------------------------------
+struct UndistortParams {
+    double cx, cy, ifx, ify;
+    double k[12];
+    int iters;
+    double RR[3][3];
+};
+
+__device__ __forceinline__ void undistort_point(const UndistortParams& u, float& px, float& py)
+{
+    const double* k = u.k;
+    double x = px, y = py;
+    x = (x - u.cx) * u.ifx;
+    y = (y - u.cy) * u.ify;
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < u.iters; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+        const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+        const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    const double xx = u.RR[0][0] * x + u.RR[0][1] * y + u.RR[0][2];
+    const double yy = u.RR[1][0] * x + u.RR[1][1] * y + u.RR[1][2];
+    const double ww = 1. / (u.RR[2][0] * x + u.RR[2][1] * y + u.RR[2][2]);
+    px = (float)(xx * ww);
+    py = (float)(yy * ww);
+}
+
+__global__ __launch_bounds__(256) void undistort_kernel(UndistortParams u, mage_keypoint* __restrict__ kp,
+                                                        long long pitch, const uint32_t* __restrict__ n)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y;
+    if (i >= (int)n[f]) return;
+    mage_keypoint& k = kp[(long long)f * pitch + i];
+    float x = k.x, y = k.y;
+    undistort_point(u, x, y);
+    k.x = x;
+    k.y = y;
+}
+
+UndistortParams undistort_params(const mage_calibration& d, const mage_calibration& p)
+{
+    UndistortParams u{};
+    const double fx = d.fx, fy = d.fy;
+    u.cx = d.cx;
+    u.cy = d.cy;
+    u.ifx = 1. / fx;
+    u.ify = 1. / fy;
+    for (int i = 0; i < d.ndist && i < 8; i++) u.k[i] = d.dist[i];
+    u.iters = d.ndist > 0 ? 5 : 0;
+    const double P[3][3] = {{p.fx, 0, p.cx}, {0, p.fy, p.cy}, {0, 0, 1}};
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) u.RR[r][c] = P[r][c];  // P * R with R = I
+    return u;
+}
+
+mage_status check_calibration(const mage_calibration* c)
+{
+    MAGE_REQUIRE(c, MAGE_EINVAL, "null calibration");
+    MAGE_REQUIRE(c->ndist == 0 || c->ndist == 5 || c->ndist == 8, MAGE_EINVAL,
+                 "ndist must be 0 (None), 5 (Poly3k) or 8 (Rational6k)");
+    MAGE_REQUIRE(c->fx != 0.f && c->fy != 0.f, MAGE_EINVAL, "zero focal length");
+    return MAGE_OK;
+}
+
+struct UndistortScratch {
+    DeviceBuffer kp, n;
+    hipStream_t st = nullptr;
+};
+UndistortScratch g_undistort[16];
+
 }  // namespace
 }  // namespace mage
 
@@ -1432,6 +1511,45 @@ using mage::OrbDetector;
 struct mage_orb : OrbDetector {};
 
 extern "C" {
+
+mage_status mage_undistort_keypoints_batch_device(const mage_calibration* distorted,
+                                                  const mage_calibration* undistorted, mage_keypoint* d_kp,
+                                                  int64_t pitch, const uint32_t* d_n, uint32_t batch,
+                                                  mage_stream stream)
+{
+    using namespace mage;
+    mage_status r;
+    if ((r = check_calibration(distorted)) != MAGE_OK || (r = check_calibration(undistorted)) != MAGE_OK) return r;
+    if (batch == 0 || pitch <= 0) return MAGE_OK;
+    MAGE_REQUIRE(d_kp && d_n, MAGE_EINVAL, "null buffer");
+    const UndistortParams u = undistort_params(*distorted, *undistorted);
+    launch("orb.undistort", undistort_kernel, dim3((unsigned)((pitch + 255) / 256), batch), dim3(256), 0,
+           (hipStream_t)stream, u, d_kp, (long long)pitch, d_n);
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}
+
+mage_status mage_undistort_keypoints(const mage_calibration* distorted, const mage_calibration* undistorted,
+                                     mage_keypoint* kp, uint32_t n, int device)
+{
+    using namespace mage;
+    mage_status r;
+    if ((r = check_calibration(distorted)) != MAGE_OK || (r = check_calibration(undistorted)) != MAGE_OK) return r;
+    if (n == 0) return MAGE_OK;
+    MAGE_REQUIRE(kp, MAGE_EINVAL, "null keypoints");
+    if ((r = bind_device(device)) != MAGE_OK) return r;
+    UndistortScratch& S = g_undistort[device & 15];
+    if (!S.st) MAGE_HIP(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+    if ((r = S.kp.reserve(sizeof(mage_keypoint) * (size_t)n)) != MAGE_OK || (r = S.n.reserve(4)) != MAGE_OK) return r;
+    MAGE_HIP(hipMemcpyAsync(S.kp.ptr, kp, sizeof(mage_keypoint) * (size_t)n, hipMemcpyHostToDevice, S.st));
+    MAGE_HIP(hipMemcpyAsync(S.n.ptr, &n, 4, hipMemcpyHostToDevice, S.st));
+    if ((r = mage_undistort_keypoints_batch_device(distorted, undistorted, S.kp.as<mage_keypoint>(), n,
+                                                   S.n.as<uint32_t>(), 1, (mage_stream)S.st)) != MAGE_OK)
+        return r;
+    MAGE_HIP(hipMemcpyAsync(kp, S.kp.ptr, sizeof(mage_keypoint) * (size_t)n, hipMemcpyDeviceToHost, S.st));
+    MAGE_HIP(hipStreamSynchronize(S.st));
+    return MAGE_OK;
+}
 
 mage_status mage_orb_create(const mage_orb_settings* settings, int device, mage_orb** out)
 {

@@ -133,3 +133,37 @@ def synth_frames_device(out, count: int, width: int, height: int, t0: int, seed:
     pitch = width * height if frame_pitch is None else frame_pitch
     check(_lib.load().mage_synth_frames_device(ptr(out), count, width, height, pitch, t0, seed,
                                                C.c_void_p(stream) if stream else None))
+
+
+def _cal_key(c):
+    return (c.fx, c.fy, c.cx, c.cy, c.ndist, tuple(c.dist[: c.ndist]))
+
+
+def UndistortKeypoints(keypoints: np.ndarray, distortedCalibration, undistortedCalibration,
+                       device: int = 0) -> np.ndarray:
+    """OrbFeatureDetector::UndistortKeypoints (OrbFeatureDetector.cpp:30-62) on the GPU: returns a
+    copy of the keypoints with positions through cv::undistortPoints(distorted K, distortion,
+    noArray(), undistorted K).  Calibrations are `_lib.Calibration` records."""
+    kp = np.array(keypoints, dtype=KP_DTYPE, copy=True)
+    check(_lib.load().mage_undistort_keypoints(C.byref(distortedCalibration), C.byref(undistortedCalibration),
+                                               ptr(kp), len(kp), int(device)))
+    return kp
+
+
+class OrbFeatureDetector:
+    """OrbFeatureDetector (Image/OrbFeatureDetector.cpp:64-100): DetectAndCompute, then keypoint
+    undistortion when the distorted and undistorted calibrations differ (operator!=)."""
+
+    def __init__(self, settings: FeatureExtractorSettings | None = None, device: int = 0):
+        s = settings or FeatureExtractorSettings()
+        self.detector = OrbDetector(s.GaussianKernelSize, s.NumFeatures, s.ScaleFactor, s.NumLevels, s.PatchSize,
+                                    s.FastThreshold, s.UseOrientation, s.FeatureFactor, s.FeatureStrength,
+                                    s.StrongResponse, s.MinRobustnessFactor, s.MaxRobustnessFactor, s.NumCellsX,
+                                    s.NumCellsY, device=device)
+        self.device = device
+
+    def Process(self, distortedCalibration, undistortedCalibration, image: np.ndarray):
+        kp, desc = self.detector.DetectAndCompute(image)
+        if _cal_key(distortedCalibration) != _cal_key(undistortedCalibration):
+            kp = UndistortKeypoints(kp, distortedCalibration, undistortedCalibration, self.device)
+        return kp, desc

@@ -75,6 +75,7 @@ def _declare(L):
     L.oracle_fast_atan2.restype = f32
     L.oracle_umax.argtypes = [i32, vp]
     L.oracle_random_pattern.argtypes = [i32, vp]
+    L.oracle_undistort_points.argtypes = [vp, vp, i32, vp, vp, i32]
     L.oracle_radius_match.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, u32, f32, i32, i32, vp, u32]
     L.oracle_radius_match.restype = u32
     L.oracle_ic_angle.argtypes = [vp, i32, i32, i32, vp, i32]
@@ -137,6 +138,17 @@ def random_pattern(patch_size: int) -> np.ndarray:
     out = np.zeros(1024, np.int8)
     lib().oracle_random_pattern(int(patch_size), _p(out))
     return out
+
+
+def undistort_points(pts, k_dist, dist, k_new) -> np.ndarray:
+    """cv::undistortPoints(pts, K_dist, dist, noArray(), K_new) (OrbFeatureDetector.cpp:55);
+    k_* = (fx, fy, cx, cy), dist = 0, 5 or 8 OpenCV-ordered coefficients."""
+    p = np.ascontiguousarray(pts, np.float32).reshape(-1, 2).copy()
+    kd = np.ascontiguousarray(k_dist, np.float32)
+    kn = np.ascontiguousarray(k_new, np.float32)
+    d = np.ascontiguousarray(dist, np.float32)
+    lib().oracle_undistort_points(_p(kd), _p(d) if len(d) else None, len(d), _p(kn), _p(p), len(p))
+    return p
 
 
 def umax(half_patch: int) -> np.ndarray:

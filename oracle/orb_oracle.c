@@ -746,6 +746,40 @@ static void best_rows(const uint8_t* q, const int* qi, int nq, const uint8_t* t,
     }
 }
 
+/* UndistortKeypoints (OrbFeatureDetector.cpp:30-62): OpenCV 3.4.0 cvUndistortPoints with
+ * R = noArray() and P = the undistorted camera matrix — f64 normalisation, 5 fixed-point
+ * iterations (tilt compensation is the identity for zero tilt terms), RR = P * I in homogeneous
+ * form, float output.  kd / kp: fx, fy, cx, cy; dist: ndist (0, 5 or 8) coefficients K1 K2 P1 P2
+ * K3 [K4 K5 K6]; pts: n (x, y) pairs, in place. */
+void oracle_undistort_points(const float* kd, const float* dist, int ndist, const float* kp, float* pts, int n)
+{
+    double k[14] = {0};
+    for (int i = 0; i < ndist && i < 8; i++) k[i] = dist[i];
+    const int iters = ndist > 0 ? 5 : 0;
+    const double fx = kd[0], fy = kd[1], cx = kd[2], cy = kd[3];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    const double RR[3][3] = {{kp[0], 0, kp[2]}, {0, kp[1], kp[3]}, {0, 0, 1}};
+    for (int i = 0; i < n; i++) {
+        double x = pts[2 * i], y = pts[2 * i + 1];
+        x = (x - cx) * ifx;
+        y = (y - cy) * ify;
+        const double x0 = x, y0 = y;
+        for (int j = 0; j < iters; j++) {
+            double r2 = x * x + y * y;
+            double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+            double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        double xx = RR[0][0] * x + RR[0][1] * y + RR[0][2];
+        double yy = RR[1][0] * x + RR[1][1] * y + RR[1][2];
+        double ww = 1. / (RR[2][0] * x + RR[2][1] * y + RR[2][2]);
+        pts[2 * i] = (float)(xx * ww);
+        pts[2 * i + 1] = (float)(yy * ww);
+    }
+}
+
 /* RadiusMatch (FeatureMatcher.cpp:294-378 batch, :386-446 per query) with the target
  * KeypointSpatialIndex (KeypointSpatialIndex.cpp:46-106): the R-tree box query keeps targets with
  * |x - qx| <= radius, |y - qy| <= radius (boundary inclusive) and the query's octave (octave

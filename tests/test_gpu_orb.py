@@ -222,3 +222,65 @@ def test_pyramid_batch_device_equals_single(gpu):
         assert ni == len(k1)
         assert np.array_equal(kp[i, : ni * 28].cpu().numpy(), kp_bytes(k1))
         assert np.array_equal(desc[i, :ni].cpu().numpy(), d1)
+
+
+# ------------------------- UndistortKeypoints (OrbFeatureDetector.cpp:30-62) -------------------------
+
+
+@pytest.mark.parametrize("dist", [(-0.12, 0.03, 1e-4, -2e-4, 0.0),
+                                  (0.05, -0.01, -3e-4, 1e-4, 0.002, 0.02, -0.005, 0.001),
+                                  (-0.3, 0.1, 0.0, 0.0, -0.02)])
+def test_undistort_keypoints_matches_oracle(gpu, oracle, dist):
+    from mageslam_amd._lib import Calibration
+
+    img = synth.frame(2, 1280, 720)
+    kp, _ = orb.OrbDetector(nfeatures=2000).DetectAndCompute(img)
+    cd = Calibration.make(900.0, 905.0, 640.0, 360.0, dist)
+    cu = Calibration.make(880.0, 880.0, 642.5, 358.0)
+    g = orb.UndistortKeypoints(kp, cd, cu)
+    pts = np.stack([kp["x"], kp["y"]], 1)
+    o = oracle.undistort_points(pts, (900.0, 905.0, 640.0, 360.0), dist, (880.0, 880.0, 642.5, 358.0))
+    assert np.array_equal(g["x"], o[:, 0]) and np.array_equal(g["y"], o[:, 1])
+    for f in ("size", "angle", "response", "octave", "class_id"):
+        assert np.array_equal(g[f], kp[f])
+
+
+def test_undistort_batch_device_and_process(gpu, oracle):
+    import torch
+
+    from mageslam_amd._lib import KP_DTYPE, Calibration, MageError
+
+    w, h, B, cap = 640, 480, 3, 1000
+    frames = torch.empty((B, h, w), dtype=torch.uint8, device="cuda")
+    orb.synth_frames_device(frames, B, w, h, 0, synth.FRAME_SEED)
+    det = orb.OrbDetector(nfeatures=cap)
+    kp = torch.zeros((B, cap * 28), dtype=torch.uint8, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    det.detect_and_compute_batch_device(frames, w, h, kp, desc, n, cap)
+    before = kp.cpu().numpy().copy()
+    cd = Calibration.make(500.0, 500.0, 320.0, 240.0, (-0.2, 0.05, 0.0, 0.0, 0.0))
+    cu = Calibration.make(500.0, 500.0, 320.0, 240.0)
+    from mageslam_amd import _lib
+    import ctypes as C
+
+    _lib.check(_lib.load().mage_undistort_keypoints_batch_device(C.byref(cd), C.byref(cu), _lib.ptr(kp), cap,
+                                                                  _lib.ptr(n), B, None))
+    torch.cuda.synchronize()
+    after = kp.cpu().numpy()
+    for i in range(B):
+        ni = int(n[i])
+        k0 = before[i, : 28 * ni].view(KP_DTYPE)
+        k1 = after[i, : 28 * ni].view(KP_DTYPE)
+        assert np.array_equal(k1, orb.UndistortKeypoints(k0, cd, cu))
+        assert np.array_equal(after[i, 28 * ni:], before[i, 28 * ni:])  # beyond the count: untouched
+    # Process: undistortion only when the calibrations differ (OrbFeatureDetector.cpp:96-99)
+    fd = orb.OrbFeatureDetector(orb.FeatureExtractorSettings(NumFeatures=cap))
+    img = frames[0].cpu().numpy()
+    k_same, _ = fd.Process(cu, cu, img)
+    k_plain, _ = det.DetectAndCompute(img)
+    assert np.array_equal(k_same, k_plain)
+    k_und, _ = fd.Process(cd, cu, img)
+    assert np.array_equal(k_und, orb.UndistortKeypoints(k_plain, cd, cu))
+    with pytest.raises(MageError):
+        orb.UndistortKeypoints(k_plain, Calibration(500.0, 500.0, 320.0, 240.0, (C.c_float * 8)(), 3), cu)

@@ -362,3 +362,32 @@ def test_radius_match_known_answers(oracle):
     assert len(oracle.radius_match(q2, np.stack([base, base]), t5, td5, 5.0)) == 0
     # ... but a single query keeps its match
     assert len(oracle.radius_match(q2[:1], base[None], t5, td5, 5.0)) == 1
+
+
+# ------------------------- UndistortKeypoints (cv::undistortPoints restatement) -------------------
+
+
+def _distort(pts, k, dist):
+    """Forward OpenCV distortion model (cv::projectPoints): normalised -> distorted pixels."""
+    fx, fy, cx, cy = k
+    d = list(dist) + [0.0] * (8 - len(dist))
+    k1, k2, p1, p2, k3, k4, k5, k6 = d
+    x, y = pts[:, 0].astype(np.float64), pts[:, 1].astype(np.float64)
+    r2 = x * x + y * y
+    radial = (1 + ((k3 * r2 + k2) * r2 + k1) * r2) / (1 + ((k6 * r2 + k5) * r2 + k4) * r2)
+    xd = x * radial + 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
+    yd = y * radial + p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
+    return np.stack([xd * fx + cx, yd * fy + cy], 1)
+
+
+@pytest.mark.parametrize("dist", [(-0.12, 0.03, 1e-4, -2e-4, 0.0),
+                                  (0.05, -0.01, -3e-4, 1e-4, 0.002, 0.02, -0.005, 0.001)])
+def test_undistort_points_inverts_distortion(oracle, dist):
+    rng = np.random.default_rng(2)
+    kd = (900.0, 905.0, 640.0, 360.0)
+    norm = np.stack([rng.uniform(-0.5, 0.5, 400), rng.uniform(-0.3, 0.3, 400)], 1)
+    distorted = _distort(norm, kd, dist).astype(np.float32)
+    out = oracle.undistort_points(distorted, kd, dist, kd)  # P = the same K: back to the ideal pixels
+    ideal = np.stack([norm[:, 0] * kd[0] + kd[2], norm[:, 1] * kd[1] + kd[3]], 1)
+    assert np.abs(out - ideal).max() < 0.02  # 5 fixed-point iterations on mild distortion
+    assert np.array_equal(oracle.undistort_points(distorted, kd, (), kd), distorted)  # no coefficients
