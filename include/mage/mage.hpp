@@ -190,6 +190,33 @@ public:
         m_info[idx] = informationMatrixScalar;
         m_dirty = true;
     }
+    // Tether constraints (BundlerLib.cpp:229-257, 311-350); quaternions are (x, y, z, w).
+    void AllocateFixedDistanceConstraints(size_t count) { m_teth[MAGE_TETHER_DISTANCE].resize(count); m_dirty = true; }
+    void SetFixedDistanceConstraint(size_t idx, size_t cameraIndex1, size_t cameraIndex2, float distance = 1.0f,
+                                    float weight = 1.0f)
+    {
+        m_teth[MAGE_TETHER_DISTANCE][idx] = {(uint32_t)cameraIndex1, (uint32_t)cameraIndex2, weight, {distance}};
+        m_dirty = true;
+    }
+    void AllocateRelativeRotationConstraints(size_t count) { m_teth[MAGE_TETHER_ROTATION].resize(count); m_dirty = true; }
+    void SetRelativeRotationConstraint(size_t idx, size_t cameraIndex1, size_t cameraIndex2, const float* deltaRotationXYZW,
+                                       float weight = 1.0f)
+    {
+        Tether t{(uint32_t)cameraIndex1, (uint32_t)cameraIndex2, weight, {}};
+        std::copy(deltaRotationXYZW, deltaRotationXYZW + 4, t.params);
+        m_teth[MAGE_TETHER_ROTATION][idx] = t;
+        m_dirty = true;
+    }
+    void AllocateRelativeTransformConstraints(size_t count) { m_teth[MAGE_TETHER_TRANSFORM].resize(count); m_dirty = true; }
+    void SetRelativeTransformConstraint(size_t idx, size_t cameraIndex1, size_t cameraIndex2, const float* deltaPosition,
+                                        const float* deltaRotationXYZW, float weight)
+    {
+        Tether t{(uint32_t)cameraIndex1, (uint32_t)cameraIndex2, weight, {}};
+        std::copy(deltaPosition, deltaPosition + 3, t.params);
+        std::copy(deltaRotationXYZW, deltaRotationXYZW + 4, t.params + 3);
+        m_teth[MAGE_TETHER_TRANSFORM][idx] = t;
+        m_dirty = true;
+    }
     void SetCurrentLambda(float userLambda) { check(mage_ba_set_lambda(m_handle, userLambda)); }
     float GetCurrentLambda() const
     {
@@ -234,8 +261,29 @@ private:
         check(mage_ba_set_points(m_handle, (uint32_t)(m_points.size() / 3), m_points.data()));
         check(mage_ba_set_observations(m_handle, (uint32_t)m_cam.size(), m_uv.data(), m_cam.data(), m_pt.data(),
                                        m_info.data()));
+        static const int stride[3] = {1, 4, 7};
+        for (uint32_t kind = 0; kind < 3; kind++) {
+            const auto& v = m_teth[kind];
+            std::vector<uint32_t> c1(v.size()), c2(v.size());
+            std::vector<float> params(v.size() * stride[kind]), weight(v.size());
+            for (size_t i = 0; i < v.size(); i++) {
+                c1[i] = v[i].cam1;
+                c2[i] = v[i].cam2;
+                weight[i] = v[i].weight;
+                std::copy(v[i].params, v[i].params + stride[kind], &params[i * stride[kind]]);
+            }
+            check(mage_ba_set_tethers(m_handle, kind, (uint32_t)v.size(), c1.data(), c2.data(), params.data(),
+                                      weight.data()));
+        }
         m_dirty = false;
     }
+
+    struct Tether {
+        uint32_t cam1, cam2;
+        float weight;
+        float params[7];
+    };
+    std::vector<Tether> m_teth[3];
 
     BundlerParameters m_params;
     mage_ba* m_handle = nullptr;

@@ -230,8 +230,16 @@ mage_status mage_ba_set_observations(mage_ba* ba, uint32_t n, const float* uv,
 /* SetCurrentLambda / GetCurrentLambda (BundlerLib.cpp:354-362). */
 mage_status mage_ba_set_lambda(mage_ba* ba, float lambda);
 mage_status mage_ba_get_lambda(mage_ba* ba, float* lambda);
-/* Tether constraints (SetFixedDistance/RelativeRotation/RelativeTransformConstraint,
- * BundlerLib.cpp:311-350).  Not implemented yet: returns MAGE_EUNSUPPORTED. */
+/* Tether constraints: Allocate*Constraints(n) + Set*Constraint(i, ...) for one kind
+ * (BundlerLib.cpp:229-257, 311-350; called from BundleAdjust.cpp:155-189).  Replaces the set of
+ * that kind; the others are kept.  params per tether:
+ *   MAGE_TETHER_DISTANCE  (SetFixedDistanceConstraint)     1 float: distance
+ *   MAGE_TETHER_ROTATION  (SetRelativeRotationConstraint)  4 floats: quaternion x, y, z, w
+ *   MAGE_TETHER_TRANSFORM (SetRelativeTransformConstraint) 7 floats: position x, y, z, then
+ *                                                          quaternion x, y, z, w
+ * weight[i] is the constraint weight.  Camera indices must be < the camera count and distinct
+ * (MAGE_EINVAL otherwise); set the cameras first. */
+enum { MAGE_TETHER_DISTANCE = 0, MAGE_TETHER_ROTATION = 1, MAGE_TETHER_TRANSFORM = 2 };
 mage_status mage_ba_set_tethers(mage_ba* ba, uint32_t kind, uint32_t n, const uint32_t* cam1,
                                 const uint32_t* cam2, const float* params, const float* weight);
 

@@ -13,6 +13,7 @@ import numpy as np
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libmage_hot.so"
 
 MAGE_OK, MAGE_EINVAL, MAGE_EDEVICE, MAGE_ENOMEM, MAGE_EUNSUPPORTED, MAGE_ECAPACITY = range(6)
+MAGE_TETHER_DISTANCE, MAGE_TETHER_ROTATION, MAGE_TETHER_TRANSFORM = range(3)
 STATUS_NAMES = {0: "MAGE_OK", 1: "MAGE_EINVAL", 2: "MAGE_EDEVICE", 3: "MAGE_ENOMEM",
                 4: "MAGE_EUNSUPPORTED", 5: "MAGE_ECAPACITY"}
 

@@ -29,7 +29,8 @@ class BundlerLib:
         self._cams = None
         self._pts = None
         self._obs = None
-        self._uploaded = {"cams": False, "pts": False, "obs": False}
+        self._teth = {}
+        self._uploaded = {"cams": False, "pts": False, "obs": False, "teth": True}
 
     def close(self) -> None:
         if getattr(self, "_h", None) and self._h.value:
@@ -94,14 +95,60 @@ class BundlerLib:
         self._pts = np.ascontiguousarray(g.points, np.float32)
         self._obs = dict(uv=np.ascontiguousarray(g.uv, np.float32), cam=np.ascontiguousarray(g.cam, np.uint32),
                          pt=np.ascontiguousarray(g.pt, np.uint32), info=np.ascontiguousarray(g.info, np.float32))
-        self._uploaded = {"cams": False, "pts": False, "obs": False}
+        for kind in range(3):  # a fresh graph carries no tethers until set_tethers
+            self._alloc_tethers(kind, 0)
+        self._uploaded.update(cams=False, pts=False, obs=False, teth=False)
+
+    # --- tether constraints (BundlerLib.cpp:229-257, 311-350) ---
+    _TETHER_STRIDE = (1, 4, 7)
+
+    def _alloc_tethers(self, kind: int, count: int) -> None:
+        self._teth[kind] = dict(c1=np.zeros(count, np.uint32), c2=np.zeros(count, np.uint32),
+                                params=np.zeros((count, self._TETHER_STRIDE[kind]), np.float32),
+                                weight=np.ones(count, np.float32))
+        self._uploaded["teth"] = False
+
+    def _set_tether(self, kind: int, idx: int, c1: int, c2: int, params, weight: float) -> None:
+        t = self._teth[kind]
+        t["c1"][idx], t["c2"][idx] = c1, c2
+        t["params"][idx] = np.asarray(params, np.float32).reshape(-1)
+        t["weight"][idx] = weight
+        self._uploaded["teth"] = False
 
     def AllocateFixedDistanceConstraints(self, count: int) -> None:
-        if count:
-            raise NotImplementedError("tether constraints are not implemented in this build")
+        self._alloc_tethers(_lib.MAGE_TETHER_DISTANCE, count)
 
-    AllocateRelativeRotationConstraints = AllocateFixedDistanceConstraints
-    AllocateRelativeTransformConstraints = AllocateFixedDistanceConstraints
+    def SetFixedDistanceConstraint(self, idx: int, cameraIndex1: int, cameraIndex2: int, distance: float = 1.0,
+                                   weight: float = 1.0) -> None:
+        self._set_tether(_lib.MAGE_TETHER_DISTANCE, idx, cameraIndex1, cameraIndex2, [distance], weight)
+
+    def AllocateRelativeRotationConstraints(self, count: int) -> None:
+        self._alloc_tethers(_lib.MAGE_TETHER_ROTATION, count)
+
+    def SetRelativeRotationConstraint(self, idx: int, cameraIndex1: int, cameraIndex2: int, deltaRotation,
+                                      weight: float = 1.0) -> None:
+        """deltaRotation: quaternion (x, y, z, w) (Eigen::Quaternionf coefficient order)."""
+        self._set_tether(_lib.MAGE_TETHER_ROTATION, idx, cameraIndex1, cameraIndex2, deltaRotation, weight)
+
+    def AllocateRelativeTransformConstraints(self, count: int) -> None:
+        self._alloc_tethers(_lib.MAGE_TETHER_TRANSFORM, count)
+
+    def SetRelativeTransformConstraint(self, idx: int, cameraIndex1: int, cameraIndex2: int, deltaPosition,
+                                       deltaRotation, weight: float) -> None:
+        p = np.concatenate([np.asarray(deltaPosition, np.float32).reshape(3),
+                            np.asarray(deltaRotation, np.float32).reshape(4)])
+        self._set_tether(_lib.MAGE_TETHER_TRANSFORM, idx, cameraIndex1, cameraIndex2, p, weight)
+
+    def set_tethers(self, t) -> None:
+        """Bulk form for a synth.Tethers-like object (distance, rotation, transform tuples of
+        (cam1, cam2, params, weight))."""
+        for kind, (c1, c2, params, w) in enumerate((t.distance, t.rotation, t.transform)):
+            self._alloc_tethers(kind, len(c1))
+            tt = self._teth[kind]
+            tt["c1"][:] = c1
+            tt["c2"][:] = c2
+            tt["params"][:] = np.asarray(params, np.float32).reshape(len(c1), self._TETHER_STRIDE[kind])
+            tt["weight"][:] = w
 
     def SetCurrentLambda(self, userLambda: float) -> None:
         check(_lib.load().mage_ba_set_lambda(self._h, float(userLambda)))
@@ -126,6 +173,11 @@ class BundlerLib:
             check(L.mage_ba_set_observations(self._h, len(o["cam"]), ptr(o["uv"]), ptr(o["cam"]), ptr(o["pt"]),
                                              ptr(o["info"])))
             self._uploaded["obs"] = True
+        if not self._uploaded["teth"]:
+            for kind, t in sorted(self._teth.items()):
+                check(L.mage_ba_set_tethers(self._h, kind, len(t["c1"]), ptr(t["c1"]), ptr(t["c2"]),
+                                            ptr(np.ascontiguousarray(t["params"])), ptr(t["weight"])))
+            self._uploaded["teth"] = True
 
     def StepBundleAdjustment(self, huberWidthPerIteration, maxErrorSquare: float, outliers: list | None = None) -> float:
         """BundlerLib::StepBundleAdjustment (BundlerLib.cpp:364-447): returns the mean squared

@@ -141,6 +141,94 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
     maxd_part[p] = free_p ? fmax(fabs(H[0]), fmax(fabs(H[3]), fabs(H[5]))) : 0.0;
 }
 
+// Tether edges (thread per tether; a window carries a handful): error and chi2 = e^T Omega e
+// into chi[t] (appended after the points' robust chi2); with `linearize`, the Jacobians —
+// BaseMultiEdge::linearizeOplus central differences (delta 1e-9 through the exp-map oplus) for the
+// distance / rotation constraints, EdgeSE3Expmap's adjoints for the transform — and the blocks
+// H11 = J1^T Omega J1, H22, H12 = J1^T Omega J2, b_v = J_v^T (-Omega e) into out[t][TETHER_OUT].
+__global__ __launch_bounds__(64) void tether_eval(const Tether* __restrict__ teth, int nt, State s, int linearize,
+                                                  double* __restrict__ chi, double* __restrict__ out)
+{
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= nt) return;
+    const Tether T = teth[i];
+    if (!T.active) {
+        chi[i] = 0;
+        return;
+    }
+    double q1[4], t1[3], q2[4], t2[3];
+    for (int k = 0; k < 4; k++) {
+        q1[k] = s.q[4 * T.c1 + k];
+        q2[k] = s.q[4 * T.c2 + k];
+    }
+    for (int k = 0; k < 3; k++) {
+        t1[k] = s.t[3 * T.c1 + k];
+        t2[k] = s.t[3 * T.c2 + k];
+    }
+    double e[6];
+    const int dim = d_tether_error(T, q1, t1, q2, t2, e);
+    const double om = T.kind == 2 ? T.w : 1.0;
+    double c2 = 0;
+    for (int r = 0; r < dim; r++) c2 += e[r] * e[r];
+    chi[i] = om * c2;
+    if (!linearize) return;
+    double J[2][36];
+    if (T.kind == 2) {
+        double a[4], at[3], b[4], bt[3], iq[4], it[3], mq[4], mt[3];
+        d_se3_inv(T.mq, T.mt, mq, mt);  // Tij^-1
+        d_se3_inv(q2, t2, iq, it);
+        d_se3_mul(iq, it, T.mq, T.mt, a, at);  // Tj^-1 Tij
+        d_se3_inv(q1, t1, iq, it);
+        d_se3_mul(iq, it, mq, mt, b, bt);  // Ti^-1 Tij^-1
+        d_se3_adj(a, at, false, J[0]);
+        d_se3_adj(b, bt, true, J[1]);
+    } else {
+        const double delta = 1e-9, scalar = 1 / (2 * delta);
+        for (int v = 0; v < 2; v++) {
+            if ((v ? T.h2 : T.h1) < 0) continue;
+            for (int d = 0; d < 6; d++) {
+                double add[6] = {0, 0, 0, 0, 0, 0}, ep[6], em[6];
+                double pq[4], pt[3];
+                add[d] = delta;
+                for (int k = 0; k < 4; k++) pq[k] = v ? q2[k] : q1[k];
+                for (int k = 0; k < 3; k++) pt[k] = v ? t2[k] : t1[k];
+                d_oplus(pq, pt, add);
+                if (v) d_tether_error(T, q1, t1, pq, pt, ep);
+                else d_tether_error(T, pq, pt, q2, t2, ep);
+                add[d] = -delta;
+                for (int k = 0; k < 4; k++) pq[k] = v ? q2[k] : q1[k];
+                for (int k = 0; k < 3; k++) pt[k] = v ? t2[k] : t1[k];
+                d_oplus(pq, pt, add);
+                if (v) d_tether_error(T, q1, t1, pq, pt, em);
+                else d_tether_error(T, pq, pt, q2, t2, em);
+                J[v][d] = scalar * (ep[0] - em[0]);
+            }
+        }
+    }
+    double* o = out + (long long)i * TETHER_OUT;
+    for (int v = 0; v < 2; v++) {
+        if ((v ? T.h2 : T.h1) < 0) continue;
+        const double* Jv = J[v];
+        for (int r = 0; r < 6; r++) {
+            double g = 0;
+            for (int m = 0; m < dim; m++) g += Jv[m * 6 + r] * (-om * e[m]);
+            o[108 + 6 * v + r] = g;
+            for (int c = 0; c < 6; c++) {
+                double h = 0;
+                for (int m = 0; m < dim; m++) h += Jv[m * 6 + r] * Jv[m * 6 + c];
+                o[36 * v + r * 6 + c] = h * om;
+            }
+        }
+    }
+    if (T.h1 >= 0 && T.h2 >= 0)
+        for (int r = 0; r < 6; r++)
+            for (int c = 0; c < 6; c++) {
+                double h = 0;
+                for (int m = 0; m < dim; m++) h += J[0][m * 6 + r] * J[1][m * 6 + c];
+                o[72 + r * 6 + c] = h * om;
+            }
+}
+
 // Block sum of `acc[N]` over a workgroup of T threads; the result lands in red[0][0..N).
 template <int N, int T = BA_THREADS>
 __device__ __forceinline__ void block_sum(double (&acc)[N], double (*red)[N])
@@ -206,6 +294,8 @@ __global__ __launch_bounds__(1024) void linearize_finish(int nb, const int* __re
                                                          const double* __restrict__ part,
                                                          const double* __restrict__ chi, int P,
                                                          const double* __restrict__ maxd_pts,
+                                                         const Tether* __restrict__ teth, int nt,
+                                                         const double* __restrict__ tout,
                                                          double* __restrict__ Hpp, double* __restrict__ bp,
                                                          double* __restrict__ out)
 {
@@ -216,6 +306,24 @@ __global__ __launch_bounds__(1024) void linearize_finish(int nb, const int* __re
         const int h = i / 27, k = i % 27;
         double v = 0;
         for (int q = 0; q < CAM_CHUNKS; q++) v += part[((long long)h * CAM_CHUNKS + q) * 27 + k];
+        // tethers after the observations (g2o's addEdge order), each in its set order
+        if (nt > 0) {
+            int r = 0, c = k;
+            if (k < 21)
+                while (c >= 6 - r) {
+                    c -= 6 - r;
+                    r++;
+                }
+            for (int t = 0; t < nt; t++) {
+                const Tether& T = teth[t];
+                if (!T.active) continue;
+                for (int vtx = 0; vtx < 2; vtx++) {
+                    if ((vtx ? T.h2 : T.h1) != h) continue;
+                    const double* o = tout + (long long)t * TETHER_OUT;
+                    v += k < 21 ? o[36 * vtx + r * 6 + (r + c)] : o[108 + 6 * vtx + (k - 21)];
+                }
+            }
+        }
         cams[h][k] = v;
     }
     __syncthreads();
@@ -238,6 +346,7 @@ __global__ __launch_bounds__(1024) void linearize_finish(int nb, const int* __re
         va += chi[i];
         vm = fmax(vm, maxd_pts[i]);
     }
+    for (int i = tid; i < nt; i += 1024) va += chi[P + i];
     for (int h = tid; h < nb; h += 1024)
         for (int r = 0; r < 6; r++) vm = fmax(vm, fabs(cams[h][r * 6 - r * (r - 1) / 2]));
     sa[tid] = va;
@@ -360,7 +469,9 @@ __global__ __launch_bounds__(BA_THREADS) void schur_pairs(Problem pb, const int2
                                                           const double* __restrict__ Hpl,
                                                           const double* __restrict__ Z,
                                                           const double* __restrict__ bl, double lambda,
-                                                          int np, int npairs, double* __restrict__ S,
+                                                          int np, int npairs, const int* __restrict__ ptstart,
+                                                          const int* __restrict__ ptlist,
+                                                          const double* __restrict__ tout, double* __restrict__ S,
                                                           double* __restrict__ rhs)
 {
     __shared__ double red[BA_THREADS / kWave][42];
@@ -417,6 +528,12 @@ __global__ __launch_bounds__(BA_THREADS) void schur_pairs(Problem pb, const int2
         const int r = i / 6, k = i % 6;
         double v = -red[0][i];
         if (diag) v += Hpp[36 * (long long)c1 + i] + (r == k ? lambda : 0.0);
+        // tether H12 blocks of this camera pair (code = 2 t + transposed)
+        for (int j = ptstart[pi]; j < ptstart[pi + 1]; j++) {
+            const int code = ptlist[j];
+            const double* H12 = tout + (long long)(code >> 1) * TETHER_OUT + 72;
+            v += (code & 1) ? H12[k * 6 + r] : H12[r * 6 + k];
+        }
         S[(long long)(6 * h1 + r) * np + 6 * h2 + k] = v;
         S[(long long)(6 * h2 + k) * np + 6 * h1 + r] = v;
     }
@@ -1091,6 +1208,8 @@ struct BundleAdjuster {
     std::vector<double> q, t, camk, p, uv, info;
     std::vector<int> fixed, ecam, ept;
     std::vector<unsigned char> removed;
+    std::vector<Tether> teth;      // distance, rotation, transform tethers (set order)
+    std::vector<int> cam_tethers;  // active tethers per camera (keeps a camera in the system)
     bool dirty = true;  // full (re)initialisation needed: setters or a camera left the system
     bool useless = false, state_on_device = false, host_state_stale = false, err_initialized = false;
     int iteration = 0;
@@ -1125,7 +1244,7 @@ struct BundleAdjuster {
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
-        d_pairs, d_olist, d_camcnt, d_blkidx, d_Z, d_campart;
+        d_pairs, d_olist, d_camcnt, d_blkidx, d_Z, d_campart, d_teth, d_tout, d_ptstart, d_ptlist;
     int n_entries = 0;  // point-CSR entries (active edges at initialisation)
     int nb_free = 0;    // cameras in the reduced system
     mage_ba_stats stats{};
@@ -1161,7 +1280,8 @@ struct BundleAdjuster {
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_db, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk, &d_pairs,
-                        &d_olist, &d_camcnt, &d_blkidx, &d_Z, &d_campart})
+                        &d_olist, &d_camcnt, &d_blkidx, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptstart,
+                        &d_ptlist})
             b->release();
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
@@ -1204,6 +1324,16 @@ struct BundleAdjuster {
             if (a) {
                 camHas[ecam[e]] = 1;
                 ptHas[ept[e]] = 1;
+            }
+        }
+        // tethers: active unless both cameras are fixed; their cameras join the system
+        cam_tethers.assign(C, 0);
+        for (auto& T : teth) {
+            T.active = !(fixed[T.c1] && fixed[T.c2]);
+            if (T.active) {
+                camHas[T.c1] = camHas[T.c2] = 1;
+                cam_tethers[T.c1]++;
+                cam_tethers[T.c2]++;
             }
         }
         camh.assign(C, -1);
@@ -1265,11 +1395,28 @@ struct BundleAdjuster {
                         if (x <= y) mark[(size_t)x * nb + y] = 1;
             }
             for (int h = 0; h < nb; h++) mark[(size_t)h * nb + h] = 1;
+            for (auto& T : teth) {
+                T.h1 = camh[T.c1];
+                T.h2 = camh[T.c2];
+                if (T.active && T.h1 >= 0 && T.h2 >= 0)
+                    mark[(size_t)std::min(T.h1, T.h2) * nb + std::max(T.h1, T.h2)] = 1;
+            }
             for (int x = 0; x < nb; x++)
                 for (int y = x; y < nb; y++)
                     if (mark[(size_t)x * nb + y]) pairs.push_back(make_int2(x, y));
         }
         npairs = (int)pairs.size();
+        // per pair: the tethers whose H12 lands in its block (code 2 t + transposed), set order
+        std::vector<int> ptstart(npairs + 1, 0), ptlist;
+        for (int pi = 0; pi < npairs; pi++) {
+            for (int ti = 0; ti < (int)teth.size(); ti++) {
+                const Tether& T = teth[ti];
+                if (!T.active || T.h1 < 0 || T.h2 < 0) continue;
+                if (T.h1 == pairs[pi].x && T.h2 == pairs[pi].y) ptlist.push_back(2 * ti);
+                else if (T.h2 == pairs[pi].x && T.h1 == pairs[pi].y) ptlist.push_back(2 * ti + 1);
+            }
+            ptstart[pi + 1] = (int)ptlist.size();
+        }
         // block x point index for the Schur pairs: the edge of the camera of block h on point i,
         // -2 - (first list position) when that camera observes i more than once, -1 if never
         std::vector<int> blkidx(std::max((size_t)nb * P, (size_t)1), -1);
@@ -1292,6 +1439,13 @@ struct BundleAdjuster {
         if ((r = upload(d_cpt, cpt)) != MAGE_OK) return r;
         if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
         if ((r = upload(d_pairs, pairs)) != MAGE_OK) return r;
+        if ((r = upload(d_ptstart, ptstart)) != MAGE_OK) return r;
+        if ((r = upload(d_ptlist, ptlist)) != MAGE_OK) return r;
+        for (auto& T : teth) {
+            T.h1 = camh[T.c1];
+            T.h2 = camh[T.c2];
+        }
+        if ((r = upload(d_teth, teth)) != MAGE_OK) return r;
         if (!state_on_device) {
             if ((r = upload(d_q[0], q)) != MAGE_OK) return r;
             if ((r = upload(d_t[0], t)) != MAGE_OK) return r;
@@ -1311,7 +1465,8 @@ struct BundleAdjuster {
                         std::make_pair(&d_Z, Em * 18 * 8),
                         std::make_pair(&d_campart, Cm * CAM_CHUNKS * 27 * 8),
                         std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
-                        std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, Pm * 8),
+                        std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, (Pm + teth.size()) * 8),
+                        std::make_pair(&d_tout, std::max<size_t>(teth.size(), 1) * TETHER_OUT * 8),
                         std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
                         std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 4 * 8),
                         std::make_pair(&d_olist, Em * 2 * 4 + 16), std::make_pair(&d_camcnt, Cm * 4)})
@@ -1344,9 +1499,14 @@ struct BundleAdjuster {
             launch("ba.cam_linearize", cam_linearize, dim3(nb_free * CAM_CHUNKS), dim3(BA_THREADS), 0, st, pb, state(cur),
                    (const int*)d_camblk.as<int>(), (const double*)d_err.as<double>(), d_campart.as<double>());
         }
+        const int nt = (int)teth.size();
+        if (nt > 0)
+            launch("ba.tether_eval", tether_eval, dim3((nt + 63) / 64), dim3(64), 0, st, (const Tether*)d_teth.as<Tether>(),
+                   nt, state(cur), 1, d_chi.as<double>() + P, d_tout.as<double>());
         launch("ba.reduce", linearize_finish, dim3(1), dim3(1024), 0, st, nb_free, (const int*)d_camblk.as<int>(),
                (const double*)d_campart.as<double>(), (const double*)d_chi.as<double>(), P,
-               (const double*)d_maxd.as<double>(), d_Hpp.as<double>(), d_bp.as<double>(), d_red.as<double>());
+               (const double*)d_maxd.as<double>(), (const Tether*)d_teth.as<Tether>(), nt,
+               (const double*)d_tout.as<double>(), d_Hpp.as<double>(), d_bp.as<double>(), d_red.as<double>());
         MAGE_HIP(hipGetLastError());
         return MAGE_OK;
     }
@@ -1371,8 +1531,9 @@ struct BundleAdjuster {
             {
                 launch("ba.schur_pairs", schur_pairs, dim3(8 * ((npairs + 7) / 8)), dim3(BA_THREADS), 0, st, pb, d_pairs.as<int2>(),
                                    d_camblk.as<int>(), d_blkidx.as<int>(), d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(),
-                                   d_Z.as<double>(), d_bl.as<double>(), lam, np, npairs, d_S.as<double>(),
-                                   d_rhs.as<double>());
+                                   d_Z.as<double>(), d_bl.as<double>(), lam, np, npairs,
+                                   (const int*)d_ptstart.as<int>(), (const int*)d_ptlist.as<int>(),
+                                   (const double*)d_tout.as<double>(), d_S.as<double>(), d_rhs.as<double>());
             }
             {
                 if (np <= 16 * CT_MAXT)
@@ -1397,10 +1558,12 @@ struct BundleAdjuster {
                                d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
                                d_chi.as<double>(), d_maxd.as<double>());
         }
-        {
-            launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P, d_scale.as<double>(),
-                               P + C, d_maxd.as<double>(), 0, d_red.as<double>() + 3);
-        }
+        const int nt = (int)teth.size();
+        if (nt > 0)
+            launch("ba.tether_eval", tether_eval, dim3((nt + 63) / 64), dim3(64), 0, st, (const Tether*)d_teth.as<Tether>(),
+                   nt, state(1 - cur), 0, d_chi.as<double>() + P, d_tout.as<double>());
+        launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P + nt, d_scale.as<double>(),
+               P + C, d_maxd.as<double>(), 0, d_red.as<double>() + 3);
         if (speculate && E > 0) launch_outlier_pass(state(1 - cur), state(cur), 2);  // read back with this sync
         MAGE_HIP(hipGetLastError());
         mage_status r = read_ctl();
@@ -1555,7 +1718,7 @@ struct BundleAdjuster {
                 if (k < cap) outliers[k] = list[k];
             }
             for (int c = 0; c < C; c++)
-                if (camh[c] >= 0 && camcnt[c] == 0) dirty = true;
+                if (camh[c] >= 0 && camcnt[c] == 0 && cam_tethers[c] == 0) dirty = true;
             iteration = 0;  // removeEdge dirties the optimizer: next Step re-initialises (lambda init)
         }
         *nOut = std::min(no, cap);
@@ -1721,13 +1884,53 @@ mage_status mage_ba_get_lambda(mage_ba* b, float* lambda)
     return MAGE_OK;
 }
 
-mage_status mage_ba_set_tethers(mage_ba* b, uint32_t, uint32_t n, const uint32_t*, const uint32_t*, const float*,
-                                const float*)
+mage_status mage_ba_set_tethers(mage_ba* b, uint32_t kind, uint32_t n, const uint32_t* cam1, const uint32_t* cam2,
+                                const float* params, const float* weight)
 {
     MAGE_REQUIRE(b, MAGE_EINVAL, "null handle");
-    if (n == 0) return MAGE_OK;
-    mage::set_error("tether constraints are not implemented in this build");
-    return MAGE_EUNSUPPORTED;
+    MAGE_REQUIRE(kind <= MAGE_TETHER_TRANSFORM, MAGE_EINVAL, "unknown tether kind");
+    MAGE_REQUIRE(n == 0 || (cam1 && cam2 && params && weight), MAGE_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; i++) {
+        MAGE_REQUIRE((int)cam1[i] < b->C && (int)cam2[i] < b->C, MAGE_EINVAL, "tether camera index out of range");
+        MAGE_REQUIRE(cam1[i] != cam2[i], MAGE_EINVAL, "tether joins a camera to itself");
+    }
+    // Allocate*Constraints + Set*Constraint for one kind; the other kinds are kept, and the edge
+    // order is distance, rotation, transform as BuildDataForG2O adds them (BundleAdjust.cpp:155-189)
+    std::vector<mage::ba::Tether> nt;
+    const int stride = kind == MAGE_TETHER_DISTANCE ? 1 : kind == MAGE_TETHER_ROTATION ? 4 : 7;
+    for (uint32_t k = 0; k <= MAGE_TETHER_TRANSFORM; k++) {
+        if (k != kind) {
+            for (const auto& T : b->teth)
+                if ((uint32_t)T.kind == k) nt.push_back(T);
+            continue;
+        }
+        for (uint32_t i = 0; i < n; i++) {
+            mage::ba::Tether T{};
+            const float* pr = params + (size_t)stride * i;
+            T.kind = (int)kind;
+            T.c1 = (int)cam1[i];
+            T.c2 = (int)cam2[i];
+            T.h1 = T.h2 = -1;
+            T.w = (double)weight[i];
+            if (kind == MAGE_TETHER_DISTANCE) {
+                T.dist = (double)pr[0];
+            } else if (kind == MAGE_TETHER_ROTATION) {
+                for (int a = 0; a < 4; a++) T.mq[a] = (double)pr[a];  // setMeasurement, not normalised
+            } else {
+                for (int a = 0; a < 3; a++) T.mt[a] = (double)pr[a];
+                double q[4];
+                for (int a = 0; a < 4; a++) q[a] = (double)pr[3 + a];
+                if (q[3] < 0)  // SE3Quat(q, t): normalizeRotation
+                    for (int a = 0; a < 4; a++) q[a] = -q[a];
+                const double nq = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+                for (int a = 0; a < 4; a++) T.mq[a] = q[a] / nq;
+            }
+            nt.push_back(T);
+        }
+    }
+    b->teth.swap(nt);
+    b->dirty = true;  // addEdge dirties the StepOptimizer
+    return MAGE_OK;
 }
 
 mage_status mage_ba_step(mage_ba* b, const float* huber, uint32_t nsteps, float max_error_square, uint32_t* outliers,

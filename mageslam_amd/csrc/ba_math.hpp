@@ -129,6 +129,143 @@ __device__ __forceinline__ void d_huber(double delta, double e2, double& rho0, d
     }
 }
 
+// ---------------- tether edges (BundlerLib.cpp:22-88, 311-350; g2o EdgeSE3Expmap) ----------------
+
+struct Tether {
+    int kind;    // 0 EdgeScaleConstraint (distance), 1 EdgeRotationConstraint, 2 EdgeSE3Expmap
+    int c1, c2;  // cameras (vertex 0, vertex 1)
+    int h1, h2;  // their Hessian blocks, -1 if not in the system
+    int active;  // not both cameras fixed
+    double w;    // weight (kinds 0, 1: inside the error) / information scale (kind 2)
+    double dist; // kind 0 measurement
+    double mq[4], mt[3];  // kind 1: rotation (x, y, z, w, as given); kind 2: SE3Quat(q, t)
+};
+
+// per-tether linearisation record: H11, H22, H12 (6x6 row-major), b1, b2
+constexpr int TETHER_OUT = 3 * 36 + 12;
+
+__device__ __forceinline__ void d_qmul(const double a[4], const double b[4], double o[4])
+{
+    const double w = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    const double x = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    const double y = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    const double z = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+    o[0] = x;
+    o[1] = y;
+    o[2] = z;
+    o[3] = w;
+}
+
+// SE3Quat::inverse
+__device__ __forceinline__ void d_se3_inv(const double q[4], const double t[3], double oq[4], double ot[3])
+{
+    oq[0] = -q[0];
+    oq[1] = -q[1];
+    oq[2] = -q[2];
+    oq[3] = q[3];
+    const double mt[3] = {-t[0], -t[1], -t[2]};
+    d_qrot(oq, mt, ot);
+}
+
+// SE3Quat::operator* (normalizeRotation on the product)
+__device__ __forceinline__ void d_se3_mul(const double aq[4], const double at[3], const double bq[4],
+                                          const double bt[3], double oq[4], double ot[3])
+{
+    double rt[3];
+    d_qrot(aq, bt, rt);
+    for (int i = 0; i < 3; i++) ot[i] = at[i] + rt[i];
+    d_qmul(aq, bq, oq);
+    d_se3_normalize(oq);
+}
+
+__device__ __forceinline__ void d_skew(const double v[3], double m[9])
+{
+    m[0] = 0;
+    m[1] = -v[2];
+    m[2] = v[1];
+    m[3] = v[2];
+    m[4] = 0;
+    m[5] = -v[0];
+    m[6] = -v[1];
+    m[7] = v[0];
+    m[8] = 0;
+}
+
+// SE3Quat::log -> (omega, upsilon)
+__device__ void d_se3_log(const double q[4], const double t[3], double res[6])
+{
+    double R[9];
+    d_qmat(q, R);
+    const double d = 0.5 * (R[0] + R[4] + R[8] - 1);
+    const double dR[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
+    double omega[3], Om[9];
+    double k;
+    if (fabs(d) > 0.99999) {
+        for (int i = 0; i < 3; i++) omega[i] = 0.5 * dR[i];
+        k = 1.0 / 12.0;
+    } else {
+        const double theta = acos(d);
+        const double s = theta / (2 * sqrt(1 - d * d));
+        for (int i = 0; i < 3; i++) omega[i] = s * dR[i];
+        k = (1 - theta / (2 * tan(theta / 2))) / (theta * theta);
+    }
+    d_skew(omega, Om);
+    for (int r = 0; r < 3; r++) {
+        double row[3];
+        for (int c = 0; c < 3; c++) {
+            const double o2 = Om[r * 3] * Om[c] + Om[r * 3 + 1] * Om[3 + c] + Om[r * 3 + 2] * Om[6 + c];
+            row[c] = (r == c ? 1.0 : 0.0) - 0.5 * Om[r * 3 + c] + k * o2;
+        }
+        res[r] = omega[r];
+        res[3 + r] = row[0] * t[0] + row[1] * t[1] + row[2] * t[2];
+    }
+}
+
+// SE3Quat::adj (6x6 row-major), negated if neg
+__device__ void d_se3_adj(const double q[4], const double t[3], bool neg, double A[36])
+{
+    double R[9], St[9];
+    d_qmat(q, R);
+    d_skew(t, St);
+    const double sg = neg ? -1.0 : 1.0;
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            const double sr = St[r * 3] * R[c] + St[r * 3 + 1] * R[3 + c] + St[r * 3 + 2] * R[6 + c];
+            A[r * 6 + c] = sg * R[r * 3 + c];
+            A[r * 6 + 3 + c] = 0.0 * sg;
+            A[(3 + r) * 6 + c] = sg * sr;
+            A[(3 + r) * 6 + 3 + c] = sg * R[r * 3 + c];
+        }
+}
+
+// computeError of a tether for camera estimates (q1, t1), (q2, t2); returns the dimension
+__device__ int d_tether_error(const Tether& T, const double q1[4], const double t1[3], const double q2[4],
+                              const double t2[3], double e[6])
+{
+    if (T.kind == 0) {
+        const double dx = t2[0] - t1[0], dy = t2[1] - t1[1], dz = t2[2] - t1[2];
+        e[0] = (T.dist - sqrt(dx * dx + dy * dy + dz * dz)) * T.w;
+        return 1;
+    }
+    if (T.kind == 1) {
+        double iq[4], it[3], rq[4], rt[3];
+        d_se3_inv(q1, t1, iq, it);
+        d_se3_mul(iq, it, q2, t2, rq, rt);
+        const double mc[4] = {-T.mq[0], -T.mq[1], -T.mq[2], T.mq[3]};
+        double d[4];
+        d_qmul(rq, mc, d);
+        const double vn = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+        e[0] = 2.0 * atan2(vn, fabs(d[3])) * T.w;
+        return 1;
+    }
+    double iq[4], it[3], aq[4], at[3], rq[4], rt[3];
+    d_se3_inv(q2, t2, iq, it);
+    d_se3_mul(iq, it, T.mq, T.mt, aq, at);
+    d_se3_mul(aq, at, q1, t1, rq, rt);
+    d_se3_log(rq, rt, e);
+    return 6;
+}
+
 struct State {  // one copy of the optimisable state
     double* q;  // C x 4
     double* t;  // C x 3

@@ -157,3 +157,64 @@ def ba_graph(
         true_pos=true_pos,
         true_rot=true_rot,
     )
+
+
+def quat_from_rot(R: np.ndarray) -> np.ndarray:
+    """Unit quaternion (x, y, z, w) of a rotation matrix (w >= 0)."""
+    R = np.asarray(R, np.float64)
+    w = np.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2
+    x = np.sqrt(max(0.0, 1.0 + R[0, 0] - R[1, 1] - R[2, 2])) / 2
+    y = np.sqrt(max(0.0, 1.0 - R[0, 0] + R[1, 1] - R[2, 2])) / 2
+    z = np.sqrt(max(0.0, 1.0 - R[0, 0] - R[1, 1] + R[2, 2])) / 2
+    x = np.copysign(x, R[2, 1] - R[1, 2])
+    y = np.copysign(y, R[0, 2] - R[2, 0])
+    z = np.copysign(z, R[1, 0] - R[0, 1])
+    q = np.array([x, y, z, w])
+    return q / np.linalg.norm(q)
+
+
+@dataclass
+class Tethers:
+    """Camera-camera constraints in the BundlerLib setter shapes (BundlerLib.cpp:311-350):
+    distance (cam1, cam2, distance, weight), rotation (cam1, cam2, quaternion xyzw, weight),
+    transform (cam1, cam2, position xyz + quaternion xyzw, weight)."""
+    distance: tuple
+    rotation: tuple
+    transform: tuple
+
+
+def ba_tethers(g: BAGraph, seed: int = BA_SEED + 7, count: int = 4, weight: float = 50.0) -> Tethers:
+    """Tethers measured on the true poses of `g` (slightly perturbed), mirroring KeyframeBuilder's
+    distance / three-dof / extrinsic tethers (BundleAdjust.cpp:57-105, 155-189).  Pairs mix free
+    and fixed cameras; one pair of fixed cameras is included (an inactive edge)."""
+    rng = np.random.default_rng(seed)
+    C = len(g.pos)
+    nfix = int(g.fixed.sum())
+    free = np.arange(nfix, C)
+
+    def pairs(k):
+        a = rng.choice(free, k)
+        b = np.where(rng.random(k) < 0.3, rng.integers(0, max(nfix, 1), k), rng.choice(free, k))
+        b = np.where(b == a, (a + 1) % C, b)
+        return a.astype(np.uint32), b.astype(np.uint32)
+
+    R, t = g.true_rot, g.true_pos
+    # distance between the SE3Quat translations (EdgeScaleConstraint::computeError)
+    c1, c2 = pairs(count)
+    if nfix >= 2:
+        c1[-1], c2[-1] = 0, 1  # both fixed: not an active edge
+    d = np.linalg.norm(t[c2] - t[c1], axis=1) * (1 + rng.normal(0, 0.01, count))
+    dist = (c1, c2, d.astype(np.float32), np.full(count, weight, np.float32))
+    # relative rotation (T1^-1 T2).rotation()
+    c1, c2 = pairs(count)
+    q = np.stack([quat_from_rot(R[a].T @ R[b]) for a, b in zip(c1, c2)]).astype(np.float32)
+    rot = (c1, c2, q, np.full(count, weight / 5, np.float32))
+    # relative transform C with log(T2^-1 C T1) = 0 at the truth: C = T2 T1^-1
+    c1, c2 = pairs(count)
+    p7 = []
+    for a, b in zip(c1, c2):
+        Rc = R[b] @ R[a].T
+        tc = t[b] - Rc @ t[a]
+        p7.append(np.concatenate([tc + rng.normal(0, 0.002, 3), quat_from_rot(Rc)]))
+    tr = (c1, c2, np.asarray(p7, np.float32), np.full(count, weight, np.float32))
+    return Tethers(distance=dist, rotation=rot, transform=tr)

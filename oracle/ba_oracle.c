@@ -46,12 +46,26 @@ typedef struct {
     double hpl[18]; /* 6x3 row-major, J_pose^T W J_point */
 } edge_t;
 
+/* Camera-camera constraint edges (BundlerLib.cpp:22-88, 311-350): kind 0 = EdgeScaleConstraint
+ * (fixed distance), 1 = EdgeRotationConstraint, 2 = g2o EdgeSE3Expmap (relative transform). */
+typedef struct {
+    int kind, c1, c2;
+    double w;       /* SetWeight (kinds 0, 1) or the information scale (kind 2) */
+    double dist;    /* kind 0 measurement */
+    se3q meas;      /* kind 1: meas.q; kind 2: SE3Quat(q, t) */
+    int active;
+    int dim;        /* error dimension: 1 or 6 */
+    double err[6];
+    double J[2][36]; /* dim x 6 row-major, per vertex */
+} tether_t;
+
 typedef struct oracle_ba {
     int points_fixed;
-    int nc, np, ne;
+    int nc, np, ne, nt;
     cam_t* cams;
     pt_t* pts;
     edge_t* edges;
+    tether_t* teth; /* distance, rotation, transform tethers in insertion (addEdge) order */
     double huber;
     /* optimizer state (StepOptimizer, BundlerLib.cpp:92-166) */
     int dirty, useless, iteration;
@@ -262,6 +276,224 @@ static void huber(double delta, double e2, double rho[3])
     }
 }
 
+/* ---------------- tether edges (BundlerLib.cpp:22-88; g2o EdgeSE3Expmap) ---------------- */
+
+/* SE3Quat::inverse: r' = conj(r), t' = r' * (-t) */
+static void se3_inverse(const se3q* s, se3q* o)
+{
+    o->q[0] = -s->q[0];
+    o->q[1] = -s->q[1];
+    o->q[2] = -s->q[2];
+    o->q[3] = s->q[3];
+    double mt[3] = {-s->t[0], -s->t[1], -s->t[2]};
+    quat_rotate(o->q, mt, o->t);
+}
+
+/* SE3Quat::operator*: t = a.t + a.r * b.t, r = a.r * b.r, normalizeRotation */
+static void se3_mul(const se3q* a, const se3q* b, se3q* o)
+{
+    se3q r;
+    double rt[3];
+    quat_rotate(a->q, b->t, rt);
+    for (int i = 0; i < 3; i++) r.t[i] = a->t[i] + rt[i];
+    quat_mul(a->q, b->q, r.q);
+    se3_normalize(&r);
+    *o = r;
+}
+
+static void skew3(const double v[3], double m[9])
+{
+    m[0] = 0;
+    m[1] = -v[2];
+    m[2] = v[1];
+    m[3] = v[2];
+    m[4] = 0;
+    m[5] = -v[0];
+    m[6] = -v[1];
+    m[7] = v[0];
+    m[8] = 0;
+}
+
+static void mat3_mul(const double a[9], const double b[9], double o[9])
+{
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) o[r * 3 + c] = a[r * 3] * b[c] + a[r * 3 + 1] * b[3 + c] + a[r * 3 + 2] * b[6 + c];
+}
+
+/* SE3Quat::log (g2o se3quat.h): (omega, upsilon) */
+static void se3_log(const se3q* s, double res[6])
+{
+    double R[9];
+    quat_to_matrix(s->q, R);
+    double d = 0.5 * (R[0] + R[4] + R[8] - 1);
+    double dR[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
+    double omega[3], Om[9], Om2[9], Vinv[9];
+    if (fabs(d) > 0.99999) {
+        for (int i = 0; i < 3; i++) omega[i] = 0.5 * dR[i];
+        skew3(omega, Om);
+        mat3_mul(Om, Om, Om2);
+        for (int i = 0; i < 9; i++) Vinv[i] = (i % 4 == 0 ? 1.0 : 0.0) - 0.5 * Om[i] + (1. / 12.) * Om2[i];
+    } else {
+        double theta = acos(d);
+        for (int i = 0; i < 3; i++) omega[i] = theta / (2 * sqrt(1 - d * d)) * dR[i];
+        skew3(omega, Om);
+        mat3_mul(Om, Om, Om2);
+        double k = (1 - theta / (2 * tan(theta / 2))) / (theta * theta);
+        for (int i = 0; i < 9; i++) Vinv[i] = (i % 4 == 0 ? 1.0 : 0.0) - 0.5 * Om[i] + k * Om2[i];
+    }
+    for (int i = 0; i < 3; i++) {
+        res[i] = omega[i];
+        res[3 + i] = Vinv[i * 3] * s->t[0] + Vinv[i * 3 + 1] * s->t[1] + Vinv[i * 3 + 2] * s->t[2];
+    }
+}
+
+/* SE3Quat::adj: [R 0; skew(t) R, R], 6x6 row-major */
+static void se3_adj(const se3q* s, double A[36])
+{
+    double R[9], St[9], SR[9];
+    quat_to_matrix(s->q, R);
+    skew3(s->t, St);
+    mat3_mul(St, R, SR);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            A[r * 6 + c] = R[r * 3 + c];
+            A[r * 6 + 3 + c] = 0;
+            A[(3 + r) * 6 + c] = SR[r * 3 + c];
+            A[(3 + r) * 6 + 3 + c] = R[r * 3 + c];
+        }
+}
+
+/* computeError of one tether at the current camera estimates */
+static void tether_error(const oracle_ba* b, const tether_t* t, double e[6])
+{
+    const se3q* T1 = &b->cams[t->c1].pose;
+    const se3q* T2 = &b->cams[t->c2].pose;
+    if (t->kind == 0) {
+        /* EdgeScaleConstraint: (measurement - |t2 - t1|) * weight, t = SE3Quat translation */
+        double dt[3] = {T2->t[0] - T1->t[0], T2->t[1] - T1->t[1], T2->t[2] - T1->t[2]};
+        e[0] = (t->dist - sqrt(dt[0] * dt[0] + dt[1] * dt[1] + dt[2] * dt[2])) * t->w;
+    } else if (t->kind == 1) {
+        /* EdgeRotationConstraint: (T1^-1 T2).rotation().angularDistance(measurement) * weight;
+         * Eigen 3.3 angularDistance: d = this * other.conjugate(), 2 atan2(|d.vec|, |d.w|) */
+        se3q i1, rel;
+        se3_inverse(T1, &i1);
+        se3_mul(&i1, T2, &rel);
+        double mc[4] = {-t->meas.q[0], -t->meas.q[1], -t->meas.q[2], t->meas.q[3]};
+        double d[4];
+        quat_mul(rel.q, mc, d);
+        double vn = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+        e[0] = 2.0 * atan2(vn, fabs(d[3])) * t->w;
+    } else {
+        /* EdgeSE3Expmap::computeError: (T2^-1 * C * T1).log() */
+        se3q i2, a, r;
+        se3_inverse(T2, &i2);
+        se3_mul(&i2, &t->meas, &a);
+        se3_mul(&a, T1, &r);
+        se3_log(&r, e);
+    }
+}
+
+/* linearizeOplus: BaseMultiEdge numeric differences (delta 1e-9, central) for kinds 0 / 1,
+ * EdgeSE3Expmap's analytic adjoints for kind 2.  Only vertices in the system get a Jacobian. */
+static void tether_jacobians(oracle_ba* b, tether_t* t)
+{
+    const int cams[2] = {t->c1, t->c2};
+    if (t->kind == 2) {
+        const se3q* Ti = &b->cams[t->c1].pose;
+        const se3q* Tj = &b->cams[t->c2].pose;
+        se3q invTij, invTj, invTi, invTj_Tij, invTi_invTij;
+        se3_inverse(&t->meas, &invTij);
+        se3_inverse(Tj, &invTj);
+        se3_inverse(Ti, &invTi);
+        se3_mul(&invTj, &t->meas, &invTj_Tij);
+        se3_mul(&invTi, &invTij, &invTi_invTij);
+        se3_adj(&invTj_Tij, t->J[0]);
+        se3_adj(&invTi_invTij, t->J[1]);
+        for (int k = 0; k < 36; k++) t->J[1][k] = -t->J[1][k];
+        return;
+    }
+    const double delta = 1e-9, scalar = 1 / (2 * delta);
+    for (int v = 0; v < 2; v++) {
+        cam_t* c = &b->cams[cams[v]];
+        if (c->hidx < 0) continue;
+        for (int dd = 0; dd < 6; dd++) {
+            double add[6] = {0, 0, 0, 0, 0, 0}, ep[6], em[6];
+            se3q keep = c->pose;
+            add[dd] = delta;
+            se3_oplus(&c->pose, add);
+            tether_error(b, t, ep);
+            c->pose = keep;
+            add[dd] = -delta;
+            se3_oplus(&c->pose, add);
+            tether_error(b, t, em);
+            c->pose = keep;
+            for (int r = 0; r < t->dim; r++) t->J[v][r * 6 + dd] = scalar * (ep[r] - em[r]);
+        }
+    }
+}
+
+/* information scale: Identity (kinds 0, 1; the weight is inside the error), weight * I6 (kind 2) */
+static double tether_omega(const tether_t* t) { return t->kind == 2 ? t->w : 1.0; }
+
+static double tether_chi2(const tether_t* t)
+{
+    double s = 0;
+    for (int r = 0; r < t->dim; r++) s += t->err[r] * t->err[r];
+    return tether_omega(t) * s;
+}
+
+/* H12 (6x6 row-major) = J1^T Omega J2 of an active tether with both cameras in the system */
+static void tether_h12(const tether_t* t, double H[36])
+{
+    const double om = tether_omega(t);
+    for (int r = 0; r < 6; r++)
+        for (int c = 0; c < 6; c++) {
+            double s = 0;
+            for (int m = 0; m < t->dim; m++) s += t->J[0][m * 6 + r] * t->J[1][m * 6 + c];
+            H[r * 6 + c] = s * om;
+        }
+}
+
+void oracle_ba_set_tethers(oracle_ba* b, int kind, int n, const uint32_t* cam1, const uint32_t* cam2,
+                           const float* params, const float* weight)
+{
+    /* keep the other kinds, replace this one; order distance, rotation, transform */
+    int keep = 0;
+    tether_t* nt = (tether_t*)calloc((size_t)(b->nt + n) + 1, sizeof(tether_t));
+    for (int k = 0; k <= 2; k++) {
+        if (k == kind) {
+            const int stride = kind == 0 ? 1 : kind == 1 ? 4 : 7;
+            for (int i = 0; i < n; i++) {
+                tether_t* t = &nt[keep++];
+                const float* pr = params + (size_t)stride * i;
+                t->kind = kind;
+                t->c1 = (int)cam1[i];
+                t->c2 = (int)cam2[i];
+                t->w = (double)weight[i];
+                t->dim = kind == 2 ? 6 : 1;
+                if (kind == 0) {
+                    t->dist = (double)pr[0];
+                } else if (kind == 1) {
+                    /* setMeasurement(Quaternionf.cast<double>()), not normalised */
+                    for (int a = 0; a < 4; a++) t->meas.q[a] = (double)pr[a];
+                } else {
+                    /* SE3Quat(q.cast<double>(), t.cast<double>()) normalises the rotation */
+                    for (int a = 0; a < 3; a++) t->meas.t[a] = (double)pr[a];
+                    for (int a = 0; a < 4; a++) t->meas.q[a] = (double)pr[3 + a];
+                    se3_normalize(&t->meas);
+                }
+            }
+        } else {
+            for (int i = 0; i < b->nt; i++)
+                if (b->teth[i].kind == k) nt[keep++] = b->teth[i];
+        }
+    }
+    free(b->teth);
+    b->teth = nt;
+    b->nt = keep;
+    b->dirty = 1;
+}
+
 /* ---------------- optimizer ---------------- */
 
 oracle_ba* oracle_ba_create(int points_fixed)
@@ -298,6 +530,7 @@ void oracle_ba_destroy(oracle_ba* b)
     free(b->cams);
     free(b->pts);
     free(b->edges);
+    free(b->teth);
     free(b);
 }
 
@@ -383,6 +616,16 @@ static void initialize(oracle_ba* b)
             ptHas[e->pt] = 1;
         }
     }
+    /* a tether is active unless both cameras are fixed (edges with all vertices fixed are not
+     * active); its cameras then belong to the system even without observations */
+    for (int i = 0; i < b->nt; i++) {
+        tether_t* t = &b->teth[i];
+        t->active = !(b->cams[t->c1].fixed && b->cams[t->c2].fixed);
+        if (t->active) {
+            camHas[t->c1] = 1;
+            camHas[t->c2] = 1;
+        }
+    }
     b->nfree_c = 0;
     for (int c = 0; c < b->nc; c++)
         b->cams[c].hidx = (!b->cams[c].fixed && camHas[c]) ? b->nfree_c++ : -1;
@@ -432,6 +675,13 @@ static double compute_errors(oracle_ba* b)
         double chi2 = e->info * (e->err[0] * e->err[0] + e->err[1] * e->err[1]);
         huber(b->huber, chi2, rho);
         chi += rho[0];
+    }
+    /* tethers follow the observations in addEdge (internal id) order; no robust kernel */
+    for (int i = 0; i < b->nt; i++) {
+        tether_t* t = &b->teth[i];
+        if (!t->active) continue;
+        tether_error(b, t, t->err);
+        chi += tether_chi2(t);
     }
     return chi;
 }
@@ -506,6 +756,31 @@ static void build_system(oracle_ba* b)
             }
         }
     }
+    /* tethers: BaseMultiEdge / BaseBinaryEdge::constructQuadraticForm without a robust kernel:
+     * H_vv += J_v^T Omega J_v, b_v += J_v^T (-Omega e); the H_12 block enters S in solve_system */
+    for (int i = 0; i < b->nt; i++) {
+        tether_t* t = &b->teth[i];
+        if (!t->active) continue;
+        tether_jacobians(b, t);
+        const double om = tether_omega(t);
+        const int cams[2] = {t->c1, t->c2};
+        for (int v = 0; v < 2; v++) {
+            if (b->cams[cams[v]].hidx < 0) continue;
+            double* H = &b->Hpp[36 * cams[v]];
+            double* g = &b->bp[6 * cams[v]];
+            const double* J = t->J[v];
+            for (int r = 0; r < 6; r++) {
+                double s = 0;
+                for (int m = 0; m < t->dim; m++) s += J[m * 6 + r] * (-om * t->err[m]);
+                g[r] += s;
+                for (int c = 0; c < 6; c++) {
+                    double h = 0;
+                    for (int m = 0; m < t->dim; m++) h += J[m * 6 + r] * J[m * 6 + c];
+                    H[r * 6 + c] += h * om;
+                }
+            }
+        }
+    }
 }
 
 /* computeLambdaInit: tau * max |H_ii| over vertices in the system (tau = 1e-5). */
@@ -556,6 +831,18 @@ static int solve_system(oracle_ba* b, double lambda)
             S[(6 * h + r) * n + 6 * h + r] += lambda;
             b->rhs[6 * h + r] = b->bp[6 * c + r];
         }
+    }
+    for (int i = 0; i < b->nt; i++) {
+        const tether_t* t = &b->teth[i];
+        const int h1 = b->cams[t->c1].hidx, h2 = b->cams[t->c2].hidx;
+        if (!t->active || h1 < 0 || h2 < 0) continue;
+        double H[36];
+        tether_h12(t, H);
+        for (int r = 0; r < 6; r++)
+            for (int c = 0; c < 6; c++) {
+                S[(6 * h1 + r) * n + 6 * h2 + c] += H[r * 6 + c];
+                S[(6 * h2 + c) * n + 6 * h1 + r] += H[r * 6 + c];
+            }
     }
     /* landmarks in Hessian order (descending index); Hpl columns per landmark by pose row */
     for (int p = b->np - 1; p >= 0; p--) {
@@ -824,4 +1111,19 @@ void oracle_ba_perturb_camera(oracle_ba* b, int c, const double u[6]) { se3_oplu
 void oracle_ba_perturb_point(oracle_ba* b, int p, const double u[3])
 {
     for (int k = 0; k < 3; k++) b->pts[p].p[k] += u[k];
+}
+
+/* Error and Jacobians of tether i at the current state (indices after set order), for tests.
+ * Returns the error dimension, or 0 if the tether is inactive / out of range. */
+int oracle_ba_tether_linearization(oracle_ba* b, int i, double err[6], double J1[36], double J2[36])
+{
+    if (b->dirty) initialize(b);
+    if (i < 0 || i >= b->nt || !b->teth[i].active) return 0;
+    tether_t* t = &b->teth[i];
+    tether_error(b, t, t->err);
+    tether_jacobians(b, t);
+    memcpy(err, t->err, sizeof(t->err));
+    memcpy(J1, t->J[0], sizeof(t->J[0]));
+    memcpy(J2, t->J[1], sizeof(t->J[1]));
+    return t->dim;
 }

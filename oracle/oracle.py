@@ -95,6 +95,9 @@ def _declare(L):
     L.oracle_ba_set_points.argtypes = [vp, i32, vp]
     L.oracle_ba_set_observations.argtypes = [vp, i32, vp, vp, vp, vp]
     L.oracle_ba_set_lambda.argtypes = [vp, f32]
+    L.oracle_ba_set_tethers.argtypes = [vp, i32, i32, vp, vp, vp, vp]
+    L.oracle_ba_tether_linearization.argtypes = [vp, i32, vp, vp, vp]
+    L.oracle_ba_tether_linearization.restype = i32
     L.oracle_ba_get_lambda.argtypes = [vp]
     L.oracle_ba_get_lambda.restype = f32
     L.oracle_ba_step.argtypes = [vp, vp, i32, f32, vp, u32, C.POINTER(u32), C.POINTER(f32)]
@@ -293,6 +296,23 @@ class BundlerOracle:
 
     def set_lambda(self, lam):
         lib().oracle_ba_set_lambda(self.h, lam)
+
+    def set_tethers(self, kind, cam1, cam2, params, weight):
+        """kind 0: params (n,) distances; 1: (n, 4) quaternions x,y,z,w; 2: (n, 7) = position
+        xyz + quaternion x,y,z,w (BundlerLib::Set*Constraint, BundlerLib.cpp:311-350)."""
+        cam1 = np.ascontiguousarray(cam1, np.uint32)
+        cam2 = np.ascontiguousarray(cam2, np.uint32)
+        params = np.ascontiguousarray(params, np.float32).reshape(-1)
+        weight = np.ascontiguousarray(weight, np.float32)
+        lib().oracle_ba_set_tethers(self.h, kind, len(cam1), _p(cam1), _p(cam2), _p(params), _p(weight))
+
+    def tether_linearization(self, i):
+        """(error, J1, J2) of tether i (all kinds in distance, rotation, transform order)."""
+        e = np.zeros(6)
+        j1 = np.zeros(36)
+        j2 = np.zeros(36)
+        d = lib().oracle_ba_tether_linearization(self.h, i, _p(e), _p(j1), _p(j2))
+        return e[:d], j1[: 6 * d].reshape(d, 6), j2[: 6 * d].reshape(d, 6)
 
     def get_lambda(self):
         return float(lib().oracle_ba_get_lambda(self.h))

@@ -45,6 +45,11 @@ int main(int argc, char** argv)
                 ba.SetObservation(3 * p + c, uv, c, p, 1.0f);
             }
         }
+        ba.AllocateFixedDistanceConstraints(1);  // cameras 1 and 2 are 0.2 apart
+        ba.SetFixedDistanceConstraint(0, 1, 2, 0.2f, 50.f);
+        const float qI[4] = {0, 0, 0, 1}, d12[3] = {-0.2f, 0.f, 0.f};
+        ba.AllocateRelativeTransformConstraints(1);
+        ba.SetRelativeTransformConstraint(0, 1, 2, d12, qI, 10.f);
         std::vector<mage::hot::DMatch> rmatches;
         const unsigned nr = mage::hot::RadiusMatch(kps, nullptr, nullptr, desc, kps, nullptr, desc, 2.0f, 30, 1, rmatches);
         std::vector<unsigned> outliers;

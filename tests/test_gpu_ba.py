@@ -27,13 +27,18 @@ def compare(gb, ob, tol=POSE_TOL):
     assert np.abs(pg - po).max() < 10 * tol
 
 
-def run_pair(g, steps, huber=1.8, max_err=7.25, scale=0.95, points_fixed=False, lam=None, nsteps=1):
+def run_pair(g, steps, huber=1.8, max_err=7.25, scale=0.95, points_fixed=False, lam=None, nsteps=1,
+             tethers=None):
     gb = bundler.BundlerLib(bundler.BundlerParameters(points_fixed))
     gb.set_graph(g)
     from oracle import oracle as O
 
     ob = O.BundlerOracle(points_fixed)
     ob.set_graph(g)
+    if tethers is not None:
+        gb.set_tethers(tethers)
+        for kind, tt in enumerate((tethers.distance, tethers.rotation, tethers.transform)):
+            ob.set_tethers(kind, *tt)
     if lam is not None:
         gb.SetCurrentLambda(lam)
         ob.set_lambda(lam)
@@ -105,3 +110,73 @@ def test_reference_facade_setters(gpu):
     assert ms == ms2 and outl == list(out2)
     pos, R = b.GetPose(3)
     assert np.allclose(R @ R.T, np.eye(3), atol=1e-5)
+
+
+def test_tethers(gpu):
+    # distance / rotation / transform tethers (BundlerLib.cpp:22-88, 311-350), incl. an inactive
+    # fixed-fixed pair and tethers to fixed cameras
+    g = synth.ba_graph(cameras=12, points=400, obs_per_point=8, fixed_cameras=3, seed=1)
+    gb, ob = run_pair(g, 5, tethers=synth.ba_tethers(g))
+    compare(gb, ob)
+    sg, so = gb.stats(), ob.stats()
+    assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
+    assert abs(sg["chi2"] - so["chi2"]) <= 1e-6 * abs(so["chi2"])
+
+
+def test_tethers_c3_and_pose_only(gpu):
+    g = synth.ba_graph()
+    gb, ob = run_pair(g, 4, tethers=synth.ba_tethers(g, count=8))
+    compare(gb, ob)
+    g = synth.ba_graph(cameras=6, points=500, obs_per_point=6, fixed_cameras=4, seed=3)
+    gb, ob = run_pair(g, 3, huber=0.9, max_err=4.5 ** 2, points_fixed=True, tethers=synth.ba_tethers(g, count=2))
+    compare(gb, ob)
+
+
+def test_tether_only_camera(gpu):
+    # a free camera without observations joins the system through its transform tether
+    g = tethered_extra_camera()
+    t = synth.Tethers(distance=_empty(1), rotation=_empty(4),
+                      transform=(np.array([len(g.pos) - 2], np.uint32), np.array([len(g.pos) - 1], np.uint32),
+                                 g.extra_tether[None, :], np.array([50.0], np.float32)))
+    gb, ob = run_pair(g, 4, tethers=t)
+    compare(gb, ob)
+
+
+def test_tether_argument_errors(gpu):
+    from mageslam_amd import _lib
+
+    g = synth.ba_graph(cameras=6, points=100, obs_per_point=4, fixed_cameras=2, seed=5)
+    b = bundler.BundlerLib()
+    b.set_graph(g)
+    b._upload()
+    L = _lib.load()
+    one = np.array([1], np.uint32)
+    p = np.ones(7, np.float32)
+    w = np.ones(1, np.float32)
+    assert L.mage_ba_set_tethers(b._h, 0, 1, _lib.ptr(one), _lib.ptr(one), _lib.ptr(p), _lib.ptr(w)) == _lib.MAGE_EINVAL
+    big = np.array([99], np.uint32)
+    assert L.mage_ba_set_tethers(b._h, 2, 1, _lib.ptr(one), _lib.ptr(big), _lib.ptr(p), _lib.ptr(w)) == _lib.MAGE_EINVAL
+    assert L.mage_ba_set_tethers(b._h, 3, 0, None, None, None, None) == _lib.MAGE_EINVAL
+
+
+def _empty(stride):
+    return (np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros((0, stride), np.float32), np.zeros(0, np.float32))
+
+
+def tethered_extra_camera():
+    """C = 10 graph plus one unobserved camera near the last one (see test_tether_only_camera)."""
+    g = synth.ba_graph(cameras=10, points=300, obs_per_point=6, fixed_cameras=3, seed=11)
+    R, t = g.true_rot[-1], g.true_pos[-1]
+    Rx = synth._rot(0.02) @ R
+    tx = t + np.array([0.1, 0.0, 0.0])
+    Rc = Rx @ R.T
+    tc = tx - Rc @ t
+    import dataclasses
+
+    g2 = dataclasses.replace(
+        g, pos=np.vstack([g.pos, (tx + 0.01).astype(np.float32)]),
+        rot=np.concatenate([g.rot, (synth._rot(0.025) @ R)[None].astype(np.float32)]),
+        intr=np.vstack([g.intr, g.intr[-1:]]), fixed=np.append(g.fixed, 0).astype(np.uint8),
+        true_rot=np.concatenate([g.true_rot, Rx[None]]), true_pos=np.vstack([g.true_pos, tx]))
+    g2.extra_tether = np.concatenate([tc, synth.quat_from_rot(Rc)]).astype(np.float32)
+    return g2

@@ -391,3 +391,106 @@ def test_undistort_points_inverts_distortion(oracle, dist):
     ideal = np.stack([norm[:, 0] * kd[0] + kd[2], norm[:, 1] * kd[1] + kd[3]], 1)
     assert np.abs(out - ideal).max() < 0.02  # 5 fixed-point iterations on mild distortion
     assert np.array_equal(oracle.undistort_points(distorted, kd, (), kd), distorted)  # no coefficients
+
+
+def _oracle_with_tethers(O, g, t):
+    b = O.BundlerOracle()
+    b.set_graph(g)
+    for kind, tt in enumerate((t.distance, t.rotation, t.transform)):
+        b.set_tethers(kind, *tt)
+    return b
+
+
+def test_ba_tether_jacobians_finite_difference(oracle):
+    """BaseMultiEdge numeric Jacobians (distance / rotation) agree with wider central differences;
+    EdgeSE3Expmap's adjoint Jacobians are exact at zero error (BundlerLib.cpp:22-88)."""
+    from mageslam_amd import synth
+
+    g = synth.ba_graph(cameras=12, points=400, obs_per_point=8, fixed_cameras=3)
+    t = synth.ba_tethers(g)
+    # transform measurements consistent with the current estimates: zero error
+    R = g.rot.astype(np.float64)
+    tt = g.pos.astype(np.float64)
+    p7 = []
+    for a, b_ in zip(t.transform[0], t.transform[1]):
+        Rc = R[b_] @ R[a].T
+        p7.append(np.concatenate([tt[b_] - Rc @ tt[a], synth.quat_from_rot(Rc)]))
+    t.transform = (t.transform[0], t.transform[1], np.asarray(p7, np.float32), t.transform[3])
+    b = _oracle_with_tethers(oracle, g, t)
+    cams = [(int(c1), int(c2)) for tt_ in (t.distance, t.rotation, t.transform) for c1, c2 in zip(tt_[0], tt_[1])]
+    checked = 0
+    for i, pair in enumerate(cams):
+        e, J1, J2 = b.tether_linearization(i)
+        if len(e) == 0:
+            assert g.fixed[pair[0]] and g.fixed[pair[1]]
+            continue
+        for v, J in enumerate((J1, J2)):
+            c = pair[v]
+            if g.fixed[c]:
+                continue
+            Jfd = np.zeros_like(J)
+            h = 1e-6
+            for d in range(6):
+                u = np.zeros(6)
+                u[d] = h
+                b.perturb_camera(c, u)
+                ep, _, _ = b.tether_linearization(i)
+                u[d] = -2 * h
+                b.perturb_camera(c, u)
+                em, _, _ = b.tether_linearization(i)
+                u[d] = h
+                b.perturb_camera(c, u)
+                Jfd[:, d] = (ep - em) / (2 * h)
+            tol = 2e-5 * max(1.0, np.abs(J).max()) if len(e) == 1 else 1e-3
+            assert np.abs(J - Jfd).max() < tol, (i, v, np.abs(J - Jfd).max())
+            checked += 1
+    assert checked >= 12
+
+
+def test_ba_tethers_pull_cameras(oracle):
+    """A distance tether with a longer measurement pulls the two translations towards it (against
+    the photogrammetric evidence): closer to the measurement than the untethered solution."""
+    from mageslam_amd import synth
+
+    g = synth.ba_graph(cameras=12, points=400, obs_per_point=8, fixed_cameras=3, seed=4)
+    none = (np.zeros(0, np.uint32),) * 2
+    d0 = float(np.linalg.norm(g.pos[8].astype(np.float64) - g.pos[5]))
+    t = synth.Tethers(distance=(np.array([5], np.uint32), np.array([8], np.uint32),
+                                np.array([d0 * 1.05], np.float32), np.array([200.0], np.float32)),
+                      rotation=none + (np.zeros((0, 4), np.float32), np.zeros(0, np.float32)),
+                      transform=none + (np.zeros((0, 7), np.float32), np.zeros(0, np.float32)))
+    b = _oracle_with_tethers(oracle, g, t)
+    for _ in range(10):
+        b.step([1.8], 7.25)
+    qt, _ = b.state()
+    d1 = float(np.linalg.norm(qt[8, 4:] - qt[5, 4:]))
+    # without the tether the pair keeps its photogrammetric distance
+    b2 = oracle.BundlerOracle()
+    b2.set_graph(g)
+    for _ in range(10):
+        b2.step([1.8], 7.25)
+    qt2, _ = b2.state()
+    assert abs(float(np.linalg.norm(qt2[8, 4:] - qt2[5, 4:])) - d0 * 1.05) > abs(d1 - d0 * 1.05)
+
+
+def test_ba_tether_only_camera_joins_system(oracle):
+    """An unobserved free camera with a transform tether is optimised (it moves onto the tether)."""
+    from tests.test_gpu_ba import tethered_extra_camera
+    from mageslam_amd import synth
+
+    g = tethered_extra_camera()
+    C = len(g.pos)
+    none = (np.zeros(0, np.uint32),) * 2
+    t = synth.Tethers(distance=none + (np.zeros((0, 1), np.float32), np.zeros(0, np.float32)),
+                      rotation=none + (np.zeros((0, 4), np.float32), np.zeros(0, np.float32)),
+                      transform=(np.array([C - 2], np.uint32), np.array([C - 1], np.uint32),
+                                 g.extra_tether[None, :], np.array([50.0], np.float32)))
+    b = _oracle_with_tethers(oracle, g, t)
+    before = b.state()[0][C - 1].copy()
+    for _ in range(10):  # lambda starts large against the tether's Hessian: LM closes slowly
+        b.step([1.8], 7.25)
+    qt, _ = b.state()
+    assert np.abs(qt[C - 1] - before).max() > 1e-3
+    # the constraint holds: log(T2^-1 C T1) ~ 0
+    e, _, _ = b.tether_linearization(0)
+    assert np.abs(e).max() < 1e-4
