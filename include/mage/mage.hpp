@@ -122,6 +122,48 @@ inline unsigned RadiusMatch(const std::vector<KeyPoint>& queryKeypoints, const s
     return n;
 }
 
+// OnlineBow vocabulary tree on the device (OnlineBow.cpp:289-311 FindLeafNode; nodes as CreateTree
+// builds them: node i's descriptor, children in childrenIDs order, root 0).
+class OnlineBowTree {
+public:
+    OnlineBowTree(const std::vector<Descriptor>& nodes, const std::vector<uint32_t>& childStart,
+                  const std::vector<uint32_t>& children, int device = 0)
+    {
+        check(mage_bow_create(nodes.empty() ? nullptr : nodes.front().data(), childStart.data(),
+                              children.empty() ? nullptr : children.data(), (uint32_t)nodes.size(), device, &m_handle));
+    }
+    ~OnlineBowTree() { mage_bow_destroy(m_handle); }
+    OnlineBowTree(const OnlineBowTree&) = delete;
+    OnlineBowTree& operator=(const OnlineBowTree&) = delete;
+    ptrdiff_t FindLeafNode(const Descriptor& d) const
+    {
+        uint32_t leaf = 0;
+        check(mage_bow_find_leaves(m_handle, d.data(), 1, &leaf));
+        return (ptrdiff_t)leaf;
+    }
+    mage_bow* handle() const { return m_handle; }
+
+private:
+    mage_bow* m_handle = nullptr;
+};
+
+// IndexedMatch (FeatureMatcher.cpp:192-292) with the BoW candidate lists of `tree` (what
+// OnlineBowFeatureMatcher / OnlineBow::QueryFeatures return); masks as in Match.
+inline unsigned IndexedMatch(const OnlineBowTree& tree, const std::vector<Descriptor>& a, const std::vector<Descriptor>& b,
+                             const std::vector<bool>& maskA, const std::vector<bool>& maskB, int maxHammingDist,
+                             int minHammingDifference, std::vector<DMatch>& goodMatches)
+{
+    std::vector<uint8_t> ma(maskA.begin(), maskA.end()), mb(maskB.begin(), maskB.end());
+    goodMatches.resize(a.size());
+    uint32_t n = 0;
+    check(mage_indexed_match(tree.handle(), a.empty() ? nullptr : a.front().data(), (uint32_t)a.size(),
+                             ma.empty() ? nullptr : ma.data(), b.empty() ? nullptr : b.front().data(), (uint32_t)b.size(),
+                             mb.empty() ? nullptr : mb.data(), maxHammingDist, minHammingDifference, goodMatches.data(),
+                             (uint32_t)goodMatches.size(), &n));
+    goodMatches.resize(n);
+    return n;
+}
+
 struct BundlerParameters {
     bool ArePointsFixed{false};
 };

@@ -204,6 +204,49 @@ mage_status mage_radius_match_batch_device(const mage_keypoint* d_query_kp, cons
                                            uint32_t* d_n, uint32_t* d_status, mage_stream stream);
 
 /* ------------------------------------------------------------------------------------------ */
+/* Vocabulary tree + IndexedMatch — replaces OnlineBow::FindLeafNode / QueryFeatures and          */
+/* IndexedMatch (Core/.../Source/BoW/OnlineBow.cpp, Tracking/FeatureMatcher.cpp:192-292)          */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct mage_bow mage_bow;
+
+/* The OnlineBow tree as CreateTree / Kmean build it (OnlineBow.cpp:325-411): node i has the
+ * 32-byte descriptor node_desc + 32 i and children children[child_start[i] .. child_start[i+1])
+ * in childrenIDs order; node 0 is the root.  Children must have larger ids than their parent
+ * (Kmean appends them after it) — MAGE_EINVAL otherwise. */
+mage_status mage_bow_create(const uint8_t* node_desc, const uint32_t* child_start, const uint32_t* children,
+                            uint32_t n_nodes, int device, mage_bow** out);
+mage_status mage_bow_destroy(mage_bow* bow);
+
+/* FindLeafNode (OnlineBow.cpp:289-311) of n descriptors: leaf[i] = node id.  Host buffers,
+ * synchronous; _device: device buffers, asynchronous on `stream`. */
+mage_status mage_bow_find_leaves(mage_bow* bow, const uint8_t* desc, uint32_t n, uint32_t* leaf);
+mage_status mage_bow_find_leaves_device(mage_bow* bow, const uint8_t* d_desc, uint32_t n, uint32_t* d_leaf,
+                                        mage_stream stream);
+
+/* IndexedMatch (FeatureMatcher.cpp:192-292) with the BoW candidate lists (OnlineBowFeatureMatcher::
+ * QueryFeatures / OnlineBow::QueryFeatures: the other image's features in the query's leaf, in
+ * index order): forward TrackMatch best / second best, accepted when best < max_distance + 1 and
+ * (second >= max_distance + 1 or second - best >= min_difference); kept when the reverse match
+ * of B[j] over A's features of the same leaf returns A[i] with the same test.  Masks may be NULL
+ * (all true).  At most 4096 features per side.  Host buffers, synchronous; output in A order,
+ * DMatch(queryIdx = A index, trainIdx = B index, imgIdx = -1, distance). */
+mage_status mage_indexed_match(mage_bow* bow, const uint8_t* desc_a, uint32_t n_a, const uint8_t* mask_a,
+                               const uint8_t* desc_b, uint32_t n_b, const uint8_t* mask_b, int32_t max_distance,
+                               int32_t min_difference, mage_dmatch* out, uint32_t cap, uint32_t* n);
+
+/* Batched device form, one (A, B) pair per workgroup, leaves precomputed (e.g. by
+ * mage_bow_find_leaves_device): pair p reads a_pitch / b_pitch entries further on (descriptors,
+ * leaves, optional masks), counts d_n_a[p] / d_n_b[p].  Results at d_out + p*cap, count in d_n[p];
+ * bit 0 of *d_status is set when a side exceeds 4096 (that pair reports 0).  Asynchronous. */
+mage_status mage_indexed_match_batch_device(const uint8_t* d_desc_a, const uint32_t* d_leaf_a, const uint8_t* d_mask_a,
+                                            int64_t a_pitch, const uint32_t* d_n_a, const uint8_t* d_desc_b,
+                                            const uint32_t* d_leaf_b, const uint8_t* d_mask_b, int64_t b_pitch,
+                                            const uint32_t* d_n_b, uint32_t pairs, int32_t max_distance,
+                                            int32_t min_difference, mage_dmatch* d_out, uint32_t cap, uint32_t* d_n,
+                                            uint32_t* d_status, mage_stream stream);
+
+/* ------------------------------------------------------------------------------------------ */
 /* Local bundle adjustment — replaces BundlerLib (Dependencies/BundlerLib/Include/BundlerLib.h) */
 /* ------------------------------------------------------------------------------------------ */
 

@@ -1,0 +1,92 @@
+"""Vocabulary tree + IndexedMatch — host mirror of OnlineBow's feature lookup and IndexedMatch.
+
+`OnlineBowTree` holds the tree OnlineBow::CreateTree builds (Core/MAGESLAM/Source/BoW/OnlineBow.cpp:
+325-411) on the GPU; `FindLeafNode` mirrors OnlineBow::FindLeafNode (:289-311).  `IndexedMatch`
+mirrors `IndexedMatch(bagOfWords, matcherA, matcherB, idA, idB, imageA, imageB, maskA, maskB, countA,
+countB, maxHammingDist, minHammingDifference, memory, goodMatches)` (Tracking/FeatureMatcher.h:30-62,
+FeatureMatcher.cpp:192-292) for the BoW candidate source every caller uses — OnlineBowFeatureMatcher
+or OnlineBow::QueryFeatures, both "the other image's features in the query's leaf" — with the
+descriptors passed directly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import DM_DTYPE, check, ptr
+
+
+class OnlineBowTree:
+    def __init__(self, node_desc, child_start, children, device: int = 0):
+        self._nd = np.ascontiguousarray(node_desc, np.uint8).reshape(-1, 32)
+        self._cs = np.ascontiguousarray(child_start, np.uint32)
+        self._ch = np.ascontiguousarray(children, np.uint32)
+        if len(self._cs) != len(self._nd) + 1:
+            raise ValueError("child_start needs n_nodes + 1 entries")
+        self._h = C.c_void_p()
+        check(_lib.load().mage_bow_create(ptr(self._nd), ptr(self._cs), ptr(self._ch), len(self._nd), device,
+                                          C.byref(self._h)))
+
+    @classmethod
+    def from_tuple(cls, tree, device: int = 0) -> "OnlineBowTree":
+        return cls(*tree, device=device)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.load().mage_bow_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def find_leaves(self, descriptors) -> np.ndarray:
+        d = np.ascontiguousarray(descriptors, np.uint8).reshape(-1, 32)
+        out = np.zeros(len(d), np.uint32)
+        check(_lib.load().mage_bow_find_leaves(self._h, ptr(d), len(d), ptr(out)))
+        return out
+
+    def FindLeafNode(self, descriptor) -> int:
+        return int(self.find_leaves(descriptor)[0])
+
+    def find_leaves_device(self, desc, n: int, leaf, stream=None) -> None:
+        """Device form over n descriptors (torch device tensors)."""
+        check(_lib.load().mage_bow_find_leaves_device(self._h, ptr(desc), n, ptr(leaf),
+                                                      C.c_void_p(stream) if stream else None))
+
+
+def IndexedMatch(tree: OnlineBowTree, descA, descB, maskA=None, maskB=None, maxHammingDist: int = 30,
+                 minHammingDifference: int = 1) -> np.ndarray:
+    """Two-way BoW-indexed match on the GPU; DMatch records (imgIdx -1) in ascending A index."""
+    da = np.ascontiguousarray(descA, np.uint8).reshape(-1, 32)
+    db = np.ascontiguousarray(descB, np.uint8).reshape(-1, 32)
+    ma = None if maskA is None else np.ascontiguousarray(np.asarray(maskA, bool), np.uint8)
+    mb = None if maskB is None else np.ascontiguousarray(np.asarray(maskB, bool), np.uint8)
+    if ma is not None and len(ma) != len(da):
+        raise ValueError("maskA length must equal the number of A descriptors")
+    if mb is not None and len(mb) != len(db):
+        raise ValueError("maskB length must equal the number of B descriptors")
+    cap = max(len(da), 1)
+    out = np.zeros(cap, DM_DTYPE)
+    n = C.c_uint32(0)
+    check(_lib.load().mage_indexed_match(tree.handle, ptr(da), len(da), ptr(ma), ptr(db), len(db), ptr(mb),
+                                         int(maxHammingDist), int(minHammingDifference), ptr(out), cap, C.byref(n)))
+    return out[: n.value].copy()
+
+
+def indexed_match_batch_device(desc_a, leaf_a, mask_a, a_pitch: int, n_a, desc_b, leaf_b, mask_b, b_pitch: int, n_b,
+                               pairs: int, max_distance: int, min_difference: int, out, capacity: int, n_out, status,
+                               stream=None) -> None:
+    """Batched device IndexedMatch over `pairs` (A_p, B_p) sets (torch device tensors; masks may be None)."""
+    check(_lib.load().mage_indexed_match_batch_device(
+        ptr(desc_a), ptr(leaf_a), ptr(mask_a), a_pitch, ptr(n_a), ptr(desc_b), ptr(leaf_b), ptr(mask_b), b_pitch,
+        ptr(n_b), pairs, max_distance, min_difference, ptr(out), capacity, ptr(n_out), ptr(status),
+        C.c_void_p(stream) if stream else None))

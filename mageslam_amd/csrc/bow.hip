@@ -1,0 +1,451 @@
+// bow.hip — OnlineBow vocabulary-tree descent and IndexedMatch on MI355X (gfx950).
+//
+// Replaces OnlineBow::FindLeafNode (Core/MAGESLAM/Source/BoW/OnlineBow.cpp:289-311), the leaf ->
+// feature lists of OnlineBowFeatureMatcher / OnlineBow::QueryFeatures (OnlineBowFeatureMatcher.cpp:
+// 8-31, OnlineBow.cpp:115-133) and IndexedMatch (Tracking/FeatureMatcher.cpp:192-292).
+//
+//   bow_leaves_kernel     thread per descriptor: descend from the root, first child with the
+//                         strictly smallest Hamming distance per level (the tree is tiny and
+//                         stays in L2 / the scalar cache: 6^2 leaves by default, MageSettings.h:230)
+//   indexed_match_kernel  one 1024-thread workgroup per (A, B) feature-set pair:
+//     1. masked features of each side -> 64-bit keys (leaf, index) sorted ascending in LDS (the
+//        shared hybrid bitonic sort): a leaf's candidates are one contiguous run in ascending
+//        index order — exactly QueryFeatures' lists, which hold every feature of that leaf in
+//        insertion order (the masks only filter inside TrackMatch);
+//     2. a 16-lane group per A feature: lanes stride over B's run of its leaf.  TrackMatch
+//        (:28-54) visited in ascending order is order-free: best = min (d, index) over d <
+//        maxHamming, second = the second smallest such d (the strict-< updates keep ties as
+//        second); merged with four shuffle steps.  The reverse check of an accepted pair (i, j)
+//        (:255-276) needs only B_j and A's run of the same leaf (leaf(B_j) = leaf(A_i) since j came
+//        from that run), so the same group runs it immediately — no barrier between the passes;
+//     3. ordered compaction in A order (the reference appends in forward-match order).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+#include "lds_sort.hpp"
+
+struct mage_bow {
+    int device = 0;
+    uint32_t n_nodes = 0;
+    mage::DeviceBuffer nodes, child_start, children;
+    mage::DeviceBuffer scratch;
+    hipStream_t st = nullptr;
+};
+
+namespace mage {
+namespace {
+
+constexpr int IM_MAX = 4096;  // features per side held in LDS (NumFeatures-sized sets)
+constexpr int IM_GROUP = 16;  // lanes per A feature
+constexpr int IM_GROUPS = SORT_THREADS / IM_GROUP;
+
+struct IndexedParams {
+    const uint8_t* da;
+    const uint32_t* la;
+    const uint8_t* ma;  // optional
+    const uint32_t* na;
+    long long a_pitch;
+    const uint8_t* db;
+    const uint32_t* lb;
+    const uint8_t* mb;  // optional
+    const uint32_t* nb;
+    long long b_pitch;
+    int max_dist, min_diff;
+    unsigned cap;
+    mage_dmatch* out;
+    uint32_t* n_out;
+    uint32_t* status;  // bit 0: a feature set exceeded IM_MAX
+};
+
+__device__ __forceinline__ unsigned hamming32(const uint4& qa, const uint4& qb, const uint8_t* t)
+{
+    const uint4 ta = *reinterpret_cast<const uint4*>(t);
+    const uint4 tb = *reinterpret_cast<const uint4*>(t + 16);
+    return __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w) +
+           __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
+}
+
+__global__ __launch_bounds__(256) void bow_leaves_kernel(const uint8_t* __restrict__ nodes,
+                                                         const uint32_t* __restrict__ child_start,
+                                                         const uint32_t* __restrict__ children,
+                                                         const uint8_t* __restrict__ desc, uint32_t n,
+                                                         uint32_t* __restrict__ leaf)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint4 qa = *reinterpret_cast<const uint4*>(desc + 32ull * i);
+    const uint4 qb = *reinterpret_cast<const uint4*>(desc + 32ull * i + 16);
+    uint32_t cur = 0;
+    for (;;) {
+        const uint32_t c0 = child_start[cur], c1 = child_start[cur + 1];
+        if (c0 == c1) break;
+        unsigned best = UINT_MAX;
+        uint32_t next = cur;
+        for (uint32_t k = c0; k < c1; k++) {
+            const uint32_t c = children[k];
+            const unsigned d = hamming32(qa, qb, nodes + 32ull * c);
+            if (d < best) {
+                best = d;
+                next = c;
+            }
+        }
+        cur = next;  // children have larger ids than their parent (checked at creation): terminates
+    }
+    leaf[i] = cur;
+}
+
+// first position in keys[0, n) (ascending) with keys[pos] >= k
+__device__ __forceinline__ int lower_bound_u64(const unsigned long long* keys, int n, unsigned long long k)
+{
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// TrackMatch over a run keys[lo, hi) of one leaf (indices in the low 32 bits) against query
+// (qa, qb): returns best (d << 12 | index) and the second smallest d, both capped at max_h.
+__device__ __forceinline__ void track_run(const unsigned long long* keys, int lo, int hi, int sub,
+                                          const uint8_t* __restrict__ desc, const uint4& qa, const uint4& qb,
+                                          unsigned max_h, unsigned& bestk, unsigned& second)
+{
+    unsigned m1 = max_h << 12 | 0xFFFu, m2 = max_h;
+    for (int k = lo + sub; k < hi; k += IM_GROUP) {
+        const unsigned idx = (unsigned)(keys[k] & 0xFFFFFFFFull);
+        const unsigned d = hamming32(qa, qb, desc + 32ull * idx);
+        if (d >= max_h) continue;
+        const unsigned key = d << 12 | idx;
+        if (key < m1) {
+            m2 = min(m2, m1 >> 12);
+            m1 = key;
+        } else {
+            m2 = min(m2, d);
+        }
+    }
+#pragma unroll
+    for (int off = IM_GROUP / 2; off > 0; off >>= 1) {
+        const unsigned o1 = (unsigned)__shfl_xor((int)m1, off), o2 = (unsigned)__shfl_xor((int)m2, off);
+        // two smallest of the union of {m1 <= m2} and {o1 <= o2}
+        m2 = min(max(m1 >> 12, o1 >> 12), min(m2, o2));
+        m1 = min(m1, o1);
+    }
+    bestk = m1;
+    second = m2;
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void indexed_match_kernel(IndexedParams p)
+{
+    __shared__ unsigned long long keysA[IM_MAX], keysB[IM_MAX];
+    __shared__ int res[IM_MAX];
+    __shared__ int wsum[SORT_THREADS / kWave];
+    __shared__ int s_cnt[2], s_base;
+    const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int na = (int)p.na[pr], nb = (int)p.nb[pr];
+    const uint8_t* da = p.da + pr * p.a_pitch * 32;
+    const uint8_t* db = p.db + pr * p.b_pitch * 32;
+    const uint32_t* la = p.la + pr * p.a_pitch;
+    const uint32_t* lb = p.lb + pr * p.b_pitch;
+    const uint8_t* ma = p.ma ? p.ma + pr * p.a_pitch : nullptr;
+    const uint8_t* mb = p.mb ? p.mb + pr * p.b_pitch : nullptr;
+    if (na > IM_MAX || nb > IM_MAX) {
+        if (tid == 0) {
+            p.n_out[pr] = 0;
+            atomicOr(p.status, 1u);
+        }
+        return;
+    }
+    // 1. masked (leaf, index) keys of both sides, ascending (descending sort of complements)
+    if (tid < 2) s_cnt[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < na; i += SORT_THREADS)
+        if (!ma || ma[i]) keysA[atomicAdd(&s_cnt[0], 1)] = ~((unsigned long long)la[i] << 32 | (unsigned)i);
+    for (int i = tid; i < nb; i += SORT_THREADS)
+        if (!mb || mb[i]) keysB[atomicAdd(&s_cnt[1], 1)] = ~((unsigned long long)lb[i] << 32 | (unsigned)i);
+    __syncthreads();
+    const int ca = s_cnt[0], cb = s_cnt[1];
+    if (ca == 0 || cb == 0) {  // IndexedMatch returns 0 when either mask count is 0 (:209)
+        if (tid == 0) p.n_out[pr] = 0;
+        return;
+    }
+    int PA = 1, PB = 1;
+    while (PA < ca) PA <<= 1;
+    while (PB < cb) PB <<= 1;
+    for (int i = ca + tid; i < max(PA, SORT_THREADS); i += SORT_THREADS) keysA[i] = 0ull;
+    for (int i = cb + tid; i < max(PB, SORT_THREADS); i += SORT_THREADS) keysB[i] = 0ull;
+    __syncthreads();
+    sort_desc(keysA, PA);
+    sort_desc(keysB, PB);
+    for (int i = tid; i < ca; i += SORT_THREADS) keysA[i] = ~keysA[i];
+    for (int i = tid; i < cb; i += SORT_THREADS) keysB[i] = ~keysB[i];
+    __syncthreads();
+
+    // 2. forward TrackMatch over B's run of the leaf, then the reverse check over A's run
+    const unsigned max_h = (unsigned)(p.max_dist + 1);
+    const int group = tid / IM_GROUP, sub = tid % IM_GROUP;
+    for (int i = group; i < na; i += IM_GROUPS) {
+        int r = -1;
+        if (!ma || ma[i]) {
+            const unsigned long long leaf = la[i];
+            const uint4 qa = *reinterpret_cast<const uint4*>(da + 32ll * i);
+            const uint4 qb = *reinterpret_cast<const uint4*>(da + 32ll * i + 16);
+            const int lo = lower_bound_u64(keysB, cb, leaf << 32), hi = lower_bound_u64(keysB, cb, (leaf + 1) << 32);
+            unsigned bk, sd;
+            track_run(keysB, lo, hi, sub, db, qa, qb, max_h, bk, sd);
+            const unsigned bd = bk >> 12;
+            if (bd < max_h && (sd >= max_h || (int)(sd - bd) >= p.min_diff)) {
+                const int j = (int)(bk & 0xFFFu);
+                const uint4 ra = *reinterpret_cast<const uint4*>(db + 32ll * j);
+                const uint4 rb = *reinterpret_cast<const uint4*>(db + 32ll * j + 16);
+                const unsigned long long lj = lb[j];
+                const int lo2 = lower_bound_u64(keysA, ca, lj << 32), hi2 = lower_bound_u64(keysA, ca, (lj + 1) << 32);
+                unsigned bk2, sd2;
+                track_run(keysA, lo2, hi2, sub, da, ra, rb, max_h, bk2, sd2);
+                const unsigned bd2 = bk2 >> 12;
+                if (bd2 < max_h && (int)(bk2 & 0xFFFu) == i && (sd2 >= max_h || (int)(sd2 - bd2) >= p.min_diff))
+                    r = j << 9 | (int)bd2;
+            }
+        }
+        if (sub == 0) res[i] = r;
+    }
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+
+    // 3. ordered compaction in A order
+    for (int q0 = 0; q0 < na; q0 += SORT_THREADS) {
+        const int q = q0 + tid;
+        const int v = q < na ? res[q] : -1;
+        const bool keep = v >= 0;
+        const unsigned long long b = __ballot(keep);
+        const int before = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = __popcll(b);
+        __syncthreads();
+        int off = s_base;
+        for (int w = 0; w < wave; w++) off += wsum[w];
+        if (keep) {
+            const int pos = off + before;
+            if (pos < (int)p.cap) {
+                mage_dmatch m;
+                m.query_idx = q;
+                m.train_idx = v >> 9;
+                m.img_idx = -1;  // cv::DMatch(int, int, float) (FeatureMatcher.cpp:274)
+                m.distance = (float)(v & 0x1FF);
+                p.out[(long long)pr * p.cap + pos] = m;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int w = 0; w < SORT_THREADS / kWave; w++) tot += wsum[w];
+            s_base += tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) p.n_out[pr] = (uint32_t)s_base;
+}
+
+mage_status leaves_launch(const mage_bow* b, const uint8_t* d_desc, uint32_t n, uint32_t* d_leaf, hipStream_t st)
+{
+    if (n == 0) return MAGE_OK;
+    launch("bow.leaves", bow_leaves_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b->nodes.as<const uint8_t>(),
+           b->child_start.as<const uint32_t>(), b->children.as<const uint32_t>(), d_desc, n, d_leaf);
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}
+
+mage_status indexed_launch(const IndexedParams& p, uint32_t pairs, hipStream_t st)
+{
+    launch("match.indexed", indexed_match_kernel, dim3(pairs), dim3(SORT_THREADS), 0, st, p);
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}
+
+}  // namespace
+}  // namespace mage
+
+extern "C" {
+
+mage_status mage_bow_create(const uint8_t* node_desc, const uint32_t* child_start, const uint32_t* children,
+                            uint32_t n_nodes, int device, mage_bow** out)
+{
+    using namespace mage;
+    MAGE_REQUIRE(out, MAGE_EINVAL, "null output");
+    *out = nullptr;
+    MAGE_REQUIRE(n_nodes >= 1 && node_desc && child_start, MAGE_EINVAL, "empty tree");
+    MAGE_REQUIRE(child_start[0] == 0, MAGE_EINVAL, "child_start[0] must be 0");
+    const uint32_t nc = child_start[n_nodes];
+    MAGE_REQUIRE(nc == 0 || children, MAGE_EINVAL, "null children");
+    for (uint32_t i = 0; i < n_nodes; i++) {
+        MAGE_REQUIRE(child_start[i + 1] >= child_start[i], MAGE_EINVAL, "child_start must be non-decreasing");
+        for (uint32_t k = child_start[i]; k < child_start[i + 1]; k++)
+            // OnlineBow::Kmean appends children after their parent: ids grow downwards, which
+            // also guarantees that every descent terminates
+            MAGE_REQUIRE(children[k] > i && children[k] < n_nodes, MAGE_EINVAL,
+                         "child ids must exceed their parent's and be < n_nodes");
+    }
+    mage_status r = bind_device(device);
+    if (r != MAGE_OK) return r;
+    auto* b = new mage_bow();
+    b->device = device;
+    b->n_nodes = n_nodes;
+    auto fail = [&](mage_status s) {
+        b->nodes.release();
+        b->child_start.release();
+        b->children.release();
+        if (b->st) (void)hipStreamDestroy(b->st);
+        delete b;
+        return s;
+    };
+    if ((r = b->nodes.reserve(32ull * n_nodes)) != MAGE_OK) return fail(r);
+    if ((r = b->child_start.reserve(4ull * (n_nodes + 1))) != MAGE_OK) return fail(r);
+    if ((r = b->children.reserve(4ull * (nc + 1))) != MAGE_OK) return fail(r);
+    if (hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess ||
+        hipMemcpy(b->nodes.ptr, node_desc, 32ull * n_nodes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b->child_start.ptr, child_start, 4ull * (n_nodes + 1), hipMemcpyHostToDevice) != hipSuccess ||
+        (nc > 0 && hipMemcpy(b->children.ptr, children, 4ull * nc, hipMemcpyHostToDevice) != hipSuccess)) {
+        set_error("tree upload failed");
+        return fail(MAGE_EDEVICE);
+    }
+    *out = b;
+    return MAGE_OK;
+}
+
+mage_status mage_bow_destroy(mage_bow* b)
+{
+    if (!b) return MAGE_OK;
+    (void)hipSetDevice(b->device);
+    b->nodes.release();
+    b->child_start.release();
+    b->children.release();
+    b->scratch.release();
+    if (b->st) (void)hipStreamDestroy(b->st);
+    delete b;
+    return MAGE_OK;
+}
+
+mage_status mage_bow_find_leaves_device(mage_bow* b, const uint8_t* d_desc, uint32_t n, uint32_t* d_leaf,
+                                        mage_stream stream)
+{
+    using namespace mage;
+    MAGE_REQUIRE(b && (n == 0 || (d_desc && d_leaf)), MAGE_EINVAL, "null argument");
+    return leaves_launch(b, d_desc, n, d_leaf, (hipStream_t)stream);
+}
+
+mage_status mage_bow_find_leaves(mage_bow* b, const uint8_t* desc, uint32_t n, uint32_t* leaf)
+{
+    using namespace mage;
+    MAGE_REQUIRE(b && (n == 0 || (desc && leaf)), MAGE_EINVAL, "null argument");
+    if (n == 0) return MAGE_OK;
+    MAGE_HIP(hipSetDevice(b->device));
+    mage_status r = b->scratch.reserve(36ull * n);
+    if (r != MAGE_OK) return r;
+    uint8_t* d = b->scratch.as<uint8_t>();
+    uint32_t* dl = reinterpret_cast<uint32_t*>(d + 32ull * n);
+    MAGE_HIP(hipMemcpyAsync(d, desc, 32ull * n, hipMemcpyHostToDevice, b->st));
+    if ((r = leaves_launch(b, d, n, dl, b->st)) != MAGE_OK) return r;
+    MAGE_HIP(hipMemcpyAsync(leaf, dl, 4ull * n, hipMemcpyDeviceToHost, b->st));
+    MAGE_HIP(hipStreamSynchronize(b->st));
+    return MAGE_OK;
+}
+
+mage_status mage_indexed_match(mage_bow* b, const uint8_t* desc_a, uint32_t n_a, const uint8_t* mask_a,
+                               const uint8_t* desc_b, uint32_t n_b, const uint8_t* mask_b, int32_t max_distance,
+                               int32_t min_difference, mage_dmatch* out, uint32_t cap, uint32_t* n)
+{
+    using namespace mage;
+    MAGE_REQUIRE(b && n && (cap == 0 || out), MAGE_EINVAL, "null argument");
+    *n = 0;
+    MAGE_REQUIRE((n_a == 0 || desc_a) && (n_b == 0 || desc_b), MAGE_EINVAL, "null input");
+    MAGE_REQUIRE(n_a <= (uint32_t)IM_MAX && n_b <= (uint32_t)IM_MAX, MAGE_EUNSUPPORTED, "more than 4096 features");
+    MAGE_REQUIRE(max_distance >= -1 && max_distance <= 256, MAGE_EINVAL, "maxHammingDist must be in [-1, 256]");
+    if (n_a == 0 || n_b == 0) return MAGE_OK;
+    MAGE_HIP(hipSetDevice(b->device));
+    // device layout: [da][db][la][lb][ma][mb][out][counts]
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t oda = 0, odb = al(32ull * n_a), ola = al(odb + 32ull * n_b), olb = al(ola + 4ull * n_a),
+                 oma = al(olb + 4ull * n_b), omb = al(oma + n_a), oout = al(omb + n_b), ocnt = al(oout + 16ull * n_a),
+                 total = ocnt + 32;
+    mage_status r = b->scratch.reserve(total);
+    if (r != MAGE_OK) return r;
+    char* d = b->scratch.as<char>();
+    MAGE_HIP(hipMemcpyAsync(d + oda, desc_a, 32ull * n_a, hipMemcpyHostToDevice, b->st));
+    MAGE_HIP(hipMemcpyAsync(d + odb, desc_b, 32ull * n_b, hipMemcpyHostToDevice, b->st));
+    if (mask_a) MAGE_HIP(hipMemcpyAsync(d + oma, mask_a, n_a, hipMemcpyHostToDevice, b->st));
+    if (mask_b) MAGE_HIP(hipMemcpyAsync(d + omb, mask_b, n_b, hipMemcpyHostToDevice, b->st));
+    const uint32_t counts[4] = {n_a, n_b, 0, 0};
+    MAGE_HIP(hipMemcpyAsync(d + ocnt, counts, 16, hipMemcpyHostToDevice, b->st));
+    // CreateFeatureMatcher / AddImage: every feature of both images to its leaf
+    if ((r = leaves_launch(b, reinterpret_cast<const uint8_t*>(d + oda), n_a, reinterpret_cast<uint32_t*>(d + ola),
+                           b->st)) != MAGE_OK)
+        return r;
+    if ((r = leaves_launch(b, reinterpret_cast<const uint8_t*>(d + odb), n_b, reinterpret_cast<uint32_t*>(d + olb),
+                           b->st)) != MAGE_OK)
+        return r;
+    IndexedParams p{};
+    p.da = reinterpret_cast<const uint8_t*>(d + oda);
+    p.la = reinterpret_cast<const uint32_t*>(d + ola);
+    p.ma = mask_a ? reinterpret_cast<const uint8_t*>(d + oma) : nullptr;
+    p.na = reinterpret_cast<const uint32_t*>(d + ocnt);
+    p.a_pitch = n_a;
+    p.db = reinterpret_cast<const uint8_t*>(d + odb);
+    p.lb = reinterpret_cast<const uint32_t*>(d + olb);
+    p.mb = mask_b ? reinterpret_cast<const uint8_t*>(d + omb) : nullptr;
+    p.nb = reinterpret_cast<const uint32_t*>(d + ocnt) + 1;
+    p.b_pitch = n_b;
+    p.max_dist = max_distance;
+    p.min_diff = min_difference;
+    p.cap = n_a;
+    p.out = reinterpret_cast<mage_dmatch*>(d + oout);
+    p.n_out = reinterpret_cast<uint32_t*>(d + ocnt) + 2;
+    p.status = reinterpret_cast<uint32_t*>(d + ocnt) + 3;
+    if ((r = indexed_launch(p, 1, b->st)) != MAGE_OK) return r;
+    uint32_t got = 0;
+    MAGE_HIP(hipMemcpyAsync(&got, d + ocnt + 8, 4, hipMemcpyDeviceToHost, b->st));
+    MAGE_HIP(hipStreamSynchronize(b->st));
+    if (got > 0 && cap > 0) MAGE_HIP(hipMemcpy(out, d + oout, 16ull * (got < cap ? got : cap), hipMemcpyDeviceToHost));
+    *n = got < cap ? got : cap;
+    MAGE_REQUIRE(got <= cap, MAGE_ECAPACITY, "output capacity too small");
+    return MAGE_OK;
+}
+
+mage_status mage_indexed_match_batch_device(const uint8_t* d_desc_a, const uint32_t* d_leaf_a, const uint8_t* d_mask_a,
+                                            int64_t a_pitch, const uint32_t* d_n_a, const uint8_t* d_desc_b,
+                                            const uint32_t* d_leaf_b, const uint8_t* d_mask_b, int64_t b_pitch,
+                                            const uint32_t* d_n_b, uint32_t pairs, int32_t max_distance,
+                                            int32_t min_difference, mage_dmatch* d_out, uint32_t cap, uint32_t* d_n,
+                                            uint32_t* d_status, mage_stream stream)
+{
+    using namespace mage;
+    if (pairs == 0) return MAGE_OK;
+    MAGE_REQUIRE(d_desc_a && d_leaf_a && d_n_a && d_desc_b && d_leaf_b && d_n_b && d_out && d_n && d_status,
+                 MAGE_EINVAL, "null buffer");
+    MAGE_REQUIRE(a_pitch > 0 && b_pitch > 0, MAGE_EINVAL, "pitches must be positive");
+    MAGE_REQUIRE(max_distance >= -1 && max_distance <= 256, MAGE_EINVAL, "maxHammingDist must be in [-1, 256]");
+    IndexedParams p{};
+    p.da = d_desc_a;
+    p.la = d_leaf_a;
+    p.ma = d_mask_a;
+    p.na = d_n_a;
+    p.a_pitch = a_pitch;
+    p.db = d_desc_b;
+    p.lb = d_leaf_b;
+    p.mb = d_mask_b;
+    p.nb = d_n_b;
+    p.b_pitch = b_pitch;
+    p.max_dist = max_distance;
+    p.min_diff = min_difference;
+    p.cap = cap;
+    p.out = d_out;
+    p.n_out = d_n;
+    p.status = d_status;
+    return indexed_launch(p, pairs, (hipStream_t)stream);
+}
+
+}  // extern "C"

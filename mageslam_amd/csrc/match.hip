@@ -495,7 +495,7 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
                 mage_dmatch mm;
                 mm.query_idx = i;
                 mm.train_idx = j;
-                mm.img_idx = 0;
+                mm.img_idx = -1;  // cv::DMatch(query, train, distance) (FeatureMatcher.cpp:159-162)
                 mm.distance = (float)d;
                 o[pos] = mm;
             }

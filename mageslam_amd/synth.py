@@ -218,3 +218,60 @@ def ba_tethers(g: BAGraph, seed: int = BA_SEED + 7, count: int = 4, weight: floa
         p7.append(np.concatenate([tc + rng.normal(0, 0.002, 3), quat_from_rot(Rc)]))
     tr = (c1, c2, np.asarray(p7, np.float32), np.full(count, weight, np.float32))
     return Tethers(distance=dist, rotation=rot, transform=tr)
+
+
+def _hamming_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """(len(a), len(b)) Hamming distances of 32-byte descriptors."""
+    ab = np.unpackbits(np.ascontiguousarray(a, np.uint8).reshape(-1, 32), axis=1).astype(np.int32)
+    bb = np.unpackbits(np.ascontiguousarray(b, np.uint8).reshape(-1, 32), axis=1).astype(np.int32)
+    return ab @ (1 - bb).T + (1 - ab) @ bb.T
+
+
+def bow_tree(train: np.ndarray, levels: int = 2, branching: int = 6, max_iter: int = 12, seed: int = 0x0B0E):
+    """OnlineBow vocabulary tree (OnlineBow.cpp:325-337 CreateTree, :451-485 Kmean, :517-587
+    KmeanCenter / IterateClusteringKmean, :631-639 FindCluster) over training descriptors, with
+    BagOfWordsSettings defaults (MageSettings.h:230-232).  InitializeTraining's std::shuffle with a
+    default-seeded mt19937 (:404) is implementation-defined; a seeded numpy permutation stands in.
+    Returns (node_desc (N, 32) u8, child_start (N + 1,) u32, children (N - 1,) u32)."""
+    rng = np.random.default_rng(seed)
+    train = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)
+    nodes = [np.zeros(32, np.uint8)]
+    kids: list[list[int]] = [[]]
+
+    def kmean(parent: int, desc: np.ndarray, level: int) -> None:
+        perm = rng.permutation(len(desc))
+        centers = [desc[i].copy() for i in perm[:branching]]
+        for _ in range(max_iter):
+            d = _hamming_matrix(desc, np.stack(centers))
+            assign = np.argmin(d, axis=1)  # first minimum, as std::min_element
+            changed = 0
+            for g in range(len(centers)):
+                members = desc[assign == g]
+                bits = np.unpackbits(members, axis=1).reshape(-1, 32, 8)[:, :, ::-1]  # LSB first
+                half = (len(members) + 1) // 2
+                newbits = (bits.sum(axis=0) >= half).astype(np.uint8)  # KmeanCenter majority
+                new = np.packbits(newbits[:, ::-1], axis=1).reshape(32)
+                if not np.array_equal(new, centers[g]):
+                    changed += 1
+                centers[g] = new
+            if changed == 0:
+                break
+        d = _hamming_matrix(desc, np.stack(centers))
+        assign = np.argmin(d, axis=1)
+        ids = []
+        for c in centers:
+            ids.append(len(nodes))
+            nodes.append(c)
+            kids.append([])
+        kids[parent].extend(ids)
+        if level < levels:
+            for g, nid in enumerate(ids):
+                sub = desc[assign == g]
+                if len(sub) > 1:
+                    kmean(nid, sub, level + 1)
+
+    kmean(0, train, 1)
+    child_start = np.zeros(len(nodes) + 1, np.uint32)
+    child_start[1:] = np.cumsum([len(k) for k in kids])
+    children = np.array([c for k in kids for c in k], np.uint32)
+    return np.stack(nodes).astype(np.uint8), child_start, children

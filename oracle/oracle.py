@@ -96,6 +96,10 @@ def _declare(L):
     L.oracle_ba_set_observations.argtypes = [vp, i32, vp, vp, vp, vp]
     L.oracle_ba_set_lambda.argtypes = [vp, f32]
     L.oracle_ba_set_tethers.argtypes = [vp, i32, i32, vp, vp, vp, vp]
+    L.oracle_bow_find_leaf.argtypes = [vp, vp, vp, vp]
+    L.oracle_bow_find_leaf.restype = u32
+    L.oracle_indexed_match.argtypes = [vp, vp, vp, vp, u32, vp, vp, u32, vp, i32, i32, vp, u32]
+    L.oracle_indexed_match.restype = u32
     L.oracle_ba_tether_linearization.argtypes = [vp, i32, vp, vp, vp]
     L.oracle_ba_tether_linearization.restype = i32
     L.oracle_ba_get_lambda.argtypes = [vp]
@@ -250,6 +254,28 @@ def match(desc_a, desc_b, mask_a=None, mask_b=None, max_distance=30, min_differe
     out = np.zeros(cap, DM_DTYPE)
     n = lib().oracle_match(_p(da), len(da), _p(ma), _p(db), len(db), _p(mb), max_distance,
                            min_difference, _p(out), cap)
+    return out[:n].copy()
+
+
+def bow_find_leaves(tree, desc):
+    """OnlineBow::FindLeafNode (OnlineBow.cpp:289-311) of each descriptor; tree = (node_desc,
+    child_start, children)."""
+    nd, cs, ch = (np.ascontiguousarray(x) for x in tree)
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    return np.array([lib().oracle_bow_find_leaf(_p(nd), _p(cs), _p(ch), _p(d[i])) for i in range(len(d))], np.uint32)
+
+
+def indexed_match(tree, desc_a, desc_b, mask_a=None, mask_b=None, max_distance=30, min_difference=1):
+    """IndexedMatch (FeatureMatcher.cpp:192-292) with BoW candidate lists; (n,) DM_DTYPE in A order."""
+    nd, cs, ch = (np.ascontiguousarray(x) for x in tree)
+    da = np.ascontiguousarray(desc_a, np.uint8).reshape(-1, 32)
+    db = np.ascontiguousarray(desc_b, np.uint8).reshape(-1, 32)
+    ma = None if mask_a is None else np.ascontiguousarray(mask_a, np.uint8)
+    mb = None if mask_b is None else np.ascontiguousarray(mask_b, np.uint8)
+    cap = max(len(da), 1)
+    out = np.zeros(cap, DM_DTYPE)
+    n = lib().oracle_indexed_match(_p(nd), _p(cs), _p(ch), _p(da), len(da), _p(ma), _p(db), len(db), _p(mb),
+                                   int(max_distance), int(min_difference), _p(out), cap)
     return out[:n].copy()
 
 

@@ -881,7 +881,7 @@ uint32_t oracle_match(const uint8_t* da, uint32_t na, const uint8_t* ma, const u
             if (n < cap) {
                 out[n].query_idx = ia[i];
                 out[n].train_idx = ib[j];
-                out[n].img_idx = 0;
+                out[n].img_idx = -1; /* cv::DMatch(int, int, float): imgIdx = -1 */
                 out[n].distance = (float)fwdD[i];
             }
             n++;

@@ -50,6 +50,13 @@ int main(int argc, char** argv)
         const float qI[4] = {0, 0, 0, 1}, d12[3] = {-0.2f, 0.f, 0.f};
         ba.AllocateRelativeTransformConstraints(1);
         ba.SetRelativeTransformConstraint(0, 1, 2, d12, qI, 10.f);
+        // a two-level tree whose nodes are the first keypoints' descriptors
+        std::vector<mage::hot::Descriptor> nodes(desc.begin(), desc.begin() + 7);
+        const std::vector<uint32_t> childStart = {0, 3, 6, 6, 6, 6, 6, 6}, children = {1, 2, 3, 4, 5, 6};
+        mage::hot::OnlineBowTree tree(nodes, childStart, children);
+        std::vector<mage::hot::DMatch> imatches;
+        const unsigned ni = mage::hot::IndexedMatch(tree, desc, desc, std::vector<bool>(desc.size(), true),
+                                                    std::vector<bool>(desc.size(), true), 30, 1, imatches);
         std::vector<mage::hot::DMatch> rmatches;
         const unsigned nr = mage::hot::RadiusMatch(kps, nullptr, nullptr, desc, kps, nullptr, desc, 2.0f, 30, 1, rmatches);
         std::vector<unsigned> outliers;
@@ -63,6 +70,7 @@ int main(int argc, char** argv)
         o.write((const char*)&nm, 4);
         o.write((const char*)&ms, 4);
         o.write((const char*)&nr, 4);
+        o.write((const char*)&ni, 4);
         std::cout << "keypoints " << n << " self-matches " << nm << " ba_mean_sq " << ms << "\n";
     } catch (const mage::hot::Error& e) {
         std::cerr << "mage error: " << e.what() << "\n";

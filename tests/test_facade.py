@@ -64,3 +64,9 @@ def test_facade_matches_python_api(gpu, tmp_path):
     from mageslam_amd import matcher
 
     assert nr == len(matcher.RadiusMatch(pk, pd, pk, pd, 2.0))
+    ni = int(np.frombuffer(data[16 + 60 * n:20 + 60 * n], np.uint32)[0])
+    from mageslam_amd import bow
+
+    nodes = pd[:7]
+    tree = bow.OnlineBowTree(nodes, np.array([0, 3, 6, 6, 6, 6, 6, 6], np.uint32), np.arange(1, 7, dtype=np.uint32))
+    assert ni == len(bow.IndexedMatch(tree, pd, pd))

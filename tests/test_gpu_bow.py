@@ -1,0 +1,111 @@
+"""GPU parity: vocabulary-tree descent and IndexedMatch through the C-ABI vs the CPU oracle.
+
+Bit-exact: leaf ids, and the full cv::DMatch records (queryIdx, trainIdx, imgIdx = -1, distance)
+in the same order.  The oracle runs the reference's sequential TrackMatch loops
+(FeatureMatcher.cpp:192-292); the kernel uses order-free reductions.
+"""
+import numpy as np
+import pytest
+
+from mageslam_amd import bow, synth
+from mageslam_amd._lib import DM_DTYPE, MAGE_EINVAL, MageError
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def frames(oracle):
+    from mageslam_amd import orb
+
+    det = orb.OrbDetector(nfeatures=2000)
+    descs = [det.DetectAndCompute(synth.frame(t, 640, 480))[1] for t in range(4)]
+    tree = synth.bow_tree(np.concatenate(descs[:2]))
+    return descs, tree
+
+
+def test_find_leaves(gpu, oracle, frames):
+    descs, tree = frames
+    t = bow.OnlineBowTree(*tree)
+    for d in descs:
+        assert np.array_equal(t.find_leaves(d), oracle.bow_find_leaves(tree, d))
+    # a deeper, narrower tree (levels 3, branching 3) and a single-node tree (root is the leaf)
+    deep = synth.bow_tree(descs[2], levels=3, branching=3)
+    assert np.array_equal(bow.OnlineBowTree(*deep).find_leaves(descs[3]), oracle.bow_find_leaves(deep, descs[3]))
+    single = (np.zeros((1, 32), np.uint8), np.zeros(2, np.uint32), np.zeros(0, np.uint32))
+    assert (bow.OnlineBowTree(*single).find_leaves(descs[0][:10]) == 0).all()
+
+
+@pytest.mark.parametrize("maxd,mind", [(30, 1), (50, 0), (64, 5), (10, 1)])
+def test_indexed_match_parity(gpu, oracle, frames, maxd, mind):
+    descs, tree = frames
+    t = bow.OnlineBowTree(*tree)
+    for a, b in [(1, 0), (2, 1), (3, 0)]:
+        g = bow.IndexedMatch(t, descs[a], descs[b], maxHammingDist=maxd, minHammingDifference=mind)
+        o = oracle.indexed_match(tree, descs[a], descs[b], max_distance=maxd, min_difference=mind)
+        assert np.array_equal(g.view(np.uint8), o.view(np.uint8)), (a, b, len(g), len(o))
+
+
+def test_indexed_match_masks_ties_and_edges(gpu, oracle, frames):
+    descs, tree = frames
+    t = bow.OnlineBowTree(*tree)
+    rng = np.random.default_rng(3)
+    a, b = descs[1], descs[0]
+    ma = rng.random(len(a)) < 0.6
+    mb = rng.random(len(b)) < 0.7
+    g = bow.IndexedMatch(t, a, b, ma, mb)
+    o = oracle.indexed_match(tree, a, b, ma.astype(np.uint8), mb.astype(np.uint8))
+    assert np.array_equal(g.view(np.uint8), o.view(np.uint8))
+    # exact duplicates in B create best-distance ties (rejected for min_difference >= 1, the lower
+    # index wins at 0)
+    bd = np.concatenate([b, b[::3]])
+    for mind in (0, 1):
+        g = bow.IndexedMatch(t, a, bd, minHammingDifference=mind)
+        o = oracle.indexed_match(tree, a, bd, min_difference=mind)
+        assert np.array_equal(g.view(np.uint8), o.view(np.uint8))
+    # self match, one-element sets, empty masks
+    g = bow.IndexedMatch(t, a, a)
+    assert np.array_equal(g.view(np.uint8), oracle.indexed_match(tree, a, a).view(np.uint8))
+    assert len(bow.IndexedMatch(t, a[:1], a[:1])) == 1
+    assert len(bow.IndexedMatch(t, a, b, np.zeros(len(a), bool))) == 0
+    assert len(bow.IndexedMatch(t, a[:0], b)) == 0
+
+
+def test_indexed_match_batch_device(gpu, oracle, frames):
+    import torch
+
+    descs, tree = frames
+    t = bow.OnlineBowTree(*tree)
+    pitch = 2048
+    n = len(descs)
+    D = torch.zeros((n, pitch, 32), dtype=torch.uint8, device="cuda")
+    L = torch.zeros((n, pitch), dtype=torch.int32, device="cuda")
+    M = torch.zeros((n, pitch), dtype=torch.uint8, device="cuda")
+    rng = np.random.default_rng(9)
+    masks = [rng.random(len(d)) < 0.8 for d in descs]
+    for i, d in enumerate(descs):
+        D[i, : len(d)] = torch.from_numpy(d).cuda()
+        M[i, : len(d)] = torch.from_numpy(masks[i].astype(np.uint8)).cuda()
+        t.find_leaves_device(D[i], len(d), L[i])
+    counts = torch.tensor([len(d) for d in descs], dtype=torch.int32, device="cuda")
+    # pairs (i + 1, i): A = frames 1..3, B = frames 0..2
+    out = torch.zeros((n - 1, pitch * 16), dtype=torch.uint8, device="cuda")
+    nout = torch.zeros(n - 1, dtype=torch.int32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    bow.indexed_match_batch_device(D[1:], L[1:], M[1:], pitch, counts[1:], D[:-1], L[:-1], M[:-1], pitch, counts[:-1],
+                                   n - 1, 30, 1, out, pitch, nout, status)
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0
+    for p in range(n - 1):
+        o = oracle.indexed_match(tree, descs[p + 1], descs[p], masks[p + 1].astype(np.uint8), masks[p].astype(np.uint8))
+        k = int(nout[p].item())
+        g = out[p, : 16 * k].cpu().numpy().view(DM_DTYPE)
+        assert np.array_equal(g.view(np.uint8), o.view(np.uint8)), p
+
+
+def test_tree_validation(gpu):
+    nd = np.zeros((3, 32), np.uint8)
+    with pytest.raises(MageError) as e:
+        bow.OnlineBowTree(nd, np.array([0, 1, 2, 2], np.uint32), np.array([2, 1], np.uint32))  # 1 -> 1: a cycle
+    assert e.value.status == MAGE_EINVAL
+    with pytest.raises(MageError):
+        bow.OnlineBowTree(nd, np.array([0, 1, 1, 1], np.uint32), np.array([7], np.uint32))  # out of range

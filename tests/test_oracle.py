@@ -106,6 +106,7 @@ def test_orb_golden_vga(oracle):
 def test_match_golden(oracle):
     g = np.load(GOLDEN / "match_vga_t1_t0.npz")
     m = oracle.match(g["desc_a"], g["desc_b"], max_distance=30, min_difference=1)
+    assert (m["img_idx"] == -1).all()  # cv::DMatch(int, int, float) (FeatureMatcher.cpp:159-162)
     assert np.array_equal(np.stack([m["query_idx"], m["train_idx"], m["distance"].astype(np.int32)], 1),
                           g["matches"])
 
@@ -494,3 +495,74 @@ def test_ba_tether_only_camera_joins_system(oracle):
     # the constraint holds: log(T2^-1 C T1) ~ 0
     e, _, _ = b.tether_linearization(0)
     assert np.abs(e).max() < 1e-4
+
+
+def _tiny_tree():
+    """root -> {1, 2}; 1 -> {3, 4}; 2 -> {5}: node descriptors chosen for tie cases."""
+    nd = np.zeros((6, 32), np.uint8)
+    nd[1, 0] = 0x0F
+    nd[2, 0] = 0xF0
+    nd[3, 1] = 0x01
+    nd[4, 1] = 0x02
+    nd[5, 2] = 0xFF
+    cs = np.array([0, 2, 4, 5, 5, 5, 5], np.uint32)
+    ch = np.array([1, 2, 3, 4, 5], np.uint32)
+    return nd, cs, ch
+
+
+def test_bow_find_leaf_known_answers(oracle):
+    """OnlineBow::FindLeafNode (OnlineBow.cpp:289-311): strictly-smaller updates, so the first
+    child wins ties; descent stops at a node without children."""
+    tree = _tiny_tree()
+    q = np.zeros((4, 32), np.uint8)
+    # q0: d(1) = 4, d(2) = 4 -> child 1 (first); then d(3) = d(4) = 1 -> 3
+    q[1, 1] = 0x02  # d(3) = 2, d(4) = 0 -> 4 (under 1: d(1) = d(2) = 4)
+    q[2, 0] = 0xF0  # -> 2, then its only child 5
+    q[3, 0] = 0x0F
+    q[3, 1] = 0x03  # -> 1, then d(3) = 1, d(4) = 1 -> 3
+    assert list(oracle.bow_find_leaves(tree, q)) == [3, 4, 5, 3]
+
+
+def test_bow_tree_builder_shape(oracle):
+    from mageslam_amd import synth
+
+    g = np.load(GOLDEN / "match_vga_t1_t0.npz")
+    nd, cs, ch = synth.bow_tree(np.concatenate([g["desc_a"], g["desc_b"]]))
+    assert len(nd) == 1 + 6 + 36 and cs[0] == 0 and cs[-1] == len(ch) == len(nd) - 1
+    # children follow their parent (OnlineBow::Kmean appends)
+    for i in range(len(nd)):
+        assert all(c > i for c in ch[cs[i]:cs[i + 1]])
+    leaves = oracle.bow_find_leaves((nd, cs, ch), g["desc_a"])
+    assert all(cs[l] == cs[l + 1] for l in np.unique(leaves))
+
+
+def test_indexed_match_semantics(oracle):
+    """IndexedMatch (FeatureMatcher.cpp:192-292) on hand-made sets in one leaf: TrackMatch's
+    second best keeps ties, the min-difference test, masks and the reverse check."""
+    tree = _tiny_tree()
+    base = np.zeros(32, np.uint8)
+    base[0] = 0x0F  # leaf 3 region
+    base[1] = 0x01
+
+    def with_bits(k):
+        d = base.copy()
+        for b in k:
+            d[4 + b // 8] |= 1 << (b % 8)
+        return d
+
+    A = np.stack([with_bits([]), with_bits([0, 1, 2]), with_bits(range(20, 40))])
+    B = np.stack([with_bits([5]), with_bits([0, 1]), with_bits([0, 1, 2, 3]), with_bits([6])])
+    # A0: d(B0)=1, d(B1)=2, d(B2)=4, d(B3)=1 -> best B0 (first), second 1 -> diff 0 < 1: rejected
+    # A1: d(B0)=4, d(B1)=1, d(B2)=1, d(B3)=4 -> tie again: rejected
+    m = oracle.indexed_match(tree, A, B, max_distance=30, min_difference=1)
+    assert len(m) == 0
+    # min_difference 0 accepts ties: A0 -> B0; reverse of B0 over A: d(A0)=1 best -> kept
+    m = oracle.indexed_match(tree, A, B, max_distance=30, min_difference=0)
+    assert [(r["query_idx"], r["train_idx"], r["distance"], r["img_idx"]) for r in m] == [(0, 0, 1.0, -1), (1, 1, 1.0, -1)]
+    # mask B0 out: A0 -> B3 (d = 1), second B1 (d = 2): diff 1 >= 1 accepted; B3's reverse -> A0
+    m = oracle.indexed_match(tree, A, B, mask_b=np.array([0, 1, 1, 1], np.uint8), min_difference=1)
+    assert [(r["query_idx"], r["train_idx"]) for r in m] == [(0, 3)]
+    # max_distance: A2 is 20 bits away from everything: only a max above 20 lets it compete
+    assert all(r["query_idx"] != 2 for r in oracle.indexed_match(tree, A, B, max_distance=19, min_difference=0))
+    # empty mask -> 0 matches
+    assert len(oracle.indexed_match(tree, A, B, mask_a=np.zeros(3, np.uint8))) == 0
