@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--ba-iters", type=int, default=30)
     p.add_argument("--ba-warmup", type=int, default=3)
     p.add_argument("--no-ba", action="store_true")
+    p.add_argument("--pose-problems", type=int, default=2048, help="pose-only BA problems per launch")
+    p.add_argument("--pose-iters", type=int, default=20)
+    p.add_argument("--no-pose", action="store_true")
     p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
@@ -245,6 +248,94 @@ def run_ba(args, local_rank, torch):
     return res, g
 
 
+POSE_STEPS, POSE_HUBER, POSE_MAXE = 3, 4.0, 36.0  # TrackLocalMap's first OptimizeCameraPose (MageSettings.h:184-189)
+
+
+def run_pose(args, local_rank, torch):
+    """Batched pose-only BA (SURVEY.md §8(f) 2): TrackLocalMap::OptimizeCameraPose for a batch of
+    frames per launch (mage_ba_pose_batch_device), inputs resident in HBM."""
+    from mageslam_amd import _lib, bundler, synth
+
+    pb = synth.pose_batch(problems=args.pose_problems, obs=600)
+    K = args.pose_problems
+    E = int(pb.obs_start[-1])
+    dev = f"cuda:{local_rank}"
+    T = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)  # noqa: E731
+    pos, r9, intr = T(pb.pos, np.float32), T(pb.r9, np.float32), T(pb.intr, np.float32)
+    ost, pts, uv, info = T(pb.obs_start.astype(np.int32), np.int32), T(pb.points, np.float32), T(pb.uv, np.float32), \
+        T(pb.info, np.float32)
+    pos_o = torch.empty((K, 3), dtype=torch.float32, device=dev)
+    r9_o = torch.empty((K, 9), dtype=torch.float32, device=dev)
+    qt_o = torch.empty((K, 7), dtype=torch.float64, device=dev)
+    outl = torch.empty(E, dtype=torch.uint8, device=dev)
+    ms = torch.empty(K, dtype=torch.float32, device=dev)
+    stats = torch.empty((K, 2), dtype=torch.int32, device=dev)
+
+    def once():
+        bundler.pose_batch_device(K, pos, r9, intr, ost, pts, uv, info, POSE_STEPS, POSE_HUBER, POSE_MAXE, pos_o,
+                                  r9_o, qt_o, outl, ms, stats)
+
+    for _ in range(3):
+        once()
+    torch.cuda.synchronize()
+    n = args.pose_iters
+    t0 = time.perf_counter()
+    for _ in range(n):
+        once()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    lib = _lib.load()
+    lib.mage_profile_reset()
+    lib.mage_profile_enable(1)
+    for _ in range(3):
+        once()
+    torch.cuda.synchronize()
+    lib.mage_profile_enable(0)
+    kern = _lib.profile_report()
+    st = stats.cpu().numpy()
+    res = {"metric": "pose-only BA problems/sec (OptimizeCameraPose: 1 camera, ~600 fixed points, 3 LM steps)",
+           "value": n * K / el, "unit": "problems/s", "dtype": "f64", "problems_per_launch": K,
+           "observations": E, "lm_iterations_per_problem": float(st[:, 0].mean()),
+           "trials_per_problem": float(st[:, 1].mean()),
+           "config": {"workload": f"{K} synthetic 720p frames x {E / K:.0f} observations, huber {POSE_HUBER}, "
+                                  f"maxErrorSquare {POSE_MAXE}, {POSE_STEPS} steps (TrackLocalMap.cpp:96-107)"},
+           "kernels": {k: {"launches": c, "avg_ms": v / max(c, 1)} for k, (c, v) in kern.items()}}
+    if "ba.pose_batch" in kern:
+        c, v = kern["ba.pose_batch"]
+        avg_s = v / c / 1000.0
+        # compulsory bytes per launch: observations (point 12 + uv 8 + info 4 + flag 1) and per-problem
+        # pose in/out (12 + 36 + 16 in, 12 + 36 + 56 + 4 + 8 out)
+        byts = E * 25 + K * (64 + 116)
+        res["roofline"] = {"bound": "hbm", "kernel": "ba.pose_batch", "achieved": byts / avg_s / 1e9,
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": byts / avg_s / 1e9 / HBM_PEAK_GBS,
+                           "traffic": None, "algorithmic_bytes_per_launch": byts, "avg_launch_ms": v / c}
+    return res, pb
+
+
+def cpu_pose_baseline(pb, budget_s):
+    from oracle import oracle as O
+
+    K = len(pb.pos)
+    el, n = 0.0, 0
+    chunk = 32
+    import dataclasses
+
+    while el < budget_s or n == 0:
+        k0 = (n * chunk) % K
+        k1 = min(k0 + chunk, K)
+        s0, s1 = int(pb.obs_start[k0]), int(pb.obs_start[k1])
+        sub = dataclasses.replace(pb, pos=pb.pos[k0:k1], r9=pb.r9[k0:k1], intr=pb.intr[k0:k1],
+                                  obs_start=(pb.obs_start[k0:k1 + 1] - pb.obs_start[k0]).astype(np.uint32),
+                                  points=pb.points[s0:s1], uv=pb.uv[s0:s1], info=pb.info[s0:s1])
+        t0 = time.perf_counter()
+        O.pose_batch(sub, POSE_STEPS, POSE_HUBER, POSE_MAXE)
+        el += time.perf_counter() - t0
+        n += 1
+    return {"value": n * chunk / el, "unit": "problems/s", "cores": 1, "kind": "port",
+            "sample": f"{n * chunk} problems of the same batch, oracle (fresh BundlerLib per frame), single thread, "
+                      f"{el:.1f} s"}
+
+
 def cpu_ba_baseline(g, budget_s):
     from oracle import oracle as O
 
@@ -313,6 +404,7 @@ def main():
 
     orb_res = run_orb(args, rank, world, local_rank, torch, dist)
     ba_res, g = (None, None) if args.no_ba else run_ba(args, local_rank, torch)
+    pose_res, pb = (None, None) if args.no_pose else run_pose(args, local_rank, torch)
     if world > 1:
         dist.barrier()
 
@@ -342,12 +434,18 @@ def main():
         }
         if ba_res is not None:
             out["ba"] = ba_res
+        if pose_res is not None:
+            out["pose_ba"] = pose_res
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_orb_baseline(args, args.cpu_sample_s)
             if ba_res is not None:
                 cb = cpu_ba_baseline(g, args.cpu_sample_s)
                 ba_res["cpu_baseline"] = cb
                 ba_res["vs_cpu"] = ba_res["value"] / cb["value"]
+            if pose_res is not None:
+                cp = cpu_pose_baseline(pb, min(args.cpu_sample_s, 6.0))
+                pose_res["cpu_baseline"] = cp
+                pose_res["vs_cpu"] = pose_res["value"] / cp["value"]
             out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
         print(json.dumps(out))
     if world > 1:

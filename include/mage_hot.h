@@ -313,6 +313,25 @@ typedef struct mage_ba_stats {
 } mage_ba_stats;
 mage_status mage_ba_get_stats(mage_ba* ba, mage_ba_stats* stats);
 
+/* Batched pose-only BA: TrackLocalMap::OptimizeCameraPose (TrackLocalMap.cpp:421-501) for many
+ * independent frames in one launch.  Problem k = a fresh BundlerLib with ArePointsFixed, camera 0 =
+ * (pos3[k], r9[k] column-major, intr4[k] = {cx, cy, fx, fy}, not fixed), observations obs_start[k] ..
+ * obs_start[k+1]-1 each on its own fixed map point (points3, uv, info = MapPointRefinementConfidence),
+ * then StepBundleAdjustment(nsteps x huber, max_error_square).  Outputs per problem: GetPose(0)
+ * (pos3_out, r9_out column-major), mean_sq (the post-pass mean, NaN if nothing kept), optionally
+ * qt7_out (fp64 q xyzw + t) and stats {LM iterations, trials}; per observation outlier = 1 where
+ * the post-pass rejects it (outlierIndices = the flagged indices, ascending).  Host buffers,
+ * synchronous; _device: device buffers, asynchronous on `stream`. */
+mage_status mage_ba_pose_batch(uint32_t problems, const float* pos3, const float* r9, const float* intr4,
+                               const uint32_t* obs_start, const float* points3, const float* uv, const float* info,
+                               uint32_t nsteps, float huber, float max_error_square, float* pos3_out, float* r9_out,
+                               double* qt7_out, uint8_t* outlier, float* mean_sq, uint32_t* stats, int device);
+mage_status mage_ba_pose_batch_device(uint32_t problems, const float* d_pos3, const float* d_r9, const float* d_intr4,
+                                      const uint32_t* d_obs_start, const float* d_points3, const float* d_uv,
+                                      const float* d_info, uint32_t nsteps, float huber, float max_error_square,
+                                      float* d_pos3_out, float* d_r9_out, double* d_qt7_out, uint8_t* d_outlier,
+                                      float* d_mean_sq, uint32_t* d_stats, mage_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

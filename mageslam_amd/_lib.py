@@ -31,7 +31,7 @@ EXPORTS = [
     "mage_ba_create", "mage_ba_destroy", "mage_ba_set_cameras", "mage_ba_fix_camera",
     "mage_ba_set_points", "mage_ba_set_observations", "mage_ba_set_lambda", "mage_ba_get_lambda",
     "mage_ba_set_tethers", "mage_ba_step", "mage_ba_get_poses", "mage_ba_get_points",
-    "mage_ba_get_stats", "mage_ba_get_state_f64",
+    "mage_ba_get_stats", "mage_ba_get_state_f64", "mage_ba_pose_batch", "mage_ba_pose_batch_device",
 ]
 
 
@@ -173,3 +173,5 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_ba_get_points", st, vp, vp)
     sig("mage_ba_get_state_f64", st, vp, vp, vp)
     sig("mage_ba_get_stats", st, vp, C.POINTER(BAStats))
+    sig("mage_ba_pose_batch", st, u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp, C.c_int)
+    sig("mage_ba_pose_batch_device", st, u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp, vp)

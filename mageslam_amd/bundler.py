@@ -235,3 +235,35 @@ class BundlerLib:
         check(_lib.load().mage_ba_get_stats(self._h, C.byref(s)))
         return dict(iterations=s.iterations, trials=s.trials, rejected=s.rejected_trials, chi2=s.last_chi2,
                     lambda_=s.lambda_)
+
+
+def OptimizeCameraPoses(pb, numIterations: int, maxOutlierErrorSquared: float, huberWidth: float, device: int = 0):
+    """TrackLocalMap::OptimizeCameraPose (TrackLocalMap.cpp:421-501) for a batch of frames in one
+    launch.  `pb` holds pos (K,3), r9 (K,9 column-major), intr (K,4), obs_start (K+1), points (E,3),
+    uv (E,2), info (E) (synth.PoseBatch).  Returns dict(pos, r9, qt7, outlier (E,) u8, mean_sq,
+    stats (K, 2) = LM iterations / trials); outlierIndices of problem k are the flagged entries of
+    its observation range."""
+    K = len(pb.pos)
+    E = int(pb.obs_start[-1])
+    c = np.ascontiguousarray
+    out = dict(pos=np.zeros((K, 3), np.float32), r9=np.zeros((K, 9), np.float32), qt7=np.zeros((K, 7)),
+               outlier=np.zeros(max(E, 1), np.uint8), mean_sq=np.zeros(K, np.float32),
+               stats=np.zeros((K, 2), np.uint32))
+    check(_lib.load().mage_ba_pose_batch(
+        K, ptr(c(pb.pos, np.float32)), ptr(c(pb.r9, np.float32)), ptr(c(pb.intr, np.float32)),
+        ptr(c(pb.obs_start, np.uint32)), ptr(c(pb.points, np.float32)), ptr(c(pb.uv, np.float32)),
+        ptr(c(pb.info, np.float32)), int(numIterations), float(huberWidth), float(maxOutlierErrorSquared),
+        ptr(out["pos"]), ptr(out["r9"]), ptr(out["qt7"]), ptr(out["outlier"]), ptr(out["mean_sq"]),
+        ptr(out["stats"]), device))
+    out["outlier"] = out["outlier"][:E]
+    return out
+
+
+def pose_batch_device(problems: int, pos3, r9, intr4, obs_start, points3, uv, info, nsteps: int, huber: float,
+                      max_error_square: float, pos3_out, r9_out, qt7_out, outlier, mean_sq, stats=None,
+                      stream=None) -> None:
+    """Device form of OptimizeCameraPoses over torch device tensors (asynchronous)."""
+    check(_lib.load().mage_ba_pose_batch_device(
+        problems, ptr(pos3), ptr(r9), ptr(intr4), ptr(obs_start), ptr(points3), ptr(uv), ptr(info), nsteps,
+        float(huber), float(max_error_square), ptr(pos3_out), ptr(r9_out), ptr(qt7_out), ptr(outlier), ptr(mean_sq),
+        ptr(stats), C.c_void_p(stream) if stream else None))

@@ -1,0 +1,413 @@
+// pose.hip — batched pose-only bundle adjustment on MI355X (gfx950).
+//
+// TrackLocalMap::OptimizeCameraPose (Core/MAGESLAM/Source/Tracking/TrackLocalMap.cpp:421-501) builds
+// a fresh BundlerLib with ArePointsFixed, one free camera and one observation per map point, and
+// runs StepBundleAdjustment(numIterations x huberWidth, maxOutlierErrorSquared) — every tracked frame,
+// twice (:96-121).  Through the general BA path each of those tiny problems costs a dozen launches and
+// a host round trip per LM trial; here a whole batch of them is ONE launch: one 256-thread workgroup
+// per problem runs g2o's complete StepBundleAdjustment on device:
+//   per step   linearise at the current pose (errors, Huber, the 6x6 Hpp / bp of J_pose^T w J_pose)
+//              with one workgroup reduction; lambda = 1e-5 max diag at iteration 0 (computeLambdaInit)
+//   per trial  (<= 10, OptimizationAlgorithmLevenberg::solve) lane 0 factors Hpp + lambda I (6x6
+//              Cholesky; on failure x keeps the previous solve, as LinearSolverDense leaves it), the
+//              trial pose exp(x) * T, computeScale; one reduction evaluates the trial chi2; accept /
+//              reject exactly as g2o (rho, alpha, ni); a failed solve() ends the step loop
+//   post-pass  (BundlerLib.cpp:385-446) each edge's squared error from the LAST evaluated state (g2o
+//              keeps _error of the last computeActiveErrors, i.e. the last trial, even when it was
+//              rejected) and the cheirality test at the current pose; outlier flags, mean of the kept.
+// Points are fixed (ArePointsFixed): no Schur complement, the reduced system is the camera block.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "ba_math.hpp"
+#include "common.hpp"
+
+namespace mage {
+namespace {
+
+using namespace ba;
+
+constexpr int PB_THREADS = 256;
+
+struct PoseParams {
+    const float* pos3;    // per problem: view-space t
+    const float* r9;      // per problem: rotation, Eigen column-major
+    const float* intr4;   // per problem: cx, cy, fx, fy
+    const uint32_t* obs_start;  // problems + 1
+    const float* points3;       // per observation: map point (fixed)
+    const float* uv;            // per observation
+    const float* info;          // per observation: information scalar
+    uint32_t nsteps;
+    double huber;
+    double max_err_sq;
+    float* pos3_out;
+    float* r9_out;
+    double* qt7_out;      // optional fp64 state
+    uint8_t* outlier;     // per observation
+    float* mean_sq;       // per problem
+    uint32_t* stats;      // optional: per problem {iterations, trials}
+};
+
+// SetCameraPose: Eigen::Quaternionf{Matrix3f}.normalized() in float, then SE3Quat(q, t) in double
+// (BundlerLib.cpp:269-273; the same arithmetic as mage_ba_set_cameras)
+__device__ void pose_from_input(const float* r9, const float* t3, double q[4], double t[3])
+{
+    float m[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) m[r * 3 + c] = r9[c * 3 + r];
+    float qf[4];
+    const float tr = m[0] + m[4] + m[8];
+    if (tr > 0.f) {
+        float s = sqrtf(tr + 1.0f);
+        qf[3] = 0.5f * s;
+        s = 0.5f / s;
+        qf[0] = (m[7] - m[5]) * s;
+        qf[1] = (m[2] - m[6]) * s;
+        qf[2] = (m[3] - m[1]) * s;
+    } else {
+        int a = 0;
+        if (m[4] > m[0]) a = 1;
+        if (m[8] > m[a * 4]) a = 2;
+        const int j = (a + 1) % 3, k = (j + 1) % 3;
+        float s = sqrtf(m[a * 4] - m[j * 4] - m[k * 4] + 1.0f);
+        qf[a] = 0.5f * s;
+        s = 0.5f / s;
+        qf[3] = (m[k * 3 + j] - m[j * 3 + k]) * s;
+        qf[j] = (m[j * 3 + a] + m[a * 3 + j]) * s;
+        qf[k] = (m[k * 3 + a] + m[a * 3 + k]) * s;
+    }
+    const float nrm = sqrtf(qf[0] * qf[0] + qf[1] * qf[1] + qf[2] * qf[2] + qf[3] * qf[3]);
+    for (int k = 0; k < 4; k++) q[k] = (double)(qf[k] / nrm);
+    d_se3_normalize(q);
+    for (int k = 0; k < 3; k++) t[k] = (double)t3[k];
+}
+
+// reprojection error, robust chi2 and (if H) the pose normal-equation terms of one edge
+struct EdgeIn {
+    double X[3], u, v, info;
+};
+
+__device__ __forceinline__ void edge_terms(const EdgeIn& e, const double q[4], const double t[3], double f, double cx,
+                                           double cy, double huber, double ev[2], double& rho0, double* acc28)
+{
+    double xc[3];
+    d_qrot(q, e.X, xc);
+    xc[0] += t[0];
+    xc[1] += t[1];
+    xc[2] += t[2];
+    ev[0] = e.u - (xc[0] / xc[2] * f + cx);
+    ev[1] = e.v - (xc[1] / xc[2] * f + cy);
+    const double chi2 = e.info * (ev[0] * ev[0] + ev[1] * ev[1]);
+    double rho1;
+    d_huber(huber, chi2, rho0, rho1);
+    if (!acc28) return;
+    double Jp[12];
+    jac_pose(xc, f, Jp);
+    const double w = rho1 * e.info;
+    const double or0 = -e.info * ev[0] * rho1, or1 = -e.info * ev[1] * rho1;
+    int k = 0;
+    for (int r = 0; r < 6; r++)
+        for (int c = r; c < 6; c++) acc28[k++] += (Jp[r] * Jp[c] + Jp[6 + r] * Jp[6 + c]) * w;
+    for (int r = 0; r < 6; r++) acc28[21 + r] += Jp[r] * or0 + Jp[6 + r] * or1;
+}
+
+// fixed-order workgroup sum of acc[0..N) into out[0..N) (all threads read out afterwards)
+template <int N>
+__device__ __forceinline__ void wg_sum(double (&acc)[N], double (*red)[N], double* out)
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        double v = acc[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[wave][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < N) {
+        double v = 0;
+        for (int w = 0; w < PB_THREADS / kWave; w++) v += red[w][threadIdx.x];
+        out[threadIdx.x] = v;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
+{
+    __shared__ double red[PB_THREADS / kWave][28];
+    __shared__ double sum[28];
+    __shared__ double cur_q[4], cur_t[3], tr_q[4], tr_t[3], ev_q[4], ev_t[3];
+    __shared__ double s_lambda, s_ni, s_chi, s_x[6], s_scale;
+    __shared__ int s_ok2, s_have_eval;
+    const int pr = blockIdx.x, tid = threadIdx.x;
+    const uint32_t e0 = p.obs_start[pr], e1 = p.obs_start[pr + 1];
+    const int E = (int)(e1 - e0);
+    const double f = p.intr4[4 * pr + 2], cx = p.intr4[4 * pr], cy = p.intr4[4 * pr + 1];
+    if (tid == 0) {
+        pose_from_input(p.r9 + 9 * pr, p.pos3 + 3 * pr, cur_q, cur_t);
+        for (int k = 0; k < 6; k++) s_x[k] = 0;
+        s_have_eval = 0;
+    }
+    __syncthreads();
+    auto load_edge = [&](int i) {
+        EdgeIn e;
+        const uint32_t g = e0 + i;
+        e.X[0] = p.points3[3 * g];
+        e.X[1] = p.points3[3 * g + 1];
+        e.X[2] = p.points3[3 * g + 2];
+        e.u = p.uv[2 * g];
+        e.v = p.uv[2 * g + 1];
+        e.info = p.info[g];
+        return e;
+    };
+    uint32_t iters = 0, trials = 0;
+    // StepOptimizer::Step: no active vertex (no observations) -> useless, every Step fails
+    for (uint32_t step = 0; E > 0 && step < p.nsteps; step++) {
+        // linearise at the current pose
+        double acc[28];
+        for (int k = 0; k < 28; k++) acc[k] = 0;
+        for (int i = tid; i < E; i += PB_THREADS) {
+            const EdgeIn e = load_edge(i);
+            double ev[2], rho0;
+            edge_terms(e, cur_q, cur_t, f, cx, cy, p.huber, ev, rho0, acc);
+            acc[27] += rho0;
+        }
+        wg_sum<28>(acc, red, sum);
+        double currentChi = sum[27];
+        if (step == 0) {
+            double m = 0;
+            for (int r = 0, k = 0; r < 6; k += 6 - r, r++) m = fmax(fabs(sum[k]), m);
+            if (tid == 0) {
+                s_lambda = 1e-5 * m;  // computeLambdaInit, tau 1e-5 (fresh BundlerLib: no user lambda)
+                s_ni = 2;
+            }
+        }
+        __syncthreads();
+        double rho = 0;
+        int qmax = 0;
+        do {
+            if (tid == 0) {
+                // S = Hpp + lambda I; Cholesky (LLT) and solve; on failure x keeps the previous solve
+                double L[36];
+                const double lam = s_lambda;
+                for (int r = 0, k = 0; r < 6; r++)
+                    for (int c = r; c < 6; c++, k++) {
+                        L[r * 6 + c] = sum[k];
+                        L[c * 6 + r] = sum[k];
+                    }
+                for (int r = 0; r < 6; r++) L[r * 6 + r] += lam;
+                int ok = 1;
+                for (int j = 0; j < 6 && ok; j++) {
+                    double d = L[j * 6 + j];
+                    for (int k = 0; k < j; k++) d -= L[j * 6 + k] * L[j * 6 + k];
+                    if (!(d > 0)) {
+                        ok = 0;
+                        break;
+                    }
+                    d = sqrt(d);
+                    L[j * 6 + j] = d;
+                    for (int i = j + 1; i < 6; i++) {
+                        double s = L[i * 6 + j];
+                        for (int k = 0; k < j; k++) s -= L[i * 6 + k] * L[j * 6 + k];
+                        L[i * 6 + j] = s / d;
+                    }
+                }
+                if (ok) {
+                    double x[6];
+                    for (int i = 0; i < 6; i++) {
+                        double s = sum[21 + i];
+                        for (int k = 0; k < i; k++) s -= L[i * 6 + k] * x[k];
+                        x[i] = s / L[i * 6 + i];
+                    }
+                    for (int i = 5; i >= 0; i--) {
+                        double s = x[i];
+                        for (int k = i + 1; k < 6; k++) s -= L[k * 6 + i] * x[k];
+                        x[i] = s / L[i * 6 + i];
+                    }
+                    for (int k = 0; k < 6; k++) s_x[k] = x[k];
+                }
+                s_ok2 = ok;
+                double q[4] = {cur_q[0], cur_q[1], cur_q[2], cur_q[3]}, t[3] = {cur_t[0], cur_t[1], cur_t[2]};
+                double u[6];
+                for (int k = 0; k < 6; k++) u[k] = s_x[k];
+                d_oplus(q, t, u);
+                for (int k = 0; k < 4; k++) tr_q[k] = ev_q[k] = q[k];
+                for (int k = 0; k < 3; k++) tr_t[k] = ev_t[k] = t[k];
+                s_have_eval = 1;
+                double sc = 0;
+                for (int k = 0; k < 6; k++) sc += s_x[k] * (lam * s_x[k] + sum[21 + k]);
+                s_scale = sc + 1e-3;
+            }
+            __syncthreads();
+            double c = 0;
+            for (int i = tid; i < E; i += PB_THREADS) {
+                const EdgeIn e = load_edge(i);
+                double ev[2], rho0;
+                edge_terms(e, tr_q, tr_t, f, cx, cy, p.huber, ev, rho0, nullptr);
+                c += rho0;
+            }
+            double one[1] = {c};
+            wg_sum<1>(one, reinterpret_cast<double(*)[1]>(red), &s_chi);
+            double tempChi = s_chi;
+            if (!s_ok2) tempChi = DBL_MAX;
+            rho = (currentChi - tempChi) / s_scale;
+            trials++;
+            const bool accept = rho > 0 && isfinite(tempChi);
+            __syncthreads();
+            if (tid == 0) {
+                if (accept) {
+                    double alpha = 1. - pow((2 * rho - 1), 3);
+                    alpha = fmin(alpha, 2. / 3.);
+                    const double scaleFactor = fmax(1. / 3., alpha);
+                    s_lambda *= scaleFactor;
+                    s_ni = 2;
+                    for (int k = 0; k < 4; k++) cur_q[k] = tr_q[k];
+                    for (int k = 0; k < 3; k++) cur_t[k] = tr_t[k];
+                } else {
+                    s_lambda *= s_ni;
+                    s_ni *= 2;
+                }
+            }
+            if (accept) currentChi = tempChi;
+            qmax++;
+            __syncthreads();
+        } while (rho < 0 && qmax < 10);
+        iters++;
+        const bool ok = !(qmax == 10 || rho == 0 || !isfinite(s_lambda));
+        if (!ok) break;
+    }
+    __syncthreads();
+    // post-pass: errors of the last evaluated state, cheirality at the current pose
+    double qc[4] = {-cur_q[0], -cur_q[1], -cur_q[2], cur_q[3]};
+    double it[3], fwd[3];
+    d_qrot(qc, cur_t, it);
+    const double z[3] = {0, 0, 1};
+    d_qrot(qc, z, fwd);
+    double acc2[2] = {0, 0};
+    for (int i = tid; i < E; i += PB_THREADS) {
+        const EdgeIn e = load_edge(i);
+        double ev[2] = {0, 0}, rho0;
+        if (s_have_eval) edge_terms(e, ev_q, ev_t, f, cx, cy, p.huber, ev, rho0, nullptr);
+        const double ss = ev[0] * ev[0] + ev[1] * ev[1];
+        const double dot = (e.X[0] + it[0]) * fwd[0] + (e.X[1] + it[1]) * fwd[1] + (e.X[2] + it[2]) * fwd[2];
+        const bool out = dot <= 0 || ss > p.max_err_sq;
+        p.outlier[e0 + i] = out ? 1 : 0;
+        if (!out) {
+            acc2[0] += ss;
+            acc2[1] += 1;
+        }
+    }
+    wg_sum<2>(acc2, reinterpret_cast<double(*)[2]>(red), sum);
+    if (tid == 0) {
+        p.mean_sq[pr] = (float)(sum[0] / sum[1]);
+        // GetPose (BundlerLib.cpp:457-465): t as float, R of the normalised quaternion as float
+        double q[4] = {cur_q[0], cur_q[1], cur_q[2], cur_q[3]};
+        const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        for (int k = 0; k < 4; k++) q[k] /= n;
+        double R[9];
+        d_qmat(q, R);
+        for (int k = 0; k < 3; k++) p.pos3_out[3 * pr + k] = (float)cur_t[k];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) p.r9_out[9 * pr + c * 3 + r] = (float)R[r * 3 + c];
+        if (p.qt7_out) {
+            for (int k = 0; k < 4; k++) p.qt7_out[7 * pr + k] = cur_q[k];
+            for (int k = 0; k < 3; k++) p.qt7_out[7 * pr + 4 + k] = cur_t[k];
+        }
+        if (p.stats) {
+            p.stats[2 * pr] = iters;
+            p.stats[2 * pr + 1] = trials;
+        }
+    }
+}
+
+struct PoseScratch {
+    DeviceBuffer buf;
+    hipStream_t st = nullptr;
+};
+PoseScratch g_pose[16];
+
+mage_status pose_launch(const PoseParams& p, uint32_t problems, hipStream_t st)
+{
+    if (problems == 0) return MAGE_OK;
+    launch("ba.pose_batch", pose_ba_kernel, dim3(problems), dim3(PB_THREADS), 0, st, p);
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}
+
+}  // namespace
+}  // namespace mage
+
+extern "C" {
+
+mage_status mage_ba_pose_batch_device(uint32_t problems, const float* d_pos3, const float* d_r9, const float* d_intr4,
+                                      const uint32_t* d_obs_start, const float* d_points3, const float* d_uv,
+                                      const float* d_info, uint32_t nsteps, float huber, float max_error_square,
+                                      float* d_pos3_out, float* d_r9_out, double* d_qt7_out, uint8_t* d_outlier,
+                                      float* d_mean_sq, uint32_t* d_stats, mage_stream stream)
+{
+    using namespace mage;
+    if (problems == 0) return MAGE_OK;
+    MAGE_REQUIRE(d_pos3 && d_r9 && d_intr4 && d_obs_start && d_points3 && d_uv && d_info && d_pos3_out && d_r9_out &&
+                     d_outlier && d_mean_sq,
+                 MAGE_EINVAL, "null buffer");
+    MAGE_REQUIRE(huber >= 0.f, MAGE_EINVAL, "Huber widths must be nonnegative");
+    PoseParams p{d_pos3, d_r9, d_intr4, d_obs_start, d_points3, d_uv, d_info, nsteps, (double)huber,
+                 (double)max_error_square, d_pos3_out, d_r9_out, d_qt7_out, d_outlier, d_mean_sq, d_stats};
+    return pose_launch(p, problems, (hipStream_t)stream);
+}
+
+mage_status mage_ba_pose_batch(uint32_t problems, const float* pos3, const float* r9, const float* intr4,
+                               const uint32_t* obs_start, const float* points3, const float* uv, const float* info,
+                               uint32_t nsteps, float huber, float max_error_square, float* pos3_out, float* r9_out,
+                               double* qt7_out, uint8_t* outlier, float* mean_sq, uint32_t* stats, int device)
+{
+    using namespace mage;
+    if (problems == 0) return MAGE_OK;
+    MAGE_REQUIRE(pos3 && r9 && intr4 && obs_start && pos3_out && r9_out && mean_sq, MAGE_EINVAL, "null argument");
+    MAGE_REQUIRE(obs_start[0] == 0, MAGE_EINVAL, "obs_start[0] must be 0");
+    for (uint32_t k = 0; k < problems; k++)
+        MAGE_REQUIRE(obs_start[k + 1] >= obs_start[k], MAGE_EINVAL, "obs_start must be non-decreasing");
+    const uint32_t E = obs_start[problems];
+    MAGE_REQUIRE(E == 0 || (points3 && uv && info && outlier), MAGE_EINVAL, "null observation arrays");
+    MAGE_REQUIRE(huber >= 0.f, MAGE_EINVAL, "Huber widths must be nonnegative");
+    mage_status r = bind_device(device);
+    if (r != MAGE_OK) return r;
+    PoseScratch& S = g_pose[device & 15];
+    if (!S.st) MAGE_HIP(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t P = problems;
+    const size_t o_pos = 0, o_r9 = al(o_pos + 12 * P), o_in = al(o_r9 + 36 * P), o_os = al(o_in + 16 * P),
+                 o_pt = al(o_os + 4 * (P + 1)), o_uv = al(o_pt + 12ull * E), o_inf = al(o_uv + 8ull * E),
+                 o_pos2 = al(o_inf + 4ull * E), o_r92 = al(o_pos2 + 12 * P), o_qt = al(o_r92 + 36 * P),
+                 o_out = al(o_qt + 56 * P), o_ms = al(o_out + E + 1), o_st = al(o_ms + 4 * P), total = o_st + 8 * P;
+    if ((r = S.buf.reserve(total)) != MAGE_OK) return r;
+    char* b = S.buf.as<char>();
+    auto up = [&](size_t off, const void* src, size_t n) -> mage_status {
+        if (n) MAGE_HIP(hipMemcpyAsync(b + off, src, n, hipMemcpyHostToDevice, S.st));
+        return MAGE_OK;
+    };
+    if ((r = up(o_pos, pos3, 12 * P)) != MAGE_OK || (r = up(o_r9, r9, 36 * P)) != MAGE_OK ||
+        (r = up(o_in, intr4, 16 * P)) != MAGE_OK || (r = up(o_os, obs_start, 4 * (P + 1))) != MAGE_OK ||
+        (r = up(o_pt, points3, 12ull * E)) != MAGE_OK || (r = up(o_uv, uv, 8ull * E)) != MAGE_OK ||
+        (r = up(o_inf, info, 4ull * E)) != MAGE_OK)
+        return r;
+    PoseParams p{reinterpret_cast<const float*>(b + o_pos), reinterpret_cast<const float*>(b + o_r9),
+                 reinterpret_cast<const float*>(b + o_in), reinterpret_cast<const uint32_t*>(b + o_os),
+                 reinterpret_cast<const float*>(b + o_pt), reinterpret_cast<const float*>(b + o_uv),
+                 reinterpret_cast<const float*>(b + o_inf), nsteps, (double)huber, (double)max_error_square,
+                 reinterpret_cast<float*>(b + o_pos2), reinterpret_cast<float*>(b + o_r92),
+                 reinterpret_cast<double*>(b + o_qt), reinterpret_cast<uint8_t*>(b + o_out),
+                 reinterpret_cast<float*>(b + o_ms), reinterpret_cast<uint32_t*>(b + o_st)};
+    if ((r = pose_launch(p, problems, S.st)) != MAGE_OK) return r;
+    MAGE_HIP(hipMemcpyAsync(pos3_out, b + o_pos2, 12 * P, hipMemcpyDeviceToHost, S.st));
+    MAGE_HIP(hipMemcpyAsync(r9_out, b + o_r92, 36 * P, hipMemcpyDeviceToHost, S.st));
+    MAGE_HIP(hipMemcpyAsync(mean_sq, b + o_ms, 4 * P, hipMemcpyDeviceToHost, S.st));
+    if (E) MAGE_HIP(hipMemcpyAsync(outlier, b + o_out, E, hipMemcpyDeviceToHost, S.st));
+    if (qt7_out) MAGE_HIP(hipMemcpyAsync(qt7_out, b + o_qt, 56 * P, hipMemcpyDeviceToHost, S.st));
+    if (stats) MAGE_HIP(hipMemcpyAsync(stats, b + o_st, 8 * P, hipMemcpyDeviceToHost, S.st));
+    MAGE_HIP(hipStreamSynchronize(S.st));
+    return MAGE_OK;
+}
+
+}  // extern "C"

@@ -275,3 +275,67 @@ def bow_tree(train: np.ndarray, levels: int = 2, branching: int = 6, max_iter: i
     child_start[1:] = np.cumsum([len(k) for k in kids])
     children = np.array([c for k in kids for c in k], np.uint32)
     return np.stack(nodes).astype(np.uint8), child_start, children
+
+
+@dataclass
+class PoseBatch:
+    """Independent pose-only problems (TrackLocalMap::OptimizeCameraPose inputs, TrackLocalMap.cpp:
+    421-501): one camera each, observations obs_start[k] .. obs_start[k+1]-1 on fixed map points."""
+    pos: np.ndarray  # (K, 3) f32 view-space t
+    r9: np.ndarray  # (K, 9) f32 column-major R
+    intr: np.ndarray  # (K, 4) f32 {cx, cy, fx, fy}
+    obs_start: np.ndarray  # (K + 1,) u32
+    points: np.ndarray  # (E, 3) f32
+    uv: np.ndarray  # (E, 2) f32
+    info: np.ndarray  # (E,) f32
+    true_pos: np.ndarray
+    true_rot: np.ndarray
+
+
+def pose_batch(problems: int = 256, obs: int = 600, seed: int = BA_SEED + 1, noise_px: float = 0.5,
+               outlier_frac: float = 0.05, vary: bool = True) -> PoseBatch:
+    """K frames of a 720p camera (fx = fy = 900) tracking map points 3-10 m ahead: observation =
+    projection + N(0, noise_px) with outlier_frac offset by U(10, 40) px; initial pose = the true
+    one perturbed by N(0, 0.5 deg) per axis and N(0, 0.02) in translation (a motion-model
+    prediction); refinement counts 0..5.  With `vary`, per-problem observation counts vary."""
+    rng = np.random.default_rng(seed)
+    f, cx, cy = 900.0, 640.0, 360.0
+    counts = rng.integers(max(obs // 2, 1), obs + obs // 2 + 1, problems) if vary else np.full(problems, obs)
+    obs_start = np.zeros(problems + 1, np.uint32)
+    obs_start[1:] = np.cumsum(counts)
+    E = int(obs_start[-1])
+    pos = np.zeros((problems, 3))
+    r9 = np.zeros((problems, 9))
+    true_pos = np.zeros((problems, 3))
+    true_rot = np.zeros((problems, 3, 3))
+    pts = np.zeros((E, 3))
+    uv = np.zeros((E, 2))
+    for k in range(problems):
+        R = _rot(rng.uniform(-0.5, 0.5), rng.uniform(-0.1, 0.1), rng.uniform(-0.1, 0.1))
+        c = rng.normal(0, 2, 3)
+        t = -R @ c
+        true_pos[k], true_rot[k] = t, R
+        n = int(counts[k])
+        # points in the camera frustum: pixel uniform, depth 3-10 m
+        u = rng.uniform(20, 1260, n)
+        v = rng.uniform(20, 700, n)
+        z = rng.uniform(3, 10, n)
+        Xc = np.stack([(u - cx) / f * z, (v - cy) / f * z, z], axis=1)
+        Xw = (Xc - t) @ R  # R^T (Xc - t)
+        s = slice(int(obs_start[k]), int(obs_start[k + 1]))
+        pts[s] = Xw
+        o = np.stack([u, v], axis=1) + rng.normal(0, noise_px, (n, 2))
+        bad = rng.random(n) < outlier_frac
+        ang = rng.uniform(0, 2 * np.pi, n)
+        mag = rng.uniform(10, 40, n)
+        o[bad] += np.stack([mag * np.cos(ang), mag * np.sin(ang)], axis=1)[bad]
+        uv[s] = o
+        d = np.deg2rad(rng.normal(0, 0.5, 3))
+        R0 = _rot(d[0], d[1], d[2]) @ R
+        pos[k] = t + rng.normal(0, 0.02, 3)
+        r9[k] = R0.T.reshape(9)  # column-major
+    info = refinement_confidence(rng.integers(0, 6, E))
+    intr = np.tile(np.array([cx, cy, f, f], np.float32), (problems, 1))
+    return PoseBatch(pos=pos.astype(np.float32), r9=r9.astype(np.float32), intr=intr, obs_start=obs_start,
+                     points=pts.astype(np.float32), uv=uv.astype(np.float32), info=info, true_pos=true_pos,
+                     true_rot=true_rot)

@@ -1127,3 +1127,46 @@ int oracle_ba_tether_linearization(oracle_ba* b, int i, double err[6], double J1
     memcpy(J2, t->J[1], sizeof(t->J[1]));
     return t->dim;
 }
+
+/* TrackLocalMap::OptimizeCameraPose (TrackLocalMap.cpp:421-501) for a batch of independent
+ * problems, each through a fresh BundlerLib with ArePointsFixed: one free camera, observation i
+ * of problem k on point i, nsteps x huber, then the StepBundleAdjustment post-pass.  Outputs as
+ * mage_ba_pose_batch (outlier flags per observation). */
+void oracle_ba_pose_batch(uint32_t problems, const float* pos3, const float* r9, const float* intr4,
+                          const uint32_t* obs_start, const float* points3, const float* uv, const float* info,
+                          uint32_t nsteps, float huber, float max_error_square, float* pos3_out, float* r9_out,
+                          double* qt7_out, uint8_t* outlier, float* mean_sq, uint32_t* stats)
+{
+    for (uint32_t k = 0; k < problems; k++) {
+        const uint32_t e0 = obs_start[k], n = obs_start[k + 1] - e0;
+        oracle_ba* b = oracle_ba_create(1);
+        const uint8_t nofix = 0;
+        oracle_ba_set_cameras(b, 1, pos3 + 3 * k, r9 + 9 * k, intr4 + 4 * k, &nofix);
+        oracle_ba_set_points(b, (int)n, points3 + 3 * (size_t)e0);
+        uint32_t* cam = (uint32_t*)calloc((size_t)n + 1, sizeof(uint32_t));
+        uint32_t* pt = (uint32_t*)calloc((size_t)n + 1, sizeof(uint32_t));
+        for (uint32_t i = 0; i < n; i++) pt[i] = i;
+        oracle_ba_set_observations(b, (int)n, uv + 2 * (size_t)e0, cam, pt, info + e0);
+        float* hw = (float*)malloc(sizeof(float) * ((size_t)nsteps + 1));
+        for (uint32_t s = 0; s < nsteps; s++) hw[s] = huber;
+        uint32_t* outl = (uint32_t*)calloc((size_t)n + 1, sizeof(uint32_t));
+        uint32_t no = 0;
+        oracle_ba_step(b, hw, (int)nsteps, max_error_square, outl, n, &no, &mean_sq[k]);
+        for (uint32_t i = 0; i < n; i++) outlier[e0 + i] = 0;
+        for (uint32_t i = 0; i < no && i < n; i++) outlier[e0 + outl[i]] = 1;
+        oracle_ba_get_poses(b, pos3_out + 3 * k, r9_out + 9 * k);
+        if (qt7_out) {
+            memcpy(qt7_out + 7 * k, b->cams[0].pose.q, 4 * sizeof(double));
+            memcpy(qt7_out + 7 * k + 4, b->cams[0].pose.t, 3 * sizeof(double));
+        }
+        if (stats) {
+            stats[2 * k] = (uint32_t)b->iters;
+            stats[2 * k + 1] = (uint32_t)b->trials;
+        }
+        free(cam);
+        free(pt);
+        free(hw);
+        free(outl);
+        oracle_ba_destroy(b);
+    }
+}

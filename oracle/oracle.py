@@ -96,6 +96,7 @@ def _declare(L):
     L.oracle_ba_set_observations.argtypes = [vp, i32, vp, vp, vp, vp]
     L.oracle_ba_set_lambda.argtypes = [vp, f32]
     L.oracle_ba_set_tethers.argtypes = [vp, i32, i32, vp, vp, vp, vp]
+    L.oracle_ba_pose_batch.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp]
     L.oracle_bow_find_leaf.argtypes = [vp, vp, vp, vp]
     L.oracle_bow_find_leaf.restype = u32
     L.oracle_indexed_match.argtypes = [vp, vp, vp, vp, u32, vp, vp, u32, vp, i32, i32, vp, u32]
@@ -277,6 +278,22 @@ def indexed_match(tree, desc_a, desc_b, mask_a=None, mask_b=None, max_distance=3
     n = lib().oracle_indexed_match(_p(nd), _p(cs), _p(ch), _p(da), len(da), _p(ma), _p(db), len(db), _p(mb),
                                    int(max_distance), int(min_difference), _p(out), cap)
     return out[:n].copy()
+
+
+def pose_batch(pb, nsteps, huber, max_error_square):
+    """TrackLocalMap::OptimizeCameraPose per problem (fresh BundlerLib, ArePointsFixed); pb is a
+    synth.PoseBatch.  Returns dict(pos, r9, qt7, outlier, mean_sq, stats)."""
+    K = len(pb.pos)
+    E = int(pb.obs_start[-1])
+    out = dict(pos=np.zeros((K, 3), np.float32), r9=np.zeros((K, 9), np.float32), qt7=np.zeros((K, 7)),
+               outlier=np.zeros(max(E, 1), np.uint8), mean_sq=np.zeros(K, np.float32), stats=np.zeros((K, 2), np.uint32))
+    c = lambda a, t: np.ascontiguousarray(a, t)  # noqa: E731
+    lib().oracle_ba_pose_batch(K, _p(c(pb.pos, np.float32)), _p(c(pb.r9, np.float32)), _p(c(pb.intr, np.float32)),
+                               _p(c(pb.obs_start, np.uint32)), _p(c(pb.points, np.float32)), _p(c(pb.uv, np.float32)),
+                               _p(c(pb.info, np.float32)), nsteps, huber, max_error_square, _p(out["pos"]),
+                               _p(out["r9"]), _p(out["qt7"]), _p(out["outlier"]), _p(out["mean_sq"]), _p(out["stats"]))
+    out["outlier"] = out["outlier"][:E]
+    return out
 
 
 class BundlerOracle:

@@ -180,3 +180,63 @@ def tethered_extra_camera():
         true_rot=np.concatenate([g.true_rot, Rx[None]]), true_pos=np.vstack([g.true_pos, tx]))
     g2.extra_tether = np.concatenate([tc, synth.quat_from_rot(Rc)]).astype(np.float32)
     return g2
+
+
+@pytest.mark.parametrize("steps,huber,maxe", [(3, 4.0, 36.0), (4, 0.9, 4.5 ** 2)])
+def test_pose_batch_matches_per_frame_oracle(gpu, steps, huber, maxe):
+    """Batched OptimizeCameraPose (TrackLocalMap.cpp:96-140 settings: 3 x 4.0 / 6^2, then
+    4 x 0.9 / 4.5^2) vs a fresh oracle BundlerLib per frame."""
+    from oracle import oracle as O
+
+    pb = synth.pose_batch(problems=96, obs=500)
+    g = bundler.OptimizeCameraPoses(pb, steps, maxe, huber)
+    o = O.pose_batch(pb, steps, huber, maxe)
+    assert np.array_equal(g["stats"], o["stats"])
+    assert np.array_equal(g["outlier"], o["outlier"])
+    assert np.abs(g["qt7"][:, 4:] - o["qt7"][:, 4:]).max() < POSE_TOL
+    assert quat_angle(g["qt7"][:, :4], o["qt7"][:, :4]).max() < POSE_TOL
+    assert np.allclose(g["mean_sq"], o["mean_sq"], rtol=1e-4)
+    assert np.abs(g["pos"] - o["pos"]).max() < 1e-4 and np.abs(g["r9"] - o["r9"]).max() < 1e-4
+
+
+def test_pose_batch_edges_and_single_problem_path(gpu):
+    """Zero-observation problems (useless optimizer: NaN mean), a one-observation problem, zero
+    steps (post-pass only), and agreement with the general BundlerLib path (ArePointsFixed)."""
+    from oracle import oracle as O
+
+    pb = synth.pose_batch(problems=6, obs=40, vary=False)
+    counts = np.diff(pb.obs_start.astype(np.int64))
+    counts[1] = 0
+    counts[3] = 1
+    starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint32)
+    sel = np.concatenate([np.arange(pb.obs_start[k], pb.obs_start[k] + counts[k]) for k in range(6)]).astype(int)
+    import dataclasses
+
+    pb2 = dataclasses.replace(pb, obs_start=starts, points=pb.points[sel], uv=pb.uv[sel], info=pb.info[sel])
+    for steps in (0, 3):
+        g = bundler.OptimizeCameraPoses(pb2, steps, 36.0, 4.0)
+        o = O.pose_batch(pb2, steps, 4.0, 36.0)
+        assert np.array_equal(g["outlier"], o["outlier"]) and np.array_equal(g["stats"], o["stats"])
+        assert np.isnan(g["mean_sq"][1]) and np.isnan(o["mean_sq"][1])
+        ok = ~np.isnan(o["mean_sq"])
+        assert np.allclose(g["mean_sq"][ok], o["mean_sq"][ok], rtol=1e-4)
+        assert np.abs(g["qt7"] - o["qt7"]).max() < POSE_TOL
+    # the same problem through the general C-ABI BundlerLib (points fixed) gives the same pose
+    k = 0
+    s = slice(int(pb.obs_start[k]), int(pb.obs_start[k + 1]))
+    b = bundler.BundlerLib(bundler.BundlerParameters(True))
+    b.AllocateCameras(1)
+    b.SetCameraPose(0, pb.pos[k], pb.r9[k].reshape(3, 3).T, pb.intr[k], False)
+    n = s.stop - s.start
+    b.AllocateMapPoints(n)
+    b.AllocateObservations(n)
+    for i in range(n):
+        b.SetMapPoint(i, pb.points[s][i])
+        b.SetObservation(i, pb.uv[s][i], 0, i, float(pb.info[s][i]))
+    outl = []
+    ms = b.StepBundleAdjustment([4.0] * 3, 36.0, outl)
+    g = bundler.OptimizeCameraPoses(pb, 3, 36.0, 4.0)
+    qt, _ = b.state()
+    assert np.abs(qt[0, 4:] - g["qt7"][0, 4:]).max() < POSE_TOL
+    assert list(np.nonzero(g["outlier"][s])[0]) == outl
+    assert abs(ms - g["mean_sq"][0]) <= 1e-4 * abs(ms)

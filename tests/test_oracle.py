@@ -566,3 +566,16 @@ def test_indexed_match_semantics(oracle):
     assert all(r["query_idx"] != 2 for r in oracle.indexed_match(tree, A, B, max_distance=19, min_difference=0))
     # empty mask -> 0 matches
     assert len(oracle.indexed_match(tree, A, B, mask_a=np.zeros(3, np.uint8))) == 0
+
+
+def test_pose_batch_oracle_converges(oracle):
+    """The batched pose-only oracle (fresh BundlerLib per frame, TrackLocalMap.cpp:421-501) recovers
+    the true poses and flags the planted outliers."""
+    from mageslam_amd import synth
+
+    pb = synth.pose_batch(problems=16, obs=300, outlier_frac=0.05)
+    r = oracle.pose_batch(pb, 3, 4.0, 36.0)
+    r = oracle.pose_batch(pb, 4, 0.9, 4.5 ** 2)
+    assert np.abs(r["qt7"][:, 4:] - pb.true_pos).max() < 0.01
+    assert (r["stats"][:, 0] >= 1).all()
+    assert 0.02 < r["outlier"].mean() < 0.1
