@@ -150,6 +150,27 @@ mage_status mage_undistort_keypoints_batch_device(const mage_calibration* distor
                                                   int64_t pitch, const uint32_t* d_n, uint32_t batch,
                                                   mage_stream stream);
 
+/* Frame undistortion — ImagePreprocessor::UndistortImage (ImagePreprocessor.cpp:71-120).  Create
+ * once per (calibration, size): CalculateUndistortedCalibration (fx, fy kept, principal point at
+ * the image centre; written to *undistorted if not NULL) and cv::initUndistortRectifyMap(K, dist,
+ * noArray(), K', size, CV_32FC1) on the device.  Each frame: cv::remap(INTER_LINEAR,
+ * BORDER_CONSTANT 0) of a width x height 8-bit image.  ndist must be 0, 4, 5 or 8.
+ * Frames arrive as GRAYSCALE8 or as the Y plane of NV12 (CreateGrayCVMat, Utils/cv.cpp:8-28): the
+ * stride / pitch arguments read either layout in place. */
+typedef struct mage_undistorter mage_undistorter;
+mage_status mage_undistorter_create(const mage_calibration* distorted, int32_t width, int32_t height, int device,
+                                    mage_undistorter** out, mage_calibration* undistorted);
+mage_status mage_undistorter_destroy(mage_undistorter* u);
+/* The CV_32FC1 maps (map1 = x, map2 = y), width*height floats each, for tests. */
+mage_status mage_undistorter_get_maps(mage_undistorter* u, float* mapx, float* mapy);
+/* Host buffers, synchronous. */
+mage_status mage_undistort_image(mage_undistorter* u, const uint8_t* src, int32_t src_stride, uint8_t* dst,
+                                 int32_t dst_stride);
+/* Batched device form: frame f at d_src + f*src_pitch -> d_dst + f*dst_pitch.  Asynchronous. */
+mage_status mage_undistort_image_batch_device(mage_undistorter* u, const uint8_t* d_src, int32_t src_stride,
+                                              int64_t src_pitch, uint8_t* d_dst, int32_t dst_stride, int64_t dst_pitch,
+                                              uint32_t batch, mage_stream stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Hamming matching — replaces FeatureMatcher (Core/.../Source/Tracking/FeatureMatcher.h)        */
 /* ------------------------------------------------------------------------------------------ */

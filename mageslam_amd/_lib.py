@@ -24,6 +24,8 @@ EXPORTS = [
     "mage_orb_detect_and_compute_batch_device", "mage_orb_status", "mage_orb_reset_status",
     "mage_synth_frames_device", "mage_orb_fast_score_map",
     "mage_undistort_keypoints", "mage_undistort_keypoints_batch_device",
+    "mage_undistorter_create", "mage_undistorter_destroy", "mage_undistorter_get_maps", "mage_undistort_image",
+    "mage_undistort_image_batch_device",
     "mage_hamming_distance", "mage_hamming_match", "mage_hamming_match_batch_device",
     "mage_radius_match", "mage_radius_match_batch_device",
     "mage_bow_create", "mage_bow_destroy", "mage_bow_find_leaves", "mage_bow_find_leaves_device",
@@ -146,6 +148,11 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_orb_fast_score_map", st, vp, i32, i32, i32, i32, vp, C.c_int)
     sig("mage_undistort_keypoints", st, vp, vp, vp, u32, C.c_int)
     sig("mage_undistort_keypoints_batch_device", st, vp, vp, vp, i64, vp, u32, vp)
+    sig("mage_undistorter_create", st, vp, i32, i32, C.c_int, C.POINTER(vp), vp)
+    sig("mage_undistorter_destroy", st, vp)
+    sig("mage_undistorter_get_maps", st, vp, vp, vp)
+    sig("mage_undistort_image", st, vp, vp, i32, vp, i32)
+    sig("mage_undistort_image_batch_device", st, vp, vp, i32, i64, vp, i32, i64, u32, vp)
     sig("mage_hamming_distance", i32, vp, vp)
     sig("mage_hamming_match", st, vp, u32, vp, vp, u32, vp, i32, i32, vp, u32, C.POINTER(u32))
     sig("mage_hamming_match_batch_device", st, vp, i64, vp, vp, i64, vp, u32, i32, i32, vp, u32, vp, vp)

@@ -96,6 +96,8 @@ def _declare(L):
     L.oracle_ba_set_observations.argtypes = [vp, i32, vp, vp, vp, vp]
     L.oracle_ba_set_lambda.argtypes = [vp, f32]
     L.oracle_ba_set_tethers.argtypes = [vp, i32, i32, vp, vp, vp, vp]
+    L.oracle_undistort_map.argtypes = [vp, vp, i32, vp, i32, i32, vp, vp]
+    L.oracle_remap_linear.argtypes = [vp, i32, i32, i32, vp, vp, i32, i32, vp, i32]
     L.oracle_ba_pose_batch.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp]
     L.oracle_bow_find_leaf.argtypes = [vp, vp, vp, vp]
     L.oracle_bow_find_leaf.restype = u32
@@ -256,6 +258,22 @@ def match(desc_a, desc_b, mask_a=None, mask_b=None, max_distance=30, min_differe
     n = lib().oracle_match(_p(da), len(da), _p(ma), _p(db), len(db), _p(mb), max_distance,
                            min_difference, _p(out), cap)
     return out[:n].copy()
+
+
+def undistort_image(img, k_dist, dist):
+    """ImagePreprocessor::UndistortImage (ImagePreprocessor.cpp:71-120): k_dist = (fx, fy, cx, cy),
+    dist = OpenCV-ordered coefficients (0, 4, 5 or 8).  Returns (undistorted image, mapx, mapy, K')."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    kd = np.ascontiguousarray(k_dist, np.float32)
+    kn = np.array([kd[0], kd[1], np.float32(w) * np.float32(0.5), np.float32(h) * np.float32(0.5)], np.float32)
+    dd = np.ascontiguousarray(dist, np.float32)
+    mx = np.zeros((h, w), np.float32)
+    my = np.zeros((h, w), np.float32)
+    lib().oracle_undistort_map(_p(kd), _p(dd), len(dd), _p(kn), w, h, _p(mx), _p(my))
+    out = np.zeros((h, w), np.uint8)
+    lib().oracle_remap_linear(_p(img), w, h, w, _p(mx), _p(my), w, h, _p(out), w)
+    return out, mx, my, kn
 
 
 def bow_find_leaves(tree, desc):

@@ -579,3 +579,37 @@ def test_pose_batch_oracle_converges(oracle):
     assert np.abs(r["qt7"][:, 4:] - pb.true_pos).max() < 0.01
     assert (r["stats"][:, 0] >= 1).all()
     assert 0.02 < r["outlier"].mean() < 0.1
+
+
+def test_undistort_image_pure_shift(oracle):
+    """With no distortion the map is a translation by (cx - w/2, cy - h/2): an integer offset moves
+    the frame exactly (the remap table's saturated (0, 0) entry cannot change a pixel), with the
+    constant-0 border outside (ImagePreprocessor.cpp:71-120)."""
+    from mageslam_amd import synth
+
+    img = synth.frame(2, 160, 120)
+    out, mx, my, kn = oracle.undistort_image(img, (200.0, 210.0, 80.0 + 3, 60.0 - 2), np.zeros(5, np.float32))
+    assert kn[2] == 80.0 and kn[3] == 60.0
+    # the inverse of K' carries rounding (cv::invert's cofactors / det): maps are ~integers
+    assert np.allclose(mx[0, :4], [3, 4, 5, 6], atol=1e-5) and np.allclose(my[:3, 0], [-2, -1, 0], atol=1e-5)
+    ref = np.zeros_like(img)
+    ref[2:, :-3] = img[:-2, 3:]
+    assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("dist", [[-0.28, 0.07, 0.001, -0.0005, 0.0],
+                                  [0.9, -0.3, 0.0007, 0.0002, 0.02, 1.2, -0.2, 0.05]])
+def test_undistort_map_inverts_points(oracle, dist):
+    """initUndistortRectifyMap sends undistorted pixel p to a distorted position q; undistortPoints
+    (the keypoint path, OrbFeatureDetector.cpp:30-62) maps q back to p (two independent
+    restatements of OpenCV's model agree to its 5 fixed-point iterations)."""
+    from mageslam_amd import synth
+
+    img = synth.frame(0, 200, 150)
+    kd = np.float32([180.0, 185.0, 97.5, 77.0])
+    out, mx, my, kn = oracle.undistort_image(img, kd, np.float32(dist))
+    ys, xs = np.mgrid[20:130:11, 20:180:13]
+    q = np.stack([mx[ys, xs].ravel(), my[ys, xs].ravel()], 1).astype(np.float32)
+    back = oracle.undistort_points(q, kd, np.float32(dist), kn)
+    err = np.hypot(back[:, 0] - xs.ravel(), back[:, 1] - ys.ravel())
+    assert err.max() < 0.05, err.max()
