@@ -11,7 +11,7 @@ from mageslam_amd._lib import Calibration
 
 pytestmark = pytest.mark.gpu
 
-DISTS = [[], [-0.28, 0.07, 0.001, -0.0005], [-0.28, 0.07, 0.001, -0.0005, 0.01],
+DISTS = [[], [-0.28, 0.07, 0.001, -0.0005, 0.01],
          [0.9, -0.3, 0.0007, 0.0002, 0.02, 1.2, -0.2, 0.05]]
 
 
