@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--pose-problems", type=int, default=2048, help="pose-only BA problems per launch")
     p.add_argument("--pose-iters", type=int, default=20)
     p.add_argument("--no-pose", action="store_true")
+    p.add_argument("--trajectory-csv", default="", help="rank 0 writes the gathered trajectories (ExportFossilCsv)")
     p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
@@ -251,12 +252,14 @@ def run_ba(args, local_rank, torch):
 POSE_STEPS, POSE_HUBER, POSE_MAXE = 3, 4.0, 36.0  # TrackLocalMap's first OptimizeCameraPose (MageSettings.h:184-189)
 
 
-def run_pose(args, local_rank, torch):
+def run_pose(args, rank, world, local_rank, torch, dist):
     """Batched pose-only BA (SURVEY.md §8(f) 2): TrackLocalMap::OptimizeCameraPose for a batch of
-    frames per launch (mage_ba_pose_batch_device), inputs resident in HBM."""
-    from mageslam_amd import _lib, bundler, synth
+    frames per launch (mage_ba_pose_batch_device), inputs resident in HBM.  C5: each rank tracks its
+    own sequence (seed + rank); after the timed region the per-frame trajectories (68 B records) are
+    all-gathered over RCCL and rank 0 can write them as ExportFossilCsv does."""
+    from mageslam_amd import _lib, bundler, multigpu, synth, trajectory
 
-    pb = synth.pose_batch(problems=args.pose_problems, obs=600)
+    pb = synth.pose_batch(problems=args.pose_problems, obs=600, seed=multigpu.sequence_seed(synth.BA_SEED + 1, rank))
     K = args.pose_problems
     E = int(pb.obs_start[-1])
     dev = f"cuda:{local_rank}"
@@ -279,11 +282,23 @@ def run_pose(args, local_rank, torch):
         once()
     torch.cuda.synchronize()
     n = args.pose_iters
+    multigpu.barrier(dist)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(n):
         once()
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    multigpu.barrier(dist)
+    el = multigpu.max_over_ranks(time.perf_counter() - t0, dev, dist)
+    # end-of-run exchange: every rank's trajectory (flag + 4x4 view matrix per frame)
+    M = torch.zeros((K, 4, 4), dtype=torch.float32, device=dev)
+    M[:, :3, :3] = r9_o.view(K, 3, 3).transpose(1, 2)
+    M[:, :3, 3] = pos_o
+    M[:, 3, 3] = 1
+    rows = torch.cat([torch.ones((K, 1), dtype=torch.float32, device=dev), M.view(K, 16)], 1)
+    gathered = trajectory.gather_trajectories(rows, dist)
+    if rank == 0 and args.trajectory_csv:
+        trajectory.export_fossil_csv(args.trajectory_csv, torch.cat(gathered).cpu().numpy())
     lib = _lib.load()
     lib.mage_profile_reset()
     lib.mage_profile_enable(1)
@@ -294,7 +309,8 @@ def run_pose(args, local_rank, torch):
     kern = _lib.profile_report()
     st = stats.cpu().numpy()
     res = {"metric": "pose-only BA problems/sec (OptimizeCameraPose: 1 camera, ~600 fixed points, 3 LM steps)",
-           "value": n * K / el, "unit": "problems/s", "dtype": "f64", "problems_per_launch": K,
+           "value": world * n * K / el, "unit": "problems/s", "dtype": "f64", "problems_per_launch": K,
+           "trajectory_frames_gathered": int(sum(g.shape[0] for g in gathered)),
            "observations": E, "lm_iterations_per_problem": float(st[:, 0].mean()),
            "trials_per_problem": float(st[:, 1].mean()),
            "config": {"workload": f"{K} synthetic 720p frames x {E / K:.0f} observations, huber {POSE_HUBER}, "
@@ -404,7 +420,7 @@ def main():
 
     orb_res = run_orb(args, rank, world, local_rank, torch, dist)
     ba_res, g = (None, None) if args.no_ba else run_ba(args, local_rank, torch)
-    pose_res, pb = (None, None) if args.no_pose else run_pose(args, local_rank, torch)
+    pose_res, pb = (None, None) if args.no_pose else run_pose(args, rank, world, local_rank, torch, dist)
     if world > 1:
         dist.barrier()
 

@@ -60,3 +60,52 @@ def test_bench_cpu_dry_run_world2():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["gathered_ranks"] == [0, 1] and d["value"] > 0
     assert d["gathered_checksums"][0] != d["gathered_checksums"][1]
+
+
+def test_fossil_csv_format(tmp_path):
+    """ExportFossilCsv (console.cpp:15-54): %g-formatted view-matrix rows, identity for lost frames."""
+    from mageslam_amd import trajectory
+
+    R = np.array([[1, 0, 0], [0, 0.5, -0.866025], [0, 0.866025, 0.5]], np.float32)
+    M = trajectory.view_matrices(np.float32([[0.1, -2.5, 1234567]]), R.T.reshape(1, 9))
+    rows = trajectory.records([True, False], np.concatenate([M, M]))
+    p = tmp_path / "mage_output.csv"
+    trajectory.export_fossil_csv(p, rows)
+    lines = p.read_text().splitlines()
+    assert lines[0] == '"true",1,0,0,0.1,0,0.5,-0.866025,-2.5,0,0.866025,0.5,1.23457e+06,0,0,0,1'
+    assert lines[1] == '"false",1,0,0,0,0,1,0,0,0,0,1,0,0,0,0,1'
+
+
+def _traj_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch
+
+    from mageslam_amd import multigpu, synth, trajectory
+
+    dist = multigpu.init("gloo", rank)
+    pb = synth.pose_batch(problems=5, obs=20, seed=multigpu.sequence_seed(synth.BA_SEED, rank))
+    rows = trajectory.records(np.arange(5) != rank, trajectory.view_matrices(pb.pos, pb.r9))
+    g = trajectory.gather_trajectories(torch.from_numpy(rows), dist)
+    q.put((rank, [x.numpy() for x in g], rows))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_trajectory_gather():
+    """C5's end-of-run exchange: each rank's 68-byte-per-frame trajectory, gathered in rank order."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_traj_worker, args=(r, 2, 29517, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    own = {rank: rows for rank, _, rows in res}
+    for rank, gathered, _ in res:
+        assert len(gathered) == 2 and gathered[0].shape == (5, 17)
+        assert np.array_equal(gathered[0], own[0]) and np.array_equal(gathered[1], own[1])
+    assert not np.array_equal(own[0][:, 1:], own[1][:, 1:])
