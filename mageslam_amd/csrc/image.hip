@@ -7,15 +7,21 @@
 //   undistort_map_kernel  once per calibration: thread per row, the row-sequential accumulation
 //                         _x += ir[0] ... of OpenCV 3.4.0 in fp64 (built with -ffp-contract=off:
 //                         bit-exact maps), written as the two CV_32FC1 planes
-//   remap_linear_kernel   per batch of frames: thread per 4 output pixels (one dword store), the
-//                         maps read as float4 (coalesced, 32 B per thread), X = rint(u * 32): the
-//                         short integer part and the 5+5-bit fraction index of remap's fixed-point
-//                         path, initInterTab2D's bilinear weights (x 32768, the saturated (0,0) entry
-//                         included), (sum + 2^14) >> 15; constant-0 border as remapBilinear treats
-//                         outliers.  HBM-bound: 8 B of map + 1 B out per pixel, the source taps hit
-//                         L2 (the map is shared by every frame of the batch).
+//   remap_boxes_kernel    once per calibration: per 64x16 output tile, the bounding box of its
+//                         in-range source taps
+//   remap_linear_kernel   per batch of frames: workgroup per 64x16 tile x 64 frames, thread per 4
+//                         output pixels.  The maps are read once as float4 (coalesced) and kept as
+//                         register coefficients: X = rint(u * 32) -> the short integer part and the
+//                         5+5-bit fraction index of remap's fixed-point path, initInterTab2D's
+//                         bilinear weights (x 32768, the saturated (0,0) entry included).  Per frame
+//                         the tile's source box is staged in LDS with dword loads and the 4 taps of
+//                         each pixel are LDS byte reads; (sum + 2^14) >> 15, one dword store;
+//                         constant-0 border as remapBilinear treats outliers.  HBM-bound: ~2 B per
+//                         pixel and frame (box in, pixel out) + the map / 64.  The box of frame f + 1
+//                         is loaded into registers while frame f is computed (LDS double buffer).
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
 
 #include "common.hpp"
@@ -25,6 +31,7 @@ struct mage_undistorter {
     int width = 0, height = 0;
     mage_calibration undistorted{};
     mage::DeviceBuffer maps;     // [mapx (W*H floats)][mapy (W*H floats)]
+    mage::DeviceBuffer boxes;    // per 64x16 output tile: the source box staged in LDS (int4)
     mage::DeviceBuffer scratch;  // host-path frames
     hipStream_t st = nullptr;
 };
@@ -74,63 +81,218 @@ struct RemapParams {
     long long dpitch;
 };
 
-__device__ __forceinline__ unsigned remap_px(const uint8_t* __restrict__ S0, int sw, int sh, int sstride, float fu,
-                                             float fv)
+// One output pixel's remap coefficients: the map-dependent part, shared by every frame.
+struct RemapTap {
+    int sx, sy;  // integer source position (short range)
+    int w0, w1, w2, w3;
+    int mode;  // 0: inlier 2x2 block, 1: outlier with some taps inside, 2: entirely outside
+};
+
+__device__ __forceinline__ RemapTap remap_tap(int sw, int sh, float fu, float fv)
 {
+    RemapTap t;
     const int X = __float2int_rn(fu * 32.0f), Y = __float2int_rn(fv * 32.0f);
-    const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
+    t.sx = min(max(X >> 5, -32768), 32767);
+    t.sy = min(max(Y >> 5, -32768), 32767);
     const int tx = X & 31, ty = Y & 31;
-    int w0 = (32 - ty) * (32 - tx) * 32, w1 = (32 - ty) * tx * 32, w2 = ty * (32 - tx) * 32, w3 = ty * tx * 32;
+    t.w0 = (32 - ty) * (32 - tx) * 32;
+    t.w1 = (32 - ty) * tx * 32;
+    t.w2 = ty * (32 - tx) * 32;
+    t.w3 = ty * tx * 32;
     if ((tx | ty) == 0) {  // initInterTab2D: saturate_cast<short>(32768.f) = 32767, fix-up +1 on entry 3
-        w0 = 32767;
-        w3 = 1;
+        t.w0 = 32767;
+        t.w3 = 1;
     }
+    if ((unsigned)t.sx < (unsigned)max(sw - 1, 0) && (unsigned)t.sy < (unsigned)max(sh - 1, 0)) t.mode = 0;
+    else if (t.sx >= sw || t.sx + 1 < 0 || t.sy >= sh || t.sy + 1 < 0) t.mode = 2;
+    else t.mode = 1;
+    return t;
+}
+
+__device__ __forceinline__ unsigned remap_apply(const RemapTap& t, const uint8_t* __restrict__ S0, int sw, int sh,
+                                                int sstride)
+{
     int v0, v1, v2, v3;
-    if ((unsigned)sx < (unsigned)max(sw - 1, 0) && (unsigned)sy < (unsigned)max(sh - 1, 0)) {
-        const uint8_t* S = S0 + (long long)sy * sstride + sx;
+    if (t.mode == 0) {
+        const uint8_t* S = S0 + (long long)t.sy * sstride + t.sx;
         v0 = S[0];
         v1 = S[1];
         v2 = S[sstride];
         v3 = S[sstride + 1];
-    } else if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) {
+    } else if (t.mode == 2) {
         return 0;
     } else {
-        const bool x0 = sx >= 0 && sx < sw, x1 = sx + 1 >= 0 && sx + 1 < sw;
-        const bool y0 = sy >= 0 && sy < sh, y1 = sy + 1 >= 0 && sy + 1 < sh;
-        v0 = x0 && y0 ? S0[(long long)sy * sstride + sx] : 0;
-        v1 = x1 && y0 ? S0[(long long)sy * sstride + sx + 1] : 0;
-        v2 = x0 && y1 ? S0[(long long)(sy + 1) * sstride + sx] : 0;
-        v3 = x1 && y1 ? S0[(long long)(sy + 1) * sstride + sx + 1] : 0;
+        const bool x0 = t.sx >= 0 && t.sx < sw, x1 = t.sx + 1 >= 0 && t.sx + 1 < sw;
+        const bool y0 = t.sy >= 0 && t.sy < sh, y1 = t.sy + 1 >= 0 && t.sy + 1 < sh;
+        v0 = x0 && y0 ? S0[(long long)t.sy * sstride + t.sx] : 0;
+        v1 = x1 && y0 ? S0[(long long)t.sy * sstride + t.sx + 1] : 0;
+        v2 = x0 && y1 ? S0[(long long)(t.sy + 1) * sstride + t.sx] : 0;
+        v3 = x1 && y1 ? S0[(long long)(t.sy + 1) * sstride + t.sx + 1] : 0;
     }
-    const int r = (v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3 + (1 << 14)) >> 15;
+    const int r = (v0 * t.w0 + v1 * t.w1 + v2 * t.w2 + v3 * t.w3 + (1 << 14)) >> 15;
     return (unsigned)min(max(r, 0), 255);
 }
 
-__global__ __launch_bounds__(256) void remap_linear_kernel(RemapParams p)
+// Output tiles of 64 x 16 pixels: 256 threads x 4 consecutive pixels.  Each tile's source taps
+// fall in a small box (the map is smooth); the box is computed once per calibration and, per frame,
+// staged into LDS with dword loads, so the 4 taps per pixel are LDS byte reads instead of four
+// scattered global byte loads.  Tiles whose box exceeds RM_BOX_BYTES read taps from global memory.
+constexpr int RM_TW = 64, RM_TH = 16;
+constexpr int RM_BOX_BYTES = 8192;
+// Frames per workgroup: the map (8 B per pixel) is read once per RM_FRAMES frames and its
+// coefficients stay in registers.
+constexpr int RM_FRAMES = 64;
+
+// Per tile: (x0 aligned down to 4, y0, padded width (multiple of 4), height) of the box holding every
+// in-range tap; width -1 = global fallback, 0 = no in-range tap.
+__global__ __launch_bounds__(256) void remap_boxes_kernel(const float* __restrict__ mapx, const float* __restrict__ mapy,
+                                                          int w, int h, int4* __restrict__ boxes)
 {
-    const int qx = blockIdx.x * 256 + threadIdx.x;  // group of 4 output pixels
-    const int y = blockIdx.y, f = blockIdx.z;
-    const int x0 = qx * 4;
-    if (x0 >= p.dw) return;
-    const uint8_t* S0 = p.src + f * p.spitch;
-    uint8_t* D = p.dst + f * p.dpitch + (long long)y * p.dstride;
+    __shared__ int bx0, bx1, by0, by1;
+    if (threadIdx.x == 0) {
+        bx0 = by0 = INT_MAX;
+        bx1 = by1 = INT_MIN;
+    }
+    __syncthreads();
+    const int x = blockIdx.x * RM_TW + (threadIdx.x % (RM_TW / 4)) * 4, y = blockIdx.y * RM_TH + threadIdx.x / (RM_TW / 4);
+    int lx0 = INT_MAX, lx1 = INT_MIN, ly0 = INT_MAX, ly1 = INT_MIN;
+    if (y < h)
+        for (int k = 0; k < 4 && x + k < w; k++) {
+            const RemapTap t = remap_tap(w, h, mapx[(long long)y * w + x + k], mapy[(long long)y * w + x + k]);
+            if (t.mode == 2) continue;
+            for (int dy = 0; dy < 2; dy++)
+                for (int dx = 0; dx < 2; dx++) {
+                    const int sx = t.sx + dx, sy = t.sy + dy;
+                    if (sx < 0 || sx >= w || sy < 0 || sy >= h) continue;
+                    lx0 = min(lx0, sx);
+                    lx1 = max(lx1, sx);
+                    ly0 = min(ly0, sy);
+                    ly1 = max(ly1, sy);
+                }
+        }
+    atomicMin(&bx0, lx0);
+    atomicMax(&bx1, lx1);
+    atomicMin(&by0, ly0);
+    atomicMax(&by1, ly1);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    int4 b = make_int4(0, 0, 0, 0);
+    if (bx1 >= bx0) {
+        const int xa = bx0 & ~3, wp = ((bx1 + 1 - xa) + 3) & ~3, hh = by1 - by0 + 1;
+        b = make_int4(xa, by0, wp * hh <= RM_BOX_BYTES ? wp : -1, hh);
+    }
+    boxes[blockIdx.y * gridDim.x + blockIdx.x] = b;
+}
+
+__global__ __launch_bounds__(256) void remap_linear_kernel(RemapParams p, const int4* __restrict__ boxes, int batch,
+                                                           int aligned)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t box[2 * RM_BOX_BYTES];  // double buffered
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * RM_TW + (tid % (RM_TW / 4)) * 4, y = blockIdx.y * RM_TH + tid / (RM_TW / 4);
+    const int f0 = blockIdx.z * RM_FRAMES, nf = min(RM_FRAMES, batch - f0);
+    const int4 bb = boxes[blockIdx.y * gridDim.x + blockIdx.x];
+    const bool live = x0 < p.dw && y < p.dh;
+    const int npx = live ? min(4, p.dw - x0) : 0;
     const long long m = (long long)y * p.dw + x0;
-    if (x0 + 4 <= p.dw && (m & 3) == 0) {
+    RemapTap t[4];
+    if (npx == 4 && (m & 3) == 0) {
         const float4 u = *reinterpret_cast<const float4*>(p.mapx + m);
         const float4 v = *reinterpret_cast<const float4*>(p.mapy + m);
-        const unsigned r = remap_px(S0, p.sw, p.sh, p.sstride, u.x, v.x) |
-                           remap_px(S0, p.sw, p.sh, p.sstride, u.y, v.y) << 8 |
-                           remap_px(S0, p.sw, p.sh, p.sstride, u.z, v.z) << 16 |
-                           remap_px(S0, p.sw, p.sh, p.sstride, u.w, v.w) << 24;
-        if ((reinterpret_cast<uintptr_t>(D + x0) & 3) == 0) {
-            *reinterpret_cast<unsigned*>(D + x0) = r;
-            return;
-        }
-        for (int k = 0; k < 4; k++) D[x0 + k] = (uint8_t)(r >> (8 * k));
-        return;
+        t[0] = remap_tap(p.sw, p.sh, u.x, v.x);
+        t[1] = remap_tap(p.sw, p.sh, u.y, v.y);
+        t[2] = remap_tap(p.sw, p.sh, u.z, v.z);
+        t[3] = remap_tap(p.sw, p.sh, u.w, v.w);
+    } else {
+        for (int k = 0; k < 4; k++)
+            t[k] = remap_tap(p.sw, p.sh, k < npx ? p.mapx[m + k] : 0.f, k < npx ? p.mapy[m + k] : 0.f);
     }
-    for (int k = 0; k < 4 && x0 + k < p.dw; k++)
-        D[x0 + k] = (uint8_t)remap_px(S0, p.sw, p.sh, p.sstride, p.mapx[m + k], p.mapy[m + k]);
+    const bool staged = bb.z > 0;
+    // Staged tiles run branch-free per pixel: the 4 taps' LDS offsets (clamped into the box) and
+    // their weights packed as u16 pairs, with the weight of every out-of-range tap set to 0 —
+    // remapBilinear's constant-0 border, since a 0 weight removes that tap's value from the sum.
+    int off[4][4];
+    uint32_t w01[4], w23[4];
+    if (staged) {
+        const int last = bb.z * bb.w - 1;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const RemapTap& q = t[k];
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                const int sx = q.sx + (d & 1), sy = q.sy + (d >> 1);
+                const bool in = q.mode != 2 && sx >= 0 && sx < p.sw && sy >= 0 && sy < p.sh;
+                off[k][d] = in ? min(max((sy - bb.y) * bb.z + (sx - bb.x), 0), last) : 0;
+            }
+            const bool i0 = q.mode != 2 && q.sx >= 0 && q.sx < p.sw && q.sy >= 0 && q.sy < p.sh;
+            const bool i1 = q.mode != 2 && q.sx + 1 >= 0 && q.sx + 1 < p.sw && q.sy >= 0 && q.sy < p.sh;
+            const bool i2 = q.mode != 2 && q.sx >= 0 && q.sx < p.sw && q.sy + 1 >= 0 && q.sy + 1 < p.sh;
+            const bool i3 = q.mode != 2 && q.sx + 1 >= 0 && q.sx + 1 < p.sw && q.sy + 1 >= 0 && q.sy + 1 < p.sh;
+            w01[k] = (uint32_t)(i0 ? q.w0 : 0) | (uint32_t)(i1 ? q.w1 : 0) << 16;
+            w23[k] = (uint32_t)(i2 ? q.w2 : 0) | (uint32_t)(i3 ? q.w3 : 0) << 16;
+        }
+    }
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    // box staging, software-pipelined: frame f + 1's dwords are loaded into registers while frame f
+    // is computed from the other LDS buffer (one barrier per frame)
+    const int wd = staged ? bb.z >> 2 : 1, nd = staged ? wd * bb.w : 0;
+    uint32_t stage[RM_BOX_BYTES / 4 / 256];
+    auto fetch = [&](int f) {
+        const uint8_t* S0 = p.src + f * p.spitch;
+#pragma unroll
+        for (int j = 0; j < RM_BOX_BYTES / 4 / 256; j++) {
+            const int i = tid + 256 * j;
+            if (i >= nd) break;
+            const int rr = i / wd, c = (i - rr * wd) * 4;
+            const uint8_t* s = S0 + (long long)(bb.y + rr) * p.sstride + bb.x + c;
+            uint32_t v;
+            if (aligned && bb.x + c + 3 < p.sw) {
+                v = *reinterpret_cast<const uint32_t*>(s);
+            } else {  // row end: bytes inside the frame only
+                v = 0;
+                for (int k = 0; k < 4; k++)
+                    if (bb.x + c + k < p.sw) v |= (uint32_t)s[k] << (8 * k);
+            }
+            stage[j] = v;
+        }
+    };
+    if (staged) fetch(f0);
+    for (int f = f0; f < f0 + nf; f++) {
+        const uint8_t* S0 = p.src + f * p.spitch;
+        unsigned r = 0;
+        if (staged) {
+            uint8_t* buf = box + (f & 1) * RM_BOX_BYTES;
+#pragma unroll
+            for (int j = 0; j < RM_BOX_BYTES / 4 / 256; j++) {
+                const int i = tid + 256 * j;
+                if (i >= nd) break;
+                const int rr = i / wd, c = (i - rr * wd) * 4;
+                *reinterpret_cast<uint32_t*>(buf + rr * bb.z + c) = stage[j];
+            }
+            if (f + 1 < f0 + nf) fetch(f + 1);
+            __syncthreads();  // buf complete; the other buffer's readers (frame f - 1) are done
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t v01 = (uint32_t)buf[off[k][0]] | (uint32_t)buf[off[k][1]] << 16;
+                const uint32_t v23 = (uint32_t)buf[off[k][2]] | (uint32_t)buf[off[k][3]] << 16;
+                const uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, v23), __builtin_bit_cast(u16x2, w23[k]),
+                                                          __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, v01),
+                                                                                 __builtin_bit_cast(u16x2, w01[k]),
+                                                                                 1u << 14, false),
+                                                          false);
+                r |= (s >> 15) << (8 * k);  // weights sum to <= 2^15: the result is <= 255
+            }
+        } else {
+            for (int k = 0; k < npx; k++) r |= remap_apply(t[k], S0, p.sw, p.sh, p.sstride) << (8 * k);
+        }
+        if (!live) continue;
+        uint8_t* D = p.dst + f * p.dpitch + (long long)y * p.dstride + x0;
+        if (npx == 4 && (reinterpret_cast<uintptr_t>(D) & 3) == 0) {
+            *reinterpret_cast<unsigned*>(D) = r;
+        } else {
+            for (int k = 0; k < npx; k++) D[k] = (uint8_t)(r >> (8 * k));
+        }
+    }
 }
 
 mage_status remap_launch(const mage_undistorter* u, const uint8_t* d_src, int src_stride, long long src_pitch,
@@ -150,8 +312,11 @@ mage_status remap_launch(const mage_undistorter* u, const uint8_t* d_src, int sr
     p.dh = u->height;
     p.dstride = dst_stride;
     p.dpitch = dst_pitch;
-    const int quads = (u->width + 3) / 4;
-    launch("image.remap", remap_linear_kernel, dim3((quads + 255) / 256, u->height, batch), dim3(256), 0, st, p);
+    // dword staging loads need 4-byte aligned rows in every frame
+    const int aligned = ((reinterpret_cast<uintptr_t>(d_src) | (uintptr_t)src_stride | (uintptr_t)src_pitch) & 3) == 0;
+    launch("image.remap", remap_linear_kernel,
+           dim3((u->width + RM_TW - 1) / RM_TW, (u->height + RM_TH - 1) / RM_TH, (batch + RM_FRAMES - 1) / RM_FRAMES),
+           dim3(256), 0, st, p, (const int4*)u->boxes.as<int4>(), (int)batch, aligned);
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;
 }
@@ -234,8 +399,13 @@ mage_status mage_undistorter_create(const mage_calibration* distorted, int32_t w
         return MAGE_EDEVICE;
     }
     launch("image.undistort_map", undistort_map_kernel, dim3((height + 63) / 64), dim3(64), 0, u->st, p);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(u->st) != hipSuccess) {
+    const dim3 tiles((width + RM_TW - 1) / RM_TW, (height + RM_TH - 1) / RM_TH);
+    if (u->boxes.reserve(16ull * tiles.x * tiles.y) == MAGE_OK)
+        launch("image.remap_boxes", remap_boxes_kernel, tiles, dim3(256), 0, u->st, (const float*)p.mapx,
+               (const float*)p.mapy, width, height, u->boxes.as<int4>());
+    if (!u->boxes.ptr || hipGetLastError() != hipSuccess || hipStreamSynchronize(u->st) != hipSuccess) {
         u->maps.release();
+        u->boxes.release();
         (void)hipStreamDestroy(u->st);
         delete u;
         set_error("undistortion map kernel failed");
@@ -250,6 +420,7 @@ mage_status mage_undistorter_destroy(mage_undistorter* u)
     if (!u) return MAGE_OK;
     (void)hipSetDevice(u->device);
     u->maps.release();
+    u->boxes.release();
     u->scratch.release();
     if (u->st) (void)hipStreamDestroy(u->st);
     delete u;

@@ -150,6 +150,15 @@ def UndistortKeypoints(keypoints: np.ndarray, distortedCalibration, undistortedC
     return kp
 
 
+def undistort_keypoints_batch_device(distortedCalibration, undistortedCalibration, keypoints, pitch: int, counts,
+                                     batch: int, stream=None) -> None:
+    """Batched device form: frame f's keypoints at keypoints + f * pitch (in keypoints), counts[f]
+    of them, undistorted in place (torch device tensors)."""
+    check(_lib.load().mage_undistort_keypoints_batch_device(
+        C.byref(distortedCalibration), C.byref(undistortedCalibration), ptr(keypoints), pitch, ptr(counts), batch,
+        C.c_void_p(stream) if stream else None))
+
+
 class OrbFeatureDetector:
     """OrbFeatureDetector (Image/OrbFeatureDetector.cpp:64-100): DetectAndCompute, then keypoint
     undistortion when the distorted and undistorted calibrations differ (operator!=)."""
