@@ -120,6 +120,15 @@ mage_status mage_synth_frames_device(uint8_t* d_out, uint32_t count, int32_t wid
                                      int32_t height, int64_t frame_pitch, uint32_t t0,
                                      uint64_t seed, mage_stream stream);
 
+/* Benchmark / test input for the tracking loop (BASELINE.json C4): `count` frames of a textured plane
+ * Z = plane_z seen by a pinhole camera; d_cams holds per frame R (row-major, world -> camera) and
+ * the camera centre C (12 doubles).  Texel (floor(X s) + off, floor(Y s) + off) of the panning
+ * sequence's texture; identical to mageslam_amd/synth.py scene_frames(). */
+mage_status mage_synth_scene_device(uint8_t* d_out, uint32_t count, int32_t width, int32_t height,
+                                    int64_t frame_pitch, const double* d_cams, double fx, double fy, double cx,
+                                    double cy, double plane_z, double texel_scale, int64_t texel_offset,
+                                    uint64_t seed, mage_stream stream);
+
 /* FAST-9/16 score map of FAST_t<16> with NMS disabled-equivalent view: score[y*W+x] =
  * cornerScore if (x,y) passes the segment test, else 0 (OpenCVModified.cpp:1225-1512,
  * 927-1071).  Host buffers, synchronous.  Used for the VERIFY_SIMD-style parity check. */

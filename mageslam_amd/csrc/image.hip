@@ -321,6 +321,46 @@ mage_status remap_launch(const mage_undistorter* u, const uint8_t* d_src, int sr
     return MAGE_OK;
 }
 
+// Benchmark / test input (BASELINE.json C4): a textured plane Z = plane_z seen by a moving pinhole
+// camera.  Pixel (x, y) casts the ray R^T K^-1 (x, y, 1) from the camera centre C; the hit (X, Y)
+// picks texel (floor(X s) + off, floor(Y s) + off) of the same seeded texture as the panning
+// sequence.  fp64 in a fixed operation order (no contraction): synth.scene_frames reproduces it
+// byte for byte.
+struct SceneParams {
+    int w, h;
+    long long pitch;
+    double fx, fy, cx, cy, plane_z, scale;
+    long long off;
+    unsigned long long seed;
+    const double* cams;  // per frame: R row-major (9), C (3)
+};
+
+__global__ __launch_bounds__(256) void synth_scene_kernel(uint8_t* __restrict__ out, SceneParams p)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= p.w) return;
+    const double* c = p.cams + 12 * f;
+    const double dx = ((double)x - p.cx) / p.fx, dy = ((double)y - p.cy) / p.fy;
+    const double dwx = (c[0] * dx + c[3] * dy) + c[6];
+    const double dwy = (c[1] * dx + c[4] * dy) + c[7];
+    const double dwz = (c[2] * dx + c[5] * dy) + c[8];
+    const double lam = (p.plane_z - c[11]) / dwz;
+    const double X = c[9] + lam * dwx, Y = c[10] + lam * dwy;
+    const unsigned long long u = (unsigned long long)((long long)floor(X * p.scale) + p.off);
+    const unsigned long long v = (unsigned long long)((long long)floor(Y * p.scale) + p.off);
+    auto mix = [](unsigned long long z) {
+        z += 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    const unsigned long long K1 = 0x9E3779B97F4A7C15ull, K2 = 0xC2B2AE3D27D4EB4Full;
+    const unsigned long long base = mix(p.seed ^ ((u >> 3) * K1) ^ ((v >> 3) * K2));
+    const unsigned long long fine = mix(p.seed ^ 0xA5A5A5A5ull ^ ((u / 3) * K1) ^ ((v / 3) * K2));
+    const int g = (int)(base >> 56) + (int)((fine >> 56) % 49ull) - 24;
+    out[f * p.pitch + (long long)y * p.w + x] = (uint8_t)(g < 0 ? 0 : (g > 255 ? 255 : g));
+}
+
 }  // namespace
 }  // namespace mage
 
@@ -469,3 +509,20 @@ mage_status mage_undistort_image_batch_device(mage_undistorter* u, const uint8_t
 }
 
 }  // extern "C"
+
+extern "C" mage_status mage_synth_scene_device(uint8_t* d_out, uint32_t count, int32_t width, int32_t height,
+                                              int64_t frame_pitch, const double* d_cams, double fx, double fy,
+                                              double cx, double cy, double plane_z, double texel_scale,
+                                              int64_t texel_offset, uint64_t seed, mage_stream stream)
+{
+    using namespace mage;
+    MAGE_REQUIRE(d_out && d_cams && width > 0 && height > 0 && frame_pitch >= (int64_t)width * height, MAGE_EINVAL,
+                 "bad arguments");
+    if (count == 0) return MAGE_OK;
+    SceneParams p{width, height, (long long)frame_pitch, fx, fy, cx, cy, plane_z, texel_scale,
+                  (long long)texel_offset, (unsigned long long)seed, d_cams};
+    launch("synth.scene", synth_scene_kernel, dim3((width + 255) / 256, height, count), dim3(256), 0,
+           (hipStream_t)stream, d_out, p);
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}

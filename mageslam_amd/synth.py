@@ -339,3 +339,67 @@ def pose_batch(problems: int = 256, obs: int = 600, seed: int = BA_SEED + 1, noi
     return PoseBatch(pos=pos.astype(np.float32), r9=r9.astype(np.float32), intr=intr, obs_start=obs_start,
                      points=pts.astype(np.float32), uv=uv.astype(np.float32), info=info, true_pos=true_pos,
                      true_rot=true_rot)
+
+
+# ------------------------------------------------------------------------------------------
+# C4 tracking sequence: a textured plane seen by a moving 720p camera
+# ------------------------------------------------------------------------------------------
+SCENE_PLANE_Z = 5.0
+SCENE_TEXEL_SCALE = 180.0  # texels per metre: ~1 texel per pixel at 5 m with f = 900
+SCENE_TEXEL_OFFSET = 1 << 20
+
+
+@dataclass
+class SceneSequence:
+    """Ground truth of a tracking sequence: per frame world -> camera rotation R (row-major), the
+    camera centre C and the view-space translation t = -R C (Pose::GetViewSpacePosition)."""
+    R: np.ndarray  # (T, 3, 3)
+    C: np.ndarray  # (T, 3)
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+    width: int
+    height: int
+
+    @property
+    def t(self) -> np.ndarray:
+        return -np.einsum("tij,tj->ti", self.R, self.C)
+
+    def cams(self) -> np.ndarray:
+        """(T, 12) float64: R row-major, C — mage_synth_scene_device's camera records."""
+        return np.ascontiguousarray(np.concatenate([self.R.reshape(-1, 9), self.C], 1), np.float64)
+
+
+def scene_sequence(frames: int, width: int = 1280, height: int = 720, step: float = 0.015) -> SceneSequence:
+    """A 'video.mp4-shaped' hand-held pan over the plane: ~2.7 px of motion per frame at 720p plus
+    slow yaw / pitch / roll and depth oscillations (BASELINE.json C4)."""
+    f = 900.0 * width / 1280.0
+    t = np.arange(frames, dtype=np.float64)
+    yaw = 0.03 * np.sin(t / 17.0)
+    pitch = 0.02 * np.sin(t / 23.0)
+    roll = 0.01 * np.sin(t / 31.0)
+    R = np.stack([_rot(a, b, c) for a, b, c in zip(yaw, pitch, roll)])
+    C = np.stack([step * t, 0.08 * np.sin(t / 19.0), 0.15 * np.sin(t / 29.0)], 1)
+    return SceneSequence(R=R, C=C, fx=f, fy=f, cx=width / 2.0, cy=height / 2.0, width=width, height=height)
+
+
+def scene_frames(seq: SceneSequence, first: int = 0, count: int | None = None, seed: int = FRAME_SEED) -> np.ndarray:
+    """(count, H, W) uint8 renderings, byte-identical to mage_synth_scene_device (same fp64 order)."""
+    count = len(seq.R) - first if count is None else count
+    y, x = np.mgrid[0:seq.height, 0:seq.width]
+    dx = (x.astype(np.float64) - seq.cx) / seq.fx
+    dy = (y.astype(np.float64) - seq.cy) / seq.fy
+    out = np.zeros((count, seq.height, seq.width), np.uint8)
+    for i in range(count):
+        c = seq.cams()[first + i]
+        dwx = (c[0] * dx + c[3] * dy) + c[6]
+        dwy = (c[1] * dx + c[4] * dy) + c[7]
+        dwz = (c[2] * dx + c[5] * dy) + c[8]
+        lam = (SCENE_PLANE_Z - c[11]) / dwz
+        X = c[9] + lam * dwx
+        Y = c[10] + lam * dwy
+        u = np.floor(X * SCENE_TEXEL_SCALE).astype(np.int64) + SCENE_TEXEL_OFFSET
+        v = np.floor(Y * SCENE_TEXEL_SCALE).astype(np.int64) + SCENE_TEXEL_OFFSET
+        out[i] = texture(u, v, seed)
+    return out

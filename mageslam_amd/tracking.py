@@ -1,0 +1,245 @@
+"""Tracking loop over the hot path (BASELINE.json C4).
+
+Per frame, the reference's tracker does (Core/MAGESLAM/Source/Tracking):
+  * PoseEstimator::TryEstimatePoseFromKeyframe (PoseEstimator.cpp:439-607): project the reference
+    keyframe's map points with the predicted pose (ProjectUndistorted), RadiusMatch them against the
+    frame's keypoints at SearchRadius, widened to WiderSearchRadius and then ExtraWiderSearchRadius
+    without position overrides when too few match (PoseEstimationSettings, MageSettings.h:170-176);
+  * TrackLocalMap::RunTrackLocalMap (TrackLocalMap.cpp:37-140): OptimizeCameraPose with
+    InitialPoseEstimateBundleAdjustmentSteps x InitialPoseEstimateBundleAdjustmentHuberWidth at
+    MaxOutlierErrorPoseEstimation^2, drop the outliers, OptimizeCameraPose again with
+    BundleAdjustmentG2OSteps x BundleAdjustmentHuberWidth at MaxOutlierError^2 (MageSettings.h:182-189).
+This module runs that sequence on the hot-path kernels: ORB extraction of every frame (batched),
+RadiusMatch and the pose-only BundlerLib per frame.  Map creation is NOT the reference's
+(MapInitialization / NewMapPointsCreation triangulate; they are outside the hot path): a new
+keyframe's keypoints are back-projected onto the scene plane with the keyframe's estimated pose.
+
+`Backend` abstracts the three kernels so the identical loop also runs on the CPU oracle (tests /
+bench.py's cpu_baseline leg), which is how the pose parity of the whole loop is measured.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ._lib import KP_DTYPE
+
+
+@dataclass
+class TrackerSettings:
+    search_radius: float = 12.0            # PoseEstimationSettings::SearchRadius
+    wider_search_radius: float = 24.0      # ::WiderSearchRadius
+    extra_wider_search_radius: float = 36.0  # ::ExtraWiderSearchRadius
+    small_match_ratio: float = 0.333780871615353  # ::FeatureSmallMatchRatioThreshold
+    min_matches: int = 20
+    max_hamming: int = 30                  # OrbMatcherSettings::MaxHammingDistance
+    min_hamming_difference: int = 1        # OrbMatcherSettings::MinHammingDifference
+    initial_ba: tuple = (3, 4.0, 6.0)      # steps, Huber width, MaxOutlierErrorPoseEstimation
+    final_ba: tuple = (4, 0.9, 4.5)        # steps, Huber width, MaxOutlierError
+    refinement_info: float = float(np.float32(1.0) - np.float32(1.0) / np.float32(1.5) ** 2)  # count 0
+    keyframe_ratio: float = 0.25           # new keyframe when fewer map points are tracked
+    keyframe_min: int = 100
+
+
+@dataclass
+class Pose:
+    R: np.ndarray  # world -> camera rotation (3, 3) float64
+    t: np.ndarray  # view-space translation (3,)
+
+    def inverse(self) -> "Pose":
+        return Pose(self.R.T, -self.R.T @ self.t)
+
+    def __mul__(self, o: "Pose") -> "Pose":
+        return Pose(self.R @ o.R, self.R @ o.t + self.t)
+
+
+@dataclass
+class Keyframe:
+    pose: Pose
+    kp: np.ndarray       # its keypoints (KP_DTYPE)
+    desc: np.ndarray     # (n, 32)
+    points: np.ndarray   # (n, 3) float32 map point per keypoint
+
+
+@dataclass
+class TrackResult:
+    poses: list = field(default_factory=list)      # Pose per frame
+    matches: list = field(default_factory=list)    # RadiusMatch count per frame
+    inliers: list = field(default_factory=list)    # associations after the outlier removal
+    keyframes: list = field(default_factory=list)  # frame indices that became keyframes
+
+    def translations(self) -> np.ndarray:
+        return np.stack([p.t for p in self.poses])
+
+    def rotations(self) -> np.ndarray:
+        return np.stack([p.R for p in self.poses])
+
+
+def backproject_to_plane(kp: np.ndarray, pose: Pose, K, plane_z: float) -> np.ndarray:
+    """World points where the keypoints' rays meet the plane Z = plane_z (the scene's depth)."""
+    fx, fy, cx, cy = K
+    d = np.stack([(kp["x"].astype(np.float64) - cx) / fx, (kp["y"].astype(np.float64) - cy) / fy,
+                  np.ones(len(kp))], 1) @ pose.R  # rows: R^T d
+    C = -pose.R.T @ pose.t
+    lam = (plane_z - C[2]) / d[:, 2]
+    return (C[None, :] + lam[:, None] * d).astype(np.float32)
+
+
+def project(points: np.ndarray, pose: Pose, K):
+    """ProjectUndistorted (Tracking/Reprojection): float32 view matrix and camera matrix; returns
+    (positions (n, 2) float32, in_front mask)."""
+    fx, fy, cx, cy = (np.float32(v) for v in K)
+    R = pose.R.astype(np.float32)
+    t = pose.t.astype(np.float32)
+    Xc = points.astype(np.float32) @ R.T + t
+    z = Xc[:, 2]
+    ok = z > 0
+    zs = np.where(ok, z, np.float32(1))
+    pos = np.stack([fx * Xc[:, 0] / zs + cx, fy * Xc[:, 1] / zs + cy], 1).astype(np.float32)
+    return pos, ok
+
+
+class Backend:
+    """The three hot-path operations the loop needs."""
+
+    def extract(self, frames: np.ndarray):  # -> list of (kp, desc)
+        raise NotImplementedError
+
+    def radius_match(self, qkp, qdesc, tkp, tdesc, radius, qpos, max_hamming, min_diff) -> np.ndarray:
+        raise NotImplementedError
+
+    def optimize_pose(self, pose: Pose, K, points, uv, info, steps, huber, max_err_sq):
+        """-> (Pose, outlier flags (n,) bool)"""
+        raise NotImplementedError
+
+
+class GpuBackend(Backend):
+    """libmage_hot.so: batched ORB, RadiusMatch, batched pose-only BA (one problem)."""
+
+    def __init__(self, nfeatures: int = 2000, device: int = 0, batch: int = 64):
+        from . import orb
+
+        self.det = orb.OrbDetector(nfeatures=nfeatures, device=device)
+        self.nfeatures, self.device, self.batch = nfeatures, device, batch
+
+    def extract(self, frames):
+        import torch
+
+        N = self.nfeatures
+        out = []
+        if isinstance(frames, np.ndarray):
+            frames = torch.from_numpy(np.ascontiguousarray(frames)).to(f"cuda:{self.device}")
+        T, H, W = frames.shape
+        for s in range(0, T, self.batch):
+            fr = frames[s:s + self.batch]
+            B = fr.shape[0]
+            kp = torch.zeros((B, N * 28), dtype=torch.uint8, device=fr.device)
+            desc = torch.zeros((B, N, 32), dtype=torch.uint8, device=fr.device)
+            n = torch.zeros(B, dtype=torch.int32, device=fr.device)
+            self.det.detect_and_compute_batch_device(fr, W, H, kp, desc, n, N)
+            kp_h, desc_h, n_h = kp.cpu().numpy(), desc.cpu().numpy(), n.cpu().numpy()
+            for i in range(B):
+                out.append((kp_h[i, : 28 * n_h[i]].view(KP_DTYPE).copy(), desc_h[i, : n_h[i]].copy()))
+        self.det.device_status()
+        return out
+
+    def radius_match(self, qkp, qdesc, tkp, tdesc, radius, qpos, max_hamming, min_diff):
+        from . import matcher
+
+        return matcher.RadiusMatch(qkp, qdesc, tkp, tdesc, radius, max_hamming, min_diff,
+                                   queryKeypointPositionOverrides=qpos)
+
+    def optimize_pose(self, pose, K, points, uv, info, steps, huber, max_err_sq):
+        from . import bundler
+
+        r = bundler.OptimizeCameraPoses(pose_problem(pose, K, points, uv, info), steps, max_err_sq, huber,
+                                        device=self.device)
+        return pose_from_result(r), r["outlier"].astype(bool)
+
+
+@dataclass
+class _Problem:
+    pos: np.ndarray
+    r9: np.ndarray
+    intr: np.ndarray
+    obs_start: np.ndarray
+    points: np.ndarray
+    uv: np.ndarray
+    info: np.ndarray
+
+
+def pose_problem(pose: Pose, K, points, uv, info) -> _Problem:
+    """OptimizeCameraPose's BundlerLib inputs (TrackLocalMap.cpp:445-475): camera 0 = the frame's
+    float pose, observation i on map point i."""
+    fx, fy, cx, cy = K
+    n = len(points)
+    return _Problem(pos=pose.t.astype(np.float32)[None], r9=pose.R.astype(np.float32).T.reshape(1, 9),
+                    intr=np.float32([[cx, cy, fx, fy]]), obs_start=np.array([0, n], np.uint32),
+                    points=np.ascontiguousarray(points, np.float32), uv=np.ascontiguousarray(uv, np.float32),
+                    info=np.full(n, info, np.float32))
+
+
+def pose_from_result(r) -> Pose:
+    """GetPose (BundlerLib.cpp:457-465) output -> Pose (float values, as the reference's Pose)."""
+    R = r["r9"][0].reshape(3, 3).T.astype(np.float64)
+    return Pose(R, r["pos"][0].astype(np.float64))
+
+
+def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
+          settings: TrackerSettings | None = None, frames: int | None = None) -> TrackResult:
+    """Run the loop over precomputed per-frame (keypoints, descriptors); frame 0 is the first
+    keyframe at `first_pose` (its map from the scene plane)."""
+    s = settings or TrackerSettings()
+    T = len(features) if frames is None else frames
+    res = TrackResult()
+    kp0, d0 = features[0]
+    kf = Keyframe(first_pose, kp0, d0, backproject_to_plane(kp0, first_pose, K, plane_z))
+    res.poses.append(first_pose)
+    res.matches.append(len(kp0))
+    res.inliers.append(len(kp0))
+    res.keyframes.append(0)
+    for t in range(1, T):
+        kp, desc = features[t]
+        # motion model: constant velocity on SE3 (the tracker's predicted pose)
+        prev = res.poses[-1]
+        pred = prev if t < 2 else (prev * res.poses[-2].inverse()) * prev
+        qpos, front = project(kf.points, pred, K)
+        sel = np.nonzero(front)[0]
+        qkp, qdesc, qp = kf.kp[sel], kf.desc[sel], qpos[sel]
+        m = backend.radius_match(qkp, qdesc, kp, desc, s.search_radius, qp, s.max_hamming, s.min_hamming_difference)
+        if len(m) < s.min_matches or len(m) / max(len(sel), 1) < s.small_match_ratio:
+            m = backend.radius_match(qkp, qdesc, kp, desc, s.wider_search_radius, qp, s.max_hamming,
+                                     s.min_hamming_difference)
+        if len(m) < s.min_matches or len(m) / max(len(sel), 1) < s.small_match_ratio:
+            m = backend.radius_match(qkp, qdesc, kp, desc, s.extra_wider_search_radius, None, s.max_hamming,
+                                     s.min_hamming_difference)
+        res.matches.append(len(m))
+        if len(m) < s.min_matches:  # lost: keep the prediction (relocalisation is outside the hot path)
+            res.poses.append(pred)
+            res.inliers.append(0)
+            continue
+        pts = kf.points[sel[m["query_idx"]]]
+        uv = np.stack([kp["x"][m["train_idx"]], kp["y"][m["train_idx"]]], 1)
+        steps, huber, err = s.initial_ba
+        pose, out = backend.optimize_pose(pred, K, pts, uv, s.refinement_info, steps, huber, err * err)
+        keep = ~out
+        steps, huber, err = s.final_ba
+        pose, out2 = backend.optimize_pose(pose, K, pts[keep], uv[keep], s.refinement_info, steps, huber, err * err)
+        n_in = int((~out2).sum())
+        res.poses.append(pose)
+        res.inliers.append(n_in)
+        if n_in < max(s.keyframe_min, s.keyframe_ratio * len(sel)):
+            kf = Keyframe(pose, kp, desc, backproject_to_plane(kp, pose, K, plane_z))
+            res.keyframes.append(t)
+    return res
+
+
+def pose_rmse(a: TrackResult, b: TrackResult) -> tuple[float, float]:
+    """(translation RMSE, rotation RMSE in radians) between two runs over the same frames."""
+    n = min(len(a.poses), len(b.poses))
+    dt = np.array([np.linalg.norm(a.poses[i].t - b.poses[i].t) for i in range(n)])
+    # angle between rotations as 2 asin(|Ra - Rb|_F / sqrt 8): exact for rotation matrices and 0 for
+    # identical ones (arccos of the trace is ~1e-4 of noise on float32-rounded matrices)
+    dr = [2 * np.arcsin(min(np.linalg.norm(a.poses[i].R - b.poses[i].R) / np.sqrt(8.0), 1.0)) for i in range(n)]
+    return float(np.sqrt(np.mean(dt ** 2))), float(np.sqrt(np.mean(np.square(dr))))
