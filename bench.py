@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--pose-problems", type=int, default=2048, help="pose-only BA problems per launch")
     p.add_argument("--pose-iters", type=int, default=20)
     p.add_argument("--no-pose", action="store_true")
+    p.add_argument("--track-frames", type=int, default=240, help="C4 tracking-loop sequence length")
+    p.add_argument("--no-tracking", action="store_true")
     p.add_argument("--trajectory-csv", default="", help="rank 0 writes the gathered trajectories (ExportFossilCsv)")
     p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -352,6 +354,76 @@ def cpu_pose_baseline(pb, budget_s):
                       f"{el:.1f} s"}
 
 
+def run_tracking(args, local_rank, torch):
+    """C4 (BASELINE.json configs[3]): the tracking loop (mageslam_amd.tracking) over a synthetic
+    hand-held 720p sequence of a textured plane, frames rendered into HBM first.  A step is the
+    whole sequence: batched ORB extraction of every frame, then per frame RadiusMatch + two
+    pose-only BundlerLib passes (sequential: each frame's prediction needs the previous pose)."""
+    from mageslam_amd import _lib, synth, tracking
+
+    T = args.track_frames
+    seq = synth.scene_sequence(T, args.width, args.height)
+    dev = f"cuda:{local_rank}"
+    cams = torch.from_numpy(seq.cams()).to(dev)
+    frames = torch.empty((T, args.height, args.width), dtype=torch.uint8, device=dev)
+    _lib.check(_lib.load().mage_synth_scene_device(_lib.ptr(frames), T, args.width, args.height,
+                                                   args.width * args.height, _lib.ptr(cams), seq.fx, seq.fy, seq.cx,
+                                                   seq.cy, synth.SCENE_PLANE_Z, synth.SCENE_TEXEL_SCALE,
+                                                   synth.SCENE_TEXEL_OFFSET, synth.FRAME_SEED, None))
+    torch.cuda.synchronize()
+    K = (seq.fx, seq.fy, seq.cx, seq.cy)
+    p0 = tracking.Pose(seq.R[0], seq.t[0])
+    be = tracking.GpuBackend(args.features, device=local_rank, batch=64)
+    feats = be.extract(frames[:8])  # warm-up
+    tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    feats = be.extract(frames)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    res = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)])
+    return {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose)",
+            "value": T / (t2 - t0), "unit": "frames/s", "frames": T, "dtype": "u8 / f64",
+            "extract_ms_per_frame": 1000 * (t1 - t0) / T, "track_ms_per_frame": 1000 * (t2 - t1) / T,
+            "mean_matches": float(np.mean(res.matches[1:])), "mean_inliers": float(np.mean(res.inliers[1:])),
+            "keyframes": len(res.keyframes), "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
+            "config": {"workload": f"C4: {T}-frame {args.width}x{args.height} hand-held pan over a textured plane "
+                                   f"(synthetic), {args.features} features/frame"}}, (seq, frames, res, feats)
+
+
+def cpu_tracking_baseline(args, ctx, budget_s):
+    """The identical loop on the CPU oracle over the first frames of the same sequence; also the
+    GPU-vs-CPU pose RMSE of those frames (north star: <= 1e-4)."""
+    from oracle.tracking_backend import OracleBackend
+
+    from mageslam_amd import synth, tracking
+
+    seq, frames, gres, gfeats = ctx
+    ob = OracleBackend(args.features)
+    host = frames.cpu().numpy()
+    feats, el = [], 0.0
+    t0 = time.perf_counter()
+    while len(feats) < len(host) and (el < budget_s or len(feats) < 4):
+        feats += ob.extract(host[len(feats):len(feats) + 1])
+        el = time.perf_counter() - t0
+    K = (seq.fx, seq.fy, seq.cx, seq.cy)
+    p0 = tracking.Pose(seq.R[0], seq.t[0])
+    t1 = time.perf_counter()
+    ores = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, ob)
+    el = time.perf_counter() - t1 + el
+    n = len(feats)
+    gsub = tracking.TrackResult(poses=gres.poses[:n])
+    same = all(np.array_equal(a[0].view(np.uint8), b[0].view(np.uint8)) for a, b in zip(gfeats[:n], feats))
+    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} frames of the same sequence, oracle extract + RadiusMatch + pose BA, single thread, "
+                      f"{el:.1f} s"}, {"frames": n, "keypoints_identical": bool(same),
+                                       "pose_rmse_gpu_vs_cpu": tracking.pose_rmse(gsub, ores),
+                                       "matches_identical": gres.matches[:n] == ores.matches}
+
+
 def cpu_ba_baseline(g, budget_s):
     from oracle import oracle as O
 
@@ -421,6 +493,7 @@ def main():
     orb_res = run_orb(args, rank, world, local_rank, torch, dist)
     ba_res, g = (None, None) if args.no_ba else run_ba(args, local_rank, torch)
     pose_res, pb = (None, None) if args.no_pose else run_pose(args, rank, world, local_rank, torch, dist)
+    track_res, tctx = (None, None) if (args.no_tracking or rank != 0) else run_tracking(args, local_rank, torch)
     if world > 1:
         dist.barrier()
 
@@ -452,12 +525,19 @@ def main():
             out["ba"] = ba_res
         if pose_res is not None:
             out["pose_ba"] = pose_res
+        if track_res is not None:
+            out["tracking"] = track_res
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_orb_baseline(args, args.cpu_sample_s)
             if ba_res is not None:
                 cb = cpu_ba_baseline(g, args.cpu_sample_s)
                 ba_res["cpu_baseline"] = cb
                 ba_res["vs_cpu"] = ba_res["value"] / cb["value"]
+            if track_res is not None:
+                ct, parity = cpu_tracking_baseline(args, tctx, min(args.cpu_sample_s, 6.0))
+                track_res["cpu_baseline"] = ct
+                track_res["vs_cpu"] = track_res["value"] / ct["value"]
+                track_res["parity"] = parity
             if pose_res is not None:
                 cp = cpu_pose_baseline(pb, min(args.cpu_sample_s, 6.0))
                 pose_res["cpu_baseline"] = cp

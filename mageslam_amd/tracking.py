@@ -38,8 +38,12 @@ class TrackerSettings:
     initial_ba: tuple = (3, 4.0, 6.0)      # steps, Huber width, MaxOutlierErrorPoseEstimation
     final_ba: tuple = (4, 0.9, 4.5)        # steps, Huber width, MaxOutlierError
     refinement_info: float = float(np.float32(1.0) - np.float32(1.0) / np.float32(1.5) ** 2)  # count 0
-    keyframe_ratio: float = 0.25           # new keyframe when fewer map points are tracked
-    keyframe_min: int = 100
+    # NewKeyFrameDecision.cpp:196: a new keyframe when the frame tracks fewer than overlap x the
+    # reference keyframe's map points + KeyframeDecisionMinTrackingPointCount; the overlap is the
+    # console's 0.5 (console.cpp:141; MageSettings.h:86-87).  It has to sit above
+    # small_match_ratio, or the SearchRadius match falls back to the position-free wide search first.
+    keyframe_ratio: float = 0.5
+    keyframe_min: int = 25
 
 
 @dataclass
@@ -229,7 +233,7 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
         n_in = int((~out2).sum())
         res.poses.append(pose)
         res.inliers.append(n_in)
-        if n_in < max(s.keyframe_min, s.keyframe_ratio * len(sel)):
+        if n_in < s.keyframe_ratio * len(kf.points) + s.keyframe_min:
             kf = Keyframe(pose, kp, desc, backproject_to_plane(kp, pose, K, plane_z))
             res.keyframes.append(t)
     return res
