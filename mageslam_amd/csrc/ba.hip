@@ -1503,7 +1503,7 @@ struct BundleAdjuster {
         if (nt > 0)
             launch("ba.tether_eval", tether_eval, dim3((nt + 63) / 64), dim3(64), 0, st, (const Tether*)d_teth.as<Tether>(),
                    nt, state(cur), 1, d_chi.as<double>() + P, d_tout.as<double>());
-        launch("ba.reduce", linearize_finish, dim3(1), dim3(1024), 0, st, nb_free, (const int*)d_camblk.as<int>(),
+        launch("ba.linearize_finish", linearize_finish, dim3(1), dim3(1024), 0, st, nb_free, (const int*)d_camblk.as<int>(),
                (const double*)d_campart.as<double>(), (const double*)d_chi.as<double>(), P,
                (const double*)d_maxd.as<double>(), (const Tether*)d_teth.as<Tether>(), nt,
                (const double*)d_tout.as<double>(), d_Hpp.as<double>(), d_bp.as<double>(), d_red.as<double>());

@@ -29,7 +29,9 @@ namespace {
 
 using namespace ba;
 
-constexpr int PB_THREADS = 256;
+// threads per problem: 256 for large batches (2 problems per CU at 220 VGPRs), 512 when the
+// batch cannot fill the chip (the tracker's per-frame single problem: half the edge-loop latency)
+constexpr int PB_THREADS_BATCH = 256, PB_THREADS_FEW = 512;
 
 struct PoseParams {
     const float* pos3;    // per problem: view-space t
@@ -107,22 +109,47 @@ __device__ __forceinline__ void edge_terms(const EdgeIn& e, const double q[4], c
     jac_pose(xc, f, Jp);
     const double w = rho1 * e.info;
     const double or0 = -e.info * ev[0] * rho1, or1 = -e.info * ev[1] * rho1;
-    int k = 0;
+#pragma unroll
     for (int r = 0; r < 6; r++)
-        for (int c = r; c < 6; c++) acc28[k++] += (Jp[r] * Jp[c] + Jp[6 + r] * Jp[6 + c]) * w;
+#pragma unroll
+        for (int c = r; c < 6; c++) acc28[r * 6 - r * (r - 1) / 2 + c - r] += (Jp[r] * Jp[c] + Jp[6 + r] * Jp[6 + c]) * w;
+#pragma unroll
     for (int r = 0; r < 6; r++) acc28[21 + r] += Jp[r] * or0 + Jp[6 + r] * or1;
 }
 
-// fixed-order workgroup sum of acc[0..N) into out[0..N) (all threads read out afterwards)
-template <int N>
+// fixed-order workgroup sum of acc[0..N) into out[0..N) (all threads read out afterwards).
+// N > 4: butterfly reduce-scatter inside the wave (each xor round halves the values a lane holds:
+// 16 + 8 + 4 + 2 + 1 + 1 shuffles instead of 6 per value; lane 2i ends with value i), then the
+// per-wave partials in LDS
+template <int PB_THREADS, int N>
 __device__ __forceinline__ void wg_sum(double (&acc)[N], double (*red)[N], double* out)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if constexpr (N > 4) {
+        static_assert(N <= 32, "wg_sum: at most 32 values");
+        double v[32];
 #pragma unroll
-    for (int k = 0; k < N; k++) {
-        double v = acc[k];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) red[wave][k] = v;
+        for (int k = 0; k < 32; k++) v[k] = k < N ? acc[k] : 0.0;
+#pragma unroll
+        for (int h = 16; h >= 1; h >>= 1) {
+            const bool up = (lane & (2 * h)) != 0;
+#pragma unroll
+            for (int j = 0; j < h; j++) {
+                const double send = up ? v[j] : v[j + h];
+                const double keep = up ? v[j + h] : v[j];
+                v[j] = keep + __shfl_xor(send, 2 * h);
+            }
+        }
+        const double s = v[0] + __shfl_xor(v[0], 1);
+        if (!(lane & 1) && (lane >> 1) < N) red[wave][lane >> 1] = s;
+    } else {
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            double v = acc[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) red[wave][k] = v;
+        }
     }
     __syncthreads();
     if (threadIdx.x < N) {
@@ -133,6 +160,7 @@ __device__ __forceinline__ void wg_sum(double (&acc)[N], double (*red)[N], doubl
     __syncthreads();
 }
 
+template <int PB_THREADS>
 __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
 {
     __shared__ double red[PB_THREADS / kWave][28];
@@ -166,14 +194,22 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
     for (uint32_t step = 0; E > 0 && step < p.nsteps; step++) {
         // linearise at the current pose
         double acc[28];
+#pragma unroll
         for (int k = 0; k < 28; k++) acc[k] = 0;
         for (int i = tid; i < E; i += PB_THREADS) {
             const EdgeIn e = load_edge(i);
             double ev[2], rho0;
-            edge_terms(e, cur_q, cur_t, f, cx, cy, p.huber, ev, rho0, acc);
+            // per-edge terms into a fresh array, then added (0 + x is exact): accumulating through
+            // the pointer directly kept acc in scratch memory across the loop
+            double a2[28];
+#pragma unroll
+            for (int k = 0; k < 28; k++) a2[k] = 0;
+            edge_terms(e, cur_q, cur_t, f, cx, cy, p.huber, ev, rho0, a2);
+#pragma unroll
+            for (int k = 0; k < 27; k++) acc[k] += a2[k];
             acc[27] += rho0;
         }
-        wg_sum<28>(acc, red, sum);
+        wg_sum<PB_THREADS, 28>(acc, red, sum);
         double currentChi = sum[27];
         if (step == 0) {
             double m = 0;
@@ -197,31 +233,38 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
                         L[c * 6 + r] = sum[k];
                     }
                 for (int r = 0; r < 6; r++) L[r * 6 + r] += lam;
-                int ok = 1;
-                for (int j = 0; j < 6 && ok; j++) {
+                // fully unrolled (static register indexing, no scratch); a non-positive pivot only
+                // clears ok — the rest of the factor is then unused, as after the oracle's break
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
                     double d = L[j * 6 + j];
+#pragma unroll
                     for (int k = 0; k < j; k++) d -= L[j * 6 + k] * L[j * 6 + k];
-                    if (!(d > 0)) {
-                        ok = 0;
-                        break;
-                    }
+                    ok = ok && d > 0;
                     d = sqrt(d);
                     L[j * 6 + j] = d;
+#pragma unroll
                     for (int i = j + 1; i < 6; i++) {
                         double s = L[i * 6 + j];
+#pragma unroll
                         for (int k = 0; k < j; k++) s -= L[i * 6 + k] * L[j * 6 + k];
                         L[i * 6 + j] = s / d;
                     }
                 }
                 if (ok) {
                     double x[6];
+#pragma unroll
                     for (int i = 0; i < 6; i++) {
                         double s = sum[21 + i];
+#pragma unroll
                         for (int k = 0; k < i; k++) s -= L[i * 6 + k] * x[k];
                         x[i] = s / L[i * 6 + i];
                     }
+#pragma unroll
                     for (int i = 5; i >= 0; i--) {
                         double s = x[i];
+#pragma unroll
                         for (int k = i + 1; k < 6; k++) s -= L[k * 6 + i] * x[k];
                         x[i] = s / L[i * 6 + i];
                     }
@@ -248,7 +291,7 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
                 c += rho0;
             }
             double one[1] = {c};
-            wg_sum<1>(one, reinterpret_cast<double(*)[1]>(red), &s_chi);
+            wg_sum<PB_THREADS, 1>(one, reinterpret_cast<double(*)[1]>(red), &s_chi);
             double tempChi = s_chi;
             if (!s_ok2) tempChi = DBL_MAX;
             rho = (currentChi - tempChi) / s_scale;
@@ -298,7 +341,7 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
             acc2[1] += 1;
         }
     }
-    wg_sum<2>(acc2, reinterpret_cast<double(*)[2]>(red), sum);
+    wg_sum<PB_THREADS, 2>(acc2, reinterpret_cast<double(*)[2]>(red), sum);
     if (tid == 0) {
         p.mean_sq[pr] = (float)(sum[0] / sum[1]);
         // GetPose (BundlerLib.cpp:457-465): t as float, R of the normalised quaternion as float
@@ -330,7 +373,10 @@ PoseScratch g_pose[16];
 mage_status pose_launch(const PoseParams& p, uint32_t problems, hipStream_t st)
 {
     if (problems == 0) return MAGE_OK;
-    launch("ba.pose_batch", pose_ba_kernel, dim3(problems), dim3(PB_THREADS), 0, st, p);
+    if (problems >= 512)
+        launch("ba.pose_batch", pose_ba_kernel<PB_THREADS_BATCH>, dim3(problems), dim3(PB_THREADS_BATCH), 0, st, p);
+    else
+        launch("ba.pose_batch", pose_ba_kernel<PB_THREADS_FEW>, dim3(problems), dim3(PB_THREADS_FEW), 0, st, p);
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;
 }

@@ -19,6 +19,7 @@
 //      query order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstring>
 
@@ -81,11 +82,67 @@ __device__ __forceinline__ unsigned wave_min(unsigned v)
     return v;
 }
 
+// 3. batch post-pass of pair pr: unique minimum per target, then ordered compaction in query order
+__device__ void radius_post(const RadiusParams& p, int pr, const int* res, int nq, int ntr, int* bestD, int* cnt,
+                            int* wsum, int& s_base)
+{
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < ntr; i += SORT_THREADS) {
+        bestD[i] = INT_MAX;
+        cnt[i] = 0;
+    }
+    __syncthreads();
+    for (int q = tid; q < nq; q += SORT_THREADS) {
+        const int v = res[q];
+        if (v >= 0) atomicMin(&bestD[v >> 9], v & 0x1FF);
+    }
+    __syncthreads();
+    for (int q = tid; q < nq; q += SORT_THREADS) {
+        const int v = res[q];
+        if (v >= 0 && (v & 0x1FF) == bestD[v >> 9]) atomicAdd(&cnt[v >> 9], 1);
+    }
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    for (int q0 = 0; q0 < nq; q0 += SORT_THREADS) {
+        const int q = q0 + tid;
+        const int v = q < nq ? res[q] : -1;
+        const bool keep = v >= 0 && (v & 0x1FF) == bestD[v >> 9] && cnt[v >> 9] == 1;
+        const unsigned long long b = __ballot(keep);
+        const int before = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = __popcll(b);
+        __syncthreads();
+        int off = s_base;
+        for (int w = 0; w < wave; w++) off += wsum[w];
+        if (keep) {
+            const int pos = off + before;
+            if (pos < (int)p.cap) {
+                mage_dmatch m;
+                m.query_idx = q;
+                m.train_idx = v >> 9;
+                m.img_idx = 0;
+                m.distance = (float)(v & 0x1FF);
+                p.out[(long long)pr * p.cap + pos] = m;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int w = 0; w < SORT_THREADS / kWave; w++) tot += wsum[w];
+            s_base += tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) p.n_out[pr] = (uint32_t)s_base;
+}
+
+// blockIdx.y of gridDim.y workgroups handles every gridDim.y-th wave slot of the pair's queries
+// (gridDim.y > 1 spreads one pair over many CUs: the per-frame tracking call is a single pair);
+// FUSED (gridDim.y == 1) runs the post-pass in the same workgroup, otherwise radius_post_kernel does
+template <bool FUSED>
 __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams p)
 {
     __shared__ unsigned long long keys[RM_MAXT];
-    __shared__ int bestD[RM_MAXT];
-    __shared__ int cnt[RM_MAXT];
     __shared__ int wsum[SORT_THREADS / kWave];
     __shared__ int s_base;
     const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -100,7 +157,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
     const float* qpos = p.qpos ? p.qpos + 2 * pr * p.q_pitch : nullptr;
     int* res = p.res + pr * p.q_pitch;
     if (ntr > RM_MAXT) {
-        if (tid == 0) {
+        if (tid == 0 && blockIdx.y == 0) {
             p.n_out[pr] = 0;
             atomicOr(p.status, 1u);
         }
@@ -115,15 +172,12 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
     __syncthreads();
     sort_desc(keys, P);
     for (int i = tid; i < ntr; i += SORT_THREADS) keys[i] = ~keys[i];
-    for (int i = tid; i < ntr; i += SORT_THREADS) {
-        bestD[i] = INT_MAX;
-        cnt[i] = 0;
-    }
     __syncthreads();
 
     // 2. one wave per query
     const float r = p.radius;
-    for (int q = wave; q < nq; q += SORT_THREADS / kWave) {
+    constexpr int NW = SORT_THREADS / kWave;
+    for (int q = (int)blockIdx.y * NW + wave; q < nq; q += NW * (int)gridDim.y) {
         if (qmask && !qmask[q]) {
             if (lane == 0) res[q] = -1;
             continue;
@@ -171,50 +225,24 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
         sec = wave_min(sec);
         if (lane == 0) res[q] = ((int)sec - best > p.min_diff) ? (tbest << 9 | best) : -1;
     }
-    __syncthreads();
+    if constexpr (FUSED) {
+        __syncthreads();
+        // LDS of the band keys is reused for the post-pass arrays
+        int* bestD = reinterpret_cast<int*>(keys);
+        radius_post(p, pr, res, nq, ntr, bestD, bestD + RM_MAXT, wsum, s_base);
+    }
+}
 
-    // 3. unique minimum per target, then ordered compaction in query order
-    for (int q = tid; q < nq; q += SORT_THREADS) {
-        const int v = res[q];
-        if (v >= 0) atomicMin(&bestD[v >> 9], v & 0x1FF);
-    }
-    __syncthreads();
-    for (int q = tid; q < nq; q += SORT_THREADS) {
-        const int v = res[q];
-        if (v >= 0 && (v & 0x1FF) == bestD[v >> 9]) atomicAdd(&cnt[v >> 9], 1);
-    }
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    for (int q0 = 0; q0 < nq; q0 += SORT_THREADS) {
-        const int q = q0 + tid;
-        const int v = q < nq ? res[q] : -1;
-        const bool keep = v >= 0 && (v & 0x1FF) == bestD[v >> 9] && cnt[v >> 9] == 1;
-        const unsigned long long b = __ballot(keep);
-        const int before = __popcll(b & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[wave] = __popcll(b);
-        __syncthreads();
-        int off = s_base;
-        for (int w = 0; w < wave; w++) off += wsum[w];
-        if (keep) {
-            const int pos = off + before;
-            if (pos < (int)p.cap) {
-                mage_dmatch m;
-                m.query_idx = q;
-                m.train_idx = v >> 9;
-                m.img_idx = 0;
-                m.distance = (float)(v & 0x1FF);
-                p.out[(long long)pr * p.cap + pos] = m;
-            }
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int tot = 0;
-            for (int w = 0; w < SORT_THREADS / kWave; w++) tot += wsum[w];
-            s_base += tot;
-        }
-        __syncthreads();
-    }
-    if (tid == 0) p.n_out[pr] = (uint32_t)s_base;
+__global__ __launch_bounds__(SORT_THREADS) void radius_post_kernel(RadiusParams p)
+{
+    __shared__ int bestD[RM_MAXT];
+    __shared__ int cnt[RM_MAXT];
+    __shared__ int wsum[SORT_THREADS / kWave];
+    __shared__ int s_base;
+    const int pr = blockIdx.x;
+    const int nq = (int)p.nq[pr], ntr = (int)p.nt[pr];
+    if (ntr > RM_MAXT) return;
+    radius_post(p, pr, p.res + pr * p.q_pitch, nq, ntr, bestD, cnt, wsum, s_base);
 }
 
 // host-side scratch for the synchronous single-pair entry point (one per device)
@@ -228,7 +256,16 @@ RadiusScratch g_radius[16];
 
 mage_status radius_match_launch(const RadiusParams& p, uint32_t pairs, hipStream_t st)
 {
-    launch("match.radius", radius_match_kernel, dim3(pairs), dim3(SORT_THREADS), 0, st, p);
+    // a few pairs (the tracker's per-frame call) are spread over ~256 workgroups; batches of
+    // >= 128 pairs already fill the chip with one fused workgroup per pair
+    const uint32_t split = pairs >= 128 ? 1u : std::min(64u, (256u + pairs - 1) / pairs);
+    if (split == 1) {
+        launch("match.radius", radius_match_kernel<true>, dim3(pairs), dim3(SORT_THREADS), 0, st, p);
+    } else {
+        launch("match.radius", radius_match_kernel<false>, dim3(pairs, split), dim3(SORT_THREADS), 0, st, p);
+        MAGE_HIP(hipGetLastError());
+        launch("match.radius_post", radius_post_kernel, dim3(pairs), dim3(SORT_THREADS), 0, st, p);
+    }
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;
 }

@@ -1,18 +1,29 @@
 #!/bin/bash
 # Profiling recipe for the committed evidence (run on the GPU box from the repo root):
 #   kernel trace + stats, then FETCH_SIZE, WRITE_SIZE and SQ VALU/MFMA counters in separate passes
-#   (never combined with trace domains), then the summary into profiles/<tag>_*.
+#   (never combined with trace domains), for bench.py and for tools/bench_rows.py (the §8 rows the
+#   headline does not exercise), then the summaries into profiles/<tag>_*.
 # usage: bash tools/profile_round.sh <tag>
 set -eo pipefail
 TAG=${1:-r1}
 export TMPDIR=/tmp
+run_set() {  # <out dir> <command...>
+    local OUT=$1; shift
+    mkdir -p $OUT
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- "$@" > $OUT/trace.json 2> $OUT/trace.err
+    timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- "$@" > /dev/null 2> $OUT/fetch.err
+    timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- "$@" > /dev/null 2> $OUT/write.err
+    timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES -d $OUT/pmc_valu -o run --output-format csv -- "$@" > /dev/null 2> $OUT/valu.err
+}
 OUT=gpurun_out/prof_$TAG
-mkdir -p $OUT
-CMD="python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $CMD > $OUT/bench_trace.json 2> $OUT/trace.err
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- $CMD > /dev/null 2> $OUT/fetch.err
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- $CMD > /dev/null 2> $OUT/write.err
-timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES -d $OUT/pmc_valu -o run --output-format csv -- $CMD > /dev/null 2> $OUT/valu.err
+run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline
+cp $OUT/trace.json $OUT/bench_trace.json
 python3 tools/rocprof_summary.py $OUT $TAG > $OUT/summary.md
 cp $OUT/trace/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
+ROWS=gpurun_out/prof_${TAG}_rows
+run_set $ROWS python3 tools/bench_rows.py
+python3 tools/rocprof_summary.py $ROWS ${TAG}_rows "python tools/bench_rows.py" > $ROWS/summary.md
+cp $ROWS/trace/run_kernel_stats.csv profiles/${TAG}_rows_kernel_stats.csv
+cp $ROWS/trace.json profiles/${TAG}_rows.jsonl
 timeout -k 10 400 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
+cp $OUT/bench_final.json profiles/${TAG}_bench.json

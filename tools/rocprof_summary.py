@@ -35,7 +35,13 @@ KERNEL_TAG = {
     "match_kernel": "match.two_way", "build_schur": "ba.build_schur", "cholesky_solve": "ba.cholesky_solve",
     "point_linearize": "ba.point_linearize", "cam_linearize": "ba.cam_linearize",
     "point_backsub": "ba.point_backsub", "edge_schur": "ba.edge_schur", "chol_tiles": "ba.cholesky_solve", "drop_edges": "ba.drop_edges", "update_state": "ba.update_state",
-    "outlier_pass": "ba.outlier_pass", "reduce3": "ba.reduce",
+    "outlier_pass": "ba.outlier_pass", "reduce3": "ba.reduce", "linearize_finish": "ba.linearize_finish",
+    "schur_pairs": "ba.schur_pairs", "tether_eval": "ba.tether_eval", "refresh_membership": "ba.refresh_membership",
+    "pose_ba_kernel": "pose.ba", "radius_match_kernel": "match.radius", "radius_post_kernel": "match.radius_post", "indexed_match_kernel": "match.indexed",
+    "bow_leaves_kernel": "bow.leaves", "remap_linear_kernel": "image.remap", "remap_boxes_kernel": "image.boxes",
+    "undistort_map_kernel": "image.map", "undistort_kernel": "orb.undistort", "synth_scene_kernel": "synth.scene",
+    "synth_frames_kernel": "synth.frames", "fast_score_map_kernel": "orb.fast_score", "orient_kernel": "orb.orient",
+    "resize_linear_kernel": "orb.resize",
 }
 
 
@@ -66,6 +72,7 @@ def read_pmc(path: Path, counter: str):
 def main():
     prof = Path(sys.argv[1])
     tag = sys.argv[2]
+    cmd = sys.argv[3] if len(sys.argv) > 3 else "python bench.py"
     out_dir = ROOT / "profiles"
     out_dir.mkdir(exist_ok=True)
     stats = read_stats(prof / "trace" / "run_kernel_stats.csv")
@@ -75,7 +82,7 @@ def main():
     mfma = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_VALU_MFMA_BUSY_CYCLES")
     lines = [f"# rocprofv3 summary — {tag}", "",
              "`rocprofv3 --kernel-trace --stats` (durations) and separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` "
-             "passes of `python bench.py` on one MI355X.  KiB counters converted to bytes; FETCH x2 is the "
+             f"passes of `{cmd}` on one MI355X.  KiB counters converted to bytes; FETCH x2 is the "
              "gfx950 wide-stream correction (MI355X_MICROARCH.md §HBM).", "",
              "VALU issue: SQ_INSTS_VALU wave-instructions per launch (own pass) over the launch time, against "
              "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction (614 G/s; tools/valu_probe.hip measures "
