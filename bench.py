@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--trajectory-csv", default="", help="rank 0 writes the gathered trajectories (ExportFossilCsv)")
     p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-all-cores", action="store_true", help="skip the all-host-cores CPU baselines")
     p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
     p.add_argument("--cpu-dry-run", action="store_true", help="gloo rehearsal of the multi-rank flow (tests)")
     return p.parse_args()
@@ -100,6 +101,49 @@ def cpu_orb_baseline(args, budget_s):
             "sample": f"{n_timed} consecutive {args.width}x{args.height} synthetic frames, oracle "
                       f"extract ({args.features} features) + match vs previous frame, single thread, "
                       f"{el:.1f} s"}
+
+
+def host_threads() -> int:
+    """The host cores this process may use, capped at the box's CPU share for one GPU (16)."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _per_thread(fn, n):
+    """Run fn(worker) on n threads (the oracle's ctypes calls release the GIL); returns the list
+    of (units, timed seconds).  The aggregate rate is the sum of the per-thread rates, each
+    measured while all n threads run."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(n) as ex:
+        return list(ex.map(fn, range(n)))
+
+
+def cpu_orb_baseline_all(args, budget_s):
+    """the oracle on all host cores, frames in parallel (one detector per thread,
+    each matching against its own previous frame)."""
+    from mageslam_amd import synth
+    from oracle import oracle as O
+
+    n = host_threads()
+    s = O.default_settings(args.features)
+    frames = [synth.frame(i, args.width, args.height) for i in range(n + 1)]  # not timed
+
+    def work(w):
+        _, _, prev = O.orb_detect(frames[w], s)
+        k, el, i = 0, 0.0, 1
+        while el < budget_s or k < 2:
+            t0 = time.perf_counter()
+            _, _, d = O.orb_detect(frames[w + i], s)
+            O.match(d, prev, max_distance=30, min_difference=1)
+            el += time.perf_counter() - t0
+            prev, i, k = d, 1 - i, k + 1
+        return k, el
+
+    res = _per_thread(work, n)
+    return {"value": sum(k / el for k, el in res), "unit": "frames/s", "cores": n, "kind": "port",
+            "sample": f"{n} threads, each alternating two consecutive {args.width}x{args.height} synthetic frames "
+                      f"(extract + match vs its previous frame) for ~{budget_s:.0f} s; {sum(k for k, _ in res)} "
+                      f"frames in total; sum of per-thread rates"}
 
 
 def run_orb(args, rank, world, local_rank, torch, dist):
@@ -443,6 +487,32 @@ def cpu_ba_baseline(g, budget_s):
                       f"the C3 graph (same schedule as the GPU leg), oracle, single thread, {el:.1f} s"}
 
 
+def cpu_ba_baseline_all(g, budget_s):
+    """Independent copies of the C3 window on all host cores (one oracle BundlerLib per thread,
+    the GPU leg's schedule) — the many-windows throughput of SURVEY.md §8(e)."""
+    from oracle import oracle as O
+
+    class _NoSync:
+        @staticmethod
+        def sync():
+            pass
+
+    n = host_threads()
+
+    def work(_w):
+        b = O.BundlerOracle()
+        el, k = 0.0, 0
+        while el < budget_s or k == 0:
+            el += ba_round(b, g, 7.25, BA_ROUND_STEPS, _NoSync)
+            k += BA_ROUND_STEPS
+        return k, el
+
+    res = _per_thread(work, n)
+    return {"value": sum(k / el for k, el in res), "unit": "iters/s", "cores": n, "kind": "port",
+            "sample": f"{n} threads, each its own copy of the C3 window on the GPU leg's schedule for ~{budget_s:.0f} s; "
+                      f"sum of per-thread rates"}
+
+
 def run_dry(args, rank, world, dist):
     """CPU rehearsal of the multi-rank control flow (gloo): per-rank sequences, timed loop,
     max-reduce and the end-of-run gather, with the GPU kernels replaced by frame synthesis."""
@@ -529,9 +599,16 @@ def main():
             out["tracking"] = track_res
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_orb_baseline(args, args.cpu_sample_s)
+            if not args.no_all_cores:
+                out["cpu_baseline_all_cores"] = cpu_orb_baseline_all(args, args.cpu_sample_s / 2)
+                out["vs_cpu_all_cores"] = out["value"] / out["cpu_baseline_all_cores"]["value"]
             if ba_res is not None:
                 cb = cpu_ba_baseline(g, args.cpu_sample_s)
                 ba_res["cpu_baseline"] = cb
+                if not args.no_all_cores:
+                    ca = cpu_ba_baseline_all(g, args.cpu_sample_s / 2)
+                    ba_res["cpu_baseline_all_cores"] = ca
+                    ba_res["vs_cpu_all_cores"] = ba_res["value"] / ca["value"]
                 ba_res["vs_cpu"] = ba_res["value"] / cb["value"]
             if track_res is not None:
                 ct, parity = cpu_tracking_baseline(args, tctx, min(args.cpu_sample_s, 6.0))

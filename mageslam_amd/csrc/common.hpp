@@ -67,6 +67,30 @@ struct DeviceBuffer {
     }
 };
 
+// Page-locked host staging for the synchronous host-buffer entry points: the caller's inputs are
+// packed at their device offsets and moved with ONE copy each way (a per-array hipMemcpyAsync costs
+// ~5 us of DMA setup each, which dominated the per-frame tracker calls)
+struct PinnedBuffer {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    mage_status reserve(size_t n) {
+        if (n <= bytes) return MAGE_OK;
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        if (hipHostMalloc(&ptr, n, hipHostMallocDefault) != hipSuccess) {
+            set_error("hipHostMalloc of " + std::to_string(n) + " bytes failed");
+            return MAGE_ENOMEM;
+        }
+        bytes = n;
+        return MAGE_OK;
+    }
+    template <typename T>
+    T* as() const {
+        return static_cast<T*>(ptr);
+    }
+};
+
 constexpr int kWave = 64;
 
 // Optional per-kernel timing with HIP events recorded on the launch stream (mage_profile_*).

@@ -18,6 +18,8 @@
 // Points are fixed (ArePointsFixed): no Schur complement, the reduced system is the camera block.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include <cfloat>
 #include <cmath>
 
@@ -366,6 +368,7 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
 
 struct PoseScratch {
     DeviceBuffer buf;
+    PinnedBuffer host;
     hipStream_t st = nullptr;
 };
 PoseScratch g_pose[16];
@@ -427,17 +430,21 @@ mage_status mage_ba_pose_batch(uint32_t problems, const float* pos3, const float
                  o_pt = al(o_os + 4 * (P + 1)), o_uv = al(o_pt + 12ull * E), o_inf = al(o_uv + 8ull * E),
                  o_pos2 = al(o_inf + 4ull * E), o_r92 = al(o_pos2 + 12 * P), o_qt = al(o_r92 + 36 * P),
                  o_out = al(o_qt + 56 * P), o_ms = al(o_out + E + 1), o_st = al(o_ms + 4 * P), total = o_st + 8 * P;
-    if ((r = S.buf.reserve(total)) != MAGE_OK) return r;
+    if ((r = S.buf.reserve(total)) != MAGE_OK || (r = S.host.reserve(total)) != MAGE_OK) return r;
     char* b = S.buf.as<char>();
-    auto up = [&](size_t off, const void* src, size_t n) -> mage_status {
-        if (n) MAGE_HIP(hipMemcpyAsync(b + off, src, n, hipMemcpyHostToDevice, S.st));
-        return MAGE_OK;
+    char* h = S.host.as<char>();
+    // inputs packed at their device offsets in pinned memory, one H2D copy
+    auto put = [&](size_t off, const void* src, size_t n) {
+        if (n) std::memcpy(h + off, src, n);
     };
-    if ((r = up(o_pos, pos3, 12 * P)) != MAGE_OK || (r = up(o_r9, r9, 36 * P)) != MAGE_OK ||
-        (r = up(o_in, intr4, 16 * P)) != MAGE_OK || (r = up(o_os, obs_start, 4 * (P + 1))) != MAGE_OK ||
-        (r = up(o_pt, points3, 12ull * E)) != MAGE_OK || (r = up(o_uv, uv, 8ull * E)) != MAGE_OK ||
-        (r = up(o_inf, info, 4ull * E)) != MAGE_OK)
-        return r;
+    put(o_pos, pos3, 12 * P);
+    put(o_r9, r9, 36 * P);
+    put(o_in, intr4, 16 * P);
+    put(o_os, obs_start, 4 * (P + 1));
+    put(o_pt, points3, 12ull * E);
+    put(o_uv, uv, 8ull * E);
+    put(o_inf, info, 4ull * E);
+    MAGE_HIP(hipMemcpyAsync(b, h, o_pos2, hipMemcpyHostToDevice, S.st));
     PoseParams p{reinterpret_cast<const float*>(b + o_pos), reinterpret_cast<const float*>(b + o_r9),
                  reinterpret_cast<const float*>(b + o_in), reinterpret_cast<const uint32_t*>(b + o_os),
                  reinterpret_cast<const float*>(b + o_pt), reinterpret_cast<const float*>(b + o_uv),
@@ -446,13 +453,15 @@ mage_status mage_ba_pose_batch(uint32_t problems, const float* pos3, const float
                  reinterpret_cast<double*>(b + o_qt), reinterpret_cast<uint8_t*>(b + o_out),
                  reinterpret_cast<float*>(b + o_ms), reinterpret_cast<uint32_t*>(b + o_st)};
     if ((r = pose_launch(p, problems, S.st)) != MAGE_OK) return r;
-    MAGE_HIP(hipMemcpyAsync(pos3_out, b + o_pos2, 12 * P, hipMemcpyDeviceToHost, S.st));
-    MAGE_HIP(hipMemcpyAsync(r9_out, b + o_r92, 36 * P, hipMemcpyDeviceToHost, S.st));
-    MAGE_HIP(hipMemcpyAsync(mean_sq, b + o_ms, 4 * P, hipMemcpyDeviceToHost, S.st));
-    if (E) MAGE_HIP(hipMemcpyAsync(outlier, b + o_out, E, hipMemcpyDeviceToHost, S.st));
-    if (qt7_out) MAGE_HIP(hipMemcpyAsync(qt7_out, b + o_qt, 56 * P, hipMemcpyDeviceToHost, S.st));
-    if (stats) MAGE_HIP(hipMemcpyAsync(stats, b + o_st, 8 * P, hipMemcpyDeviceToHost, S.st));
+    // outputs: one D2H copy of the contiguous output region, then unpacked on the host
+    MAGE_HIP(hipMemcpyAsync(h + o_pos2, b + o_pos2, total - o_pos2, hipMemcpyDeviceToHost, S.st));
     MAGE_HIP(hipStreamSynchronize(S.st));
+    std::memcpy(pos3_out, h + o_pos2, 12 * P);
+    std::memcpy(r9_out, h + o_r92, 36 * P);
+    std::memcpy(mean_sq, h + o_ms, 4 * P);
+    if (E) std::memcpy(outlier, h + o_out, E);
+    if (qt7_out) std::memcpy(qt7_out, h + o_qt, 56 * P);
+    if (stats) std::memcpy(stats, h + o_st, 8 * P);
     return MAGE_OK;
 }
 

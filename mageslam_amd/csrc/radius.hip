@@ -248,6 +248,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_post_kernel(RadiusParams 
 // host-side scratch for the synchronous single-pair entry point (one per device)
 struct RadiusScratch {
     DeviceBuffer buf;
+    PinnedBuffer host;
     hipStream_t st = nullptr;
 };
 RadiusScratch g_radius[16];
@@ -294,23 +295,27 @@ mage_status mage_radius_match(const mage_keypoint* query_kp, const float* query_
     if (r != MAGE_OK) return r;
     RadiusScratch& S = g_radius[dev & 15];
     if (!S.st) MAGE_HIP(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
-    // device layout: [qkp][tkp][qdesc][tdesc][qpos][qmask][tmask][res][out][counts]
+    // device layout: [qkp][tkp][qdesc][tdesc][qpos][qmask][tmask][counts] (inputs, one H2D copy)
+    // [res][out]; the D2H copy takes [counts, end)
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t oqk = 0, otk = al(oqk + 28ull * n_query), oqd = al(otk + 28ull * n_target),
                  otd = al(oqd + 32ull * n_query), oqp = al(otd + 32ull * n_target), oqm = al(oqp + 8ull * n_query),
-                 otm = al(oqm + n_query), ores = al(otm + n_target), oout = al(ores + 4ull * n_query),
-                 ocnt = al(oout + 16ull * n_query), total = ocnt + 16;
-    if ((r = S.buf.reserve(total)) != MAGE_OK) return r;
+                 otm = al(oqm + n_query), ocnt = al(otm + n_target), ores = al(ocnt + 16),
+                 oout = al(ores + 4ull * n_query), total = oout + 16ull * n_query;
+    if ((r = S.buf.reserve(total)) != MAGE_OK || (r = S.host.reserve(total)) != MAGE_OK) return r;
     char* b = S.buf.as<char>();
-    MAGE_HIP(hipMemcpyAsync(b + oqk, query_kp, 28ull * n_query, hipMemcpyHostToDevice, S.st));
-    MAGE_HIP(hipMemcpyAsync(b + otk, target_kp, 28ull * n_target, hipMemcpyHostToDevice, S.st));
-    MAGE_HIP(hipMemcpyAsync(b + oqd, query_desc, 32ull * n_query, hipMemcpyHostToDevice, S.st));
-    MAGE_HIP(hipMemcpyAsync(b + otd, target_desc, 32ull * n_target, hipMemcpyHostToDevice, S.st));
-    if (query_pos) MAGE_HIP(hipMemcpyAsync(b + oqp, query_pos, 8ull * n_query, hipMemcpyHostToDevice, S.st));
-    if (query_mask) MAGE_HIP(hipMemcpyAsync(b + oqm, query_mask, n_query, hipMemcpyHostToDevice, S.st));
-    if (target_mask) MAGE_HIP(hipMemcpyAsync(b + otm, target_mask, n_target, hipMemcpyHostToDevice, S.st));
+    char* h = S.host.as<char>();
+    // inputs packed at their device offsets in pinned memory: one H2D copy of [0, ores)
+    std::memcpy(h + oqk, query_kp, 28ull * n_query);
+    std::memcpy(h + otk, target_kp, 28ull * n_target);
+    std::memcpy(h + oqd, query_desc, 32ull * n_query);
+    std::memcpy(h + otd, target_desc, 32ull * n_target);
+    if (query_pos) std::memcpy(h + oqp, query_pos, 8ull * n_query);
+    if (query_mask) std::memcpy(h + oqm, query_mask, n_query);
+    if (target_mask) std::memcpy(h + otm, target_mask, n_target);
     const uint32_t counts[4] = {n_query, n_target, 0, 0};
-    MAGE_HIP(hipMemcpyAsync(b + ocnt, counts, 16, hipMemcpyHostToDevice, S.st));
+    std::memcpy(h + ocnt, counts, 16);
+    MAGE_HIP(hipMemcpyAsync(b, h, ores, hipMemcpyHostToDevice, S.st));
     RadiusParams p{};
     p.qkp = reinterpret_cast<const mage_keypoint*>(b + oqk);
     p.qpos = query_pos ? reinterpret_cast<const float*>(b + oqp) : nullptr;
@@ -332,12 +337,11 @@ mage_status mage_radius_match(const mage_keypoint* query_kp, const float* query_
     p.n_out = reinterpret_cast<uint32_t*>(b + ocnt) + 2;
     p.status = reinterpret_cast<uint32_t*>(b + ocnt) + 3;
     if ((r = radius_match_launch(p, 1, S.st)) != MAGE_OK) return r;
-    uint32_t got[2] = {0, 0};
-    MAGE_HIP(hipMemcpyAsync(got, b + ocnt + 8, 8, hipMemcpyDeviceToHost, S.st));
+    // matches + counts come back in one copy
+    MAGE_HIP(hipMemcpyAsync(h + ocnt, b + ocnt, total - ocnt, hipMemcpyDeviceToHost, S.st));
     MAGE_HIP(hipStreamSynchronize(S.st));
-    const uint32_t m = got[0];
-    if (m > 0 && cap > 0)
-        MAGE_HIP(hipMemcpy(out, b + oout, 16ull * (m < cap ? m : cap), hipMemcpyDeviceToHost));
+    const uint32_t m = reinterpret_cast<const uint32_t*>(h + ocnt)[2];
+    if (m > 0 && cap > 0) std::memcpy(out, h + oout, 16ull * (m < cap ? m : cap));
     *n = m < cap ? m : cap;
     MAGE_REQUIRE(m <= cap, MAGE_ECAPACITY, "output capacity too small");
     return MAGE_OK;

@@ -3,7 +3,8 @@
 #   kernel trace + stats, then FETCH_SIZE, WRITE_SIZE and SQ VALU/MFMA counters in separate passes
 #   (never combined with trace domains), for bench.py and for tools/bench_rows.py (the §8 rows the
 #   headline does not exercise), then the summaries into profiles/<tag>_*.
-# usage: bash tools/profile_round.sh <tag>
+# usage: bash tools/profile_round.sh <tag>      (on the box; only gpurun_out/ comes back)
+#        bash tools/profile_round.sh <tag> collect   (here: summaries from gpurun_out/ into profiles/)
 set -eo pipefail
 TAG=${1:-r1}
 export TMPDIR=/tmp
@@ -16,14 +17,16 @@ run_set() {  # <out dir> <command...>
     timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES -d $OUT/pmc_valu -o run --output-format csv -- "$@" > /dev/null 2> $OUT/valu.err
 }
 OUT=gpurun_out/prof_$TAG
-run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline
-cp $OUT/trace.json $OUT/bench_trace.json
-python3 tools/rocprof_summary.py $OUT $TAG > $OUT/summary.md
-cp $OUT/trace/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
 ROWS=gpurun_out/prof_${TAG}_rows
+if [ "$2" = collect ]; then
+    python3 tools/rocprof_summary.py $OUT $TAG > /dev/null
+    cp $OUT/trace/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
+    python3 tools/rocprof_summary.py $ROWS ${TAG}_rows "python tools/bench_rows.py" > /dev/null
+    cp $ROWS/trace/run_kernel_stats.csv profiles/${TAG}_rows_kernel_stats.csv
+    cp $ROWS/trace.json profiles/${TAG}_rows.jsonl
+    cp $OUT/bench_final.json profiles/${TAG}_bench.json
+    exit 0
+fi
+run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline
 run_set $ROWS python3 tools/bench_rows.py
-python3 tools/rocprof_summary.py $ROWS ${TAG}_rows "python tools/bench_rows.py" > $ROWS/summary.md
-cp $ROWS/trace/run_kernel_stats.csv profiles/${TAG}_rows_kernel_stats.csv
-cp $ROWS/trace.json profiles/${TAG}_rows.jsonl
 timeout -k 10 400 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
-cp $OUT/bench_final.json profiles/${TAG}_bench.json
