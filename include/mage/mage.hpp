@@ -132,6 +132,14 @@ public:
         check(mage_bow_create(nodes.empty() ? nullptr : nodes.front().data(), childStart.data(),
                               children.empty() ? nullptr : children.data(), (uint32_t)nodes.size(), device, &m_handle));
     }
+    // OnlineBow::CreateTree (OnlineBow.cpp:325-337) over training descriptors on the GPU
+    // (BagOfWordsSettings TrainingTreeLevels / TrainingTreeBranchingFactor / MaxTrainingIteration)
+    explicit OnlineBowTree(const std::vector<Descriptor>& training, unsigned levels = 2, unsigned branching = 6,
+                           unsigned maxIterations = 12, int device = 0)
+    {
+        check(mage_bow_train(training.empty() ? nullptr : training.front().data(), (uint32_t)training.size(), levels,
+                             branching, maxIterations, device, &m_handle));
+    }
     ~OnlineBowTree() { mage_bow_destroy(m_handle); }
     OnlineBowTree(const OnlineBowTree&) = delete;
     OnlineBowTree& operator=(const OnlineBowTree&) = delete;

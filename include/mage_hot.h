@@ -246,6 +246,20 @@ typedef struct mage_bow mage_bow;
  * (Kmean appends them after it) — MAGE_EINVAL otherwise. */
 mage_status mage_bow_create(const uint8_t* node_desc, const uint32_t* child_start, const uint32_t* children,
                             uint32_t n_nodes, int device, mage_bow** out);
+/* OnlineBow::CreateTree (Core/MAGESLAM/Source/BoW/OnlineBow.cpp:325-337) over n training
+ * descriptors (host, 32 B each): hierarchical Kmean (:451-485) with InitializeTraining's
+ * std::shuffle(mt19937{}) (:396-411, MSVC STL algorithm), IterateClusteringKmean (:587-614),
+ * KmeanCenter (:551-585) and FindCluster (:631-638) — the clustering iterations run on the GPU,
+ * every node of a tree level at once.  levels / branching / max_iter = BagOfWordsSettings
+ * TrainingTreeLevels / TrainingTreeBranchingFactor / MaxTrainingIteration (MageSettings.h:230-232;
+ * branching <= 16 here).  Node ids follow the reference's recursion.  SetNodeWeights (IDF, used by
+ * place recognition only) is not computed. */
+mage_status mage_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
+                           int device, mage_bow** out);
+/* The tree of `bow` (node_desc n x 32, child_start n + 1, children n - 1); MAGE_ECAPACITY with
+ * *n_nodes set when cap_nodes is too small. */
+mage_status mage_bow_get_tree(mage_bow* bow, uint8_t* node_desc, uint32_t* child_start, uint32_t* children,
+                              uint32_t cap_nodes, uint32_t* n_nodes);
 mage_status mage_bow_destroy(mage_bow* bow);
 
 /* FindLeafNode (OnlineBow.cpp:289-311) of n descriptors: leaf[i] = node id.  Host buffers,

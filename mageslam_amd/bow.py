@@ -33,6 +33,30 @@ class OnlineBowTree:
     def from_tuple(cls, tree, device: int = 0) -> "OnlineBowTree":
         return cls(*tree, device=device)
 
+    @classmethod
+    def CreateTree(cls, descriptors, levels: int = 2, branching: int = 6, max_iter: int = 12,
+                   device: int = 0) -> "OnlineBowTree":
+        """OnlineBow::CreateTree (OnlineBow.cpp:325-337) on the GPU: hierarchical Kmean over the
+        training descriptors with BagOfWordsSettings TrainingTreeLevels / TrainingTreeBranchingFactor
+        / MaxTrainingIteration (MageSettings.h:230-232)."""
+        d = np.ascontiguousarray(descriptors, np.uint8).reshape(-1, 32)
+        self = cls.__new__(cls)
+        self._h = C.c_void_p()
+        check(_lib.load().mage_bow_train(ptr(d), len(d), levels, branching, max_iter, device, C.byref(self._h)))
+        self._nd, self._cs, self._ch = self.tree()
+        return self
+
+    def tree(self):
+        """(node_desc (n, 32) u8, child_start (n + 1,) u32, children (n - 1,) u32) of the device tree."""
+        n = C.c_uint32(0)
+        L = _lib.load()
+        L.mage_bow_get_tree(self._h, None, None, None, 0, C.byref(n))
+        nd = np.zeros((n.value, 32), np.uint8)
+        cs = np.zeros(n.value + 1, np.uint32)
+        ch = np.zeros(max(n.value, 1), np.uint32)
+        check(L.mage_bow_get_tree(self._h, ptr(nd), ptr(cs), ptr(ch), n.value, C.byref(n)))
+        return nd, cs, ch[: int(cs[-1])]
+
     @property
     def handle(self):
         return self._h

@@ -21,7 +21,9 @@
 //     3. ordered compaction in A order (the reference appends in forward-match order).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
+#include <functional>
 #include <cstring>
 #include <vector>
 
@@ -267,6 +269,175 @@ mage_status indexed_launch(const IndexedParams& p, uint32_t pairs, hipStream_t s
     return MAGE_OK;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Vocabulary training (OnlineBow::CreateTree, OnlineBow.cpp:325-337): the Kmean of every node of
+// one tree level runs concurrently.  The host keeps the control flow of Kmean (subsets, the
+// InitializeTraining shuffle, node numbering); the GPU runs IterateClusteringKmean (:587-614):
+//   km_assign_kernel  FindCluster of every entry (first smallest distance) + the KmeanCenter bit
+//                     sums: per wave 256 ballots (one per bit) are kept in LDS, each lane then
+//                     counts 4 bits for every cluster present in the wave (popc of ballot &
+//                     cluster mask), LDS sums per block, one global atomic per nonzero counter;
+//   km_update_kernel  per node: majority bits (count >= (members + 1) / 2, an empty cluster
+//                     becomes all ones as in the reference), the changed test, iteration count and
+//                     the loop's exit condition — after it, both kernels are no-ops for the node,
+//                     so the host launches MaxTrainingIteration rounds without reading anything back.
+// ---------------------------------------------------------------------------------------------
+constexpr int KM_THREADS = 1024;
+constexpr int KM_MAXB = 16;  // branching factors handled on the GPU
+
+struct KmParams {
+    const uint8_t* desc;        // training descriptors, 32 B each
+    const uint32_t* entry_desc; // entry -> descriptor index (entries grouped by slot, ascending)
+    const uint32_t* blk_slot;   // block -> slot
+    const uint32_t* blk_start;  // block -> first entry
+    const uint32_t* slot_end;   // slot -> end entry (exclusive)
+    const uint32_t* ncent;      // slot -> number of clusters
+    uint8_t* centers;           // slot x KM_MAXB x 32
+    uint32_t* counts;           // slot x KM_MAXB x 256
+    uint32_t* members;          // slot x KM_MAXB
+    uint32_t* assign;           // entry -> cluster
+    uint32_t* state;            // slot -> {iterations, done}
+    uint32_t max_iter;
+};
+
+__global__ __launch_bounds__(KM_THREADS) void km_assign_kernel(KmParams p)
+{
+    __shared__ unsigned long long wbal[KM_THREADS / kWave][256];
+    __shared__ uint32_t lcnt[KM_MAXB * 256];
+    __shared__ uint32_t lmem[KM_MAXB];
+    __shared__ uint4 cen[KM_MAXB * 2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t s = p.blk_slot[blockIdx.x];
+    if (p.state[2 * s + 1]) return;  // this node's loop has ended
+    const int k = (int)p.ncent[s];
+    const uint32_t e = p.blk_start[blockIdx.x] + tid;
+    const bool valid = e < p.slot_end[s];
+    for (int i = tid; i < k * 256; i += KM_THREADS) lcnt[i] = 0;
+    if (tid < k) lmem[tid] = 0;
+    if (tid < 2 * k) cen[tid] = reinterpret_cast<const uint4*>(p.centers + (size_t)s * KM_MAXB * 32)[tid];
+    __syncthreads();
+    uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int g = -1;
+    if (valid) {
+        const uint4* dp = reinterpret_cast<const uint4*>(p.desc + 32ull * p.entry_desc[e]);
+        const uint4 a = dp[0], b = dp[1];
+        d[0] = a.x, d[1] = a.y, d[2] = a.z, d[3] = a.w, d[4] = b.x, d[5] = b.y, d[6] = b.z, d[7] = b.w;
+        int best = INT_MAX;
+        for (int c = 0; c < k; c++) {
+            const uint4 ca = cen[2 * c], cb = cen[2 * c + 1];
+            const int dist = __popc(d[0] ^ ca.x) + __popc(d[1] ^ ca.y) + __popc(d[2] ^ ca.z) + __popc(d[3] ^ ca.w) +
+                             __popc(d[4] ^ cb.x) + __popc(d[5] ^ cb.y) + __popc(d[6] ^ cb.z) + __popc(d[7] ^ cb.w);
+            if (dist < best) {  // FindCluster: min_element keeps the first smallest
+                best = dist;
+                g = c;
+            }
+        }
+        p.assign[e] = (uint32_t)g;
+    }
+    // one ballot per bit (bit j*8+b of the descriptor = bit b of byte j: KmeanCenter's order)
+#pragma unroll
+    for (int w = 0; w < 8; w++)
+        for (int b = 0; b < 32; b++) {
+            const unsigned long long bal = __ballot((d[w] >> b) & 1u);
+            if (lane == 0) wbal[wave][w * 32 + b] = bal;
+        }
+    __syncthreads();
+    for (int c = 0; c < k; c++) {
+        const unsigned long long m = __ballot(g == c);
+        if (m == 0) continue;
+        if (lane == 0) atomicAdd(&lmem[c], (uint32_t)__popcll(m));
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int bit = lane + 64 * r;
+            const uint32_t cnt = (uint32_t)__popcll(m & wbal[wave][bit]);
+            if (cnt) atomicAdd(&lcnt[c * 256 + bit], cnt);
+        }
+    }
+    __syncthreads();
+    uint32_t* gc = p.counts + (size_t)s * KM_MAXB * 256;
+    for (int i = tid; i < k * 256; i += KM_THREADS)
+        if (lcnt[i]) atomicAdd(&gc[i], lcnt[i]);
+    if (tid < k && lmem[tid]) atomicAdd(&p.members[s * KM_MAXB + tid], lmem[tid]);
+}
+
+__global__ __launch_bounds__(256) void km_update_kernel(KmParams p)
+{
+    __shared__ uint32_t changed[KM_MAXB];
+    const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (p.state[2 * s + 1]) return;
+    const int k = (int)p.ncent[s];
+    if (t < KM_MAXB) changed[t] = 0;
+    __syncthreads();
+    uint32_t* gc = p.counts + (size_t)s * KM_MAXB * 256;
+    unsigned long long* cen = reinterpret_cast<unsigned long long*>(p.centers + (size_t)s * KM_MAXB * 32);
+    for (int c = 0; c < k; c++) {
+        const uint32_t half = (p.members[s * KM_MAXB + c] + 1) / 2;
+        const unsigned long long nb = __ballot(gc[c * 256 + t] >= half);  // bits 64*wave .. +63
+        if (lane == 0) {
+            if (nb != cen[4 * c + wave]) changed[c] = 1;
+            cen[4 * c + wave] = nb;
+        }
+        gc[c * 256 + t] = 0;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t ch = 0;
+        for (int c = 0; c < k; c++) {
+            ch += changed[c];
+            p.members[s * KM_MAXB + c] = 0;
+        }
+        const uint32_t it = p.state[2 * s] + 1;
+        p.state[2 * s] = it;
+        // do { ... } while (iterationCounter < MaxTrainingIteration && changedKmeanCounter > 0)
+        if (!(it < p.max_iter && ch > 0)) p.state[2 * s + 1] = 1;
+    }
+}
+
+// std::shuffle(refs, mt19937{}) as the reference's MSVC STL computes it (InitializeTraining,
+// OnlineBow.cpp:404): a fresh default-seeded engine per call, target t swapped with a draw in
+// [0, t] from _Rng_from_urng (one 32-bit output per draw for sizes < 2^32, rejection of the biased
+// tail).  Host-side: the positions of the first `branching` refs of an n-element subset.
+struct Mt19937 {
+    uint32_t mt[624];
+    int idx = 624;
+    explicit Mt19937(uint32_t seed) {
+        mt[0] = seed;
+        for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    }
+    uint32_t operator()() {
+        if (idx >= 624) {
+            for (int i = 0; i < 624; i++) {
+                const uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7FFFFFFFu);
+                mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908B0DFu : 0u);
+            }
+            idx = 0;
+        }
+        uint32_t y = mt[idx++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9D2C5680u;
+        y ^= (y << 15) & 0xEFC60000u;
+        return y ^ (y >> 18);
+    }
+};
+
+std::vector<uint32_t> shuffled_head(uint32_t n, uint32_t k)
+{
+    std::vector<uint32_t> perm(n);
+    for (uint32_t i = 0; i < n; i++) perm[i] = i;
+    Mt19937 rng(5489u);
+    for (uint32_t t = 1; t < n; t++) {
+        const uint64_t index = (uint64_t)t + 1, mask = 0xFFFFFFFFull;
+        uint64_t r;
+        do r = rng();
+        while (!(r / index < mask / index || mask % index == index - 1));
+        const uint32_t off = (uint32_t)(r % index);
+        if (off != t) std::swap(perm[t], perm[off]);
+    }
+    perm.resize(k < n ? k : n);
+    return perm;
+}
+
 }  // namespace
 }  // namespace mage
 
@@ -446,6 +617,169 @@ mage_status mage_indexed_match_batch_device(const uint8_t* d_desc_a, const uint3
     p.n_out = d_n;
     p.status = d_status;
     return indexed_launch(p, pairs, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+extern "C" {
+
+mage_status mage_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
+                           int device, mage_bow** out)
+{
+    using namespace mage;
+    MAGE_REQUIRE(out, MAGE_EINVAL, "null output");
+    *out = nullptr;
+    MAGE_REQUIRE(n == 0 || desc, MAGE_EINVAL, "null descriptors");
+    MAGE_REQUIRE(levels >= 1, MAGE_EINVAL, "TrainingTreeLevels must be >= 1");
+    MAGE_REQUIRE(branching >= 1 && branching <= (uint32_t)KM_MAXB, MAGE_EUNSUPPORTED,
+                 "TrainingTreeBranchingFactor must be in [1, 16]");
+    mage_status r = bind_device(device);
+    if (r != MAGE_OK) return r;
+    struct HNode {
+        uint8_t d[32];
+        std::vector<uint32_t> kids;
+    };
+    std::vector<HNode> nodes(1);
+    std::memset(nodes[0].d, 0, 32);
+    struct Slot {
+        uint32_t node;
+        std::vector<uint32_t> idx;  // descriptor indices, ascending (child_features keep the order)
+    };
+    std::vector<Slot> slots;
+    if (n > 0) {
+        Slot s0{0, std::vector<uint32_t>(n)};
+        for (uint32_t i = 0; i < n; i++) s0.idx[i] = i;
+        slots.push_back(std::move(s0));
+    }
+    hipStream_t st = nullptr;
+    MAGE_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    DeviceBuffer d_desc, d_work;
+    auto fail = [&](mage_status e) {
+        (void)hipStreamDestroy(st);
+        return e;
+    };
+    if (n > 0) {
+        if ((r = d_desc.reserve(32ull * n)) != MAGE_OK) return fail(r);
+        if (hipMemcpyAsync(d_desc.ptr, desc, 32ull * n, hipMemcpyHostToDevice, st) != hipSuccess)
+            return fail(MAGE_EDEVICE);
+    }
+    for (uint32_t level = 1; !slots.empty(); level++) {
+        const uint32_t S = (uint32_t)slots.size();
+        std::vector<uint32_t> entry, blk_slot, blk_start, slot_end(S), ncent(S);
+        std::vector<uint8_t> centers((size_t)S * KM_MAXB * 32, 0);
+        for (uint32_t si = 0; si < S; si++) {
+            const Slot& sl = slots[si];
+            const uint32_t base = (uint32_t)entry.size(), cnt = (uint32_t)sl.idx.size();
+            for (uint32_t b = 0; b < cnt; b += KM_THREADS) {
+                blk_slot.push_back(si);
+                blk_start.push_back(base + b);
+            }
+            entry.insert(entry.end(), sl.idx.begin(), sl.idx.end());
+            slot_end[si] = (uint32_t)entry.size();
+            // InitializeTraining: the first min(branching, n) refs after the shuffle
+            const std::vector<uint32_t> head = shuffled_head(cnt, branching);
+            ncent[si] = (uint32_t)head.size();
+            for (size_t g = 0; g < head.size(); g++)
+                std::memcpy(&centers[((size_t)si * KM_MAXB + g) * 32], desc + 32ull * sl.idx[head[g]], 32);
+        }
+        const uint32_t E = (uint32_t)entry.size(), B = (uint32_t)blk_slot.size();
+        auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+        const size_t o_entry = 0, o_bs = al(4ull * E), o_bst = al(o_bs + 4ull * B), o_se = al(o_bst + 4ull * B),
+                     o_nc = al(o_se + 4ull * S), o_cen = al(o_nc + 4ull * S), o_cnt = al(o_cen + centers.size()),
+                     o_mem = al(o_cnt + 4ull * S * KM_MAXB * 256), o_st = al(o_mem + 4ull * S * KM_MAXB),
+                     o_as = al(o_st + 8ull * S), total = o_as + 4ull * E;
+        if ((r = d_work.reserve(total)) != MAGE_OK) return fail(r);
+        char* w = d_work.as<char>();
+        if (hipMemcpyAsync(w + o_entry, entry.data(), 4ull * E, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(w + o_bs, blk_slot.data(), 4ull * B, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(w + o_bst, blk_start.data(), 4ull * B, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(w + o_se, slot_end.data(), 4ull * S, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(w + o_nc, ncent.data(), 4ull * S, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(w + o_cen, centers.data(), centers.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemsetAsync(w + o_cnt, 0, o_as - o_cnt, st) != hipSuccess)
+            return fail(MAGE_EDEVICE);
+        KmParams p{d_desc.as<const uint8_t>(),
+                   reinterpret_cast<const uint32_t*>(w + o_entry),
+                   reinterpret_cast<const uint32_t*>(w + o_bs),
+                   reinterpret_cast<const uint32_t*>(w + o_bst),
+                   reinterpret_cast<const uint32_t*>(w + o_se),
+                   reinterpret_cast<const uint32_t*>(w + o_nc),
+                   reinterpret_cast<uint8_t*>(w + o_cen),
+                   reinterpret_cast<uint32_t*>(w + o_cnt),
+                   reinterpret_cast<uint32_t*>(w + o_mem),
+                   reinterpret_cast<uint32_t*>(w + o_as),
+                   reinterpret_cast<uint32_t*>(w + o_st),
+                   max_iter};
+        // the do-while body runs at least once
+        for (uint32_t it = 0; it < std::max(max_iter, 1u); it++) {
+            launch("bow.km_assign", km_assign_kernel, dim3(B), dim3(KM_THREADS), 0, st, p);
+            if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
+            launch("bow.km_update", km_update_kernel, dim3(S), dim3(256), 0, st, p);
+            if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
+        }
+        std::vector<uint32_t> assign(E);
+        if (hipMemcpyAsync(assign.data(), w + o_as, 4ull * E, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(centers.data(), w + o_cen, centers.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return fail(MAGE_EDEVICE);
+        // Kmean: the centers become children of the node (in cluster order); groups recurse
+        std::vector<Slot> next;
+        for (uint32_t si = 0; si < S; si++) {
+            const uint32_t k = ncent[si], base = si ? slot_end[si - 1] : 0;
+            std::vector<std::vector<uint32_t>> groups(k);
+            for (uint32_t e = base; e < slot_end[si]; e++) groups[assign[e]].push_back(entry[e]);
+            for (uint32_t g = 0; g < k; g++) {
+                HNode c;
+                std::memcpy(c.d, &centers[((size_t)si * KM_MAXB + g) * 32], 32);
+                nodes.push_back(c);
+                const uint32_t id = (uint32_t)nodes.size() - 1;
+                nodes[slots[si].node].kids.push_back(id);
+                if (level < levels && groups[g].size() > 1) next.push_back(Slot{id, std::move(groups[g])});
+            }
+        }
+        slots = std::move(next);
+    }
+    (void)hipStreamDestroy(st);
+    // ids as the recursive Kmean hands them out: a node's children consecutively, then each
+    // child's subtree in order (depth first)
+    std::vector<uint32_t> nid(nodes.size(), 0);
+    uint32_t next_id = 1;
+    std::function<void(uint32_t)> number = [&](uint32_t v) {
+        for (uint32_t c : nodes[v].kids) nid[c] = next_id++;
+        for (uint32_t c : nodes[v].kids)
+            if (!nodes[c].kids.empty()) number(c);
+    };
+    number(0);
+    const uint32_t N = (uint32_t)nodes.size();
+    std::vector<uint8_t> nd(32ull * N);
+    std::vector<std::vector<uint32_t>> kids(N);
+    for (uint32_t v = 0; v < N; v++) {
+        std::memcpy(&nd[32ull * nid[v]], nodes[v].d, 32);
+        for (uint32_t c : nodes[v].kids) kids[nid[v]].push_back(nid[c]);
+    }
+    std::vector<uint32_t> cs(N + 1, 0), ch;
+    for (uint32_t v = 0; v < N; v++) {
+        cs[v] = (uint32_t)ch.size();
+        ch.insert(ch.end(), kids[v].begin(), kids[v].end());
+    }
+    cs[N] = (uint32_t)ch.size();
+    return mage_bow_create(nd.data(), cs.data(), ch.empty() ? nullptr : ch.data(), N, device, out);
+}
+
+mage_status mage_bow_get_tree(mage_bow* b, uint8_t* node_desc, uint32_t* child_start, uint32_t* children,
+                              uint32_t cap_nodes, uint32_t* n_nodes)
+{
+    using namespace mage;
+    MAGE_REQUIRE(b && n_nodes, MAGE_EINVAL, "null argument");
+    *n_nodes = b->n_nodes;
+    if (cap_nodes < b->n_nodes) return MAGE_ECAPACITY;
+    MAGE_REQUIRE(node_desc && child_start && children, MAGE_EINVAL, "null output");
+    MAGE_HIP(hipSetDevice(b->device));
+    MAGE_HIP(hipMemcpy(node_desc, b->nodes.ptr, 32ull * b->n_nodes, hipMemcpyDeviceToHost));
+    MAGE_HIP(hipMemcpy(child_start, b->child_start.ptr, 4ull * (b->n_nodes + 1), hipMemcpyDeviceToHost));
+    const uint32_t nc = child_start[b->n_nodes];
+    if (nc) MAGE_HIP(hipMemcpy(children, b->children.ptr, 4ull * nc, hipMemcpyDeviceToHost));
+    return MAGE_OK;
 }
 
 }  // extern "C"

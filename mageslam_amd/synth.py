@@ -227,21 +227,48 @@ def _hamming_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     return ab @ (1 - bb).T + (1 - ab) @ bb.T
 
 
-def bow_tree(train: np.ndarray, levels: int = 2, branching: int = 6, max_iter: int = 12, seed: int = 0x0B0E):
-    """OnlineBow vocabulary tree (OnlineBow.cpp:325-337 CreateTree, :451-485 Kmean, :517-587
-    KmeanCenter / IterateClusteringKmean, :631-639 FindCluster) over training descriptors, with
-    BagOfWordsSettings defaults (MageSettings.h:230-232).  InitializeTraining's std::shuffle with a
-    default-seeded mt19937 (:404) is implementation-defined; a seeded numpy permutation stands in.
-    Returns (node_desc (N, 32) u8, child_start (N + 1,) u32, children (N - 1,) u32)."""
-    rng = np.random.default_rng(seed)
+def msvc_shuffle(n: int) -> np.ndarray:
+    """std::shuffle(0..n-1, mt19937{}) as MSVC's STL computes it (OnlineBow::InitializeTraining,
+    OnlineBow.cpp:404): a default-seeded (5489) engine, target t swapped with _Rng_from_urng(t + 1)
+    = one 32-bit draw r kept when r // (t+1) < 0xFFFFFFFF // (t+1) or 0xFFFFFFFF % (t+1) == t,
+    giving r % (t+1).  numpy's MT19937 with legacy seeding is std::mt19937 (same raw outputs)."""
+    bg = np.random.MT19937(0)
+    bg._legacy_seeding(5489)
+    perm = list(range(n))
+    mask = 0xFFFFFFFF
+    raw = iter(())
+    for t in range(1, n):
+        index = t + 1
+        while True:
+            r = next(raw, None)
+            if r is None:
+                raw = iter(bg.random_raw(4096).tolist())
+                r = next(raw)
+            if r // index < mask // index or mask % index == index - 1:
+                off = r % index
+                break
+        if off != t:
+            perm[t], perm[off] = perm[off], perm[t]
+    return np.array(perm, np.int64)
+
+
+def bow_tree(train: np.ndarray, levels: int = 2, branching: int = 6, max_iter: int = 12):
+    """OnlineBow::CreateTree (OnlineBow.cpp:325-337) restated in numpy: Kmean (:451-485) with
+    InitializeTraining's shuffle (msvc_shuffle), IterateClusteringKmean (:587-614: the groups are
+    those of the last iteration's assignment, made before its center update), KmeanCenter (:551-585)
+    and FindCluster (:631-638, first smallest distance); BagOfWordsSettings defaults
+    (MageSettings.h:230-232).  Returns (node_desc (N, 32) u8, child_start (N + 1,) u32,
+    children (N - 1,) u32)."""
     train = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)
     nodes = [np.zeros(32, np.uint8)]
     kids: list[list[int]] = [[]]
 
     def kmean(parent: int, desc: np.ndarray, level: int) -> None:
-        perm = rng.permutation(len(desc))
+        perm = msvc_shuffle(len(desc))
         centers = [desc[i].copy() for i in perm[:branching]]
-        for _ in range(max_iter):
+        it = 0
+        while True:
+            it += 1
             d = _hamming_matrix(desc, np.stack(centers))
             assign = np.argmin(d, axis=1)  # first minimum, as std::min_element
             changed = 0
@@ -254,10 +281,8 @@ def bow_tree(train: np.ndarray, levels: int = 2, branching: int = 6, max_iter: i
                 if not np.array_equal(new, centers[g]):
                     changed += 1
                 centers[g] = new
-            if changed == 0:
+            if not (it < max_iter and changed > 0):
                 break
-        d = _hamming_matrix(desc, np.stack(centers))
-        assign = np.argmin(d, axis=1)
         ids = []
         for c in centers:
             ids.append(len(nodes))
@@ -270,7 +295,8 @@ def bow_tree(train: np.ndarray, levels: int = 2, branching: int = 6, max_iter: i
                 if len(sub) > 1:
                     kmean(nid, sub, level + 1)
 
-    kmean(0, train, 1)
+    if len(train):
+        kmean(0, train, 1)
     child_start = np.zeros(len(nodes) + 1, np.uint32)
     child_start[1:] = np.cumsum([len(k) for k in kids])
     children = np.array([c for k in kids for c in k], np.uint32)

@@ -103,6 +103,11 @@ def _declare(L):
     L.oracle_bow_find_leaf.restype = u32
     L.oracle_indexed_match.argtypes = [vp, vp, vp, vp, u32, vp, vp, u32, vp, i32, i32, vp, u32]
     L.oracle_indexed_match.restype = u32
+    L.oracle_bow_train.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, u32]
+    L.oracle_bow_train.restype = u32
+    L.oracle_msvc_shuffle.argtypes = [u32, vp]
+    L.oracle_mt19937_first.argtypes = [u32, u32]
+    L.oracle_mt19937_first.restype = u32
     L.oracle_ba_tether_linearization.argtypes = [vp, i32, vp, vp, vp]
     L.oracle_ba_tether_linearization.restype = i32
     L.oracle_ba_get_lambda.argtypes = [vp]
@@ -282,6 +287,32 @@ def bow_find_leaves(tree, desc):
     nd, cs, ch = (np.ascontiguousarray(x) for x in tree)
     d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
     return np.array([lib().oracle_bow_find_leaf(_p(nd), _p(cs), _p(ch), _p(d[i])) for i in range(len(d))], np.uint32)
+
+
+def bow_train(desc, levels=2, branching=6, max_iter=12):
+    """OnlineBow::CreateTree (OnlineBow.cpp:325-337, Kmean :451-485) over training descriptors
+    (BagOfWordsSettings defaults, MageSettings.h:230-232); returns (node_desc, child_start, children)."""
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    cap = 1
+    for _ in range(levels):
+        cap = cap * branching + 1
+    nd = np.zeros((cap, 32), np.uint8)
+    cs = np.zeros(cap + 1, np.uint32)
+    ch = np.zeros(max(cap, 1), np.uint32)
+    n = lib().oracle_bow_train(_p(d), len(d), levels, branching, max_iter, _p(nd), _p(cs), _p(ch), cap)
+    assert n > 0
+    return nd[:n].copy(), cs[: n + 1].copy(), ch[: int(cs[n])].copy()
+
+
+def msvc_shuffle(n):
+    """std::shuffle(0..n-1, mt19937{}) as MSVC's STL computes it (InitializeTraining, OnlineBow.cpp:404)."""
+    out = np.zeros(max(n, 1), np.uint32)
+    lib().oracle_msvc_shuffle(n, _p(out))
+    return out[:n]
+
+
+def mt19937_output(seed, k):
+    return int(lib().oracle_mt19937_first(seed, k))
 
 
 def indexed_match(tree, desc_a, desc_b, mask_a=None, mask_b=None, max_distance=30, min_difference=1):

@@ -57,6 +57,11 @@ int main(int argc, char** argv)
         std::vector<mage::hot::DMatch> imatches;
         const unsigned ni = mage::hot::IndexedMatch(tree, desc, desc, std::vector<bool>(desc.size(), true),
                                                     std::vector<bool>(desc.size(), true), 30, 1, imatches);
+        // OnlineBow::CreateTree over the frame's descriptors (defaults), then IndexedMatch through it
+        mage::hot::OnlineBowTree trained(desc);
+        std::vector<mage::hot::DMatch> tmatches;
+        const unsigned nt = mage::hot::IndexedMatch(trained, desc, desc, std::vector<bool>(desc.size(), true),
+                                                    std::vector<bool>(desc.size(), true), 30, 1, tmatches);
         std::vector<mage::hot::DMatch> rmatches;
         const unsigned nr = mage::hot::RadiusMatch(kps, nullptr, nullptr, desc, kps, nullptr, desc, 2.0f, 30, 1, rmatches);
         std::vector<unsigned> outliers;
@@ -71,6 +76,7 @@ int main(int argc, char** argv)
         o.write((const char*)&ms, 4);
         o.write((const char*)&nr, 4);
         o.write((const char*)&ni, 4);
+        o.write((const char*)&nt, 4);
         std::cout << "keypoints " << n << " self-matches " << nm << " ba_mean_sq " << ms << "\n";
     } catch (const mage::hot::Error& e) {
         std::cerr << "mage error: " << e.what() << "\n";

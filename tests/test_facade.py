@@ -70,3 +70,5 @@ def test_facade_matches_python_api(gpu, tmp_path):
     nodes = pd[:7]
     tree = bow.OnlineBowTree(nodes, np.array([0, 3, 6, 6, 6, 6, 6, 6], np.uint32), np.arange(1, 7, dtype=np.uint32))
     assert ni == len(bow.IndexedMatch(tree, pd, pd))
+    nt = int(np.frombuffer(data[20 + 60 * n:24 + 60 * n], np.uint32)[0])
+    assert nt == len(bow.IndexedMatch(bow.OnlineBowTree.CreateTree(pd), pd, pd))

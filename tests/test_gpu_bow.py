@@ -109,3 +109,41 @@ def test_tree_validation(gpu):
     assert e.value.status == MAGE_EINVAL
     with pytest.raises(MageError):
         bow.OnlineBowTree(nd, np.array([0, 1, 1, 1], np.uint32), np.array([7], np.uint32))  # out of range
+
+
+@pytest.mark.parametrize("levels,branching,max_iter", [(2, 6, 12), (3, 4, 3), (1, 6, 12), (2, 6, 1), (2, 16, 12)])
+def test_create_tree_parity(gpu, oracle, frames, levels, branching, max_iter):
+    """OnlineBow::CreateTree on the GPU (mage_bow_train) vs the oracle's literal recursion: the
+    whole tree (node descriptors, child lists, ids) bit-exact."""
+    descs, _ = frames
+    rng = np.random.default_rng(11)
+    sets = [np.concatenate(descs), rng.integers(0, 256, (2500, 32), dtype=np.uint8),
+            np.repeat(rng.integers(0, 256, (3, 32), dtype=np.uint8), 40, axis=0), descs[0][:1], descs[0][:4]]
+    for d in sets:
+        t = bow.OnlineBowTree.CreateTree(d, levels, branching, max_iter)
+        ref = oracle.bow_train(d, levels, branching, max_iter)
+        for x, y in zip(t.tree(), ref):
+            assert np.array_equal(x, y)
+        assert np.array_equal(t.find_leaves(descs[3]), oracle.bow_find_leaves(ref, descs[3]))
+
+
+def test_create_tree_training_frames(gpu, oracle):
+    """BagOfWordsSettings::TrainingFrames (15) x 2000 features of 720p frames: the reference's
+    training set size."""
+    from mageslam_amd import orb
+
+    det = orb.OrbDetector(nfeatures=2000)
+    d = np.concatenate([det.DetectAndCompute(synth.frame(t, 1280, 720))[1] for t in range(15)])
+    t = bow.OnlineBowTree.CreateTree(d)
+    for x, y in zip(t.tree(), oracle.bow_train(d)):
+        assert np.array_equal(x, y)
+
+
+def test_create_tree_empty_and_errors(gpu):
+    t = bow.OnlineBowTree.CreateTree(np.zeros((0, 32), np.uint8))
+    nd, cs, ch = t.tree()
+    assert len(nd) == 1 and list(cs) == [0, 0] and len(ch) == 0
+    with pytest.raises(MageError):
+        bow.OnlineBowTree.CreateTree(np.zeros((10, 32), np.uint8), branching=17)
+    with pytest.raises(MageError):
+        bow.OnlineBowTree.CreateTree(np.zeros((10, 32), np.uint8), levels=0)

@@ -536,6 +536,41 @@ def test_bow_tree_builder_shape(oracle):
     assert all(cs[l] == cs[l + 1] for l in np.unique(leaves))
 
 
+def test_mt19937_known_answers(oracle):
+    """std::mt19937 as InitializeTraining default-constructs it (seed 5489): first output and the
+    10000th output required by the C++ standard ([rand.predef])."""
+    assert oracle.mt19937_output(5489, 1) == 3499211612
+    assert oracle.mt19937_output(5489, 10000) == 4123659995
+
+
+def test_msvc_shuffle_two_restatements(oracle):
+    from mageslam_amd import synth
+
+    for n in (0, 1, 2, 7, 1000, 30001):
+        a, b = oracle.msvc_shuffle(n), synth.msvc_shuffle(n)
+        assert np.array_equal(a, b) and sorted(a.tolist()) == list(range(n))
+
+
+@pytest.mark.parametrize("levels,branching,max_iter", [(2, 6, 12), (3, 4, 3), (1, 6, 12), (2, 6, 1), (2, 2, 12)])
+def test_bow_train_two_restatements(oracle, levels, branching, max_iter):
+    """CreateTree / Kmean (OnlineBow.cpp:325-614): the C oracle (literal recursive loops) against
+    the numpy restatement (matrix distances, vectorised majority), on ORB descriptors of two
+    golden frames, random descriptors and a degenerate set (duplicates -> empty clusters)."""
+    from mageslam_amd import synth
+
+    g = np.load(GOLDEN / "match_vga_t1_t0.npz")
+    rng = np.random.default_rng(7)
+    sets = [np.concatenate([g["desc_a"], g["desc_b"]]), rng.integers(0, 256, (900, 32), dtype=np.uint8),
+            np.repeat(rng.integers(0, 256, (3, 32), dtype=np.uint8), 40, axis=0), g["desc_a"][:5]]
+    for d in sets:
+        a = oracle.bow_train(d, levels, branching, max_iter)
+        b = synth.bow_tree(d, levels, branching, max_iter)
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))
+        nd, cs, ch = a
+        for i in range(len(nd)):  # ids grow downwards (Kmean appends children after the parent)
+            assert all(c > i for c in ch[cs[i]:cs[i + 1]])
+
+
 def test_indexed_match_semantics(oracle):
     """IndexedMatch (FeatureMatcher.cpp:192-292) on hand-made sets in one leaf: TrackMatch's
     second best keeps ties, the min-difference test, masks and the reverse check."""

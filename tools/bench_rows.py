@@ -11,6 +11,8 @@ fraction.  Run under `rocprofv3 --kernel-trace --stats` for the committed summar
   indexed   OnlineBow FindLeafNode + IndexedMatch (FeatureMatcher.cpp:192-292): 256 pairs, default tree
   remap     UndistortImage (ImagePreprocessor.cpp:106-120): 256 x 720p Rational6k frames
   kpundist  UndistortKeypoints (OrbFeatureDetector.cpp:30-62): 256 x 2000 keypoints
+  train     OnlineBow::CreateTree (OnlineBow.cpp:325-337): TrainingFrames (15) x 2000 descriptors,
+            2 levels x 6 branches, <= 12 Kmean iterations (host-driven: wall time per tree)
 """
 from __future__ import annotations
 
@@ -77,7 +79,7 @@ def leg(name, unit, units_per_launch, wall, kern, tag, bytes_per_launch):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--legs", default="radius,indexed,remap,kpundist")
+    p.add_argument("--legs", default="radius,indexed,remap,kpundist,train")
     p.add_argument("--batch", type=int, default=256)
     p.add_argument("--iters", type=int, default=10)
     a = p.parse_args()
@@ -90,7 +92,7 @@ def main():
     B, W, H, N = a.batch, 1280, 720, 2000
     legs = a.legs.split(",")
     frames = kp = desc = cnt = None
-    if {"radius", "indexed", "kpundist"} & set(legs):
+    if {"radius", "indexed", "kpundist", "train"} & set(legs):
         frames, kp, desc, cnt = frames_features(torch, B, W, H, N)
     if "radius" in legs:
         scratch = torch.zeros(B * N, dtype=torch.int32, device="cuda")
@@ -144,6 +146,22 @@ def main():
 
         wall, kern = timed(lib, kpundist, a.iters, torch)
         leg("a12 UndistortKeypoints", "frames/s", B, wall, kern, "orb.undistort", B * N * 28 * 2)
+
+    if "train" in legs:
+        tcnt = cnt[:15].cpu().numpy()
+        tdesc = np.concatenate([desc[i, : tcnt[i]].cpu().numpy() for i in range(15)])
+
+        def train():
+            bow.OnlineBowTree.CreateTree(tdesc).close()
+
+        wall, kern = timed(lib, train, a.iters, torch)
+        ka = kern.get("bow.km_assign", (0, 0.0))
+        ku = kern.get("bow.km_update", (0, 0.0))
+        out = {"row": "f4 CreateTree", "value": 1.0 / wall, "unit": "trees/s", "wall_ms_per_tree": wall * 1e3,
+               "descriptors": int(len(tdesc)),
+               "kernel_ms_per_tree": (ka[0] * ka[1] + ku[0] * ku[1]) / a.iters,
+               "kernels": {k: {"launches": n, "avg_ms": v} for k, (n, v) in kern.items()}}
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
