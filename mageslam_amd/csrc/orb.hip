@@ -924,6 +924,7 @@ struct ResizeParams {
     int dw, dh, dstride;
     long long dpitch;
     int xmax, xv;
+    int area2;  // both scales exactly 2: cv::resize takes resizeAreaFast_ instead (xv = its SIMD bound)
     const int* xofs;
     const uint32_t* alpha;  // a0 | a1 << 16
     const int* yofs;
@@ -937,6 +938,15 @@ __global__ __launch_bounds__(256) void resize_linear_kernel(const uint8_t* __res
     const int dx = blockIdx.x * blockDim.x + threadIdx.x;
     if (dx >= p.dw) return;
     const uint8_t* S = src + (long long)f * p.spitch;
+    if (p.area2) {
+        // is_area_fast && iscale_x == iscale_y == 2: INTER_LINEAR becomes INTER_AREA; the SSE2
+        // 8-wide blocks round (sum + 2) >> 2, the scalar tail cvRound(sum * 0.25f)
+        const uint8_t* s0 = S + (long long)(2 * dy) * p.sstride + 2 * dx;
+        const int sum = s0[0] + s0[1] + s0[p.sstride] + s0[p.sstride + 1];
+        dst[(long long)f * p.dpitch + (long long)dy * p.dstride + dx] =
+            (uint8_t)(dx < p.xv ? (sum + 2) >> 2 : __float2int_rn((float)sum * 0.25f));
+        return;
+    }
     const int sy = p.yofs[dy];
     const uint8_t* r0 = S + (long long)min(max(sy, 0), p.sh - 1) * p.sstride;
     const uint8_t* r1 = S + (long long)min(max(sy + 1, 0), p.sh - 1) * p.sstride;
@@ -1070,6 +1080,7 @@ struct LevelGeom {
     size_t off = 0, boff = 0, coff = 0;  // pyramid / blurred / candidate offsets (per frame)
     unsigned cand_cap = 0;
     int xmax = 0, xv = 0;                 // resize tables (levels > 0)
+    int area2 = 0;                        // exact 2x: INTER_AREA fast path
     size_t xofs = 0, yofs = 0, alpha = 0, beta = 0;
 };
 
@@ -1214,6 +1225,8 @@ void level_geometry(OrbDetector* o, int w, int h)
         while (xv <= dst.w - 16) xv += 16;
         while (xv < dst.w - 4) xv += 4;
         v.xv = xv;
+        v.area2 = scale_x == 2.0 && scale_y == 2.0;
+        if (v.area2) v.xv = dst.w / 8 * 8;
     }
     g.tab_ints = ints;
     g.tab_words = words;
@@ -1275,6 +1288,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             rp.dpitch = dst.pitch;
             rp.xmax = dst.xmax;
             rp.xv = dst.xv;
+            rp.area2 = dst.area2;
             rp.xofs = ints + dst.xofs;
             rp.yofs = ints + dst.yofs;
             rp.alpha = words + dst.alpha;

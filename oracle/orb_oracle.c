@@ -425,6 +425,22 @@ void oracle_resize_linear(const uint8_t* src, int sw, int sh, int sstride, uint8
                           int dstride)
 {
     const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    if (scale_x == 2.0 && scale_y == 2.0) {
+        /* cv::resize turns INTER_LINEAR into INTER_AREA when both scales are exactly 2
+         * (is_area_fast && iscale_x == iscale_y == 2); resizeAreaFast_: SSE2 8-wide blocks while
+         * dx <= w - 8 give (sum + 2) >> 2, the scalar tail saturate_cast<uchar>(sum * 0.25f)
+         * (cvRound: half to even) */
+        const int xv8 = dw / 8 * 8;
+        for (int dy = 0; dy < dh; dy++) {
+            const uint8_t* S0 = src + (size_t)(2 * dy) * sstride;
+            const uint8_t* S1 = S0 + sstride;
+            for (int dx = 0; dx < dw; dx++) {
+                const int sum = S0[2 * dx] + S0[2 * dx + 1] + S1[2 * dx] + S1[2 * dx + 1];
+                dst[(size_t)dy * dstride + dx] = (uint8_t)(dx < xv8 ? (sum + 2) >> 2 : cv_roundf((float)sum * 0.25f));
+            }
+        }
+        return;
+    }
     int* xofs = (int*)malloc(sizeof(int) * dw);
     short* ialpha = (short*)malloc(sizeof(short) * 2 * dw);
     int xmax = dw;

@@ -160,8 +160,10 @@ def test_720p_properties(gpu):
                                 dict(nlevels=3, patchSize=31),
                                 dict(nlevels=2, patchSize=15, useOrientation=True, scaleFactor=1.2),
                                 dict(nlevels=1, patchSize=31, useOrientation=True),
-                                dict(nlevels=8, patchSize=31, useOrientation=True, scaleFactor=1.3)])
-@pytest.mark.parametrize("size", [(640, 480), (1280, 720), (333, 211)])
+                                dict(nlevels=8, patchSize=31, useOrientation=True, scaleFactor=1.3),
+                                # exact 2x levels: cv::resize's INTER_AREA fast path
+                                dict(nlevels=3, patchSize=31, useOrientation=True, scaleFactor=2.0)])
+@pytest.mark.parametrize("size", [(640, 480), (1280, 720), (333, 211), (1000, 600)])
 def test_pyramid_orientation_matches_oracle(gpu, oracle, kw, size):
     w, h = size
     nfeat = 2000

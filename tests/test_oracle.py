@@ -146,6 +146,12 @@ def test_resize_linear_properties(oracle):
     blocks = rng.integers(0, 256, (20, 30), dtype=np.uint8)
     big = np.repeat(np.repeat(blocks, 2, 0), 2, 1)
     assert np.array_equal(oracle.resize_linear(big, 30, 20), blocks)
+    # exact 2x takes cv::resize's INTER_AREA fast path: (sum + 2) >> 2 in the SSE2 8-wide blocks,
+    # cvRound(sum * 0.25f) (half to even) in the tail — a 2x2 sum of 10 gives 3 there and 2 here
+    tens = np.tile(np.array([[2, 3], [2, 3]], np.uint8), (1, 13))
+    assert oracle.resize_linear(tens, 13, 1).tolist() == [[3] * 8 + [2] * 5]
+    fourteen = np.tile(np.array([[3, 4], [3, 4]], np.uint8), (1, 13))  # 3.5: half-up and half-even agree
+    assert oracle.resize_linear(fourteen, 13, 1).tolist() == [[4] * 13]
 
 
 def test_fast_atan2_accuracy(oracle):
