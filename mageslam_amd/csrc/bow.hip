@@ -142,9 +142,43 @@ __device__ __forceinline__ void track_run(const unsigned long long* keys, int lo
     second = m2;
 }
 
+// the same over B's run with B's descriptors staged in LDS in key order (position k holds the
+// descriptor of keys[k]): a 16-lane group reads 16 consecutive 32-byte entries
+constexpr int IM_STAGE = 2048;  // B sets up to NumFeatures-sized 2048 are staged (64 KB of LDS)
+
+__device__ __forceinline__ void track_run_lds(const unsigned long long* keys, int lo, int hi, int sub,
+                                              const uint4* __restrict__ sdesc, const uint4& qa, const uint4& qb,
+                                              unsigned max_h, unsigned& bestk, unsigned& second)
+{
+    unsigned m1 = max_h << 12 | 0xFFFu, m2 = max_h;
+    for (int k = lo + sub; k < hi; k += IM_GROUP) {
+        const unsigned idx = (unsigned)(keys[k] & 0xFFFFFFFFull);
+        const uint4 ta = sdesc[2 * k], tb = sdesc[2 * k + 1];
+        const unsigned d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w) +
+                           __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
+        if (d >= max_h) continue;
+        const unsigned key = d << 12 | idx;
+        if (key < m1) {
+            m2 = min(m2, m1 >> 12);
+            m1 = key;
+        } else {
+            m2 = min(m2, d);
+        }
+    }
+#pragma unroll
+    for (int off = IM_GROUP / 2; off > 0; off >>= 1) {
+        const unsigned o1 = (unsigned)__shfl_xor((int)m1, off), o2 = (unsigned)__shfl_xor((int)m2, off);
+        m2 = min(max(m1 >> 12, o1 >> 12), min(m2, o2));
+        m1 = min(m1, o1);
+    }
+    bestk = m1;
+    second = m2;
+}
+
 __global__ __launch_bounds__(SORT_THREADS) void indexed_match_kernel(IndexedParams p)
 {
     __shared__ unsigned long long keysA[IM_MAX], keysB[IM_MAX];
+    __shared__ uint4 sdescB[2 * IM_STAGE];
     __shared__ int res[IM_MAX];
     __shared__ int wsum[SORT_THREADS / kWave];
     __shared__ int s_cnt[2], s_base;
@@ -188,6 +222,15 @@ __global__ __launch_bounds__(SORT_THREADS) void indexed_match_kernel(IndexedPara
     for (int i = tid; i < ca; i += SORT_THREADS) keysA[i] = ~keysA[i];
     for (int i = tid; i < cb; i += SORT_THREADS) keysB[i] = ~keysB[i];
     __syncthreads();
+    // B's descriptors in key order into LDS (each is read by ~all A features of its leaf)
+    const bool staged = cb <= IM_STAGE;
+    if (staged) {
+        for (int i = tid; i < 2 * cb; i += SORT_THREADS) {
+            const unsigned idx = (unsigned)(keysB[i >> 1] & 0xFFFFFFFFull);
+            sdescB[i] = reinterpret_cast<const uint4*>(db + 32ull * idx)[i & 1];
+        }
+        __syncthreads();
+    }
 
     // 2. forward TrackMatch over B's run of the leaf, then the reverse check over A's run
     const unsigned max_h = (unsigned)(p.max_dist + 1);
@@ -200,7 +243,10 @@ __global__ __launch_bounds__(SORT_THREADS) void indexed_match_kernel(IndexedPara
             const uint4 qb = *reinterpret_cast<const uint4*>(da + 32ll * i + 16);
             const int lo = lower_bound_u64(keysB, cb, leaf << 32), hi = lower_bound_u64(keysB, cb, (leaf + 1) << 32);
             unsigned bk, sd;
-            track_run(keysB, lo, hi, sub, db, qa, qb, max_h, bk, sd);
+            if (staged)
+                track_run_lds(keysB, lo, hi, sub, sdescB, qa, qb, max_h, bk, sd);
+            else
+                track_run(keysB, lo, hi, sub, db, qa, qb, max_h, bk, sd);
             const unsigned bd = bk >> 12;
             if (bd < max_h && (sd >= max_h || (int)(sd - bd) >= p.min_diff)) {
                 const int j = (int)(bk & 0xFFFu);
