@@ -3,16 +3,17 @@
 // target KeypointSpatialIndex (Image/KeypointSpatialIndex.cpp:46-106) replaced by an LDS-sorted
 // band index.
 //
-// One 1024-thread workgroup per (query set, target set) pair:
+// One 1024-thread workgroup per (query set, target set) pair (or several, see radius_match_kernel):
 //   1. targets -> 64-bit keys (octave, orderable f32 y, index), sorted ascending in LDS (the
 //      shared hybrid bitonic sort); the R-tree box query |x - qx| <= r, |y - qy| <= r, same
 //      octave becomes a binary search for the y band of the query's octave plus an exact f32
 //      box test on each band entry;
-//   2. one wave per query: lanes scan the band, mask, 32-byte Hamming distance.  The reference
+//   2. a 16-lane group per query: lanes scan the band (positions and descriptors staged in LDS in
+//      band order), mask, 32-byte Hamming distance.  The reference
 //      visits candidates in R-tree order and keeps "second best" = the previous best at the last
 //      improvement (:425-437).  With the deterministic ascending-index order
 //      that is order-free: best = min d (lowest index on ties, only if d <= maxDist) and
-//      second = min(maxDist + 1, min d over candidates with a lower index) — two wave reductions;
+//      second = min(maxDist + 1, min d over candidates with a lower index) — two group reductions;
 //      accepted when second - best > minDiff (:441);
 //   3. batch post-pass (:342-371): a match survives when its distance is the unique minimum among
 //      the matches to its target (LDS atomicMin, then a count of the minima), ordered compaction in
@@ -29,7 +30,8 @@
 namespace mage {
 namespace {
 
-constexpr int RM_MAXT = 4096;  // targets per pair held in LDS (NumFeatures-sized sets)
+constexpr int RM_MAXT = 4096;   // targets per pair held in LDS (NumFeatures-sized sets)
+constexpr int RM_STAGE = 2048;  // target sets up to this size also get positions + descriptors in LDS
 
 struct RadiusParams {
     const mage_keypoint* qkp;
@@ -75,10 +77,13 @@ __device__ __forceinline__ int lower_bound_keys(const unsigned long long* keys, 
     return lo;
 }
 
-__device__ __forceinline__ unsigned wave_min(unsigned v)
+constexpr int RM_GROUP = 16;  // lanes per query (a band holds ~20-150 candidates)
+constexpr int RM_GROUPS = SORT_THREADS / RM_GROUP;
+
+__device__ __forceinline__ unsigned group_min(unsigned v)
 {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, off));
+    for (int off = RM_GROUP / 2; off > 0; off >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, off));
     return v;
 }
 
@@ -136,17 +141,18 @@ __device__ void radius_post(const RadiusParams& p, int pr, const int* res, int n
     if (tid == 0) p.n_out[pr] = (uint32_t)s_base;
 }
 
-// blockIdx.y of gridDim.y workgroups handles every gridDim.y-th wave slot of the pair's queries
+// blockIdx.y of gridDim.y workgroups handles every gridDim.y-th group slot of the pair's queries
 // (gridDim.y > 1 spreads one pair over many CUs: the per-frame tracking call is a single pair);
 // FUSED (gridDim.y == 1) runs the post-pass in the same workgroup, otherwise radius_post_kernel does
 template <bool FUSED>
 __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams p)
 {
     __shared__ unsigned long long keys[RM_MAXT];
+    __shared__ float2 sxy[RM_STAGE];
+    __shared__ uint4 sdesc[2 * RM_STAGE];
     __shared__ int wsum[SORT_THREADS / kWave];
     __shared__ int s_base;
-    const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int pr = blockIdx.x, tid = threadIdx.x;
     const int nq = (int)p.nq[pr], ntr = (int)p.nt[pr];
     const mage_keypoint* qkp = p.qkp + pr * p.q_pitch;
     const mage_keypoint* tkp = p.tkp + pr * p.t_pitch;
@@ -173,13 +179,27 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
     sort_desc(keys, P);
     for (int i = tid; i < ntr; i += SORT_THREADS) keys[i] = ~keys[i];
     __syncthreads();
+    // targets in key order into LDS: a band is then a contiguous run of positions + descriptors;
+    // a masked target gets a NaN position, which fails the box test exactly like the mask check
+    const bool staged = ntr <= RM_STAGE;
+    if (staged) {
+        for (int i = tid; i < 2 * ntr; i += SORT_THREADS) {
+            const int t = (int)(keys[i >> 1] & 0xFFFFFFu);
+            sdesc[i] = reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t)[i & 1];
+            if (!(i & 1)) {
+                const bool off = tmask && !tmask[t];
+                sxy[i >> 1] = off ? make_float2(__int_as_float(0x7FC00000), 0.f) : make_float2(tkp[t].x, tkp[t].y);
+            }
+        }
+        __syncthreads();
+    }
 
-    // 2. one wave per query
+    // 2. a 16-lane group per query (four queries per wave)
     const float r = p.radius;
-    constexpr int NW = SORT_THREADS / kWave;
-    for (int q = (int)blockIdx.y * NW + wave; q < nq; q += NW * (int)gridDim.y) {
+    const int group = tid / RM_GROUP, sub = tid % RM_GROUP;
+    for (int q = (int)blockIdx.y * RM_GROUPS + group; q < nq; q += RM_GROUPS * (int)gridDim.y) {
         if (qmask && !qmask[q]) {
-            if (lane == 0) res[q] = -1;
+            if (sub == 0) res[q] = -1;
             continue;
         }
         const float px = qpos ? qpos[2 * q] : qkp[q].x, py = qpos ? qpos[2 * q + 1] : qkp[q].y;
@@ -191,39 +211,55 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
         uint4 qb = *reinterpret_cast<const uint4*>(qdesc + 32 * (long long)q + 16);
         // pass 1: best = min (d << 12 | t) over the box candidates
         unsigned bestk = 0xFFFFFFFFu;
-        for (int i = lo + lane; i < hi; i += kWave) {
+        for (int i = lo + sub; i < hi; i += RM_GROUP) {
             const int t = (int)(keys[i] & 0xFFFFFFu);
-            const float tx = tkp[t].x, ty = tkp[t].y;
-            if (!(tx >= x0 && tx <= x1 && ty >= y0 && ty <= y1)) continue;
-            if (tmask && !tmask[t]) continue;
-            const uint4 ta = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t);
-            const uint4 tb = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t + 16);
+            uint4 ta, tb;
+            if (staged) {
+                const float2 xy = sxy[i];
+                if (!(xy.x >= x0 && xy.x <= x1 && xy.y >= y0 && xy.y <= y1)) continue;
+                ta = sdesc[2 * i];
+                tb = sdesc[2 * i + 1];
+            } else {
+                const float tx = tkp[t].x, ty = tkp[t].y;
+                if (!(tx >= x0 && tx <= x1 && ty >= y0 && ty <= y1)) continue;
+                if (tmask && !tmask[t]) continue;
+                ta = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t);
+                tb = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t + 16);
+            }
             const unsigned d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w) +
                                __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
             bestk = min(bestk, d << 12 | (unsigned)t);
         }
-        bestk = wave_min(bestk);
+        bestk = group_min(bestk);
         const int best = bestk == 0xFFFFFFFFu ? INT_MAX : (int)(bestk >> 12), tbest = (int)(bestk & 0xFFFu);
         if (best > p.max_dist) {
-            if (lane == 0) res[q] = -1;
+            if (sub == 0) res[q] = -1;
             continue;
         }
         // pass 2: second = min(maxDist + 1, min d over candidates with a lower target index)
         unsigned sec = (unsigned)(p.max_dist + 1);
-        for (int i = lo + lane; i < hi; i += kWave) {
+        for (int i = lo + sub; i < hi; i += RM_GROUP) {
             const int t = (int)(keys[i] & 0xFFFFFFu);
             if (t >= tbest) continue;
-            const float tx = tkp[t].x, ty = tkp[t].y;
-            if (!(tx >= x0 && tx <= x1 && ty >= y0 && ty <= y1)) continue;
-            if (tmask && !tmask[t]) continue;
-            const uint4 ta = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t);
-            const uint4 tb = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t + 16);
+            uint4 ta, tb;
+            if (staged) {
+                const float2 xy = sxy[i];
+                if (!(xy.x >= x0 && xy.x <= x1 && xy.y >= y0 && xy.y <= y1)) continue;
+                ta = sdesc[2 * i];
+                tb = sdesc[2 * i + 1];
+            } else {
+                const float tx = tkp[t].x, ty = tkp[t].y;
+                if (!(tx >= x0 && tx <= x1 && ty >= y0 && ty <= y1)) continue;
+                if (tmask && !tmask[t]) continue;
+                ta = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t);
+                tb = *reinterpret_cast<const uint4*>(tdesc + 32 * (long long)t + 16);
+            }
             const unsigned d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w) +
                                __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
             sec = min(sec, d);
         }
-        sec = wave_min(sec);
-        if (lane == 0) res[q] = ((int)sec - best > p.min_diff) ? (tbest << 9 | best) : -1;
+        sec = group_min(sec);
+        if (sub == 0) res[q] = ((int)sec - best > p.min_diff) ? (tbest << 9 | best) : -1;
     }
     if constexpr (FUSED) {
         __syncthreads();
