@@ -50,6 +50,11 @@ def parse():
     p.add_argument("--trajectory-csv", default="", help="rank 0 writes the gathered trajectories (ExportFossilCsv)")
     p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--streams", type=int, default=1,
+                   help="HIP streams the ORB batches are pipelined over (the headline uses 1: with overlapping "
+                        "batches the per-kernel durations behind the roofline stretch)")
+    p.add_argument("--pipelined-streams", type=int, default=2,
+                   help="also report the ORB rate pipelined over this many streams (0: skip; 1 GPU runs only)")
     p.add_argument("--no-all-cores", action="store_true", help="skip the all-host-cores CPU baselines")
     p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
     p.add_argument("--cpu-dry-run", action="store_true", help="gloo rehearsal of the multi-rank flow (tests)")
@@ -153,30 +158,57 @@ def run_orb(args, rank, world, local_rank, torch, dist):
     F = max(B, (args.frames // B) * B)
     dev = torch.device("cuda", local_rank)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    det = orb.OrbDetector(nfeatures=N, device=local_rank)
+    # batches are pipelined over NSTR HIP streams (one detector each: its scratch is per detector)
+    # and NSTR + 1 buffer sets: batch s+1's FAST pass overlaps batch s's latency-bound select /
+    # describe / match kernels.  Only real dependency: batch s matches its first frame against the
+    # last frame of batch s-1 (an event on s-1's extraction).
+    NSTR = max(1, args.streams)
+    NSET = NSTR + 1 if NSTR > 1 else 1
+    dets = [orb.OrbDetector(nfeatures=N, device=local_rank) for _ in range(NSTR)]
+    det = dets[0]
     frames = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
     orb.synth_frames_device(frames, F, W, H, 0, multigpu.sequence_seed(synth.FRAME_SEED, rank), stream=stream)
-    kp = torch.zeros((B + 1, N * 28), dtype=torch.uint8, device=dev)
-    desc = torch.zeros((B + 1, N, 32), dtype=torch.uint8, device=dev)
-    cnt = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-    mt = torch.zeros((B, N * 16), dtype=torch.uint8, device=dev)
-    nm = torch.zeros(B, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    sets = [dict(kp=torch.zeros((B + 1, N * 28), dtype=torch.uint8, device=dev),
+                 desc=torch.zeros((B + 1, N, 32), dtype=torch.uint8, device=dev),
+                 cnt=torch.zeros(B + 1, dtype=torch.int32, device=dev),
+                 mt=torch.zeros((B, N * 16), dtype=torch.uint8, device=dev),
+                 nm=torch.zeros(B, dtype=torch.int32, device=dev)) for _ in range(NSET)]
+    streams = [torch.cuda.current_stream(dev)] if NSTR == 1 else [torch.cuda.Stream(dev) for _ in range(NSTR)]
+    ev_x = [torch.cuda.Event() for _ in range(NSET)]  # extraction of the batch in set i done
+    ev_m = [torch.cuda.Event() for _ in range(NSET)]  # match of the batch in set i done (set reusable)
 
     def step(s):
         start = (s * B) % F
         fr = frames[start:start + B]
-        det.detect_and_compute_batch_device(fr, W, H, kp[1:], desc[1:], cnt[1:], N, stream=stream)
-        matcher.match_batch_device(desc[1:], N * 32, cnt[1:], desc[:-1], N * 32, cnt[:-1], B, 30, 1,
-                                   mt, N, nm, stream=stream)
-        # the batch's last frame becomes the predecessor of the next batch's first frame
-        kp[0].copy_(kp[B])
-        desc[0].copy_(desc[B])
-        cnt[0:1].copy_(cnt[B:B + 1])
+        X, P = sets[s % NSET], sets[(s - 1) % NSET]
+        st = streams[s % NSTR]
+        d = dets[s % NSTR]
+        with torch.cuda.stream(st):
+            if NSET > 1:
+                st.wait_event(ev_m[s % NSET])  # the previous batch in this set has been matched
+            d.detect_and_compute_batch_device(fr, W, H, X["kp"][1:], X["desc"][1:], X["cnt"][1:], N,
+                                              stream=st.cuda_stream)
+            ev_x[s % NSET].record(st)
+            if NSET > 1:
+                # the previous batch's last frame is the predecessor of this batch's first frame
+                st.wait_event(ev_x[(s - 1) % NSET])
+                X["kp"][0].copy_(P["kp"][B])
+                X["desc"][0].copy_(P["desc"][B])
+                X["cnt"][0:1].copy_(P["cnt"][B:B + 1])
+            matcher.match_batch_device(X["desc"][1:], N * 32, X["cnt"][1:], X["desc"][:-1], N * 32, X["cnt"][:-1], B,
+                                       30, 1, X["mt"], N, X["nm"], stream=st.cuda_stream)
+            if NSET == 1:  # one set: the last frame moves to slot 0 after the match
+                X["kp"][0].copy_(X["kp"][B])
+                X["desc"][0].copy_(X["desc"][B])
+                X["cnt"][0:1].copy_(X["cnt"][B:B + 1])
+            ev_m[s % NSET].record(st)
 
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize(dev)
-    det.device_status()
+    for d in dets:
+        d.device_status()
     lib = _lib.load()
     if args.profile:
         lib.mage_profile_reset()
@@ -191,7 +223,10 @@ def run_orb(args, rank, world, local_rank, torch, dist):
     el = time.perf_counter() - t0
     lib.mage_profile_enable(0)
     kern = _lib.profile_report() if args.profile else {}
-    det.device_status()
+    for d in dets:
+        d.device_status()
+    last = sets[(args.warmup + args.steps - 1) % NSET]
+    cnt, nm = last["cnt"], last["nm"]
     el_max = multigpu.max_over_ranks(el, dev, dist)
     # end-of-run exchange (RCCL over xGMI): per-frame (keypoints, matches) of the last batch
     summary = torch.stack([cnt[1:].to(torch.int64), nm.to(torch.int64)], 1)
@@ -561,6 +596,18 @@ def main():
     dist = multigpu.init("nccl", local_rank)
 
     orb_res = run_orb(args, rank, world, local_rank, torch, dist)
+    pipe_res = None
+    if world == 1 and args.pipelined_streams > 1 and args.streams == 1:
+        import copy
+
+        pa = copy.copy(args)
+        pa.streams, pa.profile = args.pipelined_streams, False
+        pr = run_orb(pa, rank, world, local_rank, torch, dist)
+        pipe_res = {"value": pr["value"], "unit": "frames/s", "ms_per_step": pr["ms_per_step"],
+                    "hip_streams": pa.streams, "mean_matches": pr["mean_matches"],
+                    "note": "the same workload with batch s+1's extraction overlapping batch s's select / describe "
+                            "/ match on another stream (not the headline: overlapping batches stretch the "
+                            "per-kernel durations the roofline is priced on)"}
     ba_res, g = (None, None) if args.no_ba else run_ba(args, local_rank, torch)
     pose_res, pb = (None, None) if args.no_pose else run_pose(args, rank, world, local_rank, torch, dist)
     track_res, tctx = (None, None) if (args.no_tracking or rank != 0) else run_tracking(args, local_rank, torch)
@@ -584,13 +631,15 @@ def main():
             "config": {"workload": f"C2: {args.width}x{args.height} synthetic pan sequence, {args.features} "
                                    f"features/frame, ORB extract + two-way match vs previous frame"
                                    + (f"; C5: {world} independent sequences, one per GPU" if world > 1 else ""),
-                       "frames_per_step": args.batch, "resident_frames_per_rank": max(args.batch, (args.frames // args.batch) * args.batch),
+                       "frames_per_step": args.batch, "hip_streams": args.streams, "resident_frames_per_rank": max(args.batch, (args.frames // args.batch) * args.batch),
                        "parallelism": f"sequence-sharded x{world}"},
             "roofline": orb_res.get("roofline"),
             "kernels": orb_res["kernels"],
             "mean_keypoints": orb_res["mean_keypoints"],
             "mean_matches": orb_res["mean_matches"],
         }
+        if pipe_res is not None:
+            out["pipelined"] = pipe_res
         if ba_res is not None:
             out["ba"] = ba_res
         if pose_res is not None:
