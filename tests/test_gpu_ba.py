@@ -182,13 +182,14 @@ def tethered_extra_camera():
     return g2
 
 
+@pytest.mark.parametrize("problems,obs", [(96, 500), (600, 200)])  # 512- and 256-thread kernel variants
 @pytest.mark.parametrize("steps,huber,maxe", [(3, 4.0, 36.0), (4, 0.9, 4.5 ** 2)])
-def test_pose_batch_matches_per_frame_oracle(gpu, steps, huber, maxe):
+def test_pose_batch_matches_per_frame_oracle(gpu, steps, huber, maxe, problems, obs):
     """Batched OptimizeCameraPose (TrackLocalMap.cpp:96-140 settings: 3 x 4.0 / 6^2, then
     4 x 0.9 / 4.5^2) vs a fresh oracle BundlerLib per frame."""
     from oracle import oracle as O
 
-    pb = synth.pose_batch(problems=96, obs=500)
+    pb = synth.pose_batch(problems=problems, obs=obs)
     g = bundler.OptimizeCameraPoses(pb, steps, maxe, huber)
     o = O.pose_batch(pb, steps, huber, maxe)
     assert np.array_equal(g["stats"], o["stats"])

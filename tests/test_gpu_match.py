@@ -168,20 +168,22 @@ def test_radius_match_edges(gpu, oracle):
         matcher.RadiusMatch(qk, qd, big, np.zeros((4097, 32), np.uint8), 10.0)
 
 
-def test_radius_match_batch_device(gpu, oracle):
+@pytest.mark.parametrize("pairs", [3, 130])  # split (< 128 pairs: several workgroups per pair) and fused paths
+def test_radius_match_batch_device(gpu, oracle, pairs):
     import torch
 
     from mageslam_amd._lib import KP_DTYPE
 
-    pairs, pitch = 3, 2000
+    pitch = 2000
     sets = []
-    for t in range(pairs + 1):
+    for t in range(4):
         _, k, d = oracle.orb_detect(synth.frame(t, 640, 480), oracle.default_settings(pitch))
         sets.append((k, d))
     kp = np.zeros((pairs + 1, pitch), KP_DTYPE)
     de = np.zeros((pairs + 1, pitch, 32), np.uint8)
     nn = np.zeros(pairs + 1, np.uint32)
-    for i, (k, d) in enumerate(sets):
+    for i in range(pairs + 1):
+        k, d = sets[i % 4]
         kp[i, : len(k)] = k
         de[i, : len(k)] = d
         nn[i] = len(k)
@@ -198,8 +200,12 @@ def test_radius_match_batch_device(gpu, oracle):
                                       pairs, 12.0, 30, 1, scratch, out, pitch, nout, status)
     torch.cuda.synchronize()
     assert int(status[0]) == 0
+    ref = {}
     for p in range(pairs):
-        o = oracle.radius_match(sets[p + 1][0], sets[p + 1][1], sets[p][0], sets[p][1], 12.0)
+        key = (p + 1) % 4, p % 4
+        if key not in ref:
+            ref[key] = oracle.radius_match(sets[key[0]][0], sets[key[0]][1], sets[key[1]][0], sets[key[1]][1], 12.0)
+        o = ref[key]
         n = int(nout[p])
         assert n == len(o)
         assert np.array_equal(out[p, : 16 * n].cpu().numpy(), dm_bytes(o))
