@@ -147,3 +147,20 @@ def test_create_tree_empty_and_errors(gpu):
         bow.OnlineBowTree.CreateTree(np.zeros((10, 32), np.uint8), branching=17)
     with pytest.raises(MageError):
         bow.OnlineBowTree.CreateTree(np.zeros((10, 32), np.uint8), levels=0)
+
+
+def test_indexed_and_radius_large_sets(gpu, oracle):
+    """Sets above the 2048 entries staged in LDS (the kernels' global-memory path): 3000-feature
+    frames through IndexedMatch and RadiusMatch, bit-exact vs the oracle."""
+    from mageslam_amd import matcher, orb
+
+    det = orb.OrbDetector(nfeatures=3000)
+    (ka, da), (kb, db) = (det.DetectAndCompute(synth.frame(t, 1280, 720)) for t in (0, 1))
+    assert len(da) > 2048 and len(db) > 2048
+    tree = synth.bow_tree(np.concatenate([da, db]))
+    got = bow.IndexedMatch(bow.OnlineBowTree(*tree), da, db)
+    ref = oracle.indexed_match(tree, da, db)
+    assert np.array_equal(got.view(np.uint8), ref.view(np.uint8))
+    got = matcher.RadiusMatch(kb, db, ka, da, 15.0)
+    ref = oracle.radius_match(kb, db, ka, da, 15.0)
+    assert len(got) > 0 and np.array_equal(got.view(np.uint8), ref.view(np.uint8))
