@@ -454,19 +454,26 @@ def run_tracking(args, local_rank, torch):
     p0 = tracking.Pose(seq.R[0], seq.t[0])
     be = tracking.GpuBackend(args.features, device=local_rank, batch=64)
     feats = be.extract(frames[:8])  # warm-up
-    tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
+    tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, device=local_rank)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     feats = be.extract(frames)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    res = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
+    res = tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, device=local_rank)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
+    # the same loop driven from Python (tracking.track over GpuBackend): identical results
+    py = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
+    t3 = time.perf_counter()
+    same = py.matches == res.matches and all(np.array_equal(a.t, b.t) and np.array_equal(a.R, b.R)
+                                             for a, b in zip(py.poses, res.poses))
     gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)])
     return {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose)",
             "value": T / (t2 - t0), "unit": "frames/s", "frames": T, "dtype": "u8 / f64",
             "extract_ms_per_frame": 1000 * (t1 - t0) / T, "track_ms_per_frame": 1000 * (t2 - t1) / T,
+            "loop": "native (mage_track_sequence)", "python_loop_track_ms_per_frame": 1000 * (t3 - t2) / T,
+            "python_loop_identical": bool(same),
             "mean_matches": float(np.mean(res.matches[1:])), "mean_inliers": float(np.mean(res.inliers[1:])),
             "keyframes": len(res.keyframes), "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
             "config": {"workload": f"C4: {T}-frame {args.width}x{args.height} hand-held pan over a textured plane "

@@ -34,6 +34,7 @@ EXPORTS = [
     "mage_ba_set_points", "mage_ba_set_observations", "mage_ba_set_lambda", "mage_ba_get_lambda",
     "mage_ba_set_tethers", "mage_ba_step", "mage_ba_get_poses", "mage_ba_get_points",
     "mage_ba_get_stats", "mage_ba_get_state_f64", "mage_ba_pose_batch", "mage_ba_pose_batch_device",
+    "mage_track_sequence",
 ]
 
 
@@ -71,6 +72,16 @@ class OrbSettingsC(C.Structure):
                 ("strong_response", C.c_int32), ("min_robust_factor", C.c_float),
                 ("max_robust_factor", C.c_float), ("num_cells_x", C.c_int32),
                 ("num_cells_y", C.c_int32)]
+
+
+class TrackSettingsC(C.Structure):
+    """mage_track_settings (include/mage_hot.h)."""
+    _fields_ = [("search_radius", C.c_float), ("wider_search_radius", C.c_float),
+                ("extra_wider_search_radius", C.c_float), ("small_match_ratio", C.c_double),
+                ("min_matches", C.c_uint32), ("max_hamming", C.c_int32), ("min_hamming_difference", C.c_int32),
+                ("initial_steps", C.c_uint32), ("initial_huber", C.c_float), ("initial_max_error", C.c_double),
+                ("final_steps", C.c_uint32), ("final_huber", C.c_float), ("final_max_error", C.c_double),
+                ("refinement_info", C.c_float), ("keyframe_ratio", C.c_double), ("keyframe_min", C.c_uint32)]
 
 
 class BAStats(C.Structure):
@@ -184,5 +195,6 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_ba_get_points", st, vp, vp)
     sig("mage_ba_get_state_f64", st, vp, vp, vp)
     sig("mage_ba_get_stats", st, vp, C.POINTER(BAStats))
+    sig("mage_track_sequence", st, vp, vp, vp, u32, vp, vp, C.c_double, vp, vp, vp, vp, vp, C.c_int)
     sig("mage_ba_pose_batch", st, u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp, C.c_int)
     sig("mage_ba_pose_batch_device", st, u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp, vp)

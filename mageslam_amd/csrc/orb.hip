@@ -1246,7 +1246,10 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
     if ((r = o->cand.reserve((size_t)batch * g.cand_total * 4)) != MAGE_OK) return r;
     if ((r = o->counts.reserve((size_t)batch * L * 4)) != MAGE_OK) return r;
     if ((r = o->xy.reserve((size_t)batch * std::max(cap, 1u) * 4)) != MAGE_OK) return r;
+    // the sticky status word starts at zero (a fresh allocation may hold stale bytes)
+    const bool fresh_status = o->status.ptr == nullptr;
     if ((r = o->status.reserve(4)) != MAGE_OK) return r;
+    if (fresh_status) MAGE_HIP(hipMemsetAsync(o->status.ptr, 0, 4, st));
     if (multi && (r = o->lvl.reserve((size_t)batch * std::max(cap, 1u) * 2)) != MAGE_OK) return r;
     if (L > 1 && (r = o->pyr.reserve((size_t)batch * g.pyr_bytes)) != MAGE_OK) return r;
     if (!g.tab_valid && L > 1) {

@@ -1,0 +1,231 @@
+// track.cpp — the C4 tracking loop in native host code over the hot-path C-ABI
+// (mage_radius_match, mage_ba_pose_batch): per frame PoseEstimator::TryEstimatePoseFromKeyframe
+// (PoseEstimator.cpp:439-607: prediction, ProjectUndistorted of the reference keyframe's map
+// points, RadiusMatch at SearchRadius / WiderSearchRadius / ExtraWiderSearchRadius) and
+// TrackLocalMap's two OptimizeCameraPose passes (TrackLocalMap.cpp:37-140, 421-501), then the
+// keyframe decision of NewKeyFrameDecision.cpp:196.
+//
+// It is the same specification as mageslam_amd/tracking.py's `track` (which also runs on the CPU
+// oracle for parity): every expression below is evaluated in the same order and precision as
+// there (elementwise products, left-to-right sums, float32 projection, float64 poses; compiled
+// with -ffp-contract=off), so the two loops produce identical poses, matches and keyframes.
+// Map creation is not the reference's (its triangulation is outside the hot path): a keyframe's
+// keypoints are back-projected onto the scene plane Z = plane_z.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+
+namespace {
+
+struct Pose {
+    double R[9];  // world -> camera, row-major
+    double t[3];
+};
+
+void mv(const double* R, const double* v, double* out)
+{
+    for (int i = 0; i < 3; i++) out[i] = (R[3 * i] * v[0] + R[3 * i + 1] * v[1]) + R[3 * i + 2] * v[2];
+}
+
+Pose inverse(const Pose& p)
+{
+    Pose q;
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) q.R[3 * r + c] = p.R[3 * c + r];
+    double m[3];
+    mv(q.R, p.t, m);
+    for (int i = 0; i < 3; i++) q.t[i] = -m[i];
+    return q;
+}
+
+Pose mul(const Pose& a, const Pose& b)
+{
+    Pose o;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            o.R[3 * i + j] = (a.R[3 * i] * b.R[j] + a.R[3 * i + 1] * b.R[3 + j]) + a.R[3 * i + 2] * b.R[6 + j];
+    double m[3];
+    mv(a.R, b.t, m);
+    for (int i = 0; i < 3; i++) o.t[i] = m[i] + a.t[i];
+    return o;
+}
+
+struct Keyframe {
+    std::vector<mage_keypoint> kp;
+    std::vector<uint8_t> desc;
+    std::vector<float> pts;  // n x 3
+};
+
+// keypoint rays of `pose` meet the plane Z = plane_z
+void backproject(const mage_keypoint* kp, uint32_t n, const Pose& p, const double K[4], double plane_z,
+                 std::vector<float>& out)
+{
+    const double fx = K[0], fy = K[1], cx = K[2], cy = K[3];
+    const double* R = p.R;
+    double C[3];
+    for (int j = 0; j < 3; j++) C[j] = -((R[j] * p.t[0] + R[3 + j] * p.t[1]) + R[6 + j] * p.t[2]);
+    out.resize(3ull * n);
+    for (uint32_t i = 0; i < n; i++) {
+        const double u = ((double)kp[i].x - cx) / fx, v = ((double)kp[i].y - cy) / fy;
+        double d[3];
+        for (int j = 0; j < 3; j++) d[j] = (u * R[j] + v * R[3 + j]) + R[6 + j];
+        const double lam = (plane_z - C[2]) / d[2];
+        for (int j = 0; j < 3; j++) out[3 * i + j] = (float)(C[j] + lam * d[j]);
+    }
+}
+
+// optimise one pose: returns the new pose and the outlier flags of the observations
+mage_status optimize(const Pose& pred, const double K[4], const std::vector<float>& pts, const std::vector<float>& uv,
+                     float info, uint32_t steps, float huber, float max_err_sq, int device, Pose& out,
+                     std::vector<uint8_t>& outlier)
+{
+    const uint32_t n = (uint32_t)(uv.size() / 2);
+    float pos[3], r9[9], intr[4] = {(float)K[2], (float)K[3], (float)K[0], (float)K[1]};
+    for (int i = 0; i < 3; i++) pos[i] = (float)pred.t[i];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) r9[3 * c + r] = (float)pred.R[3 * r + c];  // column-major
+    const uint32_t os[2] = {0, n};
+    std::vector<float> inf(n, info);
+    float pos_o[3], r9_o[9], ms;
+    outlier.assign(std::max(n, 1u), 0);
+    const mage_status st = mage_ba_pose_batch(1, pos, r9, intr, os, pts.data(), uv.data(), inf.data(), steps, huber,
+                                              max_err_sq, pos_o, r9_o, nullptr, outlier.data(), &ms, nullptr, device);
+    if (st != MAGE_OK) return st;
+    outlier.resize(n);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) out.R[3 * r + c] = (double)r9_o[3 * c + r];
+    for (int i = 0; i < 3; i++) out.t[i] = (double)pos_o[i];
+    return MAGE_OK;
+}
+
+}  // namespace
+
+extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_t* desc, const uint32_t* frame_start,
+                                           uint32_t frames, const double K[4], const double first_pose[12],
+                                           double plane_z, const mage_track_settings* s, double* poses,
+                                           uint32_t* matches, uint32_t* inliers, uint8_t* keyframe, int device)
+{
+    using namespace mage;
+    MAGE_REQUIRE(frame_start && K && first_pose && s && poses && matches && inliers && keyframe, MAGE_EINVAL,
+                 "null argument");
+    if (frames == 0) return MAGE_OK;
+    MAGE_REQUIRE(frame_start[0] == 0, MAGE_EINVAL, "frame_start[0] must be 0");
+    for (uint32_t f = 0; f < frames; f++)
+        MAGE_REQUIRE(frame_start[f + 1] >= frame_start[f], MAGE_EINVAL, "frame_start must be non-decreasing");
+    MAGE_REQUIRE(frame_start[frames] == 0 || (kp && desc), MAGE_EINVAL, "null features");
+    MAGE_HIP(hipSetDevice(device));
+    const float fx = (float)K[0], fy = (float)K[1], cx = (float)K[2], cy = (float)K[3];
+    auto frame_kp = [&](uint32_t f) { return kp + frame_start[f]; };
+    auto frame_desc = [&](uint32_t f) { return desc + 32ull * frame_start[f]; };
+    auto frame_n = [&](uint32_t f) { return frame_start[f + 1] - frame_start[f]; };
+
+    std::vector<Pose> P(frames);
+    std::memcpy(P[0].R, first_pose, 9 * sizeof(double));
+    std::memcpy(P[0].t, first_pose + 9, 3 * sizeof(double));
+    Keyframe kf;
+    kf.kp.assign(frame_kp(0), frame_kp(0) + frame_n(0));
+    kf.desc.assign(frame_desc(0), frame_desc(0) + 32ull * frame_n(0));
+    backproject(kf.kp.data(), frame_n(0), P[0], K, plane_z, kf.pts);
+    matches[0] = inliers[0] = frame_n(0);
+    std::memset(keyframe, 0, frames);
+    keyframe[0] = 1;
+
+    std::vector<uint32_t> sel;
+    std::vector<mage_keypoint> qkp;
+    std::vector<uint8_t> qdesc, out1, out2;
+    std::vector<float> qpos, pts, uv, pts2, uv2;
+    std::vector<mage_dmatch> m;
+    for (uint32_t f = 1; f < frames; f++) {
+        const mage_keypoint* fk = frame_kp(f);
+        const uint8_t* fd = frame_desc(f);
+        const uint32_t nf = frame_n(f);
+        // motion model: constant velocity on SE3
+        const Pose pred = f < 2 ? P[f - 1] : mul(mul(P[f - 1], inverse(P[f - 2])), P[f - 1]);
+        // ProjectUndistorted of the keyframe's map points (float32 view and camera matrices)
+        float R32[9], t32[3];
+        for (int i = 0; i < 9; i++) R32[i] = (float)pred.R[i];
+        for (int i = 0; i < 3; i++) t32[i] = (float)pred.t[i];
+        const uint32_t nk = (uint32_t)kf.kp.size();
+        sel.clear();
+        qkp.clear();
+        qdesc.clear();
+        qpos.clear();
+        for (uint32_t i = 0; i < nk; i++) {
+            const float X = kf.pts[3 * i], Y = kf.pts[3 * i + 1], Z = kf.pts[3 * i + 2];
+            float xc[3];
+            for (int r = 0; r < 3; r++) xc[r] = ((R32[3 * r] * X + R32[3 * r + 1] * Y) + R32[3 * r + 2] * Z) + t32[r];
+            if (!(xc[2] > 0.f)) continue;
+            sel.push_back(i);
+            qkp.push_back(kf.kp[i]);
+            qdesc.insert(qdesc.end(), kf.desc.begin() + 32ull * i, kf.desc.begin() + 32ull * (i + 1));
+            qpos.push_back(fx * xc[0] / xc[2] + cx);
+            qpos.push_back(fy * xc[1] / xc[2] + cy);
+        }
+        const uint32_t ns = (uint32_t)sel.size();
+        auto radius = [&](float r, bool positions) -> mage_status {
+            m.resize(std::max(ns, 1u));
+            uint32_t got = 0;
+            mage_status st = MAGE_OK;
+            if (ns > 0 && nf > 0)
+                st = mage_radius_match(qkp.data(), positions ? qpos.data() : nullptr, nullptr, qdesc.data(), ns, fk,
+                                       nullptr, fd, nf, r, s->max_hamming, s->min_hamming_difference, m.data(), ns,
+                                       &got);
+            m.resize(got);
+            return st;
+        };
+        auto weak = [&]() {
+            return m.size() < s->min_matches || (double)m.size() / (double)std::max(ns, 1u) < s->small_match_ratio;
+        };
+        mage_status st = radius(s->search_radius, true);
+        if (st == MAGE_OK && weak()) st = radius(s->wider_search_radius, true);
+        if (st == MAGE_OK && weak()) st = radius(s->extra_wider_search_radius, false);
+        if (st != MAGE_OK) return st;
+        matches[f] = (uint32_t)m.size();
+        if (m.size() < s->min_matches) {  // lost: keep the prediction
+            P[f] = pred;
+            inliers[f] = 0;
+            continue;
+        }
+        pts.resize(3 * m.size());
+        uv.resize(2 * m.size());
+        for (size_t k = 0; k < m.size(); k++) {
+            const uint32_t q = sel[m[k].query_idx], t = (uint32_t)m[k].train_idx;
+            std::memcpy(&pts[3 * k], &kf.pts[3 * q], 3 * sizeof(float));
+            uv[2 * k] = fk[t].x;
+            uv[2 * k + 1] = fk[t].y;
+        }
+        Pose p1, p2;
+        st = optimize(pred, K, pts, uv, s->refinement_info, s->initial_steps, s->initial_huber,
+                      (float)(s->initial_max_error * s->initial_max_error), device, p1, out1);
+        if (st != MAGE_OK) return st;
+        pts2.clear();
+        uv2.clear();
+        for (size_t k = 0; k < m.size(); k++)
+            if (!out1[k]) {
+                pts2.insert(pts2.end(), &pts[3 * k], &pts[3 * k] + 3);
+                uv2.insert(uv2.end(), &uv[2 * k], &uv[2 * k] + 2);
+            }
+        st = optimize(p1, K, pts2, uv2, s->refinement_info, s->final_steps, s->final_huber,
+                      (float)(s->final_max_error * s->final_max_error), device, p2, out2);
+        if (st != MAGE_OK) return st;
+        uint32_t n_in = 0;
+        for (uint8_t o : out2) n_in += o ? 0u : 1u;
+        P[f] = p2;
+        inliers[f] = n_in;
+        if ((double)n_in < s->keyframe_ratio * (double)nk + (double)s->keyframe_min) {
+            kf.kp.assign(fk, fk + nf);
+            kf.desc.assign(fd, fd + 32ull * nf);
+            backproject(fk, nf, p2, K, plane_z, kf.pts);
+            keyframe[f] = 1;
+        }
+    }
+    for (uint32_t f = 0; f < frames; f++) {
+        std::memcpy(poses + 12ull * f, P[f].R, 9 * sizeof(double));
+        std::memcpy(poses + 12ull * f + 9, P[f].t, 3 * sizeof(double));
+    }
+    return MAGE_OK;
+}

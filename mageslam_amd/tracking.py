@@ -51,11 +51,23 @@ class Pose:
     R: np.ndarray  # world -> camera rotation (3, 3) float64
     t: np.ndarray  # view-space translation (3,)
 
+    # elementwise products with left-to-right sums (no BLAS, no FMA): the native loop
+    # (csrc/track.cpp) evaluates the same expressions in the same order
     def inverse(self) -> "Pose":
-        return Pose(self.R.T, -self.R.T @ self.t)
+        Rt = np.ascontiguousarray(self.R.T)
+        return Pose(Rt, -_mv(Rt, self.t))
 
     def __mul__(self, o: "Pose") -> "Pose":
-        return Pose(self.R @ o.R, self.R @ o.t + self.t)
+        return Pose(_mm(self.R, o.R), _mv(self.R, o.t) + self.t)
+
+
+def _mv(R, v):
+    return np.array([(R[i, 0] * v[0] + R[i, 1] * v[1]) + R[i, 2] * v[2] for i in range(3)], np.float64)
+
+
+def _mm(A, B):
+    return np.array([[(A[i, 0] * B[0, j] + A[i, 1] * B[1, j]) + A[i, 2] * B[2, j] for j in range(3)]
+                     for i in range(3)], np.float64)
 
 
 @dataclass
@@ -83,11 +95,13 @@ class TrackResult:
 def backproject_to_plane(kp: np.ndarray, pose: Pose, K, plane_z: float) -> np.ndarray:
     """World points where the keypoints' rays meet the plane Z = plane_z (the scene's depth)."""
     fx, fy, cx, cy = K
-    d = np.stack([(kp["x"].astype(np.float64) - cx) / fx, (kp["y"].astype(np.float64) - cy) / fy,
-                  np.ones(len(kp))], 1) @ pose.R  # rows: R^T d
-    C = -pose.R.T @ pose.t
-    lam = (plane_z - C[2]) / d[:, 2]
-    return (C[None, :] + lam[:, None] * d).astype(np.float32)
+    R = pose.R
+    u = (kp["x"].astype(np.float64) - cx) / fx
+    v = (kp["y"].astype(np.float64) - cy) / fy
+    d = [(u * R[0, j] + v * R[1, j]) + R[2, j] for j in range(3)]  # R^T (u, v, 1)
+    C = [-((R[0, j] * pose.t[0] + R[1, j] * pose.t[1]) + R[2, j] * pose.t[2]) for j in range(3)]
+    lam = (plane_z - C[2]) / d[2]
+    return np.stack([C[j] + lam * d[j] for j in range(3)], 1).astype(np.float32)
 
 
 def project(points: np.ndarray, pose: Pose, K):
@@ -96,11 +110,12 @@ def project(points: np.ndarray, pose: Pose, K):
     fx, fy, cx, cy = (np.float32(v) for v in K)
     R = pose.R.astype(np.float32)
     t = pose.t.astype(np.float32)
-    Xc = points.astype(np.float32) @ R.T + t
-    z = Xc[:, 2]
+    P = points.astype(np.float32)
+    Xc = [((R[i, 0] * P[:, 0] + R[i, 1] * P[:, 1]) + R[i, 2] * P[:, 2]) + t[i] for i in range(3)]
+    z = Xc[2]
     ok = z > 0
     zs = np.where(ok, z, np.float32(1))
-    pos = np.stack([fx * Xc[:, 0] / zs + cx, fy * Xc[:, 1] / zs + cy], 1).astype(np.float32)
+    pos = np.stack([fx * Xc[0] / zs + cx, fy * Xc[1] / zs + cy], 1).astype(np.float32)
     return pos, ok
 
 
@@ -236,6 +251,44 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
         if n_in < s.keyframe_ratio * len(kf.points) + s.keyframe_min:
             kf = Keyframe(pose, kp, desc, backproject_to_plane(kp, pose, K, plane_z))
             res.keyframes.append(t)
+    return res
+
+
+def track_native(features, K, first_pose: Pose, plane_z: float, settings: TrackerSettings | None = None,
+                 device: int = 0) -> TrackResult:
+    """The same loop as `track` with GpuBackend, run by the library's native host code
+    (mage_track_sequence, csrc/track.cpp): no Python between the per-frame kernel calls."""
+    from . import _lib
+
+    s = settings or TrackerSettings()
+    T = len(features)
+    counts = np.array([len(k) for k, _ in features], np.uint32)
+    start = np.zeros(T + 1, np.uint32)
+    start[1:] = np.cumsum(counts)
+    kp = np.ascontiguousarray(np.concatenate([k for k, _ in features]) if T else np.zeros(0, KP_DTYPE), KP_DTYPE)
+    desc = np.ascontiguousarray(np.concatenate([d for _, d in features]).reshape(-1, 32) if T else
+                                np.zeros((0, 32), np.uint8), np.uint8)
+    cs = _lib.TrackSettingsC(s.search_radius, s.wider_search_radius, s.extra_wider_search_radius,
+                             s.small_match_ratio, s.min_matches, s.max_hamming, s.min_hamming_difference,
+                             s.initial_ba[0], s.initial_ba[1], s.initial_ba[2], s.final_ba[0], s.final_ba[1],
+                             s.final_ba[2], s.refinement_info, s.keyframe_ratio, s.keyframe_min)
+    Kd = np.array(K, np.float64)
+    p0 = np.concatenate([np.asarray(first_pose.R, np.float64).reshape(9), np.asarray(first_pose.t, np.float64)])
+    poses = np.zeros((max(T, 1), 12))
+    matches = np.zeros(max(T, 1), np.uint32)
+    inliers = np.zeros(max(T, 1), np.uint32)
+    kf = np.zeros(max(T, 1), np.uint8)
+    import ctypes as C
+
+    _lib.check(_lib.load().mage_track_sequence(_lib.ptr(kp), _lib.ptr(desc), _lib.ptr(start), T, _lib.ptr(Kd),
+                                               _lib.ptr(p0), float(plane_z), C.byref(cs), _lib.ptr(poses),
+                                               _lib.ptr(matches), _lib.ptr(inliers), _lib.ptr(kf), device))
+    res = TrackResult()
+    for f in range(T):
+        res.poses.append(Pose(poses[f, :9].reshape(3, 3).copy(), poses[f, 9:].copy()))
+    res.matches = [int(x) for x in matches[:T]]
+    res.inliers = [int(x) for x in inliers[:T]]
+    res.keyframes = [int(f) for f in np.nonzero(kf[:T])[0]]
     return res
 
 

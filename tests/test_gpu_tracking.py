@@ -46,3 +46,36 @@ def test_tracking_loop_gpu_vs_oracle(gpu, oracle):
     gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(len(seq.R))])
     assert tracking.pose_rmse(g, gt)[0] < 0.03
     assert min(g.inliers[1:]) >= 100
+    # the native loop (mage_track_sequence) is the same specification: identical to the Python loop
+    n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z)
+    assert n.matches == g.matches and n.inliers == g.inliers and n.keyframes == g.keyframes
+    assert all(np.array_equal(a.R, b.R) and np.array_equal(a.t, b.t) for a, b in zip(n.poses, g.poses))
+
+
+def test_native_tracking_loop_720p_keyframes(gpu):
+    """A 720p pan long enough for keyframe switches: native loop == Python loop over the GPU
+    kernels, frame by frame (poses bit-identical), and within a centimetre of the ground truth."""
+    seq = synth.scene_sequence(160, 1280, 720)
+    frames = synth.scene_frames(seq)
+    K = (seq.fx, seq.fy, seq.cx, seq.cy)
+    p0 = tracking.Pose(seq.R[0], seq.t[0])
+    gb = tracking.GpuBackend(2000)
+    gf = gb.extract(frames)
+    g = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb)
+    n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z)
+    assert len(g.keyframes) >= 2
+    assert n.matches == g.matches and n.inliers == g.inliers and n.keyframes == g.keyframes
+    assert all(np.array_equal(a.R, b.R) and np.array_equal(a.t, b.t) for a, b in zip(n.poses, g.poses))
+    gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(len(seq.R))])
+    assert tracking.pose_rmse(n, gt)[0] < 0.01
+
+
+def test_native_tracking_errors(gpu):
+    from mageslam_amd._lib import MageError
+
+    p0 = tracking.Pose(np.eye(3), np.zeros(3))
+    assert tracking.track_native([], (500.0, 500.0, 320.0, 240.0), p0, 5.0).poses == []
+    with pytest.raises(MageError):
+        from mageslam_amd import _lib
+
+        _lib.check(_lib.load().mage_track_sequence(None, None, None, 3, None, None, 5.0, None, None, None, None, None, 0))
