@@ -182,7 +182,7 @@ def tethered_extra_camera():
     return g2
 
 
-@pytest.mark.parametrize("problems,obs", [(96, 500), (600, 200)])  # 512- and 256-thread kernel variants
+@pytest.mark.parametrize("problems,obs", [(96, 500), (600, 200), (4, 2500)])  # 512 / 256 threads, > 2048 obs (not staged)
 @pytest.mark.parametrize("steps,huber,maxe", [(3, 4.0, 36.0), (4, 0.9, 4.5 ** 2)])
 def test_pose_batch_matches_per_frame_oracle(gpu, steps, huber, maxe, problems, obs):
     """Batched OptimizeCameraPose (TrackLocalMap.cpp:96-140 settings: 3 x 4.0 / 6^2, then
