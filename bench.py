@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--pipelined-streams", type=int, default=2,
                    help="also report the ORB rate pipelined over this many streams (0: skip; 1 GPU runs only)")
     p.add_argument("--no-all-cores", action="store_true", help="skip the all-host-cores CPU baselines")
+    p.add_argument("--ba-many-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
     p.add_argument("--cpu-dry-run", action="store_true", help="gloo rehearsal of the multi-rank flow (tests)")
     return p.parse_args()
@@ -558,6 +559,23 @@ def run_ba_many(args, local_rank, g, budget_s):
                       f"~{budget_s:.0f} s; sum of per-window rates"}
 
 
+def run_ba_many_child(local_rank):
+    """run_ba_many in a child process (its own GPU context): the multi-threaded leg cannot take
+    the headline run down with it."""
+    import subprocess
+
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", str(local_rank)))
+    try:
+        r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--ba-many-child"], capture_output=True, text=True,
+                           timeout=180, env=env, cwd=str(ROOT))
+        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        if r.returncode == 0 and lines:
+            return json.loads(lines[-1])
+        return {"error": f"child exited with {r.returncode}", "stderr_tail": r.stderr[-400:]}
+    except subprocess.TimeoutExpired:
+        return {"error": "child timed out"}
+
+
 def cpu_ba_baseline_all(g, budget_s):
     """Independent copies of the C3 window on all host cores (one oracle BundlerLib per thread,
     the GPU leg's schedule) — the many-windows throughput of SURVEY.md §8(e)."""
@@ -616,6 +634,13 @@ def main():
     rank, world, local_rank = multigpu.rank_env()
     import torch
 
+    if args.ba_many_child:  # see run_ba_many_child: one visible device
+        from mageslam_amd import synth
+
+        torch.cuda.set_device(0)
+        print(json.dumps(run_ba_many(args, 0, synth.ba_graph(), 3.0)), flush=True)
+        return
+
     if args.cpu_dry_run:
         dist = multigpu.init("gloo", local_rank)
         res = run_dry(args, rank, world, dist)
@@ -646,7 +671,7 @@ def main():
                             "per-kernel durations the roofline is priced on)"}
     ba_res, g = (None, None) if args.no_ba else run_ba(args, local_rank, torch)
     if ba_res is not None and world == 1 and not args.no_all_cores:
-        ba_res["many_windows"] = run_ba_many(args, local_rank, g, 3.0)
+        ba_res["many_windows"] = run_ba_many_child(local_rank)
     pose_res, pb = (None, None) if args.no_pose else run_pose(args, rank, world, local_rank, torch, dist)
     track_res, tctx = (None, None) if (args.no_tracking or rank != 0) else run_tracking(args, local_rank, torch)
     if world > 1:

@@ -27,6 +27,6 @@ if [ "$2" = collect ]; then
     cp $OUT/bench_final.json profiles/${TAG}_bench.json
     exit 0
 fi
-run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0
+run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores
 run_set $ROWS python3 tools/bench_rows.py
 timeout -k 10 400 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
