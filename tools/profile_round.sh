@@ -25,6 +25,8 @@ if [ "$2" = collect ]; then
     cp $ROWS/trace/run_kernel_stats.csv profiles/${TAG}_rows_kernel_stats.csv
     cp $ROWS/trace.json profiles/${TAG}_rows.jsonl
     cp $OUT/bench_final.json profiles/${TAG}_bench.json
+    # bench.py prices roofline.traffic on the headline run's counters
+    cp profiles/${TAG}_pmc_summary.json profiles/pmc_summary.json
     exit 0
 fi
 run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores
