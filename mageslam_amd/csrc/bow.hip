@@ -235,10 +235,16 @@ __global__ __launch_bounds__(SORT_THREADS) void indexed_match_kernel(IndexedPara
     // 2. forward TrackMatch over B's run of the leaf, then the reverse check over A's run
     const unsigned max_h = (unsigned)(p.max_dist + 1);
     const int group = tid / IM_GROUP, sub = tid % IM_GROUP;
-    for (int i = group; i < na; i += IM_GROUPS) {
+    // A features are visited in (leaf, index) order: neighbouring groups scan the same B run and,
+    // for the reverse check, the same A run (its descriptors stay in the CU's L1); masked-out
+    // features are not in keysA and keep -1
+    for (int i = tid; i < na; i += SORT_THREADS) res[i] = -1;
+    __syncthreads();
+    for (int pos = group; pos < ca; pos += IM_GROUPS) {
+        const int i = (int)(keysA[pos] & 0xFFFFFFFFull);
         int r = -1;
-        if (!ma || ma[i]) {
-            const unsigned long long leaf = la[i];
+        {
+            const unsigned long long leaf = keysA[pos] >> 32;
             const uint4 qa = *reinterpret_cast<const uint4*>(da + 32ll * i);
             const uint4 qb = *reinterpret_cast<const uint4*>(da + 32ll * i + 16);
             const int lo = lower_bound_u64(keysB, cb, leaf << 32), hi = lower_bound_u64(keysB, cb, (leaf + 1) << 32);
@@ -252,7 +258,7 @@ __global__ __launch_bounds__(SORT_THREADS) void indexed_match_kernel(IndexedPara
                 const int j = (int)(bk & 0xFFFu);
                 const uint4 ra = *reinterpret_cast<const uint4*>(db + 32ll * j);
                 const uint4 rb = *reinterpret_cast<const uint4*>(db + 32ll * j + 16);
-                const unsigned long long lj = lb[j];
+                const unsigned long long lj = leaf;  // j is in B's run of this leaf
                 const int lo2 = lower_bound_u64(keysA, ca, lj << 32), hi2 = lower_bound_u64(keysA, ca, (lj + 1) << 32);
                 unsigned bk2, sd2;
                 track_run(keysA, lo2, hi2, sub, da, ra, rb, max_h, bk2, sd2);
