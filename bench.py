@@ -666,6 +666,8 @@ def main():
         pr = run_orb(pa, rank, world, local_rank, torch, dist)
         pipe_res = {"value": pr["value"], "unit": "frames/s", "ms_per_step": pr["ms_per_step"],
                     "hip_streams": pa.streams, "mean_matches": pr["mean_matches"],
+                    "same_last_batch_as_single_stream": pr["mean_matches"] == orb_res["mean_matches"]
+                    and pr["mean_keypoints"] == orb_res["mean_keypoints"],
                     "note": "the same workload with batch s+1's extraction overlapping batch s's select / describe "
                             "/ match on another stream (not the headline: overlapping batches stretch the "
                             "per-kernel durations the roofline is priced on)"}
