@@ -77,15 +77,24 @@ def ba_flops(g, trials_per_iter):
 
 
 def load_pmc(kernel):
-    """HBM bytes per launch for `kernel` from the committed rocprofv3 PMC summary, if any."""
+    """(HBM bytes per launch, provenance) for `kernel` from the committed rocprofv3 PMC summary.
+    The summary records the hash of the kernel sources it was collected on; counters of other
+    sources are stale and not reported (traffic None)."""
+    from mageslam_amd.build import kernel_sources_sha
+
     f = ROOT / "profiles" / "pmc_summary.json"
     if not f.exists():
-        return None
+        return None, "no committed PMC summary"
     try:
         d = json.loads(f.read_text())
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+    except Exception as e:
+        return None, f"unreadable PMC summary ({e})"
+    meta = d.get("_meta", {})
+    sha, now = meta.get("kernel_sources_sha"), kernel_sources_sha()
+    if sha != now:
+        return None, f"stale: profiles/pmc_summary.json was collected on kernel sources {sha}, these are {now}"
+    return d.get(kernel, {}).get("hbm_bytes_per_launch"), \
+        f"profiles/pmc_summary.json ({meta.get('tag')}, kernel sources {sha}, FETCH_SIZE + WRITE_SIZE passes)"
 
 
 def cpu_orb_baseline(args, budget_s):
@@ -247,10 +256,10 @@ def run_orb(args, rank, world, local_rank, torch, dist):
         per_frame = orb_bytes_per_frame(W, H, N)
         avg_s = orb_k[dom]["avg_ms"] / 1000.0
         achieved = per_frame * B / avg_s / 1e9
-        traffic = load_pmc(dom)
+        traffic, traffic_source = load_pmc(dom)
         res["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                           "algorithmic_bytes_per_launch": per_frame * B,
+                           "traffic_source": traffic_source, "algorithmic_bytes_per_launch": per_frame * B,
                            "avg_launch_ms": orb_k[dom]["avg_ms"]}
     return res
 
@@ -564,16 +573,21 @@ def run_ba_many_child(local_rank):
     the headline run down with it."""
     import subprocess
 
-    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", str(local_rank)))
+    # the child sees exactly this rank's GPU: entry local_rank of the parent's visible list
+    visible = os.environ.get("HIP_VISIBLE_DEVICES")
+    dev = visible.split(",")[local_rank] if visible else str(local_rank)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=dev, PYTHONFAULTHANDLER="1")
     try:
         r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--ba-many-child"], capture_output=True, text=True,
                            timeout=180, env=env, cwd=str(ROOT))
         lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
         if r.returncode == 0 and lines:
-            return json.loads(lines[-1])
-        return {"error": f"child exited with {r.returncode}", "stderr_tail": r.stderr[-400:]}
+            return dict(json.loads(lines[-1]), status="ok")
+        fail = {"status": "failed", "error": f"child exited with {r.returncode}", "stderr_tail": r.stderr[-1500:]}
     except subprocess.TimeoutExpired:
-        return {"error": "child timed out"}
+        fail = {"status": "failed", "error": "child timed out (180 s)"}
+    print(f"bench: many-windows BA leg FAILED: {fail}", file=sys.stderr, flush=True)
+    return fail
 
 
 def cpu_ba_baseline_all(g, budget_s):
@@ -703,6 +717,9 @@ def main():
             "mean_keypoints": orb_res["mean_keypoints"],
             "mean_matches": orb_res["mean_matches"],
         }
+        failed = [k for k, v in (("ba.many_windows", (ba_res or {}).get("many_windows")),) if v and v.get("status") == "failed"]
+        if failed:
+            out["failed_legs"] = failed
         if pipe_res is not None:
             out["pipelined"] = pipe_res
         if ba_res is not None:

@@ -26,6 +26,18 @@ COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unus
           f"-I{PKG.parent / 'include'}"]
 
 
+def kernel_sources_sha() -> str:
+    """SHA-256 (first 16 hex digits) of the HIP / C++ sources and headers the library is built
+    from: ties committed profiler counters (profiles/pmc_summary.json) to the kernels they measured."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("*.hpp")) + list(CSRC.glob("*.cpp"))):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and Path(cand).exists():

@@ -4,8 +4,10 @@
 #include <atomic>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "common.hpp"
@@ -19,6 +21,13 @@ thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 const char* last_error() { return g_last_error.c_str(); }
 
+namespace {
+// devices whose architecture was checked (gfx950), so the per-frame entry points do not query
+// the device properties on every call
+std::mutex g_arch_mu;
+std::map<int, std::string> g_arch;
+}  // namespace
+
 mage_status bind_device(int device)
 {
     int count = 0;
@@ -31,13 +40,65 @@ mage_status bind_device(int device)
         return MAGE_EDEVICE;
     }
     MAGE_HIP(hipSetDevice(device));
-    hipDeviceProp_t prop;
-    MAGE_HIP(hipGetDeviceProperties(&prop, device));
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        set_error(std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only");
+    std::string arch;
+    {
+        std::lock_guard<std::mutex> lk(g_arch_mu);
+        auto it = g_arch.find(device);
+        if (it != g_arch.end()) arch = it->second;
+    }
+    if (arch.empty()) {
+        hipDeviceProp_t prop;
+        MAGE_HIP(hipGetDeviceProperties(&prop, device));
+        arch = prop.gcnArchName;
+        std::lock_guard<std::mutex> lk(g_arch_mu);
+        g_arch[device] = arch;
+    }
+    if (std::strncmp(arch.c_str(), "gfx950", 6) != 0) {
+        set_error("device is " + arch + ", this build targets gfx950 only");
         return MAGE_EDEVICE;
     }
     return MAGE_OK;
+}
+
+HostScratch::~HostScratch()
+{
+    if (st) (void)hipStreamDestroy(st);
+    buf.release();
+    aux.release();
+    host.release();
+}
+
+HostScratch* host_scratch(int device, ScratchSlot slot)
+{
+    thread_local std::map<std::pair<int, int>, std::unique_ptr<HostScratch>> per_thread;
+    std::unique_ptr<HostScratch>& s = per_thread[{device, (int)slot}];
+    if (!s) s.reset(new HostScratch());
+    if (!s->st && hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) {
+        s->st = nullptr;
+        set_error("hipStreamCreateWithFlags failed");
+        return nullptr;
+    }
+    return s.get();
+}
+
+void* stream_scratch(hipStream_t st, StreamSlot slot, size_t bytes)
+{
+    static std::mutex mu;
+    static std::map<std::tuple<int, hipStream_t, int>, DeviceBuffer> bufs;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        set_error("hipGetDevice failed");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    DeviceBuffer& b = bufs[std::make_tuple(dev, st, (int)slot)];
+    // growing frees the old buffer: let this stream's launches that still use it finish first
+    if (bytes > b.bytes && b.ptr && hipStreamSynchronize(st) != hipSuccess) {
+        set_error("hipStreamSynchronize failed");
+        return nullptr;
+    }
+    if (b.reserve(bytes) != MAGE_OK) return nullptr;
+    return b.ptr;
 }
 
 namespace {

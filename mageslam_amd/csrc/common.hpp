@@ -85,11 +85,42 @@ struct PinnedBuffer {
         bytes = n;
         return MAGE_OK;
     }
+    void release() {
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
     template <typename T>
     T* as() const {
         return static_cast<T*>(ptr);
     }
 };
+
+// Scratch of a synchronous host-buffer entry point (device staging, pinned staging, a private
+// stream), one per (calling thread, device, entry point): concurrent callers never share buffers
+// or a stream.  The reference calls these paths from several threads at once — both stereo
+// frames' OrbFeatureDetector::Process (UndistortKeypoints) run in parallel
+// (ImageAnalyzer.cpp:160-216) and the matchers take a per-thread thread_memory.  Released when the
+// thread exits.
+enum ScratchSlot : int { SCRATCH_RADIUS = 0, SCRATCH_POSE = 1, SCRATCH_UNDISTORT = 2, SCRATCH_MATCH = 3 };
+struct HostScratch {
+    DeviceBuffer buf, aux;
+    PinnedBuffer host;
+    hipStream_t st = nullptr;
+    HostScratch() = default;
+    HostScratch(const HostScratch&) = delete;
+    HostScratch& operator=(const HostScratch&) = delete;
+    ~HostScratch();
+};
+// The calling thread's scratch for `slot` on `device` (already bound by bind_device), with its
+// stream created; nullptr (and the error set) if the stream cannot be created.
+HostScratch* host_scratch(int device, ScratchSlot slot);
+
+// Device scratch private to one (current device, stream, slot) and at least `bytes` long:
+// kernels on different streams may run concurrently, so they never share it, while launches on
+// one stream are ordered.  nullptr (error set) if the allocation fails.
+enum StreamSlot : int { STREAM_MATCH_ROWS = 0, STREAM_MATCH_STATUS = 1 };
+void* stream_scratch(hipStream_t st, StreamSlot slot, size_t bytes);
 
 constexpr int kWave = 64;
 

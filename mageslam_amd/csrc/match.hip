@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstring>
 #include <vector>
 
 #include "common.hpp"
@@ -506,11 +507,6 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
     if (tid == 0) n_out[pair] = base;
 }
 
-struct MatchScratch {
-    DeviceBuffer a, b, n, out, status, rows;
-};
-thread_local MatchScratch g_match;
-
 }  // namespace
 
 mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA, const uint8_t* dB,
@@ -518,10 +514,10 @@ mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA
                         int minDiff, mage_dmatch* dOut, uint32_t cap, uint32_t* dN,
                         uint32_t* dStatus, hipStream_t st)
 {
-    mage_status r = g_match.rows.reserve((size_t)pairs * NMAX * sizeof(int2));
-    if (r != MAGE_OK) return r;
+    void* rows = stream_scratch(st, STREAM_MATCH_ROWS, (size_t)pairs * NMAX * sizeof(int2));
+    if (!rows) return MAGE_ENOMEM;
     MatchParams mp{};
-    mp.rows = g_match.rows.as<int2>();
+    mp.rows = static_cast<int2*>(rows);
     mp.max_dist = maxDist;
     mp.min_diff = minDiff;
     mp.out_cap = cap;
@@ -556,11 +552,10 @@ mage_status mage_hamming_match_batch_device(const uint8_t* d_desc_a, int64_t a_p
     MAGE_REQUIRE(d_desc_a && d_desc_b && d_n_a && d_n_b && d_out && d_n, MAGE_EINVAL, "null buffer");
     MAGE_REQUIRE(a_pitch % 16 == 0 && b_pitch % 16 == 0, MAGE_EINVAL, "pair pitch must be a multiple of 16");
     if (pairs == 0) return MAGE_OK;
-    auto& s = mage::g_match;
-    mage_status r = s.status.reserve(4);
-    if (r != MAGE_OK) return r;
+    void* status = mage::stream_scratch((hipStream_t)stream, mage::STREAM_MATCH_STATUS, 4);
+    if (!status) return MAGE_ENOMEM;
     return mage::match_batch(d_desc_a, a_pitch, d_n_a, d_desc_b, b_pitch, d_n_b, pairs, max_distance,
-                             min_difference, d_out, cap, d_n, s.status.as<uint32_t>(), (hipStream_t)stream);
+                             min_difference, d_out, cap, d_n, static_cast<uint32_t*>(status), (hipStream_t)stream);
 }
 
 mage_status mage_hamming_match(const uint8_t* desc_a, uint32_t n_a, const uint8_t* mask_a,
@@ -584,30 +579,32 @@ mage_status mage_hamming_match(const uint8_t* desc_a, uint32_t n_a, const uint8_
     MAGE_HIP(hipGetDevice(&dev));
     mage_status r = mage::bind_device(dev);
     if (r != MAGE_OK) return r;
-    std::vector<uint8_t> ha(ia.size() * 32), hb(ib.size() * 32);
-    for (size_t k = 0; k < ia.size(); k++) std::copy(desc_a + 32 * (size_t)ia[k], desc_a + 32 * (size_t)ia[k] + 32, &ha[32 * k]);
-    for (size_t k = 0; k < ib.size(); k++) std::copy(desc_b + 32 * (size_t)ib[k], desc_b + 32 * (size_t)ib[k] + 32, &hb[32 * k]);
-    auto& s = mage::g_match;
-    const uint32_t ocap = (uint32_t)ia.size();
-    if ((r = s.a.reserve(ha.size())) != MAGE_OK) return r;
-    if ((r = s.b.reserve(hb.size())) != MAGE_OK) return r;
-    if ((r = s.n.reserve(16)) != MAGE_OK) return r;
-    if ((r = s.out.reserve(sizeof(mage_dmatch) * ocap)) != MAGE_OK) return r;
-    if ((r = s.status.reserve(4)) != MAGE_OK) return r;
-    uint32_t counts[3] = {(uint32_t)ia.size(), (uint32_t)ib.size(), 0};
-    MAGE_HIP(hipMemcpy(s.a.ptr, ha.data(), ha.size(), hipMemcpyHostToDevice));
-    MAGE_HIP(hipMemcpy(s.b.ptr, hb.data(), hb.size(), hipMemcpyHostToDevice));
-    MAGE_HIP(hipMemcpy(s.n.ptr, counts, 12, hipMemcpyHostToDevice));
-    MAGE_HIP(hipMemset(s.status.ptr, 0, 4));
-    uint32_t* dn = s.n.as<uint32_t>();
-    r = mage::match_batch(s.a.as<uint8_t>(), 0, dn, s.b.as<uint8_t>(), 0, dn + 1, 1, max_distance,
-                          min_difference, s.out.as<mage_dmatch>(), ocap, dn + 2, s.status.as<uint32_t>(), nullptr);
+    mage::HostScratch* sp = mage::host_scratch(dev, mage::SCRATCH_MATCH);
+    if (!sp) return MAGE_EDEVICE;
+    mage::HostScratch& S = *sp;
+    // device layout [a][b][counts: nA, nB, total, status][out]: inputs packed at their device
+    // offsets in pinned memory, one copy each way
+    const size_t na = ia.size(), nb = ib.size(), ocap = na;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t oa = 0, ob = al(32 * na), oc = al(ob + 32 * nb), oo = al(oc + 16), total_bytes = oo + sizeof(mage_dmatch) * ocap;
+    if ((r = S.buf.reserve(total_bytes)) != MAGE_OK || (r = S.host.reserve(total_bytes)) != MAGE_OK) return r;
+    char* h = S.host.as<char>();
+    char* d = S.buf.as<char>();
+    for (size_t k = 0; k < na; k++) std::memcpy(h + oa + 32 * k, desc_a + 32 * (size_t)ia[k], 32);
+    for (size_t k = 0; k < nb; k++) std::memcpy(h + ob + 32 * k, desc_b + 32 * (size_t)ib[k], 32);
+    const uint32_t counts[4] = {(uint32_t)na, (uint32_t)nb, 0, 0};
+    std::memcpy(h + oc, counts, 16);
+    MAGE_HIP(hipMemcpyAsync(d, h, oo, hipMemcpyHostToDevice, S.st));
+    uint32_t* dn = reinterpret_cast<uint32_t*>(d + oc);
+    r = mage::match_batch(reinterpret_cast<const uint8_t*>(d + oa), 0, dn, reinterpret_cast<const uint8_t*>(d + ob), 0,
+                          dn + 1, 1, max_distance, min_difference, reinterpret_cast<mage_dmatch*>(d + oo),
+                          (uint32_t)ocap, dn + 2, dn + 3, S.st);
     if (r != MAGE_OK) return r;
-    uint32_t total = 0;
-    MAGE_HIP(hipMemcpy(&total, dn + 2, 4, hipMemcpyDeviceToHost));
-    std::vector<mage_dmatch> tmp(std::min(total, ocap));
-    if (!tmp.empty()) MAGE_HIP(hipMemcpy(tmp.data(), s.out.ptr, sizeof(mage_dmatch) * tmp.size(), hipMemcpyDeviceToHost));
-    const uint32_t nw = std::min<uint32_t>((uint32_t)tmp.size(), cap);
+    MAGE_HIP(hipMemcpyAsync(h + oc, d + oc, total_bytes - oc, hipMemcpyDeviceToHost, S.st));
+    MAGE_HIP(hipStreamSynchronize(S.st));
+    const uint32_t total = reinterpret_cast<const uint32_t*>(h + oc)[2];
+    const mage_dmatch* tmp = reinterpret_cast<const mage_dmatch*>(h + oo);
+    const uint32_t nw = std::min<uint32_t>(std::min<uint32_t>(total, (uint32_t)ocap), cap);
     for (uint32_t k = 0; k < nw; k++) {
         out[k] = tmp[k];
         out[k].query_idx = (int32_t)ia[tmp[k].query_idx];

@@ -1514,12 +1514,6 @@ mage_status check_calibration(const mage_calibration* c)
     return MAGE_OK;
 }
 
-struct UndistortScratch {
-    DeviceBuffer kp, n;
-    hipStream_t st = nullptr;
-};
-UndistortScratch g_undistort[16];
-
 }  // namespace
 }  // namespace mage
 
@@ -1555,15 +1549,16 @@ mage_status mage_undistort_keypoints(const mage_calibration* distorted, const ma
     if (n == 0) return MAGE_OK;
     MAGE_REQUIRE(kp, MAGE_EINVAL, "null keypoints");
     if ((r = bind_device(device)) != MAGE_OK) return r;
-    UndistortScratch& S = g_undistort[device & 15];
-    if (!S.st) MAGE_HIP(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
-    if ((r = S.kp.reserve(sizeof(mage_keypoint) * (size_t)n)) != MAGE_OK || (r = S.n.reserve(4)) != MAGE_OK) return r;
-    MAGE_HIP(hipMemcpyAsync(S.kp.ptr, kp, sizeof(mage_keypoint) * (size_t)n, hipMemcpyHostToDevice, S.st));
-    MAGE_HIP(hipMemcpyAsync(S.n.ptr, &n, 4, hipMemcpyHostToDevice, S.st));
-    if ((r = mage_undistort_keypoints_batch_device(distorted, undistorted, S.kp.as<mage_keypoint>(), n,
-                                                   S.n.as<uint32_t>(), 1, (mage_stream)S.st)) != MAGE_OK)
+    HostScratch* sp = host_scratch(device, SCRATCH_UNDISTORT);
+    if (!sp) return MAGE_EDEVICE;
+    HostScratch& S = *sp;
+    if ((r = S.buf.reserve(sizeof(mage_keypoint) * (size_t)n)) != MAGE_OK || (r = S.aux.reserve(4)) != MAGE_OK) return r;
+    MAGE_HIP(hipMemcpyAsync(S.buf.ptr, kp, sizeof(mage_keypoint) * (size_t)n, hipMemcpyHostToDevice, S.st));
+    MAGE_HIP(hipMemcpyAsync(S.aux.ptr, &n, 4, hipMemcpyHostToDevice, S.st));
+    if ((r = mage_undistort_keypoints_batch_device(distorted, undistorted, S.buf.as<mage_keypoint>(), n,
+                                                   S.aux.as<uint32_t>(), 1, (mage_stream)S.st)) != MAGE_OK)
         return r;
-    MAGE_HIP(hipMemcpyAsync(kp, S.kp.ptr, sizeof(mage_keypoint) * (size_t)n, hipMemcpyDeviceToHost, S.st));
+    MAGE_HIP(hipMemcpyAsync(kp, S.buf.ptr, sizeof(mage_keypoint) * (size_t)n, hipMemcpyDeviceToHost, S.st));
     MAGE_HIP(hipStreamSynchronize(S.st));
     return MAGE_OK;
 }

@@ -366,13 +366,6 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
     }
 }
 
-struct PoseScratch {
-    DeviceBuffer buf;
-    PinnedBuffer host;
-    hipStream_t st = nullptr;
-};
-PoseScratch g_pose[16];
-
 mage_status pose_launch(const PoseParams& p, uint32_t problems, hipStream_t st)
 {
     if (problems == 0) return MAGE_OK;
@@ -422,8 +415,9 @@ mage_status mage_ba_pose_batch(uint32_t problems, const float* pos3, const float
     MAGE_REQUIRE(huber >= 0.f, MAGE_EINVAL, "Huber widths must be nonnegative");
     mage_status r = bind_device(device);
     if (r != MAGE_OK) return r;
-    PoseScratch& S = g_pose[device & 15];
-    if (!S.st) MAGE_HIP(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+    HostScratch* sp = host_scratch(device, SCRATCH_POSE);
+    if (!sp) return MAGE_EDEVICE;
+    HostScratch& S = *sp;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t P = problems;
     const size_t o_pos = 0, o_r9 = al(o_pos + 12 * P), o_in = al(o_r9 + 36 * P), o_os = al(o_in + 16 * P),

@@ -281,14 +281,6 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_post_kernel(RadiusParams 
     radius_post(p, pr, p.res + pr * p.q_pitch, nq, ntr, bestD, cnt, wsum, s_base);
 }
 
-// host-side scratch for the synchronous single-pair entry point (one per device)
-struct RadiusScratch {
-    DeviceBuffer buf;
-    PinnedBuffer host;
-    hipStream_t st = nullptr;
-};
-RadiusScratch g_radius[16];
-
 }  // namespace
 
 mage_status radius_match_launch(const RadiusParams& p, uint32_t pairs, hipStream_t st)
@@ -329,8 +321,9 @@ mage_status mage_radius_match(const mage_keypoint* query_kp, const float* query_
     MAGE_HIP(hipGetDevice(&dev));
     mage_status r = bind_device(dev);
     if (r != MAGE_OK) return r;
-    RadiusScratch& S = g_radius[dev & 15];
-    if (!S.st) MAGE_HIP(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+    HostScratch* sp = host_scratch(dev, SCRATCH_RADIUS);
+    if (!sp) return MAGE_EDEVICE;
+    HostScratch& S = *sp;
     // device layout: [qkp][tkp][qdesc][tdesc][qpos][qmask][tmask][counts] (inputs, one H2D copy)
     // [res][out]; the D2H copy takes [counts, end)
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };

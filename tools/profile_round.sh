@@ -11,6 +11,7 @@ export TMPDIR=/tmp
 run_set() {  # <out dir> <command...>
     local OUT=$1; shift
     mkdir -p $OUT
+    python3 -c "from mageslam_amd.build import kernel_sources_sha; print(kernel_sources_sha())" > $OUT/sources_sha
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- "$@" > $OUT/trace.json 2> $OUT/trace.err
     timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- "$@" > /dev/null 2> $OUT/fetch.err
     timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- "$@" > /dev/null 2> $OUT/write.err

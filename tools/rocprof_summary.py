@@ -89,7 +89,17 @@ def main():
              "~4.6-4.8 cycles per instruction per SIMD for every form used here).", "",
              "| kernel | calls | avg µs | total ms | % | FETCH MB/launch (raw) | FETCH x2 | WRITE MB/launch | VALU G inst/s | VALU issue frac |",
              "|---|---|---|---|---|---|---|---|---|---|"]
-    summary = {}
+    # provenance: the kernel sources the counters were collected on (written on the GPU box by
+    # tools/profile_round.sh; bench.py reports traffic only for matching sources)
+    sha_file = prof / "sources_sha"
+    if sha_file.exists():
+        sha = sha_file.read_text().strip()
+    else:
+        sys.path.insert(0, str(ROOT))
+        from mageslam_amd.build import kernel_sources_sha
+
+        sha = kernel_sources_sha()
+    summary = {"_meta": {"tag": tag, "kernel_sources_sha": sha, "command": cmd}}
     for r in stats:
         k = r["kernel"]
         f = fetch.get(k)
