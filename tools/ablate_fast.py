@@ -1,0 +1,65 @@
+"""Timing ablation of fast_nms_kernel (development tool, not part of the product).
+
+  python tools/ablate_fast.py build     # compile variants into abl/f<N>/libmage_hot.so (CPU)
+  python tools/ablate_fast.py run       # time orb.fast_nms of each variant on the GPU (C2 batch)
+
+MAGE_FAST_ABLATE bits: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load.
+"""
+import ctypes as C
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+VARIANTS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 2, 3, 5, 7, 15]
+
+
+def build():
+    sys.path.insert(0, str(ROOT))
+    from mageslam_amd import build as B
+    B.build()
+    objs = [p for p in (B.OBJ).glob("*.o") if not p.name.startswith("orb")]
+    for v in VARIANTS:
+        out = ROOT / "abl" / f"f{v}"
+        out.mkdir(parents=True, exist_ok=True)
+        obj = out / "orb.o"
+        subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON,
+                        f"-DMAGE_FAST_ABLATE={v}", "-c", str(B.CSRC / "orb.hip"), "-o", str(obj)], check=True)
+        subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
+                        str(obj), *map(str, objs)], check=True)
+        print("built", out)
+
+
+def run():
+    import torch
+    sys.path.insert(0, str(ROOT))
+    from mageslam_amd import _lib, orb, synth
+    W, H, B, N = 1280, 720, 256, 2000
+    frames = torch.empty((B, H, W), dtype=torch.uint8, device="cuda")
+    kp = torch.zeros((B, N * 28), dtype=torch.uint8, device="cuda")
+    desc = torch.zeros((B, N, 32), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    for v in VARIANTS:
+        L = C.CDLL(str(ROOT / "abl" / f"f{v}" / "libmage_hot.so"))
+        _lib._declare(L)
+        _lib._lib = L
+        orb.synth_frames_device(frames, B, W, H, 0, synth.FRAME_SEED)
+        det = orb.OrbDetector(nfeatures=N)
+        for _ in range(3):
+            det.detect_and_compute_batch_device(frames, W, H, kp, desc, cnt, N)
+        torch.cuda.synchronize()
+        L.mage_profile_reset()
+        L.mage_profile_enable(1)
+        for _ in range(10):
+            det.detect_and_compute_batch_device(frames, W, H, kp, desc, cnt, N)
+        torch.cuda.synchronize()
+        rep = _lib.profile_report()
+        L.mage_profile_enable(0)
+        c, ms = rep.get("orb.fast_nms", (1, float("nan")))
+        print(f"variant {v:2d}: fast_nms {ms / c:.4f} ms  select {rep.get('orb.select', (1, 0))[1] / 10:.4f} ms  "
+              f"mean keypoints {cnt.float().mean().item():.0f}", flush=True)
+        det.close()
+
+
+if __name__ == "__main__":
+    {"build": build, "run": run}[sys.argv[1]]()
