@@ -43,7 +43,7 @@ constexpr int LW = TW + 16;            // 136 image bytes per LDS row (34 dwords
 constexpr int LH = TH + 8;             // 38 image rows
 constexpr int FAST_THREADS = GX * (SROWS / SR);  // 128
 static_assert(SROWS % SR == 0, "strips tile the score rows");
-static_assert(TW % 4 == 0, "tile origin stays dword aligned");
+static_assert(TW % 8 == 0, "tile origin stays qword aligned");
 
 struct FastParams {
     int w, h, stride;
@@ -52,13 +52,17 @@ struct FastParams {
     int xlo, xhi, ylo, yhi;  // emission window (FAST range ∩ RunByImageBorder)
     unsigned cand_cap;
     int dword_ok;  // frames 4-byte aligned with width, stride and pitch multiples of 4
+    int qword_ok;  // frames 8-byte aligned, stride and pitch multiples of 8 (interior tiles)
     // fused 7-tap Gaussian (8U fixed point) of the tile into `blur` (null: no blur)
     uint8_t* blur;
     int blur_stride;           // multiple of 4, >= w
     long long blur_pitch;      // bytes between blurred frames
-    uint32_t t0, t1;           // taps 0-3 and 4-6 (+0) as bytes (the MFMA band operands)
+    const uint4* blur_ops;     // per lane: the MFMA band operands of the taps (blur_operands)
 };
 
+#ifndef MAGE_FAST_SCHED
+#define MAGE_FAST_SCHED 0  // 1: scheduling barriers between the ladders (register pressure experiment)
+#endif
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
 __device__ __forceinline__ uint32_t as_u32(h2 h) { return __builtin_bit_cast(uint32_t, h); }
@@ -126,26 +130,22 @@ __device__ __forceinline__ h2 fast_raw2(const h2 (&w)[7][9])
     h2 x[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) x[k] = w[ring_dy(k) + 3][4 + 2 * P + ring_dx(k) - 1];
-    h2 n3[16], x3[16];
+    // the two ladders one after the other (16 3-arc extrema live at a time, not 32)
+    h2 t3[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        n3[k] = min3h(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
-        x3[k] = max3h(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
-    }
-    h2 n9[16], x9[16];
+    for (int k = 0; k < 16; k++) t3[k] = max3h(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
+    h2 lo = min3h(max3h(t3[0], t3[3], t3[6]), max3h(t3[1], t3[4], t3[7]), max3h(t3[2], t3[5], t3[8]));
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        n9[k] = min3h(n3[k], n3[(k + 3) & 15], n3[(k + 6) & 15]);
-        x9[k] = max3h(x3[k], x3[(k + 3) & 15], x3[(k + 6) & 15]);
-    }
-    h2 lo = min3h(x9[0], x9[1], x9[2]), hi = max3h(n9[0], n9[1], n9[2]);
+    for (int k = 3; k < 15; k += 2)
+        lo = min3h(lo, max3h(t3[k], t3[(k + 3) & 15], t3[(k + 6) & 15]), max3h(t3[k + 1], t3[(k + 4) & 15], t3[(k + 7) & 15]));
+    lo = __builtin_elementwise_minimum(lo, max3h(t3[15], t3[2], t3[5]));  // A = v - lo
 #pragma unroll
-    for (int k = 3; k < 15; k += 2) {
-        lo = min3h(lo, x9[k], x9[k + 1]);
-        hi = max3h(hi, n9[k], n9[k + 1]);
-    }
-    lo = __builtin_elementwise_minimum(lo, x9[15]);  // A = v - lo
-    hi = __builtin_elementwise_maximum(hi, n9[15]);  // -B = hi - v
+    for (int k = 0; k < 16; k++) t3[k] = min3h(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
+    h2 hi = max3h(min3h(t3[0], t3[3], t3[6]), min3h(t3[1], t3[4], t3[7]), min3h(t3[2], t3[5], t3[8]));
+#pragma unroll
+    for (int k = 3; k < 15; k += 2)
+        hi = max3h(hi, min3h(t3[k], t3[(k + 3) & 15], t3[(k + 6) & 15]), min3h(t3[k + 1], t3[(k + 4) & 15], t3[(k + 7) & 15]));
+    hi = __builtin_elementwise_maximum(hi, min3h(t3[15], t3[2], t3[5]));  // -B = hi - v
     return __builtin_elementwise_maximum(v - lo, hi - v);
 }
 
@@ -173,6 +173,19 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const
                                           uint8_t (*img)[LW])
 {
     const int gx0 = blockIdx.x * TW - 8, gy0 = blockIdx.y * TH - 4;
+    if (p.qword_ok && gx0 >= 0 && gx0 + LW <= p.w && gy0 >= 0 && gy0 + LH <= p.h) {
+        // interior tile (most of them): 8-byte loads, no reflection, addresses by increment
+        constexpr int QW = LW / 8, RSTEP = FAST_THREADS / QW;  // 17 qwords per row, 7 rows per pass
+        const int c = threadIdx.x % QW, r0 = threadIdx.x / QW;
+        if (r0 < RSTEP) {
+            const uint8_t* g = src + (long long)(gy0 + r0) * p.stride + gx0 + 8 * c;
+            const long long gstep = (long long)RSTEP * p.stride;
+#pragma unroll
+            for (int r = r0; r < LH; r += RSTEP, g += gstep)
+                *reinterpret_cast<uint2*>(&img[r][8 * c]) = *reinterpret_cast<const uint2*>(g);
+        }
+        return;
+    }
     constexpr int DW = LW / 4;
     for (int i = threadIdx.x; i < LH * DW; i += FAST_THREADS) {
         const int r = i / DW, c = i - r * DW;
@@ -204,26 +217,40 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
         if (X0 + q >= 3 && X0 + q <= p.w - 4) colmask |= 0xFFu << (8 * q);
     const _Float16 t = (_Float16)(float)p.threshold;
     const h2 tf = {t, t};
-    // window rows: LDS row (score row) + dy + 3; the strip needs LDS rows SR*chunk .. +SR+5
-    h2 w[SR + 6][9];
+    // window rows: LDS row (score row) + dy + 3; the strip needs LDS rows SR*chunk .. +SR+5.
+    // A rolling 7-row window of f16 pairs; row r + 7's dwords are fetched one row ahead, and a
+    // scheduling barrier per row keeps the compiler from hoisting every row's LDS reads (and
+    // their registers) to the top: the strip fits 96 VGPRs, 5 waves per SIMD.
     const uint32_t* base = reinterpret_cast<const uint32_t*>(&img[SR * chunk][0]) + gx;
+    h2 win[7][9];
 #pragma unroll
-    for (int r = 0; r < SR + 6; r++) {
+    for (int r = 0; r < 6; r++) {
         const uint32_t* rp = base + r * (LW / 4);
-        window_row(rp[0], rp[1], rp[2], w[r]);
+        window_row(rp[0], rp[1], rp[2], win[r + 1]);
     }
+    uint32_t nx0 = base[6 * (LW / 4)], nx1 = base[6 * (LW / 4) + 1], nx2 = base[6 * (LW / 4) + 2];
 #pragma unroll
     for (int r = 0; r < SR; r++) {
-        h2 win[7][9];
 #pragma unroll
-        for (int k = 0; k < 7; k++)
+        for (int k = 0; k < 6; k++)
 #pragma unroll
-            for (int i = 0; i < 9; i++) win[k][i] = w[r + k][i];
-        const uint32_t s0 = score2(fast_raw2<0>(win), tf), s1 = score2(fast_raw2<1>(win), tf);
+            for (int i = 0; i < 9; i++) win[k][i] = win[k + 1][i];
+        window_row(nx0, nx1, nx2, win[6]);
+        if (r + 1 < SR) {
+            const uint32_t* rp = base + (r + 7) * (LW / 4);
+            nx0 = rp[0];
+            nx1 = rp[1];
+            nx2 = rp[2];
+        }
+        const uint32_t s0 = score2(fast_raw2<0>(win), tf);
+        const uint32_t s1 = score2(fast_raw2<1>(win), tf);
         uint32_t bytes = __builtin_amdgcn_perm(s1, s0, 0x06040200u);  // low bytes of the 4 lanes
         const int Y = Y0 + r;
         if (Y < 3 || Y > p.h - 4) bytes = 0;
         sc[SR * chunk + r][gx] = bytes & colmask;
+#if MAGE_FAST_SCHED
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 }
 
@@ -239,38 +266,19 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
 //             (C = 128 * 257 for each, + 2^15 for lo); out = min(255, (Y + 2^15) >> 16).
 // The output (lane = column, registers = 4 rows) goes to the LDS tile as bytes.
 constexpr int BLUR_STRIPS = (TW + 15) / 16;  // 8 (the last is half used)
+constexpr int BT_W = 16 * BLUR_STRIPS;       // blurred tile row pitch (bytes)
+static_assert(32 * BT_W <= SROWS * GX * 4, "the blurred tile reuses the score buffer");
 
 __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], uint8_t* bt, const FastParams& p)
 {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n = lane & 15, g = lane >> 4;
-    auto tap = [&](int t) -> uint32_t {  // tap t (0..6), 0 outside the band
-        const uint32_t w = t < 4 ? p.t0 >> (8 * (t & 3)) : p.t1 >> (8 * ((t - 4) & 3));
-        return (t >= 0 && t <= 6) ? (w & 0xFFu) : 0u;
-    };
-    // row-pass B: lane holds B[k = 16 g + j][n] = tap[k - n - 5], j = 0..15 (bytes)
-    v4i tb;
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int e = 0; e < 4; e++) w |= tap(16 * g + 4 * d + e - n - 5) << (8 * e);
-        tb[d] = (int)w;
-    }
-    // col-pass A for output block o: lane holds A[m = n][K element j = 4 b + r] = tap of H row
-    // 16 b - 3 + 4 g + r for output row 16 o + m: tap[16 (b - o) + 4 g + r - n]; elements 12..15 zero
-    v4i ta[2];
-#pragma unroll
-    for (int o = 0; o < 2; o++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            uint32_t w = 0;
-            if (b < 3)
-#pragma unroll
-                for (int r = 0; r < 4; r++) w |= tap(16 * (b - o) + 4 * g + r - n) << (8 * r);
-            ta[o][b] = (int)w;
-        }
+    // the lane's band operands (host-built, blur_operands): row-pass B and col-pass A of both
+    // output blocks
+    const uint4 o0 = p.blur_ops[3 * lane], o1 = p.blur_ops[3 * lane + 1], o2 = p.blur_ops[3 * lane + 2];
+    const v4i tb = {(int)o0.x, (int)o0.y, (int)o0.z, (int)o0.w};
+    const v4i ta[2] = {{(int)o1.x, (int)o1.y, (int)o1.z, (int)o1.w}, {(int)o2.x, (int)o2.y, (int)o2.z, (int)o2.w}};
     const v4i c_row = {32896, 32896, 32896, 32896};                      // 128 * 257
     const v4i c_hi = c_row, c_lo = {65664, 65664, 65664, 65664};         // + 2^15
     for (int s = wave; s < BLUR_STRIPS; s += FAST_THREADS / kWave) {
@@ -280,17 +288,13 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], uint8_t* bt,
         v4i H[3];
 #pragma unroll
         for (int b = 0; b < 3; b++) {
-            v4i a = {0, 0, 0, 0};
-            if (g < 2) {
-                const int row = min(16 * b + 1 + n, LH - 1);
-                const int c0 = min(16 * s + 16 * g, LW - 8), c1 = min(16 * s + 16 * g + 8, LW - 8);
-                const uint2 d0 = *reinterpret_cast<const uint2*>(&img[row][c0]);
-                const uint2 d1 = *reinterpret_cast<const uint2*>(&img[row][c1]);
-                a[0] = (int)(d0.x ^ 0x80808080u);
-                a[1] = (int)(d0.y ^ 0x80808080u);
-                a[2] = (int)(d1.x ^ 0x80808080u);
-                a[3] = (int)(d1.y ^ 0x80808080u);
-            }
+            // lanes g >= 2 meet zero band bytes: whatever they load (clamped in the row) adds 0
+            const int row = min(16 * b + 1 + n, LH - 1);
+            const int c0 = min(16 * s + 16 * g, LW - 8), c1 = min(16 * s + 16 * g + 8, LW - 8);
+            const uint2 d0 = *reinterpret_cast<const uint2*>(&img[row][c0]);
+            const uint2 d1 = *reinterpret_cast<const uint2*>(&img[row][c1]);
+            const v4i a = {(int)(d0.x ^ 0x80808080u), (int)(d0.y ^ 0x80808080u), (int)(d1.x ^ 0x80808080u),
+                           (int)(d1.y ^ 0x80808080u)};
             H[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, tb, c_row, 0, 0, 0);
         }
         // bytes of H (<= 65535): per block one dword of lo bytes and one of hi bytes (^ 0x80)
@@ -302,22 +306,23 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], uint8_t* bt,
             lo[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u);
             hi[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x07060302u) ^ 0x80808080u);
         }
-        const int c = 16 * s + n;
+        // bt is 32 x BT_W bytes: the discarded rows 30, 31 and columns 120..127 land in padding
+        uint8_t* o_col = bt + 16 * s + n + 4 * g * BT_W;
 #pragma unroll
         for (int o = 0; o < 2; o++) {
             const v4i yh = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[o], hi, c_hi, 0, 0, 0);
             const v4i yl = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[o], lo, c_lo, 0, 0, 0);
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = 16 * o + 4 * g + r;
-                const uint32_t v = min(255u, (((uint32_t)yh[r] << 8) + (uint32_t)yl[r]) >> 16);
-                if (row < TH && c < TW) bt[row * TW + c] = (uint8_t)v;
-            }
+            for (int r = 0; r < 4; r++)
+                o_col[(16 * o + r) * BT_W] = (uint8_t)min(255u, (((uint32_t)yh[r] << 8) + (uint32_t)yl[r]) >> 16);
         }
     }
 }
 
-__global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* __restrict__ frames,
+#ifndef MAGE_FAST_WAVES_PER_EU
+#define MAGE_FAST_WAVES_PER_EU 5  // 86 VGPRs, no spills (tools/ablate_fast.py)
+#endif
+__global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms_kernel(const uint8_t* __restrict__ frames,
                                                                 FastParams p,
                                                                 uint32_t* __restrict__ cand,
                                                                 uint32_t* __restrict__ counts)
@@ -425,12 +430,14 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_nms_kernel(const uint8_t* _
         blur_mfma(img, reinterpret_cast<uint8_t*>(bt), p);
         __syncthreads();
         // blurred tile -> frame (rows < h, dword columns < blur_stride)
-        uint8_t* dst = p.blur + (long long)f * p.blur_pitch;
-        for (int i = threadIdx.x; i < TH * (TW / 4); i += FAST_THREADS) {
-            const int r = i / (TW / 4), c = i - r * (TW / 4);
-            const int Y = blockIdx.y * TH + r, X = blockIdx.x * TW + 4 * c;
-            if (Y < p.h && X < p.blur_stride)
-                *reinterpret_cast<uint32_t*>(dst + (long long)Y * p.blur_stride + X) = bt[r * (TW / 4) + c];
+        constexpr int CW = TW / 4, RSTEP = FAST_THREADS / CW;  // 30 dword columns, 4 rows per pass
+        const int c = threadIdx.x % CW, r0 = threadIdx.x / CW;
+        const int X = blockIdx.x * TW + 4 * c, ylim = min(TH, p.h - (int)blockIdx.y * TH);
+        if (r0 < RSTEP && X < p.blur_stride) {
+            uint8_t* dst = p.blur + (long long)f * p.blur_pitch + (long long)(blockIdx.y * TH + r0) * p.blur_stride + X;
+            const long long dstep = (long long)RSTEP * p.blur_stride;
+            for (int r = r0; r < ylim; r += RSTEP, dst += dstep)
+                *reinterpret_cast<uint32_t*>(dst) = bt[r * (BT_W / 4) + c];
         }
     }
     if (kSink || !kEmit) {  // ablation: keep the skipped stages' inputs alive
@@ -1166,7 +1173,7 @@ struct OrbDetector {
     int R = 7;
     bool random_pattern = false;  // PatchSize not 15 / 31: MakeRandomPattern + per-keypoint rotation
     Geometry geo;
-    DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n, blurred, pyr, rtab, lvl;
+    DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n, blurred, pyr, rtab, lvl, blur_ops;
 };
 
 namespace {
@@ -1189,6 +1196,32 @@ void make_random_pattern(int patch, int8_t out[1024])
 
 // cv::getGaussianKernel(ksize, 2, CV_32F) -> convertTo(CV_32S, 1<<8) (OpenCV 3.4.0
 // createSeparableLinearFilter, 8U smoothing path; see DESIGN.md §Blur for why this path).
+// Lane operands of blur_mfma for the 7 taps, 3 x uint4 per lane (i8 bytes):
+//   [0] row-pass B: B[k = 16 g + j][n] = tap[k - n - 5]
+//   [1], [2] col-pass A of output block o = 0, 1: A[m = n][K element 4 b + r] = tap of H row
+//            16 b - 3 + 4 g + r for output row 16 o + m = tap[16 (b - o) + 4 g + r - n] (b < 3)
+// with n = lane & 15, g = lane >> 4, out-of-band taps 0.
+void blur_operands(const int* taps, uint32_t out[64 * 12])
+{
+    auto tap = [&](int t) -> uint32_t { return (t >= 0 && t <= 6) ? (uint32_t)taps[t] & 0xFFu : 0u; };
+    for (int lane = 0; lane < 64; lane++) {
+        const int n = lane & 15, g = lane >> 4;
+        uint32_t* o = out + 12 * lane;
+        for (int d = 0; d < 4; d++) {
+            uint32_t w = 0;
+            for (int e = 0; e < 4; e++) w |= tap(16 * g + 4 * d + e - n - 5) << (8 * e);
+            o[d] = w;
+        }
+        for (int ob = 0; ob < 2; ob++)
+            for (int b = 0; b < 4; b++) {
+                uint32_t w = 0;
+                if (b < 3)
+                    for (int r = 0; r < 4; r++) w |= tap(16 * (b - ob) + 4 * g + r - n) << (8 * r);
+                o[4 + 4 * ob + b] = w;
+            }
+    }
+}
+
 void gaussian_taps(int ksize, double sigma, int* taps)
 {
     std::vector<float> cf(ksize);
@@ -1392,16 +1425,15 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         if (H <= 2 * border || W <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
         fp.cand_cap = v.cand_cap;
         fp.dword_ok = (fp.stride % 4 == 0) && (fp.pitch % 4 == 0) && ((uintptr_t)raw.base[l] % 4 == 0);
+        fp.qword_ok = (fp.stride % 8 == 0) && (fp.pitch % 8 == 0) && ((uintptr_t)raw.base[l] % 8 == 0);
         if (fused_blur) {
-            const int* k = o->taps;
             blurred.base[l] = o->blurred.as<uint8_t>() + (size_t)batch * v.boff;
             blurred.pitch[l] = v.pitch;
             blurred.stride[l] = v.stride;
             fp.blur = const_cast<uint8_t*>(blurred.base[l]);
             fp.blur_stride = v.stride;
             fp.blur_pitch = v.pitch;
-            fp.t0 = (uint32_t)k[0] | ((uint32_t)k[1] << 8) | ((uint32_t)k[2] << 16) | ((uint32_t)k[3] << 24);
-            fp.t1 = (uint32_t)k[4] | ((uint32_t)k[5] << 8) | ((uint32_t)k[6] << 16);
+            fp.blur_ops = o->blur_ops.as<uint4>();
         }
         uint32_t* cand = o->cand.as<uint32_t>() + (size_t)batch * v.coff;
         uint32_t* counts = o->counts.as<uint32_t>() + (size_t)batch * l;
@@ -1677,6 +1709,19 @@ mage_status mage_orb_create(const mage_orb_settings* settings, int device, mage_
         mage::set_error("pattern upload failed");
         return MAGE_EDEVICE;
     }
+    if (s.gaussian_kernel_size == 7) {  // the fused MFMA blur's band operands
+        uint32_t ops[64 * 12];
+        mage::blur_operands(o->taps, ops);
+        if ((r = o->blur_ops.reserve(sizeof(ops))) != MAGE_OK) {
+            delete o;
+            return r;
+        }
+        if (hipMemcpy(o->blur_ops.ptr, ops, sizeof(ops), hipMemcpyHostToDevice) != hipSuccess) {
+            delete o;
+            mage::set_error("blur operand upload failed");
+            return MAGE_EDEVICE;
+        }
+    }
     *out = o;
     return MAGE_OK;
 }
@@ -1685,7 +1730,7 @@ mage_status mage_orb_destroy(mage_orb* orb)
 {
     if (!orb) return MAGE_OK;
     for (auto* b : {&orb->pattern, &orb->cand, &orb->counts, &orb->xy, &orb->status, &orb->img, &orb->kp,
-                    &orb->desc, &orb->n, &orb->blurred, &orb->pyr, &orb->rtab, &orb->lvl})
+                    &orb->desc, &orb->n, &orb->blurred, &orb->pyr, &orb->rtab, &orb->lvl, &orb->blur_ops})
         b->release();
     delete orb;
     return MAGE_OK;
@@ -1777,6 +1822,7 @@ mage_status mage_orb_fast_score_map(const uint8_t* img, int32_t width, int32_t h
     fp.stride = stride;
     fp.threshold = std::min(std::max((int)threshold, 0), 255);
     fp.dword_ok = (width % 4 == 0) && (stride % 4 == 0);
+    fp.qword_ok = (stride % 8 == 0);
     hipError_t e = hipMemcpy(dimg.ptr, img, (size_t)stride * height, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
         dim3 g((width + mage::TW - 1) / mage::TW, (height + mage::TH - 1) / mage::TH);

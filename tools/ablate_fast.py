@@ -3,7 +3,8 @@
   python tools/ablate_fast.py build     # compile variants into abl/f<N>/libmage_hot.so (CPU)
   python tools/ablate_fast.py run       # time orb.fast_nms of each variant on the GPU (C2 batch)
 
-MAGE_FAST_ABLATE bits: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load.
+MAGE_FAST_ABLATE bits: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load, 16 NMS without
+emission, 32 keep the skipped stages' inputs alive.  "a:w:s" also sets __launch_bounds__ min waves per EU (w) and MAGE_FAST_SCHED (s).
 """
 import ctypes as C
 import subprocess
@@ -11,7 +12,8 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-VARIANTS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 2, 3, 5, 7, 15]
+# variant "a" or "a:w" (ablation bits a, __launch_bounds__ min waves per EU w)
+VARIANTS = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "17", "35", "39", "47"]
 
 
 def build():
@@ -20,11 +22,14 @@ def build():
     B.build()
     objs = [p for p in (B.OBJ).glob("*.o") if not p.name.startswith("orb")]
     for v in VARIANTS:
-        out = ROOT / "abl" / f"f{v}"
+        out = ROOT / "abl" / ("f" + v.replace(":", "w"))
         out.mkdir(parents=True, exist_ok=True)
         obj = out / "orb.o"
+        a, w, sch = (v.split(":") + ["", ""])[:3]
         subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON,
-                        f"-DMAGE_FAST_ABLATE={v}", "-c", str(B.CSRC / "orb.hip"), "-o", str(obj)], check=True)
+                        f"-DMAGE_FAST_ABLATE={a}", f"-DMAGE_FAST_WAVES_PER_EU={w or 5}", f"-DMAGE_FAST_SCHED={sch or 0}",
+                        "-c", str(B.CSRC / "orb.hip"),
+                        "-o", str(obj)], check=True)
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
                         str(obj), *map(str, objs)], check=True)
         print("built", out)
@@ -40,7 +45,7 @@ def run():
     desc = torch.zeros((B, N, 32), dtype=torch.uint8, device="cuda")
     cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
     for v in VARIANTS:
-        L = C.CDLL(str(ROOT / "abl" / f"f{v}" / "libmage_hot.so"))
+        L = C.CDLL(str(ROOT / "abl" / ("f" + v.replace(":", "w")) / "libmage_hot.so"))
         _lib._declare(L)
         _lib._lib = L
         orb.synth_frames_device(frames, B, W, H, 0, synth.FRAME_SEED)
@@ -56,7 +61,7 @@ def run():
         rep = _lib.profile_report()
         L.mage_profile_enable(0)
         c, ms = rep.get("orb.fast_nms", (1, float("nan")))
-        print(f"variant {v:2d}: fast_nms {ms / c:.4f} ms  select {rep.get('orb.select', (1, 0))[1] / 10:.4f} ms  "
+        print(f"variant {v:>5}: fast_nms {ms / c:.4f} ms  select {rep.get('orb.select', (1, 0))[1] / 10:.4f} ms  "
               f"mean keypoints {cnt.float().mean().item():.0f}", flush=True)
         det.close()
 
