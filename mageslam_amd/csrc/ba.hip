@@ -13,10 +13,11 @@
 //   reject on the host):
 //     edge_schur      thread/point-edge: Dinv_p = (Hll + lambda I)^-1, db = Dinv bl (first edge
 //                     of each point), Z_e = Hpl_e Dinv_p (6x3) for every edge
-//     schur_pairs     workgroup per covisible camera pair (h1 <= h2): walk c1's point-sorted
-//                     edges, find c2's edge on the same point in the block x point index,
-//                     accumulate sum_p Z_{c1 p} Hpl_{c2 p}^T in registers, one deterministic
-//                     workgroup reduction, write the 6x6 block (+ Hpp + lambda I, rhs on h1 = h2)
+//     schur_chunks    per covisible camera pair (h1 <= h2) the Schur products (e1, e2) of its
+//                     shared points, listed at initialisation and cut into 512-entry chunks: a
+//                     workgroup per chunk (no dependent index walk), reduce-scatter sums, the
+//                     last chunk of a pair adds the partials in order and writes the 6x6 block
+//                     (+ Hpp + lambda I, rhs on h1 = h2); block rows grouped per XCD
 //     chol_tiles      one workgroup, np <= 240: register-resident 16x16 upper tiles over 8
 //                     waves; per step the owner factors the diagonal block (Cholesky, inverse
 //                     and forward substitution in one column loop, look-ahead under the
@@ -52,6 +53,9 @@ constexpr int BA_THREADS = 256;
 // parallel and the point sums close with a fixed shuffle tree (deterministic).
 constexpr int PG = 32;
 
+// components of the per-edge Schur records (edge_schur): Q = (x/z, y/z, f/z, W), G
+constexpr int EQ_N = 9, EG_N = 6;
+
 template <int N>
 __device__ __forceinline__ void group_sum(double (&v)[N])
 {
@@ -59,6 +63,57 @@ __device__ __forceinline__ void group_sum(double (&v)[N])
     for (int off = PG / 2; off > 0; off >>= 1)
 #pragma unroll
         for (int k = 0; k < N; k++) v[k] += __shfl_xor(v[k], off);
+}
+
+// Butterfly reduce-scatter of N doubles over a group of LANES lanes (xor offsets LANES/2 .. 1):
+// per step the lanes without the offset bit keep the first ceil(n/2) entries and the others the
+// rest; each lane sends the half it gives up, so a step costs ceil(n/2) shuffles instead of n
+// (42 entries over 64 lanes: 44 shuffles instead of 252).  Afterwards the lane holds the group
+// total of entry rs_entry() in a[0] (-1: none).  Fixed order, deterministic.
+template <int N, int LANES>
+__device__ __forceinline__ int reduce_scatter(double (&a)[N], int lane)
+{
+    static_assert(N <= LANES, "one entry per lane at most");
+    // the split sizes are uniform (n, h at compile time); `cnt` is the lane's count of real
+    // entries in its range (the upper half of an odd range carries one zero pad)
+    int lo = 0, cnt = N;
+    int n = N;
+#pragma unroll
+    for (int off = LANES / 2; off > 0; off >>= 1) {
+        const int h = (n + 1) / 2;
+        const bool hi = (lane & off) != 0;
+#pragma unroll
+        for (int i = 0; i < h; i++) {
+            const double up = (i + h < n) ? a[i + h] : 0.0;
+            const double send = hi ? a[i] : up;
+            const double keep = hi ? up : a[i];
+            a[i] = keep + __shfl_xor(send, off);
+        }
+        if (hi) {
+            lo += h;
+            cnt -= h;
+        } else {
+            cnt = cnt < h ? cnt : h;
+        }
+        n = h;
+    }
+    return cnt > 0 ? lo : -1;
+}
+
+// The lane (within its group) that reduce_scatter<N, LANES> leaves entry k in.
+template <int N, int LANES>
+__host__ __device__ constexpr int rs_lane_of(int k)
+{
+    int lane = 0, lo = 0, n = N;
+    for (int off = LANES / 2; off > 0; off >>= 1) {
+        const int h = (n + 1) / 2;
+        if (k >= lo + h) {
+            lane |= off;
+            lo += h;
+        }
+        n = h;
+    }
+    return lane;
 }
 
 // Per point: edge errors, robust chi2, Hll, bl, Hpl per edge (BlockSolver::buildSystem with
@@ -82,7 +137,14 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
     const int e0 = pb.pstart[p], e1 = pb.pstart[p + 1];
     for (int a = e0 + sub; a < e1; a += PG) {
         const int e = pb.pedges[a];
-        if (!pb.active[e]) continue;
+        if (!pb.active[e]) {
+            // the Schur products read Hpl of every listed edge: a removed edge contributes zero
+            if (free_p && pb.camh[pb.ecam[e]] >= 0) {
+                double* o = Hpl + pb.epos[e];
+                for (int k = 0; k < EQ_N; k++) o[(long long)k * pb.ecsr] = 0;
+            }
+            continue;
+        }
         double ev[2], xc[3], rho0, rho1;
         edge_eval(pb, s, e, ev, xc, rho0, rho1);
         err[2 * e] = ev[0];
@@ -114,31 +176,38 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
         H[4] += (J[1] * J[2] + J[4] * J[5]) * w;
         H[5] += (J[2] * J[2] + J[5] * J[5]) * w;
         if (pb.camh[c] >= 0) {
-            double Jp[12];
-            jac_pose(xc, f, Jp);
-            double* o = Hpl + 18 * (long long)e;
-            for (int r = 0; r < 6; r++)
-                for (int k = 0; k < 3; k++) o[r * 3 + k] = (Jp[r] * J[k] + Jp[6 + r] * J[3 + k]) * w;
+            // Hpl_e = Jp^T (w J): kept factored as (x/z, y/z, f/z) + W = w J (camera-major
+            // component arrays; schur_chunks reads them coalesced)
+            double* o = Hpl + pb.epos[e];
+            const long long es = pb.ecsr;
+            o[0] = xi;
+            o[es] = yi;
+            o[2 * es] = f * iz;
+            for (int k = 0; k < 6; k++) o[(3 + k) * es] = J[k] * w;
         }
     }
-    group_sum(acc);
-    if (sub != 0) return;
-    chi_part[p] = chi;
-    if (!linearize) return;
+    // group sums by reduce-scatter: lane `sub` ends up with entry k of acc (H 00 01 02 11 12 22,
+    // g 0 1 2, chi) and writes it
+    const int k = reduce_scatter<10, PG>(acc, sub);
+    const double v = acc[0];
+    const int gbase = (threadIdx.x & (kWave - 1)) & ~(PG - 1);
+    if (linearize) {
+        const double d0 = __shfl(v, gbase + rs_lane_of<10, PG>(0)), d1 = __shfl(v, gbase + rs_lane_of<10, PG>(3)),
+                     d2 = __shfl(v, gbase + rs_lane_of<10, PG>(5));
+        if (sub == rs_lane_of<10, PG>(0)) maxd_part[p] = free_p ? fmax(fabs(d0), fmax(fabs(d1), fabs(d2))) : 0.0;
+    }
+    if (k == 9) chi_part[p] = v;
+    if (!linearize || k < 0 || k == 9) return;
+    if (k >= 6) {
+        bl[3 * p + (k - 6)] = v;
+        return;
+    }
+    // packed upper (00 01 02 11 12 22) -> both symmetric positions of the 3x3
+    constexpr int r_of[6] = {0, 0, 0, 1, 1, 2}, c_of[6] = {0, 1, 2, 1, 2, 2};
     double* Ho = Hll + 9 * (long long)p;
-    Ho[0] = H[0];
-    Ho[1] = H[1];
-    Ho[2] = H[2];
-    Ho[3] = H[1];
-    Ho[4] = H[3];
-    Ho[5] = H[4];
-    Ho[6] = H[2];
-    Ho[7] = H[4];
-    Ho[8] = H[5];
-    bl[3 * p] = g[0];
-    bl[3 * p + 1] = g[1];
-    bl[3 * p + 2] = g[2];
-    maxd_part[p] = free_p ? fmax(fabs(H[0]), fmax(fabs(H[3]), fabs(H[5]))) : 0.0;
+    const int r = r_of[k], c = c_of[k];
+    Ho[3 * r + c] = v;
+    Ho[3 * c + r] = v;
 }
 
 // Tether edges (thread per tether; a window carries a handful): error and chi2 = e^T Omega e
@@ -229,17 +298,14 @@ __global__ __launch_bounds__(64) void tether_eval(const Tether* __restrict__ tet
             }
 }
 
-// Block sum of `acc[N]` over a workgroup of T threads; the result lands in red[0][0..N).
+// Block sum of `acc[N]` over a workgroup of T threads; the result lands in red[0][0..N).  Per
+// wave a reduce-scatter (each lane ends with one entry), then the waves' partials in order.
 template <int N, int T = BA_THREADS>
 __device__ __forceinline__ void block_sum(double (&acc)[N], double (*red)[N])
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        double v = acc[k];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) red[wave][k] = v;
-    }
+    const int k = reduce_scatter<N, kWave>(acc, lane);
+    if (k >= 0) red[wave][k] = acc[0];
     __syncthreads();
     if (threadIdx.x < N) {
         double v = 0;
@@ -366,11 +432,21 @@ __global__ __launch_bounds__(1024) void linearize_finish(int nb, const int* __re
     }
 }
 
-// Fixed-order reduction of two sum arrays and one max array into out[0..2].
+struct OutlierCtl {
+    double osum[2][2];
+    int fail;
+    uint32_t count[2];
+    uint32_t ticket;
+};
+
+// Fixed-order reduction of two sum arrays and one max array into out[0..2]; with ns > 0 also
+// the outlier pass's per-block (sum, count) partials of its ns states into ctl->osum.
 __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, int na,
                                                 const double* __restrict__ b, int nb,
                                                 const double* __restrict__ m, int nm,
-                                                double* __restrict__ out)
+                                                double* __restrict__ out,
+                                                const double* __restrict__ opart, int oblocks, int ns,
+                                                OutlierCtl* __restrict__ ctl)
 {
     __shared__ double sa[1024], sb[1024], sm[1024];
     double va = 0, vb = 0, vm = 0;
@@ -394,6 +470,28 @@ __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, in
         out[1] = sb[0];
         out[2] = sm[0];
     }
+    for (int k = 0; k < ns; k++) {
+        __syncthreads();
+        double vs = 0, vc = 0;
+        for (int i = threadIdx.x; i < oblocks; i += 1024) {
+            vs += opart[(2 * k) * oblocks + i];
+            vc += opart[(2 * k + 1) * oblocks + i];
+        }
+        sa[threadIdx.x] = vs;
+        sb[threadIdx.x] = vc;
+        __syncthreads();
+        for (int s = 512; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) {
+                sa[threadIdx.x] += sa[threadIdx.x + s];
+                sb[threadIdx.x] += sb[threadIdx.x + s];
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            ctl->osum[k][0] = sa[0];
+            ctl->osum[k][1] = sb[0];
+        }
+    }
 }
 
 // Eigen Matrix3d::inverse (cofactors)
@@ -415,21 +513,30 @@ __device__ __forceinline__ void d_inv3(const double m[9], double o[9])
     o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
 }
 
-// Per point-edge entry a (point-CSR order, so a point's entries are adjacent): D_p = Hll_p +
-// lambda I, Dinv_p by cofactors (each entry of the point recomputes it; the first one stores
-// db_p = Dinv_p bl_p) and Z_e = Hpl_e Dinv_p (6x3), the factor every Schur product and the
-// point back-substitution of edge e reuse.
-__global__ __launch_bounds__(BA_THREADS) void edge_schur(Problem pb, int nentries, const double* __restrict__ Hll,
-                                                         const double* __restrict__ bl,
-                                                         const double* __restrict__ Hpl, double lambda,
-                                                         double* __restrict__ db,
-                                                         double* __restrict__ Z)
+// Per-edge factors of the Schur sweeps, camera-major component arrays (entry k of edge record a
+// at k * ecsr + a, a = the edge's camera-CSR position):
+//   Q (EQ_N = 9): x/z, y/z, f/z of the point in the camera (the pose Jacobian Jp, jac_pose_q)
+//                 and W = w J_point (2x3), so Hpl_e = Jp^T W;
+//   G (6):        G = W Dinv_p (2x3), so Z_e = Hpl_e Dinv_p = Jp^T G.
+// A Schur product Z_e1 Hpl_e2^T = Jp1^T (G1 W2^T) Jp2 then reads 18 doubles instead of 36.
+
+// Per camera-CSR entry a: D_p = Hll_p + lambda I, Dinv_p by cofactors (recomputed per entry) and
+// G_a = W_a Dinv_p.  Entries of fixed cameras take no part; a point that lost its last edge gets
+// G = 0.
+__global__ __launch_bounds__(BA_THREADS) void edge_schur(Problem pb, const double* __restrict__ Hll,
+                                                         const double* __restrict__ Q, double lambda,
+                                                         double* __restrict__ G)
 {
     const int a = blockIdx.x * BA_THREADS + threadIdx.x;
-    if (a >= nentries) return;
-    const int e = pb.pedges[a];
-    const int p = pb.ept[e];
-    if (!pb.ptfree[p]) return;
+    if (a >= pb.ecsr) return;
+    const int e = pb.cedges[a];
+    if (pb.camh[pb.ecam[e]] < 0) return;
+    const int p = pb.cpt[a];
+    const long long es = pb.ecsr;
+    if (!pb.ptfree[p]) {
+        for (int k = 0; k < EG_N; k++) G[k * es + a] = 0;
+        return;
+    }
     double D[9], Di[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
@@ -437,107 +544,192 @@ __global__ __launch_bounds__(BA_THREADS) void edge_schur(Problem pb, int nentrie
     D[4] += lambda;
     D[8] += lambda;
     d_inv3(D, Di);
-    if (a == pb.pstart[p]) {
-        const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
+    double w[6];
 #pragma unroll
-        for (int r = 0; r < 3; r++) db[3 * p + r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
-    }
-    const double* W = Hpl + 18 * (long long)e;
-    double w[18];
+    for (int k = 0; k < 6; k++) w[k] = Q[(3 + k) * es + a];
 #pragma unroll
-    for (int k = 0; k < 18; k++) w[k] = W[k];
-    double* Ze = Z + 18 * (long long)e;
-#pragma unroll
-    for (int r = 0; r < 6; r++)
+    for (int i = 0; i < 2; i++)
 #pragma unroll
         for (int k = 0; k < 3; k++)
-            Ze[r * 3 + k] = w[r * 3] * Di[k] + w[r * 3 + 1] * Di[3 + k] + w[r * 3 + 2] * Di[6 + k];
+            G[(i * 3 + k) * es + a] = w[i * 3] * Di[k] + w[i * 3 + 1] * Di[3 + k] + w[i * 3 + 2] * Di[6 + k];
 }
 
-// One covisible camera pair (h1 <= h2) per workgroup (BlockSolver::solve Schur loop):
+// Schur complement (BlockSolver::solve's Schur loop), per covisible camera pair (h1 <= h2):
 //   S[h1][h2] = delta(h1,h2) (Hpp_c1 + lambda I) - sum_p Hpl_{c1 p} Dinv_p Hpl_{c2 p}^T
 //   rhs[h1]   = bp_c1 - sum_p Hpl_{c1 p} Dinv_p bl_p                          (h1 == h2 only)
-// The shared points come from walking c1's point-sorted edges and looking each point up in
-// c2's row of the block x point index (first position of the point in c2's list, -1 if c2 does
-// not see it): one dependent load instead of a binary search.  Each thread accumulates its 6x6
-// partial in registers (no atomics, deterministic).
-__global__ __launch_bounds__(BA_THREADS) void schur_pairs(Problem pb, const int2* __restrict__ pairs,
-                                                          const int* __restrict__ cam_of_block,
-                                                          const int* __restrict__ blkidx,
-                                                          const double* __restrict__ Hpp,
-                                                          const double* __restrict__ bp,
-                                                          const double* __restrict__ Hpl,
-                                                          const double* __restrict__ Z,
-                                                          const double* __restrict__ bl, double lambda,
-                                                          int np, int npairs, const int* __restrict__ ptstart,
-                                                          const int* __restrict__ ptlist,
-                                                          const double* __restrict__ tout, double* __restrict__ S,
-                                                          double* __restrict__ rhs)
+// The products are enumerated once per initialisation: a pair's list holds (e1, e2) for every
+// shared free point (c1's edge e1, c2's edge e2; on the diagonal every ordered pair of the
+// camera's edges on the point), and the diagonal pair carries a second list of (e, p) for the rhs.
+// Lists are cut into chunks of <= SC_CHUNK entries, one 256-thread workgroup per chunk: each
+// thread loads its two entries, then Z_e1 = Hpl_e1 Dinv_p (edge_schur) and Hpl_e2 (or bl_p) with
+// no further dependent load, accumulates the 6x6 (+ 6 rhs) in registers, and the chunk sum is
+// a reduce-scatter + LDS tree.  Inactive edges have zero Hpl / Z (point_linearize, edge_schur),
+// so no flag is read.  A pair of one chunk finishes in place; otherwise its chunks write partials
+// and schur_finish adds them in chunk order (deterministic; a last-arriver ticket would need an
+// agent-scope fence = a full L2 write-back per workgroup on gfx950).  XCD-aware: the chunks of
+// one block row of S run on one XCD (block b on XCD b % 8), so Z_{c1 .} stays in that L2.
+constexpr int SC_THREADS = 256;
+constexpr int SC_CHUNK = 2 * SC_THREADS;
+
+struct SchurChunk {
+    int pair;   // -1: padding block
+    int start;  // first entry
+    int count;  // entries (<= SC_CHUNK); the rhs list's chunks have kind 1
+    int kind;   // 0 products (e1, e2), 1 rhs (e, p)
+    int slot;   // partial slot of this chunk (pairs of more than one chunk)
+    int pad0, pad1, pad2;
+};
+struct SchurPair {
+    int h1, h2, c1;
+    int slot0, nslots;  // partial slots [slot0, slot0 + nslots); nslots = 1: finished in place
+    int tbeg, tend;     // tether H12 blocks of this pair: ptlist[tbeg, tend)
+    int c2;
+};
+
+// Entry k < 42 of a pair's sum -> S (both triangles; + Hpp + lambda I on the diagonal, + tether
+// H12 blocks) or rhs (k >= 36, diagonal pairs).
+__device__ __forceinline__ void schur_write(const SchurPair& pr, int k, double sum, const double* __restrict__ Hpp,
+                                            const double* __restrict__ bp, double lambda, int np,
+                                            const int* __restrict__ ptlist, const double* __restrict__ tout,
+                                            double* __restrict__ S, double* __restrict__ rhs)
 {
-    __shared__ double red[BA_THREADS / kWave][42];
-    // XCD-aware order: block b runs on XCD b % 8; each XCD takes a contiguous run of the
-    // row-major pair list, so a row's Z_{c1 .} stays in that XCD's L2 across its pairs
-    const int chunk = (npairs + 7) >> 3;
-    const int pi = (blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
-    if (pi >= npairs) return;
-    const int2 hp = pairs[pi];
-    const int h1 = hp.x, h2 = hp.y;
-    const int c1 = cam_of_block[h1], c2 = cam_of_block[h2];
-    const bool diag = h1 == h2;
+    const bool diag = pr.h1 == pr.h2;
+    if (k < 36) {
+        const int r = k / 6, c = k % 6;
+        double v = -sum;
+        if (diag) v += Hpp[36 * (long long)pr.c1 + k] + (r == c ? lambda : 0.0);
+        // tether H12 blocks of this camera pair (code = 2 t + transposed)
+        for (int j = pr.tbeg; j < pr.tend; j++) {
+            const int code = ptlist[j];
+            const double* H12 = tout + (long long)(code >> 1) * TETHER_OUT + 72;
+            v += (code & 1) ? H12[c * 6 + r] : H12[r * 6 + c];
+        }
+        S[(long long)(6 * pr.h1 + r) * np + 6 * pr.h2 + c] = v;
+        S[(long long)(6 * pr.h2 + c) * np + 6 * pr.h1 + r] = v;
+    } else if (diag) {
+        rhs[6 * pr.h1 + (k - 36)] = bp[6 * pr.c1 + (k - 36)] - sum;
+    }
+}
+
+__global__ __launch_bounds__(SC_THREADS) void schur_chunks(const SchurChunk* __restrict__ chunks,
+                                                           const SchurPair* __restrict__ pairs,
+                                                           const int2* __restrict__ entries,
+                                                           const double* __restrict__ G,
+                                                           const double* __restrict__ Q,
+                                                           const double* __restrict__ camk,
+                                                           const double* __restrict__ bl,
+                                                           const double* __restrict__ Hpp,
+                                                           const double* __restrict__ bp, double lambda, int np, int ecsr,
+                                                           const int* __restrict__ ptlist,
+                                                           const double* __restrict__ tout,
+                                                           double* __restrict__ part,
+                                                           double* __restrict__ S, double* __restrict__ rhs)
+{
+    __shared__ double red[SC_THREADS / kWave][42];
+    const SchurChunk ch = chunks[blockIdx.x];
+    if (ch.pair < 0) return;
+    const int t = threadIdx.x;
+    const long long es = ecsr;
     double acc[42];
 #pragma unroll
     for (int k = 0; k < 42; k++) acc[k] = 0;
-    const int b1 = pb.cstart[c2 + 1];
-    const int* __restrict__ idx2 = blkidx + (long long)h2 * pb.P;
-    auto add = [&](const double* z, int e2) {
-        const double* W2 = Hpl + 18 * (long long)e2;
-        double w2[18];
+    // both entries' indices first (padding -> the zero record), then every operand load
+    // (a chunk of count 0 reads the list's padding entry; invalid lanes repeat the last entry)
+    const int2 x0 = entries[ch.start + max(0, min(t, ch.count - 1))];
+    const int2 x1 = entries[ch.start + max(0, min(t + SC_THREADS, ch.count - 1))];
+    const bool v0 = t < ch.count, v1 = t + SC_THREADS < ch.count;
+    const SchurPair pr = pairs[ch.pair];
+    const double f1 = camk[3 * pr.c1], f2 = camk[3 * pr.c2];
+    // records at camera-CSR positions, component arrays of stride es: consecutive entries of a
+    // pair are (mostly) consecutive positions, so every load below is coalesced
+    double q0[3], g0[6], q1[3], g1[6];
 #pragma unroll
-        for (int k = 0; k < 18; k++) w2[k] = W2[k];
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-            for (int k = 0; k < 6; k++)
-                acc[r * 6 + k] += z[r * 3] * w2[k * 3] + z[r * 3 + 1] * w2[k * 3 + 1] + z[r * 3 + 2] * w2[k * 3 + 2];
-    };
-    for (int a = pb.cstart[c1] + threadIdx.x; a < pb.cstart[c1 + 1]; a += BA_THREADS) {
-        const int e1 = pb.cedges[a];
-        const int p = pb.cpt[a];
-        const int x = idx2[p];  // edge of c2 on p, or -2 - list position (several), -1 none
-        if (x == -1 || !pb.active[e1] || !pb.ptfree[p]) continue;
-        const double* Z1 = Z + 18 * (long long)e1;
-        double z[18];  // Hpl_e1 Dinv_p (6x3)
-#pragma unroll
-        for (int k = 0; k < 18; k++) z[k] = Z1[k];
-        if (diag) {
-            const double g0 = bl[3 * p], g1 = bl[3 * p + 1], g2 = bl[3 * p + 2];
-#pragma unroll
-            for (int r = 0; r < 6; r++) acc[36 + r] += z[r * 3] * g0 + z[r * 3 + 1] * g1 + z[r * 3 + 2] * g2;
-        }
-        if (x >= 0) {
-            if (pb.active[x]) add(z, x);
-        } else {
-            for (int q = -2 - x; q < b1 && pb.cpt[q] == p; q++) {
-                const int e2 = pb.cedges[q];
-                if (pb.active[e2]) add(z, e2);
-            }
-        }
+    for (int k = 0; k < 3; k++) {
+        q0[k] = Q[k * es + x0.x];
+        q1[k] = Q[k * es + x1.x];
     }
-    block_sum<42>(acc, red);
-    for (int i = threadIdx.x; i < 36; i += BA_THREADS) {
-        const int r = i / 6, k = i % 6;
-        double v = -red[0][i];
-        if (diag) v += Hpp[36 * (long long)c1 + i] + (r == k ? lambda : 0.0);
-        // tether H12 blocks of this camera pair (code = 2 t + transposed)
-        for (int j = ptstart[pi]; j < ptstart[pi + 1]; j++) {
-            const int code = ptlist[j];
-            const double* H12 = tout + (long long)(code >> 1) * TETHER_OUT + 72;
-            v += (code & 1) ? H12[k * 6 + r] : H12[r * 6 + k];
-        }
-        S[(long long)(6 * h1 + r) * np + 6 * h2 + k] = v;
-        S[(long long)(6 * h2 + k) * np + 6 * h1 + r] = v;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        g0[k] = G[k * es + x0.x];
+        g1[k] = G[k * es + x1.x];
     }
-    if (diag && threadIdx.x < 6) rhs[6 * h1 + threadIdx.x] = bp[6 * c1 + threadIdx.x] - red[0][36 + threadIdx.x];
+    if (ch.kind == 0) {
+        // Z_e1 Hpl_e2^T = Jp1^T (G1 W2^T) Jp2
+        double r0[3], w0[6], r1[3], w1[6];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            r0[k] = Q[k * es + x0.y];
+            r1[k] = Q[k * es + x1.y];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            w0[k] = Q[(3 + k) * es + x0.y];
+            w1[k] = Q[(3 + k) * es + x1.y];
+        }
+        auto product = [&](const double (&q)[3], const double (&g)[6], const double (&rq)[3], const double (&w)[6],
+                           bool valid) {
+            double J1[12], J2[12];
+            jac_pose_q(q[0], q[1], q[2], f1, J1);
+            jac_pose_q(rq[0], rq[1], rq[2], f2, J2);
+            double M[4];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) M[i * 2 + j] = g[i * 3] * w[j * 3] + g[i * 3 + 1] * w[j * 3 + 1] + g[i * 3 + 2] * w[j * 3 + 2];
+            if (!valid) M[0] = M[1] = M[2] = M[3] = 0;
+            double T[12];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int c = 0; c < 6; c++) T[i * 6 + c] = M[i * 2] * J2[c] + M[i * 2 + 1] * J2[6 + c];
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int c = 0; c < 6; c++) acc[r * 6 + c] = fma(J1[r], T[c], fma(J1[6 + r], T[6 + c], acc[r * 6 + c]));
+        };
+        product(q0, g0, r0, w0, v0);
+        product(q1, g1, r1, w1, v1);
+    } else {
+        // Z_e bl_p = Jp^T (G bl_p)
+        double b0[3], b1[3];
+#pragma unroll
+        for (int m = 0; m < 3; m++) {
+            b0[m] = bl[3 * x0.y + m];
+            b1[m] = bl[3 * x1.y + m];
+        }
+        auto term = [&](const double (&q)[3], const double (&g)[6], const double (&b)[3], bool valid) {
+            double J[12];
+            jac_pose_q(q[0], q[1], q[2], f1, J);
+            double u0 = g[0] * b[0] + g[1] * b[1] + g[2] * b[2], u1 = g[3] * b[0] + g[4] * b[1] + g[5] * b[2];
+            if (!valid) u0 = u1 = 0;
+#pragma unroll
+            for (int r = 0; r < 6; r++) acc[36 + r] = fma(J[r], u0, fma(J[6 + r], u1, acc[36 + r]));
+        };
+        term(q0, g0, b0, v0);
+        term(q1, g1, b1, v1);
+    }
+    block_sum<42, SC_THREADS>(acc, red);  // red[0][k] = chunk total of entry k
+    if (pr.nslots > 1) {  // schur_finish adds the partials (a kernel boundary, no L2 write-back fence)
+        if (t < 42) part[(long long)ch.slot * 42 + t] = red[0][t];
+        return;
+    }
+    if (t < 42) schur_write(pr, t, red[0][t], Hpp, bp, lambda, np, ptlist, tout, S, rhs);
+}
+
+// Pairs of more than one chunk: a 64-lane wave per pair adds its chunk partials in chunk order.
+__global__ __launch_bounds__(64) void schur_finish(const int* __restrict__ multi, const SchurPair* __restrict__ pairs,
+                                                   const double* __restrict__ part,
+                                                   const double* __restrict__ Hpp, const double* __restrict__ bp,
+                                                   double lambda, int np, const int* __restrict__ ptlist,
+                                                   const double* __restrict__ tout, double* __restrict__ S,
+                                                   double* __restrict__ rhs)
+{
+    const SchurPair pr = pairs[multi[blockIdx.x]];
+    const int t = threadIdx.x;
+    if (t >= 42) return;
+    double v = 0;
+    for (int q = 0; q < pr.nslots; q++) v += part[(long long)(pr.slot0 + q) * 42 + t];
+    schur_write(pr, t, v, Hpp, bp, lambda, np, ptlist, tout, S, rhs);
 }
 
 // Dense SPD solve S x = b in one workgroup, S of padded order np (multiple of 16, rows n..np-1
@@ -997,7 +1189,8 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
 // Z_e = Hpl_e Dinv from edge_schur); a PG-lane group per point, one edge per lane.  Also the
 // point part of computeScale.
 __global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const double* __restrict__ Z,
-                                                            const double* __restrict__ db,
+                                                            const double* __restrict__ Q,
+                                                            const double* __restrict__ Hll,
                                                             const double* __restrict__ bl,
                                                             const double* __restrict__ xp, double lambda,
                                                             double* __restrict__ xl,
@@ -1016,18 +1209,36 @@ __global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const do
         if (!pb.active[e]) continue;
         const int h = pb.camh[pb.ecam[e]];
         if (h < 0) continue;
-        const double* Ze = Z + 18 * (long long)e;
+        // Z_e^T xp = G^T (Jp xp)
+        const int a2 = pb.epos[e];
+        const long long es = pb.ecsr;
+        double J[12];
+        jac_pose_q(Q[a2], Q[es + a2], Q[2 * es + a2], pb.camk[3 * pb.ecam[e]], J);
         const double* X = xp + 6 * h;
+        double u0 = 0, u1 = 0;
 #pragma unroll
-        for (int k = 0; k < 3; k++)
+        for (int r = 0; r < 6; r++) {
+            u0 += J[r] * X[r];
+            u1 += J[6 + r] * X[r];
+        }
 #pragma unroll
-            for (int r = 0; r < 6; r++) cl[k] += Ze[r * 3 + k] * X[r];
+        for (int k = 0; k < 3; k++) cl[k] += Z[k * es + a2] * u0 + Z[(3 + k) * es + a2] * u1;
     }
     group_sum(cl);
     if (sub != 0) return;
+    // db_p = Dinv_p bl_p, Dinv_p = (Hll_p + lambda I)^-1 as in edge_schur
+    double D[9], Di[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
+    D[0] += lambda;
+    D[4] += lambda;
+    D[8] += lambda;
+    d_inv3(D, Di);
+    const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
     double sc = 0;
     for (int r = 0; r < 3; r++) {
-        const double v = db[3 * p + r] - cl[r];
+        const double dbr = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
+        const double v = dbr - cl[r];
         xl[3 * p + r] = v;
         sc += v * (lambda * v + bl[3 * p + r]);
     }
@@ -1071,15 +1282,8 @@ __global__ __launch_bounds__(BA_THREADS) void update_state(Problem pb, State A, 
 // the host sorts the short list into g2o's active-edge order and drop_edges removes them).
 // Read-only on the graph, so it runs speculatively with the last trial for NS candidate states
 // at once (ns = 2: the trial state if accepted, the current state if rejected); list k lives at
-// out_list + k E.  Block partials are reduced in fixed order by the last block to finish, which
-// writes ctl->osum[k] = (sum of inlier |e|^2, inlier count) and resets the ticket.
-struct OutlierCtl {
-    double osum[2][2];
-    int fail;
-    uint32_t count[2];
-    uint32_t ticket;
-};
-
+// out_list + k E.  Block partials (sum of inlier |e|^2, inlier count) go to `part`; reduce3 adds
+// them in fixed order into ctl->osum[k].
 __global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s0, State s1, int ns, int E,
                                                            const unsigned char* __restrict__ active,
                                                            const double* __restrict__ err,
@@ -1089,7 +1293,6 @@ __global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s0,
                                                            OutlierCtl* __restrict__ ctl)
 {
     __shared__ double ssum[2][BA_THREADS / kWave], scnt[2][BA_THREADS / kWave];
-    __shared__ int s_last;
     const int e = blockIdx.x * BA_THREADS + threadIdx.x;
     double vs[2] = {0, 0}, vc[2] = {0, 0};
     if (e < E && active[e]) {
@@ -1139,32 +1342,9 @@ __global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s0,
             part[(2 * k) * gridDim.x + blockIdx.x] = a;
             part[(2 * k + 1) * gridDim.x + blockIdx.x] = b;
         }
-        __threadfence();
-        s_last = atomicAdd(&ctl->ticket, 1u) == gridDim.x - 1;
     }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    for (int k = 0; k < ns; k++) {
-        for (int h = 0; h < 2; h++) {
-            double v = 0;
-            for (int i = threadIdx.x; i < (int)gridDim.x; i += BA_THREADS) v += part[(2 * k + h) * gridDim.x + i];
-            for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
-            if (lane == 0) ssum[h][w] = v;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double a = 0, b = 0;
-            for (int i = 0; i < BA_THREADS / kWave; i++) {
-                a += ssum[0][i];
-                b += ssum[1][i];
-            }
-            ctl->osum[k][0] = a;
-            ctl->osum[k][1] = b;
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) ctl->ticket = 0;
+    // the block partials are added by reduce3 (the next launch): a last-block ticket here would
+    // need an agent-scope fence per workgroup, i.e. a full L2 write-back on gfx950
 }
 
 __global__ __launch_bounds__(BA_THREADS) void drop_edges(unsigned char* __restrict__ active,
@@ -1215,13 +1395,14 @@ struct BundleAdjuster {
     int iteration = 0;
     double user_lambda = 0, lambda = 0, ni = 2, huber = 0;
     int n = 0, np = 0;  // 6 * cameras in the system, padded to a multiple of 16
-    int npairs = 0;
+    int npairs = 0, n_slots = 0, n_sblocks = 0, n_smulti = 0;  // Schur pairs, partial slots, blocks, multi-chunk pairs
     std::vector<int> camh, ptfree, cam_of_block;
     hipStream_t st = nullptr;
     // Control block read back at every host decision (one pinned copy per synchronisation):
     // doubles [0,3) linearisation chi2 / max diag, [3,6) trial, then the outlier pass's
     // OutlierCtl (sums, Cholesky failure flag, counts, ticket).
-    static constexpr int CTL_DOUBLES = 16, CTL_OUTLIER = 6;
+    static constexpr int CTL_DOUBLES = 16, CTL_OUTLIER = 6, CTL_SCRATCH = 12;
+    static_assert(CTL_OUTLIER * 8 + sizeof(OutlierCtl) <= CTL_SCRATCH * 8, "control block layout");
     double* h_ctl = nullptr;
     OutlierCtl* d_octl() const { return reinterpret_cast<OutlierCtl*>(d_red.as<double>() + CTL_OUTLIER); }
     const OutlierCtl& h_octl() const { return *reinterpret_cast<const OutlierCtl*>(h_ctl + CTL_OUTLIER); }
@@ -1243,8 +1424,9 @@ struct BundleAdjuster {
     // device buffers
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
-        d_bp, d_db, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
-        d_pairs, d_olist, d_camcnt, d_blkidx, d_Z, d_campart, d_teth, d_tout, d_ptstart, d_ptlist;
+        d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
+        d_olist, d_camcnt, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
+        d_smulti, d_epos;
     int n_entries = 0;  // point-CSR entries (active edges at initialisation)
     int nb_free = 0;    // cameras in the reduced system
     mage_ba_stats stats{};
@@ -1269,6 +1451,8 @@ struct BundleAdjuster {
         pb.cstart = d_cstart.as<int>();
         pb.cedges = d_cedges.as<int>();
         pb.cpt = d_cpt.as<int>();
+        pb.epos = d_epos.as<int>();
+        pb.ecsr = n_entries;
         pb.huber = huber;
         return pb;
     }
@@ -1278,10 +1462,10 @@ struct BundleAdjuster {
     {
         for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
-                        &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_db, &d_S, &d_rhs,
-                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk, &d_pairs,
-                        &d_olist, &d_camcnt, &d_blkidx, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptstart,
-                        &d_ptlist})
+                        &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
+                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk, &d_olist,
+                        &d_camcnt, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
+                        &d_schunks, &d_spart, &d_smulti, &d_epos})
             b->release();
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
@@ -1378,21 +1562,30 @@ struct BundleAdjuster {
                     cpt[cf[ecam[e]]++] = i;
                 }
         }
+        // camera-CSR position of every listed edge: Hpl and Z are stored camera-major (component
+        // arrays indexed by this position), so a pair's Schur products read them coalesced
+        std::vector<int> epos(std::max(E, 1), -1);
+        for (int a = 0; a < cstart[C]; a++) epos[cedges[a]] = a;
         // covisible camera pairs (h1 <= h2) of the reduced system
         std::vector<int2> pairs;
+        std::vector<int> pairidx((size_t)std::max(nb, 1) * std::max(nb, 1), -1);
+        std::vector<std::pair<int, int>> hs;  // (block, edge) of a point's edges in the system
+        auto point_edges = [&](int i) {
+            hs.clear();
+            for (int a = pstart[i]; a < pstart[i + 1]; a++) {
+                const int e = pedges[a];
+                const int h = camh[ecam[e]];
+                if (h >= 0) hs.emplace_back(h, e);
+            }
+            std::stable_sort(hs.begin(), hs.end(), [](const std::pair<int, int>& u, const std::pair<int, int>& v) { return u.first < v.first; });
+        };
         if (nb > 0) {
             std::vector<unsigned char> mark((size_t)nb * nb, 0);
-            std::vector<int> hs;
             for (int i = 0; i < P; i++) {
                 if (!ptfree[i]) continue;
-                hs.clear();
-                for (int a = pstart[i]; a < pstart[i + 1]; a++) {
-                    const int h = camh[ecam[pedges[a]]];
-                    if (h >= 0) hs.push_back(h);
-                }
-                for (int x : hs)
-                    for (int y : hs)
-                        if (x <= y) mark[(size_t)x * nb + y] = 1;
+                point_edges(i);
+                for (size_t x = 0; x < hs.size(); x++)
+                    for (size_t y = x; y < hs.size(); y++) mark[(size_t)hs[x].first * nb + hs[y].first] = 1;
             }
             for (int h = 0; h < nb; h++) mark[(size_t)h * nb + h] = 1;
             for (auto& T : teth) {
@@ -1403,7 +1596,10 @@ struct BundleAdjuster {
             }
             for (int x = 0; x < nb; x++)
                 for (int y = x; y < nb; y++)
-                    if (mark[(size_t)x * nb + y]) pairs.push_back(make_int2(x, y));
+                    if (mark[(size_t)x * nb + y]) {
+                        pairidx[(size_t)x * nb + y] = (int)pairs.size();
+                        pairs.push_back(make_int2(x, y));
+                    }
         }
         npairs = (int)pairs.size();
         // per pair: the tethers whose H12 lands in its block (code 2 t + transposed), set order
@@ -1417,18 +1613,117 @@ struct BundleAdjuster {
             }
             ptstart[pi + 1] = (int)ptlist.size();
         }
-        // block x point index for the Schur pairs: the edge of the camera of block h on point i,
-        // -2 - (first list position) when that camera observes i more than once, -1 if never
-        std::vector<int> blkidx(std::max((size_t)nb * P, (size_t)1), -1);
-        for (int h = 0; h < nb; h++) {
-            const int c = cam_of_block[h];
-            for (int a = cstart[c]; a < cstart[c + 1]; a++) {
-                int& x = blkidx[(size_t)h * P + cpt[a]];
-                x = x == -1 ? cedges[a] : -2 - (x >= 0 ? a - 1 : -2 - x);
+        // Schur product lists (schur_chunks): per pair the (e1, e2) products of its shared free
+        // points in point order, then for a diagonal pair the rhs entries (e, p) in the camera's
+        // point order; two passes (count, fill)
+        std::vector<int> pcount(npairs, 0), rcount(npairs, 0);
+        for (int i = 0; i < P; i++) {
+            if (!ptfree[i]) continue;
+            point_edges(i);
+            for (size_t x = 0; x < hs.size(); x++) {
+                rcount[pairidx[(size_t)hs[x].first * nb + hs[x].first]]++;
+                for (size_t y = 0; y < hs.size(); y++)
+                    if (hs[x].first <= hs[y].first) pcount[pairidx[(size_t)hs[x].first * nb + hs[y].first]]++;
             }
         }
+        std::vector<long long> pbeg(npairs + 1, 0);
+        for (int pi = 0; pi < npairs; pi++) pbeg[pi + 1] = pbeg[pi] + pcount[pi] + rcount[pi];
+        std::vector<int2> sentries((size_t)pbeg[npairs] + 1, make_int2(0, 0));  // + one padding entry
+        {
+            std::vector<long long> pf(npairs), rf(npairs);
+            for (int pi = 0; pi < npairs; pi++) {
+                pf[pi] = pbeg[pi];
+                rf[pi] = pbeg[pi] + pcount[pi];
+            }
+            for (int i = 0; i < P; i++) {
+                if (!ptfree[i]) continue;
+                point_edges(i);
+                for (size_t x = 0; x < hs.size(); x++)
+                    for (size_t y = 0; y < hs.size(); y++)
+                        if (hs[x].first <= hs[y].first)
+                            sentries[(size_t)pf[pairidx[(size_t)hs[x].first * nb + hs[y].first]]++] =
+                                make_int2(epos[hs[x].second], epos[hs[y].second]);
+            }
+            for (int h = 0; h < nb; h++) {  // rhs: the camera's edges in point order
+                const int c = cam_of_block[h], pi = pairidx[(size_t)h * nb + h];
+                for (int a = cstart[c]; a < cstart[c + 1]; a++)
+                    if (ptfree[cpt[a]]) sentries[(size_t)rf[pi]++] = make_int2(a, cpt[a]);
+            }
+        }
+        // chunks; the block rows of S split into 8 contiguous groups of about equal work, one per
+        // XCD (block b runs on XCD b % 8)
+        std::vector<SchurPair> spairs(npairs);
+        std::vector<std::vector<SchurChunk>> xcd_chunks(8);
+        {
+            std::vector<long long> roww(std::max(nb, 1), 0);
+            for (int pi = 0; pi < npairs; pi++) roww[pairs[pi].x] += pbeg[pi + 1] - pbeg[pi] + SC_CHUNK / 4;
+            long long tot = 0;
+            for (long long w : roww) tot += w;
+            int slot = 0, x = 0;
+            long long acc_w = 0;
+            int row = -1;
+            for (int pi = 0; pi < npairs; pi++) {
+                const int h1 = pairs[pi].x;
+                if (h1 != row) {  // next row: move to the next XCD once this one has its share
+                    while (x < 7 && acc_w >= (tot * (x + 1) + 7) / 8) x++;
+                    row = h1;
+                    acc_w += roww[h1];
+                }
+                const int np_ = (pcount[pi] + SC_CHUNK - 1) / SC_CHUNK, nr = (rcount[pi] + SC_CHUNK - 1) / SC_CHUNK;
+                const int nch = std::max(np_ + nr, 1);
+                SchurPair& sp = spairs[pi];
+                sp.h1 = pairs[pi].x;
+                sp.h2 = pairs[pi].y;
+                sp.c1 = cam_of_block[sp.h1];
+                sp.slot0 = slot;
+                sp.nslots = nch;
+                sp.tbeg = ptstart[pi];
+                sp.tend = ptstart[pi + 1];
+                sp.c2 = cam_of_block[sp.h2];
+                for (int k = 0; k < nch; k++) {
+                    SchurChunk ch{};
+                    ch.pair = pi;
+                    ch.slot = slot + k;
+                    if (k < np_) {
+                        ch.kind = 0;
+                        ch.start = (int)(pbeg[pi] + (long long)k * SC_CHUNK);
+                        ch.count = std::min(SC_CHUNK, pcount[pi] - k * SC_CHUNK);
+                    } else if (k - np_ < nr) {
+                        ch.kind = 1;
+                        ch.start = (int)(pbeg[pi] + pcount[pi] + (long long)(k - np_) * SC_CHUNK);
+                        ch.count = std::min(SC_CHUNK, rcount[pi] - (k - np_) * SC_CHUNK);
+                    } else {  // nothing to sum (tether-only or empty block): Hpp / tethers only
+                        ch.kind = 0;
+                        ch.start = (int)pbeg[pi];
+                        ch.count = 0;
+                    }
+                    xcd_chunks[x].push_back(ch);
+                }
+                slot += nch;
+            }
+            n_slots = slot;
+        }
+        size_t L = 0;
+        for (auto& v : xcd_chunks) L = std::max(L, v.size());
+        std::vector<SchurChunk> schunks(8 * L);
+        for (size_t j = 0; j < L; j++)
+            for (int x = 0; x < 8; x++) {
+                SchurChunk ch{};
+                ch.pair = -1;
+                schunks[8 * j + x] = j < xcd_chunks[x].size() ? xcd_chunks[x][j] : ch;
+            }
+        n_sblocks = (int)schunks.size();
+        std::vector<int> smulti;  // pairs finished by schur_finish
+        for (int pi = 0; pi < npairs; pi++)
+            if (spairs[pi].nslots > 1) smulti.push_back(pi);
+        n_smulti = (int)smulti.size();
+        MAGE_REQUIRE(pbeg[npairs] < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
         n_entries = pstart[P];
-        if ((r = upload(d_blkidx, blkidx)) != MAGE_OK) return r;
+        if ((r = upload(d_sentries, sentries)) != MAGE_OK) return r;
+        if ((r = upload(d_epos, epos)) != MAGE_OK) return r;
+        if ((r = upload(d_smulti, smulti)) != MAGE_OK) return r;
+        if ((r = upload(d_spairs, spairs)) != MAGE_OK) return r;
+        if ((r = upload(d_schunks, schunks)) != MAGE_OK) return r;
         if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
         if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
         if ((r = upload(d_active, active)) != MAGE_OK) return r;
@@ -1438,8 +1733,6 @@ struct BundleAdjuster {
         if ((r = upload(d_cedges, cedges)) != MAGE_OK) return r;
         if ((r = upload(d_cpt, cpt)) != MAGE_OK) return r;
         if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
-        if ((r = upload(d_pairs, pairs)) != MAGE_OK) return r;
-        if ((r = upload(d_ptstart, ptstart)) != MAGE_OK) return r;
         if ((r = upload(d_ptlist, ptlist)) != MAGE_OK) return r;
         for (auto& T : teth) {
             T.h1 = camh[T.c1];
@@ -1459,17 +1752,17 @@ struct BundleAdjuster {
         const size_t Pm = std::max(P, 1), Cm = std::max(C, 1), Em = std::max(E, 1);
         const size_t npm = std::max(np, 16);
         for (auto pr : {std::make_pair(&d_err, Em * 2 * 8), std::make_pair(&d_Hll, Pm * 9 * 8),
-                        std::make_pair(&d_bl, Pm * 3 * 8), std::make_pair(&d_Hpl, Em * 18 * 8),
+                        std::make_pair(&d_bl, Pm * 3 * 8), std::make_pair(&d_Hpl, (size_t)std::max(n_entries, 1) * EQ_N * 8),
                         std::make_pair(&d_Hpp, Cm * 36 * 8), std::make_pair(&d_bp, Cm * 6 * 8),
-                        std::make_pair(&d_db, Pm * 3 * 8),
-                        std::make_pair(&d_Z, Em * 18 * 8),
+                        std::make_pair(&d_Z, (size_t)std::max(n_entries, 1) * EG_N * 8),
                         std::make_pair(&d_campart, Cm * CAM_CHUNKS * 27 * 8),
                         std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
                         std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, (Pm + teth.size()) * 8),
                         std::make_pair(&d_tout, std::max<size_t>(teth.size(), 1) * TETHER_OUT * 8),
                         std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
                         std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 4 * 8),
-                        std::make_pair(&d_olist, Em * 2 * 4 + 16), std::make_pair(&d_camcnt, Cm * 4)})
+                        std::make_pair(&d_olist, Em * 2 * 4 + 16), std::make_pair(&d_camcnt, Cm * 4),
+                        std::make_pair(&d_spart, (size_t)std::max(n_slots, 1) * 42 * 8)})
             if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
         MAGE_HIP(hipMemsetAsync(d_maxd.ptr, 0, (Pm + Cm) * 8, st));
         MAGE_HIP(hipMemsetAsync(d_scale.ptr, 0, (Pm + Cm) * 8, st));
@@ -1523,17 +1816,22 @@ struct BundleAdjuster {
         if ((r0 = reset_ctl_words()) != MAGE_OK) return r0;
         if (n_entries > 0 && !points_fixed) {
             launch("ba.edge_schur", edge_schur, dim3((n_entries + BA_THREADS - 1) / BA_THREADS), dim3(BA_THREADS), 0, st,
-                   pb, n_entries, (const double*)d_Hll.as<double>(), (const double*)d_bl.as<double>(),
-                   (const double*)d_Hpl.as<double>(), lam, d_db.as<double>(), d_Z.as<double>());
+                   pb, (const double*)d_Hll.as<double>(), (const double*)d_Hpl.as<double>(), lam, d_Z.as<double>());
         }
         if (n > 0) {
             if (np > 16 * CT_MAXT) MAGE_HIP(hipMemsetAsync(d_S.ptr, 0, (size_t)np * np * 8, st));
             {
-                launch("ba.schur_pairs", schur_pairs, dim3(8 * ((npairs + 7) / 8)), dim3(BA_THREADS), 0, st, pb, d_pairs.as<int2>(),
-                                   d_camblk.as<int>(), d_blkidx.as<int>(), d_Hpp.as<double>(), d_bp.as<double>(), d_Hpl.as<double>(),
-                                   d_Z.as<double>(), d_bl.as<double>(), lam, np, npairs,
-                                   (const int*)d_ptstart.as<int>(), (const int*)d_ptlist.as<int>(),
-                                   (const double*)d_tout.as<double>(), d_S.as<double>(), d_rhs.as<double>());
+                launch("ba.schur_pairs", schur_chunks, dim3(n_sblocks), dim3(SC_THREADS), 0, st,
+                       (const SchurChunk*)d_schunks.as<SchurChunk>(), (const SchurPair*)d_spairs.as<SchurPair>(),
+                       (const int2*)d_sentries.as<int2>(), (const double*)d_Z.as<double>(), (const double*)d_Hpl.as<double>(),
+                       (const double*)d_camk.as<double>(), (const double*)d_bl.as<double>(), (const double*)d_Hpp.as<double>(), (const double*)d_bp.as<double>(),
+                       lam, np, n_entries, (const int*)d_ptlist.as<int>(), (const double*)d_tout.as<double>(), d_spart.as<double>(),
+                       d_S.as<double>(), d_rhs.as<double>());
+                if (n_smulti > 0)
+                    launch("ba.schur_finish", schur_finish, dim3(n_smulti), dim3(64), 0, st, (const int*)d_smulti.as<int>(),
+                           (const SchurPair*)d_spairs.as<SchurPair>(), (const double*)d_spart.as<double>(),
+                           (const double*)d_Hpp.as<double>(), (const double*)d_bp.as<double>(), lam, np,
+                           (const int*)d_ptlist.as<int>(), (const double*)d_tout.as<double>(), d_S.as<double>(), d_rhs.as<double>());
             }
             {
                 if (np <= 16 * CT_MAXT)
@@ -1546,7 +1844,8 @@ struct BundleAdjuster {
         }
         if (P > 0) {
             launch("ba.point_backsub", point_backsub, dim3(group_grid(P)), dim3(BA_THREADS), 0, st, pb,
-                   (const double*)d_Z.as<double>(), (const double*)d_db.as<double>(), (const double*)d_bl.as<double>(),
+                   (const double*)d_Z.as<double>(), (const double*)d_Hpl.as<double>(), (const double*)d_Hll.as<double>(),
+                   (const double*)d_bl.as<double>(),
                    (const double*)xp, lam, xl, d_scale.as<double>());
         }
         if (std::max(P, C) > 0) {
@@ -1562,9 +1861,11 @@ struct BundleAdjuster {
         if (nt > 0)
             launch("ba.tether_eval", tether_eval, dim3((nt + 63) / 64), dim3(64), 0, st, (const Tether*)d_teth.as<Tether>(),
                    nt, state(1 - cur), 0, d_chi.as<double>() + P, d_tout.as<double>());
-        launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, d_chi.as<double>(), P + nt, d_scale.as<double>(),
-               P + C, d_maxd.as<double>(), 0, d_red.as<double>() + 3);
-        if (speculate && E > 0) launch_outlier_pass(state(1 - cur), state(cur), 2);  // read back with this sync
+        const bool spec = speculate && E > 0;
+        if (spec) launch_outlier_pass(state(1 - cur), state(cur), 2);  // read back with this sync
+        launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)d_chi.as<double>(), P + nt,
+               (const double*)d_scale.as<double>(), P + C, (const double*)d_maxd.as<double>(), 0, d_red.as<double>() + 3,
+               (const double*)d_osum.as<double>(), outlier_blocks(), spec ? 2 : 0, d_octl());
         MAGE_HIP(hipGetLastError());
         mage_status r = read_ctl();
         if (r != MAGE_OK) return r;
@@ -1649,9 +1950,10 @@ struct BundleAdjuster {
     double outlier_max_err_sq = 0;
     // outlier lists, counts and inlier (sum, count) of ns states into the control block (counts
     // and ticket zeroed by reset_ctl_words beforehand)
+    int outlier_blocks() const { return (E + BA_THREADS - 1) / BA_THREADS; }
     void launch_outlier_pass(State s0, State s1, int ns)
     {
-        const int ge = (E + BA_THREADS - 1) / BA_THREADS;
+        const int ge = outlier_blocks();
         launch("ba.outlier_pass", outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), s0, s1, ns, E,
                            d_active.as<unsigned char>(), d_err.as<double>(), outlier_max_err_sq,
                            d_olist.as<uint32_t>(), d_osum.as<double>(), d_octl());
@@ -1690,6 +1992,10 @@ struct BundleAdjuster {
         if (k < 0) {
             if ((r = reset_ctl_words()) != MAGE_OK) return r;
             launch_outlier_pass(state(cur), state(cur), 1);
+            // its block partials -> ctl->osum[0] (the chi2 outputs go to a scratch slot)
+            launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)nullptr, 0, (const double*)nullptr, 0,
+                   (const double*)nullptr, 0, d_red.as<double>() + CTL_SCRATCH, (const double*)d_osum.as<double>(),
+                   outlier_blocks(), 1, d_octl());
             MAGE_HIP(hipGetLastError());
             if ((r = read_ctl()) != MAGE_OK) return r;
             k = 0;

@@ -287,6 +287,8 @@ struct Problem {
     const int* cstart;            // C+1
     const int* cedges;            // edges by camera, sorted by point id, filtered by `active`
     const int* cpt;               // point id of each cedges entry (binary search key)
+    const int* epos;              // E: position of the edge in the camera CSR (-1: not listed)
+    int ecsr;                     // camera-CSR entries = row stride of the Hpl / Z component arrays
     double huber;
 };
 
@@ -330,6 +332,23 @@ __device__ __forceinline__ void jac_pose(const double xc[3], double f, double Jp
     Jp[11] = yi * fi;
 }
 
+// The same pose Jacobian from (x/z, y/z, f/z) and f (jac_pose's expressions): the Schur sweeps
+// keep these 3 numbers per edge instead of the 6x3 Hpl.
+__device__ __forceinline__ void jac_pose_q(double xi, double yi, double fi, double f, double Jp[12])
+{
+    Jp[0] = xi * yi * f;
+    Jp[1] = -(1 + xi * xi) * f;
+    Jp[2] = yi * f;
+    Jp[3] = -fi;
+    Jp[4] = 0;
+    Jp[5] = xi * fi;
+    Jp[6] = (1 + yi * yi) * f;
+    Jp[7] = -xi * yi * f;
+    Jp[8] = -xi * f;
+    Jp[9] = 0;
+    Jp[10] = -fi;
+    Jp[11] = yi * fi;
+}
 
 }  // namespace ba
 }  // namespace mage

@@ -1,11 +1,13 @@
-"""Timing ablation of the BA dense solve (development tool, not part of the product).
+"""Timing ablation of the BA kernels (development tool, not part of the product).
 
-  python tools/ablate_ba.py build   # variants of ba.hip (MAGE_CHOL_ABLATE) into abl/ba<N>/ (CPU)
-  python tools/ablate_ba.py run     # per-kernel times of the C3 graph for each variant (GPU)
+  python tools/ablate_ba.py build [V1 V2 ...]   # variants of ba.hip into abl/ba_<i>/ (CPU)
+  python tools/ablate_ba.py run   [V1 V2 ...]   # per-kernel times of the C3 graph per variant (GPU)
 
-MAGE_CHOL_ABLATE: 0 full, 2 trivial diagonal-block factorisation (time of the serial block factor),
-3 = 0 + per-phase s_memtime cycle counts of wave 0 printed by the kernel.
-The variant library is loaded by this script alone; the product loader is untouched.
+A variant is a '+'-joined list of NAME=VALUE preprocessor definitions ("0" = the product build),
+e.g. MAGE_CHOL_ABLATE=3.  Switches in ba.hip:
+MAGE_CHOL_ABLATE (0 full, 2 trivial diagonal-block factorisation, 3 per-phase s_memtime cycles of
+wave 0 printed by the kernel),.  The variant library is loaded by this script alone; the product
+loader is untouched.
 """
 import ctypes as C
 import subprocess
@@ -13,7 +15,11 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-VARIANTS = [0, 2, 3]
+VARIANTS = sys.argv[2:] or ["0", "MAGE_CHOL_ABLATE=2", "MAGE_CHOL_ABLATE=3"]
+
+
+def defines(v):
+    return [] if v == "0" else ["-D" + d for d in v.split("+")]
 
 
 def build():
@@ -21,14 +27,15 @@ def build():
     from mageslam_amd import build as B
     B.build()
     objs = [p for p in B.OBJ.glob("*.o") if not p.name.startswith("ba.")]
-    for v in VARIANTS:
-        out = ROOT / "abl" / f"ba{v}"
+    for i, v in enumerate(VARIANTS):
+        out = ROOT / "abl" / f"ba_{i}"
         out.mkdir(parents=True, exist_ok=True)
         subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON,
-                        f"-DMAGE_CHOL_ABLATE={v}", "-c", str(B.CSRC / "ba.hip"), "-o", str(out / "ba.o")], check=True)
+                        *defines(v), "-c", str(B.CSRC / "ba.hip"), "-o", str(out / "ba.o")], check=True)
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
                         str(out / "ba.o"), *map(str, objs)], check=True)
-        print("built", out)
+        (out / "variant.txt").write_text(v)
+        print("built", out, v)
 
 
 def run():
@@ -36,8 +43,10 @@ def run():
     sys.path.insert(0, str(ROOT))
     from mageslam_amd import _lib, bundler, synth
     g = synth.ba_graph()
-    for v in VARIANTS:
-        lib = C.CDLL(str(ROOT / "abl" / f"ba{v}" / "libmage_hot.so"))
+    for i, v in enumerate(VARIANTS):
+        d = ROOT / "abl" / f"ba_{i}"
+        assert (d / "variant.txt").read_text() == v, f"abl/ba_{i} was built for another variant"
+        lib = C.CDLL(str(d / "libmage_hot.so"))
         _lib._declare(lib)
         _lib._lib = lib  # this process only: route the mirror classes to the variant
         b = bundler.BundlerLib(device=0)
@@ -46,11 +55,13 @@ def run():
             b.step([1.8], 7.25)
         lib.mage_profile_reset()
         lib.mage_profile_enable(1)
-        for _ in range(1 if v == 3 else 20):
+        n = 1 if "MAGE_CHOL_ABLATE=3" in v else 20
+        for _ in range(n):
             b.step([1.8], 7.25)
         lib.mage_profile_enable(0)
         rep = _lib.profile_report()
-        print(f"variant {v}: " + ", ".join(f"{k} {ms / max(c, 1):.4f} ms" for k, (c, ms) in sorted(rep.items())), flush=True)
+        tot = sum(ms for c, ms in rep.values()) / n
+        print(f"variant {v}: total {tot:.4f} ms/it | " + ", ".join(f"{k[3:]} {ms / max(c, 1):.4f}" for k, (c, ms) in sorted(rep.items())), flush=True)
         del b
 
 

@@ -13,6 +13,7 @@ figures are kept; `hbm_bytes_per_launch` uses the raw FETCH (lower bound) + WRIT
 from __future__ import annotations
 
 import csv
+import gzip
 import json
 import re
 import sys
@@ -45,9 +46,19 @@ KERNEL_TAG = {
 }
 
 
+def _open(path: Path):
+    """The CSV or its gzip (tools/profile_round.sh compresses the counter files on the box)."""
+    gz = path.with_name(path.name + ".gz")
+    return gzip.open(gz, "rt") if gz.exists() else open(path)
+
+
+def _exists(path: Path) -> bool:
+    return path.exists() or path.with_name(path.name + ".gz").exists()
+
+
 def read_stats(path: Path):
     rows = []
-    with open(path) as f:
+    with _open(path) as f:
         for r in csv.DictReader(f):
             rows.append({"kernel": short(r["Name"]), "calls": int(r["Calls"]),
                          "avg_us": float(r["AverageNs"]) / 1e3, "total_ms": float(r["TotalDurationNs"]) / 1e6,
@@ -57,9 +68,9 @@ def read_stats(path: Path):
 
 def read_pmc(path: Path, counter: str):
     acc = defaultdict(lambda: [0.0, 0])
-    if not path.exists():
+    if not _exists(path):
         return {}
-    with open(path) as f:
+    with _open(path) as f:
         for r in csv.DictReader(f):
             if r["Counter_Name"] != counter:
                 continue
