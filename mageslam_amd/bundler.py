@@ -185,7 +185,9 @@ class BundlerLib:
         self._upload()
         hw = np.ascontiguousarray(np.asarray(huberWidthPerIteration, np.float32).reshape(-1))
         cap = max(len(self._obs["cam"]) if self._obs is not None else 0, 1)
-        out = np.zeros(cap, np.uint32)
+        if getattr(self, "_outbuf", None) is None or len(self._outbuf) < cap:
+            self._outbuf = np.empty(cap, np.uint32)  # reused: the call writes only the first n entries
+        out = self._outbuf
         n = C.c_uint32(0)
         ms = C.c_float(0)
         check(_lib.load().mage_ba_step(self._h, ptr(hw), len(hw), float(maxErrorSquare), ptr(out), cap,

@@ -56,6 +56,23 @@ constexpr int PG = 32;
 // components of the per-edge Schur records (edge_schur): Q = (x/z, y/z, f/z, W), G
 constexpr int EQ_N = 9, EG_N = 6;
 
+// StepBundleAdjustment post-pass results in the pinned control block: per candidate state the
+// inlier (sum of |e|^2, count), the Cholesky failure flag and the outlier counts.
+// Device-side counters of one trial (appends and the Cholesky failure flag); reduce3 copies them
+// into the host-mapped OutlierCtl and zeroes them for the next trial (no memset per trial).
+struct LiveCtl {
+    int fail;
+    uint32_t count[2];
+    uint32_t pad;
+};
+struct OutlierCtl {
+    double osum[2][2];
+    int fail;
+    uint32_t count[2];
+    uint32_t ticket;
+};
+
+
 template <int N>
 __device__ __forceinline__ void group_sum(double (&v)[N])
 {
@@ -116,40 +133,113 @@ __host__ __device__ constexpr int rs_lane_of(int k)
     return lane;
 }
 
-// Per point: edge errors, robust chi2, Hll, bl, Hpl per edge (BlockSolver::buildSystem with
-// BaseBinaryEdge::constructQuadraticForm, robust first-order weighting).
-__global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State s, int linearize,
-                                                              double* __restrict__ err,
-                                                              double* __restrict__ Hll,
-                                                              double* __restrict__ bl,
-                                                              double* __restrict__ Hpl,
-                                                              double* __restrict__ chi_part,
-                                                              double* __restrict__ maxd_part)
+// Eigen Matrix3d::inverse (cofactors)
+__device__ __forceinline__ void d_inv3(const double m[9], double o[9])
 {
-    const int gid = blockIdx.x * BA_THREADS + threadIdx.x;
-    const int p = gid / PG, sub = gid % PG;
-    if (p >= pb.P) return;  // whole groups: P * PG threads
-    const int free_p = linearize && pb.ptfree[p];
+    const double c0 = m[4] * m[8] - m[5] * m[7];
+    const double c1 = m[5] * m[6] - m[3] * m[8];
+    const double c2 = m[3] * m[7] - m[4] * m[6];
+    const double det = m[0] * c0 + m[1] * c1 + m[2] * c2;
+    const double id = 1.0 / det;
+    o[0] = c0 * id;
+    o[1] = (m[2] * m[7] - m[1] * m[8]) * id;
+    o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    o[3] = c1 * id;
+    o[4] = (m[0] * m[8] - m[2] * m[6]) * id;
+    o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    o[6] = c2 * id;
+    o[7] = (m[1] * m[6] - m[0] * m[7]) * id;
+    o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+// Outputs of a point pass.
+struct PointOut {
+    double* err;        // E x 2: edge errors (g2o keeps _error of the last evaluation)
+    double* Hll;        // P x 9
+    double* bl;         // P x 3
+    double* Q;          // EQ_N x ecsr: x/z, y/z, f/z and W = w J_point (camera-major)
+    double* G;          // EG_N x ecsr: W Dinv_p (linearisation with a known lambda)
+    double* chi_part;   // P: robust chi2 of the point's edges
+    double* maxd_part;  // P: max |diag Hll| (computeLambdaInit)
+};
+
+// The StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) run speculatively inside the
+// evaluation of the last trial, for two candidate states at once: list 0 = the evaluated (trial)
+// state if it is accepted, list 1 = the current state if it is rejected (g2o's pop restores the
+// vertices but keeps the trial's _error, so both lists test the trial errors).  An active edge
+// behind the camera or with |e|^2 > maxErrorSquare is an outlier (index appended; the host sorts
+// the short list into g2o's active-edge order); inliers add |e|^2 to block partials that reduce3
+// sums in fixed order.
+struct SpecPass {
+    State cur;
+    int on;
+    double maxErrSq;
+    uint32_t* out_list;  // [2][E]
+    int E;
+    double* part;        // [2 lists][2][gridDim.x]: inlier sum, count
+    LiveCtl* ctl;
+};
+
+__device__ __forceinline__ double cheirality(const State& s, int c, int p)
+{
+    // SE3Quat::inverse: q*, -(q* t); forward = q* (0,0,1)
+    const double qc[4] = {-s.q[4 * c], -s.q[4 * c + 1], -s.q[4 * c + 2], s.q[4 * c + 3]};
+    const double tt[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
+    double it[3], fwd[3];
+    d_qrot(qc, tt, it);
+    const double z[3] = {0, 0, 1};
+    d_qrot(qc, z, fwd);
+    return (s.p[3 * p] + it[0]) * fwd[0] + (s.p[3 * p + 1] + it[1]) * fwd[1] + (s.p[3 * p + 2] + it[2]) * fwd[2];
+}
+
+// One point by a group of PG lanes (one edge per lane, strided): edge errors, robust chi2 and,
+// when linearising (BlockSolver::buildSystem with BaseBinaryEdge::constructQuadraticForm, robust
+// first-order weighting), Hll, bl and the per-edge Schur records Q; with a known lambda also
+// G = W Dinv_p (what edge_schur computes), so the first trial needs no extra sweep.
+template <bool LIN>
+__device__ __forceinline__ void point_group(const Problem& pb, const State& s, int p, int sub, const PointOut& o,
+                                            double lambda, bool with_g, const SpecPass* sp, double (&vs)[2],
+                                            double (&vc)[2])
+{
+    const int free_p = LIN && pb.ptfree[p];
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // H 00 01 02 11 12 22, g 0 1 2, chi
     double* H = acc;
     double* g = acc + 6;
     double& chi = acc[9];
+    const long long es = pb.ecsr;
     const int e0 = pb.pstart[p], e1 = pb.pstart[p + 1];
     for (int a = e0 + sub; a < e1; a += PG) {
         const int e = pb.pedges[a];
         if (!pb.active[e]) {
-            // the Schur products read Hpl of every listed edge: a removed edge contributes zero
+            // the Schur products read Q of every listed edge: a removed edge contributes zero
             if (free_p && pb.camh[pb.ecam[e]] >= 0) {
-                double* o = Hpl + pb.epos[e];
-                for (int k = 0; k < EQ_N; k++) o[(long long)k * pb.ecsr] = 0;
+                double* q = o.Q + pb.epos[e];
+                for (int k = 0; k < EQ_N; k++) q[k * es] = 0;
             }
             continue;
         }
         double ev[2], xc[3], rho0, rho1;
         edge_eval(pb, s, e, ev, xc, rho0, rho1);
-        err[2 * e] = ev[0];
-        err[2 * e + 1] = ev[1];
+        o.err[2 * e] = ev[0];
+        o.err[2 * e + 1] = ev[1];
         chi += rho0;
+        if (!LIN) {
+            if (sp) {
+                const double sumSquares = ev[0] * ev[0] + ev[1] * ev[1];
+                const int c = pb.ecam[e];
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const double dot = cheirality(k == 0 ? s : sp->cur, c, p);
+                    if (dot <= 0 || sumSquares > sp->maxErrSq) {
+                        sp->out_list[(long long)k * sp->E + atomicAdd(&sp->ctl->count[k], 1u)] = (uint32_t)e;
+                    } else {
+                        vs[k] += sumSquares;
+                        vc[k] += 1;
+                    }
+                }
+            }
+            continue;
+        }
         if (!free_p) continue;
         const int c = pb.ecam[e];
         const double f = pb.camk[3 * c];
@@ -178,12 +268,11 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
         if (pb.camh[c] >= 0) {
             // Hpl_e = Jp^T (w J): kept factored as (x/z, y/z, f/z) + W = w J (camera-major
             // component arrays; schur_chunks reads them coalesced)
-            double* o = Hpl + pb.epos[e];
-            const long long es = pb.ecsr;
-            o[0] = xi;
-            o[es] = yi;
-            o[2 * es] = f * iz;
-            for (int k = 0; k < 6; k++) o[(3 + k) * es] = J[k] * w;
+            double* qo = o.Q + pb.epos[e];
+            qo[0] = xi;
+            qo[es] = yi;
+            qo[2 * es] = f * iz;
+            for (int k = 0; k < 6; k++) qo[(3 + k) * es] = J[k] * w;
         }
     }
     // group sums by reduce-scatter: lane `sub` ends up with entry k of acc (H 00 01 02 11 12 22,
@@ -191,20 +280,46 @@ __global__ __launch_bounds__(BA_THREADS) void point_linearize(Problem pb, State 
     const int k = reduce_scatter<10, PG>(acc, sub);
     const double v = acc[0];
     const int gbase = (threadIdx.x & (kWave - 1)) & ~(PG - 1);
-    if (linearize) {
-        const double d0 = __shfl(v, gbase + rs_lane_of<10, PG>(0)), d1 = __shfl(v, gbase + rs_lane_of<10, PG>(3)),
-                     d2 = __shfl(v, gbase + rs_lane_of<10, PG>(5));
-        if (sub == rs_lane_of<10, PG>(0)) maxd_part[p] = free_p ? fmax(fabs(d0), fmax(fabs(d1), fabs(d2))) : 0.0;
+    if (LIN) {
+        double h6[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) h6[j] = __shfl(v, gbase + rs_lane_of<10, PG>(j));
+        if (sub == rs_lane_of<10, PG>(0)) o.maxd_part[p] = free_p ? fmax(fabs(h6[0]), fmax(fabs(h6[3]), fabs(h6[5]))) : 0.0;
+        if (with_g) {
+            // D_p = Hll_p + lambda I and its inverse exactly as edge_schur forms them from Hll
+            double D[9] = {h6[0], h6[1], h6[2], h6[1], h6[3], h6[4], h6[2], h6[4], h6[5]}, Di[9];
+            D[0] += lambda;
+            D[4] += lambda;
+            D[8] += lambda;
+            d_inv3(D, Di);
+            for (int a = e0 + sub; a < e1; a += PG) {
+                const int e = pb.pedges[a];
+                if (pb.camh[pb.ecam[e]] < 0) continue;
+                const int ap = pb.epos[e];
+                if (!free_p) {
+                    for (int j = 0; j < EG_N; j++) o.G[j * es + ap] = 0;
+                    continue;
+                }
+                double W[6];
+#pragma unroll
+                for (int j = 0; j < 6; j++) W[j] = o.Q[(3 + j) * es + ap];
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int kk = 0; kk < 3; kk++)
+                        o.G[(i * 3 + kk) * es + ap] = W[i * 3] * Di[kk] + W[i * 3 + 1] * Di[3 + kk] + W[i * 3 + 2] * Di[6 + kk];
+            }
+        }
     }
-    if (k == 9) chi_part[p] = v;
-    if (!linearize || k < 0 || k == 9) return;
+    if (k == 9) o.chi_part[p] = v;
+    if (!LIN || k < 0 || k == 9) return;
     if (k >= 6) {
-        bl[3 * p + (k - 6)] = v;
+        o.bl[3 * p + (k - 6)] = v;
         return;
     }
     // packed upper (00 01 02 11 12 22) -> both symmetric positions of the 3x3
     constexpr int r_of[6] = {0, 0, 0, 1, 1, 2}, c_of[6] = {0, 1, 2, 1, 2, 2};
-    double* Ho = Hll + 9 * (long long)p;
+    double* Ho = o.Hll + 9 * (long long)p;
     const int r = r_of[k], c = c_of[k];
     Ho[3 * r + c] = v;
     Ho[3 * c + r] = v;
@@ -317,18 +432,17 @@ __device__ __forceinline__ void block_sum(double (&acc)[N], double (*red)[N])
     __syncthreads();
 }
 
-// Per free camera: Hpp (6x6, packed upper 21) and bp (6) partial sums from its active edges;
-// errors come from point_linearize.  CAM_CHUNKS workgroups per camera (block = h * CAM_CHUNKS +
-// chunk) take interleaved slices of its edge list and write their partials; linearize_finish
-// adds them in chunk order (no cross-workgroup hand-off inside the kernel).
+// Per free camera: Hpp (6x6, packed upper 21) and bp (6) partial sums from its active edges.
+// CAM_CHUNKS workgroups per camera (block = h * CAM_CHUNKS + chunk) take interleaved slices of its
+// edge list and write their partials; schur_finish (or linearize_finish) adds them in chunk order
+// (no cross-workgroup hand-off inside the kernel).
 constexpr int CAM_CHUNKS = 8;
 constexpr int MAX_FREE_CAMS = 96;  // = CH_PANEL_ROWS / 6, the system-size limit checked at initialisation
 
-__global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s, const int* __restrict__ cam_of_block,
-                                                            const double* __restrict__ err,
-                                                            double* __restrict__ part)  // [nb][CAM_CHUNKS][27]
+__device__ __forceinline__ void cam_chunk(const Problem& pb, const State& s, const int* __restrict__ cam_of_block,
+                                          double* __restrict__ part, int blk)  // part: [nb][CAM_CHUNKS][27]
 {
-    const int h = blockIdx.x / CAM_CHUNKS, chunk = blockIdx.x % CAM_CHUNKS;
+    const int h = blk / CAM_CHUNKS, chunk = blk % CAM_CHUNKS;
     const int c = cam_of_block[h];
     __shared__ double red[BA_THREADS / kWave][27];
     double acc[27];
@@ -338,12 +452,12 @@ __global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s,
         const int e = pb.cedges[a];
         if (!pb.active[e]) continue;
         double ev[2], xc[3], rho0, rho1;
-        edge_eval(pb, s, e, ev, xc, rho0, rho1);
+        edge_eval(pb, s, e, ev, xc, rho0, rho1);  // the same error point_group computes for e
         double Jp[12];
         jac_pose(xc, f, Jp);
         const double inf = pb.info[e];
         const double w = rho1 * inf;
-        const double or0 = -inf * err[2 * e] * rho1, or1 = -inf * err[2 * e + 1] * rho1;
+        const double or0 = -inf * ev[0] * rho1, or1 = -inf * ev[1] * rho1;
         int k = 0;
         for (int r = 0; r < 6; r++)
             for (int cc = r; cc < 6; cc++) acc[k++] += (Jp[r] * Jp[cc] + Jp[6 + r] * Jp[6 + cc]) * w;
@@ -351,6 +465,38 @@ __global__ __launch_bounds__(BA_THREADS) void cam_linearize(Problem pb, State s,
     }
     block_sum<27>(acc, red);
     if (threadIdx.x < 27) part[((long long)h * CAM_CHUNKS + chunk) * 27 + threadIdx.x] = red[0][threadIdx.x];
+}
+
+// The linearisation sweep in one launch: blocks [0, npb) are point groups (point_group<true>),
+// the rest camera chunks (CAM_CHUNKS per free camera: Hpp packed upper 21 + bp 6 partials,
+// added in chunk order by schur_finish / linearize_finish).
+__global__ __launch_bounds__(BA_THREADS) void linearize_kernel(Problem pb, State s, PointOut o, double lambda, int with_g,
+                                                               int npb, const int* __restrict__ cam_of_block,
+                                                               double* __restrict__ campart)
+{
+    if ((int)blockIdx.x >= npb) {
+        cam_chunk(pb, s, cam_of_block, campart, blockIdx.x - npb);
+        return;
+    }
+    const int gid = blockIdx.x * BA_THREADS + threadIdx.x;
+    const int p = gid / PG, sub = gid % PG;
+    if (p >= pb.P) return;  // whole groups
+    double vs[2], vc[2];
+    point_group<true>(pb, s, p, sub, o, lambda, with_g != 0, nullptr, vs, vc);
+}
+
+// Evaluation of a trial state (errors + robust chi2) with the speculative post-pass.
+__global__ __launch_bounds__(BA_THREADS) void evaluate_kernel(Problem pb, State s, PointOut o, SpecPass sp)
+{
+    const int gid = blockIdx.x * BA_THREADS + threadIdx.x;
+    const int p = gid / PG, sub = gid % PG;
+    double vs[2] = {0, 0}, vc[2] = {0, 0};
+    if (p < pb.P) point_group<false>(pb, s, p, sub, o, 0.0, false, sp.on ? &sp : nullptr, vs, vc);
+    if (!sp.on) return;
+    __shared__ double red[BA_THREADS / kWave][4];
+    double v4[4] = {vs[0], vc[0], vs[1], vc[1]};
+    block_sum<4>(v4, red);
+    if (threadIdx.x < 4) sp.part[(long long)threadIdx.x * gridDim.x + blockIdx.x] = red[0][threadIdx.x];
 }
 
 // After the linearisation (one workgroup): Hpp / bp of every free camera from its chunk partials,
@@ -432,36 +578,35 @@ __global__ __launch_bounds__(1024) void linearize_finish(int nb, const int* __re
     }
 }
 
-struct OutlierCtl {
-    double osum[2][2];
-    int fail;
-    uint32_t count[2];
-    uint32_t ticket;
-};
 
-// Fixed-order reduction of two sum arrays and one max array into out[0..2]; with ns > 0 also
-// the outlier pass's per-block (sum, count) partials of its ns states into ctl->osum.
+// Fixed-order reduction of two sum arrays and one max array into out[0..2], a third sum array into
+// outc[0] (the linearisation's chi2), and with ns > 0 the post-pass's per-block (sum, count)
+// partials of its ns states into ctl->osum.
 __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, int na,
                                                 const double* __restrict__ b, int nb,
                                                 const double* __restrict__ m, int nm,
                                                 double* __restrict__ out,
+                                                const double* __restrict__ c, int nc, double* __restrict__ outc,
                                                 const double* __restrict__ opart, int oblocks, int ns,
-                                                OutlierCtl* __restrict__ ctl)
+                                                OutlierCtl* __restrict__ ctl, LiveCtl* __restrict__ live)
 {
-    __shared__ double sa[1024], sb[1024], sm[1024];
-    double va = 0, vb = 0, vm = 0;
+    __shared__ double sa[1024], sb[1024], sm[1024], sc[1024];
+    double va = 0, vb = 0, vm = 0, vc = 0;
     for (int i = threadIdx.x; i < na; i += 1024) va += a[i];
     for (int i = threadIdx.x; i < nb; i += 1024) vb += b[i];
     for (int i = threadIdx.x; i < nm; i += 1024) vm = fmax(vm, m[i]);
+    for (int i = threadIdx.x; i < nc; i += 1024) vc += c[i];
     sa[threadIdx.x] = va;
     sb[threadIdx.x] = vb;
     sm[threadIdx.x] = vm;
+    sc[threadIdx.x] = vc;
     __syncthreads();
     for (int s = 512; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) {
             sa[threadIdx.x] += sa[threadIdx.x + s];
             sb[threadIdx.x] += sb[threadIdx.x + s];
             sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + s]);
+            sc[threadIdx.x] += sc[threadIdx.x + s];
         }
         __syncthreads();
     }
@@ -469,6 +614,14 @@ __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, in
         out[0] = sa[0];
         out[1] = sb[0];
         out[2] = sm[0];
+        if (nc > 0) outc[0] = sc[0];
+        // the trial's counters to the host block, and zero for the next trial
+        ctl->fail = live->fail;
+        ctl->count[0] = live->count[0];
+        ctl->count[1] = live->count[1];
+        live->fail = 0;
+        live->count[0] = 0;
+        live->count[1] = 0;
     }
     for (int k = 0; k < ns; k++) {
         __syncthreads();
@@ -494,24 +647,6 @@ __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, in
     }
 }
 
-// Eigen Matrix3d::inverse (cofactors)
-__device__ __forceinline__ void d_inv3(const double m[9], double o[9])
-{
-    const double c0 = m[4] * m[8] - m[5] * m[7];
-    const double c1 = m[5] * m[6] - m[3] * m[8];
-    const double c2 = m[3] * m[7] - m[4] * m[6];
-    const double det = m[0] * c0 + m[1] * c1 + m[2] * c2;
-    const double id = 1.0 / det;
-    o[0] = c0 * id;
-    o[1] = (m[2] * m[7] - m[1] * m[8]) * id;
-    o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
-    o[3] = c1 * id;
-    o[4] = (m[0] * m[8] - m[2] * m[6]) * id;
-    o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
-    o[6] = c2 * id;
-    o[7] = (m[1] * m[6] - m[0] * m[7]) * id;
-    o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
-}
 
 // Per-edge factors of the Schur sweeps, camera-major component arrays (entry k of edge record a
 // at k * ecsr + a, a = the edge's camera-CSR position):
@@ -587,9 +722,9 @@ struct SchurPair {
 };
 
 // Entry k < 42 of a pair's sum -> S (both triangles; + Hpp + lambda I on the diagonal, + tether
-// H12 blocks) or rhs (k >= 36, diagonal pairs).
-__device__ __forceinline__ void schur_write(const SchurPair& pr, int k, double sum, const double* __restrict__ Hpp,
-                                            const double* __restrict__ bp, double lambda, int np,
+// H12 blocks) or rhs (k >= 36, diagonal pairs: bp - sum).  `cam` is Hpp[k] (k < 36) or bp[k - 36]
+// of the diagonal pair's camera.
+__device__ __forceinline__ void schur_write(const SchurPair& pr, int k, double sum, double cam, double lambda, int np,
                                             const int* __restrict__ ptlist, const double* __restrict__ tout,
                                             double* __restrict__ S, double* __restrict__ rhs)
 {
@@ -597,7 +732,7 @@ __device__ __forceinline__ void schur_write(const SchurPair& pr, int k, double s
     if (k < 36) {
         const int r = k / 6, c = k % 6;
         double v = -sum;
-        if (diag) v += Hpp[36 * (long long)pr.c1 + k] + (r == c ? lambda : 0.0);
+        if (diag) v += cam + (r == c ? lambda : 0.0);
         // tether H12 blocks of this camera pair (code = 2 t + transposed)
         for (int j = pr.tbeg; j < pr.tend; j++) {
             const int code = ptlist[j];
@@ -607,7 +742,7 @@ __device__ __forceinline__ void schur_write(const SchurPair& pr, int k, double s
         S[(long long)(6 * pr.h1 + r) * np + 6 * pr.h2 + c] = v;
         S[(long long)(6 * pr.h2 + c) * np + 6 * pr.h1 + r] = v;
     } else if (diag) {
-        rhs[6 * pr.h1 + (k - 36)] = bp[6 * pr.c1 + (k - 36)] - sum;
+        rhs[6 * pr.h1 + (k - 36)] = cam - sum;
     }
 }
 
@@ -617,9 +752,7 @@ __global__ __launch_bounds__(SC_THREADS) void schur_chunks(const SchurChunk* __r
                                                            const double* __restrict__ G,
                                                            const double* __restrict__ Q,
                                                            const double* __restrict__ camk,
-                                                           const double* __restrict__ bl,
-                                                           const double* __restrict__ Hpp,
-                                                           const double* __restrict__ bp, double lambda, int np, int ecsr,
+                                                           const double* __restrict__ bl, double lambda, int np, int ecsr,
                                                            const int* __restrict__ ptlist,
                                                            const double* __restrict__ tout,
                                                            double* __restrict__ part,
@@ -709,27 +842,55 @@ __global__ __launch_bounds__(SC_THREADS) void schur_chunks(const SchurChunk* __r
         term(q1, g1, b1, v1);
     }
     block_sum<42, SC_THREADS>(acc, red);  // red[0][k] = chunk total of entry k
-    if (pr.nslots > 1) {  // schur_finish adds the partials (a kernel boundary, no L2 write-back fence)
+    if (pr.nslots > 1 || pr.h1 == pr.h2) {  // schur_finish: partials in order, the camera blocks
         if (t < 42) part[(long long)ch.slot * 42 + t] = red[0][t];
         return;
     }
-    if (t < 42) schur_write(pr, t, red[0][t], Hpp, bp, lambda, np, ptlist, tout, S, rhs);
+    if (t < 42) schur_write(pr, t, red[0][t], 0.0, lambda, np, ptlist, tout, S, rhs);
 }
 
-// Pairs of more than one chunk: a 64-lane wave per pair adds its chunk partials in chunk order.
-__global__ __launch_bounds__(64) void schur_finish(const int* __restrict__ multi, const SchurPair* __restrict__ pairs,
-                                                   const double* __restrict__ part,
-                                                   const double* __restrict__ Hpp, const double* __restrict__ bp,
+// Diagonal pairs and pairs of more than one chunk: a 64-lane wave per pair adds its chunk partials
+// in chunk order.  A diagonal pair's camera block comes from the linearisation partials (chunk
+// order, then the tethers in set order: g2o's addEdge order), written to Hpp / bp as well
+// (update_state's computeScale reads bp).
+__global__ __launch_bounds__(64) void schur_finish(const int* __restrict__ flist, const SchurPair* __restrict__ pairs,
+                                                   const double* __restrict__ part, const double* __restrict__ campart,
+                                                   const Tether* __restrict__ teth, int nt,
+                                                   double* __restrict__ Hpp, double* __restrict__ bp,
                                                    double lambda, int np, const int* __restrict__ ptlist,
                                                    const double* __restrict__ tout, double* __restrict__ S,
                                                    double* __restrict__ rhs)
 {
-    const SchurPair pr = pairs[multi[blockIdx.x]];
+    const SchurPair pr = pairs[flist[blockIdx.x]];
     const int t = threadIdx.x;
     if (t >= 42) return;
     double v = 0;
     for (int q = 0; q < pr.nslots; q++) v += part[(long long)(pr.slot0 + q) * 42 + t];
-    schur_write(pr, t, v, Hpp, bp, lambda, np, ptlist, tout, S, rhs);
+    double cam = 0;
+    if (pr.h1 == pr.h2) {
+        const int h = pr.h1;
+        int pk, r = 0, c = 0;  // packed upper index of (min, max), or 21 + rhs entry
+        if (t < 36) {
+            r = min(t / 6, t % 6);
+            c = max(t / 6, t % 6);
+            pk = r * 6 - r * (r - 1) / 2 + (c - r);
+        } else {
+            pk = 21 + (t - 36);
+        }
+        for (int q = 0; q < CAM_CHUNKS; q++) cam += campart[((long long)h * CAM_CHUNKS + q) * 27 + pk];
+        for (int i = 0; i < nt; i++) {
+            const Tether& T = teth[i];
+            if (!T.active) continue;
+            for (int vtx = 0; vtx < 2; vtx++) {
+                if ((vtx ? T.h2 : T.h1) != h) continue;
+                const double* o = tout + (long long)i * TETHER_OUT;
+                cam += t < 36 ? o[36 * vtx + r * 6 + c] : o[108 + 6 * vtx + (t - 36)];
+            }
+        }
+        if (t < 36) Hpp[36 * (long long)pr.c1 + t] = cam;
+        else bp[6 * pr.c1 + (t - 36)] = cam;
+    }
+    schur_write(pr, t, v, cam, lambda, np, ptlist, tout, S, rhs);
 }
 
 // Dense SPD solve S x = b in one workgroup, S of padded order np (multiple of 16, rows n..np-1
@@ -990,7 +1151,22 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         }
     };
     tick(-1);
+#if MAGE_CHOL_ABLATE == 4  // per-step timestamps of every wave (rel. to the first barrier)
+    __shared__ long long ttr[CT_MAXT][CT_WAVES][4];
+    long long tbase = 0;
+#define CT_STAMP(k, ph)                                                                   \
+    do {                                                                                  \
+        if (lane == 0 && (k) < CT_MAXT) ttr[k][wave][ph] = __builtin_amdgcn_s_memtime() - tbase; \
+    } while (0)
+#else
+#define CT_STAMP(k, ph) \
+    do {                \
+    } while (0)
+#endif
     __syncthreads();
+#if MAGE_CHOL_ABLATE == 4
+    tbase = __builtin_amdgcn_s_memtime();
+#endif
     tick(0);
 
     // --- diagonal block: Cholesky of A_kk and inv(L_kk) by its owner wave (slot `slot`), with
@@ -1101,7 +1277,9 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         }
         if (tid < 16) vb[16 * k + tid] = yk[buf][tid];
         tick(3);
+        CT_STAMP(k, 0);
         __syncthreads();
+        CT_STAMP(k, 1);
         tick(2);
         // --- SYRK: A_ij -= U_ki^T U_kj for the owned tiles with k < i <= j ---
         auto syrk = [&](int sl) {
@@ -1126,7 +1304,9 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             if (i > k && i < mt && !(i == kn && j == kn)) syrk(sl);
         }
         tick(4);
+        CT_STAMP(k, 2);
         __syncthreads();
+        CT_STAMP(k, 3);
         tick(2);
     }
     if (s_fail) {
@@ -1179,31 +1359,68 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         __syncthreads();
     }
     tick(5);
+#if MAGE_CHOL_ABLATE == 4
+    if (tid == 0) {
+        printf("chol_tiles np=%d backward end %lld\n", np, (long long)(__builtin_amdgcn_s_memtime() - tbase));
+        for (int k = 0; k < mt; k++) {
+            printf("step %2d:", k);
+            for (int w = 0; w < CT_WAVES; w++)
+                printf(" |%lld %lld %lld %lld", ttr[k][w][0], ttr[k][w][1], ttr[k][w][2], ttr[k][w][3]);
+            printf("\n");
+        }
+    }
+#endif
     for (int i = tid; i < np; i += CT_THREADS) x[i] = i < n ? vb[i] : 0.0;
     if (MAGE_CHOL_ABLATE == 3 && tid == 0)
         printf("chol_tiles np=%d cycles: load %lld diag %lld barrier %lld trsm %lld syrk %lld backward %lld | factor0 stage %lld columns %lld\n", np, tm[0],
                tm[1], tm[2], tm[3], tm[4], tm[5], tm[6], tm[7]);
 }
 
-// xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]) = db - sum_e Z_e^T xp[h(e)] (Dinv symmetric,
-// Z_e = Hpl_e Dinv from edge_schur); a PG-lane group per point, one edge per lane.  Also the
-// point part of computeScale.
-__global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const double* __restrict__ Z,
-                                                            const double* __restrict__ Q,
-                                                            const double* __restrict__ Hll,
-                                                            const double* __restrict__ bl,
-                                                            const double* __restrict__ xp, double lambda,
-                                                            double* __restrict__ xl,
-                                                            double* __restrict__ scale_part)
+// Back-substitution and the trial state in one launch.  Blocks [0, npb): a PG-lane group per
+// point: xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]) = Dinv bl - sum_e Z_e^T xp[h(e)] (Dinv
+// symmetric; Z_e^T xp = G_e^T (Jp_e xp)), trial point B.p = A.p + xl (copy for points outside the
+// system) and the point part of computeScale.  The remaining blocks: thread per camera, trial
+// pose exp(xp) * T (VertexSE3Expmap::oplusImpl) or copy, and the camera part of computeScale.
+__global__ __launch_bounds__(BA_THREADS) void backsub_update(Problem pb, const double* __restrict__ G,
+                                                             const double* __restrict__ Q,
+                                                             const double* __restrict__ Hll,
+                                                             const double* __restrict__ bl,
+                                                             const double* __restrict__ xp, double lambda,
+                                                             State A, State B, const double* __restrict__ bp,
+                                                             double* __restrict__ scale_part, int npb)
 {
+    if ((int)blockIdx.x >= npb) {
+        const int i = (blockIdx.x - npb) * BA_THREADS + threadIdx.x;
+        if (i >= pb.C) return;
+        double q[4] = {A.q[4 * i], A.q[4 * i + 1], A.q[4 * i + 2], A.q[4 * i + 3]};
+        double t[3] = {A.t[3 * i], A.t[3 * i + 1], A.t[3 * i + 2]};
+        const int h = pb.camh[i];
+        double sc = 0;
+        if (h >= 0) {
+            double u[6];
+            for (int k = 0; k < 6; k++) {
+                u[k] = xp[6 * h + k];
+                sc += u[k] * (lambda * u[k] + bp[6 * i + k]);
+            }
+            d_oplus(q, t, u);
+        }
+        for (int k = 0; k < 4; k++) B.q[4 * i + k] = q[k];
+        for (int k = 0; k < 3; k++) B.t[3 * i + k] = t[k];
+        scale_part[pb.P + i] = sc;
+        return;
+    }
     const int gid = blockIdx.x * BA_THREADS + threadIdx.x;
     const int p = gid / PG, sub = gid % PG;
     if (p >= pb.P) return;
     if (!pb.ptfree[p]) {
-        if (sub == 0) scale_part[p] = 0;
+        if (sub == 0) {
+            for (int k = 0; k < 3; k++) B.p[3 * p + k] = A.p[3 * p + k];
+            scale_part[p] = 0;
+        }
         return;
     }
     double cl[3] = {0, 0, 0};
+    const long long es = pb.ecsr;
     for (int a = pb.pstart[p] + sub; a < pb.pstart[p + 1]; a += PG) {
         const int e = pb.pedges[a];
         if (!pb.active[e]) continue;
@@ -1211,7 +1428,6 @@ __global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const do
         if (h < 0) continue;
         // Z_e^T xp = G^T (Jp xp)
         const int a2 = pb.epos[e];
-        const long long es = pb.ecsr;
         double J[12];
         jac_pose_q(Q[a2], Q[es + a2], Q[2 * es + a2], pb.camk[3 * pb.ecam[e]], J);
         const double* X = xp + 6 * h;
@@ -1222,7 +1438,7 @@ __global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const do
             u1 += J[6 + r] * X[r];
         }
 #pragma unroll
-        for (int k = 0; k < 3; k++) cl[k] += Z[k * es + a2] * u0 + Z[(3 + k) * es + a2] * u1;
+        for (int k = 0; k < 3; k++) cl[k] += G[k * es + a2] * u0 + G[(3 + k) * es + a2] * u1;
     }
     group_sum(cl);
     if (sub != 0) return;
@@ -1239,42 +1455,10 @@ __global__ __launch_bounds__(BA_THREADS) void point_backsub(Problem pb, const do
     for (int r = 0; r < 3; r++) {
         const double dbr = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
         const double v = dbr - cl[r];
-        xl[3 * p + r] = v;
+        B.p[3 * p + r] = A.p[3 * p + r] + v;
         sc += v * (lambda * v + bl[3 * p + r]);
     }
     scale_part[p] = sc;
-}
-
-// Trial state B from A: cameras exp(xp) * T (free) or copy; points p + xl (free) or copy.
-// Also the camera part of computeScale.
-__global__ __launch_bounds__(BA_THREADS) void update_state(Problem pb, State A, State B,
-                                                           const double* __restrict__ xp,
-                                                           const double* __restrict__ xl,
-                                                           const double* __restrict__ bp, double lambda,
-                                                           double* __restrict__ scale_part_cam)
-{
-    const int i = blockIdx.x * BA_THREADS + threadIdx.x;
-    if (i < pb.C) {
-        double q[4] = {A.q[4 * i], A.q[4 * i + 1], A.q[4 * i + 2], A.q[4 * i + 3]};
-        double t[3] = {A.t[3 * i], A.t[3 * i + 1], A.t[3 * i + 2]};
-        const int h = pb.camh[i];
-        double sc = 0;
-        if (h >= 0) {
-            double u[6];
-            for (int k = 0; k < 6; k++) {
-                u[k] = xp[6 * h + k];
-                sc += u[k] * (lambda * u[k] + bp[6 * i + k]);
-            }
-            d_oplus(q, t, u);
-        }
-        for (int k = 0; k < 4; k++) B.q[4 * i + k] = q[k];
-        for (int k = 0; k < 3; k++) B.t[3 * i + k] = t[k];
-        scale_part_cam[i] = sc;
-    }
-    if (i < pb.P) {
-        const bool fr = pb.ptfree[i];
-        for (int k = 0; k < 3; k++) B.p[3 * i + k] = A.p[3 * i + k] + (fr ? xl[3 * i + k] : 0.0);
-    }
 }
 
 // StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) per active edge using the stored
@@ -1290,7 +1474,7 @@ __global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s0,
                                                            double maxErrSq,
                                                            uint32_t* __restrict__ out_list,
                                                            double* __restrict__ part,  // [ns][2][gridDim.x]
-                                                           OutlierCtl* __restrict__ ctl)
+                                                           LiveCtl* __restrict__ ctl)
 {
     __shared__ double ssum[2][BA_THREADS / kWave], scnt[2][BA_THREADS / kWave];
     const int e = blockIdx.x * BA_THREADS + threadIdx.x;
@@ -1395,7 +1579,7 @@ struct BundleAdjuster {
     int iteration = 0;
     double user_lambda = 0, lambda = 0, ni = 2, huber = 0;
     int n = 0, np = 0;  // 6 * cameras in the system, padded to a multiple of 16
-    int npairs = 0, n_slots = 0, n_sblocks = 0, n_smulti = 0;  // Schur pairs, partial slots, blocks, multi-chunk pairs
+    int npairs = 0, n_slots = 0, n_sblocks = 0, n_sfinish = 0;  // Schur pairs, partial slots, blocks, schur_finish pairs
     std::vector<int> camh, ptfree, cam_of_block;
     hipStream_t st = nullptr;
     // Control block read back at every host decision (one pinned copy per synchronisation):
@@ -1403,19 +1587,16 @@ struct BundleAdjuster {
     // OutlierCtl (sums, Cholesky failure flag, counts, ticket).
     static constexpr int CTL_DOUBLES = 16, CTL_OUTLIER = 6, CTL_SCRATCH = 12;
     static_assert(CTL_OUTLIER * 8 + sizeof(OutlierCtl) <= CTL_SCRATCH * 8, "control block layout");
+    // The control block is host memory the kernels write directly (pinned, coherent, mapped):
+    // h_ctl on the host, h_ctl_dev in kernels; a trial's results need only the stream sync.
     double* h_ctl = nullptr;
-    OutlierCtl* d_octl() const { return reinterpret_cast<OutlierCtl*>(d_red.as<double>() + CTL_OUTLIER); }
+    double* h_ctl_dev = nullptr;
+    OutlierCtl* d_octl() const { return reinterpret_cast<OutlierCtl*>(h_ctl_dev + CTL_OUTLIER); }
     const OutlierCtl& h_octl() const { return *reinterpret_cast<const OutlierCtl*>(h_ctl + CTL_OUTLIER); }
-    int* d_failp() const { return &d_octl()->fail; }
-    // zero the failure flag, counts and ticket (the sums are written, not accumulated)
-    mage_status reset_ctl_words()
-    {
-        MAGE_HIP(hipMemsetAsync(&d_octl()->fail, 0, sizeof(OutlierCtl) - offsetof(OutlierCtl, fail), st));
-        return MAGE_OK;
-    }
+    LiveCtl* d_live() const { return reinterpret_cast<LiveCtl*>(d_livebuf.ptr); }
+    int* d_failp() const { return &d_live()->fail; }
     mage_status read_ctl()
     {
-        MAGE_HIP(hipMemcpyAsync(h_ctl, d_red.ptr, CTL_DOUBLES * sizeof(double), hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipStreamSynchronize(st));
         return MAGE_OK;
     }
@@ -1426,7 +1607,7 @@ struct BundleAdjuster {
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
         d_olist, d_camcnt, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
-        d_smulti, d_epos;
+        d_sfinish, d_epos, d_chi_lin, d_livebuf;
     int n_entries = 0;  // point-CSR entries (active edges at initialisation)
     int nb_free = 0;    // cameras in the reduced system
     mage_ba_stats stats{};
@@ -1465,7 +1646,7 @@ struct BundleAdjuster {
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk, &d_olist,
                         &d_camcnt, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
-                        &d_schunks, &d_spart, &d_smulti, &d_epos})
+                        &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf})
             b->release();
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
@@ -1713,15 +1894,15 @@ struct BundleAdjuster {
                 schunks[8 * j + x] = j < xcd_chunks[x].size() ? xcd_chunks[x][j] : ch;
             }
         n_sblocks = (int)schunks.size();
-        std::vector<int> smulti;  // pairs finished by schur_finish
+        std::vector<int> sfinish;  // pairs finished by schur_finish: diagonal or more than one chunk
         for (int pi = 0; pi < npairs; pi++)
-            if (spairs[pi].nslots > 1) smulti.push_back(pi);
-        n_smulti = (int)smulti.size();
+            if (spairs[pi].nslots > 1 || spairs[pi].h1 == spairs[pi].h2) sfinish.push_back(pi);
+        n_sfinish = (int)sfinish.size();
         MAGE_REQUIRE(pbeg[npairs] < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
         n_entries = pstart[P];
         if ((r = upload(d_sentries, sentries)) != MAGE_OK) return r;
         if ((r = upload(d_epos, epos)) != MAGE_OK) return r;
-        if ((r = upload(d_smulti, smulti)) != MAGE_OK) return r;
+        if ((r = upload(d_sfinish, sfinish)) != MAGE_OK) return r;
         if ((r = upload(d_spairs, spairs)) != MAGE_OK) return r;
         if ((r = upload(d_schunks, schunks)) != MAGE_OK) return r;
         if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
@@ -1757,13 +1938,15 @@ struct BundleAdjuster {
                         std::make_pair(&d_Z, (size_t)std::max(n_entries, 1) * EG_N * 8),
                         std::make_pair(&d_campart, Cm * CAM_CHUNKS * 27 * 8),
                         std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
-                        std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, (Pm + teth.size()) * 8),
+                        std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, (Pm + teth.size()) * 8), std::make_pair(&d_chi_lin, (Pm + teth.size()) * 8),
                         std::make_pair(&d_tout, std::max<size_t>(teth.size(), 1) * TETHER_OUT * 8),
                         std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
-                        std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, (Em / BA_THREADS + 2) * 4 * 8),
+                        std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, ((size_t)std::max<int>((int)(Em / BA_THREADS), group_grid((int)Pm)) + 2) * 4 * 8),
                         std::make_pair(&d_olist, Em * 2 * 4 + 16), std::make_pair(&d_camcnt, Cm * 4),
                         std::make_pair(&d_spart, (size_t)std::max(n_slots, 1) * 42 * 8)})
             if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
+        if ((r = d_livebuf.reserve(sizeof(LiveCtl))) != MAGE_OK) return r;
+        MAGE_HIP(hipMemsetAsync(d_livebuf.ptr, 0, sizeof(LiveCtl), st));
         MAGE_HIP(hipMemsetAsync(d_maxd.ptr, 0, (Pm + Cm) * 8, st));
         MAGE_HIP(hipMemsetAsync(d_scale.ptr, 0, (Pm + Cm) * 8, st));
         // chol_tiles reads S without writing it and every trial rewrites the same covisible pair
@@ -1780,96 +1963,99 @@ struct BundleAdjuster {
 
     // Linearise the current state (errors, Hll/bl/Hpl, Hpp/bp) and reduce chi2 / max diagonal
     // into d_red[0..2]; no host synchronisation.
-    mage_status linearize()
+    // G (edge_schur's records) is valid for this lambda (NaN: not computed)
+    double g_lambda = std::numeric_limits<double>::quiet_NaN();
+    int eval_blocks() const { return P > 0 ? group_grid(P) : 0; }
+    PointOut point_out(double* chi) const
+    {
+        return PointOut{d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(), d_Z.as<double>(),
+                        chi, d_maxd.as<double>()};
+    }
+
+    // Linearise the current state (errors, Hll / bl / per-edge records, camera partials) in one
+    // launch; with a known lambda (every iteration but the first) also G, so the first trial
+    // needs no edge_schur.  init_lambda: linearize_finish reduces chi2 / max diagonal
+    // (computeLambdaInit) for the host right away.  No host synchronisation.
+    mage_status linearize(double lam_for_g, bool init_lambda)
     {
         Problem pb = problem();
-        if (P > 0) {
-            launch("ba.point_linearize", point_linearize, dim3(group_grid(P)), dim3(BA_THREADS), 0, st, pb, state(cur), 1,
-                               d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
-                               d_chi.as<double>(), d_maxd.as<double>());
-        }
-        if (nb_free > 0) {
-            launch("ba.cam_linearize", cam_linearize, dim3(nb_free * CAM_CHUNKS), dim3(BA_THREADS), 0, st, pb, state(cur),
-                   (const int*)d_camblk.as<int>(), (const double*)d_err.as<double>(), d_campart.as<double>());
-        }
+        const int npb = eval_blocks(), ncb = nb_free * CAM_CHUNKS;
+        const bool with_g = std::isfinite(lam_for_g) && n_entries > 0 && !points_fixed;
+        if (npb + ncb > 0)
+            launch("ba.linearize", linearize_kernel, dim3(npb + ncb), dim3(BA_THREADS), 0, st, pb, state(cur),
+                   point_out(d_chi_lin.as<double>()), with_g ? lam_for_g : 0.0, with_g ? 1 : 0, npb,
+                   (const int*)d_camblk.as<int>(), d_campart.as<double>());
+        g_lambda = with_g ? lam_for_g : std::numeric_limits<double>::quiet_NaN();
         const int nt = (int)teth.size();
         if (nt > 0)
             launch("ba.tether_eval", tether_eval, dim3((nt + 63) / 64), dim3(64), 0, st, (const Tether*)d_teth.as<Tether>(),
-                   nt, state(cur), 1, d_chi.as<double>() + P, d_tout.as<double>());
-        launch("ba.linearize_finish", linearize_finish, dim3(1), dim3(1024), 0, st, nb_free, (const int*)d_camblk.as<int>(),
-               (const double*)d_campart.as<double>(), (const double*)d_chi.as<double>(), P,
-               (const double*)d_maxd.as<double>(), (const Tether*)d_teth.as<Tether>(), nt,
-               (const double*)d_tout.as<double>(), d_Hpp.as<double>(), d_bp.as<double>(), d_red.as<double>());
+                   nt, state(cur), 1, d_chi_lin.as<double>() + P, d_tout.as<double>());
+        if (init_lambda)
+            launch("ba.linearize_finish", linearize_finish, dim3(1), dim3(1024), 0, st, nb_free, (const int*)d_camblk.as<int>(),
+                   (const double*)d_campart.as<double>(), (const double*)d_chi_lin.as<double>(), P,
+                   (const double*)d_maxd.as<double>(), (const Tether*)d_teth.as<Tether>(), nt,
+                   (const double*)d_tout.as<double>(), d_Hpp.as<double>(), d_bp.as<double>(), h_ctl_dev);
         MAGE_HIP(hipGetLastError());
         return MAGE_OK;
     }
 
     // One trial: solve with lambda, build the trial state in the other buffer, evaluate it.
-    // Reads back red[0..5] = {chi(current), -, maxdiag, chi(trial), scale, -} and the fail flag.
+    // Reads back red[0..5] = {chi(current), -, -, chi(trial), scale, -} and the fail flag.
     mage_status trial(double lam, bool* ok, double red[6], bool speculate)
     {
-        mage_status r0;
         Problem pb = problem();
-        const int gmax = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
         double* xp = d_x.as<double>();
-        double* xl = d_x.as<double>() + np;
-        if ((r0 = reset_ctl_words()) != MAGE_OK) return r0;
-        if (n_entries > 0 && !points_fixed) {
+        const int npb = eval_blocks();
+        if (n_entries > 0 && !points_fixed && !(g_lambda == lam)) {
             launch("ba.edge_schur", edge_schur, dim3((n_entries + BA_THREADS - 1) / BA_THREADS), dim3(BA_THREADS), 0, st,
                    pb, (const double*)d_Hll.as<double>(), (const double*)d_Hpl.as<double>(), lam, d_Z.as<double>());
+            g_lambda = lam;
         }
         if (n > 0) {
             if (np > 16 * CT_MAXT) MAGE_HIP(hipMemsetAsync(d_S.ptr, 0, (size_t)np * np * 8, st));
-            {
-                launch("ba.schur_pairs", schur_chunks, dim3(n_sblocks), dim3(SC_THREADS), 0, st,
-                       (const SchurChunk*)d_schunks.as<SchurChunk>(), (const SchurPair*)d_spairs.as<SchurPair>(),
-                       (const int2*)d_sentries.as<int2>(), (const double*)d_Z.as<double>(), (const double*)d_Hpl.as<double>(),
-                       (const double*)d_camk.as<double>(), (const double*)d_bl.as<double>(), (const double*)d_Hpp.as<double>(), (const double*)d_bp.as<double>(),
-                       lam, np, n_entries, (const int*)d_ptlist.as<int>(), (const double*)d_tout.as<double>(), d_spart.as<double>(),
-                       d_S.as<double>(), d_rhs.as<double>());
-                if (n_smulti > 0)
-                    launch("ba.schur_finish", schur_finish, dim3(n_smulti), dim3(64), 0, st, (const int*)d_smulti.as<int>(),
-                           (const SchurPair*)d_spairs.as<SchurPair>(), (const double*)d_spart.as<double>(),
-                           (const double*)d_Hpp.as<double>(), (const double*)d_bp.as<double>(), lam, np,
-                           (const int*)d_ptlist.as<int>(), (const double*)d_tout.as<double>(), d_S.as<double>(), d_rhs.as<double>());
-            }
-            {
-                if (np <= 16 * CT_MAXT)
-                    launch("ba.cholesky_solve", chol_tiles, dim3(1), dim3(CT_THREADS), 0, st,
-                           (const double*)d_S.as<double>(), np, n, (const double*)d_rhs.as<double>(), xp, d_failp());
-                else
-                    launch("ba.cholesky_solve", cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np,
-                           n, (const double*)d_rhs.as<double>(), xp, d_failp());
-            }
+            launch("ba.schur_pairs", schur_chunks, dim3(n_sblocks), dim3(SC_THREADS), 0, st,
+                   (const SchurChunk*)d_schunks.as<SchurChunk>(), (const SchurPair*)d_spairs.as<SchurPair>(),
+                   (const int2*)d_sentries.as<int2>(), (const double*)d_Z.as<double>(), (const double*)d_Hpl.as<double>(),
+                   (const double*)d_camk.as<double>(), (const double*)d_bl.as<double>(), lam, np, n_entries,
+                   (const int*)d_ptlist.as<int>(), (const double*)d_tout.as<double>(), d_spart.as<double>(), d_S.as<double>(),
+                   d_rhs.as<double>());
+            launch("ba.schur_finish", schur_finish, dim3(n_sfinish), dim3(64), 0, st, (const int*)d_sfinish.as<int>(),
+                   (const SchurPair*)d_spairs.as<SchurPair>(), (const double*)d_spart.as<double>(),
+                   (const double*)d_campart.as<double>(), (const Tether*)d_teth.as<Tether>(), (int)teth.size(),
+                   d_Hpp.as<double>(), d_bp.as<double>(), lam, np, (const int*)d_ptlist.as<int>(),
+                   (const double*)d_tout.as<double>(), d_S.as<double>(), d_rhs.as<double>());
+            if (np <= 16 * CT_MAXT)
+                launch("ba.cholesky_solve", chol_tiles, dim3(1), dim3(CT_THREADS), 0, st,
+                       (const double*)d_S.as<double>(), np, n, (const double*)d_rhs.as<double>(), xp, d_failp());
+            else
+                launch("ba.cholesky_solve", cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np,
+                       n, (const double*)d_rhs.as<double>(), xp, d_failp());
         }
-        if (P > 0) {
-            launch("ba.point_backsub", point_backsub, dim3(group_grid(P)), dim3(BA_THREADS), 0, st, pb,
+        const int ncb = (C + BA_THREADS - 1) / BA_THREADS;
+        if (npb + ncb > 0)
+            launch("ba.backsub_update", backsub_update, dim3(npb + ncb), dim3(BA_THREADS), 0, st, pb,
                    (const double*)d_Z.as<double>(), (const double*)d_Hpl.as<double>(), (const double*)d_Hll.as<double>(),
-                   (const double*)d_bl.as<double>(),
-                   (const double*)xp, lam, xl, d_scale.as<double>());
-        }
-        if (std::max(P, C) > 0) {
-            launch("ba.update_state", update_state, dim3(gmax), dim3(BA_THREADS), 0, st, pb, state(cur), state(1 - cur),
-                               xp, xl, d_bp.as<double>(), lam, d_scale.as<double>() + P);
-        }
-        if (P > 0) {
-            launch("ba.point_linearize", point_linearize, dim3(group_grid(P)), dim3(BA_THREADS), 0, st, pb, state(1 - cur), 0,
-                               d_err.as<double>(), d_Hll.as<double>(), d_bl.as<double>(), d_Hpl.as<double>(),
-                               d_chi.as<double>(), d_maxd.as<double>());
-        }
+                   (const double*)d_bl.as<double>(), (const double*)xp, lam, state(cur), state(1 - cur),
+                   (const double*)d_bp.as<double>(), d_scale.as<double>(), npb);
         const int nt = (int)teth.size();
         if (nt > 0)
             launch("ba.tether_eval", tether_eval, dim3((nt + 63) / 64), dim3(64), 0, st, (const Tether*)d_teth.as<Tether>(),
                    nt, state(1 - cur), 0, d_chi.as<double>() + P, d_tout.as<double>());
+        // evaluation of the trial state with the speculative post-pass (read back with this sync)
         const bool spec = speculate && E > 0;
-        if (spec) launch_outlier_pass(state(1 - cur), state(cur), 2);  // read back with this sync
+        SpecPass sp{state(cur), spec ? 1 : 0, outlier_max_err_sq, d_olist.as<uint32_t>(), E, d_osum.as<double>(), d_live()};
+        if (npb > 0)
+            launch("ba.evaluate", evaluate_kernel, dim3(npb), dim3(BA_THREADS), 0, st, pb, state(1 - cur),
+                   point_out(d_chi.as<double>()), sp);
         launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)d_chi.as<double>(), P + nt,
-               (const double*)d_scale.as<double>(), P + C, (const double*)d_maxd.as<double>(), 0, d_red.as<double>() + 3,
-               (const double*)d_osum.as<double>(), outlier_blocks(), spec ? 2 : 0, d_octl());
+               (const double*)d_scale.as<double>(), P + C, (const double*)d_maxd.as<double>(), 0, h_ctl_dev + 3,
+               (const double*)d_chi_lin.as<double>(), P + nt, h_ctl_dev + CTL_SCRATCH,
+               (const double*)d_osum.as<double>(), npb, spec ? 2 : 0, d_octl(), d_live());
         MAGE_HIP(hipGetLastError());
         mage_status r = read_ctl();
         if (r != MAGE_OK) return r;
         for (int k = 0; k < 6; k++) red[k] = h_ctl[k];
+        red[0] = h_ctl[CTL_SCRATCH];  // chi2 of the linearised (current) state
         *ok = ctl_fail() == 0;
         return MAGE_OK;
     }
@@ -1877,18 +2063,20 @@ struct BundleAdjuster {
     // OptimizationAlgorithmLevenberg::solve (g2o); result 1 = OK, 0 = Terminate
     mage_status lm_solve(int* result, bool speculate, int* spec_valid)
     {
-        mage_status r = linearize();
+        const bool init_lambda = iteration == 0 && user_lambda <= 0;
+        if (iteration == 0 && !init_lambda) {
+            lambda = user_lambda;
+            ni = 2;
+        }
+        mage_status r = linearize(init_lambda ? std::numeric_limits<double>::quiet_NaN() : lambda, init_lambda);
         if (r != MAGE_OK) return r;
         double currentChi = 0;
         bool haveChi = false;
-        if (iteration == 0 && user_lambda <= 0) {
+        if (init_lambda) {
             if ((r = read_ctl()) != MAGE_OK) return r;
             currentChi = h_ctl[0];
             haveChi = true;
             lambda = 1e-5 * h_ctl[2];  // computeLambdaInit, tau = 1e-5
-            ni = 2;
-        } else if (iteration == 0) {
-            lambda = user_lambda;
             ni = 2;
         }
         double rho = 0;
@@ -1948,15 +2136,15 @@ struct BundleAdjuster {
     }
 
     double outlier_max_err_sq = 0;
-    // outlier lists, counts and inlier (sum, count) of ns states into the control block (counts
-    // and ticket zeroed by reset_ctl_words beforehand)
+    // outlier lists and counts (live counters) and inlier (sum, count) block partials of ns states;
+    // reduce3 moves them into the control block
     int outlier_blocks() const { return (E + BA_THREADS - 1) / BA_THREADS; }
     void launch_outlier_pass(State s0, State s1, int ns)
     {
         const int ge = outlier_blocks();
         launch("ba.outlier_pass", outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), s0, s1, ns, E,
                            d_active.as<unsigned char>(), d_err.as<double>(), outlier_max_err_sq,
-                           d_olist.as<uint32_t>(), d_osum.as<double>(), d_octl());
+                           d_olist.as<uint32_t>(), d_osum.as<double>(), d_live());
     }
 
     mage_status step(const float* hw, uint32_t nsteps, float maxErrSq, uint32_t* outliers, uint32_t cap,
@@ -1990,12 +2178,11 @@ struct BundleAdjuster {
         }
         int k = spec_valid;
         if (k < 0) {
-            if ((r = reset_ctl_words()) != MAGE_OK) return r;
             launch_outlier_pass(state(cur), state(cur), 1);
             // its block partials -> ctl->osum[0] (the chi2 outputs go to a scratch slot)
             launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)nullptr, 0, (const double*)nullptr, 0,
-                   (const double*)nullptr, 0, d_red.as<double>() + CTL_SCRATCH, (const double*)d_osum.as<double>(),
-                   outlier_blocks(), 1, d_octl());
+                   (const double*)nullptr, 0, h_ctl_dev + CTL_SCRATCH, (const double*)nullptr, 0,
+                   h_ctl_dev + CTL_SCRATCH, (const double*)d_osum.as<double>(), outlier_blocks(), 1, d_octl(), d_live());
             MAGE_HIP(hipGetLastError());
             if ((r = read_ctl()) != MAGE_OK) return r;
             k = 0;
@@ -2050,7 +2237,8 @@ mage_status mage_ba_create(int32_t points_fixed, int device, mage_ba** out)
     b->points_fixed = points_fixed != 0;
     if (hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), mage::BundleAdjuster::CTL_DOUBLES * sizeof(double),
-                      hipHostMallocDefault) != hipSuccess) {
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&b->h_ctl_dev), b->h_ctl, 0) != hipSuccess) {
         b->release();
         delete b;
         mage::set_error("hipStreamCreate / hipHostMalloc failed");
