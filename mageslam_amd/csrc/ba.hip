@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -588,33 +590,50 @@ __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, in
                                                 double* __restrict__ out,
                                                 const double* __restrict__ c, int nc, double* __restrict__ outc,
                                                 const double* __restrict__ opart, int oblocks, int ns,
-                                                OutlierCtl* __restrict__ ctl, LiveCtl* __restrict__ live)
+                                                OutlierCtl* __restrict__ ctl, LiveCtl* __restrict__ live,
+                                                unsigned* __restrict__ seq_out, unsigned seq)
 {
-    __shared__ double sa[1024], sb[1024], sm[1024], sc[1024];
-    double va = 0, vb = 0, vm = 0, vc = 0;
-    for (int i = threadIdx.x; i < na; i += 1024) va += a[i];
-    for (int i = threadIdx.x; i < nb; i += 1024) vb += b[i];
-    for (int i = threadIdx.x; i < nm; i += 1024) vm = fmax(vm, m[i]);
-    for (int i = threadIdx.x; i < nc; i += 1024) vc += c[i];
-    sa[threadIdx.x] = va;
-    sb[threadIdx.x] = vb;
-    sm[threadIdx.x] = vm;
-    sc[threadIdx.x] = vc;
-    __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            sa[threadIdx.x] += sa[threadIdx.x + s];
-            sb[threadIdx.x] += sb[threadIdx.x + s];
-            sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + s]);
-            sc[threadIdx.x] += sc[threadIdx.x + s];
+    // the seven sums in one pass (strided per thread, fixed order), one reduce-scatter per wave,
+    // then the 16 wave partials in order; the max separately (only linearize_finish's callers
+    // need it, nm = 0 here in practice)
+    __shared__ double red[1024 / kWave][8];
+    __shared__ double smax[1024 / kWave];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double v[7] = {0, 0, 0, 0, 0, 0, 0};  // a, b, c, osum[0] (sum, count), osum[1] (sum, count)
+    double vm = 0;
+    for (int i = tid; i < na; i += 1024) v[0] += a[i];
+    for (int i = tid; i < nb; i += 1024) v[1] += b[i];
+    for (int i = tid; i < nc; i += 1024) v[2] += c[i];
+    for (int k = 0; k < ns; k++)
+        for (int i = tid; i < oblocks; i += 1024) {
+            v[3 + 2 * k] += opart[(2 * k) * oblocks + i];
+            v[4 + 2 * k] += opart[(2 * k + 1) * oblocks + i];
         }
-        __syncthreads();
+    for (int i = tid; i < nm; i += 1024) vm = fmax(vm, m[i]);
+    const int e = reduce_scatter<7, kWave>(v, lane);
+    if (e >= 0) red[wave][e] = v[0];
+    for (int off = 32; off > 0; off >>= 1) vm = fmax(vm, __shfl_xor(vm, off));
+    if (lane == 0) smax[wave] = vm;
+    __syncthreads();
+    if (tid < 7) {
+        double t = 0;
+        for (int w = 0; w < 1024 / kWave; w++) t += red[w][tid];
+        red[0][tid] = t;
+    } else if (tid == 7) {
+        double t = 0;
+        for (int w = 0; w < 1024 / kWave; w++) t = fmax(t, smax[w]);
+        red[0][7] = t;
     }
-    if (threadIdx.x == 0) {
-        out[0] = sa[0];
-        out[1] = sb[0];
-        out[2] = sm[0];
-        if (nc > 0) outc[0] = sc[0];
+    __syncthreads();
+    if (tid == 0) {
+        out[0] = red[0][0];
+        out[1] = red[0][1];
+        out[2] = red[0][7];
+        if (nc > 0) outc[0] = red[0][2];
+        for (int k = 0; k < ns; k++) {
+            ctl->osum[k][0] = red[0][3 + 2 * k];
+            ctl->osum[k][1] = red[0][4 + 2 * k];
+        }
         // the trial's counters to the host block, and zero for the next trial
         ctl->fail = live->fail;
         ctl->count[0] = live->count[0];
@@ -622,28 +641,9 @@ __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, in
         live->fail = 0;
         live->count[0] = 0;
         live->count[1] = 0;
-    }
-    for (int k = 0; k < ns; k++) {
-        __syncthreads();
-        double vs = 0, vc = 0;
-        for (int i = threadIdx.x; i < oblocks; i += 1024) {
-            vs += opart[(2 * k) * oblocks + i];
-            vc += opart[(2 * k + 1) * oblocks + i];
-        }
-        sa[threadIdx.x] = vs;
-        sb[threadIdx.x] = vc;
-        __syncthreads();
-        for (int s = 512; s > 0; s >>= 1) {
-            if ((int)threadIdx.x < s) {
-                sa[threadIdx.x] += sa[threadIdx.x + s];
-                sb[threadIdx.x] += sb[threadIdx.x + s];
-            }
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) {
-            ctl->osum[k][0] = sa[0];
-            ctl->osum[k][1] = sb[0];
-        }
+        // completion word for the host's spin-wait: every result above reaches host memory first
+        __threadfence_system();
+        *reinterpret_cast<volatile unsigned*>(seq_out) = seq;
     }
 }
 
@@ -1091,17 +1091,40 @@ __device__ __forceinline__ double readlane_f64(double v, int l)
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// One double through a 32-bit DPP move per half (bound_ctrl: lanes shifted in from outside the
+// row read 0).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(u & 0xFFFFFFFFull), CTRL, 0xF, 0xF, true);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// Inclusive prefix sum over the 16 lanes of a DPP row (row_shr 1, 2, 4, 8): lane 15 of the row
+// ends with the row total.
+__device__ __forceinline__ double row_sum16(double v)
+{
+    v += dpp_f64<0x111>(v);
+    v += dpp_f64<0x112>(v);
+    v += dpp_f64<0x114>(v);
+    v += dpp_f64<0x118>(v);
+    return v;
+}
+
 __device__ __forceinline__ int upper_tile_index(int i, int j, int mt) { return i * mt - i * (i - 1) / 2 + (j - i); }
 
 __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restrict__ S, int np, int n,
                                                          const double* __restrict__ b, double* __restrict__ x,
                                                          int* __restrict__ fail)
 {
-    __shared__ double invL[CT_MAXT][16][17];      // inverse of L_kk = U_kk^T per diagonal block
-    __shared__ double pan[2][CT_MAXT][16][17];    // U row-block k tiles (k, j); [.][k] = scratch
-    __shared__ double vb[CT_MAXT * 16];           // b -> y -> x
-    __shared__ double yk[2][16];                  // y_k, double-buffered (look-ahead factor)
-    __shared__ double red[CT_WAVES][16][17];      // per-wave row-reduction scratch (backward solve)
+    // inverse of L_kk = U_kk^T per diagonal block, column-major: invT[k][c][m] = inv(L_kk)[m][c]
+    // (the factor writes a column with 16-byte stores; 18-double rows keep them aligned and the
+    // MFMA / solve readers conflict-free)
+    __shared__ __attribute__((aligned(16))) double invT[CT_MAXT][16][18];
+    __shared__ double pan[2][CT_MAXT][16][17];    // U row-block k tiles (k, j)
+    __shared__ __attribute__((aligned(16))) double dsc[16][18];  // the factor's scratch: A_kk transposed
+    __shared__ __attribute__((aligned(16))) double vb[CT_MAXT * 16];  // b -> y -> x
     __shared__ int s_fail;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: tile bookkeeping on the SALU
@@ -1169,43 +1192,48 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
 #endif
     tick(0);
 
-    // --- diagonal block: Cholesky of A_kk and inv(L_kk) by its owner wave (slot `slot`), with
-    // D = pan[dbuf][k] as scratch (row-block k's panel never uses its own column k) ---
-    auto factor_diag = [&](int k, int slot, int dbuf) {
-        double(*D)[17] = pan[dbuf][k];
+    // --- diagonal block: Cholesky of A_kk and inv(L_kk) by its owner wave (slot `slot`); A_kk
+    // goes through dsc transposed, so each lane reads its row with 16-byte loads ---
+    auto factor_diag = [&](int k, int slot) {
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++)
             if (sl == slot)
 #pragma unroll
-                for (int r = 0; r < 4; r++) D[lr + 4 * r][lc] = C[sl][r];
+                for (int r = 0; r < 4; r++) dsc[lc][lr + 4 * r] = C[sl][r];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int l = lane;
-        double* y_out = yk[k & 1];
         if (MAGE_CHOL_ABLATE == 2) {
             if (l < 16)
-                for (int q = 0; q < 16; q++) invL[k][l][q] = (q == l) ? 1.0 / sqrt(D[l][l]) : 0.0;
-            if (l < 16) y_out[l] = 0;
+                for (int q = 0; q < 16; q++) invT[k][q][l] = (q == l) ? 1.0 / sqrt(dsc[l][l]) : 0.0;
+            if (l < 16) vb[16 * k + l] = 0;
         } else {
             // Right-looking Cholesky of the 16x16 block with the triangular inverse and the
             // forward substitution fused into the same column loop, one register array v[] over
             // three lane groups that all take the same update v[q] -= v[j] L[q][j]:
             //   lanes 0-15:  row l of A -> row l of L (entries above the diagonal are never read)
             //   lanes 16-31: column l-16 of I -> column l-16 of inv(L)
-            //   lane 32:     vb_k (final: every block above has updated it) -> y_k
+            //   lane 32:     vb_k (final: every block above has updated it) -> y_k, in place
             // Column j's L[q][j] are broadcast once with v_readlane (scalar registers).  Lane j's
             // own v[j] is the pivot d, so v[j] *= 1/sqrt(d) yields sqrt(d) there with no select.
             // (An LDS column broadcast instead measured 2x slower.)
             double v[16];
             const double* vbk = &vb[16 * k];
             const int c = l - 16;
-            // unconditional loads (one batch, one wait), then per-lane selects
+            // unconditional 16-byte loads (one batch, one wait), then per-lane selects
             double dq[16], bq[16];
+            {
+                const double2* dr = reinterpret_cast<const double2*>(&dsc[l & 15][0]);
+                const double2* br = reinterpret_cast<const double2*>(vbk);
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
-                dq[q] = D[q][l & 15];
-                bq[q] = vbk[q];
+                for (int q = 0; q < 8; q++) {
+                    const double2 d2 = dr[q], b2 = br[q];
+                    dq[2 * q] = d2.x;
+                    dq[2 * q + 1] = d2.y;
+                    bq[2 * q] = b2.x;
+                    bq[2 * q + 1] = b2.y;
+                }
             }
 #pragma unroll
             for (int q = 0; q < 16; q++)
@@ -1233,15 +1261,19 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             }
             if (k == 0) tick(7);
             if (l == 0 && bad) s_fail = 1;
-            if (l >= 16 && l < 32)
+            if (l >= 16 && l < 32) {
+                double2* o = reinterpret_cast<double2*>(&invT[k][c][0]);
 #pragma unroll
-                for (int m = 0; m < 16; m++) invL[k][m][c] = v[m];
-            if (l == 32)
+                for (int m = 0; m < 8; m++) o[m] = double2{v[2 * m], v[2 * m + 1]};
+            }
+            if (l == 32) {  // y_k replaces b_k in the solution vector
+                double2* o = reinterpret_cast<double2*>(&vb[16 * k]);
 #pragma unroll
-                for (int m = 0; m < 16; m++) y_out[m] = v[m];
+                for (int m = 0; m < 8; m++) o[m] = double2{v[2 * m], v[2 * m + 1]};
+            }
         }
     };
-    if (mt > 0 && wave == 0) factor_diag(0, 0, 0);  // tile (0, 0) is tile 0: wave 0, slot 0
+    if (mt > 0 && wave == 0) factor_diag(0, 0);  // tile (0, 0) is tile 0: wave 0, slot 0
     tick(1);
     __syncthreads();
     tick(2);
@@ -1261,7 +1293,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 dbl4 acc = {0, 0, 0, 0};
 #pragma unroll
                 for (int q = 0; q < 4; q++)
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(invL[k][lc][4 * q + lr], C[sl][q], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(invT[k][4 * q + lr][lc], C[sl][q], acc, 0, 0, 0);
                 C[sl] = acc;
 #pragma unroll
                 for (int r = 0; r < 4; r++) pan[buf][tj][lr + 4 * r][lc] = acc[r];
@@ -1269,13 +1301,12 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 // in this step)
                 double pacc = 0;
 #pragma unroll
-                for (int r = 0; r < 4; r++) pacc = __builtin_fma(acc[r], yk[buf][lr + 4 * r], pacc);
+                for (int r = 0; r < 4; r++) pacc = __builtin_fma(acc[r], vb[16 * k + lr + 4 * r], pacc);
                 pacc += __shfl_xor(pacc, 16);
                 pacc += __shfl_xor(pacc, 32);
                 if (lr == 0) vb[16 * tj + lc] -= pacc;
             }
         }
-        if (tid < 16) vb[16 * k + tid] = yk[buf][tid];
         tick(3);
         CT_STAMP(k, 0);
         __syncthreads();
@@ -1295,7 +1326,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             for (int sl = 0; sl < CT_TPW; sl++)
                 if (sl == slot) syrk(sl);
             tick(4);
-            factor_diag(kn, slot, buf ^ 1);
+            factor_diag(kn, slot);
             tick(1);
         }
 #pragma unroll
@@ -1319,8 +1350,14 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     auto solve_block = [&](int k) {  // by one wave: vb_k := inv(U_kk) vb_k, inv(U) = inv(L)^T
         double xv = 0;
         if (lane < 16) {
+            const double2* ir = reinterpret_cast<const double2*>(&invT[k][lane][0]);
+            const double2* vr = reinterpret_cast<const double2*>(&vb[16 * k]);
 #pragma unroll
-            for (int c = 0; c < 16; c++) xv += invL[k][c][lane] * vb[16 * k + c];
+            for (int c = 0; c < 8; c++) {
+                const double2 a = ir[c], v2 = vr[c];
+                xv += a.x * v2.x;
+                xv += a.y * v2.y;
+            }
         }
         __builtin_amdgcn_wave_barrier();
         if (lane < 16) vb[16 * k + lane] = xv;
@@ -1328,26 +1365,21 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     if (mt > 0 && wave == 0) solve_block(mt - 1);
     __syncthreads();
     for (int k = mt - 1; k >= 1; k--) {
+        // slots in reverse (row-major) order: the tile (k - 1, k) of the critical chain first
 #pragma unroll
-        for (int sl = 0; sl < CT_TPW; sl++) {
+        for (int sl = CT_TPW - 1; sl >= 0; sl--) {
             int ti, tj;
             tile_of(sl, ti, tj);
             if (tj == k && ti < k) {
-                // (U_ik x_k)[r] = sum_c U_ik[r][c] x_k[c]: products through the wave's LDS
-                // scratch, row sums by lanes 0-15
+                // (U_ik x_k)[r] = sum_c U_ik[r][c] x_k[c]: row sums over the 16 lanes of a DPP row
+                // (lane 15 of the row holds rows lr + 4r)
                 const double xk = vb[16 * k + lc];
-                double(*P)[17] = red[wave];
+                double rs[4];
 #pragma unroll
-                for (int r = 0; r < 4; r++) P[lr + 4 * r][lc] = C[sl][r] * xk;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (lane < 16) {
-                    double sum = 0;
+                for (int r = 0; r < 4; r++) rs[r] = row_sum16(C[sl][r] * xk);
+                if (lc == 15)
 #pragma unroll
-                    for (int c = 0; c < 16; c++) sum += P[lane][c];
-                    vb[16 * ti + lane] -= sum;
-                }
+                    for (int r = 0; r < 4; r++) vb[16 * ti + lr + 4 * r] -= rs[r];
                 if (ti == k - 1) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
@@ -1578,6 +1610,10 @@ struct BundleAdjuster {
     bool useless = false, state_on_device = false, host_state_stale = false, err_initialized = false;
     int iteration = 0;
     double user_lambda = 0, lambda = 0, ni = 2, huber = 0;
+    // a linearisation launched at the end of the previous step for the next one (see step())
+    bool eager = false;
+    double eager_huber = 0, eager_lambda = 0;
+    int eager_cur = -1;
     int n = 0, np = 0;  // 6 * cameras in the system, padded to a multiple of 16
     int npairs = 0, n_slots = 0, n_sblocks = 0, n_sfinish = 0;  // Schur pairs, partial slots, blocks, schur_finish pairs
     std::vector<int> camh, ptfree, cam_of_block;
@@ -1585,7 +1621,7 @@ struct BundleAdjuster {
     // Control block read back at every host decision (one pinned copy per synchronisation):
     // doubles [0,3) linearisation chi2 / max diag, [3,6) trial, then the outlier pass's
     // OutlierCtl (sums, Cholesky failure flag, counts, ticket).
-    static constexpr int CTL_DOUBLES = 16, CTL_OUTLIER = 6, CTL_SCRATCH = 12;
+    static constexpr int CTL_DOUBLES = 16, CTL_OUTLIER = 6, CTL_SCRATCH = 12, CTL_SEQ = 15;
     static_assert(CTL_OUTLIER * 8 + sizeof(OutlierCtl) <= CTL_SCRATCH * 8, "control block layout");
     // The control block is host memory the kernels write directly (pinned, coherent, mapped):
     // h_ctl on the host, h_ctl_dev in kernels; a trial's results need only the stream sync.
@@ -1598,6 +1634,25 @@ struct BundleAdjuster {
     mage_status read_ctl()
     {
         MAGE_HIP(hipStreamSynchronize(st));
+        return MAGE_OK;
+    }
+    // reduce3's completion: spin on its sequence word in the host-mapped block (a blocking
+    // stream sync costs ~10-20 us of wake-up per LM trial); after 2 ms fall back to the sync,
+    // which also reports a failed launch
+    unsigned seq_counter = 0;
+    unsigned* seq_dev() const { return reinterpret_cast<unsigned*>(h_ctl_dev + CTL_SEQ); }
+    mage_status wait_seq(unsigned seq)
+    {
+        volatile unsigned* f = reinterpret_cast<volatile unsigned*>(h_ctl + CTL_SEQ);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (*f != seq) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                MAGE_HIP(hipStreamSynchronize(st));
+                MAGE_REQUIRE(*f == seq, MAGE_EDEVICE, "BA control block not updated after the stream completed");
+                break;
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
         return MAGE_OK;
     }
     int ctl_fail() const { return h_octl().fail; }
@@ -1641,6 +1696,7 @@ struct BundleAdjuster {
 
     void release()
     {
+        if (st) (void)hipStreamSynchronize(st);  // an eager linearisation may still be running
         for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
@@ -1958,6 +2014,7 @@ struct BundleAdjuster {
         }
         iteration = 0;
         dirty = false;
+        eager = false;
         return MAGE_OK;
     }
 
@@ -2050,9 +2107,9 @@ struct BundleAdjuster {
         launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)d_chi.as<double>(), P + nt,
                (const double*)d_scale.as<double>(), P + C, (const double*)d_maxd.as<double>(), 0, h_ctl_dev + 3,
                (const double*)d_chi_lin.as<double>(), P + nt, h_ctl_dev + CTL_SCRATCH,
-               (const double*)d_osum.as<double>(), npb, spec ? 2 : 0, d_octl(), d_live());
+               (const double*)d_osum.as<double>(), npb, spec ? 2 : 0, d_octl(), d_live(), seq_dev(), ++seq_counter);
         MAGE_HIP(hipGetLastError());
-        mage_status r = read_ctl();
+        mage_status r = wait_seq(seq_counter);
         if (r != MAGE_OK) return r;
         for (int k = 0; k < 6; k++) red[k] = h_ctl[k];
         red[0] = h_ctl[CTL_SCRATCH];  // chi2 of the linearised (current) state
@@ -2068,8 +2125,11 @@ struct BundleAdjuster {
             lambda = user_lambda;
             ni = 2;
         }
-        mage_status r = linearize(init_lambda ? std::numeric_limits<double>::quiet_NaN() : lambda, init_lambda);
-        if (r != MAGE_OK) return r;
+        const bool reuse = eager && iteration > 0 && eager_huber == huber && eager_lambda == lambda && eager_cur == cur;
+        eager = false;
+        mage_status r = MAGE_OK;
+        if (!reuse && (r = linearize(init_lambda ? std::numeric_limits<double>::quiet_NaN() : lambda, init_lambda)) != MAGE_OK)
+            return r;
         double currentChi = 0;
         bool haveChi = false;
         if (init_lambda) {
@@ -2182,7 +2242,8 @@ struct BundleAdjuster {
             // its block partials -> ctl->osum[0] (the chi2 outputs go to a scratch slot)
             launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)nullptr, 0, (const double*)nullptr, 0,
                    (const double*)nullptr, 0, h_ctl_dev + CTL_SCRATCH, (const double*)nullptr, 0,
-                   h_ctl_dev + CTL_SCRATCH, (const double*)d_osum.as<double>(), outlier_blocks(), 1, d_octl(), d_live());
+                   h_ctl_dev + CTL_SCRATCH, (const double*)d_osum.as<double>(), outlier_blocks(), 1, d_octl(), d_live(),
+                   seq_dev(), ++seq_counter);
             MAGE_HIP(hipGetLastError());
             if ((r = read_ctl()) != MAGE_OK) return r;
             k = 0;
@@ -2216,6 +2277,16 @@ struct BundleAdjuster {
         }
         *nOut = std::min(no, cap);
         *meanSq = (float)(h[0] / h[1]);
+        // Eager linearisation for the caller's usual next call (BundleAdjust.cpp:311-318: the same
+        // huber width, no setter in between): it runs while control is with the caller, and
+        // lm_solve reuses it only when the huber width, lambda and state still match.
+        if (!dirty && !useless && iteration > 0) {
+            if ((r = linearize(lambda, false)) != MAGE_OK) return r;
+            eager = true;
+            eager_huber = huber;
+            eager_lambda = lambda;
+            eager_cur = cur;
+        }
         return no > cap ? MAGE_ECAPACITY : MAGE_OK;
     }
 };
@@ -2238,7 +2309,8 @@ mage_status mage_ba_create(int32_t points_fixed, int device, mage_ba** out)
     if (hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), mage::BundleAdjuster::CTL_DOUBLES * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void**>(&b->h_ctl_dev), b->h_ctl, 0) != hipSuccess) {
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&b->h_ctl_dev), b->h_ctl, 0) != hipSuccess ||
+        (std::memset(b->h_ctl, 0, mage::BundleAdjuster::CTL_DOUBLES * sizeof(double)), false)) {
         b->release();
         delete b;
         mage::set_error("hipStreamCreate / hipHostMalloc failed");
@@ -2368,6 +2440,7 @@ mage_status mage_ba_set_lambda(mage_ba* b, float lambda)
     MAGE_REQUIRE(b, MAGE_EINVAL, "null handle");
     b->iteration = 0;  // StepOptimizer::SetCurrentLambda (BundlerLib.cpp:123-130)
     b->user_lambda = (double)lambda;
+    b->eager = false;
     return MAGE_OK;
 }
 

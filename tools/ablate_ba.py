@@ -6,7 +6,8 @@
 A variant is a '+'-joined list of NAME=VALUE preprocessor definitions ("0" = the product build),
 e.g. MAGE_CHOL_ABLATE=3.  Switches in ba.hip:
 MAGE_CHOL_ABLATE (0 full, 2 trivial diagonal-block factorisation, 3 per-phase s_memtime cycles of
-wave 0 printed by the kernel, 4 per-step barrier timestamps of every wave).  The variant library is loaded by this script alone; the product
+wave 0 printed by the kernel, 4 per-step barrier timestamps of every wave; 5 the same per segment of
+chol_lead), MAGE_CHOL_LEAD (1 chol_lead, 0 chol_tiles).  The variant library is loaded by this script alone; the product
 loader is untouched.
 """
 import ctypes as C
@@ -55,7 +56,7 @@ def run():
             b.step([1.8], 7.25)
         lib.mage_profile_reset()
         lib.mage_profile_enable(1)
-        n = 1 if ("MAGE_CHOL_ABLATE=3" in v or "MAGE_CHOL_ABLATE=4" in v) else 20
+        n = 1 if any(f"MAGE_CHOL_ABLATE={i}" in v for i in (3, 4, 5)) else 20
         for _ in range(n):
             b.step([1.8], 7.25)
         lib.mage_profile_enable(0)
