@@ -21,7 +21,9 @@ run_set() {  # <out dir> <command...>
     find $OUT -name run_counter_collection.csv -exec gzip -f {} \;
 }
 OUT=gpurun_out/prof_$TAG
+ORB=gpurun_out/prof_${TAG}_orb
 ROWS=gpurun_out/prof_${TAG}_rows
+ORB_CMD="python3 bench.py --steps 10 --warmup 3 --no-ba --no-pose --no-tracking --no-cpu-baseline --pipelined-streams 0 --no-all-cores"
 if [ "$2" = collect ]; then
     python3 tools/rocprof_summary.py $OUT $TAG > /dev/null
     cp $OUT/trace/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
@@ -29,10 +31,16 @@ if [ "$2" = collect ]; then
     cp $ROWS/trace/run_kernel_stats.csv profiles/${TAG}_rows_kernel_stats.csv
     cp $ROWS/trace.json profiles/${TAG}_rows.jsonl
     cp $OUT/bench_final.json profiles/${TAG}_bench.json
-    # bench.py prices roofline.traffic on the headline run's counters
-    cp profiles/${TAG}_pmc_summary.json profiles/pmc_summary.json
+    # the headline ORB leg alone (every fast_nms launch is a 256-frame batch, so the average
+    # duration is the one bench.py prices the roofline on); its counters become
+    # profiles/pmc_summary.json, which bench.py reads for roofline.traffic
+    python3 tools/rocprof_summary.py $ORB ${TAG}_orb "${ORB_CMD#python3 }" > /dev/null
+    cp $ORB/trace/run_kernel_stats.csv profiles/${TAG}_orb_kernel_stats.csv
+    cp $ORB/trace.json profiles/${TAG}_orb_bench.json
+    cp profiles/${TAG}_orb_pmc_summary.json profiles/pmc_summary.json
     exit 0
 fi
 run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores
+run_set $ORB $ORB_CMD
 run_set $ROWS python3 tools/bench_rows.py
 timeout -k 10 400 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
