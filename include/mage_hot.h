@@ -113,6 +113,16 @@ mage_status mage_orb_detect_and_compute_batch_device(mage_orb* orb, const uint8_
 mage_status mage_orb_status(mage_orb* orb, mage_stream stream);
 mage_status mage_orb_reset_status(mage_orb* orb, mage_stream stream);
 
+/* Candidate gate of the FAST pass (no reference counterpart; a speed-only state, DESIGN.md §2
+ * ORB): each batch scores exactly only the pixels that can reach a gate G derived from the
+ * detector's previous batch and re-runs the exact path for frames whose retain bound lies below
+ * G, so outputs never depend on it.  set: the gate of the next batch on `level` (0 = none;
+ * tests and tuning).  stats: the gate the last batch used, the gate the next batch will use and
+ * how many frames of the last batch took the exact path again.  Both synchronise `stream`. */
+mage_status mage_orb_set_fast_gate(mage_orb* orb, uint32_t level, int32_t gate, mage_stream stream);
+mage_status mage_orb_fast_gate_stats(mage_orb* orb, uint32_t level, int32_t* last_gate,
+                                     int32_t* next_gate, uint32_t* last_redo, mage_stream stream);
+
 /* Benchmark/test input generator: writes frames t0..t0+count-1 of the seeded
  * panning texture sequence, each width*height bytes at d_out + i*frame_pitch.  Identical to
  * mageslam_amd/synth.py frame(). */

@@ -22,6 +22,7 @@ EXPORTS = [
     "mage_version", "mage_last_error", "mage_profile_enable", "mage_profile_reset",
     "mage_profile_report", "mage_orb_create", "mage_orb_destroy", "mage_orb_detect_and_compute",
     "mage_orb_detect_and_compute_batch_device", "mage_orb_status", "mage_orb_reset_status",
+    "mage_orb_set_fast_gate", "mage_orb_fast_gate_stats",
     "mage_synth_frames_device", "mage_synth_scene_device", "mage_orb_fast_score_map",
     "mage_undistort_keypoints", "mage_undistort_keypoints_batch_device",
     "mage_undistorter_create", "mage_undistorter_destroy", "mage_undistorter_get_maps", "mage_undistort_image",
@@ -155,6 +156,8 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_orb_detect_and_compute_batch_device", st, vp, vp, u32, i32, i32, i32, i64, vp, vp, u32, vp, vp)
     sig("mage_orb_status", st, vp, vp)
     sig("mage_orb_reset_status", st, vp, vp)
+    sig("mage_orb_set_fast_gate", st, vp, u32, i32, vp)
+    sig("mage_orb_fast_gate_stats", st, vp, u32, C.POINTER(i32), C.POINTER(i32), C.POINTER(u32), vp)
     sig("mage_synth_frames_device", st, vp, u32, i32, i32, i64, u32, u64, vp)
     f64 = C.c_double
     sig("mage_synth_scene_device", st, vp, u32, i32, i32, i64, vp, f64, f64, f64, f64, f64, f64, i64, u64, vp)

@@ -42,6 +42,7 @@ constexpr int SROWS = TH + 2;          // 32 score rows
 constexpr int LW = TW + 16;            // 136 image bytes per LDS row (34 dwords)
 constexpr int LH = TH + 8;             // 38 image rows
 constexpr int FAST_THREADS = GX * (SROWS / SR);  // 128
+constexpr int TCAP = (TW / 2) * (TH / 2);        // candidates per tile: strict 3x3 maxima are never 8-adjacent
 static_assert(SROWS % SR == 0, "strips tile the score rows");
 static_assert(TW % 8 == 0, "tile origin stays qword aligned");
 
@@ -50,7 +51,8 @@ struct FastParams {
     long long pitch;
     int threshold;
     int xlo, xhi, ylo, yhi;  // emission window (FAST range ∩ RunByImageBorder)
-    unsigned cand_cap;
+    unsigned cand_cap;  // per frame: tiles x TCAP
+    int tiles;          // tiles per frame (per-tile candidate counts)
     int dword_ok;  // frames 4-byte aligned with width, stride and pitch multiples of 4
     int qword_ok;  // frames 8-byte aligned, stride and pitch multiples of 8 (interior tiles)
     // fused 7-tap Gaussian (8U fixed point) of the tile into `blur` (null: no blur)
@@ -58,11 +60,25 @@ struct FastParams {
     int blur_stride;           // multiple of 4, >= w
     long long blur_pitch;      // bytes between blurred frames
     const uint4* blur_ops;     // per lane: the MFMA band operands of the taps (blur_operands)
+    // candidate gate (see gate_strip): the batch's gate G is *gate; the launch re-arms the next
+    // batch's gate word (*gate_next = 255, lowered by select_kernel) and the redo list (redo[0])
+    const int* gate;
+    int* gate_next;
+    uint32_t* redo;  // [count, frame...]: frames select_kernel sends back through the exact path
 };
 
 #ifndef MAGE_FAST_SCHED
 #define MAGE_FAST_SCHED 0  // 1: scheduling barriers between the ladders (register pressure experiment)
 #endif
+// Orders one wave's LDS writes before its other lanes' reads (when the waves of a workgroup
+// work on disjoint data no workgroup barrier is needed).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
 __device__ __forceinline__ uint32_t as_u32(h2 h) { return __builtin_bit_cast(uint32_t, h); }
@@ -254,6 +270,79 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
     }
 }
 
+// Candidate gate.  Only keypoints with a score of at least the retain cut survive
+// RetainBestFeatures (OpenCVModified.cpp:571-617), and the cut of a frame is never below
+// `lower` = max((int)(minNumThreshold * FeatureStrength), FastThreshold).  Given a gate G that
+// is at most the frame's `lower`, the kept set only depends on the scores >= G and on the strict
+// 3x3 maxima among them, so pixels that cannot reach G need no exact score:
+//   * score >= G needs 9 contiguous ring pixels all darker than v - G (or all brighter than
+//     v + G), and every 9-arc of the 16-ring holds at least two of the compass pixels 0, 4, 8,
+//     12; so the second largest of (v - x_c), or of (x_c - v), over the compass exceeds G;
+//   * a pixel failing that test scores < G; its stored score 0 is still below every score >= G,
+//     so the strict 3x3 maxima with scores >= G are exactly those of the full score map;
+//   * the passing 4-pixel groups are scored exactly with the threshold raised to G (scores < G
+//     become 0, so only maxima >= G are emitted).
+// select_kernel checks that G <= lower for the frame (the histogram above G is exact) and sends
+// every frame that fails the check through the exact path again (fast_redo_kernel +
+// select_redo_kernel); the output never depends on G.  G comes from the previous batch of the
+// same detector: 7/8 of the smallest `lower` over its frames (frames of a stream change slowly).
+//
+// gate_strip: the compass test of the thread's 4-px x 8-row strip; zeroes the strip's score
+// dwords and returns bit r set when some pixel of score row SR * chunk + r passes.
+__device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], int G)
+{
+    const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
+    constexpr int RP = LW / 4;
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(&img[0][0]) + gx;
+    const _Float16 g1 = (_Float16)(float)(G + 1);
+    const h2 gp1 = {g1, g1};
+    uint32_t rows = 0;
+#pragma unroll
+    for (int r = 0; r < SR; r++) {
+        const int sr = SR * chunk + r;
+        const uint32_t* rp = w32 + (sr + 3) * RP;  // LDS row of score row sr
+        const uint32_t l = rp[0], c = rp[1], n = rp[2], up = rp[1 - 3 * RP], dn = rp[1 + 3 * RP];
+        const uint32_t lf = __builtin_amdgcn_alignbyte(c, l, 1);  // x - 3
+        const uint32_t rt = __builtin_amdgcn_alignbyte(n, c, 3);  // x + 3
+        uint32_t all = 0x80008000u;
+#pragma unroll
+        for (int P = 0; P < 2; P++) {
+            const h2 v = pair_in(c, 2 * P), a = pair_in(up, 2 * P), b = pair_in(dn, 2 * P);
+            const h2 e = pair_in(lf, 2 * P), d = pair_in(rt, 2 * P);
+            const h2 pab = __builtin_elementwise_maximum(a, b), qab = __builtin_elementwise_minimum(a, b);
+            const h2 pde = __builtin_elementwise_maximum(d, e), qde = __builtin_elementwise_minimum(d, e);
+            const h2 x2l = max3h(__builtin_elementwise_minimum(pab, pde), qab, qde);  // second largest
+            const h2 x2s = min3h(__builtin_elementwise_maximum(qab, qde), pab, pde);  // second smallest
+            const h2 t = __builtin_elementwise_maximum(x2l - v, v - x2s) - gp1;      // >= 0: may reach G
+            all &= as_u32(t);
+        }
+        sc[sr][gx] = 0u;
+        if (all != 0x80008000u) rows |= 1u << r;
+    }
+    return rows;
+}
+
+// Exact scores of one 4-pixel group (score row sr, group gx) with threshold tf, as score_strip.
+__device__ __forceinline__ void score_group(const uint8_t (*img)[LW], uint32_t (*sc)[GX], const FastParams& p,
+                                            int sr, int gx, h2 tf)
+{
+    constexpr int RP = LW / 4;
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(&img[sr][0]) + gx;
+    h2 win[7][9];
+#pragma unroll
+    for (int k = 0; k < 7; k++) window_row(base[k * RP], base[k * RP + 1], base[k * RP + 2], win[k]);
+    const uint32_t s0 = score2(fast_raw2<0>(win), tf);
+    const uint32_t s1 = score2(fast_raw2<1>(win), tf);
+    uint32_t bytes = __builtin_amdgcn_perm(s1, s0, 0x06040200u);
+    const int X0 = blockIdx.x * TW - 4 + 4 * gx, Y = blockIdx.y * TH - 1 + sr;
+    uint32_t colmask = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (X0 + q >= 3 && X0 + q <= p.w - 4) colmask |= 0xFFu << (8 * q);
+    if (Y < 3 || Y > p.h - 4) bytes = 0;
+    sc[sr][gx] = bytes & colmask;
+}
+
 // Fused Gaussian 7x7 on the matrix cores (v_mfma_i32_16x16x64_i8, integer-exact).  Both separable
 // passes are GEMMs with a constant banded (Toeplitz) operand of the taps; per 16-column strip:
 //   row pass  H = I · T: A = 16 image rows x a 64-byte window (only its first 32 bytes reach the
@@ -322,15 +411,19 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], uint8_t* bt,
 #ifndef MAGE_FAST_WAVES_PER_EU
 #define MAGE_FAST_WAVES_PER_EU 5  // 86 VGPRs, no spills (tools/ablate_fast.py)
 #endif
-__global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms_kernel(const uint8_t* __restrict__ frames,
-                                                                FastParams p,
-                                                                uint32_t* __restrict__ cand,
-                                                                uint32_t* __restrict__ counts)
+// One tile of frame f: load, score (gated when G > threshold, see gate_strip), NMS, emission,
+// and the fused blur when `blur`.
+template <bool kMayGate>
+__device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, const FastParams& p, int f, int G,
+                                          bool blur, uint32_t* __restrict__ cand, uint32_t* __restrict__ counts)
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
     __shared__ uint32_t sc[SROWS][GX];  // scores; then the blurred tile
-    __shared__ uint32_t list[(TW / 2) * (TH / 2)];  // strict 3x3 maxima are never 8-adjacent
-    __shared__ uint32_t s_cnt, s_base;
+    // strict 3x3 maxima are never 8-adjacent; before the NMS: the gated pass's per-wave lists of
+    // 4-pixel groups to score (u16, <= 8 x 64 per wave)
+    __shared__ uint32_t list[TCAP];
+    static_assert(TCAP * 2 >= (FAST_THREADS / kWave) * SR * kWave, "group lists fit the list");
+    __shared__ uint32_t s_cnt;
 #ifndef MAGE_FAST_ABLATE
 #define MAGE_FAST_ABLATE 0  // tools/ablate_fast.py: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load
 #endif
@@ -338,11 +431,41 @@ __global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms
     constexpr bool kScore = !(MAGE_FAST_ABLATE & 4), kLoad = !(MAGE_FAST_ABLATE & 8);
     constexpr bool kEmit = !(MAGE_FAST_ABLATE & 16), kSink = (MAGE_FAST_ABLATE & 32) != 0;
     uint32_t s_sink_acc = 0;
-    const int f = blockIdx.z;
     if (kLoad) load_tile(frames + (long long)f * p.pitch, p, img);
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
-    if (kScore) score_strip(img, sc, p);
+    if (kScore) {
+        if (kMayGate && G > p.threshold) {
+            // gated: compass test per strip, then the wave's passing groups scored exactly,
+            // compacted over the wave's lanes
+            const uint32_t rows = gate_strip(img, sc, G);
+            const uint32_t cnt = __builtin_popcount(rows);
+            uint32_t pre = 0, total = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint64_t b = __ballot((cnt >> j) & 1u);
+                pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u)) << j;
+                total += (uint32_t)__builtin_popcountll(b) << j;
+            }
+            uint16_t* wl = reinterpret_cast<uint16_t*>(list) + (threadIdx.x / kWave) * (SR * kWave);
+            const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
+            uint32_t rb = rows;
+            while (rb) {
+                const int r = __builtin_ctz(rb);
+                rb &= rb - 1u;
+                wl[pre++] = (uint16_t)(((SR * chunk + r) << 5) | gx);
+            }
+            wave_lds_sync();
+            const _Float16 gt = (_Float16)(float)G;
+            const h2 tg = {gt, gt};
+            for (uint32_t i = __lane_id(); i < total; i += kWave) {
+                const uint32_t item = wl[i];
+                score_group(img, sc, p, (int)(item >> 5), (int)(item & 31u), tg);
+            }
+        } else {
+            score_strip(img, sc, p);
+        }
+    }
     __syncthreads();
     // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter, four
     // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8).  Scores
@@ -425,7 +548,7 @@ __global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms
         }
     }
     __syncthreads();
-    if (kBlur && p.blur) {
+    if (kBlur && blur) {
         uint32_t* bt = &sc[0][0];
         blur_mfma(img, reinterpret_cast<uint8_t*>(bt), p);
         __syncthreads();
@@ -447,13 +570,42 @@ __global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms
             s_sink_acc ^= reinterpret_cast<const uint32_t*>(&img[0][0])[threadIdx.x];
         }
         if (s_sink_acc == 0x12345678u) counts[f] = s_sink_acc;
+        __syncthreads();
     }
-    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&counts[f], s_cnt) : 0u;
-    __syncthreads();
-    uint32_t* out = cand + (long long)f * p.cand_cap;
-    for (uint32_t k = threadIdx.x; k < s_cnt; k += FAST_THREADS) {
-        const uint32_t idx = s_base + k;
-        if (idx < p.cand_cap) out[idx] = list[k];
+    // the tile's own slot of the frame's candidate buffer (TCAP entries) and count: no global
+    // atomics (the 264 tiles of a 720p frame run at once, and one counter per frame serialised
+    // them at the L2)
+    const int tix = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t n = s_cnt;
+    if (threadIdx.x == 0) counts[(long long)f * p.tiles + tix] = n;
+    uint32_t* out = cand + (long long)f * p.cand_cap + (long long)tix * TCAP;
+    for (uint32_t k = threadIdx.x; k < n; k += FAST_THREADS) out[k] = list[k];
+}
+
+__global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms_kernel(const uint8_t* __restrict__ frames,
+                                                                FastParams p,
+                                                                uint32_t* __restrict__ cand,
+                                                                uint32_t* __restrict__ counts)
+{
+    const int G = p.gate ? *p.gate : 0;
+    if (p.gate_next && (blockIdx.x | blockIdx.y | blockIdx.z | threadIdx.x) == 0) {
+        *p.gate_next = 255;  // lowered by this batch's select_kernel
+        p.redo[0] = 0;
+    }
+    fast_tile<true>(frames, p, blockIdx.z, G, p.blur != nullptr, cand, counts);
+}
+
+// The exact (ungated) pass over the frames select_kernel listed in p.redo; no blur (the gated
+// pass wrote it).  blockIdx.z strides over the list.
+__global__ __launch_bounds__(FAST_THREADS, 4) void fast_redo_kernel(const uint8_t* __restrict__ frames,
+                                                                 FastParams p,
+                                                                 uint32_t* __restrict__ cand,
+                                                                 uint32_t* __restrict__ counts)
+{
+    const uint32_t n = p.redo[0];
+    for (uint32_t z = blockIdx.z; z < n; z += gridDim.z) {
+        fast_tile<false>(frames, p, (int)p.redo[1 + z], 0, false, cand, counts);
+        __syncthreads();
     }
 }
 
@@ -486,6 +638,7 @@ constexpr int CELLMAX = 4096;  // grid cells (NumCellsX * NumCellsY)
 struct SelectParams {
     int w, h;
     unsigned cand_cap;
+    int tiles;  // FAST tiles per frame (per-tile candidate slots of TCAP entries)
     int nfeatures;
     int max_num;  // (int)(nfeatures * FeatureFactor)  (ComputeKeyPoints :723)
     unsigned out_cap;
@@ -499,6 +652,9 @@ struct SelectParams {
     float scale;     // layerScale: pt *= scale (:756-760)
     int accumulate;  // append after the n_out[f] keypoints of the previous levels (Insert)
     uint16_t* lvl;   // per keypoint (level << 8 | rotation); rotation filled by orient_kernel
+    const int* gate;  // the gate of this batch's FAST pass (FastParams::gate)
+    int* gate_next;   // atomicMin of 7/8 of each frame's `lower` (0: no retain, no gate)
+    uint32_t* redo;   // frames to run through the exact path again
 };
 
 enum : uint32_t { ST_KMAX = 1u, ST_CELLS = 2u };
@@ -509,13 +665,11 @@ __device__ __forceinline__ int cand_s(uint32_t c) { return (int)(c & 0xFFu); }
 
 static_assert(SEL_THREADS == SORT_THREADS, "select_kernel sorts with the shared LDS sort");
 
-__global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __restrict__ cand,
-                                                             const uint32_t* __restrict__ counts,
-                                                             SelectParams p,
-                                                             mage_keypoint* __restrict__ kp_out,
-                                                             uint32_t* __restrict__ xy_out,
-                                                             uint32_t* __restrict__ n_out,
-                                                             uint32_t* __restrict__ status)
+// Frame f; G is the candidate gate its FAST pass ran with (no gate when G <= fast_threshold).
+__device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __restrict__ cand,
+                                             const uint32_t* __restrict__ counts, const SelectParams& p,
+                                             mage_keypoint* __restrict__ kp_out, uint32_t* __restrict__ xy_out,
+                                             uint32_t* __restrict__ n_out, uint32_t* __restrict__ status)
 {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t items[KMAX];
@@ -525,10 +679,10 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
     __shared__ int s_cut, s_K, s_minX, s_maxX, s_minY, s_maxY, s_minS, s_gmax, s_mcd2, s_mode;
     __shared__ float s_rob, s_robInv;
 
-    const int f = blockIdx.x;
     const int tid = threadIdx.x;
+    // per-tile candidate slots (fast_tile): tile t holds CNT[t] entries at C + t * TCAP
     const uint32_t* C = cand + (long long)f * p.cand_cap;
-    const int n0 = (int)min(counts[f], p.cand_cap);
+    const uint32_t* CNT = counts + (long long)f * p.tiles;
     const int base = p.accumulate ? (int)n_out[f] : 0;  // read before any barrier; updated at the end
     for (int i = tid; i < 256; i += SEL_THREADS) hist[i] = 0;
     if (tid == 0) {
@@ -536,12 +690,46 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
         s_minX = s_minY = s_minS = 0x7FFFFFFF;
         s_maxX = s_maxY = -1;
     }
+    // tile offsets: all counts fetched at once, exclusive scan by one wave (in `sorted`, free
+    // until the cell sort); candidate i then lives in tile tile_of(i)
+    const int T = p.tiles;
+    uint32_t* tstart = sorted;
+    for (int t = tid; t < T; t += SEL_THREADS) tstart[t] = min(CNT[t], (uint32_t)TCAP);
     __syncthreads();
-    for (int i = tid; i < n0; i += SEL_THREADS) atomicAdd(&hist[cand_s(C[i])], 1u);
+    if (tid < kWave) {
+        const int per = (T + kWave) / kWave;
+        const int b0 = tid * per, b1 = min(b0 + per, T + 1);
+        uint32_t sum = 0;
+        for (int i = b0; i < b1; i++) sum += i < T ? tstart[i] : 0u;
+        uint32_t incl = sum;
+        for (int off = 1; off < kWave; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if (tid >= off) incl += o;
+        }
+        uint32_t run = incl - sum;
+        for (int i = b0; i < b1; i++) {
+            const uint32_t c = i < T ? tstart[i] : 0u;
+            tstart[i] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    const int n0 = (int)tstart[T];
+    auto cand_at = [&](int i) {  // tstart[lo] <= i < tstart[hi]
+        int lo = 0, hi = T;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if ((int)tstart[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        return C[lo * TCAP + (i - (int)tstart[lo])];
+    };
+    for (int i = tid; i < n0; i += SEL_THREADS) atomicAdd(&hist[cand_s(cand_at(i))], 1u);
     __syncthreads();
 
     const int N = p.nfeatures;
     if (tid == 0) {
+        int lower = 0;
         if (n0 <= N) {
             s_mode = 0;  // no retain / ANMS: keep all, raster order
             s_cut = 0;
@@ -557,7 +745,7 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
                     break;
                 }
             }
-            int lower = max((int)__fmul_rn((float)minNumThreshold, p.feature_strength), minThreshold);
+            lower = max((int)__fmul_rn((float)minNumThreshold, p.feature_strength), minThreshold);
             num = 0;
             int i;
             for (i = 255; i >= lower; i--) {
@@ -567,11 +755,22 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
             s_cut = i < lower ? lower : i;
             s_mode = 1;
         }
+        // gated FAST pass (gate_strip): only the candidates >= G are here, so the decision
+        // above is the reference's only when more than N of them exist and lower >= G;
+        // otherwise the frame goes through the exact path again
+        if (G > p.fast_threshold && (s_mode == 0 || lower < G)) {
+            s_mode = 2;
+            const uint32_t k = atomicAdd(&p.redo[0], 1u);
+            p.redo[1 + k] = (uint32_t)f;  // fast_redo_kernel rewrites the frame's tile slots
+        } else if (p.gate_next) {
+            atomicMin(p.gate_next, s_mode == 1 ? lower - (lower >> 3) : 0);
+        }
     }
     __syncthreads();
+    if (s_mode == 2) return;
     const int cut = s_cut;
     for (int i = tid; i < n0; i += SEL_THREADS) {
-        uint32_t c = C[i];
+        const uint32_t c = cand_at(i);
         if (cand_s(c) >= cut) {
             int pos = atomicAdd(&s_K, 1);
             if (pos < KMAX) items[pos] = c;
@@ -754,6 +953,31 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __r
     if (tid == 0) n_out[f] = (uint32_t)(base + nout);
 }
 
+__global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __restrict__ cand,
+                                                             const uint32_t* __restrict__ counts, SelectParams p,
+                                                             mage_keypoint* __restrict__ kp_out,
+                                                             uint32_t* __restrict__ xy_out,
+                                                             uint32_t* __restrict__ n_out,
+                                                             uint32_t* __restrict__ status)
+{
+    select_frame(blockIdx.x, p.gate ? *p.gate : 0, cand, counts, p, kp_out, xy_out, n_out, status);
+}
+
+// The frames of p.redo after fast_redo_kernel; blockIdx.x strides over the list.
+__global__ __launch_bounds__(SEL_THREADS) void select_redo_kernel(const uint32_t* __restrict__ cand,
+                                                                  const uint32_t* __restrict__ counts, SelectParams p,
+                                                                  mage_keypoint* __restrict__ kp_out,
+                                                                  uint32_t* __restrict__ xy_out,
+                                                                  uint32_t* __restrict__ n_out,
+                                                                  uint32_t* __restrict__ status)
+{
+    const uint32_t n = p.redo[0];
+    for (uint32_t z = blockIdx.x; z < n; z += gridDim.x) {
+        select_frame((int)p.redo[1 + z], 0, cand, counts, p, kp_out, xy_out, n_out, status);
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // 3. Blur-in-window + pre-rotated BRIEF
 // ------------------------------------------------------------------------------------------
@@ -802,15 +1026,6 @@ __device__ __forceinline__ void pattern_rotation(float angle_deg, float& a, floa
     const float ang = __fmul_rn(angle_deg, (float)(3.1415926535897932384626433832795 / 180.0f));
     a = (float)cos((double)ang);
     b = (float)sin((double)ang);
-}
-
-// Orders one wave's LDS writes before its other lanes' reads (waves of a workgroup work on
-// different keypoints, so no workgroup barrier is needed).
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // One wave per keypoint.  RB bounds the pattern radius (7: patch 15, 13: patch 31, rotation 0;
@@ -1152,6 +1367,8 @@ struct LevelGeom {
     int nfeatures = 0;
     size_t off = 0, boff = 0, coff = 0;  // pyramid / blurred / candidate offsets (per frame)
     unsigned cand_cap = 0;
+    int tiles = 0;    // FAST tiles of the level
+    size_t toff = 0;  // per-tile count offset (per frame)
     int xmax = 0, xv = 0;                 // resize tables (levels > 0)
     int area2 = 0;                        // exact 2x: INTER_AREA fast path
     size_t xofs = 0, yofs = 0, alpha = 0, beta = 0;
@@ -1160,7 +1377,7 @@ struct LevelGeom {
 struct Geometry {
     int w = -1, h = -1, L = 0;
     LevelGeom lv[MAGE_MAX_LEVELS];
-    size_t pyr_bytes = 0, blur_bytes = 0, cand_total = 0;
+    size_t pyr_bytes = 0, blur_bytes = 0, cand_total = 0, tile_total = 0;
     std::vector<int> tab_ints;
     std::vector<uint32_t> tab_words;
     bool tab_valid = false;
@@ -1174,6 +1391,11 @@ struct OrbDetector {
     bool random_pattern = false;  // PatchSize not 15 / 31: MakeRandomPattern + per-keypoint rotation
     Geometry geo;
     DeviceBuffer pattern, cand, counts, xy, status, img, kp, desc, n, blurred, pyr, rtab, lvl, blur_ops;
+    // candidate gates (gate_strip): int[2][MAGE_MAX_LEVELS], slot gate_par is read by the next
+    // batch, the other slot is re-armed and lowered by it; redo lists per level
+    DeviceBuffer gates, redo;
+    int gate_par = 0;
+    uint32_t last_batch = 0;  // redo list stride of the last batch
 };
 
 namespace {
@@ -1261,7 +1483,7 @@ void level_geometry(OrbDetector* o, int w, int h)
     const float factor = 1.0f / s.scale_factor;
     float nd = (int)s.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)g.L));
     int sum = 0;
-    size_t off = 0, boff = 0, coff = 0;
+    size_t off = 0, boff = 0, coff = 0, toff = 0;
     for (int l = 0; l < g.L; l++) {
         LevelGeom& v = g.lv[l];
         v.scale = (float)std::pow((double)s.scale_factor, (double)l);
@@ -1273,9 +1495,12 @@ void level_geometry(OrbDetector* o, int w, int h)
         if (l > 0) off += (size_t)v.pitch;
         v.boff = boff;
         boff += (size_t)v.pitch;
-        v.cand_cap = (unsigned)(((v.w + 1) / 2) * ((v.h + 1) / 2));
+        v.tiles = ((v.w + TW - 1) / TW) * ((v.h + TH - 1) / TH);
+        v.cand_cap = (unsigned)v.tiles * TCAP;
         v.coff = coff;
         coff += v.cand_cap;
+        v.toff = toff;
+        toff += v.tiles;
         if (l < g.L - 1) {
             v.nfeatures = (int)std::lrint(nd);
             sum += v.nfeatures;
@@ -1287,6 +1512,7 @@ void level_geometry(OrbDetector* o, int w, int h)
     g.pyr_bytes = off;
     g.blur_bytes = boff;
     g.cand_total = coff;
+    g.tile_total = toff;
     // resize(INTER_LINEAR) tables of levels > 0 (OpenCV 3.4.0 resize.cpp, see resize_linear_kernel)
     std::vector<int> ints;
     std::vector<uint32_t> words;
@@ -1340,15 +1566,26 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
     Geometry& g = o->geo;
     if (g.w != w || g.h != h || g.L != (int)s.nlevels) level_geometry(o, w, h);
     const int L = g.L;
+    // select_kernel's tile offsets live in its KMAX-entry LDS array (frames up to ~29 MP)
+    MAGE_REQUIRE(g.lv[0].tiles < KMAX, MAGE_EUNSUPPORTED, "frame too large for the candidate tile table");
     const bool multi = L > 1 || s.use_orientation;
     mage_status r;
     if ((r = o->cand.reserve((size_t)batch * g.cand_total * 4)) != MAGE_OK) return r;
-    if ((r = o->counts.reserve((size_t)batch * L * 4)) != MAGE_OK) return r;
+    if ((r = o->counts.reserve((size_t)batch * g.tile_total * 4)) != MAGE_OK) return r;
     if ((r = o->xy.reserve((size_t)batch * std::max(cap, 1u) * 4)) != MAGE_OK) return r;
     // the sticky status word starts at zero (a fresh allocation may hold stale bytes)
     const bool fresh_status = o->status.ptr == nullptr;
     if ((r = o->status.reserve(4)) != MAGE_OK) return r;
     if (fresh_status) MAGE_HIP(hipMemsetAsync(o->status.ptr, 0, 4, st));
+    // gates start at 0 (no gate: the first batch runs the exact path and sets the next gate)
+    const bool fresh_gates = o->gates.ptr == nullptr;
+    if ((r = o->gates.reserve(2 * MAGE_MAX_LEVELS * sizeof(int))) != MAGE_OK) return r;
+    if (fresh_gates) MAGE_HIP(hipMemsetAsync(o->gates.ptr, 0, 2 * MAGE_MAX_LEVELS * sizeof(int), st));
+    if ((r = o->redo.reserve((size_t)L * (1 + batch) * 4)) != MAGE_OK) return r;
+    o->last_batch = batch;
+    int* gate_cur = o->gates.as<int>() + o->gate_par * MAGE_MAX_LEVELS;
+    int* gate_nxt = o->gates.as<int>() + (1 - o->gate_par) * MAGE_MAX_LEVELS;
+    o->gate_par ^= 1;
     if (multi && (r = o->lvl.reserve((size_t)batch * std::max(cap, 1u) * 2)) != MAGE_OK) return r;
     if (L > 1 && (r = o->pyr.reserve((size_t)batch * g.pyr_bytes)) != MAGE_OK) return r;
     if (!g.tab_valid && L > 1) {
@@ -1358,7 +1595,6 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         MAGE_HIP(hipMemcpy(o->rtab.as<uint8_t>() + ib, g.tab_words.data(), wb, hipMemcpyHostToDevice));
         g.tab_valid = true;
     }
-    MAGE_HIP(hipMemsetAsync(o->counts.ptr, 0, (size_t)batch * L * 4, st));
 
     // level images: 0 = the caller's frames, > 0 = the pyramid buffer (batch-major per level)
     LevelImages raw{};
@@ -1424,6 +1660,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         fp.yhi = std::min(H - 4, H - border - 1);
         if (H <= 2 * border || W <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
         fp.cand_cap = v.cand_cap;
+        fp.tiles = v.tiles;
         fp.dword_ok = (fp.stride % 4 == 0) && (fp.pitch % 4 == 0) && ((uintptr_t)raw.base[l] % 4 == 0);
         fp.qword_ok = (fp.stride % 8 == 0) && (fp.pitch % 8 == 0) && ((uintptr_t)raw.base[l] % 8 == 0);
         if (fused_blur) {
@@ -1436,17 +1673,20 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             fp.blur_ops = o->blur_ops.as<uint4>();
         }
         uint32_t* cand = o->cand.as<uint32_t>() + (size_t)batch * v.coff;
-        uint32_t* counts = o->counts.as<uint32_t>() + (size_t)batch * l;
-        {
-            launch("orb.fast_nms", fast_nms_kernel, dim3((W + TW - 1) / TW, (H + TH - 1) / TH, batch), dim3(FAST_THREADS), 0,
-                               st, raw.base[l], fp, cand, counts);
-        }
+        uint32_t* counts = o->counts.as<uint32_t>() + (size_t)batch * v.toff;  // every tile writes its count
+        uint32_t* redo = o->redo.as<uint32_t>() + (size_t)l * (1 + batch);
+        fp.gate = gate_cur + l;
+        fp.gate_next = gate_nxt + l;
+        fp.redo = redo;
+        const dim3 fgrid((W + TW - 1) / TW, (H + TH - 1) / TH, batch);
+        launch("orb.fast_nms", fast_nms_kernel, fgrid, dim3(FAST_THREADS), 0, st, raw.base[l], fp, cand, counts);
         MAGE_HIP(hipGetLastError());
 
         SelectParams sp{};
         sp.w = W;
         sp.h = H;
         sp.cand_cap = v.cand_cap;
+        sp.tiles = v.tiles;
         sp.nfeatures = v.nfeatures;  // nfeaturesPerLevel[level] (:659-669)
         sp.max_num = (int)((float)v.nfeatures * s.feature_factor);
         sp.out_cap = cap;
@@ -1462,10 +1702,17 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         sp.scale = v.scale;
         sp.accumulate = l > 0;
         sp.lvl = multi ? o->lvl.as<uint16_t>() : nullptr;
-        {
-            launch("orb.select", select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, cand, counts, sp, d_kp,
-                               o->xy.as<uint32_t>(), d_n, o->status.as<uint32_t>());
-        }
+        sp.gate = gate_cur + l;
+        sp.gate_next = gate_nxt + l;
+        sp.redo = redo;
+        launch("orb.select", select_kernel, dim3(batch), dim3(SEL_THREADS), 0, st, cand, counts, sp, d_kp,
+               o->xy.as<uint32_t>(), d_n, o->status.as<uint32_t>());
+        MAGE_HIP(hipGetLastError());
+        // frames whose gate was above their retain bound: the exact path (no-ops when none)
+        launch("orb.fast_redo", fast_redo_kernel, dim3(fgrid.x, fgrid.y, std::min(batch, 8u)), dim3(FAST_THREADS), 0,
+               st, raw.base[l], fp, cand, counts);
+        launch("orb.select_redo", select_redo_kernel, dim3(std::min(batch, 256u)), dim3(SEL_THREADS), 0, st, cand,
+               counts, sp, d_kp, o->xy.as<uint32_t>(), d_n, o->status.as<uint32_t>());
         MAGE_HIP(hipGetLastError());
     }
 
@@ -1730,7 +1977,8 @@ mage_status mage_orb_destroy(mage_orb* orb)
 {
     if (!orb) return MAGE_OK;
     for (auto* b : {&orb->pattern, &orb->cand, &orb->counts, &orb->xy, &orb->status, &orb->img, &orb->kp,
-                    &orb->desc, &orb->n, &orb->blurred, &orb->pyr, &orb->rtab, &orb->lvl, &orb->blur_ops})
+                    &orb->desc, &orb->n, &orb->blurred, &orb->pyr, &orb->rtab, &orb->lvl, &orb->blur_ops,
+                    &orb->gates, &orb->redo})
         b->release();
     delete orb;
     return MAGE_OK;
@@ -1800,6 +2048,43 @@ mage_status mage_orb_reset_status(mage_orb* orb, mage_stream stream)
     mage_status r = orb->status.reserve(4);
     if (r != MAGE_OK) return r;
     MAGE_HIP(hipMemsetAsync(orb->status.ptr, 0, 4, (hipStream_t)stream));
+    return MAGE_OK;
+}
+
+mage_status mage_orb_set_fast_gate(mage_orb* orb, uint32_t level, int32_t gate, mage_stream stream)
+{
+    MAGE_REQUIRE(orb && level < MAGE_MAX_LEVELS && gate >= 0 && gate <= 255, MAGE_EINVAL, "bad arguments");
+    MAGE_HIP(hipSetDevice(orb->device));
+    const bool fresh = orb->gates.ptr == nullptr;
+    mage_status r = orb->gates.reserve(2 * MAGE_MAX_LEVELS * sizeof(int));
+    if (r != MAGE_OK) return r;
+    hipStream_t st = (hipStream_t)stream;
+    if (fresh) MAGE_HIP(hipMemsetAsync(orb->gates.ptr, 0, 2 * MAGE_MAX_LEVELS * sizeof(int), st));
+    int* slot = orb->gates.as<int>() + orb->gate_par * MAGE_MAX_LEVELS + level;
+    MAGE_HIP(hipMemcpyAsync(slot, &gate, sizeof(int), hipMemcpyHostToDevice, st));
+    MAGE_HIP(hipStreamSynchronize(st));
+    return MAGE_OK;
+}
+
+mage_status mage_orb_fast_gate_stats(mage_orb* orb, uint32_t level, int32_t* last_gate, int32_t* next_gate,
+                                     uint32_t* last_redo, mage_stream stream)
+{
+    MAGE_REQUIRE(orb && level < MAGE_MAX_LEVELS && last_gate && next_gate && last_redo, MAGE_EINVAL, "bad arguments");
+    MAGE_HIP(hipSetDevice(orb->device));
+    *last_gate = *next_gate = 0;
+    *last_redo = 0;
+    if (!orb->gates.ptr) return MAGE_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int* g = orb->gates.as<int>();
+    MAGE_HIP(hipMemcpyAsync(last_gate, g + (1 - orb->gate_par) * MAGE_MAX_LEVELS + level, sizeof(int),
+                            hipMemcpyDeviceToHost, st));
+    MAGE_HIP(hipMemcpyAsync(next_gate, g + orb->gate_par * MAGE_MAX_LEVELS + level, sizeof(int),
+                            hipMemcpyDeviceToHost, st));
+    const int L = orb->geo.L;
+    if (orb->redo.ptr && (int)level < L)
+        MAGE_HIP(hipMemcpyAsync(last_redo, orb->redo.as<uint32_t>() + (size_t)level * (1 + orb->last_batch), 4,
+                                hipMemcpyDeviceToHost, st));
+    MAGE_HIP(hipStreamSynchronize(st));
     return MAGE_OK;
 }
 

@@ -114,6 +114,19 @@ class OrbDetector:
             self._h, ptr(frames), b, width, height, stride, pitch, ptr(keypoints), ptr(descriptors),
             capacity, ptr(counts), C.c_void_p(stream) if stream else None))
 
+    def set_fast_gate(self, gate: int, level: int = 0, stream=None) -> None:
+        """Gate of the next batch's FAST pass on `level` (0: none).  Speed only: outputs are
+        identical for every gate (frames it does not fit run the exact path again)."""
+        check(_lib.load().mage_orb_set_fast_gate(self._h, level, int(gate), C.c_void_p(stream) if stream else None))
+
+    def fast_gate_stats(self, level: int = 0, stream=None) -> dict:
+        """{'last_gate', 'next_gate', 'last_redo'}: the gate the last batch ran with, the gate of
+        the next batch and the number of the last batch's frames that took the exact path."""
+        lg, ng, rd = C.c_int32(0), C.c_int32(0), C.c_uint32(0)
+        check(_lib.load().mage_orb_fast_gate_stats(self._h, level, C.byref(lg), C.byref(ng), C.byref(rd),
+                                                   C.c_void_p(stream) if stream else None))
+        return {"last_gate": lg.value, "next_gate": ng.value, "last_redo": rd.value}
+
     def device_status(self, stream=None) -> None:
         check(_lib.load().mage_orb_status(self._h, C.c_void_p(stream) if stream else None))
 

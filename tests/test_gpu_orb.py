@@ -286,3 +286,76 @@ def test_undistort_batch_device_and_process(gpu, oracle):
     assert np.array_equal(k_und, orb.UndistortKeypoints(k_plain, cd, cu))
     with pytest.raises(MageError):
         orb.UndistortKeypoints(k_plain, Calibration(500.0, 500.0, 320.0, 240.0, (C.c_float * 8)(), 3), cu)
+
+
+# ------------------------- candidate gate (speed-only state, DESIGN.md §2 ORB) -------------------------
+
+
+def _batch_vs_oracle(det, oracle, frames_np, settings, cap):
+    """Runs one device batch of `frames_np` and checks every frame against the oracle."""
+    import torch
+
+    B, h, w = frames_np.shape
+    frames = torch.from_numpy(frames_np).cuda()
+    kp = torch.zeros((B, cap * 28), dtype=torch.uint8, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    det.detect_and_compute_batch_device(frames, w, h, kp, desc, n, cap)
+    det.device_status()
+    kp_h, desc_h, n_h = kp.cpu().numpy(), desc.cpu().numpy(), n.cpu().numpy()
+    for i in range(B):
+        st, okp, od = oracle.orb_detect(frames_np[i], settings)
+        assert st == 0
+        assert n_h[i] == len(okp), i
+        assert np.array_equal(kp_h[i, : 28 * n_h[i]], kp_bytes(okp).reshape(-1)), i
+        assert np.array_equal(desc_h[i, : n_h[i]], od), i
+
+
+def test_fast_gate_from_previous_batch(gpu, oracle):
+    # batch 1 runs ungated and sets a gate; batch 2 (later frames of the stream) runs gated
+    w, h, cap = 640, 480, 2000
+    det = orb.OrbDetector(nfeatures=cap)
+    s = oracle.default_settings(cap)
+    _batch_vs_oracle(det, oracle, np.stack([synth.frame(t, w, h) for t in range(4)]), s, cap)
+    st = det.fast_gate_stats()
+    assert st["last_gate"] == 0 and st["next_gate"] > 4 and st["last_redo"] == 0
+    _batch_vs_oracle(det, oracle, np.stack([synth.frame(t, w, h) for t in range(4, 10)]), s, cap)
+    st2 = det.fast_gate_stats()
+    assert st2["last_gate"] == st["next_gate"] and st2["last_redo"] == 0
+
+
+@pytest.mark.parametrize("gate", [250, 120, 60, 5])
+def test_fast_gate_forced_mixed_frames(gpu, oracle, gate):
+    # forced gates over frames the gate does and does not fit: blank, low-texture, noise,
+    # textured; frames above their retain bound take the exact path again
+    w, h, cap = 640, 480, 1500
+    rng = np.random.default_rng(gate)
+    yy, xx = np.mgrid[0:h, 0:w]
+    frames = np.stack([synth.frame(3, w, h),
+                       np.full((h, w), 128, np.uint8),
+                       ((xx + yy) // 5 % 256).astype(np.uint8),
+                       rng.integers(0, 256, (h, w), dtype=np.uint8),
+                       np.clip(synth.frame(9, w, h).astype(int) // 8 + 100, 0, 255).astype(np.uint8),
+                       synth.frame(20, w, h)])
+    det = orb.OrbDetector(nfeatures=cap)
+    det.set_fast_gate(gate)
+    _batch_vs_oracle(det, oracle, frames, oracle.default_settings(cap), cap)
+    st = det.fast_gate_stats()
+    assert st["last_gate"] == gate
+    if gate == 250:
+        assert st["last_redo"] == len(frames)
+    if gate == 5:
+        assert st["last_redo"] >= 1  # the blank frame has no candidates above the gate
+
+
+def test_fast_gate_pyramid(gpu, oracle):
+    # per-level gates (nlevels 4, oriented rBRIEF-31) over two batches, one level forced high
+    w, h, cap = 640, 480, 2000
+    kw = dict(nlevels=4, patchSize=31, useOrientation=True)
+    det = orb.OrbDetector(nfeatures=cap, **kw)
+    s = oracle.default_settings(cap, nlevels=4, patch_size=31, use_orientation=True)
+    _batch_vs_oracle(det, oracle, np.stack([synth.frame(t, w, h) for t in range(3)]), s, cap)
+    det.set_fast_gate(200, level=2)
+    _batch_vs_oracle(det, oracle, np.stack([synth.frame(t, w, h) for t in range(3, 7)]), s, cap)
+    assert det.fast_gate_stats(level=2)["last_redo"] == 4
+    assert det.fast_gate_stats(level=0)["last_gate"] > 4

@@ -7,6 +7,7 @@ MAGE_FAST_ABLATE bits: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile loa
 emission, 32 keep the skipped stages' inputs alive.  "a:w:s" also sets __launch_bounds__ min waves per EU (w) and MAGE_FAST_SCHED (s).
 """
 import ctypes as C
+import os
 import subprocess
 import sys
 from pathlib import Path
@@ -14,6 +15,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 # variant "a" or "a:w" (ablation bits a, __launch_bounds__ min waves per EU w)
 VARIANTS = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "17", "35", "39", "47"]
+# MAGE_ABLATE_GATE=<g>: force the candidate gate of every timed batch
+GATE = int(os.environ["MAGE_ABLATE_GATE"]) if os.environ.get("MAGE_ABLATE_GATE") else None
 
 
 def build():
@@ -56,6 +59,8 @@ def run():
         L.mage_profile_reset()
         L.mage_profile_enable(1)
         for _ in range(10):
+            if GATE is not None:  # ablations without emission never set a gate themselves
+                det.set_fast_gate(GATE)
             det.detect_and_compute_batch_device(frames, W, H, kp, desc, cnt, N)
         torch.cuda.synchronize()
         rep = _lib.profile_report()
