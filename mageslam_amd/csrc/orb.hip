@@ -139,13 +139,8 @@ __host__ __device__ constexpr int ring_dy(int k)
 // B = v - max_k N9[k] with X9 / N9 the 9-arc max / min of the ring values themselves: 9-arc
 // extrema are min3/max3 of three 3-arc extrema.  Every value is an integer (offset 1024), exact
 // in f16, so the packed f16 min3/max3 give the integer result.
-template <int P>
-__device__ __forceinline__ h2 fast_raw2(const h2 (&w)[7][9])
+__device__ __forceinline__ h2 fast_raw_ring(h2 v, const h2 (&x)[16])
 {
-    const h2 v = w[3][4 + 2 * P - 1];
-    h2 x[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) x[k] = w[ring_dy(k) + 3][4 + 2 * P + ring_dx(k) - 1];
     // the two ladders one after the other (16 3-arc extrema live at a time, not 32)
     h2 t3[16];
 #pragma unroll
@@ -163,6 +158,15 @@ __device__ __forceinline__ h2 fast_raw2(const h2 (&w)[7][9])
         hi = max3h(hi, min3h(t3[k], t3[(k + 3) & 15], t3[(k + 6) & 15]), min3h(t3[k + 1], t3[(k + 4) & 15], t3[(k + 7) & 15]));
     hi = __builtin_elementwise_maximum(hi, min3h(t3[15], t3[2], t3[5]));  // -B = hi - v
     return __builtin_elementwise_maximum(v - lo, hi - v);
+}
+
+template <int P>
+__device__ __forceinline__ h2 fast_raw2(const h2 (&w)[7][9])
+{
+    h2 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = w[ring_dy(k) + 3][4 + 2 * P + ring_dx(k) - 1];
+    return fast_raw_ring(w[3][4 + 2 * P - 1], x);
 }
 
 // Score bytes of two pixels from their raw scores: raw > t ? raw - 1 : 0, as 1024 + score.
@@ -288,7 +292,7 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
 // same detector: 7/8 of the smallest `lower` over its frames (frames of a stream change slowly).
 //
 // gate_strip: the compass test of the thread's 4-px x 8-row strip; zeroes the strip's score
-// dwords and returns bit r set when some pixel of score row SR * chunk + r passes.
+// dwords and returns bit 4 r + q set when pixel q of score row SR * chunk + r passes.
 __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], int G)
 {
     const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
@@ -304,7 +308,7 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
         const uint32_t l = rp[0], c = rp[1], n = rp[2], up = rp[1 - 3 * RP], dn = rp[1 + 3 * RP];
         const uint32_t lf = __builtin_amdgcn_alignbyte(c, l, 1);  // x - 3
         const uint32_t rt = __builtin_amdgcn_alignbyte(n, c, 3);  // x + 3
-        uint32_t all = 0x80008000u;
+        uint32_t sg[2];
 #pragma unroll
         for (int P = 0; P < 2; P++) {
             const h2 v = pair_in(c, 2 * P), a = pair_in(up, 2 * P), b = pair_in(dn, 2 * P);
@@ -314,33 +318,43 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
             const h2 x2l = max3h(__builtin_elementwise_minimum(pab, pde), qab, qde);  // second largest
             const h2 x2s = min3h(__builtin_elementwise_maximum(qab, qde), pab, pde);  // second smallest
             const h2 t = __builtin_elementwise_maximum(x2l - v, v - x2s) - gp1;      // >= 0: may reach G
-            all &= as_u32(t);
+            sg[P] = as_u32(t) & 0x80008000u;
         }
         sc[sr][gx] = 0u;
-        if (all != 0x80008000u) rows |= 1u << r;
+        // sign bits of pixels 0, 1 (pair 0) and 2, 3 (pair 1) -> nibble, set = passes
+        const uint32_t neg = (sg[0] >> 15) | (sg[0] >> 30) | (sg[1] >> 13) | (sg[1] >> 28);
+        rows |= (~neg & 0xFu) << (4 * r);
     }
     return rows;
 }
 
-// Exact scores of one 4-pixel group (score row sr, group gx) with threshold tf, as score_strip.
-__device__ __forceinline__ void score_group(const uint8_t (*img)[LW], uint32_t (*sc)[GX], const FastParams& p,
-                                            int sr, int gx, h2 tf)
+// Exact scores of two listed pixels (score row << 7 | score column) at once, one per f16 lane,
+// with threshold tf; pixels outside the FAST range [3, w-4] x [3, h-4] score 0.  Returns the two
+// score bytes (a in bits 0-7, b in bits 16-23).
+__device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8_t* scb, const FastParams& p,
+                                             uint32_t ia, uint32_t ib, h2 tf)
 {
-    constexpr int RP = LW / 4;
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(&img[sr][0]) + gx;
-    h2 win[7][9];
+    // LDS centre of score pixel (sr, x): image row sr + 3, column x + 4
+    const uint8_t* ca = &img[(ia >> 7) + 3][(ia & 127u) + 4];
+    const uint8_t* cb = &img[(ib >> 7) + 3][(ib & 127u) + 4];
+    auto pack = [](uint32_t a, uint32_t b) { return as_h2((a | (b << 16)) | 0x64006400u); };
+    h2 x[16];
 #pragma unroll
-    for (int k = 0; k < 7; k++) window_row(base[k * RP], base[k * RP + 1], base[k * RP + 2], win[k]);
-    const uint32_t s0 = score2(fast_raw2<0>(win), tf);
-    const uint32_t s1 = score2(fast_raw2<1>(win), tf);
-    uint32_t bytes = __builtin_amdgcn_perm(s1, s0, 0x06040200u);
-    const int X0 = blockIdx.x * TW - 4 + 4 * gx, Y = blockIdx.y * TH - 1 + sr;
-    uint32_t colmask = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-        if (X0 + q >= 3 && X0 + q <= p.w - 4) colmask |= 0xFFu << (8 * q);
-    if (Y < 3 || Y > p.h - 4) bytes = 0;
-    sc[sr][gx] = bytes & colmask;
+    for (int k = 0; k < 16; k++) {
+        const int off = ring_dy(k) * LW + ring_dx(k);
+        x[k] = pack(ca[off], cb[off]);
+    }
+    const h2 v = pack(ca[0], cb[0]);
+    const uint32_t sv = score2(fast_raw_ring(v, x), tf);
+    const int X0 = blockIdx.x * TW - 4, Y0 = blockIdx.y * TH - 1;
+    auto inside = [&](uint32_t it) {
+        const int X = X0 + (int)(it & 127u), Y = Y0 + (int)(it >> 7);
+        return X >= 3 && X <= p.w - 4 && Y >= 3 && Y <= p.h - 4;
+    };
+    const uint32_t sa = inside(ia) ? (sv & 0xFFu) : 0u, sb = inside(ib) ? ((sv >> 16) & 0xFFu) : 0u;
+    scb[(ia >> 7) * (4 * GX) + (ia & 127u)] = (uint8_t)sa;
+    scb[(ib >> 7) * (4 * GX) + (ib & 127u)] = (uint8_t)sb;
+    return sa | (sb << 16);
 }
 
 // Fused Gaussian 7x7 on the matrix cores (v_mfma_i32_16x16x64_i8, integer-exact).  Both separable
@@ -419,48 +433,82 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
     __shared__ uint32_t sc[SROWS][GX];  // scores; then the blurred tile
-    // strict 3x3 maxima are never 8-adjacent; before the NMS: the gated pass's per-wave lists of
-    // 4-pixel groups to score (u16, <= 8 x 64 per wave)
-    __shared__ uint32_t list[TCAP];
-    static_assert(TCAP * 2 >= (FAST_THREADS / kWave) * SR * kWave, "group lists fit the list");
-    __shared__ uint32_t s_cnt;
+    __shared__ uint32_t list[TCAP];  // the tile's candidates (strict 3x3 maxima are never 8-adjacent)
+    // gated pass: per wave, the pixels (score row << 7 | score column) that may reach the gate;
+    // a wave with more than ICAP of them sends its tile through the exact strips (s_dense)
+    constexpr uint32_t ICAP = 512;
+    __shared__ uint16_t items[FAST_THREADS / kWave][ICAP];
+    __shared__ uint32_t s_cnt, s_dense;
 #ifndef MAGE_FAST_ABLATE
-#define MAGE_FAST_ABLATE 0  // tools/ablate_fast.py: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load
+#define MAGE_FAST_ABLATE 0  // tools/ablate_fast.py: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load,
+                            // 64 gated: no exact scoring of the listed groups
 #endif
     constexpr bool kBlur = !(MAGE_FAST_ABLATE & 1), kNms = !(MAGE_FAST_ABLATE & 2);
     constexpr bool kScore = !(MAGE_FAST_ABLATE & 4), kLoad = !(MAGE_FAST_ABLATE & 8);
     constexpr bool kEmit = !(MAGE_FAST_ABLATE & 16), kSink = (MAGE_FAST_ABLATE & 32) != 0;
     uint32_t s_sink_acc = 0;
     if (kLoad) load_tile(frames + (long long)f * p.pitch, p, img);
-    if (threadIdx.x == 0) s_cnt = 0;
+    if (threadIdx.x == 0) s_cnt = s_dense = 0;
     __syncthreads();
+    const bool gated = kMayGate && kScore && G > p.threshold;
+    uint32_t total = 0;  // gated: the wave's listed pixels
     if (kScore) {
-        if (kMayGate && G > p.threshold) {
+        if (gated) {
             // gated: compass test per strip, then the wave's passing groups scored exactly,
             // compacted over the wave's lanes
-            const uint32_t rows = gate_strip(img, sc, G);
-            const uint32_t cnt = __builtin_popcount(rows);
-            uint32_t pre = 0, total = 0;
+            const uint32_t pix = gate_strip(img, sc, G);
+            const uint32_t cnt = __builtin_popcount(pix);
+            uint32_t pre = 0;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < 6; j++) {
                 const uint64_t b = __ballot((cnt >> j) & 1u);
                 pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u)) << j;
                 total += (uint32_t)__builtin_popcountll(b) << j;
             }
-            uint16_t* wl = reinterpret_cast<uint16_t*>(list) + (threadIdx.x / kWave) * (SR * kWave);
-            const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
-            uint32_t rb = rows;
-            while (rb) {
-                const int r = __builtin_ctz(rb);
-                rb &= rb - 1u;
-                wl[pre++] = (uint16_t)(((SR * chunk + r) << 5) | gx);
+            if (total > ICAP) {
+                if (__lane_id() == 0) s_dense = 1u;  // this tile goes through the exact strips
+            } else {
+                uint16_t* wl = items[threadIdx.x / kWave];
+                const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
+                uint32_t rb = pix;
+                while (rb) {
+                    const int b = __builtin_ctz(rb);
+                    rb &= rb - 1u;
+                    wl[pre++] = (uint16_t)(((SR * chunk + (b >> 2)) << 7) | (4 * gx + (b & 3)));
+                }
             }
-            wave_lds_sync();
-            const _Float16 gt = (_Float16)(float)G;
-            const h2 tg = {gt, gt};
-            for (uint32_t i = __lane_id(); i < total; i += kWave) {
-                const uint32_t item = wl[i];
-                score_group(img, sc, p, (int)(item >> 5), (int)(item & 31u), tg);
+            __syncthreads();  // s_dense is final
+            if (s_dense) {
+                score_strip(img, sc, p);
+            } else if (!(MAGE_FAST_ABLATE & 64)) {
+                // the wave's listed pixels, two per lane; the ones that reach G (the only
+                // possible maxima) are compacted in place to the front of the list for the NMS
+                uint16_t* wl = items[threadIdx.x / kWave];
+                const _Float16 gt = (_Float16)(float)G;
+                const h2 tg = {gt, gt};
+                uint8_t* scb = reinterpret_cast<uint8_t*>(&sc[0][0]);
+                uint32_t nz = 0;
+                for (uint32_t i0 = 0; i0 < total; i0 += 2 * kWave) {
+                    const uint32_t i = i0 + 2 * __lane_id();
+                    uint32_t ia = 0, ib = 0;
+                    bool fa = false, fb = false;
+                    if (i < total) {
+                        ia = wl[i];
+                        ib = i + 1 < total ? wl[i + 1] : ia;
+                        const uint32_t ss = score_pixels(img, scb, p, ia, ib, tg);
+                        fa = (ss & 0xFFu) != 0;
+                        fb = i + 1 < total && (ss >> 16) != 0;
+                    }
+                    // every lane read its items before any lane writes (writes land below i0 + 128)
+                    const uint64_t ba = __ballot(fa), bb = __ballot(fb);
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(ba >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ba, 0u)) +
+                                           __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
+                    const uint32_t pa = nz + below;
+                    if (fa) wl[pa] = (uint16_t)ia;
+                    if (fb) wl[pa + (fa ? 1u : 0u)] = (uint16_t)ib;
+                    nz += (uint32_t)(__builtin_popcountll(ba) + __builtin_popcountll(bb));
+                }
+                total = nz;
             }
         } else {
             score_strip(img, sc, p);
@@ -472,7 +520,44 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
     // are split into even / odd pixels as f16 lanes (1024 + s); per score row the left / right
     // neighbour-aligned copies and the 3-wide maximum are formed once and rolled down, so a
     // pixel's 8-neighbour maximum is max(H3(up), H3(down), left, right).
-    if (kNms) {
+    if (kNms && gated && !s_dense) {
+        // gated: every score outside the listed pixels is 0, so the strict 3x3 maxima are among
+        // them; per listed output pixel (score rows 1..TH, columns 4..TW+3) the 8 neighbours
+        const uint16_t* wl = items[threadIdx.x / kWave];
+        const uint8_t* scb = reinterpret_cast<const uint8_t*>(&sc[0][0]);
+        constexpr int RB = 4 * GX;  // score row bytes
+        for (uint32_t i0 = 0; i0 < total; i0 += kWave) {
+            const uint32_t i = i0 + __lane_id();
+            bool m = false;
+            uint32_t c = 0;
+            if (i < total) {
+                const uint32_t it = wl[i];
+                const int sr = (int)(it >> 7), x = (int)(it & 127u);
+                const int X = blockIdx.x * TW + x - 4, Y = blockIdx.y * TH + sr - 1;
+                if (sr >= 1 && sr <= TH && x >= 4 && x < TW + 4 && X >= p.xlo && X <= p.xhi && Y >= p.ylo &&
+                    Y <= p.yhi) {
+                    const uint8_t* q = scb + sr * RB + x;
+                    const uint32_t v = q[0];
+                    const uint32_t nb = max(max(max(q[-RB - 1], q[-RB]), max(q[-RB + 1], q[-1])),
+                                            max(max(q[1], q[RB - 1]), max(q[RB], q[RB + 1])));
+                    m = v > nb;  // v = 0 never is: its neighbours are >= 0
+                    c = ((uint32_t)Y << 20) | ((uint32_t)X << 8) | v;
+                }
+            }
+            if (!kEmit) {
+                s_sink_acc |= c;
+                continue;
+            }
+            const uint64_t b = __ballot(m);
+            if (b) {
+                uint32_t base = 0;
+                if (__lane_id() == 0) base = atomicAdd(&s_cnt, (uint32_t)__builtin_popcountll(b));
+                base = __builtin_amdgcn_readfirstlane(base);  // all lanes active here: lane 0's value
+                const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+                if (m) list[base + pre] = c;
+            }
+        }
+    } else if (kNms) {
         constexpr int OG = TW / 4;  // 30 output groups per row
         const int og = threadIdx.x % 32, chunk = threadIdx.x / 32;
         const int X0 = blockIdx.x * TW + 4 * og;
