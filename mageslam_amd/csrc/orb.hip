@@ -750,6 +750,17 @@ __device__ __forceinline__ int cand_s(uint32_t c) { return (int)(c & 0xFFu); }
 
 static_assert(SEL_THREADS == SORT_THREADS, "select_kernel sorts with the shared LDS sort");
 
+#ifndef MAGE_SELECT_STAMPS
+#define MAGE_SELECT_STAMPS 0  // tools/select_stamps.py: per-phase s_memtime of each frame's workgroup
+#endif
+#if MAGE_SELECT_STAMPS
+__device__ unsigned long long g_sel_stamps[1024][16];
+#define SEL_STAMP(k) \
+    if (threadIdx.x == 0 && f < 1024) g_sel_stamps[f][k] = __builtin_amdgcn_s_memtime()
+#else
+#define SEL_STAMP(k)
+#endif
+
 // Frame f; G is the candidate gate its FAST pass ran with (no gate when G <= fast_threshold).
 __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __restrict__ cand,
                                              const uint32_t* __restrict__ counts, const SelectParams& p,
@@ -765,6 +776,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
     __shared__ float s_rob, s_robInv;
 
     const int tid = threadIdx.x;
+    SEL_STAMP(0);
     // per-tile candidate slots (fast_tile): tile t holds CNT[t] entries at C + t * TCAP
     const uint32_t* C = cand + (long long)f * p.cand_cap;
     const uint32_t* CNT = counts + (long long)f * p.tiles;
@@ -799,6 +811,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
         }
     }
     __syncthreads();
+    SEL_STAMP(1);
     const int n0 = (int)tstart[T];
     auto cand_at = [&](int i) {  // tstart[lo] <= i < tstart[hi]
         int lo = 0, hi = T;
@@ -811,47 +824,64 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
     };
     for (int i = tid; i < n0; i += SEL_THREADS) atomicAdd(&hist[cand_s(cand_at(i))], 1u);
     __syncthreads();
+    SEL_STAMP(2);
 
     const int N = p.nfeatures;
-    if (tid == 0) {
-        int lower = 0;
-        if (n0 <= N) {
-            s_mode = 0;  // no retain / ANMS: keep all, raster order
-            s_cut = 0;
-        } else {
-            // RetainBestFeatures (OpenCVModified.cpp:571-617)
-            int minThreshold = p.fast_threshold;
-            int minNumThreshold = minThreshold;
-            int num = 0;
-            for (int i = 255; i >= minThreshold; i--) {
-                num += (int)hist[i];
-                if (num >= N) {
-                    minNumThreshold = i;
-                    break;
-                }
-            }
-            lower = max((int)__fmul_rn((float)minNumThreshold, p.feature_strength), minThreshold);
-            num = 0;
-            int i;
-            for (i = 255; i >= lower; i--) {
-                num += (int)hist[i];
-                if (num >= p.max_num) break;
-            }
-            s_cut = i < lower ? lower : i;
-            s_mode = 1;
+    if (tid < kWave) {
+        // RetainBestFeatures (OpenCVModified.cpp:571-617) by one wave: suffix sums of the
+        // histogram (lane l holds bins 4l..4l+3), then the two downward scans as the largest bins
+        // whose suffix reaches N and max_num (the reference's loops stop at the first such bin)
+        const int minThreshold = p.fast_threshold;
+        int sfx[4];
+        int run = 0;
+#pragma unroll
+        for (int j = 3; j >= 0; j--) {
+            run += (int)hist[4 * tid + j];
+            sfx[j] = run;
         }
-        // gated FAST pass (gate_strip): only the candidates >= G are here, so the decision
-        // above is the reference's only when more than N of them exist and lower >= G;
-        // otherwise the frame goes through the exact path again
-        if (G > p.fast_threshold && (s_mode == 0 || lower < G)) {
-            s_mode = 2;
-            const uint32_t k = atomicAdd(&p.redo[0], 1u);
-            p.redo[1 + k] = (uint32_t)f;  // fast_redo_kernel rewrites the frame's tile slots
-        } else if (p.gate_next) {
-            atomicMin(p.gate_next, s_mode == 1 ? lower - (lower >> 3) : 0);
+        int above = run;  // inclusive suffix over lanes >= tid, then exclusive
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int o = __shfl_down(above, off);
+            if (tid + off < kWave) above += o;
+        }
+        above -= run;
+        int hiN = -1, hiM = -1;  // largest bin with suffix >= N / >= max_num
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (sfx[j] + above >= N) hiN = 4 * tid + j;
+            if (sfx[j] + above >= p.max_num) hiM = 4 * tid + j;
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            hiN = max(hiN, __shfl_xor(hiN, m));
+            hiM = max(hiM, __shfl_xor(hiM, m));
+        }
+        if (tid == 0) {
+            int lower = 0;
+            if (n0 <= N) {
+                s_mode = 0;  // no retain / ANMS: keep all, raster order
+                s_cut = 0;
+            } else {
+                const int minNumThreshold = hiN >= minThreshold ? hiN : minThreshold;
+                lower = max((int)__fmul_rn((float)minNumThreshold, p.feature_strength), minThreshold);
+                s_cut = max(hiM, lower);
+                s_mode = 1;
+            }
+            // gated FAST pass (gate_strip): only the candidates >= G are here, so the decision
+            // above is the reference's only when more than N of them exist and lower >= G;
+            // otherwise the frame goes through the exact path again
+            if (G > p.fast_threshold && (s_mode == 0 || lower < G)) {
+                s_mode = 2;
+                const uint32_t k = atomicAdd(&p.redo[0], 1u);
+                p.redo[1 + k] = (uint32_t)f;  // fast_redo_kernel rewrites the frame's tile slots
+            } else if (p.gate_next) {
+                atomicMin(p.gate_next, s_mode == 1 ? lower - (lower >> 3) : 0);
+            }
         }
     }
     __syncthreads();
+    SEL_STAMP(3);
     if (s_mode == 2) return;
     const int cut = s_cut;
     for (int i = tid; i < n0; i += SEL_THREADS) {
@@ -862,6 +892,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
         }
     }
     __syncthreads();
+    SEL_STAMP(4);
     int K = s_K;
     if (K > KMAX) {
         if (tid == 0) atomicOr(status, ST_KMAX);
@@ -892,16 +923,37 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
             }
             return;
         }
-        for (int i = tid; i < K; i += SEL_THREADS) {
-            uint32_t c = items[i];
-            atomicMin(&s_minX, cand_x(c));
-            atomicMax(&s_maxX, cand_x(c));
-            atomicMin(&s_minY, cand_y(c));
-            atomicMax(&s_maxY, cand_y(c));
-            atomicMin(&s_minS, cand_s(c));
+        {
+            // bounding box and weakest response: per thread, then per wave (butterfly), then one
+            // LDS atomic per wave and quantity (1024 threads on 5 words serialised the LDS)
+            int mnX = 0x7FFFFFFF, mxX = -1, mnY = 0x7FFFFFFF, mxY = -1, mnS = 0x7FFFFFFF;
+            for (int i = tid; i < K; i += SEL_THREADS) {
+                const uint32_t c = items[i];
+                mnX = min(mnX, cand_x(c));
+                mxX = max(mxX, cand_x(c));
+                mnY = min(mnY, cand_y(c));
+                mxY = max(mxY, cand_y(c));
+                mnS = min(mnS, cand_s(c));
+            }
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                mnX = min(mnX, __shfl_xor(mnX, m));
+                mxX = max(mxX, __shfl_xor(mxX, m));
+                mnY = min(mnY, __shfl_xor(mnY, m));
+                mxY = max(mxY, __shfl_xor(mxY, m));
+                mnS = min(mnS, __shfl_xor(mnS, m));
+            }
+            if ((tid & (kWave - 1)) == 0 && mxX >= 0) {
+                atomicMin(&s_minX, mnX);
+                atomicMax(&s_maxX, mxX);
+                atomicMin(&s_minY, mnY);
+                atomicMax(&s_maxY, mxY);
+                atomicMin(&s_minS, mnS);
+            }
         }
         for (int i = tid; i <= ncell; i += SEL_THREADS) cellStart[i] = 0;
         __syncthreads();
+        SEL_STAMP(5);
         const int minX = s_minX, maxX = s_maxX, minY = s_minY, maxY = s_maxY;
         if (tid == 0) {
             // robustness factor (OpenCVModified.cpp:205-214), float arithmetic as written
@@ -941,6 +993,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
             }
         }
         __syncthreads();
+        SEL_STAMP(6);
         uint32_t* fill = reinterpret_cast<uint32_t*>(keys);  // cell fill cursors (keys unused yet)
         for (int i = tid; i < ncell; i += SEL_THREADS) fill[i] = cellStart[i];
         __syncthreads();
@@ -952,15 +1005,26 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
             sorted[pos] = c;
         }
         __syncthreads();
+        SEL_STAMP(7);
         const float rob = s_rob, robInv = s_robInv;
         const int gmax = s_gmax, mcd2 = s_mcd2;
+        // Ring search (OpenCVModified.cpp:266-326).  Its result is min(gmax, d^2 to the nearest
+        // stronger item): an item in ring d is at least (d - 1) cells of side >= sqrt(mcd2) away,
+        // so the rings it stops before cannot lower minR2.  Every ring it can visit lies within
+        // D - 1 of the item's cell, D the first ring with max(0, D - 1)^2 mcd2 >= gmax; for small D
+        // the (2D - 1)^2 square is searched row by row (a row's cells are one contiguous run of
+        // the cell-sorted items) without the ring loop's per-cell bookkeeping, and items are taken
+        // in cell order so neighbouring lanes read the same runs.
+        int D = 0;
+        while (max(0, D - 1) * max(0, D - 1) * mcd2 < gmax && D < 5) D++;
+        const bool square = max(0, D - 1) * max(0, D - 1) * mcd2 >= gmax;
         unsigned long long mykeys[KMAX / SEL_THREADS];
 #pragma unroll
         for (int q = 0; q < KMAX / SEL_THREADS; q++) {
             int i = tid + q * SEL_THREADS;
             unsigned long long key = 0;
             if (i < K) {
-                uint32_t c = items[i];
+                uint32_t c = sorted[i];
                 const int x = cand_x(c), y = cand_y(c), s = cand_s(c);
                 const int cx = (x - minX) * numX / (maxX + 1 - minX);
                 const int cy = (y - minY) * numY / (maxY + 1 - minY);
@@ -968,23 +1032,37 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
                 const float sth = strength >= 0 ? __fadd_rn(__fmul_rn(strength, rob), 0.002f)
                                                  : __fadd_rn(__fmul_rn(strength, robInv), 0.002f);
                 int minR2 = gmax;
-                // ring search (OpenCVModified.cpp:266-326)
-                for (int d = 0; max(0, d - 1) * max(0, d - 1) * mcd2 < minR2; d++) {
-                    for (int yy = -d; yy <= d; yy++) {
-                        const int cYY = cy + yy;
-                        if (cYY < 0 || cYY >= numY) continue;
-                        const bool edgeRow = (yy == -d || yy == d);
-                        const int step = edgeRow ? 1 : max(2 * d, 1);
-                        for (int xx = -d; xx <= d; xx += step) {
-                            const int cXX = cx + xx;
-                            if (cXX < 0 || cXX >= numX) continue;
-                            const int cell = cYY * numX + cXX;
-                            const uint32_t e = cellStart[cell + 1];
-                            for (uint32_t qq = cellStart[cell]; qq < e; qq++) {
-                                uint32_t o = sorted[qq];
-                                if ((float)cand_s(o) > sth) {
-                                    int ddx = x - cand_x(o), ddy = y - cand_y(o);
-                                    minR2 = min(minR2, ddx * ddx + ddy * ddy);
+                if (square) {
+                    const int x0 = max(cx - (D - 1), 0), x1 = min(cx + (D - 1), numX - 1);
+                    const int y0 = max(cy - (D - 1), 0), y1 = min(cy + (D - 1), numY - 1);
+                    for (int cYY = y0; cYY <= y1; cYY++) {
+                        const uint32_t e = cellStart[cYY * numX + x1 + 1];
+                        for (uint32_t qq = cellStart[cYY * numX + x0]; qq < e; qq++) {
+                            const uint32_t o = sorted[qq];
+                            if ((float)cand_s(o) > sth) {
+                                const int ddx = x - cand_x(o), ddy = y - cand_y(o);
+                                minR2 = min(minR2, ddx * ddx + ddy * ddy);
+                            }
+                        }
+                    }
+                } else {
+                    for (int d = 0; max(0, d - 1) * max(0, d - 1) * mcd2 < minR2; d++) {
+                        for (int yy = -d; yy <= d; yy++) {
+                            const int cYY = cy + yy;
+                            if (cYY < 0 || cYY >= numY) continue;
+                            const bool edgeRow = (yy == -d || yy == d);
+                            const int step = edgeRow ? 1 : max(2 * d, 1);
+                            for (int xx = -d; xx <= d; xx += step) {
+                                const int cXX = cx + xx;
+                                if (cXX < 0 || cXX >= numX) continue;
+                                const int cell = cYY * numX + cXX;
+                                const uint32_t e = cellStart[cell + 1];
+                                for (uint32_t qq = cellStart[cell]; qq < e; qq++) {
+                                    uint32_t o = sorted[qq];
+                                    if ((float)cand_s(o) > sth) {
+                                        int ddx = x - cand_x(o), ddy = y - cand_y(o);
+                                        minR2 = min(minR2, ddx * ddx + ddy * ddy);
+                                    }
                                 }
                             }
                         }
@@ -997,6 +1075,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
             mykeys[q] = key;
         }
         __syncthreads();  // fill cursors (aliasing keys) are dead now
+        SEL_STAMP(8);
 #pragma unroll
         for (int q = 0; q < KMAX / SEL_THREADS; q++) {
             int i = tid + q * SEL_THREADS;
@@ -1004,6 +1083,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
         }
         __syncthreads();
         sort_desc(keys, P);
+        SEL_STAMP(9);
     }
 
     int nout = anms ? min(N, K) : K;
@@ -1036,6 +1116,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
         if (lv) lv[i] = (uint16_t)(p.level << 8);
     }
     if (tid == 0) n_out[f] = (uint32_t)(base + nout);
+    SEL_STAMP(10);
 }
 
 __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const uint32_t* __restrict__ cand,
@@ -2172,6 +2253,15 @@ mage_status mage_orb_fast_gate_stats(mage_orb* orb, uint32_t level, int32_t* las
     MAGE_HIP(hipStreamSynchronize(st));
     return MAGE_OK;
 }
+
+#if MAGE_SELECT_STAMPS
+// development build only (tools/select_stamps.py): the per-frame phase stamps of the last select
+mage_status mage_debug_select_stamps(unsigned long long* out)
+{
+    MAGE_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(mage::g_sel_stamps), sizeof(mage::g_sel_stamps)));
+    return MAGE_OK;
+}
+#endif
 
 mage_status mage_orb_fast_score_map(const uint8_t* img, int32_t width, int32_t height,
                                     int32_t stride, int32_t threshold, uint8_t* score_map,
