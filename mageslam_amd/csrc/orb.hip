@@ -292,40 +292,47 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
 // same detector: 7/8 of the smallest `lower` over its frames (frames of a stream change slowly).
 //
 // gate_strip: the compass test of the thread's 4-px x 8-row strip; zeroes the strip's score
-// dwords and returns bit 4 r + q set when pixel q of score row SR * chunk + r passes.
+// dwords and returns bit 8 q + r set when pixel q of score row SR * chunk + r passes.
 __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], int G)
 {
     const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
     constexpr int RP = LW / 4;
-    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(&img[0][0]) + gx;
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(&img[SR * chunk][0]) + gx;
     const _Float16 g1 = (_Float16)(float)(G + 1);
     const h2 gp1 = {g1, g1};
-    uint32_t rows = 0;
+    // the centre dwords of LDS rows SR*chunk .. +SR+5 as f16 pairs, once: a row is the centre of
+    // one score row and the up / down compass pixels of the rows 3 below / above
+    h2 cp[SR + 6][2];
+#pragma unroll
+    for (int k = 0; k < SR + 6; k++) {
+        const uint32_t c = w32[k * RP + 1];
+        cp[k][0] = pair_in(c, 0);
+        cp[k][1] = pair_in(c, 2);
+    }
+    uint32_t neg = 0;  // bit 8 q + r: pixel q of score row SR*chunk + r fails
 #pragma unroll
     for (int r = 0; r < SR; r++) {
-        const int sr = SR * chunk + r;
-        const uint32_t* rp = w32 + (sr + 3) * RP;  // LDS row of score row sr
-        const uint32_t l = rp[0], c = rp[1], n = rp[2], up = rp[1 - 3 * RP], dn = rp[1 + 3 * RP];
+        const uint32_t* rp = w32 + (r + 3) * RP;  // LDS row of score row SR*chunk + r
+        const uint32_t l = rp[0], c = rp[1], n = rp[2];
         const uint32_t lf = __builtin_amdgcn_alignbyte(c, l, 1);  // x - 3
         const uint32_t rt = __builtin_amdgcn_alignbyte(n, c, 3);  // x + 3
-        uint32_t sg[2];
+        uint32_t t2[2];
 #pragma unroll
         for (int P = 0; P < 2; P++) {
-            const h2 v = pair_in(c, 2 * P), a = pair_in(up, 2 * P), b = pair_in(dn, 2 * P);
+            const h2 v = cp[r + 3][P], a = cp[r][P], b = cp[r + 6][P];
             const h2 e = pair_in(lf, 2 * P), d = pair_in(rt, 2 * P);
             const h2 pab = __builtin_elementwise_maximum(a, b), qab = __builtin_elementwise_minimum(a, b);
             const h2 pde = __builtin_elementwise_maximum(d, e), qde = __builtin_elementwise_minimum(d, e);
             const h2 x2l = max3h(__builtin_elementwise_minimum(pab, pde), qab, qde);  // second largest
             const h2 x2s = min3h(__builtin_elementwise_maximum(qab, qde), pab, pde);  // second smallest
-            const h2 t = __builtin_elementwise_maximum(x2l - v, v - x2s) - gp1;      // >= 0: may reach G
-            sg[P] = as_u32(t) & 0x80008000u;
+            t2[P] = as_u32(__builtin_elementwise_maximum(x2l - v, v - x2s) - gp1);   // >= 0: may reach G
         }
-        sc[sr][gx] = 0u;
-        // sign bits of pixels 0, 1 (pair 0) and 2, 3 (pair 1) -> nibble, set = passes
-        const uint32_t neg = (sg[0] >> 15) | (sg[0] >> 30) | (sg[1] >> 13) | (sg[1] >> 28);
-        rows |= (~neg & 0xFu) << (4 * r);
+        sc[SR * chunk + r][gx] = 0u;
+        // the sign bytes of pixels 0..3 (bit 7 of each byte), moved to bits 8 q + r
+        const uint32_t sb = __builtin_amdgcn_perm(t2[1], t2[0], 0x07050301u);
+        neg |= (sb >> (7 - r)) & (0x01010101u << r);
     }
-    return rows;
+    return ~neg;
 }
 
 // Exact scores of two listed pixels (score row << 7 | score column) at once, one per f16 lane,
@@ -474,7 +481,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                 while (rb) {
                     const int b = __builtin_ctz(rb);
                     rb &= rb - 1u;
-                    wl[pre++] = (uint16_t)(((SR * chunk + (b >> 2)) << 7) | (4 * gx + (b & 3)));
+                    wl[pre++] = (uint16_t)(((SR * chunk + (b & 7)) << 7) | (4 * gx + (b >> 3)));
                 }
             }
             __syncthreads();  // s_dense is final
@@ -1285,7 +1292,10 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
 // Descriptors from the frame blurred by fast_nms_kernel: each wave handles KPW keypoints; it
 // issues the window loads of all of them (aligned dwords, rows kept at byte phase s) before
 // the first LDS write, so the L2 round trips overlap, then runs the 256 tests per keypoint.
-constexpr int KPW = 4;
+#ifndef MAGE_DESC_KPW
+#define MAGE_DESC_KPW 4
+#endif
+constexpr int KPW = MAGE_DESC_KPW;
 
 // MULTI = false (one level, no orientation: the default configuration): level 0 and rotation 0
 // without the per-keypoint level lookups.

@@ -4,7 +4,7 @@
   python tools/ablate_fast.py run       # time orb.fast_nms of each variant on the GPU (C2 batch)
 
 MAGE_FAST_ABLATE bits: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load, 16 NMS without
-emission, 32 keep the skipped stages' inputs alive.  "a:w:s" also sets __launch_bounds__ min waves per EU (w) and MAGE_FAST_SCHED (s).
+emission, 32 keep the skipped stages' inputs alive.  "a:w:s:k" also sets __launch_bounds__ min waves per EU (w), MAGE_FAST_SCHED (s) and MAGE_DESC_KPW (k).
 """
 import ctypes as C
 import os
@@ -28,9 +28,9 @@ def build():
         out = ROOT / "abl" / ("f" + v.replace(":", "w"))
         out.mkdir(parents=True, exist_ok=True)
         obj = out / "orb.o"
-        a, w, sch = (v.split(":") + ["", ""])[:3]
+        a, w, sch, kpw = (v.split(":") + ["", "", ""])[:4]
         subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON,
-                        f"-DMAGE_FAST_ABLATE={a}", f"-DMAGE_FAST_WAVES_PER_EU={w or 5}", f"-DMAGE_FAST_SCHED={sch or 0}",
+                        f"-DMAGE_FAST_ABLATE={a}", f"-DMAGE_FAST_WAVES_PER_EU={w or 5}", f"-DMAGE_FAST_SCHED={sch or 0}", f"-DMAGE_DESC_KPW={kpw or 4}",
                         "-c", str(B.CSRC / "orb.hip"),
                         "-o", str(obj)], check=True)
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
@@ -67,7 +67,7 @@ def run():
         L.mage_profile_enable(0)
         c, ms = rep.get("orb.fast_nms", (1, float("nan")))
         print(f"variant {v:>5}: fast_nms {ms / c:.4f} ms  select {rep.get('orb.select', (1, 0))[1] / 10:.4f} ms  "
-              f"mean keypoints {cnt.float().mean().item():.0f}", flush=True)
+              f"describe {rep.get('orb.describe', (1, 0))[1] / 10:.4f} ms  mean keypoints {cnt.float().mean().item():.0f}", flush=True)
         det.close()
 
 
