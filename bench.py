@@ -448,7 +448,7 @@ def run_tracking(args, local_rank, torch):
     hand-held 720p sequence of a textured plane, frames rendered into HBM first.  A step is the
     whole sequence: batched ORB extraction of every frame, then per frame RadiusMatch + two
     pose-only BundlerLib passes (sequential: each frame's prediction needs the previous pose)."""
-    from mageslam_amd import _lib, synth, tracking
+    from mageslam_amd import _lib, orb, synth, tracking
 
     T = args.track_frames
     seq = synth.scene_sequence(T, args.width, args.height)
@@ -463,27 +463,52 @@ def run_tracking(args, local_rank, torch):
     K = (seq.fx, seq.fy, seq.cx, seq.cy)
     p0 = tracking.Pose(seq.R[0], seq.t[0])
     be = tracking.GpuBackend(args.features, device=local_rank, batch=64)
-    feats = be.extract(frames[:8])  # warm-up
+    N = args.features
+    det = orb.OrbDetector(nfeatures=N, device=local_rank)
+    d_kp = torch.zeros((T, N * 28), dtype=torch.uint8, device=dev)
+    d_desc = torch.zeros((T, N, 32), dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(T, dtype=torch.int32, device=dev)
+
+    def extract_device(n):  # batched extraction into the device layout the device loop reads
+        for b0 in range(0, n, 64):
+            b1 = min(n, b0 + 64)
+            det.detect_and_compute_batch_device(frames[b0:b1], args.width, args.height, d_kp[b0:b1],
+                                                d_desc[b0:b1], d_n[b0:b1], N)
+
+    feats = be.extract(frames[:8])  # warm-up of both loops
     tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, device=local_rank)
+    extract_device(8)
+    tracking.track_native_device(d_kp, d_desc, N, d_n, 8, K, p0, synth.SCENE_PLANE_Z)
     torch.cuda.synchronize()
+    # the timed loop: device-resident extraction + mage_track_sequence_device (one sync)
     t0 = time.perf_counter()
-    feats = be.extract(frames)
+    extract_device(T)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    res = tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, device=local_rank)
-    torch.cuda.synchronize()
+    res = tracking.track_native_device(d_kp, d_desc, N, d_n, T, K, p0, synth.SCENE_PLANE_Z)
     t2 = time.perf_counter()
-    # the same loop driven from Python (tracking.track over GpuBackend): identical results
-    py = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
+    # the host-driven native loop over host features (mage_track_sequence): identical results
+    feats = be.extract(frames)
+    torch.cuda.synchronize()
     t3 = time.perf_counter()
-    same = py.matches == res.matches and all(np.array_equal(a.t, b.t) and np.array_equal(a.R, b.R)
-                                             for a, b in zip(py.poses, res.poses))
+    host = tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, device=local_rank)
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
+    # and the same loop driven from Python (tracking.track over GpuBackend)
+    py = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
+    t5 = time.perf_counter()
+
+    def same(a, b):
+        return a.matches == b.matches and a.inliers == b.inliers and a.keyframes == b.keyframes and all(
+            np.array_equal(x.t, y.t) and np.array_equal(x.R, y.R) for x, y in zip(a.poses, b.poses))
+
     gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)])
     return {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose)",
             "value": T / (t2 - t0), "unit": "frames/s", "frames": T, "dtype": "u8 / f64",
             "extract_ms_per_frame": 1000 * (t1 - t0) / T, "track_ms_per_frame": 1000 * (t2 - t1) / T,
-            "loop": "native (mage_track_sequence)", "python_loop_track_ms_per_frame": 1000 * (t3 - t2) / T,
-            "python_loop_identical": bool(same),
+            "loop": "device-resident (mage_track_sequence_device: per-frame decisions on the GPU, one sync)",
+            "host_loop_track_ms_per_frame": 1000 * (t4 - t3) / T, "host_loop_identical": bool(same(host, res)),
+            "python_loop_track_ms_per_frame": 1000 * (t5 - t4) / T, "python_loop_identical": bool(same(py, res)),
             "mean_matches": float(np.mean(res.matches[1:])), "mean_inliers": float(np.mean(res.inliers[1:])),
             "keyframes": len(res.keyframes), "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
             "config": {"workload": f"C4: {T}-frame {args.width}x{args.height} hand-held pan over a textured plane "

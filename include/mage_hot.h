@@ -421,6 +421,17 @@ mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_t* desc, co
                                 const mage_track_settings* settings, double* poses, uint32_t* matches,
                                 uint32_t* inliers, uint8_t* keyframe, int device);
 
+/* The same loop device-resident (csrc/track.hip): features in device memory as the batched
+ * extraction leaves them — frame f's keypoints at d_kp + f*pitch (pitch <= 4096), descriptors at
+ * d_desc + 32*f*pitch, count d_n[f]; every per-frame decision (fallback radii, lost frames,
+ * keyframes) is taken on the device, the host enqueues all frames on `stream` and synchronises
+ * once.  Outputs (host) as mage_track_sequence, identical to it. */
+mage_status mage_track_sequence_device(const mage_keypoint* d_kp, const uint8_t* d_desc, uint32_t pitch,
+                                       const uint32_t* d_n, uint32_t frames, const double K[4],
+                                       const double first_pose[12], double plane_z,
+                                       const mage_track_settings* settings, double* poses, uint32_t* matches,
+                                       uint32_t* inliers, uint8_t* keyframe, mage_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,7 +35,7 @@ EXPORTS = [
     "mage_ba_set_points", "mage_ba_set_observations", "mage_ba_set_lambda", "mage_ba_get_lambda",
     "mage_ba_set_tethers", "mage_ba_step", "mage_ba_get_poses", "mage_ba_get_points",
     "mage_ba_get_stats", "mage_ba_get_state_f64", "mage_ba_pose_batch", "mage_ba_pose_batch_device",
-    "mage_track_sequence",
+    "mage_track_sequence", "mage_track_sequence_device",
 ]
 
 
@@ -199,5 +199,6 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_ba_get_state_f64", st, vp, vp, vp)
     sig("mage_ba_get_stats", st, vp, C.POINTER(BAStats))
     sig("mage_track_sequence", st, vp, vp, vp, u32, vp, vp, C.c_double, vp, vp, vp, vp, vp, C.c_int)
+    sig("mage_track_sequence_device", st, vp, vp, u32, vp, u32, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp)
     sig("mage_ba_pose_batch", st, u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp, C.c_int)
     sig("mage_ba_pose_batch_device", st, u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp, vp)

@@ -162,6 +162,10 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
     const uint8_t* tmask = p.tmask ? p.tmask + pr * p.t_pitch : nullptr;
     const float* qpos = p.qpos ? p.qpos + 2 * pr * p.q_pitch : nullptr;
     int* res = p.res + pr * p.q_pitch;
+    if (nq == 0) {  // no queries (the tracker's skipped fallback passes): no target sort either
+        if (FUSED && tid == 0) p.n_out[pr] = 0;
+        return;
+    }
     if (ntr > RM_MAXT) {
         if (tid == 0 && blockIdx.y == 0) {
             p.n_out[pr] = 0;
@@ -277,6 +281,10 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_post_kernel(RadiusParams 
     __shared__ int s_base;
     const int pr = blockIdx.x;
     const int nq = (int)p.nq[pr], ntr = (int)p.nt[pr];
+    if (nq == 0) {
+        if (threadIdx.x == 0) p.n_out[pr] = 0;
+        return;
+    }
     if (ntr > RM_MAXT) return;
     radius_post(p, pr, p.res + pr * p.q_pitch, nq, ntr, bestD, cnt, wsum, s_base);
 }

@@ -1,0 +1,471 @@
+// track.hip — the C4 tracking loop device-resident: the same specification as csrc/track.cpp
+// (PoseEstimator::TryEstimatePoseFromKeyframe, PoseEstimator.cpp:439-607; TrackLocalMap's two
+// OptimizeCameraPose passes, TrackLocalMap.cpp:37-140; NewKeyFrameDecision.cpp:196) with every
+// per-frame decision taken on the device, so the host enqueues the whole sequence and
+// synchronises once.  Per frame, in one stream:
+//   trk_project     prediction (constant velocity on SE3, fp64) + ProjectUndistorted of the
+//                   keyframe's map points (f32), ordered compaction of the points in front
+//   radius x 3      RadiusMatch at SearchRadius / WiderSearchRadius (position overrides) /
+//                   ExtraWiderSearchRadius (keypoint positions); pass k+1 gets a zero query
+//                   count unless pass k ran and was weak (trk_weak), which the kernels skip
+//   trk_gather      the last pass's matches -> pose-BA observations, "lost" when too few
+//   pose BA 1       mage_ba_pose_batch_device (3 steps, Huber 4, 6^2)
+//   trk_filter      ordered compaction of pass 1's inliers
+//   pose BA 2       (4 steps, Huber 0.9, 4.5^2)
+//   trk_finish      the frame's pose / counts, keyframe decision, new keyframe's map points
+// Every expression matches track.cpp (same order, f32 projection, fp64 poses, no contraction:
+// the library is built with -ffp-contract=off), so the two loops give identical results.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "common.hpp"
+
+namespace mage {
+namespace {
+
+constexpr int TT = 1024;  // threads of the per-frame control kernels
+
+struct DPose {
+    double R[9];  // world -> camera, row-major
+    double t[3];
+};
+
+__device__ void d_mv(const double* R, const double* v, double* out)
+{
+    for (int i = 0; i < 3; i++) out[i] = (R[3 * i] * v[0] + R[3 * i + 1] * v[1]) + R[3 * i + 2] * v[2];
+}
+
+__device__ DPose d_inverse(const DPose& p)
+{
+    DPose q;
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) q.R[3 * r + c] = p.R[3 * c + r];
+    double m[3];
+    d_mv(q.R, p.t, m);
+    for (int i = 0; i < 3; i++) q.t[i] = -m[i];
+    return q;
+}
+
+__device__ DPose d_mul(const DPose& a, const DPose& b)
+{
+    DPose o;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            o.R[3 * i + j] = (a.R[3 * i] * b.R[j] + a.R[3 * i + 1] * b.R[3 + j]) + a.R[3 * i + 2] * b.R[6 + j];
+    double m[3];
+    d_mv(a.R, b.t, m);
+    for (int i = 0; i < 3; i++) o.t[i] = m[i] + a.t[i];
+    return o;
+}
+
+__device__ DPose load_pose(const double* p)
+{
+    DPose q;
+    for (int i = 0; i < 9; i++) q.R[i] = p[i];
+    for (int i = 0; i < 3; i++) q.t[i] = p[9 + i];
+    return q;
+}
+
+__device__ void store_pose(double* p, const DPose& q)
+{
+    for (int i = 0; i < 9; i++) p[i] = q.R[i];
+    for (int i = 0; i < 3; i++) p[9 + i] = q.t[i];
+}
+
+// Exclusive position of this thread's item among the block's items with pr set, in thread order;
+// *total = their count.  wsum: 16 words of LDS.
+__device__ uint32_t block_prefix(bool pr, uint32_t* wsum, uint32_t* total)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t b = __ballot(pr);
+    const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    if (lane == 0) wsum[wave] = (uint32_t)__builtin_popcountll(b);
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+    for (int w = 0; w < TT / 64; w++) {
+        if (w < wave) woff += wsum[w];
+        tot += wsum[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return woff + before;
+}
+
+struct Ctl {              // per-call control words (device)
+    uint32_t exec[3];     // radius pass k ran
+    uint32_t ns;          // queries (keyframe points in front of the predicted camera)
+    uint32_t lost;
+    uint32_t kf_n;        // keyframe feature count
+};
+
+struct TrackBufs {
+    Ctl* ctl;
+    double* pred;          // 12
+    // keyframe
+    mage_keypoint* kf_kp;
+    uint8_t* kf_desc;
+    float* kf_pts;
+    // queries
+    mage_keypoint* qkp;
+    uint8_t* qdesc;
+    float* qpos;
+    uint32_t* sel;
+    uint32_t* nq;          // 3: query count of each radius pass
+    mage_dmatch* m;        // 3 x cap
+    uint32_t* mn;          // 3
+    // pose BA
+    float* pos3;
+    float* r9;
+    float* intr4;
+    uint32_t* os1;         // 2
+    uint32_t* os2;         // 2
+    float* pts1;
+    float* uv1;
+    float* pts2;
+    float* uv2;
+    float* info;
+    float* pos3_o1;
+    float* r9_o1;
+    float* pos3_o2;
+    float* r9_o2;
+    uint8_t* out1;
+    uint8_t* out2;
+    float* msq;
+};
+
+struct TrackConst {
+    float fx, fy, cx, cy;  // (float)K
+    double K[4];
+    double plane_z;
+    mage_track_settings s;
+    uint32_t cap;          // keypoints per frame slot
+};
+
+// Keyframe <- frame features (kp, desc, n) with map points back-projected at pose P onto the plane.
+__device__ void make_keyframe(const TrackBufs& b, const TrackConst& c, const mage_keypoint* fk, const uint8_t* fd,
+                              uint32_t nf, const DPose& P)
+{
+    const double fx = c.K[0], fy = c.K[1], cx = c.K[2], cy = c.K[3];
+    const double* R = P.R;
+    double C[3];
+    for (int j = 0; j < 3; j++) C[j] = -((R[j] * P.t[0] + R[3 + j] * P.t[1]) + R[6 + j] * P.t[2]);
+    for (uint32_t i = threadIdx.x; i < nf; i += TT) {
+        b.kf_kp[i] = fk[i];
+        const uint4* s = reinterpret_cast<const uint4*>(fd + 32ull * i);
+        uint4* d = reinterpret_cast<uint4*>(b.kf_desc + 32ull * i);
+        d[0] = s[0];
+        d[1] = s[1];
+        const double u = ((double)fk[i].x - cx) / fx, v = ((double)fk[i].y - cy) / fy;
+        double dd[3];
+        for (int j = 0; j < 3; j++) dd[j] = (u * R[j] + v * R[3 + j]) + R[6 + j];
+        const double lam = (c.plane_z - C[2]) / dd[2];
+        for (int j = 0; j < 3; j++) b.kf_pts[3 * i + j] = (float)(C[j] + lam * dd[j]);
+    }
+}
+
+// Frame 0: its keyframe at the first pose (already in poses[0]).
+__global__ __launch_bounds__(TT) void trk_init(TrackBufs b, TrackConst c, const mage_keypoint* fk, const uint8_t* fd,
+                                               const uint32_t* nf, double* poses, uint32_t* matches,
+                                               uint32_t* inliers, uint8_t* keyframe)
+{
+    const uint32_t n = *nf;
+    make_keyframe(b, c, fk, fd, n, load_pose(poses));
+    if (threadIdx.x == 0) {
+        b.ctl->kf_n = n;
+        matches[0] = inliers[0] = n;
+        keyframe[0] = 1;
+        b.intr4[0] = c.cx;  // BundlerLib's {cx, cy, fx, fy}
+        b.intr4[1] = c.cy;
+        b.intr4[2] = c.fx;
+        b.intr4[3] = c.fy;
+    }
+}
+
+__global__ __launch_bounds__(TT) void trk_project(TrackBufs b, TrackConst c, int f, const double* poses)
+{
+    __shared__ float R32[9], t32[3];
+    __shared__ uint32_t wsum[TT / 64];
+    if (threadIdx.x == 0) {
+        const DPose p1 = load_pose(poses + 12ll * (f - 1));
+        const DPose pred = f < 2 ? p1 : d_mul(d_mul(p1, d_inverse(load_pose(poses + 12ll * (f - 2)))), p1);
+        store_pose(b.pred, pred);
+        for (int i = 0; i < 9; i++) R32[i] = (float)pred.R[i];
+        for (int i = 0; i < 3; i++) t32[i] = (float)pred.t[i];
+    }
+    __syncthreads();
+    const uint32_t nk = b.ctl->kf_n;
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < nk; c0 += TT) {
+        const uint32_t i = c0 + threadIdx.x;
+        bool front = false;
+        float u = 0.f, v = 0.f;
+        if (i < nk) {
+            const float X = b.kf_pts[3 * i], Y = b.kf_pts[3 * i + 1], Z = b.kf_pts[3 * i + 2];
+            float xc[3];
+            for (int r = 0; r < 3; r++) xc[r] = ((R32[3 * r] * X + R32[3 * r + 1] * Y) + R32[3 * r + 2] * Z) + t32[r];
+            front = xc[2] > 0.f;
+            u = c.fx * xc[0] / xc[2] + c.cx;
+            v = c.fy * xc[1] / xc[2] + c.cy;
+        }
+        uint32_t tot;
+        const uint32_t pos = base + block_prefix(front, wsum, &tot);
+        if (front) {
+            b.qkp[pos] = b.kf_kp[i];
+            const uint4* s = reinterpret_cast<const uint4*>(b.kf_desc + 32ull * i);
+            uint4* d = reinterpret_cast<uint4*>(b.qdesc + 32ull * pos);
+            d[0] = s[0];
+            d[1] = s[1];
+            b.qpos[2 * pos] = u;
+            b.qpos[2 * pos + 1] = v;
+            b.sel[pos] = i;
+        }
+        base += tot;
+    }
+    if (threadIdx.x == 0) {
+        b.ctl->ns = base;
+        b.ctl->exec[0] = 1;
+        b.ctl->exec[1] = b.ctl->exec[2] = 0;
+        b.nq[0] = base;
+        b.nq[1] = b.nq[2] = 0;
+    }
+}
+
+// Pass k + 1 runs when pass k ran and its result is weak (too few matches or ratio).
+__global__ void trk_weak(TrackBufs b, TrackConst c, int k)
+{
+    if (threadIdx.x != 0) return;
+    const uint32_t ns = b.ctl->ns, n = b.mn[k];
+    const bool weak = n < c.s.min_matches || (double)n / (double)max(ns, 1u) < c.s.small_match_ratio;
+    const uint32_t run = b.ctl->exec[k] && weak;
+    b.ctl->exec[k + 1] = run;
+    b.nq[k + 1] = run ? ns : 0u;
+}
+
+__global__ __launch_bounds__(TT) void trk_gather(TrackBufs b, TrackConst c, const mage_keypoint* fk, int f,
+                                                 uint32_t* matches)
+{
+    const int fin = b.ctl->exec[2] ? 2 : (b.ctl->exec[1] ? 1 : 0);
+    const uint32_t n = b.mn[fin];
+    const bool lost = n < c.s.min_matches;
+    const mage_dmatch* m = b.m + (size_t)fin * c.cap;
+    if (!lost) {
+        for (uint32_t k = threadIdx.x; k < n; k += TT) {
+            const uint32_t q = b.sel[m[k].query_idx], t = (uint32_t)m[k].train_idx;
+            for (int j = 0; j < 3; j++) b.pts1[3 * k + j] = b.kf_pts[3 * q + j];
+            b.uv1[2 * k] = fk[t].x;
+            b.uv1[2 * k + 1] = fk[t].y;
+            b.info[k] = c.s.refinement_info;
+        }
+    }
+    if (threadIdx.x == 0) {
+        matches[f] = n;
+        b.ctl->lost = lost;
+        b.os1[0] = 0;
+        b.os1[1] = lost ? 0u : n;
+        for (int i = 0; i < 3; i++) b.pos3[i] = (float)b.pred[9 + i];
+        for (int r = 0; r < 3; r++)
+            for (int cc = 0; cc < 3; cc++) b.r9[3 * cc + r] = (float)b.pred[3 * r + cc];  // column-major
+    }
+}
+
+__global__ __launch_bounds__(TT) void trk_filter(TrackBufs b)
+{
+    __shared__ uint32_t wsum[TT / 64];
+    const uint32_t n = b.os1[1];
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += TT) {
+        const uint32_t k = c0 + threadIdx.x;
+        const bool keep = k < n && !b.out1[k];
+        uint32_t tot;
+        const uint32_t pos = base + block_prefix(keep, wsum, &tot);
+        if (keep) {
+            for (int j = 0; j < 3; j++) b.pts2[3 * pos + j] = b.pts1[3 * k + j];
+            b.uv2[2 * pos] = b.uv1[2 * k];
+            b.uv2[2 * pos + 1] = b.uv1[2 * k + 1];
+        }
+        base += tot;
+    }
+    if (threadIdx.x == 0) {
+        b.os2[0] = 0;
+        b.os2[1] = base;
+    }
+}
+
+__global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int f, const mage_keypoint* fk,
+                                                 const uint8_t* fd, const uint32_t* nf, double* poses,
+                                                 uint32_t* inliers, uint8_t* keyframe)
+{
+    __shared__ uint32_t wsum[TT / 64];
+    __shared__ int s_kf;
+    __shared__ double sP[12];
+    const bool lost = b.ctl->lost != 0;
+    uint32_t n_in = 0;
+    if (!lost) {
+        const uint32_t n2 = b.os2[1];
+        for (uint32_t c0 = 0; c0 < n2; c0 += TT) {
+            const uint32_t k = c0 + threadIdx.x;
+            uint32_t tot;
+            (void)block_prefix(k < n2 && !b.out2[k], wsum, &tot);
+            n_in += tot;
+        }
+    }
+    if (threadIdx.x == 0) {
+        DPose P;
+        if (lost) {
+            P = load_pose(b.pred);
+        } else {
+            for (int r = 0; r < 3; r++)
+                for (int cc = 0; cc < 3; cc++) P.R[3 * r + cc] = (double)b.r9_o2[3 * cc + r];
+            for (int i = 0; i < 3; i++) P.t[i] = (double)b.pos3_o2[i];
+        }
+        store_pose(poses + 12ll * f, P);
+        store_pose(sP, P);
+        inliers[f] = n_in;
+        const uint32_t nk = b.ctl->kf_n;
+        s_kf = !lost && (double)n_in < c.s.keyframe_ratio * (double)nk + (double)c.s.keyframe_min;
+        keyframe[f] = (uint8_t)s_kf;
+    }
+    __syncthreads();
+    if (s_kf) {
+        const uint32_t n = *nf;
+        make_keyframe(b, c, fk, fd, n, load_pose(sP));
+        if (threadIdx.x == 0) b.ctl->kf_n = n;
+    }
+}
+
+}  // namespace
+}  // namespace mage
+
+extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, const uint8_t* d_desc, uint32_t pitch,
+                                                  const uint32_t* d_n, uint32_t frames, const double K[4],
+                                                  const double first_pose[12], double plane_z,
+                                                  const mage_track_settings* s, double* poses, uint32_t* matches,
+                                                  uint32_t* inliers, uint8_t* keyframe, mage_stream stream)
+{
+    using namespace mage;
+    MAGE_REQUIRE(K && first_pose && s && poses && matches && inliers && keyframe, MAGE_EINVAL, "null argument");
+    if (frames == 0) return MAGE_OK;
+    MAGE_REQUIRE(d_kp && d_desc && d_n, MAGE_EINVAL, "null features");
+    MAGE_REQUIRE(pitch > 0 && pitch <= 4096, MAGE_EINVAL, "frame pitch must be in [1, 4096] keypoints");
+    hipStream_t st = (hipStream_t)stream;
+    const size_t cap = pitch;
+    // one device allocation for the per-call scratch and outputs
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off = al(off + bytes);
+        return o;
+    };
+    const size_t o_ctl = take(sizeof(Ctl)), o_pred = take(12 * 8), o_kfkp = take(28 * cap), o_kfd = take(32 * cap),
+                 o_kfp = take(12 * cap), o_qkp = take(28 * cap), o_qd = take(32 * cap), o_qp = take(8 * cap),
+                 o_sel = take(4 * cap), o_nq = take(16), o_m = take(3 * 16 * cap), o_mn = take(16),
+                 o_rs = take(4 * cap), o_rst = take(4), o_pos = take(12), o_r9 = take(36), o_in = take(16),
+                 o_os1 = take(8), o_os2 = take(8), o_p1 = take(12 * cap), o_u1 = take(8 * cap), o_p2 = take(12 * cap),
+                 o_u2 = take(8 * cap), o_inf = take(4 * cap), o_po1 = take(12), o_ro1 = take(36), o_po2 = take(12),
+                 o_ro2 = take(36), o_out1 = take(cap), o_out2 = take(cap), o_msq = take(8),
+                 o_poses = take(96ull * frames), o_mt = take(4ull * frames), o_il = take(4ull * frames),
+                 o_kf = take(frames);
+    DeviceBuffer buf;
+    mage_status r = buf.reserve(off);
+    if (r != MAGE_OK) return r;
+    char* d = buf.as<char>();
+    TrackBufs b{};
+    b.ctl = reinterpret_cast<Ctl*>(d + o_ctl);
+    b.pred = reinterpret_cast<double*>(d + o_pred);
+    b.kf_kp = reinterpret_cast<mage_keypoint*>(d + o_kfkp);
+    b.kf_desc = reinterpret_cast<uint8_t*>(d + o_kfd);
+    b.kf_pts = reinterpret_cast<float*>(d + o_kfp);
+    b.qkp = reinterpret_cast<mage_keypoint*>(d + o_qkp);
+    b.qdesc = reinterpret_cast<uint8_t*>(d + o_qd);
+    b.qpos = reinterpret_cast<float*>(d + o_qp);
+    b.sel = reinterpret_cast<uint32_t*>(d + o_sel);
+    b.nq = reinterpret_cast<uint32_t*>(d + o_nq);
+    b.m = reinterpret_cast<mage_dmatch*>(d + o_m);
+    b.mn = reinterpret_cast<uint32_t*>(d + o_mn);
+    b.pos3 = reinterpret_cast<float*>(d + o_pos);
+    b.r9 = reinterpret_cast<float*>(d + o_r9);
+    b.intr4 = reinterpret_cast<float*>(d + o_in);
+    b.os1 = reinterpret_cast<uint32_t*>(d + o_os1);
+    b.os2 = reinterpret_cast<uint32_t*>(d + o_os2);
+    b.pts1 = reinterpret_cast<float*>(d + o_p1);
+    b.uv1 = reinterpret_cast<float*>(d + o_u1);
+    b.pts2 = reinterpret_cast<float*>(d + o_p2);
+    b.uv2 = reinterpret_cast<float*>(d + o_u2);
+    b.info = reinterpret_cast<float*>(d + o_inf);
+    b.pos3_o1 = reinterpret_cast<float*>(d + o_po1);
+    b.r9_o1 = reinterpret_cast<float*>(d + o_ro1);
+    b.pos3_o2 = reinterpret_cast<float*>(d + o_po2);
+    b.r9_o2 = reinterpret_cast<float*>(d + o_ro2);
+    b.out1 = reinterpret_cast<uint8_t*>(d + o_out1);
+    b.out2 = reinterpret_cast<uint8_t*>(d + o_out2);
+    b.msq = reinterpret_cast<float*>(d + o_msq);
+    int32_t* rscratch = reinterpret_cast<int32_t*>(d + o_rs);
+    uint32_t* rstatus = reinterpret_cast<uint32_t*>(d + o_rst);
+    double* dposes = reinterpret_cast<double*>(d + o_poses);
+    uint32_t* dmt = reinterpret_cast<uint32_t*>(d + o_mt);
+    uint32_t* dil = reinterpret_cast<uint32_t*>(d + o_il);
+    uint8_t* dkf = reinterpret_cast<uint8_t*>(d + o_kf);
+
+    TrackConst c{};
+    c.fx = (float)K[0];
+    c.fy = (float)K[1];
+    c.cx = (float)K[2];
+    c.cy = (float)K[3];
+    for (int i = 0; i < 4; i++) c.K[i] = K[i];
+    c.plane_z = plane_z;
+    c.s = *s;
+    c.cap = pitch;
+    const float e1 = (float)(s->initial_max_error * s->initial_max_error);
+    const float e2 = (float)(s->final_max_error * s->final_max_error);
+
+    auto fail = [&](mage_status st2) {
+        (void)hipStreamSynchronize(st);
+        buf.release();
+        return st2;
+    };
+    if (hipMemsetAsync(d, 0, off, st) != hipSuccess ||
+        hipMemcpyAsync(dposes, first_pose, 96, hipMemcpyHostToDevice, st) != hipSuccess)
+        return fail(MAGE_EDEVICE);
+    hipLaunchKernelGGL(trk_init, dim3(1), dim3(TT), 0, st, b, c, d_kp, d_desc, d_n, dposes, dmt, dil, dkf);
+    const float radius[3] = {s->search_radius, s->wider_search_radius, s->extra_wider_search_radius};
+    for (uint32_t f = 1; f < frames; f++) {
+        const mage_keypoint* fk = d_kp + (size_t)f * pitch;
+        const uint8_t* fd = d_desc + 32ull * f * pitch;
+        const uint32_t* nf = d_n + f;
+        launch("track.project", trk_project, dim3(1), dim3(TT), 0, st, b, c, (int)f, (const double*)dposes);
+        for (int k = 0; k < 3; k++) {
+            r = mage_radius_match_batch_device(b.qkp, k < 2 ? b.qpos : nullptr, b.qdesc, (int64_t)pitch, b.nq + k, fk,
+                                               fd, (int64_t)pitch, nf, 1, radius[k], s->max_hamming,
+                                               s->min_hamming_difference, rscratch, b.m + (size_t)k * pitch, pitch,
+                                               b.mn + k, rstatus, stream);
+            if (r != MAGE_OK) return fail(r);
+            if (k < 2) launch("track.weak", trk_weak, dim3(1), dim3(64), 0, st, b, c, k);
+        }
+        launch("track.gather", trk_gather, dim3(1), dim3(TT), 0, st, b, c, fk, (int)f, dmt);
+        r = mage_ba_pose_batch_device(1, b.pos3, b.r9, b.intr4, b.os1, b.pts1, b.uv1, b.info, s->initial_steps,
+                                      s->initial_huber, e1, b.pos3_o1, b.r9_o1, nullptr, b.out1, b.msq, nullptr,
+                                      stream);
+        if (r != MAGE_OK) return fail(r);
+        launch("track.filter", trk_filter, dim3(1), dim3(TT), 0, st, b);
+        r = mage_ba_pose_batch_device(1, b.pos3_o1, b.r9_o1, b.intr4, b.os2, b.pts2, b.uv2, b.info, s->final_steps,
+                                      s->final_huber, e2, b.pos3_o2, b.r9_o2, nullptr, b.out2, b.msq + 1, nullptr,
+                                      stream);
+        if (r != MAGE_OK) return fail(r);
+        launch("track.finish", trk_finish, dim3(1), dim3(TT), 0, st, b, c, (int)f, fk, fd, nf, dposes, dil, dkf);
+    }
+    if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
+    uint32_t rst = 0;
+    if (hipMemcpyAsync(poses, dposes, 96ull * frames, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(matches, dmt, 4ull * frames, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(inliers, dil, 4ull * frames, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(keyframe, dkf, frames, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&rst, rstatus, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return fail(MAGE_EDEVICE);
+    buf.release();
+    MAGE_REQUIRE(!(rst & 1u), MAGE_ECAPACITY, "a frame has more than 4096 keypoints");
+    return MAGE_OK;
+}

@@ -268,10 +268,7 @@ def track_native(features, K, first_pose: Pose, plane_z: float, settings: Tracke
     kp = np.ascontiguousarray(np.concatenate([k for k, _ in features]) if T else np.zeros(0, KP_DTYPE), KP_DTYPE)
     desc = np.ascontiguousarray(np.concatenate([d for _, d in features]).reshape(-1, 32) if T else
                                 np.zeros((0, 32), np.uint8), np.uint8)
-    cs = _lib.TrackSettingsC(s.search_radius, s.wider_search_radius, s.extra_wider_search_radius,
-                             s.small_match_ratio, s.min_matches, s.max_hamming, s.min_hamming_difference,
-                             s.initial_ba[0], s.initial_ba[1], s.initial_ba[2], s.final_ba[0], s.final_ba[1],
-                             s.final_ba[2], s.refinement_info, s.keyframe_ratio, s.keyframe_min)
+    cs = _settings_c(s)
     Kd = np.array(K, np.float64)
     p0 = np.concatenate([np.asarray(first_pose.R, np.float64).reshape(9), np.asarray(first_pose.t, np.float64)])
     poses = np.zeros((max(T, 1), 12))
@@ -290,6 +287,65 @@ def track_native(features, K, first_pose: Pose, plane_z: float, settings: Tracke
     res.inliers = [int(x) for x in inliers[:T]]
     res.keyframes = [int(f) for f in np.nonzero(kf[:T])[0]]
     return res
+
+
+def _settings_c(s: TrackerSettings):
+    from . import _lib
+
+    return _lib.TrackSettingsC(s.search_radius, s.wider_search_radius, s.extra_wider_search_radius,
+                               s.small_match_ratio, s.min_matches, s.max_hamming, s.min_hamming_difference,
+                               s.initial_ba[0], s.initial_ba[1], s.initial_ba[2], s.final_ba[0], s.final_ba[1],
+                               s.final_ba[2], s.refinement_info, s.keyframe_ratio, s.keyframe_min)
+
+
+def track_native_device(d_kp, d_desc, pitch: int, d_counts, frames: int, K, first_pose: Pose, plane_z: float,
+                        settings: TrackerSettings | None = None, stream=None) -> TrackResult:
+    """The same loop device-resident (mage_track_sequence_device, csrc/track.hip): features stay
+    in device memory as the batched extraction leaves them (torch tensors: keypoints frame-major
+    with `pitch` slots per frame, 32-byte descriptors, uint32 counts); the host enqueues every
+    frame and synchronises once."""
+    import ctypes as C
+
+    from . import _lib
+
+    s = settings or TrackerSettings()
+    cs = _settings_c(s)
+    Kd = np.array(K, np.float64)
+    p0 = np.concatenate([np.asarray(first_pose.R, np.float64).reshape(9), np.asarray(first_pose.t, np.float64)])
+    T = int(frames)
+    poses = np.zeros((max(T, 1), 12))
+    matches = np.zeros(max(T, 1), np.uint32)
+    inliers = np.zeros(max(T, 1), np.uint32)
+    kf = np.zeros(max(T, 1), np.uint8)
+    _lib.check(_lib.load().mage_track_sequence_device(
+        _lib.ptr(d_kp), _lib.ptr(d_desc), int(pitch), _lib.ptr(d_counts), T, _lib.ptr(Kd), _lib.ptr(p0),
+        float(plane_z), C.byref(cs), _lib.ptr(poses), _lib.ptr(matches), _lib.ptr(inliers), _lib.ptr(kf),
+        C.c_void_p(stream) if stream else None))
+    res = TrackResult()
+    for f in range(T):
+        res.poses.append(Pose(poses[f, :9].reshape(3, 3).copy(), poses[f, 9:].copy()))
+    res.matches = [int(x) for x in matches[:T]]
+    res.inliers = [int(x) for x in inliers[:T]]
+    res.keyframes = [int(f) for f in np.nonzero(kf[:T])[0]]
+    return res
+
+
+def features_to_device(features, pitch: int | None = None):
+    """Host per-frame (keypoints, descriptors) -> (d_kp, d_desc, pitch, d_counts) torch tensors in
+    the batched extraction's layout (tests)."""
+    import torch
+
+    T = len(features)
+    pitch = int(pitch or max([len(k) for k, _ in features] + [1]))
+    kp = np.zeros((T, pitch), KP_DTYPE)
+    desc = np.zeros((T, pitch, 32), np.uint8)
+    counts = np.zeros(T, np.uint32)
+    for f, (k, d) in enumerate(features):
+        kp[f, :len(k)] = k
+        desc[f, :len(k)] = np.asarray(d).reshape(-1, 32)
+        counts[f] = len(k)
+    return (torch.from_numpy(kp.view(np.uint8).reshape(T, -1)).cuda(), torch.from_numpy(desc).cuda(), pitch,
+            torch.from_numpy(counts.view(np.int32)).cuda())
 
 
 def pose_rmse(a: TrackResult, b: TrackResult) -> tuple[float, float]:

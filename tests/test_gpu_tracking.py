@@ -79,3 +79,41 @@ def test_native_tracking_errors(gpu):
         from mageslam_amd import _lib
 
         _lib.check(_lib.load().mage_track_sequence(None, None, None, 3, None, None, 5.0, None, None, None, None, None, 0))
+
+
+def _same(a, b):
+    assert a.matches == b.matches and a.inliers == b.inliers and a.keyframes == b.keyframes
+    assert all(np.array_equal(x.R, y.R) and np.array_equal(x.t, y.t) for x, y in zip(a.poses, b.poses))
+
+
+def test_device_tracking_loop_equals_native(gpu):
+    """mage_track_sequence_device (every per-frame decision on the device) == the host-driven
+    native loop, frame by frame, over a 720p pan with keyframe switches."""
+    seq = synth.scene_sequence(120, 1280, 720)
+    frames = synth.scene_frames(seq)
+    K = (seq.fx, seq.fy, seq.cx, seq.cy)
+    p0 = tracking.Pose(seq.R[0], seq.t[0])
+    gf = tracking.GpuBackend(2000).extract(frames)
+    n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z)
+    d = tracking.track_native_device(*tracking.features_to_device(gf), len(gf), K, p0, synth.SCENE_PLANE_Z)
+    assert len(n.keyframes) >= 2
+    _same(d, n)
+
+
+def test_device_tracking_loop_fallbacks_and_lost(gpu):
+    """The device-side decisions of the fallback radii and of lost frames: a sequence with
+    feature-less frames (lost: prediction kept, no keyframe) and strict settings that force the
+    wider and the position-free searches."""
+    seq = synth.scene_sequence(30, 640, 480)
+    frames = synth.scene_frames(seq).copy()
+    frames[10:13] = 128  # blank: no keypoints at all
+    frames[20] = np.roll(frames[20], 9, axis=1)  # a jump the 12 px search misses
+    K = (seq.fx, seq.fy, seq.cx, seq.cy)
+    p0 = tracking.Pose(seq.R[0], seq.t[0])
+    gf = tracking.GpuBackend(1000).extract(frames)
+    for s in (tracking.TrackerSettings(), tracking.TrackerSettings(small_match_ratio=0.9, min_matches=200)):
+        n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z, settings=s)
+        d = tracking.track_native_device(*tracking.features_to_device(gf, pitch=1000), len(gf), K, p0,
+                                         synth.SCENE_PLANE_Z, settings=s)
+        assert 0 in n.inliers[1:]
+        _same(d, n)
