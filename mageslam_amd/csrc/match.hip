@@ -34,7 +34,9 @@ namespace mage {
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v8i __attribute__((ext_vector_type(8)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int MW = 8;          // waves per workgroup (2 per SIMD)
 constexpr int MT = MW * kWave; // threads per workgroup
@@ -108,11 +110,29 @@ __device__ __forceinline__ v4i expand16(uint32_t w)
     return r;
 }
 
+// 32 descriptor bits -> 32 fp4 (e2m1) elements s(bit) = +1 (0x2) / -1 (0xA), element j in
+// nibble j (low nibble first) of the 16 bytes.  Per output dword (byte q of w): the even and odd
+// bits of the byte are spread to the byte LSBs (multiply by 1 + 2^6 + 2^12 + 2^18: bit 2m lands at
+// 8m, the colliding sums at 6 / 12 / 18 carry only into bits the mask drops), and v_perm picks
+// one of the four two-element bytes {0x22, 0x2A, 0xA2, 0xAA}.
+__device__ __forceinline__ v4i expand32_fp4(uint32_t w)
+{
+    const uint32_t E = w & 0x55555555u, O = (w >> 1) & 0x55555555u;
+    v4i r;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t xe = (((E >> (8 * q)) & 0xFFu) * 0x00041041u) & 0x01010101u;
+        const uint32_t xo = (((O >> (8 * q)) & 0xFFu) * 0x00041041u) & 0x01010101u;
+        r[q] = (int)__builtin_amdgcn_perm(0u, 0xAAA22A22u, xe | (xo << 1));
+    }
+    return r;
+}
+
 // Row offset (within a 32-row tile, lane half 0) of accumulator register g of a 32x32 MFMA.
 __host__ __device__ constexpr int acc_row(int g) { return (g & 3) + 8 * (g >> 2); }
 
-// D = 256 - 2d for the wave's 32 rows x one 32-column B tile: 8 chained MFMAs over K = 256.
-__device__ __forceinline__ v16i tile_mfma(const v4i (&a)[8], const v4i (&b)[8])
+// D = 256 - 2d for the wave's 32 rows x one 32-column B tile: 8 chained i8 MFMAs over K = 256.
+__device__ __forceinline__ v16i tile_mfma_i8(const v4i (&a)[8], const v4i (&b)[8])
 {
     v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -120,23 +140,70 @@ __device__ __forceinline__ v16i tile_mfma(const v4i (&a)[8], const v4i (&b)[8])
     return acc;
 }
 
+// The same product on the MX fp4 MFMA (K = 64 per instruction: 4 instead of 8, half the matrix
+// cycles).  Elements are +-1 with E8M0 block scales 2^-11 (A) and 2^-10 (B), so each bit
+// contributes +-2^-21 and the sum is x = 2^-20 (128 - d).  The accumulator starts at the inline
+// constant C0 = 1/(2 pi) (f32 0x3E22F983, no register set to initialise per tile): C0 + x stays in
+// C0's binade [1/8, 1/4) (|x| <= 2^-13), whose ulp is 2^-26, and every partial sum is C0 plus a
+// multiple of 2^-21, so the result is exact and its bit pattern is 0x3E22F983 + 64 (128 - d).
+// The low 16 bits, read as i16, are 64 (128 - d - FP4_K0) + 3 (0xF983 + [-8192, 8192] stays
+// within [32768, 98304), so the wrap is the same for every d): monotone in d, low 6 bits = 3.
+constexpr int FP4_K0 = 26;  // (0x10000 - 0xF983 + 3) / 64
+__device__ __forceinline__ v16i tile_mfma_fp4(const v4i (&a)[8], const v4i (&b)[8])
+{
+    v16f acc;
+#pragma unroll
+    for (int g = 0; g < 16; g++) acc[g] = 0.15915494309189535f;  // 1 / (2 pi): inline constant
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const v8i av = {a[s][0], a[s][1], a[s][2], a[s][3], 0, 0, 0, 0};
+        const v8i bv = {b[s][0], b[s][1], b[s][2], b[s][3], 0, 0, 0, 0};
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc, 4, 4, 0, 127 - 11, 0, 127 - 10);
+    }
+    return __builtin_bit_cast(v16i, acc);
+}
+
+template <int KS>
 __device__ __forceinline__ void load_frags(v4i (&b)[8], const v4i* __restrict__ bt, int lane)
 {
 #pragma unroll
-    for (int s = 0; s < 8; s++) b[s] = bt[s * kWave + lane];
+    for (int s = 0; s < KS; s++) b[s] = bt[s * kWave + lane];
 }
+
+// The value of lane l ^ 32 (v_permlane32_swap: a VALU exchange, no LDS round trip).
+__device__ __forceinline__ int xor32(int x, int lane)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+    return (int)(lane < 32 ? r[1] : r[0]);
+}
+
+// A column flush whose second atomic is still to be issued (flush_finish).
+struct PendingCol {
+    int j, c1, c2, old;
+    bool live;
+};
 
 // Column partial of one B tile, as global keys (D << 15 | 0x7FFF - i), merged with the partner
 // half-wave, then into the workgroup's column top-2 with two LDS atomicMax (no CAS loop: a key
-// that loses, or is displaced from, the best slot is pushed into the second slot).
-__device__ __forceinline__ void flush_global(int c1, int c2, int lane, int colbase, int nb, int* colM1, int* colM2)
+// that loses, or is displaced from, the best slot is pushed into the second slot).  The second
+// atomic needs the first one's return value; it is issued later (flush_finish, after the next
+// fold) so the LDS round trip overlaps VALU work.
+__device__ __forceinline__ PendingCol flush_global(int c1, int c2, int lane, int colbase, int nb, int* colM1)
 {
-    merge2(c1, c2, __shfl_xor(c1, 32), __shfl_xor(c2, 32));
-    const int j = colbase + (lane & 31);
-    if ((lane >> 5) == 0 && j < nb && c1 != NONE) {
-        const int old = atomicMax(&colM1[j], c1);
-        atomicMax(&colM2[j], old > c1 ? c1 : max(old, c2));
-    }
+    merge2(c1, c2, xor32(c1, lane), xor32(c2, lane));
+    PendingCol pc;
+    pc.j = colbase + (lane & 31);
+    pc.c1 = c1;
+    pc.c2 = c2;
+    pc.live = (lane >> 5) == 0 && pc.j < nb && c1 != NONE;
+    pc.old = pc.live ? atomicMax(&colM1[pc.j], c1) : NONE;
+    return pc;
+}
+
+__device__ __forceinline__ void flush_finish(PendingCol& pc, int* colM2)
+{
+    if (pc.live) atomicMax(&colM2[pc.j], pc.old > pc.c1 ? pc.c1 : max(pc.old, pc.c2));
+    pc.live = false;
 }
 
 // 32-bit keys: operands s = +-1, D = 256 - 2d.  Row keys (D << 15 | 0x7FFF - j); column
@@ -144,7 +211,19 @@ __device__ __forceinline__ void flush_global(int c1, int c2, int lane, int colba
 // columns are masked (needed only when maxDist >= 128, see fold_any).
 template <bool PADMASK>
 struct Keys32 {
-    static constexpr uint32_t ATAB = 0x0000FF01u, BTAB = 0x0000FF01u;
+    // i8 operands: k-step s = descriptor dword s, lane half h = its 16-bit half h
+    static constexpr int KS = 8;
+    static __device__ __forceinline__ v4i a_frag(const uint32_t (&dw)[8], int half, int s)
+    {
+        return expand16<0x0000FF01u>(half ? (dw[s] >> 16) : (dw[s] & 0xFFFFu));
+    }
+    static __device__ __forceinline__ void fill(v4i (*tile)[kWave], int fs, int c, uint32_t dw, bool ok)
+    {
+        const v4i zero = {0, 0, 0, 0};
+        tile[fs][c] = ok ? expand16<0x0000FF01u>(dw & 0xFFFFu) : zero;
+        tile[fs][32 + c] = ok ? expand16<0x0000FF01u>(dw >> 16) : zero;
+    }
+    static __device__ __forceinline__ v16i tile_mfma(const v4i (&a)[8], const v4i (&b)[8]) { return tile_mfma_i8(a, b); }
     struct Rows {
         int r1[RT][16], r2[RT][16];
     };
@@ -195,15 +274,15 @@ struct Keys32 {
         else
             fold_m<false>(acc, rt, lane, colbase, nb, rowbase, na, R, C);
     }
-    static __device__ __forceinline__ void flush(const Part& C, int lane, int colbase, int nb, int rowbase,
-                                                 int* colM1, int* colM2)
+    static __device__ __forceinline__ PendingCol flush(const Part& C, int lane, int colbase, int nb, int rowbase,
+                                                       int* colM1)
     {
-        if (MAGE_MATCH_ABLATE == 1 || MAGE_MATCH_ABLATE == 4) return;
+        if (MAGE_MATCH_ABLATE == 1 || MAGE_MATCH_ABLATE == 4) return PendingCol{0, 0, 0, 0, false};
         const int ib = rowbase + 4 * (lane >> 5) + 63;
         int c1 = C.c1, c2 = C.c2;
         if (c1 != NONE) c1 = ((c1 >> 6) << 15) | (0x7FFF - (ib - (c1 & 63)));
         if (c2 != NONE) c2 = ((c2 >> 6) << 15) | (0x7FFF - (ib - (c2 & 63)));
-        flush_global(c1, c2, lane, colbase, nb, colM1, colM2);
+        return flush_global(c1, c2, lane, colbase, nb, colM1);
     }
     // row state q = rt * 16 + g as global keys
     static __device__ __forceinline__ void export_rows(const Rows& R, int lane, int (&s1)[RT * 16], int (&s2)[RT * 16])
@@ -216,12 +295,23 @@ struct Keys32 {
     }
 };
 
-// Packed 16-bit keys, two accumulator registers per VGPR: operands +-8 (A) and +-4 (B), so the
-// MFMA yields 64 (128 - d) with six zero low bits.  Row keys ((128 - d) << 6 | 63 - tile),
-// column keys ((128 - d) << 6 | 63 - wave row); both top-2 updates are v_pk_max_i16 /
-// v_pk_min_i16 on two elements at once.  Requires nb <= 2048 (64 tiles) and maxDist < 128.
+// Packed 16-bit keys, two accumulator registers per VGPR: the low 16 bits of the fp4 MFMA result
+// (tile_mfma_fp4) are (128 - d - FP4_K0) << 6 | 3.  Row keys ((128 - d - FP4_K0) << 6 | 63 - tile),
+// column keys ((128 - d - FP4_K0) << 6 | 63 - wave row): the index replaces the 3 by one XOR;
+// both top-2 updates are v_pk_max_i16 / v_pk_min_i16 on two elements at once.  Requires nb <= 2048 (64 tiles) and maxDist < 128.
 struct Keys16 {
-    static constexpr uint32_t ATAB = 0x0000F808u, BTAB = 0x0000FC04u;
+    // fp4 operands: k-step s = descriptor dwords 2s (lane half 0) and 2s + 1 (half 1)
+    static constexpr int KS = 4;
+    static __device__ __forceinline__ v4i a_frag(const uint32_t (&dw)[8], int half, int s)
+    {
+        return expand32_fp4(half ? dw[2 * s + 1] : dw[2 * s]);
+    }
+    static __device__ __forceinline__ void fill(v4i (*tile)[kWave], int fs, int c, uint32_t dw, bool ok)
+    {
+        const v4i zero = {0, 0, 0, 0};
+        tile[fs >> 1][32 * (fs & 1) + c] = ok ? expand32_fp4(dw) : zero;
+    }
+    static __device__ __forceinline__ v16i tile_mfma(const v4i (&a)[8], const v4i (&b)[8]) { return tile_mfma_fp4(a, b); }
     static constexpr uint32_t NONE2 = 0x80008000u;
     struct Rows {
         uint32_t r1[RT][8], r2[RT][8];
@@ -249,38 +339,38 @@ struct Keys16 {
     static __device__ __forceinline__ void fold(const v16i& acc, int rt, int lane, int colbase, int nb, int rowbase,
                                                 int na, Rows& R, Part& C)
     {
-        const uint32_t tpair = (uint32_t)(63 - (colbase >> 5)) * 0x00010001u;
+        const uint32_t tpair = ((uint32_t)(63 - (colbase >> 5)) ^ 3u) * 0x00010001u;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             const uint32_t P = __builtin_amdgcn_perm((uint32_t)acc[2 * q + 1], (uint32_t)acc[2 * q], 0x05040100u);
-            const uint32_t kr = P | tpair;
+            const uint32_t kr = P ^ tpair;
             R.r2[rt][q] = pmax(R.r2[rt][q], pmin(R.r1[rt][q], kr));
             R.r1[rt][q] = pmax(R.r1[rt][q], kr);
-            const uint32_t rc = (uint32_t)(63 - (rt * 32 + acc_row(2 * q))) |
-                                ((uint32_t)(63 - (rt * 32 + acc_row(2 * q + 1))) << 16);
-            const uint32_t kc = P | rc;
+            const uint32_t rc = ((uint32_t)(63 - (rt * 32 + acc_row(2 * q))) ^ 3u) |
+                                (((uint32_t)(63 - (rt * 32 + acc_row(2 * q + 1))) ^ 3u) << 16);
+            const uint32_t kc = P ^ rc;
             C.c2 = pmax(C.c2, pmin(C.c1, kc));
             C.c1 = pmax(C.c1, kc);
         }
     }
     static __device__ __forceinline__ int lo16(uint32_t v) { return (int)(short)(v & 0xFFFFu); }
     static __device__ __forceinline__ int hi16(uint32_t v) { return (int)v >> 16; }
-    static __device__ __forceinline__ void flush(const Part& C, int lane, int colbase, int nb, int rowbase,
-                                                 int* colM1, int* colM2)
+    static __device__ __forceinline__ PendingCol flush(const Part& C, int lane, int colbase, int nb, int rowbase,
+                                                       int* colM1)
     {
         // merge the even / odd register halves, then local -> global keys
         int m1 = lo16(C.c1), m2 = lo16(C.c2);
         merge2(m1, m2, hi16(C.c1), hi16(C.c2));
         const int ib = rowbase + 4 * (lane >> 5) + 63;
-        int c1 = m1 == -32768 ? NONE : ((m1 >> 6) << 16) | (0x7FFF - (ib - (m1 & 63)));
-        int c2 = m2 == -32768 ? NONE : ((m2 >> 6) << 16) | (0x7FFF - (ib - (m2 & 63)));
-        flush_global(c1, c2, lane, colbase, nb, colM1, colM2);
+        int c1 = m1 == -32768 ? NONE : (((m1 >> 6) + FP4_K0) << 16) | (0x7FFF - (ib - (m1 & 63)));
+        int c2 = m2 == -32768 ? NONE : (((m2 >> 6) + FP4_K0) << 16) | (0x7FFF - (ib - (m2 & 63)));
+        return flush_global(c1, c2, lane, colbase, nb, colM1);
     }
     static __device__ __forceinline__ int row_global(int k, int lane)
     {
         if (k == -32768) return NONE;
         const int j = (63 - (k & 63)) * 32 + (lane & 31);
-        return ((k >> 6) << 16) | (0x7FFF - j);
+        return (((k >> 6) + FP4_K0) << 16) | (0x7FFF - j);
     }
     static __device__ __forceinline__ void export_rows(const Rows& R, int lane, int (&s1)[RT * 16], int (&s2)[RT * 16])
     {
@@ -315,10 +405,8 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
         return RES ? Bres[8 * j + fs] : Bw[8 * j + fs];
     };
     auto fill = [&](int buf, int st, uint32_t dw) {
-        const bool ok = st * SC + fc < nb;  // padding columns: zero operands
-        const v4i zero = {0, 0, 0, 0};
-        stage[buf][fc >> 5][fs][fc & 31] = ok ? expand16<K::BTAB>(dw & 0xFFFFu) : zero;
-        stage[buf][fc >> 5][fs][32 + (fc & 31)] = ok ? expand16<K::BTAB>(dw >> 16) : zero;
+        // padding columns: zero operands
+        K::fill(stage[buf][fc >> 5], fs, fc & 31, dw, st * SC + fc < nb);
     };
 
     for (int pb = 0; pb < na; pb += ROWS) {
@@ -335,8 +423,8 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
 #pragma unroll
             for (int s = 0; s < 8; s++) dw[s] = Aw[8 * ic + s];
 #pragma unroll
-            for (int s = 0; s < 8; s++) {
-                a[rt][s] = expand16<K::ATAB>((lane >> 5) ? (dw[s] >> 16) : (dw[s] & 0xFFFFu));
+            for (int s = 0; s < K::KS; s++) {
+                a[rt][s] = K::a_frag(dw, lane >> 5, s);
                 if (i >= na) a[rt][s] = v4i{0, 0, 0, 0};  // padding rows: zero operands
             }
         }
@@ -351,9 +439,10 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
         // three buffers):  MFMA(t, rows 0-31) | fold(t-1, rows 32-63) + column flush(t-1) |
         // MFMA(t, rows 32-63) | fragments of t+1 | fold(t, rows 0-31).
         v4i bf[8];
-        load_frags(bf, &stage[0][0][0][0], lane);
+        load_frags<K::KS>(bf, &stage[0][0][0][0], lane);
         v16i acc1;
         int cbp = -1;
+        PendingCol pc{0, 0, 0, 0, false};
         typename K::Part C;
         K::reset(C);
         for (int st = 0; st < nstages; st++) {
@@ -365,18 +454,19 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
                 for (int ct = 0; ct < SC / 32; ct++) {
                     const int colbase = st * SC + ct * 32;
                     if (colbase >= nb) break;
-                    const v16i acc0 = tile_mfma(a[0], bf);
+                    const v16i acc0 = K::tile_mfma(a[0], bf);
                     if (cbp >= 0) {
                         K::fold(acc1, 1, lane, cbp, nb, rowbase, na, R, C);
-                        K::flush(C, lane, cbp, nb, rowbase, colM1, colM2);
+                        pc = K::flush(C, lane, cbp, nb, rowbase, colM1);
                     }
-                    acc1 = tile_mfma(a[1], bf);
+                    acc1 = K::tile_mfma(a[1], bf);
                     if (ct + 1 < SC / 32 && colbase + 32 < nb)
-                        load_frags(bf, &stage[buf][ct + 1][0][0], lane);
+                        load_frags<K::KS>(bf, &stage[buf][ct + 1][0][0], lane);
                     else if (st + 1 < nstages)
-                        load_frags(bf, &stage[(st + 1) % NBUF][0][0][0], lane);
+                        load_frags<K::KS>(bf, &stage[(st + 1) % NBUF][0][0][0], lane);
                     K::reset(C);
                     K::fold(acc0, 0, lane, colbase, nb, rowbase, na, R, C);
+                    flush_finish(pc, colM2);
                     cbp = colbase;
                 }
             }
@@ -386,7 +476,8 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
         if (active) {
             if (cbp >= 0) {
                 K::fold(acc1, 1, lane, cbp, nb, rowbase, na, R, C);
-                K::flush(C, lane, cbp, nb, rowbase, colM1, colM2);
+                pc = K::flush(C, lane, cbp, nb, rowbase, colM1);
+                flush_finish(pc, colM2);
             }
             // reduce-scatter the 32 row states (row tile q >> 4, register q & 15) over the 32
             // lanes of each half: lane c ends with state q = c.
