@@ -374,12 +374,13 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
 //             are its 12 K elements (order free: A and B share the lane-local K order).  H is split
 //             into bytes (hi, lo), two MFMAs per 16 output rows; Y + 2^15 = 256 hi-sum + lo-sum
 //             (C = 128 * 257 for each, + 2^15 for lo); out = min(255, (Y + 2^15) >> 16).
-// The output (lane = column, registers = 4 rows) goes to the LDS tile as bytes.
+//             The column pass is computed transposed (Y^T = H^T Tc^T: the H bytes as the A
+//             operand, the band as B; A and B share the lane layout), so a lane holds 4
+//             consecutive columns of one output row: one dword, stored straight to the frame
+//             (no LDS tile, no barrier, no copy loop).
 constexpr int BLUR_STRIPS = (TW + 15) / 16;  // 8 (the last is half used)
-constexpr int BT_W = 16 * BLUR_STRIPS;       // blurred tile row pitch (bytes)
-static_assert(32 * BT_W <= SROWS * GX * 4, "the blurred tile reuses the score buffer");
 
-__device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], uint8_t* bt, const FastParams& p)
+__device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastParams& p, int f)
 {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -416,15 +417,21 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], uint8_t* bt,
             lo[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u);
             hi[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x07060302u) ^ 0x80808080u);
         }
-        // bt is 32 x BT_W bytes: the discarded rows 30, 31 and columns 120..127 land in padding
-        uint8_t* o_col = bt + 16 * s + n + 4 * g * BT_W;
+        // lane: output row 16 o + n, tile columns 16 s + 4 g .. + 3 (rows >= TH, columns >= TW
+        // and columns past the blurred frame's stride are not stored)
+        const int x = 16 * s + 4 * g, X = (int)blockIdx.x * TW + x;
+        const int ylim = min(TH, p.h - (int)blockIdx.y * TH);
+        uint8_t* dst = p.blur + (long long)f * p.blur_pitch + (long long)(blockIdx.y * TH + n) * p.blur_stride + X;
 #pragma unroll
         for (int o = 0; o < 2; o++) {
-            const v4i yh = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[o], hi, c_hi, 0, 0, 0);
-            const v4i yl = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[o], lo, c_lo, 0, 0, 0);
+            const v4i yh = __builtin_amdgcn_mfma_i32_16x16x64_i8(hi, ta[o], c_hi, 0, 0, 0);
+            const v4i yl = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo, ta[o], c_lo, 0, 0, 0);
+            uint32_t w = 0;
 #pragma unroll
             for (int r = 0; r < 4; r++)
-                o_col[(16 * o + r) * BT_W] = (uint8_t)min(255u, (((uint32_t)yh[r] << 8) + (uint32_t)yl[r]) >> 16);
+                w |= min(255u, (((uint32_t)yh[r] << 8) + (uint32_t)yl[r]) >> 16) << (8 * r);
+            if (16 * o + n < ylim && x < TW && X < p.blur_stride)
+                *reinterpret_cast<uint32_t*>(dst + (long long)(16 * o) * p.blur_stride) = w;
         }
     }
 }
@@ -639,22 +646,9 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
             }
         }
     }
-    __syncthreads();
-    if (kBlur && blur) {
-        uint32_t* bt = &sc[0][0];
-        blur_mfma(img, reinterpret_cast<uint8_t*>(bt), p);
-        __syncthreads();
-        // blurred tile -> frame (rows < h, dword columns < blur_stride)
-        constexpr int CW = TW / 4, RSTEP = FAST_THREADS / CW;  // 30 dword columns, 4 rows per pass
-        const int c = threadIdx.x % CW, r0 = threadIdx.x / CW;
-        const int X = blockIdx.x * TW + 4 * c, ylim = min(TH, p.h - (int)blockIdx.y * TH);
-        if (r0 < RSTEP && X < p.blur_stride) {
-            uint8_t* dst = p.blur + (long long)f * p.blur_pitch + (long long)(blockIdx.y * TH + r0) * p.blur_stride + X;
-            const long long dstep = (long long)RSTEP * p.blur_stride;
-            for (int r = r0; r < ylim; r += RSTEP, dst += dstep)
-                *reinterpret_cast<uint32_t*>(dst) = bt[r * (BT_W / 4) + c];
-        }
-    }
+    // the blur reads only the image tile and writes the frame directly: no barrier before it
+    if (kBlur && blur) blur_mfma(img, p, f);
+    __syncthreads();  // s_cnt and the tile's list are final
     if (kSink || !kEmit) {  // ablation: keep the skipped stages' inputs alive
         if (kSink) {
             const uint32_t* w = &sc[0][0];

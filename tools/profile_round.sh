@@ -3,7 +3,7 @@
 #   kernel trace + stats, then FETCH_SIZE, WRITE_SIZE and SQ VALU/MFMA counters in separate passes
 #   (never combined with trace domains), for bench.py and for tools/bench_rows.py (the §8 rows the
 #   headline does not exercise), then the summaries into profiles/<tag>_*.
-# usage: bash tools/profile_round.sh <tag>      (on the box; only gpurun_out/ comes back)
+# usage: bash tools/profile_round.sh <tag> [main|rows]   (on the box; only gpurun_out/ comes back)
 #        bash tools/profile_round.sh <tag> collect   (here: summaries from gpurun_out/ into profiles/)
 set -eo pipefail
 TAG=${1:-r1}
@@ -40,7 +40,14 @@ if [ "$2" = collect ]; then
     cp profiles/${TAG}_orb_pmc_summary.json profiles/pmc_summary.json
     exit 0
 fi
-run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores
-run_set $ORB $ORB_CMD
-run_set $ROWS python3 tools/bench_rows.py
-timeout -k 10 400 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
+# optional phase (one gpurun call each when the whole round would not fit one call's limit):
+#   main = headline + ORB-only sets, rows = the per-row set + the final default bench line
+PHASE=${2:-all}
+if [ "$PHASE" = all ] || [ "$PHASE" = main ]; then
+    run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores
+    run_set $ORB $ORB_CMD
+fi
+if [ "$PHASE" = all ] || [ "$PHASE" = rows ]; then
+    run_set $ROWS python3 tools/bench_rows.py
+    timeout -k 10 400 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
+fi
