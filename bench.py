@@ -76,10 +76,10 @@ def ba_flops(g, trials_per_iter):
     return 330.0 * len(g.cam) + trials_per_iter * (schur + n ** 3 / 3 + 2 * n ** 2)
 
 
-def load_pmc(kernel):
-    """(HBM bytes per launch, provenance) for `kernel` from the committed rocprofv3 PMC summary.
-    The summary records the hash of the kernel sources it was collected on; counters of other
-    sources are stale and not reported (traffic None)."""
+def load_pmc(kernel, field="hbm_bytes_per_launch"):
+    """(`field` of `kernel`, provenance) from the committed rocprofv3 PMC summary (default: HBM
+    bytes per launch).  The summary records the hash of the kernel sources it was collected on;
+    counters of other sources are stale and not reported (None)."""
     from mageslam_amd.build import kernel_sources_sha
 
     f = ROOT / "profiles" / "pmc_summary.json"
@@ -93,7 +93,7 @@ def load_pmc(kernel):
     sha, now = meta.get("kernel_sources_sha"), kernel_sources_sha()
     if sha != now:
         return None, f"stale: profiles/pmc_summary.json was collected on kernel sources {sha}, these are {now}"
-    return d.get(kernel, {}).get("hbm_bytes_per_launch"), \
+    return d.get(kernel, {}).get(field), \
         f"profiles/pmc_summary.json ({meta.get('tag')}, kernel sources {sha}, FETCH_SIZE + WRITE_SIZE passes)"
 
 
@@ -257,10 +257,15 @@ def run_orb(args, rank, world, local_rank, torch, dist):
         avg_s = orb_k[dom]["avg_ms"] / 1000.0
         achieved = per_frame * B / avg_s / 1e9
         traffic, traffic_source = load_pmc(dom)
+        valu, _ = load_pmc(dom, "valu_issue_frac")
         res["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                            "traffic_source": traffic_source, "algorithmic_bytes_per_launch": per_frame * B,
-                           "avg_launch_ms": orb_k[dom]["avg_ms"]}
+                           "avg_launch_ms": orb_k[dom]["avg_ms"],
+                           # what actually binds the kernel: SQ_INSTS_VALU per launch
+                           # over its duration against 1024 SIMDs x 2.4 GHz / 4 cycles, same PMC run
+                           "binding": {"resource": "VALU issue", "frac": valu,
+                                       "source": "SQ_INSTS_VALU pass of the same profile" if valu is not None else traffic_source}}
     return res
 
 
