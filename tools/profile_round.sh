@@ -49,5 +49,6 @@ if [ "$PHASE" = all ] || [ "$PHASE" = main ]; then
 fi
 if [ "$PHASE" = all ] || [ "$PHASE" = rows ]; then
     run_set $ROWS python3 tools/bench_rows.py
+    mkdir -p $OUT
     timeout -k 10 400 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
 fi
