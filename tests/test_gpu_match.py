@@ -41,6 +41,27 @@ def test_match_random(gpu, oracle, na, nb):
         assert np.array_equal(dm_bytes(g), dm_bytes(o)), (na, nb, md, mdiff)
 
 
+@pytest.mark.parametrize("na,nb", [(2048, 2048), (100, 2049), (2049, 100), (33, 2047)])
+def test_match_fp4_path_boundaries(gpu, oracle, na, nb):
+    """The packed-key fp4 MFMA path serves nb <= 2048 and maxDist < 128; nb = 2049 and maxDist
+    >= 128 take the i8 path.  Both sides of each boundary, plus extreme distances (0 and 256:
+    the accumulator's full range) and exact ties."""
+    rng = np.random.default_rng(na + 3 * nb)
+    base = rng.integers(0, 256, (max(na, nb), 32), dtype=np.uint8)
+    base[:4] = 0
+    base[4:8] = 255
+    A = base[:na].copy()
+    flip = rng.integers(0, 256, (nb, 32), dtype=np.uint8) & rng.integers(0, 256, (nb, 32), dtype=np.uint8) \
+        & rng.integers(0, 256, (nb, 32), dtype=np.uint8)
+    B = base[rng.integers(0, na, nb)] ^ flip
+    B[:8] = base[:8]
+    B[8:12] = B[12:16]  # duplicated columns: tied distances for every row
+    for md, mdiff in ((30, 1), (127, 2), (128, 2), (0, 0)):
+        g = matcher.Match(A, B, maxHammingDist=md, minHammingDifference=mdiff)
+        o = oracle.match(A, B, max_distance=md, min_difference=mdiff)
+        assert np.array_equal(dm_bytes(g), dm_bytes(o)), (na, nb, md, mdiff)
+
+
 def test_match_masks_and_empty(gpu, oracle):
     rng = np.random.default_rng(3)
     A = rng.integers(0, 256, (400, 32), dtype=np.uint8)
