@@ -1071,16 +1071,25 @@ __global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict_
 // registers (k-step q = register q):
 //   TRSM  U_kj = inv(L_kk) A_kj            (A operand inv(L_kk) from LDS; L = U^T)
 //   SYRK  A_ij -= U_ki^T U_kj, k < i <= j  (both operands from the LDS panel of row-block k)
-// Step k: the owner of tile (k, k) factors it (Cholesky + triangular inverse in one wave) ->
-// barrier -> TRSM of row-block k into the double-buffered panel -> barrier -> SYRK.  Nothing
-// of S leaves the chip between steps; the solves use the per-block inverses kept in LDS.
+// Step k: TRSM of row-block k into the double-buffered panel -> barrier -> SYRK, in which the
+// owner of tile (k+1, k+1) updates that tile first and hands it (LDS + flag) to the factor wave,
+// which factors it (Cholesky + triangular inverse + forward substitution in one column loop)
+// while the tile waves finish their SYRKs -> barrier.  (With the owner factoring its own tile,
+// its remaining SYRKs queued behind the ~3.4k-cycle column loop: the owner finished its phase
+// ~5k cycles after every other wave, every step.)  Nothing of S leaves the chip between steps;
+// the solves use the per-block inverses kept in LDS.
 #ifndef MAGE_CHOL_ABLATE  // timing experiments only (tools/ablate_ba.py); 0 in the product
 #define MAGE_CHOL_ABLATE 0
 #endif
+#ifndef MAGE_CHOL_FW
+#define MAGE_CHOL_FW 1  // 1: a dedicated factor wave (no tiles); 0: the next diagonal tile's owner factors it
+#endif
 constexpr int CT_WAVES = 8;   // 2 per SIMD: 256 VGPRs hold 18 resident tiles + the block factor
 constexpr int CT_THREADS = CT_WAVES * kWave;
-constexpr int CT_TPW = 15;    // tiles per wave: 8 x 15 = 120 upper tiles of np = 240
+constexpr int CT_TW = MAGE_CHOL_FW ? CT_WAVES - 1 : CT_WAVES;  // tile waves (wave CT_TW: the factor wave)
+constexpr int CT_TPW = MAGE_CHOL_FW ? 18 : 15;  // tiles per tile wave: 7 x 18 (8 x 15) >= 120 upper tiles of np = 240
 constexpr int CT_MAXT = 15;
+static_assert(CT_TW * CT_TPW >= CT_MAXT * (CT_MAXT + 1) / 2, "every upper tile has a slot");
 
 // Broadcast of lane l's double (two v_readlane_b32: scalar result, no LDS crossbar).
 __device__ __forceinline__ double readlane_f64(double v, int l)
@@ -1126,6 +1135,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     __shared__ __attribute__((aligned(16))) double dsc[16][18];  // the factor's scratch: A_kk transposed
     __shared__ __attribute__((aligned(16))) double vb[CT_MAXT * 16];  // b -> y -> x
     __shared__ int s_fail;
+    __shared__ int s_diag_ready;  // index of the diagonal block staged in dsc for the factor wave
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: tile bookkeeping on the SALU
     const int mt = np >> 4, T = mt * (mt + 1) / 2;
@@ -1136,7 +1146,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     {
         int i = 0, rowend = mt;  // tiles [rowend - (mt - i), rowend) are row i
         for (int sl = 0; sl < CT_TPW; sl++) {
-            const int t = wave + CT_WAVES * sl;
+            const int t = wave < CT_TW ? wave + CT_TW * sl : T;  // the factor wave holds no tile
             while (i < mt && t >= rowend) {
                 i++;
                 rowend += mt - i;
@@ -1163,7 +1173,10 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             C[sl] = dbl4{0, 0, 0, 0};
         }
     }
-    if (tid == 0) s_fail = 0;
+    if (tid == 0) {
+        s_fail = 0;
+        s_diag_ready = -1;
+    }
     for (int i = tid; i < np; i += CT_THREADS) vb[i] = i < n ? b[i] : 0.0;
     long long tm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0;  // MAGE_CHOL_ABLATE == 3: phase cycles of wave 0
     auto tick = [&](int ph) {
@@ -1194,15 +1207,14 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
 
     // --- diagonal block: Cholesky of A_kk and inv(L_kk) by its owner wave (slot `slot`); A_kk
     // goes through dsc transposed, so each lane reads its row with 16-byte loads ---
-    auto factor_diag = [&](int k, int slot) {
+    auto stage_diag = [&](int slot) {  // the owner's tile (k, k) -> dsc, transposed
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++)
             if (sl == slot)
 #pragma unroll
                 for (int r = 0; r < 4; r++) dsc[lc][lr + 4 * r] = C[sl][r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto factor_diag = [&](int k) {  // from dsc
         const int l = lane;
         if (MAGE_CHOL_ABLATE == 2) {
             if (l < 16)
@@ -1273,7 +1285,17 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             }
         }
     };
-    if (mt > 0 && wave == 0) factor_diag(0, 0);  // tile (0, 0) is tile 0: wave 0, slot 0
+    if (mt > 0 && wave == 0) {  // tile (0, 0) is tile 0: wave 0, slot 0
+        stage_diag(0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (!MAGE_CHOL_FW) factor_diag(0);
+    }
+    if (MAGE_CHOL_FW) {
+        __syncthreads();  // dsc holds A_00
+        if (mt > 0 && wave == CT_TW) factor_diag(0);
+    }
     tick(1);
     __syncthreads();
     tick(2);
@@ -1320,14 +1342,36 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                                                             C[sl], 0, 0, 0);
         };
         const int kn = k + 1, tnn = upper_tile_index(kn, kn, mt);
-        if (kn < mt && wave == tnn % CT_WAVES) {
-            const int slot = tnn / CT_WAVES;
+        if (kn < mt && wave == tnn % CT_TW) {
+            const int slot = tnn / CT_TW;
+            if (MAGE_CHOL_FW) __builtin_amdgcn_s_setprio(2);  // the critical chain first on this SIMD
 #pragma unroll
             for (int sl = 0; sl < CT_TPW; sl++)
                 if (sl == slot) syrk(sl);
             tick(4);
-            factor_diag(kn, slot);
+            stage_diag(slot);
+            if (MAGE_CHOL_FW) {
+                // hand A_{k+1,k+1} to the factor wave: the fence drains the staging stores before
+                // the flag store
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&s_diag_ready, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_s_setprio(0);
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                factor_diag(kn);
+            }
             tick(1);
+        }
+        if (MAGE_CHOL_FW && kn < mt && wave == CT_TW) {
+            // the owner reaches its SYRK phase without waiting on this wave, so the spin ends
+            while (__hip_atomic_load(&s_diag_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != kn)
+                __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            __builtin_amdgcn_s_setprio(3);  // the column loop is the critical chain: issue before the SYRKs
+            factor_diag(kn);
+            __builtin_amdgcn_s_setprio(0);
         }
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++) {
