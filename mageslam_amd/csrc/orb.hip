@@ -1172,6 +1172,7 @@ struct DescParams {
     // its angle (ComputeOrbDescriptors); kp_angle[7 * index] is the keypoint's angle field
     int random;
     const float* kp_angle;
+    const uint4* blur_ops;  // describe_win_kernel: the fused blur's MFMA band operands (blur_operands)
 };
 
 // GetComputeOrbDescriptorsValue (OpenCVModified.cpp:442-448): the pattern point rotated in f32
@@ -1362,6 +1363,136 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
             if (p.random) e = rotate_test(e, ra, rb_);
             const int t0 = wb[(R + e.y) * WP + R + e.x];
             const int t1 = wb[(R + e.w) * WP + R + e.z];
+            const unsigned long long m = __ballot(t0 < t1);
+            if (lane == 0) dst[c] = m;
+        }
+    }
+}
+
+
+// Descriptors with the 7-tap Gaussian computed per keypoint window on the matrix cores instead of
+// over the whole frame (the default configuration: one level, rotation 0, pattern radius <= 7).
+// The 2000 windows of a 720p frame cover about half of its pixels, and the full-frame blur was
+// ~30 % of the FAST pass (and its 1 byte / pixel write).  Per keypoint: a 32-row x 48-byte raw
+// window (16-byte loads, any 16-byte phase) staged in LDS; the H blocks of the row pass and the
+// transposed column pass exactly as blur_mfma (same band operands, same integer arithmetic:
+// H = sum tap * b, out = min(255, (sum tap * H + 2^15) >> 16)), giving the 16 x 16 blurred block
+// at (cx - R, cy - R); then the 256 tests.  Windows whose 7x7 support leaves the image take the
+// reflect-101 gather path.
+__global__ __launch_bounds__(DESC_WAVES * kWave) void describe_win_kernel(
+    DescParams p, const uint32_t* __restrict__ xy_in, const uint32_t* __restrict__ n_in,
+    const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
+{
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    constexpr int WR = 32, WB = 48;  // window rows (two H blocks), bytes per row (16-byte phase)
+    __shared__ __attribute__((aligned(16))) uint8_t raw[DESC_WAVES][KPW][WR * WB];
+    __shared__ __attribute__((aligned(16))) uint8_t bw[DESC_WAVES][KPW][256];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;  // XCD-aware, as describe_blurred_kernel
+    const int chunk = slot % p.chunks, f = (slot / p.chunks) * 8 + xcd;
+    if (f >= p.frames) return;
+    const int k0 = (chunk * DESC_WAVES + wave) * KPW;
+    const int n = (int)n_in[f];
+    if (k0 >= n) return;
+    const int R = p.R;
+    const uint8_t* src = p.lev.base[0] + (long long)f * p.lev.pitch[0];
+    const int stride = p.lev.stride[0], W = p.lw[0], H = p.lh[0];
+    // staging items: 32 rows x 3 segments of 16 bytes, lanes 0..63 then 0..31
+    uint4 v[KPW][2];
+    int cx[KPW], cy[KPW], sh[KPW];
+#pragma unroll
+    for (int q = 0; q < KPW; q++) {
+        const uint32_t xy = xy_in[(long long)f * p.out_cap + min(k0 + q, n - 1)];
+        cx[q] = (int)(xy & 0xFFFFu);
+        cy[q] = (int)(xy >> 16);
+        const int wx = cx[q] - R - 8, wy = cy[q] - R - 3;  // band byte 0, H row 0
+        const int xa = wx & ~15;
+        sh[q] = wx - xa;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int i = min(lane + 64 * j, 95), r = i / 3, c = i - 3 * r;
+            const int gy = min(max(wy + r, 0), H - 1), gx = min(max(xa + 16 * c, 0), stride - 16);
+            v[q][j] = *reinterpret_cast<const uint4*>(src + (long long)gy * stride + gx);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < KPW; q++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int i = lane + 64 * j;
+            if (i < 96) *reinterpret_cast<uint4*>(&raw[wave][q][(i / 3) * WB + 16 * (i % 3)]) = v[q][j];
+        }
+    wave_lds_sync();
+    const int n16 = lane & 15, g = lane >> 4;
+    const uint4 o0 = p.blur_ops[3 * lane], o1 = p.blur_ops[3 * lane + 1];
+    const v4i tb = {(int)o0.x, (int)o0.y, (int)o0.z, (int)o0.w};
+    const v4i ta = {(int)o1.x, (int)o1.y, (int)o1.z, (int)o1.w};  // output block 0
+    const v4i c_row = {32896, 32896, 32896, 32896};                // 128 * 257
+    const v4i c_hi = c_row, c_lo = {65664, 65664, 65664, 65664};   // + 2^15
+#pragma unroll
+    for (int q = 0; q < KPW; q++) {
+        const bool inside = cx[q] - R - 3 >= 0 && cx[q] + R + 3 < W && cy[q] - R - 3 >= 0 && cy[q] + R + 3 < H;
+        if (inside) {
+            // row pass: lane (row n16 of block b, K group g) takes window bytes 16 (g & 1) ..
+            // + 15 of row 16 b + n16 (groups 2, 3 meet zero band bytes)
+            const int bo = sh[q] + 16 * (g & 1);
+            v4i Hb[2];
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                const uint32_t* rw = reinterpret_cast<const uint32_t*>(&raw[wave][q][(16 * b + n16) * WB + (bo & ~3)]);
+                uint32_t d[5];
+#pragma unroll
+                for (int i = 0; i < 5; i++) d[i] = rw[i];
+                v4i a;
+#pragma unroll
+                for (int i = 0; i < 4; i++) a[i] = (int)(__builtin_amdgcn_alignbyte(d[i + 1], d[i], bo & 3) ^ 0x80808080u);
+                Hb[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, tb, c_row, 0, 0, 0);
+            }
+            v4i lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)Hb[b][1], (uint32_t)Hb[b][0], 0x05010400u);
+                const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)Hb[b][3], (uint32_t)Hb[b][2], 0x05010400u);
+                lo[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u);
+                hi[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x07060302u) ^ 0x80808080u);
+            }
+            // column pass, transposed: lane (output row n16, group g) gets columns 4g .. 4g + 3
+            const v4i yh = __builtin_amdgcn_mfma_i32_16x16x64_i8(hi, ta, c_hi, 0, 0, 0);
+            const v4i yl = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo, ta, c_lo, 0, 0, 0);
+            uint32_t w = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++) w |= min(255u, (((uint32_t)yh[r] << 8) + (uint32_t)yl[r]) >> 16) << (8 * r);
+            *reinterpret_cast<uint32_t*>(&bw[wave][q][16 * n16 + 4 * g]) = w;
+        } else {
+            // reflect-101 at the image border (BORDER_REFLECT_101 of the full-frame blur)
+            const int bd = 2 * R + 1;
+            for (int i = lane; i < bd * bd; i += kWave) {
+                const int oy = i / bd, ox = i - oy * bd;
+                const int y = cy[q] - R + oy, x = cx[q] - R + ox;
+                int acc = 0;
+                for (int ty = 0; ty < 7; ty++) {
+                    const uint8_t* row = src + (long long)reflect101(y + ty - 3, H) * stride;
+                    int hs = 0;
+                    for (int tx = 0; tx < 7; tx++) hs += p.taps[tx] * row[reflect101(x + tx - 3, W)];
+                    acc += p.taps[ty] * hs;
+                }
+                bw[wave][q][16 * oy + ox] = (uint8_t)min(255, (acc + (1 << 15)) >> 16);
+            }
+        }
+    }
+    wave_lds_sync();
+    const char4* pat = reinterpret_cast<const char4*>(pattern);
+#pragma unroll
+    for (int q = 0; q < KPW; q++) {
+        const int k = k0 + q;
+        if (k >= n) break;
+        const uint8_t* wb = bw[wave][q];
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const char4 e = pat[c * kWave + lane];  // (x0, y0, x1, y1) of bit 64*c + lane, rotation 0
+            const int t0 = wb[(R + e.y) * 16 + R + e.x];
+            const int t1 = wb[(R + e.w) * 16 + R + e.z];
             const unsigned long long m = __ballot(t0 < t1);
             if (lane == 0) dst[c] = m;
         }
@@ -1809,7 +1940,15 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
 
     // the default 7-tap Gaussian is fused into the FAST pass (the tile is already in LDS);
     // other kernel sizes blur inside the descriptor windows instead
-    const bool fused_blur = cap > 0 && s.gaussian_kernel_size == 7;
+    // MAGE_WIN_BLUR=1 (experiment, off by default): in the default configuration (one level,
+    // rotation 0, radius <= 7, 16-byte aligned frames) blur per keypoint window inside
+    // describe_win_kernel instead of over the frame.  Bit-exact, but at C2 it moved 0.16 ms into
+    // describe for 0.09 ms out of FAST, so the fused frame blur stays the default.
+    static const bool win_blur_opt = getenv("MAGE_WIN_BLUR") && getenv("MAGE_WIN_BLUR")[0] == '1';
+    const bool win_blur = win_blur_opt && cap > 0 && s.gaussian_kernel_size == 7 && L == 1 && !s.use_orientation &&
+                          !o->random_pattern && o->R <= 7 && stride % 16 == 0 && pitch % 16 == 0 &&
+                          (uintptr_t)d_frames % 16 == 0;
+    const bool fused_blur = cap > 0 && s.gaussian_kernel_size == 7 && !win_blur;
     if (fused_blur && (r = o->blurred.reserve((size_t)batch * g.blur_bytes)) != MAGE_OK) return r;
     LevelImages blurred{};
     const int half = (int)s.patch_size / 2;
@@ -1920,7 +2059,14 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         dp.random = o->random_pattern;
         dp.kp_angle = reinterpret_cast<const float*>(d_kp) + 3;  // mage_keypoint.angle
         {
-            if (fused_blur) {
+            if (win_blur) {
+                dp.chunks = (int)((cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW));
+                dp.frames = (int)batch;
+                dp.blur_ops = o->blur_ops.as<uint4>();
+                const dim3 g3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
+                launch("orb.describe", describe_win_kernel, g3, dim3(DESC_WAVES * kWave), 0, st, dp,
+                       (const uint32_t*)o->xy.as<uint32_t>(), d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
+            } else if (fused_blur) {
                 dp.chunks = (int)((cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW));
                 dp.frames = (int)batch;
                 const dim3 g3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);

@@ -359,3 +359,39 @@ def test_fast_gate_pyramid(gpu, oracle):
     _batch_vs_oracle(det, oracle, np.stack([synth.frame(t, w, h) for t in range(3, 7)]), s, cap)
     assert det.fast_gate_stats(level=2)["last_redo"] == 4
     assert det.fast_gate_stats(level=0)["last_gate"] > 4
+
+
+WIN_BLUR_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from mageslam_amd import orb, synth
+from oracle import oracle as O
+for (w, h), nfeat in (((640, 480), 2000), ((1280, 720), 2000), ((320, 180), 440)):
+    det = orb.OrbDetector(nfeatures=nfeat)
+    for t in (0, 3):
+        img = synth.frame(t, w, h)
+        kp, d = det.DetectAndCompute(img)
+        st, okp, od = O.orb_detect(img, O.default_settings(nfeat))
+        assert st == 0 and len(kp) == len(okp), (w, h, t)
+        assert np.array_equal(np.ascontiguousarray(kp).view(np.uint8), np.ascontiguousarray(okp).view(np.uint8))
+        assert np.array_equal(d, od), (w, h, t)
+        # keypoints whose 7x7 support leaves the frame take the reflect-101 path
+        assert ((kp["x"] < 10) | (kp["y"] < 10) | (kp["x"] > w - 11) | (kp["y"] > h - 11)).any() or w > 640
+print("ok")
+"""
+
+
+def test_window_blur_descriptors_match_oracle(gpu):
+    """MAGE_WIN_BLUR=1 (describe_win_kernel: the Gaussian per keypoint window on the matrix cores,
+    reflect-101 gathers at the border) is bit-exact vs the oracle; the switch is read once per
+    process, so the case runs in a child."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parent.parent)
+    r = subprocess.run([sys.executable, "-c", WIN_BLUR_CHILD, root], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MAGE_WIN_BLUR="1"), cwd=root)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
