@@ -1397,8 +1397,9 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_win_kernel(
     const int R = p.R;
     const uint8_t* src = p.lev.base[0] + (long long)f * p.lev.pitch[0];
     const int stride = p.lev.stride[0], W = p.lw[0], H = p.lh[0];
-    // staging items: 32 rows x 3 segments of 16 bytes, lanes 0..63 then 0..31
-    uint4 v[KPW][2];
+    // staging items: the 2R + 7 <= 21 window rows the kept outputs read x 3 segments of 16 bytes,
+    // one per lane (rows 21..31 of the H blocks feed only output rows >= 15, never read)
+    uint4 v[KPW];
     int cx[KPW], cy[KPW], sh[KPW];
 #pragma unroll
     for (int q = 0; q < KPW; q++) {
@@ -1408,20 +1409,13 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_win_kernel(
         const int wx = cx[q] - R - 8, wy = cy[q] - R - 3;  // band byte 0, H row 0
         const int xa = wx & ~15;
         sh[q] = wx - xa;
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int i = min(lane + 64 * j, 95), r = i / 3, c = i - 3 * r;
-            const int gy = min(max(wy + r, 0), H - 1), gx = min(max(xa + 16 * c, 0), stride - 16);
-            v[q][j] = *reinterpret_cast<const uint4*>(src + (long long)gy * stride + gx);
-        }
+        const int i = min(lane, 62), r = i / 3, c = i - 3 * r;
+        const int gy = min(max(wy + r, 0), H - 1), gx = min(max(xa + 16 * c, 0), stride - 16);
+        v[q] = *reinterpret_cast<const uint4*>(src + (long long)gy * stride + gx);
     }
 #pragma unroll
     for (int q = 0; q < KPW; q++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int i = lane + 64 * j;
-            if (i < 96) *reinterpret_cast<uint4*>(&raw[wave][q][(i / 3) * WB + 16 * (i % 3)]) = v[q][j];
-        }
+        if (lane < 63) *reinterpret_cast<uint4*>(&raw[wave][q][(lane / 3) * WB + 16 * (lane % 3)]) = v[q];
     wave_lds_sync();
     const int n16 = lane & 15, g = lane >> 4;
     const uint4 o0 = p.blur_ops[3 * lane], o1 = p.blur_ops[3 * lane + 1];
