@@ -57,8 +57,9 @@ struct FastParams {
     int qword_ok;  // frames 8-byte aligned, stride and pitch multiples of 8 (interior tiles)
     // fused 7-tap Gaussian (8U fixed point) of the tile into `blur` (null: no blur)
     uint8_t* blur;
-    int blur_stride;           // multiple of 4, >= w
+    int blur_stride;           // multiple of 4, >= w: columns written
     long long blur_pitch;      // bytes between blurred frames
+    int blur_bcols;            // brick columns per brick row (BLUR_BRICK layout)
     const uint4* blur_ops;     // per lane: the MFMA band operands of the taps (blur_operands)
     // candidate gate (see gate_strip): the batch's gate G is *gate; the launch re-arms the next
     // batch's gate word (*gate_next = 255, lowered by select_kernel) and the redo list (redo[0])
@@ -380,6 +381,15 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
 //             (no LDS tile, no barrier, no copy loop).
 constexpr int BLUR_STRIPS = (TW + 15) / 16;  // 8 (the last is half used)
 
+// BLUR_BRICK layout of the blurred frames (written here, read only by describe_blurred_kernel):
+// 128-byte bricks of 4 rows x 32 bytes, row-major over bricks.  A keypoint's 15-row window then
+// touches ~8 cache lines instead of ~20 (one per row), and describe was bound by the L1 / TA
+// line traffic of its window loads.
+__device__ __forceinline__ long long brick_offset(int y, int x, int bcols)
+{
+    return ((long long)(y >> 2) * bcols + (x >> 5)) * 128 + (y & 3) * 32 + (x & 31);
+}
+
 __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastParams& p, int f)
 {
     typedef int v4i __attribute__((ext_vector_type(4)));
@@ -421,7 +431,7 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
         // and columns past the blurred frame's stride are not stored)
         const int x = 16 * s + 4 * g, X = (int)blockIdx.x * TW + x;
         const int ylim = min(TH, p.h - (int)blockIdx.y * TH);
-        uint8_t* dst = p.blur + (long long)f * p.blur_pitch + (long long)(blockIdx.y * TH + n) * p.blur_stride + X;
+        uint8_t* fb = p.blur + (long long)f * p.blur_pitch;
 #pragma unroll
         for (int o = 0; o < 2; o++) {
             const v4i yh = __builtin_amdgcn_mfma_i32_16x16x64_i8(hi, ta[o], c_hi, 0, 0, 0);
@@ -430,8 +440,10 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
 #pragma unroll
             for (int r = 0; r < 4; r++)
                 w |= min(255u, (((uint32_t)yh[r] << 8) + (uint32_t)yl[r]) >> 16) << (8 * r);
-            if (16 * o + n < ylim && x < TW && X < p.blur_stride)
-                *reinterpret_cast<uint32_t*>(dst + (long long)(16 * o) * p.blur_stride) = w;
+            if (16 * o + n < ylim && x < TW && X < p.blur_stride) {
+                const int Y = (int)blockIdx.y * TH + 16 * o + n;
+                *reinterpret_cast<uint32_t*>(fb + brick_offset(Y, X, p.blur_bcols)) = w;
+            }
         }
     }
 }
@@ -1300,11 +1312,12 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
 {
     constexpr int BDMAX = 2 * RB + 1;
-    constexpr int ND = (BDMAX + 3 + 3) / 4;  // dwords per window row: covers any byte phase
-    constexpr int WP = 4 * ND;
-    constexpr int RPI = kWave / ND;          // window rows per load instruction
-    constexpr int NLD = (BDMAX + RPI - 1) / RPI;
-    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KPW][NLD * RPI * WP];
+    // the window's bricks (BLUR_BRICK: 4 rows x 32 bytes): any row / column phase
+    constexpr int NBR = (BDMAX + 3 + 3) / 4, NBC = (BDMAX + 31 + 31) / 32;
+    constexpr int NIT = NBR * NBC * 8;  // 16-byte items, 8 per brick (one 128-byte line)
+    constexpr int NLD = (NIT + kWave - 1) / kWave;
+    constexpr int WP = 32 * NBC;        // LDS window row pitch
+    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KPW][4 * NBR * WP];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave: scalar
     // XCD-aware 1-D grid: workgroups are dispatched round-robin over the 8 XCDs, so block b runs
     // on XCD b % 8; all keypoint chunks of frame f get blocks = f (mod 8) and consecutive slots,
@@ -1316,11 +1329,11 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     const int n = (int)n_in[f];
     if (k0 >= n) return;
     const int R = p.R;
-    // lane -> (row lane / ND, dword lane % ND); keypoints keep the pattern radius from the
-    // border (RunByImageBorder), so the clamps are inert: they only keep reads inside the level
-    const int lr = lane / ND, lc = lane - lr * ND;
-    uint32_t v[KPW][NLD];
-    int sh[KPW], rot[KPW];
+    // lane item i -> brick i / 8 of the window, 16-byte part i % 8; keypoints keep the pattern
+    // radius from the border (RunByImageBorder), so the clamps are inert: they only keep reads
+    // inside the level
+    uint4 v[KPW][NLD];
+    int off[KPW], rot[KPW];
 #pragma unroll
     for (int q = 0; q < KPW; q++) {
         const long long ki = (long long)f * p.out_cap + min(k0 + q, n - 1);
@@ -1328,31 +1341,32 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
         const int lv = MULTI ? __builtin_amdgcn_readfirstlane(p.lvl[ki]) : 0, l = lv >> 8;  // wave-uniform
         rot[q] = lv & 0xFF;
         const uint8_t* src = p.lev.base[l] + (long long)f * p.lev.pitch[l];
-        const int stride = p.lev.stride[l];
+        const int bcols = p.lev.stride[l], brows = (p.lh[MULTI ? l : 0] + 3) >> 2;
         const int x0 = (int)(xy & 0xFFFFu) - R, y0 = (int)(xy >> 16) - R;
-        const int xa = x0 & ~3;
-        sh[q] = x0 - xa;
-        const int gx = min(max(xa + 4 * lc, 0), stride - 4);
+        const int bx0 = max(x0, 0) >> 5, by0 = max(y0, 0) >> 2;
+        off[q] = (y0 - 4 * by0) * WP + (x0 - 32 * bx0);
 #pragma unroll
         for (int ld = 0; ld < NLD; ld++) {
-            const int gy = min(max(y0 + ld * RPI + lr, 0), p.lh[MULTI ? l : 0] - 1);
-            v[q][ld] = *reinterpret_cast<const uint32_t*>(src + (long long)gy * stride + gx);
+            const int i = min(lane + kWave * ld, NIT - 1), b = i >> 3, br = b / NBC, bc = b - br * NBC;
+            const int gbr = min(by0 + br, brows - 1), gbc = min(bx0 + bc, bcols - 1);
+            v[q][ld] = *reinterpret_cast<const uint4*>(src + ((long long)gbr * bcols + gbc) * 128 + 16 * (i & 7));
         }
     }
-    if (lr < RPI) {
 #pragma unroll
-        for (int q = 0; q < KPW; q++)
+    for (int q = 0; q < KPW; q++)
 #pragma unroll
-            for (int ld = 0; ld < NLD; ld++)
-                *reinterpret_cast<uint32_t*>(&win[wave][q][(ld * RPI + lr) * WP + 4 * lc]) = v[q][ld];
-    }
+        for (int ld = 0; ld < NLD; ld++) {
+            const int i = lane + kWave * ld, b = i >> 3, br = b / NBC, bc = b - br * NBC;
+            if (i < NIT)
+                *reinterpret_cast<uint4*>(&win[wave][q][(4 * br + ((i & 7) >> 1)) * WP + 32 * bc + 16 * (i & 1)]) = v[q][ld];
+        }
     wave_lds_sync();
     const char4* pat = reinterpret_cast<const char4*>(pattern);
 #pragma unroll
     for (int q = 0; q < KPW; q++) {
         const int k = k0 + q;
         if (k >= n) break;
-        const uint8_t* wb = &win[wave][q][sh[q]];
+        const uint8_t* wb = &win[wave][q][off[q]];
         const char4* pr = pat + (p.random ? 0 : rot[q] * 256);  // cvRound(angle / 12) % 30 (:526)
         float ra = 1.f, rb_ = 0.f;  // random pattern: rotation by the keypoint angle
         if (p.random) pattern_rotation(p.kp_angle[7 * ((long long)f * p.out_cap + k)], ra, rb_);
@@ -1658,6 +1672,8 @@ __global__ void synth_frames_kernel(uint8_t* __restrict__ out, int w, int h, lon
 struct LevelGeom {
     int w = 0, h = 0, stride = 0;
     long long pitch = 0;
+    int bcols = 0;           // blurred level: 32-byte brick columns per brick row (4 image rows)
+    long long bpitch = 0;    // blurred level: bytes per frame (bcols x 128 x brick rows)
     float scale = 1.f;
     int nfeatures = 0;
     size_t off = 0, boff = 0, coff = 0;  // pyramid / blurred / candidate offsets (per frame)
@@ -1788,8 +1804,10 @@ void level_geometry(OrbDetector* o, int w, int h)
         v.pitch = (long long)v.stride * v.h;
         v.off = l == 0 ? 0 : off;
         if (l > 0) off += (size_t)v.pitch;
+        v.bcols = (v.stride + 31) / 32;
+        v.bpitch = (long long)v.bcols * 128 * ((v.h + 3) / 4);
         v.boff = boff;
-        boff += (size_t)v.pitch;
+        boff += (size_t)v.bpitch;
         v.tiles = ((v.w + TW - 1) / TW) * ((v.h + TH - 1) / TH);
         v.cand_cap = (unsigned)v.tiles * TCAP;
         v.coff = coff;
@@ -1968,11 +1986,12 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         fp.qword_ok = (fp.stride % 8 == 0) && (fp.pitch % 8 == 0) && ((uintptr_t)raw.base[l] % 8 == 0);
         if (fused_blur) {
             blurred.base[l] = o->blurred.as<uint8_t>() + (size_t)batch * v.boff;
-            blurred.pitch[l] = v.pitch;
-            blurred.stride[l] = v.stride;
+            blurred.pitch[l] = v.bpitch;
+            blurred.stride[l] = v.bcols;  // brick layout (BLUR_BRICK): brick columns, not bytes
             fp.blur = const_cast<uint8_t*>(blurred.base[l]);
             fp.blur_stride = v.stride;
-            fp.blur_pitch = v.pitch;
+            fp.blur_pitch = v.bpitch;
+            fp.blur_bcols = v.bcols;
             fp.blur_ops = o->blur_ops.as<uint4>();
         }
         uint32_t* cand = o->cand.as<uint32_t>() + (size_t)batch * v.coff;
