@@ -114,3 +114,108 @@ def indexed_match_batch_device(desc_a, leaf_a, mask_a, a_pitch: int, n_a, desc_b
         ptr(desc_a), ptr(leaf_a), ptr(mask_a), a_pitch, ptr(n_a), ptr(desc_b), ptr(leaf_b), ptr(mask_b), b_pitch,
         ptr(n_b), pairs, max_distance, min_difference, ptr(out), capacity, ptr(n_out), ptr(status),
         C.c_void_p(stream) if stream else None))
+
+
+class OnlineBow:
+    """OnlineBow's keyframe database over a vocabulary tree (Core/MAGESLAM/Source/BoW/OnlineBow.cpp):
+    the IDF node weights CreateTree ends with (SetNodeWeights :340-394), AddImage / InsertDescriptors
+    (:94-98, :413-449), RemoveImage (:100-113), QueryFeatures (:115-133) and QueryUnknownImage
+    (:155-271).  The descriptor -> leaf descent (FindLeafNode, the Hamming part) runs on the GPU
+    (mage_bow_find_leaves); the bookkeeping is host code, as in the reference, in float32 with the
+    reference's expression order.  The reference iterates unordered_maps (node -> keyframe entries,
+    query node values), so its float sums and its std::sort tie order are implementation-defined:
+    here nodes and keyframes are visited in ascending id and equal scores keep ascending keyframe id.
+    The root's weight is left 0 (the reference leaves it uninitialised; no descriptor reaches it)."""
+
+    def __init__(self, tree: OnlineBowTree, qualifying_candidate_score: float = 0.75):
+        self.tree = tree
+        self.weights = np.zeros(len(tree._nd), np.float32)
+        self.node_kf: dict = {}  # leaf -> {keyframe id: [nodeValue (f32), feature indexes]}
+        self.image_set: set = set()
+        self.qualifying = np.float32(qualifying_candidate_score)  # BagOfWordsSettings (MageSettings.h:226)
+
+    @classmethod
+    def CreateTree(cls, training, descriptors_count, levels: int = 2, branching: int = 6, max_iter: int = 12,
+                   device: int = 0, qualifying_candidate_score: float = 0.75) -> "OnlineBow":
+        """OnlineBow::CreateTree (:325-338) over the training set AddTrainingDescriptors collected
+        (`descriptors_count` = descriptors per training image, m_descriptorsCount)."""
+        t = OnlineBowTree.CreateTree(training, levels, branching, max_iter, device)
+        self = cls(t, qualifying_candidate_score)
+        self.SetNodeWeights(training, descriptors_count)
+        return self
+
+    def SetNodeWeights(self, training, descriptors_count) -> None:
+        leaves = self.tree.find_leaves(training).tolist()
+        images = {}  # leaf -> training images with a descriptor in it
+        start = 0
+        for c in descriptors_count:
+            for leaf in set(leaves[start:start + int(c)]):
+                images[leaf] = images.get(leaf, 0) + 1
+            start += int(c)
+        n_images = len(descriptors_count)
+        for leaf, cnt in images.items():  # log((float)(nImages + 1) / (float)count), std::log(float)
+            self.weights[leaf] = np.log(np.float32(n_images + 1) / np.float32(cnt))
+
+    def InsertDescriptors(self, kf_id: int, descriptors) -> None:
+        leaves = self.tree.find_leaves(descriptors).tolist()
+        fresh = []  # entries created by this call: normalised at the end (the reference's pts)
+        total = np.float32(0)
+        for i, leaf in enumerate(leaves):
+            entries = self.node_kf.setdefault(leaf, {})
+            e = entries.get(kf_id)
+            if e is None:
+                e = entries[kf_id] = [np.float32(0), []]
+                fresh.append(e)
+            e[1].append(i)
+            e[0] = np.float32(e[0] + self.weights[leaf])
+            total = np.float32(total + self.weights[leaf])
+        if total == 0:
+            return
+        for e in fresh:
+            e[0] = np.float32(e[0] / total)
+        self.image_set.add(kf_id)
+
+    AddImage = InsertDescriptors
+
+    def RemoveImage(self, kf_id: int) -> None:
+        for entries in self.node_kf.values():
+            entries.pop(kf_id, None)
+        self.image_set.discard(kf_id)
+
+    def QueryFeatures(self, descriptor, kf_id: int) -> list:
+        """Feature indexes of keyframe kf_id in the descriptor's leaf."""
+        if kf_id not in self.image_set:
+            raise KeyError("QueryFeatures for a keyframe that is not in the BoW")
+        leaf = int(self.tree.find_leaves(descriptor)[0])
+        e = self.node_kf.get(leaf, {}).get(kf_id)
+        return [] if e is None else list(e[1])
+
+    def QueryUnknownImage(self, descriptors, max_results: int) -> list:
+        """[(keyframe id, score)] most similar first: L1 scoring of the normalised node values."""
+        leaves = self.tree.find_leaves(descriptors).tolist()
+        cur: dict = {}
+        total = np.float32(0)
+        for leaf in leaves:
+            w = self.weights[leaf]
+            cur[leaf] = np.float32(cur[leaf] + w) if leaf in cur else w
+            total = np.float32(total + w)
+        if total == 0:
+            return []
+        for leaf in cur:
+            cur[leaf] = np.float32(cur[leaf] / total)
+        score: dict = {}
+        for leaf in sorted(cur):
+            a = cur[leaf]
+            entries = self.node_kf.get(leaf, {})
+            for kf in sorted(entries):
+                b = entries[kf][0]
+                v = np.float32(np.float32(np.abs(np.float32(a - b)) - np.abs(a)) - np.abs(b))
+                score[kf] = np.float32(score[kf] + v) if kf in score else v
+        best = np.float32(0)
+        for kf in score:
+            score[kf] = np.float32(-score[kf] / np.float32(2.0))
+            if score[kf] > best:
+                best = score[kf]
+        q = np.float32(best * self.qualifying)
+        out = sorted(((kf, s) for kf, s in score.items() if s >= q), key=lambda t: (-t[1], t[0]))
+        return [(int(kf), float(s)) for kf, s in out[:max_results]]

@@ -458,3 +458,93 @@ class BundlerOracle:
     def perturb_point(self, p, u):
         u = np.ascontiguousarray(u, np.float64)
         lib().oracle_ba_perturb_point(self.h, p, _p(u))
+
+
+class OnlineBowOracle:
+    """Literal restatement of OnlineBow's keyframe database (OnlineBow.cpp:94-271, 340-449) over an
+    oracle tree (bow_train / FindLeafNode in C), float32 throughout.  Test infrastructure only.
+    Canonical orders where the reference iterates unordered_maps: ascending node and keyframe id;
+    equal scores keep ascending keyframe id (std::sort is unstable)."""
+
+    def __init__(self, tree, qualifying_candidate_score=0.75):
+        self.tree = tree
+        self.nodes_weight = [np.float32(0)] * len(tree[0])
+        self.m_NodeKeyframeMap = {}
+        self.m_imageSet = set()
+        self.QualifyingCandidateScore = np.float32(qualifying_candidate_score)
+
+    def FindLeafNode(self, desc):
+        return int(bow_find_leaves(self.tree, np.asarray(desc, np.uint8).reshape(1, 32))[0])
+
+    def SetNodeWeights(self, training_features, descriptorsCount):  # :340-394
+        nImages = len(descriptorsCount)
+        leafNodeImageMap = {}
+        start = 0
+        leaves = bow_find_leaves(self.tree, training_features)
+        for imageIndex in range(nImages):
+            leafNodeFound = set()
+            for j in range(int(descriptorsCount[imageIndex])):
+                leafNodeID = int(leaves[start + j])
+                if leafNodeID not in leafNodeFound:
+                    leafNodeImageMap[leafNodeID] = leafNodeImageMap.get(leafNodeID, 0) + 1
+                    leafNodeFound.add(leafNodeID)
+            start += int(descriptorsCount[imageIndex])
+        for nodeId, count in leafNodeImageMap.items():
+            self.nodes_weight[nodeId] = np.float32(np.log(np.float32(np.float32(nImages + 1) / np.float32(count))))
+
+    def InsertDescriptors(self, kf, descriptors):  # :413-449
+        pts = []
+        s = np.float32(0)
+        leaves = bow_find_leaves(self.tree, descriptors)
+        for i in range(len(leaves)):
+            nodeId = int(leaves[i])
+            m = self.m_NodeKeyframeMap.setdefault(nodeId, {})
+            if kf not in m:
+                m[kf] = {"nodeValue": np.float32(0), "indexes": []}
+                pts.append(m[kf])
+            m[kf]["indexes"].append(i)
+            m[kf]["nodeValue"] = np.float32(m[kf]["nodeValue"] + self.nodes_weight[nodeId])
+            s = np.float32(s + self.nodes_weight[nodeId])
+        if s == 0:
+            return
+        for p in pts:
+            p["nodeValue"] = np.float32(p["nodeValue"] / s)
+        self.m_imageSet.add(kf)
+
+    def RemoveImage(self, kf):  # :100-113
+        for m in self.m_NodeKeyframeMap.values():
+            m.pop(kf, None)
+        self.m_imageSet.discard(kf)
+
+    def QueryFeatures(self, desc, kf):  # :115-133
+        e = self.m_NodeKeyframeMap.get(self.FindLeafNode(desc), {}).get(kf)
+        return [] if e is None else list(e["indexes"])
+
+    def QueryUnknownImage(self, descriptors, maxResults):  # :155-271
+        curMap = {}
+        s = np.float32(0)
+        for leaf in bow_find_leaves(self.tree, descriptors):
+            w = self.nodes_weight[int(leaf)]
+            curMap[int(leaf)] = np.float32(curMap[int(leaf)] + w) if int(leaf) in curMap else w
+            s = np.float32(s + w)
+        if s == 0:
+            return []
+        for k in curMap:
+            curMap[k] = np.float32(curMap[k] / s)
+        scores = {}
+        for nodeId in sorted(curMap):
+            imageNodeValue = curMap[nodeId]
+            for kf in sorted(self.m_NodeKeyframeMap.get(nodeId, {})):
+                keyFrameNodeValue = self.m_NodeKeyframeMap[nodeId][kf]["nodeValue"]
+                value = np.float32(np.float32(np.abs(np.float32(imageNodeValue - keyFrameNodeValue)) - np.abs(imageNodeValue))
+                                   - np.abs(keyFrameNodeValue))
+                scores[kf] = np.float32(scores[kf] + value) if kf in scores else value
+        maxScore = np.float32(0)
+        for kf in scores:
+            scores[kf] = np.float32(-scores[kf] / np.float32(2.0))
+            if scores[kf] > maxScore:
+                maxScore = scores[kf]
+        qualifyingScore = np.float32(maxScore * self.QualifyingCandidateScore)
+        v = [(kf, sc) for kf, sc in scores.items() if sc >= qualifyingScore]
+        v.sort(key=lambda t: (-t[1], t[0]))
+        return [(int(kf), float(sc)) for kf, sc in v[:maxResults]]

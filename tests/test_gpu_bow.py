@@ -164,3 +164,36 @@ def test_indexed_and_radius_large_sets(gpu, oracle):
     got = matcher.RadiusMatch(kb, db, ka, da, 15.0)
     ref = oracle.radius_match(kb, db, ka, da, 15.0)
     assert len(got) > 0 and np.array_equal(got.view(np.uint8), ref.view(np.uint8))
+
+
+def test_online_bow_weights_insert_query_parity(gpu, oracle):
+    """OnlineBow's keyframe database (SetNodeWeights, InsertDescriptors, QueryFeatures,
+    QueryUnknownImage, RemoveImage) with GPU leaf descent vs the oracle's literal restatement:
+    identical IDF weights, node values, query results and scores (float32, canonical orders)."""
+    from mageslam_amd import orb
+
+    det = orb.OrbDetector(nfeatures=2000)
+    train = [det.DetectAndCompute(synth.frame(t, 640, 480))[1] for t in range(15)]
+    counts = [len(d) for d in train]
+    g = bow.OnlineBow.CreateTree(np.concatenate(train), counts)
+    o = oracle.OnlineBowOracle(oracle.bow_train(np.concatenate(train)))
+    o.SetNodeWeights(np.concatenate(train), counts)
+    assert np.array_equal(g.weights, np.array(o.nodes_weight, np.float32))
+    assert (g.weights > 0).sum() > 10
+    kfs = {kf: det.DetectAndCompute(synth.frame(40 + 7 * kf, 640, 480))[1] for kf in range(6)}
+    for kf, d in kfs.items():
+        g.InsertDescriptors(kf, d)
+        o.InsertDescriptors(kf, d)
+    for leaf, entries in o.m_NodeKeyframeMap.items():
+        for kf, e in entries.items():
+            assert g.node_kf[leaf][kf][0] == e["nodeValue"] and g.node_kf[leaf][kf][1] == e["indexes"]
+    for kf in (0, 3, 5):
+        rg = g.QueryUnknownImage(kfs[kf], 4)
+        ro = o.QueryUnknownImage(kfs[kf], 4)
+        assert rg == ro and rg[0][0] == kf and abs(rg[0][1] - 1.0) < 1e-4, (kf, rg)
+        q = kfs[kf][17]
+        assert g.QueryFeatures(q, kf) == o.QueryFeatures(q, kf) and 17 in g.QueryFeatures(q, kf)
+    g.RemoveImage(3)
+    o.RemoveImage(3)
+    assert g.QueryUnknownImage(kfs[3], 6) == o.QueryUnknownImage(kfs[3], 6)
+    assert all(kf != 3 for kf, _ in g.QueryUnknownImage(kfs[3], 6))

@@ -654,3 +654,26 @@ def test_undistort_map_inverts_points(oracle, dist):
     back = oracle.undistort_points(q, kd, np.float32(dist), kn)
     err = np.hypot(back[:, 0] - xs.ravel(), back[:, 1] - ys.ravel())
     assert err.max() < 0.05, err.max()
+
+
+def test_online_bow_oracle_database(oracle):
+    """The oracle's OnlineBow database on random descriptors: IDF weights (a leaf every training
+    image reaches gets log((n + 1) / n)), an image queried with its own descriptors scores 1 and
+    ranks first, QueryFeatures returns the inserted index, removed keyframes drop out."""
+    rng = np.random.default_rng(5)
+    train = rng.integers(0, 256, (6 * 200, 32), dtype=np.uint8)
+    o = oracle.OnlineBowOracle(oracle.bow_train(train, levels=2, branching=4, max_iter=6))
+    o.SetNodeWeights(train, [200] * 6)
+    w = np.array(o.nodes_weight, np.float32)
+    leaves = oracle.bow_find_leaves(o.tree, train)
+    for leaf in set(leaves.tolist()):
+        n_img = len({i // 200 for i in np.flatnonzero(leaves == leaf)})
+        assert w[leaf] == np.float32(np.log(np.float32(7) / np.float32(n_img)))
+    imgs = {kf: rng.integers(0, 256, (150, 32), dtype=np.uint8) for kf in range(4)}
+    for kf, d in imgs.items():
+        o.InsertDescriptors(kf, d)
+    r = o.QueryUnknownImage(imgs[2], 3)
+    assert r[0][0] == 2 and abs(r[0][1] - 1.0) < 1e-5
+    assert 11 in o.QueryFeatures(imgs[1][11], 1)
+    o.RemoveImage(2)
+    assert all(kf != 2 for kf, _ in o.QueryUnknownImage(imgs[2], 4))
