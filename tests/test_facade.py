@@ -72,3 +72,39 @@ def test_facade_matches_python_api(gpu, tmp_path):
     assert ni == len(bow.IndexedMatch(tree, pd, pd))
     nt = int(np.frombuffer(data[20 + 60 * n:24 + 60 * n], np.uint32)[0])
     assert nt == len(bow.IndexedMatch(bow.OnlineBowTree.CreateTree(pd), pd, pd))
+
+
+def test_bundler_step_argument_reuse(monkeypatch):
+    """StepBundleAdjustment reuses its huber array and outlier buffer across calls (no GPU: the
+    library call is stubbed): a changed huber schedule must reach the library, and the outliers
+    the library reports are appended in order."""
+    import ctypes as C
+
+    from mageslam_amd import bundler
+
+    seen = []
+
+    class Lib:
+        def mage_ba_step(self, h, hw, nhw, maxerr, out, cap, n_ref, ms_ref):
+            arr = (C.c_float * nhw).from_address(hw.value)
+            seen.append((list(arr), maxerr))
+            outs = (C.c_uint32 * cap).from_address(out.value)
+            k = len(seen)  # call k reports k outliers: 10, 11, ...
+            for i in range(k):
+                outs[i] = 10 + i
+            C.cast(n_ref, C.POINTER(C.c_uint32))[0] = k
+            C.cast(ms_ref, C.POINTER(C.c_float))[0] = 0.5 * k
+            return 0
+
+    monkeypatch.setattr(bundler._lib, "load", lambda: Lib())
+    b = bundler.BundlerLib.__new__(bundler.BundlerLib)
+    b._obs = {"cam": np.zeros(16, np.uint32)}
+    b._upload = lambda: None
+    b._h = C.c_void_p(0)
+    o1, o2, o3 = [], [], []
+    assert b.StepBundleAdjustment([1.8], 7.25, o1) == 0.5
+    assert b.StepBundleAdjustment([1.8], 7.25, o2) == 1.0
+    assert b.StepBundleAdjustment(np.array([4.0, 0.9], np.float32), 20.25, o3) == 1.5
+    assert [s[0] for s in seen] == [[np.float32(1.8)], [np.float32(1.8)], [4.0, np.float32(0.9)]]
+    assert [s[1] for s in seen] == [7.25, 7.25, 20.25]
+    assert o1 == [10] and o2 == [10, 11] and o3 == [10, 11, 12]
