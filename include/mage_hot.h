@@ -262,10 +262,16 @@ mage_status mage_bow_create(const uint8_t* node_desc, const uint32_t* child_star
  * KmeanCenter (:551-585) and FindCluster (:631-638) — the clustering iterations run on the GPU,
  * every node of a tree level at once.  levels / branching / max_iter = BagOfWordsSettings
  * TrainingTreeLevels / TrainingTreeBranchingFactor / MaxTrainingIteration (MageSettings.h:230-232;
- * branching <= 16 here).  Node ids follow the reference's recursion.  SetNodeWeights (IDF, used by
- * place recognition only) is not computed. */
+ * branching <= 16 here).  Node ids follow the reference's recursion.  SetNodeWeights (IDF) is host
+ * bookkeeping over mage_bow_find_leaves (mageslam_amd/bow.py OnlineBow). */
 mage_status mage_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
                            int device, mage_bow** out);
+/* The same tree built by OnlineBow::Kmedoid (OnlineBow.cpp:487-521, IterateClusteringKmedoid
+ * :590-639) instead of Kmean: every node is the member of its group with the first smallest sum of
+ * distances to the group (an empty group keeps its medoid; the reference reads past an empty
+ * vector there). */
+mage_status mage_bow_train_kmedoid(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching,
+                                   uint32_t max_iter, int device, mage_bow** out);
 /* The tree of `bow` (node_desc n x 32, child_start n + 1, children n - 1); MAGE_ECAPACITY with
  * *n_nodes set when cap_nodes is too small. */
 mage_status mage_bow_get_tree(mage_bow* bow, uint8_t* node_desc, uint32_t* child_start, uint32_t* children,

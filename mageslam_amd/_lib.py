@@ -29,7 +29,7 @@ EXPORTS = [
     "mage_undistort_image_batch_device",
     "mage_hamming_distance", "mage_hamming_match", "mage_hamming_match_batch_device",
     "mage_radius_match", "mage_radius_match_batch_device",
-    "mage_bow_create", "mage_bow_destroy", "mage_bow_train", "mage_bow_get_tree", "mage_bow_find_leaves", "mage_bow_find_leaves_device",
+    "mage_bow_create", "mage_bow_destroy", "mage_bow_train", "mage_bow_train_kmedoid", "mage_bow_get_tree", "mage_bow_find_leaves", "mage_bow_find_leaves_device",
     "mage_indexed_match", "mage_indexed_match_batch_device",
     "mage_ba_create", "mage_ba_destroy", "mage_ba_set_cameras", "mage_ba_fix_camera",
     "mage_ba_set_points", "mage_ba_set_observations", "mage_ba_set_lambda", "mage_ba_get_lambda",
@@ -178,6 +178,7 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_bow_create", st, vp, vp, vp, u32, C.c_int, C.POINTER(vp))
     sig("mage_bow_destroy", st, vp)
     sig("mage_bow_train", st, vp, u32, u32, u32, u32, C.c_int, C.POINTER(vp))
+    sig("mage_bow_train_kmedoid", st, vp, u32, u32, u32, u32, C.c_int, C.POINTER(vp))
     sig("mage_bow_get_tree", st, vp, vp, vp, vp, u32, C.POINTER(u32))
     sig("mage_bow_find_leaves", st, vp, vp, u32, vp)
     sig("mage_bow_find_leaves_device", st, vp, vp, u32, vp, vp)

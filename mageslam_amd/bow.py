@@ -35,14 +35,15 @@ class OnlineBowTree:
 
     @classmethod
     def CreateTree(cls, descriptors, levels: int = 2, branching: int = 6, max_iter: int = 12,
-                   device: int = 0) -> "OnlineBowTree":
+                   device: int = 0, kmedoid: bool = False) -> "OnlineBowTree":
         """OnlineBow::CreateTree (OnlineBow.cpp:325-337) on the GPU: hierarchical Kmean over the
         training descriptors with BagOfWordsSettings TrainingTreeLevels / TrainingTreeBranchingFactor
-        / MaxTrainingIteration (MageSettings.h:230-232)."""
+        / MaxTrainingIteration (MageSettings.h:230-232); kmedoid: the Kmedoid recursion (:487-521)."""
         d = np.ascontiguousarray(descriptors, np.uint8).reshape(-1, 32)
         self = cls.__new__(cls)
         self._h = C.c_void_p()
-        check(_lib.load().mage_bow_train(ptr(d), len(d), levels, branching, max_iter, device, C.byref(self._h)))
+        train = _lib.load().mage_bow_train_kmedoid if kmedoid else _lib.load().mage_bow_train
+        check(train(ptr(d), len(d), levels, branching, max_iter, device, C.byref(self._h)))
         self._nd, self._cs, self._ch = self.tree()
         return self
 

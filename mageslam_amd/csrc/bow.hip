@@ -446,6 +446,94 @@ __global__ __launch_bounds__(256) void km_update_kernel(KmParams p)
     }
 }
 
+
+// Kmedoid's update (IterateClusteringKmedoid, OnlineBow.cpp:608-637): the member of a group with
+// the first smallest sum of Hamming distances to all members becomes the medoid.  The reference's
+// O(g^2) scan is linear here: with c_b the number of members with bit b set (km_assign_kernel's
+// KmeanCenter counts) and m the group size, member i's sum is sum_b (bit_ib ? m - c_b : c_b) =
+// sum_b c_b + sum over its set bits of (m - 2 c_b), exact in integers.  Entries of a slot are in
+// group order, so the smallest (sum, entry) key is the reference's first minimum.  An empty group
+// (the reference reads groups[g][0] of an empty vector) keeps its medoid.  Then the same
+// bookkeeping as km_update_kernel: counts reset, changed test, iteration count and exit rule.
+__global__ __launch_bounds__(256) void km_medoid_kernel(KmParams p)
+{
+    __shared__ int wtab[KM_MAXB][256];
+    __shared__ int base[KM_MAXB];
+    __shared__ unsigned long long best[KM_MAXB][4];
+    __shared__ uint32_t changed;
+    const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (p.state[2 * s + 1]) return;
+    const int k = (int)p.ncent[s];
+    uint32_t* gc = p.counts + (size_t)s * KM_MAXB * 256;
+    for (int c = 0; c < k; c++) {
+        const int m = (int)p.members[s * KM_MAXB + c], cb = (int)gc[c * 256 + t];
+        wtab[c][t] = m - 2 * cb;
+        // base[c] = sum_b c_b: one wave-reduced partial per wave
+        int v = cb;
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) best[c][wave] = (unsigned long long)(uint32_t)v;  // reuse as scratch
+    }
+    if (t == 0) changed = 0;
+    __syncthreads();
+    if (t < k) base[t] = (int)(best[t][0] + best[t][1] + best[t][2] + best[t][3]);
+    __syncthreads();
+    unsigned long long mine[KM_MAXB];
+#pragma unroll
+    for (int c = 0; c < KM_MAXB; c++) mine[c] = ~0ull;
+    const uint32_t e0 = s ? p.slot_end[s - 1] : 0, e1 = p.slot_end[s];
+    for (uint32_t e = e0 + t; e < e1; e += 256) {
+        const int c = (int)p.assign[e];
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(p.desc + 32ull * p.entry_desc[e]);
+        int cost = base[c];
+        for (int w = 0; w < 8; w++) {
+            uint32_t x = d[w];
+            while (x) {
+                cost += wtab[c][32 * w + __builtin_ctz(x)];
+                x &= x - 1u;
+            }
+        }
+        const unsigned long long key = ((unsigned long long)(uint32_t)cost << 32) | (e - e0);
+#pragma unroll
+        for (int g = 0; g < KM_MAXB; g++)
+            if (g == c && key < mine[g]) mine[g] = key;
+    }
+    __syncthreads();  // best[] was scratch above
+#pragma unroll
+    for (int c = 0; c < KM_MAXB; c++) {
+        if (c >= k) break;
+        unsigned long long v = mine[c];
+        for (int o = 32; o >= 1; o >>= 1) {
+            const unsigned long long u = __shfl_xor(v, o);
+            v = u < v ? u : v;
+        }
+        if (lane == 0) best[c][wave] = v;
+    }
+    __syncthreads();
+    unsigned long long* cen = reinterpret_cast<unsigned long long*>(p.centers + (size_t)s * KM_MAXB * 32);
+    if (t < k) {
+        unsigned long long v = best[t][0];
+        for (int w = 1; w < 4; w++) v = best[t][w] < v ? best[t][w] : v;
+        if (p.members[s * KM_MAXB + t] > 0 && v != ~0ull) {
+            const uint32_t e = e0 + (uint32_t)(v & 0xFFFFFFFFull);
+            const unsigned long long* d = reinterpret_cast<const unsigned long long*>(p.desc + 32ull * p.entry_desc[e]);
+            bool diff = false;
+            for (int q = 0; q < 4; q++) diff |= d[q] != cen[4 * t + q];
+            if (diff) {
+                for (int q = 0; q < 4; q++) cen[4 * t + q] = d[q];
+                atomicAdd(&changed, 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = 0; c < k; c++) gc[c * 256 + t] = 0;
+    if (t == 0) {
+        for (int c = 0; c < k; c++) p.members[s * KM_MAXB + c] = 0;
+        const uint32_t it = p.state[2 * s] + 1;
+        p.state[2 * s] = it;
+        if (!(it < p.max_iter && changed > 0)) p.state[2 * s + 1] = 1;
+    }
+}
+
 // std::shuffle(refs, mt19937{}) as the reference's MSVC STL computes it (InitializeTraining,
 // OnlineBow.cpp:404): a fresh default-seeded engine per call, target t swapped with a draw in
 // [0, t] from _Rng_from_urng (one 32-bit output per draw for sizes < 2^32, rejection of the biased
@@ -673,12 +761,13 @@ mage_status mage_indexed_match_batch_device(const uint8_t* d_desc_a, const uint3
 
 }  // extern "C"
 
-extern "C" {
+namespace mage {
+namespace {
 
-mage_status mage_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
-                           int device, mage_bow** out)
+// OnlineBow::CreateTree's recursion with Kmean (medoid = false) or Kmedoid (medoid = true)
+mage_status bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
+                      int device, bool medoid, mage_bow** out)
 {
-    using namespace mage;
     MAGE_REQUIRE(out, MAGE_EINVAL, "null output");
     *out = nullptr;
     MAGE_REQUIRE(n == 0 || desc, MAGE_EINVAL, "null descriptors");
@@ -766,7 +855,10 @@ mage_status mage_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uin
         for (uint32_t it = 0; it < std::max(max_iter, 1u); it++) {
             launch("bow.km_assign", km_assign_kernel, dim3(B), dim3(KM_THREADS), 0, st, p);
             if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
-            launch("bow.km_update", km_update_kernel, dim3(S), dim3(256), 0, st, p);
+            if (medoid)
+                launch("bow.km_medoid", km_medoid_kernel, dim3(S), dim3(256), 0, st, p);
+            else
+                launch("bow.km_update", km_update_kernel, dim3(S), dim3(256), 0, st, p);
             if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
         }
         std::vector<uint32_t> assign(E);
@@ -816,6 +908,23 @@ mage_status mage_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uin
     }
     cs[N] = (uint32_t)ch.size();
     return mage_bow_create(nd.data(), cs.data(), ch.empty() ? nullptr : ch.data(), N, device, out);
+}
+
+}  // namespace
+}  // namespace mage
+
+extern "C" {
+
+mage_status mage_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
+                           int device, mage_bow** out)
+{
+    return mage::bow_train(desc, n, levels, branching, max_iter, device, false, out);
+}
+
+mage_status mage_bow_train_kmedoid(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching,
+                                   uint32_t max_iter, int device, mage_bow** out)
+{
+    return mage::bow_train(desc, n, levels, branching, max_iter, device, true, out);
 }
 
 mage_status mage_bow_get_tree(mage_bow* b, uint8_t* node_desc, uint32_t* child_start, uint32_t* children,

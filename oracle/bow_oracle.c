@@ -257,8 +257,32 @@ static void kmean_center(const uint8_t* descs, const uint32_t* idx, uint32_t cnt
         }
 }
 
+/* IterateClusteringKmedoid's update (OnlineBow.cpp:608-637), literally: the member with the
+ * first smallest sum of distances to all members of its group becomes the medoid.  An empty
+ * group (the reference would read groups[g][0] of an empty vector) keeps its medoid. */
+static int kmedoid_update(const uint8_t* descs, const uint32_t* idx, uint32_t cnt, uint8_t* c)
+{
+    if (cnt == 0) return 0;
+    long long minD = 0x7FFFFFFFFFFFFFFFll;
+    uint32_t minI = 0;
+    for (uint32_t i = 0; i < cnt; i++) {
+        long long distance = 0;
+        for (uint32_t k = 0; k < cnt; k++) distance += oracle_hamming(descs + 32ull * idx[i], descs + 32ull * idx[k]);
+        if (distance < minD) {
+            minD = distance;
+            minI = i;
+        }
+    }
+    if (oracle_hamming(descs + 32ull * idx[minI], c) != 0) {
+        memcpy(c, descs + 32ull * idx[minI], 32);
+        return 1;
+    }
+    return 0;
+}
+
+/* Kmean (OnlineBow.cpp:451-485) or, with medoid, Kmedoid (:487-521): the same recursion */
 static void kmean(bow_tree_t* t, uint32_t parent, const uint8_t* descs, uint32_t n, uint32_t level, uint32_t levels,
-                  uint32_t branching, uint32_t max_iter)
+                  uint32_t branching, uint32_t max_iter, int medoid)
 {
     uint32_t* perm = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
     oracle_msvc_shuffle(n, perm);
@@ -286,6 +310,10 @@ static void kmean(bow_tree_t* t, uint32_t parent, const uint8_t* descs, uint32_t
             free(fill);
         }
         for (uint32_t g = 0; g < k; g++) {
+            if (medoid) {
+                changed += (uint32_t)kmedoid_update(descs, gidx + gstart[g], gstart[g + 1] - gstart[g], centers + 32 * g);
+                continue;
+            }
             uint8_t pre[32];
             memcpy(pre, centers + 32 * g, 32);
             kmean_center(descs, gidx + gstart[g], gstart[g + 1] - gstart[g], centers + 32 * g);
@@ -304,7 +332,7 @@ static void kmean(bow_tree_t* t, uint32_t parent, const uint8_t* descs, uint32_t
             if (cnt > 1) {
                 uint8_t* sub = (uint8_t*)malloc(32ull * cnt);
                 for (uint32_t i = 0; i < cnt; i++) memcpy(sub + 32ull * i, descs + 32ull * gidx[gstart[g] + i], 32);
-                kmean(t, ids[g], sub, cnt, level + 1, levels, branching, max_iter);
+                kmean(t, ids[g], sub, cnt, level + 1, levels, branching, max_iter, medoid);
                 free(sub);
             }
         }
@@ -319,13 +347,13 @@ static void kmean(bow_tree_t* t, uint32_t parent, const uint8_t* descs, uint32_t
 
 /* CreateTree over n descriptors: fills node_desc (cap nodes), child_start (n_nodes + 1) and
  * children (n_nodes - 1); returns the node count (0 when it exceeds cap). */
-uint32_t oracle_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
-                          uint8_t* node_desc, uint32_t* child_start, uint32_t* children, uint32_t cap)
+uint32_t oracle_bow_train2(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
+                           uint8_t* node_desc, uint32_t* child_start, uint32_t* children, uint32_t cap, int medoid)
 {
     bow_tree_t t = {0};
     static const uint8_t zero[32] = {0};
     tree_add(&t, zero); /* Node(0): the root's descriptor is never compared */
-    if (n > 0) kmean(&t, 0, desc, n, 1, levels, branching, max_iter);
+    if (n > 0) kmean(&t, 0, desc, n, 1, levels, branching, max_iter, medoid);
     uint32_t out = 0;
     if (t.n <= cap) {
         uint32_t c = 0;
@@ -342,4 +370,10 @@ uint32_t oracle_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint
     free(t.nkids);
     free(t.desc);
     return out;
+}
+
+uint32_t oracle_bow_train(const uint8_t* desc, uint32_t n, uint32_t levels, uint32_t branching, uint32_t max_iter,
+                          uint8_t* node_desc, uint32_t* child_start, uint32_t* children, uint32_t cap)
+{
+    return oracle_bow_train2(desc, n, levels, branching, max_iter, node_desc, child_start, children, cap, 0);
 }

@@ -105,6 +105,8 @@ def _declare(L):
     L.oracle_indexed_match.restype = u32
     L.oracle_bow_train.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, u32]
     L.oracle_bow_train.restype = u32
+    L.oracle_bow_train2.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, u32, C.c_int]
+    L.oracle_bow_train2.restype = u32
     L.oracle_msvc_shuffle.argtypes = [u32, vp]
     L.oracle_mt19937_first.argtypes = [u32, u32]
     L.oracle_mt19937_first.restype = u32
@@ -289,9 +291,10 @@ def bow_find_leaves(tree, desc):
     return np.array([lib().oracle_bow_find_leaf(_p(nd), _p(cs), _p(ch), _p(d[i])) for i in range(len(d))], np.uint32)
 
 
-def bow_train(desc, levels=2, branching=6, max_iter=12):
-    """OnlineBow::CreateTree (OnlineBow.cpp:325-337, Kmean :451-485) over training descriptors
-    (BagOfWordsSettings defaults, MageSettings.h:230-232); returns (node_desc, child_start, children)."""
+def bow_train(desc, levels=2, branching=6, max_iter=12, kmedoid=False):
+    """OnlineBow::CreateTree (OnlineBow.cpp:325-337, Kmean :451-485; with kmedoid the Kmedoid
+    recursion :487-521) over training descriptors (BagOfWordsSettings defaults, MageSettings.h:
+    230-232); returns (node_desc, child_start, children)."""
     d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
     cap = 1
     for _ in range(levels):
@@ -299,7 +302,7 @@ def bow_train(desc, levels=2, branching=6, max_iter=12):
     nd = np.zeros((cap, 32), np.uint8)
     cs = np.zeros(cap + 1, np.uint32)
     ch = np.zeros(max(cap, 1), np.uint32)
-    n = lib().oracle_bow_train(_p(d), len(d), levels, branching, max_iter, _p(nd), _p(cs), _p(ch), cap)
+    n = lib().oracle_bow_train2(_p(d), len(d), levels, branching, max_iter, _p(nd), _p(cs), _p(ch), cap, int(kmedoid))
     assert n > 0
     return nd[:n].copy(), cs[: n + 1].copy(), ch[: int(cs[n])].copy()
 

@@ -197,3 +197,27 @@ def test_online_bow_weights_insert_query_parity(gpu, oracle):
     o.RemoveImage(3)
     assert g.QueryUnknownImage(kfs[3], 6) == o.QueryUnknownImage(kfs[3], 6)
     assert all(kf != 3 for kf, _ in g.QueryUnknownImage(kfs[3], 6))
+
+
+@pytest.mark.parametrize("levels,branching,max_iter", [(2, 6, 12), (3, 4, 8), (1, 16, 5)])
+def test_create_tree_kmedoid_parity(gpu, oracle, frames, levels, branching, max_iter):
+    """OnlineBow::Kmedoid (OnlineBow.cpp:487-521): the GPU's linear medoid selection (per-bit
+    member counts) gives the same tree as the oracle's literal O(g^2) IterateClusteringKmedoid."""
+    descs, _ = frames
+    d = np.concatenate(descs[:2])
+    t = bow.OnlineBowTree.CreateTree(d, levels, branching, max_iter, kmedoid=True)
+    ref = oracle.bow_train(d, levels, branching, max_iter, kmedoid=True)
+    for x, y in zip(t.tree(), ref):
+        assert np.array_equal(x, y)
+    rows = {bytes(r) for r in d}
+    assert all(bytes(r) in rows for r in t.tree()[0][1:])  # every node is a training descriptor
+
+
+def test_create_tree_kmedoid_training_frames(gpu, oracle):
+    from mageslam_amd import orb
+
+    det = orb.OrbDetector(nfeatures=2000)
+    d = np.concatenate([det.DetectAndCompute(synth.frame(t, 640, 480))[1] for t in range(6)])
+    t = bow.OnlineBowTree.CreateTree(d, kmedoid=True)
+    for x, y in zip(t.tree(), oracle.bow_train(d, kmedoid=True)):
+        assert np.array_equal(x, y)

@@ -677,3 +677,23 @@ def test_online_bow_oracle_database(oracle):
     assert 11 in o.QueryFeatures(imgs[1][11], 1)
     o.RemoveImage(2)
     assert all(kf != 2 for kf, _ in o.QueryUnknownImage(imgs[2], 4))
+
+
+def test_bow_train_kmedoid_oracle(oracle):
+    """The oracle's Kmedoid tree: every node a training descriptor and, once the loop has
+    converged, each medoid minimises the summed distances over the group assigned to it (numpy)."""
+    rng = np.random.default_rng(9)
+    d = rng.integers(0, 256, (400, 32), dtype=np.uint8)
+    nd, cs, ch = oracle.bow_train(d, levels=1, branching=5, max_iter=100, kmedoid=True)
+    rows = [bytes(r) for r in d]
+    assert all(bytes(r) in set(rows) for r in nd[1:])
+    bits = np.unpackbits(d, axis=1).astype(np.int64)
+    dist = (bits[:, None, :] != np.unpackbits(nd[1:], axis=1)[None, :, :]).sum(2)
+    g = dist.argmin(1)  # FindCluster: first smallest distance
+    for c in range(len(nd) - 1):
+        mem = np.flatnonzero(g == c)
+        if len(mem) == 0:
+            continue
+        sums = (bits[mem][:, None, :] != bits[mem][None, :, :]).sum((1, 2))
+        med = [k for k, m in enumerate(mem) if rows[m] == bytes(nd[1 + c])]
+        assert med and sums[med[0]] == sums.min()
