@@ -221,3 +221,26 @@ def test_create_tree_kmedoid_training_frames(gpu, oracle):
     t = bow.OnlineBowTree.CreateTree(d, kmedoid=True)
     for x, y in zip(t.tree(), oracle.bow_train(d, kmedoid=True)):
         assert np.array_equal(x, y)
+
+
+def test_online_bow_query_edges(gpu, oracle, frames):
+    """QueryUnknownImage edge cases against the oracle: an empty query, maxResults truncation, the
+    QualifyingCandidateScore filter, and a keyframe inserted twice (only the first call's entries
+    are normalised, as in the reference)."""
+    descs, tree = frames
+    train = np.concatenate(descs[:2])
+    counts = [len(descs[0]), len(descs[1])]
+    g = bow.OnlineBow(bow.OnlineBowTree(*tree), qualifying_candidate_score=0.3)
+    o = oracle.OnlineBowOracle(tree, qualifying_candidate_score=0.3)
+    g.SetNodeWeights(train, counts)
+    o.SetNodeWeights(train, counts)
+    assert g.QueryUnknownImage(descs[2][:0], 5) == o.QueryUnknownImage(descs[2][:0], 5) == []
+    for kf, d in enumerate(descs):
+        g.InsertDescriptors(kf, d)
+        o.InsertDescriptors(kf, d)
+    g.InsertDescriptors(1, descs[3][:50])
+    o.InsertDescriptors(1, descs[3][:50])
+    for q in (descs[0], descs[3][:300]):
+        for m in (1, 2, 10):
+            assert g.QueryUnknownImage(q, m) == o.QueryUnknownImage(q, m)
+    assert len(g.QueryUnknownImage(descs[0], 1)) == 1
