@@ -11,6 +11,7 @@ descriptors passed directly.
 from __future__ import annotations
 
 import ctypes as C
+import math
 
 import numpy as np
 
@@ -155,7 +156,7 @@ class OnlineBow:
             start += int(c)
         n_images = len(descriptors_count)
         for leaf, cnt in images.items():  # log((float)(nImages + 1) / (float)count), std::log(float)
-            self.weights[leaf] = np.log(np.float32(n_images + 1) / np.float32(cnt))
+            self.weights[leaf] = np.float32(math.log(float(np.float32(n_images + 1) / np.float32(cnt))))  # logf, correctly rounded
 
     def InsertDescriptors(self, kf_id: int, descriptors) -> None:
         leaves = self.tree.find_leaves(descriptors).tolist()

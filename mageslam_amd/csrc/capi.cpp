@@ -60,9 +60,54 @@ mage_status bind_device(int device)
     return MAGE_OK;
 }
 
+namespace {
+// Per-thread stream scratch (stream_scratch): keyed by (device, stream, slot) inside the calling
+// thread's own map, so a buffer is only ever grown — and its old storage freed — by the one thread
+// that hands it to its own launches.  Two threads on one stream get two buffers; their launches
+// are ordered by the stream, and neither can free memory the other still has to launch on.
+thread_local bool g_stream_scratch_alive = false;
+struct StreamScratchMap {
+    std::map<std::tuple<int, hipStream_t, int>, DeviceBuffer> bufs;
+    StreamScratchMap() { g_stream_scratch_alive = true; }
+    ~StreamScratchMap()
+    {
+        g_stream_scratch_alive = false;
+        // the streams may be gone by now (a caller's stream destroyed before its thread exits):
+        // wait for the device instead of per stream before the buffers are freed
+        if (!bufs.empty()) (void)hipDeviceSynchronize();
+        for (auto& kv : bufs) kv.second.release();
+    }
+};
+StreamScratchMap& stream_scratch_map()
+{
+    thread_local StreamScratchMap m;
+    return m;
+}
+
+// Drops the calling thread's stream scratch of `st` (before the stream is destroyed, so a later
+// stream that reuses the handle value starts without it).
+void release_stream_scratch(hipStream_t st)
+{
+    if (!g_stream_scratch_alive) return;  // the map was already destroyed at thread exit
+    auto& bufs = stream_scratch_map().bufs;
+    for (auto it = bufs.begin(); it != bufs.end();) {
+        if (std::get<1>(it->first) == st) {
+            it->second.release();
+            it = bufs.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+}  // namespace
+
 HostScratch::~HostScratch()
 {
-    if (st) (void)hipStreamDestroy(st);
+    if (st) {
+        (void)hipStreamSynchronize(st);
+        release_stream_scratch(st);
+        (void)hipStreamDestroy(st);
+    }
     buf.release();
     aux.release();
     host.release();
@@ -83,16 +128,14 @@ HostScratch* host_scratch(int device, ScratchSlot slot)
 
 void* stream_scratch(hipStream_t st, StreamSlot slot, size_t bytes)
 {
-    static std::mutex mu;
-    static std::map<std::tuple<int, hipStream_t, int>, DeviceBuffer> bufs;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) {
         set_error("hipGetDevice failed");
         return nullptr;
     }
-    std::lock_guard<std::mutex> lk(mu);
-    DeviceBuffer& b = bufs[std::make_tuple(dev, st, (int)slot)];
-    // growing frees the old buffer: let this stream's launches that still use it finish first
+    DeviceBuffer& b = stream_scratch_map().bufs[std::make_tuple(dev, st, (int)slot)];
+    // growing frees the old buffer: this thread's launches on the stream that still use it are
+    // the only ones that can (the buffer is private to the thread), let them finish first
     if (bytes > b.bytes && b.ptr && hipStreamSynchronize(st) != hipSuccess) {
         set_error("hipStreamSynchronize failed");
         return nullptr;

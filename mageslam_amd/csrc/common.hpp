@@ -116,9 +116,11 @@ struct HostScratch {
 // stream created; nullptr (and the error set) if the stream cannot be created.
 HostScratch* host_scratch(int device, ScratchSlot slot);
 
-// Device scratch private to one (current device, stream, slot) and at least `bytes` long:
-// kernels on different streams may run concurrently, so they never share it, while launches on
-// one stream are ordered.  nullptr (error set) if the allocation fails.
+// Device scratch private to one (calling thread, current device, stream, slot) and at least
+// `bytes` long: kernels on different streams may run concurrently, so they never share it, and a
+// thread that grows its buffer (sync of the stream, then free) can only free memory its own
+// launches used — never a pointer another thread is about to launch on.  Freed at thread exit or
+// when the stream's HostScratch is destroyed.  nullptr (error set) if the allocation fails.
 enum StreamSlot : int { STREAM_MATCH_ROWS = 0, STREAM_MATCH_STATUS = 1 };
 void* stream_scratch(hipStream_t st, StreamSlot slot, size_t bytes);
 

@@ -51,7 +51,7 @@ struct RadiusParams {
     int* res;  // per query: target << 9 | distance, or -1 (pairs x q_pitch)
     mage_dmatch* out;
     uint32_t* n_out;
-    uint32_t* status;  // bit 0: a target set exceeded RM_MAXT
+    uint32_t* status;  // bit 0: a target set exceeded RM_MAXT; bit 1: a count exceeded its pitch
 };
 
 __device__ __forceinline__ unsigned orderable(float v)
@@ -166,10 +166,11 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
         if (FUSED && tid == 0) p.n_out[pr] = 0;
         return;
     }
-    if (ntr > RM_MAXT) {
+    // a count above its pair's pitch would read the next pair's (or unallocated) entries
+    if (ntr > RM_MAXT || ntr > p.t_pitch || nq > p.q_pitch) {
         if (tid == 0 && blockIdx.y == 0) {
             p.n_out[pr] = 0;
-            atomicOr(p.status, 1u);
+            atomicOr(p.status, ntr > RM_MAXT ? 1u : 2u);
         }
         return;
     }
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_post_kernel(RadiusParams 
         if (threadIdx.x == 0) p.n_out[pr] = 0;
         return;
     }
-    if (ntr > RM_MAXT) return;
+    if (ntr > RM_MAXT || ntr > p.t_pitch || nq > p.q_pitch) return;
     radius_post(p, pr, p.res + pr * p.q_pitch, nq, ntr, bestD, cnt, wsum, s_base);
 }
 

@@ -166,11 +166,24 @@ __device__ void make_keyframe(const TrackBufs& b, const TrackConst& c, const mag
 }
 
 // Frame 0: its keyframe at the first pose (already in poses[0]).
-__global__ __launch_bounds__(TT) void trk_init(TrackBufs b, TrackConst c, const mage_keypoint* fk, const uint8_t* fd,
-                                               const uint32_t* nf, double* poses, uint32_t* matches,
-                                               uint32_t* inliers, uint8_t* keyframe)
+// A frame's keypoint count, clamped to the frame slot (`cap` keypoints): a larger count would copy
+// the next frame's (or unallocated) entries into the keyframe buffers, which hold `cap`; the
+// overflow is reported through status bit 1 (MAGE_ECAPACITY on return).
+__device__ uint32_t frame_count(const TrackConst& c, const uint32_t* nf, uint32_t* status)
 {
     const uint32_t n = *nf;
+    if (n > c.cap) {
+        if (threadIdx.x == 0) atomicOr(status, 2u);
+        return c.cap;
+    }
+    return n;
+}
+
+__global__ __launch_bounds__(TT) void trk_init(TrackBufs b, TrackConst c, const mage_keypoint* fk, const uint8_t* fd,
+                                               const uint32_t* nf, double* poses, uint32_t* matches,
+                                               uint32_t* inliers, uint8_t* keyframe, uint32_t* status)
+{
+    const uint32_t n = frame_count(c, nf, status);
     make_keyframe(b, c, fk, fd, n, load_pose(poses));
     if (threadIdx.x == 0) {
         b.ctl->kf_n = n;
@@ -295,7 +308,7 @@ __global__ __launch_bounds__(TT) void trk_filter(TrackBufs b)
 
 __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int f, const mage_keypoint* fk,
                                                  const uint8_t* fd, const uint32_t* nf, double* poses,
-                                                 uint32_t* inliers, uint8_t* keyframe)
+                                                 uint32_t* inliers, uint8_t* keyframe, uint32_t* status)
 {
     __shared__ uint32_t wsum[TT / 64];
     __shared__ int s_kf;
@@ -329,7 +342,7 @@ __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int 
     }
     __syncthreads();
     if (s_kf) {
-        const uint32_t n = *nf;
+        const uint32_t n = frame_count(c, nf, status);
         make_keyframe(b, c, fk, fd, n, load_pose(sP));
         if (threadIdx.x == 0) b.ctl->kf_n = n;
     }
@@ -429,7 +442,7 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     if (hipMemsetAsync(d, 0, off, st) != hipSuccess ||
         hipMemcpyAsync(dposes, first_pose, 96, hipMemcpyHostToDevice, st) != hipSuccess)
         return fail(MAGE_EDEVICE);
-    hipLaunchKernelGGL(trk_init, dim3(1), dim3(TT), 0, st, b, c, d_kp, d_desc, d_n, dposes, dmt, dil, dkf);
+    hipLaunchKernelGGL(trk_init, dim3(1), dim3(TT), 0, st, b, c, d_kp, d_desc, d_n, dposes, dmt, dil, dkf, rstatus);
     const float radius[3] = {s->search_radius, s->wider_search_radius, s->extra_wider_search_radius};
     for (uint32_t f = 1; f < frames; f++) {
         const mage_keypoint* fk = d_kp + (size_t)f * pitch;
@@ -454,7 +467,7 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
                                       s->final_huber, e2, b.pos3_o2, b.r9_o2, nullptr, b.out2, b.msq + 1, nullptr,
                                       stream);
         if (r != MAGE_OK) return fail(r);
-        launch("track.finish", trk_finish, dim3(1), dim3(TT), 0, st, b, c, (int)f, fk, fd, nf, dposes, dil, dkf);
+        launch("track.finish", trk_finish, dim3(1), dim3(TT), 0, st, b, c, (int)f, fk, fd, nf, dposes, dil, dkf, rstatus);
     }
     if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
     uint32_t rst = 0;
@@ -467,5 +480,6 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         return fail(MAGE_EDEVICE);
     buf.release();
     MAGE_REQUIRE(!(rst & 1u), MAGE_ECAPACITY, "a frame has more than 4096 keypoints");
+    MAGE_REQUIRE(!(rst & 2u), MAGE_ECAPACITY, "a frame's keypoint count exceeds the frame pitch");
     return MAGE_OK;
 }

@@ -7,6 +7,7 @@ Parity unpinned: see the headers of orb_oracle.c / ba_oracle.c and DESIGN.md §P
 from __future__ import annotations
 
 import ctypes as C
+import math
 import subprocess
 from pathlib import Path
 
@@ -67,6 +68,7 @@ def _p(a):
 def _declare(L):
     vp, i32, u32, f32 = C.c_void_p, C.c_int, C.c_uint32, C.c_float
     L.oracle_fast_score_map.argtypes = [vp, i32, i32, i32, i32, vp]
+    L.oracle_fast_score_map_sse2.argtypes = [vp, i32, i32, i32, i32, vp, vp]
     L.oracle_gaussian_blur.argtypes = [vp, i32, i32, i32, i32, vp]
     L.oracle_gaussian_taps.argtypes = [i32, C.c_double, vp]
     L.oracle_orb_detect.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, u32, C.POINTER(u32)]
@@ -200,6 +202,17 @@ def fast_score_map(img: np.ndarray, threshold: int = 4) -> np.ndarray:
     out = np.zeros((h, w), np.uint8)
     lib().oracle_fast_score_map(_p(img), w, h, w, threshold, _p(out))
     return out
+
+
+def fast_score_map_sse2(img: np.ndarray, threshold: int = 4):
+    """FAST_t<16> score map as the reference's x64 (SSE2) build computes it (fast_sse2.c):
+    (score map, per-row column where the 16-pixel SIMD loop handed over to the scalar tail)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((h, w), np.uint8)
+    cols = np.zeros(h, np.int32)
+    lib().oracle_fast_score_map_sse2(_p(img), w, h, w, threshold, _p(out), _p(cols))
+    return out, cols
 
 
 def gaussian_blur(img: np.ndarray, ksize: int = 7) -> np.ndarray:
@@ -493,7 +506,7 @@ class OnlineBowOracle:
                     leafNodeFound.add(leafNodeID)
             start += int(descriptorsCount[imageIndex])
         for nodeId, count in leafNodeImageMap.items():
-            self.nodes_weight[nodeId] = np.float32(np.log(np.float32(np.float32(nImages + 1) / np.float32(count))))
+            self.nodes_weight[nodeId] = np.float32(math.log(float(np.float32(np.float32(nImages + 1) / np.float32(count)))))  # logf, correctly rounded
 
     def InsertDescriptors(self, kf, descriptors):  # :413-449
         pts = []

@@ -38,8 +38,10 @@ static const int kRing16[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0}
 static int imin(int a, int b) { return a < b ? a : b; }
 static int imax(int a, int b) { return a > b ? a : b; }
 
-/* cornerScore<16>, scalar branch (OpenCVModified.cpp:1030-1064); equals the SSE2 branch for
- * every detected corner (VERIFY_SIMD, :1265-1271). */
+/* cornerScore<16>, scalar branch (OpenCVModified.cpp:1030-1064).  The x64 reference runs the
+ * SSE2 branches (:935-972, :1278-1338); oracle/fast_sse2.c restates them and
+ * tests/test_oracle.py::test_verify_simd_sse2_build_equals_scalar_oracle checks that the SSE2
+ * build's score map equals this scalar one (the reference's VERIFY_SIMD property, :1265-1271). */
 static int corner_score16(const uint8_t* p, const int pixel[25], int threshold)
 {
     int d[25];

@@ -79,6 +79,9 @@ def test_self_match_and_duplicates(gpu, oracle):
     det = orb.OrbDetector(nfeatures=2000)
     kp, d = det.DetectAndCompute(synth.frame(0, 640, 480))
     g = matcher.Match(d, d)
+    # C1 (BASELINE configs[0]): the full self-match byte for byte against the oracle, and the
+    # expected result — every keypoint matched to itself (no exact-duplicate descriptors here)
+    assert np.array_equal(dm_bytes(g), dm_bytes(oracle.match(d, d)))
     assert len(g) == len(d) and (g["query_idx"] == g["train_idx"]).all()
     dd = np.concatenate([d[:100], d[:100]])  # exact duplicates: delta 0 -> rejected both ways
     g2 = matcher.Match(dd, dd)

@@ -64,6 +64,50 @@ def test_concurrent_host_entry_points_match_single_thread(gpu):
         assert list(ex.map(worker, range(THREADS))) == [0] * THREADS
 
 
+def test_match_batch_device_threads_share_one_stream(gpu):
+    """Several host threads launch mage_hamming_match_batch_device on ONE stream with growing pair
+    counts: each growth of the per-stream scratch must never free a buffer another thread is about
+    to launch on (capi.cpp stream_scratch, keyed per thread)."""
+    import torch
+
+    det = orb.OrbDetector(nfeatures=2000)
+    feats = [det.DetectAndCompute(synth.frame(t, 640, 480)) for t in range(9)]
+    det.close()
+    N = 2000
+    desc = torch.zeros((9, N, 32), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(9, dtype=torch.int32, device="cuda")
+    for i, (_, d) in enumerate(feats):
+        desc[i, :len(d)] = torch.from_numpy(d)
+        cnt[i] = len(d)
+    shared = torch.cuda.Stream()
+
+    def run(pairs, stream):
+        out = torch.zeros((pairs, N * 16), dtype=torch.uint8, device="cuda")
+        nm = torch.zeros(pairs, dtype=torch.int32, device="cuda")
+        matcher.match_batch_device(desc[1:1 + pairs], N * 32, cnt[1:1 + pairs], desc[:pairs], N * 32, cnt[:pairs],
+                                   pairs, 30, 1, out, N, nm, stream=stream)
+        return out, nm
+
+    expect = {}
+    for p in range(1, 9):
+        out, nm = run(p, None)
+        torch.cuda.synchronize()
+        expect[p] = (out.cpu(), nm.cpu())
+
+    def worker(w):
+        bad = 0
+        for r in range(ROUNDS):
+            p = 1 + (w + r) % 8  # every thread walks its own growing / shrinking pair counts
+            with torch.cuda.stream(shared):
+                out, nm = run(p, shared.cuda_stream)
+            shared.synchronize()
+            bad += not (torch.equal(out.cpu(), expect[p][0]) and torch.equal(nm.cpu(), expect[p][1]))
+        return bad
+
+    with cf.ThreadPoolExecutor(THREADS) as ex:
+        assert list(ex.map(worker, range(THREADS))) == [0] * THREADS
+
+
 def test_thread_scratch_released_on_thread_exit(gpu):
     """Short-lived threads (one per call) do not accumulate device memory."""
     import torch

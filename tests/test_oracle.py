@@ -4,6 +4,7 @@ The oracle is pinned only by these restated semantics and by the pattern tables 
 the reference (no reference fixtures exist) — "parity unpinned".
 """
 import hashlib
+import math
 from pathlib import Path
 
 import numpy as np
@@ -60,6 +61,62 @@ def test_fast_known_answers(oracle):
     assert oracle.fast_score_map(ring_image(vals), 4)[3, 3] == 0
     vals = [105] * 16
     assert oracle.fast_score_map(ring_image(vals), 4)[3, 3] == 4
+
+
+def _verify_simd_frames(w, h):
+    """Frames for the VERIFY_SIMD property: the synthetic stream, uniform noise, 0/255 binary
+    noise (saturating adds / subs in the SIMD test), flat frames with isolated extreme pixels,
+    low-contrast noise around a mid level, and ring-exact corners."""
+    rng = np.random.default_rng(w * 7 + h)
+    yield "synthetic", synth.frame(5, w, h)
+    yield "uniform", rng.integers(0, 256, (h, w), dtype=np.uint8)
+    yield "binary", (rng.integers(0, 2, (h, w), dtype=np.uint8) * 255).astype(np.uint8)
+    for level in (0, 255):
+        img = np.full((h, w), level, np.uint8)
+        ys, xs = rng.integers(0, h, 3000), rng.integers(0, w, 3000)
+        img[ys, xs] = 255 - level
+        yield f"spikes{level}", img
+    yield "lowcontrast", np.clip(128 + rng.integers(-6, 7, (h, w)), 0, 255).astype(np.uint8)
+    img = np.full((h, w), 100, np.uint8)
+    for k, (cy, cx) in enumerate(zip(range(10, h - 10, 17), range(10, w - 10, 23))):
+        for j, (dx, dy) in enumerate(RING):  # arcs of 8 / 9 / 10 ring pixels, bright and dark
+            if (j - k) % 16 < 8 + k % 3:
+                img[cy + dy, cx + dx] = 100 + (60 if k % 2 else -60) + (j % 5)
+    yield "rings", img
+
+
+@pytest.mark.parametrize("shape", [(640, 480), (1280, 720)])
+def test_verify_simd_sse2_build_equals_scalar_oracle(oracle, shape):
+    """The reference's own self-check VERIFY_SIMD (OpenCVModified.cpp:1265-1271, 1408-1486), made
+    stronger: the score map of the x64 SSE2 build — the 16-pixel SIMD row loop (:1278-1338), the
+    scalar tail, and the SSE2 cornerScore<16> (:935-972) — restated in oracle/fast_sse2.c, equals
+    the scalar oracle's map (scalar loop + scalar cornerScore, :1030-1064, :1415-1479) that the
+    GPU parity tests use.  Equal score maps give equal keypoints: NMS and emission (:1489-1509)
+    read only the score rows."""
+    w, h = shape
+    for name, img in _verify_simd_frames(w, h):
+        for t in (0, 4, 20, 100, 254, 255):
+            simd, cols = oracle.fast_score_map_sse2(img, t)
+            scalar = oracle.fast_score_map(img, t)
+            bad = np.argwhere(simd != scalar)
+            assert len(bad) == 0, (name, t, bad[:5], simd[tuple(bad[0])], scalar[tuple(bad[0])])
+            # the SIMD loop covered all but the row tail (< 16 + 3 columns, + 8 after a step back)
+            assert (cols[3:h - 3] >= w - 16 - 3 - 8).all(), (name, t)
+            if name == "synthetic" and t == 4:
+                assert (scalar > 0).mean() > 0.1  # the comparison is over a dense corner map
+
+
+def test_sse2_corner_score_ring_cases(oracle):
+    """SSE2 cornerScore<16> vs the scalar branch on the ring known-answer cases, in the SIMD
+    loop's columns (a 64-px wide frame puts them inside the 16-pixel blocks)."""
+    for vals, center in (([90] * 9 + [100] * 7, 100), ([130] * 16, 100), ([105] * 16, 100),
+                         ([0, 255] * 8, 128), ([255] * 9 + [0] * 7, 128)):
+        img = np.full((7, 64), center, np.uint8)
+        for off in (3, 20, 37):
+            for (dx, dy), v in zip(RING, vals):
+                img[3 + dy, off + dx] = v
+        for t in (0, 4, 9, 100):
+            assert np.array_equal(oracle.fast_score_map_sse2(img, t)[0], oracle.fast_score_map(img, t)), (vals, t)
 
 
 def test_hamming_known(oracle):
@@ -668,7 +725,7 @@ def test_online_bow_oracle_database(oracle):
     leaves = oracle.bow_find_leaves(o.tree, train)
     for leaf in set(leaves.tolist()):
         n_img = len({i // 200 for i in np.flatnonzero(leaves == leaf)})
-        assert w[leaf] == np.float32(np.log(np.float32(7) / np.float32(n_img)))
+        assert w[leaf] == np.float32(math.log(float(np.float32(7) / np.float32(n_img))))
     imgs = {kf: rng.integers(0, 256, (150, 32), dtype=np.uint8) for kf in range(4)}
     for kf, d in imgs.items():
         o.InsertDescriptors(kf, d)
