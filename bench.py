@@ -76,13 +76,14 @@ def ba_flops(g, trials_per_iter):
     return 330.0 * len(g.cam) + trials_per_iter * (schur + n ** 3 / 3 + 2 * n ** 2)
 
 
-def load_pmc(kernel, field="hbm_bytes_per_launch"):
-    """(`field` of `kernel`, provenance) from the committed rocprofv3 PMC summary (default: HBM
-    bytes per launch).  The summary records the hash of the kernel sources it was collected on;
+def load_pmc(kernel, field="hbm_bytes_per_launch", summary="pmc_summary.json"):
+    """(`field` of `kernel`, provenance) from a committed rocprofv3 PMC summary (default: HBM
+    bytes per launch of the ORB-only profile; pmc_summary_ba.json: the full bench profile, which
+    holds the BA kernels).  The summary records the hash of the kernel sources it was collected on;
     counters of other sources are stale and not reported (None)."""
     from mageslam_amd.build import kernel_sources_sha
 
-    f = ROOT / "profiles" / "pmc_summary.json"
+    f = ROOT / "profiles" / summary
     if not f.exists():
         return None, "no committed PMC summary"
     try:
@@ -94,7 +95,7 @@ def load_pmc(kernel, field="hbm_bytes_per_launch"):
     if sha != now:
         return None, f"stale: profiles/pmc_summary.json was collected on kernel sources {sha}, these are {now}"
     return d.get(kernel, {}).get(field), \
-        f"profiles/pmc_summary.json ({meta.get('tag')}, kernel sources {sha}, FETCH_SIZE + WRITE_SIZE passes)"
+        f"profiles/pmc_summary.json ({meta.get('tag')}, kernel sources {sha})"
 
 
 def cpu_orb_baseline(args, budget_s):
@@ -116,6 +117,27 @@ def cpu_orb_baseline(args, budget_s):
             "sample": f"{n_timed} consecutive {args.width}x{args.height} synthetic frames, oracle "
                       f"extract ({args.features} features) + match vs previous frame, single thread, "
                       f"{el:.1f} s"}
+
+
+def host_info() -> dict:
+    """The host the CPU baselines ran on (record nproc and the CPU model)."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0))}
+
+
+def median_of(fn, budget_s, k=5):
+    """the median of k samples of a CPU baseline leg, each with budget_s / k."""
+    runs = [fn(budget_s / k) for _ in range(k)]
+    vals = [r["value"] for r in runs]
+    med = sorted(range(k), key=lambda i: vals[i])[k // 2]
+    return dict(runs[med], statistic=f"median of {k} samples", samples=vals, host=host_info())
 
 
 def host_threads() -> int:
@@ -256,12 +278,30 @@ def run_orb(args, rank, world, local_rank, torch, dist):
         per_frame = orb_bytes_per_frame(W, H, N)
         avg_s = orb_k[dom]["avg_ms"] / 1000.0
         achieved = per_frame * B / avg_s / 1e9
-        traffic, traffic_source = load_pmc(dom)
+        # traffic: 2 x FETCH_SIZE + WRITE_SIZE (the guide's gfx950 correction of the wide-stream
+        # read counter), per steady-state launch of the committed profile of these kernel sources
+        traffic, traffic_source = load_pmc(dom, "hbm_bytes_per_launch_fetch_x2")
+        traffic_raw, _ = load_pmc(dom, "hbm_bytes_per_launch")
         valu, _ = load_pmc(dom, "valu_issue_frac")
+        prof_us, _ = load_pmc(dom, "avg_us_steady")
+        step_s = el_max / args.steps
         res["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                           "traffic_source": traffic_source, "algorithmic_bytes_per_launch": per_frame * B,
+                           "traffic_raw_fetch": traffic_raw,
+                           "traffic_source": traffic_source + " (2 x FETCH_SIZE + WRITE_SIZE)",
+                           "algorithmic_bytes_per_launch": per_frame * B,
                            "avg_launch_ms": orb_k[dom]["avg_ms"],
+                           "avg_launch_source": "dispatch timestamps (hipExtLaunchKernel events) on the launch stream, "
+                                                "timed region only",
+                           # the same figure priced on the committed rocprofv3 kernel trace (launches after
+                           # the warm-up), so frac can be recomputed from profiles/
+                           "rocprof": None if prof_us is None else {
+                               "avg_launch_ms": prof_us / 1000.0,
+                               "frac": per_frame * B / (prof_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                               "source": traffic_source.split(" (")[0] + ", avg_us_steady"},
+                           # whole step (extract + match of B frames) against the same bytes
+                           "step": {"algorithmic_bytes": per_frame * B, "ms": 1000 * step_s,
+                                    "frac": per_frame * B / step_s / 1e9 / HBM_PEAK_GBS},
                            # what actually binds the kernel: SQ_INSTS_VALU per launch
                            # over its duration against 1024 SIMDs x 2.4 GHz / 4 cycles, same PMC run
                            "binding": {"resource": "VALU issue", "frac": valu,
@@ -285,6 +325,52 @@ def ba_round(b, g, me, steps, timer):
         b.step([1.8], me)
     timer.sync()
     return time.perf_counter() - t0
+
+
+REF_WINDOW_STEPS = 10  # StepBundleAdjustment calls per local-BA window on the reference schedule
+MIN_LAMBDA = 1e-3      # MappingSettings::MinLambda (MageSettings.h:260)
+
+
+def ba_reference_window(b, g, lam, steps, set_lambda, get_lambda, removed=None):
+    """One local BA in the reference's invocation shape, all of it timed by the caller:
+    BuildDataForG2O (graph load), the lambda persisted from the previous window
+    (MappingWorker.cpp:272-293, PersistLambda), then `steps` x BundleAdjustTask::Impl::Iterate
+    (BundleAdjust.cpp:380-404): StepBundleAdjustment at MaxOutlierErrorSquared, which starts at the
+    NON-squared MaxOutlierError (:375) and is multiplied by 0.95^2 after every call (:396), and
+    UpdateData's GetPose / GetPoint (:195-226).  Returns the next window's lambda
+    (max(GetCurrentLambda, MinLambda), MappingWorker.cpp:293)."""
+    b.set_graph(g)
+    if lam is not None:
+        set_lambda(lam)
+    me = 7.25
+    for _ in range(steps):
+        _, out = b.step([1.8], me)
+        if removed is not None:
+            removed.append(len(out))
+        b.poses()
+        b.points()
+        me *= np.float32(0.95) * np.float32(0.95)
+    return max(get_lambda(), MIN_LAMBDA)
+
+
+def run_ba_reference_schedule(b, g, budget_s, set_lambda, get_lambda, sync, steps=REF_WINDOW_STEPS):
+    """Windows on the reference schedule for ~budget_s (at least 2), each timed whole (graph load,
+    steps, readbacks).  The first window (lambda from computeLambdaInit) is untimed warm-up."""
+    lam = ba_reference_window(b, g, None, steps, set_lambda, get_lambda)
+    sync()
+    el, n, removed = 0.0, 0, []
+    s0 = b.stats()
+    while el < budget_s or n < 2:
+        t0 = time.perf_counter()
+        lam = ba_reference_window(b, g, lam, steps, set_lambda, get_lambda, removed)
+        sync()
+        el += time.perf_counter() - t0
+        n += 1
+    s1 = b.stats()
+    return {"value": n * steps / el, "unit": "iters/s", "windows": n, "steps_per_window": steps, "seconds": el,
+            "trials_per_iteration": (s1["trials"] - s0["trials"]) / max(s1["iterations"] - s0["iterations"], 1),
+            "outliers_per_call": float(np.mean(removed)), "calls_removing_edges": float(np.mean(np.array(removed) > 0)),
+            "final_lambda": lam}
 
 
 def run_ba(args, local_rank, torch):
@@ -336,12 +422,28 @@ def run_ba(args, local_rank, torch):
            "kernels": {k: {"launches": c, "avg_ms": ms / max(c, 1), "total_ms": ms} for k, (c, ms) in kern.items()},
            "kernel_timing": "dispatch timestamps (hipExtLaunchKernel events) of one more round, outside the "
                             "timed region"}
+    # the reference's invocation shape (BundleAdjustTask::Iterate per call, lambda persisted across
+    # windows): decaying outlier thresholds remove edges on most calls
+    res["reference_schedule"] = dict(
+        run_ba_reference_schedule(b, g, 3.0, b.SetCurrentLambda, b.GetCurrentLambda, torch.cuda.synchronize),
+        schedule=f"windows of (BuildDataForG2O + SetCurrentLambda(persisted) + {REF_WINDOW_STEPS} x "
+                 f"[StepBundleAdjustment(huber 1.8, maxErrSq 7.25 x 0.9025^k) + GetPose/GetPoint]), all timed")
     flops_iter = ba_flops(g, trials_per_iter)
     achieved = flops_iter * res["value"] / 1e12
     dom = max(kern, key=lambda k: kern[k][1]) if kern else None
+    # HBM bytes per LM iteration from the committed counters of the same kernel sources: each
+    # kernel's 2 x FETCH_SIZE + WRITE_SIZE per launch x its launches per iteration (profiled round)
+    traffic, tsrc = 0.0, None
+    for k, (c, _) in kern.items():
+        v, tsrc = load_pmc(k, "hbm_bytes_per_launch_fetch_x2", "pmc_summary_ba.json")
+        if v is None:
+            traffic = None
+            break
+        traffic += v * c / BA_ROUND_STEPS
     res["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                       "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "flops_per_iteration": flops_iter,
-                       "dominant_kernel": dom}
+                       "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic if kern else None,
+                       "traffic_unit": "HBM bytes per LM iteration (2 x FETCH_SIZE + WRITE_SIZE over the BA kernels)",
+                       "traffic_source": tsrc, "flops_per_iteration": flops_iter, "dominant_kernel": dom}
     return res, g
 
 
@@ -350,10 +452,9 @@ POSE_STEPS, POSE_HUBER, POSE_MAXE = 3, 4.0, 36.0  # TrackLocalMap's first Optimi
 
 def run_pose(args, rank, world, local_rank, torch, dist):
     """Batched pose-only BA (SURVEY.md §8(f) 2): TrackLocalMap::OptimizeCameraPose for a batch of
-    frames per launch (mage_ba_pose_batch_device), inputs resident in HBM.  C5: each rank tracks its
-    own sequence (seed + rank); after the timed region the per-frame trajectories (68 B records) are
-    all-gathered over RCCL and rank 0 can write them as ExportFossilCsv does."""
-    from mageslam_amd import _lib, bundler, multigpu, synth, trajectory
+    frames per launch (mage_ba_pose_batch_device), inputs resident in HBM; with several ranks each
+    solves its own batch (seed + rank), no collective."""
+    from mageslam_amd import _lib, bundler, multigpu, synth
 
     pb = synth.pose_batch(problems=args.pose_problems, obs=600, seed=multigpu.sequence_seed(synth.BA_SEED + 1, rank))
     K = args.pose_problems
@@ -386,15 +487,6 @@ def run_pose(args, rank, world, local_rank, torch, dist):
     torch.cuda.synchronize()
     multigpu.barrier(dist)
     el = multigpu.max_over_ranks(time.perf_counter() - t0, dev, dist)
-    # end-of-run exchange: every rank's trajectory (flag + 4x4 view matrix per frame)
-    M = torch.zeros((K, 4, 4), dtype=torch.float32, device=dev)
-    M[:, :3, :3] = r9_o.view(K, 3, 3).transpose(1, 2)
-    M[:, :3, 3] = pos_o
-    M[:, 3, 3] = 1
-    rows = torch.cat([torch.ones((K, 1), dtype=torch.float32, device=dev), M.view(K, 16)], 1)
-    gathered = trajectory.gather_trajectories(rows, dist)
-    if rank == 0 and args.trajectory_csv:
-        trajectory.export_fossil_csv(args.trajectory_csv, torch.cat(gathered).cpu().numpy())
     lib = _lib.load()
     lib.mage_profile_reset()
     lib.mage_profile_enable(1)
@@ -406,7 +498,6 @@ def run_pose(args, rank, world, local_rank, torch, dist):
     st = stats.cpu().numpy()
     res = {"metric": "pose-only BA problems/sec (OptimizeCameraPose: 1 camera, ~600 fixed points, 3 LM steps)",
            "value": world * n * K / el, "unit": "problems/s", "dtype": "f64", "problems_per_launch": K,
-           "trajectory_frames_gathered": int(sum(g.shape[0] for g in gathered)),
            "observations": E, "lm_iterations_per_problem": float(st[:, 0].mean()),
            "trials_per_problem": float(st[:, 1].mean()),
            "config": {"workload": f"{K} synthetic 720p frames x {E / K:.0f} observations, huber {POSE_HUBER}, "
@@ -448,26 +539,47 @@ def cpu_pose_baseline(pb, budget_s):
                       f"{el:.1f} s"}
 
 
-def run_tracking(args, local_rank, torch):
-    """C4 (BASELINE.json configs[3]): the tracking loop (mageslam_amd.tracking) over a synthetic
-    hand-held 720p sequence of a textured plane, frames rendered into HBM first.  A step is the
-    whole sequence: batched ORB extraction of every frame, then per frame RadiusMatch + two
-    pose-only BundlerLib passes (sequential: each frame's prediction needs the previous pose)."""
-    from mageslam_amd import _lib, orb, synth, tracking
+def c5_exchange(res, rank, dist, device, csv_path=""):
+    """C5's one exchange step: every rank's tracked trajectory as 68-byte records
+    (tracked flag + view matrix per frame, GetTrackingResultsForFrames, MAGESlam.cpp:410-428) is
+    all-gathered (RCCL over xGMI; gloo in the CPU rehearsal); rank 0 writes them in rank order as
+    ExportFossilCsv does (console.cpp:15-54).  Returns the gathered (T, 17) arrays, rank-ordered."""
+    import torch
+
+    from mageslam_amd import trajectory
+
+    T = len(res.poses)
+    tracked = np.array([f == 0 or res.inliers[f] > 0 for f in range(T)])
+    rows = trajectory.records_from_poses(res.rotations(), res.translations(), tracked)
+    gathered = [g.cpu().numpy() for g in trajectory.gather_trajectories(torch.from_numpy(rows).to(device), dist)]
+    if rank == 0 and csv_path:
+        trajectory.export_fossil_csv(csv_path, np.concatenate(gathered))
+    return gathered, rows
+
+
+def run_tracking(args, rank, world, local_rank, torch, dist):
+    """C4 (BASELINE.json configs[3]) and, with several ranks, C5 (configs[4]): the tracking loop
+    (mageslam_amd.tracking) over a synthetic hand-held 720p sequence of a textured plane, frames
+    rendered into HBM first.  A step is the whole sequence: batched ORB extraction of every frame,
+    then the device-resident loop (RadiusMatch + two pose-only BundlerLib passes per frame,
+    sequential: each frame's prediction needs the previous pose).  Every rank tracks its own
+    sequence (texture seed + rank, camera path from synth.rank_origin); after the timed region the
+    tracked trajectories are all-gathered (c5_exchange)."""
+    from mageslam_amd import _lib, multigpu, orb, synth, tracking
 
     T = args.track_frames
-    seq = synth.scene_sequence(T, args.width, args.height)
+    seq = synth.scene_sequence(T, args.width, args.height, origin=synth.rank_origin(rank))
+    seed = multigpu.sequence_seed(synth.FRAME_SEED, rank)
     dev = f"cuda:{local_rank}"
     cams = torch.from_numpy(seq.cams()).to(dev)
     frames = torch.empty((T, args.height, args.width), dtype=torch.uint8, device=dev)
     _lib.check(_lib.load().mage_synth_scene_device(_lib.ptr(frames), T, args.width, args.height,
                                                    args.width * args.height, _lib.ptr(cams), seq.fx, seq.fy, seq.cx,
                                                    seq.cy, synth.SCENE_PLANE_Z, synth.SCENE_TEXEL_SCALE,
-                                                   synth.SCENE_TEXEL_OFFSET, synth.FRAME_SEED, None))
+                                                   synth.SCENE_TEXEL_OFFSET, seed, None))
     torch.cuda.synchronize()
     K = (seq.fx, seq.fy, seq.cx, seq.cy)
     p0 = tracking.Pose(seq.R[0], seq.t[0])
-    be = tracking.GpuBackend(args.features, device=local_rank, batch=64)
     N = args.features
     det = orb.OrbDetector(nfeatures=N, device=local_rank)
     d_kp = torch.zeros((T, N * 28), dtype=torch.uint8, device=dev)
@@ -480,26 +592,49 @@ def run_tracking(args, local_rank, torch):
             det.detect_and_compute_batch_device(frames[b0:b1], args.width, args.height, d_kp[b0:b1],
                                                 d_desc[b0:b1], d_n[b0:b1], N)
 
-    feats = be.extract(frames[:8])  # warm-up of both loops
-    tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, device=local_rank)
-    extract_device(8)
+    extract_device(8)  # warm-up
     tracking.track_native_device(d_kp, d_desc, N, d_n, 8, K, p0, synth.SCENE_PLANE_Z)
     torch.cuda.synchronize()
     # the timed loop: device-resident extraction + mage_track_sequence_device (one sync)
+    multigpu.barrier(dist)
     t0 = time.perf_counter()
     extract_device(T)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     res = tracking.track_native_device(d_kp, d_desc, N, d_n, T, K, p0, synth.SCENE_PLANE_Z)
     t2 = time.perf_counter()
-    # the host-driven native loop over host features (mage_track_sequence): identical results
+    multigpu.barrier(dist)
+    el_max = multigpu.max_over_ranks(t2 - t0, dev, dist)
+    per_rank = [float(x[0]) for x in multigpu.gather_rows(
+        torch.tensor([T / (t2 - t0)], dtype=torch.float64, device=dev), dist)]
+    gathered, own = c5_exchange(res, rank, dist, dev, args.trajectory_csv)
+    gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)])
+    out = {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose)",
+           "value": world * T / el_max, "unit": "frames/s", "frames": T, "dtype": "u8 / f64",
+           "extract_ms_per_frame": 1000 * (t1 - t0) / T, "track_ms_per_frame": 1000 * (t2 - t1) / T,
+           "loop": "device-resident (mage_track_sequence_device: per-frame decisions on the GPU, one sync)",
+           "mean_matches": float(np.mean(res.matches[1:])), "mean_inliers": float(np.mean(res.inliers[1:])),
+           "keyframes": len(res.keyframes), "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
+           "config": {"workload": f"C4: {T}-frame {args.width}x{args.height} hand-held pan over a textured plane "
+                                  f"(synthetic), {args.features} features/frame"
+                                  + (f"; C5: {world} independent sequences (seed + rank), one per GPU, RCCL "
+                                     f"all-gather of the tracked trajectories" if world > 1 else "")}}
+    if world > 1:
+        out["per_gpu_fps"] = per_rank
+        out["scaling"] = "weak"
+    out["trajectory_frames_gathered"] = int(sum(len(g) for g in gathered))
+    out["trajectory_gather_consistent"] = bool(np.array_equal(gathered[rank], own))
+    if world > 1:
+        return out, None
+    # one GPU: the host-driven native loop over host features (mage_track_sequence) and the same loop
+    # driven from Python (tracking.track over GpuBackend) must give identical results
+    be = tracking.GpuBackend(args.features, device=local_rank, batch=64)
     feats = be.extract(frames)
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     host = tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, device=local_rank)
     torch.cuda.synchronize()
     t4 = time.perf_counter()
-    # and the same loop driven from Python (tracking.track over GpuBackend)
     py = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
     t5 = time.perf_counter()
 
@@ -507,17 +642,9 @@ def run_tracking(args, local_rank, torch):
         return a.matches == b.matches and a.inliers == b.inliers and a.keyframes == b.keyframes and all(
             np.array_equal(x.t, y.t) and np.array_equal(x.R, y.R) for x, y in zip(a.poses, b.poses))
 
-    gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)])
-    return {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose)",
-            "value": T / (t2 - t0), "unit": "frames/s", "frames": T, "dtype": "u8 / f64",
-            "extract_ms_per_frame": 1000 * (t1 - t0) / T, "track_ms_per_frame": 1000 * (t2 - t1) / T,
-            "loop": "device-resident (mage_track_sequence_device: per-frame decisions on the GPU, one sync)",
-            "host_loop_track_ms_per_frame": 1000 * (t4 - t3) / T, "host_loop_identical": bool(same(host, res)),
-            "python_loop_track_ms_per_frame": 1000 * (t5 - t4) / T, "python_loop_identical": bool(same(py, res)),
-            "mean_matches": float(np.mean(res.matches[1:])), "mean_inliers": float(np.mean(res.inliers[1:])),
-            "keyframes": len(res.keyframes), "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
-            "config": {"workload": f"C4: {T}-frame {args.width}x{args.height} hand-held pan over a textured plane "
-                                   f"(synthetic), {args.features} features/frame"}}, (seq, frames, res, feats)
+    out.update(host_loop_track_ms_per_frame=1000 * (t4 - t3) / T, host_loop_identical=bool(same(host, res)),
+               python_loop_track_ms_per_frame=1000 * (t5 - t4) / T, python_loop_identical=bool(same(py, res)))
+    return out, (seq, frames, res, feats)
 
 
 def cpu_tracking_baseline(args, ctx, budget_s):
@@ -567,6 +694,17 @@ def cpu_ba_baseline(g, budget_s):
     return {"value": n / el, "unit": "iters/s", "cores": 1, "kind": "port",
             "sample": f"{n // BA_ROUND_STEPS} rounds x {BA_ROUND_STEPS} timed StepBundleAdjustment iterations of "
                       f"the C3 graph (same schedule as the GPU leg), oracle, single thread, {el:.1f} s"}
+
+
+def cpu_ba_reference_baseline(g, budget_s):
+    """The oracle on the reference schedule (run_ba_reference_schedule), single thread."""
+    from oracle import oracle as O
+
+    b = O.BundlerOracle()
+    r = run_ba_reference_schedule(b, g, budget_s, b.set_lambda, b.get_lambda, lambda: None)
+    return dict(r, cores=1, kind="port",
+                sample=f"{r['windows']} windows x {r['steps_per_window']} calls of the C3 graph on the reference "
+                       f"schedule (same as the GPU leg), oracle, single thread, {r['seconds']:.1f} s")
 
 
 def run_ba_many(args, local_rank, g, budget_s):
@@ -665,7 +803,15 @@ def run_dry(args, rank, world, dist):
     el_max = multigpu.max_over_ranks(el, "cpu", dist)
     summary = torch.tensor(np.stack([np.full(B, rank), sums[-1]], 1), dtype=torch.int64)
     gathered = multigpu.gather_rows(summary, dist)
-    return {"value": world * args.steps * B / el_max, "ms_per_step": 1000 * el_max / args.steps, "kernels": {},
+    # C5's trajectory exchange with stand-in tracking results: the ground-truth poses of this rank's
+    # scene sequence in place of the device loop's (which needs the GPU)
+    from mageslam_amd import tracking
+
+    T = min(args.track_frames, 16)
+    seq = synth.scene_sequence(T, args.width, args.height, origin=synth.rank_origin(rank))
+    res = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)], inliers=[1] * T)
+    traj, _ = c5_exchange(res, rank, dist, "cpu", args.trajectory_csv)
+    return {"trajectory_frames_gathered": int(sum(len(t) for t in traj)),"value": world * args.steps * B / el_max, "ms_per_step": 1000 * el_max / args.steps, "kernels": {},
             "mean_keypoints": 0.0, "mean_matches": 0.0, "frames_per_step": B,
             "gathered_ranks": [int(g[0, 0]) for g in gathered],
             "gathered_checksums": [int(g[:, 1].sum()) for g in gathered]}
@@ -692,7 +838,8 @@ def main():
             print(json.dumps({"metric": METRIC, "value": res["value"], "unit": "frames/s", "n_gpus": world,
                               "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
                               "dry_run": True, "scaling": "weak", "gathered_ranks": res["gathered_ranks"],
-                              "gathered_checksums": res["gathered_checksums"]}))
+                              "gathered_checksums": res["gathered_checksums"],
+                              "trajectory_frames_gathered": res["trajectory_frames_gathered"]}))
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -719,7 +866,7 @@ def main():
     if ba_res is not None and world == 1 and not args.no_all_cores:
         ba_res["many_windows"] = run_ba_many_child(local_rank)
     pose_res, pb = (None, None) if args.no_pose else run_pose(args, rank, world, local_rank, torch, dist)
-    track_res, tctx = (None, None) if (args.no_tracking or rank != 0) else run_tracking(args, local_rank, torch)
+    track_res, tctx = (None, None) if args.no_tracking else run_tracking(args, rank, world, local_rank, torch, dist)
     if world > 1:
         dist.barrier()
 
@@ -759,13 +906,16 @@ def main():
         if track_res is not None:
             out["tracking"] = track_res
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_orb_baseline(args, args.cpu_sample_s)
+            out["cpu_baseline"] = median_of(lambda b: cpu_orb_baseline(args, b), args.cpu_sample_s)
             if not args.no_all_cores:
                 out["cpu_baseline_all_cores"] = cpu_orb_baseline_all(args, args.cpu_sample_s / 2)
                 out["vs_cpu_all_cores"] = out["value"] / out["cpu_baseline_all_cores"]["value"]
             if ba_res is not None:
-                cb = cpu_ba_baseline(g, args.cpu_sample_s)
+                cb = median_of(lambda b: cpu_ba_baseline(g, b), args.cpu_sample_s)
                 ba_res["cpu_baseline"] = cb
+                rs = ba_res["reference_schedule"]
+                rs["cpu_baseline"] = median_of(lambda b: cpu_ba_reference_baseline(g, b), args.cpu_sample_s)
+                rs["vs_cpu"] = rs["value"] / rs["cpu_baseline"]["value"]
                 if not args.no_all_cores:
                     ca = cpu_ba_baseline_all(g, args.cpu_sample_s / 2)
                     ba_res["cpu_baseline_all_cores"] = ca
@@ -779,7 +929,7 @@ def main():
                 track_res["vs_cpu"] = track_res["value"] / ct["value"]
                 track_res["parity"] = parity
             if pose_res is not None:
-                cp = cpu_pose_baseline(pb, min(args.cpu_sample_s, 6.0))
+                cp = median_of(lambda b: cpu_pose_baseline(pb, b), min(args.cpu_sample_s, 6.0))
                 pose_res["cpu_baseline"] = cp
                 pose_res["vs_cpu"] = pose_res["value"] / cp["value"]
             out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]

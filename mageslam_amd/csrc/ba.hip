@@ -1607,31 +1607,23 @@ __global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s0,
     // need an agent-scope fence per workgroup, i.e. a full L2 write-back on gfx950
 }
 
-__global__ __launch_bounds__(BA_THREADS) void drop_edges(unsigned char* __restrict__ active,
-                                                         const uint32_t* __restrict__ list, uint32_t n)
+// removeEdge for the listed observations (thread per removed edge): the edge leaves the active set
+// and its point's active-edge count drops; the point leaves the system with its last edge
+// (SparseOptimizer::initializeOptimization keeps only vertices with active edges).  Cameras' counts
+// are kept by the host, which decides whether the block numbering must be rebuilt.  The Schur
+// product lists keep the removed edges' entries: their W / G records are zero from the next
+// linearisation on.
+__global__ __launch_bounds__(BA_THREADS) void drop_edges(const int* __restrict__ ept,
+                                                         const uint32_t* __restrict__ list, uint32_t n,
+                                                         unsigned char* __restrict__ active,
+                                                         int* __restrict__ ptcnt, int* __restrict__ ptfree)
 {
     const uint32_t i = blockIdx.x * BA_THREADS + threadIdx.x;
-    if (i < n) active[list[i]] = 0;
-}
-
-// After removals: points keep their system membership only while they have an active edge
-// (SparseOptimizer::initializeOptimization); cameras' active-edge counts tell the host whether
-// the block numbering must be rebuilt.
-__global__ __launch_bounds__(BA_THREADS) void refresh_membership(Problem pb, int points_fixed,
-                                                                 int* __restrict__ ptfree,
-                                                                 int* __restrict__ cam_active)
-{
-    const int i = blockIdx.x * BA_THREADS + threadIdx.x;
-    if (i < pb.P) {
-        int any = 0;
-        for (int a = pb.pstart[i]; a < pb.pstart[i + 1] && !any; a++) any = pb.active[pb.pedges[a]];
-        ptfree[i] = !points_fixed && any;
-    }
-    if (i < pb.C) {
-        int cnt = 0;
-        for (int a = pb.cstart[i]; a < pb.cstart[i + 1]; a++) cnt += pb.active[pb.cedges[a]];
-        cam_active[i] = cnt;
-    }
+    if (i >= n) return;
+    const uint32_t e = list[i];
+    active[e] = 0;
+    const int p = ept[e];
+    if (atomicSub(&ptcnt[p], 1) == 1) ptfree[p] = 0;
 }
 
 }  // namespace
@@ -1655,7 +1647,7 @@ struct BundleAdjuster {
     int iteration = 0;
     double user_lambda = 0, lambda = 0, ni = 2, huber = 0;
     // a linearisation launched at the end of the previous step for the next one (see step())
-    bool eager = false;
+    bool eager = false, eager_init = false;
     double eager_huber = 0, eager_lambda = 0;
     int eager_cur = -1;
     int n = 0, np = 0;  // 6 * cameras in the system, padded to a multiple of 16
@@ -1705,8 +1697,12 @@ struct BundleAdjuster {
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
-        d_olist, d_camcnt, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
+        d_ptcnt, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
         d_sfinish, d_epos, d_chi_lin, d_livebuf;
+    // outlier lists of the speculative / final post-pass (2 x E entries), written by the kernels
+    // straight into host memory: the host sorts and returns them after the completion wait
+    MappedBuffer h_olist;
+    std::vector<int> camcnt;  // active observation edges per camera (host-side bookkeeping)
     int n_entries = 0;  // point-CSR entries (active edges at initialisation)
     int nb_free = 0;    // cameras in the reduced system
     mage_ba_stats stats{};
@@ -1744,10 +1740,11 @@ struct BundleAdjuster {
         for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
-                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk, &d_olist,
-                        &d_camcnt, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
+                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
+                        &d_ptcnt, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf})
             b->release();
+        h_olist.release();
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
         if (h_ctl) (void)hipHostFree(h_ctl);
@@ -2007,6 +2004,13 @@ struct BundleAdjuster {
         if ((r = upload(d_schunks, schunks)) != MAGE_OK) return r;
         if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
         if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
+        {
+            std::vector<int> ptcnt(P);
+            for (int i = 0; i < P; i++) ptcnt[i] = pstart[i + 1] - pstart[i];
+            if ((r = upload(d_ptcnt, ptcnt)) != MAGE_OK) return r;
+            camcnt.assign(C, 0);
+            for (int c = 0; c < C; c++) camcnt[c] = cstart[c + 1] - cstart[c];
+        }
         if ((r = upload(d_active, active)) != MAGE_OK) return r;
         if ((r = upload(d_pstart, pstart)) != MAGE_OK) return r;
         if ((r = upload(d_pedges, pedges)) != MAGE_OK) return r;
@@ -2042,10 +2046,11 @@ struct BundleAdjuster {
                         std::make_pair(&d_tout, std::max<size_t>(teth.size(), 1) * TETHER_OUT * 8),
                         std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
                         std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, ((size_t)std::max<int>((int)(Em / BA_THREADS), group_grid((int)Pm)) + 2) * 4 * 8),
-                        std::make_pair(&d_olist, Em * 2 * 4 + 16), std::make_pair(&d_camcnt, Cm * 4),
+                        
                         std::make_pair(&d_spart, (size_t)std::max(n_slots, 1) * 42 * 8)})
             if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
         if ((r = d_livebuf.reserve(sizeof(LiveCtl))) != MAGE_OK) return r;
+        if ((r = h_olist.reserve(Em * 2 * 4 + 16)) != MAGE_OK) return r;
         MAGE_HIP(hipMemsetAsync(d_livebuf.ptr, 0, sizeof(LiveCtl), st));
         MAGE_HIP(hipMemsetAsync(d_maxd.ptr, 0, (Pm + Cm) * 8, st));
         MAGE_HIP(hipMemsetAsync(d_scale.ptr, 0, (Pm + Cm) * 8, st));
@@ -2144,7 +2149,7 @@ struct BundleAdjuster {
                    nt, state(1 - cur), 0, d_chi.as<double>() + P, d_tout.as<double>());
         // evaluation of the trial state with the speculative post-pass (read back with this sync)
         const bool spec = speculate && E > 0;
-        SpecPass sp{state(cur), spec ? 1 : 0, outlier_max_err_sq, d_olist.as<uint32_t>(), E, d_osum.as<double>(), d_live()};
+        SpecPass sp{state(cur), spec ? 1 : 0, outlier_max_err_sq, h_olist.device<uint32_t>(), E, d_osum.as<double>(), d_live()};
         if (npb > 0)
             launch("ba.evaluate", evaluate_kernel, dim3(npb), dim3(BA_THREADS), 0, st, pb, state(1 - cur),
                    point_out(d_chi.as<double>()), sp);
@@ -2169,7 +2174,8 @@ struct BundleAdjuster {
             lambda = user_lambda;
             ni = 2;
         }
-        const bool reuse = eager && iteration > 0 && eager_huber == huber && eager_lambda == lambda && eager_cur == cur;
+        const bool reuse = eager && eager_init == init_lambda && eager_huber == huber && eager_cur == cur &&
+                           (init_lambda || eager_lambda == lambda);
         eager = false;
         mage_status r = MAGE_OK;
         if (!reuse && (r = linearize(init_lambda ? std::numeric_limits<double>::quiet_NaN() : lambda, init_lambda)) != MAGE_OK)
@@ -2248,7 +2254,7 @@ struct BundleAdjuster {
         const int ge = outlier_blocks();
         launch("ba.outlier_pass", outlier_pass, dim3(ge), dim3(BA_THREADS), 0, st, problem(), s0, s1, ns, E,
                            d_active.as<unsigned char>(), d_err.as<double>(), outlier_max_err_sq,
-                           d_olist.as<uint32_t>(), d_osum.as<double>(), d_live());
+                           h_olist.device<uint32_t>(), d_osum.as<double>(), d_live());
     }
 
     mage_status step(const float* hw, uint32_t nsteps, float maxErrSq, uint32_t* outliers, uint32_t cap,
@@ -2295,26 +2301,19 @@ struct BundleAdjuster {
         const double h[2] = {h_octl().osum[k][0], h_octl().osum[k][1]};
         const uint32_t no = h_octl().count[k];
         if (no > 0) {
-            std::vector<uint32_t> list(no);
-            const uint32_t* d_list = d_olist.as<uint32_t>() + (size_t)k * E;
-            MAGE_HIP(hipMemcpyAsync(list.data(), d_list, 4 * (size_t)no, hipMemcpyDeviceToHost, st));
-            hipLaunchKernelGGL(drop_edges, dim3((no + BA_THREADS - 1) / BA_THREADS), dim3(BA_THREADS), 0, st,
-                               d_active.as<unsigned char>(), d_list, no);
-            // membership after the removal (points drop out with their last edge; a free camera
-            // without edges changes the block numbering -> full re-initialisation)
-            const int gm = (std::max(P, C) + BA_THREADS - 1) / BA_THREADS;
-            {
-                launch("ba.refresh_membership", refresh_membership, dim3(gm), dim3(BA_THREADS), 0, st, problem(),
-                                   points_fixed ? 1 : 0, d_ptfree.as<int>(), d_camcnt.as<int>());
-            }
-            std::vector<int> camcnt(C);
-            MAGE_HIP(hipMemcpyAsync(camcnt.data(), d_camcnt.ptr, 4 * (size_t)C, hipMemcpyDeviceToHost, st));
-            MAGE_HIP(hipStreamSynchronize(st));
+            // the pass wrote the list into mapped host memory before the completion word
+            const uint32_t* h_list = h_olist.host<uint32_t>() + (size_t)k * E;
+            std::vector<uint32_t> list(h_list, h_list + no);
+            launch("ba.drop_edges", drop_edges, dim3((no + BA_THREADS - 1) / BA_THREADS), dim3(BA_THREADS), 0, st,
+                   (const int*)d_ept.as<int>(), (const uint32_t*)(h_olist.device<uint32_t>() + (size_t)k * E), no,
+                   d_active.as<unsigned char>(), d_ptcnt.as<int>(), d_ptfree.as<int>());
             std::sort(list.begin(), list.end());  // g2o active-edge order = insertion order
             for (uint32_t k = 0; k < no; k++) {
                 removed[list[k]] = 1;
+                camcnt[ecam[list[k]]]--;
                 if (k < cap) outliers[k] = list[k];
             }
+            // a free camera without edges changes the block numbering -> full re-initialisation
             for (int c = 0; c < C; c++)
                 if (camh[c] >= 0 && camcnt[c] == 0 && cam_tethers[c] == 0) dirty = true;
             iteration = 0;  // removeEdge dirties the optimizer: next Step re-initialises (lambda init)
@@ -2324,11 +2323,17 @@ struct BundleAdjuster {
         // Eager linearisation for the caller's usual next call (BundleAdjust.cpp:311-318: the same
         // huber width, no setter in between): it runs while control is with the caller, and
         // lm_solve reuses it only when the huber width, lambda and state still match.
-        if (!dirty && !useless && iteration > 0) {
-            if ((r = linearize(lambda, false)) != MAGE_OK) return r;
+        // After an outlier removal the next Step starts at iteration 0 (lambda re-initialised from
+        // the user lambda or computeLambdaInit): the eager linearisation is that iteration's, with
+        // the reduction computeLambdaInit reads when no user lambda is set.
+        if (!dirty && !useless) {
+            const bool init = iteration == 0 && user_lambda <= 0;
+            const double lam = iteration > 0 ? lambda : user_lambda;
+            if ((r = linearize(init ? std::numeric_limits<double>::quiet_NaN() : lam, init)) != MAGE_OK) return r;
             eager = true;
+            eager_init = init;
             eager_huber = huber;
-            eager_lambda = lambda;
+            eager_lambda = init ? 0.0 : lam;
             eager_cur = cur;
         }
         return no > cap ? MAGE_ECAPACITY : MAGE_OK;

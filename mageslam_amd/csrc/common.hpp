@@ -96,6 +96,39 @@ struct PinnedBuffer {
     }
 };
 
+// Host memory that kernels write directly (pinned, coherent, mapped): results a host decision
+// needs right after a completion wait arrive without a D2H copy + stream sync.
+struct MappedBuffer {
+    void* ptr = nullptr;  // host view
+    void* dev = nullptr;  // device view
+    size_t bytes = 0;
+    mage_status reserve(size_t n) {
+        if (n <= bytes) return MAGE_OK;
+        release();
+        if (hipHostMalloc(&ptr, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) {
+            release();
+            set_error("mapped hipHostMalloc of " + std::to_string(n) + " bytes failed");
+            return MAGE_ENOMEM;
+        }
+        bytes = n;
+        return MAGE_OK;
+    }
+    void release() {
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = dev = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* host() const {
+        return static_cast<T*>(ptr);
+    }
+    template <typename T>
+    T* device() const {
+        return static_cast<T*>(dev);
+    }
+};
+
 // Scratch of a synchronous host-buffer entry point (device staging, pinned staging, a private
 // stream), one per (calling thread, device, entry point): concurrent callers never share buffers
 // or a stream.  The reference calls these paths from several threads at once — both stereo

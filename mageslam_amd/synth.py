@@ -397,17 +397,24 @@ class SceneSequence:
         return np.ascontiguousarray(np.concatenate([self.R.reshape(-1, 9), self.C], 1), np.float64)
 
 
-def scene_sequence(frames: int, width: int = 1280, height: int = 720, step: float = 0.015) -> SceneSequence:
+def scene_sequence(frames: int, width: int = 1280, height: int = 720, step: float = 0.015,
+                   origin: tuple = (0.0, 0.0)) -> SceneSequence:
     """A 'video.mp4-shaped' hand-held pan over the plane: ~2.7 px of motion per frame at 720p plus
-    slow yaw / pitch / roll and depth oscillations (BASELINE.json C4)."""
+    slow yaw / pitch / roll and depth oscillations (BASELINE.json C4).  `origin` shifts the camera
+    path over the plane (C5: every rank's sequence starts elsewhere, rank_origin)."""
     f = 900.0 * width / 1280.0
     t = np.arange(frames, dtype=np.float64)
     yaw = 0.03 * np.sin(t / 17.0)
     pitch = 0.02 * np.sin(t / 23.0)
     roll = 0.01 * np.sin(t / 31.0)
     R = np.stack([_rot(a, b, c) for a, b, c in zip(yaw, pitch, roll)])
-    C = np.stack([step * t, 0.08 * np.sin(t / 19.0), 0.15 * np.sin(t / 29.0)], 1)
+    C = np.stack([step * t + origin[0], 0.08 * np.sin(t / 19.0) + origin[1], 0.15 * np.sin(t / 29.0)], 1)
     return SceneSequence(R=R, C=C, fx=f, fy=f, cx=width / 2.0, cy=height / 2.0, width=width, height=height)
+
+
+def rank_origin(rank: int) -> tuple:
+    """Start of rank r's camera path on the plane (C5: independent sequences)."""
+    return (0.37 * rank, -0.21 * rank)
 
 
 def scene_frames(seq: SceneSequence, first: int = 0, count: int | None = None, seed: int = FRAME_SEED) -> np.ndarray:

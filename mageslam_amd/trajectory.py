@@ -32,6 +32,17 @@ def records(tracked: np.ndarray, mats: np.ndarray) -> np.ndarray:
     return out
 
 
+def records_from_poses(R: np.ndarray, t: np.ndarray, tracked) -> np.ndarray:
+    """(T, 17) float32 rows from per-frame world -> camera rotations (T, 3, 3) and view-space
+    translations (T, 3) (the tracker's Pose, as GetTrackingResultsForFrames reports it)."""
+    R = np.asarray(R, np.float64).reshape(-1, 3, 3)
+    M = np.zeros((len(R), 4, 4), np.float32)
+    M[:, :3, :3] = R
+    M[:, :3, 3] = np.asarray(t, np.float64).reshape(-1, 3)
+    M[:, 3, 3] = 1
+    return records(tracked, M)
+
+
 def gather_trajectories(rows, dist):
     """All-gather every rank's (T, 17) record tensor (RCCL over xGMI on GPU, gloo in tests);
     returns the list ordered by rank — the one exchange of the C5 configuration."""

@@ -241,3 +241,54 @@ def test_pose_batch_edges_and_single_problem_path(gpu):
     assert np.abs(qt[0, 4:] - g["qt7"][0, 4:]).max() < POSE_TOL
     assert list(np.nonzero(g["outlier"][s])[0]) == outl
     assert abs(ms - g["mean_sq"][0]) <= 1e-4 * abs(ms)
+
+
+def test_reference_schedule_windows(gpu):
+    """BundleAdjustTask::Impl::Iterate's schedule (BundleAdjust.cpp:380-404): maxErrorSquare starts
+    at the non-squared MaxOutlierError and shrinks by 0.95^2 per call, so edges are removed on most
+    calls (removal re-initialises lambda at the next Step); the second window is seeded with the
+    first one's lambda (PersistLambda, MappingWorker.cpp:272-293) — both lambda paths after removals."""
+    from oracle import oracle as O
+
+    g = synth.ba_graph(cameras=20, points=1500, obs_per_point=10, fixed_cameras=5, seed=11)
+    gb = bundler.BundlerLib()
+    ob = O.BundlerOracle()
+    lam_g = lam_o = None
+    removed = 0
+    for w in range(2):
+        gb.set_graph(g)
+        ob.set_graph(g)
+        if lam_g is not None:
+            gb.SetCurrentLambda(lam_g)
+            ob.set_lambda(lam_o)
+        me = np.float32(7.25)
+        for it in range(8):
+            ms_g, out_g = gb.step([1.8], float(me))
+            ms_o, out_o = ob.step([1.8], float(me))
+            assert np.array_equal(out_g, out_o), f"window {w}: outliers differ at call {it}"
+            assert abs(ms_g - ms_o) <= 1e-4 * max(1.0, abs(ms_o)), (w, it, ms_g, ms_o)
+            removed += len(out_o)
+            me = np.float32(me * np.float32(0.95) * np.float32(0.95))
+        compare(gb, ob)
+        sg, so = gb.stats(), ob.stats()
+        assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
+        lam_g, lam_o = max(gb.GetCurrentLambda(), 1e-3), max(ob.get_lambda(), 1e-3)
+        assert abs(lam_g - lam_o) <= 1e-3 * lam_o
+    assert removed > 16  # the decaying threshold really removes edges call after call
+
+
+def test_removals_drop_points_and_cameras(gpu):
+    """Outlier removal that empties points (they leave the system with their last edge) and a whole
+    free camera (the block numbering is rebuilt: full re-initialisation), then keeps stepping."""
+    from oracle import oracle as O
+
+    g = synth.ba_graph(cameras=12, points=400, obs_per_point=8, fixed_cameras=3, seed=5)
+    rng = np.random.default_rng(3)
+    # offsets no pose or point can absorb: every observation of free camera 6 and of point 17
+    # becomes an outlier
+    for m, d in ((g.cam == 6, 40.0), (g.pt == 17, 25.0)):
+        g.uv[m] += rng.choice(np.float32([-d, d]), size=(int(m.sum()), 2))
+    gb, ob = run_pair(g, 5, max_err=9.0)
+    compare(gb, ob)
+    sg, so = gb.stats(), ob.stats()
+    assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]

@@ -48,11 +48,17 @@ def test_gloo_world2_gather_and_max():
         assert m == 2.0
 
 
-def test_bench_cpu_dry_run_world2():
+def test_bench_cpu_dry_run_world2(tmp_path):
+    """bench.py's N>1 flow under torch.distributed.run (gloo): per-rank sequences, max-over-ranks
+    timing, and C5's exchange — every rank's trajectory all-gathered and written by rank 0 in rank
+    order as ExportFossilCsv (stand-in tracking results: each rank's ground-truth poses)."""
+    from mageslam_amd import synth, trajectory
+
+    csv = tmp_path / "c5.csv"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29513", str(ROOT / "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--cpu-dry-run"]
+           "--steps", "3", "--warmup", "1", "--cpu-dry-run", "--track-frames", "12", "--trajectory-csv", str(csv)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(ROOT))
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -60,6 +66,16 @@ def test_bench_cpu_dry_run_world2():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["gathered_ranks"] == [0, 1] and d["value"] > 0
     assert d["gathered_checksums"][0] != d["gathered_checksums"][1]
+    assert d["trajectory_frames_gathered"] == 24
+    # the CSV holds rank 0's sequence, then rank 1's, each exactly its own trajectory
+    expect = tmp_path / "expect.csv"
+    rows = []
+    for rank in range(2):
+        seq = synth.scene_sequence(12, 1280, 720, origin=synth.rank_origin(rank))
+        rows.append(trajectory.records_from_poses(seq.R, seq.t, np.ones(12, bool)))
+    trajectory.export_fossil_csv(expect, np.concatenate(rows))
+    assert csv.read_text() == expect.read_text()
+    assert not np.array_equal(rows[0], rows[1])
 
 
 def test_fossil_csv_format(tmp_path):

@@ -17,16 +17,17 @@ run_set() {  # <out dir> <command...>
     timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- "$@" > /dev/null 2> $OUT/write.err
     timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES -d $OUT/pmc_valu -o run --output-format csv -- "$@" > /dev/null 2> $OUT/valu.err
     # only the stats and counter tables come back (gpurun returns <= 64 MiB of gpurun_out/)
-    find $OUT -name '*.csv' ! -name run_kernel_stats.csv ! -name run_counter_collection.csv -delete
-    find $OUT -name run_counter_collection.csv -exec gzip -f {} \;
+    find $OUT -name '*.csv' ! -name run_kernel_stats.csv ! -name run_counter_collection.csv ! -name run_kernel_trace.csv -delete
+    find $OUT \( -name run_counter_collection.csv -o -name run_kernel_trace.csv \) -exec gzip -f {} \;
 }
 OUT=gpurun_out/prof_$TAG
 ORB=gpurun_out/prof_${TAG}_orb
 ROWS=gpurun_out/prof_${TAG}_rows
 ORB_CMD="python3 bench.py --steps 10 --warmup 3 --no-ba --no-pose --no-tracking --no-cpu-baseline --pipelined-streams 0 --no-all-cores"
 if [ "$2" = collect ]; then
-    python3 tools/rocprof_summary.py $OUT $TAG > /dev/null
+    python3 tools/rocprof_summary.py $OUT $TAG "python bench.py" 3 > /dev/null
     cp $OUT/trace/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
+    cp profiles/${TAG}_pmc_summary.json profiles/pmc_summary_ba.json  # BA kernels' counters (bench.py)
     python3 tools/rocprof_summary.py $ROWS ${TAG}_rows "python tools/bench_rows.py" > /dev/null
     cp $ROWS/trace/run_kernel_stats.csv profiles/${TAG}_rows_kernel_stats.csv
     cp $ROWS/trace.json profiles/${TAG}_rows.jsonl
@@ -34,7 +35,7 @@ if [ "$2" = collect ]; then
     # the headline ORB leg alone (every fast_nms launch is a 256-frame batch, so the average
     # duration is the one bench.py prices the roofline on); its counters become
     # profiles/pmc_summary.json, which bench.py reads for roofline.traffic
-    python3 tools/rocprof_summary.py $ORB ${TAG}_orb "${ORB_CMD#python3 }" > /dev/null
+    python3 tools/rocprof_summary.py $ORB ${TAG}_orb "${ORB_CMD#python3 }" 3 > /dev/null
     cp $ORB/trace/run_kernel_stats.csv profiles/${TAG}_orb_kernel_stats.csv
     cp $ORB/trace.json profiles/${TAG}_orb_bench.json
     cp profiles/${TAG}_orb_pmc_summary.json profiles/pmc_summary.json

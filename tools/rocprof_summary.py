@@ -1,14 +1,16 @@
 """Summarise rocprofv3 outputs into profiles/ (committed evidence).
 
-Usage: python tools/rocprof_summary.py <prof_dir> <round_tag>
+Usage: python tools/rocprof_summary.py <prof_dir> <round_tag> [command] [warm-up launches to skip]
   <prof_dir>/trace/run_kernel_stats.csv          (--kernel-trace --stats)
+  <prof_dir>/trace/run_kernel_trace.csv[.gz]     (per-dispatch durations: steady-state averages)
   <prof_dir>/pmc_fetch/run_counter_collection.csv (--pmc FETCH_SIZE, its own pass)
   <prof_dir>/pmc_write/run_counter_collection.csv (--pmc WRITE_SIZE, its own pass)
 
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB; on gfx950
 FETCH_SIZE reads half the bytes of a wide (16 B/lane) coalesced stream, so the corrected read
 side is 2 x FETCH_SIZE for such kernels.  Our kernels mix widths, so both the raw and the x2
-figures are kept; `hbm_bytes_per_launch` uses the raw FETCH (lower bound) + WRITE.
+figures are kept; `hbm_bytes_per_launch` uses the raw FETCH (lower bound) + WRITE and
+`hbm_bytes_per_launch_fetch_x2` the corrected 2 x FETCH + WRITE (what bench.py reports as traffic).
 """
 from __future__ import annotations
 
@@ -69,31 +71,56 @@ def read_stats(path: Path):
     return rows
 
 
-def read_pmc(path: Path, counter: str):
-    acc = defaultdict(lambda: [0.0, 0])
+def read_pmc(path: Path, counter: str, skip: int = 0):
+    """Per-kernel mean of `counter` per dispatch, without each kernel's first `skip` dispatches
+    (the bench's warm-up launches: the first ORB batch runs without the candidate gate)."""
+    per = defaultdict(list)
     if not _exists(path):
         return {}
     with _open(path) as f:
         for r in csv.DictReader(f):
             if r["Counter_Name"] != counter:
                 continue
-            k = short(r["Kernel_Name"])
-            acc[k][0] += float(r["Counter_Value"])
-            acc[k][1] += 1
-    return {k: v[0] / v[1] for k, v in acc.items()}
+            per[short(r["Kernel_Name"])].append((int(r.get("Dispatch_Id") or 0), float(r["Counter_Value"])))
+    out = {}
+    for k, v in per.items():
+        v.sort()
+        v = v[skip:] if len(v) > skip else v
+        out[k] = sum(x for _, x in v) / len(v)
+    return out
+
+
+def read_trace(path: Path, skip: int = 0):
+    """Per-kernel (launches, mean duration in us) from the kernel trace, without each kernel's first
+    `skip` dispatches — the steady-state launch time bench.py's HIP events measure."""
+    per = defaultdict(list)
+    if not _exists(path):
+        return {}
+    with _open(path) as f:
+        for r in csv.DictReader(f):
+            per[short(r["Kernel_Name"])].append(
+                (int(r.get("Dispatch_Id") or 0), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    out = {}
+    for k, v in per.items():
+        v.sort()
+        v = v[skip:] if len(v) > skip else v
+        out[k] = (len(v), sum(x for _, x in v) / len(v))
+    return out
 
 
 def main():
     prof = Path(sys.argv[1])
     tag = sys.argv[2]
     cmd = sys.argv[3] if len(sys.argv) > 3 else "python bench.py"
+    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # warm-up launches per kernel to leave out
     out_dir = ROOT / "profiles"
     out_dir.mkdir(exist_ok=True)
     stats = read_stats(prof / "trace" / "run_kernel_stats.csv")
-    fetch = read_pmc(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
-    write = read_pmc(prof / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
-    valu = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_INSTS_VALU")
-    mfma = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_VALU_MFMA_BUSY_CYCLES")
+    trace = read_trace(prof / "trace" / "run_kernel_trace.csv", skip)
+    fetch = read_pmc(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE", skip)
+    write = read_pmc(prof / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE", skip)
+    valu = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_INSTS_VALU", skip)
+    mfma = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_VALU_MFMA_BUSY_CYCLES", skip)
     lines = [f"# rocprofv3 summary — {tag}", "",
              "`rocprofv3 --kernel-trace --stats` (durations) and separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` "
              f"passes of `{cmd}` on one MI355X.  KiB counters converted to bytes; FETCH x2 is the "
@@ -101,8 +128,11 @@ def main():
              "VALU issue: SQ_INSTS_VALU wave-instructions per launch (own pass) over the launch time, against "
              "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction (614 G/s; tools/valu_probe.hip measures "
              "~4.6-4.8 cycles per instruction per SIMD for every form used here).", "",
-             "| kernel | calls | avg µs | total ms | % | FETCH MB/launch (raw) | FETCH x2 | WRITE MB/launch | VALU G inst/s | VALU issue frac |",
-             "|---|---|---|---|---|---|---|---|---|---|"]
+             f"Steady-state columns (avg µs steady, counters) leave out each kernel's first {skip} launches "
+             "(the command's warm-up steps; the first ORB batch runs without the candidate gate), from the "
+             "per-dispatch kernel trace and counter rows.", "",
+             "| kernel | calls | avg µs (all) | avg µs steady | total ms | % | FETCH MB/launch (raw) | FETCH x2 | WRITE MB/launch | VALU G inst/s | VALU issue frac |",
+             "|---|---|---|---|---|---|---|---|---|---|---|"]
     # provenance: the kernel sources the counters were collected on (written on the GPU box by
     # tools/profile_round.sh; bench.py reports traffic only for matching sources)
     sha_file = prof / "sources_sha"
@@ -113,7 +143,7 @@ def main():
         from mageslam_amd.build import kernel_sources_sha
 
         sha = kernel_sources_sha()
-    summary = {"_meta": {"tag": tag, "kernel_sources_sha": sha, "command": cmd}}
+    summary = {"_meta": {"tag": tag, "kernel_sources_sha": sha, "command": cmd, "skipped_warmup_launches": skip}}
     for r in stats:
         k = r["kernel"]
         f = fetch.get(k)
@@ -121,15 +151,17 @@ def main():
         fmb = f * 1024 / 1e6 if f is not None else None
         wmb = w * 1024 / 1e6 if w is not None else None
         v = valu.get(k)
-        vrate = v / (r["avg_us"] * 1e-6) / 1e9 if v is not None and r["avg_us"] > 0 else None
+        steady = trace[k][1] if k in trace else r["avg_us"]
+        vrate = v / (steady * 1e-6) / 1e9 if v is not None and steady > 0 else None
         vfrac = vrate / VALU_PEAK_G if vrate is not None else None
-        lines.append(f"| {k} | {r['calls']} | {r['avg_us']:.1f} | {r['total_ms']:.2f} | {r['pct']:.1f} | "
+        lines.append(f"| {k} | {r['calls']} | {r['avg_us']:.1f} | {steady:.1f} | {r['total_ms']:.2f} | {r['pct']:.1f} | "
                      f"{'' if fmb is None else f'{fmb:.3f}'} | {'' if fmb is None else f'{2 * fmb:.3f}'} | "
                      f"{'' if wmb is None else f'{wmb:.3f}'} | {'' if vrate is None else f'{vrate:.0f}'} | "
                      f"{'' if vfrac is None else f'{vfrac:.2f}'} |")
         tagname = KERNEL_TAG.get(k)
         if tagname:
-            summary[tagname] = {"avg_us": r["avg_us"], "calls": r["calls"],
+            summary[tagname] = {"avg_us": r["avg_us"], "calls": r["calls"], "avg_us_steady": steady,
+                                "steady_launches": trace[k][0] if k in trace else None, "skipped_warmup_launches": skip,
                                 "fetch_bytes_per_launch": None if f is None else f * 1024,
                                 "write_bytes_per_launch": None if w is None else w * 1024,
                                 "hbm_bytes_per_launch": None if (f is None or w is None) else (f + w) * 1024,
