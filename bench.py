@@ -731,9 +731,20 @@ def run_ba_many(args, local_rank, g, budget_s):
         return k, el
 
     res = _per_thread(work, n)
+
+    def work_ref(w):  # the reference schedule (run_ba_reference_schedule) per thread
+        b = libs[w]
+        r = run_ba_reference_schedule(b, g, budget_s, b.SetCurrentLambda, b.GetCurrentLambda, lambda: None)
+        return r["value"]
+
+    ref = _per_thread(work_ref, n)
     return {"value": sum(k / el for k, el in res), "unit": "iters/s", "windows": n,
             "config": f"{n} concurrent copies of the C3 window (one BundlerLib + HIP stream + host thread each), "
-                      f"~{budget_s:.0f} s; sum of per-window rates"}
+                      f"~{budget_s:.0f} s; sum of per-window rates",
+            "reference_schedule": {"value": sum(ref), "unit": "iters/s", "windows": n,
+                                   "config": f"{n} concurrent windows on the reference schedule (graph load + "
+                                             f"{REF_WINDOW_STEPS} decaying-threshold calls with GetPose/GetPoint, "
+                                             f"lambda persisted), ~{budget_s:.0f} s each; sum of per-thread rates"}}
 
 
 def run_ba_many_child(local_rank):
@@ -782,6 +793,22 @@ def cpu_ba_baseline_all(g, budget_s):
     return {"value": sum(k / el for k, el in res), "unit": "iters/s", "cores": n, "kind": "port",
             "sample": f"{n} threads, each its own copy of the C3 window on the GPU leg's schedule for ~{budget_s:.0f} s; "
                       f"sum of per-thread rates"}
+
+
+def cpu_ba_reference_baseline_all(g, budget_s):
+    """The reference schedule on all host cores: one oracle window sequence per thread."""
+    from oracle import oracle as O
+
+    n = host_threads()
+
+    def work(_w):
+        b = O.BundlerOracle()
+        return run_ba_reference_schedule(b, g, budget_s, b.set_lambda, b.get_lambda, lambda: None)["value"]
+
+    vals = _per_thread(work, n)
+    return {"value": sum(vals), "unit": "iters/s", "cores": n, "kind": "port",
+            "sample": f"{n} threads, each its own window sequence on the reference schedule for ~{budget_s:.0f} s; "
+                      f"sum of per-thread rates", "host": host_info()}
 
 
 def run_dry(args, rank, world, dist):
@@ -922,6 +949,12 @@ def main():
                     ba_res["vs_cpu_all_cores"] = ba_res["value"] / ca["value"]
                     if "many_windows" in ba_res:
                         ba_res["many_windows"]["vs_cpu_all_cores"] = ba_res["many_windows"]["value"] / ca["value"]
+                    rca = cpu_ba_reference_baseline_all(g, args.cpu_sample_s / 2)
+                    rs["cpu_baseline_all_cores"] = rca
+                    rs["vs_cpu_all_cores"] = rs["value"] / rca["value"]
+                    mref = (ba_res.get("many_windows") or {}).get("reference_schedule")
+                    if mref:
+                        mref["vs_cpu_all_cores"] = mref["value"] / rca["value"]
                 ba_res["vs_cpu"] = ba_res["value"] / cb["value"]
             if track_res is not None:
                 ct, parity = cpu_tracking_baseline(args, tctx, min(args.cpu_sample_s, 6.0))

@@ -32,6 +32,7 @@
 // then the StepBundleAdjustment post-pass (BundlerLib.cpp:385-446): outlier indices from the
 // speculative (or a fresh) outlier_pass, drop_edges clears their `active` byte.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <atomic>
@@ -1626,6 +1627,143 @@ __global__ __launch_bounds__(BA_THREADS) void drop_edges(const int* __restrict__
     if (atomicSub(&ptcnt[p], 1) == 1) ptfree[p] = 0;
 }
 
+// ---- Schur product lists built on the device (SparseOptimizer::initializeOptimization + g2o's
+// BlockSolver::buildStructure: which pose blocks couple through a shared point) --------------
+// Per free point: its edges in free camera blocks as (block, camera-CSR position), stably sorted
+// by block (insertion sort in place; a point has few edges), and the number of (x, y) products
+// with block(x) <= block(y) (both orders inside one block, as the host lists had them).
+__global__ __launch_bounds__(256) void schur_point_lists(int P, const int* __restrict__ pstart,
+                                                         const int* __restrict__ pedges, const int* __restrict__ ecam,
+                                                         const int* __restrict__ camh, const int* __restrict__ epos,
+                                                         const int* __restrict__ ptfree, int2* __restrict__ plist,
+                                                         int* __restrict__ pcnt, int* __restrict__ klen)
+{
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    if (!ptfree[p]) {
+        pcnt[p] = 0;
+        klen[p] = 0;
+        return;
+    }
+    const int b = pstart[p], end = pstart[p + 1];
+    int k = 0;
+    for (int a = b; a < end; a++) {
+        const int e = pedges[a];
+        const int h = camh[ecam[e]];
+        if (h < 0) continue;
+        int j = k;
+        while (j > 0 && plist[b + j - 1].x > h) {
+            plist[b + j] = plist[b + j - 1];
+            j--;
+        }
+        plist[b + j] = make_int2(h, epos[e]);
+        k++;
+    }
+    int c = 0, g = 0;
+    for (int x = 0; x < k; x++) {
+        if (x > 0 && plist[b + x].x != plist[b + x - 1].x) g = x;
+        c += k - g;
+    }
+    pcnt[p] = c;
+    klen[p] = k;
+}
+
+// The products of one point at its exclusive-scan offset: key = pair (h1 * nb + h2), value =
+// the two camera-CSR positions; in (x, y) order, so a stable sort by key leaves every pair's
+// list in point order.
+__global__ __launch_bounds__(256) void schur_point_products(int P, int nb, const int* __restrict__ pstart,
+                                                            const int2* __restrict__ plist, const int* __restrict__ poff,
+                                                            const int* __restrict__ klen, uint16_t* __restrict__ keys,
+                                                            unsigned long long* __restrict__ vals)
+{
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const int k = klen[p];
+    if (k == 0) return;
+    const int b = pstart[p];
+    int o = poff[p], g = 0;
+    for (int x = 0; x < k; x++) {
+        const int2 hx = plist[b + x];
+        if (x > 0 && hx.x != plist[b + x - 1].x) g = x;
+        for (int y = g; y < k; y++) {
+            const int2 hy = plist[b + y];
+            keys[o] = (uint16_t)(hx.x * nb + hy.x);
+            vals[o] = (unsigned long long)(uint32_t)hx.y | ((unsigned long long)(uint32_t)hy.y << 32);
+            o++;
+        }
+    }
+}
+
+// First and one-past-last sorted position of every pair key (0xFFFF: unused slot).
+__global__ __launch_bounds__(256) void schur_list_bounds(const uint16_t* __restrict__ keys, int n, int nk,
+                                                         int* __restrict__ kb)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int k = keys[i];
+    if (k == 0xFFFF) return;
+    if (i == 0 || keys[i - 1] != k) kb[k] = i;
+    if (i + 1 == n || keys[i + 1] != k) kb[nk + k] = i + 1;
+}
+
+__global__ __launch_bounds__(256) void schur_scatter(const uint16_t* __restrict__ keys,
+                                                     const unsigned long long* __restrict__ vals, int n,
+                                                     const int* __restrict__ kdst, int2* __restrict__ sentries)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int k = keys[i];
+    if (k == 0xFFFF) return;
+    const unsigned long long v = vals[i];
+    sentries[kdst[k] + i] = make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+}
+
+// A free camera block's rhs entries (camera-CSR position, point) over its free-point edges in
+// camera-CSR order: one workgroup per block, a block-wide prefix of the free flags per 256 entries.
+__global__ __launch_bounds__(256) void schur_rhs(const int* __restrict__ camblk, const int* __restrict__ cstart,
+                                                 const int* __restrict__ cpt, const int* __restrict__ ptfree,
+                                                 const int* __restrict__ rblk, int2* __restrict__ sentries)
+{
+    __shared__ int wsum[256 / kWave];
+    const int h = blockIdx.x, c = camblk[h];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int end = cstart[c + 1];
+    int base = rblk[h];
+    for (int a0 = cstart[c]; a0 < end; a0 += 256) {
+        const int a = a0 + (int)threadIdx.x;
+        const int pt = a < end ? cpt[a] : 0;
+        const bool f = a < end && ptfree[pt];
+        const unsigned long long m = __ballot(f);
+        const int below = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = 0, tot = 0;
+        for (int i = 0; i < 256 / kWave; i++) {
+            off += i < w ? wsum[i] : 0;
+            tot += wsum[i];
+        }
+        if (f) sentries[base + off + below] = make_int2(a, pt);
+        base += tot;
+        __syncthreads();
+    }
+}
+
+// The current state (q C x 4, t C x 3, p P x 3 doubles) copied into mapped host memory after a
+// step, so GetPose / GetPoint (UpdateData after every StepBundleAdjustment, BundleAdjust.cpp:
+// 195-226) read it without a D2H copy + stream sync; the completion word is written last.
+__global__ __launch_bounds__(1024) void export_state(State s, int C, int P, double* __restrict__ out,
+                                                     unsigned* __restrict__ seq_out, unsigned seq)
+{
+    const int nq = 4 * C, nt = 3 * C, np = 3 * P;
+    for (int i = threadIdx.x; i < nq + nt + np; i += 1024)
+        out[i] = i < nq ? s.q[i] : i < nq + nt ? s.t[i - nq] : s.p[i - nq - nt];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        *reinterpret_cast<volatile unsigned*>(seq_out) = seq;
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -1697,11 +1835,12 @@ struct BundleAdjuster {
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
-        d_ptcnt, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
+        d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_cub, d_kdst, d_rblk, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
         d_sfinish, d_epos, d_chi_lin, d_livebuf;
     // outlier lists of the speculative / final post-pass (2 x E entries), written by the kernels
     // straight into host memory: the host sorts and returns them after the completion wait
     MappedBuffer h_olist;
+    PinnedBuffer h_kb;  // per-pair list bounds read back by build_product_lists
     std::vector<int> camcnt;  // active observation edges per camera (host-side bookkeeping)
     int n_entries = 0;  // point-CSR entries (active edges at initialisation)
     int nb_free = 0;    // cameras in the reduced system
@@ -1741,10 +1880,12 @@ struct BundleAdjuster {
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
-                        &d_ptcnt, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
+                        &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_cub, &d_kdst, &d_rblk, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf})
             b->release();
         h_olist.release();
+        h_state.release();
+        h_kb.release();
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
         if (h_ctl) (void)hipHostFree(h_ctl);
@@ -1760,10 +1901,37 @@ struct BundleAdjuster {
         return MAGE_OK;
     }
 
+    // export_state's mirror of the current estimate (valid while export_seq is the last sequence
+    // number launched and export_cur the current buffer)
+    MappedBuffer h_state;
+    unsigned export_seq = 0;
+    int export_cur = -1;
+    void launch_export()
+    {
+        if (h_state.reserve((size_t)(7 * C + 3 * P + 1) * sizeof(double)) != MAGE_OK) {
+            export_cur = -1;
+            return;
+        }
+        launch("ba.export_state", export_state, dim3(1), dim3(1024), 0, st, state(cur), C, P, h_state.device<double>(),
+               seq_dev(), ++seq_counter);
+        export_seq = seq_counter;
+        export_cur = cur;
+    }
+
     // Pull the current estimate back to the host vectors.
     mage_status sync_host_state()
     {
         if (!state_on_device || !host_state_stale) return MAGE_OK;
+        if (export_cur == cur && export_seq == seq_counter) {
+            mage_status r = wait_seq(export_seq);
+            if (r != MAGE_OK) return r;
+            const double* m = h_state.host<double>();
+            std::memcpy(q.data(), m, sizeof(double) * 4 * C);
+            std::memcpy(t.data(), m + 4 * C, sizeof(double) * 3 * C);
+            std::memcpy(p.data(), m + 7 * C, sizeof(double) * 3 * P);
+            host_state_stale = false;
+            return MAGE_OK;
+        }
         MAGE_HIP(hipMemcpyAsync(q.data(), d_q[cur].ptr, sizeof(double) * 4 * C, hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipMemcpyAsync(t.data(), d_t[cur].ptr, sizeof(double) * 3 * C, hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipMemcpyAsync(p.data(), d_p[cur].ptr, sizeof(double) * 3 * P, hipMemcpyDeviceToHost, st));
@@ -1774,10 +1942,78 @@ struct BundleAdjuster {
 
     // SparseOptimizer::initializeOptimization (+ StepOptimizer::InitializeOptimization):
     // active edges, vertices in the system, CSR structures, covisible camera pairs; iteration 0.
+    static size_t nprod_pad(long long n) { return (size_t)((n + 255) / 256 * 256); }
+    // Builds every pair's product list on the device (schur_point_lists -> exclusive scan ->
+    // schur_point_products -> stable radix sort by pair key -> schur_list_bounds) and reads back
+    // each dense pair key's first sorted position and count.  nmax bounds the products (sum of
+    // k_p^2); the unused tail holds key 0xFFFF, which sorts after every pair.
+    mage_status build_product_lists(int nmax, int nb, int ncsr, std::vector<int>& kstart, std::vector<int>& kcount)
+    {
+        mage_status r;
+        const int Pm = std::max(P, 1), nk = nb * nb;
+        const size_t pad = nprod_pad(nmax);
+        if ((r = d_plist.reserve((size_t)std::max(ncsr, 1) * sizeof(int2))) != MAGE_OK) return r;
+        if ((r = d_pcnt.reserve((size_t)3 * Pm * sizeof(int))) != MAGE_OK) return r;
+        if ((r = d_skeys.reserve(2 * pad * sizeof(uint16_t))) != MAGE_OK) return r;
+        if ((r = d_svals.reserve(2 * pad * sizeof(unsigned long long))) != MAGE_OK) return r;
+        if ((r = d_kb.reserve((size_t)2 * nk * sizeof(int))) != MAGE_OK) return r;
+        int* pcnt = d_pcnt.as<int>();
+        int* poff = pcnt + Pm;
+        int* klen = pcnt + 2 * Pm;
+        uint16_t* kin = d_skeys.as<uint16_t>();
+        uint16_t* kout = kin + pad;
+        unsigned long long* vin = d_svals.as<unsigned long long>();
+        unsigned long long* vout = vin + pad;
+        int bits = 1;
+        while ((1 << bits) < nk + 1) bits++;
+        size_t tb_scan = 0, tb_sort = 0;
+        MAGE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, pcnt, poff, P, st));
+        MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, kin, kout, vin, vout, nmax, 0, bits, st));
+        if ((r = d_cub.reserve(std::max<size_t>(std::max(tb_scan, tb_sort), 16))) != MAGE_OK) return r;
+        MAGE_HIP(hipMemsetAsync(kin, 0xFF, (size_t)nmax * sizeof(uint16_t), st));
+        MAGE_HIP(hipMemsetAsync(d_kb.ptr, 0, (size_t)2 * nk * sizeof(int), st));
+        const unsigned gp = (unsigned)((P + 255) / 256), gn = (unsigned)((nmax + 255) / 256);
+        launch("ba.schur_lists", schur_point_lists, dim3(gp), dim3(256), 0, st, P, (const int*)d_pstart.as<int>(),
+               (const int*)d_pedges.as<int>(), (const int*)d_ecam.as<int>(), (const int*)d_camh.as<int>(),
+               (const int*)d_epos.as<int>(), (const int*)d_ptfree.as<int>(), d_plist.as<int2>(), pcnt, klen);
+        size_t tb = d_cub.bytes;
+        MAGE_HIP(hipcub::DeviceScan::ExclusiveSum(d_cub.ptr, tb, pcnt, poff, P, st));
+        launch("ba.schur_products", schur_point_products, dim3(gp), dim3(256), 0, st, P, nb,
+               (const int*)d_pstart.as<int>(), (const int2*)d_plist.as<int2>(), (const int*)poff, (const int*)klen, kin, vin);
+        tb = d_cub.bytes;
+        MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(d_cub.ptr, tb, kin, kout, vin, vout, nmax, 0, bits, st));
+        launch("ba.schur_bounds", schur_list_bounds, dim3(gn), dim3(256), 0, st, (const uint16_t*)kout, nmax, nk,
+               d_kb.as<int>());
+        MAGE_HIP(hipGetLastError());
+        if ((r = h_kb.reserve((size_t)2 * nk * sizeof(int))) != MAGE_OK) return r;
+        MAGE_HIP(hipMemcpyAsync(h_kb.ptr, d_kb.ptr, (size_t)2 * nk * sizeof(int), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        const int* kb = h_kb.as<int>();
+        for (int k = 0; k < nk; k++) {
+            kstart[k] = kb[k];
+            kcount[k] = kb[nk + k] - kb[k];
+        }
+        return MAGE_OK;
+    }
+
+    // MAGE_BA_TIMING=1: host phase times of initialize() on stderr (development probe)
+    struct PhaseTimer {
+        bool on = getenv("MAGE_BA_TIMING") != nullptr;
+        std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+        void mark(const char* what)
+        {
+            if (!on) return;
+            const auto n = std::chrono::steady_clock::now();
+            fprintf(stderr, "[ba.init] %-28s %8.1f us\n", what, std::chrono::duration<double, std::micro>(n - t).count());
+            t = n;
+        }
+    };
     mage_status initialize()
     {
+        PhaseTimer pt;
         mage_status r = sync_host_state();
         if (r != MAGE_OK) return r;
+        pt.mark("sync_host_state");
         std::vector<unsigned char> active(E);
         std::vector<int> camHas(C, 0), ptHas(P, 0);
         for (int e = 0; e < E; e++) {
@@ -1818,6 +2054,7 @@ struct BundleAdjuster {
         np = (n + 15) / 16 * 16;
         useless = (nb == 0 && nfp == 0);
         MAGE_REQUIRE(nb <= CH_PANEL_ROWS / 6, MAGE_EUNSUPPORTED, "more than 96 free cameras in one bundle adjustment");
+        pt.mark("active / blocks");
         // CSR by point (edge order) and by camera (point order, then edge order)
         std::vector<int> pstart(P + 1, 0), cstart(C + 1, 0);
         for (int e = 0; e < E; e++)
@@ -1840,31 +2077,42 @@ struct BundleAdjuster {
                     cpt[cf[ecam[e]]++] = i;
                 }
         }
+        pt.mark("CSR");
         // camera-CSR position of every listed edge: Hpl and Z are stored camera-major (component
         // arrays indexed by this position), so a pair's Schur products read them coalesced
         std::vector<int> epos(std::max(E, 1), -1);
         for (int a = 0; a < cstart[C]; a++) epos[cedges[a]] = a;
-        // covisible camera pairs (h1 <= h2) of the reduced system
+        // The structure the Schur products need goes to the device first; the per-pair product
+        // lists are built there (schur_point_lists / _products, a stable radix sort by pair,
+        // schur_list_bounds), the host only reads back the per-pair counts.
+        if ((r = upload(d_epos, epos)) != MAGE_OK) return r;
+        if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
+        if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
+        if ((r = upload(d_pstart, pstart)) != MAGE_OK) return r;
+        if ((r = upload(d_pedges, pedges)) != MAGE_OK) return r;
+        // covisible camera pairs (h1 <= h2) of the reduced system: every pair sharing a free point
+        // (a product list), the diagonal, and the tethered pairs
         std::vector<int2> pairs;
         std::vector<int> pairidx((size_t)std::max(nb, 1) * std::max(nb, 1), -1);
-        std::vector<std::pair<int, int>> hs;  // (block, edge) of a point's edges in the system
-        auto point_edges = [&](int i) {
-            hs.clear();
-            for (int a = pstart[i]; a < pstart[i + 1]; a++) {
-                const int e = pedges[a];
-                const int h = camh[ecam[e]];
-                if (h >= 0) hs.emplace_back(h, e);
-            }
-            std::stable_sort(hs.begin(), hs.end(), [](const std::pair<int, int>& u, const std::pair<int, int>& v) { return u.first < v.first; });
-        };
-        if (nb > 0) {
-            std::vector<unsigned char> mark((size_t)nb * nb, 0);
+        const int nk = std::max(nb, 1) * std::max(nb, 1);  // dense pair keys h1 * nb + h2
+        std::vector<int> kcount(nk, 0), kstart(nk, 0);
+        long long nprod_max = 0;  // sum over free points of k_p^2 bounds the products
+        if (nb > 0 && nfp > 0) {
             for (int i = 0; i < P; i++) {
                 if (!ptfree[i]) continue;
-                point_edges(i);
-                for (size_t x = 0; x < hs.size(); x++)
-                    for (size_t y = x; y < hs.size(); y++) mark[(size_t)hs[x].first * nb + hs[y].first] = 1;
+                long long k = 0;
+                for (int a = pstart[i]; a < pstart[i + 1]; a++) k += camh[ecam[pedges[a]]] >= 0;
+                nprod_max += k * k;
             }
+        }
+        MAGE_REQUIRE(nprod_max < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
+        if (nprod_max > 0) {
+            if ((r = build_product_lists((int)nprod_max, nb, pstart[P], kstart, kcount)) != MAGE_OK) return r;
+        }
+        pt.mark("pairs + product lists (device)");
+        if (nb > 0) {
+            std::vector<unsigned char> mark((size_t)nb * nb, 0);
+            for (int k = 0; k < nb * nb; k++) mark[k] = kcount[k] > 0;
             for (int h = 0; h < nb; h++) mark[(size_t)h * nb + h] = 1;
             for (auto& T : teth) {
                 T.h1 = camh[T.c1];
@@ -1893,41 +2141,51 @@ struct BundleAdjuster {
         }
         // Schur product lists (schur_chunks): per pair the (e1, e2) products of its shared free
         // points in point order, then for a diagonal pair the rhs entries (e, p) in the camera's
-        // point order; two passes (count, fill)
+        // point order (a camera's free-point edges: rcount)
         std::vector<int> pcount(npairs, 0), rcount(npairs, 0);
-        for (int i = 0; i < P; i++) {
-            if (!ptfree[i]) continue;
-            point_edges(i);
-            for (size_t x = 0; x < hs.size(); x++) {
-                rcount[pairidx[(size_t)hs[x].first * nb + hs[x].first]]++;
-                for (size_t y = 0; y < hs.size(); y++)
-                    if (hs[x].first <= hs[y].first) pcount[pairidx[(size_t)hs[x].first * nb + hs[y].first]]++;
-            }
+        for (int pi = 0; pi < npairs; pi++) pcount[pi] = kcount[(size_t)pairs[pi].x * nb + pairs[pi].y];
+        std::vector<int> rblk(std::max(nb, 1), 0);
+        for (int h = 0; h < nb; h++) {
+            const int c = cam_of_block[h];
+            int cnt = 0;
+            for (int a = cstart[c]; a < cstart[c + 1]; a++) cnt += ptfree[cpt[a]];
+            rcount[pairidx[(size_t)h * nb + h]] = cnt;
         }
         std::vector<long long> pbeg(npairs + 1, 0);
         for (int pi = 0; pi < npairs; pi++) pbeg[pi + 1] = pbeg[pi] + pcount[pi] + rcount[pi];
-        std::vector<int2> sentries((size_t)pbeg[npairs] + 1, make_int2(0, 0));  // + one padding entry
+        MAGE_REQUIRE(pbeg[npairs] < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
         {
-            std::vector<long long> pf(npairs), rf(npairs);
+            // destinations: sorted product i of pair key k goes to pbeg[pair] + (i - kstart[k]);
+            // camera block h's rhs entries start at pbeg[diag pair] + pcount
+            std::vector<int> kdst(nk, 0);
             for (int pi = 0; pi < npairs; pi++) {
-                pf[pi] = pbeg[pi];
-                rf[pi] = pbeg[pi] + pcount[pi];
+                const int k = pairs[pi].x * nb + pairs[pi].y;
+                kdst[k] = (int)(pbeg[pi] - kstart[k]);
             }
-            for (int i = 0; i < P; i++) {
-                if (!ptfree[i]) continue;
-                point_edges(i);
-                for (size_t x = 0; x < hs.size(); x++)
-                    for (size_t y = 0; y < hs.size(); y++)
-                        if (hs[x].first <= hs[y].first)
-                            sentries[(size_t)pf[pairidx[(size_t)hs[x].first * nb + hs[y].first]]++] =
-                                make_int2(epos[hs[x].second], epos[hs[y].second]);
+            for (int h = 0; h < nb; h++) {
+                const int pi = pairidx[(size_t)h * nb + h];
+                rblk[h] = (int)(pbeg[pi] + pcount[pi]);
             }
-            for (int h = 0; h < nb; h++) {  // rhs: the camera's edges in point order
-                const int c = cam_of_block[h], pi = pairidx[(size_t)h * nb + h];
-                for (int a = cstart[c]; a < cstart[c + 1]; a++)
-                    if (ptfree[cpt[a]]) sentries[(size_t)rf[pi]++] = make_int2(a, cpt[a]);
-            }
+            if ((r = d_sentries.reserve(((size_t)pbeg[npairs] + 1) * sizeof(int2))) != MAGE_OK) return r;
+            // the padding entry after the last list (schur_chunks reads one past a chunk's end)
+            MAGE_HIP(hipMemsetAsync(d_sentries.as<int2>() + pbeg[npairs], 0, sizeof(int2), st));
+            if ((r = upload(d_kdst, kdst)) != MAGE_OK) return r;
+            if ((r = upload(d_rblk, rblk)) != MAGE_OK) return r;
+            if ((r = upload(d_cstart, cstart)) != MAGE_OK) return r;
+            if ((r = upload(d_cpt, cpt)) != MAGE_OK) return r;
+            if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
+            if (nprod_max > 0)
+                launch("ba.schur_scatter", schur_scatter, dim3((unsigned)((nprod_max + 255) / 256)), dim3(256), 0, st,
+                       (const uint16_t*)d_skeys.as<uint16_t>() + nprod_pad(nprod_max),
+                       (const unsigned long long*)d_svals.as<unsigned long long>() + nprod_pad(nprod_max),
+                       (int)nprod_max, (const int*)d_kdst.as<int>(), d_sentries.as<int2>());
+            if (nb > 0)
+                launch("ba.schur_rhs", schur_rhs, dim3(nb), dim3(256), 0, st, (const int*)d_camblk.as<int>(),
+                       (const int*)d_cstart.as<int>(), (const int*)d_cpt.as<int>(), (const int*)d_ptfree.as<int>(),
+                       (const int*)d_rblk.as<int>(), d_sentries.as<int2>());
+            MAGE_HIP(hipGetLastError());
         }
+        pt.mark("list scatter");
         // chunks; the block rows of S split into 8 contiguous groups of about equal work, one per
         // XCD (block b runs on XCD b % 8)
         std::vector<SchurPair> spairs(npairs);
@@ -1996,14 +2254,11 @@ struct BundleAdjuster {
             if (spairs[pi].nslots > 1 || spairs[pi].h1 == spairs[pi].h2) sfinish.push_back(pi);
         n_sfinish = (int)sfinish.size();
         MAGE_REQUIRE(pbeg[npairs] < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
+        pt.mark("chunks");
         n_entries = pstart[P];
-        if ((r = upload(d_sentries, sentries)) != MAGE_OK) return r;
-        if ((r = upload(d_epos, epos)) != MAGE_OK) return r;
         if ((r = upload(d_sfinish, sfinish)) != MAGE_OK) return r;
         if ((r = upload(d_spairs, spairs)) != MAGE_OK) return r;
         if ((r = upload(d_schunks, schunks)) != MAGE_OK) return r;
-        if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
-        if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
         {
             std::vector<int> ptcnt(P);
             for (int i = 0; i < P; i++) ptcnt[i] = pstart[i + 1] - pstart[i];
@@ -2012,18 +2267,14 @@ struct BundleAdjuster {
             for (int c = 0; c < C; c++) camcnt[c] = cstart[c + 1] - cstart[c];
         }
         if ((r = upload(d_active, active)) != MAGE_OK) return r;
-        if ((r = upload(d_pstart, pstart)) != MAGE_OK) return r;
-        if ((r = upload(d_pedges, pedges)) != MAGE_OK) return r;
-        if ((r = upload(d_cstart, cstart)) != MAGE_OK) return r;
         if ((r = upload(d_cedges, cedges)) != MAGE_OK) return r;
-        if ((r = upload(d_cpt, cpt)) != MAGE_OK) return r;
-        if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
         if ((r = upload(d_ptlist, ptlist)) != MAGE_OK) return r;
         for (auto& T : teth) {
             T.h1 = camh[T.c1];
             T.h2 = camh[T.c2];
         }
         if ((r = upload(d_teth, teth)) != MAGE_OK) return r;
+        pt.mark("uploads");
         if (!state_on_device) {
             if ((r = upload(d_q[0], q)) != MAGE_OK) return r;
             if ((r = upload(d_t[0], t)) != MAGE_OK) return r;
@@ -2061,6 +2312,7 @@ struct BundleAdjuster {
             MAGE_HIP(hipMemsetAsync(d_err.ptr, 0, Em * 2 * 8, st));
             err_initialized = true;
         }
+        pt.mark("buffers");
         iteration = 0;
         dirty = false;
         eager = false;
@@ -2323,6 +2575,7 @@ struct BundleAdjuster {
         // Eager linearisation for the caller's usual next call (BundleAdjust.cpp:311-318: the same
         // huber width, no setter in between): it runs while control is with the caller, and
         // lm_solve reuses it only when the huber width, lambda and state still match.
+        if (host_state_stale) launch_export();
         // After an outlier removal the next Step starts at iteration 0 (lambda re-initialised from
         // the user lambda or computeLambdaInit): the eager linearisation is that iteration's, with
         // the reduction computeLambdaInit reads when no user lambda is set.

@@ -1709,6 +1709,50 @@ struct OrbDetector {
     uint32_t last_batch = 0;  // redo list stride of the last batch
 };
 
+// cv::resize(INTER_LINEAR) 8UC1 tables from a sw x sh source to dw x dh (OpenCV 3.4.0
+// resize.cpp resizeGeneric_ setup, see resize_linear_kernel): per output column xofs and the
+// fixed-point (a0, a1), per output row yofs and (b0, b1), appended to ints / words; the offsets,
+// xmax (first column that reads the last source column), the SIMD bound xv and the exact-2x
+// INTER_AREA switch go to v.
+void resize_tables(int sw, int sh, int dw, int dh, std::vector<int>& ints, std::vector<uint32_t>& words, LevelGeom& v)
+{
+    struct Dim { int w, h; };
+    const Dim src{sw, sh}, dst{dw, dh};
+    const double scale_x = 1. / ((double)dst.w / src.w), scale_y = 1. / ((double)dst.h / src.h);
+    v.xmax = dst.w;
+    v.xofs = ints.size();
+    v.alpha = words.size();
+    for (int dx = 0; dx < dst.w; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) fx = 0, sx = 0;
+        if (sx + 1 >= src.w) {
+            v.xmax = std::min(v.xmax, dx);
+            if (sx >= src.w - 1) fx = 0, sx = src.w - 1;
+        }
+        ints.push_back(sx);
+        const int a0 = (int)std::lrint((1.f - fx) * 2048), a1 = (int)std::lrint(fx * 2048);
+        words.push_back((uint32_t)(uint16_t)a0 | ((uint32_t)(uint16_t)a1 << 16));
+    }
+    v.yofs = ints.size();
+    v.beta = words.size();
+    for (int dy = 0; dy < dst.h; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)std::floor(fy);
+        fy -= sy;
+        ints.push_back(sy);
+        const int b0 = (int)std::lrint((1.f - fy) * 2048), b1 = (int)std::lrint(fy * 2048);
+        words.push_back((uint32_t)(uint16_t)b0 | ((uint32_t)(uint16_t)b1 << 16));
+    }
+    int xv = 0;
+    while (xv <= dst.w - 16) xv += 16;
+    while (xv < dst.w - 4) xv += 4;
+    v.xv = xv;
+    v.area2 = scale_x == 2.0 && scale_y == 2.0;
+    if (v.area2) v.xv = dst.w / 8 * 8;
+}
+
 namespace {
 
 // MakeRandomPattern (OpenCVModified.cpp:551-560) with OpenCV 3.4.0's cv::RNG (multiply-with-carry:
@@ -1830,41 +1874,7 @@ void level_geometry(OrbDetector* o, int w, int h)
     std::vector<int> ints;
     std::vector<uint32_t> words;
     for (int l = 1; l < g.L; l++) {
-        const LevelGeom &src = g.lv[l - 1], &dst = g.lv[l];
-        LevelGeom& v = g.lv[l];
-        const double scale_x = 1. / ((double)dst.w / src.w), scale_y = 1. / ((double)dst.h / src.h);
-        v.xmax = dst.w;
-        v.xofs = ints.size();
-        v.alpha = words.size();
-        for (int dx = 0; dx < dst.w; dx++) {
-            float fx = (float)((dx + 0.5) * scale_x - 0.5);
-            int sx = (int)std::floor(fx);
-            fx -= sx;
-            if (sx < 0) fx = 0, sx = 0;
-            if (sx + 1 >= src.w) {
-                v.xmax = std::min(v.xmax, dx);
-                if (sx >= src.w - 1) fx = 0, sx = src.w - 1;
-            }
-            ints.push_back(sx);
-            const int a0 = (int)std::lrint((1.f - fx) * 2048), a1 = (int)std::lrint(fx * 2048);
-            words.push_back((uint32_t)(uint16_t)a0 | ((uint32_t)(uint16_t)a1 << 16));
-        }
-        v.yofs = ints.size();
-        v.beta = words.size();
-        for (int dy = 0; dy < dst.h; dy++) {
-            float fy = (float)((dy + 0.5) * scale_y - 0.5);
-            int sy = (int)std::floor(fy);
-            fy -= sy;
-            ints.push_back(sy);
-            const int b0 = (int)std::lrint((1.f - fy) * 2048), b1 = (int)std::lrint(fy * 2048);
-            words.push_back((uint32_t)(uint16_t)b0 | ((uint32_t)(uint16_t)b1 << 16));
-        }
-        int xv = 0;
-        while (xv <= dst.w - 16) xv += 16;
-        while (xv < dst.w - 4) xv += 4;
-        v.xv = xv;
-        v.area2 = scale_x == 2.0 && scale_y == 2.0;
-        if (v.area2) v.xv = dst.w / 8 * 8;
+        resize_tables(g.lv[l - 1].w, g.lv[l - 1].h, g.lv[l].w, g.lv[l].h, ints, words, g.lv[l]);
     }
     g.tab_ints = ints;
     g.tab_words = words;

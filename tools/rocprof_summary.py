@@ -38,7 +38,7 @@ KERNEL_TAG = {
     "select_redo_kernel": "orb.select_redo", "describe_kernel": "orb.describe", "describe_blurred_kernel": "orb.describe",
     "match_kernel": "match.two_way", "build_schur": "ba.build_schur", "cholesky_solve": "ba.cholesky_solve",
     "point_linearize": "ba.point_linearize", "cam_linearize": "ba.cam_linearize",
-    "point_backsub": "ba.point_backsub", "edge_schur": "ba.edge_schur", "chol_tiles": "ba.cholesky_solve", "drop_edges": "ba.drop_edges", "update_state": "ba.update_state",
+    "point_backsub": "ba.point_backsub", "edge_schur": "ba.edge_schur", "chol_tiles": "ba.cholesky_solve", "drop_edges": "ba.drop_edges", "export_state": "ba.export_state", "update_state": "ba.update_state",
     "outlier_pass": "ba.outlier_pass", "reduce3": "ba.reduce", "linearize_finish": "ba.linearize_finish",
     "schur_pairs": "ba.schur_pairs", "schur_chunks": "ba.schur_pairs", "schur_finish": "ba.schur_finish",
     "linearize_kernel": "ba.linearize", "evaluate_kernel": "ba.evaluate", "backsub_update": "ba.backsub_update",
