@@ -190,6 +190,44 @@ mage_status mage_undistort_image_batch_device(mage_undistorter* u, const uint8_t
                                               int64_t src_pitch, uint8_t* d_dst, int32_t dst_stride, int64_t dst_pitch,
                                               uint32_t batch, mage_stream stream);
 
+/* cv::resize(src, dst, Size(dw, dh), 0, 0, INTER_LINEAR) for CV_8UC1 (OpenCV 3.4.0 fixed-point
+ * path, the pyramid levels' resize of OpenCVModified.cpp:833), any scale.  Device buffers,
+ * asynchronous on `stream`. */
+mage_status mage_resize_linear_device(const uint8_t* d_src, int32_t sw, int32_t sh, int32_t src_stride, uint8_t* d_dst,
+                                      int32_t dw, int32_t dh, int32_t dst_stride, mage_stream stream);
+
+/* Stereo frame preparation — ImagePreprocessor::ScaleImageForCameraConfiguration
+ * (Core/.../Source/Image/ImagePreprocessor.cpp:18-65).  A camera as the reference passes it: its
+ * MAGESlam::CameraConfiguration (Extrinsics: mage::Matrix M11..M44 row-major; Size) and the
+ * undistorted pinhole CameraCalibration of the same size (fx, fy, cx, cy). */
+typedef struct mage_camera_config {
+    float extrinsics[16];
+    float fx, fy, cx, cy;
+    uint32_t width, height;
+} mage_camera_config;
+
+/* The geometry: targetToSource = source.Extrinsics * inverse(target.Extrinsics) (cv::Matx44f, LU
+ * inverse), the overlap crop of the source frame in the target frame at max_depth_meters
+ * (CalculateOverlapCropSourceInTarget, MageUtil.cpp:13-58; crop_xywh = the cv::Rect), *ok = 0 when
+ * it lies entirely offscreen (IsEntirelyOffscreen, Utils/cv.h:405-418; the reference returns
+ * false), else scaleSourceToTarget and the prepared camera: size (int)(size * scale) and
+ * GetScaledIntrinsics (CameraCalibration.cpp:150-157) when scale != 1, the source otherwise.
+ * Host only. */
+mage_status mage_scale_for_camera_configuration(const mage_camera_config* source, const mage_camera_config* target,
+                                                float max_depth_meters, int32_t crop_xywh[4], float* scale,
+                                                mage_camera_config* prepared, int32_t* ok);
+
+/* The whole call on a device image: the geometry above, then the source->width x source->height
+ * image at d_src (src_stride) resized with INTER_LINEAR into d_dst (dst_stride; prepared->height
+ * rows of prepared->width bytes; dst_capacity bytes available), or copied when scale == 1.
+ * Nothing is written when *ok = 0.  Asynchronous on `stream`. */
+mage_status mage_scale_image_for_camera_configuration_device(const mage_camera_config* source,
+                                                             const mage_camera_config* target, float max_depth_meters,
+                                                             const uint8_t* d_src, int32_t src_stride, uint8_t* d_dst,
+                                                             int32_t dst_stride, int64_t dst_capacity,
+                                                             mage_camera_config* prepared, float* scale, int32_t* ok,
+                                                             mage_stream stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Hamming matching — replaces FeatureMatcher (Core/.../Source/Tracking/FeatureMatcher.h)        */
 /* ------------------------------------------------------------------------------------------ */

@@ -26,7 +26,8 @@ EXPORTS = [
     "mage_synth_frames_device", "mage_synth_scene_device", "mage_orb_fast_score_map",
     "mage_undistort_keypoints", "mage_undistort_keypoints_batch_device",
     "mage_undistorter_create", "mage_undistorter_destroy", "mage_undistorter_get_maps", "mage_undistort_image",
-    "mage_undistort_image_batch_device",
+    "mage_undistort_image_batch_device", "mage_resize_linear_device", "mage_scale_for_camera_configuration",
+    "mage_scale_image_for_camera_configuration_device",
     "mage_hamming_distance", "mage_hamming_match", "mage_hamming_match_batch_device",
     "mage_radius_match", "mage_radius_match_batch_device",
     "mage_bow_create", "mage_bow_destroy", "mage_bow_train", "mage_bow_train_kmedoid", "mage_bow_get_tree", "mage_bow_find_leaves", "mage_bow_find_leaves_device",
@@ -56,6 +57,18 @@ class Calibration(C.Structure):
         if len(d) not in (0, 5, 8):
             raise ValueError("distortion: 0 (None), 5 (Poly3k) or 8 (Rational6k) coefficients")
         return cls(fx, fy, cx, cy, (C.c_float * 8)(*(d + [0.0] * (8 - len(d)))), len(d))
+
+
+class CameraConfig(C.Structure):
+    """mage_camera_config: MAGESlam::CameraConfiguration (Extrinsics M11..M44 row-major, Size) with
+    its undistorted pinhole calibration."""
+    _fields_ = [("extrinsics", C.c_float * 16), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float),
+                ("cy", C.c_float), ("width", C.c_uint32), ("height", C.c_uint32)]
+
+    @classmethod
+    def make(cls, extrinsics, fx, fy, cx, cy, width, height):
+        e = np.asarray(extrinsics, np.float32).reshape(16)
+        return cls((C.c_float * 16)(*e.tolist()), fx, fy, cx, cy, width, height)
 
 
 class KeyPoint(C.Structure):
@@ -169,6 +182,10 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_undistorter_get_maps", st, vp, vp, vp)
     sig("mage_undistort_image", st, vp, vp, i32, vp, i32)
     sig("mage_undistort_image_batch_device", st, vp, vp, i32, i64, vp, i32, i64, u32, vp)
+    sig("mage_resize_linear_device", st, vp, i32, i32, i32, vp, i32, i32, i32, vp)
+    sig("mage_scale_for_camera_configuration", st, vp, vp, f32, vp, C.POINTER(f32), vp, C.POINTER(i32))
+    sig("mage_scale_image_for_camera_configuration_device", st, vp, vp, f32, vp, i32, vp, i32, i64, vp,
+        C.POINTER(f32), C.POINTER(i32), vp)
     sig("mage_hamming_distance", i32, vp, vp)
     sig("mage_hamming_match", st, vp, u32, vp, vp, u32, vp, i32, i32, vp, u32, C.POINTER(u32))
     sig("mage_hamming_match_batch_device", st, vp, i64, vp, vp, i64, vp, u32, i32, i32, vp, u32, vp, vp)

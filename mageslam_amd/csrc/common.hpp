@@ -154,10 +154,15 @@ HostScratch* host_scratch(int device, ScratchSlot slot);
 // thread that grows its buffer (sync of the stream, then free) can only free memory its own
 // launches used — never a pointer another thread is about to launch on.  Freed at thread exit or
 // when the stream's HostScratch is destroyed.  nullptr (error set) if the allocation fails.
-enum StreamSlot : int { STREAM_MATCH_ROWS = 0, STREAM_MATCH_STATUS = 1 };
+enum StreamSlot : int { STREAM_MATCH_ROWS = 0, STREAM_MATCH_STATUS = 1, STREAM_RESIZE_TABLES = 2 };
 void* stream_scratch(hipStream_t st, StreamSlot slot, size_t bytes);
 
 constexpr int kWave = 64;
+
+// cv::resize(INTER_LINEAR) 8UC1 of one device image (orb.hip, the pyramid's resize_linear_kernel);
+// asynchronous on st.
+mage_status resize_linear_device(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh,
+                                 int dstride, hipStream_t st);
 
 // Optional per-kernel timing with HIP events recorded on the launch stream (mage_profile_*).
 // When disabled (the default) a KernelTimer costs one relaxed flag check.

@@ -21,7 +21,11 @@
 //                         is loaded into registers while frame f is computed (LDS double buffer).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cfloat>
 #include <climits>
+#include <limits>
+#include <utility>
 #include <cmath>
 
 #include "common.hpp"
@@ -361,10 +365,203 @@ __global__ __launch_bounds__(256) void synth_scene_kernel(uint8_t* __restrict__ 
     out[f * p.pitch + (long long)y * p.w + x] = (uint8_t)(g < 0 ? 0 : (g > 255 ? 255 : g));
 }
 
+// ---- ScaleImageForCameraConfiguration geometry (ImagePreprocessor.cpp:18-65) ----------------
+// cv::Matx44f arithmetic as OpenCV 3.4.0 evaluates it in float: products element by element with
+// the sum started at 0 and taken left to right (Matx_MatMulOp), inverse() by LU with partial
+// pivoting (Matx_FastInvOp -> hal::LU32f, eps = 10 FLT_EPSILON; zeros if singular), the 3x3
+// inverse by the adjugate over a float determinant (Matx_FastInvOp<_Tp, 3>).
+void matx_mul(const float* a, const float* b, float* out, int m, int l, int n)
+{
+    for (int i = 0; i < m; i++)
+        for (int j = 0; j < n; j++) {
+            float s = 0.f;
+            for (int k = 0; k < l; k++) s += a[i * l + k] * b[k * n + j];
+            out[i * n + j] = s;
+        }
+}
+
+void matx44_inv_lu(const float* a, float* b)
+{
+    float A[16];
+    for (int i = 0; i < 16; i++) A[i] = a[i], b[i] = (i % 5 == 0) ? 1.f : 0.f;
+    const int m = 4;
+    for (int i = 0; i < m; i++) {
+        int k = i;
+        for (int j = i + 1; j < m; j++)
+            if (std::fabs(A[j * m + i]) > std::fabs(A[k * m + i])) k = j;
+        if (std::fabs(A[k * m + i]) < FLT_EPSILON * 10) {
+            for (int t = 0; t < 16; t++) b[t] = 0.f;
+            return;
+        }
+        if (k != i) {
+            for (int j = i; j < m; j++) std::swap(A[i * m + j], A[k * m + j]);
+            for (int j = 0; j < m; j++) std::swap(b[i * m + j], b[k * m + j]);
+        }
+        const float d = -1.f / A[i * m + i];
+        for (int j = i + 1; j < m; j++) {
+            const float alpha = A[j * m + i] * d;
+            for (int t = i + 1; t < m; t++) A[j * m + t] += alpha * A[i * m + t];
+            for (int t = 0; t < m; t++) b[j * m + t] += alpha * b[i * m + t];
+        }
+    }
+    for (int i = m - 1; i >= 0; i--)
+        for (int j = 0; j < m; j++) {
+            float s = b[i * m + j];
+            for (int t = i + 1; t < m; t++) s -= A[i * m + t] * b[t * m + j];
+            b[i * m + j] = s / A[i * m + i];
+        }
+}
+
+void matx33_inv(const float* a, float* b)
+{
+#define A_(i, j) a[(i) * 3 + (j)]
+    float d = (float)(double)(A_(0, 0) * (A_(1, 1) * A_(2, 2) - A_(2, 1) * A_(1, 2)) -
+                              A_(0, 1) * (A_(1, 0) * A_(2, 2) - A_(2, 0) * A_(1, 2)) +
+                              A_(0, 2) * (A_(1, 0) * A_(2, 1) - A_(2, 0) * A_(1, 1)));
+    if (d == 0) {
+        for (int t = 0; t < 9; t++) b[t] = 0.f;
+        return;
+    }
+    d = 1 / d;
+    b[0] = (A_(1, 1) * A_(2, 2) - A_(1, 2) * A_(2, 1)) * d;
+    b[1] = (A_(0, 2) * A_(2, 1) - A_(0, 1) * A_(2, 2)) * d;
+    b[2] = (A_(0, 1) * A_(1, 2) - A_(0, 2) * A_(1, 1)) * d;
+    b[3] = (A_(1, 2) * A_(2, 0) - A_(1, 0) * A_(2, 2)) * d;
+    b[4] = (A_(0, 0) * A_(2, 2) - A_(0, 2) * A_(2, 0)) * d;
+    b[5] = (A_(0, 2) * A_(1, 0) - A_(0, 0) * A_(1, 2)) * d;
+    b[6] = (A_(1, 0) * A_(2, 1) - A_(1, 1) * A_(2, 0)) * d;
+    b[7] = (A_(0, 1) * A_(2, 0) - A_(0, 0) * A_(2, 1)) * d;
+    b[8] = (A_(0, 0) * A_(1, 1) - A_(0, 1) * A_(1, 0)) * d;
+#undef A_
+}
+
+// Utils/cv.h:226-262 Invert: the rigid inverse (transposed rotation) x (negated translation)
+void rigid_invert(const float* T, float* out)
+{
+    const float R[16] = {T[0], T[4], T[8], 0, T[1], T[5], T[9], 0, T[2], T[6], T[10], 0, 0, 0, 0, 1};
+    const float Tr[16] = {1, 0, 0, -T[3], 0, 1, 0, -T[7], 0, 0, 1, -T[11], 0, 0, 0, 1};
+    matx_mul(R, Tr, out, 4, 4, 4);
+}
+
+void camera_matrix(const mage_camera_config& c, float K[9])
+{
+    const float k[9] = {c.fx, 0, c.cx, 0, c.fy, c.cy, 0, 0, 1};
+    for (int i = 0; i < 9; i++) K[i] = k[i];
+}
+
+}  // namespace
+
+// ScaleImageForCameraConfiguration's geometry (ImagePreprocessor.cpp:32-57 with
+// CalculateOverlapCropSourceInTarget, MageUtil.cpp:13-58, UnProject / ProjectUndistorted,
+// Utils/cv.h:270-278 and Reprojection.cpp:26-42, IsEntirelyOffscreen, Utils/cv.h:405-418).
+mage_status scale_geometry(const mage_camera_config& src, const mage_camera_config& tgt, float depth, int crop[4],
+                           float* scale, mage_camera_config* prepared, int* ok)
+{
+    MAGE_REQUIRE(src.width > 0 && src.height > 0 && tgt.width > 0 && tgt.height > 0, MAGE_EINVAL,
+                 "camera configurations need a nonzero size");
+    float tinv[16], t2s[16];
+    matx44_inv_lu(tgt.extrinsics, tinv);
+    matx_mul(src.extrinsics, tinv, t2s, 4, 4, 4);  // targetToSource
+    float Ks[9], Ksi[9], Kt[9], view_inv[16];
+    camera_matrix(src, Ks);
+    matx33_inv(Ks, Ksi);
+    camera_matrix(tgt, Kt);
+    rigid_invert(t2s, view_inv);
+    const float maxc = (float)src.width - 1, maxr = (float)(src.height - 1);
+    const float corners[4][2] = {{0, 0}, {maxc, 0}, {0, maxr}, {maxc, maxr}};
+    float mnx = std::numeric_limits<float>::max(), mny = std::numeric_limits<float>::max();
+    float mxx = std::numeric_limits<float>::min(), mxy = std::numeric_limits<float>::min();
+    for (auto& pt : corners) {
+        const float pix[3] = {(float)(int)pt[0], (float)(int)pt[1], 1.f};
+        float cs[3];
+        matx_mul(Ksi, pix, cs, 3, 3, 1);
+        for (float& v : cs) v *= depth;
+        const float c4[4] = {cs[0], cs[1], cs[2], 1};
+        float w[4];
+        matx_mul(view_inv, c4, w, 4, 4, 1);
+        // ProjectUndistorted with the identity 3x4 view matrix
+        const float eye[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        const float w4[4] = {w[0], w[1], w[2], 1};
+        float cam[3];
+        matx_mul(eye, w4, cam, 3, 4, 1);
+        const float div = cam[2] != 0 ? cam[2] : 1;
+        const float px = (cam[0] / div) * Kt[0] + Kt[2], py = (cam[1] / div) * Kt[4] + Kt[5];
+        mnx = std::min(mnx, px);
+        mny = std::min(mny, py);
+        mxx = std::max(mxx, px);
+        mxy = std::max(mxy, py);
+    }
+    const float width = mxx - mnx + 1, height = mxy - mny + 1;
+    MAGE_REQUIRE(width >= 0 && height >= 0, MAGE_EINVAL, "overlap crop with a negative extent (camera behind)");
+    // mage::Rect {int, int, size_t, size_t} -> cv::Rect (ToCVRect, Utils/cv.h:429-432)
+    crop[0] = (int)mnx;
+    crop[1] = (int)mny;
+    crop[2] = (int)(size_t)width;
+    crop[3] = (int)(size_t)height;
+    const int maxh = crop[2] + crop[0] - 1, maxv = crop[3] + crop[1] - 1;
+    const bool offx = maxh < 0 || crop[0] > (int)(tgt.width - 1);
+    const bool offy = maxv < 0 || crop[1] > (int)(tgt.height - 1);
+    *prepared = src;
+    if (offx || offy) {
+        *ok = 0;
+        *scale = 0.f;
+        return MAGE_OK;
+    }
+    *ok = 1;
+    const float s = std::max(crop[2] / (float)src.width, crop[3] / (float)src.height);
+    *scale = s;
+    if (s != 1.0f) {
+        // cv::Size{(int)(Width * scale), ...}; GetScaledIntrinsics for the calibration
+        prepared->width = (uint32_t)(int)((float)src.width * s);
+        prepared->height = (uint32_t)(int)((float)src.height * s);
+        prepared->cx = src.cx * s;
+        prepared->cy = src.cy * s;
+        prepared->fx = src.fx * s;
+        prepared->fy = src.fy * s;
+    }
+    return MAGE_OK;
+}
+
+namespace {
 }  // namespace
 }  // namespace mage
 
 extern "C" {
+
+mage_status mage_scale_for_camera_configuration(const mage_camera_config* source, const mage_camera_config* target,
+                                                float max_depth_meters, int32_t crop_xywh[4], float* scale,
+                                                mage_camera_config* prepared, int32_t* ok)
+{
+    MAGE_REQUIRE(source && target && crop_xywh && scale && prepared && ok, MAGE_EINVAL, "null argument");
+    int crop[4], k = 0;
+    mage_status r = mage::scale_geometry(*source, *target, max_depth_meters, crop, scale, prepared, &k);
+    for (int i = 0; i < 4; i++) crop_xywh[i] = crop[i];
+    *ok = k;
+    return r;
+}
+
+mage_status mage_scale_image_for_camera_configuration_device(const mage_camera_config* source,
+                                                             const mage_camera_config* target, float max_depth_meters,
+                                                             const uint8_t* d_src, int32_t src_stride, uint8_t* d_dst,
+                                                             int32_t dst_stride, int64_t dst_capacity,
+                                                             mage_camera_config* prepared, float* scale, int32_t* ok,
+                                                             mage_stream stream)
+{
+    MAGE_REQUIRE(source && target && prepared && scale && ok && d_src && d_dst, MAGE_EINVAL, "null argument");
+    int crop[4], k = 0;
+    mage_status r = mage::scale_geometry(*source, *target, max_depth_meters, crop, scale, prepared, &k);
+    *ok = k;
+    if (r != MAGE_OK || !k) return r;
+    const int sw = (int)source->width, sh = (int)source->height, dw = (int)prepared->width, dh = (int)prepared->height;
+    MAGE_REQUIRE(src_stride >= sw && dst_stride >= dw && dw > 0 && dh > 0, MAGE_EINVAL, "invalid image strides");
+    MAGE_REQUIRE((int64_t)dst_stride * (dh - 1) + dw <= dst_capacity, MAGE_ECAPACITY,
+                 "destination too small for the prepared image");
+    hipStream_t st = (hipStream_t)stream;
+    if (*scale != 1.0f) return mage::resize_linear_device(d_src, sw, sh, src_stride, d_dst, dw, dh, dst_stride, st);
+    // preparedImage = rawSourceImage.clone()
+    MAGE_HIP(hipMemcpy2DAsync(d_dst, dst_stride, d_src, src_stride, sw, sh, hipMemcpyDeviceToDevice, st));
+    return MAGE_OK;
+}
 
 mage_status mage_undistorter_create(const mage_calibration* distorted, int32_t width, int32_t height, int device,
                                     mage_undistorter** out, mage_calibration* undistorted)

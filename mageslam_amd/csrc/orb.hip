@@ -1753,6 +1753,61 @@ void resize_tables(int sw, int sh, int dw, int dh, std::vector<int>& ints, std::
     if (v.area2) v.xv = dst.w / 8 * 8;
 }
 
+mage_status resize_linear_device(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh,
+                                 int dstride, hipStream_t st)
+{
+    MAGE_REQUIRE(src && dst && sw > 0 && sh > 0 && dw > 0 && dh > 0 && sstride >= sw && dstride >= dw, MAGE_EINVAL,
+                 "resize: invalid image geometry");
+    // the tables of the last geometry stay in this thread's stream scratch; a new geometry is
+    // uploaded (and waited for: the source vectors are pageable) before the launch
+    struct Key {
+        int dev, sw, sh, dw, dh;
+        hipStream_t st;
+        const void* tab;
+    };
+    thread_local std::vector<Key> cache;
+    int dev = 0;
+    MAGE_HIP(hipGetDevice(&dev));
+    Key* k = nullptr;
+    for (auto& c : cache)
+        if (c.dev == dev && c.st == st && c.sw == sw && c.sh == sh && c.dw == dw && c.dh == dh) k = &c;
+    std::vector<int> ints;
+    std::vector<uint32_t> words;
+    LevelGeom v;
+    resize_tables(sw, sh, dw, dh, ints, words, v);
+    const size_t ib = ints.size() * 4, wb = words.size() * 4;
+    uint8_t* tab = static_cast<uint8_t*>(stream_scratch(st, STREAM_RESIZE_TABLES, ib + wb));
+    if (!tab) return MAGE_ENOMEM;
+    if (!k || k->tab != tab) {
+        MAGE_HIP(hipMemcpyAsync(tab, ints.data(), ib, hipMemcpyHostToDevice, st));
+        MAGE_HIP(hipMemcpyAsync(tab + ib, words.data(), wb, hipMemcpyHostToDevice, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        for (auto& c : cache)
+            if (c.dev == dev && c.st == st) c.sw = -1;  // the scratch now holds the new tables
+        if (k) k->tab = tab, k->sw = sw;
+        else cache.push_back(Key{dev, sw, sh, dw, dh, st, tab});
+    }
+    const int* it = reinterpret_cast<const int*>(tab);
+    const uint32_t* wt = reinterpret_cast<const uint32_t*>(tab + ib);
+    ResizeParams rp{};
+    rp.sw = sw;
+    rp.sh = sh;
+    rp.sstride = sstride;
+    rp.dw = dw;
+    rp.dh = dh;
+    rp.dstride = dstride;
+    rp.xmax = v.xmax;
+    rp.xv = v.xv;
+    rp.area2 = v.area2;
+    rp.xofs = it + v.xofs;
+    rp.yofs = it + v.yofs;
+    rp.alpha = wt + v.alpha;
+    rp.beta = wt + v.beta;
+    launch("image.resize", resize_linear_kernel, dim3((dw + 255) / 256, dh, 1), dim3(256), 0, st, src, dst, rp);
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}
+
 namespace {
 
 // MakeRandomPattern (OpenCVModified.cpp:551-560) with OpenCV 3.4.0's cv::RNG (multiply-with-carry:
@@ -2485,6 +2540,12 @@ mage_status mage_synth_frames_device(uint8_t* d_out, uint32_t count, int32_t wid
                        width, height, (long long)frame_pitch, t0, (unsigned long long)seed);
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;
+}
+
+mage_status mage_resize_linear_device(const uint8_t* d_src, int32_t sw, int32_t sh, int32_t src_stride, uint8_t* d_dst,
+                                      int32_t dw, int32_t dh, int32_t dst_stride, mage_stream stream)
+{
+    return mage::resize_linear_device(d_src, sw, sh, src_stride, d_dst, dw, dh, dst_stride, (hipStream_t)stream);
 }
 
 }  // extern "C"

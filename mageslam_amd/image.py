@@ -1,6 +1,8 @@
 """Frame ingest and undistortion — host mirror of ImagePreprocessor (Core/MAGESLAM/Source/Image/
 ImagePreprocessor.cpp:71-120) and CreateGrayCVMat (Utils/cv.cpp:8-28).
 
+`ScaleImageForCameraConfiguration` (ImagePreprocessor.cpp:18-65) brings a stereo frame to the other
+camera's resolution (overlap-crop geometry on the host, resize on the GPU).
 `ImagePreprocessor.UndistortImage(distortedImage, distortedCalibration)` returns the undistorted
 frame and calibration like the reference, caching the device-resident CV_32FC1 maps per
 (size, calibration) as `CachedUndistortDataValid` does.  `gray_view` is CreateGrayCVMat without the
@@ -14,7 +16,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import Calibration, check, ptr
+from ._lib import Calibration, CameraConfig, check, load, ptr
 
 GRAYSCALE8, NV12 = 0, 1
 
@@ -93,3 +95,54 @@ class ImagePreprocessor:
             self._u = Undistorter(distortedCameraCal, w, h, self.device)
             self._key = key
         return self._u(distortedImage), self._u.undistorted
+
+
+def scale_geometry(source: CameraConfig, target: CameraConfig, max_depth_meters: float = 2.3):
+    """ScaleImageForCameraConfiguration's geometry (mage_scale_for_camera_configuration):
+    (ok, crop (x, y, w, h), scaleSourceToTarget, prepared CameraConfig).  max_depth_meters defaults
+    to StereoMapInitializationSettings::MaxDepthMeters (MageSettings.h:144)."""
+    crop = (C.c_int32 * 4)()
+    scale, ok = C.c_float(0), C.c_int32(0)
+    prepared = CameraConfig()
+    check(load().mage_scale_for_camera_configuration(C.byref(source), C.byref(target), float(max_depth_meters), crop,
+                                                      C.byref(scale), C.byref(prepared), C.byref(ok)))
+    return bool(ok.value), tuple(crop), float(scale.value), prepared
+
+
+def ScaleImageForCameraConfiguration(source: CameraConfig, target: CameraConfig, rawSourceImage,
+                                     max_depth_meters: float = 2.3, device: int = 0):
+    """ImagePreprocessor::ScaleImageForCameraConfiguration (ImagePreprocessor.cpp:18-65) on the GPU:
+    -> (ok, preparedImage, prepared CameraConfig, scaleSourceToTarget).  The image (H x W uint8,
+    numpy or a CUDA tensor) is resized with cv::resize INTER_LINEAR (or copied when the scale is 1)
+    by mage_scale_image_for_camera_configuration_device; preparedImage is None when there is no overlap."""
+    import torch
+
+    dev = torch.device("cuda", device)
+    src = rawSourceImage if isinstance(rawSourceImage, torch.Tensor) else torch.from_numpy(
+        np.ascontiguousarray(rawSourceImage, np.uint8))
+    src = src.to(dev).contiguous()
+    h, w = src.shape
+    if (w, h) != (source.width, source.height):
+        raise ValueError("the image size must match the source camera configuration")
+    ok, _, scale, prepared = scale_geometry(source, target, max_depth_meters)
+    if not ok:
+        return False, None, prepared, scale
+    out = torch.empty((prepared.height, prepared.width), dtype=torch.uint8, device=dev)
+    s2, k2, p2 = C.c_float(0), C.c_int32(0), CameraConfig()
+    check(load().mage_scale_image_for_camera_configuration_device(
+        C.byref(source), C.byref(target), float(max_depth_meters), ptr(src), w, ptr(out), prepared.width,
+        out.numel(), C.byref(p2), C.byref(s2), C.byref(k2), None))
+    torch.cuda.synchronize(dev)
+    res = out if isinstance(rawSourceImage, torch.Tensor) else out.cpu().numpy()
+    return True, res, p2, float(s2.value)
+
+
+def resize_linear_device(src, dw: int, dh: int, stream=None):
+    """cv::resize(INTER_LINEAR) 8UC1 of a CUDA tensor (mage_resize_linear_device)."""
+    import torch
+
+    h, w = src.shape
+    out = torch.empty((dh, dw), dtype=torch.uint8, device=src.device)
+    check(load().mage_resize_linear_device(ptr(src), w, h, w, ptr(out), dw, dh, dw,
+                                           C.c_void_p(stream) if stream else None))
+    return out

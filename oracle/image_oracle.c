@@ -131,3 +131,160 @@ void oracle_remap_linear(const uint8_t* src, int sw, int sh, int sstride, const 
             dst[(size_t)y * dstride + x] = (uint8_t)(r < 0 ? 0 : r > 255 ? 255 : r);
         }
 }
+
+/* ---- ImagePreprocessor::ScaleImageForCameraConfiguration (ImagePreprocessor.cpp:18-65) ------
+ * Restated geometry (the image step is oracle_resize_linear, orb_oracle.c):
+ *   targetToSource = ToCVMat4x4(source.Extrinsics) * ToCVMat4x4(target.Extrinsics).inv()   (:34)
+ *     cv::Matx44f: products with the sum started at 0 and taken left to right; inv() = LU with
+ *     partial pivoting (OpenCV 3.4.0 Matx_FastInvOp -> hal::LU32f / LUImpl, eps 10*FLT_EPSILON,
+ *     all zeros if singular);
+ *   CalculateOverlapCropSourceInTarget (MageUtil.cpp:13-58): the 4 source corners (0,0), (W-1,0),
+ *     (0,H-1), (W-1,H-1) UnProject'ed (Utils/cv.h:270-278: inv(K_src) (3x3 adjugate over the float
+ *     determinant, Matx_FastInvOp<_Tp,3>) x pixel, * depth, then Invert(targetToSource) (cv.h:226-262:
+ *     transposed rotation x negated translation) x (p, 1)), ProjectUndistorted with the identity view
+ *     (Reprojection.cpp:26-42); min initialised to FLT_MAX, max to FLT_MIN (the smallest positive
+ *     float, as the reference does); width = max - min + 1; Rect{(int)min.x, (int)min.y,
+ *     (size_t)width, (size_t)height} -> cv::Rect (ToCVRect, cv.h:429-432);
+ *   IsEntirelyOffscreen (cv.h:405-418) -> not ok;
+ *   scale = max(crop.width / (float)W, crop.height / (float)H); size (int)(W * scale);
+ *   GetScaledIntrinsics (CameraCalibration.cpp:150-157) when scale != 1.
+ * cfg layout (float[22] view of mage_camera_config): extrinsics[16] (M11..M44), fx, fy, cx, cy, then
+ * width / height as uint32 (read through w_h). */
+#include <float.h>
+
+static void o_mul(const float* a, const float* b, float* c, int m, int l, int n)
+{
+    for (int i = 0; i < m; i++)
+        for (int j = 0; j < n; j++) {
+            float s = 0.f;
+            for (int k = 0; k < l; k++) s += a[i * l + k] * b[k * n + j];
+            c[i * n + j] = s;
+        }
+}
+
+static void o_inv4(const float* src, float* inv)
+{
+    float a[4][4], b[4][4];
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            a[i][j] = src[4 * i + j];
+            b[i][j] = i == j ? 1.f : 0.f;
+        }
+    for (int i = 0; i < 4; i++) {
+        int p = i;
+        for (int j = i + 1; j < 4; j++)
+            if (fabsf(a[j][i]) > fabsf(a[p][i])) p = j;
+        if (fabsf(a[p][i]) < FLT_EPSILON * 10) {
+            memset(inv, 0, 16 * sizeof(float));
+            return;
+        }
+        if (p != i) {
+            for (int j = i; j < 4; j++) {
+                float t = a[i][j];
+                a[i][j] = a[p][j];
+                a[p][j] = t;
+            }
+            for (int j = 0; j < 4; j++) {
+                float t = b[i][j];
+                b[i][j] = b[p][j];
+                b[p][j] = t;
+            }
+        }
+        float d = -1.f / a[i][i];
+        for (int j = i + 1; j < 4; j++) {
+            float alpha = a[j][i] * d;
+            for (int k = i + 1; k < 4; k++) a[j][k] += alpha * a[i][k];
+            for (int k = 0; k < 4; k++) b[j][k] += alpha * b[i][k];
+        }
+    }
+    for (int i = 3; i >= 0; i--)
+        for (int j = 0; j < 4; j++) {
+            float s = b[i][j];
+            for (int k = i + 1; k < 4; k++) s -= a[i][k] * b[k][j];
+            b[i][j] = s / a[i][i];
+        }
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) inv[4 * i + j] = b[i][j];
+}
+
+static void o_inv3(const float* m, float* r)
+{
+    float d = m[0] * (m[4] * m[8] - m[7] * m[5]) - m[1] * (m[3] * m[8] - m[6] * m[5]) +
+              m[2] * (m[3] * m[7] - m[6] * m[4]);
+    if (d == 0) {
+        memset(r, 0, 9 * sizeof(float));
+        return;
+    }
+    d = 1 / d;
+    r[0] = (m[4] * m[8] - m[5] * m[7]) * d;
+    r[1] = (m[2] * m[7] - m[1] * m[8]) * d;
+    r[2] = (m[1] * m[5] - m[2] * m[4]) * d;
+    r[3] = (m[5] * m[6] - m[3] * m[8]) * d;
+    r[4] = (m[0] * m[8] - m[2] * m[6]) * d;
+    r[5] = (m[2] * m[3] - m[0] * m[5]) * d;
+    r[6] = (m[3] * m[7] - m[4] * m[6]) * d;
+    r[7] = (m[1] * m[6] - m[0] * m[7]) * d;
+    r[8] = (m[0] * m[4] - m[1] * m[3]) * d;
+}
+
+/* returns ok; crop[4], scale, out_wh[2], out_k[4] = {fx, fy, cx, cy} of the prepared camera */
+int oracle_scale_geometry(const float* src_ext, const float* src_k, const uint32_t* src_wh, const float* tgt_ext,
+                          const float* tgt_k, const uint32_t* tgt_wh, float depth, int* crop, float* scale,
+                          uint32_t* out_wh, float* out_k)
+{
+    float ti[16], t2s[16];
+    o_inv4(tgt_ext, ti);
+    o_mul(src_ext, ti, t2s, 4, 4, 4);
+    const float Ks[9] = {src_k[0], 0, src_k[2], 0, src_k[1], src_k[3], 0, 0, 1};
+    float Ki[9];
+    o_inv3(Ks, Ki);
+    const float rot[16] = {t2s[0], t2s[4], t2s[8], 0, t2s[1], t2s[5], t2s[9], 0, t2s[2], t2s[6], t2s[10], 0, 0, 0, 0, 1};
+    const float tr[16] = {1, 0, 0, -t2s[3], 0, 1, 0, -t2s[7], 0, 0, 1, -t2s[11], 0, 0, 0, 1};
+    float vinv[16];
+    o_mul(rot, tr, vinv, 4, 4, 4);
+    const float mc = (float)src_wh[0] - 1, mr = (float)(src_wh[1] - 1);
+    const float cx[4] = {0, mc, 0, mc}, cy[4] = {0, 0, mr, mr};
+    float lox = FLT_MAX, loy = FLT_MAX, hix = FLT_MIN, hiy = FLT_MIN;
+    for (int c = 0; c < 4; c++) {
+        const float pix[3] = {(float)(int)cx[c], (float)(int)cy[c], 1.f};
+        float cam[3];
+        o_mul(Ki, pix, cam, 3, 3, 1);
+        for (int k = 0; k < 3; k++) cam[k] *= depth;
+        const float h4[4] = {cam[0], cam[1], cam[2], 1};
+        float w[4];
+        o_mul(vinv, h4, w, 4, 4, 1);
+        const float eye[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        const float w4[4] = {w[0], w[1], w[2], 1};
+        float v[3];
+        o_mul(eye, w4, v, 3, 4, 1);
+        const float z = v[2] != 0 ? v[2] : 1;
+        const float px = (v[0] / z) * tgt_k[0] + tgt_k[2];
+        const float py = (v[1] / z) * tgt_k[1] + tgt_k[3];
+        if (px < lox) lox = px;
+        if (py < loy) loy = py;
+        if (px > hix) hix = px;
+        if (py > hiy) hiy = py;
+    }
+    const float wd = hix - lox + 1, ht = hiy - loy + 1;
+    crop[0] = (int)lox;
+    crop[1] = (int)loy;
+    crop[2] = (int)(size_t)wd;
+    crop[3] = (int)(size_t)ht;
+    out_wh[0] = src_wh[0];
+    out_wh[1] = src_wh[1];
+    for (int k = 0; k < 4; k++) out_k[k] = src_k[k];
+    const int mxh = crop[2] + crop[0] - 1, mxv = crop[3] + crop[1] - 1;
+    if (mxh < 0 || crop[0] > (int)(tgt_wh[0] - 1) || mxv < 0 || crop[1] > (int)(tgt_wh[1] - 1)) {
+        *scale = 0.f;
+        return 0;
+    }
+    const float sx = crop[2] / (float)src_wh[0], sy = crop[3] / (float)src_wh[1];
+    const float s = sx > sy ? sx : sy;
+    *scale = s;
+    if (s != 1.0f) {
+        out_wh[0] = (uint32_t)(int)((float)src_wh[0] * s);
+        out_wh[1] = (uint32_t)(int)((float)src_wh[1] * s);
+        for (int k = 0; k < 4; k++) out_k[k] = src_k[k] * s;
+    }
+    return 1;
+}

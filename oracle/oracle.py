@@ -100,6 +100,8 @@ def _declare(L):
     L.oracle_ba_set_tethers.argtypes = [vp, i32, i32, vp, vp, vp, vp]
     L.oracle_undistort_map.argtypes = [vp, vp, i32, vp, i32, i32, vp, vp]
     L.oracle_remap_linear.argtypes = [vp, i32, i32, i32, vp, vp, i32, i32, vp, i32]
+    L.oracle_scale_geometry.argtypes = [vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp]
+    L.oracle_scale_geometry.restype = i32
     L.oracle_ba_pose_batch.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp]
     L.oracle_bow_find_leaf.argtypes = [vp, vp, vp, vp]
     L.oracle_bow_find_leaf.restype = u32
@@ -564,3 +566,28 @@ class OnlineBowOracle:
         v = [(kf, sc) for kf, sc in scores.items() if sc >= qualifyingScore]
         v.sort(key=lambda t: (-t[1], t[0]))
         return [(int(kf), float(sc)) for kf, sc in v[:maxResults]]
+
+
+def scale_geometry(src_ext, src_k, src_wh, tgt_ext, tgt_k, tgt_wh, depth=2.3):
+    """ScaleImageForCameraConfiguration geometry restated (image_oracle.c): k = (fx, fy, cx, cy),
+    wh = (width, height).  -> (ok, crop (x, y, w, h), scale, (width, height), (fx, fy, cx, cy))."""
+    se, te = np.ascontiguousarray(src_ext, np.float32).reshape(16), np.ascontiguousarray(tgt_ext, np.float32).reshape(16)
+    sk, tk = np.ascontiguousarray(src_k, np.float32), np.ascontiguousarray(tgt_k, np.float32)
+    sw, tw = np.ascontiguousarray(src_wh, np.uint32), np.ascontiguousarray(tgt_wh, np.uint32)
+    crop = np.zeros(4, np.int32)
+    scale = np.zeros(1, np.float32)
+    owh = np.zeros(2, np.uint32)
+    ok_k = np.zeros(4, np.float32)
+    ok = lib().oracle_scale_geometry(_p(se), _p(sk), _p(sw), _p(te), _p(tk), _p(tw), float(depth), _p(crop), _p(scale),
+                                     _p(owh), _p(ok_k))
+    return bool(ok), tuple(int(v) for v in crop), float(scale[0]), tuple(int(v) for v in owh), tuple(ok_k.tolist())
+
+
+def scale_image_for_camera_configuration(img, src_ext, src_k, tgt_ext, tgt_k, tgt_wh, depth=2.3):
+    """The whole ScaleImageForCameraConfiguration: geometry, then resize INTER_LINEAR (or the clone)."""
+    h, w = img.shape
+    ok, crop, scale, (ow, oh), k = scale_geometry(src_ext, src_k, (w, h), tgt_ext, tgt_k, tgt_wh, depth)
+    if not ok:
+        return False, None, scale, k
+    out = resize_linear(img, ow, oh) if scale != 1.0 else img.copy()
+    return True, out, scale, k
