@@ -267,6 +267,20 @@ mage_status mage_radius_match(const mage_keypoint* query_kp, const float* query_
                               int32_t max_distance, int32_t min_difference, mage_dmatch* out,
                               uint32_t cap, uint32_t* n);
 
+/* TrackLocalMap's per-map-point matching (TrackLocalMap.cpp:175-256: ProjectMapPointIntoCurrentFrame
+ * -> MatchMapPointToCurrentFrame -> the single-query RadiusMatch of FeatureMatcher.cpp:386-446) over
+ * projected map points in order: point i searches the frame keypoints in its box (|x - qx| <=
+ * radius, |y - qy| <= radius, same octave) that are still unassociated (mask[t] != 0), keeps the best
+ * Hamming distance with the reference's "second = previous best" rule (candidates in ascending
+ * keypoint order) and, when best <= max_distance and second - best > min_difference, associates
+ * keypoint t: result[i] = t and mask[t] = 0 for every later point.  query_hide[i] >= 0 is the
+ * keypoint a pose-estimation outlier point was matched to, hidden from its own search (:192-229);
+ * NULL = none.  result[i] = -1 when no match.  Host buffers, synchronous; n_target <= 4096. */
+mage_status mage_local_map_match(const float* query_pos, const int32_t* query_octave, const uint8_t* query_desc,
+                                 const int32_t* query_hide, uint32_t n_query, const mage_keypoint* target_kp,
+                                 const uint8_t* target_desc, uint32_t n_target, uint8_t* mask, float radius,
+                                 int32_t max_distance, int32_t min_difference, int32_t* result, int device);
+
 /* Batched device form, one (query set, target set) pair per workgroup: pair p reads
  * query_pitch / target_pitch entries further on (keypoints, positions, 32-byte descriptors),
  * counts from d_n_query[p] / d_n_target[p]; no masks.  d_scratch: pairs x query_pitch int32.

@@ -29,7 +29,7 @@ EXPORTS = [
     "mage_undistort_image_batch_device", "mage_resize_linear_device", "mage_scale_for_camera_configuration",
     "mage_scale_image_for_camera_configuration_device",
     "mage_hamming_distance", "mage_hamming_match", "mage_hamming_match_batch_device",
-    "mage_radius_match", "mage_radius_match_batch_device",
+    "mage_radius_match", "mage_radius_match_batch_device", "mage_local_map_match",
     "mage_bow_create", "mage_bow_destroy", "mage_bow_train", "mage_bow_train_kmedoid", "mage_bow_get_tree", "mage_bow_find_leaves", "mage_bow_find_leaves_device",
     "mage_indexed_match", "mage_indexed_match_batch_device",
     "mage_ba_create", "mage_ba_destroy", "mage_ba_set_cameras", "mage_ba_fix_camera",
@@ -192,6 +192,7 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_radius_match", st, vp, vp, vp, vp, u32, vp, vp, vp, u32, C.c_float, i32, i32, vp, u32, C.POINTER(u32))
     sig("mage_radius_match_batch_device", st, vp, vp, vp, i64, vp, vp, vp, i64, vp, u32, C.c_float, i32, i32, vp,
         vp, u32, vp, vp, vp)
+    sig("mage_local_map_match", st, vp, vp, vp, vp, u32, vp, vp, u32, vp, C.c_float, i32, i32, vp, C.c_int)
     sig("mage_bow_create", st, vp, vp, vp, u32, C.c_int, C.POINTER(vp))
     sig("mage_bow_destroy", st, vp)
     sig("mage_bow_train", st, vp, u32, u32, u32, u32, C.c_int, C.POINTER(vp))

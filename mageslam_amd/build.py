@@ -19,7 +19,7 @@ OBJ = OUT / "obj"
 LIB = OUT / "libmage_hot.so"
 ARCH = os.environ.get("MAGE_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["orb.hip", "match.hip", "radius.hip", "bow.hip", "ba.hip", "pose.hip", "image.hip", "track.hip"]
+HIP_SOURCES = ["orb.hip", "match.hip", "radius.hip", "localmap.hip", "bow.hip", "ba.hip", "pose.hip", "image.hip", "track.hip"]
 CXX_SOURCES = ["capi.cpp", "tables.cpp", "track.cpp"]
 
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function",

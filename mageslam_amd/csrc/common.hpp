@@ -135,7 +135,7 @@ struct MappedBuffer {
 // frames' OrbFeatureDetector::Process (UndistortKeypoints) run in parallel
 // (ImageAnalyzer.cpp:160-216) and the matchers take a per-thread thread_memory.  Released when the
 // thread exits.
-enum ScratchSlot : int { SCRATCH_RADIUS = 0, SCRATCH_POSE = 1, SCRATCH_UNDISTORT = 2, SCRATCH_MATCH = 3 };
+enum ScratchSlot : int { SCRATCH_RADIUS = 0, SCRATCH_POSE = 1, SCRATCH_UNDISTORT = 2, SCRATCH_MATCH = 3, SCRATCH_LOCALMAP = 4 };
 struct HostScratch {
     DeviceBuffer buf, aux;
     PinnedBuffer host;
@@ -158,6 +158,29 @@ enum StreamSlot : int { STREAM_MATCH_ROWS = 0, STREAM_MATCH_STATUS = 1, STREAM_R
 void* stream_scratch(hipStream_t st, StreamSlot slot, size_t bytes);
 
 constexpr int kWave = 64;
+
+// TrackLocalMap's sequential per-map-point matching (localmap.hip): queries in order (projected
+// position, octave, descriptor, hidden keypoint or -1), the frame's keypoints, the unassociated
+// mask as bit words (bit t = keypoint t available; updated in place), result[q] = keypoint or -1.
+// Counts are device words (q_cap / 4096 bound them); status bits report bad counts.
+struct LocalMapArgs {
+    const float* qpos;
+    const int* qoct;
+    const int* qhide;
+    const uint8_t* qdesc;
+    const uint32_t* nq;
+    uint32_t q_cap;
+    const mage_keypoint* tkp;
+    const uint8_t* tdesc;
+    const uint32_t* nt;
+    uint32_t* mask_words;
+    float radius;
+    int max_dist, min_diff;
+    int* result;
+    uint32_t* status;
+};
+size_t local_map_scratch_bytes(uint32_t q_cap);
+mage_status local_map_match_launch(const LocalMapArgs& a, void* scratch, hipStream_t st);
 
 // cv::resize(INTER_LINEAR) 8UC1 of one device image (orb.hip, the pyramid's resize_linear_kernel);
 // asynchronous on st.

@@ -25,6 +25,7 @@
 #include <cstring>
 
 #include "common.hpp"
+#include "band_index.hpp"
 #include "lds_sort.hpp"
 
 namespace mage {
@@ -53,29 +54,6 @@ struct RadiusParams {
     uint32_t* n_out;
     uint32_t* status;  // bit 0: a target set exceeded RM_MAXT; bit 1: a count exceeded its pitch
 };
-
-__device__ __forceinline__ unsigned orderable(float v)
-{
-    const unsigned u = __float_as_uint(v);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-
-__device__ __forceinline__ unsigned long long band_key(int octave, float y, unsigned idx)
-{
-    return ((unsigned long long)(octave & 0xFF) << 56) | ((unsigned long long)orderable(y) << 24) | idx;
-}
-
-// first position in keys[0, n) (ascending) with keys[pos] >= k
-__device__ __forceinline__ int lower_bound_keys(const unsigned long long* keys, int n, unsigned long long k)
-{
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (keys[mid] < k) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
 
 constexpr int RM_GROUP = 16;  // lanes per query (a band holds ~20-150 candidates)
 constexpr int RM_GROUPS = SORT_THREADS / RM_GROUP;

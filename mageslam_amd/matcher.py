@@ -14,7 +14,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import DM_DTYPE, check, ptr
+from ._lib import DM_DTYPE, KP_DTYPE, check, load, ptr
 
 
 def GetDescriptorDistance(d0: np.ndarray, d1: np.ndarray) -> int:
@@ -95,3 +95,24 @@ def radius_match_batch_device(query_kp, query_pos, query_desc, query_pitch: int,
         ptr(query_kp), ptr(query_pos), ptr(query_desc), query_pitch, ptr(n_query), ptr(target_kp), ptr(target_desc),
         target_pitch, ptr(n_target), pairs, float(radius), max_distance, min_difference, ptr(scratch), ptr(out),
         capacity, ptr(n_out), ptr(status), C.c_void_p(stream) if stream else None))
+
+
+def LocalMapMatch(queryPositions, queryOctaves, queryDescriptors, targetKeypoints, targetDescriptors, unassociatedMask,
+                  radius: float = 8.0, maxHammingDist: int = 30, minHammingDifference: int = 1, queryHidden=None,
+                  device: int = 0):
+    """TrackLocalMap's per-map-point matching over projected map points in order
+    (TrackLocalMap.cpp:175-256 -> MatchMapPointToCurrentFrame -> RadiusMatch, FeatureMatcher.cpp:386-446),
+    through mage_local_map_match: -> (result (n,) int32 keypoint index or -1, updated mask (True =
+    still unassociated))."""
+    qp = np.ascontiguousarray(queryPositions, np.float32).reshape(-1, 2)
+    n = len(qp)
+    qo = np.ascontiguousarray(queryOctaves, np.int32).reshape(n)
+    qd = np.ascontiguousarray(queryDescriptors, np.uint8).reshape(n, 32)
+    qh = None if queryHidden is None else np.ascontiguousarray(queryHidden, np.int32).reshape(n)
+    tk = np.ascontiguousarray(targetKeypoints, KP_DTYPE)
+    td = np.ascontiguousarray(targetDescriptors, np.uint8).reshape(-1, 32)
+    m = np.ascontiguousarray(unassociatedMask, np.uint8).reshape(len(tk)).copy()
+    res = np.full(max(n, 1), -1, np.int32)
+    check(load().mage_local_map_match(ptr(qp), ptr(qo), ptr(qd), ptr(qh), n, ptr(tk), ptr(td), len(tk), ptr(m),
+                                      float(radius), int(maxHammingDist), int(minHammingDifference), ptr(res), device))
+    return res[:n].copy(), m.astype(bool)

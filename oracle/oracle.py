@@ -100,6 +100,7 @@ def _declare(L):
     L.oracle_ba_set_tethers.argtypes = [vp, i32, i32, vp, vp, vp, vp]
     L.oracle_undistort_map.argtypes = [vp, vp, i32, vp, i32, i32, vp, vp]
     L.oracle_remap_linear.argtypes = [vp, i32, i32, i32, vp, vp, i32, i32, vp, i32]
+    L.oracle_local_map_match.argtypes = [vp, vp, vp, vp, u32, vp, vp, u32, vp, f32, i32, i32, vp]
     L.oracle_scale_geometry.argtypes = [vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp]
     L.oracle_scale_geometry.restype = i32
     L.oracle_ba_pose_batch.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp]
@@ -268,6 +269,22 @@ def radius_match(qkp, qdesc, tkp, tdesc, radius, qpos=None, qmask=None, tmask=No
     n = lib().oracle_radius_match(_p(qkp), _p(qp), _p(qm), _p(qd), len(qkp), _p(tkp), _p(tm), _p(td), len(tkp),
                                   float(radius), int(max_distance), int(min_difference), _p(out), cap)
     return out[:n].copy()
+
+
+def local_map_match(qpos, qoct, qdesc, hide, tkp, tdesc, mask, radius=8.0, max_distance=30, min_difference=1):
+    """TrackLocalMap's sequential per-map-point matching (orb_oracle.c oracle_local_map_match):
+    -> (result (n,) int32 keypoint or -1, updated mask)."""
+    qp = np.ascontiguousarray(qpos, np.float32).reshape(-1, 2)
+    qo = np.ascontiguousarray(qoct, np.int32)
+    qd = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+    hd = None if hide is None else np.ascontiguousarray(hide, np.int32)
+    tk = np.ascontiguousarray(tkp, KP_DTYPE)
+    td = np.ascontiguousarray(tdesc, np.uint8).reshape(-1, 32)
+    m = np.ascontiguousarray(mask, np.uint8).copy()
+    res = np.zeros(max(len(qp), 1), np.int32)
+    lib().oracle_local_map_match(_p(qp), _p(qo), _p(qd), _p(hd), len(qp), _p(tk), _p(td), len(tk), _p(m),
+                                 float(radius), int(max_distance), int(min_difference), _p(res))
+    return res[:len(qp)].copy(), m
 
 
 def match(desc_a, desc_b, mask_a=None, mask_b=None, max_distance=30, min_difference=1):

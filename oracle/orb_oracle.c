@@ -913,3 +913,47 @@ uint32_t oracle_match(const uint8_t* da, uint32_t na, const uint8_t* ma, const u
     free(ib);
     return n;
 }
+
+/* TrackLocalMap's per-map-point loop (TrackLocalMap.cpp:175-256) reduced to its matching: for each
+ * projected map point in order — hide the keypoint a pose-estimation outlier point was matched to
+ * when it is currently unassociated (:192-203), MatchMapPointToCurrentFrame = the single-query
+ * RadiusMatch (FeatureMatcher.cpp:386-446) against the unassociated keypoints (box |x - qx| <= r,
+ * |y - qy| <= r, the query's octave; ascending keypoint order as above), unhide (:224-229), and on a
+ * match associate the keypoint: unassociatedMask[t] = false (:249-255).  mask: 1 = unassociated,
+ * updated in place; hide[i] = -1 for none; result[i] = keypoint or -1. */
+void oracle_local_map_match(const float* qpos, const int32_t* qoct, const uint8_t* qdesc, const int32_t* hide,
+                            uint32_t nq, const mage_keypoint* tkp, const uint8_t* tdesc, uint32_t nt, uint8_t* mask,
+                            float radius, int maxDist, int minDiff, int32_t* result)
+{
+    for (uint32_t q = 0; q < nq; q++) {
+        const int h = hide ? hide[q] : -1;
+        int hidden = 0;
+        if (h >= 0 && mask[h]) {
+            mask[h] = 0;
+            hidden = 1;
+        }
+        const float px = qpos[2 * q], py = qpos[2 * q + 1];
+        const float oq = (float)qoct[q] * 100.0f;
+        int best = maxDist + 1, second = 2147483647, train = -1;
+        for (uint32_t t = 0; t < nt; t++) {
+            const float ot = (float)tkp[t].octave * 100.0f;
+            if (!(tkp[t].x >= px - radius && tkp[t].x <= px + radius && tkp[t].y >= py - radius &&
+                  tkp[t].y <= py + radius && ot >= oq - 1.0f && ot <= oq + 1.0f))
+                continue;
+            if (!mask[t]) continue;
+            const int d = oracle_hamming(qdesc + 32 * (size_t)q, tdesc + 32 * (size_t)t);
+            if (d < best) {
+                train = (int)t;
+                second = best;
+                best = d;
+            }
+        }
+        if (hidden) mask[h] = 1;
+        if (train != -1 && (second - best) > minDiff) {
+            result[q] = train;
+            mask[train] = 0;
+        } else {
+            result[q] = -1;
+        }
+    }
+}
