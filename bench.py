@@ -580,6 +580,7 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
     torch.cuda.synchronize()
     K = (seq.fx, seq.fy, seq.cx, seq.cy)
     p0 = tracking.Pose(seq.R[0], seq.t[0])
+    ts = tracking.TrackerSettings(width=args.width, height=args.height)
     N = args.features
     det = orb.OrbDetector(nfeatures=N, device=local_rank)
     d_kp = torch.zeros((T, N * 28), dtype=torch.uint8, device=dev)
@@ -593,7 +594,7 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
                                                 d_desc[b0:b1], d_n[b0:b1], N)
 
     extract_device(8)  # warm-up
-    tracking.track_native_device(d_kp, d_desc, N, d_n, 8, K, p0, synth.SCENE_PLANE_Z)
+    tracking.track_native_device(d_kp, d_desc, N, d_n, 8, K, p0, synth.SCENE_PLANE_Z, settings=ts)
     torch.cuda.synchronize()
     # the timed loop: device-resident extraction + mage_track_sequence_device (one sync)
     multigpu.barrier(dist)
@@ -601,7 +602,7 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
     extract_device(T)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    res = tracking.track_native_device(d_kp, d_desc, N, d_n, T, K, p0, synth.SCENE_PLANE_Z)
+    res = tracking.track_native_device(d_kp, d_desc, N, d_n, T, K, p0, synth.SCENE_PLANE_Z, settings=ts)
     t2 = time.perf_counter()
     multigpu.barrier(dist)
     el_max = multigpu.max_over_ranks(t2 - t0, dev, dist)
@@ -609,12 +610,13 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
         torch.tensor([T / (t2 - t0)], dtype=torch.float64, device=dev), dist)]
     gathered, own = c5_exchange(res, rank, dist, dev, args.trajectory_csv)
     gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)])
-    out = {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose)",
+    out = {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose + local map)",
            "value": world * T / el_max, "unit": "frames/s", "frames": T, "dtype": "u8 / f64",
            "extract_ms_per_frame": 1000 * (t1 - t0) / T, "track_ms_per_frame": 1000 * (t2 - t1) / T,
            "loop": "device-resident (mage_track_sequence_device: per-frame decisions on the GPU, one sync)",
            "mean_matches": float(np.mean(res.matches[1:])), "mean_inliers": float(np.mean(res.inliers[1:])),
            "keyframes": len(res.keyframes), "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
+           "local_map": f"TrackLocalMap local-map search over the last {ts.local_map_keyframes} keyframes",
            "config": {"workload": f"C4: {T}-frame {args.width}x{args.height} hand-held pan over a textured plane "
                                   f"(synthetic), {args.features} features/frame"
                                   + (f"; C5: {world} independent sequences (seed + rank), one per GPU, RCCL "
@@ -632,10 +634,10 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
     feats = be.extract(frames)
     torch.cuda.synchronize()
     t3 = time.perf_counter()
-    host = tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, device=local_rank)
+    host = tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, settings=ts, device=local_rank)
     torch.cuda.synchronize()
     t4 = time.perf_counter()
-    py = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be)
+    py = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be, ts)
     t5 = time.perf_counter()
 
     def same(a, b):
@@ -665,7 +667,8 @@ def cpu_tracking_baseline(args, ctx, budget_s):
     K = (seq.fx, seq.fy, seq.cx, seq.cy)
     p0 = tracking.Pose(seq.R[0], seq.t[0])
     t1 = time.perf_counter()
-    ores = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, ob)
+    ores = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, ob, tracking.TrackerSettings(width=args.width,
+                                                                                          height=args.height))
     el = time.perf_counter() - t1 + el
     n = len(feats)
     gsub = tracking.TrackResult(poses=gres.poses[:n])

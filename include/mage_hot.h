@@ -468,6 +468,18 @@ typedef struct mage_track_settings {
     float refinement_info;                                               /* 1 - 1/1.5^2 */
     double keyframe_ratio;                                               /* 0.5 */
     uint32_t keyframe_min;                                               /* 25 */
+    /* TrackLocalMap's local-map search between the two pose passes (TrackLocalMap.cpp:114-265,
+     * TrackLocalMapSettings MageSettings.h:180-194); local_map_keyframes = 0 turns it off.  The
+     * local map is the last local_map_keyframes keyframes, visited in ascending keyframe id. */
+    uint32_t local_map_keyframes;                                        /* 4 (<= 8) */
+    float match_search_radius;                                           /* MatchSearchRadius 8 */
+    int32_t local_max_hamming, local_min_hamming_difference;             /* OrbMatcherSettings 30, 1 */
+    float min_view_cos;         /* cosf(deg2rad(MinDegreesBetweenCurrentViewAndMapPointView = 60)) */
+    float image_border;                                                  /* PatchSize / 2 = 7.5 */
+    uint32_t min_tracked;                                                /* MinTrackedFeatureCount 20 */
+    float scale_factor;                                                  /* pyramid ScaleFactor 1.5 */
+    uint32_t num_levels;                                                 /* pyramid levels 1 */
+    int32_t width, height;                                               /* image size */
 } mage_track_settings;
 
 /* Features of `frames` frames (host): keypoints kp[frame_start[f] .. frame_start[f+1]) and their

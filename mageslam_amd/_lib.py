@@ -95,7 +95,11 @@ class TrackSettingsC(C.Structure):
                 ("min_matches", C.c_uint32), ("max_hamming", C.c_int32), ("min_hamming_difference", C.c_int32),
                 ("initial_steps", C.c_uint32), ("initial_huber", C.c_float), ("initial_max_error", C.c_double),
                 ("final_steps", C.c_uint32), ("final_huber", C.c_float), ("final_max_error", C.c_double),
-                ("refinement_info", C.c_float), ("keyframe_ratio", C.c_double), ("keyframe_min", C.c_uint32)]
+                ("refinement_info", C.c_float), ("keyframe_ratio", C.c_double), ("keyframe_min", C.c_uint32),
+                ("local_map_keyframes", C.c_uint32), ("match_search_radius", C.c_float),
+                ("local_max_hamming", C.c_int32), ("local_min_hamming_difference", C.c_int32),
+                ("min_view_cos", C.c_float), ("image_border", C.c_float), ("min_tracked", C.c_uint32),
+                ("scale_factor", C.c_float), ("num_levels", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32)]
 
 
 class BAStats(C.Structure):

@@ -60,6 +60,7 @@ __global__ __launch_bounds__(SORT_THREADS) void lm_keys_kernel(LocalMapArgs a, u
 {
     __shared__ unsigned long long keys[LM_MAXT];
     const int n = (int)*a.nt, tid = threadIdx.x;
+    if (*a.nq == 0) return;  // the tracker's frames without local-map queries
     if (n > LM_MAXT) {
         if (tid == 0) atomicOr(a.status, 1u);
         return;

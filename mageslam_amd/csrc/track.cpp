@@ -14,7 +14,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
+#include <deque>
 #include <vector>
 
 #include "common.hpp"
@@ -55,10 +57,60 @@ Pose mul(const Pose& a, const Pose& b)
 }
 
 struct Keyframe {
+    uint32_t id = 0;
     std::vector<mage_keypoint> kp;
     std::vector<uint8_t> desc;
     std::vector<float> pts;  // n x 3
+    std::vector<float> mvd;  // n x 3 mean viewing direction
+    std::vector<float> dmin, dmax;
 };
+
+// Pose::GetWorldSpacePosition: column 3 of Invert(viewMatrix) (Utils/cv.h:226-262), float
+void world_position(const Pose& p, float C[3])
+{
+    float R[9], t[3];
+    for (int i = 0; i < 9; i++) R[i] = (float)p.R[i];
+    for (int i = 0; i < 3; i++) t[i] = (float)p.t[i];
+    for (int i = 0; i < 3; i++) {
+        float s = 0.f;
+        for (int k = 0; k < 3; k++) s = s + R[3 * k + i] * -t[k];
+        C[i] = s + 0.f;
+    }
+}
+
+float dot3(const float* a, const float* b) { return ((0.f + a[0] * b[0]) + a[1] * b[1]) + a[2] * b[2]; }
+
+// MapPoint::UpdateMeanViewDirectionAndDistances (Map/MapPoint.cpp:131-154) for points seen by one
+// keyframe: Normalize(Normalize(point - centre)), dmax / dmin from |centre - point|
+void map_point_attributes(Keyframe& kf, const Pose& p, const float fmax[8], const float fmin[8])
+{
+    float C[3];
+    world_position(p, C);
+    const size_t n = kf.kp.size();
+    kf.mvd.resize(3 * n);
+    kf.dmin.resize(n);
+    kf.dmax.resize(n);
+    for (size_t i = 0; i < n; i++) {
+        const float* P = &kf.pts[3 * i];
+        float v[3] = {P[0] - C[0], P[1] - C[1], P[2] - C[2]};
+        const float d = sqrtf(dot3(v, v));
+        if (d != 0) {
+            const float inv = 1.f / d;
+            for (float& x : v) x = x * inv;
+        }
+        const float d2 = sqrtf(dot3(v, v));
+        if (d2 != 0) {
+            const float inv = 1.f / d2;
+            for (float& x : v) x = x * inv;
+        }
+        for (int j = 0; j < 3; j++) kf.mvd[3 * i + j] = v[j];
+        const float dl[3] = {C[0] - P[0], C[1] - P[1], C[2] - P[2]};
+        const float dist = sqrtf((dl[0] * dl[0] + dl[1] * dl[1]) + dl[2] * dl[2]);
+        const int o = std::min(std::max(kf.kp[i].octave, 0), 7);
+        kf.dmin[i] = dist * fmin[o];
+        kf.dmax[i] = dist * fmax[o];
+    }
+}
 
 // keypoint rays of `pose` meet the plane Z = plane_z
 void backproject(const mage_keypoint* kp, uint32_t n, const Pose& p, const double K[4], double plane_z,
@@ -126,10 +178,28 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
     std::vector<Pose> P(frames);
     std::memcpy(P[0].R, first_pose, 9 * sizeof(double));
     std::memcpy(P[0].t, first_pose + 9, 3 * sizeof(double));
-    Keyframe kf;
-    kf.kp.assign(frame_kp(0), frame_kp(0) + frame_n(0));
-    kf.desc.assign(frame_desc(0), frame_desc(0) + 32ull * frame_n(0));
-    backproject(kf.kp.data(), frame_n(0), P[0], K, plane_z, kf.pts);
+    // ComputeDMax / ComputeDMin factors per octave (MappingMath.h:32-40), ComputeOctave's log2f(scale)
+    float fmax[8], fmin[8];
+    for (int o = 0; o < 8; o++) {
+        fmax[o] = powf(s->scale_factor, (float)s->num_levels - ((float)o + 0.5f));
+        fmin[o] = powf(s->scale_factor, 0.f - ((float)o + 0.5f));
+    }
+    const float log2s = (float)std::log2((double)s->scale_factor);
+    const uint32_t NK = std::max(s->local_map_keyframes, 1u);
+    MAGE_REQUIRE(s->local_map_keyframes <= 8, MAGE_EINVAL, "local_map_keyframes must be <= 8");
+    std::deque<Keyframe> kfs(1);
+    Keyframe* kfp = &kfs.back();
+    auto make_kf = [&](uint32_t f, const Pose& p) {
+        Keyframe k;
+        k.id = f;
+        k.kp.assign(frame_kp(f), frame_kp(f) + frame_n(f));
+        k.desc.assign(frame_desc(f), frame_desc(f) + 32ull * frame_n(f));
+        backproject(k.kp.data(), frame_n(f), p, K, plane_z, k.pts);
+        map_point_attributes(k, p, fmax, fmin);
+        return k;
+    };
+    kfs.back() = make_kf(0, P[0]);
+    kfp = &kfs.back();
     matches[0] = inliers[0] = frame_n(0);
     std::memset(keyframe, 0, frames);
     keyframe[0] = 1;
@@ -137,7 +207,9 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
     std::vector<uint32_t> sel;
     std::vector<mage_keypoint> qkp;
     std::vector<uint8_t> qdesc, out1, out2;
-    std::vector<float> qpos, pts, uv, pts2, uv2;
+    std::vector<float> qpos, pts, uv, pts2, uv2, lpos, lpts;
+    std::vector<int32_t> loct, lhide, lres;
+    std::vector<uint8_t> ldesc;
     std::vector<mage_dmatch> m;
     for (uint32_t f = 1; f < frames; f++) {
         const mage_keypoint* fk = frame_kp(f);
@@ -149,6 +221,7 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
         float R32[9], t32[3];
         for (int i = 0; i < 9; i++) R32[i] = (float)pred.R[i];
         for (int i = 0; i < 3; i++) t32[i] = (float)pred.t[i];
+        const Keyframe& kf = *kfp;
         const uint32_t nk = (uint32_t)kf.kp.size();
         sel.clear();
         qkp.clear();
@@ -162,8 +235,8 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
             sel.push_back(i);
             qkp.push_back(kf.kp[i]);
             qdesc.insert(qdesc.end(), kf.desc.begin() + 32ull * i, kf.desc.begin() + 32ull * (i + 1));
-            qpos.push_back(fx * xc[0] / xc[2] + cx);
-            qpos.push_back(fy * xc[1] / xc[2] + cy);
+            qpos.push_back((xc[0] / xc[2]) * fx + cx);
+            qpos.push_back((xc[1] / xc[2]) * fy + cy);
         }
         const uint32_t ns = (uint32_t)sel.size();
         auto radius = [&](float r, bool positions) -> mage_status {
@@ -185,9 +258,12 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
         if (st == MAGE_OK && weak()) st = radius(s->extra_wider_search_radius, false);
         if (st != MAGE_OK) return st;
         matches[f] = (uint32_t)m.size();
-        if (m.size() < s->min_matches) {  // lost: keep the prediction
+        auto lost = [&]() {  // keep the prediction
             P[f] = pred;
             inliers[f] = 0;
+        };
+        if (m.size() < s->min_matches) {
+            lost();
             continue;
         }
         pts.resize(3 * m.size());
@@ -209,17 +285,90 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
                 pts2.insert(pts2.end(), &pts[3 * k], &pts[3 * k] + 3);
                 uv2.insert(uv2.end(), &uv[2 * k], &uv[2 * k] + 2);
             }
+        if (s->local_map_keyframes > 0) {
+            if (pts2.empty()) {  // mapPoints.empty() after the outliers are unassociated
+                lost();
+                continue;
+            }
+            // TrackLocalMap.cpp:114-265 (see tracking.py local_map_queries)
+            std::vector<uint8_t> mask(nf, 1), visited(nk, 0);
+            std::vector<int32_t> hide(nk, -1);
+            for (size_t k = 0; k < m.size(); k++) {
+                const uint32_t q = sel[m[k].query_idx], t = (uint32_t)m[k].train_idx;
+                if (!out1[k]) {
+                    mask[t] = 0;
+                    visited[q] = 1;
+                } else {
+                    hide[q] = (int32_t)t;
+                }
+            }
+            float R32[9], t32[3], C[3];
+            for (int i = 0; i < 9; i++) R32[i] = (float)p1.R[i];
+            for (int i = 0; i < 3; i++) t32[i] = (float)p1.t[i];
+            world_position(p1, C);
+            const float fw[3] = {R32[6], R32[7], R32[8]};
+            const float border = s->image_border, W = (float)s->width, H = (float)s->height;
+            lpos.clear();
+            loct.clear();
+            ldesc.clear();
+            lhide.clear();
+            lpts.clear();
+            for (const Keyframe& k : kfs) {  // ascending keyframe id
+                const bool is_ref = &k == kfp;
+                for (size_t i = 0; i < k.kp.size(); i++) {
+                    if (is_ref && visited[i]) continue;
+                    const float* Pp = &k.pts[3 * i];
+                    float cs[3];
+                    for (int r = 0; r < 3; r++)
+                        cs[r] = (((0.f + R32[3 * r] * Pp[0]) + R32[3 * r + 1] * Pp[1]) + R32[3 * r + 2] * Pp[2]) + t32[r] * 1.f;
+                    const float depth = cs[2], div = depth != 0 ? depth : 1.f;
+                    const float px = (cs[0] / div) * fx + cx, py = (cs[1] / div) * fy + cy;
+                    if (depth < 0 || !(border <= px && border <= py && px < W - border && py < H - border)) continue;
+                    if (dot3(&k.mvd[3 * i], fw) < s->min_view_cos) continue;
+                    const float dl[3] = {Pp[0] - C[0], Pp[1] - C[1], Pp[2] - C[2]};
+                    const float d2 = (dl[0] * dl[0] + dl[1] * dl[1]) + dl[2] * dl[2];
+                    if (d2 < k.dmin[i] * k.dmin[i] || k.dmax[i] * k.dmax[i] < d2) continue;
+                    const float r = sqrtf(d2) / k.dmin[i];
+                    const int o = (int)roundf((float)std::log2((double)r) / log2s - 0.5f);
+                    if (o < 0 || o > (int)s->num_levels) continue;
+                    lpos.push_back(px);
+                    lpos.push_back(py);
+                    loct.push_back(o);
+                    ldesc.insert(ldesc.end(), k.desc.begin() + 32 * i, k.desc.begin() + 32 * (i + 1));
+                    lhide.push_back(is_ref ? hide[i] : -1);
+                    lpts.insert(lpts.end(), Pp, Pp + 3);
+                }
+            }
+            const uint32_t nq = (uint32_t)loct.size();
+            if (nq > 0) {
+                lres.resize(nq);
+                st = mage_local_map_match(lpos.data(), loct.data(), ldesc.data(), lhide.data(), nq, fk, fd, nf,
+                                          mask.data(), s->match_search_radius, s->local_max_hamming,
+                                          s->local_min_hamming_difference, lres.data(), device);
+                if (st != MAGE_OK) return st;
+                for (uint32_t q = 0; q < nq; q++)
+                    if (lres[q] >= 0) {
+                        pts2.insert(pts2.end(), &lpts[3 * q], &lpts[3 * q] + 3);
+                        uv2.push_back(fk[lres[q]].x);
+                        uv2.push_back(fk[lres[q]].y);
+                    }
+            }
+        }
         st = optimize(p1, K, pts2, uv2, s->refinement_info, s->final_steps, s->final_huber,
                       (float)(s->final_max_error * s->final_max_error), device, p2, out2);
         if (st != MAGE_OK) return st;
         uint32_t n_in = 0;
         for (uint8_t o : out2) n_in += o ? 0u : 1u;
+        if (s->local_map_keyframes > 0 && n_in < s->min_tracked) {
+            lost();
+            continue;
+        }
         P[f] = p2;
         inliers[f] = n_in;
         if ((double)n_in < s->keyframe_ratio * (double)nk + (double)s->keyframe_min) {
-            kf.kp.assign(fk, fk + nf);
-            kf.desc.assign(fd, fd + 32ull * nf);
-            backproject(fk, nf, p2, K, plane_z, kf.pts);
+            kfs.push_back(make_kf(f, p2));
+            while (kfs.size() > NK) kfs.pop_front();
+            kfp = &kfs.back();
             keyframe[f] = 1;
         }
     }

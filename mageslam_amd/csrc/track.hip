@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include "common.hpp"
@@ -93,20 +94,40 @@ __device__ uint32_t block_prefix(bool pr, uint32_t* wsum, uint32_t* total)
     return woff + before;
 }
 
+constexpr int NKMAX = 8;  // keyframes of the local map
+
 struct Ctl {              // per-call control words (device)
     uint32_t exec[3];     // radius pass k ran
     uint32_t ns;          // queries (keyframe points in front of the predicted camera)
     uint32_t lost;
-    uint32_t kf_n;        // keyframe feature count
+    uint32_t kf_first;    // keyframe ring: oldest slot, slots in use (ascending keyframe id)
+    uint32_t kf_count;
+    uint32_t kf_n[NKMAX]; // keyframe feature counts per slot
+    uint32_t lm_nq;       // local-map queries of the frame
 };
 
 struct TrackBufs {
     Ctl* ctl;
     double* pred;          // 12
-    // keyframe
+    // keyframe ring (NKMAX slots of cap entries; the reference keyframe is the newest slot)
     mage_keypoint* kf_kp;
     uint8_t* kf_desc;
     float* kf_pts;
+    float* kf_mvd;   // mean viewing directions (3 per point)
+    float* kf_dmin;
+    float* kf_dmax;
+    // local-map search
+    uint32_t* lm_mask;    // unassociated keypoints (bit words)
+    uint8_t* lm_visited;  // reference-keyframe points associated as pass-1 inliers
+    int32_t* lm_hide;     // reference-keyframe points of pass-1 outliers: their keypoint
+    float* lm_qpos;
+    int32_t* lm_qoct;
+    int32_t* lm_qhide;
+    uint8_t* lm_qdesc;
+    float* lm_qpt;        // the queries' map point positions
+    int32_t* lm_res;
+    uint32_t* lm_status;
+    void* lm_scratch;
     // queries
     mage_keypoint* qkp;
     uint8_t* qdesc;
@@ -141,28 +162,73 @@ struct TrackConst {
     double plane_z;
     mage_track_settings s;
     uint32_t cap;          // keypoints per frame slot
+    uint32_t nk;           // keyframe ring slots (max(local_map_keyframes, 1))
+    uint32_t qcap;         // local-map queries per frame (nk x cap)
+    float fmax[8], fmin[8];  // ComputeDMax / ComputeDMin factors per octave (powf on the host)
+    float log2s;           // log2(scale factor)
 };
 
-// Keyframe <- frame features (kp, desc, n) with map points back-projected at pose P onto the plane.
-__device__ void make_keyframe(const TrackBufs& b, const TrackConst& c, const mage_keypoint* fk, const uint8_t* fd,
-                              uint32_t nf, const DPose& P)
+__device__ float dot3f(const float* a, const float* b) { return ((0.f + a[0] * b[0]) + a[1] * b[1]) + a[2] * b[2]; }
+
+// Pose::GetWorldSpacePosition of the float view matrix (see track.cpp world_position)
+__device__ void world_position(const double* R, const double* t, float C[3])
+{
+    for (int i = 0; i < 3; i++) {
+        float s = 0.f;
+        for (int k = 0; k < 3; k++) s = s + (float)R[3 * k + i] * -(float)t[k];
+        C[i] = s + 0.f;
+    }
+}
+
+// Keyframe slot <- frame features (kp, desc, n) with map points back-projected at pose P onto the
+// plane and their MapPoint::UpdateMeanViewDirectionAndDistances attributes (track.cpp
+// map_point_attributes).
+__device__ void make_keyframe(const TrackBufs& b, const TrackConst& c, uint32_t slot, const mage_keypoint* fk,
+                              const uint8_t* fd, uint32_t nf, const DPose& P)
 {
     const double fx = c.K[0], fy = c.K[1], cx = c.K[2], cy = c.K[3];
     const double* R = P.R;
     double C[3];
     for (int j = 0; j < 3; j++) C[j] = -((R[j] * P.t[0] + R[3 + j] * P.t[1]) + R[6 + j] * P.t[2]);
+    float Cf[3];
+    world_position(P.R, P.t, Cf);
+    const size_t o = (size_t)slot * c.cap;
     for (uint32_t i = threadIdx.x; i < nf; i += TT) {
-        b.kf_kp[i] = fk[i];
+        b.kf_kp[o + i] = fk[i];
         const uint4* s = reinterpret_cast<const uint4*>(fd + 32ull * i);
-        uint4* d = reinterpret_cast<uint4*>(b.kf_desc + 32ull * i);
+        uint4* d = reinterpret_cast<uint4*>(b.kf_desc + 32ull * (o + i));
         d[0] = s[0];
         d[1] = s[1];
         const double u = ((double)fk[i].x - cx) / fx, v = ((double)fk[i].y - cy) / fy;
         double dd[3];
         for (int j = 0; j < 3; j++) dd[j] = (u * R[j] + v * R[3 + j]) + R[6 + j];
         const double lam = (c.plane_z - C[2]) / dd[2];
-        for (int j = 0; j < 3; j++) b.kf_pts[3 * i + j] = (float)(C[j] + lam * dd[j]);
+        float Pp[3];
+        for (int j = 0; j < 3; j++) Pp[j] = (float)(C[j] + lam * dd[j]);
+        for (int j = 0; j < 3; j++) b.kf_pts[3 * (o + i) + j] = Pp[j];
+        float vv[3] = {Pp[0] - Cf[0], Pp[1] - Cf[1], Pp[2] - Cf[2]};
+        const float d1 = sqrtf(dot3f(vv, vv));
+        if (d1 != 0) {
+            const float inv = 1.f / d1;
+            for (int j = 0; j < 3; j++) vv[j] = vv[j] * inv;
+        }
+        const float d2 = sqrtf(dot3f(vv, vv));
+        if (d2 != 0) {
+            const float inv = 1.f / d2;
+            for (int j = 0; j < 3; j++) vv[j] = vv[j] * inv;
+        }
+        for (int j = 0; j < 3; j++) b.kf_mvd[3 * (o + i) + j] = vv[j];
+        const float dl[3] = {Cf[0] - Pp[0], Cf[1] - Pp[1], Cf[2] - Pp[2]};
+        const float dist = sqrtf((dl[0] * dl[0] + dl[1] * dl[1]) + dl[2] * dl[2]);
+        const int oc = min(max(fk[i].octave, 0), 7);
+        b.kf_dmin[o + i] = dist * c.fmin[oc];
+        b.kf_dmax[o + i] = dist * c.fmax[oc];
     }
+}
+
+__device__ __forceinline__ uint32_t ref_slot(const Ctl* ctl, const TrackConst& c)
+{
+    return (ctl->kf_first + ctl->kf_count - 1) % c.nk;
 }
 
 // Frame 0: its keyframe at the first pose (already in poses[0]).
@@ -184,9 +250,12 @@ __global__ __launch_bounds__(TT) void trk_init(TrackBufs b, TrackConst c, const 
                                                uint32_t* inliers, uint8_t* keyframe, uint32_t* status)
 {
     const uint32_t n = frame_count(c, nf, status);
-    make_keyframe(b, c, fk, fd, n, load_pose(poses));
+    make_keyframe(b, c, 0, fk, fd, n, load_pose(poses));
+    for (uint32_t k = threadIdx.x; k < c.cap + c.qcap; k += TT) b.info[k] = c.s.refinement_info;
     if (threadIdx.x == 0) {
-        b.ctl->kf_n = n;
+        b.ctl->kf_first = 0;
+        b.ctl->kf_count = 1;
+        b.ctl->kf_n[0] = n;
         matches[0] = inliers[0] = n;
         keyframe[0] = 1;
         b.intr4[0] = c.cx;  // BundlerLib's {cx, cy, fx, fy}
@@ -208,25 +277,26 @@ __global__ __launch_bounds__(TT) void trk_project(TrackBufs b, TrackConst c, int
         for (int i = 0; i < 3; i++) t32[i] = (float)pred.t[i];
     }
     __syncthreads();
-    const uint32_t nk = b.ctl->kf_n;
+    const uint32_t slot = ref_slot(b.ctl, c), nk = b.ctl->kf_n[slot];
+    const size_t o = (size_t)slot * c.cap;
     uint32_t base = 0;
     for (uint32_t c0 = 0; c0 < nk; c0 += TT) {
         const uint32_t i = c0 + threadIdx.x;
         bool front = false;
         float u = 0.f, v = 0.f;
         if (i < nk) {
-            const float X = b.kf_pts[3 * i], Y = b.kf_pts[3 * i + 1], Z = b.kf_pts[3 * i + 2];
+            const float X = b.kf_pts[3 * (o + i)], Y = b.kf_pts[3 * (o + i) + 1], Z = b.kf_pts[3 * (o + i) + 2];
             float xc[3];
             for (int r = 0; r < 3; r++) xc[r] = ((R32[3 * r] * X + R32[3 * r + 1] * Y) + R32[3 * r + 2] * Z) + t32[r];
             front = xc[2] > 0.f;
-            u = c.fx * xc[0] / xc[2] + c.cx;
-            v = c.fy * xc[1] / xc[2] + c.cy;
+            u = (xc[0] / xc[2]) * c.fx + c.cx;
+            v = (xc[1] / xc[2]) * c.fy + c.cy;
         }
         uint32_t tot;
         const uint32_t pos = base + block_prefix(front, wsum, &tot);
         if (front) {
-            b.qkp[pos] = b.kf_kp[i];
-            const uint4* s = reinterpret_cast<const uint4*>(b.kf_desc + 32ull * i);
+            b.qkp[pos] = b.kf_kp[o + i];
+            const uint4* s = reinterpret_cast<const uint4*>(b.kf_desc + 32ull * (o + i));
             uint4* d = reinterpret_cast<uint4*>(b.qdesc + 32ull * pos);
             d[0] = s[0];
             d[1] = s[1];
@@ -264,9 +334,10 @@ __global__ __launch_bounds__(TT) void trk_gather(TrackBufs b, TrackConst c, cons
     const bool lost = n < c.s.min_matches;
     const mage_dmatch* m = b.m + (size_t)fin * c.cap;
     if (!lost) {
+        const size_t o = (size_t)ref_slot(b.ctl, c) * c.cap;
         for (uint32_t k = threadIdx.x; k < n; k += TT) {
             const uint32_t q = b.sel[m[k].query_idx], t = (uint32_t)m[k].train_idx;
-            for (int j = 0; j < 3; j++) b.pts1[3 * k + j] = b.kf_pts[3 * q + j];
+            for (int j = 0; j < 3; j++) b.pts1[3 * k + j] = b.kf_pts[3 * (o + q) + j];
             b.uv1[2 * k] = fk[t].x;
             b.uv1[2 * k + 1] = fk[t].y;
             b.info[k] = c.s.refinement_info;
@@ -283,7 +354,11 @@ __global__ __launch_bounds__(TT) void trk_gather(TrackBufs b, TrackConst c, cons
     }
 }
 
-__global__ __launch_bounds__(TT) void trk_filter(TrackBufs b)
+// Pass-1 inliers -> the pose-BA 2 observations (ordered compaction); with the local map on, the
+// frame's associations after TrackLocalMap unassociates the outliers (:116-147): the unassociated
+// keypoint mask, the reference points associated as inliers (visited) and each outlier point's
+// keypoint (hidden from its own local-map search).
+__global__ __launch_bounds__(TT) void trk_filter(TrackBufs b, TrackConst c, const uint32_t* nf_ptr)
 {
     __shared__ uint32_t wsum[TT / 64];
     const uint32_t n = b.os1[1];
@@ -304,6 +379,126 @@ __global__ __launch_bounds__(TT) void trk_filter(TrackBufs b)
         b.os2[0] = 0;
         b.os2[1] = base;
     }
+    if (c.s.local_map_keyframes == 0 || b.ctl->lost) return;
+    const uint32_t nf = min(*nf_ptr, c.cap);
+    const uint32_t nk = b.ctl->kf_n[ref_slot(b.ctl, c)];
+    for (uint32_t w = threadIdx.x; w < (nf + 31) / 32; w += TT)
+        b.lm_mask[w] = (32 * w + 32 <= nf) ? 0xFFFFFFFFu : ((1u << (nf - 32 * w)) - 1u);
+    for (uint32_t i = threadIdx.x; i < nk; i += TT) {
+        b.lm_visited[i] = 0;
+        b.lm_hide[i] = -1;
+    }
+    __syncthreads();
+    const int fin = b.ctl->exec[2] ? 2 : (b.ctl->exec[1] ? 1 : 0);
+    const mage_dmatch* m = b.m + (size_t)fin * c.cap;
+    for (uint32_t k = threadIdx.x; k < n; k += TT) {
+        const uint32_t q = b.sel[m[k].query_idx], t = (uint32_t)m[k].train_idx;
+        if (!b.out1[k]) {
+            atomicAnd(&b.lm_mask[t >> 5], ~(1u << (t & 31)));
+            b.lm_visited[q] = 1;
+        } else {
+            b.lm_hide[q] = (int32_t)t;
+        }
+    }
+}
+
+// TrackLocalMap.cpp:149-223: the local map's unvisited points, keyframe by keyframe in ascending id,
+// through ProjectMapPointIntoCurrentFrame / IsGoodCandidate / ComputeOctave with the pass-1 pose
+// (tracking.py local_map_queries, track.cpp): ordered compaction of the candidates into queries.
+// No pass-1 inlier left (mapPoints.empty(), :149-150) is a lost frame.
+__global__ __launch_bounds__(TT) void trk_lm_project(TrackBufs b, TrackConst c)
+{
+    __shared__ uint32_t wsum[TT / 64];
+    const bool off = c.s.local_map_keyframes == 0 || b.ctl->lost;
+    if (off || b.os2[1] == 0) {
+        if (threadIdx.x == 0) {
+            if (!off) b.ctl->lost = 1;
+            b.ctl->lm_nq = 0;
+        }
+        return;
+    }
+    float R[9], t[3], C[3];
+    for (int r = 0; r < 3; r++)
+        for (int cc = 0; cc < 3; cc++) R[3 * r + cc] = b.r9_o1[3 * cc + r];
+    for (int i = 0; i < 3; i++) t[i] = b.pos3_o1[i];
+    for (int i = 0; i < 3; i++) {
+        float sum = 0.f;
+        for (int k = 0; k < 3; k++) sum = sum + R[3 * k + i] * -t[k];
+        C[i] = sum + 0.f;
+    }
+    const float fw[3] = {R[6], R[7], R[8]};
+    const float border = c.s.image_border, W = (float)c.s.width, H = (float)c.s.height;
+    const uint32_t first = b.ctl->kf_first, count = b.ctl->kf_count;
+    uint32_t base = 0;
+    for (uint32_t si = 0; si < count; si++) {
+        const uint32_t slot = (first + si) % c.nk, n = b.ctl->kf_n[slot];
+        const bool is_ref = si + 1 == count;
+        const size_t o = (size_t)slot * c.cap;
+        for (uint32_t c0 = 0; c0 < n; c0 += TT) {
+            const uint32_t i = c0 + threadIdx.x;
+            bool ok = i < n && !(is_ref && b.lm_visited[i]);
+            float px = 0.f, py = 0.f;
+            int oc = 0;
+            if (ok) {
+                const float* P = b.kf_pts + 3 * (o + i);
+                float cs[3];
+                for (int r = 0; r < 3; r++)
+                    cs[r] = (((0.f + R[3 * r] * P[0]) + R[3 * r + 1] * P[1]) + R[3 * r + 2] * P[2]) + t[r] * 1.f;
+                const float depth = cs[2], div = depth != 0 ? depth : 1.f;
+                px = (cs[0] / div) * c.fx + c.cx;
+                py = (cs[1] / div) * c.fy + c.cy;
+                ok = !(depth < 0) && border <= px && border <= py && px < W - border && py < H - border;
+                ok = ok && !(dot3f(b.kf_mvd + 3 * (o + i), fw) < c.s.min_view_cos);
+                const float dl[3] = {P[0] - C[0], P[1] - C[1], P[2] - C[2]};
+                const float d2 = (dl[0] * dl[0] + dl[1] * dl[1]) + dl[2] * dl[2];
+                const float dmin = b.kf_dmin[o + i], dmax = b.kf_dmax[o + i];
+                ok = ok && !(d2 < dmin * dmin || dmax * dmax < d2);
+                if (ok) {
+                    const float rr = sqrtf(d2) / dmin;
+                    oc = (int)roundf((float)log2((double)rr) / c.log2s - 0.5f);
+                    ok = oc >= 0 && oc <= (int)c.s.num_levels;
+                }
+            }
+            uint32_t tot;
+            const uint32_t pos = base + block_prefix(ok, wsum, &tot);
+            if (ok && pos < c.qcap) {
+                b.lm_qpos[2 * pos] = px;
+                b.lm_qpos[2 * pos + 1] = py;
+                b.lm_qoct[pos] = oc;
+                b.lm_qhide[pos] = is_ref ? b.lm_hide[i] : -1;
+                const uint4* sd = reinterpret_cast<const uint4*>(b.kf_desc + 32ull * (o + i));
+                uint4* dd = reinterpret_cast<uint4*>(b.lm_qdesc + 32ull * pos);
+                dd[0] = sd[0];
+                dd[1] = sd[1];
+                for (int j = 0; j < 3; j++) b.lm_qpt[3 * pos + j] = b.kf_pts[3 * (o + i) + j];
+            }
+            base += tot;
+        }
+    }
+    if (threadIdx.x == 0) b.ctl->lm_nq = min(base, c.qcap);
+}
+
+// The local map's new associations appended to the pass-2 observations in query order.
+__global__ __launch_bounds__(TT) void trk_lm_assemble(TrackBufs b, const mage_keypoint* fk)
+{
+    __shared__ uint32_t wsum[TT / 64];
+    const uint32_t nq = b.ctl->lm_nq;
+    if (b.ctl->lost || nq == 0) return;
+    const uint32_t base0 = b.os2[1];
+    uint32_t base = base0;
+    for (uint32_t c0 = 0; c0 < nq; c0 += TT) {
+        const uint32_t q = c0 + threadIdx.x;
+        const int r = q < nq ? b.lm_res[q] : -1;
+        uint32_t tot;
+        const uint32_t pos = base + block_prefix(r >= 0, wsum, &tot);
+        if (r >= 0) {
+            for (int j = 0; j < 3; j++) b.pts2[3 * pos + j] = b.lm_qpt[3 * q + j];
+            b.uv2[2 * pos] = fk[r].x;
+            b.uv2[2 * pos + 1] = fk[r].y;
+        }
+        base += tot;
+    }
+    if (threadIdx.x == 0) b.os2[1] = base;
 }
 
 __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int f, const mage_keypoint* fk,
@@ -312,8 +507,9 @@ __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int 
 {
     __shared__ uint32_t wsum[TT / 64];
     __shared__ int s_kf;
+    __shared__ uint32_t s_slot;
     __shared__ double sP[12];
-    const bool lost = b.ctl->lost != 0;
+    bool lost = b.ctl->lost != 0;
     uint32_t n_in = 0;
     if (!lost) {
         const uint32_t n2 = b.os2[1];
@@ -323,6 +519,8 @@ __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int 
             (void)block_prefix(k < n2 && !b.out2[k], wsum, &tot);
             n_in += tot;
         }
+        // TrackLocalMap.cpp:309-314: too few associations after the second pass
+        if (c.s.local_map_keyframes > 0 && n_in < c.s.min_tracked) lost = true;
     }
     if (threadIdx.x == 0) {
         DPose P;
@@ -335,16 +533,25 @@ __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int 
         }
         store_pose(poses + 12ll * f, P);
         store_pose(sP, P);
-        inliers[f] = n_in;
-        const uint32_t nk = b.ctl->kf_n;
+        inliers[f] = lost ? 0u : n_in;
+        const uint32_t nk = b.ctl->kf_n[ref_slot(b.ctl, c)];
         s_kf = !lost && (double)n_in < c.s.keyframe_ratio * (double)nk + (double)c.s.keyframe_min;
         keyframe[f] = (uint8_t)s_kf;
+        if (s_kf) {  // the keyframe ring: a free slot, or the oldest keyframe's
+            if (b.ctl->kf_count < c.nk) {
+                s_slot = (b.ctl->kf_first + b.ctl->kf_count) % c.nk;
+                b.ctl->kf_count++;
+            } else {
+                s_slot = b.ctl->kf_first;
+                b.ctl->kf_first = (b.ctl->kf_first + 1) % c.nk;
+            }
+        }
     }
     __syncthreads();
     if (s_kf) {
         const uint32_t n = frame_count(c, nf, status);
-        make_keyframe(b, c, fk, fd, n, load_pose(sP));
-        if (threadIdx.x == 0) b.ctl->kf_n = n;
+        make_keyframe(b, c, s_slot, fk, fd, n, load_pose(sP));
+        if (threadIdx.x == 0) b.ctl->kf_n[s_slot] = n;
     }
 }
 
@@ -363,7 +570,11 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     MAGE_REQUIRE(d_kp && d_desc && d_n, MAGE_EINVAL, "null features");
     MAGE_REQUIRE(pitch > 0 && pitch <= 4096, MAGE_EINVAL, "frame pitch must be in [1, 4096] keypoints");
     hipStream_t st = (hipStream_t)stream;
+    MAGE_REQUIRE(s->local_map_keyframes <= (uint32_t)NKMAX, MAGE_EINVAL, "local_map_keyframes must be <= 8");
     const size_t cap = pitch;
+    const uint32_t NK = std::max(s->local_map_keyframes, 1u);
+    const size_t qcap = s->local_map_keyframes > 0 ? (size_t)NK * cap : 0;  // local-map queries
+    const size_t c2 = cap + qcap;                                           // pose-BA 2 observations
     // one device allocation for the per-call scratch and outputs
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     size_t off = 0;
@@ -372,13 +583,17 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         off = al(off + bytes);
         return o;
     };
-    const size_t o_ctl = take(sizeof(Ctl)), o_pred = take(12 * 8), o_kfkp = take(28 * cap), o_kfd = take(32 * cap),
-                 o_kfp = take(12 * cap), o_qkp = take(28 * cap), o_qd = take(32 * cap), o_qp = take(8 * cap),
-                 o_sel = take(4 * cap), o_nq = take(16), o_m = take(3 * 16 * cap), o_mn = take(16),
+    const size_t o_ctl = take(sizeof(Ctl)), o_pred = take(12 * 8), o_kfkp = take(28 * cap * NK),
+                 o_kfd = take(32 * cap * NK), o_kfp = take(12 * cap * NK), o_kfv = take(12 * cap * NK),
+                 o_kfdn = take(4 * cap * NK), o_kfdx = take(4 * cap * NK), o_qkp = take(28 * cap), o_qd = take(32 * cap),
+                 o_qp = take(8 * cap), o_sel = take(4 * cap), o_nq = take(16), o_m = take(3 * 16 * cap), o_mn = take(16),
                  o_rs = take(4 * cap), o_rst = take(4), o_pos = take(12), o_r9 = take(36), o_in = take(16),
-                 o_os1 = take(8), o_os2 = take(8), o_p1 = take(12 * cap), o_u1 = take(8 * cap), o_p2 = take(12 * cap),
-                 o_u2 = take(8 * cap), o_inf = take(4 * cap), o_po1 = take(12), o_ro1 = take(36), o_po2 = take(12),
-                 o_ro2 = take(36), o_out1 = take(cap), o_out2 = take(cap), o_msq = take(8),
+                 o_os1 = take(8), o_os2 = take(8), o_p1 = take(12 * cap), o_u1 = take(8 * cap), o_p2 = take(12 * c2),
+                 o_u2 = take(8 * c2), o_inf = take(4 * c2), o_po1 = take(12), o_ro1 = take(36), o_po2 = take(12),
+                 o_ro2 = take(36), o_out1 = take(cap), o_out2 = take(c2), o_msq = take(8),
+                 o_lmm = take(4 * 4096 / 32), o_lmv = take(cap), o_lmh = take(4 * cap), o_lqp = take(8 * qcap),
+                 o_lqo = take(4 * qcap), o_lqh = take(4 * qcap), o_lqd = take(32 * qcap), o_lqt = take(12 * qcap),
+                 o_lres = take(4 * qcap), o_lst = take(4), o_lscr = take(local_map_scratch_bytes((uint32_t)qcap)),
                  o_poses = take(96ull * frames), o_mt = take(4ull * frames), o_il = take(4ull * frames),
                  o_kf = take(frames);
     DeviceBuffer buf;
@@ -391,6 +606,20 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     b.kf_kp = reinterpret_cast<mage_keypoint*>(d + o_kfkp);
     b.kf_desc = reinterpret_cast<uint8_t*>(d + o_kfd);
     b.kf_pts = reinterpret_cast<float*>(d + o_kfp);
+    b.kf_mvd = reinterpret_cast<float*>(d + o_kfv);
+    b.kf_dmin = reinterpret_cast<float*>(d + o_kfdn);
+    b.kf_dmax = reinterpret_cast<float*>(d + o_kfdx);
+    b.lm_mask = reinterpret_cast<uint32_t*>(d + o_lmm);
+    b.lm_visited = reinterpret_cast<uint8_t*>(d + o_lmv);
+    b.lm_hide = reinterpret_cast<int32_t*>(d + o_lmh);
+    b.lm_qpos = reinterpret_cast<float*>(d + o_lqp);
+    b.lm_qoct = reinterpret_cast<int32_t*>(d + o_lqo);
+    b.lm_qhide = reinterpret_cast<int32_t*>(d + o_lqh);
+    b.lm_qdesc = reinterpret_cast<uint8_t*>(d + o_lqd);
+    b.lm_qpt = reinterpret_cast<float*>(d + o_lqt);
+    b.lm_res = reinterpret_cast<int32_t*>(d + o_lres);
+    b.lm_status = reinterpret_cast<uint32_t*>(d + o_lst);
+    b.lm_scratch = d + o_lscr;
     b.qkp = reinterpret_cast<mage_keypoint*>(d + o_qkp);
     b.qdesc = reinterpret_cast<uint8_t*>(d + o_qd);
     b.qpos = reinterpret_cast<float*>(d + o_qp);
@@ -431,6 +660,13 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     c.plane_z = plane_z;
     c.s = *s;
     c.cap = pitch;
+    c.nk = NK;
+    c.qcap = (uint32_t)qcap;
+    for (int o = 0; o < 8; o++) {
+        c.fmax[o] = powf(s->scale_factor, (float)s->num_levels - ((float)o + 0.5f));
+        c.fmin[o] = powf(s->scale_factor, 0.f - ((float)o + 0.5f));
+    }
+    c.log2s = (float)std::log2((double)s->scale_factor);
     const float e1 = (float)(s->initial_max_error * s->initial_max_error);
     const float e2 = (float)(s->final_max_error * s->final_max_error);
 
@@ -462,7 +698,28 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
                                       s->initial_huber, e1, b.pos3_o1, b.r9_o1, nullptr, b.out1, b.msq, nullptr,
                                       stream);
         if (r != MAGE_OK) return fail(r);
-        launch("track.filter", trk_filter, dim3(1), dim3(TT), 0, st, b);
+        launch("track.filter", trk_filter, dim3(1), dim3(TT), 0, st, b, c, nf);
+        if (s->local_map_keyframes > 0) {
+            launch("track.lm_project", trk_lm_project, dim3(1), dim3(TT), 0, st, b, c);
+            LocalMapArgs la{};
+            la.qpos = b.lm_qpos;
+            la.qoct = b.lm_qoct;
+            la.qhide = b.lm_qhide;
+            la.qdesc = b.lm_qdesc;
+            la.nq = &b.ctl->lm_nq;
+            la.q_cap = (uint32_t)qcap;
+            la.tkp = fk;
+            la.tdesc = fd;
+            la.nt = nf;
+            la.mask_words = b.lm_mask;
+            la.radius = s->match_search_radius;
+            la.max_dist = s->local_max_hamming;
+            la.min_diff = s->local_min_hamming_difference;
+            la.result = b.lm_res;
+            la.status = b.lm_status;
+            if ((r = local_map_match_launch(la, b.lm_scratch, st)) != MAGE_OK) return fail(r);
+            launch("track.lm_assemble", trk_lm_assemble, dim3(1), dim3(TT), 0, st, b, fk);
+        }
         r = mage_ba_pose_batch_device(1, b.pos3_o1, b.r9_o1, b.intr4, b.os2, b.pts2, b.uv2, b.info, s->final_steps,
                                       s->final_huber, e2, b.pos3_o2, b.r9_o2, nullptr, b.out2, b.msq + 1, nullptr,
                                       stream);
@@ -470,16 +727,18 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         launch("track.finish", trk_finish, dim3(1), dim3(TT), 0, st, b, c, (int)f, fk, fd, nf, dposes, dil, dkf, rstatus);
     }
     if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
-    uint32_t rst = 0;
+    uint32_t rst = 0, lst = 0;
     if (hipMemcpyAsync(poses, dposes, 96ull * frames, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(matches, dmt, 4ull * frames, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(inliers, dil, 4ull * frames, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(keyframe, dkf, frames, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(&rst, rstatus, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&lst, b.lm_status, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return fail(MAGE_EDEVICE);
     buf.release();
     MAGE_REQUIRE(!(rst & 1u), MAGE_ECAPACITY, "a frame has more than 4096 keypoints");
     MAGE_REQUIRE(!(rst & 2u), MAGE_ECAPACITY, "a frame's keypoint count exceeds the frame pitch");
+    MAGE_REQUIRE(lst == 0, MAGE_ECAPACITY, "local-map search: a frame has more than 4096 keypoints");
     return MAGE_OK;
 }

@@ -19,6 +19,7 @@ bench.py's cpu_baseline leg), which is how the pose parity of the whole loop is 
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -44,6 +45,50 @@ class TrackerSettings:
     # small_match_ratio, or the SearchRadius match falls back to the position-free wide search first.
     keyframe_ratio: float = 0.5
     keyframe_min: int = 25
+    # TrackLocalMap's local-map search between the two OptimizeCameraPose passes
+    # (TrackLocalMap.cpp:114-265; TrackLocalMapSettings, MageSettings.h:180-194); 0 keyframes = off.
+    # The local map is the last `local_map_keyframes` keyframes (the covisible set of this
+    # plane-backprojection map), visited in ascending keyframe id like GetConnectedMapPoints' sorted K1K2s.
+    local_map_keyframes: int = 4
+    match_search_radius: float = 8.0       # TrackLocalMapSettings::MatchSearchRadius
+    local_max_hamming: int = 30            # TrackLocalMapSettings::OrbMatcherSettings
+    local_min_hamming_difference: int = 1
+    min_view_degrees: float = 60.0         # MinDegreesBetweenCurrentViewAndMapPointView
+    image_border: float = 7.5              # FeatureExtractorSettings::GetImageBorder() = PatchSize / 2
+    min_tracked: int = 20                  # MinTrackedFeatureCount
+    scale_factor: float = 1.5              # the frames' pyramid (ComputeOctave / ComputeDMin / ComputeDMax)
+    num_levels: int = 1
+    width: int = 1280                      # AnalyzedImage size (PointWithinImageBorder)
+    height: int = 720
+
+    def min_view_cos(self) -> np.float32:
+        """std::cos(mira::deg2rad(degrees)) in float (arcana/math.h:86-90: degrees * (PI / 180))."""
+        return _libm_f("cosf", np.float32(self.min_view_degrees) * (np.float32(np.pi) / np.float32(180)))
+
+    def octave_factors(self):
+        """ComputeDMax / ComputeDMin factors per keypoint octave (MappingMath.h:32-40) with powf."""
+        L, s = self.num_levels, np.float32(self.scale_factor)
+        dmax = np.float32([_libm_f("powf", s, np.float32(L) - (np.float32(o) + np.float32(0.5))) for o in range(8)])
+        dmin = np.float32([_libm_f("powf", s, np.float32(0) - (np.float32(o) + np.float32(0.5))) for o in range(8)])
+        return dmax, dmin
+
+
+_LIBM = None
+
+
+def _libm_f(name: str, *args) -> np.float32:
+    """A float function of the C library (the host loops' cosf / powf), so every loop uses the
+    same rounding."""
+    import ctypes as C
+
+    global _LIBM
+    if _LIBM is None:
+        _LIBM = C.CDLL("libm.so.6")
+        for fn, n in (("cosf", 1), ("powf", 2)):
+            f = getattr(_LIBM, fn)
+            f.restype = C.c_float
+            f.argtypes = [C.c_float] * n
+    return np.float32(getattr(_LIBM, name)(*[float(np.float32(a)) for a in args]))
 
 
 @dataclass
@@ -76,6 +121,108 @@ class Keyframe:
     kp: np.ndarray       # its keypoints (KP_DTYPE)
     desc: np.ndarray     # (n, 32)
     points: np.ndarray   # (n, 3) float32 map point per keypoint
+    id: int = 0          # frame index
+    mvd: np.ndarray | None = None   # (n, 3) float32 mean viewing direction
+    dmin: np.ndarray | None = None  # (n,) float32 scale-invariance distances
+    dmax: np.ndarray | None = None
+
+
+def _dot3(a, b):
+    """cv::Matx / Vec dot in float32: s = 0, s += a_i b_i left to right."""
+    return ((np.float32(0) + a[..., 0] * b[..., 0]) + a[..., 1] * b[..., 1]) + a[..., 2] * b[..., 2]
+
+
+def world_position_f32(pose: Pose) -> np.ndarray:
+    """Pose::GetWorldSpacePosition (Data/Pose.cpp:110-113): column 3 of Invert(viewMatrix) (Utils/cv.h:
+    226-262: the transposed rotation times the negated translation, float 4x4 product)."""
+    R, t = pose.R.astype(np.float32), pose.t.astype(np.float32)
+    C = np.zeros(3, np.float32)
+    for i in range(3):
+        s = np.float32(0)
+        for k in range(3):
+            s = np.float32(s + np.float32(R[k, i] * np.float32(-t[k])))
+        C[i] = np.float32(s + np.float32(0))
+    return C
+
+
+def make_keyframe(fid: int, pose: Pose, kp, desc, K, plane_z: float, s: "TrackerSettings") -> Keyframe:
+    """A keyframe and its map points: plane back-projection plus MapPoint::
+    UpdateMeanViewDirectionAndDistances (Map/MapPoint.cpp:131-154) for a point seen by this keyframe
+    alone: mean viewing direction = Normalize(Normalize(point - centre)) (cv::Vec / float scales by
+    1.f / length), d = |centre - point|, dmax / dmin = d x the octave's ComputeDMax / DMin factor."""
+    pts = backproject_to_plane(kp, pose, K, plane_z)
+    C = world_position_f32(pose)
+    v = (pts - C).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        d = np.sqrt(_dot3(v, v)).astype(np.float32)
+        n1 = np.where(d[:, None] == 0, v, v * (np.float32(1) / d)[:, None]).astype(np.float32)
+        d2 = np.sqrt(_dot3(n1, n1)).astype(np.float32)
+        mvd = np.where(d2[:, None] == 0, n1, n1 * (np.float32(1) / d2)[:, None]).astype(np.float32)
+    delta = (C - pts).astype(np.float32)
+    dist = np.sqrt((delta[:, 0] * delta[:, 0] + delta[:, 1] * delta[:, 1]) + delta[:, 2] * delta[:, 2]).astype(np.float32)
+    fmax, fmin = s.octave_factors()
+    octv = np.asarray(kp["octave"], np.int64)
+    return Keyframe(pose, kp, desc, pts, fid, mvd, (dist * fmin[octv]).astype(np.float32),
+                    (dist * fmax[octv]).astype(np.float32))
+
+
+def local_map_queries(kfs, ref: Keyframe, visited_ref: np.ndarray, hide_ref: np.ndarray, pose: Pose, K,
+                      s: "TrackerSettings"):
+    """TrackLocalMap.cpp:175-223: the connected keyframes' map points in order (keyframe id, then
+    point index), skipping the visited ones (the frame's inlier associations), through
+    ProjectMapPointIntoCurrentFrame (:325-370): ProjectUndistorted with the updated pose, IsGoodCandidate
+    (:519-554: in front, inside the image border, viewing angle, scale-invariance distance) and
+    ComputeOctave (MappingMath.h:13-16).  Returns (positions (n, 2), octaves, descriptors, hidden
+    keypoint or -1, (keyframe, point) of each query)."""
+    fx, fy, cx, cy = (np.float32(v) for v in K)
+    R, t = pose.R.astype(np.float32), pose.t.astype(np.float32)
+    C = world_position_f32(pose)
+    fwd = R[2].astype(np.float32)  # GetWorldSpaceForward: column 2 of the inverse view matrix
+    cmin = s.min_view_cos()
+    border, W, H = np.float32(s.image_border), np.float32(s.width), np.float32(s.height)
+    log2s = np.float32(math.log2(float(np.float32(s.scale_factor))))
+    out_pos, out_oct, out_desc, out_hide, out_src = [], [], [], [], []
+    for kf in sorted(kfs, key=lambda k: k.id):
+        P = kf.points
+        n = len(P)
+        if n == 0:
+            continue
+        cs = [(((np.float32(0) + R[r, 0] * P[:, 0]) + R[r, 1] * P[:, 1]) + R[r, 2] * P[:, 2]) + t[r] * np.float32(1)
+              for r in range(3)]
+        depth = cs[2].astype(np.float32)
+        div = np.where(depth != 0, depth, np.float32(1)).astype(np.float32)
+        px = ((cs[0] / div) * fx + cx).astype(np.float32)
+        py = ((cs[1] / div) * fy + cy).astype(np.float32)
+        ok = ~(depth < 0)
+        ok &= (border <= px) & (border <= py) & (px < W - border) & (py < H - border)
+        ok &= ~(_dot3(kf.mvd, np.broadcast_to(fwd, kf.mvd.shape)) < cmin)
+        dl = (P - C).astype(np.float32)
+        d2 = ((dl[:, 0] * dl[:, 0] + dl[:, 1] * dl[:, 1]) + dl[:, 2] * dl[:, 2]).astype(np.float32)
+        ok &= ~((d2 < kf.dmin * kf.dmin) | (kf.dmax * kf.dmax < d2))
+        is_ref = kf is ref
+        if is_ref:
+            ok &= ~visited_ref
+        idx = np.nonzero(ok)[0]
+        octv = []
+        keep = []
+        for i in idx:
+            # (int)roundf(log2f(d / dmin) / log2f(scale) - 0.5f); log2 taken in double and rounded
+            r = np.float32(np.sqrt(d2[i]) / kf.dmin[i])
+            x = np.float32(np.float32(np.float32(math.log2(float(r))) / log2s) - np.float32(0.5))
+            o = int(np.copysign(np.floor(abs(float(x)) + 0.5), float(x)))
+            if 0 <= o <= s.num_levels:
+                keep.append(i)
+                octv.append(o)
+        keep = np.asarray(keep, np.int64)
+        out_pos.append(np.stack([px[keep], py[keep]], 1))
+        out_oct.append(np.asarray(octv, np.int32))
+        out_desc.append(kf.desc[keep])
+        out_hide.append(hide_ref[keep] if is_ref else np.full(len(keep), -1, np.int32))
+        out_src.append((kf, keep))
+    if not out_pos:
+        return np.zeros((0, 2), np.float32), np.zeros(0, np.int32), np.zeros((0, 32), np.uint8), np.zeros(0, np.int32), []
+    return (np.concatenate(out_pos).astype(np.float32), np.concatenate(out_oct), np.concatenate(out_desc),
+            np.concatenate(out_hide).astype(np.int32), out_src)
 
 
 @dataclass
@@ -84,6 +231,7 @@ class TrackResult:
     matches: list = field(default_factory=list)    # RadiusMatch count per frame
     inliers: list = field(default_factory=list)    # associations after the outlier removal
     keyframes: list = field(default_factory=list)  # frame indices that became keyframes
+    local_matches: list = field(default_factory=list)  # new associations of the local-map search
 
     def translations(self) -> np.ndarray:
         return np.stack([p.t for p in self.poses])
@@ -115,7 +263,7 @@ def project(points: np.ndarray, pose: Pose, K):
     z = Xc[2]
     ok = z > 0
     zs = np.where(ok, z, np.float32(1))
-    pos = np.stack([fx * Xc[0] / zs + cx, fy * Xc[1] / zs + cy], 1).astype(np.float32)
+    pos = np.stack([(Xc[0] / zs) * fx + cx, (Xc[1] / zs) * fy + cy], 1).astype(np.float32)
     return pos, ok
 
 
@@ -130,6 +278,10 @@ class Backend:
 
     def optimize_pose(self, pose: Pose, K, points, uv, info, steps, huber, max_err_sq):
         """-> (Pose, outlier flags (n,) bool)"""
+        raise NotImplementedError
+
+    def local_map_match(self, qpos, qoct, qdesc, qhide, tkp, tdesc, mask, radius, max_hamming, min_diff):
+        """TrackLocalMap's sequential per-point matching -> (keypoint per query or -1, updated mask)"""
         raise NotImplementedError
 
 
@@ -176,6 +328,12 @@ class GpuBackend(Backend):
                                         device=self.device)
         return pose_from_result(r), r["outlier"].astype(bool)
 
+    def local_map_match(self, qpos, qoct, qdesc, qhide, tkp, tdesc, mask, radius, max_hamming, min_diff):
+        from . import matcher
+
+        return matcher.LocalMapMatch(qpos, qoct, qdesc, tkp, tdesc, mask, radius, max_hamming, min_diff,
+                                     queryHidden=qhide, device=self.device)
+
 
 @dataclass
 class _Problem:
@@ -208,16 +366,24 @@ def pose_from_result(r) -> Pose:
 def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
           settings: TrackerSettings | None = None, frames: int | None = None) -> TrackResult:
     """Run the loop over precomputed per-frame (keypoints, descriptors); frame 0 is the first
-    keyframe at `first_pose` (its map from the scene plane)."""
+    keyframe at `first_pose` (its map from the scene plane).  Per frame: prediction, RadiusMatch of
+    the reference keyframe's points (three radii), OptimizeCameraPose 1, and — with
+    local_map_keyframes > 0 — TrackLocalMap's local-map search (TrackLocalMap.cpp:114-265): the
+    pass-1 outliers are unassociated (their keypoints hidden from their own points), the local map's
+    unvisited points are projected with the updated pose and matched one by one against the
+    still-unassociated keypoints, and OptimizeCameraPose 2 runs over the pass-1 inliers followed by
+    the new associations; fewer than MinTrackedFeatureCount associations after it is a lost frame."""
     s = settings or TrackerSettings()
     T = len(features) if frames is None else frames
     res = TrackResult()
     kp0, d0 = features[0]
-    kf = Keyframe(first_pose, kp0, d0, backproject_to_plane(kp0, first_pose, K, plane_z))
+    kf = make_keyframe(0, first_pose, kp0, d0, K, plane_z, s)
+    kfs = [kf]
     res.poses.append(first_pose)
     res.matches.append(len(kp0))
     res.inliers.append(len(kp0))
     res.keyframes.append(0)
+    res.local_matches.append(0)
     for t in range(1, T):
         kp, desc = features[t]
         # motion model: constant velocity on SE3 (the tracker's predicted pose)
@@ -234,22 +400,55 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
             m = backend.radius_match(qkp, qdesc, kp, desc, s.extra_wider_search_radius, None, s.max_hamming,
                                      s.min_hamming_difference)
         res.matches.append(len(m))
-        if len(m) < s.min_matches:  # lost: keep the prediction (relocalisation is outside the hot path)
+
+        def lost():  # keep the prediction (relocalisation is outside the hot path)
             res.poses.append(pred)
             res.inliers.append(0)
+            res.local_matches.append(0)
+
+        if len(m) < s.min_matches:
+            lost()
             continue
-        pts = kf.points[sel[m["query_idx"]]]
-        uv = np.stack([kp["x"][m["train_idx"]], kp["y"][m["train_idx"]]], 1)
+        qidx = sel[m["query_idx"]]              # the reference keyframe's matched points
+        tidx = m["train_idx"].astype(np.int64)  # their keypoints
+        pts = kf.points[qidx]
+        uv = np.stack([kp["x"][tidx], kp["y"][tidx]], 1)
         steps, huber, err = s.initial_ba
         pose, out = backend.optimize_pose(pred, K, pts, uv, s.refinement_info, steps, huber, err * err)
         keep = ~out
+        pts2, uv2 = pts[keep], uv[keep]
+        n_new = 0
+        if s.local_map_keyframes > 0:
+            if not keep.any():  # mapPoints.empty() after the outliers are unassociated (:149-150)
+                lost()
+                continue
+            mask = np.ones(len(kp), bool)
+            mask[tidx[keep]] = False
+            visited = np.zeros(len(kf.points), bool)
+            visited[qidx[keep]] = True
+            hide = np.full(len(kf.points), -1, np.int32)
+            hide[qidx[out]] = tidx[out]
+            lp, lo, ld, lh, src = local_map_queries(kfs, kf, visited, hide, pose, K, s)
+            if len(lp):
+                r, _ = backend.local_map_match(lp, lo, ld, lh, kp, desc, mask, s.match_search_radius,
+                                               s.local_max_hamming, s.local_min_hamming_difference)
+                qpts = np.concatenate([k.points[i] for k, i in src]).reshape(-1, 3)
+                hit = r >= 0
+                n_new = int(hit.sum())
+                pts2 = np.concatenate([pts2, qpts[hit]]).astype(np.float32)
+                uv2 = np.concatenate([uv2, np.stack([kp["x"][r[hit]], kp["y"][r[hit]]], 1)]).astype(np.float32)
         steps, huber, err = s.final_ba
-        pose, out2 = backend.optimize_pose(pose, K, pts[keep], uv[keep], s.refinement_info, steps, huber, err * err)
+        pose, out2 = backend.optimize_pose(pose, K, pts2, uv2, s.refinement_info, steps, huber, err * err)
         n_in = int((~out2).sum())
+        if s.local_map_keyframes > 0 and n_in < s.min_tracked:  # TrackLocalMap.cpp:309-314
+            lost()
+            continue
         res.poses.append(pose)
         res.inliers.append(n_in)
+        res.local_matches.append(n_new)
         if n_in < s.keyframe_ratio * len(kf.points) + s.keyframe_min:
-            kf = Keyframe(pose, kp, desc, backproject_to_plane(kp, pose, K, plane_z))
+            kf = make_keyframe(t, pose, kp, desc, K, plane_z, s)
+            kfs = (kfs + [kf])[-max(s.local_map_keyframes, 1):]
             res.keyframes.append(t)
     return res
 
@@ -295,7 +494,10 @@ def _settings_c(s: TrackerSettings):
     return _lib.TrackSettingsC(s.search_radius, s.wider_search_radius, s.extra_wider_search_radius,
                                s.small_match_ratio, s.min_matches, s.max_hamming, s.min_hamming_difference,
                                s.initial_ba[0], s.initial_ba[1], s.initial_ba[2], s.final_ba[0], s.final_ba[1],
-                               s.final_ba[2], s.refinement_info, s.keyframe_ratio, s.keyframe_min)
+                               s.final_ba[2], s.refinement_info, s.keyframe_ratio, s.keyframe_min,
+                               s.local_map_keyframes, s.match_search_radius, s.local_max_hamming,
+                               s.local_min_hamming_difference, float(s.min_view_cos()), s.image_border, s.min_tracked,
+                               s.scale_factor, s.num_levels, s.width, s.height)
 
 
 def track_native_device(d_kp, d_desc, pitch: int, d_counts, frames: int, K, first_pose: Pose, plane_z: float,

@@ -28,3 +28,8 @@ class OracleBackend(tracking.Backend):
     def optimize_pose(self, pose, K, points, uv, info, steps, huber, max_err_sq):
         r = O.pose_batch(tracking.pose_problem(pose, K, points, uv, info), steps, huber, max_err_sq)
         return tracking.pose_from_result(r), r["outlier"].astype(bool)
+
+    def local_map_match(self, qpos, qoct, qdesc, qhide, tkp, tdesc, mask, radius, max_hamming, min_diff):
+        r, m = O.local_map_match(qpos, qoct, qdesc, qhide, tkp, tdesc, mask.astype(np.uint8), radius, max_hamming,
+                                 min_diff)
+        return r, m.astype(bool)

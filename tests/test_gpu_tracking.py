@@ -1,7 +1,8 @@
-"""GPU parity of the whole tracking loop (BASELINE.json C4): ORB extraction, RadiusMatch and the
-pose-only BundlerLib on the GPU vs the same loop on the CPU oracle, over a synthetic hand-held
-sequence of a textured plane.  Bar (north star): pose RMSE <= 1e-4 (translation, rotation in rad);
-the per-frame match / inlier counts and keyframe decisions must be identical."""
+"""GPU parity of the whole tracking loop (BASELINE.json C4): ORB extraction, RadiusMatch, the
+pose-only BundlerLib and TrackLocalMap's local-map search on the GPU vs the same loop on the CPU
+oracle, over a synthetic hand-held sequence of a textured plane.  Bar (north star): pose RMSE <=
+1e-4 (translation, rotation in rad); the per-frame match / inlier / local-map association counts
+and keyframe decisions must be identical."""
 import numpy as np
 import pytest
 
@@ -26,6 +27,11 @@ def test_scene_renderer_matches_numpy(gpu):
     assert np.array_equal(out.cpu().numpy(), synth.scene_frames(seq))
 
 
+def _same(a, b):
+    assert a.matches == b.matches and a.inliers == b.inliers and a.keyframes == b.keyframes
+    assert all(np.array_equal(x.R, y.R) and np.array_equal(x.t, y.t) for x, y in zip(a.poses, b.poses))
+
+
 def test_tracking_loop_gpu_vs_oracle(gpu, oracle):
     from oracle.tracking_backend import OracleBackend
 
@@ -37,19 +43,50 @@ def test_tracking_loop_gpu_vs_oracle(gpu, oracle):
     gf, of = gb.extract(frames), ob.extract(frames)
     for (k1, d1), (k2, d2) in zip(gf, of):
         assert np.array_equal(k1.view(np.uint8), k2.view(np.uint8)) and np.array_equal(d1, d2)
-    g = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb)
-    o = tracking.track(of, K, p0, synth.SCENE_PLANE_Z, ob)
-    assert g.matches == o.matches and g.inliers == o.inliers and g.keyframes == o.keyframes
-    rt, rr = tracking.pose_rmse(g, o)
-    assert rt <= 1e-4 and rr <= 1e-4, (rt, rr)
-    # and the loop actually tracks: within a couple of centimetres of the ground truth at 5 m
     gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(len(seq.R))])
-    assert tracking.pose_rmse(g, gt)[0] < 0.03
-    assert min(g.inliers[1:]) >= 100
-    # the native loop (mage_track_sequence) is the same specification: identical to the Python loop
-    n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z)
-    assert n.matches == g.matches and n.inliers == g.inliers and n.keyframes == g.keyframes
-    assert all(np.array_equal(a.R, b.R) and np.array_equal(a.t, b.t) for a, b in zip(n.poses, g.poses))
+    for nk in (4, 0):  # with and without TrackLocalMap's local-map search
+        s = tracking.TrackerSettings(local_map_keyframes=nk, width=640, height=480)
+        g = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb, s)
+        o = tracking.track(of, K, p0, synth.SCENE_PLANE_Z, ob, s)
+        assert g.matches == o.matches and g.inliers == o.inliers and g.keyframes == o.keyframes
+        assert g.local_matches == o.local_matches
+        rt, rr = tracking.pose_rmse(g, o)
+        assert rt <= 1e-4 and rr <= 1e-4, (rt, rr)
+        # and the loop actually tracks: within a couple of centimetres of the ground truth at 5 m
+        assert tracking.pose_rmse(g, gt)[0] < 0.03
+        assert min(g.inliers[1:]) >= 100
+        if nk:
+            assert sum(g.local_matches) > 0
+        # the native loops (mage_track_sequence, mage_track_sequence_device) are the same specification
+        n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z, settings=s)
+        _same(n, g)
+        d = tracking.track_native_device(*tracking.features_to_device(gf), len(gf), K, p0, synth.SCENE_PLANE_Z,
+                                         settings=s)
+        _same(d, g)
+
+
+def test_tracking_loop_720p_gpu_vs_oracle(gpu, oracle):
+    """C4 at 1280 x 720 over 64 frames with keyframe switches: the device-resident loop
+    (mage_track_sequence_device, local map on) against the oracle loop, frame by frame."""
+    from oracle.tracking_backend import OracleBackend
+
+    seq = synth.scene_sequence(64, 1280, 720, step=0.06)
+    frames = synth.scene_frames(seq)
+    K = (seq.fx, seq.fy, seq.cx, seq.cy)
+    p0 = tracking.Pose(seq.R[0], seq.t[0])
+    gf = tracking.GpuBackend(2000).extract(frames)
+    ob = OracleBackend(2000)
+    of = ob.extract(frames)
+    for (k1, d1), (k2, d2) in zip(gf, of):
+        assert np.array_equal(k1.view(np.uint8), k2.view(np.uint8)) and np.array_equal(d1, d2)
+    s = tracking.TrackerSettings()
+    d = tracking.track_native_device(*tracking.features_to_device(gf), len(gf), K, p0, synth.SCENE_PLANE_Z,
+                                     settings=s)
+    o = tracking.track(of, K, p0, synth.SCENE_PLANE_Z, ob, s)
+    assert len(o.keyframes) >= 3 and sum(o.local_matches) > 0
+    assert d.matches == o.matches and d.inliers == o.inliers and d.keyframes == o.keyframes
+    rt, rr = tracking.pose_rmse(d, o)
+    assert rt <= 1e-4 and rr <= 1e-4, (rt, rr)
 
 
 def test_native_tracking_loop_720p_keyframes(gpu):
@@ -63,7 +100,7 @@ def test_native_tracking_loop_720p_keyframes(gpu):
     gf = gb.extract(frames)
     g = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb)
     n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z)
-    assert len(g.keyframes) >= 2
+    assert len(g.keyframes) >= 2 and sum(g.local_matches) > 0
     assert n.matches == g.matches and n.inliers == g.inliers and n.keyframes == g.keyframes
     assert all(np.array_equal(a.R, b.R) and np.array_equal(a.t, b.t) for a, b in zip(n.poses, g.poses))
     gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(len(seq.R))])
@@ -81,11 +118,6 @@ def test_native_tracking_errors(gpu):
         _lib.check(_lib.load().mage_track_sequence(None, None, None, 3, None, None, 5.0, None, None, None, None, None, 0))
 
 
-def _same(a, b):
-    assert a.matches == b.matches and a.inliers == b.inliers and a.keyframes == b.keyframes
-    assert all(np.array_equal(x.R, y.R) and np.array_equal(x.t, y.t) for x, y in zip(a.poses, b.poses))
-
-
 def test_device_tracking_loop_equals_native(gpu):
     """mage_track_sequence_device (every per-frame decision on the device) == the host-driven
     native loop, frame by frame, over a 720p pan with keyframe switches."""
@@ -94,10 +126,13 @@ def test_device_tracking_loop_equals_native(gpu):
     K = (seq.fx, seq.fy, seq.cx, seq.cy)
     p0 = tracking.Pose(seq.R[0], seq.t[0])
     gf = tracking.GpuBackend(2000).extract(frames)
-    n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z)
-    d = tracking.track_native_device(*tracking.features_to_device(gf), len(gf), K, p0, synth.SCENE_PLANE_Z)
-    assert len(n.keyframes) >= 2
-    _same(d, n)
+    for nk in (4, 1, 0):
+        s = tracking.TrackerSettings(local_map_keyframes=nk)
+        n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z, settings=s)
+        d = tracking.track_native_device(*tracking.features_to_device(gf), len(gf), K, p0, synth.SCENE_PLANE_Z,
+                                         settings=s)
+        assert len(n.keyframes) >= 2
+        _same(d, n)
 
 
 def test_device_tracking_loop_fallbacks_and_lost(gpu):
@@ -111,7 +146,10 @@ def test_device_tracking_loop_fallbacks_and_lost(gpu):
     K = (seq.fx, seq.fy, seq.cx, seq.cy)
     p0 = tracking.Pose(seq.R[0], seq.t[0])
     gf = tracking.GpuBackend(1000).extract(frames)
-    for s in (tracking.TrackerSettings(), tracking.TrackerSettings(small_match_ratio=0.9, min_matches=200)):
+    for s in (tracking.TrackerSettings(width=640, height=480),
+              tracking.TrackerSettings(small_match_ratio=0.9, min_matches=200, width=640, height=480),
+              tracking.TrackerSettings(min_tracked=900, width=640, height=480),  # lost after the local map
+              tracking.TrackerSettings(local_map_keyframes=0, width=640, height=480)):
         n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z, settings=s)
         d = tracking.track_native_device(*tracking.features_to_device(gf, pitch=1000), len(gf), K, p0,
                                          synth.SCENE_PLANE_Z, settings=s)
