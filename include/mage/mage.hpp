@@ -123,6 +123,30 @@ inline unsigned RadiusMatch(const std::vector<KeyPoint>& queryKeypoints, const s
 }
 
 // OnlineBow vocabulary tree on the device (OnlineBow.cpp:289-311 FindLeafNode; nodes as CreateTree
+// TrackLocalMap's per-map-point matching loop (TrackLocalMap.cpp:175-256): projected map points in
+// order (positions x, y interleaved; octaves; descriptors; the keypoint to hide for a
+// pose-estimation outlier point, -1 otherwise) against a frame's keypoints; unassociatedMask is
+// updated like the reference's (a match takes its keypoint).  Returns the keypoint per point or -1.
+inline std::vector<int32_t> LocalMapMatch(const std::vector<float>& positions, const std::vector<int32_t>& octaves,
+                                          const std::vector<Descriptor>& descriptors, const std::vector<int32_t>& hidden,
+                                          const std::vector<KeyPoint>& targetKeypoints,
+                                          const std::vector<Descriptor>& targetDescriptors,
+                                          std::vector<bool>& unassociatedMask, float radius, int maxHammingDist,
+                                          int minHammingDifference, int device = 0)
+{
+    const uint32_t n = (uint32_t)octaves.size();
+    std::vector<uint8_t> mask(unassociatedMask.begin(), unassociatedMask.end());
+    std::vector<int32_t> result(n, -1);
+    check(mage_local_map_match(positions.data(), octaves.data(), descriptors.empty() ? nullptr : descriptors.front().data(),
+                               hidden.empty() ? nullptr : hidden.data(), n, targetKeypoints.data(),
+                               targetDescriptors.empty() ? nullptr : targetDescriptors.front().data(),
+                               (uint32_t)targetKeypoints.size(), mask.data(), radius, maxHammingDist,
+                               minHammingDifference, result.data(), device));
+    for (size_t t = 0; t < mask.size(); t++) unassociatedMask[t] = mask[t] != 0;
+    return result;
+}
+
+
 // builds them: node i's descriptor, children in childrenIDs order, root 0).
 class OnlineBowTree {
 public:

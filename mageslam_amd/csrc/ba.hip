@@ -1748,6 +1748,109 @@ __global__ __launch_bounds__(256) void schur_rhs(const int* __restrict__ camblk,
     }
 }
 
+// ---- the common case: every camera observes a point at most once ---------------------------
+// Then a pair's products are its cameras' shared free points, one each: with A_h the bit set of the
+// points camera block h observes (its camera-CSR run is sorted by point) and F the points in the
+// system, pair (a, b)'s list in point order is the set bits of A_a & A_b & F, and the edge of point
+// p in camera block h sits at camera-CSR position cstart[c_h] + (rank of p in A_h).
+constexpr int SC_LDS_WORDS = 16384;  // point bit words staged in LDS (P <= 524288)
+
+__global__ __launch_bounds__(1024) void sc_bitmaps(int P, int nb, const int* __restrict__ camblk,
+                                                   const int* __restrict__ cstart, const int* __restrict__ cpt,
+                                                   const int* __restrict__ ptfree, uint32_t* __restrict__ A,
+                                                   int* __restrict__ R, uint32_t* __restrict__ F)
+{
+    __shared__ uint32_t bm[SC_LDS_WORDS];
+    __shared__ int part[1024];
+    const int PW = (P + 31) / 32, tid = threadIdx.x, h = blockIdx.x;
+    if (h == nb) {
+        for (int w = tid; w < PW; w += 1024) {
+            uint32_t v = 0;
+            for (int j = 0; j < 32 && 32 * w + j < P; j++) v |= (ptfree[32 * w + j] ? 1u : 0u) << j;
+            F[w] = v;
+        }
+        return;
+    }
+    for (int w = tid; w < PW; w += 1024) bm[w] = 0;
+    __syncthreads();
+    const int c = camblk[h];
+    for (int a = cstart[c] + tid; a < cstart[c + 1]; a += 1024) {
+        const int p = cpt[a];
+        atomicOr(&bm[p >> 5], 1u << (p & 31));
+    }
+    __syncthreads();
+    // exclusive prefix popcount per word: each thread a contiguous segment of words
+    const int seg = (PW + 1023) / 1024, w0 = tid * seg, w1 = min(PW, w0 + seg);
+    int sum = 0;
+    for (int w = w0; w < w1; w++) sum += __popc(bm[w]);
+    part[tid] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan of the thread sums
+        const int v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int run = part[tid] - sum;
+    uint32_t* Ah = A + (size_t)h * PW;
+    int* Rh = R + (size_t)h * PW;
+    for (int w = w0; w < w1; w++) {
+        Ah[w] = bm[w];
+        Rh[w] = run;
+        run += __popc(bm[w]);
+    }
+}
+
+__global__ __launch_bounds__(64) void sc_pair_counts(int nb, int PW, const uint32_t* __restrict__ A,
+                                                     const uint32_t* __restrict__ F, int* __restrict__ cnt)
+{
+    const int a = blockIdx.x, b = blockIdx.y;
+    if (b < a) return;
+    const uint32_t* Aa = A + (size_t)a * PW;
+    const uint32_t* Ab = A + (size_t)b * PW;
+    int n = 0;
+    for (int w = threadIdx.x; w < PW; w += 64) n += __popc(Aa[w] & Ab[w] & F[w]);
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+    if (threadIdx.x == 0) cnt[a * nb + b] = n;
+}
+
+// Pair (a, b)'s products (camera-CSR positions of its two edges) in point order at kbase[a nb + b].
+__global__ __launch_bounds__(64) void sc_pair_fill(int nb, int PW, const uint32_t* __restrict__ A,
+                                                   const int* __restrict__ R, const uint32_t* __restrict__ F,
+                                                   const int* __restrict__ camblk, const int* __restrict__ cstart,
+                                                   const int* __restrict__ kbase, int2* __restrict__ sentries)
+{
+    const int a = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+    if (b < a) return;
+    int base = kbase[a * nb + b];
+    if (base < 0) return;
+    const uint32_t* Aa = A + (size_t)a * PW;
+    const uint32_t* Ab = A + (size_t)b * PW;
+    const int* Ra = R + (size_t)a * PW;
+    const int* Rb = R + (size_t)b * PW;
+    const int ea = cstart[camblk[a]], eb = cstart[camblk[b]];
+    for (int w0 = 0; w0 < PW; w0 += 64) {
+        const int w = w0 + lane;
+        const uint32_t wa = w < PW ? Aa[w] : 0u, wb = w < PW ? Ab[w] : 0u;
+        uint32_t m = w < PW ? wa & wb & F[w] : 0u;
+        const int c = __popc(m);
+        int inc = c;  // inclusive wave scan of the counts
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(inc, o);
+            if (lane >= o) inc += v;
+        }
+        int pos = base + inc - c;
+        const int ra = w < PW ? Ra[w] : 0, rb = w < PW ? Rb[w] : 0;
+        while (m) {
+            const int j = __builtin_ctz(m);
+            m &= m - 1u;
+            const uint32_t below = (1u << j) - 1u;
+            sentries[pos++] = make_int2(ea + ra + __popc(wa & below), eb + rb + __popc(wb & below));
+        }
+        base += __shfl(inc, 63);
+    }
+}
+
 // The current state (q C x 4, t C x 3, p P x 3 doubles) copied into mapped host memory after a
 // step, so GetPose / GetPoint (UpdateData after every StepBundleAdjustment, BundleAdjust.cpp:
 // 195-226) read it without a D2H copy + stream sync; the completion word is written last.
@@ -1755,8 +1858,16 @@ __global__ __launch_bounds__(1024) void export_state(State s, int C, int P, doub
                                                      unsigned* __restrict__ seq_out, unsigned seq)
 {
     const int nq = 4 * C, nt = 3 * C, np = 3 * P;
-    for (int i = threadIdx.x; i < nq + nt + np; i += 1024)
-        out[i] = i < nq ? s.q[i] : i < nq + nt ? s.t[i - nq] : s.p[i - nq - nt];
+    // 16-byte stores (the host mirror is written over the fabric)
+    for (int i = 2 * threadIdx.x; i < nq + nt + np; i += 2048) {
+        double v[2];
+        for (int k = 0; k < 2; k++) {
+            const int j = i + k;
+            v[k] = j < nq ? s.q[j] : j < nq + nt ? s.t[j - nq] : j < nq + nt + np ? s.p[j - nq - nt] : 0.0;
+        }
+        if (i + 1 < nq + nt + np) *reinterpret_cast<double2*>(out + i) = make_double2(v[0], v[1]);
+        else out[i] = v[0];
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence_system();
@@ -1835,7 +1946,7 @@ struct BundleAdjuster {
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
-        d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_cub, d_kdst, d_rblk, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
+        d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_cub, d_kdst, d_rblk, d_sbits, d_srank, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
         d_sfinish, d_epos, d_chi_lin, d_livebuf;
     // outlier lists of the speculative / final post-pass (2 x E entries), written by the kernels
     // straight into host memory: the host sorts and returns them after the completion wait
@@ -1880,7 +1991,7 @@ struct BundleAdjuster {
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
-                        &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_cub, &d_kdst, &d_rblk, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
+                        &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_cub, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf})
             b->release();
         h_olist.release();
@@ -1906,6 +2017,7 @@ struct BundleAdjuster {
     MappedBuffer h_state;
     unsigned export_seq = 0;
     int export_cur = -1;
+    bool export_wanted = false;  // the caller read the state since the last step
     void launch_export()
     {
         if (h_state.reserve((size_t)(7 * C + 3 * P + 1) * sizeof(double)) != MAGE_OK) {
@@ -2083,13 +2195,27 @@ struct BundleAdjuster {
         std::vector<int> epos(std::max(E, 1), -1);
         for (int a = 0; a < cstart[C]; a++) epos[cedges[a]] = a;
         // The structure the Schur products need goes to the device first; the per-pair product
-        // lists are built there (schur_point_lists / _products, a stable radix sort by pair,
-        // schur_list_bounds), the host only reads back the per-pair counts.
+        // lists are built there and the host only reads back the per-pair counts: from the cameras'
+        // point bit sets when no camera observes a point twice (sc_bitmaps / sc_pair_counts /
+        // sc_pair_fill), else per point (schur_point_lists / _products, a stable radix sort by
+        // pair, schur_list_bounds).
         if ((r = upload(d_epos, epos)) != MAGE_OK) return r;
         if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
         if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
         if ((r = upload(d_pstart, pstart)) != MAGE_OK) return r;
         if ((r = upload(d_pedges, pedges)) != MAGE_OK) return r;
+        if ((r = upload(d_cstart, cstart)) != MAGE_OK) return r;
+        if ((r = upload(d_cpt, cpt)) != MAGE_OK) return r;
+        if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
+        bool dup = false;  // a camera observing a point twice (its CSR run lists the point twice)
+        for (int c = 0; c < C && !dup; c++)
+            for (int a = cstart[c] + 1; a < cstart[c + 1]; a++)
+                if (cpt[a] == cpt[a - 1]) {
+                    dup = true;
+                    break;
+                }
+        const int PW = (P + 31) / 32;
+        const bool bitmaps = !dup && PW <= SC_LDS_WORDS && nb > 0 && nfp > 0;
         // covisible camera pairs (h1 <= h2) of the reduced system: every pair sharing a free point
         // (a product list), the diagonal, and the tethered pairs
         std::vector<int2> pairs;
@@ -2097,7 +2223,24 @@ struct BundleAdjuster {
         const int nk = std::max(nb, 1) * std::max(nb, 1);  // dense pair keys h1 * nb + h2
         std::vector<int> kcount(nk, 0), kstart(nk, 0);
         long long nprod_max = 0;  // sum over free points of k_p^2 bounds the products
-        if (nb > 0 && nfp > 0) {
+        if (bitmaps) {
+            if ((r = d_sbits.reserve(((size_t)nb + 1) * PW * 4)) != MAGE_OK) return r;
+            if ((r = d_srank.reserve((size_t)nb * PW * 4)) != MAGE_OK) return r;
+            if ((r = d_kb.reserve((size_t)nk * sizeof(int))) != MAGE_OK) return r;
+            uint32_t* A = d_sbits.as<uint32_t>();
+            uint32_t* F = A + (size_t)nb * PW;
+            launch("ba.schur_bitmaps", sc_bitmaps, dim3(nb + 1), dim3(1024), 0, st, P, nb, (const int*)d_camblk.as<int>(),
+                   (const int*)d_cstart.as<int>(), (const int*)d_cpt.as<int>(), (const int*)d_ptfree.as<int>(), A,
+                   d_srank.as<int>(), F);
+            launch("ba.schur_counts", sc_pair_counts, dim3(nb, nb), dim3(64), 0, st, nb, PW, (const uint32_t*)A,
+                   (const uint32_t*)F, d_kb.as<int>());
+            MAGE_HIP(hipGetLastError());
+            if ((r = h_kb.reserve((size_t)nk * sizeof(int))) != MAGE_OK) return r;
+            MAGE_HIP(hipMemcpyAsync(h_kb.ptr, d_kb.ptr, (size_t)nk * sizeof(int), hipMemcpyDeviceToHost, st));
+            MAGE_HIP(hipStreamSynchronize(st));
+            for (int x = 0; x < nb; x++)
+                for (int y = x; y < nb; y++) kcount[(size_t)x * nb + y] = h_kb.as<int>()[(size_t)x * nb + y];
+        } else if (nb > 0 && nfp > 0) {
             for (int i = 0; i < P; i++) {
                 if (!ptfree[i]) continue;
                 long long k = 0;
@@ -2169,11 +2312,16 @@ struct BundleAdjuster {
             if ((r = d_sentries.reserve(((size_t)pbeg[npairs] + 1) * sizeof(int2))) != MAGE_OK) return r;
             // the padding entry after the last list (schur_chunks reads one past a chunk's end)
             MAGE_HIP(hipMemsetAsync(d_sentries.as<int2>() + pbeg[npairs], 0, sizeof(int2), st));
+            if (bitmaps)  // sc_pair_fill: a pair's first product slot (-1: no products)
+                for (int k = 0; k < nk; k++) kdst[k] = kcount[k] > 0 ? kdst[k] + kstart[k] : -1;
             if ((r = upload(d_kdst, kdst)) != MAGE_OK) return r;
             if ((r = upload(d_rblk, rblk)) != MAGE_OK) return r;
-            if ((r = upload(d_cstart, cstart)) != MAGE_OK) return r;
-            if ((r = upload(d_cpt, cpt)) != MAGE_OK) return r;
-            if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
+            if (bitmaps) {
+                uint32_t* A = d_sbits.as<uint32_t>();
+                launch("ba.schur_fill", sc_pair_fill, dim3(nb, nb), dim3(64), 0, st, nb, PW, (const uint32_t*)A,
+                       (const int*)d_srank.as<int>(), (const uint32_t*)(A + (size_t)nb * PW), (const int*)d_camblk.as<int>(),
+                       (const int*)d_cstart.as<int>(), (const int*)d_kdst.as<int>(), d_sentries.as<int2>());
+            }
             if (nprod_max > 0)
                 launch("ba.schur_scatter", schur_scatter, dim3((unsigned)((nprod_max + 255) / 256)), dim3(256), 0, st,
                        (const uint16_t*)d_skeys.as<uint16_t>() + nprod_pad(nprod_max),
@@ -2575,7 +2723,10 @@ struct BundleAdjuster {
         // Eager linearisation for the caller's usual next call (BundleAdjust.cpp:311-318: the same
         // huber width, no setter in between): it runs while control is with the caller, and
         // lm_solve reuses it only when the huber width, lambda and state still match.
-        if (host_state_stale) launch_export();
+        // the mirror is written when the caller reads the state between steps (UpdateData after every
+        // StepBundleAdjustment, BundleAdjust.cpp:400-403); a caller that stops reading stops paying for it
+        if (host_state_stale && export_wanted) launch_export();
+        export_wanted = false;
         // After an outlier removal the next Step starts at iteration 0 (lambda re-initialised from
         // the user lambda or computeLambdaInit): the eager linearisation is that iteration's, with
         // the reduction computeLambdaInit reads when no user lambda is set.
@@ -2815,6 +2966,7 @@ mage_status mage_ba_get_poses(mage_ba* b, float* pos3, float* r9)
 {
     MAGE_REQUIRE(b && pos3 && r9, MAGE_EINVAL, "null argument");
     (void)hipSetDevice(b->device);
+    b->export_wanted = true;  // GetPose / GetPoint between steps: keep the mapped mirror current
     mage_status r = b->sync_host_state();
     if (r != MAGE_OK) return r;
     for (int c = 0; c < b->C; c++) {
@@ -2839,6 +2991,7 @@ mage_status mage_ba_get_points(mage_ba* b, float* xyz)
 {
     MAGE_REQUIRE(b && xyz, MAGE_EINVAL, "null argument");
     (void)hipSetDevice(b->device);
+    b->export_wanted = true;  // GetPose / GetPoint between steps: keep the mapped mirror current
     mage_status r = b->sync_host_state();
     if (r != MAGE_OK) return r;
     for (int i = 0; i < 3 * b->P; i++) xyz[i] = (float)b->p[i];
@@ -2849,6 +3002,7 @@ mage_status mage_ba_get_state_f64(mage_ba* b, double* qt7, double* xyz)
 {
     MAGE_REQUIRE(b, MAGE_EINVAL, "null handle");
     (void)hipSetDevice(b->device);
+    b->export_wanted = true;  // GetPose / GetPoint between steps: keep the mapped mirror current
     mage_status r = b->sync_host_state();
     if (r != MAGE_OK) return r;
     if (qt7)

@@ -292,3 +292,19 @@ def test_removals_drop_points_and_cameras(gpu):
     compare(gb, ob)
     sg, so = gb.stats(), ob.stats()
     assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
+
+
+def test_camera_observing_a_point_twice(gpu):
+    """A camera with two observations of the same point (the reference API allows it): the Schur
+    product lists take the general per-point path (both orders of the same-camera pair) instead of
+    the cameras' point bit sets; same outliers, counts and poses as the oracle."""
+    g = synth.ba_graph(cameras=12, points=400, obs_per_point=8, fixed_cameras=3, seed=21)
+    rng = np.random.default_rng(4)
+    dup = rng.choice(np.flatnonzero(g.fixed[g.cam] == 0), 60, replace=False)
+    for f in ("cam", "pt", "info"):
+        setattr(g, f, np.concatenate([getattr(g, f), getattr(g, f)[dup]]))
+    g.uv = np.concatenate([g.uv, g.uv[dup] + rng.normal(0, 0.3, (60, 2)).astype(np.float32)])
+    gb, ob = run_pair(g, 4)
+    compare(gb, ob)
+    sg, so = gb.stats(), ob.stats()
+    assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
