@@ -1082,6 +1082,9 @@ __global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict_
 #ifndef MAGE_CHOL_ABLATE  // timing experiments only (tools/ablate_ba.py); 0 in the product
 #define MAGE_CHOL_ABLATE 0
 #endif
+#ifndef MAGE_CHOL_SYRK2
+#define MAGE_CHOL_SYRK2 0  // 1: the SYRK phase over slot pairs (two MFMA chains per basic block)
+#endif
 #ifndef MAGE_CHOL_FW
 #define MAGE_CHOL_FW 1  // 1: a dedicated factor wave (no tiles); 0: the next diagonal tile's owner factors it
 #endif
@@ -1374,11 +1377,37 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             factor_diag(kn);
             __builtin_amdgcn_s_setprio(0);
         }
+#if MAGE_CHOL_SYRK2
+        // slot pairs in one basic block: two independent MFMA chains the scheduler can interleave
+        auto does = [&](int sl) {
+            const int i = tIJ[sl] & 0xFF, j = tIJ[sl] >> 8;
+            return i > k && i < mt && !(i == kn && j == kn);
+        };
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl += 2) {
+            const bool d0 = does(sl), d1 = sl + 1 < CT_TPW && does(sl + 1);
+            if (d0 && d1) {
+                const int i0 = tIJ[sl] & 0xFF, j0 = tIJ[sl] >> 8;
+                const int i1 = tIJ[sl + 1] & 0xFF, j1 = tIJ[sl + 1] >> 8;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const double a0 = -pan[buf][i0][4 * q + lr][lc], b0 = pan[buf][j0][4 * q + lr][lc];
+                    const double a1 = -pan[buf][i1][4 * q + lr][lc], b1 = pan[buf][j1][4 * q + lr][lc];
+                    C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, C[sl], 0, 0, 0);
+                    C[sl + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, C[sl + 1], 0, 0, 0);
+                }
+            } else {
+                if (d0) syrk(sl);
+                if (d1) syrk(sl + 1);
+            }
+        }
+#else
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++) {
             const int i = tIJ[sl] & 0xFF, j = tIJ[sl] >> 8;
             if (i > k && i < mt && !(i == kn && j == kn)) syrk(sl);
         }
+#endif
         tick(4);
         CT_STAMP(k, 2);
         __syncthreads();
@@ -1617,14 +1646,267 @@ __global__ __launch_bounds__(BA_THREADS) void outlier_pass(Problem pb, State s0,
 __global__ __launch_bounds__(BA_THREADS) void drop_edges(const int* __restrict__ ept,
                                                          const uint32_t* __restrict__ list, uint32_t n,
                                                          unsigned char* __restrict__ active,
+                                                         unsigned char* __restrict__ removed,
                                                          int* __restrict__ ptcnt, int* __restrict__ ptfree)
 {
     const uint32_t i = blockIdx.x * BA_THREADS + threadIdx.x;
     if (i >= n) return;
     const uint32_t e = list[i];
     active[e] = 0;
+    removed[e] = 1;
     const int p = ept[e];
     if (atomicSub(&ptcnt[p], 1) == 1) ptfree[p] = 0;
+}
+
+// Queued small host-to-device copies in one launch: the sources are in mapped host memory (the
+// staging arena), read over the fabric; workgroup b copies GATHER_BLOCK_BYTES of the entry whose
+// block range holds b.
+constexpr int GATHER_MAX = 12;
+constexpr unsigned GATHER_BLOCK_BYTES = 4096;
+struct GatherList {
+    const char* src[GATHER_MAX];
+    char* dst[GATHER_MAX];
+    unsigned bytes[GATHER_MAX];
+    unsigned first[GATHER_MAX + 1];  // first workgroup of each entry
+    int k;
+};
+__global__ __launch_bounds__(256) void gather_copy(GatherList L)
+{
+    int i = 0;
+    while (i + 1 < L.k && blockIdx.x >= L.first[i + 1]) i++;
+    const unsigned base = (blockIdx.x - L.first[i]) * GATHER_BLOCK_BYTES, n = L.bytes[i];
+    const unsigned o = base + 16 * threadIdx.x;
+    if (o >= n) return;
+    const char* s = L.src[i] + o;
+    char* d = L.dst[i] + o;
+    // the arena offsets are 256-byte aligned and device buffers start aligned: 16-byte moves
+    // except for an entry's tail
+    if (o + 16 <= n) *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+    else
+        for (unsigned j = 0; o + j < n; j++) d[j] = s[j];
+}
+
+// Zero-fill of up to 8 word ranges in one launch (instead of one memset call per buffer).
+struct ClearList {
+    uint32_t* p[8];
+    unsigned n[8];  // 32-bit words
+    int k;
+};
+__global__ __launch_bounds__(256) void clear_words(ClearList L)
+{
+    const unsigned stride = gridDim.x * 256;
+    for (int r = 0; r < L.k; r++)
+        for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < L.n[r]; i += stride) L.p[r][i] = 0;
+}
+
+// ---- SparseOptimizer::initializeOptimization on the device ---------------------------------
+// The active edge set, the vertices in the system, the point CSR (edge order) and the camera CSR
+// (point order, then edge order) are built from the edge arrays already resident in HBM; the host
+// reads back one summary (block count, camera counts, Schur pair counts) per initialisation.
+// Summary layout (ints): INIT_HDR header words {nb, free points, active edges, a camera observes a
+// point twice}, then per camera its active edge count, then the camera of every free block, then
+// per block its free-point edge count, then the nbm x nbm pair counts (row stride nb).
+constexpr int INIT_HDR = 8;
+constexpr int INIT_LDS_CAMS = 4096;  // per-block camera histograms in LDS up to this many cameras
+
+// Counters the chain accumulates into (per point, per camera, per-point fill cursors) are zero
+// between initialisations: their single consumer clears what it read (init_scan, init_psort), so
+// no clearing launch precedes the chain.
+
+// Thread per edge: active = not removed and not (points fixed and camera fixed) (the vertices of
+// an edge between two fixed vertices leave the system); active edges counted per point (one
+// global atomic per distinct point of a wave) and per camera (LDS histogram per block, one global
+// atomic per camera).  Also resets the edge's camera-CSR position and its camera sort key (C: an
+// inactive tail entry; init_psort overwrites the active positions).
+__global__ __launch_bounds__(256) void init_edges(int E, int C, int points_fixed, const int* __restrict__ ecam,
+                                                  const int* __restrict__ ept, const unsigned char* __restrict__ removed,
+                                                  const unsigned char* __restrict__ camflag,
+                                                  unsigned char* __restrict__ active, int* __restrict__ pacc,
+                                                  int* __restrict__ cacc, int* __restrict__ epos,
+                                                  unsigned* __restrict__ ckey)
+{
+    extern __shared__ int hist[];
+    const bool lds = C <= INIT_LDS_CAMS;
+    if (lds)
+        for (int c = threadIdx.x; c < C; c += 256) hist[c] = 0;
+    __syncthreads();
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    bool a = false;
+    int p = -1;
+    if (e < E) {
+        const int c = ecam[e];
+        p = ept[e];
+        a = !removed[e] && !(points_fixed && (camflag[c] & 1));
+        active[e] = a ? 1 : 0;
+        epos[e] = -1;
+        ckey[e] = (unsigned)C;
+        if (a) {
+            if (lds) atomicAdd(&hist[c], 1);
+            else atomicAdd(&cacc[c], 1);
+        }
+    }
+    // one global atomic per distinct point of the wave (a point's edges are usually adjacent:
+    // BuildDataForG2O adds them point by point)
+    unsigned long long todo = __ballot(a);
+    while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const int lp = __shfl(p, leader);
+        const unsigned long long same = __ballot(a && p == lp);
+        if ((int)(threadIdx.x & (kWave - 1)) == leader) atomicAdd(&pacc[lp], __popcll(same));
+        todo &= ~same;
+    }
+    if (!lds) return;
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256)
+        if (hist[c]) atomicAdd(&cacc[c], hist[c]);
+}
+
+// Exclusive scan of n values by one 1024-thread workgroup (load(i) / store(i, prefix)); returns the total.
+template <class Load, class Store>
+__device__ int block_scan_1024(int n, Load load, Store store)
+{
+    __shared__ int ws[1024 / kWave];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    int carry = 0;
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + tid;
+        const int v = i < n ? load(i) : 0;
+        int inc = v;
+        for (int o = 1; o < kWave; o <<= 1) {
+            const int t = __shfl_up(inc, o);
+            if (lane >= o) inc += t;
+        }
+        if (lane == kWave - 1) ws[w] = inc;
+        __syncthreads();
+        int off = 0, tot = 0;
+        for (int k = 0; k < 1024 / kWave; k++) {
+            const int sw = ws[k];
+            off += k < w ? sw : 0;
+            tot += sw;
+        }
+        if (i < n) store(i, carry + off + inc - v);
+        carry += tot;
+        __syncthreads();
+    }
+    return carry;
+}
+
+// One workgroup: point CSR offsets, the points in the system (+ their live edge counts, which
+// drop_edges decrements), and how many; camera CSR offsets and counts; the free camera blocks in
+// camera order (not fixed, with an active edge or an active tether).  Clears the accumulators it
+// read and the per-block rhs counts init_camcsr accumulates.
+__global__ __launch_bounds__(1024) void init_scan(int C, int P, int nbm, int points_fixed,
+                                                  const unsigned char* __restrict__ camflag, int* __restrict__ pacc,
+                                                  int* __restrict__ cacc, int* __restrict__ ptcnt,
+                                                  int* __restrict__ pstart, int* __restrict__ ptfree,
+                                                  int* __restrict__ cstart, int* __restrict__ camh,
+                                                  int* __restrict__ camblk, int* __restrict__ sum)
+{
+    int* s_ccnt = sum + INIT_HDR;
+    int* s_camblk = s_ccnt + C;
+    int* s_rc = s_camblk + C;
+    const int nact = block_scan_1024(
+        P, [&](int i) { return pacc[i]; },
+        [&](int i, int x) {
+            const int k = pacc[i];
+            pstart[i] = x;
+            ptcnt[i] = k;
+            ptfree[i] = !points_fixed && k > 0;
+        });
+    const int nfp = points_fixed ? 0 : block_scan_1024(P, [&](int i) { return pacc[i] > 0 ? 1 : 0; }, [](int, int) {});
+    block_scan_1024(C, [&](int c) { return cacc[c]; },
+                    [&](int c, int x) {
+                        cstart[c] = x;
+                        s_ccnt[c] = cacc[c];
+                    });
+    auto is_free = [&](int c) { return !(camflag[c] & 1) && (cacc[c] > 0 || (camflag[c] & 2)); };
+    const int nb = block_scan_1024(
+        C, [&](int c) { return is_free(c) ? 1 : 0; },
+        [&](int c, int x) {
+            const bool f = is_free(c);
+            camh[c] = f ? x : -1;
+            if (f) {
+                camblk[x] = c;
+                s_camblk[x] = c;
+            }
+        });
+    __syncthreads();  // every read of the accumulators is done
+    for (int i = threadIdx.x; i < P; i += 1024) pacc[i] = 0;
+    for (int c = threadIdx.x; c < C; c += 1024) cacc[c] = 0;
+    for (int h = threadIdx.x; h < nbm; h += 1024) s_rc[h] = 0;
+    if (threadIdx.x == 0) {
+        pstart[P] = nact;
+        cstart[C] = nact;
+        sum[0] = nb;
+        sum[1] = nfp;
+        sum[2] = nact;
+        sum[3] = 0;
+    }
+}
+
+// Thread per active edge: its slot in its point's CSR run (unordered; init_psort orders each run).
+__global__ __launch_bounds__(256) void init_pfill(int E, const int* __restrict__ ept, const unsigned char* __restrict__ active,
+                                                  const int* __restrict__ pstart, int* __restrict__ pcur,
+                                                  int* __restrict__ pedges)
+{
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= E || !active[e]) return;
+    const int p = ept[e];
+    pedges[pstart[p] + atomicAdd(&pcur[p], 1)] = e;
+}
+
+// Thread per point: its CSR run in edge order (insertion sort: a point has few edges), the camera
+// sort keys of its positions, and the fill cursor back to zero.
+__global__ __launch_bounds__(256) void init_psort(int P, const int* __restrict__ pstart, const int* __restrict__ ecam,
+                                                  int* __restrict__ pcur, int* __restrict__ pedges,
+                                                  unsigned* __restrict__ ckey)
+{
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const int b = pstart[p], end = pstart[p + 1];
+    for (int a = b + 1; a < end; a++) {
+        const int v = pedges[a];
+        int j = a;
+        while (j > b && pedges[j - 1] > v) {
+            pedges[j] = pedges[j - 1];
+            j--;
+        }
+        pedges[j] = v;
+    }
+    for (int a = b; a < end; a++) ckey[a] = (unsigned)ecam[pedges[a]];
+    pcur[p] = 0;
+}
+
+// Camera CSR from the stable sort by camera of the point-CSR order: (camera, point, edge) order.
+// Flags a camera observing a point twice (two consecutive entries of one camera on one point) and
+// counts each free block's edges on points in the system (its diagonal pair's rhs list).
+__global__ __launch_bounds__(256) void init_camcsr(int E, int C, int nbm, const unsigned* __restrict__ ckey_sorted,
+                                                   const int* __restrict__ cval, const int* __restrict__ ept,
+                                                   const int* __restrict__ camh, const int* __restrict__ ptfree,
+                                                   int* __restrict__ cedges, int* __restrict__ cpt,
+                                                   int* __restrict__ epos, int* __restrict__ sum, int* __restrict__ rc)
+{
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    const unsigned k = a < E ? ckey_sorted[a] : (unsigned)C;
+    int h = -1;
+    if (k < (unsigned)C) {
+        const int e = cval[a], p = ept[e];
+        cedges[a] = e;
+        cpt[a] = p;
+        epos[e] = a;
+        if (a > 0 && ckey_sorted[a - 1] == k && ept[cval[a - 1]] == p) atomicOr(&sum[3], 1);
+        if (ptfree[p]) h = camh[k];
+        if (h >= nbm) h = -1;  // more free blocks than the summary holds: refused by the host
+    }
+    // the entries are sorted by camera: one atomic per distinct block of the wave
+    unsigned long long todo = __ballot(h >= 0);
+    while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const int lh = __shfl(h, leader);
+        const unsigned long long same = __ballot(h == lh);
+        if ((int)(threadIdx.x & (kWave - 1)) == leader) atomicAdd(&rc[lh], __popcll(same));
+        todo &= ~same;
+    }
 }
 
 // ---- Schur product lists built on the device (SparseOptimizer::initializeOptimization + g2o's
@@ -1755,7 +2037,9 @@ __global__ __launch_bounds__(256) void schur_rhs(const int* __restrict__ camblk,
 // p in camera block h sits at camera-CSR position cstart[c_h] + (rank of p in A_h).
 constexpr int SC_LDS_WORDS = 16384;  // point bit words staged in LDS (P <= 524288)
 
-__global__ __launch_bounds__(1024) void sc_bitmaps(int P, int nb, const int* __restrict__ camblk,
+// Grid: one workgroup per possible block (the block count nb = hdr[0] is known on the device
+// only) + the last one for F.
+__global__ __launch_bounds__(1024) void sc_bitmaps(int P, const int* __restrict__ hdr, const int* __restrict__ camblk,
                                                    const int* __restrict__ cstart, const int* __restrict__ cpt,
                                                    const int* __restrict__ ptfree, uint32_t* __restrict__ A,
                                                    int* __restrict__ R, uint32_t* __restrict__ F)
@@ -1763,7 +2047,7 @@ __global__ __launch_bounds__(1024) void sc_bitmaps(int P, int nb, const int* __r
     __shared__ uint32_t bm[SC_LDS_WORDS];
     __shared__ int part[1024];
     const int PW = (P + 31) / 32, tid = threadIdx.x, h = blockIdx.x;
-    if (h == nb) {
+    if (h == (int)gridDim.x - 1) {
         for (int w = tid; w < PW; w += 1024) {
             uint32_t v = 0;
             for (int j = 0; j < 32 && 32 * w + j < P; j++) v |= (ptfree[32 * w + j] ? 1u : 0u) << j;
@@ -1771,6 +2055,7 @@ __global__ __launch_bounds__(1024) void sc_bitmaps(int P, int nb, const int* __r
         }
         return;
     }
+    if (h >= hdr[0]) return;
     for (int w = tid; w < PW; w += 1024) bm[w] = 0;
     __syncthreads();
     const int c = camblk[h];
@@ -1801,11 +2086,11 @@ __global__ __launch_bounds__(1024) void sc_bitmaps(int P, int nb, const int* __r
     }
 }
 
-__global__ __launch_bounds__(64) void sc_pair_counts(int nb, int PW, const uint32_t* __restrict__ A,
+__global__ __launch_bounds__(64) void sc_pair_counts(const int* __restrict__ hdr, int PW, const uint32_t* __restrict__ A,
                                                      const uint32_t* __restrict__ F, int* __restrict__ cnt)
 {
-    const int a = blockIdx.x, b = blockIdx.y;
-    if (b < a) return;
+    const int a = blockIdx.x, b = blockIdx.y, nb = hdr[0];
+    if (b < a || b >= nb || nb > (int)gridDim.x) return;  // more blocks than the grid: refused by the host
     const uint32_t* Aa = A + (size_t)a * PW;
     const uint32_t* Ab = A + (size_t)b * PW;
     int n = 0;
@@ -1886,9 +2171,8 @@ struct BundleAdjuster {
     bool points_fixed = false;
     // host copies of the problem
     int C = 0, P = 0, E = 0;
-    std::vector<double> q, t, camk, p, uv, info;
-    std::vector<int> fixed, ecam, ept;
-    std::vector<unsigned char> removed;
+    std::vector<double> q, t, camk, p;
+    std::vector<int> fixed, ecam;  // ecam: per-camera edge bookkeeping of outlier removals
     std::vector<Tether> teth;      // distance, rotation, transform tethers (set order)
     std::vector<int> cam_tethers;  // active tethers per camera (keeps a camera in the system)
     bool dirty = true;  // full (re)initialisation needed: setters or a camera left the system
@@ -1947,11 +2231,13 @@ struct BundleAdjuster {
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
         d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_cub, d_kdst, d_rblk, d_sbits, d_srank, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
-        d_sfinish, d_epos, d_chi_lin, d_livebuf;
+        d_sfinish, d_epos, d_chi_lin, d_livebuf, d_removed, d_camflag, d_ikeys, d_ivals, d_isum, d_iacc;
+    bool iacc_clean = false;  // d_iacc is all zero (see initialize())
     // outlier lists of the speculative / final post-pass (2 x E entries), written by the kernels
     // straight into host memory: the host sorts and returns them after the completion wait
     MappedBuffer h_olist;
-    PinnedBuffer h_kb;  // per-pair list bounds read back by build_product_lists
+    PinnedBuffer h_kb;    // per-pair list bounds read back by build_product_lists
+    PinnedBuffer h_isum;  // the device initialisation's summary (init_scan etc., INIT_HDR layout)
     std::vector<int> camcnt;  // active observation edges per camera (host-side bookkeeping)
     int n_entries = 0;  // point-CSR entries (active edges at initialisation)
     int nb_free = 0;    // cameras in the reduced system
@@ -1967,10 +2253,10 @@ struct BundleAdjuster {
         pb.camk = d_camk.as<double>();
         pb.camh = d_camh.as<int>();
         pb.ptfree = d_ptfree.as<int>();
-        pb.uv = d_uv.as<double>();
+        pb.uv = d_uv.as<float>();
         pb.ecam = d_ecam.as<int>();
         pb.ept = d_ept.as<int>();
-        pb.info = d_info.as<double>();
+        pb.info = d_info.as<float>();
         pb.active = d_active.as<unsigned char>();
         pb.pstart = d_pstart.as<int>();
         pb.pedges = d_pedges.as<int>();
@@ -1992,24 +2278,78 @@ struct BundleAdjuster {
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
                         &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_cub, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
-                        &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf})
+                        &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf, &d_removed, &d_camflag,
+                        &d_ikeys, &d_ivals, &d_isum, &d_iacc})
             b->release();
         h_olist.release();
         h_state.release();
         h_kb.release();
+        h_isum.release();
+        h_stage.release();
+        iacc_clean = false;
+        stage_off = 0;
+        pending.k = 0;
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
         if (h_ctl) (void)hipHostFree(h_ctl);
         h_ctl = nullptr;
     }
 
+    // Host-to-device copies go through a pinned, device-mapped staging arena.  Large ones are DMA
+    // copies (a hipMemcpyAsync from pageable memory would be a synchronous staged copy); small ones
+    // are queued and moved by one gather_copy launch (flush_uploads) instead of one copy call
+    // each.  The arena restarts from its beginning only after a stream synchronisation, so no
+    // pending copy sees its source change.
+    MappedBuffer h_stage;
+    size_t stage_off = 0;
+    GatherList pending{};
+    static constexpr size_t GATHER_MAX_BYTES = 64 << 10;
+    void flush_uploads()
+    {
+        if (pending.k == 0) return;
+        unsigned blocks = 0;
+        for (int i = 0; i < pending.k; i++) {
+            pending.first[i] = blocks;
+            blocks += (unsigned)((pending.bytes[i] + GATHER_BLOCK_BYTES - 1) / GATHER_BLOCK_BYTES);
+        }
+        pending.first[pending.k] = blocks;
+        launch("ba.upload_gather", gather_copy, dim3(blocks), dim3(256), 0, st, pending);
+        pending.k = 0;
+    }
+    mage_status stage_copy(void* dst, const void* src, size_t bytes)
+    {
+        if (bytes == 0) return MAGE_OK;
+        const size_t need = (bytes + 255) & ~(size_t)255;
+        if (stage_off + need > h_stage.bytes) {
+            flush_uploads();
+            MAGE_HIP(hipStreamSynchronize(st));
+            stage_off = 0;
+            mage_status r = h_stage.reserve(std::max(need, std::max<size_t>(2 * h_stage.bytes, (size_t)4 << 20)));
+            if (r != MAGE_OK) return r;
+        }
+        std::memcpy(h_stage.host<char>() + stage_off, src, bytes);
+        if (bytes >= GATHER_MAX_BYTES) {
+            MAGE_HIP(hipMemcpyAsync(dst, h_stage.host<char>() + stage_off, bytes, hipMemcpyHostToDevice, st));
+        } else {
+            if (pending.k == GATHER_MAX) flush_uploads();
+            pending.src[pending.k] = h_stage.device<const char>() + stage_off;
+            pending.dst[pending.k] = static_cast<char*>(dst);
+            pending.bytes[pending.k++] = (unsigned)bytes;
+        }
+        stage_off += need;
+        return MAGE_OK;
+    }
     template <typename T>
     mage_status upload(DeviceBuffer& b, const std::vector<T>& v)
     {
-        mage_status r = b.reserve(std::max<size_t>(v.size() * sizeof(T), 16));
+        return upload(b, v.data(), v.size());
+    }
+    template <typename T>
+    mage_status upload(DeviceBuffer& b, const T* v, size_t n)
+    {
+        mage_status r = b.reserve(std::max<size_t>(n * sizeof(T), 16));
         if (r != MAGE_OK) return r;
-        if (!v.empty()) MAGE_HIP(hipMemcpyAsync(b.ptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
-        return MAGE_OK;
+        return stage_copy(b.ptr, v, n * sizeof(T));
     }
 
     // export_state's mirror of the current estimate (valid while export_seq is the last sequence
@@ -2057,47 +2397,57 @@ struct BundleAdjuster {
     static size_t nprod_pad(long long n) { return (size_t)((n + 255) / 256 * 256); }
     // Builds every pair's product list on the device (schur_point_lists -> exclusive scan ->
     // schur_point_products -> stable radix sort by pair key -> schur_list_bounds) and reads back
-    // each dense pair key's first sorted position and count.  nmax bounds the products (sum of
-    // k_p^2); the unused tail holds key 0xFFFF, which sorts after every pair.
-    mage_status build_product_lists(int nmax, int nb, int ncsr, std::vector<int>& kstart, std::vector<int>& kcount)
+    // each dense pair key's first sorted position and count; *nprod = the number of products.
+    // Only for a camera observing a point twice (else the bit-set path of initialize()).
+    mage_status build_product_lists(int nb, int ncsr, std::vector<int>& kstart, std::vector<int>& kcount,
+                                    long long* nprod)
     {
         mage_status r;
         const int Pm = std::max(P, 1), nk = nb * nb;
-        const size_t pad = nprod_pad(nmax);
         if ((r = d_plist.reserve((size_t)std::max(ncsr, 1) * sizeof(int2))) != MAGE_OK) return r;
         if ((r = d_pcnt.reserve((size_t)3 * Pm * sizeof(int))) != MAGE_OK) return r;
-        if ((r = d_skeys.reserve(2 * pad * sizeof(uint16_t))) != MAGE_OK) return r;
-        if ((r = d_svals.reserve(2 * pad * sizeof(unsigned long long))) != MAGE_OK) return r;
-        if ((r = d_kb.reserve((size_t)2 * nk * sizeof(int))) != MAGE_OK) return r;
         int* pcnt = d_pcnt.as<int>();
         int* poff = pcnt + Pm;
         int* klen = pcnt + 2 * Pm;
+        size_t tb_scan = 0;
+        MAGE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, pcnt, poff, P, st));
+        if ((r = d_cub.reserve(std::max<size_t>(tb_scan, 16))) != MAGE_OK) return r;
+        const unsigned gp = (unsigned)((P + 255) / 256);
+        launch("ba.schur_lists", schur_point_lists, dim3(gp), dim3(256), 0, st, P, (const int*)d_pstart.as<int>(),
+               (const int*)d_pedges.as<int>(), (const int*)d_ecam.as<int>(), (const int*)d_camh.as<int>(),
+               (const int*)d_epos.as<int>(), (const int*)d_ptfree.as<int>(), d_plist.as<int2>(), pcnt, klen);
+        size_t tb = d_cub.bytes;
+        MAGE_HIP(hipcub::DeviceScan::ExclusiveSum(d_cub.ptr, tb, pcnt, poff, P, st));
+        if ((r = h_kb.reserve((size_t)std::max(2 * nk, 2) * sizeof(int))) != MAGE_OK) return r;
+        MAGE_HIP(hipMemcpyAsync(h_kb.ptr, poff + P - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipMemcpyAsync(h_kb.as<int>() + 1, pcnt + P - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        const long long nmax = (long long)h_kb.as<int>()[0] + h_kb.as<int>()[1];
+        *nprod = nmax;
+        MAGE_REQUIRE(nmax < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
+        if (nmax == 0) return MAGE_OK;
+        const size_t pad = nprod_pad(nmax);
+        if ((r = d_skeys.reserve(2 * pad * sizeof(uint16_t))) != MAGE_OK) return r;
+        if ((r = d_svals.reserve(2 * pad * sizeof(unsigned long long))) != MAGE_OK) return r;
+        if ((r = d_kb.reserve((size_t)2 * nk * sizeof(int))) != MAGE_OK) return r;
         uint16_t* kin = d_skeys.as<uint16_t>();
         uint16_t* kout = kin + pad;
         unsigned long long* vin = d_svals.as<unsigned long long>();
         unsigned long long* vout = vin + pad;
         int bits = 1;
         while ((1 << bits) < nk + 1) bits++;
-        size_t tb_scan = 0, tb_sort = 0;
-        MAGE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, pcnt, poff, P, st));
-        MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, kin, kout, vin, vout, nmax, 0, bits, st));
-        if ((r = d_cub.reserve(std::max<size_t>(std::max(tb_scan, tb_sort), 16))) != MAGE_OK) return r;
-        MAGE_HIP(hipMemsetAsync(kin, 0xFF, (size_t)nmax * sizeof(uint16_t), st));
+        size_t tb_sort = 0;
+        MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, kin, kout, vin, vout, (int)nmax, 0, bits, st));
+        if ((r = d_cub.reserve(std::max<size_t>(tb_sort, 16))) != MAGE_OK) return r;
         MAGE_HIP(hipMemsetAsync(d_kb.ptr, 0, (size_t)2 * nk * sizeof(int), st));
-        const unsigned gp = (unsigned)((P + 255) / 256), gn = (unsigned)((nmax + 255) / 256);
-        launch("ba.schur_lists", schur_point_lists, dim3(gp), dim3(256), 0, st, P, (const int*)d_pstart.as<int>(),
-               (const int*)d_pedges.as<int>(), (const int*)d_ecam.as<int>(), (const int*)d_camh.as<int>(),
-               (const int*)d_epos.as<int>(), (const int*)d_ptfree.as<int>(), d_plist.as<int2>(), pcnt, klen);
-        size_t tb = d_cub.bytes;
-        MAGE_HIP(hipcub::DeviceScan::ExclusiveSum(d_cub.ptr, tb, pcnt, poff, P, st));
         launch("ba.schur_products", schur_point_products, dim3(gp), dim3(256), 0, st, P, nb,
                (const int*)d_pstart.as<int>(), (const int2*)d_plist.as<int2>(), (const int*)poff, (const int*)klen, kin, vin);
         tb = d_cub.bytes;
-        MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(d_cub.ptr, tb, kin, kout, vin, vout, nmax, 0, bits, st));
-        launch("ba.schur_bounds", schur_list_bounds, dim3(gn), dim3(256), 0, st, (const uint16_t*)kout, nmax, nk,
+        MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(d_cub.ptr, tb, kin, kout, vin, vout, (int)nmax, 0, bits, st));
+        const unsigned gn = (unsigned)((nmax + 255) / 256);
+        launch("ba.schur_bounds", schur_list_bounds, dim3(gn), dim3(256), 0, st, (const uint16_t*)kout, (int)nmax, nk,
                d_kb.as<int>());
         MAGE_HIP(hipGetLastError());
-        if ((r = h_kb.reserve((size_t)2 * nk * sizeof(int))) != MAGE_OK) return r;
         MAGE_HIP(hipMemcpyAsync(h_kb.ptr, d_kb.ptr, (size_t)2 * nk * sizeof(int), hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipStreamSynchronize(st));
         const int* kb = h_kb.as<int>();
@@ -2117,144 +2467,167 @@ struct BundleAdjuster {
             if (!on) return;
             const auto n = std::chrono::steady_clock::now();
             fprintf(stderr, "[ba.init] %-28s %8.1f us\n", what, std::chrono::duration<double, std::micro>(n - t).count());
-            t = n;
+            t = std::chrono::steady_clock::now();  // the print is not charged to the next phase
         }
     };
+    struct ScopeTimer {  // MAGE_BA_TIMING=1: one entry point's wall time on stderr
+        PhaseTimer pt;
+        const char* what;
+        explicit ScopeTimer(const char* w) : what(w) {}
+        ~ScopeTimer() { pt.mark(what); }
+    };
+    // initialize()'s host tables, kept between calls: reused capacity instead of fresh allocations
+    // (page faults on every BuildDataForG2O window)
+    struct InitTables {
+        std::vector<unsigned char> camflag, mark;
+        std::vector<int2> pairs;
+        std::vector<int> pairidx, kcount, kstart, ptstart, ptlist, pcount, rcount, rblk, kdst, sfinish;
+        std::vector<long long> pbeg, roww;
+        std::vector<SchurPair> spairs;
+        std::vector<SchurChunk> xcd_chunks[8], schunks;
+    } ws;
     mage_status initialize()
     {
         PhaseTimer pt;
         mage_status r = sync_host_state();
         if (r != MAGE_OK) return r;
         pt.mark("sync_host_state");
-        std::vector<unsigned char> active(E);
-        std::vector<int> camHas(C, 0), ptHas(P, 0);
-        for (int e = 0; e < E; e++) {
-            const bool a = !removed[e] && !(fixed[ecam[e]] && points_fixed);
-            active[e] = a;
-            if (a) {
-                camHas[ecam[e]] = 1;
-                ptHas[ept[e]] = 1;
-            }
-        }
         // tethers: active unless both cameras are fixed; their cameras join the system
         cam_tethers.assign(C, 0);
         for (auto& T : teth) {
             T.active = !(fixed[T.c1] && fixed[T.c2]);
             if (T.active) {
-                camHas[T.c1] = camHas[T.c2] = 1;
                 cam_tethers[T.c1]++;
                 cam_tethers[T.c2]++;
             }
         }
+        // The active edge set, the point / camera CSRs and the free blocks are built on the device
+        // (init_edges, init_scan, init_pfill / init_psort, a stable radix sort by camera,
+        // init_camcsr); so are the Schur pairs' product counts when no camera observes a point twice
+        // (sc_bitmaps / sc_pair_counts).  One summary comes back.
+        const size_t Cm = std::max(C, 1), Pm = std::max(P, 1), Em = std::max(E, 1);
+        const int nbm = std::min(C, CH_PANEL_ROWS / 6);  // a larger block count is refused below
+        const int PW = (P + 31) / 32;
+        const size_t nsum = (size_t)INIT_HDR + 2 * (size_t)C + (size_t)nbm + (size_t)nbm * nbm;
+        {
+            auto& camflag = ws.camflag;
+            camflag.assign(Cm, 0);
+            for (int c = 0; c < C; c++) camflag[c] = (fixed[c] ? 1 : 0) | (cam_tethers[c] ? 2 : 0);
+            if ((r = upload(d_camflag, camflag)) != MAGE_OK) return r;
+            flush_uploads();
+        }
+        for (auto pr : {std::make_pair(&d_camh, (size_t)Cm * 4), std::make_pair(&d_camblk, (size_t)Cm * 4),
+                        std::make_pair(&d_ptfree, (size_t)Pm * 4), std::make_pair(&d_ptcnt, (size_t)Pm * 4),
+                        std::make_pair(&d_pstart, (size_t)(Pm + 1) * 4), std::make_pair(&d_cstart, (size_t)(Cm + 1) * 4),
+                        std::make_pair(&d_pedges, (size_t)Em * 4), std::make_pair(&d_cedges, (size_t)Em * 4),
+                        std::make_pair(&d_cpt, (size_t)Em * 4), std::make_pair(&d_epos, (size_t)Em * 4),
+                        std::make_pair(&d_active, (size_t)Em), std::make_pair(&d_ikeys, (size_t)Em * 8),
+                        std::make_pair(&d_ivals, (size_t)Em * 4), std::make_pair(&d_isum, nsum * 4)})
+            if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
+        if ((r = h_isum.reserve(nsum * 4)) != MAGE_OK) return r;
+        int* sum = d_isum.as<int>();
+        int* s_ccnt = sum + INIT_HDR;
+        int* s_camblk = s_ccnt + C;
+        int* s_rc = s_camblk + C;
+        int* s_kcnt = s_rc + nbm;
+        unsigned* k0 = d_ikeys.as<unsigned>();
+        unsigned* k1 = k0 + Em;
+        int* v0 = d_ivals.as<int>();
+        // accumulators kept zero between initialisations (cleared by their consumers): per point,
+        // per camera, per-point fill cursors; cleared here only when (re)allocated or after a
+        // chain that did not complete
+        const size_t acc_bytes = (2 * Pm + Cm) * 4;
+        if (d_iacc.bytes < acc_bytes || !iacc_clean) {
+            if ((r = d_iacc.reserve(acc_bytes)) != MAGE_OK) return r;
+            MAGE_HIP(hipMemsetAsync(d_iacc.ptr, 0, d_iacc.bytes, st));
+        }
+        iacc_clean = false;
+        int* pacc = d_iacc.as<int>();
+        int* cacc = pacc + Pm;
+        int* pcur = cacc + Cm;
+        int cbits = 1;
+        while ((1ll << cbits) <= C) cbits++;
+        const unsigned ge = (unsigned)((E + 255) / 256), gp = (unsigned)((P + 255) / 256);
+        if (E > 0)
+            launch("ba.init_edges", init_edges, dim3(ge), dim3(256), C <= INIT_LDS_CAMS ? C * 4 : 0, st, E, C,
+                   points_fixed ? 1 : 0, (const int*)d_ecam.as<int>(), (const int*)d_ept.as<int>(),
+                   (const unsigned char*)d_removed.as<unsigned char>(), (const unsigned char*)d_camflag.as<unsigned char>(),
+                   d_active.as<unsigned char>(), pacc, cacc, d_epos.as<int>(), k0);
+        launch("ba.init_scan", init_scan, dim3(1), dim3(1024), 0, st, C, P, nbm, points_fixed ? 1 : 0,
+               (const unsigned char*)d_camflag.as<unsigned char>(), pacc, cacc, d_ptcnt.as<int>(), d_pstart.as<int>(),
+               d_ptfree.as<int>(), d_cstart.as<int>(), d_camh.as<int>(), d_camblk.as<int>(), sum);
+        if (E > 0) {
+            // point CSR in edge order (slots by atomics, each run sorted); camera CSR: that order
+            // stably sorted by camera
+            launch("ba.init_pfill", init_pfill, dim3(ge), dim3(256), 0, st, E, (const int*)d_ept.as<int>(),
+                   (const unsigned char*)d_active.as<unsigned char>(), (const int*)d_pstart.as<int>(), pcur,
+                   d_pedges.as<int>());
+            if (P > 0)
+                launch("ba.init_psort", init_psort, dim3(gp), dim3(256), 0, st, P, (const int*)d_pstart.as<int>(),
+                       (const int*)d_ecam.as<int>(), pcur, d_pedges.as<int>(), k0);
+            size_t tb = 0;
+            MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, (const int*)d_pedges.as<int>(), v0, E, 0, cbits, st));
+            if ((r = d_cub.reserve(std::max<size_t>(tb, 16))) != MAGE_OK) return r;
+            tb = d_cub.bytes;
+            MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(d_cub.ptr, tb, k0, k1, (const int*)d_pedges.as<int>(), v0, E, 0,
+                                                        cbits, st));
+            launch("ba.init_camcsr", init_camcsr, dim3(ge), dim3(256), 0, st, E, C, nbm, (const unsigned*)k1, (const int*)v0,
+                   (const int*)d_ept.as<int>(), (const int*)d_camh.as<int>(), (const int*)d_ptfree.as<int>(),
+                   d_cedges.as<int>(), d_cpt.as<int>(), d_epos.as<int>(), sum, s_rc);
+        }
+        const bool bitmap_fits = PW <= SC_LDS_WORDS && nbm > 0 && P > 0;
+        if (bitmap_fits) {
+            if ((r = d_sbits.reserve(((size_t)nbm + 1) * PW * 4)) != MAGE_OK) return r;
+            if ((r = d_srank.reserve((size_t)nbm * PW * 4)) != MAGE_OK) return r;
+            uint32_t* A = d_sbits.as<uint32_t>();
+            launch("ba.schur_bitmaps", sc_bitmaps, dim3(nbm + 1), dim3(1024), 0, st, P, (const int*)sum,
+                   (const int*)d_camblk.as<int>(), (const int*)d_cstart.as<int>(), (const int*)d_cpt.as<int>(),
+                   (const int*)d_ptfree.as<int>(), A, d_srank.as<int>(), A + (size_t)nbm * PW);
+            launch("ba.schur_counts", sc_pair_counts, dim3(nbm, nbm), dim3(64), 0, st, (const int*)sum, PW,
+                   (const uint32_t*)A, (const uint32_t*)(A + (size_t)nbm * PW), s_kcnt);
+        }
+        MAGE_HIP(hipGetLastError());
+        MAGE_HIP(hipMemcpyAsync(h_isum.ptr, sum, nsum * 4, hipMemcpyDeviceToHost, st));
+        MAGE_HIP(hipStreamSynchronize(st));
+        iacc_clean = true;
+        pt.mark("device init + summary");
+        const int* hs = h_isum.as<int>();
+        const int nb = hs[0], nfp = hs[1], nact = hs[2];
+        const bool dup = hs[3] != 0;  // a camera observing a point twice (its CSR run lists the point twice)
+        MAGE_REQUIRE(nb <= CH_PANEL_ROWS / 6, MAGE_EUNSUPPORTED, "more than 96 free cameras in one bundle adjustment");
         camh.assign(C, -1);
-        cam_of_block.clear();
-        for (int c = 0; c < C; c++)
-            if (!fixed[c] && camHas[c]) {
-                camh[c] = (int)cam_of_block.size();
-                cam_of_block.push_back(c);
-            }
-        ptfree.assign(P, 0);
-        int nfp = 0;
-        for (int i = 0; i < P; i++)
-            if (!points_fixed && ptHas[i]) {
-                ptfree[i] = 1;
-                nfp++;
-            }
-        const int nb = (int)cam_of_block.size();
+        cam_of_block.assign(hs + INIT_HDR + C, hs + INIT_HDR + C + nb);
+        for (int h = 0; h < nb; h++) camh[cam_of_block[h]] = h;
+        camcnt.assign(hs + INIT_HDR, hs + INIT_HDR + C);
+        const int* h_rc = hs + INIT_HDR + 2 * C;
+        const int* h_kcnt = h_rc + nbm;
         nb_free = nb;
         n = 6 * nb;
         np = (n + 15) / 16 * 16;
         useless = (nb == 0 && nfp == 0);
-        MAGE_REQUIRE(nb <= CH_PANEL_ROWS / 6, MAGE_EUNSUPPORTED, "more than 96 free cameras in one bundle adjustment");
-        pt.mark("active / blocks");
-        // CSR by point (edge order) and by camera (point order, then edge order)
-        std::vector<int> pstart(P + 1, 0), cstart(C + 1, 0);
-        for (int e = 0; e < E; e++)
-            if (active[e]) {
-                pstart[ept[e] + 1]++;
-                cstart[ecam[e] + 1]++;
-            }
-        for (int i = 0; i < P; i++) pstart[i + 1] += pstart[i];
-        for (int c = 0; c < C; c++) cstart[c + 1] += cstart[c];
-        std::vector<int> pedges(std::max(pstart[P], 1)), cedges(std::max(cstart[C], 1)), cpt(std::max(cstart[C], 1));
-        {
-            std::vector<int> pf(pstart.begin(), pstart.end() - 1), cf(cstart.begin(), cstart.end() - 1);
-            for (int e = 0; e < E; e++)
-                if (active[e]) pedges[pf[ept[e]]++] = e;
-            // walking points in order makes each camera's list sorted by point id
-            for (int i = 0; i < P; i++)
-                for (int a = pstart[i]; a < pstart[i + 1]; a++) {
-                    const int e = pedges[a];
-                    cedges[cf[ecam[e]]] = e;
-                    cpt[cf[ecam[e]]++] = i;
-                }
-        }
-        pt.mark("CSR");
-        // camera-CSR position of every listed edge: Hpl and Z are stored camera-major (component
-        // arrays indexed by this position), so a pair's Schur products read them coalesced
-        std::vector<int> epos(std::max(E, 1), -1);
-        for (int a = 0; a < cstart[C]; a++) epos[cedges[a]] = a;
-        // The structure the Schur products need goes to the device first; the per-pair product
-        // lists are built there and the host only reads back the per-pair counts: from the cameras'
-        // point bit sets when no camera observes a point twice (sc_bitmaps / sc_pair_counts /
-        // sc_pair_fill), else per point (schur_point_lists / _products, a stable radix sort by
-        // pair, schur_list_bounds).
-        if ((r = upload(d_epos, epos)) != MAGE_OK) return r;
-        if ((r = upload(d_camh, camh)) != MAGE_OK) return r;
-        if ((r = upload(d_ptfree, ptfree)) != MAGE_OK) return r;
-        if ((r = upload(d_pstart, pstart)) != MAGE_OK) return r;
-        if ((r = upload(d_pedges, pedges)) != MAGE_OK) return r;
-        if ((r = upload(d_cstart, cstart)) != MAGE_OK) return r;
-        if ((r = upload(d_cpt, cpt)) != MAGE_OK) return r;
-        if ((r = upload(d_camblk, cam_of_block)) != MAGE_OK) return r;
-        bool dup = false;  // a camera observing a point twice (its CSR run lists the point twice)
-        for (int c = 0; c < C && !dup; c++)
-            for (int a = cstart[c] + 1; a < cstart[c + 1]; a++)
-                if (cpt[a] == cpt[a - 1]) {
-                    dup = true;
-                    break;
-                }
-        const int PW = (P + 31) / 32;
-        const bool bitmaps = !dup && PW <= SC_LDS_WORDS && nb > 0 && nfp > 0;
+        n_entries = nact;
+        const bool bitmaps = !dup && bitmap_fits && nb > 0 && nfp > 0;
         // covisible camera pairs (h1 <= h2) of the reduced system: every pair sharing a free point
         // (a product list), the diagonal, and the tethered pairs
-        std::vector<int2> pairs;
-        std::vector<int> pairidx((size_t)std::max(nb, 1) * std::max(nb, 1), -1);
+        auto& pairs = ws.pairs;
+        pairs.clear();
+        auto& pairidx = ws.pairidx;
+        pairidx.assign((size_t)std::max(nb, 1) * std::max(nb, 1), -1);
         const int nk = std::max(nb, 1) * std::max(nb, 1);  // dense pair keys h1 * nb + h2
-        std::vector<int> kcount(nk, 0), kstart(nk, 0);
-        long long nprod_max = 0;  // sum over free points of k_p^2 bounds the products
+        auto &kcount = ws.kcount, &kstart = ws.kstart;
+        kcount.assign(nk, 0);
+        kstart.assign(nk, 0);
+        long long nprod_max = 0;  // products of the sorted (fallback) lists
         if (bitmaps) {
-            if ((r = d_sbits.reserve(((size_t)nb + 1) * PW * 4)) != MAGE_OK) return r;
-            if ((r = d_srank.reserve((size_t)nb * PW * 4)) != MAGE_OK) return r;
-            if ((r = d_kb.reserve((size_t)nk * sizeof(int))) != MAGE_OK) return r;
-            uint32_t* A = d_sbits.as<uint32_t>();
-            uint32_t* F = A + (size_t)nb * PW;
-            launch("ba.schur_bitmaps", sc_bitmaps, dim3(nb + 1), dim3(1024), 0, st, P, nb, (const int*)d_camblk.as<int>(),
-                   (const int*)d_cstart.as<int>(), (const int*)d_cpt.as<int>(), (const int*)d_ptfree.as<int>(), A,
-                   d_srank.as<int>(), F);
-            launch("ba.schur_counts", sc_pair_counts, dim3(nb, nb), dim3(64), 0, st, nb, PW, (const uint32_t*)A,
-                   (const uint32_t*)F, d_kb.as<int>());
-            MAGE_HIP(hipGetLastError());
-            if ((r = h_kb.reserve((size_t)nk * sizeof(int))) != MAGE_OK) return r;
-            MAGE_HIP(hipMemcpyAsync(h_kb.ptr, d_kb.ptr, (size_t)nk * sizeof(int), hipMemcpyDeviceToHost, st));
-            MAGE_HIP(hipStreamSynchronize(st));
             for (int x = 0; x < nb; x++)
-                for (int y = x; y < nb; y++) kcount[(size_t)x * nb + y] = h_kb.as<int>()[(size_t)x * nb + y];
+                for (int y = x; y < nb; y++) kcount[(size_t)x * nb + y] = h_kcnt[(size_t)x * nb + y];
         } else if (nb > 0 && nfp > 0) {
-            for (int i = 0; i < P; i++) {
-                if (!ptfree[i]) continue;
-                long long k = 0;
-                for (int a = pstart[i]; a < pstart[i + 1]; a++) k += camh[ecam[pedges[a]]] >= 0;
-                nprod_max += k * k;
-            }
+            if ((r = build_product_lists(nb, nact, kstart, kcount, &nprod_max)) != MAGE_OK) return r;
         }
-        MAGE_REQUIRE(nprod_max < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
-        if (nprod_max > 0) {
-            if ((r = build_product_lists((int)nprod_max, nb, pstart[P], kstart, kcount)) != MAGE_OK) return r;
-        }
-        pt.mark("pairs + product lists (device)");
+        pt.mark("pair counts");
         if (nb > 0) {
-            std::vector<unsigned char> mark((size_t)nb * nb, 0);
+            auto& mark = ws.mark;
+            mark.assign((size_t)nb * nb, 0);
             for (int k = 0; k < nb * nb; k++) mark[k] = kcount[k] > 0;
             for (int h = 0; h < nb; h++) mark[(size_t)h * nb + h] = 1;
             for (auto& T : teth) {
@@ -2272,35 +2645,38 @@ struct BundleAdjuster {
         }
         npairs = (int)pairs.size();
         // per pair: the tethers whose H12 lands in its block (code 2 t + transposed), set order
-        std::vector<int> ptstart(npairs + 1, 0), ptlist;
-        for (int pi = 0; pi < npairs; pi++) {
-            for (int ti = 0; ti < (int)teth.size(); ti++) {
-                const Tether& T = teth[ti];
-                if (!T.active || T.h1 < 0 || T.h2 < 0) continue;
-                if (T.h1 == pairs[pi].x && T.h2 == pairs[pi].y) ptlist.push_back(2 * ti);
-                else if (T.h2 == pairs[pi].x && T.h1 == pairs[pi].y) ptlist.push_back(2 * ti + 1);
+        auto &ptstart = ws.ptstart, &ptlist = ws.ptlist;
+        ptstart.assign(npairs + 1, 0);
+        ptlist.clear();
+        if (!teth.empty())
+            for (int pi = 0; pi < npairs; pi++) {
+                for (int ti = 0; ti < (int)teth.size(); ti++) {
+                    const Tether& T = teth[ti];
+                    if (!T.active || T.h1 < 0 || T.h2 < 0) continue;
+                    if (T.h1 == pairs[pi].x && T.h2 == pairs[pi].y) ptlist.push_back(2 * ti);
+                    else if (T.h2 == pairs[pi].x && T.h1 == pairs[pi].y) ptlist.push_back(2 * ti + 1);
+                }
+                ptstart[pi + 1] = (int)ptlist.size();
             }
-            ptstart[pi + 1] = (int)ptlist.size();
-        }
         // Schur product lists (schur_chunks): per pair the (e1, e2) products of its shared free
         // points in point order, then for a diagonal pair the rhs entries (e, p) in the camera's
         // point order (a camera's free-point edges: rcount)
-        std::vector<int> pcount(npairs, 0), rcount(npairs, 0);
+        auto &pcount = ws.pcount, &rcount = ws.rcount;
+        pcount.assign(npairs, 0);
+        rcount.assign(npairs, 0);
         for (int pi = 0; pi < npairs; pi++) pcount[pi] = kcount[(size_t)pairs[pi].x * nb + pairs[pi].y];
-        std::vector<int> rblk(std::max(nb, 1), 0);
-        for (int h = 0; h < nb; h++) {
-            const int c = cam_of_block[h];
-            int cnt = 0;
-            for (int a = cstart[c]; a < cstart[c + 1]; a++) cnt += ptfree[cpt[a]];
-            rcount[pairidx[(size_t)h * nb + h]] = cnt;
-        }
-        std::vector<long long> pbeg(npairs + 1, 0);
+        auto& rblk = ws.rblk;
+        rblk.assign(std::max(nb, 1), 0);
+        for (int h = 0; h < nb; h++) rcount[pairidx[(size_t)h * nb + h]] = h_rc[h];
+        auto& pbeg = ws.pbeg;
+        pbeg.assign(npairs + 1, 0);
         for (int pi = 0; pi < npairs; pi++) pbeg[pi + 1] = pbeg[pi] + pcount[pi] + rcount[pi];
         MAGE_REQUIRE(pbeg[npairs] < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
         {
             // destinations: sorted product i of pair key k goes to pbeg[pair] + (i - kstart[k]);
             // camera block h's rhs entries start at pbeg[diag pair] + pcount
-            std::vector<int> kdst(nk, 0);
+            auto& kdst = ws.kdst;
+            kdst.assign(nk, 0);
             for (int pi = 0; pi < npairs; pi++) {
                 const int k = pairs[pi].x * nb + pairs[pi].y;
                 kdst[k] = (int)(pbeg[pi] - kstart[k]);
@@ -2309,17 +2685,17 @@ struct BundleAdjuster {
                 const int pi = pairidx[(size_t)h * nb + h];
                 rblk[h] = (int)(pbeg[pi] + pcount[pi]);
             }
+            // + the padding entry after the last list (cleared with the other buffers below)
             if ((r = d_sentries.reserve(((size_t)pbeg[npairs] + 1) * sizeof(int2))) != MAGE_OK) return r;
-            // the padding entry after the last list (schur_chunks reads one past a chunk's end)
-            MAGE_HIP(hipMemsetAsync(d_sentries.as<int2>() + pbeg[npairs], 0, sizeof(int2), st));
             if (bitmaps)  // sc_pair_fill: a pair's first product slot (-1: no products)
                 for (int k = 0; k < nk; k++) kdst[k] = kcount[k] > 0 ? kdst[k] + kstart[k] : -1;
             if ((r = upload(d_kdst, kdst)) != MAGE_OK) return r;
             if ((r = upload(d_rblk, rblk)) != MAGE_OK) return r;
+            flush_uploads();
             if (bitmaps) {
                 uint32_t* A = d_sbits.as<uint32_t>();
                 launch("ba.schur_fill", sc_pair_fill, dim3(nb, nb), dim3(64), 0, st, nb, PW, (const uint32_t*)A,
-                       (const int*)d_srank.as<int>(), (const uint32_t*)(A + (size_t)nb * PW), (const int*)d_camblk.as<int>(),
+                       (const int*)d_srank.as<int>(), (const uint32_t*)(A + (size_t)nbm * PW), (const int*)d_camblk.as<int>(),
                        (const int*)d_cstart.as<int>(), (const int*)d_kdst.as<int>(), d_sentries.as<int2>());
             }
             if (nprod_max > 0)
@@ -2336,10 +2712,13 @@ struct BundleAdjuster {
         pt.mark("list scatter");
         // chunks; the block rows of S split into 8 contiguous groups of about equal work, one per
         // XCD (block b runs on XCD b % 8)
-        std::vector<SchurPair> spairs(npairs);
-        std::vector<std::vector<SchurChunk>> xcd_chunks(8);
+        auto& spairs = ws.spairs;
+        spairs.assign(npairs, SchurPair{});
+        auto& xcd_chunks = ws.xcd_chunks;
+        for (auto& v : xcd_chunks) v.clear();
         {
-            std::vector<long long> roww(std::max(nb, 1), 0);
+            auto& roww = ws.roww;
+            roww.assign(std::max(nb, 1), 0);
             for (int pi = 0; pi < npairs; pi++) roww[pairs[pi].x] += pbeg[pi + 1] - pbeg[pi] + SC_CHUNK / 4;
             long long tot = 0;
             for (long long w : roww) tot += w;
@@ -2389,7 +2768,8 @@ struct BundleAdjuster {
         }
         size_t L = 0;
         for (auto& v : xcd_chunks) L = std::max(L, v.size());
-        std::vector<SchurChunk> schunks(8 * L);
+        auto& schunks = ws.schunks;
+        schunks.resize(8 * L);
         for (size_t j = 0; j < L; j++)
             for (int x = 0; x < 8; x++) {
                 SchurChunk ch{};
@@ -2397,25 +2777,16 @@ struct BundleAdjuster {
                 schunks[8 * j + x] = j < xcd_chunks[x].size() ? xcd_chunks[x][j] : ch;
             }
         n_sblocks = (int)schunks.size();
-        std::vector<int> sfinish;  // pairs finished by schur_finish: diagonal or more than one chunk
+        auto& sfinish = ws.sfinish;  // pairs finished by schur_finish: diagonal or more than one chunk
+        sfinish.clear();
         for (int pi = 0; pi < npairs; pi++)
             if (spairs[pi].nslots > 1 || spairs[pi].h1 == spairs[pi].h2) sfinish.push_back(pi);
         n_sfinish = (int)sfinish.size();
         MAGE_REQUIRE(pbeg[npairs] < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
         pt.mark("chunks");
-        n_entries = pstart[P];
         if ((r = upload(d_sfinish, sfinish)) != MAGE_OK) return r;
         if ((r = upload(d_spairs, spairs)) != MAGE_OK) return r;
         if ((r = upload(d_schunks, schunks)) != MAGE_OK) return r;
-        {
-            std::vector<int> ptcnt(P);
-            for (int i = 0; i < P; i++) ptcnt[i] = pstart[i + 1] - pstart[i];
-            if ((r = upload(d_ptcnt, ptcnt)) != MAGE_OK) return r;
-            camcnt.assign(C, 0);
-            for (int c = 0; c < C; c++) camcnt[c] = cstart[c + 1] - cstart[c];
-        }
-        if ((r = upload(d_active, active)) != MAGE_OK) return r;
-        if ((r = upload(d_cedges, cedges)) != MAGE_OK) return r;
         if ((r = upload(d_ptlist, ptlist)) != MAGE_OK) return r;
         for (auto& T : teth) {
             T.h1 = camh[T.c1];
@@ -2433,7 +2804,7 @@ struct BundleAdjuster {
             cur = 0;
             state_on_device = true;
         }
-        const size_t Pm = std::max(P, 1), Cm = std::max(C, 1), Em = std::max(E, 1);
+        flush_uploads();
         const size_t npm = std::max(np, 16);
         for (auto pr : {std::make_pair(&d_err, Em * 2 * 8), std::make_pair(&d_Hll, Pm * 9 * 8),
                         std::make_pair(&d_bl, Pm * 3 * 8), std::make_pair(&d_Hpl, (size_t)std::max(n_entries, 1) * EQ_N * 8),
@@ -2450,16 +2821,30 @@ struct BundleAdjuster {
             if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
         if ((r = d_livebuf.reserve(sizeof(LiveCtl))) != MAGE_OK) return r;
         if ((r = h_olist.reserve(Em * 2 * 4 + 16)) != MAGE_OK) return r;
-        MAGE_HIP(hipMemsetAsync(d_livebuf.ptr, 0, sizeof(LiveCtl), st));
-        MAGE_HIP(hipMemsetAsync(d_maxd.ptr, 0, (Pm + Cm) * 8, st));
-        MAGE_HIP(hipMemsetAsync(d_scale.ptr, 0, (Pm + Cm) * 8, st));
-        // chol_tiles reads S without writing it and every trial rewrites the same covisible pair
-        // blocks, so the zero blocks are set once here (cholesky_solve factors in place: per trial)
-        MAGE_HIP(hipMemsetAsync(d_S.ptr, 0, npm * npm * 8, st));
+        // one launch clears: the live counters, the max-diagonal / scale partials, S (chol_tiles
+        // reads S without writing it and every trial rewrites the same covisible pair blocks, so
+        // the zero blocks are set once here; cholesky_solve factors in place: per trial), the
+        // padding entry after the last product list (schur_chunks reads one past a chunk's end),
+        // and on first use the per-edge errors
+        ClearList cl{};
+        auto add = [&](void* ptr, size_t bytes) {
+            cl.p[cl.k] = static_cast<uint32_t*>(ptr);
+            cl.n[cl.k++] = (unsigned)(bytes / 4);
+        };
+        static_assert(sizeof(LiveCtl) % 4 == 0, "LiveCtl is cleared as words");
+        add(d_livebuf.ptr, sizeof(LiveCtl));
+        add(d_maxd.ptr, (Pm + Cm) * 8);
+        add(d_scale.ptr, (Pm + Cm) * 8);
+        add(d_S.ptr, npm * npm * 8);
+        add(d_sentries.as<int2>() + pbeg[npairs], sizeof(int2));
         if (!err_initialized) {
-            MAGE_HIP(hipMemsetAsync(d_err.ptr, 0, Em * 2 * 8, st));
+            add(d_err.ptr, Em * 2 * 8);
             err_initialized = true;
         }
+        size_t words = 0;
+        for (int k = 0; k < cl.k; k++) words = std::max<size_t>(words, cl.n[k]);
+        launch("ba.init_clear", clear_words, dim3((unsigned)std::min<size_t>(1024, (words + 255) / 256)), dim3(256), 0,
+               st, cl);
         pt.mark("buffers");
         iteration = 0;
         dirty = false;
@@ -2662,6 +3047,8 @@ struct BundleAdjuster {
     {
         mage_status r;
         MAGE_HIP(hipSetDevice(device));
+        flush_uploads();  // setters' queued copies (camera intrinsics)
+        PhaseTimer spt;
         float prior = -1.f;
         // The outlier pass of the final state runs speculatively with the last step's trials
         // (launched before their synchronisation): when the last trial is accepted its result is
@@ -2677,6 +3064,7 @@ struct BundleAdjuster {
             if ((r = step_once(&ok, s + 1 == nsteps, &spec_valid)) != MAGE_OK) return r;
             if (!ok) break;
         }
+        spt.mark("step: LM (incl. initialize)");
         if (dirty) {
             spec_valid = -1;
             if ((r = initialize()) != MAGE_OK) return r;
@@ -2706,10 +3094,9 @@ struct BundleAdjuster {
             std::vector<uint32_t> list(h_list, h_list + no);
             launch("ba.drop_edges", drop_edges, dim3((no + BA_THREADS - 1) / BA_THREADS), dim3(BA_THREADS), 0, st,
                    (const int*)d_ept.as<int>(), (const uint32_t*)(h_olist.device<uint32_t>() + (size_t)k * E), no,
-                   d_active.as<unsigned char>(), d_ptcnt.as<int>(), d_ptfree.as<int>());
+                   d_active.as<unsigned char>(), d_removed.as<unsigned char>(), d_ptcnt.as<int>(), d_ptfree.as<int>());
             std::sort(list.begin(), list.end());  // g2o active-edge order = insertion order
             for (uint32_t k = 0; k < no; k++) {
-                removed[list[k]] = 1;
                 camcnt[ecam[list[k]]]--;
                 if (k < cap) outliers[k] = list[k];
             }
@@ -2720,6 +3107,7 @@ struct BundleAdjuster {
         }
         *nOut = std::min(no, cap);
         *meanSq = (float)(h[0] / h[1]);
+        spt.mark("step: outliers");
         // Eager linearisation for the caller's usual next call (BundleAdjust.cpp:311-318: the same
         // huber width, no setter in between): it runs while control is with the caller, and
         // lm_solve reuses it only when the huber width, lambda and state still match.
@@ -2740,6 +3128,7 @@ struct BundleAdjuster {
             eager_lambda = init ? 0.0 : lam;
             eager_cur = cur;
         }
+        spt.mark("step: export + eager");
         return no > cap ? MAGE_ECAPACITY : MAGE_OK;
     }
 };
@@ -2785,6 +3174,7 @@ mage_status mage_ba_destroy(mage_ba* ba)
 mage_status mage_ba_set_cameras(mage_ba* b, uint32_t n, const float* pos3, const float* r9, const float* intr4,
                                 const uint8_t* fixed)
 {
+    mage::BundleAdjuster::ScopeTimer timer_("call " "set_cameras");
     MAGE_REQUIRE(b && (n == 0 || (pos3 && r9 && intr4)), MAGE_EINVAL, "null argument");
     MAGE_REQUIRE(!b->state_on_device || (int)n == b->C, MAGE_EINVAL, "cameras can only be allocated once");
     b->C = (int)n;
@@ -2849,6 +3239,7 @@ mage_status mage_ba_fix_camera(mage_ba* b, uint32_t idx, int32_t fixed)
 
 mage_status mage_ba_set_points(mage_ba* b, uint32_t n, const float* xyz)
 {
+    mage::BundleAdjuster::ScopeTimer timer_("call " "set_points");
     MAGE_REQUIRE(b && (n == 0 || xyz), MAGE_EINVAL, "null argument");
     mage_status r = b->sync_host_state();
     if (r != MAGE_OK) return r;
@@ -2863,31 +3254,30 @@ mage_status mage_ba_set_points(mage_ba* b, uint32_t n, const float* xyz)
 mage_status mage_ba_set_observations(mage_ba* b, uint32_t n, const float* uv, const uint32_t* cam,
                                      const uint32_t* pt, const float* info)
 {
+    mage::BundleAdjuster::ScopeTimer timer_("call " "set_observations");
     MAGE_REQUIRE(b && (n == 0 || (uv && cam && pt && info)), MAGE_EINVAL, "null argument");
-    for (uint32_t i = 0; i < n; i++)
-        MAGE_REQUIRE((int)cam[i] < b->C && (int)pt[i] < b->P, MAGE_EINVAL, "observation index out of range");
-    b->E = (int)n;
-    b->uv.assign(2 * n, 0);
-    b->info.assign(n, 0);
-    b->ecam.assign(n, 0);
-    b->ept.assign(n, 0);
-    b->removed.assign(n, 0);
+    uint32_t cmax = 0, pmax = 0;
     for (uint32_t i = 0; i < n; i++) {
-        b->uv[2 * i] = uv[2 * i];
-        b->uv[2 * i + 1] = uv[2 * i + 1];
-        b->ecam[i] = (int)cam[i];
-        b->ept[i] = (int)pt[i];
-        b->info[i] = info[i];
+        cmax = std::max(cmax, cam[i]);
+        pmax = std::max(pmax, pt[i]);
     }
+    MAGE_REQUIRE(n == 0 || (cmax < (uint32_t)b->C && pmax < (uint32_t)b->P), MAGE_EINVAL,
+                 "observation index out of range");
+    b->E = (int)n;
+    b->ecam.assign(cam, cam + n);
     b->dirty = true;
     (void)hipSetDevice(b->device);
+    // the measurements stay float on the device (exact in the kernels' double arithmetic, as the
+    // reference's Vector2d(float) measurement); the removal flags start clear
     mage_status r;
-    if ((r = b->upload(b->d_uv, b->uv)) != MAGE_OK) return r;
-    if ((r = b->upload(b->d_info, b->info)) != MAGE_OK) return r;
-    if ((r = b->upload(b->d_ecam, b->ecam)) != MAGE_OK) return r;
-    return b->upload(b->d_ept, b->ept);
+    if ((r = b->upload(b->d_uv, uv, 2 * (size_t)n)) != MAGE_OK) return r;
+    if ((r = b->upload(b->d_info, info, n)) != MAGE_OK) return r;
+    if ((r = b->upload(b->d_ecam, reinterpret_cast<const int*>(cam), n)) != MAGE_OK) return r;
+    if ((r = b->upload(b->d_ept, reinterpret_cast<const int*>(pt), n)) != MAGE_OK) return r;
+    if ((r = b->d_removed.reserve(std::max<size_t>(n, 16))) != MAGE_OK) return r;
+    MAGE_HIP(hipMemsetAsync(b->d_removed.ptr, 0, n, b->st));
+    return MAGE_OK;
 }
-
 mage_status mage_ba_set_lambda(mage_ba* b, float lambda)
 {
     MAGE_REQUIRE(b, MAGE_EINVAL, "null handle");
@@ -2956,6 +3346,7 @@ mage_status mage_ba_set_tethers(mage_ba* b, uint32_t kind, uint32_t n, const uin
 mage_status mage_ba_step(mage_ba* b, const float* huber, uint32_t nsteps, float max_error_square, uint32_t* outliers,
                          uint32_t cap, uint32_t* n_out, float* mean_sq)
 {
+    mage::BundleAdjuster::ScopeTimer timer_("call " "step");
     MAGE_REQUIRE(b && n_out && mean_sq && (nsteps == 0 || huber) && (cap == 0 || outliers), MAGE_EINVAL,
                  "null argument");
     for (uint32_t s = 0; s < nsteps; s++) MAGE_REQUIRE(huber[s] >= 0.f, MAGE_EINVAL, "Huber widths must be nonnegative");
@@ -2964,6 +3355,7 @@ mage_status mage_ba_step(mage_ba* b, const float* huber, uint32_t nsteps, float 
 
 mage_status mage_ba_get_poses(mage_ba* b, float* pos3, float* r9)
 {
+    mage::BundleAdjuster::ScopeTimer timer_("call " "get_poses");
     MAGE_REQUIRE(b && pos3 && r9, MAGE_EINVAL, "null argument");
     (void)hipSetDevice(b->device);
     b->export_wanted = true;  // GetPose / GetPoint between steps: keep the mapped mirror current
@@ -2989,6 +3381,7 @@ mage_status mage_ba_get_poses(mage_ba* b, float* pos3, float* r9)
 
 mage_status mage_ba_get_points(mage_ba* b, float* xyz)
 {
+    mage::BundleAdjuster::ScopeTimer timer_("call " "get_points");
     MAGE_REQUIRE(b && xyz, MAGE_EINVAL, "null argument");
     (void)hipSetDevice(b->device);
     b->export_wanted = true;  // GetPose / GetPoint between steps: keep the mapped mirror current

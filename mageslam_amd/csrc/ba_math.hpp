@@ -277,10 +277,10 @@ struct Problem {
     const double* camk;           // C x 3: f, cx, cy
     const int* camh;              // C: Hessian block index or -1
     const int* ptfree;            // P: 1 if the point is in the system
-    const double* uv;             // E x 2
+    const float* uv;              // E x 2 (the caller's float measurements)
     const int* ecam;              // E
     const int* ept;               // E
-    const double* info;           // E
+    const float* info;            // E
     const unsigned char* active;  // E: edge in the optimizer's active set
     const int* pstart;            // P+1
     const int* pedges;            // edges by point (edge order), filtered by `active`
