@@ -1065,34 +1065,34 @@ __global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict_
 }
 
 // Register-resident tiled Cholesky + solve for np <= 240 (the usual local-BA window: 40 free
-// keyframes -> n = 240; larger systems use cholesky_solve).  S = U^T U in upper form: the upper 16x16 tiles (i <= j) of S live in
-// the f64 MFMA accumulator layout of 8 waves (tile t = row-major upper index, wave t % 8, slot
-// t / 8; lane l holds rows (l >> 4) + 4r, column l & 15).  Every product then sums over a
-// tile's row index, which is exactly the B operand of v_mfma_f64_16x16x4f64 taken from those
-// registers (k-step q = register q):
+// keyframes -> n = 240; larger systems use cholesky_solve).  S = U^T U in upper form: the upper
+// 16x16 tiles (i <= j) of S live in the f64 MFMA accumulator layout of 15 tile waves (slots from
+// the host's chol_tile_table; lane l holds rows (l >> 4) + 4r, column l & 15) next to one factor
+// wave that holds no tile.  Every product sums over a tile's row index, which is exactly the B
+// operand of v_mfma_f64_16x16x4f64 taken from those registers (k-step q = register q):
 //   TRSM  U_kj = inv(L_kk) A_kj            (A operand inv(L_kk) from LDS; L = U^T)
 //   SYRK  A_ij -= U_ki^T U_kj, k < i <= j  (both operands from the LDS panel of row-block k)
-// Step k: TRSM of row-block k into the double-buffered panel -> barrier -> SYRK, in which the
-// owner of tile (k+1, k+1) updates that tile first and hands it (LDS + flag) to the factor wave,
-// which factors it (Cholesky + triangular inverse + forward substitution in one column loop)
-// while the tile waves finish their SYRKs -> barrier.  (With the owner factoring its own tile,
-// its remaining SYRKs queued behind the ~3.4k-cycle column loop: the owner finished its phase
-// ~5k cycles after every other wave, every step.)  Nothing of S leaves the chip between steps;
-// the solves use the per-block inverses kept in LDS.
+// Step k (tile waves): TRSM of row-block k into the double-buffered panel — the owner of (k, k+1)
+// also owns (k+1, k+1): it solves (k, k+1) first, applies that tile's update to (k+1, k+1) and
+// hands A_{k+1,k+1} to the factor wave (LDS + flag) — then the tile waves' own barrier (an LDS
+// counter), the SYRKs, and the workgroup barrier.  The factor wave factors block k+1 (Cholesky +
+// triangular inverse + forward substitution in one column loop) as soon as it is handed over,
+// concurrently with the TRSM and SYRK phases, and meets the tile waves only at the end of the step.
+// Factor wave and tile waves run separate code paths, so the factor's registers never add to the
+// resident tiles'.  Measured at n = 240 (tools/ablate_ba.py): 95 us with 8 waves and the factor
+// after the SYRK barrier, 74 us now (16 waves, 4 per SIMD).  Nothing of S leaves the chip between
+// steps; the solves use the per-block inverses kept in LDS.
 #ifndef MAGE_CHOL_ABLATE  // timing experiments only (tools/ablate_ba.py); 0 in the product
 #define MAGE_CHOL_ABLATE 0
 #endif
-#ifndef MAGE_CHOL_SYRK2
-#define MAGE_CHOL_SYRK2 0  // 1: the SYRK phase over slot pairs (two MFMA chains per basic block)
+#ifndef MAGE_CHOL_WAVES
+#define MAGE_CHOL_WAVES 16
 #endif
-#ifndef MAGE_CHOL_FW
-#define MAGE_CHOL_FW 1  // 1: a dedicated factor wave (no tiles); 0: the next diagonal tile's owner factors it
-#endif
-constexpr int CT_WAVES = 8;   // 2 per SIMD: 256 VGPRs hold 18 resident tiles + the block factor
+constexpr int CT_WAVES = MAGE_CHOL_WAVES;  // 16: 4 per SIMD (15 tile waves x 8 resident tiles + the factor wave)
 constexpr int CT_THREADS = CT_WAVES * kWave;
-constexpr int CT_TW = MAGE_CHOL_FW ? CT_WAVES - 1 : CT_WAVES;  // tile waves (wave CT_TW: the factor wave)
-constexpr int CT_TPW = MAGE_CHOL_FW ? 18 : 15;  // tiles per tile wave: 7 x 18 (8 x 15) >= 120 upper tiles of np = 240
+constexpr int CT_TW = CT_WAVES - 1;  // tile waves (wave CT_TW: the factor wave, which holds no tile)
 constexpr int CT_MAXT = 15;
+constexpr int CT_TPW = (CT_MAXT * (CT_MAXT + 1) / 2 + CT_TW - 1) / CT_TW;  // tiles per tile wave: 7 x 18 >= 120 upper tiles of np = 240
 static_assert(CT_TW * CT_TPW >= CT_MAXT * (CT_MAXT + 1) / 2, "every upper tile has a slot");
 
 // Broadcast of lane l's double (two v_readlane_b32: scalar result, no LDS crossbar).
@@ -1129,7 +1129,7 @@ __device__ __forceinline__ int upper_tile_index(int i, int j, int mt) { return i
 
 __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restrict__ S, int np, int n,
                                                          const double* __restrict__ b, double* __restrict__ x,
-                                                         int* __restrict__ fail)
+                                                         int* __restrict__ fail, const uint16_t* __restrict__ tab)
 {
     // inverse of L_kk = U_kk^T per diagonal block, column-major: invT[k][c][m] = inv(L_kk)[m][c]
     // (the factor writes a column with 16-byte stores; 18-double rows keep them aligned and the
@@ -1139,49 +1139,26 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     __shared__ __attribute__((aligned(16))) double dsc[16][18];  // the factor's scratch: A_kk transposed
     __shared__ __attribute__((aligned(16))) double vb[CT_MAXT * 16];  // b -> y -> x
     __shared__ int s_fail;
-    __shared__ int s_diag_ready;  // index of the diagonal block staged in dsc for the factor wave
+    __shared__ int s_diag_ready;      // index of the diagonal block staged in dsc for the factor wave
+    __shared__ unsigned s_tile_bar;   // the tile waves' barrier count (CT_TW per step)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: tile bookkeeping on the SALU
     const int mt = np >> 4, T = mt * (mt + 1) / 2;
     const int lr = lane >> 4, lc = lane & 15;  // accumulator layout: rows lr + 4r, column lc
 
-    // tile coordinates of each slot (wave uniform, scalar registers)
+    // tile coordinates of each slot (wave uniform, scalar registers), from the host's table
+    // (chol_tile_table: tiles (d-1, d) and (d, d) share an owner)
     int tIJ[CT_TPW];  // ti | tj << 8, one scalar register per slot
-    {
-        int i = 0, rowend = mt;  // tiles [rowend - (mt - i), rowend) are row i
-        for (int sl = 0; sl < CT_TPW; sl++) {
-            const int t = wave < CT_TW ? wave + CT_TW * sl : T;  // the factor wave holds no tile
-            while (i < mt && t >= rowend) {
-                i++;
-                rowend += mt - i;
-            }
-            tIJ[sl] = t < T ? i | (i + (t - (rowend - (mt - i)))) << 8 : mt | mt << 8;  // mt: no tile
-        }
+#pragma unroll
+    for (int sl = 0; sl < CT_TPW; sl++) {
+        const int v = wave < CT_TW ? (int)tab[wave * CT_TPW + sl] : 0xFFFF;  // the factor wave holds no tile
+        tIJ[sl] = v == 0xFFFF ? (mt | mt << 8) : v;                           // mt: no tile
     }
+    (void)T;
     auto tile_of = [&](int sl, int& ti, int& tj) {
         ti = tIJ[sl] & 0xFF;
         tj = tIJ[sl] >> 8;
     };
-    dbl4 C[CT_TPW];
-#pragma unroll
-    for (int sl = 0; sl < CT_TPW; sl++) {
-        int ti, tj;
-        tile_of(sl, ti, tj);
-        if (ti < mt) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = 16 * ti + lr + 4 * r, col = 16 * tj + lc;
-                C[sl][r] = (row < n && col < n) ? S[(long long)row * np + col] : (row == col ? 1.0 : 0.0);
-            }
-        } else {
-            C[sl] = dbl4{0, 0, 0, 0};
-        }
-    }
-    if (tid == 0) {
-        s_fail = 0;
-        s_diag_ready = -1;
-    }
-    for (int i = tid; i < np; i += CT_THREADS) vb[i] = i < n ? b[i] : 0.0;
     long long tm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0;  // MAGE_CHOL_ABLATE == 3: phase cycles of wave 0
     auto tick = [&](int ph) {
         if (MAGE_CHOL_ABLATE == 3) {
@@ -1190,7 +1167,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             t0 = t;
         }
     };
-    tick(-1);
 #if MAGE_CHOL_ABLATE == 4  // per-step timestamps of every wave (rel. to the first barrier)
     __shared__ long long ttr[CT_MAXT][CT_WAVES][4];
     long long tbase = 0;
@@ -1203,21 +1179,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     do {                \
     } while (0)
 #endif
-    __syncthreads();
-#if MAGE_CHOL_ABLATE == 4
-    tbase = __builtin_amdgcn_s_memtime();
-#endif
-    tick(0);
-
-    // --- diagonal block: Cholesky of A_kk and inv(L_kk) by its owner wave (slot `slot`); A_kk
-    // goes through dsc transposed, so each lane reads its row with 16-byte loads ---
-    auto stage_diag = [&](int slot) {  // the owner's tile (k, k) -> dsc, transposed
-#pragma unroll
-        for (int sl = 0; sl < CT_TPW; sl++)
-            if (sl == slot)
-#pragma unroll
-                for (int r = 0; r < 4; r++) dsc[lc][lr + 4 * r] = C[sl][r];
-    };
+    // --- the 16x16 diagonal block factor (the factor wave), from dsc ---
     auto factor_diag = [&](int k) {  // from dsc
         const int l = lane;
         if (MAGE_CHOL_ABLATE == 2) {
@@ -1237,23 +1199,21 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             double v[16];
             const double* vbk = &vb[16 * k];
             const int c = l - 16;
-            // unconditional 16-byte loads (one batch, one wait), then per-lane selects
-            double dq[16], bq[16];
+            // one batch of unconditional 16-byte loads from a per-lane source (row l of A for
+            // lanes 0-15, vb_k for the others), then per-lane selects
+            double dq[16];
             {
-                const double2* dr = reinterpret_cast<const double2*>(&dsc[l & 15][0]);
-                const double2* br = reinterpret_cast<const double2*>(vbk);
+                const double2* dr = reinterpret_cast<const double2*>(l < 16 ? &dsc[l][0] : vbk);
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
-                    const double2 d2 = dr[q], b2 = br[q];
+                    const double2 d2 = dr[q];
                     dq[2 * q] = d2.x;
                     dq[2 * q + 1] = d2.y;
-                    bq[2 * q] = b2.x;
-                    bq[2 * q + 1] = b2.y;
                 }
             }
 #pragma unroll
             for (int q = 0; q < 16; q++)
-                v[q] = l < 16 ? (q <= l ? dq[q] : 0.0) : (l < 32 ? (q == c ? 1.0 : 0.0) : (l == 32 ? bq[q] : 0.0));
+                v[q] = l < 16 ? (q <= l ? dq[q] : 0.0) : (l < 32 ? (q == c ? 1.0 : 0.0) : (l == 32 ? dq[q] : 0.0));
             bool bad = false;
             if (k == 0) tick(6);
 #pragma unroll
@@ -1289,138 +1249,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             }
         }
     };
-    if (mt > 0 && wave == 0) {  // tile (0, 0) is tile 0: wave 0, slot 0
-        stage_diag(0);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (!MAGE_CHOL_FW) factor_diag(0);
-    }
-    if (MAGE_CHOL_FW) {
-        __syncthreads();  // dsc holds A_00
-        if (mt > 0 && wave == CT_TW) factor_diag(0);
-    }
-    tick(1);
-    __syncthreads();
-    tick(2);
-
-    // Step k: TRSM of row-block k -> barrier -> SYRK, during which the owner of tile (k+1, k+1)
-    // updates that tile first and factors it (look-ahead: the serial block factor overlaps the
-    // other waves' SYRK) -> barrier.
-    for (int k = 0; k < mt; k++) {
-        const int buf = k & 1;
-        if (s_fail) break;
-        // --- TRSM: U_kj = inv(L_kk) A_kj for the owned tiles of row-block k ---
-#pragma unroll
-        for (int sl = 0; sl < CT_TPW; sl++) {
-            int ti, tj;
-            tile_of(sl, ti, tj);
-            if (ti == k && tj > k) {
-                dbl4 acc = {0, 0, 0, 0};
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(invT[k][4 * q + lr][lc], C[sl][q], acc, 0, 0, 0);
-                C[sl] = acc;
-#pragma unroll
-                for (int r = 0; r < 4; r++) pan[buf][tj][lr + 4 * r][lc] = acc[r];
-                // forward substitution: vb_j -= U_kj^T y_k (tile (k, j) is the only writer of vb_j
-                // in this step)
-                double pacc = 0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) pacc = __builtin_fma(acc[r], vb[16 * k + lr + 4 * r], pacc);
-                pacc += __shfl_xor(pacc, 16);
-                pacc += __shfl_xor(pacc, 32);
-                if (lr == 0) vb[16 * tj + lc] -= pacc;
-            }
-        }
-        tick(3);
-        CT_STAMP(k, 0);
-        __syncthreads();
-        CT_STAMP(k, 1);
-        tick(2);
-        // --- SYRK: A_ij -= U_ki^T U_kj for the owned tiles with k < i <= j ---
-        auto syrk = [&](int sl) {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pan[buf][tIJ[sl] & 0xFF][4 * q + lr][lc], pan[buf][tIJ[sl] >> 8][4 * q + lr][lc],
-                                                            C[sl], 0, 0, 0);
-        };
-        const int kn = k + 1, tnn = upper_tile_index(kn, kn, mt);
-        if (kn < mt && wave == tnn % CT_TW) {
-            const int slot = tnn / CT_TW;
-            if (MAGE_CHOL_FW) __builtin_amdgcn_s_setprio(2);  // the critical chain first on this SIMD
-#pragma unroll
-            for (int sl = 0; sl < CT_TPW; sl++)
-                if (sl == slot) syrk(sl);
-            tick(4);
-            stage_diag(slot);
-            if (MAGE_CHOL_FW) {
-                // hand A_{k+1,k+1} to the factor wave: the fence drains the staging stores before
-                // the flag store
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0) __hip_atomic_store(&s_diag_ready, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __builtin_amdgcn_s_setprio(0);
-            } else {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                factor_diag(kn);
-            }
-            tick(1);
-        }
-        if (MAGE_CHOL_FW && kn < mt && wave == CT_TW) {
-            // the owner reaches its SYRK phase without waiting on this wave, so the spin ends
-            while (__hip_atomic_load(&s_diag_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != kn)
-                __builtin_amdgcn_s_sleep(1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            __builtin_amdgcn_s_setprio(3);  // the column loop is the critical chain: issue before the SYRKs
-            factor_diag(kn);
-            __builtin_amdgcn_s_setprio(0);
-        }
-#if MAGE_CHOL_SYRK2
-        // slot pairs in one basic block: two independent MFMA chains the scheduler can interleave
-        auto does = [&](int sl) {
-            const int i = tIJ[sl] & 0xFF, j = tIJ[sl] >> 8;
-            return i > k && i < mt && !(i == kn && j == kn);
-        };
-#pragma unroll
-        for (int sl = 0; sl < CT_TPW; sl += 2) {
-            const bool d0 = does(sl), d1 = sl + 1 < CT_TPW && does(sl + 1);
-            if (d0 && d1) {
-                const int i0 = tIJ[sl] & 0xFF, j0 = tIJ[sl] >> 8;
-                const int i1 = tIJ[sl + 1] & 0xFF, j1 = tIJ[sl + 1] >> 8;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const double a0 = -pan[buf][i0][4 * q + lr][lc], b0 = pan[buf][j0][4 * q + lr][lc];
-                    const double a1 = -pan[buf][i1][4 * q + lr][lc], b1 = pan[buf][j1][4 * q + lr][lc];
-                    C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, C[sl], 0, 0, 0);
-                    C[sl + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, C[sl + 1], 0, 0, 0);
-                }
-            } else {
-                if (d0) syrk(sl);
-                if (d1) syrk(sl + 1);
-            }
-        }
-#else
-#pragma unroll
-        for (int sl = 0; sl < CT_TPW; sl++) {
-            const int i = tIJ[sl] & 0xFF, j = tIJ[sl] >> 8;
-            if (i > k && i < mt && !(i == kn && j == kn)) syrk(sl);
-        }
-#endif
-        tick(4);
-        CT_STAMP(k, 2);
-        __syncthreads();
-        CT_STAMP(k, 3);
-        tick(2);
-    }
-    if (s_fail) {
-        if (tid == 0) *fail = 1;
-        return;
-    }
-    // --- backward: U x = y, x_k = inv(U_kk) (y_k - sum_{j>k} U_kj x_j), right-looking with
-    // one barrier per block: the owner of tile (k-1, k) applies the last update of y_{k-1} and
-    // then solves block k-1 itself ---
     auto solve_block = [&](int k) {  // by one wave: vb_k := inv(U_kk) vb_k, inv(U) = inv(L)^T
         double xv = 0;
         if (lane < 16) {
@@ -1436,6 +1264,179 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         __builtin_amdgcn_wave_barrier();
         if (lane < 16) vb[16 * k + lane] = xv;
     };
+    if (wave == CT_TW) {
+        // ===== the factor wave: it holds no tile, so none of the tile registers are live here =====
+        // block 0 from S directly while the tile waves load their tiles (A_00 goes to dsc
+        // transposed, as stage_diag writes it)
+        if (lane == 0) {
+            s_fail = 0;
+            s_diag_ready = -1;
+            s_tile_bar = 0;
+        }
+        if (mt > 0) {
+            if (lane < 16) {
+#pragma unroll
+                for (int q = 0; q < 16; q++)
+                    dsc[lane][q] = (q < n && lane < n) ? S[(long long)q * np + lane] : (q == lane ? 1.0 : 0.0);
+                vb[lane] = lane < n ? b[lane] : 0.0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            factor_diag(0);
+        }
+        __syncthreads();  // tiles loaded, block 0 factored
+#if MAGE_CHOL_ABLATE == 4
+        tbase = __builtin_amdgcn_s_memtime();
+#endif
+        for (int k = 0; k < mt; k++) {
+            if (s_fail) break;
+            const int kn = k + 1;
+            // block k+1 as soon as its owner has staged it (during the TRSM phase), concurrently
+            // with the tile waves' TRSMs and SYRKs
+            if (kn < mt) {
+                while (__hip_atomic_load(&s_diag_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != kn)
+                    __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                CT_STAMP(k, 0);
+                __builtin_amdgcn_s_setprio(3);  // the column loop is the critical chain
+                factor_diag(kn);
+                __builtin_amdgcn_s_setprio(0);
+                CT_STAMP(k, 1);
+            }
+            CT_STAMP(k, 2);
+            __syncthreads();  // end of step k
+            CT_STAMP(k, 3);
+        }
+        if (s_fail) return;
+        for (int k = 0; k < (mt > 0 ? mt : 1); k++) __syncthreads();  // the backward solve's barriers
+        return;
+    }
+
+    // ===== the tile waves =====
+    dbl4 C[CT_TPW];
+    auto stage_diag = [&](int slot) {  // the owner's tile (k, k) -> dsc, transposed
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++)
+            if (sl == slot)
+#pragma unroll
+                for (int r = 0; r < 4; r++) dsc[lc][lr + 4 * r] = C[sl][r];
+    };
+    tick(-1);
+#pragma unroll
+    for (int sl = 0; sl < CT_TPW; sl++) {
+        int ti, tj;
+        tile_of(sl, ti, tj);
+        if (ti < mt) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = 16 * ti + lr + 4 * r, col = 16 * tj + lc;
+                C[sl][r] = (row < n && col < n) ? S[(long long)row * np + col] : (row == col ? 1.0 : 0.0);
+            }
+        } else {
+            C[sl] = dbl4{0, 0, 0, 0};
+        }
+    }
+    // b -> vb (block 0's entries are the factor wave's: it turns them into y_0)
+    constexpr int TT = CT_TW * kWave;  // tile-wave threads
+    for (int i = 16 + tid; i < np; i += TT) vb[i] = i < n ? b[i] : 0.0;
+    __syncthreads();  // tiles loaded, block 0 factored
+#if MAGE_CHOL_ABLATE == 4
+    tbase = __builtin_amdgcn_s_memtime();
+#endif
+    tick(0);
+    for (int k = 0; k < mt; k++) {
+        const int buf = k & 1;
+        if (s_fail) break;
+        const int kn = k + 1;
+        // --- TRSM: U_kj = inv(L_kk) A_kj for the owned tiles of row-block k.  The owner of
+        // tile (k, k+1) also owns (k+1, k+1) (chol_tile_table): it solves (k, k+1) first,
+        // applies that tile's update to (k+1, k+1) — the last one it needs — and hands
+        // A_{k+1,k+1} to the factor wave (LDS + flag) ---
+        auto trsm = [&](int sl) {
+            const int tj = tIJ[sl] >> 8;
+            dbl4 acc = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(invT[k][4 * q + lr][lc], C[sl][q], acc, 0, 0, 0);
+            C[sl] = acc;
+#pragma unroll
+            for (int r = 0; r < 4; r++) pan[buf][tj][lr + 4 * r][lc] = acc[r];
+            // forward substitution: vb_j -= U_kj^T y_k (tile (k, j) is the only writer of
+            // vb_j in this step)
+            double pacc = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++) pacc = __builtin_fma(acc[r], vb[16 * k + lr + 4 * r], pacc);
+            pacc += __shfl_xor(pacc, 16);
+            pacc += __shfl_xor(pacc, 32);
+            if (lr == 0) vb[16 * tj + lc] -= pacc;
+        };
+        auto syrk = [&](int sl) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                C[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pan[buf][tIJ[sl] & 0xFF][4 * q + lr][lc],
+                                                            pan[buf][tIJ[sl] >> 8][4 * q + lr][lc], C[sl], 0, 0, 0);
+        };
+        const int chain = k | kn << 8, diag = kn | kn << 8;
+        bool owner = false;
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++)
+            if (tIJ[sl] == chain) {
+                owner = true;
+                __builtin_amdgcn_s_setprio(2);  // the critical chain first on this SIMD
+                trsm(sl);
+            }
+        if (owner) {
+            // U_{k,k+1} in pan (read across lanes) and vb_{k+1} final
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int sl = 0; sl < CT_TPW; sl++)
+                if (tIJ[sl] == diag) {
+                    syrk(sl);
+                    stage_diag(sl);
+                }
+            // the fence drains the staging stores (and vb_{k+1}) before the flag store
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&s_diag_ready, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_s_setprio(0);
+        }
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++) {
+            const int ti = tIJ[sl] & 0xFF, tj = tIJ[sl] >> 8;
+            if (ti == k && tj > kn) trsm(sl);
+        }
+        tick(3);
+        CT_STAMP(k, 0);
+        // the tile waves' own barrier (an LDS counter: the factor wave is not held up): pan
+        // row-block k complete
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&s_tile_bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(&s_tile_bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)(CT_TW * kn))
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        CT_STAMP(k, 1);
+        tick(2);
+        // --- SYRK: A_ij -= U_ki^T U_kj for the owned tiles with k < i <= j but (k+1, k+1) ---
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++) {
+            const int i = tIJ[sl] & 0xFF;
+            if (i > k && i < mt && tIJ[sl] != diag) syrk(sl);
+        }
+        tick(4);
+        CT_STAMP(k, 2);
+        __syncthreads();  // block k+1 factored (invT, y_{k+1}), every SYRK of step k done
+        CT_STAMP(k, 3);
+        tick(2);
+    }
+    if (s_fail) {
+        if (tid == 0) *fail = 1;
+        return;
+    }
+    // --- backward: U x = y, x_k = inv(U_kk) (y_k - sum_{j>k} U_kj x_j), right-looking with
+    // one barrier per block: the owner of tile (k-1, k) applies the last update of y_{k-1} and
+    // then solves block k-1 itself ---
     if (mt > 0 && wave == 0) solve_block(mt - 1);
     __syncthreads();
     for (int k = mt - 1; k >= 1; k--) {
@@ -1476,7 +1477,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         }
     }
 #endif
-    for (int i = tid; i < np; i += CT_THREADS) x[i] = i < n ? vb[i] : 0.0;
+    for (int i = tid; i < np; i += TT) x[i] = i < n ? vb[i] : 0.0;
     if (MAGE_CHOL_ABLATE == 3 && tid == 0)
         printf("chol_tiles np=%d cycles: load %lld diag %lld barrier %lld trsm %lld syrk %lld backward %lld | factor0 stage %lld columns %lld\n", np, tm[0],
                tm[1], tm[2], tm[3], tm[4], tm[5], tm[6], tm[7]);
@@ -1762,26 +1763,26 @@ __global__ __launch_bounds__(256) void init_edges(int E, int C, int points_fixed
 }
 
 // Exclusive scan of n values by one 1024-thread workgroup (load(i) / store(i, prefix)); returns the total.
-template <class Load, class Store>
-__device__ int block_scan_1024(int n, Load load, Store store)
+template <class T, class Load, class Store>
+__device__ T block_scan_1024(int n, Load load, Store store)
 {
-    __shared__ int ws[1024 / kWave];
+    __shared__ T ws[1024 / kWave];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-    int carry = 0;
+    T carry = 0;
     for (int base = 0; base < n; base += 1024) {
         const int i = base + tid;
-        const int v = i < n ? load(i) : 0;
-        int inc = v;
+        const T v = i < n ? load(i) : T(0);
+        T inc = v;
         for (int o = 1; o < kWave; o <<= 1) {
-            const int t = __shfl_up(inc, o);
+            const T t = __shfl_up(inc, o);
             if (lane >= o) inc += t;
         }
         if (lane == kWave - 1) ws[w] = inc;
         __syncthreads();
-        int off = 0, tot = 0;
+        T off = 0, tot = 0;
         for (int k = 0; k < 1024 / kWave; k++) {
-            const int sw = ws[k];
-            off += k < w ? sw : 0;
+            const T sw = ws[k];
+            off += k < w ? sw : T(0);
             tot += sw;
         }
         if (i < n) store(i, carry + off + inc - v);
@@ -1805,22 +1806,23 @@ __global__ __launch_bounds__(1024) void init_scan(int C, int P, int nbm, int poi
     int* s_ccnt = sum + INIT_HDR;
     int* s_camblk = s_ccnt + C;
     int* s_rc = s_camblk + C;
-    const int nact = block_scan_1024(
-        P, [&](int i) { return pacc[i]; },
-        [&](int i, int x) {
+    // edges per point (low word) and points in the system (high word) in one scan
+    const long long pt = block_scan_1024<long long>(
+        P, [&](int i) { return (long long)pacc[i] | (pacc[i] > 0 ? 1ll << 32 : 0ll); },
+        [&](int i, long long x) {
             const int k = pacc[i];
-            pstart[i] = x;
+            pstart[i] = (int)(x & 0xFFFFFFFFll);
             ptcnt[i] = k;
             ptfree[i] = !points_fixed && k > 0;
         });
-    const int nfp = points_fixed ? 0 : block_scan_1024(P, [&](int i) { return pacc[i] > 0 ? 1 : 0; }, [](int, int) {});
-    block_scan_1024(C, [&](int c) { return cacc[c]; },
+    const int nact = (int)(pt & 0xFFFFFFFFll), nfp = points_fixed ? 0 : (int)(pt >> 32);
+    block_scan_1024<int>(C, [&](int c) { return cacc[c]; },
                     [&](int c, int x) {
                         cstart[c] = x;
                         s_ccnt[c] = cacc[c];
                     });
     auto is_free = [&](int c) { return !(camflag[c] & 1) && (cacc[c] > 0 || (camflag[c] & 2)); };
-    const int nb = block_scan_1024(
+    const int nb = block_scan_1024<int>(
         C, [&](int c) { return is_free(c) ? 1 : 0; },
         [&](int c, int x) {
             const bool f = is_free(c);
@@ -1844,27 +1846,56 @@ __global__ __launch_bounds__(1024) void init_scan(int C, int P, int nbm, int poi
     }
 }
 
-// Thread per active edge: its slot in its point's CSR run (unordered; init_psort orders each run).
+// Thread per active edge: its slot in its point's CSR run, one atomic per distinct point of the
+// wave (lanes of one point take consecutive slots in lane order; runs split over waves may
+// interleave, init_psort orders each run).
 __global__ __launch_bounds__(256) void init_pfill(int E, const int* __restrict__ ept, const unsigned char* __restrict__ active,
                                                   const int* __restrict__ pstart, int* __restrict__ pcur,
                                                   int* __restrict__ pedges)
 {
     const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= E || !active[e]) return;
-    const int p = ept[e];
-    pedges[pstart[p] + atomicAdd(&pcur[p], 1)] = e;
+    const bool a = e < E && active[e];
+    const int p = a ? ept[e] : -1;
+    const int lane = threadIdx.x & (kWave - 1);
+    unsigned long long todo = __ballot(a);
+    while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const int lp = __shfl(p, leader);
+        const unsigned long long same = __ballot(a && p == lp);
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&pcur[lp], __popcll(same));
+        base = __shfl(base, leader);
+        if (a && p == lp) pedges[pstart[lp] + base + __popcll(same & ((1ull << lane) - 1ull))] = e;
+        todo &= ~same;
+    }
 }
 
-// Thread per point: its CSR run in edge order (insertion sort: a point has few edges), the camera
-// sort keys of its positions, and the fill cursor back to zero.
-__global__ __launch_bounds__(256) void init_psort(int P, const int* __restrict__ pstart, const int* __restrict__ ecam,
-                                                  int* __restrict__ pcur, int* __restrict__ pedges,
-                                                  unsigned* __restrict__ ckey)
+// One wave per point: its CSR run in edge order — each entry's rank is the number of smaller
+// entries of the run (broadcast by shuffles) — then the camera sort keys of its positions and the
+// fill cursor back to zero.
+constexpr int PSORT_WAVES = 4;
+__global__ __launch_bounds__(PSORT_WAVES * kWave) void init_psort(int P, const int* __restrict__ pstart,
+                                                                  const int* __restrict__ ecam, int* __restrict__ pcur,
+                                                                  int* __restrict__ pedges, unsigned* __restrict__ ckey)
 {
-    const int p = blockIdx.x * 256 + threadIdx.x;
+    const int p = blockIdx.x * PSORT_WAVES + (int)(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
     if (p >= P) return;
-    const int b = pstart[p], end = pstart[p + 1];
-    for (int a = b + 1; a < end; a++) {
+    const int b = pstart[p], k = pstart[p + 1] - b;
+    if (lane == 0) pcur[p] = 0;
+    if (k <= kWave) {
+        const int v = lane < k ? pedges[b + lane] : INT_MAX;
+        int rank = 0;
+        for (int j = 0; j < k; j++) rank += __shfl(v, j) < v;
+        if (lane < k) {
+            pedges[b + rank] = v;
+            ckey[b + rank] = (unsigned)ecam[v];
+        }
+        return;
+    }
+    // a long run (a point observed by more than 64 edges; init_pfill leaves it nearly sorted):
+    // insertion sort by one lane
+    if (lane != 0) return;
+    for (int a = b + 1; a < b + k; a++) {
         const int v = pedges[a];
         int j = a;
         while (j > b && pedges[j - 1] > v) {
@@ -1873,8 +1904,7 @@ __global__ __launch_bounds__(256) void init_psort(int P, const int* __restrict__
         }
         pedges[j] = v;
     }
-    for (int a = b; a < end; a++) ckey[a] = (unsigned)ecam[pedges[a]];
-    pcur[p] = 0;
+    for (int a = b; a < b + k; a++) ckey[a] = (unsigned)ecam[pedges[a]];
 }
 
 // Camera CSR from the stable sort by camera of the point-CSR order: (camera, point, edge) order.
@@ -2166,6 +2196,30 @@ __global__ __launch_bounds__(1024) void export_state(State s, int C, int P, doub
 // Host: the StepOptimizer / OptimizationAlgorithmLevenberg control flow
 // ------------------------------------------------------------------------------------------
 
+// chol_tiles' slot table, ti | tj << 8 per (tile wave, slot), 0xFFFF empty.  Tiles (d-1, d) and
+// (d, d) share an owner, wave (d-1) % CT_TW: right after its TRSM of (d-1, d) it applies that
+// tile's update to (d, d) and stages A_dd for the factor wave.  The other tiles go round-robin,
+// row-major, over the waves with free slots; tile (0, 0) is read from S by the factor wave itself.
+static void chol_tile_table(int mt, std::vector<uint16_t>& tab)
+{
+    tab.assign((size_t)CT_TW * CT_TPW, 0xFFFF);
+    std::vector<int> cnt(CT_TW, 0);
+    auto put = [&](int w, int i, int j) { tab[(size_t)w * CT_TPW + cnt[w]++] = (uint16_t)(i | j << 8); };
+    for (int d = 1; d < mt; d++) {
+        put((d - 1) % CT_TW, d - 1, d);
+        put((d - 1) % CT_TW, d, d);
+    }
+    int w = 0;
+    for (int i = 0; i < mt; i++)
+        for (int j = i + 2; j < mt; j++) {
+            while (cnt[w] >= CT_TPW) w = (w + 1) % CT_TW;
+            put(w, i, j);
+            w = (w + 1) % CT_TW;
+        }
+}
+static_assert(CT_TW * CT_TPW >= CT_MAXT * (CT_MAXT + 1) / 2 - 1, "every tile but (0, 0) has a slot");
+static_assert(2 * ((CT_MAXT - 1 + CT_TW - 1) / CT_TW) <= CT_TPW, "a wave holds its chain tiles");
+
 struct BundleAdjuster {
     int device = 0;
     bool points_fixed = false;
@@ -2231,7 +2285,7 @@ struct BundleAdjuster {
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
         d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_cub, d_kdst, d_rblk, d_sbits, d_srank, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
-        d_sfinish, d_epos, d_chi_lin, d_livebuf, d_removed, d_camflag, d_ikeys, d_ivals, d_isum, d_iacc;
+        d_sfinish, d_epos, d_chi_lin, d_livebuf, d_removed, d_camflag, d_ikeys, d_ivals, d_isum, d_iacc, d_ctab;
     bool iacc_clean = false;  // d_iacc is all zero (see initialize())
     // outlier lists of the speculative / final post-pass (2 x E entries), written by the kernels
     // straight into host memory: the host sorts and returns them after the completion wait
@@ -2279,7 +2333,7 @@ struct BundleAdjuster {
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
                         &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_cub, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf, &d_removed, &d_camflag,
-                        &d_ikeys, &d_ivals, &d_isum, &d_iacc})
+                        &d_ikeys, &d_ivals, &d_isum, &d_iacc, &d_ctab})
             b->release();
         h_olist.release();
         h_state.release();
@@ -2485,6 +2539,7 @@ struct BundleAdjuster {
         std::vector<long long> pbeg, roww;
         std::vector<SchurPair> spairs;
         std::vector<SchurChunk> xcd_chunks[8], schunks;
+        std::vector<uint16_t> ctab;
     } ws;
     mage_status initialize()
     {
@@ -2547,7 +2602,7 @@ struct BundleAdjuster {
         int* pcur = cacc + Cm;
         int cbits = 1;
         while ((1ll << cbits) <= C) cbits++;
-        const unsigned ge = (unsigned)((E + 255) / 256), gp = (unsigned)((P + 255) / 256);
+        const unsigned ge = (unsigned)((E + 255) / 256);
         if (E > 0)
             launch("ba.init_edges", init_edges, dim3(ge), dim3(256), C <= INIT_LDS_CAMS ? C * 4 : 0, st, E, C,
                    points_fixed ? 1 : 0, (const int*)d_ecam.as<int>(), (const int*)d_ept.as<int>(),
@@ -2563,8 +2618,9 @@ struct BundleAdjuster {
                    (const unsigned char*)d_active.as<unsigned char>(), (const int*)d_pstart.as<int>(), pcur,
                    d_pedges.as<int>());
             if (P > 0)
-                launch("ba.init_psort", init_psort, dim3(gp), dim3(256), 0, st, P, (const int*)d_pstart.as<int>(),
-                       (const int*)d_ecam.as<int>(), pcur, d_pedges.as<int>(), k0);
+                launch("ba.init_psort", init_psort, dim3((unsigned)((P + PSORT_WAVES - 1) / PSORT_WAVES)),
+                       dim3(PSORT_WAVES * kWave), 0, st, P, (const int*)d_pstart.as<int>(), (const int*)d_ecam.as<int>(),
+                       pcur, d_pedges.as<int>(), k0);
             size_t tb = 0;
             MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, (const int*)d_pedges.as<int>(), v0, E, 0, cbits, st));
             if ((r = d_cub.reserve(std::max<size_t>(tb, 16))) != MAGE_OK) return r;
@@ -2784,6 +2840,10 @@ struct BundleAdjuster {
         n_sfinish = (int)sfinish.size();
         MAGE_REQUIRE(pbeg[npairs] < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
         pt.mark("chunks");
+        if (np <= 16 * CT_MAXT) {
+            chol_tile_table(np / 16, ws.ctab);
+            if ((r = upload(d_ctab, ws.ctab)) != MAGE_OK) return r;
+        }
         if ((r = upload(d_sfinish, sfinish)) != MAGE_OK) return r;
         if ((r = upload(d_spairs, spairs)) != MAGE_OK) return r;
         if ((r = upload(d_schunks, schunks)) != MAGE_OK) return r;
@@ -2917,7 +2977,8 @@ struct BundleAdjuster {
                    (const double*)d_tout.as<double>(), d_S.as<double>(), d_rhs.as<double>());
             if (np <= 16 * CT_MAXT)
                 launch("ba.cholesky_solve", chol_tiles, dim3(1), dim3(CT_THREADS), 0, st,
-                       (const double*)d_S.as<double>(), np, n, (const double*)d_rhs.as<double>(), xp, d_failp());
+                       (const double*)d_S.as<double>(), np, n, (const double*)d_rhs.as<double>(), xp, d_failp(),
+                       (const uint16_t*)d_ctab.as<uint16_t>());
             else
                 launch("ba.cholesky_solve", cholesky_solve, dim3(1), dim3(CH_THREADS), 0, st, d_S.as<double>(), np,
                        n, (const double*)d_rhs.as<double>(), xp, d_failp());

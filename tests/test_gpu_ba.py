@@ -308,3 +308,23 @@ def test_camera_observing_a_point_twice(gpu):
     compare(gb, ob)
     sg, so = gb.stats(), ob.stats()
     assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
+
+
+def test_point_with_more_than_64_observations(gpu):
+    """Points observed by more edges than one wave holds (device initialisation's long-run path of
+    the point CSR: init_psort), here 70 extra observations of two points spread over the cameras
+    and appended at the end of the edge list; same outliers, counts and poses as the oracle."""
+    g = synth.ba_graph(cameras=12, points=400, obs_per_point=8, fixed_cameras=3, seed=22)
+    rng = np.random.default_rng(5)
+    extra = []
+    for p in (7, 123):
+        src = np.flatnonzero(g.pt == p)
+        extra.append(rng.choice(src, 70, replace=True))
+    extra = np.concatenate(extra)
+    for f in ("cam", "pt", "info"):
+        setattr(g, f, np.concatenate([getattr(g, f), getattr(g, f)[extra]]))
+    g.uv = np.concatenate([g.uv, g.uv[extra] + rng.normal(0, 0.3, (len(extra), 2)).astype(np.float32)])
+    gb, ob = run_pair(g, 4)
+    compare(gb, ob)
+    sg, so = gb.stats(), ob.stats()
+    assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]

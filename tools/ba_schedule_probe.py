@@ -36,7 +36,7 @@ def main():
         return t1
 
     lib = _lib.load()
-    for w in range(W + 2):
+    for w in range(W + 4):
         if w == 2:
             acc.clear()
         if w == W + 1:
