@@ -209,18 +209,20 @@ class BundlerLib:
         ms = self.StepBundleAdjustment(huber_widths, max_error_square, outl)
         return ms, np.asarray(outl, np.uint32)
 
+    # GetPose / GetPoint run after every StepBundleAdjustment (UpdateData): fresh output arrays,
+    # raw addresses instead of ndarray.ctypes.data_as (several us each)
     def poses(self):
         n = len(self._cams["pos"])
-        pos = np.zeros((n, 3), np.float32)
-        r9 = np.zeros((n, 9), np.float32)
+        pos = np.empty((n, 3), np.float32)
+        r9 = np.empty((n, 9), np.float32)
         self._upload()
-        check(_lib.load().mage_ba_get_poses(self._h, ptr(pos), ptr(r9)))
+        check(_lib.load().mage_ba_get_poses(self._h, pos.ctypes.data, r9.ctypes.data))
         return pos, r9
 
     def points(self):
-        xyz = np.zeros((len(self._pts), 3), np.float32)
+        xyz = np.empty((len(self._pts), 3), np.float32)
         self._upload()
-        check(_lib.load().mage_ba_get_points(self._h, ptr(xyz)))
+        check(_lib.load().mage_ba_get_points(self._h, xyz.ctypes.data))
         return xyz
 
     def state(self):

@@ -1139,8 +1139,8 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     __shared__ __attribute__((aligned(16))) double dsc[16][18];  // the factor's scratch: A_kk transposed
     __shared__ __attribute__((aligned(16))) double vb[CT_MAXT * 16];  // b -> y -> x
     __shared__ int s_fail;
-    __shared__ int s_diag_ready;      // index of the diagonal block staged in dsc for the factor wave
-    __shared__ unsigned s_tile_bar;   // the tile waves' barrier count (CT_TW per step)
+    __shared__ unsigned s_tile_bar;   // the TRSM-phase barrier count (CT_TW + 1 arrivals per step)
+    __shared__ double cst[16][17], dst[16][17];  // A_{k,k+1}, A_{k+1,k+1} staged for the factor wave
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: tile bookkeeping on the SALU
     const int mt = np >> 4, T = mt * (mt + 1) / 2;
@@ -1265,20 +1265,36 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         if (lane < 16) vb[16 * k + lane] = xv;
     };
     if (wave == CT_TW) {
-        // ===== the factor wave: it holds no tile, so none of the tile registers are live here =====
-        // block 0 from S directly while the tile waves load their tiles (A_00 goes to dsc
-        // transposed, as stage_diag writes it)
+        // ===== the factor wave: it holds no tile, so none of the tile registers are live here.
+        // Per step k it runs the critical chain alone: TRSM of (k, k+1) with its own inv(L_kk),
+        // the update of (k+1, k+1) by it, and the factor of block k+1; the tile waves stage both
+        // tiles for it at the end of step k-1 ---
         if (lane == 0) {
             s_fail = 0;
-            s_diag_ready = -1;
             s_tile_bar = 0;
         }
+        dbl4 cA = {0, 0, 0, 0}, cD = {0, 0, 0, 0};  // A_{k,k+1}, A_{k+1,k+1} (accumulator layout)
+        auto s_tile = [&](int ti, int tj) {  // tile (ti, tj) of S, padded with the identity
+            dbl4 t;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = 16 * ti + lr + 4 * r, col = 16 * tj + lc;
+                t[r] = (row < n && col < n) ? S[(long long)row * np + col] : (row == col ? 1.0 : 0.0);
+            }
+            return t;
+        };
         if (mt > 0) {
+            // block 0 from S directly while the tile waves load their tiles (A_00 goes to dsc
+            // transposed, as stage_diag writes it)
             if (lane < 16) {
 #pragma unroll
                 for (int q = 0; q < 16; q++)
                     dsc[lane][q] = (q < n && lane < n) ? S[(long long)q * np + lane] : (q == lane ? 1.0 : 0.0);
                 vb[lane] = lane < n ? b[lane] : 0.0;
+            }
+            if (mt > 1) {
+                cA = s_tile(0, 1);
+                cD = s_tile(1, 1);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1291,18 +1307,50 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
 #endif
         for (int k = 0; k < mt; k++) {
             if (s_fail) break;
-            const int kn = k + 1;
-            // block k+1 as soon as its owner has staged it (during the TRSM phase), concurrently
-            // with the tile waves' TRSMs and SYRKs
+            const int kn = k + 1, buf = k & 1;
             if (kn < mt) {
-                while (__hip_atomic_load(&s_diag_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != kn)
-                    __builtin_amdgcn_s_sleep(1);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (k > 0)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        cA[r] = cst[lr + 4 * r][lc];
+                        cD[r] = dst[lr + 4 * r][lc];
+                    }
+                __builtin_amdgcn_s_setprio(3);  // the critical chain first on this SIMD
                 CT_STAMP(k, 0);
-                __builtin_amdgcn_s_setprio(3);  // the column loop is the critical chain
+                // TRSM U_{k,k+1} = inv(L_kk) A_{k,k+1} into the panel, y_{k+1} -= U^T y_k
+                dbl4 acc = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(invT[k][4 * q + lr][lc], cA[q], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; r++) pan[buf][kn][lr + 4 * r][lc] = acc[r];
+                double pacc = 0;
+#pragma unroll
+                for (int r = 0; r < 4; r++) pacc = __builtin_fma(acc[r], vb[16 * k + lr + 4 * r], pacc);
+                pacc += __shfl_xor(pacc, 16);
+                pacc += __shfl_xor(pacc, 32);
+                if (lr == 0) vb[16 * kn + lc] -= pacc;
+                // arrive at the TRSM-phase barrier (row-block k of the panel)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_fetch_add(&s_tile_bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_wave_barrier();  // U_{k,k+1} in the panel, read across lanes below
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // A_{k+1,k+1} -= U^T U, into dsc transposed
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    cD = __builtin_amdgcn_mfma_f64_16x16x4f64(-pan[buf][kn][4 * q + lr][lc], pan[buf][kn][4 * q + lr][lc], cD,
+                                                             0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; r++) dsc[lc][lr + 4 * r] = cD[r];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                CT_STAMP(k, 1);
                 factor_diag(kn);
                 __builtin_amdgcn_s_setprio(0);
-                CT_STAMP(k, 1);
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_fetch_add(&s_tile_bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             CT_STAMP(k, 2);
             __syncthreads();  // end of step k
@@ -1349,10 +1397,8 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         const int buf = k & 1;
         if (s_fail) break;
         const int kn = k + 1;
-        // --- TRSM: U_kj = inv(L_kk) A_kj for the owned tiles of row-block k.  The owner of
-        // tile (k, k+1) also owns (k+1, k+1) (chol_tile_table): it solves (k, k+1) first,
-        // applies that tile's update to (k+1, k+1) — the last one it needs — and hands
-        // A_{k+1,k+1} to the factor wave (LDS + flag) ---
+        // --- TRSM: U_kj = inv(L_kk) A_kj for the owned tiles of row-block k but (k, k+1), which
+        // the factor wave solves ---
         auto trsm = [&](int sl) {
             const int tj = tIJ[sl] >> 8;
             dbl4 acc = {0, 0, 0, 0};
@@ -1378,30 +1424,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                                                             pan[buf][tIJ[sl] >> 8][4 * q + lr][lc], C[sl], 0, 0, 0);
         };
         const int chain = k | kn << 8, diag = kn | kn << 8;
-        bool owner = false;
-#pragma unroll
-        for (int sl = 0; sl < CT_TPW; sl++)
-            if (tIJ[sl] == chain) {
-                owner = true;
-                __builtin_amdgcn_s_setprio(2);  // the critical chain first on this SIMD
-                trsm(sl);
-            }
-        if (owner) {
-            // U_{k,k+1} in pan (read across lanes) and vb_{k+1} final
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int sl = 0; sl < CT_TPW; sl++)
-                if (tIJ[sl] == diag) {
-                    syrk(sl);
-                    stage_diag(sl);
-                }
-            // the fence drains the staging stores (and vb_{k+1}) before the flag store
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) __hip_atomic_store(&s_diag_ready, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __builtin_amdgcn_s_setprio(0);
-        }
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++) {
             const int ti = tIJ[sl] & 0xFF, tj = tIJ[sl] >> 8;
@@ -1409,20 +1431,39 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         }
         tick(3);
         CT_STAMP(k, 0);
-        // the tile waves' own barrier (an LDS counter: the factor wave is not held up): pan
-        // row-block k complete
+        // the TRSM-phase barrier (an LDS counter: the factor wave arrives after its TRSM of
+        // (k, k+1) and goes on to the factor): pan row-block k complete
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_fetch_add(&s_tile_bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        while (__hip_atomic_load(&s_tile_bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)(CT_TW * kn))
+        while (__hip_atomic_load(&s_tile_bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)((CT_TW + 1) * kn))
             __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         CT_STAMP(k, 1);
         tick(2);
-        // --- SYRK: A_ij -= U_ki^T U_kj for the owned tiles with k < i <= j but (k+1, k+1) ---
+#pragma unroll
+        for (int sl = 0; sl < CT_TPW; sl++)  // the owner of (k, k+1) keeps U for the backward solve
+            if (tIJ[sl] == chain)
+#pragma unroll
+                for (int r = 0; r < 4; r++) C[sl][r] = pan[buf][kn][lr + 4 * r][lc];
+        // --- SYRK: A_ij -= U_ki^T U_kj for the owned tiles with k < i <= j but (k+1, k+1) (the
+        // factor wave's) ---
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++) {
             const int i = tIJ[sl] & 0xFF;
             if (i > k && i < mt && tIJ[sl] != diag) syrk(sl);
+        }
+        // the next step's chain tiles, now final, to the factor wave
+        if (kn + 1 < mt) {
+            const int nchain = kn | (kn + 1) << 8, ndiag = (kn + 1) | (kn + 1) << 8;
+#pragma unroll
+            for (int sl = 0; sl < CT_TPW; sl++) {
+                if (tIJ[sl] == nchain)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) cst[lr + 4 * r][lc] = C[sl][r];
+                if (tIJ[sl] == ndiag)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) dst[lr + 4 * r][lc] = C[sl][r];
+            }
         }
         tick(4);
         CT_STAMP(k, 2);
@@ -2196,29 +2237,22 @@ __global__ __launch_bounds__(1024) void export_state(State s, int C, int P, doub
 // Host: the StepOptimizer / OptimizationAlgorithmLevenberg control flow
 // ------------------------------------------------------------------------------------------
 
-// chol_tiles' slot table, ti | tj << 8 per (tile wave, slot), 0xFFFF empty.  Tiles (d-1, d) and
-// (d, d) share an owner, wave (d-1) % CT_TW: right after its TRSM of (d-1, d) it applies that
-// tile's update to (d, d) and stages A_dd for the factor wave.  The other tiles go round-robin,
-// row-major, over the waves with free slots; tile (0, 0) is read from S by the factor wave itself.
+// chol_tiles' slot table, ti | tj << 8 per (tile wave, slot), 0xFFFF empty: the upper tiles in
+// row-major order, round-robin over the tile waves; tile (0, 0) is the factor wave's (read from S
+// directly).
 static void chol_tile_table(int mt, std::vector<uint16_t>& tab)
 {
     tab.assign((size_t)CT_TW * CT_TPW, 0xFFFF);
     std::vector<int> cnt(CT_TW, 0);
-    auto put = [&](int w, int i, int j) { tab[(size_t)w * CT_TPW + cnt[w]++] = (uint16_t)(i | j << 8); };
-    for (int d = 1; d < mt; d++) {
-        put((d - 1) % CT_TW, d - 1, d);
-        put((d - 1) % CT_TW, d, d);
-    }
     int w = 0;
     for (int i = 0; i < mt; i++)
-        for (int j = i + 2; j < mt; j++) {
-            while (cnt[w] >= CT_TPW) w = (w + 1) % CT_TW;
-            put(w, i, j);
+        for (int j = i; j < mt; j++) {
+            if (i == 0 && j == 0) continue;
+            tab[(size_t)w * CT_TPW + cnt[w]++] = (uint16_t)(i | j << 8);
             w = (w + 1) % CT_TW;
         }
 }
 static_assert(CT_TW * CT_TPW >= CT_MAXT * (CT_MAXT + 1) / 2 - 1, "every tile but (0, 0) has a slot");
-static_assert(2 * ((CT_MAXT - 1 + CT_TW - 1) / CT_TW) <= CT_TPW, "a wave holds its chain tiles");
 
 struct BundleAdjuster {
     int device = 0;
