@@ -328,3 +328,16 @@ def test_point_with_more_than_64_observations(gpu):
     compare(gb, ob)
     sg, so = gb.stats(), ob.stats()
     assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
+
+
+@pytest.mark.parametrize("free", [2, 3, 11, 21, 27, 38])
+def test_dense_solve_block_counts(gpu, free):
+    """chol_tiles at several block counts (np = 16, 32, 80, 128, 176, 240 -> 1 to 15 block steps:
+    the factor wave's chain, the staged tiles and the TRSM-phase counter at every depth); same
+    outliers, counts and poses as the oracle."""
+    g = synth.ba_graph(cameras=free + 2, points=60 * (free + 2), obs_per_point=min(free + 2, 8), fixed_cameras=2,
+                       seed=30 + free)
+    gb, ob = run_pair(g, 3)
+    compare(gb, ob)
+    sg, so = gb.stats(), ob.stats()
+    assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
