@@ -122,7 +122,6 @@ inline unsigned RadiusMatch(const std::vector<KeyPoint>& queryKeypoints, const s
     return n;
 }
 
-// OnlineBow vocabulary tree on the device (OnlineBow.cpp:289-311 FindLeafNode; nodes as CreateTree
 // TrackLocalMap's per-map-point matching loop (TrackLocalMap.cpp:175-256): projected map points in
 // order (positions x, y interleaved; octaves; descriptors; the keypoint to hide for a
 // pose-estimation outlier point, -1 otherwise) against a frame's keypoints; unassociatedMask is
@@ -146,7 +145,7 @@ inline std::vector<int32_t> LocalMapMatch(const std::vector<float>& positions, c
     return result;
 }
 
-
+// OnlineBow vocabulary tree on the device (OnlineBow.cpp:289-311 FindLeafNode; nodes as CreateTree
 // builds them: node i's descriptor, children in childrenIDs order, root 0).
 class OnlineBowTree {
 public:

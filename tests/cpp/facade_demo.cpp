@@ -64,6 +64,19 @@ int main(int argc, char** argv)
                                                     std::vector<bool>(desc.size(), true), 30, 1, tmatches);
         std::vector<mage::hot::DMatch> rmatches;
         const unsigned nr = mage::hot::RadiusMatch(kps, nullptr, nullptr, desc, kps, nullptr, desc, 2.0f, 30, 1, rmatches);
+        // TrackLocalMap's per-map-point matching: the frame's own keypoints as projected map points
+        std::vector<float> lpos;
+        std::vector<int32_t> loct;
+        for (const auto& k : kps) {
+            lpos.push_back(k.x);
+            lpos.push_back(k.y);
+            loct.push_back(k.octave);
+        }
+        std::vector<bool> unassociated(kps.size(), true);
+        const std::vector<int32_t> lres =
+            mage::hot::LocalMapMatch(lpos, loct, desc, {}, kps, desc, unassociated, 2.0f, 30, 1);
+        uint32_t nl = 0;
+        for (int32_t v : lres) nl += v >= 0;
         std::vector<unsigned> outliers;
         float ms = 0;
         for (int it = 0; it < 5; it++) ms = ba.StepBundleAdjustment({1.8f}, 1e6f, outliers);
@@ -77,6 +90,8 @@ int main(int argc, char** argv)
         o.write((const char*)&nr, 4);
         o.write((const char*)&ni, 4);
         o.write((const char*)&nt, 4);
+        o.write((const char*)&nl, 4);
+        o.write((const char*)lres.data(), (std::streamsize)(4 * lres.size()));
         std::cout << "keypoints " << n << " self-matches " << nm << " ba_mean_sq " << ms << "\n";
     } catch (const mage::hot::Error& e) {
         std::cerr << "mage error: " << e.what() << "\n";

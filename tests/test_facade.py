@@ -72,6 +72,11 @@ def test_facade_matches_python_api(gpu, tmp_path):
     assert ni == len(bow.IndexedMatch(tree, pd, pd))
     nt = int(np.frombuffer(data[20 + 60 * n:24 + 60 * n], np.uint32)[0])
     assert nt == len(bow.IndexedMatch(bow.OnlineBowTree.CreateTree(pd), pd, pd))
+    nl = int(np.frombuffer(data[24 + 60 * n:28 + 60 * n], np.uint32)[0])
+    lres = np.frombuffer(data[28 + 60 * n:28 + 64 * n], np.int32)
+    pos = np.stack([pk["x"], pk["y"]], 1)
+    res, _ = matcher.LocalMapMatch(pos, pk["octave"], pd, pk, pd, np.ones(n, bool), 2.0, 30, 1)
+    assert nl == int((res >= 0).sum()) and np.array_equal(lres, res)
 
 
 def test_bundler_step_argument_reuse(monkeypatch):
