@@ -2374,8 +2374,9 @@ struct BundleAdjuster {
         h_kb.release();
         h_isum.release();
         h_stage.release();
+        h_dma.release();
         iacc_clean = false;
-        stage_off = 0;
+        stage_off = dma_off = 0;
         pending.k = 0;
         if (st) (void)hipStreamDestroy(st);
         st = nullptr;
@@ -2383,13 +2384,15 @@ struct BundleAdjuster {
         h_ctl = nullptr;
     }
 
-    // Host-to-device copies go through a pinned, device-mapped staging arena.  Large ones are DMA
-    // copies (a hipMemcpyAsync from pageable memory would be a synchronous staged copy); small ones
-    // are queued and moved by one gather_copy launch (flush_uploads) instead of one copy call
-    // each.  The arena restarts from its beginning only after a stream synchronisation, so no
-    // pending copy sees its source change.
-    MappedBuffer h_stage;
-    size_t stage_off = 0;
+    // Host-to-device copies are staged in pinned memory.  Large ones are DMA copies from a pinned
+    // ring (a hipMemcpyAsync from pageable memory would be a synchronous staged copy); small ones
+    // go to a device-mapped arena and are moved by one gather_copy launch (flush_uploads) instead
+    // of one copy call each.  A ring / the arena restarts from its beginning only after a stream
+    // synchronisation, so no pending copy sees its source change; it grows only when a single copy
+    // does not fit it.
+    MappedBuffer h_stage;  // small copies (read by gather_copy over the fabric)
+    PinnedBuffer h_dma;    // large copies (DMA source)
+    size_t stage_off = 0, dma_off = 0;
     GatherList pending{};
     static constexpr size_t GATHER_MAX_BYTES = 64 << 10;
     void flush_uploads()
@@ -2408,22 +2411,30 @@ struct BundleAdjuster {
     {
         if (bytes == 0) return MAGE_OK;
         const size_t need = (bytes + 255) & ~(size_t)255;
+        mage_status r;
+        if (bytes >= GATHER_MAX_BYTES) {
+            if (dma_off + need > h_dma.bytes) {
+                MAGE_HIP(hipStreamSynchronize(st));
+                dma_off = 0;
+                if (need > h_dma.bytes && (r = h_dma.reserve(std::max(need, (size_t)8 << 20))) != MAGE_OK) return r;
+            }
+            char* h = h_dma.as<char>() + dma_off;
+            std::memcpy(h, src, bytes);
+            MAGE_HIP(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, st));
+            dma_off += need;
+            return MAGE_OK;
+        }
         if (stage_off + need > h_stage.bytes) {
             flush_uploads();
             MAGE_HIP(hipStreamSynchronize(st));
             stage_off = 0;
-            mage_status r = h_stage.reserve(std::max(need, std::max<size_t>(2 * h_stage.bytes, (size_t)4 << 20)));
-            if (r != MAGE_OK) return r;
+            if (need > h_stage.bytes && (r = h_stage.reserve(std::max(need, (size_t)1 << 20))) != MAGE_OK) return r;
         }
         std::memcpy(h_stage.host<char>() + stage_off, src, bytes);
-        if (bytes >= GATHER_MAX_BYTES) {
-            MAGE_HIP(hipMemcpyAsync(dst, h_stage.host<char>() + stage_off, bytes, hipMemcpyHostToDevice, st));
-        } else {
-            if (pending.k == GATHER_MAX) flush_uploads();
-            pending.src[pending.k] = h_stage.device<const char>() + stage_off;
-            pending.dst[pending.k] = static_cast<char*>(dst);
-            pending.bytes[pending.k++] = (unsigned)bytes;
-        }
+        if (pending.k == GATHER_MAX) flush_uploads();
+        pending.src[pending.k] = h_stage.device<const char>() + stage_off;
+        pending.dst[pending.k] = static_cast<char*>(dst);
+        pending.bytes[pending.k++] = (unsigned)bytes;
         stage_off += need;
         return MAGE_OK;
     }
