@@ -329,6 +329,7 @@ def ba_round(b, g, me, steps, timer):
 
 REF_WINDOW_STEPS = 10  # StepBundleAdjustment calls per local-BA window on the reference schedule
 MIN_LAMBDA = 1e-3      # MappingSettings::MinLambda (MageSettings.h:260)
+REF_DECAY = np.float32(0.95) * np.float32(0.95)  # MaxOutlierErrorSquared *= 0.95^2 per call (BundleAdjust.cpp:396)
 
 
 def ba_reference_window(b, g, lam, steps, set_lambda, get_lambda, removed=None):
@@ -349,7 +350,7 @@ def ba_reference_window(b, g, lam, steps, set_lambda, get_lambda, removed=None):
             removed.append(len(out))
         b.poses()
         b.points()
-        me *= np.float32(0.95) * np.float32(0.95)
+        me *= REF_DECAY
     return max(get_lambda(), MIN_LAMBDA)
 
 
