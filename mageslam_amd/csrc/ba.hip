@@ -2207,22 +2207,39 @@ __global__ __launch_bounds__(64) void sc_pair_fill(int nb, int PW, const uint32_
     }
 }
 
-// The current state (q C x 4, t C x 3, p P x 3 doubles) copied into mapped host memory after a
-// step, so GetPose / GetPoint (UpdateData after every StepBundleAdjustment, BundleAdjust.cpp:
-// 195-226) read it without a D2H copy + stream sync; the completion word is written last.
-__global__ __launch_bounds__(1024) void export_state(State s, int C, int P, double* __restrict__ out,
+// GetPose / GetPoint's outputs of the current state written into mapped host memory after a step,
+// so UpdateData after every StepBundleAdjustment (BundleAdjust.cpp:195-226) reads them without a
+// D2H copy + stream sync: per camera t as float and R of the normalised quaternion as float (the
+// host's arithmetic of BundlerLib.cpp:457-465, in the same order, no contraction), per point the
+// position as float; the completion word is written last.
+__global__ __launch_bounds__(1024) void export_state(State s, int C, int P, float* __restrict__ out,
                                                      unsigned* __restrict__ seq_out, unsigned seq)
 {
-    const int nq = 4 * C, nt = 3 * C, np = 3 * P;
-    // 16-byte stores (the host mirror is written over the fabric)
-    for (int i = 2 * threadIdx.x; i < nq + nt + np; i += 2048) {
-        double v[2];
-        for (int k = 0; k < 2; k++) {
-            const int j = i + k;
-            v[k] = j < nq ? s.q[j] : j < nq + nt ? s.t[j - nq] : j < nq + nt + np ? s.p[j - nq - nt] : 0.0;
-        }
-        if (i + 1 < nq + nt + np) *reinterpret_cast<double2*>(out + i) = make_double2(v[0], v[1]);
-        else out[i] = v[0];
+    float* pos3 = out;
+    float* r9 = out + 3 * C;
+    float* xyz = out + 12 * C;
+    for (int c = threadIdx.x; c < C; c += 1024) {
+        double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
+        const double nn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        for (int k = 0; k < 4; k++) q[k] /= nn;
+        const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+        const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+        const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+        const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+        const double R[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz),
+                             tyz - twx,       txz - twy, tyz + twx, 1 - (txx + tyy)};
+        for (int k = 0; k < 3; k++) pos3[3 * c + k] = (float)s.t[3 * c + k];
+        for (int rr = 0; rr < 3; rr++)
+            for (int cc = 0; cc < 3; cc++) r9[9 * c + cc * 3 + rr] = (float)R[rr * 3 + cc];
+    }
+    // points: 16-byte stores of 4 floats (the mirror is written over the fabric)
+    const int np = 3 * P;
+    for (int i = 4 * threadIdx.x; i < np; i += 4096) {
+        if (i + 3 < np && ((12 * C + i) & 3) == 0)
+            *reinterpret_cast<float4*>(xyz + i) =
+                make_float4((float)s.p[i], (float)s.p[i + 1], (float)s.p[i + 2], (float)s.p[i + 3]);
+        else
+            for (int k = 0; k < 4 && i + k < np; k++) xyz[i + k] = (float)s.p[i + k];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2451,38 +2468,35 @@ struct BundleAdjuster {
         return stage_copy(b.ptr, v, n * sizeof(T));
     }
 
-    // export_state's mirror of the current estimate (valid while export_seq is the last sequence
-    // number launched and export_cur the current buffer)
+    // export_state's GetPose / GetPoint outputs of the current estimate (valid while export_seq is
+    // the last sequence number launched and export_cur the current buffer)
     MappedBuffer h_state;
     unsigned export_seq = 0;
     int export_cur = -1;
     bool export_wanted = false;  // the caller read the state since the last step
     void launch_export()
     {
-        if (h_state.reserve((size_t)(7 * C + 3 * P + 1) * sizeof(double)) != MAGE_OK) {
+        if (h_state.reserve((size_t)(12 * C + 3 * P + 4) * sizeof(float)) != MAGE_OK) {
             export_cur = -1;
             return;
         }
-        launch("ba.export_state", export_state, dim3(1), dim3(1024), 0, st, state(cur), C, P, h_state.device<double>(),
+        launch("ba.export_state", export_state, dim3(1), dim3(1024), 0, st, state(cur), C, P, h_state.device<float>(),
                seq_dev(), ++seq_counter);
         export_seq = seq_counter;
         export_cur = cur;
+    }
+    // the exported outputs when they are those of the current estimate (after their completion wait)
+    const float* exported()
+    {
+        if (!state_on_device || !host_state_stale || export_cur != cur || export_seq != seq_counter) return nullptr;
+        if (wait_seq(export_seq) != MAGE_OK) return nullptr;
+        return h_state.host<float>();
     }
 
     // Pull the current estimate back to the host vectors.
     mage_status sync_host_state()
     {
         if (!state_on_device || !host_state_stale) return MAGE_OK;
-        if (export_cur == cur && export_seq == seq_counter) {
-            mage_status r = wait_seq(export_seq);
-            if (r != MAGE_OK) return r;
-            const double* m = h_state.host<double>();
-            std::memcpy(q.data(), m, sizeof(double) * 4 * C);
-            std::memcpy(t.data(), m + 4 * C, sizeof(double) * 3 * C);
-            std::memcpy(p.data(), m + 7 * C, sizeof(double) * 3 * P);
-            host_state_stale = false;
-            return MAGE_OK;
-        }
         MAGE_HIP(hipMemcpyAsync(q.data(), d_q[cur].ptr, sizeof(double) * 4 * C, hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipMemcpyAsync(t.data(), d_t[cur].ptr, sizeof(double) * 3 * C, hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipMemcpyAsync(p.data(), d_p[cur].ptr, sizeof(double) * 3 * P, hipMemcpyDeviceToHost, st));
@@ -3465,6 +3479,11 @@ mage_status mage_ba_get_poses(mage_ba* b, float* pos3, float* r9)
     MAGE_REQUIRE(b && pos3 && r9, MAGE_EINVAL, "null argument");
     (void)hipSetDevice(b->device);
     b->export_wanted = true;  // GetPose / GetPoint between steps: keep the mapped mirror current
+    if (const float* m = b->exported()) {
+        std::memcpy(pos3, m, sizeof(float) * 3 * b->C);
+        std::memcpy(r9, m + 3 * b->C, sizeof(float) * 9 * b->C);
+        return MAGE_OK;
+    }
     mage_status r = b->sync_host_state();
     if (r != MAGE_OK) return r;
     for (int c = 0; c < b->C; c++) {
@@ -3491,6 +3510,10 @@ mage_status mage_ba_get_points(mage_ba* b, float* xyz)
     MAGE_REQUIRE(b && xyz, MAGE_EINVAL, "null argument");
     (void)hipSetDevice(b->device);
     b->export_wanted = true;  // GetPose / GetPoint between steps: keep the mapped mirror current
+    if (const float* m = b->exported()) {
+        std::memcpy(xyz, m + 12 * b->C, sizeof(float) * 3 * b->P);
+        return MAGE_OK;
+    }
     mage_status r = b->sync_host_state();
     if (r != MAGE_OK) return r;
     for (int i = 0; i < 3 * b->P; i++) xyz[i] = (float)b->p[i];
@@ -3501,8 +3524,7 @@ mage_status mage_ba_get_state_f64(mage_ba* b, double* qt7, double* xyz)
 {
     MAGE_REQUIRE(b, MAGE_EINVAL, "null handle");
     (void)hipSetDevice(b->device);
-    b->export_wanted = true;  // GetPose / GetPoint between steps: keep the mapped mirror current
-    mage_status r = b->sync_host_state();
+    mage_status r = b->sync_host_state();  // fp64: a D2H copy (the mapped mirror holds GetPose / GetPoint's floats)
     if (r != MAGE_OK) return r;
     if (qt7)
         for (int c = 0; c < b->C; c++) {

@@ -341,3 +341,29 @@ def test_dense_solve_block_counts(gpu, free):
     compare(gb, ob)
     sg, so = gb.stats(), ob.stats()
     assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
+
+
+def test_get_pose_point_outputs_match_fp64_state(gpu):
+    """GetPose / GetPoint after a step (UpdateData's reads) come from the device-written float
+    outputs once the caller reads between steps; they equal BundlerLib.cpp:457-471 evaluated on
+    the fp64 state (t and R of the normalised quaternion cast to float, points cast to float)."""
+    g = synth.ba_graph(cameras=12, points=400, obs_per_point=8, fixed_cameras=3, seed=1)
+    b = bundler.BundlerLib()
+    b.set_graph(g)
+    for _ in range(4):
+        b.step([1.8], 7.25)
+        pos, r9 = b.poses()
+        xyz = b.points()
+        qt, p = b.state()
+        q0, q1, q2, q3 = (qt[:, k].copy() for k in range(4))
+        nn = np.sqrt(q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3)
+        q0, q1, q2, q3 = q0 / nn, q1 / nn, q2 / nn, q3 / nn
+        tx, ty, tz = 2 * q0, 2 * q1, 2 * q2
+        twx, twy, twz = tx * q3, ty * q3, tz * q3
+        txx, txy, txz = tx * q0, ty * q0, tz * q0
+        tyy, tyz, tzz = ty * q1, tz * q1, tz * q2
+        R = np.stack([1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
+                      txz - twy, tyz + twx, 1 - (txx + tyy)], 1).reshape(-1, 3, 3)
+        assert np.array_equal(pos, qt[:, 4:].astype(np.float32))
+        assert np.array_equal(r9.reshape(-1, 3, 3), R.transpose(0, 2, 1).astype(np.float32))
+        assert np.array_equal(xyz, p.astype(np.float32))
