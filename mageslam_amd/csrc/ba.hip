@@ -1700,6 +1700,19 @@ __global__ __launch_bounds__(BA_THREADS) void drop_edges(const int* __restrict__
     if (atomicSub(&ptcnt[p], 1) == 1) ptfree[p] = 0;
 }
 
+// The initialisation summary into mapped host memory, completion word last (the host spins on it
+// instead of a D2H copy + stream synchronisation).
+__global__ __launch_bounds__(1024) void summary_out(const int* __restrict__ sum, int n, int* __restrict__ out,
+                                                    unsigned* __restrict__ seq_out, unsigned seq)
+{
+    for (int i = threadIdx.x; i < n; i += 1024) out[i] = sum[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        *reinterpret_cast<volatile unsigned*>(seq_out) = seq;
+    }
+}
+
 // Queued small host-to-device copies in one launch: the sources are in mapped host memory (the
 // staging arena), read over the fabric; workgroup b copies GATHER_BLOCK_BYTES of the entry whose
 // block range holds b.
@@ -2075,8 +2088,10 @@ __global__ __launch_bounds__(256) void schur_scatter(const uint16_t* __restrict_
 // camera-CSR order: one workgroup per block, a block-wide prefix of the free flags per 256 entries.
 __global__ __launch_bounds__(256) void schur_rhs(const int* __restrict__ camblk, const int* __restrict__ cstart,
                                                  const int* __restrict__ cpt, const int* __restrict__ ptfree,
-                                                 const int* __restrict__ rblk, int2* __restrict__ sentries)
+                                                 const int* __restrict__ rblk, int2* __restrict__ sentries, int pad_at)
 {
+    // the padding entry after the last list (schur_chunks reads one past a chunk's end)
+    if (blockIdx.x == 0 && threadIdx.x == 0) sentries[pad_at] = make_int2(0, 0);
     __shared__ int wsum[256 / kWave];
     const int h = blockIdx.x, c = camblk[h];
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -2342,7 +2357,7 @@ struct BundleAdjuster {
     // straight into host memory: the host sorts and returns them after the completion wait
     MappedBuffer h_olist;
     PinnedBuffer h_kb;    // per-pair list bounds read back by build_product_lists
-    PinnedBuffer h_isum;  // the device initialisation's summary (init_scan etc., INIT_HDR layout)
+    MappedBuffer h_isum;  // the device initialisation's summary (init_scan etc., INIT_HDR layout)
     std::vector<int> camcnt;  // active observation edges per camera (host-side bookkeeping)
     int n_entries = 0;  // point-CSR entries (active edges at initialisation)
     int nb_free = 0;    // cameras in the reduced system
@@ -2701,12 +2716,13 @@ struct BundleAdjuster {
             launch("ba.schur_counts", sc_pair_counts, dim3(nbm, nbm), dim3(64), 0, st, (const int*)sum, PW,
                    (const uint32_t*)A, (const uint32_t*)(A + (size_t)nbm * PW), s_kcnt);
         }
+        launch("ba.init_summary", summary_out, dim3(1), dim3(1024), 0, st, (const int*)sum, (int)nsum, h_isum.device<int>(),
+               seq_dev(), ++seq_counter);
         MAGE_HIP(hipGetLastError());
-        MAGE_HIP(hipMemcpyAsync(h_isum.ptr, sum, nsum * 4, hipMemcpyDeviceToHost, st));
-        MAGE_HIP(hipStreamSynchronize(st));
+        if ((r = wait_seq(seq_counter)) != MAGE_OK) return r;
         iacc_clean = true;
         pt.mark("device init + summary");
-        const int* hs = h_isum.as<int>();
+        const int* hs = h_isum.host<int>();
         const int nb = hs[0], nfp = hs[1], nact = hs[2];
         const bool dup = hs[3] != 0;  // a camera observing a point twice (its CSR run lists the point twice)
         MAGE_REQUIRE(nb <= CH_PANEL_ROWS / 6, MAGE_EUNSUPPORTED, "more than 96 free cameras in one bundle adjustment");
@@ -2721,6 +2737,74 @@ struct BundleAdjuster {
         np = (n + 15) / 16 * 16;
         useless = (nb == 0 && nfp == 0);
         n_entries = nact;
+        // The iteration's state and buffers now, so the first linearisation runs on the device while
+        // the host builds the Schur tables below
+        if (!state_on_device) {
+            if ((r = upload(d_q[0], q)) != MAGE_OK) return r;
+            if ((r = upload(d_t[0], t)) != MAGE_OK) return r;
+            if ((r = upload(d_p[0], p)) != MAGE_OK) return r;
+            if ((r = d_q[1].reserve(d_q[0].bytes)) != MAGE_OK) return r;
+            if ((r = d_t[1].reserve(d_t[0].bytes)) != MAGE_OK) return r;
+            if ((r = d_p[1].reserve(d_p[0].bytes)) != MAGE_OK) return r;
+            cur = 0;
+            state_on_device = true;
+        }
+        flush_uploads();
+        {
+            const size_t npm = std::max(np, 16);
+            for (auto pr : {std::make_pair(&d_err, Em * 2 * 8), std::make_pair(&d_Hll, Pm * 9 * 8),
+                            std::make_pair(&d_bl, Pm * 3 * 8), std::make_pair(&d_Hpl, (size_t)std::max(n_entries, 1) * EQ_N * 8),
+                            std::make_pair(&d_Hpp, Cm * 36 * 8), std::make_pair(&d_bp, Cm * 6 * 8),
+                            std::make_pair(&d_Z, (size_t)std::max(n_entries, 1) * EG_N * 8),
+                            std::make_pair(&d_campart, Cm * CAM_CHUNKS * 27 * 8),
+                            std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
+                            std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, (Pm + teth.size()) * 8),
+                            std::make_pair(&d_chi_lin, (Pm + teth.size()) * 8),
+                            std::make_pair(&d_tout, std::max<size_t>(teth.size(), 1) * TETHER_OUT * 8),
+                            std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
+                            std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8),
+                            std::make_pair(&d_osum, ((size_t)std::max<int>((int)(Em / BA_THREADS), group_grid((int)Pm)) + 2) * 4 * 8)})
+                if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
+            if ((r = d_livebuf.reserve(sizeof(LiveCtl))) != MAGE_OK) return r;
+            if ((r = h_olist.reserve(Em * 2 * 4 + 16)) != MAGE_OK) return r;
+            // one launch clears: the live counters, the max-diagonal / scale partials, S (chol_tiles
+            // reads S without writing it and every trial rewrites the same covisible pair blocks, so
+            // the zero blocks are set once here; cholesky_solve factors in place: per trial), and
+            // on first use the per-edge errors
+            ClearList cl{};
+            auto add = [&](void* ptr, size_t bytes) {
+                cl.p[cl.k] = static_cast<uint32_t*>(ptr);
+                cl.n[cl.k++] = (unsigned)(bytes / 4);
+            };
+            static_assert(sizeof(LiveCtl) % 4 == 0, "LiveCtl is cleared as words");
+            add(d_livebuf.ptr, sizeof(LiveCtl));
+            add(d_maxd.ptr, (Pm + Cm) * 8);
+            add(d_scale.ptr, (Pm + Cm) * 8);
+            add(d_S.ptr, npm * npm * 8);
+            if (!err_initialized) {
+                add(d_err.ptr, Em * 2 * 8);
+                err_initialized = true;
+            }
+            size_t words = 0;
+            for (int k = 0; k < cl.k; k++) words = std::max<size_t>(words, cl.n[k]);
+            launch("ba.init_clear", clear_words, dim3((unsigned)std::min<size_t>(1024, (words + 255) / 256)), dim3(256),
+                   0, st, cl);
+        }
+        iteration = 0;
+        dirty = false;
+        eager = false;
+        if (!useless && teth.empty()) {
+            // the first call's linearisation (the one lm_solve would launch: same huber width,
+            // lambda from the user or computeLambdaInit's reduction), taken up by lm_solve
+            const bool init = user_lambda <= 0;
+            if ((r = linearize(init ? std::numeric_limits<double>::quiet_NaN() : user_lambda, init)) != MAGE_OK) return r;
+            eager = true;
+            eager_init = init;
+            eager_huber = huber;
+            eager_lambda = init ? 0.0 : user_lambda;
+            eager_cur = cur;
+        }
+        pt.mark("state + buffers + linearisation");
         const bool bitmaps = !dup && bitmap_fits && nb > 0 && nfp > 0;
         // covisible camera pairs (h1 <= h2) of the reduced system: every pair sharing a free point
         // (a product list), the diagonal, and the tethered pairs
@@ -2800,7 +2884,7 @@ struct BundleAdjuster {
                 const int pi = pairidx[(size_t)h * nb + h];
                 rblk[h] = (int)(pbeg[pi] + pcount[pi]);
             }
-            // + the padding entry after the last list (cleared with the other buffers below)
+            // + the padding entry after the last list (written by schur_rhs)
             if ((r = d_sentries.reserve(((size_t)pbeg[npairs] + 1) * sizeof(int2))) != MAGE_OK) return r;
             if (bitmaps)  // sc_pair_fill: a pair's first product slot (-1: no products)
                 for (int k = 0; k < nk; k++) kdst[k] = kcount[k] > 0 ? kdst[k] + kstart[k] : -1;
@@ -2821,7 +2905,7 @@ struct BundleAdjuster {
             if (nb > 0)
                 launch("ba.schur_rhs", schur_rhs, dim3(nb), dim3(256), 0, st, (const int*)d_camblk.as<int>(),
                        (const int*)d_cstart.as<int>(), (const int*)d_cpt.as<int>(), (const int*)d_ptfree.as<int>(),
-                       (const int*)d_rblk.as<int>(), d_sentries.as<int2>());
+                       (const int*)d_rblk.as<int>(), d_sentries.as<int2>(), (int)pbeg[npairs]);
             MAGE_HIP(hipGetLastError());
         }
         pt.mark("list scatter");
@@ -2913,61 +2997,9 @@ struct BundleAdjuster {
         }
         if ((r = upload(d_teth, teth)) != MAGE_OK) return r;
         pt.mark("uploads");
-        if (!state_on_device) {
-            if ((r = upload(d_q[0], q)) != MAGE_OK) return r;
-            if ((r = upload(d_t[0], t)) != MAGE_OK) return r;
-            if ((r = upload(d_p[0], p)) != MAGE_OK) return r;
-            if ((r = d_q[1].reserve(d_q[0].bytes)) != MAGE_OK) return r;
-            if ((r = d_t[1].reserve(d_t[0].bytes)) != MAGE_OK) return r;
-            if ((r = d_p[1].reserve(d_p[0].bytes)) != MAGE_OK) return r;
-            cur = 0;
-            state_on_device = true;
-        }
         flush_uploads();
-        const size_t npm = std::max(np, 16);
-        for (auto pr : {std::make_pair(&d_err, Em * 2 * 8), std::make_pair(&d_Hll, Pm * 9 * 8),
-                        std::make_pair(&d_bl, Pm * 3 * 8), std::make_pair(&d_Hpl, (size_t)std::max(n_entries, 1) * EQ_N * 8),
-                        std::make_pair(&d_Hpp, Cm * 36 * 8), std::make_pair(&d_bp, Cm * 6 * 8),
-                        std::make_pair(&d_Z, (size_t)std::max(n_entries, 1) * EG_N * 8),
-                        std::make_pair(&d_campart, Cm * CAM_CHUNKS * 27 * 8),
-                        std::make_pair(&d_S, npm * npm * 8), std::make_pair(&d_rhs, npm * 8),
-                        std::make_pair(&d_x, (npm + 3 * Pm + 1) * 8), std::make_pair(&d_chi, (Pm + teth.size()) * 8), std::make_pair(&d_chi_lin, (Pm + teth.size()) * 8),
-                        std::make_pair(&d_tout, std::max<size_t>(teth.size(), 1) * TETHER_OUT * 8),
-                        std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
-                        std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_osum, ((size_t)std::max<int>((int)(Em / BA_THREADS), group_grid((int)Pm)) + 2) * 4 * 8),
-                        
-                        std::make_pair(&d_spart, (size_t)std::max(n_slots, 1) * 42 * 8)})
-            if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
-        if ((r = d_livebuf.reserve(sizeof(LiveCtl))) != MAGE_OK) return r;
-        if ((r = h_olist.reserve(Em * 2 * 4 + 16)) != MAGE_OK) return r;
-        // one launch clears: the live counters, the max-diagonal / scale partials, S (chol_tiles
-        // reads S without writing it and every trial rewrites the same covisible pair blocks, so
-        // the zero blocks are set once here; cholesky_solve factors in place: per trial), the
-        // padding entry after the last product list (schur_chunks reads one past a chunk's end),
-        // and on first use the per-edge errors
-        ClearList cl{};
-        auto add = [&](void* ptr, size_t bytes) {
-            cl.p[cl.k] = static_cast<uint32_t*>(ptr);
-            cl.n[cl.k++] = (unsigned)(bytes / 4);
-        };
-        static_assert(sizeof(LiveCtl) % 4 == 0, "LiveCtl is cleared as words");
-        add(d_livebuf.ptr, sizeof(LiveCtl));
-        add(d_maxd.ptr, (Pm + Cm) * 8);
-        add(d_scale.ptr, (Pm + Cm) * 8);
-        add(d_S.ptr, npm * npm * 8);
-        add(d_sentries.as<int2>() + pbeg[npairs], sizeof(int2));
-        if (!err_initialized) {
-            add(d_err.ptr, Em * 2 * 8);
-            err_initialized = true;
-        }
-        size_t words = 0;
-        for (int k = 0; k < cl.k; k++) words = std::max<size_t>(words, cl.n[k]);
-        launch("ba.init_clear", clear_words, dim3((unsigned)std::min<size_t>(1024, (words + 255) / 256)), dim3(256), 0,
-               st, cl);
+        if ((r = d_spart.reserve((size_t)std::max(n_slots, 1) * 42 * 8)) != MAGE_OK) return r;
         pt.mark("buffers");
-        iteration = 0;
-        dirty = false;
-        eager = false;
         return MAGE_OK;
     }
 
@@ -3238,9 +3270,13 @@ struct BundleAdjuster {
         // After an outlier removal the next Step starts at iteration 0 (lambda re-initialised from
         // the user lambda or computeLambdaInit): the eager linearisation is that iteration's, with
         // the reduction computeLambdaInit reads when no user lambda is set.
-        if (!dirty && !useless) {
-            const bool init = iteration == 0 && user_lambda <= 0;
-            const double lam = iteration > 0 ? lambda : user_lambda;
+        const bool init_next = iteration == 0 && user_lambda <= 0;
+        const double lam_next = iteration > 0 ? lambda : user_lambda;
+        const bool pending = eager && eager_init == init_next && eager_huber == huber && eager_cur == cur &&
+                             (init_next || eager_lambda == lam_next);  // (initialize() just launched it)
+        if (!dirty && !useless && !pending) {
+            const bool init = init_next;
+            const double lam = lam_next;
             if ((r = linearize(init ? std::numeric_limits<double>::quiet_NaN() : lam, init)) != MAGE_OK) return r;
             eager = true;
             eager_init = init;
