@@ -24,9 +24,9 @@
 //                     previous SYRK), TRSM and SYRK on f64 MFMA (v_mfma_f64_16x16x4f64), then a
 //                     one-barrier-per-block backward solve.  cholesky_solve: np > 240 (LDS
 //                     panels, in-place)
-//     point_backsub   xl = Dinv (bl - Hpl^T xp)
-//     update_state    trial state = exp(xp) * T, p + xl  (double-buffered: pop = no copy)
-//     point_linearize errors + robust chi2 of the trial state;  reduce: chi2 and computeScale
+//     update_evaluate xl = Dinv (bl - Hpl^T xp), trial state = exp(xp) * T, p + xl
+//                     (double-buffered: pop = no copy), and in the same point groups the errors +
+//                     robust chi2 of the trial state;  reduce: chi2 and computeScale
 //     outlier_pass    (last step of a StepBundleAdjustment only) speculatively on the trial
 //                     and the current state, so the post-pass result is already on the host
 // then the StepBundleAdjustment post-pass (BundlerLib.cpp:385-446): outlier indices from the
@@ -183,16 +183,23 @@ struct SpecPass {
     LiveCtl* ctl;
 };
 
-__device__ __forceinline__ double cheirality(const State& s, int c, int p)
+__device__ __forceinline__ double cheirality_at(const double q[4], const double t[3], const double X[3])
 {
     // SE3Quat::inverse: q*, -(q* t); forward = q* (0,0,1)
-    const double qc[4] = {-s.q[4 * c], -s.q[4 * c + 1], -s.q[4 * c + 2], s.q[4 * c + 3]};
-    const double tt[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
+    const double qc[4] = {-q[0], -q[1], -q[2], q[3]};
     double it[3], fwd[3];
-    d_qrot(qc, tt, it);
+    d_qrot(qc, t, it);
     const double z[3] = {0, 0, 1};
     d_qrot(qc, z, fwd);
-    return (s.p[3 * p] + it[0]) * fwd[0] + (s.p[3 * p + 1] + it[1]) * fwd[1] + (s.p[3 * p + 2] + it[2]) * fwd[2];
+    return (X[0] + it[0]) * fwd[0] + (X[1] + it[1]) * fwd[1] + (X[2] + it[2]) * fwd[2];
+}
+
+__device__ __forceinline__ double cheirality(const State& s, int c, int p)
+{
+    const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
+    const double t[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
+    const double X[3] = {s.p[3 * p], s.p[3 * p + 1], s.p[3 * p + 2]};
+    return cheirality_at(q, t, X);
 }
 
 // One point by a group of PG lanes (one edge per lane, strided): edge errors, robust chi2 and,
@@ -486,20 +493,6 @@ __global__ __launch_bounds__(BA_THREADS) void linearize_kernel(Problem pb, State
     if (p >= pb.P) return;  // whole groups
     double vs[2], vc[2];
     point_group<true>(pb, s, p, sub, o, lambda, with_g != 0, nullptr, vs, vc);
-}
-
-// Evaluation of a trial state (errors + robust chi2) with the speculative post-pass.
-__global__ __launch_bounds__(BA_THREADS) void evaluate_kernel(Problem pb, State s, PointOut o, SpecPass sp)
-{
-    const int gid = blockIdx.x * BA_THREADS + threadIdx.x;
-    const int p = gid / PG, sub = gid % PG;
-    double vs[2] = {0, 0}, vc[2] = {0, 0};
-    if (p < pb.P) point_group<false>(pb, s, p, sub, o, 0.0, false, sp.on ? &sp : nullptr, vs, vc);
-    if (!sp.on) return;
-    __shared__ double red[BA_THREADS / kWave][4];
-    double v4[4] = {vs[0], vc[0], vs[1], vc[1]};
-    block_sum<4>(v4, red);
-    if (threadIdx.x < 4) sp.part[(long long)threadIdx.x * gridDim.x + blockIdx.x] = red[0][threadIdx.x];
 }
 
 // After the linearisation (one workgroup): Hpp / bp of every free camera from its chunk partials,
@@ -1524,18 +1517,23 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                tm[1], tm[2], tm[3], tm[4], tm[5], tm[6], tm[7]);
 }
 
-// Back-substitution and the trial state in one launch.  Blocks [0, npb): a PG-lane group per
-// point: xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]) = Dinv bl - sum_e Z_e^T xp[h(e)] (Dinv
-// symmetric; Z_e^T xp = G_e^T (Jp_e xp)), trial point B.p = A.p + xl (copy for points outside the
-// system) and the point part of computeScale.  The remaining blocks: thread per camera, trial
-// pose exp(xp) * T (VertexSE3Expmap::oplusImpl) or copy, and the camera part of computeScale.
-__global__ __launch_bounds__(BA_THREADS) void backsub_update(Problem pb, const double* __restrict__ G,
-                                                             const double* __restrict__ Q,
-                                                             const double* __restrict__ Hll,
-                                                             const double* __restrict__ bl,
-                                                             const double* __restrict__ xp, double lambda,
-                                                             State A, State B, const double* __restrict__ bp,
-                                                             double* __restrict__ scale_part, int npb)
+// Back-substitution, the trial state and its evaluation in one launch.  Blocks [0, npb): a
+// PG-lane group per point: xl = Dinv (bl - sum_e Hpl_e^T xp[h(e)]) = Dinv bl - sum_e Z_e^T xp[h(e)]
+// (Dinv symmetric; Z_e^T xp = G_e^T (Jp_e xp)), trial point B.p = A.p + xl (copy for points
+// outside the system), the point part of computeScale, then the trial errors + robust chi2 of the
+// point's edges with the speculative StepBundleAdjustment post-pass for both candidate states
+// (cheirality + maxErrorSquare, outlier appends, inlier block partials).  Each lane forms its
+// edge's trial camera pose exp(xp) * T itself (the same d_oplus the camera threads store), so the
+// evaluation needs no second launch.  The remaining blocks: thread per camera, trial pose
+// (VertexSE3Expmap::oplusImpl) or copy, and the camera part of computeScale.
+__global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const double* __restrict__ G,
+                                                              const double* __restrict__ Q,
+                                                              const double* __restrict__ Hll,
+                                                              const double* __restrict__ bl,
+                                                              const double* __restrict__ xp, double lambda,
+                                                              State A, State B, const double* __restrict__ bp,
+                                                              double* __restrict__ scale_part, int npb, PointOut o,
+                                                              SpecPass sp)
 {
     if ((int)blockIdx.x >= npb) {
         const int i = (blockIdx.x - npb) * BA_THREADS + threadIdx.x;
@@ -1559,54 +1557,94 @@ __global__ __launch_bounds__(BA_THREADS) void backsub_update(Problem pb, const d
     }
     const int gid = blockIdx.x * BA_THREADS + threadIdx.x;
     const int p = gid / PG, sub = gid % PG;
-    if (p >= pb.P) return;
-    if (!pb.ptfree[p]) {
+    double vs[2] = {0, 0}, vc[2] = {0, 0};
+    if (p < pb.P) {  // whole groups
+        double X[3] = {A.p[3 * p], A.p[3 * p + 1], A.p[3 * p + 2]};
+        double sc = 0;
+        const long long es = pb.ecsr;
+        const int e0 = pb.pstart[p], e1 = pb.pstart[p + 1];
+        if (pb.ptfree[p]) {
+            double cl[3] = {0, 0, 0};
+            for (int a = e0 + sub; a < e1; a += PG) {
+                const int e = pb.pedges[a];
+                if (!pb.active[e]) continue;
+                const int h = pb.camh[pb.ecam[e]];
+                if (h < 0) continue;
+                const int a2 = pb.epos[e];
+                double J[12];
+                jac_pose_q(Q[a2], Q[es + a2], Q[2 * es + a2], pb.camk[3 * pb.ecam[e]], J);
+                const double* Xp = xp + 6 * h;
+                double u0 = 0, u1 = 0;
+#pragma unroll
+                for (int r = 0; r < 6; r++) {
+                    u0 += J[r] * Xp[r];
+                    u1 += J[6 + r] * Xp[r];
+                }
+#pragma unroll
+                for (int k = 0; k < 3; k++) cl[k] += G[k * es + a2] * u0 + G[(3 + k) * es + a2] * u1;
+            }
+            group_sum(cl);  // every lane of the group holds the sums
+            // db_p = Dinv_p bl_p, Dinv_p = (Hll_p + lambda I)^-1 as in edge_schur
+            double D[9], Di[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
+            D[0] += lambda;
+            D[4] += lambda;
+            D[8] += lambda;
+            d_inv3(D, Di);
+            const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
+            for (int r = 0; r < 3; r++) {
+                const double dbr = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
+                const double v = dbr - cl[r];
+                X[r] += v;
+                sc += v * (lambda * v + bl[3 * p + r]);
+            }
+        }
         if (sub == 0) {
-            for (int k = 0; k < 3; k++) B.p[3 * p + k] = A.p[3 * p + k];
-            scale_part[p] = 0;
+            for (int k = 0; k < 3; k++) B.p[3 * p + k] = X[k];
+            scale_part[p] = sc;
         }
-        return;
-    }
-    double cl[3] = {0, 0, 0};
-    const long long es = pb.ecsr;
-    for (int a = pb.pstart[p] + sub; a < pb.pstart[p + 1]; a += PG) {
-        const int e = pb.pedges[a];
-        if (!pb.active[e]) continue;
-        const int h = pb.camh[pb.ecam[e]];
-        if (h < 0) continue;
-        // Z_e^T xp = G^T (Jp xp)
-        const int a2 = pb.epos[e];
-        double J[12];
-        jac_pose_q(Q[a2], Q[es + a2], Q[2 * es + a2], pb.camk[3 * pb.ecam[e]], J);
-        const double* X = xp + 6 * h;
-        double u0 = 0, u1 = 0;
+        double chi = 0;
+        for (int a = e0 + sub; a < e1; a += PG) {
+            const int e = pb.pedges[a];
+            if (!pb.active[e]) continue;
+            const int c = pb.ecam[e];
+            double q[4] = {A.q[4 * c], A.q[4 * c + 1], A.q[4 * c + 2], A.q[4 * c + 3]};
+            double t[3] = {A.t[3 * c], A.t[3 * c + 1], A.t[3 * c + 2]};
+            const int h = pb.camh[c];
+            if (h >= 0) {
+                double u[6];
+                for (int k = 0; k < 6; k++) u[k] = xp[6 * h + k];
+                d_oplus(q, t, u);
+            }
+            double ev[2], xc[3], rho0, rho1;
+            edge_eval_at(pb, e, q, t, X, ev, xc, rho0, rho1);
+            o.err[2 * e] = ev[0];
+            o.err[2 * e + 1] = ev[1];
+            chi += rho0;
+            if (sp.on) {
+                const double sumSquares = ev[0] * ev[0] + ev[1] * ev[1];
 #pragma unroll
-        for (int r = 0; r < 6; r++) {
-            u0 += J[r] * X[r];
-            u1 += J[6 + r] * X[r];
+                for (int k = 0; k < 2; k++) {
+                    const double dot = k == 0 ? cheirality_at(q, t, X) : cheirality(sp.cur, c, p);
+                    if (dot <= 0 || sumSquares > sp.maxErrSq) {
+                        sp.out_list[(long long)k * sp.E + atomicAdd(&sp.ctl->count[k], 1u)] = (uint32_t)e;
+                    } else {
+                        vs[k] += sumSquares;
+                        vc[k] += 1;
+                    }
+                }
+            }
         }
-#pragma unroll
-        for (int k = 0; k < 3; k++) cl[k] += G[k * es + a2] * u0 + G[(3 + k) * es + a2] * u1;
+        double cv[1] = {chi};
+        group_sum(cv);
+        if (sub == 0) o.chi_part[p] = cv[0];
     }
-    group_sum(cl);
-    if (sub != 0) return;
-    // db_p = Dinv_p bl_p, Dinv_p = (Hll_p + lambda I)^-1 as in edge_schur
-    double D[9], Di[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
-    D[0] += lambda;
-    D[4] += lambda;
-    D[8] += lambda;
-    d_inv3(D, Di);
-    const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
-    double sc = 0;
-    for (int r = 0; r < 3; r++) {
-        const double dbr = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
-        const double v = dbr - cl[r];
-        B.p[3 * p + r] = A.p[3 * p + r] + v;
-        sc += v * (lambda * v + bl[3 * p + r]);
-    }
-    scale_part[p] = sc;
+    if (!sp.on) return;
+    __shared__ double red[BA_THREADS / kWave][4];
+    double v4[4] = {vs[0], vc[0], vs[1], vc[1]};
+    block_sum<4>(v4, red);
+    if (threadIdx.x < 4) sp.part[(long long)threadIdx.x * npb + blockIdx.x] = red[0][threadIdx.x];
 }
 
 // StepBundleAdjustment post-pass (BundlerLib.cpp:385-446) per active edge using the stored
@@ -3075,21 +3113,18 @@ struct BundleAdjuster {
                        n, (const double*)d_rhs.as<double>(), xp, d_failp());
         }
         const int ncb = (C + BA_THREADS - 1) / BA_THREADS;
+        // the trial state and its evaluation with the speculative post-pass (read back with this sync)
+        const bool spec = speculate && E > 0;
+        SpecPass sp{state(cur), spec ? 1 : 0, outlier_max_err_sq, h_olist.device<uint32_t>(), E, d_osum.as<double>(), d_live()};
         if (npb + ncb > 0)
-            launch("ba.backsub_update", backsub_update, dim3(npb + ncb), dim3(BA_THREADS), 0, st, pb,
+            launch("ba.update_evaluate", update_evaluate, dim3(npb + ncb), dim3(BA_THREADS), 0, st, pb,
                    (const double*)d_Z.as<double>(), (const double*)d_Hpl.as<double>(), (const double*)d_Hll.as<double>(),
                    (const double*)d_bl.as<double>(), (const double*)xp, lam, state(cur), state(1 - cur),
-                   (const double*)d_bp.as<double>(), d_scale.as<double>(), npb);
+                   (const double*)d_bp.as<double>(), d_scale.as<double>(), npb, point_out(d_chi.as<double>()), sp);
         const int nt = (int)teth.size();
         if (nt > 0)
             launch("ba.tether_eval", tether_eval, dim3((nt + 63) / 64), dim3(64), 0, st, (const Tether*)d_teth.as<Tether>(),
                    nt, state(1 - cur), 0, d_chi.as<double>() + P, d_tout.as<double>());
-        // evaluation of the trial state with the speculative post-pass (read back with this sync)
-        const bool spec = speculate && E > 0;
-        SpecPass sp{state(cur), spec ? 1 : 0, outlier_max_err_sq, h_olist.device<uint32_t>(), E, d_osum.as<double>(), d_live()};
-        if (npb > 0)
-            launch("ba.evaluate", evaluate_kernel, dim3(npb), dim3(BA_THREADS), 0, st, pb, state(1 - cur),
-                   point_out(d_chi.as<double>()), sp);
         launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)d_chi.as<double>(), P + nt,
                (const double*)d_scale.as<double>(), P + C, (const double*)d_maxd.as<double>(), 0, h_ctl_dev + 3,
                (const double*)d_chi_lin.as<double>(), P + nt, h_ctl_dev + CTL_SCRATCH,

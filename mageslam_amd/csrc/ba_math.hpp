@@ -292,6 +292,24 @@ struct Problem {
     double huber;
 };
 
+// computeError + chi2 + robustify for edge e with its camera pose (q, t) and point X given
+__device__ __forceinline__ void edge_eval_at(const Problem& pb, int e, const double q[4], const double t[3],
+                                             const double X[3], double err[2], double xc[3], double& rho0,
+                                             double& rho1)
+{
+    const int c = pb.ecam[e];
+    d_qrot(q, X, xc);
+    xc[0] += t[0];
+    xc[1] += t[1];
+    xc[2] += t[2];
+    const double f = pb.camk[3 * c], cx = pb.camk[3 * c + 1], cy = pb.camk[3 * c + 2];
+    err[0] = pb.uv[2 * e] - (xc[0] / xc[2] * f + cx);
+    err[1] = pb.uv[2 * e + 1] - (xc[1] / xc[2] * f + cy);
+    const double inf = pb.info[e];
+    const double chi2 = inf * (err[0] * err[0] + err[1] * err[1]);
+    d_huber(pb.huber, chi2, rho0, rho1);
+}
+
 // computeError + chi2 + robustify for one edge at state s; returns rho0, writes err, xc
 __device__ __forceinline__ void edge_eval(const Problem& pb, const State& s, int e, double err[2],
                                           double xc[3], double& rho0, double& rho1)
@@ -299,16 +317,8 @@ __device__ __forceinline__ void edge_eval(const Problem& pb, const State& s, int
     const int c = pb.ecam[e], p = pb.ept[e];
     const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
     const double X[3] = {s.p[3 * p], s.p[3 * p + 1], s.p[3 * p + 2]};
-    d_qrot(q, X, xc);
-    xc[0] += s.t[3 * c];
-    xc[1] += s.t[3 * c + 1];
-    xc[2] += s.t[3 * c + 2];
-    const double f = pb.camk[3 * c], cx = pb.camk[3 * c + 1], cy = pb.camk[3 * c + 2];
-    err[0] = pb.uv[2 * e] - (xc[0] / xc[2] * f + cx);
-    err[1] = pb.uv[2 * e + 1] - (xc[1] / xc[2] * f + cy);
-    const double inf = pb.info[e];
-    const double chi2 = inf * (err[0] * err[0] + err[1] * err[1]);
-    d_huber(pb.huber, chi2, rho0, rho1);
+    const double t[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
+    edge_eval_at(pb, e, q, t, X, err, xc, rho0, rho1);
 }
 
 // EdgeProjectXYZ2UV::linearizeOplus pose block (2x6, row-major).  One reciprocal of z instead of

@@ -290,7 +290,7 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
 // select_kernel checks that G <= lower for the frame (the histogram above G is exact) and sends
 // every frame that fails the check through the exact path again (fast_redo_kernel +
 // select_redo_kernel); the output never depends on G.  G comes from the previous batch of the
-// same detector: 7/8 of the smallest `lower` over its frames (frames of a stream change slowly).
+// same detector: 15/16 of the smallest `lower` over its frames (frames of a stream change slowly).
 //
 // gate_strip: the compass test of the thread's 4-px x 8-row strip; zeroes the strip's score
 // dwords and returns bit 8 q + r set when pixel q of score row SR * chunk + r passes.
@@ -751,7 +751,7 @@ struct SelectParams {
     int accumulate;  // append after the n_out[f] keypoints of the previous levels (Insert)
     uint16_t* lvl;   // per keypoint (level << 8 | rotation); rotation filled by orient_kernel
     const int* gate;  // the gate of this batch's FAST pass (FastParams::gate)
-    int* gate_next;   // atomicMin of 7/8 of each frame's `lower` (0: no retain, no gate)
+    int* gate_next;   // atomicMin of 15/16 of each frame's `lower` (0: no retain, no gate)
     uint32_t* redo;   // frames to run through the exact path again
 };
 
@@ -775,6 +775,9 @@ __device__ unsigned long long g_sel_stamps[1024][16];
 #endif
 
 // Frame f; G is the candidate gate its FAST pass ran with (no gate when G <= fast_threshold).
+#ifndef MAGE_GATE_SHIFT
+#define MAGE_GATE_SHIFT 4  // next gate = lower - lower / 2^MAGE_GATE_SHIFT (15/16: tools/gate_probe.py)
+#endif
 __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __restrict__ cand,
                                              const uint32_t* __restrict__ counts, const SelectParams& p,
                                              mage_keypoint* __restrict__ kp_out, uint32_t* __restrict__ xy_out,
@@ -889,7 +892,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
                 const uint32_t k = atomicAdd(&p.redo[0], 1u);
                 p.redo[1 + k] = (uint32_t)f;  // fast_redo_kernel rewrites the frame's tile slots
             } else if (p.gate_next) {
-                atomicMin(p.gate_next, s_mode == 1 ? lower - (lower >> 3) : 0);
+                atomicMin(p.gate_next, s_mode == 1 ? lower - (lower >> MAGE_GATE_SHIFT) : 0);
             }
         }
     }

@@ -41,7 +41,7 @@ KERNEL_TAG = {
     "point_backsub": "ba.point_backsub", "edge_schur": "ba.edge_schur", "chol_tiles": "ba.cholesky_solve", "drop_edges": "ba.drop_edges", "export_state": "ba.export_state", "update_state": "ba.update_state",
     "outlier_pass": "ba.outlier_pass", "reduce3": "ba.reduce", "linearize_finish": "ba.linearize_finish",
     "schur_pairs": "ba.schur_pairs", "schur_chunks": "ba.schur_pairs", "schur_finish": "ba.schur_finish",
-    "linearize_kernel": "ba.linearize", "evaluate_kernel": "ba.evaluate", "backsub_update": "ba.backsub_update",
+    "linearize_kernel": "ba.linearize", "update_evaluate": "ba.update_evaluate",
     "tether_eval": "ba.tether_eval", "refresh_membership": "ba.refresh_membership",
     "pose_ba_kernel": "pose.ba", "radius_match_kernel": "match.radius", "radius_post_kernel": "match.radius_post", "indexed_match_kernel": "match.indexed",
     "bow_leaves_kernel": "bow.leaves", "remap_linear_kernel": "image.remap", "remap_boxes_kernel": "image.boxes",
