@@ -2477,11 +2477,22 @@ struct BundleAdjuster {
         launch("ba.upload_gather", gather_copy, dim3(blocks), dim3(256), 0, st, pending);
         pending.k = 0;
     }
+    // a queued (not yet launched) copy writes into [p, p + n)
+    bool pending_overlaps(const void* p, size_t n) const
+    {
+        const char* a = static_cast<const char*>(p);
+        for (int i = 0; i < pending.k; i++)
+            if (pending.dst[i] < a + n && a < pending.dst[i] + pending.bytes[i]) return true;
+        return false;
+    }
     mage_status stage_copy(void* dst, const void* src, size_t bytes)
     {
         if (bytes == 0) return MAGE_OK;
         const size_t need = (bytes + 255) & ~(size_t)255;
         mage_status r;
+        // copies stay in call order: a DMA copy goes after every queued one, and a second copy
+        // into a queued destination after the first (one gather launch does not order its blocks)
+        if (bytes >= GATHER_MAX_BYTES || pending_overlaps(dst, bytes)) flush_uploads();
         if (bytes >= GATHER_MAX_BYTES) {
             if (dma_off + need > h_dma.bytes) {
                 MAGE_HIP(hipStreamSynchronize(st));
@@ -2516,6 +2527,8 @@ struct BundleAdjuster {
     template <typename T>
     mage_status upload(DeviceBuffer& b, const T* v, size_t n)
     {
+        // a growing buffer is freed by reserve(): launch the queued copies into it first
+        if (b.ptr && std::max<size_t>(n * sizeof(T), 16) > b.bytes && pending_overlaps(b.ptr, b.bytes)) flush_uploads();
         mage_status r = b.reserve(std::max<size_t>(n * sizeof(T), 16));
         if (r != MAGE_OK) return r;
         return stage_copy(b.ptr, v, n * sizeof(T));

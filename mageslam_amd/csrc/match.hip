@@ -505,6 +505,280 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
 
 constexpr int NRES = 2560;  // B descriptors kept resident in LDS up to this count
 
+// ------------------------------------------------------------------------------------------
+// fp4 matcher (nb <= 2048, maxDist < 128, minDiff >= 1: every practical call, C2 included).
+//
+// 16 waves, one 32-row A tile each per pass (A operands, row states and the accumulator fit
+// 128 VGPRs: 4 waves per SIMD hide the MFMA and LDS latencies that the 8-wave form covered with
+// a two-tile software pipeline).  Per 32x32 tile a lane folds 16 accumulator values:
+//   * the accumulator starts at C = 1/8 + (0x2400 + code) ulp (per-lane constant registers, code =
+//     63 - the lane's row in the tile), so the result's low 16 bits are the packed key
+//     64 (272 - d) + code, a positive i16 (and positive normal f16), exact: see tile_mfma_fp4;
+//   * column keys need the row -> the code is already there (no XOR);
+//   * row states keep only the two best *distances* (the code is the same constant for every
+//     tile a register sees), so the row side needs no index at all: with minDiff >= 1 an
+//     accepted row has a unique best column, and (i, j) is a match iff row i is accepted with
+//     best distance d0, column j is accepted with best row i, and d(i, j) = d0 — the column
+//     states (which carry the row index) identify j.  Same result as the reference's two
+//     radiusMatch calls + cross-check (FeatureMatcher.cpp:117-167) whenever ties are rejected.
+// ------------------------------------------------------------------------------------------
+constexpr int FW = 16;               // waves
+constexpr int FT = FW * kWave;       // 1024 threads
+constexpr int FROWS = FW * 32;       // A rows per pass
+constexpr int FSC = FT / 8;          // 128 B columns per LDS stage (one fill dword per thread)
+constexpr int FNT = FSC / 32;        // 4 column tiles per stage
+constexpr int FNB = 2048;            // max B descriptors
+constexpr int FNA = 4096;            // max A descriptors
+constexpr int FBUF = 3;              // stage buffers
+constexpr uint32_t K16_BASE = 0x2400u;  // low-16 mantissa offset of the accumulator start
+constexpr int K16_D = 272;           // key >> 6 = K16_D - d
+constexpr uint32_t NONE16 = 0x80008000u;
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pkmax(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
+}
+__device__ __forceinline__ uint32_t pkmin(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
+}
+__device__ __forceinline__ int lo16s(uint32_t v) { return (int)(short)(v & 0xFFFFu); }
+__device__ __forceinline__ int hi16s(uint32_t v) { return (int)v >> 16; }
+
+// The fp4 product of the wave's 32 rows and one 32-column B tile, accumulated onto cc (the
+// per-lane code registers).  Elements are +-1 with E8M0 scales 2^-11 (A) and 2^-10 (B): each bit
+// adds +-2^-21 = +-32 ulp of the binade [1/8, 1/4), the total is (128 - d) 64 ulp with |.| <=
+// 2^-13, and cc = 1/8 + (0x2400 + code) ulp keeps every partial sum inside the binade: exact, and
+// the low 16 bits are 0x2400 + code + 64 (128 - d) = 64 (272 - d) + code in [0x0400, 0x643F].
+__device__ __forceinline__ v16f tile_mfma_k16(const v4i (&a)[4], const v4i (&b)[4], const v16f& cc)
+{
+    v16f acc = cc;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const v8i av = {a[s][0], a[s][1], a[s][2], a[s][3], 0, 0, 0, 0};
+        const v8i bv = {b[s][0], b[s][1], b[s][2], b[s][3], 0, 0, 0, 0};
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc, 4, 4, 0, 127 - 11, 0, 127 - 10);
+    }
+    return acc;
+}
+
+// A pending column flush (the second LDS atomic needs the first one's return value; it is issued
+// after the next tile's fold so the round trip overlaps VALU work).
+struct PendingCol16 {
+    int j, c1, c2, old;
+    bool live;
+};
+
+__global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict__ A, const uint32_t* __restrict__ nA,
+                                                       const uint8_t* __restrict__ B, const uint32_t* __restrict__ nB,
+                                                       MatchParams p, mage_dmatch* __restrict__ out,
+                                                       uint32_t* __restrict__ n_out, uint32_t* __restrict__ status)
+{
+    __shared__ v4i stage[FBUF][FNT][4][kWave];          // [buffer][tile][k-step][lane] fp4 operands
+    __shared__ __attribute__((aligned(16))) uint32_t bres[FNB * 8];  // packed B
+    __shared__ int colM1[FNB], colM2[FNB];             // column (best, second) global keys
+    __shared__ uint16_t rowd[FNA];                     // accepted row: best distance, else 0xFFFF
+    __shared__ uint32_t wsum[FW];
+    uint16_t* matchOf = reinterpret_cast<uint16_t*>(&stage[0][0][0][0]);  // after the passes
+    static_assert(sizeof(stage) >= FNA * sizeof(uint16_t), "matchOf aliases the stages");
+
+    const int pair = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int na = (int)nA[pair], nb = (int)nB[pair];
+    if (na > FNA || nb > FNB) {
+        if (tid == 0) {
+            atomicOr(status, 1u);
+            n_out[pair] = 0;
+        }
+        return;
+    }
+    const int maxDist = p.max_dist, minDiff = p.min_diff;
+    const uint32_t* Aw = reinterpret_cast<const uint32_t*>(A + pair * p.a_pitch);
+    const uint32_t* Bw = reinterpret_cast<const uint32_t*>(B + pair * p.b_pitch);
+    for (int j = tid; j < nb; j += FT) {
+        colM1[j] = NONE;
+        colM2[j] = NONE;
+    }
+    if (na > 0 && nb > 0) {
+        for (int k = tid; k < 2 * nb; k += FT) reinterpret_cast<uint4*>(bres)[k] = reinterpret_cast<const uint4*>(Bw)[k];
+    }
+    // per-lane accumulator start: register g holds tile row acc_row(g) + 4 h, code 63 - row
+    v16f cc;
+#pragma unroll
+    for (int g = 0; g < 16; g++)
+        cc[g] = __builtin_bit_cast(float, (124u << 23) | (K16_BASE + (uint32_t)(63 - acc_row(g) - 4 * (lane >> 5))));
+    const int nstages = (nb + FSC - 1) / FSC;
+    const int fs = tid / FSC, fc = tid % FSC;  // stage-fill item: descriptor dword fs of column fc
+    auto fetch = [&](int st) -> uint32_t { return bres[8 * min(st * FSC + fc, nb - 1) + fs]; };
+    auto fill = [&](int buf, int st, uint32_t dw) {
+        const v4i zero = {0, 0, 0, 0};
+        stage[buf][fc >> 5][fs >> 1][32 * (fs & 1) + (fc & 31)] = st * FSC + fc < nb ? expand32_fp4(dw) : zero;
+    };
+
+    for (int pb = 0; pb < (nb > 0 ? na : 0); pb += FROWS) {
+        const int rowbase = pb + wave * 32;
+        const bool active = rowbase < na;
+        v4i a[4];
+        {
+            const int i = rowbase + (lane & 31);
+            const uint32_t* ar = Aw + 8 * min(i, na - 1);
+            const uint32_t w0 = ar[(lane >> 5)], w1 = ar[2 + (lane >> 5)], w2 = ar[4 + (lane >> 5)], w3 = ar[6 + (lane >> 5)];
+            const v4i zero = {0, 0, 0, 0};
+            a[0] = i < na ? expand32_fp4(w0) : zero;
+            a[1] = i < na ? expand32_fp4(w1) : zero;
+            a[2] = i < na ? expand32_fp4(w2) : zero;
+            a[3] = i < na ? expand32_fp4(w3) : zero;
+        }
+        uint32_t r1[8], r2[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) r1[q] = r2[q] = NONE16;
+        {
+            const uint32_t w0 = fetch(0), w1 = nstages > 1 ? fetch(1) : 0u;
+            __syncthreads();  // B resident / column states ready; the previous pass is done with the stages
+            fill(0, 0, w0);
+            if (nstages > 1) fill(1, 1, w1);
+            __syncthreads();
+        }
+        // global key of a local column key: (64 (272 - d) + code) -> ((272 - d) << 16 | 0x7FFF - row)
+        const int kadd = 0x7FFF - rowbase - 63;
+        PendingCol16 pc{0, 0, 0, 0, false};
+        for (int st = 0; st < nstages; st++) {
+            const int buf = st % FBUF;
+            const uint32_t nxt = st + 2 < nstages ? fetch(st + 2) : 0u;
+            if (active) {
+#pragma unroll
+                for (int ct = 0; ct < FNT; ct++) {
+                    const int colbase = st * FSC + ct * 32;
+                    if (colbase >= nb) break;
+                    v4i bf[4];
+#pragma unroll
+                    for (int s = 0; s < 4; s++) bf[s] = stage[buf][ct][s][lane];
+                    const v16i acc = __builtin_bit_cast(v16i, tile_mfma_k16(a, bf, cc));
+                    uint32_t P[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        P[q] = __builtin_amdgcn_perm((uint32_t)acc[2 * q + 1], (uint32_t)acc[2 * q], 0x05040100u);
+                    // row states: the two best distances over the tiles (same code per register)
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        r2[q] = pkmax(r2[q], pkmin(r1[q], P[q]));
+                        r1[q] = pkmax(r1[q], P[q]);
+                    }
+                    // column: the two best (distance, row) keys of the lane's 16 rows
+                    uint32_t c1 = pkmax(P[0], P[1]), c2 = pkmin(P[0], P[1]);
+#pragma unroll
+                    for (int q = 2; q < 8; q++) {
+                        c2 = pkmax(c2, pkmin(c1, P[q]));
+                        c1 = pkmax(c1, P[q]);
+                    }
+                    // the partner half-wave holds the same column (rows + 4)
+                    {
+                        const uint32_t o1 = (uint32_t)xor32((int)c1, lane), o2 = (uint32_t)xor32((int)c2, lane);
+                        const uint32_t lo = pkmin(c1, o1);
+                        c1 = pkmax(c1, o1);
+                        c2 = pkmax(pkmax(lo, c2), o2);
+                    }
+                    const int a1 = lo16s(c1), b1 = hi16s(c1);
+                    const int m1 = max(a1, b1), m2 = max(min(a1, b1), max(lo16s(c2), hi16s(c2)));
+                    const int g1 = ((m1 >> 6) << 16) | ((m1 & 63) + kadd);
+                    const int g2 = ((m2 >> 6) << 16) | ((m2 & 63) + kadd);
+                    if (pc.live) atomicMax(&colM2[pc.j], pc.old > pc.c1 ? pc.c1 : max(pc.old, pc.c2));
+                    pc.j = colbase + (lane & 31);
+                    pc.c1 = g1;
+                    pc.c2 = g2;
+                    pc.live = lane < 32 && pc.j < nb;
+                    pc.old = pc.live ? atomicMax(&colM1[pc.j], g1) : NONE;
+                }
+            }
+            if (st + 2 < nstages) fill((st + 2) % FBUF, st + 2, nxt);
+            __syncthreads();
+        }
+        if (pc.live) atomicMax(&colM2[pc.j], pc.old > pc.c1 ? pc.c1 : max(pc.old, pc.c2));
+        if (active) {
+            // reduce-scatter the 8 packed row states over lane bits 4, 3, 2, then all-reduce over
+            // bits 1, 0: lane (lane & 31) ends with packed state k = (lane & 31) >> 2
+#pragma unroll
+            for (int m = 16, n = 8; m >= 4; m >>= 1, n >>= 1) {
+                const bool up = (lane & m) != 0;
+                const int hf = n / 2;
+#pragma unroll
+                for (int k = 0; k < hf; k++) {
+                    const uint32_t s1 = up ? r1[k] : r1[k + hf], s2 = up ? r2[k] : r2[k + hf];
+                    uint32_t x1 = up ? r1[k + hf] : r1[k], x2 = up ? r2[k + hf] : r2[k];
+                    const uint32_t o1 = (uint32_t)__shfl_xor((int)s1, m), o2 = (uint32_t)__shfl_xor((int)s2, m);
+                    const uint32_t lo = pkmin(x1, o1);
+                    r1[k] = pkmax(x1, o1);
+                    r2[k] = pkmax(pkmax(lo, x2), o2);
+                }
+            }
+#pragma unroll
+            for (int m = 2; m >= 1; m >>= 1) {
+                const uint32_t o1 = (uint32_t)__shfl_xor((int)r1[0], m), o2 = (uint32_t)__shfl_xor((int)r2[0], m);
+                const uint32_t lo = pkmin(r1[0], o1);
+                r1[0] = pkmax(r1[0], o1);
+                r2[0] = pkmax(pkmax(lo, r2[0]), o2);
+            }
+            if ((lane & 3) == 0) {
+                const int k = (lane & 31) >> 2;
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const int i = rowbase + acc_row(2 * k + e) + 4 * (lane >> 5);
+                    const int k1 = e ? hi16s(r1[0]) : lo16s(r1[0]), k2 = e ? hi16s(r2[0]) : lo16s(r2[0]);
+                    const int d0 = K16_D - (k1 >> 6), d1 = K16_D - (k2 >> 6);  // NONE -> d > 511
+                    const bool ok = d0 <= maxDist && !(d1 <= maxDist && d1 - d0 < minDiff);
+                    if (i < na) rowd[i] = ok ? (uint16_t)d0 : (uint16_t)0xFFFFu;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // pair the accepted columns with their rows (see the section comment)
+    for (int i = tid; i < na; i += FT) matchOf[i] = 0xFFFFu;
+    __syncthreads();
+    for (int j = tid; j < (na > 0 ? nb : 0); j += FT) {
+        const int k1 = colM1[j], k2 = colM2[j];
+        if (k1 == NONE) continue;
+        const int dc = K16_D - (k1 >> 16);
+        const int d2 = k2 == NONE ? INT_MAX : K16_D - (k2 >> 16);
+        if (dc > maxDist || (d2 <= maxDist && d2 - dc < minDiff)) continue;
+        const int i = 0x7FFF - (k1 & 0x7FFF);
+        if (i < na && rowd[i] == (uint16_t)dc) matchOf[i] = (uint16_t)j;
+    }
+    __syncthreads();
+    // ordered compaction (ascending A index, FeatureMatcher.cpp:142-167)
+    uint32_t base = 0;
+    mage_dmatch* o = out + (long long)pair * p.out_cap;
+    for (int rb = 0; rb < (nb > 0 ? na : 0); rb += FT) {
+        const int i = rb + tid;
+        const int j = i < na ? (int)matchOf[i] : 0xFFFF;
+        const bool ok = j != 0xFFFF;
+        const unsigned long long m = __ballot(ok);
+        const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t woff = 0, total = 0;
+        for (int w = 0; w < FW; w++) {
+            if (w < wave) woff += wsum[w];
+            total += wsum[w];
+        }
+        if (ok) {
+            const uint32_t pos = base + woff + before;
+            if (pos < p.out_cap) {
+                mage_dmatch mm;
+                mm.query_idx = i;
+                mm.train_idx = j;
+                mm.img_idx = -1;  // cv::DMatch(query, train, distance) (FeatureMatcher.cpp:159-162)
+                mm.distance = (float)rowd[i];
+                o[pos] = mm;
+            }
+        }
+        base += total;
+        __syncthreads();
+    }
+    if (tid == 0) n_out[pair] = base;
+}
+
 template <bool PADMASK>
 __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A,
                                                    const uint32_t* __restrict__ nA,
@@ -603,17 +877,24 @@ __global__ __launch_bounds__(MT) void match_kernel(const uint8_t* __restrict__ A
 mage_status match_batch(const uint8_t* dA, long long aPitch, const uint32_t* dnA, const uint8_t* dB,
                         long long bPitch, const uint32_t* dnB, uint32_t pairs, int maxDist,
                         int minDiff, mage_dmatch* dOut, uint32_t cap, uint32_t* dN,
-                        uint32_t* dStatus, hipStream_t st)
+                        uint32_t* dStatus, hipStream_t st, long long nbMax)
 {
-    void* rows = stream_scratch(st, STREAM_MATCH_ROWS, (size_t)pairs * NMAX * sizeof(int2));
-    if (!rows) return MAGE_ENOMEM;
     MatchParams mp{};
-    mp.rows = static_cast<int2*>(rows);
     mp.max_dist = maxDist;
     mp.min_diff = minDiff;
     mp.out_cap = cap;
     mp.a_pitch = aPitch;
     mp.b_pitch = bPitch;
+    // the fp4 kernel when every pair's B side provably fits it (nbMax: the pair pitch's capacity,
+    // or the host-known count)
+    if (maxDist < 128 && minDiff >= 1 && nbMax > 0 && nbMax <= FNB) {
+        launch("match.two_way", match_fp4_kernel, dim3(pairs), dim3(FT), 0, st, dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
+        MAGE_HIP(hipGetLastError());
+        return MAGE_OK;
+    }
+    void* rows = stream_scratch(st, STREAM_MATCH_ROWS, (size_t)pairs * NMAX * sizeof(int2));
+    if (!rows) return MAGE_ENOMEM;
+    mp.rows = static_cast<int2*>(rows);
     {
         launch("match.two_way", maxDist < 128 ? match_kernel<false> : match_kernel<true>, dim3(pairs), dim3(MT), 0, st,
                dA, dnA, dB, dnB, mp, dOut, dN, dStatus);
@@ -646,7 +927,8 @@ mage_status mage_hamming_match_batch_device(const uint8_t* d_desc_a, int64_t a_p
     void* status = mage::stream_scratch((hipStream_t)stream, mage::STREAM_MATCH_STATUS, 4);
     if (!status) return MAGE_ENOMEM;
     return mage::match_batch(d_desc_a, a_pitch, d_n_a, d_desc_b, b_pitch, d_n_b, pairs, max_distance,
-                             min_difference, d_out, cap, d_n, static_cast<uint32_t*>(status), (hipStream_t)stream);
+                             min_difference, d_out, cap, d_n, static_cast<uint32_t*>(status), (hipStream_t)stream,
+                             b_pitch > 0 ? b_pitch / 32 : -1);
 }
 
 mage_status mage_hamming_match(const uint8_t* desc_a, uint32_t n_a, const uint8_t* mask_a,
@@ -689,7 +971,7 @@ mage_status mage_hamming_match(const uint8_t* desc_a, uint32_t n_a, const uint8_
     uint32_t* dn = reinterpret_cast<uint32_t*>(d + oc);
     r = mage::match_batch(reinterpret_cast<const uint8_t*>(d + oa), 0, dn, reinterpret_cast<const uint8_t*>(d + ob), 0,
                           dn + 1, 1, max_distance, min_difference, reinterpret_cast<mage_dmatch*>(d + oo),
-                          (uint32_t)ocap, dn + 2, dn + 3, S.st);
+                          (uint32_t)ocap, dn + 2, dn + 3, S.st, (long long)nb);
     if (r != MAGE_OK) return r;
     MAGE_HIP(hipMemcpyAsync(h + oc, d + oc, total_bytes - oc, hipMemcpyDeviceToHost, S.st));
     MAGE_HIP(hipStreamSynchronize(S.st));

@@ -112,6 +112,34 @@ def test_reference_facade_setters(gpu):
     assert np.allclose(R @ R.T, np.eye(3), atol=1e-5)
 
 
+def test_repeated_setters_before_a_step(gpu):
+    """Setters called several times before a step (small copies are queued until the step):
+    a growing buffer, then the same size with other data, must give exactly the last call's
+    problem (queued copies into a freed or re-queued destination)."""
+    import dataclasses
+
+    g = synth.ba_graph(cameras=12, points=400, obs_per_point=8, fixed_cameras=3, seed=1)
+    half = len(g.cam) // 2
+    g_half = dataclasses.replace(g, uv=g.uv[:half], cam=g.cam[:half], pt=g.pt[:half], info=g.info[:half])
+    rng = np.random.default_rng(5)
+    g_other = dataclasses.replace(g, uv=(g.uv + rng.normal(0, 3, g.uv.shape)).astype(g.uv.dtype),
+                                  points=(g.points + 0.05).astype(g.points.dtype),
+                                  pos=(g.pos + 0.01).astype(g.pos.dtype))
+    b = bundler.BundlerLib()
+    for gg in (g_half, g_other, g):  # grow, then same size with different data
+        b.set_graph(gg)
+        b._upload()
+    ref = bundler.BundlerLib()
+    ref.set_graph(g)
+    for _ in range(3):
+        ms_b, out_b = b.step([1.8], 7.25)
+        ms_r, out_r = ref.step([1.8], 7.25)
+        assert ms_b == ms_r and np.array_equal(out_b, out_r)
+    qb, pb = b.state()
+    qr, pr = ref.state()
+    assert np.array_equal(qb, qr) and np.array_equal(pb, pr)
+
+
 def test_tethers(gpu):
     # distance / rotation / transform tethers (BundlerLib.cpp:22-88, 311-350), incl. an inactive
     # fixed-fixed pair and tethers to fixed cameras
