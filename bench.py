@@ -56,6 +56,10 @@ def parse():
     p.add_argument("--pipelined-streams", type=int, default=2,
                    help="also report the ORB rate pipelined over this many streams (0: skip; 1 GPU runs only)")
     p.add_argument("--no-all-cores", action="store_true", help="skip the all-host-cores CPU baselines")
+    p.add_argument("--no-rbrief31", action="store_true", help="skip the rBRIEF-31 variant leg")
+    p.add_argument("--rbrief31-steps", type=int, default=10)
+    p.add_argument("--orb-variant", default="c2", choices=["c2", "rbrief31"],
+                   help="profiling only: the variant the ORB leg runs (the headline is c2)")
     p.add_argument("--ba-many-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
     p.add_argument("--cpu-dry-run", action="store_true", help="gloo rehearsal of the multi-rank flow (tests)")
@@ -93,16 +97,16 @@ def load_pmc(kernel, field="hbm_bytes_per_launch", summary="pmc_summary.json"):
     meta = d.get("_meta", {})
     sha, now = meta.get("kernel_sources_sha"), kernel_sources_sha()
     if sha != now:
-        return None, f"stale: profiles/pmc_summary.json was collected on kernel sources {sha}, these are {now}"
+        return None, f"stale: profiles/{summary} was collected on kernel sources {sha}, these are {now}"
     return d.get(kernel, {}).get(field), \
-        f"profiles/pmc_summary.json ({meta.get('tag')}, kernel sources {sha})"
+        f"profiles/{summary} ({meta.get('tag')}, kernel sources {sha})"
 
 
-def cpu_orb_baseline(args, budget_s):
+def cpu_orb_baseline(args, budget_s, okw=None):
     from mageslam_amd import synth
     from oracle import oracle as O
 
-    s = O.default_settings(args.features)
+    s = O.default_settings(args.features, **(okw or {}))
     _, _, prev = O.orb_detect(synth.frame(0, args.width, args.height), s)  # untimed warm-up
     n_timed, el = 0, 0.0
     while el < budget_s or n_timed < 2:
@@ -113,10 +117,10 @@ def cpu_orb_baseline(args, budget_s):
         el += time.perf_counter() - t0
         prev = d
         n_timed += 1
-    return {"value": n_timed / el, "unit": "frames/s", "cores": 1, "kind": "port",
+    return {"value": n_timed / el, "unit": "frames/s", "cores": 1, "kind": "port", "build": ORACLE_BUILD[0],
             "sample": f"{n_timed} consecutive {args.width}x{args.height} synthetic frames, oracle "
-                      f"extract ({args.features} features) + match vs previous frame, single thread, "
-                      f"{el:.1f} s"}
+                      f"extract ({args.features} features{', ' + str(okw) if okw else ''}) + match vs previous "
+                      f"frame, single thread, {el:.1f} s"}
 
 
 def host_info() -> dict:
@@ -137,12 +141,25 @@ def median_of(fn, budget_s, k=5):
     runs = [fn(budget_s / k) for _ in range(k)]
     vals = [r["value"] for r in runs]
     med = sorted(range(k), key=lambda i: vals[i])[k // 2]
-    return dict(runs[med], statistic=f"median of {k} samples", samples=vals, host=host_info())
+    return dict(runs[med], statistic=f"median of {k} samples", samples=vals, host=host_info(), build=ORACLE_BUILD[0])
 
 
 def host_threads() -> int:
-    """The host cores this process may use, capped at the box's CPU share for one GPU (16)."""
+    """The host cores the all-cores CPU legs use: the box's CPU share for one GPU, 16 (the GPU
+    pool's rule for one-GPU boxes: worker pools sized to 16, OMP_NUM_THREADS=16), or fewer when
+    the affinity mask allows fewer.  nproc / usable cores are recorded beside it (host_info)."""
     return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+# the oracle build the CPU legs time (bench.py switches to the -march=native + SSE2-FAST build
+# before the first CPU leg: SURVEY.md §8(d), and the reference's x64 build runs SSE2 FAST)
+ORACLE_BUILD = ["portable"]
+
+
+def use_native_oracle():
+    from oracle import oracle as O
+
+    ORACLE_BUILD[0] = O.use_native_build()
 
 
 def _per_thread(fn, n):
@@ -178,12 +195,24 @@ def cpu_orb_baseline_all(args, budget_s):
 
     res = _per_thread(work, n)
     return {"value": sum(k / el for k, el in res), "unit": "frames/s", "cores": n, "kind": "port",
+            "build": ORACLE_BUILD[0],
             "sample": f"{n} threads, each alternating two consecutive {args.width}x{args.height} synthetic frames "
                       f"(extract + match vs its previous frame) for ~{budget_s:.0f} s; {sum(k for k, _ in res)} "
                       f"frames in total; sum of per-thread rates"}
 
 
-def run_orb(args, rank, world, local_rank, torch, dist):
+# rBRIEF-31 variant (OpenCVModified.cpp:833, 867-871): 4 pyramid levels,
+# 31x31 patches, intensity-centroid orientation
+RBRIEF31 = dict(nlevels=4, patchSize=31, useOrientation=True)
+RBRIEF31_ORACLE = dict(nlevels=4, patch_size=31, use_orientation=1)
+
+
+def pyramid_level_bytes(w, h, levels, scale=1.5):
+    """Bytes of pyramid levels 1.. (OpenCVModified.cpp:785-842: size = cvRound(W / scale^l))."""
+    return sum(int(round(w / scale ** l)) * int(round(h / scale ** l)) for l in range(1, levels))
+
+
+def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
     from mageslam_amd import _lib, matcher, multigpu, orb, synth
 
     W, H, N, B = args.width, args.height, args.features, args.batch
@@ -196,7 +225,8 @@ def run_orb(args, rank, world, local_rank, torch, dist):
     # last frame of batch s-1 (an event on s-1's extraction).
     NSTR = max(1, args.streams)
     NSET = NSTR + 1 if NSTR > 1 else 1
-    dets = [orb.OrbDetector(nfeatures=N, device=local_rank) for _ in range(NSTR)]
+    det_kw = RBRIEF31 if variant == "rbrief31" else {}
+    dets = [orb.OrbDetector(nfeatures=N, device=local_rank, **det_kw) for _ in range(NSTR)]
     det = dets[0]
     frames = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
     orb.synth_frames_device(frames, F, W, H, 0, multigpu.sequence_seed(synth.FRAME_SEED, rank), stream=stream)
@@ -276,17 +306,26 @@ def run_orb(args, rank, world, local_rank, torch, dist):
     if orb_k:
         dom = max(orb_k, key=lambda k: orb_k[k]["avg_ms"] * orb_k[k]["launches"])
         per_frame = orb_bytes_per_frame(W, H, N)
+        if variant == "rbrief31":  # + each pyramid level written once and read once
+            per_frame += 2 * pyramid_level_bytes(W, H, RBRIEF31["nlevels"])
         avg_s = orb_k[dom]["avg_ms"] / 1000.0
         achieved = per_frame * B / avg_s / 1e9
         # traffic: 2 x FETCH_SIZE + WRITE_SIZE (the guide's gfx950 correction of the wide-stream
         # read counter), per steady-state launch of the committed profile of these kernel sources
-        traffic, traffic_source = load_pmc(dom, "hbm_bytes_per_launch_fetch_x2")
-        traffic_raw, _ = load_pmc(dom, "hbm_bytes_per_launch")
-        valu, _ = load_pmc(dom, "valu_issue_frac")
-        prof_us, _ = load_pmc(dom, "avg_us_steady")
+        psum = "pmc_summary_rbrief31.json" if variant == "rbrief31" else "pmc_summary.json"
+        traffic, traffic_source = load_pmc(dom, "hbm_bytes_per_launch_fetch_x2", psum)
+        traffic_raw, _ = load_pmc(dom, "hbm_bytes_per_launch", psum)
+        valu, _ = load_pmc(dom, "valu_issue_frac", psum)
+        prof_us, _ = load_pmc(dom, "avg_us_steady", psum)
         step_s = el_max / args.steps
+        frac_rocprof = None if prof_us is None else per_frame * B / (prof_us * 1e-6) / 1e9 / HBM_PEAK_GBS
         res["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                           # the same fraction priced on the committed rocprofv3 trace's steady-state
+                           # average, and on the whole step (top-level scalars: see "rocprof" / "step")
+                           "frac_rocprof": frac_rocprof,
+                           "frac_step": per_frame * B / step_s / 1e9 / HBM_PEAK_GBS,
+                           "valu_issue_frac": valu,
                            "traffic_raw_fetch": traffic_raw,
                            "traffic_source": traffic_source + " (2 x FETCH_SIZE + WRITE_SIZE)",
                            "algorithmic_bytes_per_launch": per_frame * B,
@@ -297,7 +336,7 @@ def run_orb(args, rank, world, local_rank, torch, dist):
                            # the warm-up), so frac can be recomputed from profiles/
                            "rocprof": None if prof_us is None else {
                                "avg_launch_ms": prof_us / 1000.0,
-                               "frac": per_frame * B / (prof_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                               "frac": frac_rocprof,
                                "source": traffic_source.split(" (")[0] + ", avg_us_steady"},
                            # whole step (extract + match of B frames) against the same bytes
                            "step": {"algorithmic_bytes": per_frame * B, "ms": 1000 * step_s,
@@ -510,9 +549,12 @@ def run_pose(args, rank, world, local_rank, torch, dist):
         # compulsory bytes per launch: observations (point 12 + uv 8 + info 4 + flag 1) and per-problem
         # pose in/out (12 + 36 + 16 in, 12 + 36 + 56 + 4 + 8 out)
         byts = E * 25 + K * (64 + 116)
+        # counters from the per-row profile (tools/bench_rows.py pose leg: this launch alone)
+        traffic, tsrc = load_pmc("pose.ba", "hbm_bytes_per_launch_fetch_x2", "pmc_summary_rows.json")
         res["roofline"] = {"bound": "hbm", "kernel": "ba.pose_batch", "achieved": byts / avg_s / 1e9,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": byts / avg_s / 1e9 / HBM_PEAK_GBS,
-                           "traffic": None, "algorithmic_bytes_per_launch": byts, "avg_launch_ms": v / c}
+                           "traffic": traffic, "traffic_source": tsrc + " (2 x FETCH_SIZE + WRITE_SIZE)",
+                           "algorithmic_bytes_per_launch": byts, "avg_launch_ms": v / c}
     return res, pb
 
 
@@ -930,7 +972,15 @@ def main():
     torch.cuda.set_device(local_rank)
     dist = multigpu.init("nccl", local_rank)
 
-    orb_res = run_orb(args, rank, world, local_rank, torch, dist)
+    orb_res = run_orb(args, rank, world, local_rank, torch, dist,
+                      variant=None if args.orb_variant == "c2" else args.orb_variant)
+    r31_res = None
+    if world == 1 and not args.no_rbrief31 and args.orb_variant == "c2":
+        import copy
+
+        ra = copy.copy(args)
+        ra.steps, ra.streams = args.rbrief31_steps, 1
+        r31_res = run_orb(ra, rank, world, local_rank, torch, dist, variant="rbrief31")
     pipe_res = None
     if world == 1 and args.pipelined_streams > 1 and args.streams == 1:
         import copy
@@ -982,6 +1032,16 @@ def main():
             out["failed_legs"] = failed
         if pipe_res is not None:
             out["pipelined"] = pipe_res
+        if r31_res is not None:
+            out["rbrief31"] = {
+                "metric": "frames/sec ORB extract+match @720p, rBRIEF-31 variant (4 levels x 1.5, 31x31 patch, "
+                          "orientation)", "value": r31_res["value"], "unit": "frames/s",
+                "ms_per_step": r31_res["ms_per_step"], "steps": args.rbrief31_steps,
+                "config": {"workload": f"C2 frames ({args.width}x{args.height}, {args.features} features/frame) with "
+                                       "NumLevels 4, PatchSize 31, UseOrientation (OpenCVModified.cpp:833, 867-871)",
+                           "frames_per_step": args.batch},
+                "roofline": r31_res.get("roofline"), "kernels": r31_res["kernels"],
+                "mean_keypoints": r31_res["mean_keypoints"], "mean_matches": r31_res["mean_matches"]}
         if ba_res is not None:
             out["ba"] = ba_res
         if pose_res is not None:
@@ -989,7 +1049,12 @@ def main():
         if track_res is not None:
             out["tracking"] = track_res
         if world == 1 and not args.no_cpu_baseline:
+            use_native_oracle()
             out["cpu_baseline"] = median_of(lambda b: cpu_orb_baseline(args, b), args.cpu_sample_s)
+            if r31_res is not None:
+                c31 = median_of(lambda b: cpu_orb_baseline(args, b, RBRIEF31_ORACLE), args.cpu_sample_s / 2)
+                out["rbrief31"]["cpu_baseline"] = c31
+                out["rbrief31"]["vs_cpu"] = out["rbrief31"]["value"] / c31["value"]
             if not args.no_all_cores:
                 out["cpu_baseline_all_cores"] = cpu_orb_baseline_all(args, args.cpu_sample_s / 2)
                 out["vs_cpu_all_cores"] = out["value"] / out["cpu_baseline_all_cores"]["value"]
@@ -1022,6 +1087,7 @@ def main():
                 pose_res["cpu_baseline"] = cp
                 pose_res["vs_cpu"] = pose_res["value"] / cp["value"]
             out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+            out["cpu_baseline_build"] = ORACLE_BUILD[0]
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

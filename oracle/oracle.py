@@ -61,6 +61,28 @@ def lib() -> C.CDLL:
     return _lib
 
 
+def use_native_build() -> str:
+    """bench.py's CPU baselines only: rebuild the oracle with -march=native for THIS host (in a
+    temporary directory, never the prebuilt tree) and switch every later call to it, with the
+    FAST score map of the reference's x64 build (SSE2, fast_sse2.c).  Returns a description of
+    the build used; falls back to the portable build (and says so) when gcc fails here."""
+    global _lib
+    import tempfile
+
+    d = tempfile.mkdtemp(prefix="mage_oracle_native_")
+    r = subprocess.run(["make", "-s", "-C", str(HERE), "native", f"NATIVE_DIR={d}"], capture_output=True, text=True)
+    so = Path(d) / "libmage_oracle_native.so"
+    if r.returncode == 0 and so.exists():
+        _lib = C.CDLL(str(so))
+        _declare(_lib)
+        desc = "gcc -O3 -march=native (built on this host)"
+    else:
+        lib()
+        desc = f"portable -O3 -march=x86-64-v2 build (native build failed: {r.stderr.strip()[-200:]})"
+    _lib.oracle_set_fast_sse2(1)
+    return desc + ", FAST score map of the reference's x64 SSE2 build"
+
+
 def _p(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
 
@@ -69,6 +91,7 @@ def _declare(L):
     vp, i32, u32, f32 = C.c_void_p, C.c_int, C.c_uint32, C.c_float
     L.oracle_fast_score_map.argtypes = [vp, i32, i32, i32, i32, vp]
     L.oracle_fast_score_map_sse2.argtypes = [vp, i32, i32, i32, i32, vp, vp]
+    L.oracle_set_fast_sse2.argtypes = [i32]
     L.oracle_gaussian_blur.argtypes = [vp, i32, i32, i32, i32, vp]
     L.oracle_gaussian_taps.argtypes = [i32, C.c_double, vp]
     L.oracle_orb_detect.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, u32, C.POINTER(u32)]

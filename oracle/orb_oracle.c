@@ -130,10 +130,20 @@ typedef struct {
 
 /* FAST with strict 3x3 NMS, emission in raster order (OpenCVModified.cpp:1489-1509).
  * Returns the candidate count; `out` must hold w*h/4+w+h entries. */
+/* The score map of the reference's x64 build (SSE2 cornerScore + row loop, fast_sse2.c; equal
+ * to the scalar one, tests/test_oracle.py) when set: bench.py's CPU baseline times that build. */
+static int g_fast_sse2 = 0;
+void oracle_fast_score_map_sse2(const uint8_t* img, int w, int h, int stride, int threshold, uint8_t* score,
+                                int* simd_cols);
+void oracle_set_fast_sse2(int on) { g_fast_sse2 = on != 0; }
+
 static int fast_nms(const uint8_t* img, int w, int h, int stride, int t, uint8_t* score,
                     cand_t* out)
 {
-    oracle_fast_score_map(img, w, h, stride, t, score);
+    if (g_fast_sse2)
+        oracle_fast_score_map_sse2(img, w, h, stride, t, score, NULL);
+    else
+        oracle_fast_score_map(img, w, h, stride, t, score);
     int n = 0;
     for (int y = 3; y < h - 3; y++) {
         for (int x = 3; x < w - 3; x++) {

@@ -11,6 +11,8 @@ fraction.  Run under `rocprofv3 --kernel-trace --stats` for the committed summar
   indexed   OnlineBow FindLeafNode + IndexedMatch (FeatureMatcher.cpp:192-292): 256 pairs, default tree
   remap     UndistortImage (ImagePreprocessor.cpp:106-120): 256 x 720p Rational6k frames
   kpundist  UndistortKeypoints (OrbFeatureDetector.cpp:30-62): 256 x 2000 keypoints
+  pose      batched pose-only BA (TrackLocalMap::OptimizeCameraPose, TrackLocalMap.cpp:421-501): bench.py's
+            pose leg (2048 problems x ~600 observations, 3 LM steps) alone, for its own counters
   train     OnlineBow::CreateTree (OnlineBow.cpp:325-337): TrainingFrames (15) x 2000 descriptors,
             2 levels x 6 branches, <= 12 Kmean iterations (host-driven: wall time per tree)
 """
@@ -79,7 +81,7 @@ def leg(name, unit, units_per_launch, wall, kern, tag, bytes_per_launch):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--legs", default="radius,indexed,remap,kpundist,train")
+    p.add_argument("--legs", default="radius,indexed,remap,kpundist,pose,train")
     p.add_argument("--batch", type=int, default=256)
     p.add_argument("--iters", type=int, default=10)
     a = p.parse_args()
@@ -147,6 +149,26 @@ def main():
         wall, kern = timed(lib, kpundist, a.iters, torch)
         leg("a12 UndistortKeypoints", "frames/s", B, wall, kern, "orb.undistort", B * N * 28 * 2)
 
+    if "pose" in legs:
+        from mageslam_amd import bundler
+
+        pb = synth.pose_batch(problems=2048, obs=600, seed=synth.BA_SEED + 1)
+        K, E = len(pb.pos), int(pb.obs_start[-1])
+        T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).cuda()  # noqa: E731
+        args_in = (T(pb.pos, np.float32), T(pb.r9, np.float32), T(pb.intr, np.float32),
+                   T(pb.obs_start.astype(np.int32), np.int32), T(pb.points, np.float32), T(pb.uv, np.float32),
+                   T(pb.info, np.float32))
+        outs = (torch.empty((K, 3), dtype=torch.float32, device="cuda"),
+                torch.empty((K, 9), dtype=torch.float32, device="cuda"),
+                torch.empty((K, 7), dtype=torch.float64, device="cuda"), torch.empty(E, dtype=torch.uint8, device="cuda"),
+                torch.empty(K, dtype=torch.float32, device="cuda"), torch.empty((K, 2), dtype=torch.int32, device="cuda"))
+
+        def pose():
+            bundler.pose_batch_device(K, *args_in, 3, 4.0, 36.0, *outs)
+
+        wall, kern = timed(lib, pose, a.iters, torch)
+        # bench.py run_pose: observations (point 12 + uv 8 + info 4 + flag 1), pose in / out per problem
+        leg("f2 pose-only BA (batched)", "problems/s", K, wall, kern, "ba.pose_batch", E * 25 + K * (64 + 116))
     if "train" in legs:
         tcnt = cnt[:15].cpu().numpy()
         tdesc = np.concatenate([desc[i, : tcnt[i]].cpu().numpy() for i in range(15)])

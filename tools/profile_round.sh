@@ -23,12 +23,15 @@ run_set() {  # <out dir> <command...>
 OUT=gpurun_out/prof_$TAG
 ORB=gpurun_out/prof_${TAG}_orb
 ROWS=gpurun_out/prof_${TAG}_rows
-ORB_CMD="python3 bench.py --steps 10 --warmup 3 --no-ba --no-pose --no-tracking --no-cpu-baseline --pipelined-streams 0 --no-all-cores"
+ORB_CMD="python3 bench.py --steps 10 --warmup 3 --no-ba --no-pose --no-tracking --no-cpu-baseline --pipelined-streams 0 --no-all-cores --no-rbrief31"
+ORB31=gpurun_out/prof_${TAG}_orb31
+ORB31_CMD="python3 bench.py --steps 10 --warmup 3 --no-ba --no-pose --no-tracking --no-cpu-baseline --pipelined-streams 0 --no-all-cores --orb-variant rbrief31"
 if [ "$2" = collect ]; then
     python3 tools/rocprof_summary.py $OUT $TAG "python bench.py" 3 > /dev/null
     cp $OUT/trace/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
     cp profiles/${TAG}_pmc_summary.json profiles/pmc_summary_ba.json  # BA kernels' counters (bench.py)
     python3 tools/rocprof_summary.py $ROWS ${TAG}_rows "python tools/bench_rows.py" > /dev/null
+    cp profiles/${TAG}_rows_pmc_summary.json profiles/pmc_summary_rows.json  # pose-only BA counters (bench.py)
     cp $ROWS/trace/run_kernel_stats.csv profiles/${TAG}_rows_kernel_stats.csv
     cp $ROWS/trace.json profiles/${TAG}_rows.jsonl
     cp $OUT/bench_final.json profiles/${TAG}_bench.json
@@ -39,6 +42,11 @@ if [ "$2" = collect ]; then
     cp $ORB/trace/run_kernel_stats.csv profiles/${TAG}_orb_kernel_stats.csv
     cp $ORB/trace.json profiles/${TAG}_orb_bench.json
     cp profiles/${TAG}_orb_pmc_summary.json profiles/pmc_summary.json
+    # the rBRIEF-31 variant (4 levels, patch 31, orientation) alone: profiles/pmc_summary_rbrief31.json
+    python3 tools/rocprof_summary.py $ORB31 ${TAG}_orb31 "${ORB31_CMD#python3 }" 3 > /dev/null
+    cp $ORB31/trace/run_kernel_stats.csv profiles/${TAG}_orb31_kernel_stats.csv
+    cp $ORB31/trace.json profiles/${TAG}_orb31_bench.json
+    cp profiles/${TAG}_orb31_pmc_summary.json profiles/pmc_summary_rbrief31.json
     exit 0
 fi
 # optional phase (one gpurun call each when the whole round would not fit one call's limit):
@@ -47,9 +55,10 @@ PHASE=${2:-all}
 if [ "$PHASE" = all ] || [ "$PHASE" = main ]; then
     run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores
     run_set $ORB $ORB_CMD
+    run_set $ORB31 $ORB31_CMD
 fi
 if [ "$PHASE" = all ] || [ "$PHASE" = rows ]; then
     run_set $ROWS python3 tools/bench_rows.py
     mkdir -p $OUT
-    timeout -k 10 400 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
+    timeout -k 10 600 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
 fi

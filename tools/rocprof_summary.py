@@ -36,7 +36,7 @@ VALU_PEAK_G = 1024 * 2.4 / 4.0  # G wave64 VALU instructions / s
 KERNEL_TAG = {
     "fast_nms_kernel": "orb.fast_nms", "select_kernel": "orb.select", "fast_redo_kernel": "orb.fast_redo",
     "select_redo_kernel": "orb.select_redo", "describe_kernel": "orb.describe", "describe_blurred_kernel": "orb.describe",
-    "match_kernel": "match.two_way", "build_schur": "ba.build_schur", "cholesky_solve": "ba.cholesky_solve",
+    "match_kernel": "match.two_way", "match_fp4_kernel": "match.two_way", "build_schur": "ba.build_schur", "cholesky_solve": "ba.cholesky_solve",
     "point_linearize": "ba.point_linearize", "cam_linearize": "ba.cam_linearize",
     "point_backsub": "ba.point_backsub", "edge_schur": "ba.edge_schur", "chol_tiles": "ba.cholesky_solve", "drop_edges": "ba.drop_edges", "export_state": "ba.export_state", "update_state": "ba.update_state",
     "outlier_pass": "ba.outlier_pass", "reduce3": "ba.reduce", "linearize_finish": "ba.linearize_finish",
