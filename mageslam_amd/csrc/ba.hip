@@ -32,7 +32,6 @@
 // then the StepBundleAdjustment post-pass (BundlerLib.cpp:385-446): outlier indices from the
 // speculative (or a fresh) outlier_pass, drop_edges clears their `active` byte.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <atomic>
@@ -2031,6 +2030,93 @@ __global__ __launch_bounds__(256) void init_camcsr(int E, int C, int nbm, const 
     }
 }
 
+// ---- Stable counting sort by a small key (the camera-CSR order of the point-CSR entries, and the
+// Schur product lists by pair key): per 1024-entry block a key histogram (csort_count), one
+// workgroup turning the histograms into every block's first output slot per key (csort_scan), then
+// each block scatters its entries in order (csort_scatter): ranks inside a wave from a match of the
+// key bits, across the block's waves by LDS counters taken wave after wave.  Keys < nkeys.
+constexpr int CS_BLOCK = 1024;
+constexpr int CS_WAVES = CS_BLOCK / kWave;
+constexpr int CS_MAX_KEYS = 12288;  // per-key counters in LDS (Schur pair keys: nb^2 <= 96^2)
+
+template <typename KeyT>
+__global__ __launch_bounds__(CS_BLOCK) void csort_count(int n, int nkeys, const KeyT* __restrict__ key,
+                                                        int* __restrict__ hist)
+{
+    __shared__ int h[CS_MAX_KEYS];
+    for (int c = threadIdx.x; c < nkeys; c += CS_BLOCK) h[c] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * CS_BLOCK + threadIdx.x;
+    if (i < n) atomicAdd(&h[(int)key[i]], 1);
+    __syncthreads();
+    int* row = hist + (size_t)blockIdx.x * nkeys;
+    for (int c = threadIdx.x; c < nkeys; c += CS_BLOCK) row[c] = h[c];
+}
+
+// One workgroup: hist[b][k] (block b's count of key k) becomes block b's first output slot for k
+// (keys in ascending order, blocks in order inside a key).
+__global__ __launch_bounds__(1024) void csort_scan(int nblocks, int nkeys, int* __restrict__ hist)
+{
+    __shared__ int tot[CS_MAX_KEYS];
+    for (int c = threadIdx.x; c < nkeys; c += 1024) {
+        int s = 0;
+        for (int b = 0; b < nblocks; b++) s += hist[(size_t)b * nkeys + c];
+        tot[c] = s;
+    }
+    __syncthreads();
+    block_scan_1024<int>(nkeys, [&](int c) { return tot[c]; }, [&](int c, int x) { tot[c] = x; });
+    __syncthreads();
+    for (int c = threadIdx.x; c < nkeys; c += 1024) {
+        int run = tot[c];
+        for (int b = 0; b < nblocks; b++) {
+            int* h = hist + (size_t)b * nkeys + c;
+            const int t = *h;
+            *h = run;
+            run += t;
+        }
+    }
+}
+
+template <typename KeyT, typename ValT>
+__global__ __launch_bounds__(CS_BLOCK) void csort_scatter(int n, int nkeys, int kbits, const KeyT* __restrict__ key,
+                                                          const ValT* __restrict__ val, const int* __restrict__ hist,
+                                                          KeyT* __restrict__ key_out, ValT* __restrict__ val_out)
+{
+    __shared__ int cnt[CS_MAX_KEYS];
+    const int* row = hist + (size_t)blockIdx.x * nkeys;
+    for (int c = threadIdx.x; c < nkeys; c += CS_BLOCK) cnt[c] = row[c];
+    const int i = blockIdx.x * CS_BLOCK + threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    const bool valid = i < n;
+    const int k = valid ? (int)key[i] : -1;
+    // lanes of this wave holding the same key
+    unsigned long long peers = __ballot(valid);
+    for (int b = 0; b < kbits; b++) {
+        const bool bit = ((k >> b) & 1) != 0;
+        const unsigned long long m = __ballot(bit);
+        peers &= bit ? m : ~m;
+    }
+    const int rank = __popcll(peers & ((1ull << lane) - 1ull));
+    const int leader = valid ? __ffsll((long long)peers) - 1 : lane;
+    int base = 0;
+    __syncthreads();
+    for (int w = 0; w < CS_WAVES; w++) {  // waves in order: the block's entries keep their order per key
+        if (wave == w && valid && rank == 0) base = atomicAdd(&cnt[k], __popcll(peers));
+        __syncthreads();
+    }
+    base = __shfl(base, leader);
+    if (valid) {
+        key_out[base + rank] = (KeyT)k;
+        val_out[base + rank] = val[i];
+    }
+}
+
+// Exclusive prefix sum of n ints by one workgroup (out may not alias in).
+__global__ __launch_bounds__(1024) void scan_exclusive(int n, const int* __restrict__ in, int* __restrict__ out)
+{
+    block_scan_1024<int>(n, [&](int i) { return in[i]; }, [&](int i, int x) { out[i] = x; });
+}
+
 // ---- Schur product lists built on the device (SparseOptimizer::initializeOptimization + g2o's
 // BlockSolver::buildStructure: which pose blocks couple through a shared point) --------------
 // Per free point: its edges in free camera blocks as (block, camera-CSR position), stably sorted
@@ -2388,7 +2474,7 @@ struct BundleAdjuster {
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
-        d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_cub, d_kdst, d_rblk, d_sbits, d_srank, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
+        d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_chist, d_kdst, d_rblk, d_sbits, d_srank, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
         d_sfinish, d_epos, d_chi_lin, d_livebuf, d_removed, d_camflag, d_ikeys, d_ivals, d_isum, d_iacc, d_ctab;
     bool iacc_clean = false;  // d_iacc is all zero (see initialize())
     // outlier lists of the speculative / final post-pass (2 x E entries), written by the kernels
@@ -2435,7 +2521,7 @@ struct BundleAdjuster {
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
-                        &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_cub, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
+                        &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_chist, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf, &d_removed, &d_camflag,
                         &d_ikeys, &d_ivals, &d_isum, &d_iacc, &d_ctab})
             b->release();
@@ -2571,6 +2657,24 @@ struct BundleAdjuster {
         return MAGE_OK;
     }
 
+    // Stable sort of n (key, value) entries by key (< nkeys) with the csort_* kernels.
+    template <typename KeyT, typename ValT>
+    mage_status stable_key_sort(const KeyT* kin, const ValT* vin, KeyT* kout, ValT* vout, int n, int nkeys)
+    {
+        if (n <= 0) return MAGE_OK;
+        MAGE_REQUIRE(nkeys <= CS_MAX_KEYS, MAGE_EUNSUPPORTED, "sort key range exceeds the LDS counters");
+        const int nblk = (n + CS_BLOCK - 1) / CS_BLOCK;
+        mage_status r;
+        if ((r = d_chist.reserve((size_t)nblk * nkeys * sizeof(int))) != MAGE_OK) return r;
+        int kbits = 1;
+        while ((1 << kbits) < nkeys) kbits++;
+        launch("ba.sort_count", csort_count<KeyT>, dim3(nblk), dim3(CS_BLOCK), 0, st, n, nkeys, kin, d_chist.as<int>());
+        launch("ba.sort_scan", csort_scan, dim3(1), dim3(1024), 0, st, nblk, nkeys, d_chist.as<int>());
+        launch("ba.sort_scatter", csort_scatter<KeyT, ValT>, dim3(nblk), dim3(CS_BLOCK), 0, st, n, nkeys, kbits, kin, vin,
+               (const int*)d_chist.as<int>(), kout, vout);
+        return MAGE_OK;
+    }
+
     // SparseOptimizer::initializeOptimization (+ StepOptimizer::InitializeOptimization):
     // active edges, vertices in the system, CSR structures, covisible camera pairs; iteration 0.
     static size_t nprod_pad(long long n) { return (size_t)((n + 255) / 256 * 256); }
@@ -2588,15 +2692,11 @@ struct BundleAdjuster {
         int* pcnt = d_pcnt.as<int>();
         int* poff = pcnt + Pm;
         int* klen = pcnt + 2 * Pm;
-        size_t tb_scan = 0;
-        MAGE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, pcnt, poff, P, st));
-        if ((r = d_cub.reserve(std::max<size_t>(tb_scan, 16))) != MAGE_OK) return r;
         const unsigned gp = (unsigned)((P + 255) / 256);
         launch("ba.schur_lists", schur_point_lists, dim3(gp), dim3(256), 0, st, P, (const int*)d_pstart.as<int>(),
                (const int*)d_pedges.as<int>(), (const int*)d_ecam.as<int>(), (const int*)d_camh.as<int>(),
                (const int*)d_epos.as<int>(), (const int*)d_ptfree.as<int>(), d_plist.as<int2>(), pcnt, klen);
-        size_t tb = d_cub.bytes;
-        MAGE_HIP(hipcub::DeviceScan::ExclusiveSum(d_cub.ptr, tb, pcnt, poff, P, st));
+        launch("ba.schur_scan", scan_exclusive, dim3(1), dim3(1024), 0, st, P, (const int*)pcnt, poff);
         if ((r = h_kb.reserve((size_t)std::max(2 * nk, 2) * sizeof(int))) != MAGE_OK) return r;
         MAGE_HIP(hipMemcpyAsync(h_kb.ptr, poff + P - 1, sizeof(int), hipMemcpyDeviceToHost, st));
         MAGE_HIP(hipMemcpyAsync(h_kb.as<int>() + 1, pcnt + P - 1, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -2613,16 +2713,10 @@ struct BundleAdjuster {
         uint16_t* kout = kin + pad;
         unsigned long long* vin = d_svals.as<unsigned long long>();
         unsigned long long* vout = vin + pad;
-        int bits = 1;
-        while ((1 << bits) < nk + 1) bits++;
-        size_t tb_sort = 0;
-        MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, kin, kout, vin, vout, (int)nmax, 0, bits, st));
-        if ((r = d_cub.reserve(std::max<size_t>(tb_sort, 16))) != MAGE_OK) return r;
         MAGE_HIP(hipMemsetAsync(d_kb.ptr, 0, (size_t)2 * nk * sizeof(int), st));
         launch("ba.schur_products", schur_point_products, dim3(gp), dim3(256), 0, st, P, nb,
                (const int*)d_pstart.as<int>(), (const int2*)d_plist.as<int2>(), (const int*)poff, (const int*)klen, kin, vin);
-        tb = d_cub.bytes;
-        MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(d_cub.ptr, tb, kin, kout, vin, vout, (int)nmax, 0, bits, st));
+        if ((r = stable_key_sort(kin, vin, kout, vout, (int)nmax, nk)) != MAGE_OK) return r;
         const unsigned gn = (unsigned)((nmax + 255) / 256);
         launch("ba.schur_bounds", schur_list_bounds, dim3(gn), dim3(256), 0, st, (const uint16_t*)kout, (int)nmax, nk,
                d_kb.as<int>());
@@ -2725,8 +2819,6 @@ struct BundleAdjuster {
         int* pacc = d_iacc.as<int>();
         int* cacc = pacc + Pm;
         int* pcur = cacc + Cm;
-        int cbits = 1;
-        while ((1ll << cbits) <= C) cbits++;
         const unsigned ge = (unsigned)((E + 255) / 256);
         if (E > 0)
             launch("ba.init_edges", init_edges, dim3(ge), dim3(256), C <= INIT_LDS_CAMS ? C * 4 : 0, st, E, C,
@@ -2746,12 +2838,8 @@ struct BundleAdjuster {
                 launch("ba.init_psort", init_psort, dim3((unsigned)((P + PSORT_WAVES - 1) / PSORT_WAVES)),
                        dim3(PSORT_WAVES * kWave), 0, st, P, (const int*)d_pstart.as<int>(), (const int*)d_ecam.as<int>(),
                        pcur, d_pedges.as<int>(), k0);
-            size_t tb = 0;
-            MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, (const int*)d_pedges.as<int>(), v0, E, 0, cbits, st));
-            if ((r = d_cub.reserve(std::max<size_t>(tb, 16))) != MAGE_OK) return r;
-            tb = d_cub.bytes;
-            MAGE_HIP(hipcub::DeviceRadixSort::SortPairs(d_cub.ptr, tb, k0, k1, (const int*)d_pedges.as<int>(), v0, E, 0,
-                                                        cbits, st));
+            if ((r = stable_key_sort((const unsigned*)k0, (const int*)d_pedges.as<int>(), k1, v0, E, C + 1)) != MAGE_OK)
+                return r;
             launch("ba.init_camcsr", init_camcsr, dim3(ge), dim3(256), 0, st, E, C, nbm, (const unsigned*)k1, (const int*)v0,
                    (const int*)d_ept.as<int>(), (const int*)d_camh.as<int>(), (const int*)d_ptfree.as<int>(),
                    d_cedges.as<int>(), d_cpt.as<int>(), d_epos.as<int>(), sum, s_rc);

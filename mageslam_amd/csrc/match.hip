@@ -508,9 +508,10 @@ constexpr int NRES = 2560;  // B descriptors kept resident in LDS up to this cou
 // ------------------------------------------------------------------------------------------
 // fp4 matcher (nb <= 2048, maxDist < 128, minDiff >= 1: every practical call, C2 included).
 //
-// 16 waves, one 32-row A tile each per pass (A operands, row states and the accumulator fit
-// 128 VGPRs: 4 waves per SIMD hide the MFMA and LDS latencies that the 8-wave form covered with
-// a two-tile software pipeline).  Per 32x32 tile a lane folds 16 accumulator values:
+// 12 waves (3 per SIMD, 162 VGPRs), two 32-row A tiles each per pass: one column flush (partner
+// half, LDS atomics) serves both tiles.  Measured on C2 (tools/abl.py, 256 pairs): 16 waves x 1
+// tile 0.277 ms, 8 x 2 0.261, 12 x 2 0.228; 16 x 2 spills.  Per 32x32 tile a lane folds 16
+// accumulator values:
 //   * the accumulator starts at C = 1/8 + (0x2400 + code) ulp (per-lane constant registers, code =
 //     63 - the lane's row in the tile), so the result's low 16 bits are the packed key
 //     64 (272 - d) + code, a positive i16 (and positive normal f16), exact: see tile_mfma_fp4;
@@ -522,9 +523,16 @@ constexpr int NRES = 2560;  // B descriptors kept resident in LDS up to this cou
 //     states (which carry the row index) identify j.  Same result as the reference's two
 //     radiusMatch calls + cross-check (FeatureMatcher.cpp:117-167) whenever ties are rejected.
 // ------------------------------------------------------------------------------------------
-constexpr int FW = 16;               // waves
+#ifndef MAGE_FP4_WAVES
+#define MAGE_FP4_WAVES 12
+#endif
+constexpr int FW = MAGE_FP4_WAVES;   // waves
 constexpr int FT = FW * kWave;       // 1024 threads
-constexpr int FROWS = FW * 32;       // A rows per pass
+#ifndef MAGE_FP4_RT
+#define MAGE_FP4_RT 2
+#endif
+constexpr int FRT = MAGE_FP4_RT;     // 32-row A tiles per wave per pass (the column flush serves all)
+constexpr int FROWS = FW * 32 * FRT; // A rows per pass
 constexpr int FSC = FT / 8;          // 128 B columns per LDS stage (one fill dword per thread)
 constexpr int FNT = FSC / 32;        // 4 column tiles per stage
 constexpr int FNB = 2048;            // max B descriptors
@@ -617,22 +625,22 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
     };
 
     for (int pb = 0; pb < (nb > 0 ? na : 0); pb += FROWS) {
-        const int rowbase = pb + wave * 32;
+        const int rowbase = pb + wave * 32 * FRT;
         const bool active = rowbase < na;
-        v4i a[4];
-        {
-            const int i = rowbase + (lane & 31);
-            const uint32_t* ar = Aw + 8 * min(i, na - 1);
-            const uint32_t w0 = ar[(lane >> 5)], w1 = ar[2 + (lane >> 5)], w2 = ar[4 + (lane >> 5)], w3 = ar[6 + (lane >> 5)];
-            const v4i zero = {0, 0, 0, 0};
-            a[0] = i < na ? expand32_fp4(w0) : zero;
-            a[1] = i < na ? expand32_fp4(w1) : zero;
-            a[2] = i < na ? expand32_fp4(w2) : zero;
-            a[3] = i < na ? expand32_fp4(w3) : zero;
-        }
-        uint32_t r1[8], r2[8];
+        v4i a[FRT][4];
 #pragma unroll
-        for (int q = 0; q < 8; q++) r1[q] = r2[q] = NONE16;
+        for (int rt = 0; rt < FRT; rt++) {
+            const int i = rowbase + 32 * rt + (lane & 31);
+            const uint32_t* ar = Aw + 8 * min(i, na - 1);
+            const v4i zero = {0, 0, 0, 0};
+#pragma unroll
+            for (int s = 0; s < 4; s++) a[rt][s] = i < na ? expand32_fp4(ar[2 * s + (lane >> 5)]) : zero;
+        }
+        uint32_t r1[FRT][8], r2[FRT][8];
+#pragma unroll
+        for (int rt = 0; rt < FRT; rt++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r1[rt][q] = r2[rt][q] = NONE16;
         {
             const uint32_t w0 = fetch(0), w1 = nstages > 1 ? fetch(1) : 0u;
             __syncthreads();  // B resident / column states ready; the previous pass is done with the stages
@@ -640,7 +648,8 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
             if (nstages > 1) fill(1, 1, w1);
             __syncthreads();
         }
-        // global key of a local column key: (64 (272 - d) + code) -> ((272 - d) << 16 | 0x7FFF - row)
+        // global key of a local column key (code = 63 - row in the wave's 64 rows):
+        // (64 (272 - d) + code) -> ((272 - d) << 16 | 0x7FFF - row)
         const int kadd = 0x7FFF - rowbase - 63;
         PendingCol16 pc{0, 0, 0, 0, false};
         for (int st = 0; st < nstages; st++) {
@@ -654,23 +663,37 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                     v4i bf[4];
 #pragma unroll
                     for (int s = 0; s < 4; s++) bf[s] = stage[buf][ct][s][lane];
-                    const v16i acc = __builtin_bit_cast(v16i, tile_mfma_k16(a, bf, cc));
-                    uint32_t P[8];
+                    uint32_t c1 = 0, c2 = 0;
 #pragma unroll
-                    for (int q = 0; q < 8; q++)
-                        P[q] = __builtin_amdgcn_perm((uint32_t)acc[2 * q + 1], (uint32_t)acc[2 * q], 0x05040100u);
-                    // row states: the two best distances over the tiles (same code per register)
+                    for (int rt = 0; rt < FRT; rt++) {
+                        const v16i acc = __builtin_bit_cast(v16i, tile_mfma_k16(a[rt], bf, cc));
+                        uint32_t P[8];
 #pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        r2[q] = pkmax(r2[q], pkmin(r1[q], P[q]));
-                        r1[q] = pkmax(r1[q], P[q]);
-                    }
-                    // column: the two best (distance, row) keys of the lane's 16 rows
-                    uint32_t c1 = pkmax(P[0], P[1]), c2 = pkmin(P[0], P[1]);
+                        for (int q = 0; q < 8; q++)
+                            P[q] = __builtin_amdgcn_perm((uint32_t)acc[2 * q + 1], (uint32_t)acc[2 * q], 0x05040100u);
+                        // row states: the two best distances over the tiles (same code per register)
 #pragma unroll
-                    for (int q = 2; q < 8; q++) {
-                        c2 = pkmax(c2, pkmin(c1, P[q]));
-                        c1 = pkmax(c1, P[q]);
+                        for (int q = 0; q < 8; q++) {
+                            r2[rt][q] = pkmax(r2[rt][q], pkmin(r1[rt][q], P[q]));
+                            r1[rt][q] = pkmax(r1[rt][q], P[q]);
+                        }
+                        // column: the two best (distance, row) keys of the lane's 16 rows of this tile
+                        uint32_t t1 = pkmax(P[0], P[1]), t2 = pkmin(P[0], P[1]);
+#pragma unroll
+                        for (int q = 2; q < 8; q++) {
+                            t2 = pkmax(t2, pkmin(t1, P[q]));
+                            t1 = pkmax(t1, P[q]);
+                        }
+                        if (rt == 0) {
+                            c1 = t1;
+                            c2 = t2;
+                        } else {  // rows 32..63 of the wave: codes 32..63 -> 0..31 (bit 5 cleared)
+                            t1 ^= 0x00200020u;
+                            t2 ^= 0x00200020u;
+                            const uint32_t lo = pkmin(c1, t1);
+                            c1 = pkmax(c1, t1);
+                            c2 = pkmax(pkmax(lo, c2), t2);
+                        }
                     }
                     // the partner half-wave holds the same column (rows + 4)
                     {
@@ -696,38 +719,43 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
         }
         if (pc.live) atomicMax(&colM2[pc.j], pc.old > pc.c1 ? pc.c1 : max(pc.old, pc.c2));
         if (active) {
-            // reduce-scatter the 8 packed row states over lane bits 4, 3, 2, then all-reduce over
-            // bits 1, 0: lane (lane & 31) ends with packed state k = (lane & 31) >> 2
 #pragma unroll
-            for (int m = 16, n = 8; m >= 4; m >>= 1, n >>= 1) {
-                const bool up = (lane & m) != 0;
-                const int hf = n / 2;
+            for (int rt = 0; rt < FRT; rt++) {
+                // reduce-scatter the 8 packed row states over lane bits 4, 3, 2, then all-reduce
+                // over bits 1, 0: lane (lane & 31) ends with packed state k = (lane & 31) >> 2
+                uint32_t* R1 = r1[rt];
+                uint32_t* R2 = r2[rt];
 #pragma unroll
-                for (int k = 0; k < hf; k++) {
-                    const uint32_t s1 = up ? r1[k] : r1[k + hf], s2 = up ? r2[k] : r2[k + hf];
-                    uint32_t x1 = up ? r1[k + hf] : r1[k], x2 = up ? r2[k + hf] : r2[k];
-                    const uint32_t o1 = (uint32_t)__shfl_xor((int)s1, m), o2 = (uint32_t)__shfl_xor((int)s2, m);
-                    const uint32_t lo = pkmin(x1, o1);
-                    r1[k] = pkmax(x1, o1);
-                    r2[k] = pkmax(pkmax(lo, x2), o2);
+                for (int m = 16, n = 8; m >= 4; m >>= 1, n >>= 1) {
+                    const bool up = (lane & m) != 0;
+                    const int hf = n / 2;
+#pragma unroll
+                    for (int k = 0; k < hf; k++) {
+                        const uint32_t s1 = up ? R1[k] : R1[k + hf], s2 = up ? R2[k] : R2[k + hf];
+                        const uint32_t x1 = up ? R1[k + hf] : R1[k], x2 = up ? R2[k + hf] : R2[k];
+                        const uint32_t o1 = (uint32_t)__shfl_xor((int)s1, m), o2 = (uint32_t)__shfl_xor((int)s2, m);
+                        const uint32_t lo = pkmin(x1, o1);
+                        R1[k] = pkmax(x1, o1);
+                        R2[k] = pkmax(pkmax(lo, x2), o2);
+                    }
                 }
-            }
 #pragma unroll
-            for (int m = 2; m >= 1; m >>= 1) {
-                const uint32_t o1 = (uint32_t)__shfl_xor((int)r1[0], m), o2 = (uint32_t)__shfl_xor((int)r2[0], m);
-                const uint32_t lo = pkmin(r1[0], o1);
-                r1[0] = pkmax(r1[0], o1);
-                r2[0] = pkmax(pkmax(lo, r2[0]), o2);
-            }
-            if ((lane & 3) == 0) {
-                const int k = (lane & 31) >> 2;
+                for (int m = 2; m >= 1; m >>= 1) {
+                    const uint32_t o1 = (uint32_t)__shfl_xor((int)R1[0], m), o2 = (uint32_t)__shfl_xor((int)R2[0], m);
+                    const uint32_t lo = pkmin(R1[0], o1);
+                    R1[0] = pkmax(R1[0], o1);
+                    R2[0] = pkmax(pkmax(lo, R2[0]), o2);
+                }
+                if ((lane & 3) == 0) {
+                    const int k = (lane & 31) >> 2;
 #pragma unroll
-                for (int e = 0; e < 2; e++) {
-                    const int i = rowbase + acc_row(2 * k + e) + 4 * (lane >> 5);
-                    const int k1 = e ? hi16s(r1[0]) : lo16s(r1[0]), k2 = e ? hi16s(r2[0]) : lo16s(r2[0]);
-                    const int d0 = K16_D - (k1 >> 6), d1 = K16_D - (k2 >> 6);  // NONE -> d > 511
-                    const bool ok = d0 <= maxDist && !(d1 <= maxDist && d1 - d0 < minDiff);
-                    if (i < na) rowd[i] = ok ? (uint16_t)d0 : (uint16_t)0xFFFFu;
+                    for (int e = 0; e < 2; e++) {
+                        const int i = rowbase + 32 * rt + acc_row(2 * k + e) + 4 * (lane >> 5);
+                        const int k1 = e ? hi16s(R1[0]) : lo16s(R1[0]), k2 = e ? hi16s(R2[0]) : lo16s(R2[0]);
+                        const int d0 = K16_D - (k1 >> 6), d1 = K16_D - (k2 >> 6);  // NONE -> d > 511
+                        const bool ok = d0 <= maxDist && !(d1 <= maxDist && d1 - d0 < minDiff);
+                        if (i < na) rowd[i] = ok ? (uint16_t)d0 : (uint16_t)0xFFFFu;
+                    }
                 }
             }
         }

@@ -436,10 +436,18 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
         for (int o = 0; o < 2; o++) {
             const v4i yh = __builtin_amdgcn_mfma_i32_16x16x64_i8(hi, ta[o], c_hi, 0, 0, 0);
             const v4i yl = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo, ta[o], c_lo, 0, 0, 0);
-            uint32_t w = 0;
+            // out_r = min(255, t_r >> 16), t_r = (yh << 8) + yl: the high halves of two t's as u16
+            // lanes (one v_perm), saturated two at a time (v_pk_min_u16), then their low bytes
+            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+            uint32_t t[4];
 #pragma unroll
-            for (int r = 0; r < 4; r++)
-                w |= min(255u, (((uint32_t)yh[r] << 8) + (uint32_t)yl[r]) >> 16) << (8 * r);
+            for (int r = 0; r < 4; r++) t[r] = ((uint32_t)yh[r] << 8) + (uint32_t)yl[r];
+            const u16x2 cap = {255, 255};
+            const uint32_t h01 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(
+                __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(t[1], t[0], 0x07060302u)), cap));
+            const uint32_t h23 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(
+                __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(t[3], t[2], 0x07060302u)), cap));
+            const uint32_t w = __builtin_amdgcn_perm(h23, h01, 0x06040200u);
             if (16 * o + n < ylim && x < TW && X < p.blur_stride) {
                 const int Y = (int)blockIdx.y * TH + 16 * o + n;
                 *reinterpret_cast<uint32_t*>(fb + brick_offset(Y, X, p.blur_bcols)) = w;
