@@ -45,7 +45,10 @@ def parse():
     p.add_argument("--pose-problems", type=int, default=2048, help="pose-only BA problems per launch")
     p.add_argument("--pose-iters", type=int, default=20)
     p.add_argument("--no-pose", action="store_true")
-    p.add_argument("--track-frames", type=int, default=240, help="C4 tracking-loop sequence length")
+    p.add_argument("--track-frames", type=int, default=1000, help="C4 tracking-loop sequence length (SURVEY §8(d))")
+    p.add_argument("--track-warmup", type=int, default=16, help="C4 warm-up frames (untimed run before the timed one)")
+    p.add_argument("--track-parity-frames", type=int, default=240, help="frames of the C4 oracle parity run")
+    p.add_argument("--no-local-ba", action="store_true", help="C4 without the local BA after each keyframe")
     p.add_argument("--no-tracking", action="store_true")
     p.add_argument("--trajectory-csv", default="", help="rank 0 writes the gathered trajectories (ExportFossilCsv)")
     p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
@@ -600,18 +603,23 @@ def c5_exchange(res, rank, dist, device, csv_path=""):
     return gathered, rows
 
 
+TRACK_STEP = 0.03  # camera travel per frame on the plane: ~5.4 px at 720p, a keyframe every ~60 frames
+
+
 def run_tracking(args, rank, world, local_rank, torch, dist):
     """C4 (BASELINE.json configs[3]) and, with several ranks, C5 (configs[4]): the tracking loop
     (mageslam_amd.tracking) over a synthetic hand-held 720p sequence of a textured plane, frames
-    rendered into HBM first.  A step is the whole sequence: batched ORB extraction of every frame,
-    then the device-resident loop (RadiusMatch + two pose-only BundlerLib passes per frame,
-    sequential: each frame's prediction needs the previous pose).  Every rank tracks its own
-    sequence (texture seed + rank, camera path from synth.rank_origin); after the timed region the
-    tracked trajectories are all-gathered (c5_exchange)."""
+    rendered into HBM first, composed with the local BA MappingWorker runs after every new keyframe
+    (tracking.local_bundle_adjust).  A step is the whole sequence: batched ORB extraction of every
+    frame, then the device-resident loop (RadiusMatch + two pose-only BundlerLib passes + the
+    local-map search per frame, sequential: each frame's prediction needs the previous pose; a
+    BundlerLib step between frames at every keyframe).  Every rank tracks its own sequence (texture
+    seed + rank, camera path from synth.rank_origin); after the timed region the tracked trajectories
+    are all-gathered (c5_exchange)."""
     from mageslam_amd import _lib, multigpu, orb, synth, tracking
 
     T = args.track_frames
-    seq = synth.scene_sequence(T, args.width, args.height, origin=synth.rank_origin(rank))
+    seq = synth.scene_sequence(T, args.width, args.height, step=TRACK_STEP, origin=synth.rank_origin(rank))
     seed = multigpu.sequence_seed(synth.FRAME_SEED, rank)
     dev = f"cuda:{local_rank}"
     cams = torch.from_numpy(seq.cams()).to(dev)
@@ -623,7 +631,7 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
     torch.cuda.synchronize()
     K = (seq.fx, seq.fy, seq.cx, seq.cy)
     p0 = tracking.Pose(seq.R[0], seq.t[0])
-    ts = tracking.TrackerSettings(width=args.width, height=args.height)
+    ts = tracking.TrackerSettings(width=args.width, height=args.height, local_ba=not args.no_local_ba)
     N = args.features
     det = orb.OrbDetector(nfeatures=N, device=local_rank)
     d_kp = torch.zeros((T, N * 28), dtype=torch.uint8, device=dev)
@@ -636,10 +644,11 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
             det.detect_and_compute_batch_device(frames[b0:b1], args.width, args.height, d_kp[b0:b1],
                                                 d_desc[b0:b1], d_n[b0:b1], N)
 
-    extract_device(8)  # warm-up
-    tracking.track_native_device(d_kp, d_desc, N, d_n, 8, K, p0, synth.SCENE_PLANE_Z, settings=ts)
+    W = max(2, min(args.track_warmup, T))
+    extract_device(W)  # warm-up: the first frames, extraction + loop, untimed
+    tracking.track_native_device(d_kp, d_desc, N, d_n, W, K, p0, synth.SCENE_PLANE_Z, settings=ts)
     torch.cuda.synchronize()
-    # the timed loop: device-resident extraction + mage_track_sequence_device (one sync)
+    # the timed loop: device-resident extraction + mage_track_sequence_device
     multigpu.barrier(dist)
     t0 = time.perf_counter()
     extract_device(T)
@@ -653,15 +662,21 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
         torch.tensor([T / (t2 - t0)], dtype=torch.float64, device=dev), dist)]
     gathered, own = c5_exchange(res, rank, dist, dev, args.trajectory_csv)
     gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)])
-    out = {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose + local map)",
-           "value": world * T / el_max, "unit": "frames/s", "frames": T, "dtype": "u8 / f64",
+    out = {"metric": "tracking-loop frames/sec @720p (extract + RadiusMatch + 2x OptimizeCameraPose + local map"
+                     + (" + local BA per keyframe" if ts.local_ba else "") + ")",
+           "value": world * T / el_max, "unit": "frames/s", "frames": T, "warmup_frames": W, "dtype": "u8 / f64",
            "extract_ms_per_frame": 1000 * (t1 - t0) / T, "track_ms_per_frame": 1000 * (t2 - t1) / T,
-           "loop": "device-resident (mage_track_sequence_device: per-frame decisions on the GPU, one sync)",
+           "loop": "device-resident (mage_track_sequence_device: per-frame decisions on the GPU; with the local BA "
+                   "the host runs BundlerLib between frames at each keyframe)",
            "mean_matches": float(np.mean(res.matches[1:])), "mean_inliers": float(np.mean(res.inliers[1:])),
-           "keyframes": len(res.keyframes), "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
+           "keyframes": len(res.keyframes), "local_ba_windows": len(res.ba_outliers),
+           "local_ba_outliers": int(sum(n for _, n in res.ba_outliers)),
+           "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
            "local_map": f"TrackLocalMap local-map search over the last {ts.local_map_keyframes} keyframes",
+           "local_ba": ("one StepBundleAdjustment per new keyframe over the local map's keyframes (oldest fixed), "
+                        "persisted lambda (MappingWorker.cpp:228-371)") if ts.local_ba else "off",
            "config": {"workload": f"C4: {T}-frame {args.width}x{args.height} hand-held pan over a textured plane "
-                                  f"(synthetic), {args.features} features/frame"
+                                  f"(synthetic, {TRACK_STEP} units per frame), {args.features} features/frame"
                                   + (f"; C5: {world} independent sequences (seed + rank), one per GPU, RCCL "
                                      f"all-gather of the tracked trajectories" if world > 1 else "")}}
     if world > 1:
@@ -671,56 +686,59 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
     out["trajectory_gather_consistent"] = bool(np.array_equal(gathered[rank], own))
     if world > 1:
         return out, None
-    # one GPU: the host-driven native loop over host features (mage_track_sequence) and the same loop
-    # driven from Python (tracking.track over GpuBackend) must give identical results
+    # one GPU: the same loop driven from Python over the GPU kernels must give the identical result;
+    # the host-driven native loop (mage_track_sequence, no local BA) equals the device loop without it
     be = tracking.GpuBackend(args.features, device=local_rank, batch=64)
     feats = be.extract(frames)
     torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    host = tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, settings=ts, device=local_rank)
-    torch.cuda.synchronize()
-    t4 = time.perf_counter()
-    py = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be, ts)
-    t5 = time.perf_counter()
 
     def same(a, b):
         return a.matches == b.matches and a.inliers == b.inliers and a.keyframes == b.keyframes and all(
             np.array_equal(x.t, y.t) and np.array_equal(x.R, y.R) for x, y in zip(a.poses, b.poses))
 
-    out.update(host_loop_track_ms_per_frame=1000 * (t4 - t3) / T, host_loop_identical=bool(same(host, res)),
-               python_loop_track_ms_per_frame=1000 * (t5 - t4) / T, python_loop_identical=bool(same(py, res)))
-    return out, (seq, frames, res, feats)
+    t3 = time.perf_counter()
+    py = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, be, ts)
+    t4 = time.perf_counter()
+    nb = tracking.TrackerSettings(width=args.width, height=args.height)
+    dev_nb = tracking.track_native_device(d_kp, d_desc, N, d_n, T, K, p0, synth.SCENE_PLANE_Z, settings=nb)
+    t5 = time.perf_counter()
+    host = tracking.track_native(feats, K, p0, synth.SCENE_PLANE_Z, settings=nb, device=local_rank)
+    t6 = time.perf_counter()
+    out.update(python_loop_track_ms_per_frame=1000 * (t4 - t3) / T,
+               python_loop_identical=bool(same(py, res) and py.ba_outliers == res.ba_outliers),
+               without_local_ba={"track_ms_per_frame": 1000 * (t5 - t4) / T, "keyframes": len(dev_nb.keyframes),
+                                 "pose_rmse_vs_ground_truth": tracking.pose_rmse(dev_nb, gt)},
+               host_loop_track_ms_per_frame=1000 * (t6 - t5) / T, host_loop_identical=bool(same(host, dev_nb)))
+    return out, (seq, frames, res, feats, ts)
 
 
 def cpu_tracking_baseline(args, ctx, budget_s):
-    """The identical loop on the CPU oracle over the first frames of the same sequence; also the
-    GPU-vs-CPU pose RMSE of those frames (north star: <= 1e-4)."""
+    """The identical loop (local BA included) on the CPU oracle over the first
+    --track-parity-frames frames of the same sequence: its rate, and the GPU-vs-CPU parity of those
+    frames (north star: pose RMSE <= 1e-4; identical matches, keyframes and BA outliers)."""
     from oracle.tracking_backend import OracleBackend
 
     from mageslam_amd import synth, tracking
 
-    seq, frames, gres, gfeats = ctx
+    seq, frames, gres, gfeats, ts = ctx
+    n = min(args.track_parity_frames, len(gres.poses))
     ob = OracleBackend(args.features)
-    host = frames.cpu().numpy()
-    feats, el = [], 0.0
+    host = frames[:n].cpu().numpy()
     t0 = time.perf_counter()
-    while len(feats) < len(host) and (el < budget_s or len(feats) < 4):
-        feats += ob.extract(host[len(feats):len(feats) + 1])
-        el = time.perf_counter() - t0
+    feats = ob.extract(host)
     K = (seq.fx, seq.fy, seq.cx, seq.cy)
     p0 = tracking.Pose(seq.R[0], seq.t[0])
-    t1 = time.perf_counter()
-    ores = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, ob, tracking.TrackerSettings(width=args.width,
-                                                                                          height=args.height))
-    el = time.perf_counter() - t1 + el
-    n = len(feats)
+    ores = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, ob, ts)
+    el = time.perf_counter() - t0
     gsub = tracking.TrackResult(poses=gres.poses[:n])
     same = all(np.array_equal(a[0].view(np.uint8), b[0].view(np.uint8)) for a, b in zip(gfeats[:n], feats))
-    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} frames of the same sequence, oracle extract + RadiusMatch + pose BA, single thread, "
-                      f"{el:.1f} s"}, {"frames": n, "keypoints_identical": bool(same),
-                                       "pose_rmse_gpu_vs_cpu": tracking.pose_rmse(gsub, ores),
-                                       "matches_identical": gres.matches[:n] == ores.matches}
+    gba = [x for x in gres.ba_outliers if x[0] < n]
+    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port", "build": ORACLE_BUILD[0],
+            "sample": f"first {n} frames of the same sequence, oracle extract + RadiusMatch + pose BA + local map + "
+                      f"local BA, single thread, {el:.1f} s"}, {
+        "frames": n, "keypoints_identical": bool(same), "pose_rmse_gpu_vs_cpu": tracking.pose_rmse(gsub, ores),
+        "matches_identical": gres.matches[:n] == ores.matches, "keyframes_identical": [k for k in gres.keyframes if k < n] == ores.keyframes,
+        "ba_outliers_identical": gba == ores.ba_outliers, "local_ba_windows": len(ores.ba_outliers)}
 
 
 def cpu_ba_baseline(g, budget_s):
@@ -1078,7 +1096,7 @@ def main():
                         mref["vs_cpu_all_cores"] = mref["value"] / rca["value"]
                 ba_res["vs_cpu"] = ba_res["value"] / cb["value"]
             if track_res is not None:
-                ct, parity = cpu_tracking_baseline(args, tctx, min(args.cpu_sample_s, 6.0))
+                ct, parity = cpu_tracking_baseline(args, tctx, args.cpu_sample_s)
                 track_res["cpu_baseline"] = ct
                 track_res["vs_cpu"] = track_res["value"] / ct["value"]
                 track_res["parity"] = parity

@@ -480,6 +480,16 @@ typedef struct mage_track_settings {
     float scale_factor;                                                  /* pyramid ScaleFactor 1.5 */
     uint32_t num_levels;                                                 /* pyramid levels 1 */
     int32_t width, height;                                               /* image size */
+    /* Local bundle adjustment after every new keyframe (MappingWorker.cpp:228-371; device loop
+     * only, mage_track_sequence refuses it): the local map's keyframes (oldest fixed), the points
+     * they own that a free one observes, every alive association; one StepBundleAdjustment per
+     * keyframe at MaxOutlierError with the persisted lambda (tracking.py local_bundle_adjust). */
+    uint32_t local_ba;                                                   /* 0: off */
+    float ba_huber, ba_huber_scale, ba_max_outlier_error;                /* 1.8, 0.95, 7.25 */
+    uint32_t ba_steps_per_run;                                           /* NumStepsPerRun 1 */
+    float ba_low_connectivity_scale;                                     /* 1.5 */
+    uint32_t ba_upper_connections;                                       /* UpperConnectionsForBA 2000 */
+    float min_lambda;                                                    /* MappingSettings::MinLambda 1e-3 */
 } mage_track_settings;
 
 /* Features of `frames` frames (host): keypoints kp[frame_start[f] .. frame_start[f+1]) and their
@@ -500,7 +510,8 @@ mage_status mage_track_sequence_device(const mage_keypoint* d_kp, const uint8_t*
                                        const uint32_t* d_n, uint32_t frames, const double K[4],
                                        const double first_pose[12], double plane_z,
                                        const mage_track_settings* settings, double* poses, uint32_t* matches,
-                                       uint32_t* inliers, uint8_t* keyframe, mage_stream stream);
+                                       uint32_t* inliers, uint8_t* keyframe, uint32_t* ba_outliers,
+                                       mage_stream stream);
 
 #ifdef __cplusplus
 }

@@ -99,7 +99,11 @@ class TrackSettingsC(C.Structure):
                 ("local_map_keyframes", C.c_uint32), ("match_search_radius", C.c_float),
                 ("local_max_hamming", C.c_int32), ("local_min_hamming_difference", C.c_int32),
                 ("min_view_cos", C.c_float), ("image_border", C.c_float), ("min_tracked", C.c_uint32),
-                ("scale_factor", C.c_float), ("num_levels", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32)]
+                ("scale_factor", C.c_float), ("num_levels", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32),
+                ("local_ba", C.c_uint32), ("ba_huber", C.c_float), ("ba_huber_scale", C.c_float),
+                ("ba_max_outlier_error", C.c_float), ("ba_steps_per_run", C.c_uint32),
+                ("ba_low_connectivity_scale", C.c_float), ("ba_upper_connections", C.c_uint32),
+                ("min_lambda", C.c_float)]
 
 
 class BAStats(C.Structure):
@@ -222,6 +226,6 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_ba_get_state_f64", st, vp, vp, vp)
     sig("mage_ba_get_stats", st, vp, C.POINTER(BAStats))
     sig("mage_track_sequence", st, vp, vp, vp, u32, vp, vp, C.c_double, vp, vp, vp, vp, vp, C.c_int)
-    sig("mage_track_sequence_device", st, vp, vp, u32, vp, u32, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp)
+    sig("mage_track_sequence_device", st, vp, vp, u32, vp, u32, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp, vp)
     sig("mage_ba_pose_batch", st, u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp, C.c_int)
     sig("mage_ba_pose_batch_device", st, u32, vp, vp, vp, vp, vp, vp, vp, u32, f32, f32, vp, vp, vp, vp, vp, vp, vp)

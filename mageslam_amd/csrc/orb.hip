@@ -1577,6 +1577,77 @@ __global__ __launch_bounds__(256) void resize_linear_kernel(const uint8_t* __res
     dst[(long long)f * p.dpitch + (long long)dy * p.dstride + dx] = (uint8_t)min(max(v, 0), 255);
 }
 
+// The same resize with a workgroup per output row (and frame): the two source rows it reads are
+// staged in LDS with dword loads, each thread forms four consecutive output pixels from LDS bytes
+// (exactly resize_linear_kernel's arithmetic) and stores them as one dword.  Source rows up to
+// RZ_MAXW bytes; resize_linear_kernel serves wider ones.
+constexpr int RZ_MAXW = 4096;
+__global__ __launch_bounds__(256) void resize_rows_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          ResizeParams p)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t rows[2][RZ_MAXW + 16];
+    const int f = blockIdx.z, dy = blockIdx.y, tid = threadIdx.x;
+    const uint8_t* S = src + (long long)f * p.spitch;
+    uint8_t* D = dst + (long long)f * p.dpitch + (long long)dy * p.dstride;
+    int ry[2];
+    if (p.area2) {
+        ry[0] = 2 * dy;
+        ry[1] = 2 * dy + 1;
+    } else {
+        const int sy = p.yofs[dy];
+        ry[0] = min(max(sy, 0), p.sh - 1);
+        ry[1] = min(max(sy + 1, 0), p.sh - 1);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint8_t* R = S + (long long)ry[r] * p.sstride;
+        if ((reinterpret_cast<uintptr_t>(R) & 3) == 0 && (p.sw & 3) == 0) {
+            for (int i = tid; i < (p.sw >> 2); i += 256)
+                reinterpret_cast<uint32_t*>(rows[r])[i] = reinterpret_cast<const uint32_t*>(R)[i];
+        } else {
+            for (int i = tid; i < p.sw; i += 256) rows[r][i] = R[i];
+        }
+    }
+    __syncthreads();
+    const bool dword_out = (reinterpret_cast<uintptr_t>(D) & 3) == 0;
+    for (int x4 = tid; 4 * x4 < p.dw; x4 += 256) {
+        uint32_t out = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int dx = 4 * x4 + e;
+            if (dx >= p.dw) break;
+            int v;
+            if (p.area2) {
+                const int sum = rows[0][2 * dx] + rows[0][2 * dx + 1] + rows[1][2 * dx] + rows[1][2 * dx + 1];
+                v = dx < p.xv ? (sum + 2) >> 2 : __float2int_rn((float)sum * 0.25f);
+            } else {
+                const int sx = p.xofs[dx];
+                const uint32_t a = p.alpha[dx], b = p.beta[dy];
+                const int a0 = (short)(a & 0xFFFFu), a1 = (short)(a >> 16), b0 = (short)(b & 0xFFFFu), b1 = (short)(b >> 16);
+                int h0, h1;
+                if (dx < p.xmax) {
+                    h0 = rows[0][sx] * a0 + rows[0][sx + 1] * a1;
+                    h1 = rows[1][sx] * a0 + rows[1][sx + 1] * a1;
+                } else {
+                    h0 = rows[0][sx] * 2048;
+                    h1 = rows[1][sx] * 2048;
+                }
+                if (dx < p.xv)
+                    v = (((((int)(short)(h0 >> 4)) * b0) >> 16) + ((((int)(short)(h1 >> 4)) * b1) >> 16) + 2) >> 2;
+                else
+                    v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+                v = min(max(v, 0), 255);
+            }
+            out |= (uint32_t)v << (8 * e);
+        }
+        if (dword_out && 4 * x4 + 3 < p.dw) {
+            *reinterpret_cast<uint32_t*>(D + 4 * x4) = out;
+        } else {
+            for (int e = 0; e < 4 && 4 * x4 + e < p.dw; e++) D[4 * x4 + e] = (uint8_t)(out >> (8 * e));
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // 5. ICAngles (UseOrientation, OpenCVModified.cpp:399-437) + rotation index (:526)
 // ------------------------------------------------------------------------------------------
@@ -1648,6 +1719,76 @@ __global__ __launch_bounds__(256) void orient_kernel(mage_keypoint* __restrict__
         kp[i].angle = angle;
         // rot = cvRound(angle / ROTATION_INCREMENT_DEGREES) % ROTATION_INCREMENT_COUNT (:526)
         const int rot = ((int)rintf(__fdiv_rn(angle, 12.0f))) % 30;
+        lvl[i] = (uint16_t)((l << 8) | rot);
+    }
+}
+
+// The same moments with a row per lane (5 <= half_k <= 15: two keypoints per wave, lanes 32 s + j hold
+// row v = j - half_k of keypoint s): the row's 2 half_k + 1 bytes come from 9 aligned dword loads
+// issued together, are realigned to the window start (v_alignbyte), and two v_dot4_u32_u8 per
+// dword against the row's disc mask give sum_u (u + half_k) I and sum_u I; then
+// m_10 = sum (u + half_k) I - half_k sum I and m_01 = v sum I, summed over the rows by shuffles.
+// Integer sums: identical to orient_kernel's per-pixel loop.
+constexpr int OR_ROWS = 32;  // lanes per keypoint
+__global__ __launch_bounds__(256) void orient_rows_kernel(mage_keypoint* __restrict__ kp,
+                                                          const uint32_t* __restrict__ xy, uint16_t* __restrict__ lvl,
+                                                          const uint32_t* __restrict__ n_in, OrientParams p)
+{
+    __shared__ uint32_t wmask[16][8];  // per |v|: the byte mask of the disc row (0x01 bytes in range)
+    const int h = p.half_k;
+    if (threadIdx.x < 16 * 8) {
+        const int av = threadIdx.x >> 3, d = threadIdx.x & 7;
+        const int um = av <= h ? p.umax[av] : -1;  // bytes j in [h - um, h + um]
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int j = 4 * d + b;
+            if (um >= 0 && j >= h - um && j <= h + um) m |= 1u << (8 * b);
+        }
+        wmask[av][d] = m;
+    }
+    __syncthreads();
+    const int f = blockIdx.y;
+    const int lane = threadIdx.x & 63, j = lane & (OR_ROWS - 1);
+    const int k = blockIdx.x * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
+    const int n = (int)n_in[f];
+    const long long i = (long long)f * p.out_cap + min(k, max(n - 1, 0));
+    const int l = lvl[i] >> 8;
+    const uint32_t c = xy[i];
+    const int cx = (int)(c & 0xFFFFu), cy = (int)(c >> 16);
+    const int v = j - h;
+    uint32_t s1 = 0, sw = 0;  // sum I, sum (u + h) I over the row
+    if (k < n && j <= 2 * h) {
+        const uint8_t* row = p.lev.base[l] + (long long)f * p.lev.pitch[l] + (long long)(cy + v) * p.lev.stride[l] + cx - h;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(row);
+        const uint32_t* al = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3u);
+        // only the dwords holding window bytes: the last read byte is x + h + 3 at most, inside the
+        // level for every keypoint (the oriented border ceil(h sqrt 2) >= h + 3 for h >= 5)
+        const int qlast = (int)(sh + 2 * h) >> 2;
+        uint32_t d[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) d[q] = q <= qlast ? al[q] : 0u;
+        const uint32_t* mrow = wmask[v < 0 ? -v : v];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh);  // bytes 4q .. 4q+3 of the row
+            const uint32_t m = mrow[q];
+            const uint32_t pos = 0x03020100u + 0x04040404u * (uint32_t)q;     // byte j = u + h
+            s1 = __builtin_amdgcn_udot4(w, m, s1, false);
+            sw = __builtin_amdgcn_udot4(w, pos & (m * 0xFFu), sw, false);
+        }
+    }
+    int m10 = (int)sw - h * (int)s1, m01 = v * (int)s1;
+#pragma unroll
+    for (int off = OR_ROWS / 2; off >= 1; off >>= 1) {
+        m10 += __shfl_xor(m10, off);
+        m01 += __shfl_xor(m01, off);
+    }
+    if (j == 0 && k < n) {
+        const float angle = fast_atan2_deg((float)m01, (float)m10);
+        kp[i].angle = angle;
+        const int rot = ((int)rintf(__fdiv_rn(angle, 12.0f))) % 30;  // (:526)
         lvl[i] = (uint16_t)((l << 8) | rot);
     }
 }
@@ -1814,7 +1955,10 @@ mage_status resize_linear_device(const uint8_t* src, int sw, int sh, int sstride
     rp.yofs = it + v.yofs;
     rp.alpha = wt + v.alpha;
     rp.beta = wt + v.beta;
-    launch("image.resize", resize_linear_kernel, dim3((dw + 255) / 256, dh, 1), dim3(256), 0, st, src, dst, rp);
+    if (rp.sw <= RZ_MAXW)
+        launch("image.resize", resize_rows_kernel, dim3(1, dh, 1), dim3(256), 0, st, src, dst, rp);
+    else
+        launch("image.resize", resize_linear_kernel, dim3((dw + 255) / 256, dh, 1), dim3(256), 0, st, src, dst, rp);
     MAGE_HIP(hipGetLastError());
     return MAGE_OK;
 }
@@ -2020,8 +2164,12 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             rp.yofs = ints + dst.yofs;
             rp.alpha = words + dst.alpha;
             rp.beta = words + dst.beta;
-            hipLaunchKernelGGL(resize_linear_kernel, dim3((dst.w + 255) / 256, dst.h, batch), dim3(256), 0, st,
-                               raw.base[l - 1], const_cast<uint8_t*>(raw.base[l]), rp);
+            if (src.w <= RZ_MAXW)
+                hipLaunchKernelGGL(resize_rows_kernel, dim3(1, dst.h, batch), dim3(256), 0, st, raw.base[l - 1],
+                                   const_cast<uint8_t*>(raw.base[l]), rp);
+            else
+                hipLaunchKernelGGL(resize_linear_kernel, dim3((dst.w + 255) / 256, dst.h, batch), dim3(256), 0, st,
+                                   raw.base[l - 1], const_cast<uint8_t*>(raw.base[l]), rp);
         }
     }
     MAGE_HIP(hipGetLastError());
@@ -2127,8 +2275,12 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             op.umax[v] = v0;
             ++v0;
         }
-        launch("orb.orient", orient_kernel, dim3((cap + 3) / 4, batch), dim3(256), 0, st, d_kp, o->xy.as<uint32_t>(),
-                           o->lvl.as<uint16_t>(), d_n, op);
+        if (half >= 5 && half <= 15)  // a disc row per lane, two keypoints per wave
+            launch("orb.orient", orient_rows_kernel, dim3((cap + 7) / 8, batch), dim3(256), 0, st, d_kp,
+                   o->xy.as<uint32_t>(), o->lvl.as<uint16_t>(), d_n, op);
+        else
+            launch("orb.orient", orient_kernel, dim3((cap + 3) / 4, batch), dim3(256), 0, st, d_kp, o->xy.as<uint32_t>(),
+                   o->lvl.as<uint16_t>(), d_n, op);
         MAGE_HIP(hipGetLastError());
     }
 

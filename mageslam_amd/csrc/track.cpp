@@ -169,6 +169,7 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
     for (uint32_t f = 0; f < frames; f++)
         MAGE_REQUIRE(frame_start[f + 1] >= frame_start[f], MAGE_EINVAL, "frame_start must be non-decreasing");
     MAGE_REQUIRE(frame_start[frames] == 0 || (kp && desc), MAGE_EINVAL, "null features");
+    MAGE_REQUIRE(!s->local_ba, MAGE_EUNSUPPORTED, "the local BA runs in the device loop (mage_track_sequence_device)");
     MAGE_HIP(hipSetDevice(device));
     const float fx = (float)K[0], fy = (float)K[1], cx = (float)K[2], cy = (float)K[3];
     auto frame_kp = [&](uint32_t f) { return kp + frame_start[f]; };

@@ -18,8 +18,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "common.hpp"
 
@@ -104,6 +107,9 @@ struct Ctl {              // per-call control words (device)
     uint32_t kf_count;
     uint32_t kf_n[NKMAX]; // keyframe feature counts per slot
     uint32_t lm_nq;       // local-map queries of the frame
+    uint32_t kf_id[NKMAX];  // frame index of the keyframe in each slot
+    uint32_t kf_an[NKMAX];  // associations per slot (the keyframe frame's pass-2 inliers)
+    uint32_t halt;        // local BA pending: every frame kernel is a no-op until the host clears it
 };
 
 struct TrackBufs {
@@ -116,6 +122,20 @@ struct TrackBufs {
     float* kf_mvd;   // mean viewing directions (3 per point)
     float* kf_dmin;
     float* kf_dmax;
+    double* kf_pose;      // 12 per slot (R row-major, t)
+    // mapping side (local BA): per point its refinement count and own-observation flag, per slot
+    // the associations (owner keyframe id, point index, keypoint x, y bits) and their flags
+    uint32_t* kf_ref;
+    uint8_t* kf_own;
+    int4* kf_assoc;
+    uint8_t* kf_aalive;
+    int2* src1;           // pose-BA observation sources (owner keyframe id, point index)
+    int2* src2;
+    float* info1;         // per observation: MapPointRefinementConfidence of the point
+    float* info2;
+    int2* lm_qsrc;
+    float* lm_qinfo;
+    uint32_t* prog;       // mapped host words {frame done, frame that requested a local BA}
     // local-map search
     uint32_t* lm_mask;    // unassociated keypoints (bit words)
     uint8_t* lm_visited;  // reference-keyframe points associated as pass-1 inliers
@@ -146,7 +166,6 @@ struct TrackBufs {
     float* uv1;
     float* pts2;
     float* uv2;
-    float* info;
     float* pos3_o1;
     float* r9_o1;
     float* pos3_o2;
@@ -164,11 +183,20 @@ struct TrackConst {
     uint32_t cap;          // keypoints per frame slot
     uint32_t nk;           // keyframe ring slots (max(local_map_keyframes, 1))
     uint32_t qcap;         // local-map queries per frame (nk x cap)
+    uint32_t acap;         // associations per keyframe slot (cap + qcap)
     float fmax[8], fmin[8];  // ComputeDMax / ComputeDMin factors per octave (powf on the host)
     float log2s;           // log2(scale factor)
 };
 
 __device__ float dot3f(const float* a, const float* b) { return ((0.f + a[0] * b[0]) + a[1] * b[1]) + a[2] * b[2]; }
+
+// MapPointRefinementConfidence (Map/MappingMath.h:42-49): 1 - 1 / powf(1.5 + count, 2); the square
+// of 1.5 + count is exact in float, so x * x is powf's result
+__host__ __device__ inline float refinement_confidence(uint32_t count)
+{
+    const float x = 1.5f + (float)count;
+    return 1.f - 1.f / (x * x);
+}
 
 // Pose::GetWorldSpacePosition of the float view matrix (see track.cpp world_position)
 __device__ void world_position(const double* R, const double* t, float C[3])
@@ -193,7 +221,10 @@ __device__ void make_keyframe(const TrackBufs& b, const TrackConst& c, uint32_t 
     float Cf[3];
     world_position(P.R, P.t, Cf);
     const size_t o = (size_t)slot * c.cap;
+    if (threadIdx.x < 12) b.kf_pose[12 * slot + threadIdx.x] = threadIdx.x < 9 ? P.R[threadIdx.x] : P.t[threadIdx.x - 9];
     for (uint32_t i = threadIdx.x; i < nf; i += TT) {
+        b.kf_ref[o + i] = 0;
+        b.kf_own[o + i] = 1;
         b.kf_kp[o + i] = fk[i];
         const uint4* s = reinterpret_cast<const uint4*>(fd + 32ull * i);
         uint4* d = reinterpret_cast<uint4*>(b.kf_desc + 32ull * (o + i));
@@ -251,11 +282,13 @@ __global__ __launch_bounds__(TT) void trk_init(TrackBufs b, TrackConst c, const 
 {
     const uint32_t n = frame_count(c, nf, status);
     make_keyframe(b, c, 0, fk, fd, n, load_pose(poses));
-    for (uint32_t k = threadIdx.x; k < c.cap + c.qcap; k += TT) b.info[k] = c.s.refinement_info;
     if (threadIdx.x == 0) {
         b.ctl->kf_first = 0;
         b.ctl->kf_count = 1;
         b.ctl->kf_n[0] = n;
+        b.ctl->kf_id[0] = 0;
+        b.ctl->kf_an[0] = 0;
+        b.ctl->halt = 0;
         matches[0] = inliers[0] = n;
         keyframe[0] = 1;
         b.intr4[0] = c.cx;  // BundlerLib's {cx, cy, fx, fy}
@@ -269,6 +302,13 @@ __global__ __launch_bounds__(TT) void trk_project(TrackBufs b, TrackConst c, int
 {
     __shared__ float R32[9], t32[3];
     __shared__ uint32_t wsum[TT / 64];
+    if (b.ctl->halt) {  // a local BA is pending: this frame runs again after it (zero counts downstream)
+        if (threadIdx.x == 0) {
+            b.ctl->ns = 0;
+            for (int k = 0; k < 3; k++) b.ctl->exec[k] = b.nq[k] = 0;
+        }
+        return;
+    }
     if (threadIdx.x == 0) {
         const DPose p1 = load_pose(poses + 12ll * (f - 1));
         const DPose pred = f < 2 ? p1 : d_mul(d_mul(p1, d_inverse(load_pose(poses + 12ll * (f - 2)))), p1);
@@ -329,18 +369,28 @@ __global__ void trk_weak(TrackBufs b, TrackConst c, int k)
 __global__ __launch_bounds__(TT) void trk_gather(TrackBufs b, TrackConst c, const mage_keypoint* fk, int f,
                                                  uint32_t* matches)
 {
+    if (b.ctl->halt) {
+        if (threadIdx.x == 0) {
+            b.ctl->lost = 1;
+            b.os1[0] = b.os1[1] = 0;
+        }
+        return;
+    }
     const int fin = b.ctl->exec[2] ? 2 : (b.ctl->exec[1] ? 1 : 0);
     const uint32_t n = b.mn[fin];
     const bool lost = n < c.s.min_matches;
     const mage_dmatch* m = b.m + (size_t)fin * c.cap;
     if (!lost) {
-        const size_t o = (size_t)ref_slot(b.ctl, c) * c.cap;
+        const uint32_t slot = ref_slot(b.ctl, c);
+        const size_t o = (size_t)slot * c.cap;
+        const int kid = (int)b.ctl->kf_id[slot];
         for (uint32_t k = threadIdx.x; k < n; k += TT) {
             const uint32_t q = b.sel[m[k].query_idx], t = (uint32_t)m[k].train_idx;
             for (int j = 0; j < 3; j++) b.pts1[3 * k + j] = b.kf_pts[3 * (o + q) + j];
             b.uv1[2 * k] = fk[t].x;
             b.uv1[2 * k + 1] = fk[t].y;
-            b.info[k] = c.s.refinement_info;
+            b.info1[k] = refinement_confidence(b.kf_ref[o + q]);  // TrackLocalMap.cpp:473-475
+            b.src1[k] = make_int2(kid, (int)q);
         }
     }
     if (threadIdx.x == 0) {
@@ -372,6 +422,8 @@ __global__ __launch_bounds__(TT) void trk_filter(TrackBufs b, TrackConst c, cons
             for (int j = 0; j < 3; j++) b.pts2[3 * pos + j] = b.pts1[3 * k + j];
             b.uv2[2 * pos] = b.uv1[2 * k];
             b.uv2[2 * pos + 1] = b.uv1[2 * k + 1];
+            b.info2[pos] = b.info1[k];
+            b.src2[pos] = b.src1[k];
         }
         base += tot;
     }
@@ -471,6 +523,8 @@ __global__ __launch_bounds__(TT) void trk_lm_project(TrackBufs b, TrackConst c)
                 dd[0] = sd[0];
                 dd[1] = sd[1];
                 for (int j = 0; j < 3; j++) b.lm_qpt[3 * pos + j] = b.kf_pts[3 * (o + i) + j];
+                b.lm_qsrc[pos] = make_int2((int)b.ctl->kf_id[slot], (int)i);
+                b.lm_qinfo[pos] = refinement_confidence(b.kf_ref[o + i]);
             }
             base += tot;
         }
@@ -495,6 +549,8 @@ __global__ __launch_bounds__(TT) void trk_lm_assemble(TrackBufs b, const mage_ke
             for (int j = 0; j < 3; j++) b.pts2[3 * pos + j] = b.lm_qpt[3 * q + j];
             b.uv2[2 * pos] = fk[r].x;
             b.uv2[2 * pos + 1] = fk[r].y;
+            b.info2[pos] = b.lm_qinfo[q];
+            b.src2[pos] = b.lm_qsrc[q];
         }
         base += tot;
     }
@@ -509,6 +565,7 @@ __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int 
     __shared__ int s_kf;
     __shared__ uint32_t s_slot;
     __shared__ double sP[12];
+    if (b.ctl->halt) return;  // re-run after the pending local BA
     bool lost = b.ctl->lost != 0;
     uint32_t n_in = 0;
     if (!lost) {
@@ -551,8 +608,250 @@ __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int 
     if (s_kf) {
         const uint32_t n = frame_count(c, nf, status);
         make_keyframe(b, c, s_slot, fk, fd, n, load_pose(sP));
-        if (threadIdx.x == 0) b.ctl->kf_n[s_slot] = n;
+        // its associations: the pass-2 inliers in observation order (ordered compaction)
+        const uint32_t n2 = b.os2[1];
+        int4* as = b.kf_assoc + (size_t)s_slot * c.acap;
+        uint8_t* aa = b.kf_aalive + (size_t)s_slot * c.acap;
+        uint32_t base = 0;
+        for (uint32_t c0 = 0; c0 < n2; c0 += TT) {
+            const uint32_t k = c0 + threadIdx.x;
+            const bool in = k < n2 && !b.out2[k];
+            uint32_t tot;
+            const uint32_t pos = base + block_prefix(in, wsum, &tot);
+            if (in && pos < c.acap) {
+                as[pos] = make_int4(b.src2[k].x, b.src2[k].y, __float_as_int(b.uv2[2 * k]), __float_as_int(b.uv2[2 * k + 1]));
+                aa[pos] = 1;
+            }
+            base += tot;
+        }
+        if (threadIdx.x == 0) {
+            b.ctl->kf_n[s_slot] = n;
+            b.ctl->kf_id[s_slot] = (uint32_t)f;
+            b.ctl->kf_an[s_slot] = min(base, c.acap);
+            // a window needs two keyframes: halt the queued frames until the host ran the local BA
+            if (c.s.local_ba && b.ctl->kf_count >= 2) b.ctl->halt = 1;
+        }
     }
+    if (b.prog && threadIdx.x == 0) {  // progress for the host (local BA): request word, then frame
+        if (s_kf && c.s.local_ba && b.ctl->kf_count >= 2) *reinterpret_cast<volatile uint32_t*>(b.prog + 1) = (uint32_t)f;
+        __threadfence_system();
+        *reinterpret_cast<volatile uint32_t*>(b.prog) = (uint32_t)f;
+    }
+}
+
+}  // namespace
+}  // namespace mage
+
+namespace mage {
+namespace {
+
+// ---- Local BA of the device loop (host side, between frames: MappingWorker's BundleAdjustTask) ----
+// The same window / schedule / write-back as tracking.py build_ba_window + apply_ba_window, over the
+// keyframe ring copied from the device; BundlerLib through the C-ABI (one instance per call of the
+// loop, the lambda persisted across windows as MappingWorker does).
+struct HostRing {
+    uint32_t first = 0, count = 0, nk = 0, cap = 0, acap = 0;
+    uint32_t n[NKMAX], id[NKMAX], an[NKMAX];
+    std::vector<double> pose;       // 12 per slot
+    std::vector<mage_keypoint> kp;  // cap per slot
+    std::vector<float> pts, mvd, dmin, dmax;
+    std::vector<uint32_t> ref;
+    std::vector<uint8_t> own, aalive;
+    std::vector<int4> assoc;
+};
+
+struct LocalBA {
+    mage_ba* ba = nullptr;
+    bool have_lambda = false;
+    float lambda = 0.f;
+    ~LocalBA()
+    {
+        if (ba) mage_ba_destroy(ba);
+    }
+};
+
+void host_world_position(const double* R, const double* t, float C[3])
+{
+    for (int i = 0; i < 3; i++) {
+        float sum = 0.f;
+        for (int k = 0; k < 3; k++) sum = sum + (float)R[3 * k + i] * -(float)t[k];
+        C[i] = sum + 0.f;
+    }
+}
+
+float host_dot3(const float* a, const float* b) { return ((0.f + a[0] * b[0]) + a[1] * b[1]) + a[2] * b[2]; }
+
+float bits_float(int v)
+{
+    float f;
+    std::memcpy(&f, &v, 4);
+    return f;
+}
+
+// tracking.point_attributes for point i of a slot
+void host_point_attributes(HostRing& R, uint32_t slot, uint32_t i, const TrackConst& c)
+{
+    const size_t o = (size_t)slot * R.cap + i;
+    float C[3];
+    host_world_position(&R.pose[12 * slot], &R.pose[12 * slot + 9], C);
+    const float* P = &R.pts[3 * o];
+    float v[3] = {P[0] - C[0], P[1] - C[1], P[2] - C[2]};
+    const float d = sqrtf(host_dot3(v, v));
+    if (d != 0) {
+        const float inv = 1.f / d;
+        for (float& x : v) x = x * inv;
+    }
+    const float d2 = sqrtf(host_dot3(v, v));
+    if (d2 != 0) {
+        const float inv = 1.f / d2;
+        for (float& x : v) x = x * inv;
+    }
+    for (int j = 0; j < 3; j++) R.mvd[3 * o + j] = v[j];
+    const float dl[3] = {C[0] - P[0], C[1] - P[1], C[2] - P[2]};
+    const float dist = sqrtf((dl[0] * dl[0] + dl[1] * dl[1]) + dl[2] * dl[2]);
+    const int oc = std::min(std::max(R.kp[o].octave, 0), 7);
+    R.dmin[o] = dist * c.fmin[oc];
+    R.dmax[o] = dist * c.fmax[oc];
+}
+
+// One local BA on the ring (on the host copy); returns the outlier count (UINT32_MAX: no window).
+mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int device, uint32_t* n_out,
+                          std::vector<uint8_t>& slot_changed)
+{
+    *n_out = 0xFFFFFFFFu;
+    const uint32_t nr = R.count;
+    if (nr < 2) return MAGE_OK;
+    uint32_t slot_of[NKMAX];
+    for (uint32_t r = 0; r < nr; r++) slot_of[r] = (R.first + r) % R.nk;
+    auto pos_of = [&](int id) -> int {
+        for (uint32_t r = 0; r < nr; r++)
+            if ((int)R.id[slot_of[r]] == id) return (int)r;
+        return -1;
+    };
+    struct Obs {
+        uint32_t cam, owner, idx;
+        float u, v;
+        uint32_t kind, src;  // 0: own (point index), 1: association (entry)
+    };
+    std::vector<Obs> obs;
+    for (uint32_t r = 0; r < nr; r++) {
+        const uint32_t sl = slot_of[r];
+        const size_t o = (size_t)sl * R.cap;
+        for (uint32_t i = 0; i < R.n[sl]; i++)
+            if (R.own[o + i]) obs.push_back({r, r, i, R.kp[o + i].x, R.kp[o + i].y, 0, i});
+        const size_t ao = (size_t)sl * R.acap;
+        for (uint32_t a = 0; a < R.an[sl]; a++) {
+            const int4 e = R.assoc[ao + a];
+            const int ow = pos_of(e.x);
+            if (R.aalive[ao + a] && ow >= 0)
+                obs.push_back({r, (uint32_t)ow, (uint32_t)e.y, bits_float(e.z), bits_float(e.w), 1, a});
+        }
+    }
+    // points a free camera observes, ascending (owner, index)
+    std::vector<uint64_t> keys;
+    for (const Obs& ob : obs)
+        if (ob.cam > 0) keys.push_back((uint64_t)ob.owner << 32 | ob.idx);
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    auto pidx = [&](uint32_t owner, uint32_t idx) -> int64_t {
+        const uint64_t k = (uint64_t)owner << 32 | idx;
+        auto it = std::lower_bound(keys.begin(), keys.end(), k);
+        return (it != keys.end() && *it == k) ? (int64_t)(it - keys.begin()) : -1;
+    };
+    std::vector<Obs> kept;
+    std::vector<uint32_t> cam, pt;
+    std::vector<float> uv, info;
+    for (const Obs& ob : obs) {
+        const int64_t p = pidx(ob.owner, ob.idx);
+        if (p < 0) continue;
+        kept.push_back(ob);
+        cam.push_back(ob.cam);
+        pt.push_back((uint32_t)p);
+        uv.push_back(ob.u);
+        uv.push_back(ob.v);
+    }
+    if (kept.empty()) return MAGE_OK;
+    const uint32_t P = (uint32_t)keys.size(), E = (uint32_t)kept.size();
+    std::vector<float> xyz(3ull * P);
+    std::vector<uint32_t> pref(P);
+    for (uint32_t q = 0; q < P; q++) {
+        const uint32_t sl = slot_of[keys[q] >> 32], i = (uint32_t)(keys[q] & 0xFFFFFFFFu);
+        const size_t o = (size_t)sl * R.cap + i;
+        for (int j = 0; j < 3; j++) xyz[3 * q + j] = R.pts[3 * o + j];
+        pref[q] = R.ref[o];
+    }
+    for (uint32_t e = 0; e < E; e++) info.push_back(refinement_confidence(pref[pt[e]]));
+    // cameras: view-space t, Eigen column-major R, {cx, cy, fx, fy}; the oldest fixed
+    std::vector<float> pos3(3 * nr), r9(9 * nr), intr(4 * nr);
+    std::vector<uint8_t> fixed(nr, 0);
+    fixed[0] = 1;
+    for (uint32_t r = 0; r < nr; r++) {
+        const double* ps = &R.pose[12 * slot_of[r]];
+        for (int i = 0; i < 3; i++) pos3[3 * r + i] = (float)ps[9 + i];
+        for (int rr = 0; rr < 3; rr++)
+            for (int cc = 0; cc < 3; cc++) r9[9 * r + 3 * cc + rr] = (float)ps[3 * rr + cc];
+        intr[4 * r] = (float)c.K[2];
+        intr[4 * r + 1] = (float)c.K[3];
+        intr[4 * r + 2] = (float)c.K[0];
+        intr[4 * r + 3] = (float)c.K[1];
+    }
+    // NumStepsPerRun / Huber width by the connectivity ratio (MappingWorker.cpp:254-263)
+    const uint32_t ratio = c.s.ba_upper_connections / E;
+    uint32_t steps = c.s.ba_steps_per_run;
+    float huber = c.s.ba_huber;
+    if (ratio > 0) {
+        steps = steps * (uint32_t)((float)ratio * c.s.ba_low_connectivity_scale);
+        huber = huber * powf(c.s.ba_huber_scale, (float)ratio);
+    }
+    const std::vector<float> hw(std::max(steps, 1u), huber);
+    mage_status st;
+    if (!L.ba && (st = mage_ba_create(0, device, &L.ba)) != MAGE_OK) return st;
+    if (L.have_lambda && (st = mage_ba_set_lambda(L.ba, L.lambda)) != MAGE_OK) return st;
+    if ((st = mage_ba_set_cameras(L.ba, nr, pos3.data(), r9.data(), intr.data(), fixed.data())) != MAGE_OK ||
+        (st = mage_ba_set_points(L.ba, P, xyz.data())) != MAGE_OK ||
+        (st = mage_ba_set_observations(L.ba, E, uv.data(), cam.data(), pt.data(), info.data())) != MAGE_OK)
+        return st;
+    std::vector<uint32_t> outl(E);
+    uint32_t nout = 0;
+    float ms = 0.f;
+    if ((st = mage_ba_step(L.ba, hw.data(), (uint32_t)hw.size(), c.s.ba_max_outlier_error, outl.data(), E, &nout, &ms)) !=
+        MAGE_OK)
+        return st;
+    std::vector<float> pos_o(3 * nr), r9_o(9 * nr), xyz_o(3ull * P);
+    float lam = 0.f;
+    if ((st = mage_ba_get_poses(L.ba, pos_o.data(), r9_o.data())) != MAGE_OK ||
+        (st = mage_ba_get_points(L.ba, xyz_o.data())) != MAGE_OK || (st = mage_ba_get_lambda(L.ba, &lam)) != MAGE_OK)
+        return st;
+    L.have_lambda = true;
+    L.lambda = std::max(lam, c.s.min_lambda);
+    // AdjustPosesAndMapPoints: outlier associations, free poses, points (+ refinement), attributes
+    for (uint32_t k = 0; k < std::min(nout, E); k++) {
+        const Obs& ob = kept[outl[k]];
+        const uint32_t sl = slot_of[ob.cam];
+        if (ob.kind == 0)
+            R.own[(size_t)sl * R.cap + ob.src] = 0;
+        else
+            R.aalive[(size_t)sl * R.acap + ob.src] = 0;
+        slot_changed[sl] = 1;
+    }
+    for (uint32_t r = 1; r < nr; r++) {
+        double* ps = &R.pose[12 * slot_of[r]];
+        for (int rr = 0; rr < 3; rr++)
+            for (int cc = 0; cc < 3; cc++) ps[3 * rr + cc] = (double)r9_o[9 * r + 3 * cc + rr];
+        for (int i = 0; i < 3; i++) ps[9 + i] = (double)pos_o[3 * r + i];
+        slot_changed[slot_of[r]] = 1;
+    }
+    for (uint32_t q = 0; q < P; q++) {
+        const uint32_t sl = slot_of[keys[q] >> 32], i = (uint32_t)(keys[q] & 0xFFFFFFFFu);
+        const size_t o = (size_t)sl * R.cap + i;
+        for (int j = 0; j < 3; j++) R.pts[3 * o + j] = xyz_o[3 * q + j];
+        R.ref[o] += 1;
+        slot_changed[sl] = 1;
+    }
+    for (uint32_t q = 0; q < P; q++)
+        host_point_attributes(R, slot_of[keys[q] >> 32], (uint32_t)(keys[q] & 0xFFFFFFFFu), c);
+    *n_out = nout;
+    return MAGE_OK;
 }
 
 }  // namespace
@@ -562,7 +861,8 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
                                                   const uint32_t* d_n, uint32_t frames, const double K[4],
                                                   const double first_pose[12], double plane_z,
                                                   const mage_track_settings* s, double* poses, uint32_t* matches,
-                                                  uint32_t* inliers, uint8_t* keyframe, mage_stream stream)
+                                                  uint32_t* inliers, uint8_t* keyframe, uint32_t* ba_outliers,
+                                                  mage_stream stream)
 {
     using namespace mage;
     MAGE_REQUIRE(K && first_pose && s && poses && matches && inliers && keyframe, MAGE_EINVAL, "null argument");
@@ -575,6 +875,7 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     const uint32_t NK = std::max(s->local_map_keyframes, 1u);
     const size_t qcap = s->local_map_keyframes > 0 ? (size_t)NK * cap : 0;  // local-map queries
     const size_t c2 = cap + qcap;                                           // pose-BA 2 observations
+    const size_t acap = c2;                                                 // associations per keyframe
     // one device allocation for the per-call scratch and outputs
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     size_t off = 0;
@@ -585,7 +886,10 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     };
     const size_t o_ctl = take(sizeof(Ctl)), o_pred = take(12 * 8), o_kfkp = take(28 * cap * NK),
                  o_kfd = take(32 * cap * NK), o_kfp = take(12 * cap * NK), o_kfv = take(12 * cap * NK),
-                 o_kfdn = take(4 * cap * NK), o_kfdx = take(4 * cap * NK), o_qkp = take(28 * cap), o_qd = take(32 * cap),
+                 o_kfdn = take(4 * cap * NK), o_kfdx = take(4 * cap * NK), o_kfps = take(96 * NK),
+                 o_kfr = take(4 * cap * NK), o_kfo = take(cap * NK), o_kfa = take(16 * acap * NK), o_kfaa = take(acap * NK),
+                 o_s1 = take(8 * cap), o_s2 = take(8 * c2), o_i1 = take(4 * cap), o_lqs = take(8 * qcap),
+                 o_lqi = take(4 * qcap), o_qkp = take(28 * cap), o_qd = take(32 * cap),
                  o_qp = take(8 * cap), o_sel = take(4 * cap), o_nq = take(16), o_m = take(3 * 16 * cap), o_mn = take(16),
                  o_rs = take(4 * cap), o_rst = take(4), o_pos = take(12), o_r9 = take(36), o_in = take(16),
                  o_os1 = take(8), o_os2 = take(8), o_p1 = take(12 * cap), o_u1 = take(8 * cap), o_p2 = take(12 * c2),
@@ -609,6 +913,16 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     b.kf_mvd = reinterpret_cast<float*>(d + o_kfv);
     b.kf_dmin = reinterpret_cast<float*>(d + o_kfdn);
     b.kf_dmax = reinterpret_cast<float*>(d + o_kfdx);
+    b.kf_pose = reinterpret_cast<double*>(d + o_kfps);
+    b.kf_ref = reinterpret_cast<uint32_t*>(d + o_kfr);
+    b.kf_own = reinterpret_cast<uint8_t*>(d + o_kfo);
+    b.kf_assoc = reinterpret_cast<int4*>(d + o_kfa);
+    b.kf_aalive = reinterpret_cast<uint8_t*>(d + o_kfaa);
+    b.src1 = reinterpret_cast<int2*>(d + o_s1);
+    b.src2 = reinterpret_cast<int2*>(d + o_s2);
+    b.info1 = reinterpret_cast<float*>(d + o_i1);
+    b.lm_qsrc = reinterpret_cast<int2*>(d + o_lqs);
+    b.lm_qinfo = reinterpret_cast<float*>(d + o_lqi);
     b.lm_mask = reinterpret_cast<uint32_t*>(d + o_lmm);
     b.lm_visited = reinterpret_cast<uint8_t*>(d + o_lmv);
     b.lm_hide = reinterpret_cast<int32_t*>(d + o_lmh);
@@ -636,7 +950,7 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     b.uv1 = reinterpret_cast<float*>(d + o_u1);
     b.pts2 = reinterpret_cast<float*>(d + o_p2);
     b.uv2 = reinterpret_cast<float*>(d + o_u2);
-    b.info = reinterpret_cast<float*>(d + o_inf);
+    b.info2 = reinterpret_cast<float*>(d + o_inf);
     b.pos3_o1 = reinterpret_cast<float*>(d + o_po1);
     b.r9_o1 = reinterpret_cast<float*>(d + o_ro1);
     b.pos3_o2 = reinterpret_cast<float*>(d + o_po2);
@@ -662,6 +976,7 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     c.cap = pitch;
     c.nk = NK;
     c.qcap = (uint32_t)qcap;
+    c.acap = (uint32_t)acap;
     for (int o = 0; o < 8; o++) {
         c.fmax[o] = powf(s->scale_factor, (float)s->num_levels - ((float)o + 0.5f));
         c.fmin[o] = powf(s->scale_factor, 0.f - ((float)o + 0.5f));
@@ -680,24 +995,25 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         return fail(MAGE_EDEVICE);
     hipLaunchKernelGGL(trk_init, dim3(1), dim3(TT), 0, st, b, c, d_kp, d_desc, d_n, dposes, dmt, dil, dkf, rstatus);
     const float radius[3] = {s->search_radius, s->wider_search_radius, s->extra_wider_search_radius};
-    for (uint32_t f = 1; f < frames; f++) {
+    auto enqueue = [&](uint32_t f) -> mage_status {
         const mage_keypoint* fk = d_kp + (size_t)f * pitch;
         const uint8_t* fd = d_desc + 32ull * f * pitch;
         const uint32_t* nf = d_n + f;
+        mage_status rr;
         launch("track.project", trk_project, dim3(1), dim3(TT), 0, st, b, c, (int)f, (const double*)dposes);
         for (int k = 0; k < 3; k++) {
-            r = mage_radius_match_batch_device(b.qkp, k < 2 ? b.qpos : nullptr, b.qdesc, (int64_t)pitch, b.nq + k, fk,
-                                               fd, (int64_t)pitch, nf, 1, radius[k], s->max_hamming,
-                                               s->min_hamming_difference, rscratch, b.m + (size_t)k * pitch, pitch,
-                                               b.mn + k, rstatus, stream);
-            if (r != MAGE_OK) return fail(r);
+            rr = mage_radius_match_batch_device(b.qkp, k < 2 ? b.qpos : nullptr, b.qdesc, (int64_t)pitch, b.nq + k, fk,
+                                                fd, (int64_t)pitch, nf, 1, radius[k], s->max_hamming,
+                                                s->min_hamming_difference, rscratch, b.m + (size_t)k * pitch, pitch,
+                                                b.mn + k, rstatus, stream);
+            if (rr != MAGE_OK) return rr;
             if (k < 2) launch("track.weak", trk_weak, dim3(1), dim3(64), 0, st, b, c, k);
         }
         launch("track.gather", trk_gather, dim3(1), dim3(TT), 0, st, b, c, fk, (int)f, dmt);
-        r = mage_ba_pose_batch_device(1, b.pos3, b.r9, b.intr4, b.os1, b.pts1, b.uv1, b.info, s->initial_steps,
-                                      s->initial_huber, e1, b.pos3_o1, b.r9_o1, nullptr, b.out1, b.msq, nullptr,
-                                      stream);
-        if (r != MAGE_OK) return fail(r);
+        rr = mage_ba_pose_batch_device(1, b.pos3, b.r9, b.intr4, b.os1, b.pts1, b.uv1, b.info1, s->initial_steps,
+                                       s->initial_huber, e1, b.pos3_o1, b.r9_o1, nullptr, b.out1, b.msq, nullptr,
+                                       stream);
+        if (rr != MAGE_OK) return rr;
         launch("track.filter", trk_filter, dim3(1), dim3(TT), 0, st, b, c, nf);
         if (s->local_map_keyframes > 0) {
             launch("track.lm_project", trk_lm_project, dim3(1), dim3(TT), 0, st, b, c);
@@ -717,14 +1033,112 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
             la.min_diff = s->local_min_hamming_difference;
             la.result = b.lm_res;
             la.status = b.lm_status;
-            if ((r = local_map_match_launch(la, b.lm_scratch, st)) != MAGE_OK) return fail(r);
+            if ((rr = local_map_match_launch(la, b.lm_scratch, st)) != MAGE_OK) return rr;
             launch("track.lm_assemble", trk_lm_assemble, dim3(1), dim3(TT), 0, st, b, fk);
         }
-        r = mage_ba_pose_batch_device(1, b.pos3_o1, b.r9_o1, b.intr4, b.os2, b.pts2, b.uv2, b.info, s->final_steps,
-                                      s->final_huber, e2, b.pos3_o2, b.r9_o2, nullptr, b.out2, b.msq + 1, nullptr,
-                                      stream);
-        if (r != MAGE_OK) return fail(r);
+        rr = mage_ba_pose_batch_device(1, b.pos3_o1, b.r9_o1, b.intr4, b.os2, b.pts2, b.uv2, b.info2, s->final_steps,
+                                       s->final_huber, e2, b.pos3_o2, b.r9_o2, nullptr, b.out2, b.msq + 1, nullptr,
+                                       stream);
+        if (rr != MAGE_OK) return rr;
         launch("track.finish", trk_finish, dim3(1), dim3(TT), 0, st, b, c, (int)f, fk, fd, nf, dposes, dil, dkf, rstatus);
+        return MAGE_OK;
+    };
+    if (ba_outliers)
+        for (uint32_t f = 0; f < frames; f++) ba_outliers[f] = 0xFFFFFFFFu;
+    if (!s->local_ba) {
+        for (uint32_t f = 1; f < frames; f++)
+            if ((r = enqueue(f)) != MAGE_OK) return fail(r);
+    } else {
+        // Local BA after every new keyframe (MappingWorker; tracking.py local_bundle_adjust).  The
+        // host stays up to two frames ahead; trk_finish of a keyframe frame sets ctl->halt (the
+        // queued frames become no-ops) and reports it in mapped memory: the host drains the stream,
+        // runs the BA on its copy of the keyframe ring, writes the ring back, clears the halt and
+        // enqueues the following frames again.
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return fail(MAGE_EDEVICE);
+        MappedBuffer prog;
+        if ((r = prog.reserve(64)) != MAGE_OK) return fail(r);
+        volatile uint32_t* hp = prog.host<volatile uint32_t>();
+        hp[0] = 0;
+        hp[1] = 0;
+        b.prog = prog.device<uint32_t>();
+        HostRing R;
+        R.nk = NK;
+        R.cap = (uint32_t)cap;
+        R.acap = (uint32_t)acap;
+        LocalBA L;
+        std::vector<uint8_t> changed(NK);
+        uint32_t next = 1;
+        constexpr uint32_t DEPTH = 2;
+        for (uint32_t f = 1; f < frames; f++) {
+            while (next < frames && next <= f + DEPTH)
+                if ((r = enqueue(next++)) != MAGE_OK) return fail(r);
+            const auto t0 = std::chrono::steady_clock::now();
+            while (hp[0] < f) {  // frame f done (trk_finish writes its index last)
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+                    if (hipStreamSynchronize(st) != hipSuccess) return fail(MAGE_EDEVICE);
+                    if (hp[0] < f) return fail(MAGE_EDEVICE);
+                }
+            }
+            std::atomic_thread_fence(std::memory_order_acquire);
+            if (hp[1] != f) continue;
+            // a local BA: the halted frames drain, the ring comes to the host
+            if (hipStreamSynchronize(st) != hipSuccess) return fail(MAGE_EDEVICE);
+            Ctl hc;
+            if (hipMemcpy(&hc, b.ctl, sizeof(Ctl), hipMemcpyDeviceToHost) != hipSuccess) return fail(MAGE_EDEVICE);
+            R.first = hc.kf_first;
+            R.count = hc.kf_count;
+            for (uint32_t k = 0; k < NK; k++) {
+                R.n[k] = hc.kf_n[k];
+                R.id[k] = hc.kf_id[k];
+                R.an[k] = hc.kf_an[k];
+            }
+            R.pose.resize(12 * NK);
+            R.kp.resize(cap * NK);
+            R.pts.resize(3 * cap * NK);
+            R.mvd.resize(3 * cap * NK);
+            R.dmin.resize(cap * NK);
+            R.dmax.resize(cap * NK);
+            R.ref.resize(cap * NK);
+            R.own.resize(cap * NK);
+            R.assoc.resize(acap * NK);
+            R.aalive.resize(acap * NK);
+            if (hipMemcpy(R.pose.data(), b.kf_pose, 96 * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.kp.data(), b.kf_kp, 28 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.pts.data(), b.kf_pts, 12 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.mvd.data(), b.kf_mvd, 12 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.dmin.data(), b.kf_dmin, 4 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.dmax.data(), b.kf_dmax, 4 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.ref.data(), b.kf_ref, 4 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.own.data(), b.kf_own, cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.assoc.data(), b.kf_assoc, 16 * acap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(R.aalive.data(), b.kf_aalive, acap * NK, hipMemcpyDeviceToHost) != hipSuccess)
+                return fail(MAGE_EDEVICE);
+            std::fill(changed.begin(), changed.end(), 0);
+            uint32_t nout = 0;
+            if ((r = host_local_ba(R, c, L, dev, &nout, changed)) != MAGE_OK) return fail(r);
+            if (ba_outliers) ba_outliers[f] = nout;
+            // write back the changed slots, the frame's pose (= its keyframe's) and clear the halt
+            for (uint32_t k = 0; k < NK; k++) {
+                if (!changed[k]) continue;
+                const size_t o = (size_t)k * cap, ao = (size_t)k * acap;
+                if (hipMemcpy(b.kf_pose + 12 * k, &R.pose[12 * k], 96, hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(b.kf_pts + 3 * o, &R.pts[3 * o], 12 * cap, hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(b.kf_mvd + 3 * o, &R.mvd[3 * o], 12 * cap, hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(b.kf_dmin + o, &R.dmin[o], 4 * cap, hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(b.kf_dmax + o, &R.dmax[o], 4 * cap, hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(b.kf_ref + o, &R.ref[o], 4 * cap, hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(b.kf_own + o, &R.own[o], cap, hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(b.kf_aalive + ao, &R.aalive[ao], acap, hipMemcpyHostToDevice) != hipSuccess)
+                    return fail(MAGE_EDEVICE);
+            }
+            const uint32_t newest = (R.first + R.count - 1) % NK;
+            const uint32_t zero = 0;
+            if (hipMemcpy(dposes + 12ull * f, &R.pose[12 * newest], 96, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(&b.ctl->halt, &zero, 4, hipMemcpyHostToDevice) != hipSuccess)
+                return fail(MAGE_EDEVICE);
+            next = f + 1;
+        }
     }
     if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
     uint32_t rst = 0, lst = 0;

@@ -60,6 +60,17 @@ class TrackerSettings:
     num_levels: int = 1
     width: int = 1280                      # AnalyzedImage size (PointWithinImageBorder)
     height: int = 720
+    # Local bundle adjustment after every new keyframe, as MappingWorker runs it
+    # (MappingWorker.cpp:228-371; BundleAdjustSettings / CovisibilitySettings / MappingSettings,
+    # MageSettings.h:41-52, 74-79, 253-260): see local_bundle_adjust.  Off by default.
+    local_ba: bool = False
+    ba_huber: float = 1.8                  # BundleAdjustSettings::HuberWidth
+    ba_huber_scale: float = 0.95           # ::HuberWidthScale
+    ba_max_outlier_error: float = 7.25     # ::MaxOutlierError (the first maxErrorSquare, BundleAdjust.cpp:375)
+    ba_steps_per_run: int = 1              # ::NumStepsPerRun (NumSteps = MinSteps = 1: one call per keyframe)
+    ba_low_connectivity_scale: float = 1.5  # ::LowConnectivityIterationsScale
+    ba_upper_connections: int = 2000       # CovisibilitySettings::UpperConnectionsForBA
+    min_lambda: float = 1e-3               # MappingSettings::MinLambda (PersistLambda on)
 
     def min_view_cos(self) -> np.float32:
         """std::cos(mira::deg2rad(degrees)) in float (arcana/math.h:86-90: degrees * (PI / 180))."""
@@ -125,6 +136,16 @@ class Keyframe:
     mvd: np.ndarray | None = None   # (n, 3) float32 mean viewing direction
     dmin: np.ndarray | None = None  # (n,) float32 scale-invariance distances
     dmax: np.ndarray | None = None
+    # mapping side (local_ba): per point its refinement count (MapPoint::IncrementRefinementCount)
+    # and whether the keyframe's own observation of it is still associated; the keyframe's
+    # associations to other keyframes' points (its frame's pass-2 inliers): owner keyframe id,
+    # point index, keypoint position, alive
+    refine: np.ndarray | None = None
+    own_alive: np.ndarray | None = None
+    assoc_owner: np.ndarray | None = None
+    assoc_idx: np.ndarray | None = None
+    assoc_uv: np.ndarray | None = None
+    assoc_alive: np.ndarray | None = None
 
 
 def _dot3(a, b):
@@ -162,8 +183,146 @@ def make_keyframe(fid: int, pose: Pose, kp, desc, K, plane_z: float, s: "Tracker
     dist = np.sqrt((delta[:, 0] * delta[:, 0] + delta[:, 1] * delta[:, 1]) + delta[:, 2] * delta[:, 2]).astype(np.float32)
     fmax, fmin = s.octave_factors()
     octv = np.asarray(kp["octave"], np.int64)
+    n = len(kp)
     return Keyframe(pose, kp, desc, pts, fid, mvd, (dist * fmin[octv]).astype(np.float32),
-                    (dist * fmax[octv]).astype(np.float32))
+                    (dist * fmax[octv]).astype(np.float32), refine=np.zeros(n, np.uint32),
+                    own_alive=np.ones(n, bool), assoc_owner=np.zeros(0, np.int64), assoc_idx=np.zeros(0, np.int64),
+                    assoc_uv=np.zeros((0, 2), np.float32), assoc_alive=np.zeros(0, bool))
+
+
+def point_attributes(kf: Keyframe, s: "TrackerSettings", idx: np.ndarray) -> None:
+    """make_keyframe's MapPoint::UpdateMeanViewDirectionAndDistances of kf's points `idx`, again from
+    its current pose and points (after a local BA moved them: UpdateData, then SetPosition)."""
+    C = world_position_f32(kf.pose)
+    pts = kf.points[idx]
+    v = (pts - C).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        d = np.sqrt(_dot3(v, v)).astype(np.float32)
+        n1 = np.where(d[:, None] == 0, v, v * (np.float32(1) / d)[:, None]).astype(np.float32)
+        d2 = np.sqrt(_dot3(n1, n1)).astype(np.float32)
+        kf.mvd[idx] = np.where(d2[:, None] == 0, n1, n1 * (np.float32(1) / d2)[:, None]).astype(np.float32)
+    delta = (C - pts).astype(np.float32)
+    dist = np.sqrt((delta[:, 0] * delta[:, 0] + delta[:, 1] * delta[:, 1]) + delta[:, 2] * delta[:, 2]).astype(np.float32)
+    fmax, fmin = s.octave_factors()
+    octv = np.asarray(kf.kp["octave"][idx], np.int64)
+    kf.dmin[idx] = (dist * fmin[octv]).astype(np.float32)
+    kf.dmax[idx] = (dist * fmax[octv]).astype(np.float32)
+
+
+def refinement_confidence(count) -> np.ndarray:
+    """MapPointRefinementConfidence (Map/MappingMath.h:42-49): 1 - 1 / powf(1.5 + count, 2) in float."""
+    c = np.asarray(count, np.float32)
+    return (np.float32(1.0) - np.float32(1.0) / np.power(np.float32(1.5) + c, np.float32(2.0))).astype(np.float32)
+
+
+@dataclass
+class BAWindow:
+    """One local BA problem in BundlerLib's boundary layout (synth.BAGraph's fields) and how its
+    observations map back to the keyframes' associations."""
+    pos: np.ndarray
+    rot: np.ndarray
+    intr: np.ndarray
+    fixed: np.ndarray
+    points: np.ndarray
+    uv: np.ndarray
+    cam: np.ndarray
+    pt: np.ndarray
+    info: np.ndarray
+    point_src: list        # (ring position of the owner, point index) per point
+    obs_src: list          # ("own" | "assoc", ring position of the observer, index) per observation
+    huber_widths: list
+    max_error_square: float
+
+    @property
+    def rot_colmajor(self) -> np.ndarray:
+        return np.ascontiguousarray(np.transpose(self.rot, (0, 2, 1)).reshape(-1, 9))
+
+
+def build_ba_window(ring, K, s: "TrackerSettings") -> BAWindow | None:
+    """GetMapPointsAndDistantKeyframes + BuildDataForG2O (ThreadSafeMap.cpp:880-960; BundleAdjust.cpp:
+    25-193) over this loop's map: the keyframes of the local map (ascending id), the oldest one fixed
+    (the reference fixes the observing keyframes outside the covisible set; here the local map is the
+    last keyframes, so its oldest member anchors the window); the points they own that a free keyframe
+    observes; every alive association of those points, per camera: its own points (ascending index),
+    then its associations in the order its frame made them.  info = MapPointRefinementConfidence of
+    the point's refinement count.  NumStepsPerRun and the Huber width scale with the connectivity
+    ratio UpperConnectionsForBA / associations (MappingWorker.cpp:254-263)."""
+    if len(ring) < 2:
+        return None
+    pos_of = {k.id: c for c, k in enumerate(ring)}
+    obs = []  # (cam, owner ring position, point index, u, v, src)
+    for c, k in enumerate(ring):
+        for i in np.nonzero(k.own_alive)[0]:
+            obs.append((c, c, int(i), k.kp["x"][i], k.kp["y"][i], ("own", c, int(i))))
+        for a in range(len(k.assoc_owner)):
+            o = pos_of.get(int(k.assoc_owner[a]))
+            if k.assoc_alive[a] and o is not None:
+                obs.append((c, o, int(k.assoc_idx[a]), k.assoc_uv[a, 0], k.assoc_uv[a, 1], ("assoc", c, a)))
+    seen_free = {(o, i) for c, o, i, _, _, _ in obs if c > 0}
+    point_src = sorted(seen_free)
+    pidx = {key: n for n, key in enumerate(point_src)}
+    obs = [ob for ob in obs if (ob[1], ob[2]) in pidx]
+    if not obs:
+        return None
+    fx, fy, cx, cy = K
+    npts = len(point_src)
+    points = np.zeros((npts, 3), np.float32)
+    refine = np.zeros(npts, np.uint32)
+    for n, (o, i) in enumerate(point_src):
+        points[n] = ring[o].points[i]
+        refine[n] = ring[o].refine[i]
+    pt = np.array([pidx[(ob[1], ob[2])] for ob in obs], np.uint32)
+    A = len(obs)
+    ratio = s.ba_upper_connections // A
+    steps = s.ba_steps_per_run
+    huber = np.float32(s.ba_huber)
+    if ratio > 0:
+        steps = steps * int(np.float32(ratio) * np.float32(s.ba_low_connectivity_scale))
+        huber = np.float32(huber * _libm_f("powf", np.float32(s.ba_huber_scale), np.float32(ratio)))
+    return BAWindow(pos=np.stack([k.pose.t for k in ring]).astype(np.float32),
+                    rot=np.stack([k.pose.R for k in ring]).astype(np.float32),
+                    intr=np.tile(np.float32([cx, cy, fx, fy]), (len(ring), 1)),
+                    fixed=np.array([1] + [0] * (len(ring) - 1), np.uint8), points=points,
+                    uv=np.array([[ob[3], ob[4]] for ob in obs], np.float32),
+                    cam=np.array([ob[0] for ob in obs], np.uint32), pt=pt, info=refinement_confidence(refine[pt]),
+                    point_src=point_src, obs_src=[ob[5] for ob in obs], huber_widths=[float(huber)] * max(steps, 1),
+                    max_error_square=float(np.float32(s.ba_max_outlier_error)))
+
+
+def apply_ba_window(ring, w: BAWindow, outliers, pos, r9, points, s: "TrackerSettings") -> None:
+    """AdjustPosesAndMapPoints (ThreadSafeMap.cpp:995-1046) after UpdateData (BundleAdjust.cpp:195-226):
+    the outlier associations removed, the free keyframes' poses and every point of the window from
+    GetPose / GetPoint (floats), refinement counts + 1, then the points' view attributes again.
+    (Map-point culling and the covisibility graph update are outside this loop's map.)"""
+    for e in outliers:
+        kind, c, i = w.obs_src[int(e)]
+        if kind == "own":
+            ring[c].own_alive[i] = False
+        else:
+            ring[c].assoc_alive[i] = False
+    for c, k in enumerate(ring):
+        if not w.fixed[c]:
+            k.pose = Pose(r9[c].reshape(3, 3).T.astype(np.float64), pos[c].astype(np.float64))
+    moved = [[] for _ in ring]
+    for n, (o, i) in enumerate(w.point_src):
+        ring[o].points[i] = points[n]
+        ring[o].refine[i] += 1
+        moved[o].append(i)
+    for c, k in enumerate(ring):  # the moved points' attributes (their owners' poses already updated)
+        if moved[c]:
+            point_attributes(k, s, np.asarray(moved[c], np.int64))
+
+
+def local_bundle_adjust(ring, K, s: "TrackerSettings", backend: "Backend", lam):
+    """One MappingWorker local BA after a new keyframe (NumSteps = 1: one StepBundleAdjustment at
+    MaxOutlierError, BundleAdjust.cpp:375-404, with the persisted lambda).  Returns (the next lambda,
+    the outlier observation count) or (lam, None) when there is no window."""
+    w = build_ba_window(ring, K, s)
+    if w is None:
+        return lam, None
+    outl, pos, r9, pts, lam_out = backend.bundle_adjust(w, lam)
+    apply_ba_window(ring, w, outl, pos, r9, pts, s)
+    return max(lam_out, s.min_lambda), len(outl)
 
 
 def local_map_queries(kfs, ref: Keyframe, visited_ref: np.ndarray, hide_ref: np.ndarray, pose: Pose, K,
@@ -232,6 +391,7 @@ class TrackResult:
     inliers: list = field(default_factory=list)    # associations after the outlier removal
     keyframes: list = field(default_factory=list)  # frame indices that became keyframes
     local_matches: list = field(default_factory=list)  # new associations of the local-map search
+    ba_outliers: list = field(default_factory=list)  # (keyframe frame, outlier count) per local BA
 
     def translations(self) -> np.ndarray:
         return np.stack([p.t for p in self.poses])
@@ -284,6 +444,22 @@ class Backend:
         """TrackLocalMap's sequential per-point matching -> (keypoint per query or -1, updated mask)"""
         raise NotImplementedError
 
+    def bundle_adjust(self, w: "BAWindow", lam):
+        """BuildDataForG2O(w) + SetCurrentLambda(lam) (unless None) + one StepBundleAdjustment(
+        w.huber_widths, w.max_error_square) + GetPose / GetPoint -> (outliers, pos (C, 3), r9 (C, 9)
+        column-major, points (P, 3), GetCurrentLambda())."""
+        raise NotImplementedError
+
+
+def run_bundler(b, w: "BAWindow", lam, set_lambda, get_lambda):
+    """Backend.bundle_adjust on a BundlerLib-shaped object (GPU BundlerLib or the CPU oracle's)."""
+    b.set_graph(w)
+    if lam is not None:
+        set_lambda(lam)
+    _, outl = b.step(w.huber_widths, w.max_error_square)
+    pos, r9 = b.poses()
+    return np.asarray(outl, np.int64), pos, r9, b.points(), float(get_lambda())
+
 
 class GpuBackend(Backend):
     """libmage_hot.so: batched ORB, RadiusMatch, batched pose-only BA (one problem)."""
@@ -334,6 +510,13 @@ class GpuBackend(Backend):
         return matcher.LocalMapMatch(qpos, qoct, qdesc, tkp, tdesc, mask, radius, max_hamming, min_diff,
                                      queryHidden=qhide, device=self.device)
 
+    def bundle_adjust(self, w, lam):
+        from . import bundler
+
+        if getattr(self, "_ba", None) is None:
+            self._ba = bundler.BundlerLib(device=self.device)
+        return run_bundler(self._ba, w, lam, self._ba.SetCurrentLambda, self._ba.GetCurrentLambda)
+
 
 @dataclass
 class _Problem:
@@ -354,7 +537,7 @@ def pose_problem(pose: Pose, K, points, uv, info) -> _Problem:
     return _Problem(pos=pose.t.astype(np.float32)[None], r9=pose.R.astype(np.float32).T.reshape(1, 9),
                     intr=np.float32([[cx, cy, fx, fy]]), obs_start=np.array([0, n], np.uint32),
                     points=np.ascontiguousarray(points, np.float32), uv=np.ascontiguousarray(uv, np.float32),
-                    info=np.full(n, info, np.float32))
+                    info=np.broadcast_to(np.asarray(info, np.float32), (n,)).copy())
 
 
 def pose_from_result(r) -> Pose:
@@ -384,6 +567,7 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
     res.inliers.append(len(kp0))
     res.keyframes.append(0)
     res.local_matches.append(0)
+    lam = None  # the persisted local-BA lambda (MappingWorker: CurrentLambda)
     for t in range(1, T):
         kp, desc = features[t]
         # motion model: constant velocity on SE3 (the tracker's predicted pose)
@@ -413,10 +597,14 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
         tidx = m["train_idx"].astype(np.int64)  # their keypoints
         pts = kf.points[qidx]
         uv = np.stack([kp["x"][tidx], kp["y"][tidx]], 1)
+        # information per observation: MapPointRefinementConfidence of the point's refinement count
+        # (TrackLocalMap.cpp:473-475; every count is 0 without the local BA)
+        info = refinement_confidence(kf.refine[qidx])
         steps, huber, err = s.initial_ba
-        pose, out = backend.optimize_pose(pred, K, pts, uv, s.refinement_info, steps, huber, err * err)
+        pose, out = backend.optimize_pose(pred, K, pts, uv, info, steps, huber, err * err)
         keep = ~out
-        pts2, uv2 = pts[keep], uv[keep]
+        pts2, uv2, info2 = pts[keep], uv[keep], info[keep]
+        own2, idx2 = np.full(int(keep.sum()), kf.id, np.int64), qidx[keep].astype(np.int64)  # the points' sources
         n_new = 0
         if s.local_map_keyframes > 0:
             if not keep.any():  # mapPoints.empty() after the outliers are unassociated (:149-150)
@@ -433,12 +621,18 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
                 r, _ = backend.local_map_match(lp, lo, ld, lh, kp, desc, mask, s.match_search_radius,
                                                s.local_max_hamming, s.local_min_hamming_difference)
                 qpts = np.concatenate([k.points[i] for k, i in src]).reshape(-1, 3)
+                qown = np.concatenate([np.full(len(i), k.id, np.int64) for k, i in src])
+                qidx2 = np.concatenate([np.asarray(i, np.int64) for _, i in src])
+                qinfo = np.concatenate([refinement_confidence(k.refine[i]) for k, i in src])
                 hit = r >= 0
                 n_new = int(hit.sum())
                 pts2 = np.concatenate([pts2, qpts[hit]]).astype(np.float32)
                 uv2 = np.concatenate([uv2, np.stack([kp["x"][r[hit]], kp["y"][r[hit]]], 1)]).astype(np.float32)
+                info2 = np.concatenate([info2, qinfo[hit]]).astype(np.float32)
+                own2 = np.concatenate([own2, qown[hit]])
+                idx2 = np.concatenate([idx2, qidx2[hit]])
         steps, huber, err = s.final_ba
-        pose, out2 = backend.optimize_pose(pose, K, pts2, uv2, s.refinement_info, steps, huber, err * err)
+        pose, out2 = backend.optimize_pose(pose, K, pts2, uv2, info2, steps, huber, err * err)
         n_in = int((~out2).sum())
         if s.local_map_keyframes > 0 and n_in < s.min_tracked:  # TrackLocalMap.cpp:309-314
             lost()
@@ -448,8 +642,16 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
         res.local_matches.append(n_new)
         if n_in < s.keyframe_ratio * len(kf.points) + s.keyframe_min:
             kf = make_keyframe(t, pose, kp, desc, K, plane_z, s)
+            inl = ~out2  # the new keyframe's associations: its frame's pass-2 inliers
+            kf.assoc_owner, kf.assoc_idx = own2[inl], idx2[inl]
+            kf.assoc_uv, kf.assoc_alive = uv2[inl].astype(np.float32), np.ones(int(inl.sum()), bool)
             kfs = (kfs + [kf])[-max(s.local_map_keyframes, 1):]
             res.keyframes.append(t)
+            if s.local_ba:
+                lam, n_out = local_bundle_adjust(kfs, K, s, backend, lam)
+                if n_out is not None:
+                    res.ba_outliers.append((t, n_out))
+                    res.poses[-1] = kf.pose  # this frame's pose as the BA left its keyframe
     return res
 
 
@@ -497,7 +699,9 @@ def _settings_c(s: TrackerSettings):
                                s.final_ba[2], s.refinement_info, s.keyframe_ratio, s.keyframe_min,
                                s.local_map_keyframes, s.match_search_radius, s.local_max_hamming,
                                s.local_min_hamming_difference, float(s.min_view_cos()), s.image_border, s.min_tracked,
-                               s.scale_factor, s.num_levels, s.width, s.height)
+                               s.scale_factor, s.num_levels, s.width, s.height, int(s.local_ba), s.ba_huber,
+                               s.ba_huber_scale, s.ba_max_outlier_error, s.ba_steps_per_run, s.ba_low_connectivity_scale,
+                               s.ba_upper_connections, s.min_lambda)
 
 
 def track_native_device(d_kp, d_desc, pitch: int, d_counts, frames: int, K, first_pose: Pose, plane_z: float,
@@ -519,16 +723,18 @@ def track_native_device(d_kp, d_desc, pitch: int, d_counts, frames: int, K, firs
     matches = np.zeros(max(T, 1), np.uint32)
     inliers = np.zeros(max(T, 1), np.uint32)
     kf = np.zeros(max(T, 1), np.uint8)
+    bo = np.full(max(T, 1), 0xFFFFFFFF, np.uint32)
     _lib.check(_lib.load().mage_track_sequence_device(
         _lib.ptr(d_kp), _lib.ptr(d_desc), int(pitch), _lib.ptr(d_counts), T, _lib.ptr(Kd), _lib.ptr(p0),
         float(plane_z), C.byref(cs), _lib.ptr(poses), _lib.ptr(matches), _lib.ptr(inliers), _lib.ptr(kf),
-        C.c_void_p(stream) if stream else None))
+        _lib.ptr(bo), C.c_void_p(stream) if stream else None))
     res = TrackResult()
     for f in range(T):
         res.poses.append(Pose(poses[f, :9].reshape(3, 3).copy(), poses[f, 9:].copy()))
     res.matches = [int(x) for x in matches[:T]]
     res.inliers = [int(x) for x in inliers[:T]]
     res.keyframes = [int(f) for f in np.nonzero(kf[:T])[0]]
+    res.ba_outliers = [(int(f), int(bo[f])) for f in range(T) if bo[f] != 0xFFFFFFFF]
     return res
 
 

@@ -33,3 +33,8 @@ class OracleBackend(tracking.Backend):
         r, m = O.local_map_match(qpos, qoct, qdesc, qhide, tkp, tdesc, mask.astype(np.uint8), radius, max_hamming,
                                  min_diff)
         return r, m.astype(bool)
+
+    def bundle_adjust(self, w, lam):
+        if getattr(self, "_ba", None) is None:
+            self._ba = O.BundlerOracle()
+        return tracking.run_bundler(self._ba, w, lam, self._ba.set_lambda, self._ba.get_lambda)

@@ -89,6 +89,40 @@ def test_tracking_loop_720p_gpu_vs_oracle(gpu, oracle):
     assert rt <= 1e-4 and rr <= 1e-4, (rt, rr)
 
 
+def test_tracking_loop_local_ba_720p_device_vs_oracle(gpu, oracle):
+    """C4 composed with the local BA MappingWorker runs after every new keyframe
+    (tracking.local_bundle_adjust: the local map's keyframes, oldest fixed, one StepBundleAdjustment
+    at MaxOutlierError with the persisted lambda, poses / points / refinement counts written back
+    before the next frame tracks): the device loop (mage_track_sequence_device, BundlerLib between
+    frames) and the Python loop on the GPU backend against the oracle loop at 1280 x 720 over 96
+    frames — identical matches, inliers, keyframes and BA outlier counts, pose RMSE <= 1e-4."""
+    from oracle.tracking_backend import OracleBackend
+
+    seq = synth.scene_sequence(96, 1280, 720, step=0.06)
+    frames = synth.scene_frames(seq)
+    K = (seq.fx, seq.fy, seq.cx, seq.cy)
+    p0 = tracking.Pose(seq.R[0], seq.t[0])
+    gb = tracking.GpuBackend(2000)
+    gf = gb.extract(frames)
+    ob = OracleBackend(2000)
+    of = ob.extract(frames)
+    s = tracking.TrackerSettings(local_ba=True)
+    o = tracking.track(of, K, p0, synth.SCENE_PLANE_Z, ob, s)
+    g = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb, s)
+    d = tracking.track_native_device(*tracking.features_to_device(gf), len(gf), K, p0, synth.SCENE_PLANE_Z,
+                                     settings=s)
+    assert len(o.ba_outliers) >= 2, o.ba_outliers  # at least two windows
+    for r in (g, d):
+        assert r.matches == o.matches and r.inliers == o.inliers and r.keyframes == o.keyframes
+        assert r.ba_outliers == o.ba_outliers
+        rt, rr = tracking.pose_rmse(r, o)
+        assert rt <= 1e-4 and rr <= 1e-4, (rt, rr)
+    _same(d, g)  # the device loop and the Python loop over the same GPU kernels: bit-identical
+    # the BA changed the map: without it the same frames give other poses
+    n = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb, tracking.TrackerSettings())
+    assert any(not np.array_equal(a.t, b.t) for a, b in zip(n.poses, g.poses))
+
+
 def test_native_tracking_loop_720p_keyframes(gpu):
     """A 720p pan long enough for keyframe switches: native loop == Python loop over the GPU
     kernels, frame by frame (poses bit-identical), and within a centimetre of the ground truth."""

@@ -1,4 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_match.py "tests/test_gpu_ba.py::test_repeated_setters_before_a_step" -x -q --timeout 120 --timeout-method thread > gpurun_out/t_match.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-ba --no-pose --no-tracking --no-cpu-baseline --pipelined-streams 0 --no-all-cores > gpurun_out/b_orb.json 2> gpurun_out/b_orb.err
+timeout -k 10 600 python -u -m pytest tests/test_gpu_orb.py tests/test_stereo_scale.py tests/test_gpu_image.py tests/test_gpu_tracking.py -x -q --timeout 300 --timeout-method thread > gpurun_out/t_orb.log 2>&1 || { tail -30 gpurun_out/t_orb.log; exit 1; }
+tail -2 gpurun_out/t_orb.log
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-ba --no-pose --no-tracking --no-cpu-baseline --pipelined-streams 0 --no-all-cores --orb-variant rbrief31 > gpurun_out/b_orb31.json 2> gpurun_out/b_orb31.err
