@@ -490,6 +490,7 @@ typedef struct mage_track_settings {
     float ba_low_connectivity_scale;                                     /* 1.5 */
     uint32_t ba_upper_connections;                                       /* UpperConnectionsForBA 2000 */
     float min_lambda;                                                    /* MappingSettings::MinLambda 1e-3 */
+    uint32_t ba_free_keyframes;  /* the newest keyframes of the window that move (older ones fixed, >= 1): 2 */
 } mage_track_settings;
 
 /* Features of `frames` frames (host): keypoints kp[frame_start[f] .. frame_start[f+1]) and their

@@ -103,7 +103,7 @@ class TrackSettingsC(C.Structure):
                 ("local_ba", C.c_uint32), ("ba_huber", C.c_float), ("ba_huber_scale", C.c_float),
                 ("ba_max_outlier_error", C.c_float), ("ba_steps_per_run", C.c_uint32),
                 ("ba_low_connectivity_scale", C.c_float), ("ba_upper_connections", C.c_uint32),
-                ("min_lambda", C.c_float)]
+                ("min_lambda", C.c_float), ("ba_free_keyframes", C.c_uint32)]
 
 
 class BAStats(C.Structure):

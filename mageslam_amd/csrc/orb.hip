@@ -1577,40 +1577,89 @@ __global__ __launch_bounds__(256) void resize_linear_kernel(const uint8_t* __res
     dst[(long long)f * p.dpitch + (long long)dy * p.dstride + dx] = (uint8_t)min(max(v, 0), 255);
 }
 
-// The same resize with a workgroup per output row (and frame): the two source rows it reads are
-// staged in LDS with dword loads, each thread forms four consecutive output pixels from LDS bytes
-// (exactly resize_linear_kernel's arithmetic) and stores them as one dword.  Source rows up to
-// RZ_MAXW bytes; resize_linear_kernel serves wider ones.
-constexpr int RZ_MAXW = 4096;
-__global__ __launch_bounds__(256) void resize_rows_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+// The same resize with a workgroup per band of RZ_BAND output rows (and frame): the source rows
+// the band reads are staged in LDS (dynamic size: rows x source width, from the host's row tables)
+// with dword loads, then each thread forms four consecutive output pixels from LDS bytes (exactly
+// resize_linear_kernel's arithmetic) and stores them as one dword.  One small workgroup per output
+// row left the launch dispatch-bound (0.67 ms for the 3 levels of 256 frames).
+constexpr int RZ_MAXW = 4096;  // source rows up to this width (resize_linear_kernel beyond)
+constexpr int RZ_BAND = 8;     // output rows per workgroup
+constexpr size_t RZ_MAX_LDS = 60 * 1024;
+
+// Source rows of band `band` (first, count) from the host copy of the row table.
+inline void rz_band_rows(const int* yofs, int dh, int sh, int area2, int band, int& r0, int& n)
+{
+    const int d0 = band * RZ_BAND, d1 = std::min(d0 + RZ_BAND, dh) - 1;
+    if (area2) {
+        r0 = 2 * d0;
+        n = 2 * (d1 - d0 + 1);
+        return;
+    }
+    r0 = std::min(std::max(yofs[d0], 0), sh - 1);
+    const int r1 = std::min(std::max(yofs[d1] + 1, 0), sh - 1);
+    n = r1 - r0 + 1;
+}
+
+// LDS bytes per workgroup for a resize (rows of the widest band x padded source width)
+inline size_t rz_lds_bytes(const int* yofs, int sw, int sh, int dh, int area2)
+{
+    int maxn = 0;
+    for (int b = 0; b * RZ_BAND < dh; b++) {
+        int r0, n;
+        rz_band_rows(yofs, dh, sh, area2, b, r0, n);
+        maxn = std::max(maxn, n);
+    }
+    return (size_t)maxn * (size_t)((sw + 15) & ~15);
+}
+
+__global__ __launch_bounds__(256) void resize_band_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                           ResizeParams p)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t rows[2][RZ_MAXW + 16];
-    const int f = blockIdx.z, dy = blockIdx.y, tid = threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) uint8_t rz_rows[];
+    const int f = blockIdx.z, tid = threadIdx.x;
+    const int d0 = blockIdx.x * RZ_BAND, nd = min(RZ_BAND, p.dh - d0);
+    const int swp = (p.sw + 15) & ~15;
     const uint8_t* S = src + (long long)f * p.spitch;
-    uint8_t* D = dst + (long long)f * p.dpitch + (long long)dy * p.dstride;
-    int ry[2];
+    int r0, r1;
     if (p.area2) {
-        ry[0] = 2 * dy;
-        ry[1] = 2 * dy + 1;
+        r0 = 2 * d0;
+        r1 = 2 * (d0 + nd) - 1;
     } else {
-        const int sy = p.yofs[dy];
-        ry[0] = min(max(sy, 0), p.sh - 1);
-        ry[1] = min(max(sy + 1, 0), p.sh - 1);
+        r0 = min(max(p.yofs[d0], 0), p.sh - 1);
+        r1 = min(max(p.yofs[d0 + nd - 1] + 1, 0), p.sh - 1);
     }
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-        const uint8_t* R = S + (long long)ry[r] * p.sstride;
-        if ((reinterpret_cast<uintptr_t>(R) & 3) == 0 && (p.sw & 3) == 0) {
-            for (int i = tid; i < (p.sw >> 2); i += 256)
-                reinterpret_cast<uint32_t*>(rows[r])[i] = reinterpret_cast<const uint32_t*>(R)[i];
-        } else {
-            for (int i = tid; i < p.sw; i += 256) rows[r][i] = R[i];
+    const int nr = r1 - r0 + 1;
+    const bool aligned = (reinterpret_cast<uintptr_t>(S) & 3) == 0 && (p.sstride & 3) == 0 && (p.sw & 3) == 0;
+    if (aligned) {
+        const int wq = p.sw >> 2;
+        for (int i = tid; i < nr * wq; i += 256) {
+            const int r = i / wq, q = i - r * wq;
+            reinterpret_cast<uint32_t*>(rz_rows + (size_t)r * swp)[q] =
+                reinterpret_cast<const uint32_t*>(S + (long long)(r0 + r) * p.sstride)[q];
+        }
+    } else {
+        for (int i = tid; i < nr * p.sw; i += 256) {
+            const int r = i / p.sw, x = i - r * p.sw;
+            rz_rows[(size_t)r * swp + x] = S[(long long)(r0 + r) * p.sstride + x];
         }
     }
     __syncthreads();
-    const bool dword_out = (reinterpret_cast<uintptr_t>(D) & 3) == 0;
-    for (int x4 = tid; 4 * x4 < p.dw; x4 += 256) {
+    const int nq = (p.dw + 3) >> 2;
+    for (int it = tid; it < nd * nq; it += 256) {
+        const int dr = it / nq, x4 = it - dr * nq, dy = d0 + dr;
+        const uint8_t *R0, *R1;
+        int b0 = 0, b1 = 0;
+        if (p.area2) {
+            R0 = rz_rows + (size_t)(2 * dy - r0) * swp;
+            R1 = R0 + swp;
+        } else {
+            const int sy = p.yofs[dy];
+            R0 = rz_rows + (size_t)(min(max(sy, 0), p.sh - 1) - r0) * swp;
+            R1 = rz_rows + (size_t)(min(max(sy + 1, 0), p.sh - 1) - r0) * swp;
+            const uint32_t b = p.beta[dy];
+            b0 = (short)(b & 0xFFFFu);
+            b1 = (short)(b >> 16);
+        }
         uint32_t out = 0;
 #pragma unroll
         for (int e = 0; e < 4; e++) {
@@ -1618,19 +1667,19 @@ __global__ __launch_bounds__(256) void resize_rows_kernel(const uint8_t* __restr
             if (dx >= p.dw) break;
             int v;
             if (p.area2) {
-                const int sum = rows[0][2 * dx] + rows[0][2 * dx + 1] + rows[1][2 * dx] + rows[1][2 * dx + 1];
+                const int sum = R0[2 * dx] + R0[2 * dx + 1] + R1[2 * dx] + R1[2 * dx + 1];
                 v = dx < p.xv ? (sum + 2) >> 2 : __float2int_rn((float)sum * 0.25f);
             } else {
                 const int sx = p.xofs[dx];
-                const uint32_t a = p.alpha[dx], b = p.beta[dy];
-                const int a0 = (short)(a & 0xFFFFu), a1 = (short)(a >> 16), b0 = (short)(b & 0xFFFFu), b1 = (short)(b >> 16);
+                const uint32_t a = p.alpha[dx];
+                const int a0 = (short)(a & 0xFFFFu), a1 = (short)(a >> 16);
                 int h0, h1;
                 if (dx < p.xmax) {
-                    h0 = rows[0][sx] * a0 + rows[0][sx + 1] * a1;
-                    h1 = rows[1][sx] * a0 + rows[1][sx + 1] * a1;
+                    h0 = R0[sx] * a0 + R0[sx + 1] * a1;
+                    h1 = R1[sx] * a0 + R1[sx + 1] * a1;
                 } else {
-                    h0 = rows[0][sx] * 2048;
-                    h1 = rows[1][sx] * 2048;
+                    h0 = R0[sx] * 2048;
+                    h1 = R1[sx] * 2048;
                 }
                 if (dx < p.xv)
                     v = (((((int)(short)(h0 >> 4)) * b0) >> 16) + ((((int)(short)(h1 >> 4)) * b1) >> 16) + 2) >> 2;
@@ -1640,7 +1689,8 @@ __global__ __launch_bounds__(256) void resize_rows_kernel(const uint8_t* __restr
             }
             out |= (uint32_t)v << (8 * e);
         }
-        if (dword_out && 4 * x4 + 3 < p.dw) {
+        uint8_t* D = dst + (long long)f * p.dpitch + (long long)dy * p.dstride;
+        if ((reinterpret_cast<uintptr_t>(D) & 3) == 0 && 4 * x4 + 3 < p.dw) {
             *reinterpret_cast<uint32_t*>(D + 4 * x4) = out;
         } else {
             for (int e = 0; e < 4 && 4 * x4 + e < p.dw; e++) D[4 * x4 + e] = (uint8_t)(out >> (8 * e));
@@ -1921,8 +1971,9 @@ mage_status resize_linear_device(const uint8_t* src, int sw, int sh, int sstride
     int dev = 0;
     MAGE_HIP(hipGetDevice(&dev));
     Key* k = nullptr;
-    for (auto& c : cache)
-        if (c.dev == dev && c.st == st && c.sw == sw && c.sh == sh && c.dw == dw && c.dh == dh) k = &c;
+    for (auto& c : cache)  // one entry per (device, stream): the scratch holds one table set
+        if (c.dev == dev && c.st == st) k = &c;
+    if (k && !(k->sw == sw && k->sh == sh && k->dw == dw && k->dh == dh)) k->sw = -1;
     std::vector<int> ints;
     std::vector<uint32_t> words;
     LevelGeom v;
@@ -1930,13 +1981,11 @@ mage_status resize_linear_device(const uint8_t* src, int sw, int sh, int sstride
     const size_t ib = ints.size() * 4, wb = words.size() * 4;
     uint8_t* tab = static_cast<uint8_t*>(stream_scratch(st, STREAM_RESIZE_TABLES, ib + wb));
     if (!tab) return MAGE_ENOMEM;
-    if (!k || k->tab != tab) {
+    if (!k || k->tab != tab || k->sw < 0) {
         MAGE_HIP(hipMemcpyAsync(tab, ints.data(), ib, hipMemcpyHostToDevice, st));
         MAGE_HIP(hipMemcpyAsync(tab + ib, words.data(), wb, hipMemcpyHostToDevice, st));
         MAGE_HIP(hipStreamSynchronize(st));
-        for (auto& c : cache)
-            if (c.dev == dev && c.st == st) c.sw = -1;  // the scratch now holds the new tables
-        if (k) k->tab = tab, k->sw = sw;
+        if (k) *k = Key{dev, sw, sh, dw, dh, st, tab};
         else cache.push_back(Key{dev, sw, sh, dw, dh, st, tab});
     }
     const int* it = reinterpret_cast<const int*>(tab);
@@ -1955,8 +2004,10 @@ mage_status resize_linear_device(const uint8_t* src, int sw, int sh, int sstride
     rp.yofs = it + v.yofs;
     rp.alpha = wt + v.alpha;
     rp.beta = wt + v.beta;
-    if (rp.sw <= RZ_MAXW)
-        launch("image.resize", resize_rows_kernel, dim3(1, dh, 1), dim3(256), 0, st, src, dst, rp);
+    const size_t lds = rz_lds_bytes(ints.data() + v.yofs, sw, sh, dh, v.area2);
+    if (rp.sw <= RZ_MAXW && lds <= RZ_MAX_LDS)
+        launch("image.resize", resize_band_kernel, dim3((dh + RZ_BAND - 1) / RZ_BAND, 1, 1), dim3(256), lds, st, src, dst,
+               rp);
     else
         launch("image.resize", resize_linear_kernel, dim3((dw + 255) / 256, dh, 1), dim3(256), 0, st, src, dst, rp);
     MAGE_HIP(hipGetLastError());
@@ -2164,9 +2215,10 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             rp.yofs = ints + dst.yofs;
             rp.alpha = words + dst.alpha;
             rp.beta = words + dst.beta;
-            if (src.w <= RZ_MAXW)
-                hipLaunchKernelGGL(resize_rows_kernel, dim3(1, dst.h, batch), dim3(256), 0, st, raw.base[l - 1],
-                                   const_cast<uint8_t*>(raw.base[l]), rp);
+            const size_t lds = rz_lds_bytes(g.tab_ints.data() + dst.yofs, src.w, src.h, dst.h, dst.area2);
+            if (src.w <= RZ_MAXW && lds <= RZ_MAX_LDS)
+                hipLaunchKernelGGL(resize_band_kernel, dim3((dst.h + RZ_BAND - 1) / RZ_BAND, 1, batch), dim3(256), lds, st,
+                                   raw.base[l - 1], const_cast<uint8_t*>(raw.base[l]), rp);
             else
                 hipLaunchKernelGGL(resize_linear_kernel, dim3((dst.w + 255) / 256, dst.h, batch), dim3(256), 0, st,
                                    raw.base[l - 1], const_cast<uint8_t*>(raw.base[l]), rp);

@@ -660,11 +660,14 @@ struct HostRing {
     std::vector<int4> assoc;
 };
 
-struct LocalBA {
-    mage_ba* ba = nullptr;
+struct LocalBA {  // MappingWorker's CurrentLambda, persisted across the windows
     bool have_lambda = false;
     float lambda = 0.f;
-    ~LocalBA()
+};
+
+struct BundlerHandle {  // a fresh BundlerLib per window (BundleAdjust.cpp MakeBundler)
+    mage_ba* ba = nullptr;
+    ~BundlerHandle()
     {
         if (ba) mage_ba_destroy(ba);
     }
@@ -748,9 +751,10 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
         }
     }
     // points a free camera observes, ascending (owner, index)
+    const uint32_t nfix = nr > c.s.ba_free_keyframes ? nr - c.s.ba_free_keyframes : 1u;  // the oldest are fixed
     std::vector<uint64_t> keys;
     for (const Obs& ob : obs)
-        if (ob.cam > 0) keys.push_back((uint64_t)ob.owner << 32 | ob.idx);
+        if (ob.cam >= nfix) keys.push_back((uint64_t)ob.owner << 32 | ob.idx);
     std::sort(keys.begin(), keys.end());
     keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
     auto pidx = [&](uint32_t owner, uint32_t idx) -> int64_t {
@@ -784,7 +788,7 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
     // cameras: view-space t, Eigen column-major R, {cx, cy, fx, fy}; the oldest fixed
     std::vector<float> pos3(3 * nr), r9(9 * nr), intr(4 * nr);
     std::vector<uint8_t> fixed(nr, 0);
-    fixed[0] = 1;
+    for (uint32_t r = 0; r < nfix; r++) fixed[r] = 1;
     for (uint32_t r = 0; r < nr; r++) {
         const double* ps = &R.pose[12 * slot_of[r]];
         for (int i = 0; i < 3; i++) pos3[3 * r + i] = (float)ps[9 + i];
@@ -805,22 +809,23 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
     }
     const std::vector<float> hw(std::max(steps, 1u), huber);
     mage_status st;
-    if (!L.ba && (st = mage_ba_create(0, device, &L.ba)) != MAGE_OK) return st;
-    if (L.have_lambda && (st = mage_ba_set_lambda(L.ba, L.lambda)) != MAGE_OK) return st;
-    if ((st = mage_ba_set_cameras(L.ba, nr, pos3.data(), r9.data(), intr.data(), fixed.data())) != MAGE_OK ||
-        (st = mage_ba_set_points(L.ba, P, xyz.data())) != MAGE_OK ||
-        (st = mage_ba_set_observations(L.ba, E, uv.data(), cam.data(), pt.data(), info.data())) != MAGE_OK)
+    BundlerHandle H;
+    if ((st = mage_ba_create(0, device, &H.ba)) != MAGE_OK) return st;
+    if (L.have_lambda && (st = mage_ba_set_lambda(H.ba, L.lambda)) != MAGE_OK) return st;
+    if ((st = mage_ba_set_cameras(H.ba, nr, pos3.data(), r9.data(), intr.data(), fixed.data())) != MAGE_OK ||
+        (st = mage_ba_set_points(H.ba, P, xyz.data())) != MAGE_OK ||
+        (st = mage_ba_set_observations(H.ba, E, uv.data(), cam.data(), pt.data(), info.data())) != MAGE_OK)
         return st;
     std::vector<uint32_t> outl(E);
     uint32_t nout = 0;
     float ms = 0.f;
-    if ((st = mage_ba_step(L.ba, hw.data(), (uint32_t)hw.size(), c.s.ba_max_outlier_error, outl.data(), E, &nout, &ms)) !=
+    if ((st = mage_ba_step(H.ba, hw.data(), (uint32_t)hw.size(), c.s.ba_max_outlier_error, outl.data(), E, &nout, &ms)) !=
         MAGE_OK)
         return st;
     std::vector<float> pos_o(3 * nr), r9_o(9 * nr), xyz_o(3ull * P);
     float lam = 0.f;
-    if ((st = mage_ba_get_poses(L.ba, pos_o.data(), r9_o.data())) != MAGE_OK ||
-        (st = mage_ba_get_points(L.ba, xyz_o.data())) != MAGE_OK || (st = mage_ba_get_lambda(L.ba, &lam)) != MAGE_OK)
+    if ((st = mage_ba_get_poses(H.ba, pos_o.data(), r9_o.data())) != MAGE_OK ||
+        (st = mage_ba_get_points(H.ba, xyz_o.data())) != MAGE_OK || (st = mage_ba_get_lambda(H.ba, &lam)) != MAGE_OK)
         return st;
     L.have_lambda = true;
     L.lambda = std::max(lam, c.s.min_lambda);
@@ -834,7 +839,7 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
             R.aalive[(size_t)sl * R.acap + ob.src] = 0;
         slot_changed[sl] = 1;
     }
-    for (uint32_t r = 1; r < nr; r++) {
+    for (uint32_t r = nfix; r < nr; r++) {
         double* ps = &R.pose[12 * slot_of[r]];
         for (int rr = 0; rr < 3; rr++)
             for (int cc = 0; cc < 3; cc++) ps[3 * rr + cc] = (double)r9_o[9 * r + 3 * cc + rr];

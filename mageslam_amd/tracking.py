@@ -71,6 +71,7 @@ class TrackerSettings:
     ba_low_connectivity_scale: float = 1.5  # ::LowConnectivityIterationsScale
     ba_upper_connections: int = 2000       # CovisibilitySettings::UpperConnectionsForBA
     min_lambda: float = 1e-3               # MappingSettings::MinLambda (PersistLambda on)
+    ba_free_keyframes: int = 2             # the newest keyframes of the window move, the older ones are fixed
 
     def min_view_cos(self) -> np.float32:
         """std::cos(mira::deg2rad(degrees)) in float (arcana/math.h:86-90: degrees * (PI / 180))."""
@@ -240,9 +241,10 @@ class BAWindow:
 
 def build_ba_window(ring, K, s: "TrackerSettings") -> BAWindow | None:
     """GetMapPointsAndDistantKeyframes + BuildDataForG2O (ThreadSafeMap.cpp:880-960; BundleAdjust.cpp:
-    25-193) over this loop's map: the keyframes of the local map (ascending id), the oldest one fixed
-    (the reference fixes the observing keyframes outside the covisible set; here the local map is the
-    last keyframes, so its oldest member anchors the window); the points they own that a free keyframe
+    25-193) over this loop's map: the keyframes of the local map (ascending id), the newest
+    ba_free_keyframes of them free and the older ones fixed, at least one (the reference fixes the
+    observing keyframes outside the covisible set; here the local map is the last keyframes, so its
+    oldest members anchor the window: position, orientation and scale); the points they own that a free keyframe
     observes; every alive association of those points, per camera: its own points (ascending index),
     then its associations in the order its frame made them.  info = MapPointRefinementConfidence of
     the point's refinement count.  NumStepsPerRun and the Huber width scale with the connectivity
@@ -258,7 +260,8 @@ def build_ba_window(ring, K, s: "TrackerSettings") -> BAWindow | None:
             o = pos_of.get(int(k.assoc_owner[a]))
             if k.assoc_alive[a] and o is not None:
                 obs.append((c, o, int(k.assoc_idx[a]), k.assoc_uv[a, 0], k.assoc_uv[a, 1], ("assoc", c, a)))
-    seen_free = {(o, i) for c, o, i, _, _, _ in obs if c > 0}
+    nfix = max(len(ring) - s.ba_free_keyframes, 1)  # the oldest keyframes are fixed, at least one
+    seen_free = {(o, i) for c, o, i, _, _, _ in obs if c >= nfix}
     point_src = sorted(seen_free)
     pidx = {key: n for n, key in enumerate(point_src)}
     obs = [ob for ob in obs if (ob[1], ob[2]) in pidx]
@@ -282,7 +285,8 @@ def build_ba_window(ring, K, s: "TrackerSettings") -> BAWindow | None:
     return BAWindow(pos=np.stack([k.pose.t for k in ring]).astype(np.float32),
                     rot=np.stack([k.pose.R for k in ring]).astype(np.float32),
                     intr=np.tile(np.float32([cx, cy, fx, fy]), (len(ring), 1)),
-                    fixed=np.array([1] + [0] * (len(ring) - 1), np.uint8), points=points,
+                    fixed=np.array([1 if c < max(len(ring) - s.ba_free_keyframes, 1) else 0 for c in range(len(ring))],
+                                   np.uint8), points=points,
                     uv=np.array([[ob[3], ob[4]] for ob in obs], np.float32),
                     cam=np.array([ob[0] for ob in obs], np.uint32), pt=pt, info=refinement_confidence(refine[pt]),
                     point_src=point_src, obs_src=[ob[5] for ob in obs], huber_widths=[float(huber)] * max(steps, 1),
@@ -513,9 +517,11 @@ class GpuBackend(Backend):
     def bundle_adjust(self, w, lam):
         from . import bundler
 
-        if getattr(self, "_ba", None) is None:
-            self._ba = bundler.BundlerLib(device=self.device)
-        return run_bundler(self._ba, w, lam, self._ba.SetCurrentLambda, self._ba.GetCurrentLambda)
+        b = bundler.BundlerLib(device=self.device)  # MakeBundler: a fresh BundlerLib per task
+        try:
+            return run_bundler(b, w, lam, b.SetCurrentLambda, b.GetCurrentLambda)
+        finally:
+            b.close()
 
 
 @dataclass
@@ -701,7 +707,7 @@ def _settings_c(s: TrackerSettings):
                                s.local_min_hamming_difference, float(s.min_view_cos()), s.image_border, s.min_tracked,
                                s.scale_factor, s.num_levels, s.width, s.height, int(s.local_ba), s.ba_huber,
                                s.ba_huber_scale, s.ba_max_outlier_error, s.ba_steps_per_run, s.ba_low_connectivity_scale,
-                               s.ba_upper_connections, s.min_lambda)
+                               s.ba_upper_connections, s.min_lambda, s.ba_free_keyframes)
 
 
 def track_native_device(d_kp, d_desc, pitch: int, d_counts, frames: int, K, first_pose: Pose, plane_z: float,

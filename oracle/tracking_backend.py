@@ -35,6 +35,5 @@ class OracleBackend(tracking.Backend):
         return r, m.astype(bool)
 
     def bundle_adjust(self, w, lam):
-        if getattr(self, "_ba", None) is None:
-            self._ba = O.BundlerOracle()
-        return tracking.run_bundler(self._ba, w, lam, self._ba.set_lambda, self._ba.get_lambda)
+        b = O.BundlerOracle()  # a fresh BundlerLib per task (BundleAdjust.cpp MakeBundler)
+        return tracking.run_bundler(b, w, lam, b.set_lambda, b.get_lambda)
