@@ -234,9 +234,14 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
     frames = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
     orb.synth_frames_device(frames, F, W, H, 0, multigpu.sequence_seed(synth.FRAME_SEED, rank), stream=stream)
     torch.cuda.synchronize(dev)
-    sets = [dict(kp=torch.zeros((B + 1, N * 28), dtype=torch.uint8, device=dev),
-                 desc=torch.zeros((B + 1, N, 32), dtype=torch.uint8, device=dev),
-                 cnt=torch.zeros(B + 1, dtype=torch.int32, device=dev),
+    # one stream: the features live in a ring of RING batches (+ one slot), batch s in slots
+    # [b + 1, b + B] with b = (s % RING) * B, so slot b holds the previous batch's last frame and the
+    # match reads it in place; only when the ring wraps does that frame move to slot 0 (one copy per
+    # RING batches instead of three per batch)
+    RING = 8 if NSET == 1 else 1
+    sets = [dict(kp=torch.zeros((RING * B + 1, N * 28), dtype=torch.uint8, device=dev),
+                 desc=torch.zeros((RING * B + 1, N, 32), dtype=torch.uint8, device=dev),
+                 cnt=torch.zeros(RING * B + 1, dtype=torch.int32, device=dev),
                  mt=torch.zeros((B, N * 16), dtype=torch.uint8, device=dev),
                  nm=torch.zeros(B, dtype=torch.int32, device=dev)) for _ in range(NSET)]
     streams = [torch.cuda.current_stream(dev)] if NSTR == 1 else [torch.cuda.Stream(dev) for _ in range(NSTR)]
@@ -249,11 +254,16 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
         X, P = sets[s % NSET], sets[(s - 1) % NSET]
         st = streams[s % NSTR]
         d = dets[s % NSTR]
+        b = (s % RING) * B  # ring base: slot b = the previous batch's last frame
         with torch.cuda.stream(st):
             if NSET > 1:
                 st.wait_event(ev_m[s % NSET])  # the previous batch in this set has been matched
-            d.detect_and_compute_batch_device(fr, W, H, X["kp"][1:], X["desc"][1:], X["cnt"][1:], N,
-                                              stream=st.cuda_stream)
+            elif b == 0 and s > 0:  # the ring wrapped: the previous batch's last frame to slot 0
+                X["kp"][0].copy_(X["kp"][RING * B])
+                X["desc"][0].copy_(X["desc"][RING * B])
+                X["cnt"][0:1].copy_(X["cnt"][RING * B:RING * B + 1])
+            d.detect_and_compute_batch_device(fr, W, H, X["kp"][b + 1:b + B + 1], X["desc"][b + 1:b + B + 1],
+                                              X["cnt"][b + 1:b + B + 1], N, stream=st.cuda_stream)
             ev_x[s % NSET].record(st)
             if NSET > 1:
                 # the previous batch's last frame is the predecessor of this batch's first frame
@@ -261,12 +271,9 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
                 X["kp"][0].copy_(P["kp"][B])
                 X["desc"][0].copy_(P["desc"][B])
                 X["cnt"][0:1].copy_(P["cnt"][B:B + 1])
-            matcher.match_batch_device(X["desc"][1:], N * 32, X["cnt"][1:], X["desc"][:-1], N * 32, X["cnt"][:-1], B,
+            matcher.match_batch_device(X["desc"][b + 1:b + B + 1], N * 32, X["cnt"][b + 1:b + B + 1],
+                                       X["desc"][b:b + B], N * 32, X["cnt"][b:b + B], B,
                                        30, 1, X["mt"], N, X["nm"], stream=st.cuda_stream)
-            if NSET == 1:  # one set: the last frame moves to slot 0 after the match
-                X["kp"][0].copy_(X["kp"][B])
-                X["desc"][0].copy_(X["desc"][B])
-                X["cnt"][0:1].copy_(X["cnt"][B:B + 1])
             ev_m[s % NSET].record(st)
 
     for s in range(args.warmup):
@@ -290,8 +297,10 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
     kern = _lib.profile_report() if args.profile else {}
     for d in dets:
         d.device_status()
-    last = sets[(args.warmup + args.steps - 1) % NSET]
-    cnt, nm = last["cnt"], last["nm"]
+    s_last = args.warmup + args.steps - 1
+    last = sets[s_last % NSET]
+    b_last = (s_last % RING) * B
+    cnt, nm = last["cnt"][b_last:b_last + B + 1], last["nm"]
     el_max = multigpu.max_over_ranks(el, dev, dist)
     # end-of-run exchange (RCCL over xGMI): per-frame (keypoints, matches) of the last batch
     summary = torch.stack([cnt[1:].to(torch.int64), nm.to(torch.int64)], 1)

@@ -541,6 +541,9 @@ constexpr int FBUF = 3;              // stage buffers
 constexpr uint32_t K16_BASE = 0x2400u;  // low-16 mantissa offset of the accumulator start
 constexpr int K16_D = 272;           // key >> 6 = K16_D - d
 constexpr uint32_t NONE16 = 0x80008000u;
+#ifndef MAGE_FP4_GATE
+#define MAGE_FP4_GATE 1  // skip the fold of tiles with no key within maxDist (0: fold every tile)
+#endif
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pkmax(uint32_t a, uint32_t b)
@@ -651,6 +654,9 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
         // global key of a local column key (code = 63 - row in the wave's 64 rows):
         // (64 (272 - d) + code) -> ((272 - d) << 16 | 0x7FFF - row)
         const int kadd = 0x7FFF - rowbase - 63;
+        // accumulator bits of the smallest key with d <= maxDist: (124 << 23) | 64 (272 - maxDist)
+        const uint32_t gate_bits = (124u << 23) | (uint32_t)(64 * (K16_D - min(max(maxDist, -1), 127)));
+        (void)gate_bits;
         PendingCol16 pc{0, 0, 0, 0, false};
         for (int st = 0; st < nstages; st++) {
             const int buf = st % FBUF;
@@ -663,10 +669,22 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                     v4i bf[4];
 #pragma unroll
                     for (int s = 0; s < 4; s++) bf[s] = stage[buf][ct][s][lane];
-                    uint32_t c1 = 0, c2 = 0;
+                    uint32_t c1 = NONE16, c2 = NONE16;
+                    bool any = !MAGE_FP4_GATE;
 #pragma unroll
                     for (int rt = 0; rt < FRT; rt++) {
                         const v16i acc = __builtin_bit_cast(v16i, tile_mfma_k16(a[rt], bf, cc));
+#if MAGE_FP4_GATE
+                        // maxDist gate: radiusMatch keeps only d <= maxDist, and a top-2 state over a
+                        // superset of those values decides exactly as one over them alone, so a tile
+                        // whose 1024 keys all lie below the gate key (d > maxDist) is not folded
+                        uint32_t mx = (uint32_t)acc[15];  // v_max3_u32 tree (the key order is the bits' order)
+#pragma unroll
+                        for (int g = 0; g < 15; g += 3)
+                            mx = max(mx, max(max((uint32_t)acc[g], (uint32_t)acc[g + 1]), (uint32_t)acc[g + 2]));
+                        if (__ballot(mx >= gate_bits) == 0) continue;  // wave-uniform
+                        any = true;
+#endif
                         uint32_t P[8];
 #pragma unroll
                         for (int q = 0; q < 8; q++)
@@ -684,17 +702,15 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                             t2 = pkmax(t2, pkmin(t1, P[q]));
                             t1 = pkmax(t1, P[q]);
                         }
-                        if (rt == 0) {
-                            c1 = t1;
-                            c2 = t2;
-                        } else {  // rows 32..63 of the wave: codes 32..63 -> 0..31 (bit 5 cleared)
+                        if (rt > 0) {  // rows 32..63 of the wave: codes 32..63 -> 0..31 (bit 5 cleared)
                             t1 ^= 0x00200020u;
                             t2 ^= 0x00200020u;
-                            const uint32_t lo = pkmin(c1, t1);
-                            c1 = pkmax(c1, t1);
-                            c2 = pkmax(pkmax(lo, c2), t2);
                         }
+                        const uint32_t lo = pkmin(c1, t1);
+                        c1 = pkmax(c1, t1);
+                        c2 = pkmax(pkmax(lo, c2), t2);
                     }
+                    if (!any) continue;  // no key of the column tile within maxDist: no flush
                     // the partner half-wave holds the same column (rows + 4)
                     {
                         const uint32_t o1 = (uint32_t)xor32((int)c1, lane), o2 = (uint32_t)xor32((int)c2, lane);

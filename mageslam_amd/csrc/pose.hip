@@ -162,24 +162,95 @@ __device__ __forceinline__ void wg_sum(double (&acc)[N], double (*red)[N], doubl
     __syncthreads();
 }
 
+// The 6x6 solve of one trial, computed by every thread from the reduced system (no broadcast, no
+// barrier): S = Hpp + lambda I, Cholesky (LLT) and the two triangular solves; on a non-positive
+// pivot x keeps the previous solve (LinearSolverDense) and the trial is marked failed.  The
+// diagonal of L is never stored: the factor and the solves use 1/L_jj only.
+__device__ __forceinline__ bool pose_solve(const double* sum, double lam, double x[6])
+{
+    double L[36];
+#pragma unroll
+    for (int r = 0, k = 0; r < 6; r++)
+#pragma unroll
+        for (int c = r; c < 6; c++, k++) {
+            L[r * 6 + c] = sum[k];
+            L[c * 6 + r] = sum[k];
+        }
+#pragma unroll
+    for (int r = 0; r < 6; r++) L[r * 6 + r] += lam;
+    // fully unrolled (static register indexing, no scratch); a non-positive pivot only clears ok —
+    // the rest of the factor is then unused, as after the oracle's break
+    // 1/sqrt(d) by v_rsq_f64 + one Newton step (~1e-14 relative, as chol_tiles): the factor's
+    // and the solves' divisions become multiplications, off the dependent f64 division sequence
+    bool ok = true;
+    double rinv[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        double d = L[j * 6 + j];
+#pragma unroll
+        for (int k = 0; k < j; k++) d -= L[j * 6 + k] * L[j * 6 + k];
+        ok = ok && d > 0;
+        const double h = 0.5 * d;
+        double r = __builtin_amdgcn_rsq(d);
+        r *= __builtin_fma(-h * r, r, 1.5);
+        rinv[j] = r;
+#pragma unroll
+        for (int i = j + 1; i < 6; i++) {
+            double s = L[i * 6 + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) s -= L[i * 6 + k] * L[j * 6 + k];
+            L[i * 6 + j] = s * r;
+        }
+    }
+    if (ok) {
+        double y[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            double s = sum[21 + i];
+#pragma unroll
+            for (int k = 0; k < i; k++) s -= L[i * 6 + k] * y[k];
+            y[i] = s * rinv[i];
+        }
+#pragma unroll
+        for (int i = 5; i >= 0; i--) {
+            double s = y[i];
+#pragma unroll
+            for (int k = i + 1; k < 6; k++) s -= L[k * 6 + i] * y[k];
+            y[i] = s * rinv[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) x[k] = y[k];
+    }
+    return ok;
+}
+
+// One workgroup per problem.  Every thread keeps the LM state (pose, lambda, ni, the last solve)
+// in registers and computes each trial's solve itself from the reduced system in LDS, so the only
+// barriers are the reductions'.  The trial evaluation also accumulates the normal equations at the
+// trial pose: when the trial is accepted they are the next step's linearisation (g2o linearises
+// at the accepted state), so after step 0 a step costs one edge pass per trial.
 template <int PB_THREADS>
 __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
 {
     __shared__ double red[PB_THREADS / kWave][28];
-    __shared__ double sum[28];
-    __shared__ double cur_q[4], cur_t[3], tr_q[4], tr_t[3], ev_q[4], ev_t[3];
-    __shared__ double s_lambda, s_ni, s_chi, s_x[6], s_scale;
-    __shared__ int s_ok2, s_have_eval;
+    __shared__ double sums[2][28];  // the linearisation at the current pose / at the trial pose
+    // LM state: written by every thread with the same value (each thread computes it), so a
+    // thread's reads follow its own writes and no barrier is needed; in LDS rather than registers
+    // to keep them out of the edge loops' register budget
+    __shared__ double s_cur[7], s_ev[7], s_x[6];  // current pose (q, t), last evaluated pose, last solve
     const int pr = blockIdx.x, tid = threadIdx.x;
     const uint32_t e0 = p.obs_start[pr], e1 = p.obs_start[pr + 1];
     const int E = (int)(e1 - e0);
     const double f = p.intr4[4 * pr + 2], cx = p.intr4[4 * pr], cy = p.intr4[4 * pr + 1];
-    if (tid == 0) {
-        pose_from_input(p.r9 + 9 * pr, p.pos3 + 3 * pr, cur_q, cur_t);
+    {
+        double q[4], t[3];
+        pose_from_input(p.r9 + 9 * pr, p.pos3 + 3 * pr, q, t);
+        for (int k = 0; k < 4; k++) s_cur[k] = q[k];
+        for (int k = 0; k < 3; k++) s_cur[4 + k] = t[k];
         for (int k = 0; k < 6; k++) s_x[k] = 0;
-        s_have_eval = 0;
     }
-    __syncthreads();
+    bool have_eval = false;
+    double lambda = 0, ni = 2;
     auto load_edge = [&](int i) {
         EdgeIn e;
         const uint32_t g = e0 + i;
@@ -191,10 +262,9 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
         e.info = p.info[g];
         return e;
     };
-    uint32_t iters = 0, trials = 0;
-    // StepOptimizer::Step: no active vertex (no observations) -> useless, every Step fails
-    for (uint32_t step = 0; E > 0 && step < p.nsteps; step++) {
-        // linearise at the current pose
+    // errors, robust chi2 and normal equations of every edge at pose qt = (q, t) -> sums[slot]
+    auto linearise = [&](const double* qt, int slot) {
+        const double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t[3] = {qt[4], qt[5], qt[6]};
         double acc[28];
 #pragma unroll
         for (int k = 0; k < 28; k++) acc[k] = 0;
@@ -206,123 +276,72 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
             double a2[28];
 #pragma unroll
             for (int k = 0; k < 28; k++) a2[k] = 0;
-            edge_terms(e, cur_q, cur_t, f, cx, cy, p.huber, ev, rho0, a2);
+            edge_terms(e, q, t, f, cx, cy, p.huber, ev, rho0, a2);
 #pragma unroll
             for (int k = 0; k < 27; k++) acc[k] += a2[k];
             acc[27] += rho0;
         }
-        wg_sum<PB_THREADS, 28>(acc, red, sum);
-        double currentChi = sum[27];
+        wg_sum<PB_THREADS, 28>(acc, red, sums[slot]);
+    };
+    uint32_t iters = 0, trials = 0;
+    int cur = 0;  // sums[cur]: the linearisation at the current pose
+    // StepOptimizer::Step: no active vertex (no observations) -> useless, every Step fails
+    for (uint32_t step = 0; E > 0 && step < p.nsteps; step++) {
         if (step == 0) {
+            linearise(s_cur, cur);
             double m = 0;
-            for (int r = 0, k = 0; r < 6; k += 6 - r, r++) m = fmax(fabs(sum[k]), m);
-            if (tid == 0) {
-                s_lambda = 1e-5 * m;  // computeLambdaInit, tau 1e-5 (fresh BundlerLib: no user lambda)
-                s_ni = 2;
-            }
+            for (int r = 0, k = 0; r < 6; k += 6 - r, r++) m = fmax(fabs(sums[cur][k]), m);
+            lambda = 1e-5 * m;  // computeLambdaInit, tau 1e-5 (fresh BundlerLib: no user lambda)
+            ni = 2;
         }
-        __syncthreads();
+        double currentChi = sums[cur][27];
         double rho = 0;
         int qmax = 0;
         do {
-            if (tid == 0) {
-                // S = Hpp + lambda I; Cholesky (LLT) and solve; on failure x keeps the previous solve
-                double L[36];
-                const double lam = s_lambda;
-                for (int r = 0, k = 0; r < 6; r++)
-                    for (int c = r; c < 6; c++, k++) {
-                        L[r * 6 + c] = sum[k];
-                        L[c * 6 + r] = sum[k];
-                    }
-                for (int r = 0; r < 6; r++) L[r * 6 + r] += lam;
-                // fully unrolled (static register indexing, no scratch); a non-positive pivot only
-                // clears ok — the rest of the factor is then unused, as after the oracle's break
-                bool ok = true;
-#pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    double d = L[j * 6 + j];
-#pragma unroll
-                    for (int k = 0; k < j; k++) d -= L[j * 6 + k] * L[j * 6 + k];
-                    ok = ok && d > 0;
-                    d = sqrt(d);
-                    L[j * 6 + j] = d;
-#pragma unroll
-                    for (int i = j + 1; i < 6; i++) {
-                        double s = L[i * 6 + j];
-#pragma unroll
-                        for (int k = 0; k < j; k++) s -= L[i * 6 + k] * L[j * 6 + k];
-                        L[i * 6 + j] = s / d;
-                    }
-                }
-                if (ok) {
-                    double x[6];
-#pragma unroll
-                    for (int i = 0; i < 6; i++) {
-                        double s = sum[21 + i];
-#pragma unroll
-                        for (int k = 0; k < i; k++) s -= L[i * 6 + k] * x[k];
-                        x[i] = s / L[i * 6 + i];
-                    }
-#pragma unroll
-                    for (int i = 5; i >= 0; i--) {
-                        double s = x[i];
-#pragma unroll
-                        for (int k = i + 1; k < 6; k++) s -= L[k * 6 + i] * x[k];
-                        x[i] = s / L[i * 6 + i];
-                    }
-                    for (int k = 0; k < 6; k++) s_x[k] = x[k];
-                }
-                s_ok2 = ok;
-                double q[4] = {cur_q[0], cur_q[1], cur_q[2], cur_q[3]}, t[3] = {cur_t[0], cur_t[1], cur_t[2]};
-                double u[6];
-                for (int k = 0; k < 6; k++) u[k] = s_x[k];
-                d_oplus(q, t, u);
-                for (int k = 0; k < 4; k++) tr_q[k] = ev_q[k] = q[k];
-                for (int k = 0; k < 3; k++) tr_t[k] = ev_t[k] = t[k];
-                s_have_eval = 1;
+            const double* S = sums[cur];
+            double scale;
+            bool ok;
+            {
+                double x[6];
+                for (int k = 0; k < 6; k++) x[k] = s_x[k];
+                ok = pose_solve(S, lambda, x);
+                double tq[4] = {s_cur[0], s_cur[1], s_cur[2], s_cur[3]}, tt[3] = {s_cur[4], s_cur[5], s_cur[6]};
+                d_oplus(tq, tt, x);
+                for (int k = 0; k < 4; k++) s_ev[k] = tq[k];
+                for (int k = 0; k < 3; k++) s_ev[4 + k] = tt[k];
+                for (int k = 0; k < 6; k++) s_x[k] = x[k];
                 double sc = 0;
-                for (int k = 0; k < 6; k++) sc += s_x[k] * (lam * s_x[k] + sum[21 + k]);
-                s_scale = sc + 1e-3;
+                for (int k = 0; k < 6; k++) sc += x[k] * (lambda * x[k] + S[21 + k]);
+                scale = sc + 1e-3;
             }
-            __syncthreads();
-            double c = 0;
-            for (int i = tid; i < E; i += PB_THREADS) {
-                const EdgeIn e = load_edge(i);
-                double ev[2], rho0;
-                edge_terms(e, tr_q, tr_t, f, cx, cy, p.huber, ev, rho0, nullptr);
-                c += rho0;
-            }
-            double one[1] = {c};
-            wg_sum<PB_THREADS, 1>(one, reinterpret_cast<double(*)[1]>(red), &s_chi);
-            double tempChi = s_chi;
-            if (!s_ok2) tempChi = DBL_MAX;
-            rho = (currentChi - tempChi) / s_scale;
+            have_eval = true;
+            linearise(s_ev, cur ^ 1);
+            double tempChi = sums[cur ^ 1][27];
+            if (!ok) tempChi = DBL_MAX;
+            rho = (currentChi - tempChi) / scale;
             trials++;
             const bool accept = rho > 0 && isfinite(tempChi);
-            __syncthreads();
-            if (tid == 0) {
-                if (accept) {
-                    double alpha = 1. - pow((2 * rho - 1), 3);
-                    alpha = fmin(alpha, 2. / 3.);
-                    const double scaleFactor = fmax(1. / 3., alpha);
-                    s_lambda *= scaleFactor;
-                    s_ni = 2;
-                    for (int k = 0; k < 4; k++) cur_q[k] = tr_q[k];
-                    for (int k = 0; k < 3; k++) cur_t[k] = tr_t[k];
-                } else {
-                    s_lambda *= s_ni;
-                    s_ni *= 2;
-                }
+            if (accept) {
+                double alpha = 1. - pow((2 * rho - 1), 3);
+                alpha = fmin(alpha, 2. / 3.);
+                const double scaleFactor = fmax(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                for (int k = 0; k < 7; k++) s_cur[k] = s_ev[k];
+                currentChi = tempChi;
+                cur ^= 1;  // the trial's normal equations are the next step's linearisation
+            } else {
+                lambda *= ni;
+                ni *= 2;
             }
-            if (accept) currentChi = tempChi;
             qmax++;
-            __syncthreads();
         } while (rho < 0 && qmax < 10);
         iters++;
-        const bool ok = !(qmax == 10 || rho == 0 || !isfinite(s_lambda));
+        const bool ok = !(qmax == 10 || rho == 0 || !isfinite(lambda));
         if (!ok) break;
     }
-    __syncthreads();
+    double cur_q[4] = {s_cur[0], s_cur[1], s_cur[2], s_cur[3]}, cur_t[3] = {s_cur[4], s_cur[5], s_cur[6]};
+    double ev_q[4] = {s_ev[0], s_ev[1], s_ev[2], s_ev[3]}, ev_t[3] = {s_ev[4], s_ev[5], s_ev[6]};
     // post-pass: errors of the last evaluated state, cheirality at the current pose
     double qc[4] = {-cur_q[0], -cur_q[1], -cur_q[2], cur_q[3]};
     double it[3], fwd[3];
@@ -333,7 +352,7 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
     for (int i = tid; i < E; i += PB_THREADS) {
         const EdgeIn e = load_edge(i);
         double ev[2] = {0, 0}, rho0;
-        if (s_have_eval) edge_terms(e, ev_q, ev_t, f, cx, cy, p.huber, ev, rho0, nullptr);
+        if (have_eval) edge_terms(e, ev_q, ev_t, f, cx, cy, p.huber, ev, rho0, nullptr);
         const double ss = ev[0] * ev[0] + ev[1] * ev[1];
         const double dot = (e.X[0] + it[0]) * fwd[0] + (e.X[1] + it[1]) * fwd[1] + (e.X[2] + it[2]) * fwd[2];
         const bool out = dot <= 0 || ss > p.max_err_sq;
@@ -343,9 +362,9 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
             acc2[1] += 1;
         }
     }
-    wg_sum<PB_THREADS, 2>(acc2, reinterpret_cast<double(*)[2]>(red), sum);
+    wg_sum<PB_THREADS, 2>(acc2, reinterpret_cast<double(*)[2]>(red), sums[0]);
     if (tid == 0) {
-        p.mean_sq[pr] = (float)(sum[0] / sum[1]);
+        p.mean_sq[pr] = (float)(sums[0][0] / sums[0][1]);
         // GetPose (BundlerLib.cpp:457-465): t as float, R of the normalised quaternion as float
         double q[4] = {cur_q[0], cur_q[1], cur_q[2], cur_q[3]};
         const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
