@@ -178,9 +178,24 @@ struct LocalMapArgs {
     int max_dist, min_diff;
     int* result;
     uint32_t* status;
+    const unsigned long long* keys;  // optional: the frame's band index, sorted (radius_band_index_launch)
 };
 size_t local_map_scratch_bytes(uint32_t q_cap);
 mage_status local_map_match_launch(const LocalMapArgs& a, void* scratch, hipStream_t st);
+
+// RadiusMatch's band index built once per target set (radius.hip): keys sorted ascending (8 B),
+// positions (2 floats) and descriptors (8 words) in key order, target_pitch entries per set; and
+// mage_radius_match_batch_device against sets indexed that way (same results).
+mage_status radius_band_index_launch(const mage_keypoint* d_target_kp, const uint8_t* d_target_desc,
+                                     const uint32_t* d_n_target, int64_t target_pitch, uint32_t sets,
+                                     unsigned long long* d_keys, float* d_xy, uint32_t* d_desc, hipStream_t st);
+mage_status radius_match_indexed(const mage_keypoint* d_query_kp, const float* d_query_pos, const uint8_t* d_query_desc,
+                                 int64_t query_pitch, const uint32_t* d_n_query, const mage_keypoint* d_target_kp,
+                                 const uint8_t* d_target_desc, int64_t target_pitch, const uint32_t* d_n_target,
+                                 const unsigned long long* d_keys, const float* d_xy, const uint32_t* d_desc,
+                                 uint32_t pairs, float radius, int32_t max_distance, int32_t min_difference,
+                                 int32_t* d_scratch, mage_dmatch* d_out, uint32_t cap, uint32_t* d_n, uint32_t* d_status,
+                                 hipStream_t st);
 
 // cv::resize(INTER_LINEAR) 8UC1 of one device image (orb.hip, the pyramid's resize_linear_kernel);
 // asynchronous on st.

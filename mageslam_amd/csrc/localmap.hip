@@ -247,7 +247,10 @@ mage_status local_map_match_launch(const LocalMapArgs& a, void* scratch, hipStre
 {
     unsigned long long* keys = static_cast<unsigned long long*>(scratch);
     LmRec* recs = reinterpret_cast<LmRec*>(static_cast<char*>(scratch) + ((size_t)LM_MAXT * 8 + 255) / 256 * 256);
-    launch("localmap.keys", lm_keys_kernel, dim3(1), dim3(SORT_THREADS), 0, st, a, keys);
+    if (a.keys)  // the frame's band index is built already (the tracker's, shared with RadiusMatch)
+        keys = const_cast<unsigned long long*>(a.keys);
+    else
+        launch("localmap.keys", lm_keys_kernel, dim3(1), dim3(SORT_THREADS), 0, st, a, keys);
     const unsigned groups = (unsigned)(((size_t)std::max(a.q_cap, 1u) * LM_GROUP + 1023) / 1024);
     launch("localmap.cand", lm_cand_kernel, dim3(groups), dim3(1024), 0, st, a, (const unsigned long long*)keys, recs);
     launch("localmap.resolve", lm_resolve_kernel, dim3(1), dim3(1024), 0, st, a, (const unsigned long long*)keys,

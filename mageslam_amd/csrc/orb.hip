@@ -2307,9 +2307,10 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
                o->xy.as<uint32_t>(), d_n, o->status.as<uint32_t>());
         MAGE_HIP(hipGetLastError());
         // frames whose gate was above their retain bound: the exact path (no-ops when none)
-        launch("orb.fast_redo", fast_redo_kernel, dim3(fgrid.x, fgrid.y, std::min(batch, 8u)), dim3(FAST_THREADS), 0,
+        // (small grids: a frame rarely takes this path, and an empty list should cost little)
+        launch("orb.fast_redo", fast_redo_kernel, dim3(fgrid.x, fgrid.y, std::min(batch, 2u)), dim3(FAST_THREADS), 0,
                st, raw.base[l], fp, cand, counts);
-        launch("orb.select_redo", select_redo_kernel, dim3(std::min(batch, 256u)), dim3(SEL_THREADS), 0, st, cand,
+        launch("orb.select_redo", select_redo_kernel, dim3(std::min(batch, 32u)), dim3(SEL_THREADS), 0, st, cand,
                counts, sp, d_kp, o->xy.as<uint32_t>(), d_n, o->status.as<uint32_t>());
         MAGE_HIP(hipGetLastError());
     }

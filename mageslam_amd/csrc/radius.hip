@@ -53,6 +53,11 @@ struct RadiusParams {
     mage_dmatch* out;
     uint32_t* n_out;
     uint32_t* status;  // bit 0: a target set exceeded RM_MAXT; bit 1: a count exceeded its pitch
+    // optional band index built once per target set (radius_band_index_kernel, t_pitch entries per
+    // pair): keys ascending, positions and descriptors in key order; no target mask with it
+    const unsigned long long* bkeys;
+    const float2* bxy;
+    const uint4* bdesc;
 };
 
 constexpr int RM_GROUP = 16;  // lanes per query (a band holds ~20-150 candidates)
@@ -152,6 +157,18 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
         }
         return;
     }
+    const bool staged = ntr <= RM_STAGE;
+    if (p.bkeys) {
+        // 1'. the band index of this target set is built already: contiguous copies into LDS
+        const long long tb = pr * p.t_pitch;
+        for (int i = tid; i < ntr; i += SORT_THREADS) keys[i] = p.bkeys[tb + i];
+        if (staged)
+            for (int i = tid; i < 2 * ntr; i += SORT_THREADS) {
+                sdesc[i] = p.bdesc[2 * tb + i];
+                if (!(i & 1)) sxy[i >> 1] = p.bxy[tb + (i >> 1)];
+            }
+        __syncthreads();
+    } else {
     // 1. band index: ascending keys via the descending sort of their complements (zero padding
     //    sorts last)
     int P = 1;
@@ -164,7 +181,6 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
     __syncthreads();
     // targets in key order into LDS: a band is then a contiguous run of positions + descriptors;
     // a masked target gets a NaN position, which fails the box test exactly like the mask check
-    const bool staged = ntr <= RM_STAGE;
     if (staged) {
         for (int i = tid; i < 2 * ntr; i += SORT_THREADS) {
             const int t = (int)(keys[i >> 1] & 0xFFFFFFu);
@@ -175,6 +191,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
             }
         }
         __syncthreads();
+    }
     }
 
     // 2. a 16-lane group per query (four queries per wave)
@@ -268,7 +285,52 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_post_kernel(RadiusParams 
     radius_post(p, pr, p.res + pr * p.q_pitch, nq, ntr, bestD, cnt, wsum, s_base);
 }
 
+// The band index of each target set once (one workgroup per set): the keys sorted as
+// radius_match_kernel sorts them, then positions and descriptors in key order, so every RadiusMatch
+// against the set (the tracker's passes over one frame, each spread over ~64 workgroups) starts
+// from contiguous copies instead of its own sort and gather.
+__global__ __launch_bounds__(SORT_THREADS) void radius_band_index_kernel(const mage_keypoint* __restrict__ tkp,
+                                                                         const uint8_t* __restrict__ tdesc,
+                                                                         const uint32_t* __restrict__ nt, long long t_pitch,
+                                                                         unsigned long long* __restrict__ bkeys,
+                                                                         float2* __restrict__ bxy, uint4* __restrict__ bdesc)
+{
+    __shared__ unsigned long long keys[RM_MAXT];
+    const int set = blockIdx.x, tid = threadIdx.x;
+    const int ntr = (int)nt[set];
+    if (ntr > RM_MAXT || ntr > t_pitch) return;  // radius_match_kernel reports it
+    const long long tb = set * t_pitch;
+    const mage_keypoint* k = tkp + tb;
+    int P = 1;
+    while (P < ntr) P <<= 1;
+    for (int i = tid; i < max(P, SORT_THREADS); i += SORT_THREADS)
+        keys[i] = i < ntr ? ~band_key(k[i].octave, k[i].y, (unsigned)i) : 0ull;
+    __syncthreads();
+    sort_desc(keys, P);
+    for (int i = tid; i < ntr; i += SORT_THREADS) {
+        const unsigned long long key = ~keys[i];
+        const int t = (int)(key & 0xFFFFFFu);
+        bkeys[tb + i] = key;
+        bxy[tb + i] = make_float2(k[t].x, k[t].y);
+        const uint4* d = reinterpret_cast<const uint4*>(tdesc + 32 * (tb + t));
+        bdesc[2 * (tb + i)] = d[0];
+        bdesc[2 * (tb + i) + 1] = d[1];
+    }
+}
+
 }  // namespace
+
+mage_status radius_band_index_launch(const mage_keypoint* d_target_kp, const uint8_t* d_target_desc,
+                                     const uint32_t* d_n_target, int64_t target_pitch, uint32_t sets,
+                                     unsigned long long* d_keys, float* d_xy, uint32_t* d_desc, hipStream_t st)
+{
+    if (sets == 0) return MAGE_OK;
+    launch("match.radius_index", radius_band_index_kernel, dim3(sets), dim3(SORT_THREADS), 0, st, d_target_kp,
+           d_target_desc, d_n_target, (long long)target_pitch, d_keys, reinterpret_cast<float2*>(d_xy),
+           reinterpret_cast<uint4*>(d_desc));
+    MAGE_HIP(hipGetLastError());
+    return MAGE_OK;
+}
 
 mage_status radius_match_launch(const RadiusParams& p, uint32_t pairs, hipStream_t st)
 {
@@ -401,3 +463,41 @@ mage_status mage_radius_match_batch_device(const mage_keypoint* d_query_kp, cons
 }
 
 }  // extern "C"
+
+namespace mage {
+// mage_radius_match_batch_device against target sets indexed by radius_band_index_launch (same
+// pitch); the results are those of the plain call.
+mage_status radius_match_indexed(const mage_keypoint* d_query_kp, const float* d_query_pos, const uint8_t* d_query_desc,
+                                 int64_t query_pitch, const uint32_t* d_n_query, const mage_keypoint* d_target_kp,
+                                 const uint8_t* d_target_desc, int64_t target_pitch, const uint32_t* d_n_target,
+                                 const unsigned long long* d_keys, const float* d_xy, const uint32_t* d_desc,
+                                 uint32_t pairs, float radius, int32_t max_distance, int32_t min_difference,
+                                 int32_t* d_scratch, mage_dmatch* d_out, uint32_t cap, uint32_t* d_n, uint32_t* d_status,
+                                 hipStream_t st)
+{
+    if (pairs == 0) return MAGE_OK;
+    MAGE_REQUIRE(max_distance >= -1 && max_distance <= 256, MAGE_EINVAL, "maxHammingDist must be in [-1, 256]");
+    RadiusParams p{};
+    p.qkp = d_query_kp;
+    p.qpos = d_query_pos;
+    p.qdesc = d_query_desc;
+    p.nq = d_n_query;
+    p.q_pitch = query_pitch;
+    p.tkp = d_target_kp;
+    p.tdesc = d_target_desc;
+    p.nt = d_n_target;
+    p.t_pitch = target_pitch;
+    p.radius = radius;
+    p.max_dist = max_distance;
+    p.min_diff = min_difference;
+    p.cap = cap;
+    p.res = d_scratch;
+    p.out = d_out;
+    p.n_out = d_n;
+    p.status = d_status;
+    p.bkeys = d_keys;
+    p.bxy = reinterpret_cast<const float2*>(d_xy);
+    p.bdesc = reinterpret_cast<const uint4*>(d_desc);
+    return radius_match_launch(p, pairs, st);
+}
+}  // namespace mage

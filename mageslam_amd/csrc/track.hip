@@ -904,7 +904,8 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
                  o_lqo = take(4 * qcap), o_lqh = take(4 * qcap), o_lqd = take(32 * qcap), o_lqt = take(12 * qcap),
                  o_lres = take(4 * qcap), o_lst = take(4), o_lscr = take(local_map_scratch_bytes((uint32_t)qcap)),
                  o_poses = take(96ull * frames), o_mt = take(4ull * frames), o_il = take(4ull * frames),
-                 o_kf = take(frames);
+                 o_kf = take(frames), o_bk = take(8ull * pitch * frames), o_bxy = take(8ull * pitch * frames),
+                 o_bd = take(32ull * pitch * frames);
     DeviceBuffer buf;
     mage_status r = buf.reserve(off);
     if (r != MAGE_OK) return r;
@@ -969,6 +970,10 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     uint32_t* dmt = reinterpret_cast<uint32_t*>(d + o_mt);
     uint32_t* dil = reinterpret_cast<uint32_t*>(d + o_il);
     uint8_t* dkf = reinterpret_cast<uint8_t*>(d + o_kf);
+    // every frame's RadiusMatch band index, built once (the tracker matches each frame up to 3 times)
+    unsigned long long* bkeys = reinterpret_cast<unsigned long long*>(d + o_bk);
+    float* bxy = reinterpret_cast<float*>(d + o_bxy);
+    uint32_t* bdesc = reinterpret_cast<uint32_t*>(d + o_bd);
 
     TrackConst c{};
     c.fx = (float)K[0];
@@ -999,6 +1004,8 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         hipMemcpyAsync(dposes, first_pose, 96, hipMemcpyHostToDevice, st) != hipSuccess)
         return fail(MAGE_EDEVICE);
     hipLaunchKernelGGL(trk_init, dim3(1), dim3(TT), 0, st, b, c, d_kp, d_desc, d_n, dposes, dmt, dil, dkf, rstatus);
+    if ((r = radius_band_index_launch(d_kp, d_desc, d_n, (int64_t)pitch, frames, bkeys, bxy, bdesc, st)) != MAGE_OK)
+        return fail(r);
     const float radius[3] = {s->search_radius, s->wider_search_radius, s->extra_wider_search_radius};
     auto enqueue = [&](uint32_t f) -> mage_status {
         const mage_keypoint* fk = d_kp + (size_t)f * pitch;
@@ -1007,10 +1014,10 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         mage_status rr;
         launch("track.project", trk_project, dim3(1), dim3(TT), 0, st, b, c, (int)f, (const double*)dposes);
         for (int k = 0; k < 3; k++) {
-            rr = mage_radius_match_batch_device(b.qkp, k < 2 ? b.qpos : nullptr, b.qdesc, (int64_t)pitch, b.nq + k, fk,
-                                                fd, (int64_t)pitch, nf, 1, radius[k], s->max_hamming,
-                                                s->min_hamming_difference, rscratch, b.m + (size_t)k * pitch, pitch,
-                                                b.mn + k, rstatus, stream);
+            rr = radius_match_indexed(b.qkp, k < 2 ? b.qpos : nullptr, b.qdesc, (int64_t)pitch, b.nq + k, fk, fd,
+                                      (int64_t)pitch, nf, bkeys + (size_t)f * pitch, bxy + 2ull * f * pitch,
+                                      bdesc + 8ull * f * pitch, 1, radius[k], s->max_hamming, s->min_hamming_difference,
+                                      rscratch, b.m + (size_t)k * pitch, pitch, b.mn + k, rstatus, st);
             if (rr != MAGE_OK) return rr;
             if (k < 2) launch("track.weak", trk_weak, dim3(1), dim3(64), 0, st, b, c, k);
         }
@@ -1038,6 +1045,7 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
             la.min_diff = s->local_min_hamming_difference;
             la.result = b.lm_res;
             la.status = b.lm_status;
+            la.keys = bkeys + (size_t)f * pitch;
             if ((rr = local_map_match_launch(la, b.lm_scratch, st)) != MAGE_OK) return rr;
             launch("track.lm_assemble", trk_lm_assemble, dim3(1), dim3(TT), 0, st, b, fk);
         }
