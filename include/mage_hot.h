@@ -78,6 +78,8 @@ const char* mage_last_error(void);
 /* Per-kernel timing: when enabled, every launch is bracketed by HIP events recorded on the
  * stream it is launched on.  The report is one line per kernel: "<name> <launches> <total_ms>". */
 void mage_profile_enable(int32_t enable);
+/* Time only the launches whose kernel tag starts with tag_prefix (null or "": all of them). */
+void mage_profile_filter(const char* tag_prefix);
 void mage_profile_reset(void);
 const char* mage_profile_report(void);
 

@@ -19,7 +19,7 @@ STATUS_NAMES = {0: "MAGE_OK", 1: "MAGE_EINVAL", 2: "MAGE_EDEVICE", 3: "MAGE_ENOM
 
 # Every entry point declared in include/mage_hot.h (checked by tests/test_capi.py).
 EXPORTS = [
-    "mage_version", "mage_last_error", "mage_profile_enable", "mage_profile_reset",
+    "mage_version", "mage_last_error", "mage_profile_enable", "mage_profile_filter", "mage_profile_reset",
     "mage_profile_report", "mage_orb_create", "mage_orb_destroy", "mage_orb_detect_and_compute",
     "mage_orb_detect_and_compute_batch_device", "mage_orb_status", "mage_orb_reset_status",
     "mage_orb_set_fast_gate", "mage_orb_fast_gate_stats",
@@ -169,6 +169,7 @@ def _declare(L: C.CDLL) -> None:
     sig("mage_version", C.c_char_p)
     sig("mage_last_error", C.c_char_p)
     sig("mage_profile_enable", None, i32)
+    sig("mage_profile_filter", None, C.c_char_p)
     sig("mage_profile_reset", None)
     sig("mage_profile_report", C.c_char_p)
     sig("mage_orb_create", st, vp, C.c_int, C.POINTER(vp))

@@ -688,21 +688,17 @@ __global__ __launch_bounds__(BA_THREADS) void edge_schur(Problem pb, const doubl
 // The products are enumerated once per initialisation: a pair's list holds (e1, e2) for every
 // shared free point (c1's edge e1, c2's edge e2; on the diagonal every ordered pair of the
 // camera's edges on the point), and the diagonal pair carries a second list of (e, p) for the rhs.
-// Lists are cut into chunks of <= SC_CHUNK entries, one wave per chunk (four per workgroup): each
-// lane loads its two entries, then Z_e1 = Hpl_e1 Dinv_p (edge_schur) and Hpl_e2 (or bl_p) with no
-// further dependent load, accumulates the 6x6 (+ 6 rhs) in registers, and the chunk sum is one
-// wave reduce-scatter.  Inactive edges have zero Hpl / Z (point_linearize, edge_schur), so no flag
-// is read.  A pair of one chunk finishes in place; otherwise its chunks write partials and
-// schur_finish adds them in chunk order (deterministic; a last-arriver ticket would need an
-// agent-scope fence = a full L2 write-back per workgroup on gfx950).  XCD-aware by point: a pair's
-// list is in point order, and its chunks are cut per point group (8 contiguous ranges of point
-// words, sc_pair_counts) with group g's chunks on XCD g (workgroup b runs on XCD b % 8), so an XCD
-// reads only the edge records of its own points (an eighth of them, L2-resident) instead of every
-// camera's; the rhs lists and the general (sorted-list) path keep one XCD per block row.
+// Lists are cut into chunks of <= SC_CHUNK entries, one 256-thread workgroup per chunk: each
+// thread loads its two entries, then Z_e1 = Hpl_e1 Dinv_p (edge_schur) and Hpl_e2 (or bl_p) with
+// no further dependent load, accumulates the 6x6 (+ 6 rhs) in registers, and the chunk sum is
+// a reduce-scatter + LDS tree.  Inactive edges have zero Hpl / Z (point_linearize, edge_schur),
+// so no flag is read.  A pair of one chunk finishes in place; otherwise its chunks write partials
+// and schur_finish adds them in chunk order (deterministic; a last-arriver ticket would need an
+// agent-scope fence = a full L2 write-back per workgroup on gfx950).  XCD-aware: the chunks of
+// one block row of S run on one XCD (block b on XCD b % 8), so Z_{c1 .} stays in that L2.
 constexpr int SC_THREADS = 256;
-constexpr int SC_WAVES = SC_THREADS / kWave;
-constexpr int SC_CHUNK = 2 * kWave;
-constexpr int SC_GROUPS = 8;  // point groups = XCDs
+constexpr int SC_CHUNK = 2 * SC_THREADS;
+
 struct SchurChunk {
     int pair;   // -1: padding block
     int start;  // first entry
@@ -755,18 +751,19 @@ __global__ __launch_bounds__(SC_THREADS) void schur_chunks(const SchurChunk* __r
                                                            double* __restrict__ part,
                                                            double* __restrict__ S, double* __restrict__ rhs)
 {
-    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-    const SchurChunk ch = chunks[blockIdx.x * SC_WAVES + wave];
+    __shared__ double red[SC_THREADS / kWave][42];
+    const SchurChunk ch = chunks[blockIdx.x];
     if (ch.pair < 0) return;
+    const int t = threadIdx.x;
     const long long es = ecsr;
     double acc[42];
 #pragma unroll
     for (int k = 0; k < 42; k++) acc[k] = 0;
     // both entries' indices first (padding -> the zero record), then every operand load
     // (a chunk of count 0 reads the list's padding entry; invalid lanes repeat the last entry)
-    const int2 x0 = entries[ch.start + max(0, min(lane, ch.count - 1))];
-    const int2 x1 = entries[ch.start + max(0, min(lane + kWave, ch.count - 1))];
-    const bool v0 = lane < ch.count, v1 = lane + kWave < ch.count;
+    const int2 x0 = entries[ch.start + max(0, min(t, ch.count - 1))];
+    const int2 x1 = entries[ch.start + max(0, min(t + SC_THREADS, ch.count - 1))];
+    const bool v0 = t < ch.count, v1 = t + SC_THREADS < ch.count;
     const SchurPair pr = pairs[ch.pair];
     const double f1 = camk[3 * pr.c1], f2 = camk[3 * pr.c2];
     // records at camera-CSR positions, component arrays of stride es: consecutive entries of a
@@ -837,13 +834,12 @@ __global__ __launch_bounds__(SC_THREADS) void schur_chunks(const SchurChunk* __r
         term(q0, g0, b0, v0);
         term(q1, g1, b1, v1);
     }
-    const int e = reduce_scatter<42, kWave>(acc, lane);  // lane e holds the chunk total of entry e
-    if (e < 0) return;
+    block_sum<42, SC_THREADS>(acc, red);  // red[0][k] = chunk total of entry k
     if (pr.nslots > 1 || pr.h1 == pr.h2) {  // schur_finish: partials in order, the camera blocks
-        part[(long long)ch.slot * 42 + e] = acc[0];
+        if (t < 42) part[(long long)ch.slot * 42 + t] = red[0][t];
         return;
     }
-    schur_write(pr, e, acc[0], 0.0, lambda, np, ptlist, tout, S, rhs);
+    if (t < 42) schur_write(pr, t, red[0][t], 0.0, lambda, np, ptlist, tout, S, rhs);
 }
 
 // Diagonal pairs and pairs of more than one chunk: a 64-lane wave per pair adds its chunk partials
@@ -1136,7 +1132,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     __shared__ __attribute__((aligned(16))) double vb[CT_MAXT * 16];  // b -> y -> x
     __shared__ int s_fail;
     __shared__ unsigned s_tile_bar;   // the TRSM-phase barrier count (CT_TW + 1 arrivals per step)
-    __shared__ unsigned s_xrdy[CT_MAXT], s_pcnt[CT_MAXT];  // backward solve: x_j final / products of row-block i
     __shared__ double cst[16][17], dst[16][17];  // A_{k,k+1}, A_{k+1,k+1} staged for the factor wave
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: tile bookkeeping on the SALU
@@ -1270,7 +1265,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             s_fail = 0;
             s_tile_bar = 0;
         }
-        if (lane < CT_MAXT) s_xrdy[lane] = s_pcnt[lane] = 0u;
         dbl4 cA = {0, 0, 0, 0}, cD = {0, 0, 0, 0};  // A_{k,k+1}, A_{k+1,k+1} (accumulator layout)
         auto s_tile = [&](int ti, int tj) {  // tile (ti, tj) of S, padded with the identity
             dbl4 t;
@@ -1355,7 +1349,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             CT_STAMP(k, 3);
         }
         if (s_fail) return;
-        __syncthreads();  // the backward solve's end
+        for (int k = 0; k < (mt > 0 ? mt : 1); k++) __syncthreads();  // the backward solve's barriers
         return;
     }
 
@@ -1473,33 +1467,18 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         if (tid == 0) *fail = 1;
         return;
     }
-    // --- backward: U x = y, x_i = inv(U_ii) (y_i - sum_{j>i} U_ij x_j), with no workgroup
-    // barrier per block: the owner of tile (i, j) waits for x_j (flag xrdy[j]), forms U_ij x_j
-    // into its slot of the dead panel and counts it in pcnt[i]; the owner of the chain tile
-    // (i, i+1) waits for the other products of row-block i, subtracts them from y_i in column
-    // order (mt-1 .. i+1, the order of the former barrier-per-block sweep: same bits), solves block
-    // i and raises xrdy[i].  Every wave walks its tiles by column, descending, so each wait is on
-    // a column the chain finishes first ---
-    double (*part)[16] = reinterpret_cast<double (*)[16]>(&pan[0][0][0][0]);  // [i * CT_MAXT + j][row]
-    auto wait_flag = [&](const unsigned* w, unsigned v) {
-        while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    };
-    auto raise_flag = [&](unsigned* w) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    if (mt > 0 && wave == 0) {
-        solve_block(mt - 1);
-        raise_flag(&s_xrdy[mt - 1]);
-    }
+    // --- backward: U x = y, x_k = inv(U_kk) (y_k - sum_{j>k} U_kj x_j), right-looking with
+    // one barrier per block: the owner of tile (k-1, k) applies the last update of y_{k-1} and
+    // then solves block k-1 itself ---
+    if (mt > 0 && wave == 0) solve_block(mt - 1);
+    __syncthreads();
     for (int k = mt - 1; k >= 1; k--) {
+        // slots in reverse (row-major) order: the tile (k - 1, k) of the critical chain first
 #pragma unroll
         for (int sl = CT_TPW - 1; sl >= 0; sl--) {
             int ti, tj;
             tile_of(sl, ti, tj);
             if (tj == k && ti < k) {
-                wait_flag(&s_xrdy[k], 1u);
                 // (U_ik x_k)[r] = sum_c U_ik[r][c] x_k[c]: row sums over the 16 lanes of a DPP row
                 // (lane 15 of the row holds rows lr + 4r)
                 const double xk = vb[16 * k + lc];
@@ -1508,28 +1487,17 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 for (int r = 0; r < 4; r++) rs[r] = row_sum16(C[sl][r] * xk);
                 if (lc == 15)
 #pragma unroll
-                    for (int r = 0; r < 4; r++) part[ti * CT_MAXT + k][lr + 4 * r] = rs[r];
+                    for (int r = 0; r < 4; r++) vb[16 * ti + lr + 4 * r] -= rs[r];
                 if (ti == k - 1) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the own product, across lanes
-                    __builtin_amdgcn_wave_barrier();
-                    wait_flag(&s_pcnt[ti], (unsigned)max(mt - ti - 2, 0));
-                    if (lane < 16) {
-                        double z = vb[16 * ti + lane];
-                        for (int j = mt - 1; j >= k; j--) z -= part[ti * CT_MAXT + j][lane];
-                        vb[16 * ti + lane] = z;
-                    }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    solve_block(ti);
-                    raise_flag(&s_xrdy[ti]);
-                } else {
-                    raise_flag(&s_pcnt[ti]);
+                    solve_block(k - 1);
                 }
             }
         }
+        __syncthreads();
     }
-    __syncthreads();  // every block solved
     tick(5);
 #if MAGE_CHOL_ABLATE == 4
     if (tid == 0) {
@@ -2328,34 +2296,16 @@ __global__ __launch_bounds__(1024) void sc_bitmaps(int P, const int* __restrict_
     }
 }
 
-// Pair (a, b)'s product count, and per point group (words w with w * SC_GROUPS / PW = g, in
-// point order: the pair's list is cut there for the XCD-by-point chunks) at cntg[(a nb + b) 8 + g].
 __global__ __launch_bounds__(64) void sc_pair_counts(const int* __restrict__ hdr, int PW, const uint32_t* __restrict__ A,
-                                                     const uint32_t* __restrict__ F, int* __restrict__ cnt,
-                                                     int* __restrict__ cntg)
+                                                     const uint32_t* __restrict__ F, int* __restrict__ cnt)
 {
     const int a = blockIdx.x, b = blockIdx.y, nb = hdr[0];
     if (b < a || b >= nb || nb > (int)gridDim.x) return;  // more blocks than the grid: refused by the host
     const uint32_t* Aa = A + (size_t)a * PW;
     const uint32_t* Ab = A + (size_t)b * PW;
-    int ng[SC_GROUPS] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int w = threadIdx.x; w < PW; w += 64) {
-        const int c = __popc(Aa[w] & Ab[w] & F[w]), g = (int)((long long)w * SC_GROUPS / PW);
-#pragma unroll
-        for (int k = 0; k < SC_GROUPS; k++) ng[k] += k == g ? c : 0;
-    }
     int n = 0;
-#pragma unroll
-    for (int k = 0; k < SC_GROUPS; k++) {
-        for (int o = 32; o > 0; o >>= 1) ng[k] += __shfl_xor(ng[k], o);
-        n += ng[k];
-    }
-    if (threadIdx.x < SC_GROUPS) {
-        int v = 0;
-#pragma unroll
-        for (int k = 0; k < SC_GROUPS; k++) v = (int)threadIdx.x == k ? ng[k] : v;
-        cntg[((size_t)a * nb + b) * SC_GROUPS + threadIdx.x] = v;
-    }
+    for (int w = threadIdx.x; w < PW; w += 64) n += __popc(Aa[w] & Ab[w] & F[w]);
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
     if (threadIdx.x == 0) cnt[a * nb + b] = n;
 }
 
@@ -2832,7 +2782,7 @@ struct BundleAdjuster {
         const size_t Cm = std::max(C, 1), Pm = std::max(P, 1), Em = std::max(E, 1);
         const int nbm = std::min(C, CH_PANEL_ROWS / 6);  // a larger block count is refused below
         const int PW = (P + 31) / 32;
-        const size_t nsum = (size_t)INIT_HDR + 2 * (size_t)C + (size_t)nbm + (size_t)nbm * nbm * (1 + SC_GROUPS);
+        const size_t nsum = (size_t)INIT_HDR + 2 * (size_t)C + (size_t)nbm + (size_t)nbm * nbm;
         {
             auto& camflag = ws.camflag;
             camflag.assign(Cm, 0);
@@ -2854,7 +2804,6 @@ struct BundleAdjuster {
         int* s_camblk = s_ccnt + C;
         int* s_rc = s_camblk + C;
         int* s_kcnt = s_rc + nbm;
-        int* s_kcntg = s_kcnt + (size_t)nbm * nbm;  // per pair and point group
         unsigned* k0 = d_ikeys.as<unsigned>();
         unsigned* k1 = k0 + Em;
         int* v0 = d_ivals.as<int>();
@@ -2904,7 +2853,7 @@ struct BundleAdjuster {
                    (const int*)d_camblk.as<int>(), (const int*)d_cstart.as<int>(), (const int*)d_cpt.as<int>(),
                    (const int*)d_ptfree.as<int>(), A, d_srank.as<int>(), A + (size_t)nbm * PW);
             launch("ba.schur_counts", sc_pair_counts, dim3(nbm, nbm), dim3(64), 0, st, (const int*)sum, PW,
-                   (const uint32_t*)A, (const uint32_t*)(A + (size_t)nbm * PW), s_kcnt, s_kcntg);
+                   (const uint32_t*)A, (const uint32_t*)(A + (size_t)nbm * PW), s_kcnt);
         }
         launch("ba.init_summary", summary_out, dim3(1), dim3(1024), 0, st, (const int*)sum, (int)nsum, h_isum.device<int>(),
                seq_dev(), ++seq_counter);
@@ -2922,7 +2871,6 @@ struct BundleAdjuster {
         camcnt.assign(hs + INIT_HDR, hs + INIT_HDR + C);
         const int* h_rc = hs + INIT_HDR + 2 * C;
         const int* h_kcnt = h_rc + nbm;
-        const int* h_kcntg = h_kcnt + (size_t)nbm * nbm;
         nb_free = nb;
         n = 6 * nb;
         np = (n + 15) / 16 * 16;
@@ -3100,10 +3048,8 @@ struct BundleAdjuster {
             MAGE_HIP(hipGetLastError());
         }
         pt.mark("list scatter");
-        // chunks.  Product lists of the bitmap path: per point group g (sc_pair_counts), on XCD g.
-        // The rhs lists, the sorted-list path and pairs with nothing to sum: the block rows of S
-        // split into 8 contiguous groups of about equal work, one per XCD.  Workgroup b (XCD b % 8)
-        // takes SC_WAVES chunks of its XCD's list, one per wave.
+        // chunks; the block rows of S split into 8 contiguous groups of about equal work, one per
+        // XCD (block b runs on XCD b % 8)
         auto& spairs = ws.spairs;
         spairs.assign(npairs, SchurPair{});
         auto& xcd_chunks = ws.xcd_chunks;
@@ -3117,17 +3063,6 @@ struct BundleAdjuster {
             int slot = 0, x = 0;
             long long acc_w = 0;
             int row = -1;
-            auto add_chunks = [&](int pi, int kind, long long start, int count, int xcd) {
-                for (int k = 0; k < count; k += SC_CHUNK) {
-                    SchurChunk ch{};
-                    ch.pair = pi;
-                    ch.slot = slot++;
-                    ch.kind = kind;
-                    ch.start = (int)(start + k);
-                    ch.count = std::min(SC_CHUNK, count - k);
-                    xcd_chunks[xcd].push_back(ch);
-                }
-            };
             for (int pi = 0; pi < npairs; pi++) {
                 const int h1 = pairs[pi].x;
                 if (h1 != row) {  // next row: move to the next XCD once this one has its share
@@ -3135,51 +3070,51 @@ struct BundleAdjuster {
                     row = h1;
                     acc_w += roww[h1];
                 }
+                const int np_ = (pcount[pi] + SC_CHUNK - 1) / SC_CHUNK, nr = (rcount[pi] + SC_CHUNK - 1) / SC_CHUNK;
+                const int nch = std::max(np_ + nr, 1);
                 SchurPair& sp = spairs[pi];
                 sp.h1 = pairs[pi].x;
                 sp.h2 = pairs[pi].y;
                 sp.c1 = cam_of_block[sp.h1];
                 sp.slot0 = slot;
+                sp.nslots = nch;
                 sp.tbeg = ptstart[pi];
                 sp.tend = ptstart[pi + 1];
                 sp.c2 = cam_of_block[sp.h2];
-                if (bitmaps) {
-                    const int* cg = h_kcntg + ((size_t)pairs[pi].x * nb + pairs[pi].y) * SC_GROUPS;
-                    long long off = pbeg[pi];
-                    for (int g = 0; g < SC_GROUPS; g++) {
-                        add_chunks(pi, 0, off, cg[g], g);
-                        off += cg[g];
-                    }
-                } else {
-                    add_chunks(pi, 0, pbeg[pi], pcount[pi], x);
-                }
-                add_chunks(pi, 1, pbeg[pi] + pcount[pi], rcount[pi], x);
-                if (slot == sp.slot0) {  // nothing to sum (tether-only or empty block): Hpp / tethers only
+                for (int k = 0; k < nch; k++) {
                     SchurChunk ch{};
                     ch.pair = pi;
-                    ch.slot = slot++;
-                    ch.kind = 0;
-                    ch.start = (int)pbeg[pi];
-                    ch.count = 0;
+                    ch.slot = slot + k;
+                    if (k < np_) {
+                        ch.kind = 0;
+                        ch.start = (int)(pbeg[pi] + (long long)k * SC_CHUNK);
+                        ch.count = std::min(SC_CHUNK, pcount[pi] - k * SC_CHUNK);
+                    } else if (k - np_ < nr) {
+                        ch.kind = 1;
+                        ch.start = (int)(pbeg[pi] + pcount[pi] + (long long)(k - np_) * SC_CHUNK);
+                        ch.count = std::min(SC_CHUNK, rcount[pi] - (k - np_) * SC_CHUNK);
+                    } else {  // nothing to sum (tether-only or empty block): Hpp / tethers only
+                        ch.kind = 0;
+                        ch.start = (int)pbeg[pi];
+                        ch.count = 0;
+                    }
                     xcd_chunks[x].push_back(ch);
                 }
-                sp.nslots = slot - sp.slot0;
+                slot += nch;
             }
             n_slots = slot;
         }
         size_t L = 0;
-        for (auto& v : xcd_chunks) L = std::max(L, (v.size() + SC_WAVES - 1) / SC_WAVES);
+        for (auto& v : xcd_chunks) L = std::max(L, v.size());
         auto& schunks = ws.schunks;
-        schunks.resize(8 * L * SC_WAVES);
+        schunks.resize(8 * L);
         for (size_t j = 0; j < L; j++)
-            for (int x = 0; x < 8; x++)
-                for (int w = 0; w < SC_WAVES; w++) {
-                    SchurChunk ch{};
-                    ch.pair = -1;
-                    const size_t i = j * SC_WAVES + w;
-                    schunks[(8 * j + x) * SC_WAVES + w] = i < xcd_chunks[x].size() ? xcd_chunks[x][i] : ch;
-                }
-        n_sblocks = (int)(schunks.size() / SC_WAVES);
+            for (int x = 0; x < 8; x++) {
+                SchurChunk ch{};
+                ch.pair = -1;
+                schunks[8 * j + x] = j < xcd_chunks[x].size() ? xcd_chunks[x][j] : ch;
+            }
+        n_sblocks = (int)schunks.size();
         auto& sfinish = ws.sfinish;  // pairs finished by schur_finish: diagonal or more than one chunk
         sfinish.clear();
         for (int pi = 0; pi < npairs; pi++)

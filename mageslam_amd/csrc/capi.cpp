@@ -193,6 +193,19 @@ void drain_locked()
 
 bool profiling_enabled() { return g_profiling.load(std::memory_order_relaxed); }
 
+namespace {
+std::mutex g_filter_mu;
+std::string g_filter;  // only tags starting with this are timed (empty: every tag)
+std::atomic<bool> g_filtered{false};
+}  // namespace
+
+bool profile_tag_selected(const char* tag)
+{
+    if (!g_filtered.load(std::memory_order_relaxed)) return true;
+    std::lock_guard<std::mutex> lk(g_filter_mu);
+    return std::strncmp(tag, g_filter.c_str(), g_filter.size()) == 0;
+}
+
 bool timed_event_pair(hipEvent_t* start, hipEvent_t* stop, int* device)
 {
     if (hipGetDevice(device) != hipSuccess) return false;
@@ -248,6 +261,13 @@ const char* mage_version(void) { return "mageslam_amd 0.1.0 (gfx950)"; }
 const char* mage_last_error(void) { return mage::last_error(); }
 
 void mage_profile_enable(int32_t enable) { mage::g_profiling.store(enable != 0); }
+
+void mage_profile_filter(const char* tag_prefix)
+{
+    std::lock_guard<std::mutex> lk(mage::g_filter_mu);
+    mage::g_filter = tag_prefix ? tag_prefix : "";
+    mage::g_filtered.store(!mage::g_filter.empty());
+}
 
 void mage_profile_reset(void)
 {

@@ -205,6 +205,7 @@ mage_status resize_linear_device(const uint8_t* src, int sw, int sh, int sstride
 // Optional per-kernel timing with HIP events recorded on the launch stream (mage_profile_*).
 // When disabled (the default) a KernelTimer costs one relaxed flag check.
 bool profiling_enabled();
+bool profile_tag_selected(const char* tag);  // mage_profile_filter
 // Timed single launches: the dispatch packet itself carries the start/stop events
 // (hipExtLaunchKernel), so timing adds no marker packets to the stream — the BA step launches
 // ~12 short kernels per trial, where two hipEventRecord calls per launch cost ~20% throughput.
@@ -216,7 +217,7 @@ inline void launch(const char* tag, F kernel, dim3 grid, dim3 block, uint32_t sh
 {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int dev = 0;
-    if (profiling_enabled() && timed_event_pair(&e0, &e1, &dev)) {
+    if (profiling_enabled() && profile_tag_selected(tag) && timed_event_pair(&e0, &e1, &dev)) {
         hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, e0, e1, 0, args...);
         timed_commit(tag, dev, e0, e1);
     } else {
