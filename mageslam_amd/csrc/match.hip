@@ -542,11 +542,12 @@ constexpr uint32_t K16_BASE = 0x2400u;  // low-16 mantissa offset of the accumul
 constexpr int K16_D = 272;           // key >> 6 = K16_D - d
 constexpr uint32_t NONE16 = 0x80008000u;
 #ifndef MAGE_FP4_GATE
-// 1: skip the fold of 32x32 tiles with no key within maxDist (a v_max3 tree + one ballot per tile).
-// Exact, but measured slower on C2 (tools/abl.py: 0.229 -> 0.267 ms per 256 pairs, bit-identical):
-// consecutive C2 frames match ~1980 of 2000 keypoints, so few tiles are free of candidates and
-// the gate only adds work; kept for inputs with sparse matches.
-#define MAGE_FP4_GATE 0
+// 1: skip the fold of 32x32 tiles with no key within maxDist (a v_max3 tree + one ballot per
+// tile), adaptively: a wave stops gating once more than half of its first 64 tiles held a
+// candidate.  Exact either way.  Measured (tools/abl.py, 256 pairs): the always-on gate cost C2
+// 0.229 -> 0.267 ms (consecutive C2 frames match ~1980 of 2000 keypoints: few tiles are free of
+// candidates) and saved rBRIEF-31 0.23 -> 0.14 ms (sparser candidates).
+#define MAGE_FP4_GATE 1
 #endif
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -631,6 +632,9 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
         stage[buf][fc >> 5][fs >> 1][32 * (fs & 1) + (fc & 31)] = st * FSC + fc < nb ? expand32_fp4(dw) : zero;
     };
 
+    // the maxDist gate's per-wave statistics (wave-uniform: scalar registers)
+    bool gating = MAGE_FP4_GATE != 0;
+    int g_tiles = 0, g_hits = 0;
     for (int pb = 0; pb < (nb > 0 ? na : 0); pb += FROWS) {
         const int rowbase = pb + wave * 32 * FRT;
         const bool active = rowbase < na;
@@ -660,7 +664,6 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
         const int kadd = 0x7FFF - rowbase - 63;
         // accumulator bits of the smallest key with d <= maxDist: (124 << 23) | 64 (272 - maxDist)
         const uint32_t gate_bits = (124u << 23) | (uint32_t)(64 * (K16_D - min(max(maxDist, -1), 127)));
-        (void)gate_bits;
         PendingCol16 pc{0, 0, 0, 0, false};
         for (int st = 0; st < nstages; st++) {
             const int buf = st % FBUF;
@@ -674,21 +677,24 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
 #pragma unroll
                     for (int s = 0; s < 4; s++) bf[s] = stage[buf][ct][s][lane];
                     uint32_t c1 = NONE16, c2 = NONE16;
-                    bool any = !MAGE_FP4_GATE;
+                    bool any = false;
 #pragma unroll
                     for (int rt = 0; rt < FRT; rt++) {
                         const v16i acc = __builtin_bit_cast(v16i, tile_mfma_k16(a[rt], bf, cc));
-#if MAGE_FP4_GATE
-                        // maxDist gate: radiusMatch keeps only d <= maxDist, and a top-2 state over a
-                        // superset of those values decides exactly as one over them alone, so a tile
-                        // whose 1024 keys all lie below the gate key (d > maxDist) is not folded
-                        uint32_t mx = (uint32_t)acc[15];  // v_max3_u32 tree (the key order is the bits' order)
+                        if (MAGE_FP4_GATE && gating) {
+                            // maxDist gate: radiusMatch keeps only d <= maxDist, and a top-2 state over
+                            // a superset of those values decides exactly as one over them alone, so a
+                            // tile whose 1024 keys all lie below the gate key (d > maxDist) is skipped
+                            uint32_t mx = (uint32_t)acc[15];  // v_max3_u32 tree (key order = bit order)
 #pragma unroll
-                        for (int g = 0; g < 15; g += 3)
-                            mx = max(mx, max(max((uint32_t)acc[g], (uint32_t)acc[g + 1]), (uint32_t)acc[g + 2]));
-                        if (__ballot(mx >= gate_bits) == 0) continue;  // wave-uniform
+                            for (int g = 0; g < 15; g += 3)
+                                mx = max(mx, max(max((uint32_t)acc[g], (uint32_t)acc[g + 1]), (uint32_t)acc[g + 2]));
+                            const bool hit = __ballot(mx >= gate_bits) != 0;  // wave-uniform
+                            g_tiles++;
+                            g_hits += hit ? 1 : 0;
+                            if (!hit) continue;
+                        }
                         any = true;
-#endif
                         uint32_t P[8];
 #pragma unroll
                         for (int q = 0; q < 8; q++)
@@ -714,6 +720,7 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                         c1 = pkmax(c1, t1);
                         c2 = pkmax(pkmax(lo, c2), t2);
                     }
+                    if (gating && g_tiles >= 64 && 2 * g_hits > g_tiles) gating = false;  // dense: fold all
                     if (!any) continue;  // no key of the column tile within maxDist: no flush
                     // the partner half-wave holds the same column (rows + 4)
                     {
