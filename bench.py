@@ -335,7 +335,10 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
         per_frame = orb_bytes_per_frame(W, H, N)
         if variant == "rbrief31":  # + each pyramid level written once and read once
             per_frame += 2 * pyramid_level_bytes(W, H, RBRIEF31["nlevels"])
-        avg_s = orb_k[dom]["avg_ms"] / 1000.0
+        # the kernel's time per step: one launch at C2, one per pyramid level for rBRIEF-31 (the
+        # algorithmic bytes are the step's, so they are priced on all of its launches)
+        per_step = max(1, round(orb_k[dom]["launches"] / max(args.steps, 1)))
+        avg_s = orb_k[dom]["avg_ms"] * per_step / 1000.0
         achieved = per_frame * B / avg_s / 1e9
         # traffic: 2 x FETCH_SIZE + WRITE_SIZE (the guide's gfx950 correction of the wide-stream
         # read counter), per steady-state launch of the committed profile of these kernel sources
@@ -345,7 +348,7 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
         valu, _ = load_pmc(dom, "valu_issue_frac", psum)
         prof_us, _ = load_pmc(dom, "avg_us_steady", psum)
         step_s = el_max / args.steps
-        frac_rocprof = None if prof_us is None else per_frame * B / (prof_us * 1e-6) / 1e9 / HBM_PEAK_GBS
+        frac_rocprof = None if prof_us is None else per_frame * B / (per_step * prof_us * 1e-6) / 1e9 / HBM_PEAK_GBS
         res["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                            # the same fraction priced on the committed rocprofv3 trace's steady-state
@@ -357,6 +360,7 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
                            "traffic_source": traffic_source + " (2 x FETCH_SIZE + WRITE_SIZE)",
                            "algorithmic_bytes_per_launch": per_frame * B,
                            "avg_launch_ms": orb_k[dom]["avg_ms"],
+                           "launches_per_step": per_step,
                            "avg_launch_source": "dispatch timestamps (hipExtLaunchKernel events) on the launch stream, "
                                                 "timed region only",
                            # the same figure priced on the committed rocprofv3 kernel trace (launches after

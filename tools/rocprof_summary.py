@@ -47,7 +47,9 @@ KERNEL_TAG = {
     "bow_leaves_kernel": "bow.leaves", "remap_linear_kernel": "image.remap", "remap_boxes_kernel": "image.boxes",
     "undistort_map_kernel": "image.map", "undistort_kernel": "orb.undistort", "synth_scene_kernel": "synth.scene",
     "synth_frames_kernel": "synth.frames", "fast_score_map_kernel": "orb.fast_score", "orient_kernel": "orb.orient",
-    "resize_linear_kernel": "orb.resize",
+    "resize_linear_kernel": "orb.resize", "resize_band_kernel": "orb.pyramid", "resize_rows_kernel": "orb.pyramid",
+    "orient_rows_kernel": "orb.orient", "radius_band_index_kernel": "match.radius_index",
+    "csort_count": "ba.sort_count", "csort_scan": "ba.sort_scan", "csort_scatter": "ba.sort_scatter",
 }
 
 
