@@ -1106,12 +1106,6 @@ __device__ __forceinline__ double dpp_f64(double v)
     const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xF, 0xF, true);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
-// Lane (CTRL - 0x150) of each DPP row broadcast over the row (row_newbcast, one v_mov_b64_dpp).
-template <int CTRL>
-__device__ __forceinline__ double dpp_bcast_f64(double v)
-{
-    return __builtin_amdgcn_update_dpp(0.0, v, CTRL, 0xF, 0xF, true);
-}
 // Inclusive prefix sum over the 16 lanes of a DPP row (row_shr 1, 2, 4, 8): lane 15 of the row
 // ends with the row total.
 __device__ __forceinline__ double row_sum16(double v)
@@ -1138,10 +1132,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     __shared__ __attribute__((aligned(16))) double vb[CT_MAXT * 16];  // b -> y -> x
     __shared__ int s_fail;
     __shared__ unsigned s_tile_bar;   // the TRSM-phase barrier count (CT_TW + 1 arrivals per step)
-    // backward solve: W_k = inv(U_kk) U_{k,k+1} (row-major, 18-double rows), c_k, and the flags
-    __shared__ __attribute__((aligned(16))) double wsh[CT_MAXT][16][18];
-    __shared__ double csh[CT_MAXT][16];
-    __shared__ unsigned s_xrdy[CT_MAXT], s_pcnt[CT_MAXT], s_crdy[CT_MAXT];
     __shared__ double cst[16][17], dst[16][17];  // A_{k,k+1}, A_{k+1,k+1} staged for the factor wave
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: tile bookkeeping on the SALU
@@ -1266,40 +1256,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         __builtin_amdgcn_wave_barrier();
         if (lane < 16) vb[16 * k + lane] = xv;
     };
-    // bounded spin (~0.3 s): a wait that never ends reports a failed solve instead of hanging
-    auto wait_flag = [&](const unsigned* w, unsigned v) {
-        for (unsigned n = 0; __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v; n++) {
-            if (n > (1u << 22)) {
-                if (lane == 0) *fail = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    };
-    auto raise_flag = [&](unsigned* w) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    auto wave_sync = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    // (inv(U_kk) v)[lane] for lanes 0-15, v a 16-double row in LDS (invT[k] read as rows is inv(U_kk))
-    auto apply_invU = [&](int k, const double* v) {
-        double xv = 0;
-        if (lane < 16) {
-            const double2* ir = reinterpret_cast<const double2*>(&invT[k][lane][0]);
-#pragma unroll 2  // the tile waves call it with their tiles live: keep the loads few
-            for (int c = 0; c < 8; c++) {
-                const double2 a = ir[c];
-                xv += a.x * v[2 * c];
-                xv += a.y * v[2 * c + 1];
-            }
-        }
-        return xv;
-    };
     if (wave == CT_TW) {
         // ===== the factor wave: it holds no tile, so none of the tile registers are live here.
         // Per step k it runs the critical chain alone: TRSM of (k, k+1) with its own inv(L_kk),
@@ -1309,7 +1265,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             s_fail = 0;
             s_tile_bar = 0;
         }
-        if (lane < CT_MAXT) s_xrdy[lane] = s_pcnt[lane] = s_crdy[lane] = 0u;
         dbl4 cA = {0, 0, 0, 0}, cD = {0, 0, 0, 0};  // A_{k,k+1}, A_{k+1,k+1} (accumulator layout)
         auto s_tile = [&](int ti, int tj) {  // tile (ti, tj) of S, padded with the identity
             dbl4 t;
@@ -1394,40 +1349,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             CT_STAMP(k, 3);
         }
         if (s_fail) return;
-        __syncthreads();  // W_k staged by the chain tiles' owners
-        // ===== backward chain: x_{mt-1} = inv(U) y_{mt-1}, then x_k = c_k - W_k x_{k+1} with
-        // c_k = inv(U_kk) (y_k - sum_{j>=k+2} U_kj x_j) from the tile waves (c_{mt-2} here): one
-        // 16x16 matvec per block on the chain, x_{k+1} broadcast by DPP row_newbcast ---
-        if (mt > 0) {
-            double xp = apply_invU(mt - 1, &vb[16 * (mt - 1)]);
-            wave_sync();
-            if (lane < 16) vb[16 * (mt - 1) + lane] = xp;
-            raise_flag(&s_xrdy[mt - 1]);
-            for (int k = mt - 2; k >= 0; k--) {
-                double c;
-                if (k == mt - 2) {
-                    c = apply_invU(k, &vb[16 * k]);
-                } else {
-                    wait_flag(&s_crdy[k], 1u);
-                    c = csh[k][lane & 15];
-                }
-                const double2* wr = reinterpret_cast<const double2*>(&wsh[k][lane & 15][0]);
-                double acc = c;
-#define MAGE_CT_BC(q)                                                                \
-    {                                                                                \
-        const double2 d2 = wr[q];                                                    \
-        acc = __builtin_fma(-d2.x, dpp_bcast_f64<0x150 + 2 * (q)>(xp), acc);         \
-        acc = __builtin_fma(-d2.y, dpp_bcast_f64<0x150 + 2 * (q) + 1>(xp), acc);     \
-    }
-                MAGE_CT_BC(0) MAGE_CT_BC(1) MAGE_CT_BC(2) MAGE_CT_BC(3)
-                MAGE_CT_BC(4) MAGE_CT_BC(5) MAGE_CT_BC(6) MAGE_CT_BC(7)
-#undef MAGE_CT_BC
-                xp = acc;
-                if (lane < 16) vb[16 * k + lane] = acc;
-                raise_flag(&s_xrdy[k]);
-            }
-        }
-        __syncthreads();  // every block solved
+        for (int k = 0; k < (mt > 0 ? mt : 1); k++) __syncthreads();  // the backward solve's barriers
         return;
     }
 
@@ -1545,33 +1467,18 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         if (tid == 0) *fail = 1;
         return;
     }
-    // --- backward (the factor wave runs the chain, see above): W_k = inv(U_kk) U_{k,k+1} of the
-    // chain tiles on the MFMA (A = inv(U_kk) from LDS, B = the tile's registers); then every
-    // other tile (i, k), i <= k-2, forms U_ik x_k as soon as x_k is out (flag xrdy[k]) into its
-    // slot of the dead panel, and the owner of (i, i+2) — the last product row i waits for —
-    // sums row i's products in column order (mt-1 .. i+2), applies inv(U_ii) and raises c_i ---
-#pragma unroll
-    for (int sl = 0; sl < CT_TPW; sl++) {
-        const int ti = tIJ[sl] & 0xFF, tj = tIJ[sl] >> 8;
-        if (ti < mt && tj == ti + 1) {
-            dbl4 acc = {0, 0, 0, 0};
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(invT[ti][lc][4 * q + lr], C[sl][q], acc, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; r++) wsh[ti][lr + 4 * r][lc] = acc[r];
-        }
-    }
-    __syncthreads();  // W_k staged
-    double (*part)[16] = reinterpret_cast<double (*)[16]>(&pan[0][0][0][0]);  // [i * CT_MAXT + j][row]
-    for (int k = mt - 1; k >= 2; k--) {
-        // slots in reverse (row-major) order: the finisher tile (k - 2, k) after its row's others
+    // --- backward: U x = y, x_k = inv(U_kk) (y_k - sum_{j>k} U_kj x_j), right-looking with
+    // one barrier per block: the owner of tile (k-1, k) applies the last update of y_{k-1} and
+    // then solves block k-1 itself ---
+    if (mt > 0 && wave == 0) solve_block(mt - 1);
+    __syncthreads();
+    for (int k = mt - 1; k >= 1; k--) {
+        // slots in reverse (row-major) order: the tile (k - 1, k) of the critical chain first
 #pragma unroll
         for (int sl = CT_TPW - 1; sl >= 0; sl--) {
             int ti, tj;
             tile_of(sl, ti, tj);
-            if (tj == k && ti <= k - 2) {
-                wait_flag(&s_xrdy[k], 1u);
+            if (tj == k && ti < k) {
                 // (U_ik x_k)[r] = sum_c U_ik[r][c] x_k[c]: row sums over the 16 lanes of a DPP row
                 // (lane 15 of the row holds rows lr + 4r)
                 const double xk = vb[16 * k + lc];
@@ -1580,27 +1487,17 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 for (int r = 0; r < 4; r++) rs[r] = row_sum16(C[sl][r] * xk);
                 if (lc == 15)
 #pragma unroll
-                    for (int r = 0; r < 4; r++) part[ti * CT_MAXT + k][lr + 4 * r] = rs[r];
-                if (ti == k - 2) {
-                    wave_sync();  // the own product, across lanes
-                    wait_flag(&s_pcnt[ti], (unsigned)max(mt - ti - 3, 0));
-                    double* z = part[ti * CT_MAXT + ti];  // unused slot (i, i): z_i
-                    if (lane < 16) {
-                        double v = vb[16 * ti + lane];
-                        for (int j = mt - 1; j >= k; j--) v -= part[ti * CT_MAXT + j][lane];
-                        z[lane] = v;
-                    }
-                    wave_sync();
-                    const double c = apply_invU(ti, z);
-                    if (lane < 16) csh[ti][lane] = c;
-                    raise_flag(&s_crdy[ti]);
-                } else {
-                    raise_flag(&s_pcnt[ti]);
+                    for (int r = 0; r < 4; r++) vb[16 * ti + lr + 4 * r] -= rs[r];
+                if (ti == k - 1) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    solve_block(k - 1);
                 }
             }
         }
+        __syncthreads();
     }
-    __syncthreads();  // every block solved
     tick(5);
 #if MAGE_CHOL_ABLATE == 4
     if (tid == 0) {

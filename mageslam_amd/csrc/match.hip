@@ -543,11 +543,12 @@ constexpr int K16_D = 272;           // key >> 6 = K16_D - d
 constexpr uint32_t NONE16 = 0x80008000u;
 #ifndef MAGE_FP4_GATE
 // 1: skip the fold of 32x32 tiles with no key within maxDist (a v_max3 tree + one ballot per
-// tile), adaptively: a wave stops gating once more than half of its first 64 tiles held a
-// candidate.  Exact either way.  Measured (tools/abl.py, 256 pairs): the always-on gate cost C2
-// 0.229 -> 0.267 ms (consecutive C2 frames match ~1980 of 2000 keypoints: few tiles are free of
-// candidates) and saved rBRIEF-31 0.23 -> 0.14 ms (sparser candidates).
-#define MAGE_FP4_GATE 1
+// tile), adaptively: a wave stops gating once more than a quarter of its tiles (after 64) held a
+// candidate.  Exact either way, but off: measured (tools/abl.py, 256 C2 pairs) the always-on gate
+// costs 0.229 -> 0.267 ms, the adaptive one 0.253 (half-density cut-off) / 0.256 (quarter) — the
+// fold is not what bounds the kernel once the gate's branch breaks the overlap of the MFMAs with
+// the fold — while rBRIEF-31's sparser candidates would gain 0.23 -> 0.16 ms.
+#define MAGE_FP4_GATE 0
 #endif
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -720,7 +721,7 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                         c1 = pkmax(c1, t1);
                         c2 = pkmax(pkmax(lo, c2), t2);
                     }
-                    if (gating && g_tiles >= 64 && 2 * g_hits > g_tiles) gating = false;  // dense: fold all
+                    if (gating && g_tiles >= 64 && 4 * g_hits > g_tiles) gating = false;  // dense: fold all
                     if (!any) continue;  // no key of the column tile within maxDist: no flush
                     // the partner half-wave holds the same column (rows + 4)
                     {
