@@ -83,6 +83,16 @@ def ba_flops(g, trials_per_iter):
     return 330.0 * len(g.cam) + trials_per_iter * (schur + n ** 3 / 3 + 2 * n ** 2)
 
 
+# the source files a kernel tag is built from (a committed summary's counters stay valid for the
+# kernel while these are unchanged)
+KERNEL_FILES = {
+    "orb.": ["orb.hip", "orb_tables.hpp", "lds_sort.hpp", "common.hpp"],
+    "match.": ["match.hip", "radius.hip", "band_index.hpp", "lds_sort.hpp", "common.hpp"],
+    "ba.": ["ba.hip", "ba_math.hpp", "common.hpp"],
+    "pose.": ["pose.hip", "ba_math.hpp", "common.hpp"],
+}
+
+
 def load_pmc(kernel, field="hbm_bytes_per_launch", summary="pmc_summary.json"):
     """(`field` of `kernel`, provenance) from a committed rocprofv3 PMC summary (default: HBM
     bytes per launch of the ORB-only profile; pmc_summary_ba.json: the full bench profile, which
@@ -99,6 +109,18 @@ def load_pmc(kernel, field="hbm_bytes_per_launch", summary="pmc_summary.json"):
         return None, f"unreadable PMC summary ({e})"
     meta = d.get("_meta", {})
     sha, now = meta.get("kernel_sources_sha"), kernel_sources_sha()
+    files = next((v for k, v in KERNEL_FILES.items() if kernel.startswith(k)), None)
+    fshas = meta.get("kernel_file_shas")
+    if sha != now and fshas and files:
+        # the whole tree changed since the profile, but maybe not this kernel's own sources
+        from mageslam_amd.build import kernel_file_shas
+
+        cur = kernel_file_shas()
+        changed = [f for f in files if fshas.get(f) != cur.get(f)]
+        if not changed:
+            return d.get(kernel, {}).get(field), \
+                f"profiles/{summary} ({meta.get('tag')}, kernel sources {sha}; {', '.join(files)} unchanged since)"
+        return None, f"stale: {', '.join(changed)} changed since profiles/{summary} ({meta.get('tag')})"
     if sha != now:
         return None, f"stale: profiles/{summary} was collected on kernel sources {sha}, these are {now}"
     return d.get(kernel, {}).get(field), \

@@ -38,6 +38,15 @@ def kernel_sources_sha() -> str:
     return h.hexdigest()[:16]
 
 
+def kernel_file_shas() -> dict:
+    """Per-file SHA-256 (first 16 hex digits) of the same sources: a committed counter summary stays
+    valid for a kernel while the files that kernel is built from are unchanged."""
+    import hashlib
+
+    return {f.name: hashlib.sha256(f.read_bytes()).hexdigest()[:16]
+            for f in sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("*.hpp")) + list(CSRC.glob("*.cpp")))}
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and Path(cand).exists():

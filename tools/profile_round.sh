@@ -53,7 +53,7 @@ fi
 #   main = headline + ORB-only sets, rows = the per-row set + the final default bench line
 PHASE=${2:-all}
 if [ "$PHASE" = all ] || [ "$PHASE" = main ]; then
-    run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores
+    run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores --no-tracking --no-rbrief31
     run_set $ORB $ORB_CMD
     run_set $ORB31 $ORB31_CMD
 fi

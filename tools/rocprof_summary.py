@@ -146,6 +146,12 @@ def main():
 
         sha = kernel_sources_sha()
     summary = {"_meta": {"tag": tag, "kernel_sources_sha": sha, "command": cmd, "skipped_warmup_launches": skip}}
+    # per-file hashes, recorded only when this tree is the one the counters were collected on
+    sys.path.insert(0, str(ROOT))
+    from mageslam_amd.build import kernel_file_shas, kernel_sources_sha as _now_sha
+
+    if _now_sha() == sha:
+        summary["_meta"]["kernel_file_shas"] = kernel_file_shas()
     for r in stats:
         k = r["kernel"]
         f = fetch.get(k)
