@@ -178,7 +178,6 @@ def main():
                                 "mfma_busy_cycles_per_launch": mfma.get(k)}
     (out_dir / f"{tag}_rocprof.md").write_text("\n".join(lines) + "\n")
     (out_dir / f"{tag}_pmc_summary.json").write_text(json.dumps(summary, indent=1))
-    (out_dir / "pmc_summary.json").write_text(json.dumps(summary, indent=1))
     print("\n".join(lines))
 
 
