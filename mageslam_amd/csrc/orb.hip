@@ -1317,7 +1317,7 @@ constexpr int KPW = MAGE_DESC_KPW;
 
 // MULTI = false (one level, no orientation: the default configuration): level 0 and rotation 0
 // without the per-keypoint level lookups.
-template <int RB, bool MULTI>
+template <int RB, bool MULTI, int KP>
 __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     DescParams p, const uint32_t* __restrict__ xy_in, const uint32_t* __restrict__ n_in,
     const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
@@ -1328,7 +1328,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     constexpr int NIT = NBR * NBC * 8;  // 16-byte items, 8 per brick (one 128-byte line)
     constexpr int NLD = (NIT + kWave - 1) / kWave;
     constexpr int WP = 32 * NBC;        // LDS window row pitch
-    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KPW][4 * NBR * WP];
+    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KP][4 * NBR * WP];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave: scalar
     // XCD-aware 1-D grid: workgroups are dispatched round-robin over the 8 XCDs, so block b runs
     // on XCD b % 8; all keypoint chunks of frame f get blocks = f (mod 8) and consecutive slots,
@@ -1336,17 +1336,17 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
     const int chunk = slot % p.chunks, f = (slot / p.chunks) * 8 + xcd;
     if (f >= p.frames) return;
-    const int k0 = (chunk * DESC_WAVES + wave) * KPW;
+    const int k0 = (chunk * DESC_WAVES + wave) * KP;
     const int n = (int)n_in[f];
     if (k0 >= n) return;
     const int R = p.R;
     // lane item i -> brick i / 8 of the window, 16-byte part i % 8; keypoints keep the pattern
     // radius from the border (RunByImageBorder), so the clamps are inert: they only keep reads
     // inside the level
-    uint4 v[KPW][NLD];
-    int off[KPW], rot[KPW];
+    uint4 v[KP][NLD];
+    int off[KP], rot[KP];
 #pragma unroll
-    for (int q = 0; q < KPW; q++) {
+    for (int q = 0; q < KP; q++) {
         const long long ki = (long long)f * p.out_cap + min(k0 + q, n - 1);
         const uint32_t xy = xy_in[ki];
         const int lv = MULTI ? __builtin_amdgcn_readfirstlane(p.lvl[ki]) : 0, l = lv >> 8;  // wave-uniform
@@ -1364,7 +1364,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
         }
     }
 #pragma unroll
-    for (int q = 0; q < KPW; q++)
+    for (int q = 0; q < KP; q++)
 #pragma unroll
         for (int ld = 0; ld < NLD; ld++) {
             const int i = lane + kWave * ld, b = i >> 3, br = b / NBC, bc = b - br * NBC;
@@ -1374,7 +1374,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     wave_lds_sync();
     const char4* pat = reinterpret_cast<const char4*>(pattern);
 #pragma unroll
-    for (int q = 0; q < KPW; q++) {
+    for (int q = 0; q < KP; q++) {
         const int k = k0 + q;
         if (k >= n) break;
         const uint8_t* wb = &win[wave][q][off[q]];
@@ -1706,6 +1706,7 @@ struct OrientParams {
     unsigned out_cap;
     int half_k;
     int umax[32];
+    int chunks, frames;  // orient_rows_kernel's XCD-aware 1-D grid
 };
 
 // cv::fastAtan2 (OpenCV 3.4.0 core mathfuncs_core, polynomial atan in degrees), each float
@@ -1798,9 +1799,14 @@ __global__ __launch_bounds__(256) void orient_rows_kernel(mage_keypoint* __restr
         wmask[av][d] = m;
     }
     __syncthreads();
-    const int f = blockIdx.y;
+    // XCD-aware 1-D grid (as describe_blurred_kernel): block b runs on XCD b % 8 and every keypoint
+    // chunk of frame f gets a block on XCD f % 8, so a frame's level images are fetched into one L2
+    // (a 2-D grid spread each frame's chunks over all eight and fetched every level 8 times)
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int chunk = slot % p.chunks, f = (slot / p.chunks) * 8 + xcd;
+    if (f >= p.frames) return;  // the whole workgroup
     const int lane = threadIdx.x & 63, j = lane & (OR_ROWS - 1);
-    const int k = blockIdx.x * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
+    const int k = chunk * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
     const int n = (int)n_in[f];
     const long long i = (long long)f * p.out_cap + min(k, max(n - 1, 0));
     const int l = lvl[i] >> 8;
@@ -2329,8 +2335,12 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             ++v0;
         }
         if (half >= 5 && half <= 15)  // a disc row per lane, two keypoints per wave
-            launch("orb.orient", orient_rows_kernel, dim3((cap + 7) / 8, batch), dim3(256), 0, st, d_kp,
-                   o->xy.as<uint32_t>(), o->lvl.as<uint16_t>(), d_n, op);
+        {
+            op.chunks = (int)((cap + 7) / 8);
+            op.frames = (int)batch;
+            launch("orb.orient", orient_rows_kernel, dim3((unsigned)(op.chunks * ((batch + 7) / 8) * 8)), dim3(256), 0, st,
+                   d_kp, o->xy.as<uint32_t>(), o->lvl.as<uint16_t>(), d_n, op);
+        }
         else
             launch("orb.orient", orient_kernel, dim3((cap + 3) / 4, batch), dim3(256), 0, st, d_kp, o->xy.as<uint32_t>(),
                    o->lvl.as<uint16_t>(), d_n, op);
@@ -2361,13 +2371,16 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
                 launch("orb.describe", describe_win_kernel, g3, dim3(DESC_WAVES * kWave), 0, st, dp,
                        (const uint32_t*)o->xy.as<uint32_t>(), d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
             } else if (fused_blur) {
-                dp.chunks = (int)((cap + DESC_WAVES * KPW - 1) / (DESC_WAVES * KPW));
+                // keypoints per wave: 4, or 2 for the wide (rotated, radius > 13) windows, whose
+                // LDS (37 rows x 96 bytes each) otherwise left two workgroups per CU
+                const int kp = dp.R <= 13 ? KPW : 2;
+                dp.chunks = (int)((cap + DESC_WAVES * kp - 1) / (DESC_WAVES * kp));
                 dp.frames = (int)batch;
                 const dim3 g3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
-                auto kern = multi ? (dp.R <= 7 ? describe_blurred_kernel<7, true>
-                                               : (dp.R <= 13 ? describe_blurred_kernel<13, true> : describe_blurred_kernel<RMAX, true>))
-                                  : (dp.R <= 7 ? describe_blurred_kernel<7, false>
-                                               : (dp.R <= 13 ? describe_blurred_kernel<13, false> : describe_blurred_kernel<RMAX, false>));
+                auto kern = multi ? (dp.R <= 7 ? describe_blurred_kernel<7, true, KPW>
+                                               : (dp.R <= 13 ? describe_blurred_kernel<13, true, KPW> : describe_blurred_kernel<RMAX, true, 2>))
+                                  : (dp.R <= 7 ? describe_blurred_kernel<7, false, KPW>
+                                               : (dp.R <= 13 ? describe_blurred_kernel<13, false, KPW> : describe_blurred_kernel<RMAX, false, 2>));
                 launch("orb.describe", kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, (const uint32_t*)o->xy.as<uint32_t>(),
                        d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
             } else {
