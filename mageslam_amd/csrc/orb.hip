@@ -1645,6 +1645,59 @@ __global__ __launch_bounds__(256) void resize_band_kernel(const uint8_t* __restr
     }
     __syncthreads();
     const int nq = (p.dw + 3) >> 2;
+    if (!p.area2 && nq <= 256) {
+        // a thread keeps one 4-pixel column group for the band's rows: its horizontal taps
+        // (source column, the two weights, which formula) are read once, not per output pixel
+        const int rgn = 256 / nq, x4 = tid % nq, rs = tid / nq;
+        if (rs >= rgn) return;
+        int sx[4], a0[4], a1[4];
+        bool in[4], lin[4], vec[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int dx = 4 * x4 + e;
+            in[e] = dx < p.dw;
+            sx[e] = in[e] ? p.xofs[dx] : 0;
+            const uint32_t a = in[e] ? p.alpha[dx] : 0u;
+            a0[e] = (short)(a & 0xFFFFu);
+            a1[e] = (short)(a >> 16);
+            lin[e] = dx < p.xmax;
+            vec[e] = dx < p.xv;
+        }
+        for (int dr = rs; dr < nd; dr += rgn) {
+            const int dy = d0 + dr;
+            const int sy = p.yofs[dy];
+            const uint8_t* R0 = rz_rows + (size_t)(min(max(sy, 0), p.sh - 1) - r0) * swp;
+            const uint8_t* R1 = rz_rows + (size_t)(min(max(sy + 1, 0), p.sh - 1) - r0) * swp;
+            const uint32_t bb = p.beta[dy];
+            const int b0 = (short)(bb & 0xFFFFu), b1 = (short)(bb >> 16);
+            uint32_t out = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                int h0, h1;
+                if (lin[e]) {
+                    h0 = R0[sx[e]] * a0[e] + R0[sx[e] + 1] * a1[e];
+                    h1 = R1[sx[e]] * a0[e] + R1[sx[e] + 1] * a1[e];
+                } else {
+                    h0 = R0[sx[e]] * 2048;
+                    h1 = R1[sx[e]] * 2048;
+                }
+                int v;
+                if (vec[e])
+                    v = (((((int)(short)(h0 >> 4)) * b0) >> 16) + ((((int)(short)(h1 >> 4)) * b1) >> 16) + 2) >> 2;
+                else
+                    v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+                v = min(max(v, 0), 255);
+                out |= in[e] ? (uint32_t)v << (8 * e) : 0u;
+            }
+            uint8_t* D = dst + (long long)f * p.dpitch + (long long)dy * p.dstride;
+            if ((reinterpret_cast<uintptr_t>(D) & 3) == 0 && 4 * x4 + 3 < p.dw) {
+                *reinterpret_cast<uint32_t*>(D + 4 * x4) = out;
+            } else {
+                for (int e = 0; e < 4 && 4 * x4 + e < p.dw; e++) D[4 * x4 + e] = (uint8_t)(out >> (8 * e));
+            }
+        }
+        return;
+    }
     for (int it = tid; it < nd * nq; it += 256) {
         const int dr = it / nq, x4 = it - dr * nq, dy = d0 + dr;
         const uint8_t *R0, *R1;
