@@ -432,10 +432,13 @@ __global__ __launch_bounds__(TT) void trk_filter(TrackBufs b, TrackConst c, cons
         b.os2[1] = base;
     }
     if (c.s.local_map_keyframes == 0 || b.ctl->lost) return;
-    const uint32_t nf = min(*nf_ptr, c.cap);
+    // the unassociated-keypoint mask is built in LDS (2000 atomics on ~63 global words serialised
+    // at the L2) and written out once
+    __shared__ uint32_t smask[4096 / 32];
+    const uint32_t nf = min(min(*nf_ptr, c.cap), 4096u);
     const uint32_t nk = b.ctl->kf_n[ref_slot(b.ctl, c)];
     for (uint32_t w = threadIdx.x; w < (nf + 31) / 32; w += TT)
-        b.lm_mask[w] = (32 * w + 32 <= nf) ? 0xFFFFFFFFu : ((1u << (nf - 32 * w)) - 1u);
+        smask[w] = (32 * w + 32 <= nf) ? 0xFFFFFFFFu : ((1u << (nf - 32 * w)) - 1u);
     for (uint32_t i = threadIdx.x; i < nk; i += TT) {
         b.lm_visited[i] = 0;
         b.lm_hide[i] = -1;
@@ -446,12 +449,14 @@ __global__ __launch_bounds__(TT) void trk_filter(TrackBufs b, TrackConst c, cons
     for (uint32_t k = threadIdx.x; k < n; k += TT) {
         const uint32_t q = b.sel[m[k].query_idx], t = (uint32_t)m[k].train_idx;
         if (!b.out1[k]) {
-            atomicAnd(&b.lm_mask[t >> 5], ~(1u << (t & 31)));
+            if (t < nf) atomicAnd(&smask[t >> 5], ~(1u << (t & 31)));
             b.lm_visited[q] = 1;
         } else {
             b.lm_hide[q] = (int32_t)t;
         }
     }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < (nf + 31) / 32; w += TT) b.lm_mask[w] = smask[w];
 }
 
 // TrackLocalMap.cpp:149-223: the local map's unvisited points, keyframe by keyframe in ascending id,
