@@ -1314,6 +1314,9 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
 #define MAGE_DESC_KPW 4
 #endif
 constexpr int KPW = MAGE_DESC_KPW;
+#ifndef MAGE_DESC_KP_WIDE
+#define MAGE_DESC_KP_WIDE 1  // keypoints per wave for the rotated (radius 18) windows: describe 0.254 ms per rBRIEF-31 step at 1, 0.306 at 2
+#endif
 
 // MULTI = false (one level, no orientation: the default configuration): level 0 and rotation 0
 // without the per-keypoint level lookups.
@@ -2426,14 +2429,14 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             } else if (fused_blur) {
                 // keypoints per wave: 4, or 2 for the wide (rotated, radius > 13) windows, whose
                 // LDS (37 rows x 96 bytes each) otherwise left two workgroups per CU
-                const int kp = dp.R <= 13 ? KPW : 2;
+                const int kp = dp.R <= 13 ? KPW : MAGE_DESC_KP_WIDE;
                 dp.chunks = (int)((cap + DESC_WAVES * kp - 1) / (DESC_WAVES * kp));
                 dp.frames = (int)batch;
                 const dim3 g3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
                 auto kern = multi ? (dp.R <= 7 ? describe_blurred_kernel<7, true, KPW>
-                                               : (dp.R <= 13 ? describe_blurred_kernel<13, true, KPW> : describe_blurred_kernel<RMAX, true, 2>))
+                                               : (dp.R <= 13 ? describe_blurred_kernel<13, true, KPW> : describe_blurred_kernel<RMAX, true, MAGE_DESC_KP_WIDE>))
                                   : (dp.R <= 7 ? describe_blurred_kernel<7, false, KPW>
-                                               : (dp.R <= 13 ? describe_blurred_kernel<13, false, KPW> : describe_blurred_kernel<RMAX, false, 2>));
+                                               : (dp.R <= 13 ? describe_blurred_kernel<13, false, KPW> : describe_blurred_kernel<RMAX, false, MAGE_DESC_KP_WIDE>));
                 launch("orb.describe", kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, (const uint32_t*)o->xy.as<uint32_t>(),
                        d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
             } else {
