@@ -23,6 +23,11 @@
 #include <cfloat>
 #include <cmath>
 
+// FMA contraction for this file's device arithmetic (the library is built with -ffp-contract=off):
+// the pose-only problem is a chain of short dependent fp64 sequences (per-trial 6x6 solve, exp map)
+// whose length halves when a*b+c is one instruction.  Parity with the oracle is by tolerance and
+// identical decisions (outliers, iterations, trials), which the reduction order already requires.
+#pragma clang fp contract(fast)
 #include "ba_math.hpp"
 #include "common.hpp"
 
@@ -31,9 +36,33 @@ namespace {
 
 using namespace ba;
 
-// threads per problem: 256 for large batches (2 problems per CU at 220 VGPRs), 512 when the
-// batch cannot fill the chip (the tracker's per-frame single problem: half the edge-loop latency)
-constexpr int PB_THREADS_BATCH = 256, PB_THREADS_FEW = 512;
+// threads per problem: 256 for large batches (2 problems per CU); MAGE_POSE_FEW_THREADS when the
+// batch cannot fill the chip (the tracker's per-frame single problem).  Every thread runs the
+// per-trial solve and exp map itself, so two waves per SIMD issue that chain twice: one wave per
+// SIMD (256) halves it and the reductions, while the edge passes are issue-bound either way.
+#ifndef MAGE_POSE_FEW_THREADS
+#define MAGE_POSE_FEW_THREADS 256
+#endif
+constexpr int PB_THREADS_BATCH = 256, PB_THREADS_FEW = MAGE_POSE_FEW_THREADS;
+// observations of a problem staged in LDS (X, Y, Z, info | u, v) when it has at most this many:
+// every edge pass then reads LDS instead of L2 (a lane's edges are read by that lane only)
+constexpr int POSE_STAGE = 2048;
+
+#ifndef MAGE_POSE_STAMPS
+#define MAGE_POSE_STAMPS 0  // tools/pose_stamps.py: phase stamps (s_memtime) of problem 0, thread 0
+#endif
+#if MAGE_POSE_STAMPS
+__device__ unsigned long long g_pose_st[256];
+#define PST(id)                                                                                                 \
+    do {                                                                                                        \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && nst < 254)                                                   \
+            g_pose_st[nst++] = ((unsigned long long)(id) << 56) | (__builtin_amdgcn_s_memtime() & 0xFFFFFFFFFFFFFFull); \
+    } while (0)
+#else
+#define PST(id) \
+    do {        \
+    } while (0)
+#endif
 
 struct PoseParams {
     const float* pos3;    // per problem: view-space t
@@ -58,6 +87,7 @@ struct PoseParams {
 // (BundlerLib.cpp:269-273; the same arithmetic as mage_ba_set_cameras)
 __device__ void pose_from_input(const float* r9, const float* t3, double q[4], double t[3])
 {
+#pragma clang fp contract(off)
     float m[9];
     for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++) m[r * 3 + c] = r9[c * 3 + r];
@@ -88,35 +118,58 @@ __device__ void pose_from_input(const float* r9, const float* t3, double q[4], d
     for (int k = 0; k < 3; k++) t[k] = (double)t3[k];
 }
 
-// reprojection error, robust chi2 and (if H) the pose normal-equation terms of one edge
 struct EdgeIn {
     double X[3], u, v, info;
 };
 
+// Reprojection error, robust chi2 and the pose normal-equation terms of one edge, added into acc
+// (21 upper Hpp entries, 6 bp, rho0 at 27); also the post-pass inputs: ss = |e|^2 and the depth
+// (cheirality: (R X + t)_z > 0 is the reference's (X + R^T t) . R^T z > 0).  Branch-free (Huber by
+// selects), so two edges' chains interleave; one reciprocal of the depth serves the projection and
+// the Jacobian.  This file is compiled with FMA contraction (see the pragma above): the terms are
+// w J^T J and J^T (-w e) with the weight folded into one Jacobian row first (g2o's JtWJ order is
+// not reproduced anyway: the sums run in another order than the oracle's, parity is by tolerance +
+// identical decisions); the products with the structural zeros J[0][4] and J[1][3] are skipped
+// (exact: every other operand is finite).
 __device__ __forceinline__ void edge_terms(const EdgeIn& e, const double q[4], const double t[3], double f, double cx,
-                                           double cy, double huber, double ev[2], double& rho0, double* acc28)
+                                           double cy, double huber, double& ss, double& z, double (&acc)[32])
 {
     double xc[3];
     d_qrot(q, e.X, xc);
     xc[0] += t[0];
     xc[1] += t[1];
     xc[2] += t[2];
-    ev[0] = e.u - (xc[0] / xc[2] * f + cx);
-    ev[1] = e.v - (xc[1] / xc[2] * f + cy);
-    const double chi2 = e.info * (ev[0] * ev[0] + ev[1] * ev[1]);
-    double rho1;
-    d_huber(huber, chi2, rho0, rho1);
-    if (!acc28) return;
+    z = xc[2];
+    const double iz = 1.0 / xc[2];
+    const double xi = xc[0] * iz, yi = xc[1] * iz, fi = f * iz;
+    const double ev0 = e.u - (xi * f + cx), ev1 = e.v - (yi * f + cy);
+    ss = ev0 * ev0 + ev1 * ev1;
+    const double chi2 = e.info * ss;
+    const double dsqr = huber * huber, sq = __builtin_sqrt(chi2);
+    const bool in = chi2 <= dsqr;  // RobustKernelHuber
+    acc[27] += in ? chi2 : 2 * sq * huber - dsqr;
+    const double rho1 = in ? 1.0 : huber / sq;
     double Jp[12];
-    jac_pose(xc, f, Jp);
+    jac_pose_q(xi, yi, fi, f, Jp);
     const double w = rho1 * e.info;
-    const double or0 = -e.info * ev[0] * rho1, or1 = -e.info * ev[1] * rho1;
+    const double or0 = -e.info * ev0 * rho1, or1 = -e.info * ev1 * rho1;
+    double wj[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) wj[k] = Jp[k] * w;
 #pragma unroll
     for (int r = 0; r < 6; r++)
 #pragma unroll
-        for (int c = r; c < 6; c++) acc28[r * 6 - r * (r - 1) / 2 + c - r] += (Jp[r] * Jp[c] + Jp[6 + r] * Jp[6 + c]) * w;
+        for (int c = r; c < 6; c++) {
+            double& h = acc[r * 6 - r * (r - 1) / 2 + c - r];
+            if (r != 4 && c != 4) h = __builtin_fma(wj[r], Jp[c], h);
+            if (r != 3 && c != 3) h = __builtin_fma(wj[6 + r], Jp[6 + c], h);
+        }
 #pragma unroll
-    for (int r = 0; r < 6; r++) acc28[21 + r] += Jp[r] * or0 + Jp[6 + r] * or1;
+    for (int r = 0; r < 6; r++) {
+        double& b = acc[21 + r];
+        if (r != 4) b = __builtin_fma(Jp[r], or0, b);
+        if (r != 3) b = __builtin_fma(Jp[6 + r], or1, b);
+    }
 }
 
 // fixed-order workgroup sum of acc[0..N) into out[0..N) (all threads read out afterwards).
@@ -229,16 +282,28 @@ __device__ __forceinline__ bool pose_solve(const double* sum, double lam, double
 // barriers are the reductions'.  The trial evaluation also accumulates the normal equations at the
 // trial pose: when the trial is accepted they are the next step's linearisation (g2o linearises
 // at the accepted state), so after step 0 a step costs one edge pass per trial.
+//
+// Post-pass folded into the edge passes (staged problems): BundlerLib's outlier pass reads each
+// edge's error from the LAST evaluated state and the cheirality at the CURRENT pose, which is the
+// last trial's pose if it was accepted, else the pose the current state was evaluated at.  Each
+// pass therefore keeps per lane, for its edges, a bit "error above maxErrorSquare" and a bit
+// "in front of the camera", and reduces the kept-edge sums (sum of ss, count) for both outcomes
+// (slots 28-31 of the 32-value reduction, which the butterfly carries for free); after the loop
+// the bits of the current pose give the outlier flags without another pass over the edges.
 template <int PB_THREADS>
 __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
 {
-    __shared__ double red[PB_THREADS / kWave][28];
-    __shared__ double sums[2][28];  // the linearisation at the current pose / at the trial pose
+    __shared__ double red[PB_THREADS / kWave][32];
+    __shared__ double sums[2][32];  // the linearisation at the current pose / at the trial pose
     // LM state: written by every thread with the same value (each thread computes it), so a
     // thread's reads follow its own writes and no barrier is needed; in LDS rather than registers
     // to keep them out of the edge loops' register budget
     __shared__ double s_cur[7], s_ev[7], s_x[6];  // current pose (q, t), last evaluated pose, last solve
+    __shared__ float4 s_e0[POSE_STAGE];           // staged observations: X, Y, Z, info
+    __shared__ float2 s_e1[POSE_STAGE];           // u, v
     const int pr = blockIdx.x, tid = threadIdx.x;
+    [[maybe_unused]] int nst = 0;
+    PST(0);
     const uint32_t e0 = p.obs_start[pr], e1 = p.obs_start[pr + 1];
     const int E = (int)(e1 - e0);
     const double f = p.intr4[4 * pr + 2], cx = p.intr4[4 * pr], cy = p.intr4[4 * pr + 1];
@@ -249,46 +314,109 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
         for (int k = 0; k < 3; k++) s_cur[4 + k] = t[k];
         for (int k = 0; k < 6; k++) s_x[k] = 0;
     }
+    // a lane's edges are observations tid + k PB_THREADS; staged (and post-pass bits) up to 32 per lane
+    const bool staged = E <= POSE_STAGE && E <= 32 * PB_THREADS;
+    if (staged) {
+        // every load of the lane's edges in flight before the first LDS write (a loop of
+        // load -> write pairs waited out one L2 round trip per edge)
+        constexpr int KS = POSE_STAGE / PB_THREADS;
+        float4 ga[KS];
+        float2 gb[KS];
+#pragma unroll
+        for (int k = 0; k < KS; k++) {
+            const int i = tid + k * PB_THREADS;
+            if (i < E) {
+                const uint32_t g = e0 + i;
+                ga[k] = make_float4(p.points3[3 * g], p.points3[3 * g + 1], p.points3[3 * g + 2], p.info[g]);
+                gb[k] = make_float2(p.uv[2 * g], p.uv[2 * g + 1]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KS; k++) {
+            const int i = tid + k * PB_THREADS;
+            if (i < E) {  // read back by the same thread: no barrier
+                s_e0[i] = ga[k];
+                s_e1[i] = gb[k];
+            }
+        }
+    }
+    PST(1);
     bool have_eval = false;
     double lambda = 0, ni = 2;
+    const double maxe = p.max_err_sq;
     auto load_edge = [&](int i) {
         EdgeIn e;
-        const uint32_t g = e0 + i;
-        e.X[0] = p.points3[3 * g];
-        e.X[1] = p.points3[3 * g + 1];
-        e.X[2] = p.points3[3 * g + 2];
-        e.u = p.uv[2 * g];
-        e.v = p.uv[2 * g + 1];
-        e.info = p.info[g];
+        if (staged) {
+            const float4 a = s_e0[i];
+            const float2 b = s_e1[i];
+            e.X[0] = a.x;
+            e.X[1] = a.y;
+            e.X[2] = a.z;
+            e.info = a.w;
+            e.u = b.x;
+            e.v = b.y;
+        } else {
+            const uint32_t g = e0 + i;
+            e.X[0] = p.points3[3 * g];
+            e.X[1] = p.points3[3 * g + 1];
+            e.X[2] = p.points3[3 * g + 2];
+            e.u = p.uv[2 * g];
+            e.v = p.uv[2 * g + 1];
+            e.info = p.info[g];
+        }
         return e;
     };
-    // errors, robust chi2 and normal equations of every edge at pose qt = (q, t) -> sums[slot]
+    // post-pass bits of the lane's edges: big (ss > maxErrorSquare) of the last pass, front (depth
+    // > 0) of the last pass, and front at the current pose
+    uint32_t big = 0, front = 0, front_cur = 0;
+    // errors, robust chi2 and normal equations of every edge at pose qt = (q, t) -> sums[slot];
+    // two edges per iteration (independent chains interleave)
     auto linearise = [&](const double* qt, int slot) {
         const double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t[3] = {qt[4], qt[5], qt[6]};
-        double acc[28];
+        double acc[32];
 #pragma unroll
-        for (int k = 0; k < 28; k++) acc[k] = 0;
-        for (int i = tid; i < E; i += PB_THREADS) {
-            const EdgeIn e = load_edge(i);
-            double ev[2], rho0;
-            // per-edge terms into a fresh array, then added (0 + x is exact): accumulating through
-            // the pointer directly kept acc in scratch memory across the loop
-            double a2[28];
-#pragma unroll
-            for (int k = 0; k < 28; k++) a2[k] = 0;
-            edge_terms(e, q, t, f, cx, cy, p.huber, ev, rho0, a2);
-#pragma unroll
-            for (int k = 0; k < 27; k++) acc[k] += a2[k];
-            acc[27] += rho0;
+        for (int k = 0; k < 32; k++) acc[k] = 0;
+        uint32_t nb = 0, nf = 0, bit = 1;
+        auto post = [&](double ss, double z) {
+            const bool bg = ss > maxe, fr = z > 0;
+            nb |= bg ? bit : 0u;
+            nf |= fr ? bit : 0u;
+            const bool keep_acc = fr && !bg, keep_rej = (front_cur & bit) && !bg;  // trial accepted / rejected
+            acc[28] += keep_acc ? ss : 0.0;
+            acc[29] += keep_acc ? 1.0 : 0.0;
+            acc[30] += keep_rej ? ss : 0.0;
+            acc[31] += keep_rej ? 1.0 : 0.0;
+            bit <<= 1;
+        };
+        int i = tid;
+        for (; i + PB_THREADS < E; i += 2 * PB_THREADS) {
+            const EdgeIn a = load_edge(i), b = load_edge(i + PB_THREADS);
+            double ssa, za, ssb, zb;
+            edge_terms(a, q, t, f, cx, cy, p.huber, ssa, za, acc);
+            edge_terms(b, q, t, f, cx, cy, p.huber, ssb, zb, acc);
+            post(ssa, za);
+            post(ssb, zb);
         }
-        wg_sum<PB_THREADS, 28>(acc, red, sums[slot]);
+        if (i < E) {
+            double ss, z;
+            edge_terms(load_edge(i), q, t, f, cx, cy, p.huber, ss, z, acc);
+            post(ss, z);
+        }
+        big = nb;
+        front = nf;
+        PST(2);
+        wg_sum<PB_THREADS, 32>(acc, red, sums[slot]);
+        PST(3);
     };
     uint32_t iters = 0, trials = 0;
-    int cur = 0;  // sums[cur]: the linearisation at the current pose
+    int cur = 0;                // sums[cur]: the linearisation at the current pose
+    int last = 0;               // sums[last]: the last pass's sums
+    bool last_accepted = true;  // the last pass's pose is the current one
     // StepOptimizer::Step: no active vertex (no observations) -> useless, every Step fails
     for (uint32_t step = 0; E > 0 && step < p.nsteps; step++) {
         if (step == 0) {
             linearise(s_cur, cur);
+            front_cur = front;
             double m = 0;
             for (int r = 0, k = 0; r < 6; k += 6 - r, r++) m = fmax(fabs(sums[cur][k]), m);
             lambda = 1e-5 * m;  // computeLambdaInit, tau 1e-5 (fresh BundlerLib: no user lambda)
@@ -305,6 +433,7 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
                 double x[6];
                 for (int k = 0; k < 6; k++) x[k] = s_x[k];
                 ok = pose_solve(S, lambda, x);
+                PST(9);
                 double tq[4] = {s_cur[0], s_cur[1], s_cur[2], s_cur[3]}, tt[3] = {s_cur[4], s_cur[5], s_cur[6]};
                 d_oplus(tq, tt, x);
                 for (int k = 0; k < 4; k++) s_ev[k] = tq[k];
@@ -314,15 +443,19 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
                 for (int k = 0; k < 6; k++) sc += x[k] * (lambda * x[k] + S[21 + k]);
                 scale = sc + 1e-3;
             }
+            PST(4);
             have_eval = true;
             linearise(s_ev, cur ^ 1);
+            last = cur ^ 1;
             double tempChi = sums[cur ^ 1][27];
             if (!ok) tempChi = DBL_MAX;
             rho = (currentChi - tempChi) / scale;
             trials++;
             const bool accept = rho > 0 && isfinite(tempChi);
+            last_accepted = accept;
             if (accept) {
-                double alpha = 1. - pow((2 * rho - 1), 3);
+                const double r3 = 2 * rho - 1;
+                double alpha = 1. - r3 * r3 * r3;  // g2o: 1 - pow(2 rho - 1, 3)
                 alpha = fmin(alpha, 2. / 3.);
                 const double scaleFactor = fmax(1. / 3., alpha);
                 lambda *= scaleFactor;
@@ -330,41 +463,58 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
                 for (int k = 0; k < 7; k++) s_cur[k] = s_ev[k];
                 currentChi = tempChi;
                 cur ^= 1;  // the trial's normal equations are the next step's linearisation
+                front_cur = front;
             } else {
                 lambda *= ni;
                 ni *= 2;
             }
             qmax++;
+            PST(5);
         } while (rho < 0 && qmax < 10);
         iters++;
         const bool ok = !(qmax == 10 || rho == 0 || !isfinite(lambda));
         if (!ok) break;
     }
     double cur_q[4] = {s_cur[0], s_cur[1], s_cur[2], s_cur[3]}, cur_t[3] = {s_cur[4], s_cur[5], s_cur[6]};
-    double ev_q[4] = {s_ev[0], s_ev[1], s_ev[2], s_ev[3]}, ev_t[3] = {s_ev[4], s_ev[5], s_ev[6]};
-    // post-pass: errors of the last evaluated state, cheirality at the current pose
-    double qc[4] = {-cur_q[0], -cur_q[1], -cur_q[2], cur_q[3]};
-    double it[3], fwd[3];
-    d_qrot(qc, cur_t, it);
-    const double z[3] = {0, 0, 1};
-    d_qrot(qc, z, fwd);
-    double acc2[2] = {0, 0};
-    for (int i = tid; i < E; i += PB_THREADS) {
-        const EdgeIn e = load_edge(i);
-        double ev[2] = {0, 0}, rho0;
-        if (have_eval) edge_terms(e, ev_q, ev_t, f, cx, cy, p.huber, ev, rho0, nullptr);
-        const double ss = ev[0] * ev[0] + ev[1] * ev[1];
-        const double dot = (e.X[0] + it[0]) * fwd[0] + (e.X[1] + it[1]) * fwd[1] + (e.X[2] + it[2]) * fwd[2];
-        const bool out = dot <= 0 || ss > p.max_err_sq;
-        p.outlier[e0 + i] = out ? 1 : 0;
-        if (!out) {
-            acc2[0] += ss;
-            acc2[1] += 1;
+    double mean_num, mean_den;
+    if (have_eval && staged) {
+        // post-pass from the last pass's bits and sums (see above)
+        uint32_t bit = 1;
+        for (int i = tid; i < E; i += PB_THREADS, bit <<= 1)
+            p.outlier[e0 + i] = ((front_cur & bit) && !(big & bit)) ? 0 : 1;
+        mean_num = sums[last][last_accepted ? 28 : 30];
+        mean_den = sums[last][last_accepted ? 29 : 31];
+        PST(6);
+    } else {
+        // post-pass over the edges: errors of the last evaluated state (none: zero errors),
+        // cheirality at the current pose
+        double ev_q[4] = {s_ev[0], s_ev[1], s_ev[2], s_ev[3]}, ev_t[3] = {s_ev[4], s_ev[5], s_ev[6]};
+        double qc[4] = {-cur_q[0], -cur_q[1], -cur_q[2], cur_q[3]};
+        double it[3], fwd[3];
+        d_qrot(qc, cur_t, it);
+        const double zc[3] = {0, 0, 1};
+        d_qrot(qc, zc, fwd);
+        double acc2[2] = {0, 0};
+        for (int i = tid; i < E; i += PB_THREADS) {
+            const EdgeIn e = load_edge(i);
+            double ss = 0, z, unused[32] = {};
+            if (have_eval) edge_terms(e, ev_q, ev_t, f, cx, cy, p.huber, ss, z, unused);
+            const double dot = (e.X[0] + it[0]) * fwd[0] + (e.X[1] + it[1]) * fwd[1] + (e.X[2] + it[2]) * fwd[2];
+            const bool out = dot <= 0 || ss > maxe;
+            p.outlier[e0 + i] = out ? 1 : 0;
+            if (!out) {
+                acc2[0] += ss;
+                acc2[1] += 1;
+            }
         }
+        PST(6);
+        wg_sum<PB_THREADS, 2>(acc2, reinterpret_cast<double(*)[2]>(red), sums[0]);
+        mean_num = sums[0][0];
+        mean_den = sums[0][1];
     }
-    wg_sum<PB_THREADS, 2>(acc2, reinterpret_cast<double(*)[2]>(red), sums[0]);
+    PST(7);
     if (tid == 0) {
-        p.mean_sq[pr] = (float)(sums[0][0] / sums[0][1]);
+        p.mean_sq[pr] = (float)(mean_num / mean_den);
         // GetPose (BundlerLib.cpp:457-465): t as float, R of the normalised quaternion as float
         double q[4] = {cur_q[0], cur_q[1], cur_q[2], cur_q[3]};
         const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
@@ -383,6 +533,10 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
             p.stats[2 * pr + 1] = trials;
         }
     }
+#if MAGE_POSE_STAMPS
+    PST(8);
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_pose_st[255] = (unsigned long long)nst;
+#endif
 }
 
 mage_status pose_launch(const PoseParams& p, uint32_t problems, hipStream_t st)
@@ -477,5 +631,14 @@ mage_status mage_ba_pose_batch(uint32_t problems, const float* pos3, const float
     if (stats) std::memcpy(stats, h + o_st, 8 * P);
     return MAGE_OK;
 }
+
+#if MAGE_POSE_STAMPS
+// development build only (tools/pose_stamps.py): the phase stamps of the last launch's problem 0
+mage_status mage_debug_pose_stamps(unsigned long long* out)
+{
+    MAGE_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(mage::g_pose_st), sizeof(mage::g_pose_st)));
+    return MAGE_OK;
+}
+#endif
 
 }  // extern "C"
