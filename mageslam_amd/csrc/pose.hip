@@ -145,10 +145,15 @@ __device__ __forceinline__ void edge_terms(const EdgeIn& e, const double q[4], c
     const double ev0 = e.u - (xi * f + cx), ev1 = e.v - (yi * f + cy);
     ss = ev0 * ev0 + ev1 * ev1;
     const double chi2 = e.info * ss;
-    const double dsqr = huber * huber, sq = __builtin_sqrt(chi2);
-    const bool in = chi2 <= dsqr;  // RobustKernelHuber
-    acc[27] += in ? chi2 : 2 * sq * huber - dsqr;
-    const double rho1 = in ? 1.0 : huber / sq;
+    // RobustKernelHuber; 1 / sqrt(chi2) by v_rsq_f64 + two Newton steps (only the outlier side
+    // uses it: sqrt = chi2 / sqrt, rho1 = delta / sqrt) instead of an fp64 sqrt and a division
+    const double dsqr = huber * huber, hc = 0.5 * chi2;
+    double rs = __builtin_amdgcn_rsq(chi2);
+    rs *= __builtin_fma(-hc * rs, rs, 1.5);
+    rs *= __builtin_fma(-hc * rs, rs, 1.5);
+    const bool in = chi2 <= dsqr;
+    acc[27] += in ? chi2 : 2 * (chi2 * rs) * huber - dsqr;
+    const double rho1 = in ? 1.0 : huber * rs;
     double Jp[12];
     jac_pose_q(xi, yi, fi, f, Jp);
     const double w = rho1 * e.info;
@@ -172,10 +177,42 @@ __device__ __forceinline__ void edge_terms(const EdgeIn& e, const double q[4], c
     }
 }
 
+// 64-bit lane exchanges for the butterfly below (all VALU: no LDS round trip per round)
+template <int CTRL, int BANKS>
+__device__ __forceinline__ double dpp_f64(double old, double v)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v), o = __builtin_bit_cast(unsigned long long, old);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)o, (int)(unsigned)u, CTRL, 0xF, BANKS, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(o >> 32), (int)(unsigned)(u >> 32), CTRL, 0xF,
+                                                              BANKS, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// (a, b) -> lanes l < H of each 2H-lane group: a(l) + a(l ^ H); lanes with bit H: b(l ^ H) + b(l)
+// for H = 32 / 16 by v_permlane32_swap / v_permlane16_swap
+template <int H>
+__device__ __forceinline__ double xsum_swap(double a, double b)
+{
+    const unsigned long long ua = __builtin_bit_cast(unsigned long long, a), ub = __builtin_bit_cast(unsigned long long, b);
+    unsigned a0, a1, b0, b1;
+    if constexpr (H == 32) {
+        const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+        a0 = lo[0], b0 = lo[1], a1 = hi[0], b1 = hi[1];
+    } else {
+        const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+        a0 = lo[0], b0 = lo[1], a1 = hi[0], b1 = hi[1];
+    }
+    return __builtin_bit_cast(double, ((unsigned long long)a1 << 32) | a0) +
+           __builtin_bit_cast(double, ((unsigned long long)b1 << 32) | b0);
+}
+
 // fixed-order workgroup sum of acc[0..N) into out[0..N) (all threads read out afterwards).
-// N > 4: butterfly reduce-scatter inside the wave (each xor round halves the values a lane holds:
-// 16 + 8 + 4 + 2 + 1 + 1 shuffles instead of 6 per value; lane 2i ends with value i), then the
-// per-wave partials in LDS
+// N > 4: butterfly reduce-scatter inside the wave (each round halves the values a lane holds:
+// 16 + 8 + 4 + 2 + 1 + 1 exchanges instead of 6 per value; lane 2i ends with value i) on VALU
+// lane exchanges — v_permlane32_swap / v_permlane16_swap for the 32- and 16-lane rounds (the swap
+// itself pairs the kept and the sent value: no selects), DPP row_ror:8, row_shl/shr:4 by bank,
+// quad_perm for the rest — then the per-wave partials in LDS
 template <int PB_THREADS, int N>
 __device__ __forceinline__ void wg_sum(double (&acc)[N], double (*red)[N], double* out)
 {
@@ -186,16 +223,34 @@ __device__ __forceinline__ void wg_sum(double (&acc)[N], double (*red)[N], doubl
 #pragma unroll
         for (int k = 0; k < 32; k++) v[k] = k < N ? acc[k] : 0.0;
 #pragma unroll
-        for (int h = 16; h >= 1; h >>= 1) {
-            const bool up = (lane & (2 * h)) != 0;
+        for (int j = 0; j < 16; j++) v[j] = xsum_swap<32>(v[j], v[j + 16]);  // lane bit 5 -> value bit 4
 #pragma unroll
-            for (int j = 0; j < h; j++) {
-                const double send = up ? v[j] : v[j + h];
-                const double keep = up ? v[j + h] : v[j];
-                v[j] = keep + __shfl_xor(send, 2 * h);
+        for (int j = 0; j < 8; j++) v[j] = xsum_swap<16>(v[j], v[j + 8]);  // lane bit 4 -> value bit 3
+        {
+            const bool up = (lane & 8) != 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const double send = up ? v[j] : v[j + 4], keep = up ? v[j + 4] : v[j];
+                v[j] = keep + dpp_f64<0x128, 0xF>(0.0, send);  // row_ror:8 = lane ^ 8
             }
         }
-        const double s = v[0] + __shfl_xor(v[0], 1);
+        {
+            const bool up = (lane & 4) != 0;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const double send = up ? v[j] : v[j + 2], keep = up ? v[j + 2] : v[j];
+                // lane ^ 4: banks 0 / 2 read lane + 4 (row_shl:4), banks 1 / 3 lane - 4 (row_shr:4)
+                const double x = dpp_f64<0x104, 0x5>(dpp_f64<0x114, 0xA>(0.0, send), send);
+                v[j] = keep + x;
+            }
+        }
+        {
+            const bool up = (lane & 2) != 0;
+            const double send = up ? v[0] : v[1], keep = up ? v[1] : v[0];
+            v[0] = keep + dpp_f64<0x4E, 0xF>(0.0, send);  // quad_perm [2, 3, 0, 1] = lane ^ 2
+        }
+        const double s = v[0] + dpp_f64<0xB1, 0xF>(0.0, v[0]);  // quad_perm [1, 0, 3, 2] = lane ^ 1
+        // value index of lane l: bits 5, 4, 3, 2, 1 of l -> bits 4, 3, 2, 1, 0
         if (!(lane & 1) && (lane >> 1) < N) red[wave][lane >> 1] = s;
     } else {
 #pragma unroll
@@ -307,21 +362,14 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
     const uint32_t e0 = p.obs_start[pr], e1 = p.obs_start[pr + 1];
     const int E = (int)(e1 - e0);
     const double f = p.intr4[4 * pr + 2], cx = p.intr4[4 * pr], cy = p.intr4[4 * pr + 1];
-    {
-        double q[4], t[3];
-        pose_from_input(p.r9 + 9 * pr, p.pos3 + 3 * pr, q, t);
-        for (int k = 0; k < 4; k++) s_cur[k] = q[k];
-        for (int k = 0; k < 3; k++) s_cur[4 + k] = t[k];
-        for (int k = 0; k < 6; k++) s_x[k] = 0;
-    }
     // a lane's edges are observations tid + k PB_THREADS; staged (and post-pass bits) up to 32 per lane
     const bool staged = E <= POSE_STAGE && E <= 32 * PB_THREADS;
+    // every load of the lane's edges in flight before the first LDS write (a loop of load ->
+    // write pairs waited out one L2 round trip per edge), and before the initial pose
+    constexpr int KS = POSE_STAGE / PB_THREADS;
+    float4 ga[KS];
+    float2 gb[KS];
     if (staged) {
-        // every load of the lane's edges in flight before the first LDS write (a loop of
-        // load -> write pairs waited out one L2 round trip per edge)
-        constexpr int KS = POSE_STAGE / PB_THREADS;
-        float4 ga[KS];
-        float2 gb[KS];
 #pragma unroll
         for (int k = 0; k < KS; k++) {
             const int i = tid + k * PB_THREADS;
@@ -331,6 +379,15 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
                 gb[k] = make_float2(p.uv[2 * g], p.uv[2 * g + 1]);
             }
         }
+    }
+    {
+        double q[4], t[3];
+        pose_from_input(p.r9 + 9 * pr, p.pos3 + 3 * pr, q, t);
+        for (int k = 0; k < 4; k++) s_cur[k] = q[k];
+        for (int k = 0; k < 3; k++) s_cur[4 + k] = t[k];
+        for (int k = 0; k < 6; k++) s_x[k] = 0;
+    }
+    if (staged) {
 #pragma unroll
         for (int k = 0; k < KS; k++) {
             const int i = tid + k * PB_THREADS;

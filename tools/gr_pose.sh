@@ -7,4 +7,5 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/t_pose.log
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_tracking.py > gpurun_out/t_trk.log 2>&1 || { tail -30 gpurun_out/t_trk.log; exit 1; }
 tail -2 gpurun_out/t_trk.log
+timeout -k 10 300 python -u tools/track_kernels.py 240 > gpurun_out/track_kernels.json 2> gpurun_out/track_kernels.err || { tail -20 gpurun_out/track_kernels.err; exit 1; }
 echo all-done
