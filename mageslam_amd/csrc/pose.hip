@@ -118,6 +118,112 @@ __device__ void pose_from_input(const float* r9, const float* t3, double q[4], d
     for (int k = 0; k < 3; k++) t[k] = (double)t3[k];
 }
 
+// ---- the trial's exp map (SE3Quat::exp(x) * T, g2o se3quat.h; ba_math.hpp d_oplus) with the
+// square roots and divisions of its dependent chain as v_rsq_f64 + two Newton steps (~1 ulp):
+// every thread runs this chain once per trial, and its length (~130 dependent fp64 operations,
+// ~3.3k cycles with the IEEE sequences) is part of every trial's critical path.
+__device__ __forceinline__ double rsqrt_nr(double x)
+{
+    const double h = 0.5 * x;
+    double r = __builtin_amdgcn_rsq(x);
+    r *= __builtin_fma(-h * r, r, 1.5);
+    r *= __builtin_fma(-h * r, r, 1.5);
+    return r;
+}
+
+template <int I>
+__device__ __forceinline__ void quat_from_matrix_diag(const double* m, double q[4])
+{
+    constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+    const double u = m[I * 4] - m[J * 4] - m[K * 4] + 1.0, r = rsqrt_nr(u);
+    q[I] = 0.5 * (u * r);
+    const double h = 0.5 * r;
+    q[3] = (m[K * 3 + J] - m[J * 3 + K]) * h;
+    q[J] = (m[J * 3 + I] + m[I * 3 + J]) * h;
+    q[K] = (m[K * 3 + I] + m[I * 3 + K]) * h;
+}
+
+// Eigen Quaterniond(Matrix3d) (d_quat_from_matrix), static indices only
+__device__ __forceinline__ void pose_quat_from_matrix(const double* m, double q[4])
+{
+    const double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        const double u = t + 1.0, r = rsqrt_nr(u);
+        q[3] = 0.5 * (u * r);
+        const double h = 0.5 * r;
+        q[0] = (m[7] - m[5]) * h;
+        q[1] = (m[2] - m[6]) * h;
+        q[2] = (m[3] - m[1]) * h;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > (i ? m[4] : m[0])) i = 2;
+        if (i == 0)
+            quat_from_matrix_diag<0>(m, q);
+        else if (i == 1)
+            quat_from_matrix_diag<1>(m, q);
+        else
+            quat_from_matrix_diag<2>(m, q);
+    }
+}
+
+__device__ __forceinline__ void pose_normalize(double q[4])
+{
+    if (q[3] < 0)
+        for (int i = 0; i < 4; i++) q[i] = -q[i];
+    const double r = rsqrt_nr(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; i++) q[i] *= r;
+}
+
+// T <- exp(u) * T (VertexSE3Expmap::oplusImpl); the same expressions as d_oplus
+__device__ __forceinline__ void pose_oplus(double q[4], double t[3], const double u[6])
+{
+    const double w0 = u[0], w1 = u[1], w2 = u[2];
+    const double x = w0 * w0 + w1 * w1 + w2 * w2;
+    const double rs = rsqrt_nr(x), theta = x * rs;  // 1 / theta, theta
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) O2[r * 3 + c] = O[r * 3] * O[c] + O[r * 3 + 1] * O[3 + c] + O[r * 3 + 2] * O[6 + c];
+    double R[9], V[9];
+    if (x == 0 || theta < 0.00001) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
+#pragma unroll
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        double sn, cs;
+        sincos(theta, &sn, &cs);
+        const double i2 = rs * rs;
+        const double a = sn * rs, b = (1 - cs) * i2, c = (theta - sn) * (i2 * rs);
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4 == 0 ? 1.0 : 0.0);
+            R[i] = I + a * O[i] + b * O2[i];
+            V[i] = I + b * O[i] + c * O2[i];
+        }
+    }
+    double eq[4], et[3];
+    pose_quat_from_matrix(R, eq);
+#pragma unroll
+    for (int r = 0; r < 3; r++) et[r] = V[r * 3] * u[3] + V[r * 3 + 1] * u[4] + V[r * 3 + 2] * u[5];
+    pose_normalize(eq);
+    double rt[3];
+    d_qrot(eq, t, rt);
+    double nq[4];
+    nq[3] = eq[3] * q[3] - eq[0] * q[0] - eq[1] * q[1] - eq[2] * q[2];
+    nq[0] = eq[3] * q[0] + eq[0] * q[3] + eq[1] * q[2] - eq[2] * q[1];
+    nq[1] = eq[3] * q[1] + eq[1] * q[3] + eq[2] * q[0] - eq[0] * q[2];
+    nq[2] = eq[3] * q[2] + eq[2] * q[3] + eq[0] * q[1] - eq[1] * q[0];
+    pose_normalize(nq);
+#pragma unroll
+    for (int i = 0; i < 4; i++) q[i] = nq[i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) t[i] = et[i] + rt[i];
+}
+
 struct EdgeIn {
     double X[3], u, v, info;
 };
@@ -492,7 +598,7 @@ __global__ __launch_bounds__(PB_THREADS) void pose_ba_kernel(PoseParams p)
                 ok = pose_solve(S, lambda, x);
                 PST(9);
                 double tq[4] = {s_cur[0], s_cur[1], s_cur[2], s_cur[3]}, tt[3] = {s_cur[4], s_cur[5], s_cur[6]};
-                d_oplus(tq, tt, x);
+                pose_oplus(tq, tt, x);
                 for (int k = 0; k < 4; k++) s_ev[k] = tq[k];
                 for (int k = 0; k < 3; k++) s_ev[4 + k] = tt[k];
                 for (int k = 0; k < 6; k++) s_x[k] = x[k];
