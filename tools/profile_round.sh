@@ -27,9 +27,11 @@ ORB_CMD="python3 bench.py --steps 10 --warmup 3 --no-ba --no-pose --no-tracking 
 ORB31=gpurun_out/prof_${TAG}_orb31
 ORB31_CMD="python3 bench.py --steps 10 --warmup 3 --no-ba --no-pose --no-tracking --no-cpu-baseline --pipelined-streams 0 --no-all-cores --orb-variant rbrief31"
 if [ "$2" = collect ]; then
+  if [ -d $OUT/trace ]; then
     python3 tools/rocprof_summary.py $OUT $TAG "python bench.py" 3 > /dev/null
     cp $OUT/trace/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
     cp profiles/${TAG}_pmc_summary.json profiles/pmc_summary_ba.json  # BA kernels' counters (bench.py)
+  fi
     python3 tools/rocprof_summary.py $ROWS ${TAG}_rows "python tools/bench_rows.py" > /dev/null
     cp profiles/${TAG}_rows_pmc_summary.json profiles/pmc_summary_rows.json  # pose-only BA counters (bench.py)
     cp $ROWS/trace/run_kernel_stats.csv profiles/${TAG}_rows_kernel_stats.csv
@@ -54,6 +56,10 @@ fi
 PHASE=${2:-all}
 if [ "$PHASE" = all ] || [ "$PHASE" = main ]; then
     run_set $OUT python3 bench.py --steps 10 --warmup 3 --ba-iters 20 --no-cpu-baseline --pipelined-streams 0 --no-all-cores --no-tracking --no-rbrief31
+    run_set $ORB $ORB_CMD
+    run_set $ORB31 $ORB31_CMD
+fi
+if [ "$PHASE" = orb ]; then  # the ORB-only and rBRIEF-31 sets alone (when only orb.hip changed)
     run_set $ORB $ORB_CMD
     run_set $ORB31 $ORB31_CMD
 fi
