@@ -65,6 +65,8 @@ def parse():
                    help="profiling only: the variant the ORB leg runs (the headline is c2)")
     p.add_argument("--ba-many-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--profile", type=int, default=1, help="per-kernel HIP-event timing in the timed region")
+    p.add_argument("--batch-parity", type=int, default=4,
+                   help="frames of the last timed ORB batch checked against the oracle (0: off)")
     p.add_argument("--cpu-dry-run", action="store_true", help="gloo rehearsal of the multi-rank flow (tests)")
     return p.parse_args()
 
@@ -169,11 +171,15 @@ def median_of(fn, budget_s, k=5):
     return dict(runs[med], statistic=f"median of {k} samples", samples=vals, host=host_info(), build=ORACLE_BUILD[0])
 
 
-def host_threads() -> int:
+def host_threads(cap: int = 16) -> int:
     """The host cores the all-cores CPU legs use: the box's CPU share for one GPU, 16 (the GPU
     pool's rule for one-GPU boxes: worker pools sized to 16, OMP_NUM_THREADS=16), or fewer when
-    the affinity mask allows fewer.  nproc / usable cores are recorded beside it (host_info)."""
-    return max(1, min(16, len(os.sched_getaffinity(0))))
+    the affinity mask allows fewer.  nproc / usable cores are recorded beside it (host_info).
+    cap = 32 gives the second figure the legs report: one GPU's share of a 256-core 8-GPU node."""
+    return max(1, min(cap, len(os.sched_getaffinity(0))))
+
+
+NODE_SHARE_THREADS = 32  # 256 host cores / 8 GPUs
 
 
 # the oracle build the CPU legs time (bench.py switches to the -march=native + SSE2-FAST build
@@ -197,13 +203,13 @@ def _per_thread(fn, n):
         return list(ex.map(fn, range(n)))
 
 
-def cpu_orb_baseline_all(args, budget_s):
+def cpu_orb_baseline_all(args, budget_s, n=None):
     """the oracle on all host cores, frames in parallel (one detector per thread,
     each matching against its own previous frame)."""
     from mageslam_amd import synth
     from oracle import oracle as O
 
-    n = host_threads()
+    n = n or host_threads()
     s = O.default_settings(args.features)
     frames = [synth.frame(i, args.width, args.height) for i in range(n + 1)]  # not timed
 
@@ -238,6 +244,37 @@ def pyramid_level_bytes(w, h, levels, scale=1.5):
 
 
 ROOF_KERNEL = "orb.fast_nms"  # the ORB step's dominant kernel (C2 and rBRIEF-31), priced by the roofline
+
+
+def verify_orb_batch(args, batch_frames, ring, b, out, variant):
+    """Frames 1..k of the last timed batch (gated FAST, B frames per launch) against the oracle:
+    keypoints (28-byte records), descriptors and the two-way matches against frame j - 1, byte
+    for byte.  Runs after the timed region on the results the timed launches left in the ring."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    k = min(args.batch_parity, args.batch - 1)
+    N = args.features
+    s = O.default_settings(N, **(RBRIEF31_ORACLE if variant == "rbrief31" else {}))
+    fr = batch_frames[:k + 1].cpu().numpy()
+    kp = ring["kp"][b + 1:b + k + 2].cpu().numpy()
+    de = ring["desc"][b + 1:b + k + 2].cpu().numpy()
+    cn = ring["cnt"][b + 1:b + k + 2].cpu().numpy()
+    mt, nm = out["mt"][:k + 1].cpu().numpy(), out["nm"][:k + 1].cpu().numpy()
+    ores = [O.orb_detect(fr[j], s) for j in range(k + 1)]
+    kp_ok = de_ok = m_ok = True
+    for j in range(1, k + 1):
+        _, okp, od = ores[j]
+        n = int(cn[j])
+        kp_ok &= n == len(okp) and np.array_equal(kp[j, :28 * n], okp.view(np.uint8).reshape(-1))
+        de_ok &= np.array_equal(de[j, :n], od)
+        om = O.match(od, ores[j - 1][2], max_distance=30, min_difference=1)
+        m_ok &= int(nm[j]) == len(om) and np.array_equal(mt[j, :16 * int(nm[j])], om.view(np.uint8).reshape(-1))
+    return {"frames": k, "batch": args.batch, "keypoints_identical": bool(kp_ok),
+            "descriptors_identical": bool(de_ok), "matches_identical": bool(m_ok),
+            "what": f"frames 1..{k} of the last timed {args.batch}-frame batch (gated FAST) vs the CPU oracle, "
+                    f"byte for byte; matches against frame j - 1 of the same batch"}
 
 
 def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
@@ -327,6 +364,11 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
     s_last = args.warmup + args.steps - 1
     b_last = (s_last % RING) * B
     cnt, nm = ring["cnt"][b_last:b_last + B + 1], outs[s_last % NSTR]["nm"]
+    # the last timed batch itself against the oracle: its first frames'
+    # keypoints, descriptors and matches, byte for byte (test infrastructure: the check runs after
+    # the timed region on copies of the results)
+    parity = verify_orb_batch(args, frames[(s_last * B) % F:(s_last * B) % F + B], ring, b_last,
+                              outs[s_last % NSTR], variant) if rank == 0 and args.batch_parity > 0 else None
     el_max = multigpu.max_over_ranks(el, dev, dist)
     # end-of-run exchange (RCCL over xGMI): per-frame (keypoints, matches) of the last batch
     summary = torch.stack([cnt[1:].to(torch.int64), nm.to(torch.int64)], 1)
@@ -351,6 +393,8 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
         "mean_keypoints": float(torch.cat(gathered)[:, 0].float().mean().item()),
         "mean_matches": float(torch.cat(gathered)[:, 1].float().mean().item()),
     }
+    if parity is not None:
+        res["parity"] = parity
     orb_k = {k: {"launches": c, "avg_ms": ms / max(c, 1)} for k, (c, ms) in kern_timed.items()}
     if orb_k:
         dom = ROOF_KERNEL
@@ -948,28 +992,23 @@ def run_ba_many_child(local_rank):
     return fail
 
 
-def cpu_ba_baseline_all(g, budget_s):
+def cpu_ba_baseline_all(g, budget_s, n=None):
     """Independent copies of the C3 window on all host cores (one oracle BundlerLib per thread,
     the GPU leg's schedule) — the many-windows throughput of SURVEY.md §8(e)."""
     from oracle import oracle as O
 
-    class _NoSync:
-        @staticmethod
-        def sync():
-            pass
-
-    n = host_threads()
+    n = n or host_threads()
     rate, rounds, wall = lockstep_rounds([O.BundlerOracle() for _ in range(n)], g, budget_s)
     return {"value": rate, "unit": "iters/s", "cores": n, "kind": "port",
             "sample": f"{n} threads, each its own copy of the C3 window on the GPU leg's schedule, in lock-step rounds "
                       f"({rounds} rounds, {wall:.1f} s of timed steps; lockstep_rounds)", "host": host_info()}
 
 
-def cpu_ba_reference_baseline_all(g, budget_s):
+def cpu_ba_reference_baseline_all(g, budget_s, n=None):
     """The reference schedule on all host cores: one oracle window sequence per thread."""
     from oracle import oracle as O
 
-    n = host_threads()
+    n = n or host_threads()
     val, nwin, wall = concurrent_reference_windows([O.BundlerOracle() for _ in range(n)], g, budget_s,
                                                    lambda b: b.set_lambda, lambda b: b.get_lambda)
     return {"value": val, "unit": "iters/s", "cores": n, "kind": "port",
@@ -1054,7 +1093,7 @@ def main():
         import copy
 
         pa = copy.copy(args)
-        pa.streams, pa.profile = args.pipelined_streams, False
+        pa.streams, pa.profile, pa.batch_parity = args.pipelined_streams, False, 0
         pr = run_orb(pa, rank, world, local_rank, torch, dist)
         pipe_res = {"value": pr["value"], "unit": "frames/s", "ms_per_step": pr["ms_per_step"],
                     "hip_streams": pa.streams, "mean_matches": pr["mean_matches"],
@@ -1094,6 +1133,7 @@ def main():
             "kernels": orb_res["kernels"],
             "mean_keypoints": orb_res["mean_keypoints"],
             "mean_matches": orb_res["mean_matches"],
+            "parity": orb_res.get("parity"),
         }
         failed = [k for k, v in (("ba.many_windows", (ba_res or {}).get("many_windows")),) if v and v.get("status") == "failed"]
         if failed:
@@ -1109,7 +1149,8 @@ def main():
                                        "NumLevels 4, PatchSize 31, UseOrientation (OpenCVModified.cpp:833, 867-871)",
                            "frames_per_step": args.batch},
                 "roofline": r31_res.get("roofline"), "kernels": r31_res["kernels"],
-                "mean_keypoints": r31_res["mean_keypoints"], "mean_matches": r31_res["mean_matches"]}
+                "mean_keypoints": r31_res["mean_keypoints"], "mean_matches": r31_res["mean_matches"],
+                "parity": r31_res.get("parity")}
         if ba_res is not None:
             out["ba"] = ba_res
         if pose_res is not None:
@@ -1123,9 +1164,14 @@ def main():
                 c31 = median_of(lambda b: cpu_orb_baseline(args, b, RBRIEF31_ORACLE), args.cpu_sample_s / 2)
                 out["rbrief31"]["cpu_baseline"] = c31
                 out["rbrief31"]["vs_cpu"] = out["rbrief31"]["value"] / c31["value"]
+            n32 = host_threads(NODE_SHARE_THREADS)
+            share32 = not args.no_all_cores and n32 > host_threads()
             if not args.no_all_cores:
                 out["cpu_baseline_all_cores"] = cpu_orb_baseline_all(args, args.cpu_sample_s / 2)
                 out["vs_cpu_all_cores"] = out["value"] / out["cpu_baseline_all_cores"]["value"]
+            if share32:  # one GPU's share of a 256-core 8-GPU node
+                out["cpu_baseline_node_share"] = cpu_orb_baseline_all(args, args.cpu_sample_s / 2, n32)
+                out["vs_cpu_node_share"] = out["value"] / out["cpu_baseline_node_share"]["value"]
             if ba_res is not None:
                 cb = median_of(lambda b: cpu_ba_baseline(g, b), args.cpu_sample_s)
                 ba_res["cpu_baseline"] = cb
@@ -1144,6 +1190,13 @@ def main():
                     mref = (ba_res.get("many_windows") or {}).get("reference_schedule")
                     if mref:
                         mref["vs_cpu_all_cores"] = mref["value"] / rca["value"]
+                if share32:
+                    c32 = cpu_ba_baseline_all(g, args.cpu_sample_s / 2, n32)
+                    ba_res["cpu_baseline_node_share"] = c32
+                    ba_res["vs_cpu_node_share"] = ba_res["value"] / c32["value"]
+                    r32 = cpu_ba_reference_baseline_all(g, args.cpu_sample_s / 2, n32)
+                    rs["cpu_baseline_node_share"] = r32
+                    rs["vs_cpu_node_share"] = rs["value"] / r32["value"]
                 ba_res["vs_cpu"] = ba_res["value"] / cb["value"]
             if track_res is not None:
                 ct, parity = cpu_tracking_baseline(args, tctx, args.cpu_sample_s)

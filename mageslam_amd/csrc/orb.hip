@@ -294,6 +294,13 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
 //
 // gate_strip: the compass test of the thread's 4-px x 8-row strip; zeroes the strip's score
 // dwords and returns bit 8 q + r set when pixel q of score row SR * chunk + r passes.
+// MAGE_GATE_ANTIPODAL: the tighter form of the same necessary condition — a 9-arc of the 16-ring
+// holds at least one of the antipodal pixels 0 / 8 and one of 4 / 12, so "all darker" needs
+// max(min(x0, x8), min(x4, x12)) < v - G (and "all brighter" min(max(x0, x8), max(x4, x12)) > v + G):
+// two packed ops fewer per pixel pair, and never more pixels listed.
+#ifndef MAGE_GATE_ANTIPODAL
+#define MAGE_GATE_ANTIPODAL 1
+#endif
 __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], int G)
 {
     const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
@@ -322,11 +329,18 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
         for (int P = 0; P < 2; P++) {
             const h2 v = cp[r + 3][P], a = cp[r][P], b = cp[r + 6][P];
             const h2 e = pair_in(lf, 2 * P), d = pair_in(rt, 2 * P);
+#if MAGE_GATE_ANTIPODAL
+            // every 9-arc holds one of the antipodal pixels 0 / 8 (a, b) and one of 4 / 12 (d, e)
+            const h2 hi = __builtin_elementwise_minimum(__builtin_elementwise_maximum(a, b), __builtin_elementwise_maximum(d, e));
+            const h2 lo = __builtin_elementwise_maximum(__builtin_elementwise_minimum(a, b), __builtin_elementwise_minimum(d, e));
+            t2[P] = as_u32(__builtin_elementwise_maximum(hi - v, v - lo) - gp1);  // >= 0: may reach G
+#else
             const h2 pab = __builtin_elementwise_maximum(a, b), qab = __builtin_elementwise_minimum(a, b);
             const h2 pde = __builtin_elementwise_maximum(d, e), qde = __builtin_elementwise_minimum(d, e);
             const h2 x2l = max3h(__builtin_elementwise_minimum(pab, pde), qab, qde);  // second largest
             const h2 x2s = min3h(__builtin_elementwise_maximum(qab, qde), pab, pde);  // second smallest
             t2[P] = as_u32(__builtin_elementwise_maximum(x2l - v, v - x2s) - gp1);   // >= 0: may reach G
+#endif
         }
         sc[SR * chunk + r][gx] = 0u;
         // the sign bytes of pixels 0..3 (bit 7 of each byte), moved to bits 8 q + r
@@ -334,6 +348,50 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
         neg |= (sb >> (7 - r)) & (0x01010101u << r);
     }
     return ~neg;
+}
+
+#ifndef MAGE_FAST_D16
+#define MAGE_FAST_D16 1  // ring bytes of a pixel pair by byte loads + one full-rate v_bitop3 per pair
+#endif
+// LDS byte offsets of the 16 ring pixels (and the centre, entry 16) from (centre - 3 LW - 3):
+// (dy + 3) LW + dx + 3 — every offset non-negative, as the DS offset field requires.
+static_assert(LW == 136, "ring_d16's immediate offsets assume LW = 136");
+#define MAGE_RING_D16(i, j, o)                                                  \
+    "ds_read_u8 %" #i ", %34 offset:" #o "\n\t"                                 \
+    "ds_read_u8_d16_hi %" #j ", %35 offset:" #o "\n\t"
+// The 16 ring bytes and the centre of two pixels (LDS byte addresses aa / ab of their
+// centre - 3 LW - 3): ra[k] = byte_a, rb[k] = byte_b << 16 (a d16_hi load zero-fills the low
+// half on SRAM-ECC parts such as MI355X).  One asm block with its own lgkmcnt(0): the compiler's
+// wait insertion does not see asm loads.
+__device__ __forceinline__ void ring_d16(uint32_t aa, uint32_t ab, uint32_t (&ra)[17], uint32_t (&rb)[17])
+{
+    asm volatile(MAGE_RING_D16(0, 17, 819) MAGE_RING_D16(1, 18, 820) MAGE_RING_D16(2, 19, 685)
+                 MAGE_RING_D16(3, 20, 550) MAGE_RING_D16(4, 21, 414) MAGE_RING_D16(5, 22, 278)
+                 MAGE_RING_D16(6, 23, 141) MAGE_RING_D16(7, 24, 4) MAGE_RING_D16(8, 25, 3)
+                 MAGE_RING_D16(9, 26, 2) MAGE_RING_D16(10, 27, 137) MAGE_RING_D16(11, 28, 272)
+                 MAGE_RING_D16(12, 29, 408) MAGE_RING_D16(13, 30, 544) MAGE_RING_D16(14, 31, 681)
+                 MAGE_RING_D16(15, 32, 818) MAGE_RING_D16(16, 33, 411)
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(ra[0]), "=&v"(ra[1]), "=&v"(ra[2]), "=&v"(ra[3]), "=&v"(ra[4]), "=&v"(ra[5]),
+                   "=&v"(ra[6]), "=&v"(ra[7]), "=&v"(ra[8]), "=&v"(ra[9]), "=&v"(ra[10]), "=&v"(ra[11]),
+                   "=&v"(ra[12]), "=&v"(ra[13]), "=&v"(ra[14]), "=&v"(ra[15]), "=&v"(ra[16]),
+                   "=&v"(rb[0]), "=&v"(rb[1]), "=&v"(rb[2]), "=&v"(rb[3]), "=&v"(rb[4]), "=&v"(rb[5]),
+                   "=&v"(rb[6]), "=&v"(rb[7]), "=&v"(rb[8]), "=&v"(rb[9]), "=&v"(rb[10]), "=&v"(rb[11]),
+                   "=&v"(rb[12]), "=&v"(rb[13]), "=&v"(rb[14]), "=&v"(rb[15]), "=&v"(rb[16])
+                 : "v"(aa), "v"(ab)
+                 : "memory");
+}
+#undef MAGE_RING_D16
+__host__ __device__ constexpr int ring_off(int k) { return (ring_dy(k) + 3) * LW + ring_dx(k) + 3; }
+static_assert(ring_off(0) == 819 && ring_off(1) == 820 && ring_off(2) == 685 && ring_off(3) == 550 &&
+              ring_off(4) == 414 && ring_off(5) == 278 && ring_off(6) == 141 && ring_off(7) == 4 &&
+              ring_off(8) == 3 && ring_off(9) == 2 && ring_off(10) == 137 && ring_off(11) == 272 &&
+              ring_off(12) == 408 && ring_off(13) == 544 && ring_off(14) == 681 && ring_off(15) == 818 &&
+              3 * LW + 3 == 411, "ring_d16 offsets");
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
 // Exact scores of two listed pixels (score row << 7 | score column) at once, one per f16 lane,
@@ -345,14 +403,23 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
     // LDS centre of score pixel (sr, x): image row sr + 3, column x + 4
     const uint8_t* ca = &img[(ia >> 7) + 3][(ia & 127u) + 4];
     const uint8_t* cb = &img[(ib >> 7) + 3][(ib & 127u) + 4];
-    auto pack = [](uint32_t a, uint32_t b) { return as_h2((a | (b << 16)) | 0x64006400u); };
     h2 x[16];
+#if MAGE_FAST_D16
+    uint32_t ra[17], rb[17];
+    ring_d16(lds_addr(ca - 3 * LW - 3), lds_addr(cb - 3 * LW - 3), ra, rb);
+    // [byte_a, 0x64, byte_b, 0x64]: 1024 + byte in both f16 lanes, one full-rate op per pair
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = as_h2(__builtin_amdgcn_bitop3_b32(ra[k], rb[k], 0x64006400u, 0xFE));
+    const h2 v = as_h2(__builtin_amdgcn_bitop3_b32(ra[16], rb[16], 0x64006400u, 0xFE));
+#else
+    auto pack = [](uint32_t a, uint32_t b) { return as_h2((a | (b << 16)) | 0x64006400u); };
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const int off = ring_dy(k) * LW + ring_dx(k);
         x[k] = pack(ca[off], cb[off]);
     }
     const h2 v = pack(ca[0], cb[0]);
+#endif
     const uint32_t sv = score2(fast_raw_ring(v, x), tf);
     const int X0 = blockIdx.x * TW - 4, Y0 = blockIdx.y * TH - 1;
     auto inside = [&](uint32_t it) {
@@ -390,6 +457,21 @@ __device__ __forceinline__ long long brick_offset(int y, int x, int bcols)
     return ((long long)(y >> 2) * bcols + (x >> 5)) * 128 + (y & 3) * 32 + (x & 31);
 }
 
+// The tile is biased in place before the blur (xor_tile: every byte b becomes b ^ 0x80, the
+// signed i8 b - 128), after the FAST passes have read it.
+__device__ __forceinline__ void xor_tile(uint8_t (*img)[LW])
+{
+    uint2* q = reinterpret_cast<uint2*>(&img[0][0]);
+    constexpr int NQ = LH * LW / 8;
+    static_assert(LH * LW % 8 == 0, "qword tile");
+    for (int i = threadIdx.x; i < NQ; i += FAST_THREADS) {
+        uint2 v = q[i];
+        v.x ^= 0x80808080u;
+        v.y ^= 0x80808080u;
+        q[i] = v;
+    }
+}
+
 __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastParams& p, int f)
 {
     typedef int v4i __attribute__((ext_vector_type(4)));
@@ -400,9 +482,23 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
     const uint4 o0 = p.blur_ops[3 * lane], o1 = p.blur_ops[3 * lane + 1], o2 = p.blur_ops[3 * lane + 2];
     const v4i tb = {(int)o0.x, (int)o0.y, (int)o0.z, (int)o0.w};
     const v4i ta[2] = {{(int)o1.x, (int)o1.y, (int)o1.z, (int)o1.w}, {(int)o2.x, (int)o2.y, (int)o2.z, (int)o2.w}};
-    const v4i c_row = {32896, 32896, 32896, 32896};                      // 128 * 257
-    const v4i c_hi = c_row, c_lo = {65664, 65664, 65664, 65664};         // + 2^15
-    for (int s = wave; s < BLUR_STRIPS; s += FAST_THREADS / kWave) {
+    // row pass: H' = sum tap (b - 128) + 128 = H - 32768 in [-32768, 32767] (the tile holds
+    // b ^ 0x80), so the high byte of H' is its signed i8 digit and only the low byte needs the
+    // 0x80 bias.  Column pass with C = 0: the constants ride in each lane's spare K slots 12..15
+    // (A dword 3 x B dword 3 = {-128, a1} . {-64, 1}, four K groups): hi 4 (8192 + 64) = 33024,
+    // lo 4 (8192 + 32) = 32896, so that 256 Yh + Yl = sum tc H' + 257 * 2^15 + 2^15 = Y + 2^15.
+    const v4i c_row = {128, 128, 128, 128};
+    const v4i c_zero = {0, 0, 0, 0};
+    // lane: output row 16 o + n, tile columns 16 s + 4 g .. + 3 (rows >= TH, columns >= TW
+    // and columns past the blurred frame's stride are not stored); the BLUR_BRICK offset of
+    // (Y, X) advances by one brick (128 B) per two strips and by 4 brick rows per output block
+    const int ylim = min(TH, p.h - (int)blockIdx.y * TH);
+    uint8_t* fb = p.blur + (long long)f * p.blur_pitch;
+    const int Y0 = (int)blockIdx.y * TH + n, X0 = (int)blockIdx.x * TW + 16 * wave + 4 * g;
+    uint32_t off = (uint32_t)((((Y0 >> 2) * p.blur_bcols + (X0 >> 5)) << 7) + ((Y0 & 3) << 5) + (X0 & 31));
+    const uint32_t ostep = (uint32_t)p.blur_bcols << 9;
+    const bool yok[2] = {n < ylim, 16 + n < ylim};
+    for (int s = wave; s < BLUR_STRIPS; s += FAST_THREADS / kWave, off += 128u) {
         // H block b: H rows 16 b - 3 + m (tile coordinates) = LDS rows 16 b + 1 + m; the window
         // is LDS columns 16 s .. + 63 (tile columns 16 s - 8 ..), of which lanes g < 2 load the
         // 32 bytes the band reaches; clamped reads only feed discarded outputs
@@ -414,28 +510,24 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
             const int c0 = min(16 * s + 16 * g, LW - 8), c1 = min(16 * s + 16 * g + 8, LW - 8);
             const uint2 d0 = *reinterpret_cast<const uint2*>(&img[row][c0]);
             const uint2 d1 = *reinterpret_cast<const uint2*>(&img[row][c1]);
-            const v4i a = {(int)(d0.x ^ 0x80808080u), (int)(d0.y ^ 0x80808080u), (int)(d1.x ^ 0x80808080u),
-                           (int)(d1.y ^ 0x80808080u)};
+            const v4i a = {(int)d0.x, (int)d0.y, (int)d1.x, (int)d1.y};
             H[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, tb, c_row, 0, 0, 0);
         }
-        // bytes of H (<= 65535): per block one dword of lo bytes and one of hi bytes (^ 0x80)
-        v4i lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
+        // bytes of H': per block one dword of lo bytes (^ 0x80) and one of signed hi bytes
+        v4i lo = {0, 0, 0, 0x00002080}, hi = {0, 0, 0, 0x00004080};
 #pragma unroll
         for (int b = 0; b < 3; b++) {
             const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)H[b][1], (uint32_t)H[b][0], 0x05010400u);  // lo0 lo1 hi0 hi1
             const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)H[b][3], (uint32_t)H[b][2], 0x05010400u);
             lo[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u);
-            hi[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x07060302u) ^ 0x80808080u);
+            hi[b] = (int)__builtin_amdgcn_perm(p23, p01, 0x07060302u);
         }
-        // lane: output row 16 o + n, tile columns 16 s + 4 g .. + 3 (rows >= TH, columns >= TW
-        // and columns past the blurred frame's stride are not stored)
         const int x = 16 * s + 4 * g, X = (int)blockIdx.x * TW + x;
-        const int ylim = min(TH, p.h - (int)blockIdx.y * TH);
-        uint8_t* fb = p.blur + (long long)f * p.blur_pitch;
+        const bool xok = x < TW && X < p.blur_stride;
 #pragma unroll
         for (int o = 0; o < 2; o++) {
-            const v4i yh = __builtin_amdgcn_mfma_i32_16x16x64_i8(hi, ta[o], c_hi, 0, 0, 0);
-            const v4i yl = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo, ta[o], c_lo, 0, 0, 0);
+            const v4i yh = __builtin_amdgcn_mfma_i32_16x16x64_i8(hi, ta[o], c_zero, 0, 0, 0);
+            const v4i yl = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo, ta[o], c_zero, 0, 0, 0);
             // out_r = min(255, t_r >> 16), t_r = (yh << 8) + yl: the high halves of two t's as u16
             // lanes (one v_perm), saturated two at a time (v_pk_min_u16), then their low bytes
             typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -448,10 +540,7 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
             const uint32_t h23 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(
                 __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(t[3], t[2], 0x07060302u)), cap));
             const uint32_t w = __builtin_amdgcn_perm(h23, h01, 0x06040200u);
-            if (16 * o + n < ylim && x < TW && X < p.blur_stride) {
-                const int Y = (int)blockIdx.y * TH + 16 * o + n;
-                *reinterpret_cast<uint32_t*>(fb + brick_offset(Y, X, p.blur_bcols)) = w;
-            }
+            if (yok[o] && xok) *reinterpret_cast<uint32_t*>(fb + (off + (o ? ostep : 0u))) = w;
         }
     }
 }
@@ -549,6 +638,8 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
         }
     }
     __syncthreads();
+    // the FAST passes are done with the image: bias it for the blur's i8 MFMA operands
+    if (kBlur && blur) xor_tile(img);
     // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter, four
     // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8).  Scores
     // are split into even / odd pixels as f16 lanes (1024 + s); per score row the left / right
@@ -666,8 +757,11 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
             }
         }
     }
-    // the blur reads only the image tile and writes the frame directly: no barrier before it
-    if (kBlur && blur) blur_mfma(img, p, f);
+    // the blur reads only the (biased) image tile and writes the frame directly
+    if (kBlur && blur) {
+        __syncthreads();  // xor_tile is complete
+        blur_mfma(img, p, f);
+    }
     __syncthreads();  // s_cnt and the tile's list are final
     if (kSink || !kEmit) {  // ablation: keep the skipped stages' inputs alive
         if (kSink) {
@@ -2112,11 +2206,15 @@ void blur_operands(const int* taps, uint32_t out[64 * 12])
             for (int e = 0; e < 4; e++) w |= tap(16 * g + 4 * d + e - n - 5) << (8 * e);
             o[d] = w;
         }
+        // dword 3 (K slots 12..15 of the lane's group): {-64, 1, 0, 0}, the partner of the
+        // bias bytes blur_mfma keeps in the A operands' dword 3 (an A dword 3 of 0 adds nothing)
         for (int ob = 0; ob < 2; ob++)
             for (int b = 0; b < 4; b++) {
                 uint32_t w = 0;
                 if (b < 3)
                     for (int r = 0; r < 4; r++) w |= tap(16 * (b - ob) + 4 * g + r - n) << (8 * r);
+                else
+                    w = 0x000001C0u;
                 o[4 + 4 * ob + b] = w;
             }
     }

@@ -170,6 +170,12 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
         MAGE_REQUIRE(frame_start[f + 1] >= frame_start[f], MAGE_EINVAL, "frame_start must be non-decreasing");
     MAGE_REQUIRE(frame_start[frames] == 0 || (kp && desc), MAGE_EINVAL, "null features");
     MAGE_REQUIRE(!s->local_ba, MAGE_EUNSUPPORTED, "the local BA runs in the device loop (mage_track_sequence_device)");
+    // observation information = MapPointRefinementConfidence(refinement count) (TrackLocalMap.cpp:
+    // 473-475); this loop's map points are never refined (count 0), the device loop's are
+    const float kInfo0 = 1.f - 1.f / (1.5f * 1.5f);
+    MAGE_REQUIRE(s->refinement_info == kInfo0, MAGE_EINVAL,
+                 "refinement_info must be MapPointRefinementConfidence(0) = 1 - 1/1.5^2 (the per-point "
+                 "confidences follow the refinement counts)");
     MAGE_HIP(hipSetDevice(device));
     const float fx = (float)K[0], fy = (float)K[1], cx = (float)K[2], cy = (float)K[3];
     auto frame_kp = [&](uint32_t f) { return kp + frame_start[f]; };
@@ -276,7 +282,7 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
             uv[2 * k + 1] = fk[t].y;
         }
         Pose p1, p2;
-        st = optimize(pred, K, pts, uv, s->refinement_info, s->initial_steps, s->initial_huber,
+        st = optimize(pred, K, pts, uv, kInfo0, s->initial_steps, s->initial_huber,
                       (float)(s->initial_max_error * s->initial_max_error), device, p1, out1);
         if (st != MAGE_OK) return st;
         pts2.clear();
@@ -355,7 +361,7 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
                     }
             }
         }
-        st = optimize(p1, K, pts2, uv2, s->refinement_info, s->final_steps, s->final_huber,
+        st = optimize(p1, K, pts2, uv2, kInfo0, s->final_steps, s->final_huber,
                       (float)(s->final_max_error * s->final_max_error), device, p2, out2);
         if (st != MAGE_OK) return st;
         uint32_t n_in = 0;

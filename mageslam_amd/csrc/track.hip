@@ -30,6 +30,9 @@ namespace mage {
 namespace {
 
 constexpr int TT = 1024;  // threads of the per-frame control kernels
+// RadiusMatch band-index ring of mage_track_sequence_device: chunks of BAND_CHUNK frames, two
+// chunks resident (the host runs at most a few frames ahead of the device)
+constexpr uint32_t BAND_CHUNK = 16, BAND_SLOTS = 2 * BAND_CHUNK;
 
 struct DPose {
     double R[9];  // world -> camera, row-major
@@ -881,6 +884,10 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     MAGE_REQUIRE(pitch > 0 && pitch <= 4096, MAGE_EINVAL, "frame pitch must be in [1, 4096] keypoints");
     hipStream_t st = (hipStream_t)stream;
     MAGE_REQUIRE(s->local_map_keyframes <= (uint32_t)NKMAX, MAGE_EINVAL, "local_map_keyframes must be <= 8");
+    // the observations' information is MapPointRefinementConfidence of each point's refinement
+    // count (TrackLocalMap.cpp:473-475); the setting only names its count-0 value
+    MAGE_REQUIRE(s->refinement_info == refinement_confidence(0), MAGE_EINVAL,
+                 "refinement_info must be MapPointRefinementConfidence(0) = 1 - 1/1.5^2");
     const size_t cap = pitch;
     const uint32_t NK = std::max(s->local_map_keyframes, 1u);
     const size_t qcap = s->local_map_keyframes > 0 ? (size_t)NK * cap : 0;  // local-map queries
@@ -909,8 +916,8 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
                  o_lqo = take(4 * qcap), o_lqh = take(4 * qcap), o_lqd = take(32 * qcap), o_lqt = take(12 * qcap),
                  o_lres = take(4 * qcap), o_lst = take(4), o_lscr = take(local_map_scratch_bytes((uint32_t)qcap)),
                  o_poses = take(96ull * frames), o_mt = take(4ull * frames), o_il = take(4ull * frames),
-                 o_kf = take(frames), o_bk = take(8ull * pitch * frames), o_bxy = take(8ull * pitch * frames),
-                 o_bd = take(32ull * pitch * frames);
+                 o_kf = take(frames), o_bk = take(8ull * pitch * BAND_SLOTS), o_bxy = take(8ull * pitch * BAND_SLOTS),
+                 o_bd = take(32ull * pitch * BAND_SLOTS);
     DeviceBuffer buf;
     mage_status r = buf.reserve(off);
     if (r != MAGE_OK) return r;
@@ -975,7 +982,10 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
     uint32_t* dmt = reinterpret_cast<uint32_t*>(d + o_mt);
     uint32_t* dil = reinterpret_cast<uint32_t*>(d + o_il);
     uint8_t* dkf = reinterpret_cast<uint8_t*>(d + o_kf);
-    // every frame's RadiusMatch band index, built once (the tracker matches each frame up to 3 times)
+    // RadiusMatch band indices (each frame is matched up to 3 times, so its index is built once):
+    // a ring of BAND_SLOTS frames, built BAND_CHUNK frames at a time by the enqueue of a chunk's
+    // first frame — the loop runs at most DEPTH frames ahead, so a chunk's slots are free again
+    // when the chunk two ahead is built, and device memory does not grow with the sequence
     unsigned long long* bkeys = reinterpret_cast<unsigned long long*>(d + o_bk);
     float* bxy = reinterpret_cast<float*>(d + o_bxy);
     uint32_t* bdesc = reinterpret_cast<uint32_t*>(d + o_bd);
@@ -1009,19 +1019,24 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         hipMemcpyAsync(dposes, first_pose, 96, hipMemcpyHostToDevice, st) != hipSuccess)
         return fail(MAGE_EDEVICE);
     hipLaunchKernelGGL(trk_init, dim3(1), dim3(TT), 0, st, b, c, d_kp, d_desc, d_n, dposes, dmt, dil, dkf, rstatus);
-    if ((r = radius_band_index_launch(d_kp, d_desc, d_n, (int64_t)pitch, frames, bkeys, bxy, bdesc, st)) != MAGE_OK)
-        return fail(r);
     const float radius[3] = {s->search_radius, s->wider_search_radius, s->extra_wider_search_radius};
     auto enqueue = [&](uint32_t f) -> mage_status {
         const mage_keypoint* fk = d_kp + (size_t)f * pitch;
         const uint8_t* fd = d_desc + 32ull * f * pitch;
         const uint32_t* nf = d_n + f;
+        const size_t slot = (size_t)(f % BAND_SLOTS);
         mage_status rr;
+        if (f == 1 || f % BAND_CHUNK == 0) {  // build the band indices of frames [f, next chunk)
+            const uint32_t end = std::min(frames, (f / BAND_CHUNK + 1) * BAND_CHUNK);
+            if ((rr = radius_band_index_launch(fk, fd, nf, (int64_t)pitch, end - f, bkeys + slot * pitch,
+                                               bxy + 2 * slot * pitch, bdesc + 8 * slot * pitch, st)) != MAGE_OK)
+                return rr;
+        }
         launch("track.project", trk_project, dim3(1), dim3(TT), 0, st, b, c, (int)f, (const double*)dposes);
         for (int k = 0; k < 3; k++) {
             rr = radius_match_indexed(b.qkp, k < 2 ? b.qpos : nullptr, b.qdesc, (int64_t)pitch, b.nq + k, fk, fd,
-                                      (int64_t)pitch, nf, bkeys + (size_t)f * pitch, bxy + 2ull * f * pitch,
-                                      bdesc + 8ull * f * pitch, 1, radius[k], s->max_hamming, s->min_hamming_difference,
+                                      (int64_t)pitch, nf, bkeys + slot * pitch, bxy + 2 * slot * pitch,
+                                      bdesc + 8 * slot * pitch, 1, radius[k], s->max_hamming, s->min_hamming_difference,
                                       rscratch, b.m + (size_t)k * pitch, pitch, b.mn + k, rstatus, st);
             if (rr != MAGE_OK) return rr;
             if (k < 2) launch("track.weak", trk_weak, dim3(1), dim3(64), 0, st, b, c, k);
@@ -1050,7 +1065,7 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
             la.min_diff = s->local_min_hamming_difference;
             la.result = b.lm_res;
             la.status = b.lm_status;
-            la.keys = bkeys + (size_t)f * pitch;
+            la.keys = bkeys + slot * pitch;
             if ((rr = local_map_match_launch(la, b.lm_scratch, st)) != MAGE_OK) return rr;
             launch("track.lm_assemble", trk_lm_assemble, dim3(1), dim3(TT), 0, st, b, fk);
         }

@@ -73,6 +73,12 @@ class TrackerSettings:
     min_lambda: float = 1e-3               # MappingSettings::MinLambda (PersistLambda on)
     ba_free_keyframes: int = 2             # the newest keyframes of the window move, the older ones are fixed
 
+    def __post_init__(self):
+        # every loop takes an observation's information from MapPointRefinementConfidence of its
+        # point's refinement count (TrackLocalMap.cpp:473-475); this field only names the count-0 value
+        if np.float32(self.refinement_info) != refinement_confidence(0):
+            raise ValueError("refinement_info must be MapPointRefinementConfidence(0) = 1 - 1/1.5^2")
+
     def min_view_cos(self) -> np.float32:
         """std::cos(mira::deg2rad(degrees)) in float (arcana/math.h:86-90: degrees * (PI / 180))."""
         return _libm_f("cosf", np.float32(self.min_view_degrees) * (np.float32(np.pi) / np.float32(180)))

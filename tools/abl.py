@@ -27,12 +27,21 @@ def build(src, specs):
     objs = [p for p in B.OBJ.glob("*.o") if p.name != stem + ".o"]
     for spec in specs:
         name, _, defs = spec.partition(":")
+        # name@REV: the source as committed at git revision REV (a same-box baseline)
+        name, _, rev = name.partition("@")
         out = ROOT / "abl" / name
         out.mkdir(parents=True, exist_ok=True)
         obj = out / (stem + ".o")
         flags = [f"-D{d}" for d in defs.split("+") if d]
+        src_path = B.CSRC / stem
+        if rev:
+            src_path = B.CSRC / f".abl_{name}_{stem}"
+            src_path.write_bytes(subprocess.run(["git", "show", f"{rev}:mageslam_amd/csrc/{stem}"], cwd=ROOT,
+                                                check=True, capture_output=True).stdout)
         subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON, *flags,
-                        "-c", str(B.CSRC / stem), "-o", str(obj)], check=True)
+                        "-c", str(src_path), "-o", str(obj)], check=True)
+        if rev:
+            src_path.unlink()
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
                         str(obj), *map(str, objs)], check=True)
         print("built", out, flags, flush=True)
