@@ -53,6 +53,7 @@ struct FastParams {
     int xlo, xhi, ylo, yhi;  // emission window (FAST range ∩ RunByImageBorder)
     unsigned cand_cap;  // per frame: tiles x TCAP
     int tiles;          // tiles per frame (per-tile candidate counts)
+    int tiles_x;        // tile columns per frame
     int dword_ok;  // frames 4-byte aligned with width, stride and pitch multiples of 4
     int qword_ok;  // frames 8-byte aligned, stride and pitch multiples of 8 (interior tiles)
     // fused 7-tap Gaussian (8U fixed point) of the tile into `blur` (null: no blur)
@@ -66,6 +67,10 @@ struct FastParams {
     const int* gate;
     int* gate_next;
     uint32_t* redo;  // [count, frame...]: frames select_kernel sends back through the exact path
+};
+
+struct Tile {
+    int x, y;  // tile column / row in the frame
 };
 
 #ifndef MAGE_FAST_SCHED
@@ -191,9 +196,9 @@ __device__ __forceinline__ int reflect101(int i, int n)
 // the row pitch and the width are multiples of 4, dwords wholly inside the frame are moved with
 // 4-byte loads.
 __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const FastParams& p,
-                                          uint8_t (*img)[LW])
+                                          uint8_t (*img)[LW], Tile T)
 {
-    const int gx0 = blockIdx.x * TW - 8, gy0 = blockIdx.y * TH - 4;
+    const int gx0 = T.x * TW - 8, gy0 = T.y * TH - 4;
     if (p.qword_ok && gx0 >= 0 && gx0 + LW <= p.w && gy0 >= 0 && gy0 + LH <= p.h) {
         // interior tile (most of them): 8-byte loads, no reflection, addresses by increment
         constexpr int QW = LW / 8, RSTEP = FAST_THREADS / QW;  // 17 qwords per row, 7 rows per pass
@@ -227,11 +232,11 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const
 // Scores of the thread's strip: group gx (4 columns), score rows [SR * chunk, SR * chunk + SR),
 // written as one dword per row into sc.  Pixels outside the FAST range [3, w-4] x [3, h-4]
 // score 0.
-__device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], const FastParams& p)
+__device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], const FastParams& p, Tile T)
 {
     const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
-    const int X0 = blockIdx.x * TW - 4 + 4 * gx;     // image column of the group's first pixel
-    const int Y0 = blockIdx.y * TH - 1 + SR * chunk;  // image row of the strip's first score row
+    const int X0 = T.x * TW - 4 + 4 * gx;     // image column of the group's first pixel
+    const int Y0 = T.y * TH - 1 + SR * chunk;  // image row of the strip's first score row
     uint32_t colmask = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++)
@@ -398,7 +403,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p)
 // with threshold tf; pixels outside the FAST range [3, w-4] x [3, h-4] score 0.  Returns the two
 // score bytes (a in bits 0-7, b in bits 16-23).
 __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8_t* scb, const FastParams& p,
-                                             uint32_t ia, uint32_t ib, h2 tf)
+                                             uint32_t ia, uint32_t ib, h2 tf, Tile T)
 {
     // LDS centre of score pixel (sr, x): image row sr + 3, column x + 4
     const uint8_t* ca = &img[(ia >> 7) + 3][(ia & 127u) + 4];
@@ -421,7 +426,7 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
     const h2 v = pack(ca[0], cb[0]);
 #endif
     const uint32_t sv = score2(fast_raw_ring(v, x), tf);
-    const int X0 = blockIdx.x * TW - 4, Y0 = blockIdx.y * TH - 1;
+    const int X0 = T.x * TW - 4, Y0 = T.y * TH - 1;
     auto inside = [&](uint32_t it) {
         const int X = X0 + (int)(it & 127u), Y = Y0 + (int)(it >> 7);
         return X >= 3 && X <= p.w - 4 && Y >= 3 && Y <= p.h - 4;
@@ -472,7 +477,7 @@ __device__ __forceinline__ void xor_tile(uint8_t (*img)[LW])
     }
 }
 
-__device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastParams& p, int f)
+__device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastParams& p, int f, Tile T)
 {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -492,9 +497,9 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
     // lane: output row 16 o + n, tile columns 16 s + 4 g .. + 3 (rows >= TH, columns >= TW
     // and columns past the blurred frame's stride are not stored); the BLUR_BRICK offset of
     // (Y, X) advances by one brick (128 B) per two strips and by 4 brick rows per output block
-    const int ylim = min(TH, p.h - (int)blockIdx.y * TH);
+    const int ylim = min(TH, p.h - T.y * TH);
     uint8_t* fb = p.blur + (long long)f * p.blur_pitch;
-    const int Y0 = (int)blockIdx.y * TH + n, X0 = (int)blockIdx.x * TW + 16 * wave + 4 * g;
+    const int Y0 = T.y * TH + n, X0 = T.x * TW + 16 * wave + 4 * g;
     uint32_t off = (uint32_t)((((Y0 >> 2) * p.blur_bcols + (X0 >> 5)) << 7) + ((Y0 & 3) << 5) + (X0 & 31));
     const uint32_t ostep = (uint32_t)p.blur_bcols << 9;
     const bool yok[2] = {n < ylim, 16 + n < ylim};
@@ -522,7 +527,7 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
             lo[b] = (int)(__builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u);
             hi[b] = (int)__builtin_amdgcn_perm(p23, p01, 0x07060302u);
         }
-        const int x = 16 * s + 4 * g, X = (int)blockIdx.x * TW + x;
+        const int x = 16 * s + 4 * g, X = T.x * TW + x;
         const bool xok = x < TW && X < p.blur_stride;
 #pragma unroll
         for (int o = 0; o < 2; o++) {
@@ -548,11 +553,25 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
 #ifndef MAGE_FAST_WAVES_PER_EU
 #define MAGE_FAST_WAVES_PER_EU 5  // 86 VGPRs, no spills (tools/ablate_fast.py)
 #endif
+#ifndef MAGE_FAST_STAMPS
+#define MAGE_FAST_STAMPS 0  // tools/fast_stamps.py: per-phase s_memtime of each wave of frames 0..14
+#endif
+#if MAGE_FAST_STAMPS
+__device__ unsigned long long g_fast_stamps[4096][2][16];
+#define FAST_STAMP(k)                                                                                   \
+    if ((threadIdx.x & 63) == 0 && f < 15) {                                                           \
+        const int t_ = f * p.tiles + T.y * p.tiles_x + T.x;              \
+        if (t_ < 4096) g_fast_stamps[t_][threadIdx.x >> 6][k] = __builtin_amdgcn_s_memtime();           \
+    }
+#else
+#define FAST_STAMP(k)
+#endif
 // One tile of frame f: load, score (gated when G > threshold, see gate_strip), NMS, emission,
 // and the fused blur when `blur`.
 template <bool kMayGate>
 __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, const FastParams& p, int f, int G,
-                                          bool blur, uint32_t* __restrict__ cand, uint32_t* __restrict__ counts)
+                                          bool blur, uint32_t* __restrict__ cand, uint32_t* __restrict__ counts,
+                                          Tile T)
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
     __shared__ uint32_t sc[SROWS][GX];  // scores; then the blurred tile
@@ -570,9 +589,11 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
     constexpr bool kScore = !(MAGE_FAST_ABLATE & 4), kLoad = !(MAGE_FAST_ABLATE & 8);
     constexpr bool kEmit = !(MAGE_FAST_ABLATE & 16), kSink = (MAGE_FAST_ABLATE & 32) != 0;
     uint32_t s_sink_acc = 0;
-    if (kLoad) load_tile(frames + (long long)f * p.pitch, p, img);
+    FAST_STAMP(0);
+    if (kLoad) load_tile(frames + (long long)f * p.pitch, p, img, T);
     if (threadIdx.x == 0) s_cnt = s_dense = 0;
     __syncthreads();
+    FAST_STAMP(1);
     const bool gated = kMayGate && kScore && G > p.threshold;
     uint32_t total = 0;  // gated: the wave's listed pixels
     if (kScore) {
@@ -580,6 +601,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
             // gated: compass test per strip, then the wave's passing groups scored exactly,
             // compacted over the wave's lanes
             const uint32_t pix = gate_strip(img, sc, G);
+            FAST_STAMP(2);
             const uint32_t cnt = __builtin_popcount(pix);
             uint32_t pre = 0;
 #pragma unroll
@@ -600,9 +622,11 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                     wl[pre++] = (uint16_t)(((SR * chunk + (b & 7)) << 7) | (4 * gx + (b >> 3)));
                 }
             }
+            FAST_STAMP(3);
             __syncthreads();  // s_dense is final
+            FAST_STAMP(4);
             if (s_dense) {
-                score_strip(img, sc, p);
+                score_strip(img, sc, p, T);
             } else if (!(MAGE_FAST_ABLATE & 64)) {
                 // the wave's listed pixels, two per lane; the ones that reach G (the only
                 // possible maxima) are compacted in place to the front of the list for the NMS
@@ -618,7 +642,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                     if (i < total) {
                         ia = wl[i];
                         ib = i + 1 < total ? wl[i + 1] : ia;
-                        const uint32_t ss = score_pixels(img, scb, p, ia, ib, tg);
+                        const uint32_t ss = score_pixels(img, scb, p, ia, ib, tg, T);
                         fa = (ss & 0xFFu) != 0;
                         fb = i + 1 < total && (ss >> 16) != 0;
                     }
@@ -632,14 +656,17 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                     nz += (uint32_t)(__builtin_popcountll(ba) + __builtin_popcountll(bb));
                 }
                 total = nz;
+                FAST_STAMP(5);
             }
         } else {
-            score_strip(img, sc, p);
+            score_strip(img, sc, p, T);
         }
     }
     __syncthreads();
     // the FAST passes are done with the image: bias it for the blur's i8 MFMA operands
+    FAST_STAMP(6);
     if (kBlur && blur) xor_tile(img);
+    FAST_STAMP(7);
     // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter, four
     // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8).  Scores
     // are split into even / odd pixels as f16 lanes (1024 + s); per score row the left / right
@@ -658,7 +685,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
             if (i < total) {
                 const uint32_t it = wl[i];
                 const int sr = (int)(it >> 7), x = (int)(it & 127u);
-                const int X = blockIdx.x * TW + x - 4, Y = blockIdx.y * TH + sr - 1;
+                const int X = T.x * TW + x - 4, Y = T.y * TH + sr - 1;
                 if (sr >= 1 && sr <= TH && x >= 4 && x < TW + 4 && X >= p.xlo && X <= p.xhi && Y >= p.ylo &&
                     Y <= p.yhi) {
                     const uint8_t* q = scb + sr * RB + x;
@@ -685,7 +712,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
     } else if (kNms) {
         constexpr int OG = TW / 4;  // 30 output groups per row
         const int og = threadIdx.x % 32, chunk = threadIdx.x / 32;
-        const int X0 = blockIdx.x * TW + 4 * og;
+        const int X0 = T.x * TW + 4 * og;
         const int oy0 = 8 * chunk, oy1 = min(oy0 + 8, TH);
         // strict maxima of the lane's 4 x 8 strip as a bit mask: bit 4 r + q = pixel (X0 + q, row oy0 + r)
         uint32_t bits = 0;
@@ -723,7 +750,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                 const h2 to = M.co - __builtin_elementwise_maximum(max3h(U.ho, D.ho, M.lo), M.ro) - one;
                 const uint32_t sgn = ((as_u32(te) & 0x80008000u) >> 1) | (as_u32(to) & 0x80008000u);
                 const uint32_t nib = ~(((sgn >> 14) & 3u) | ((sgn >> 28) & 0xCu)) & colbits;
-                const int Y = blockIdx.y * TH + oy;
+                const int Y = T.y * TH + oy;
                 if (Y >= p.ylo && Y <= p.yhi) bits |= nib << (4 * (oy - oy0));
                 U = M;
                 M = D;
@@ -752,17 +779,21 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                     bits &= bits - 1u;
                     const int oy = oy0 + (b >> 2), q = b & 3;
                     const uint32_t sv = scb[(oy + 1) * (4 * GX) + 4 * (og + 1) + q];
-                    list[idx++] = ((uint32_t)(blockIdx.y * TH + oy) << 20) | ((uint32_t)(X0 + q) << 8) | sv;
+                    list[idx++] = ((uint32_t)(T.y * TH + oy) << 20) | ((uint32_t)(X0 + q) << 8) | sv;
                 }
             }
         }
     }
+    FAST_STAMP(8);
     // the blur reads only the (biased) image tile and writes the frame directly
     if (kBlur && blur) {
         __syncthreads();  // xor_tile is complete
-        blur_mfma(img, p, f);
+        FAST_STAMP(9);
+        blur_mfma(img, p, f, T);
+        FAST_STAMP(10);
     }
     __syncthreads();  // s_cnt and the tile's list are final
+    FAST_STAMP(11);
     if (kSink || !kEmit) {  // ablation: keep the skipped stages' inputs alive
         if (kSink) {
             const uint32_t* w = &sc[0][0];
@@ -775,11 +806,12 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
     // the tile's own slot of the frame's candidate buffer (TCAP entries) and count: no global
     // atomics (the 264 tiles of a 720p frame run at once, and one counter per frame serialised
     // them at the L2)
-    const int tix = blockIdx.y * gridDim.x + blockIdx.x;
+    const int tix = T.y * p.tiles_x + T.x;
     const uint32_t n = s_cnt;
     if (threadIdx.x == 0) counts[(long long)f * p.tiles + tix] = n;
     uint32_t* out = cand + (long long)f * p.cand_cap + (long long)tix * TCAP;
     for (uint32_t k = threadIdx.x; k < n; k += FAST_THREADS) out[k] = list[k];
+    FAST_STAMP(12);
 }
 
 __global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms_kernel(const uint8_t* __restrict__ frames,
@@ -787,12 +819,14 @@ __global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms
                                                                 uint32_t* __restrict__ cand,
                                                                 uint32_t* __restrict__ counts)
 {
+    // one workgroup per tile (a persistent loop over tiles was measured 25 % slower: the loop's
+    // live state spilled 29 VGPRs / 10 SGPRs at 5 waves per SIMD)
     const int G = p.gate ? *p.gate : 0;
     if (p.gate_next && (blockIdx.x | blockIdx.y | blockIdx.z | threadIdx.x) == 0) {
         *p.gate_next = 255;  // lowered by this batch's select_kernel
         p.redo[0] = 0;
     }
-    fast_tile<true>(frames, p, blockIdx.z, G, p.blur != nullptr, cand, counts);
+    fast_tile<true>(frames, p, blockIdx.z, G, p.blur != nullptr, cand, counts, Tile{(int)blockIdx.x, (int)blockIdx.y});
 }
 
 // The exact (ungated) pass over the frames select_kernel listed in p.redo; no blur (the gated
@@ -804,7 +838,7 @@ __global__ __launch_bounds__(FAST_THREADS, 4) void fast_redo_kernel(const uint8_
 {
     const uint32_t n = p.redo[0];
     for (uint32_t z = blockIdx.z; z < n; z += gridDim.z) {
-        fast_tile<false>(frames, p, (int)p.redo[1 + z], 0, false, cand, counts);
+        fast_tile<false>(frames, p, (int)p.redo[1 + z], 0, false, cand, counts, Tile{(int)blockIdx.x, (int)blockIdx.y});
         __syncthreads();
     }
 }
@@ -815,9 +849,10 @@ __global__ __launch_bounds__(FAST_THREADS) void fast_score_map_kernel(const uint
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
     __shared__ uint32_t sc[SROWS][GX];
-    load_tile(src, p, img);
+    const Tile T{(int)blockIdx.x, (int)blockIdx.y};
+    load_tile(src, p, img, T);
     __syncthreads();
-    score_strip(img, sc, p);
+    score_strip(img, sc, p, T);
     __syncthreads();
     const uint8_t* scb = reinterpret_cast<const uint8_t*>(&sc[0][0]);
     for (int i = threadIdx.x; i < TW * TH; i += FAST_THREADS) {
@@ -2418,6 +2453,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         if (H <= 2 * border || W <= 2 * border) fp.xhi = -1;  // RunByImageBorder clears all
         fp.cand_cap = v.cand_cap;
         fp.tiles = v.tiles;
+        fp.tiles_x = (W + TW - 1) / TW;
         fp.dword_ok = (fp.stride % 4 == 0) && (fp.pitch % 4 == 0) && ((uintptr_t)raw.base[l] % 4 == 0);
         fp.qword_ok = (fp.stride % 8 == 0) && (fp.pitch % 8 == 0) && ((uintptr_t)raw.base[l] % 8 == 0);
         if (fused_blur) {
@@ -2865,6 +2901,14 @@ mage_status mage_orb_fast_gate_stats(mage_orb* orb, uint32_t level, int32_t* las
     return MAGE_OK;
 }
 
+#if MAGE_FAST_STAMPS
+// development build only (tools/fast_stamps.py): the per-wave phase stamps of the last FAST pass
+mage_status mage_debug_fast_stamps(unsigned long long* out)
+{
+    MAGE_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(mage::g_fast_stamps), sizeof(mage::g_fast_stamps)));
+    return MAGE_OK;
+}
+#endif
 #if MAGE_SELECT_STAMPS
 // development build only (tools/select_stamps.py): the per-frame phase stamps of the last select
 mage_status mage_debug_select_stamps(unsigned long long* out)
