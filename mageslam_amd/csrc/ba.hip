@@ -1133,6 +1133,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     __shared__ int s_fail;
     __shared__ unsigned s_tile_bar;   // the TRSM-phase barrier count (CT_TW + 1 arrivals per step)
     __shared__ double cst[16][17], dst[16][17];  // A_{k,k+1}, A_{k+1,k+1} staged for the factor wave
+    __shared__ uint16_t s_nz[CT_MAXT];  // structural row masks of U (chol_tile_table)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: tile bookkeeping on the SALU
     const int mt = np >> 4, T = mt * (mt + 1) / 2;
@@ -1377,6 +1378,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             C[sl] = dbl4{0, 0, 0, 0};
         }
     }
+    if (tid < CT_MAXT) s_nz[tid] = tab[CT_TW * CT_TPW + tid];
     // b -> vb (block 0's entries are the factor wave's: it turns them into y_0)
     constexpr int TT = CT_TW * kWave;  // tile-wave threads
     for (int i = 16 + tid; i < np; i += TT) vb[i] = i < n ? b[i] : 0.0;
@@ -1439,10 +1441,12 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 for (int r = 0; r < 4; r++) C[sl][r] = pan[buf][kn][lr + 4 * r][lc];
         // --- SYRK: A_ij -= U_ki^T U_kj for the owned tiles with k < i <= j but (k+1, k+1) (the
         // factor wave's) ---
+        // (only where both U_ki and U_kj can be nonzero: the envelope of chol_tile_table)
+        const unsigned nzk = (unsigned)__builtin_amdgcn_readfirstlane((int)s_nz[k]);
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++) {
-            const int i = tIJ[sl] & 0xFF;
-            if (i > k && i < mt && tIJ[sl] != diag) syrk(sl);
+            const int i = tIJ[sl] & 0xFF, j = tIJ[sl] >> 8;
+            if (i > k && i < mt && tIJ[sl] != diag && (nzk >> i & nzk >> j & 1u)) syrk(sl);
         }
         // the next step's chain tiles, now final, to the factor wave
         if (kn + 1 < mt) {
@@ -2393,20 +2397,43 @@ __global__ __launch_bounds__(1024) void export_state(State s, int C, int P, floa
 // Host: the StepOptimizer / OptimizationAlgorithmLevenberg control flow
 // ------------------------------------------------------------------------------------------
 
-// chol_tiles' slot table, ti | tj << 8 per (tile wave, slot), 0xFFFF empty: the upper tiles in
-// row-major order, round-robin over the tile waves; tile (0, 0) is the factor wave's (read from S
-// directly).
-static void chol_tile_table(int mt, std::vector<uint16_t>& tab)
+// chol_tiles' slot table, ti | tj << 8 per (tile wave, slot), 0xFFFF empty, followed by one
+// structural row mask per tile row (bit j of row k: tile (k, j) of U can be nonzero).  Only the
+// tiles of the factor's envelope get a slot: the 6x6 blocks the Schur pairs write (every nonzero
+// block of S, tether blocks included), the diagonal and the chain tiles (d-1, d), closed under
+// the tile-level symbolic fill (U_ki, U_kj nonzero -> A_ij filled).  Tiles outside it are zero in
+// S and stay zero in U, so their TRSMs, SYRK updates and backward products are skipped.  The
+// slots go round-robin over the tile waves in row-major order; tile (0, 0) is the factor wave's
+// (read from S directly).
+static void chol_tile_table(int mt, const SchurPair* pairs, int npairs, std::vector<uint16_t>& tab)
 {
-    tab.assign((size_t)CT_TW * CT_TPW, 0xFFFF);
+    std::vector<uint16_t> nz(CT_MAXT, 0);
+    auto mark = [&](int a, int b) {
+        if (a > b) std::swap(a, b);
+        if (a < mt && b < mt) nz[a] |= (uint16_t)(1u << b);
+    };
+    for (int d = 0; d < mt; d++) {
+        mark(d, d);
+        if (d > 0) mark(d - 1, d);
+    }
+    for (int pi = 0; pi < npairs; pi++) {
+        const int r1 = 6 * pairs[pi].h1, r2 = 6 * pairs[pi].h2;
+        for (int a : {r1 / 16, (r1 + 5) / 16})
+            for (int b : {r2 / 16, (r2 + 5) / 16}) mark(a, b);
+    }
+    for (int k = 0; k < mt; k++)  // symbolic fill, in factor order
+        for (int i = k + 1; i < mt; i++)
+            if (nz[k] >> i & 1) nz[i] |= (uint16_t)(nz[k] & ~((1u << i) - 1u));
+    tab.assign((size_t)CT_TW * CT_TPW + CT_MAXT, 0xFFFF);
     std::vector<int> cnt(CT_TW, 0);
     int w = 0;
     for (int i = 0; i < mt; i++)
         for (int j = i; j < mt; j++) {
-            if (i == 0 && j == 0) continue;
+            if ((i == 0 && j == 0) || !(nz[i] >> j & 1)) continue;
             tab[(size_t)w * CT_TPW + cnt[w]++] = (uint16_t)(i | j << 8);
             w = (w + 1) % CT_TW;
         }
+    for (int k = 0; k < CT_MAXT; k++) tab[(size_t)CT_TW * CT_TPW + k] = k < mt ? nz[k] : 0;
 }
 static_assert(CT_TW * CT_TPW >= CT_MAXT * (CT_MAXT + 1) / 2 - 1, "every tile but (0, 0) has a slot");
 
@@ -3123,7 +3150,7 @@ struct BundleAdjuster {
         MAGE_REQUIRE(pbeg[npairs] < (1ll << 31), MAGE_EUNSUPPORTED, "Schur product list exceeds 2^31 entries");
         pt.mark("chunks");
         if (np <= 16 * CT_MAXT) {
-            chol_tile_table(np / 16, ws.ctab);
+            chol_tile_table(np / 16, spairs.data(), npairs, ws.ctab);
             if ((r = upload(d_ctab, ws.ctab)) != MAGE_OK) return r;
         }
         if ((r = upload(d_sfinish, sfinish)) != MAGE_OK) return r;
