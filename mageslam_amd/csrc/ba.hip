@@ -1080,6 +1080,12 @@ __global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict_
 #ifndef MAGE_CHOL_WAVES
 #define MAGE_CHOL_WAVES 16
 #endif
+#ifndef MAGE_CHOL_LIGHT
+#define MAGE_CHOL_LIGHT 0  // tiles of each tile wave on the factor wave's SIMD (at least; chol_tile_table)
+#endif
+#ifndef MAGE_CHOL_LOOKAHEAD
+#define MAGE_CHOL_LOOKAHEAD 1  // the diagonal-block factor starts column j+1's pivot chain early
+#endif
 constexpr int CT_WAVES = MAGE_CHOL_WAVES;  // 16: 4 per SIMD (15 tile waves x 8 resident tiles + the factor wave)
 constexpr int CT_THREADS = CT_WAVES * kWave;
 constexpr int CT_TW = CT_WAVES - 1;  // tile waves (wave CT_TW: the factor wave, which holds no tile)
@@ -1209,16 +1215,39 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 v[q] = l < 16 ? (q <= l ? dq[q] : 0.0) : (l < 32 ? (q == c ? 1.0 : 0.0) : (l == 32 ? dq[q] : 0.0));
             bool bad = false;
             if (k == 0) tick(6);
+            // 1/sqrt by v_rsq_f64 + one Newton step (~1e-14 relative, no f64 sqrt / division
+            // sequence on the column's critical path)
+            auto rsq_newton = [&](double d) {
+                if (!(d > 0)) bad = true;
+                const double h = 0.5 * d;
+                double r = __builtin_amdgcn_rsq(d);
+                return r * __builtin_fma(-h * r, r, 1.5);
+            };
+#if MAGE_CHOL_LOOKAHEAD
+            // Look-ahead: column j + 1 is updated first and its pivot's 1/sqrt chain starts right
+            // away, so the chain (readlane -> rsq -> Newton -> scale, a run of dependent f64 ops)
+            // overlaps the rest of column j's update instead of following it in issue order.
+            double r = rsq_newton(readlane_f64(v[0], 0));
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                const double djj = readlane_f64(v[j], j);
-                if (!(djj > 0)) bad = true;
-                // 1/sqrt by v_rsq_f64 + one Newton step (~1e-14 relative, no f64 sqrt / division
-                // sequence on the column's critical path)
-                const double h = 0.5 * djj;
-                double r = __builtin_amdgcn_rsq(djj);
-                r *= __builtin_fma(-h * r, r, 1.5);
                 v[j] *= r;
+                if (j < 15) {
+                    const double l1 = readlane_f64(v[j], j + 1);
+                    v[j + 1] = __builtin_fma(-v[j], l1, v[j + 1]);
+                    const double rn = rsq_newton(readlane_f64(v[j + 1], j + 1));
+                    double lq[16];
+#pragma unroll
+                    for (int q = j + 2; q < 16; q++) lq[q] = readlane_f64(v[j], q);
+#pragma unroll
+                    for (int q = j + 2; q < 16; q++) v[q] = __builtin_fma(-v[j], lq[q], v[q]);
+                    r = rn;
+                }
+                __builtin_amdgcn_sched_barrier(0);  // keep each column's broadcasts in its own window
+            }
+#else
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                v[j] *= rsq_newton(readlane_f64(v[j], j));
                 // all broadcasts of the column first (distinct scalar registers: the readlane ->
                 // VALU hazard is covered by the batch instead of an s_nop per element)
                 double lq[16];
@@ -1228,6 +1257,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 for (int q = j + 1; q < 16; q++) v[q] = __builtin_fma(-v[j], lq[q], v[q]);
                 __builtin_amdgcn_sched_barrier(0);  // keep each column's broadcasts in its own window
             }
+#endif
             if (k == 0) tick(7);
             if (l == 0 && bad) s_fail = 1;
             if (l >= 16 && l < 32) {
@@ -2426,13 +2456,29 @@ static void chol_tile_table(int mt, const SchurPair* pairs, int npairs, std::vec
             if (nz[k] >> i & 1) nz[i] |= (uint16_t)(nz[k] & ~((1u << i) - 1u));
     tab.assign((size_t)CT_TW * CT_TPW + CT_MAXT, 0xFFFF);
     std::vector<int> cnt(CT_TW, 0);
-    int w = 0;
+    std::vector<std::pair<int, int>> tiles;
     for (int i = 0; i < mt; i++)
-        for (int j = i; j < mt; j++) {
-            if ((i == 0 && j == 0) || !(nz[i] >> j & 1)) continue;
-            tab[(size_t)w * CT_TPW + cnt[w]++] = (uint16_t)(i | j << 8);
-            w = (w + 1) % CT_TW;
-        }
+        for (int j = i; j < mt; j++)
+            if (!(i == 0 && j == 0) && (nz[i] >> j & 1)) tiles.emplace_back(i, j);
+    // The factor wave (wave CT_TW) shares its SIMD with the tile waves w = CT_TW (mod 4) (a
+    // workgroup's waves are dealt to the SIMDs cyclically; speed only): those get the first,
+    // earliest-finished tiles and few of them, so the factor's column loop meets fewer SYRK MFMAs.
+    std::vector<int> light, heavy;
+    for (int w = 0; w < CT_TW; w++) ((w & 3) == (CT_TW & 3) ? light : heavy).push_back(w);
+    const int nheavy = (int)heavy.size() * CT_TPW;
+    const int per_light = light.empty() ? 0
+                                        : std::min(CT_TPW, std::max(MAGE_CHOL_LIGHT, ((int)tiles.size() - nheavy +
+                                                                                      (int)light.size() - 1) /
+                                                                                         (int)light.size()));
+    size_t t = 0;
+    for (int w : light)
+        for (int c = 0; c < per_light && t < tiles.size(); c++, t++)
+            tab[(size_t)w * CT_TPW + cnt[w]++] = (uint16_t)(tiles[t].first | tiles[t].second << 8);
+    for (size_t h = 0; t < tiles.size(); t++) {
+        while (cnt[heavy[h % heavy.size()]] >= CT_TPW) h++;
+        const int w = heavy[h++ % heavy.size()];
+        tab[(size_t)w * CT_TPW + cnt[w]++] = (uint16_t)(tiles[t].first | tiles[t].second << 8);
+    }
     for (int k = 0; k < CT_MAXT; k++) tab[(size_t)CT_TW * CT_TPW + k] = k < mt ? nz[k] : 0;
 }
 static_assert(CT_TW * CT_TPW >= CT_MAXT * (CT_MAXT + 1) / 2 - 1, "every tile but (0, 0) has a slot");
