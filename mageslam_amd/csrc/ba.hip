@@ -2597,19 +2597,19 @@ struct BundleAdjuster {
                         &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_chist, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf, &d_removed, &d_camflag,
                         &d_ikeys, &d_ivals, &d_isum, &d_iacc, &d_ctab})
-            b->release();
-        h_olist.release();
-        h_state.release();
-        h_kb.release();
-        h_isum.release();
-        h_stage.release();
-        h_dma.release();
+            b->retire();  // the stream is synchronised: the blocks are idle (common.hpp block cache)
+        h_olist.retire();
+        h_state.retire();
+        h_kb.retire();
+        h_isum.retire();
+        h_stage.retire();
+        h_dma.retire();
         iacc_clean = false;
         stage_off = dma_off = 0;
         pending.k = 0;
-        if (st) (void)hipStreamDestroy(st);
+        if (st) mage::stream_retire(st);  // idle (synchronised above)
         st = nullptr;
-        if (h_ctl) (void)hipHostFree(h_ctl);
+        if (h_ctl) mage::pool_retire(2, h_ctl, CTL_DOUBLES * sizeof(double));
         h_ctl = nullptr;
     }
 
@@ -3513,9 +3513,14 @@ mage_status mage_ba_create(int32_t points_fixed, int device, mage_ba** out)
     auto* b = new mage_ba();
     b->device = device;
     b->points_fixed = points_fixed != 0;
-    if (hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), mage::BundleAdjuster::CTL_DOUBLES * sizeof(double),
-                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+    // a retired stream / control block of an earlier instance when there is one (MakeBundler
+    // creates a BundlerLib per local-BA window; creation and hipHostFree cost ~0.1 ms each)
+    size_t ctl_bytes = 0;
+    b->st = mage::stream_take();
+    b->h_ctl = static_cast<double*>(mage::pool_take(2, mage::BundleAdjuster::CTL_DOUBLES * sizeof(double), &ctl_bytes));
+    if ((!b->st && hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess) ||
+        (!b->h_ctl && hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), mage::BundleAdjuster::CTL_DOUBLES * sizeof(double),
+                                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&b->h_ctl_dev), b->h_ctl, 0) != hipSuccess ||
         (std::memset(b->h_ctl, 0, mage::BundleAdjuster::CTL_DOUBLES * sizeof(double)), false)) {
         b->release();

@@ -19,6 +19,85 @@ thread_local std::string g_last_error;
 }
 
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+namespace {
+struct BlockPool {
+    std::mutex mu;
+    std::multimap<size_t, std::pair<int, void*>> free[3];  // bytes -> (device, block)
+    size_t held[3] = {0, 0, 0};
+    std::vector<std::pair<int, hipStream_t>> streams;
+};
+BlockPool& block_pool()
+{
+    static BlockPool* p = new BlockPool();  // never destroyed: blocks outlive static teardown order
+    return *p;
+}
+constexpr size_t kPoolCap[3] = {size_t(2) << 30, size_t(512) << 20, size_t(64) << 20};  // retired bytes kept per kind
+}  // namespace
+
+void* pool_take(int kind, size_t n, size_t* got)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    BlockPool& P = block_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    // the smallest retired block that fits and wastes at most half of itself
+    for (auto it = P.free[kind].lower_bound(n); it != P.free[kind].end() && it->first <= 2 * n + 4096; ++it)
+        if (it->second.first == dev) {
+            void* p = it->second.second;
+            *got = it->first;
+            P.held[kind] -= it->first;
+            P.free[kind].erase(it);
+            return p;
+        }
+    return nullptr;
+}
+
+// Idle non-blocking streams of destroyed per-task objects (mage_ba), per device.
+hipStream_t stream_take()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    BlockPool& P = block_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (auto it = P.streams.begin(); it != P.streams.end(); ++it)
+        if (it->first == dev) {
+            hipStream_t s = it->second;
+            P.streams.erase(it);
+            return s;
+        }
+    return nullptr;
+}
+
+void stream_retire(hipStream_t s)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    BlockPool& P = block_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (P.streams.size() >= 64) {
+        (void)hipStreamDestroy(s);
+        return;
+    }
+    P.streams.emplace_back(dev, s);
+}
+
+void pool_retire(int kind, void* p, size_t bytes)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    BlockPool& P = block_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (P.held[kind] + bytes > kPoolCap[kind]) {  // over the cap: a real free
+        if (kind == 0)
+            (void)hipFree(p);
+        else
+            (void)hipHostFree(p);  // page-locked (1) and mapped (2) host memory
+        return;
+    }
+    P.free[kind].emplace(bytes, std::make_pair(dev, p));
+    P.held[kind] += bytes;
+}
 const char* last_error() { return g_last_error.c_str(); }
 
 namespace {

@@ -40,6 +40,16 @@ const char* last_error();
 // Selects `device` and verifies it is a gfx950 part; returns MAGE_OK or MAGE_EDEVICE.
 mage_status bind_device(int device);
 
+// Block cache for allocations that are created and dropped per task (BundlerLib per local-BA
+// window, MappingWorker's MakeBundler): hipFree / hipHostFree synchronise the whole device and cost
+// ~0.1 ms each.  Only blocks whose owner has synchronised every stream that used them are retired
+// here (retire_*), so a block handed out again is idle; any buffer's first allocation may take one.
+// Kind 0: device memory, 1: page-locked host memory, 2: mapped (coherent) host memory.  Thread safe.
+void* pool_take(int kind, size_t n, size_t* got);
+void pool_retire(int kind, void* p, size_t bytes);
+hipStream_t stream_take();  // an idle retired stream of the current device, or nullptr
+void stream_retire(hipStream_t s);
+
 // Grow-only device buffer.
 struct DeviceBuffer {
     void* ptr = nullptr;
@@ -49,6 +59,7 @@ struct DeviceBuffer {
         if (ptr) (void)hipFree(ptr);
         ptr = nullptr;
         bytes = 0;
+        if ((ptr = pool_take(0, n, &bytes)) != nullptr) return MAGE_OK;
         if (hipMalloc(&ptr, n) != hipSuccess) {
             set_error("hipMalloc of " + std::to_string(n) + " bytes failed");
             return MAGE_ENOMEM;
@@ -58,6 +69,12 @@ struct DeviceBuffer {
     }
     void release() {
         if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    // release into the block cache: the caller has synchronised every stream that used the buffer
+    void retire() {
+        if (ptr) pool_retire(0, ptr, bytes);
         ptr = nullptr;
         bytes = 0;
     }
@@ -78,6 +95,7 @@ struct PinnedBuffer {
         if (ptr) (void)hipHostFree(ptr);
         ptr = nullptr;
         bytes = 0;
+        if ((ptr = pool_take(1, n, &bytes)) != nullptr) return MAGE_OK;
         if (hipHostMalloc(&ptr, n, hipHostMallocDefault) != hipSuccess) {
             set_error("hipHostMalloc of " + std::to_string(n) + " bytes failed");
             return MAGE_ENOMEM;
@@ -87,6 +105,11 @@ struct PinnedBuffer {
     }
     void release() {
         if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    void retire() {
+        if (ptr) pool_retire(1, ptr, bytes);
         ptr = nullptr;
         bytes = 0;
     }
@@ -105,6 +128,12 @@ struct MappedBuffer {
     mage_status reserve(size_t n) {
         if (n <= bytes) return MAGE_OK;
         release();
+        if ((ptr = pool_take(2, n, &bytes)) != nullptr) {
+            if (hipHostGetDevicePointer(&dev, ptr, 0) == hipSuccess) return MAGE_OK;
+            pool_retire(2, ptr, bytes);
+            ptr = nullptr;
+            bytes = 0;
+        }
         if (hipHostMalloc(&ptr, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) {
             release();
@@ -116,6 +145,11 @@ struct MappedBuffer {
     }
     void release() {
         if (ptr) (void)hipHostFree(ptr);
+        ptr = dev = nullptr;
+        bytes = 0;
+    }
+    void retire() {
+        if (ptr) pool_retire(2, ptr, bytes);
         ptr = dev = nullptr;
         bytes = 0;
     }

@@ -657,15 +657,75 @@ namespace {
 // The same window / schedule / write-back as tracking.py build_ba_window + apply_ba_window, over the
 // keyframe ring copied from the device; BundlerLib through the C-ABI (one instance per call of the
 // loop, the lambda persisted across windows as MappingWorker does).
+// MAGE_TRACK_PROFILE=1 in the environment: per-window phase times of the local BA on stderr
+// (development; tools/track_kernels.py)
+struct PhaseClock {
+    bool on = false;
+    std::chrono::steady_clock::time_point t;
+    char line[512];
+    int len = 0;
+    void start()
+    {
+        if (!on) return;
+        t = std::chrono::steady_clock::now();
+        len = 0;
+    }
+    void mark(const char* name)
+    {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        len += snprintf(line + len, sizeof(line) - len, " %s %.3f", name,
+                        std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+    void flush()
+    {
+        if (on) fprintf(stderr, "local BA window ms:%s\n", line);
+    }
+};
+
+// Page-locked host array (the ring's host copy): DMA copies in both directions, queued with
+// hipMemcpyAsync on the loop's stream instead of one synchronous pageable copy per field.
+template <class T>
+struct Pinned {
+    T* p = nullptr;
+    size_t n = 0;
+    Pinned() = default;
+    Pinned(const Pinned&) = delete;
+    Pinned& operator=(const Pinned&) = delete;
+    ~Pinned()
+    {
+        if (p) (void)hipHostFree(p);
+    }
+    bool resize(size_t m)
+    {
+        if (m <= n) return true;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(m, 1) * sizeof(T), hipHostMallocDefault) != hipSuccess)
+            return false;
+        n = m;
+        return true;
+    }
+    T& operator[](size_t i) { return p[i]; }
+    const T& operator[](size_t i) const { return p[i]; }
+    T* data() { return p; }
+};
+
 struct HostRing {
     uint32_t first = 0, count = 0, nk = 0, cap = 0, acap = 0;
     uint32_t n[NKMAX], id[NKMAX], an[NKMAX];
-    std::vector<double> pose;       // 12 per slot
-    std::vector<mage_keypoint> kp;  // cap per slot
-    std::vector<float> pts, mvd, dmin, dmax;
-    std::vector<uint32_t> ref;
-    std::vector<uint8_t> own, aalive;
-    std::vector<int4> assoc;
+    // a page-locked byte-for-byte mirror of the device ring's fields (one DMA copy each way per
+    // window); the arrays below point into it at the device layout's offsets
+    Pinned<uint8_t> mirror;
+    double* pose = nullptr;       // 12 per slot
+    mage_keypoint* kp = nullptr;  // cap per slot
+    float *pts = nullptr, *mvd = nullptr, *dmin = nullptr, *dmax = nullptr;
+    uint32_t* ref = nullptr;
+    uint8_t *own = nullptr, *aalive = nullptr;
+    int4* assoc = nullptr;
+    Pinned<uint32_t> zero;  // the halt word's clear value
 };
 
 struct LocalBA {  // MappingWorker's CurrentLambda, persisted across the windows
@@ -727,7 +787,7 @@ void host_point_attributes(HostRing& R, uint32_t slot, uint32_t i, const TrackCo
 
 // One local BA on the ring (on the host copy); returns the outlier count (UINT32_MAX: no window).
 mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int device, uint32_t* n_out,
-                          std::vector<uint8_t>& slot_changed)
+                          std::vector<uint8_t>& slot_changed, PhaseClock& prof)
 {
     *n_out = 0xFFFFFFFFu;
     const uint32_t nr = R.count;
@@ -745,6 +805,7 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
         uint32_t kind, src;  // 0: own (point index), 1: association (entry)
     };
     std::vector<Obs> obs;
+    obs.reserve((size_t)nr * R.cap * 2);
     for (uint32_t r = 0; r < nr; r++) {
         const uint32_t sl = slot_of[r];
         const size_t o = (size_t)sl * R.cap;
@@ -758,23 +819,28 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
                 obs.push_back({r, (uint32_t)ow, (uint32_t)e.y, bits_float(e.z), bits_float(e.w), 1, a});
         }
     }
-    // points a free camera observes, ascending (owner, index)
+    // points a free camera observes, ascending (owner, index): a dense (ring position, index) map
+    // instead of a sorted key list (the window build runs between frames, on the loop's critical path)
     const uint32_t nfix = nr > c.s.ba_free_keyframes ? nr - c.s.ba_free_keyframes : 1u;  // the oldest are fixed
-    std::vector<uint64_t> keys;
+    std::vector<int32_t> pmap((size_t)nr * R.cap, -1);
     for (const Obs& ob : obs)
-        if (ob.cam >= nfix) keys.push_back((uint64_t)ob.owner << 32 | ob.idx);
-    std::sort(keys.begin(), keys.end());
-    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-    auto pidx = [&](uint32_t owner, uint32_t idx) -> int64_t {
-        const uint64_t k = (uint64_t)owner << 32 | idx;
-        auto it = std::lower_bound(keys.begin(), keys.end(), k);
-        return (it != keys.end() && *it == k) ? (int64_t)(it - keys.begin()) : -1;
-    };
+        if (ob.cam >= nfix) pmap[(size_t)ob.owner * R.cap + ob.idx] = 0;
+    std::vector<uint64_t> keys;
+    for (uint32_t r = 0; r < nr; r++)
+        for (uint32_t i = 0; i < R.cap; i++)
+            if (pmap[(size_t)r * R.cap + i] == 0) {
+                pmap[(size_t)r * R.cap + i] = (int32_t)keys.size();
+                keys.push_back((uint64_t)r << 32 | i);
+            }
     std::vector<Obs> kept;
     std::vector<uint32_t> cam, pt;
     std::vector<float> uv, info;
+    kept.reserve(obs.size());
+    cam.reserve(obs.size());
+    pt.reserve(obs.size());
+    uv.reserve(2 * obs.size());
     for (const Obs& ob : obs) {
-        const int64_t p = pidx(ob.owner, ob.idx);
+        const int32_t p = pmap[(size_t)ob.owner * R.cap + ob.idx];
         if (p < 0) continue;
         kept.push_back(ob);
         cam.push_back(ob.cam);
@@ -817,19 +883,23 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
     }
     const std::vector<float> hw(std::max(steps, 1u), huber);
     mage_status st;
+    prof.mark("window");
     BundlerHandle H;
     if ((st = mage_ba_create(0, device, &H.ba)) != MAGE_OK) return st;
+    prof.mark("create");
     if (L.have_lambda && (st = mage_ba_set_lambda(H.ba, L.lambda)) != MAGE_OK) return st;
     if ((st = mage_ba_set_cameras(H.ba, nr, pos3.data(), r9.data(), intr.data(), fixed.data())) != MAGE_OK ||
         (st = mage_ba_set_points(H.ba, P, xyz.data())) != MAGE_OK ||
         (st = mage_ba_set_observations(H.ba, E, uv.data(), cam.data(), pt.data(), info.data())) != MAGE_OK)
         return st;
+    prof.mark("setters");
     std::vector<uint32_t> outl(E);
     uint32_t nout = 0;
     float ms = 0.f;
     if ((st = mage_ba_step(H.ba, hw.data(), (uint32_t)hw.size(), c.s.ba_max_outlier_error, outl.data(), E, &nout, &ms)) !=
         MAGE_OK)
         return st;
+    prof.mark("step");
     std::vector<float> pos_o(3 * nr), r9_o(9 * nr), xyz_o(3ull * P);
     float lam = 0.f;
     if ((st = mage_ba_get_poses(H.ba, pos_o.data(), r9_o.data())) != MAGE_OK ||
@@ -863,6 +933,7 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
     }
     for (uint32_t q = 0; q < P; q++)
         host_point_attributes(R, slot_of[keys[q] >> 32], (uint32_t)(keys[q] & 0xFFFFFFFFu), c);
+    prof.mark("get + apply");
     *n_out = nout;
     return MAGE_OK;
 }
@@ -1100,6 +1171,11 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         R.cap = (uint32_t)cap;
         R.acap = (uint32_t)acap;
         LocalBA L;
+        PhaseClock prof;
+        {
+            const char* e = getenv("MAGE_TRACK_PROFILE");
+            prof.on = e && *e == '1';
+        }
         std::vector<uint8_t> changed(NK);
         uint32_t next = 1;
         constexpr uint32_t DEPTH = 2;
@@ -1116,7 +1192,9 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
             std::atomic_thread_fence(std::memory_order_acquire);
             if (hp[1] != f) continue;
             // a local BA: the halted frames drain, the ring comes to the host
+            prof.start();
             if (hipStreamSynchronize(st) != hipSuccess) return fail(MAGE_EDEVICE);
+            prof.mark("drain");
             Ctl hc;
             if (hipMemcpy(&hc, b.ctl, sizeof(Ctl), hipMemcpyDeviceToHost) != hipSuccess) return fail(MAGE_EDEVICE);
             R.first = hc.kf_first;
@@ -1126,52 +1204,49 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
                 R.id[k] = hc.kf_id[k];
                 R.an[k] = hc.kf_an[k];
             }
-            R.pose.resize(12 * NK);
-            R.kp.resize(cap * NK);
-            R.pts.resize(3 * cap * NK);
-            R.mvd.resize(3 * cap * NK);
-            R.dmin.resize(cap * NK);
-            R.dmax.resize(cap * NK);
-            R.ref.resize(cap * NK);
-            R.own.resize(cap * NK);
-            R.assoc.resize(acap * NK);
-            R.aalive.resize(acap * NK);
-            if (hipMemcpy(R.pose.data(), b.kf_pose, 96 * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.kp.data(), b.kf_kp, 28 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.pts.data(), b.kf_pts, 12 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.mvd.data(), b.kf_mvd, 12 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.dmin.data(), b.kf_dmin, 4 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.dmax.data(), b.kf_dmax, 4 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.ref.data(), b.kf_ref, 4 * cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.own.data(), b.kf_own, cap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.assoc.data(), b.kf_assoc, 16 * acap * NK, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(R.aalive.data(), b.kf_aalive, acap * NK, hipMemcpyDeviceToHost) != hipSuccess)
+            // the ring's fields are consecutive in the device block from kf_kp to kf_aalive
+            const size_t mbytes = o_kfaa + acap * NK - o_kfkp;
+            if (!R.mirror.resize(mbytes) || !R.zero.resize(1)) return fail(MAGE_ENOMEM);
+            uint8_t* hm = R.mirror.data();
+            R.kp = reinterpret_cast<mage_keypoint*>(hm + (o_kfkp - o_kfkp));
+            R.pts = reinterpret_cast<float*>(hm + (o_kfp - o_kfkp));
+            R.mvd = reinterpret_cast<float*>(hm + (o_kfv - o_kfkp));
+            R.dmin = reinterpret_cast<float*>(hm + (o_kfdn - o_kfkp));
+            R.dmax = reinterpret_cast<float*>(hm + (o_kfdx - o_kfkp));
+            R.pose = reinterpret_cast<double*>(hm + (o_kfps - o_kfkp));
+            R.ref = reinterpret_cast<uint32_t*>(hm + (o_kfr - o_kfkp));
+            R.own = hm + (o_kfo - o_kfkp);
+            R.assoc = reinterpret_cast<int4*>(hm + (o_kfa - o_kfkp));
+            R.aalive = hm + (o_kfaa - o_kfkp);
+            R.zero[0] = 0;
+            if (hipMemcpyAsync(hm, d + o_kfkp, mbytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
                 return fail(MAGE_EDEVICE);
+            prof.mark("ring D2H");
             std::fill(changed.begin(), changed.end(), 0);
             uint32_t nout = 0;
-            if ((r = host_local_ba(R, c, L, dev, &nout, changed)) != MAGE_OK) return fail(r);
+            if ((r = host_local_ba(R, c, L, dev, &nout, changed, prof)) != MAGE_OK) return fail(r);
             if (ba_outliers) ba_outliers[f] = nout;
-            // write back the changed slots, the frame's pose (= its keyframe's) and clear the halt
-            for (uint32_t k = 0; k < NK; k++) {
-                if (!changed[k]) continue;
-                const size_t o = (size_t)k * cap, ao = (size_t)k * acap;
-                if (hipMemcpy(b.kf_pose + 12 * k, &R.pose[12 * k], 96, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(b.kf_pts + 3 * o, &R.pts[3 * o], 12 * cap, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(b.kf_mvd + 3 * o, &R.mvd[3 * o], 12 * cap, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(b.kf_dmin + o, &R.dmin[o], 4 * cap, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(b.kf_dmax + o, &R.dmax[o], 4 * cap, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(b.kf_ref + o, &R.ref[o], 4 * cap, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(b.kf_own + o, &R.own[o], cap, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(b.kf_aalive + ao, &R.aalive[ao], acap, hipMemcpyHostToDevice) != hipSuccess)
-                    return fail(MAGE_EDEVICE);
-            }
-            const uint32_t newest = (R.first + R.count - 1) % NK;
-            const uint32_t zero = 0;
-            if (hipMemcpy(dposes + 12ull * f, &R.pose[12 * newest], 96, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(&b.ctl->halt, &zero, 4, hipMemcpyHostToDevice) != hipSuccess)
+            // write back the changed slots, the frame's pose (= its keyframe's) and clear the halt:
+            // queued on the stream ahead of the next frames (the ring's host copy is not touched
+            // again before the next window's drain)
+            bool any = false;
+            for (uint32_t k = 0; k < NK; k++) any = any || changed[k];
+            // one copy of the mirror from the points on (kf_pts .. kf_aalive: every field the window
+            // changes; the unchanged slots and the associations go back as they came)
+            if (any && hipMemcpyAsync(d + o_kfp, R.mirror.data() + (o_kfp - o_kfkp), o_kfaa + acap * NK - o_kfp,
+                                      hipMemcpyHostToDevice, st) != hipSuccess)
                 return fail(MAGE_EDEVICE);
+            const uint32_t newest = (R.first + R.count - 1) % NK;
+            if (hipMemcpyAsync(dposes + 12ull * f, &R.pose[12 * newest], 96, hipMemcpyHostToDevice, st) != hipSuccess ||
+                hipMemcpyAsync(&b.ctl->halt, R.zero.data(), 4, hipMemcpyHostToDevice, st) != hipSuccess)
+                return fail(MAGE_EDEVICE);
+            prof.mark("write-back");
+            prof.flush();
             next = f + 1;
         }
+        // the last window's write-back reads the pinned ring: done before the ring is freed
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(MAGE_EDEVICE);
     }
     if (hipGetLastError() != hipSuccess) return fail(MAGE_EDEVICE);
     uint32_t rst = 0, lst = 0;
