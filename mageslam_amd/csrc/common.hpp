@@ -223,13 +223,24 @@ mage_status local_map_match_launch(const LocalMapArgs& a, void* scratch, hipStre
 mage_status radius_band_index_launch(const mage_keypoint* d_target_kp, const uint8_t* d_target_desc,
                                      const uint32_t* d_n_target, int64_t target_pitch, uint32_t sets,
                                      unsigned long long* d_keys, float* d_xy, uint32_t* d_desc, hipStream_t st);
+// The tracker's fallback decision after a RadiusMatch pass (PoseEstimator.cpp:439-607: a wider
+// pass runs when this one ran and is weak): once the pass's match count n is final, exec[k + 1] =
+// exec[k] && (n < min_matches || n / ns < ratio) and *nq_next = exec[k + 1] ? ns : 0 (single pair).
+struct RadiusFollow {
+    const uint32_t* ns;
+    uint32_t* exec;
+    uint32_t* nq_next;
+    int k;
+    uint32_t min_matches;
+    double ratio;
+};
 mage_status radius_match_indexed(const mage_keypoint* d_query_kp, const float* d_query_pos, const uint8_t* d_query_desc,
                                  int64_t query_pitch, const uint32_t* d_n_query, const mage_keypoint* d_target_kp,
                                  const uint8_t* d_target_desc, int64_t target_pitch, const uint32_t* d_n_target,
                                  const unsigned long long* d_keys, const float* d_xy, const uint32_t* d_desc,
                                  uint32_t pairs, float radius, int32_t max_distance, int32_t min_difference,
                                  int32_t* d_scratch, mage_dmatch* d_out, uint32_t cap, uint32_t* d_n, uint32_t* d_status,
-                                 hipStream_t st);
+                                 hipStream_t st, const RadiusFollow* follow = nullptr);
 
 // cv::resize(INTER_LINEAR) 8UC1 of one device image (orb.hip, the pyramid's resize_linear_kernel);
 // asynchronous on st.

@@ -58,7 +58,21 @@ struct RadiusParams {
     const unsigned long long* bkeys;
     const float2* bxy;
     const uint4* bdesc;
+    RadiusFollow follow;  // follow.exec == nullptr: none
 };
+
+// The match count of pair pr is final (thread 0): the optional fallback decision (RadiusFollow).
+__device__ __forceinline__ void radius_done(const RadiusParams& p, int pr, uint32_t n)
+{
+    p.n_out[pr] = n;
+    const RadiusFollow& g = p.follow;
+    if (!g.exec) return;
+    const uint32_t ns = *g.ns;
+    const bool weak = n < g.min_matches || (double)n / (double)max(ns, 1u) < g.ratio;
+    const uint32_t run = g.exec[g.k] && weak;
+    g.exec[g.k + 1] = run;
+    *g.nq_next = run ? ns : 0u;
+}
 
 constexpr int RM_GROUP = 16;  // lanes per query (a band holds ~20-150 candidates)
 constexpr int RM_GROUPS = SORT_THREADS / RM_GROUP;
@@ -121,7 +135,7 @@ __device__ void radius_post(const RadiusParams& p, int pr, const int* res, int n
         }
         __syncthreads();
     }
-    if (tid == 0) p.n_out[pr] = (uint32_t)s_base;
+    if (tid == 0) radius_done(p, pr, (uint32_t)s_base);
 }
 
 // blockIdx.y of gridDim.y workgroups handles every gridDim.y-th group slot of the pair's queries
@@ -146,13 +160,13 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_match_kernel(RadiusParams
     const float* qpos = p.qpos ? p.qpos + 2 * pr * p.q_pitch : nullptr;
     int* res = p.res + pr * p.q_pitch;
     if (nq == 0) {  // no queries (the tracker's skipped fallback passes): no target sort either
-        if (FUSED && tid == 0) p.n_out[pr] = 0;
+        if (FUSED && tid == 0) radius_done(p, pr, 0);
         return;
     }
     // a count above its pair's pitch would read the next pair's (or unallocated) entries
     if (ntr > RM_MAXT || ntr > p.t_pitch || nq > p.q_pitch) {
         if (tid == 0 && blockIdx.y == 0) {
-            p.n_out[pr] = 0;
+            radius_done(p, pr, 0);
             atomicOr(p.status, ntr > RM_MAXT ? 1u : 2u);
         }
         return;
@@ -278,7 +292,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radius_post_kernel(RadiusParams 
     const int pr = blockIdx.x;
     const int nq = (int)p.nq[pr], ntr = (int)p.nt[pr];
     if (nq == 0) {
-        if (threadIdx.x == 0) p.n_out[pr] = 0;
+        if (threadIdx.x == 0) radius_done(p, pr, 0);
         return;
     }
     if (ntr > RM_MAXT || ntr > p.t_pitch || nq > p.q_pitch) return;
@@ -473,9 +487,10 @@ mage_status radius_match_indexed(const mage_keypoint* d_query_kp, const float* d
                                  const unsigned long long* d_keys, const float* d_xy, const uint32_t* d_desc,
                                  uint32_t pairs, float radius, int32_t max_distance, int32_t min_difference,
                                  int32_t* d_scratch, mage_dmatch* d_out, uint32_t cap, uint32_t* d_n, uint32_t* d_status,
-                                 hipStream_t st)
+                                 hipStream_t st, const RadiusFollow* follow)
 {
     if (pairs == 0) return MAGE_OK;
+    MAGE_REQUIRE(!follow || pairs == 1, MAGE_EINVAL, "a RadiusFollow decision is per single pair");
     MAGE_REQUIRE(max_distance >= -1 && max_distance <= 256, MAGE_EINVAL, "maxHammingDist must be in [-1, 256]");
     RadiusParams p{};
     p.qkp = d_query_kp;
@@ -498,6 +513,7 @@ mage_status radius_match_indexed(const mage_keypoint* d_query_kp, const float* d
     p.bkeys = d_keys;
     p.bxy = reinterpret_cast<const float2*>(d_xy);
     p.bdesc = reinterpret_cast<const uint4*>(d_desc);
+    if (follow) p.follow = *follow;
     return radius_match_launch(p, pairs, st);
 }
 }  // namespace mage

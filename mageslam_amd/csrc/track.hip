@@ -301,7 +301,7 @@ __global__ __launch_bounds__(TT) void trk_init(TrackBufs b, TrackConst c, const 
     }
 }
 
-__global__ __launch_bounds__(TT) void trk_project(TrackBufs b, TrackConst c, int f, const double* poses)
+__device__ void project_frame(const TrackBufs& b, const TrackConst& c, int f, const double* poses)
 {
     __shared__ float R32[9], t32[3];
     __shared__ uint32_t wsum[TT / 64];
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(TT) void trk_gather(TrackBufs b, TrackConst c, cons
 // frame's associations after TrackLocalMap unassociates the outliers (:116-147): the unassociated
 // keypoint mask, the reference points associated as inliers (visited) and each outlier point's
 // keypoint (hidden from its own local-map search).
-__global__ __launch_bounds__(TT) void trk_filter(TrackBufs b, TrackConst c, const uint32_t* nf_ptr)
+__device__ void filter_frame(const TrackBufs& b, const TrackConst& c, const uint32_t* nf_ptr)
 {
     __shared__ uint32_t wsum[TT / 64];
     const uint32_t n = b.os1[1];
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(TT) void trk_filter(TrackBufs b, TrackConst c, cons
 // through ProjectMapPointIntoCurrentFrame / IsGoodCandidate / ComputeOctave with the pass-1 pose
 // (tracking.py local_map_queries, track.cpp): ordered compaction of the candidates into queries.
 // No pass-1 inlier left (mapPoints.empty(), :149-150) is a lost frame.
-__global__ __launch_bounds__(TT) void trk_lm_project(TrackBufs b, TrackConst c)
+__device__ void lm_project_frame(const TrackBufs& b, const TrackConst& c)
 {
     __shared__ uint32_t wsum[TT / 64];
     const bool off = c.s.local_map_keyframes == 0 || b.ctl->lost;
@@ -565,9 +565,9 @@ __global__ __launch_bounds__(TT) void trk_lm_assemble(TrackBufs b, const mage_ke
     if (threadIdx.x == 0) b.os2[1] = base;
 }
 
-__global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int f, const mage_keypoint* fk,
-                                                 const uint8_t* fd, const uint32_t* nf, double* poses,
-                                                 uint32_t* inliers, uint8_t* keyframe, uint32_t* status)
+__device__ void finish_frame(const TrackBufs& b, const TrackConst& c, int f, const mage_keypoint* fk,
+                             const uint8_t* fd, const uint32_t* nf, double* poses, uint32_t* inliers,
+                             uint8_t* keyframe, uint32_t* status)
 {
     __shared__ uint32_t wsum[TT / 64];
     __shared__ int s_kf;
@@ -645,6 +645,39 @@ __global__ __launch_bounds__(TT) void trk_finish(TrackBufs b, TrackConst c, int 
         __threadfence_system();
         *reinterpret_cast<volatile uint32_t*>(b.prog) = (uint32_t)f;
     }
+}
+
+// The per-frame control kernels, and two fused pairs that save a dependent launch each per frame
+// (the parts are separated by a workgroup barrier: what one part writes to global memory the next
+// reads in the same workgroup).
+__global__ __launch_bounds__(TT) void trk_project(TrackBufs b, TrackConst c, int f, const double* poses)
+{
+    project_frame(b, c, f, poses);
+}
+
+__global__ __launch_bounds__(TT) void trk_filter(TrackBufs b, TrackConst c, const uint32_t* nf_ptr)
+{
+    filter_frame(b, c, nf_ptr);
+}
+
+// trk_filter + trk_lm_project (the local map's candidate queries of the frame)
+__global__ __launch_bounds__(TT) void trk_filter_lm(TrackBufs b, TrackConst c, const uint32_t* nf_ptr)
+{
+    filter_frame(b, c, nf_ptr);
+    __syncthreads();
+    lm_project_frame(b, c);
+}
+
+// trk_finish of frame f + trk_project of frame f + 1 (its prediction needs f's pose and ring)
+__global__ __launch_bounds__(TT) void trk_finish_project(TrackBufs b, TrackConst c, int f, const mage_keypoint* fk,
+                                                         const uint8_t* fd, const uint32_t* nf, double* poses,
+                                                         uint32_t* inliers, uint8_t* keyframe, uint32_t* status,
+                                                         int project_next)
+{
+    finish_frame(b, c, f, fk, fd, nf, poses, inliers, keyframe, status);
+    if (!project_next) return;
+    __syncthreads();
+    project_frame(b, c, f + 1, poses);
 }
 
 }  // namespace
@@ -1091,7 +1124,9 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         return fail(MAGE_EDEVICE);
     hipLaunchKernelGGL(trk_init, dim3(1), dim3(TT), 0, st, b, c, d_kp, d_desc, d_n, dposes, dmt, dil, dkf, rstatus);
     const float radius[3] = {s->search_radius, s->wider_search_radius, s->extra_wider_search_radius};
-    auto enqueue = [&](uint32_t f) -> mage_status {
+    // project: frame f's prediction is its own launch (first frame, first frame after a local BA);
+    // otherwise the previous frame's trk_finish_project made it
+    auto enqueue = [&](uint32_t f, bool project) -> mage_status {
         const mage_keypoint* fk = d_kp + (size_t)f * pitch;
         const uint8_t* fd = d_desc + 32ull * f * pitch;
         const uint32_t* nf = d_n + f;
@@ -1103,23 +1138,25 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
                                                bxy + 2 * slot * pitch, bdesc + 8 * slot * pitch, st)) != MAGE_OK)
                 return rr;
         }
-        launch("track.project", trk_project, dim3(1), dim3(TT), 0, st, b, c, (int)f, (const double*)dposes);
+        if (project) launch("track.project", trk_project, dim3(1), dim3(TT), 0, st, b, c, (int)f, (const double*)dposes);
         for (int k = 0; k < 3; k++) {
+            // passes 0 and 1 end with the fallback decision for the next (trk_weak's, in the pass's
+            // last workgroup: one dependent launch less per pass)
+            const RadiusFollow follow{&b.ctl->ns, b.ctl->exec, b.nq + k + 1, k, s->min_matches, s->small_match_ratio};
             rr = radius_match_indexed(b.qkp, k < 2 ? b.qpos : nullptr, b.qdesc, (int64_t)pitch, b.nq + k, fk, fd,
                                       (int64_t)pitch, nf, bkeys + slot * pitch, bxy + 2 * slot * pitch,
                                       bdesc + 8 * slot * pitch, 1, radius[k], s->max_hamming, s->min_hamming_difference,
-                                      rscratch, b.m + (size_t)k * pitch, pitch, b.mn + k, rstatus, st);
+                                      rscratch, b.m + (size_t)k * pitch, pitch, b.mn + k, rstatus, st,
+                                      k < 2 ? &follow : nullptr);
             if (rr != MAGE_OK) return rr;
-            if (k < 2) launch("track.weak", trk_weak, dim3(1), dim3(64), 0, st, b, c, k);
         }
         launch("track.gather", trk_gather, dim3(1), dim3(TT), 0, st, b, c, fk, (int)f, dmt);
         rr = mage_ba_pose_batch_device(1, b.pos3, b.r9, b.intr4, b.os1, b.pts1, b.uv1, b.info1, s->initial_steps,
                                        s->initial_huber, e1, b.pos3_o1, b.r9_o1, nullptr, b.out1, b.msq, nullptr,
                                        stream);
         if (rr != MAGE_OK) return rr;
-        launch("track.filter", trk_filter, dim3(1), dim3(TT), 0, st, b, c, nf);
         if (s->local_map_keyframes > 0) {
-            launch("track.lm_project", trk_lm_project, dim3(1), dim3(TT), 0, st, b, c);
+            launch("track.filter_lm", trk_filter_lm, dim3(1), dim3(TT), 0, st, b, c, nf);
             LocalMapArgs la{};
             la.qpos = b.lm_qpos;
             la.qoct = b.lm_qoct;
@@ -1139,19 +1176,22 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
             la.keys = bkeys + slot * pitch;
             if ((rr = local_map_match_launch(la, b.lm_scratch, st)) != MAGE_OK) return rr;
             launch("track.lm_assemble", trk_lm_assemble, dim3(1), dim3(TT), 0, st, b, fk);
+        } else {
+            launch("track.filter", trk_filter, dim3(1), dim3(TT), 0, st, b, c, nf);
         }
         rr = mage_ba_pose_batch_device(1, b.pos3_o1, b.r9_o1, b.intr4, b.os2, b.pts2, b.uv2, b.info2, s->final_steps,
                                        s->final_huber, e2, b.pos3_o2, b.r9_o2, nullptr, b.out2, b.msq + 1, nullptr,
                                        stream);
         if (rr != MAGE_OK) return rr;
-        launch("track.finish", trk_finish, dim3(1), dim3(TT), 0, st, b, c, (int)f, fk, fd, nf, dposes, dil, dkf, rstatus);
+        launch("track.finish", trk_finish_project, dim3(1), dim3(TT), 0, st, b, c, (int)f, fk, fd, nf, dposes, dil,
+               dkf, rstatus, (int)(f + 1 < frames));
         return MAGE_OK;
     };
     if (ba_outliers)
         for (uint32_t f = 0; f < frames; f++) ba_outliers[f] = 0xFFFFFFFFu;
     if (!s->local_ba) {
         for (uint32_t f = 1; f < frames; f++)
-            if ((r = enqueue(f)) != MAGE_OK) return fail(r);
+            if ((r = enqueue(f, f == 1)) != MAGE_OK) return fail(r);
     } else {
         // Local BA after every new keyframe (MappingWorker; tracking.py local_bundle_adjust).  The
         // host stays up to two frames ahead; trk_finish of a keyframe frame sets ctl->halt (the
@@ -1178,10 +1218,14 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
         }
         std::vector<uint8_t> changed(NK);
         uint32_t next = 1;
+        bool need_project = true;  // the next enqueued frame makes its own prediction
         constexpr uint32_t DEPTH = 2;
         for (uint32_t f = 1; f < frames; f++) {
-            while (next < frames && next <= f + DEPTH)
-                if ((r = enqueue(next++)) != MAGE_OK) return fail(r);
+            while (next < frames && next <= f + DEPTH) {
+                if ((r = enqueue(next, need_project)) != MAGE_OK) return fail(r);
+                need_project = false;
+                next++;
+            }
             const auto t0 = std::chrono::steady_clock::now();
             while (hp[0] < f) {  // frame f done (trk_finish writes its index last)
                 if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
@@ -1244,6 +1288,7 @@ extern "C" mage_status mage_track_sequence_device(const mage_keypoint* d_kp, con
             prof.mark("write-back");
             prof.flush();
             next = f + 1;
+            need_project = true;
         }
         // the last window's write-back reads the pinned ring: done before the ring is freed
         if (hipStreamSynchronize(st) != hipSuccess) return fail(MAGE_EDEVICE);
