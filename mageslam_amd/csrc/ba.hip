@@ -2073,15 +2073,26 @@ constexpr int CS_BLOCK = 1024;
 constexpr int CS_WAVES = CS_BLOCK / kWave;
 constexpr int CS_MAX_KEYS = 12288;  // per-key counters in LDS (Schur pair keys: nb^2 <= 96^2)
 
+// A pass sorts by the digit (key >> shift) & dmask (dmask = ~0: the whole key, < nkeys); keys
+// beyond CS_MAX_KEYS take several stable passes over CS_DIGIT_BITS-bit digits, least significant
+// first (stable_key_sort).
+constexpr int CS_DIGIT_BITS = 12;
+static_assert((1 << CS_DIGIT_BITS) <= CS_MAX_KEYS, "a digit's counters fit the LDS");
+template <typename KeyT>
+__device__ __forceinline__ int cs_digit(KeyT k, int shift, unsigned dmask)
+{
+    return (int)(((unsigned long long)k >> shift) & dmask);
+}
+
 template <typename KeyT>
 __global__ __launch_bounds__(CS_BLOCK) void csort_count(int n, int nkeys, const KeyT* __restrict__ key,
-                                                        int* __restrict__ hist)
+                                                        int* __restrict__ hist, int shift, unsigned dmask)
 {
     __shared__ int h[CS_MAX_KEYS];
     for (int c = threadIdx.x; c < nkeys; c += CS_BLOCK) h[c] = 0;
     __syncthreads();
     const int i = blockIdx.x * CS_BLOCK + threadIdx.x;
-    if (i < n) atomicAdd(&h[(int)key[i]], 1);
+    if (i < n) atomicAdd(&h[cs_digit(key[i], shift, dmask)], 1);
     __syncthreads();
     int* row = hist + (size_t)blockIdx.x * nkeys;
     for (int c = threadIdx.x; c < nkeys; c += CS_BLOCK) row[c] = h[c];
@@ -2114,7 +2125,8 @@ __global__ __launch_bounds__(1024) void csort_scan(int nblocks, int nkeys, int* 
 template <typename KeyT, typename ValT>
 __global__ __launch_bounds__(CS_BLOCK) void csort_scatter(int n, int nkeys, int kbits, const KeyT* __restrict__ key,
                                                           const ValT* __restrict__ val, const int* __restrict__ hist,
-                                                          KeyT* __restrict__ key_out, ValT* __restrict__ val_out)
+                                                          KeyT* __restrict__ key_out, ValT* __restrict__ val_out,
+                                                          int shift, unsigned dmask)
 {
     __shared__ int cnt[CS_MAX_KEYS];
     const int* row = hist + (size_t)blockIdx.x * nkeys;
@@ -2122,7 +2134,8 @@ __global__ __launch_bounds__(CS_BLOCK) void csort_scatter(int n, int nkeys, int 
     const int i = blockIdx.x * CS_BLOCK + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
     const bool valid = i < n;
-    const int k = valid ? (int)key[i] : -1;
+    const KeyT kfull = valid ? key[i] : (KeyT)0;
+    const int k = valid ? cs_digit(kfull, shift, dmask) : -1;
     // lanes of this wave holding the same key
     unsigned long long peers = __ballot(valid);
     for (int b = 0; b < kbits; b++) {
@@ -2140,7 +2153,7 @@ __global__ __launch_bounds__(CS_BLOCK) void csort_scatter(int n, int nkeys, int 
     }
     base = __shfl(base, leader);
     if (valid) {
-        key_out[base + rank] = (KeyT)k;
+        key_out[base + rank] = kfull;
         val_out[base + rank] = val[i];
     }
 }
@@ -2548,7 +2561,7 @@ struct BundleAdjuster {
         d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
         d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_chist, d_kdst, d_rblk, d_sbits, d_srank, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
-        d_sfinish, d_epos, d_chi_lin, d_livebuf, d_removed, d_camflag, d_ikeys, d_ivals, d_isum, d_iacc, d_ctab;
+        d_sfinish, d_epos, d_chi_lin, d_livebuf, d_removed, d_camflag, d_ikeys, d_ivals, d_isum, d_iacc, d_ctab, d_csort_tmp;
     bool iacc_clean = false;  // d_iacc is all zero (see initialize())
     // outlier lists of the speculative / final post-pass (2 x E entries), written by the kernels
     // straight into host memory: the host sorts and returns them after the completion wait
@@ -2596,7 +2609,7 @@ struct BundleAdjuster {
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
                         &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_chist, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf, &d_removed, &d_camflag,
-                        &d_ikeys, &d_ivals, &d_isum, &d_iacc, &d_ctab})
+                        &d_ikeys, &d_ivals, &d_isum, &d_iacc, &d_ctab, &d_csort_tmp})
             b->retire();  // the stream is synchronised: the blocks are idle (common.hpp block cache)
         h_olist.retire();
         h_state.retire();
@@ -2730,21 +2743,53 @@ struct BundleAdjuster {
         return MAGE_OK;
     }
 
-    // Stable sort of n (key, value) entries by key (< nkeys) with the csort_* kernels.
+    // Stable sort of n (key, value) entries by key (< nkeys) with the csort_* kernels: one pass for
+    // up to CS_MAX_KEYS keys, else stable passes over CS_DIGIT_BITS-bit digits, least significant
+    // first, through a scratch copy (a bundle adjustment with more cameras than the LDS counters).
     template <typename KeyT, typename ValT>
     mage_status stable_key_sort(const KeyT* kin, const ValT* vin, KeyT* kout, ValT* vout, int n, int nkeys)
     {
         if (n <= 0) return MAGE_OK;
-        MAGE_REQUIRE(nkeys <= CS_MAX_KEYS, MAGE_EUNSUPPORTED, "sort key range exceeds the LDS counters");
         const int nblk = (n + CS_BLOCK - 1) / CS_BLOCK;
         mage_status r;
-        if ((r = d_chist.reserve((size_t)nblk * nkeys * sizeof(int))) != MAGE_OK) return r;
         int kbits = 1;
         while ((1 << kbits) < nkeys) kbits++;
-        launch("ba.sort_count", csort_count<KeyT>, dim3(nblk), dim3(CS_BLOCK), 0, st, n, nkeys, kin, d_chist.as<int>());
-        launch("ba.sort_scan", csort_scan, dim3(1), dim3(1024), 0, st, nblk, nkeys, d_chist.as<int>());
-        launch("ba.sort_scatter", csort_scatter<KeyT, ValT>, dim3(nblk), dim3(CS_BLOCK), 0, st, n, nkeys, kbits, kin, vin,
-               (const int*)d_chist.as<int>(), kout, vout);
+        auto pass = [&](const KeyT* ki, const ValT* vi, KeyT* ko, ValT* vo, int ndig, int dbits, int shift,
+                        unsigned dmask) -> mage_status {
+            mage_status rr;
+            if ((rr = d_chist.reserve((size_t)nblk * ndig * sizeof(int))) != MAGE_OK) return rr;
+            launch("ba.sort_count", csort_count<KeyT>, dim3(nblk), dim3(CS_BLOCK), 0, st, n, ndig, ki, d_chist.as<int>(),
+                   shift, dmask);
+            launch("ba.sort_scan", csort_scan, dim3(1), dim3(1024), 0, st, nblk, ndig, d_chist.as<int>());
+            launch("ba.sort_scatter", csort_scatter<KeyT, ValT>, dim3(nblk), dim3(CS_BLOCK), 0, st, n, ndig, dbits, ki, vi,
+                   (const int*)d_chist.as<int>(), ko, vo, shift, dmask);
+            return MAGE_OK;
+        };
+        if (nkeys <= CS_MAX_KEYS) return pass(kin, vin, kout, vout, nkeys, kbits, 0, ~0u);
+        const int npass = (kbits + CS_DIGIT_BITS - 1) / CS_DIGIT_BITS;
+        if ((r = d_csort_tmp.reserve((size_t)n * (sizeof(KeyT) + sizeof(ValT)) * 2 + 256)) != MAGE_OK) return r;
+        KeyT* tk[2] = {d_csort_tmp.as<KeyT>(), nullptr};
+        ValT* tv[2] = {nullptr, nullptr};
+        {
+            char* base = d_csort_tmp.as<char>();
+            const size_t kb = ((size_t)n * sizeof(KeyT) + 127) / 128 * 128, vb = ((size_t)n * sizeof(ValT) + 127) / 128 * 128;
+            tk[0] = reinterpret_cast<KeyT*>(base);
+            tv[0] = reinterpret_cast<ValT*>(base + kb);
+            tk[1] = reinterpret_cast<KeyT*>(base + kb + vb);
+            tv[1] = reinterpret_cast<ValT*>(base + 2 * kb + vb);
+        }
+        const KeyT* ki = kin;
+        const ValT* vi = vin;
+        for (int ps = 0; ps < npass; ps++) {
+            const bool last = ps + 1 == npass;
+            KeyT* ko = last ? kout : tk[ps & 1];
+            ValT* vo = last ? vout : tv[ps & 1];
+            if ((r = pass(ki, vi, ko, vo, 1 << CS_DIGIT_BITS, CS_DIGIT_BITS, ps * CS_DIGIT_BITS,
+                          (1u << CS_DIGIT_BITS) - 1u)) != MAGE_OK)
+                return r;
+            ki = ko;
+            vi = vo;
+        }
         return MAGE_OK;
     }
 

@@ -395,3 +395,26 @@ def test_get_pose_point_outputs_match_fp64_state(gpu):
         assert np.array_equal(pos, qt[:, 4:].astype(np.float32))
         assert np.array_equal(r9.reshape(-1, 3, 3), R.transpose(0, 2, 1).astype(np.float32))
         assert np.array_equal(xyz, p.astype(np.float32))
+
+
+def test_more_cameras_than_lds_sort_counters(gpu):
+    # > CS_MAX_KEYS (12288) cameras: the camera-CSR counting sort takes its multi-pass digit path.
+    # The graph's cameras are the C3-like problem's plus 12300 fixed, unobserved ones interleaved
+    # before them, so the active edges' camera keys span the whole range.
+    import dataclasses
+    g = synth.ba_graph(cameras=24, points=1200, obs_per_point=8, fixed_cameras=6, seed=21)
+    extra = 12300
+    n = len(g.pos) + extra
+    rng = np.random.default_rng(5)
+    slots = np.sort(rng.choice(n, len(g.pos), replace=False))  # where the real cameras land
+    def spread(a, fill):
+        out = np.repeat(fill[None], n, axis=0).astype(a.dtype)
+        out[slots] = a
+        return out
+    g2 = dataclasses.replace(
+        g, pos=spread(g.pos, g.pos[0]), rot=spread(g.rot, g.rot[0]), intr=spread(g.intr, g.intr[0]),
+        fixed=spread(g.fixed, np.uint8(1)), cam=slots[g.cam].astype(np.uint32),
+        true_pos=spread(g.true_pos, g.true_pos[0]), true_rot=spread(g.true_rot, g.true_rot[0]))
+    assert len(g2.pos) > 12288
+    gb, ob = run_pair(g2, 3)
+    compare(gb, ob)
