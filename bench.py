@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--no-pose", action="store_true")
     p.add_argument("--track-frames", type=int, default=1000, help="C4 tracking-loop sequence length (SURVEY §8(d))")
     p.add_argument("--track-warmup", type=int, default=16, help="C4 warm-up frames (untimed run before the timed one)")
-    p.add_argument("--track-parity-frames", type=int, default=240, help="frames of the C4 oracle parity run")
+    p.add_argument("--track-parity-frames", type=int, default=600, help="frames of the C4 oracle parity run (>= 6 local-BA windows)")
     p.add_argument("--no-local-ba", action="store_true", help="C4 without the local BA after each keyframe")
     p.add_argument("--no-tracking", action="store_true")
     p.add_argument("--trajectory-csv", default="", help="rank 0 writes the gathered trajectories (ExportFossilCsv)")
@@ -411,7 +411,7 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
         psum = "pmc_summary_rbrief31.json" if variant == "rbrief31" else "pmc_summary.json"
         traffic, traffic_source = load_pmc(dom, "hbm_bytes_per_launch_fetch_x2", psum)
         traffic_raw, _ = load_pmc(dom, "hbm_bytes_per_launch", psum)
-        valu, _ = load_pmc(dom, "valu_issue_frac", psum)
+        valu, _ = load_pmc(dom, "valu_busy", psum)
         prof_us, _ = load_pmc(dom, "avg_us_steady", psum)
         step_s = el_max / args.steps
         frac_rocprof = None if prof_us is None else per_frame * B / (per_step * prof_us * 1e-6) / 1e9 / HBM_PEAK_GBS
@@ -421,7 +421,7 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
                            # average, and on the whole step (top-level scalars: see "rocprof" / "step")
                            "frac_rocprof": frac_rocprof,
                            "frac_step": per_frame * B / step_s / 1e9 / HBM_PEAK_GBS,
-                           "valu_issue_frac": valu,
+                           "valu_busy": valu,
                            "traffic_raw_fetch": traffic_raw,
                            "traffic_source": traffic_source + " (2 x FETCH_SIZE + WRITE_SIZE)",
                            "algorithmic_bytes_per_launch": per_frame * B,
@@ -438,10 +438,14 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
                            # whole step (extract + match of B frames) against the same bytes
                            "step": {"algorithmic_bytes": per_frame * B, "ms": 1000 * step_s,
                                     "frac": per_frame * B / step_s / 1e9 / HBM_PEAK_GBS},
-                           # what actually binds the kernel: SQ_INSTS_VALU per launch
-                           # over its duration against 1024 SIMDs x 2.4 GHz / 4 cycles, same PMC run
-                           "binding": {"resource": "VALU issue", "frac": valu,
-                                       "source": "SQ_INSTS_VALU pass of the same profile" if valu is not None else traffic_source}}
+                           # what actually binds the kernel: the SIMDs' VALU issue
+                           # occupancy, (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) quad-cycles over the
+                           # launch's GRBM_GUI_ACTIVE cycles (peak 1.0; pure-VALU probe loops read
+                           # 0.93-0.95, profiles/r5_valu_probe_pmc.md), same PMC run
+                           "binding": {"resource": "VALU issue", "frac": valu, "peak": 1.0,
+                                       "calibration": "tools/valu_probe.hip loops: 0.93-0.95",
+                                       "source": "SQ_INSTS_VALU / SQ_ACTIVE_INST_VALU2 / GRBM_GUI_ACTIVE pass of the same profile"
+                                       if valu is not None else traffic_source}}
     return res
 
 

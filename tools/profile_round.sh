@@ -15,7 +15,7 @@ run_set() {  # <out dir> <command...>
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- "$@" > $OUT/trace.json 2> $OUT/trace.err
     timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- "$@" > /dev/null 2> $OUT/fetch.err
     timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- "$@" > /dev/null 2> $OUT/write.err
-    timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES -d $OUT/pmc_valu -o run --output-format csv -- "$@" > /dev/null 2> $OUT/valu.err
+    timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE -d $OUT/pmc_valu -o run --output-format csv -- "$@" > /dev/null 2> $OUT/valu.err
     # only the stats and counter tables come back (gpurun returns <= 64 MiB of gpurun_out/)
     find $OUT -name '*.csv' ! -name run_kernel_stats.csv ! -name run_counter_collection.csv ! -name run_kernel_trace.csv -delete
     find $OUT \( -name run_counter_collection.csv -o -name run_kernel_trace.csv \) -exec gzip -f {} \;

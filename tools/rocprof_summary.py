@@ -31,7 +31,21 @@ def short(name: str) -> str:
     return base
 
 
-VALU_PEAK_G = 1024 * 2.4 / 4.0  # G wave64 VALU instructions / s
+VALU_PEAK_G = 1024 * 2.4 / 4.0  # G wave64 VALU instructions / s at one per quad-cycle (the r1-r4 pricing)
+N_SIMD = 1024
+N_XCD = 8
+
+
+def valu_busy(insts, dual_quads, grbm):
+    """VALU issue occupancy of a launch: each SIMD issues at most one VALU instruction per quad-cycle,
+    or two (one from each of two waves) when both are full-rate forms; SQ_ACTIVE_INST_VALU2 counts
+    those dual quad-cycles.  Quad-cycles with a VALU issue = SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2
+    (summed over the SIMDs); the launch lasted GRBM_GUI_ACTIVE / 8 cycles (one GRBM per XCD).
+    Calibrated on tools/valu_probe.hip (profiles/r5_valu_probe_pmc.md): every pure-VALU loop of the
+    47 forms, full- or half-rate, reads 0.93-0.95 (the rest is its loop branch and ramp)."""
+    if insts is None or dual_quads is None or not grbm:
+        return None
+    return (insts - dual_quads) * 4 / N_SIMD / (grbm / N_XCD)
 
 KERNEL_TAG = {
     "fast_nms_kernel": "orb.fast_nms", "select_kernel": "orb.select", "fast_redo_kernel": "orb.fast_redo",
@@ -123,17 +137,21 @@ def main():
     write = read_pmc(prof / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE", skip)
     valu = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_INSTS_VALU", skip)
     mfma = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_VALU_MFMA_BUSY_CYCLES", skip)
+    dual = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "SQ_ACTIVE_INST_VALU2", skip)
+    grbm = read_pmc(prof / "pmc_valu" / "run_counter_collection.csv", "GRBM_GUI_ACTIVE", skip)
     lines = [f"# rocprofv3 summary — {tag}", "",
              "`rocprofv3 --kernel-trace --stats` (durations) and separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` "
              f"passes of `{cmd}` on one MI355X.  KiB counters converted to bytes; FETCH x2 is the "
              "gfx950 wide-stream correction (MI355X_MICROARCH.md §HBM).", "",
-             "VALU issue: SQ_INSTS_VALU wave-instructions per launch (own pass) over the launch time, against "
-             "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction (614 G/s; tools/valu_probe.hip measures "
-             "~4.6-4.8 cycles per instruction per SIMD for every form used here).", "",
+             "VALU issue (own pass): `VALU busy` = (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) x 4 / (1024 SIMDs x "
+             "GRBM_GUI_ACTIVE / 8) — the quad-cycles in which a SIMD issued VALU work (one instruction, or two "
+             "full-rate ones from two waves) over the launch's cycles; tools/valu_probe.hip loops of every "
+             "form read 0.93-0.95 (profiles/r5_valu_probe_pmc.md).  `VALU G inst/s` is the raw rate; the "
+             "r1-r4 `frac` priced it at one instruction per quad-cycle (614 G/s).", "",
              f"Steady-state columns (avg µs steady, counters) leave out each kernel's first {skip} launches "
              "(the command's warm-up steps; the first ORB batch runs without the candidate gate), from the "
              "per-dispatch kernel trace and counter rows.", "",
-             "| kernel | calls | avg µs (all) | avg µs steady | total ms | % | FETCH MB/launch (raw) | FETCH x2 | WRITE MB/launch | VALU G inst/s | VALU issue frac |",
+             "| kernel | calls | avg µs (all) | avg µs steady | total ms | % | FETCH MB/launch (raw) | FETCH x2 | WRITE MB/launch | VALU G inst/s | VALU busy |",
              "|---|---|---|---|---|---|---|---|---|---|---|"]
     # provenance: the kernel sources the counters were collected on (written on the GPU box by
     # tools/profile_round.sh; bench.py reports traffic only for matching sources)
@@ -161,7 +179,7 @@ def main():
         v = valu.get(k)
         steady = trace[k][1] if k in trace else r["avg_us"]
         vrate = v / (steady * 1e-6) / 1e9 if v is not None and steady > 0 else None
-        vfrac = vrate / VALU_PEAK_G if vrate is not None else None
+        vfrac = valu_busy(v, dual.get(k), grbm.get(k))
         lines.append(f"| {k} | {r['calls']} | {r['avg_us']:.1f} | {steady:.1f} | {r['total_ms']:.2f} | {r['pct']:.1f} | "
                      f"{'' if fmb is None else f'{fmb:.3f}'} | {'' if fmb is None else f'{2 * fmb:.3f}'} | "
                      f"{'' if wmb is None else f'{wmb:.3f}'} | {'' if vrate is None else f'{vrate:.0f}'} | "
@@ -174,7 +192,8 @@ def main():
                                 "write_bytes_per_launch": None if w is None else w * 1024,
                                 "hbm_bytes_per_launch": None if (f is None or w is None) else (f + w) * 1024,
                                 "hbm_bytes_per_launch_fetch_x2": None if (f is None or w is None) else (2 * f + w) * 1024,
-                                "valu_insts_per_launch": v, "valu_issue_frac": vfrac,
+                                "valu_insts_per_launch": v, "valu_busy": vfrac,
+                                "valu_dual_quads_per_launch": dual.get(k), "grbm_gui_active_per_launch": grbm.get(k),
                                 "mfma_busy_cycles_per_launch": mfma.get(k)}
     (out_dir / f"{tag}_rocprof.md").write_text("\n".join(lines) + "\n")
     (out_dir / f"{tag}_pmc_summary.json").write_text(json.dumps(summary, indent=1))
