@@ -45,6 +45,21 @@ __device__ __forceinline__ void d_qmat(const double q[4], double r[9])
     r[8] = 1 - (txx + tyy);
 }
 
+// Eigen's non-positive-trace branch for the largest diagonal element I, with constant indices
+// (indexing m by a run-time i placed the matrix in scratch memory on every call: five stores per
+// call, i.e. per BA edge in update_evaluate)
+template <int I>
+__device__ __forceinline__ void d_quat_case(const double* m, double q[4])
+{
+    constexpr int i = I, j = (i + 1) % 3, k = (j + 1) % 3;
+    double t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
+    q[i] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (m[k * 3 + j] - m[j * 3 + k]) * t;
+    q[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
+    q[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+}
+
 __device__ __forceinline__ void d_quat_from_matrix(const double* m, double q[4])
 {
     double t = m[0] + m[4] + m[8];
@@ -58,14 +73,13 @@ __device__ __forceinline__ void d_quat_from_matrix(const double* m, double q[4])
     } else {
         int i = 0;
         if (m[4] > m[0]) i = 1;
-        if (m[8] > m[i * 4]) i = 2;
-        int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
-        q[i] = 0.5 * t;
-        t = 0.5 / t;
-        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * t;
-        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
-        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+        if (m[8] > (i == 1 ? m[4] : m[0])) i = 2;
+        if (i == 0)
+            d_quat_case<0>(m, q);
+        else if (i == 1)
+            d_quat_case<1>(m, q);
+        else
+            d_quat_case<2>(m, q);
     }
 }
 

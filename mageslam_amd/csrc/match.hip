@@ -620,6 +620,9 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
     if (na > 0 && nb > 0) {
         for (int k = tid; k < 2 * nb; k += FT) reinterpret_cast<uint4*>(bres)[k] = reinterpret_cast<const uint4*>(Bw)[k];
     }
+    // B resident before the first pass's stage fetches read it (other threads' rows; without this
+    // barrier a fetch could read a row not yet written: test_match_random[513-64] caught it)
+    __syncthreads();
     // per-lane accumulator start: register g holds tile row acc_row(g) + 4 h, code 63 - row
     v16f cc;
 #pragma unroll

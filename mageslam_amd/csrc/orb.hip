@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -145,9 +146,9 @@ __host__ __device__ constexpr int ring_dy(int k)
 // B = v - max_k N9[k] with X9 / N9 the 9-arc max / min of the ring values themselves: 9-arc
 // extrema are min3/max3 of three 3-arc extrema.  Every value is an integer (offset 1024), exact
 // in f16, so the packed f16 min3/max3 give the integer result.
-__device__ __forceinline__ h2 fast_raw_ring(h2 v, const h2 (&x)[16])
+// min_k X9[k]: the dark ladder (A = v - lo)
+__device__ __forceinline__ h2 fast_dark_lo(const h2 (&x)[16])
 {
-    // the two ladders one after the other (16 3-arc extrema live at a time, not 32)
     h2 t3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) t3[k] = max3h(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
@@ -155,14 +156,25 @@ __device__ __forceinline__ h2 fast_raw_ring(h2 v, const h2 (&x)[16])
 #pragma unroll
     for (int k = 3; k < 15; k += 2)
         lo = min3h(lo, max3h(t3[k], t3[(k + 3) & 15], t3[(k + 6) & 15]), max3h(t3[k + 1], t3[(k + 4) & 15], t3[(k + 7) & 15]));
-    lo = __builtin_elementwise_minimum(lo, max3h(t3[15], t3[2], t3[5]));  // A = v - lo
+    return __builtin_elementwise_minimum(lo, max3h(t3[15], t3[2], t3[5]));
+}
+// max_k N9[k]: the bright ladder (-B = hi - v)
+__device__ __forceinline__ h2 fast_bright_hi(const h2 (&x)[16])
+{
+    h2 t3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) t3[k] = min3h(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
     h2 hi = max3h(min3h(t3[0], t3[3], t3[6]), min3h(t3[1], t3[4], t3[7]), min3h(t3[2], t3[5], t3[8]));
 #pragma unroll
     for (int k = 3; k < 15; k += 2)
         hi = max3h(hi, min3h(t3[k], t3[(k + 3) & 15], t3[(k + 6) & 15]), min3h(t3[k + 1], t3[(k + 4) & 15], t3[(k + 7) & 15]));
-    hi = __builtin_elementwise_maximum(hi, min3h(t3[15], t3[2], t3[5]));  // -B = hi - v
+    return __builtin_elementwise_maximum(hi, min3h(t3[15], t3[2], t3[5]));
+}
+__device__ __forceinline__ h2 fast_raw_ring(h2 v, const h2 (&x)[16])
+{
+    // the two ladders one after the other (16 3-arc extrema live at a time, not 32)
+    const h2 lo = fast_dark_lo(x);
+    const h2 hi = fast_bright_hi(x);
     return __builtin_elementwise_maximum(v - lo, hi - v);
 }
 
@@ -182,6 +194,16 @@ __device__ __forceinline__ uint32_t score2(h2 raw, h2 tf)
     const h2 step = __builtin_elementwise_minimum(__builtin_elementwise_maximum(raw - tf, zero), one);
     const h2 k1024 = {(_Float16)1024.0f, (_Float16)1024.0f};
     return as_u32(raw * step - step + k1024);
+}
+// The same with the clamp output modifier: step = clamp(raw - t, 0, 1) is 0 or 1 (integers), and
+// (raw - 1) step + 1024 is exact; 3 instructions instead of 6 (the gated pass only: in the
+// exact strips the asm block costs the register allocator its freedom and the kernel spills).
+__device__ __forceinline__ uint32_t score2_clamp(h2 raw, h2 tf)
+{
+    const h2 one = {(_Float16)1.0f, (_Float16)1.0f}, k1024 = {(_Float16)1024.0f, (_Float16)1024.0f};
+    uint32_t step;
+    asm("v_pk_add_f16 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1] clamp" : "=v"(step) : "v"(as_u32(raw)), "v"(as_u32(tf)));
+    return as_u32(__builtin_elementwise_fma(raw - one, as_h2(step), k1024));
 }
 
 __device__ __forceinline__ int reflect101(int i, int n)
@@ -306,9 +328,24 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
 #ifndef MAGE_GATE_ANTIPODAL
 #define MAGE_GATE_ANTIPODAL 1
 #endif
-__device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], int G)
+__device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], int G,
+                                               const FastParams& p, Tile T)
 {
     const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
+    // pixels outside the FAST range [3, w-4] x [3, h-4] are never listed (their score is 0), so
+    // the scoring pass has no range test; only strips at the frame border build the mask
+    uint32_t keep = ~0u;
+    const int X0 = T.x * TW - 4 + 4 * gx, Y0 = T.y * TH - 1 + SR * chunk;
+    if (X0 < 3 || X0 + 3 > p.w - 4 || Y0 < 3 || Y0 + SR - 1 > p.h - 4) {
+        uint32_t rows = 0;
+#pragma unroll
+        for (int r = 0; r < SR; r++)
+            if (Y0 + r >= 3 && Y0 + r <= p.h - 4) rows |= 1u << r;
+        keep = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (X0 + q >= 3 && X0 + q <= p.w - 4) keep |= rows << (8 * q);
+    }
     constexpr int RP = LW / 4;
     const uint32_t* w32 = reinterpret_cast<const uint32_t*>(&img[SR * chunk][0]) + gx;
     const _Float16 g1 = (_Float16)(float)(G + 1);
@@ -352,7 +389,7 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
         const uint32_t sb = __builtin_amdgcn_perm(t2[1], t2[0], 0x07050301u);
         neg |= (sb >> (7 - r)) & (0x01010101u << r);
     }
-    return ~neg;
+    return ~neg & keep;
 }
 
 #ifndef MAGE_FAST_D16
@@ -400,10 +437,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p)
 }
 
 // Exact scores of two listed pixels (score row << 7 | score column) at once, one per f16 lane,
-// with threshold tf; pixels outside the FAST range [3, w-4] x [3, h-4] score 0.  Returns the two
+// with threshold tf (listed pixels lie inside the FAST range, gate_strip).  Returns the two
 // score bytes (a in bits 0-7, b in bits 16-23).
-__device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8_t* scb, const FastParams& p,
-                                             uint32_t ia, uint32_t ib, h2 tf, Tile T)
+#ifndef MAGE_FAST_ONE_SIDE
+#define MAGE_FAST_ONE_SIDE 1
+#endif
+__device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8_t* scb, uint32_t ia, uint32_t ib,
+                                             h2 tf, h2 gp1)
 {
     // LDS centre of score pixel (sr, x): image row sr + 3, column x + 4
     const uint8_t* ca = &img[(ia >> 7) + 3][(ia & 127u) + 4];
@@ -412,10 +452,36 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
 #if MAGE_FAST_D16
     uint32_t ra[17], rb[17];
     ring_d16(lds_addr(ca - 3 * LW - 3), lds_addr(cb - 3 * LW - 3), ra, rb);
+#if MAGE_FAST_ONE_SIDE
+    // One ladder per pixel.  A listed pixel passed gate_strip's dark or bright bound (antipodal
+    // compass pixels 0 / 8 and 4 / 12, the same f16 arithmetic), and a side whose bound fails
+    // scores <= G, i.e. 0 after the threshold G: so only the passing side needs its 9-arc
+    // ladder.  Pixels whose dark bound fails are mirrored (byte ^ 0xFF: the bright segment test
+    // on x is the dark one on 255 - x), so every lane runs the dark ladder; a pixel passing
+    // both bounds (none on the C2 stream) makes the wave also run the other ladder.
+    const uint32_t K = 0x64006400u;
+    const h2 c0 = as_h2(ra[0] | rb[0] | K), c4 = as_h2(ra[4] | rb[4] | K);
+    const h2 c8 = as_h2(ra[8] | rb[8] | K), c12 = as_h2(ra[12] | rb[12] | K);
+    const h2 v0 = as_h2(ra[16] | rb[16] | K);
+    const h2 hic = __builtin_elementwise_minimum(__builtin_elementwise_maximum(c0, c8), __builtin_elementwise_maximum(c4, c12));
+    const h2 loc = __builtin_elementwise_maximum(__builtin_elementwise_minimum(c0, c8), __builtin_elementwise_minimum(c4, c12));
+    const uint32_t dk = as_u32((v0 - loc) - gp1), br = as_u32((hic - v0) - gp1);  // sign set: that bound fails
+    // [m_a, 0x64, m_b, 0x64]: m = 0xFF where the dark bound fails (v_perm sign-byte selectors 8 / 9)
+    const uint32_t M = __builtin_amdgcn_perm(0x64646464u, dk, 0x04090408u);
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = as_h2((ra[k] | rb[k]) ^ M);
+    const h2 v = as_h2((ra[16] | rb[16]) ^ M);
+    h2 raw = v - fast_dark_lo(x);
+    if (__builtin_amdgcn_ballot_w64(((dk | br) & 0x80008000u) != 0x80008000u))
+        raw = __builtin_elementwise_maximum(raw, fast_bright_hi(x) - v);
+    const uint32_t sv = score2_clamp(raw, tf);
+#else
     // [byte_a, 0x64, byte_b, 0x64]: 1024 + byte in both f16 lanes, one full-rate op per pair
 #pragma unroll
     for (int k = 0; k < 16; k++) x[k] = as_h2(__builtin_amdgcn_bitop3_b32(ra[k], rb[k], 0x64006400u, 0xFE));
     const h2 v = as_h2(__builtin_amdgcn_bitop3_b32(ra[16], rb[16], 0x64006400u, 0xFE));
+    const uint32_t sv = score2(fast_raw_ring(v, x), tf);
+#endif
 #else
     auto pack = [](uint32_t a, uint32_t b) { return as_h2((a | (b << 16)) | 0x64006400u); };
 #pragma unroll
@@ -424,14 +490,10 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
         x[k] = pack(ca[off], cb[off]);
     }
     const h2 v = pack(ca[0], cb[0]);
-#endif
     const uint32_t sv = score2(fast_raw_ring(v, x), tf);
-    const int X0 = T.x * TW - 4, Y0 = T.y * TH - 1;
-    auto inside = [&](uint32_t it) {
-        const int X = X0 + (int)(it & 127u), Y = Y0 + (int)(it >> 7);
-        return X >= 3 && X <= p.w - 4 && Y >= 3 && Y <= p.h - 4;
-    };
-    const uint32_t sa = inside(ia) ? (sv & 0xFFu) : 0u, sb = inside(ib) ? ((sv >> 16) & 0xFFu) : 0u;
+#endif
+    // (listed pixels lie inside the FAST range: gate_strip)
+    const uint32_t sa = sv & 0xFFu, sb = (sv >> 16) & 0xFFu;
     scb[(ia >> 7) * (4 * GX) + (ia & 127u)] = (uint8_t)sa;
     scb[(ib >> 7) * (4 * GX) + (ib & 127u)] = (uint8_t)sb;
     return sa | (sb << 16);
@@ -600,7 +662,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
         if (gated) {
             // gated: compass test per strip, then the wave's passing groups scored exactly,
             // compacted over the wave's lanes
-            const uint32_t pix = gate_strip(img, sc, G);
+            const uint32_t pix = gate_strip(img, sc, G, p, T);
             FAST_STAMP(2);
             const uint32_t cnt = __builtin_popcount(pix);
             uint32_t pre = 0;
@@ -631,8 +693,8 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                 // the wave's listed pixels, two per lane; the ones that reach G (the only
                 // possible maxima) are compacted in place to the front of the list for the NMS
                 uint16_t* wl = items[threadIdx.x / kWave];
-                const _Float16 gt = (_Float16)(float)G;
-                const h2 tg = {gt, gt};
+                const _Float16 gt = (_Float16)(float)G, gt1 = (_Float16)(float)(G + 1);
+                const h2 tg = {gt, gt}, tg1 = {gt1, gt1};
                 uint8_t* scb = reinterpret_cast<uint8_t*>(&sc[0][0]);
                 uint32_t nz = 0;
                 for (uint32_t i0 = 0; i0 < total; i0 += 2 * kWave) {
@@ -642,7 +704,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                     if (i < total) {
                         ia = wl[i];
                         ib = i + 1 < total ? wl[i + 1] : ia;
-                        const uint32_t ss = score_pixels(img, scb, p, ia, ib, tg, T);
+                        const uint32_t ss = score_pixels(img, scb, ia, ib, tg, tg1);
                         fa = (ss & 0xFFu) != 0;
                         fb = i + 1 < total && (ss >> 16) != 0;
                     }
@@ -1443,12 +1505,115 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
 #define MAGE_DESC_KPW 4
 #endif
 constexpr int KPW = MAGE_DESC_KPW;
+#ifndef MAGE_DESC_WP_PAD
+#define MAGE_DESC_WP_PAD 0
+#endif
+static_assert(MAGE_DESC_WP_PAD % 16 == 0, "window rows stay 16-byte aligned (b128 stores)");
 #ifndef MAGE_DESC_KP_WIDE
 #define MAGE_DESC_KP_WIDE 1  // keypoints per wave for the rotated (radius 18) windows: describe 0.254 ms per rBRIEF-31 step at 1, 0.306 at 2
 #endif
 
-// MULTI = false (one level, no orientation: the default configuration): level 0 and rotation 0
-// without the per-keypoint level lookups.
+#ifndef MAGE_DESC_COMPACT
+#define MAGE_DESC_COMPACT 1
+#endif
+// f(std::integral_constant<int, j>) for j = 0 .. N-1, unrolled at compile time
+template <int N, int J = 0, class F>
+__device__ __forceinline__ void static_for(F&& f)
+{
+    if constexpr (J < N) {
+        f(std::integral_constant<int, J>{});
+        static_for<N, J + 1>(f);
+    }
+}
+// Compact windows (MAGE_DESC_COMPACT, the default): a keypoint's window is staged as its own
+// BDMAX rows x the 16-byte parts that hold its columns (from x0 & ~15), not as whole bricks:
+// C2 (patch 15): 15 rows x 2 parts = 30 16-byte loads (480 B) per keypoint instead of 5 x 2
+// bricks (80 loads, 1280 B), so two keypoints share one load instruction (lane halves); the
+// lines touched drop from 10 to 5 for the ~55 % of windows inside one 32-byte brick column.
+// LDS rows have an odd number of 16-byte parts, so the 4-5 dwords a row's tests read start 4
+// banks apart for 8 consecutive rows (tests bank as (a / 4) mod 32).
+#if MAGE_DESC_COMPACT
+template <int RB, bool MULTI, int KP>
+__global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
+    DescParams p, const uint32_t* __restrict__ xy_in, const uint32_t* __restrict__ n_in,
+    const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
+{
+    constexpr int BDMAX = 2 * RB + 1;
+    constexpr int NP = (BDMAX + 30) / 16;  // 16-byte parts per window row (any column phase)
+    constexpr int NI = BDMAX * NP;         // 16-byte items per keypoint
+    constexpr int WPC = 16 * (NP | 1);     // LDS row pitch
+    constexpr bool PAIR = !MULTI && NI <= 32 && KP % 2 == 0;  // lanes 0-31 / 32-63: two keypoints
+    constexpr int NLDC = (NI + kWave - 1) / kWave;
+    constexpr int NSLOT = PAIR ? KP / 2 : KP * NLDC;
+    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KP][BDMAX * WPC];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave: scalar
+    // XCD-aware 1-D grid (the whole-brick variant below explains it)
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int chunk = slot % p.chunks, f = (slot / p.chunks) * 8 + xcd;
+    if (f >= p.frames) return;
+    const int k0 = (chunk * DESC_WAVES + wave) * KP;
+    const int n = (int)n_in[f];
+    if (k0 >= n) return;
+    const int R = p.R;
+    // load slot j: keypoint q, item i = row i / NP, part i % NP; keypoints keep the pattern
+    // radius from the border (RunByImageBorder), so the clamps only keep reads inside the level
+    // (a native vector type: HIP's uint4 struct copies stayed memcpys through a private array,
+    // which PromoteAlloca then placed in LDS — 8 KB per workgroup of loads bounced through LDS)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 v[NSLOT];
+    static_for<NSLOT>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int q = PAIR ? 2 * j + (lane >> 5) : j / NLDC;
+        const int i = PAIR ? (lane & 31) : lane + kWave * (j % NLDC);
+        const long long ki = (long long)f * p.out_cap + min(k0 + q, n - 1);
+        const int l = MULTI ? (__builtin_amdgcn_readfirstlane(p.lvl[ki]) >> 8) : 0;  // wave-uniform (no PAIR)
+        const uint32_t xy = xy_in[ki];
+        const uint8_t* src = p.lev.base[l] + (long long)f * p.lev.pitch[l];
+        const int bcols = p.lev.stride[l], brows = (p.lh[MULTI ? l : 0] + 3) >> 2;
+        const int x0 = (int)(xy & 0xFFFFu) - R, y0 = (int)(xy >> 16) - R;
+        const int r = i / NP, pt = i - r * NP;
+        const int gy = min(max(y0 + r, 0), 4 * brows - 1);
+        const int gx = min(max((x0 & ~15) + 16 * pt, 0), 32 * bcols - 16);
+        if (i < NI)
+            v[j] = *reinterpret_cast<const u32x4*>(src + ((long long)(gy >> 2) * bcols + (gx >> 5)) * 128 +
+                                                   (gy & 3) * 32 + (gx & 31));
+    });
+    static_for<NSLOT>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int q = PAIR ? 2 * j + (lane >> 5) : j / NLDC;
+        const int i = PAIR ? (lane & 31) : lane + kWave * (j % NLDC);
+        const int r = i / NP, pt = i - r * NP;
+        if (i < NI) *reinterpret_cast<u32x4*>(&win[wave][q][r * WPC + 16 * pt]) = v[j];
+    });
+    wave_lds_sync();
+    const char4* pat = reinterpret_cast<const char4*>(pattern);
+#pragma unroll
+    for (int q = 0; q < KP; q++) {
+        const int k = k0 + q;
+        if (k >= n) break;
+        const long long ki = (long long)f * p.out_cap + k;
+        const uint32_t xy = xy_in[ki];
+        const int rot = MULTI ? (p.lvl[ki] & 0xFF) : 0;
+        const uint8_t* wb = &win[wave][q][((int)(xy & 0xFFFFu) - R) & 15];  // (x0 & 15): the window's column phase
+        const char4* pr = pat + (p.random ? 0 : rot * 256);  // cvRound(angle / 12) % 30 (:526)
+        float ra = 1.f, rb_ = 0.f;  // random pattern: rotation by the keypoint angle
+        if (p.random) pattern_rotation(p.kp_angle[7 * ki], ra, rb_);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ki * 32);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            char4 e = pr[c * kWave + lane];  // (x0, y0, x1, y1) of bit 64*c + lane
+            if (p.random) e = rotate_test(e, ra, rb_);
+            const int t0 = wb[(R + e.y) * WPC + R + e.x];
+            const int t1 = wb[(R + e.w) * WPC + R + e.z];
+            const unsigned long long m = __ballot(t0 < t1);
+            if (lane == 0) dst[c] = m;
+        }
+    }
+}
+#endif
+// Whole-brick windows (MAGE_DESC_COMPACT=0): MULTI = false (one level, no orientation: the
+// default configuration): level 0 and rotation 0 without the per-keypoint level lookups.
+#if !MAGE_DESC_COMPACT
 template <int RB, bool MULTI, int KP>
 __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     DescParams p, const uint32_t* __restrict__ xy_in, const uint32_t* __restrict__ n_in,
@@ -1459,7 +1624,12 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     constexpr int NBR = (BDMAX + 3 + 3) / 4, NBC = (BDMAX + 31 + 31) / 32;
     constexpr int NIT = NBR * NBC * 8;  // 16-byte items, 8 per brick (one 128-byte line)
     constexpr int NLD = (NIT + kWave - 1) / kWave;
-    constexpr int WP = 32 * NBC;        // LDS window row pitch
+    // LDS window row pitch: 32 NBC bytes + MAGE_DESC_WP_PAD.  The tests' byte reads bank as
+    // (a / 4) mod 32 per 32-lane group; at a 64-byte pitch rows r and r + 2 share their banks
+    // (SQ_LDS_BANK_CONFLICT 43 % of the kernel's cycles).  A 16 / 32 / 48-byte pad spreads the
+    // rows over all banks but costs occupancy (8 -> 6 workgroups per CU): describe 0.138 ->
+    // 0.176 / 0.201 / 0.230 ms on C2 — the kernel is bound by its window gathers, not the LDS.
+    constexpr int WP = 32 * NBC + MAGE_DESC_WP_PAD;
     __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KP][4 * NBR * WP];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave: scalar
     // XCD-aware 1-D grid: workgroups are dispatched round-robin over the 8 XCDs, so block b runs
@@ -1525,6 +1695,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
         }
     }
 }
+#endif
 
 
 // Descriptors with the 7-tap Gaussian computed per keypoint window on the matrix cores instead of
