@@ -613,7 +613,9 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
 }
 
 #ifndef MAGE_FAST_WAVES_PER_EU
-#define MAGE_FAST_WAVES_PER_EU 5  // 86 VGPRs, no spills (tools/ablate_fast.py)
+#define MAGE_FAST_WAVES_PER_EU 6  // 80 VGPRs, a few spilled setup values; with the candidates written straight
+                                  // to global memory (11.3 KB LDS) 12 workgroups per CU: C2 fast_nms 0.362 ->
+                                  // 0.350 ms (5 waves: 86 VGPRs, no spills; 7: 72 VGPRs, 76 B spilled, 0.353)
 #endif
 #ifndef MAGE_FAST_STAMPS
 #define MAGE_FAST_STAMPS 0  // tools/fast_stamps.py: per-phase s_memtime of each wave of frames 0..14
@@ -637,7 +639,19 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
     __shared__ uint32_t sc[SROWS][GX];  // scores; then the blurred tile
-    __shared__ uint32_t list[TCAP];  // the tile's candidates (strict 3x3 maxima are never 8-adjacent)
+#ifndef MAGE_FAST_DIRECT_OUT
+#define MAGE_FAST_DIRECT_OUT 1
+#endif
+    // the tile's candidates (strict 3x3 maxima are never 8-adjacent: <= TCAP): written straight
+    // into the tile's slot of the frame's candidate buffer (MAGE_FAST_DIRECT_OUT; no LDS list and
+    // copy loop: 3.6 KB less LDS per workgroup), or staged in LDS
+    const int tix = T.y * p.tiles_x + T.x;
+    uint32_t* const tile_out = cand + (long long)f * p.cand_cap + (long long)tix * TCAP;
+#if MAGE_FAST_DIRECT_OUT
+    uint32_t* const list = tile_out;
+#else
+    __shared__ uint32_t list[TCAP];
+#endif
     // gated pass: per wave, the pixels (score row << 7 | score column) that may reach the gate;
     // a wave with more than ICAP of them sends its tile through the exact strips (s_dense)
     constexpr uint32_t ICAP = 512;
@@ -868,11 +882,11 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
     // the tile's own slot of the frame's candidate buffer (TCAP entries) and count: no global
     // atomics (the 264 tiles of a 720p frame run at once, and one counter per frame serialised
     // them at the L2)
-    const int tix = T.y * p.tiles_x + T.x;
     const uint32_t n = s_cnt;
     if (threadIdx.x == 0) counts[(long long)f * p.tiles + tix] = n;
-    uint32_t* out = cand + (long long)f * p.cand_cap + (long long)tix * TCAP;
-    for (uint32_t k = threadIdx.x; k < n; k += FAST_THREADS) out[k] = list[k];
+#if !MAGE_FAST_DIRECT_OUT
+    for (uint32_t k = threadIdx.x; k < n; k += FAST_THREADS) tile_out[k] = list[k];
+#endif
     FAST_STAMP(12);
 }
 
