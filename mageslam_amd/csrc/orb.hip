@@ -436,6 +436,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p)
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+// Listed pixel of the gated pass: item = (thread << 5) | bit, bit 8 q + r of the thread's
+// gate_strip mask (GX = 32 groups per strip row, SR = 8 rows), so the listing loop writes
+// `base | bit`.  Score row SR * chunk + r and score column 4 gx + q:
+static_assert(GX == 32 && SR == 8, "item layout");
+__device__ __forceinline__ uint32_t item_row(uint32_t it) { return ((it >> 7) & 0x18u) | (it & 7u); }
+__device__ __forceinline__ uint32_t item_col(uint32_t it) { return __builtin_amdgcn_ubfe(it, 3, 7); }
+
 // Exact scores of two listed pixels (score row << 7 | score column) at once, one per f16 lane,
 // with threshold tf (listed pixels lie inside the FAST range, gate_strip).  Returns the two
 // score bytes (a in bits 0-7, b in bits 16-23).
@@ -446,8 +453,9 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
                                              h2 tf, h2 gp1)
 {
     // LDS centre of score pixel (sr, x): image row sr + 3, column x + 4
-    const uint8_t* ca = &img[(ia >> 7) + 3][(ia & 127u) + 4];
-    const uint8_t* cb = &img[(ib >> 7) + 3][(ib & 127u) + 4];
+    const uint32_t ra_ = item_row(ia), ca_ = item_col(ia), rb_ = item_row(ib), cb_ = item_col(ib);
+    const uint8_t* ca = &img[ra_ + 3][ca_ + 4];
+    const uint8_t* cb = &img[rb_ + 3][cb_ + 4];
     h2 x[16];
 #if MAGE_FAST_D16
     uint32_t ra[17], rb[17];
@@ -494,8 +502,8 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
 #endif
     // (listed pixels lie inside the FAST range: gate_strip)
     const uint32_t sa = sv & 0xFFu, sb = (sv >> 16) & 0xFFu;
-    scb[(ia >> 7) * (4 * GX) + (ia & 127u)] = (uint8_t)sa;
-    scb[(ib >> 7) * (4 * GX) + (ib & 127u)] = (uint8_t)sb;
+    scb[ra_ * (4 * GX) + ca_] = (uint8_t)sa;
+    scb[rb_ * (4 * GX) + cb_] = (uint8_t)sb;
     return sa | (sb << 16);
 }
 
@@ -690,12 +698,12 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                 if (__lane_id() == 0) s_dense = 1u;  // this tile goes through the exact strips
             } else {
                 uint16_t* wl = items[threadIdx.x / kWave];
-                const int gx = threadIdx.x % GX, chunk = threadIdx.x / GX;
+                const uint32_t ibase = threadIdx.x << 5;  // item layout: item_row / item_col
                 uint32_t rb = pix;
                 while (rb) {
                     const int b = __builtin_ctz(rb);
                     rb &= rb - 1u;
-                    wl[pre++] = (uint16_t)(((SR * chunk + (b & 7)) << 7) | (4 * gx + (b >> 3)));
+                    wl[pre++] = (uint16_t)(ibase | (uint32_t)b);
                 }
             }
             FAST_STAMP(3);
@@ -760,7 +768,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
             uint32_t c = 0;
             if (i < total) {
                 const uint32_t it = wl[i];
-                const int sr = (int)(it >> 7), x = (int)(it & 127u);
+                const int sr = (int)item_row(it), x = (int)item_col(it);
                 const int X = T.x * TW + x - 4, Y = T.y * TH + sr - 1;
                 if (sr >= 1 && sr <= TH && x >= 4 && x < TW + 4 && X >= p.xlo && X <= p.xhi && Y >= p.ylo &&
                     Y <= p.yhi) {
