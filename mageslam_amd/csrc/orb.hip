@@ -440,7 +440,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p)
 // gate_strip mask (GX = 32 groups per strip row, SR = 8 rows), so the listing loop writes
 // `base | bit`.  Score row SR * chunk + r and score column 4 gx + q:
 static_assert(GX == 32 && SR == 8, "item layout");
-__device__ __forceinline__ uint32_t item_row(uint32_t it) { return ((it >> 7) & 0x18u) | (it & 7u); }
+__device__ __forceinline__ uint32_t item_row(uint32_t it) { return ((it >> 7) & ~7u) | (it & 7u); }  // it < 4096
 __device__ __forceinline__ uint32_t item_col(uint32_t it) { return __builtin_amdgcn_ubfe(it, 3, 7); }
 
 // Exact scores of two listed pixels (score row << 7 | score column) at once, one per f16 lane,
@@ -663,7 +663,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
     // gated pass: per wave, the pixels (score row << 7 | score column) that may reach the gate;
     // a wave with more than ICAP of them sends its tile through the exact strips (s_dense)
     constexpr uint32_t ICAP = 512;
-    __shared__ uint16_t items[FAST_THREADS / kWave][ICAP];
+    __shared__ __attribute__((aligned(4))) uint16_t items[FAST_THREADS / kWave][ICAP];
     __shared__ uint32_t s_cnt, s_dense;
 #ifndef MAGE_FAST_ABLATE
 #define MAGE_FAST_ABLATE 0  // tools/ablate_fast.py: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load,
@@ -724,8 +724,9 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                     uint32_t ia = 0, ib = 0;
                     bool fa = false, fb = false;
                     if (i < total) {
-                        ia = wl[i];
-                        ib = i + 1 < total ? wl[i + 1] : ia;
+                        const uint32_t pr = *reinterpret_cast<const uint32_t*>(&wl[i]);  // i even: one dword
+                        ia = pr & 0xFFFFu;
+                        ib = i + 1 < total ? pr >> 16 : ia;
                         const uint32_t ss = score_pixels(img, scb, ia, ib, tg, tg1);
                         fa = (ss & 0xFFu) != 0;
                         fb = i + 1 < total && (ss >> 16) != 0;
