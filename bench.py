@@ -399,10 +399,13 @@ def run_orb(args, rank, world, local_rank, torch, dist, variant=None):
     if orb_k:
         dom = ROOF_KERNEL
         per_frame = orb_bytes_per_frame(W, H, N)
-        if variant == "rbrief31":  # + each pyramid level written once and read once
-            per_frame += 2 * pyramid_level_bytes(W, H, RBRIEF31["nlevels"])
+        if variant == "rbrief31":
+            # + each pyramid level read once by FAST (the levels are written by resize_band_kernel,
+            # whose bytes are not charged to fast_nms)
+            per_frame += pyramid_level_bytes(W, H, RBRIEF31["nlevels"])
         # the kernel's time per step: one launch at C2, one per pyramid level for rBRIEF-31 (the
-        # algorithmic bytes are the step's, so they are priced on all of its launches)
+        # path's algorithmic bytes, SURVEY.md §8(d), priced on all of its launches: `frac` is a
+        # single-kernel attribution; `frac_step` prices the same bytes on the whole step)
         per_step = max(1, round(orb_k[dom]["launches"] / max(args.steps, 1)))
         avg_s = orb_k[dom]["avg_ms"] * per_step / 1000.0
         achieved = per_frame * B / avg_s / 1e9
