@@ -533,11 +533,18 @@ constexpr int FT = FW * kWave;       // 1024 threads
 #endif
 constexpr int FRT = MAGE_FP4_RT;     // 32-row A tiles per wave per pass (the column flush serves all)
 constexpr int FROWS = FW * 32 * FRT; // A rows per pass
-constexpr int FSC = FT / 8;          // 128 B columns per LDS stage (one fill dword per thread)
-constexpr int FNT = FSC / 32;        // 4 column tiles per stage
+#ifndef MAGE_FP4_FCOLS
+#define MAGE_FP4_FCOLS 2  // B columns filled per thread per stage: 2 = twice the columns per barrier, two
+                          // stage buffers (C2 match 0.235 -> 0.231 ms; LDS 127 -> 139 KB)
+#endif
+constexpr int FCOLS = MAGE_FP4_FCOLS;
+constexpr int FSC1 = FT / 8;         // columns one fill dword per thread covers
+constexpr int FSC = FCOLS * FSC1;    // B columns per LDS stage
+constexpr int FNT = FSC / 32;        // column tiles per stage
 constexpr int FNB = 2048;            // max B descriptors
 constexpr int FNA = 4096;            // max A descriptors
-constexpr int FBUF = 3;              // stage buffers
+constexpr int FBUF = FCOLS == 1 ? 3 : 2;  // stage buffers (LDS: 160 KB per CU)
+constexpr int FPF = FBUF - 1;        // stages filled ahead
 constexpr uint32_t K16_BASE = 0x2400u;  // low-16 mantissa offset of the accumulator start
 constexpr int K16_D = 272;           // key >> 6 = K16_D - d
 constexpr uint32_t NONE16 = 0x80008000u;
@@ -629,11 +636,23 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
     for (int g = 0; g < 16; g++)
         cc[g] = __builtin_bit_cast(float, (124u << 23) | (K16_BASE + (uint32_t)(63 - acc_row(g) - 4 * (lane >> 5))));
     const int nstages = (nb + FSC - 1) / FSC;
-    const int fs = tid / FSC, fc = tid % FSC;  // stage-fill item: descriptor dword fs of column fc
-    auto fetch = [&](int st) -> uint32_t { return bres[8 * min(st * FSC + fc, nb - 1) + fs]; };
-    auto fill = [&](int buf, int st, uint32_t dw) {
+    const int fs = tid / FSC1, fc0 = tid % FSC1;  // stage-fill items: descriptor dword fs of columns fc0 + k FSC1
+    struct Fetch {
+        uint32_t dw[FCOLS];
+    };
+    auto fetch = [&](int st) -> Fetch {
+        Fetch f;
+#pragma unroll
+        for (int k = 0; k < FCOLS; k++) f.dw[k] = bres[8 * min(st * FSC + fc0 + k * FSC1, nb - 1) + fs];
+        return f;
+    };
+    auto fill = [&](int buf, int st, const Fetch& f) {
         const v4i zero = {0, 0, 0, 0};
-        stage[buf][fc >> 5][fs >> 1][32 * (fs & 1) + (fc & 31)] = st * FSC + fc < nb ? expand32_fp4(dw) : zero;
+#pragma unroll
+        for (int k = 0; k < FCOLS; k++) {
+            const int fc = fc0 + k * FSC1;
+            stage[buf][fc >> 5][fs >> 1][32 * (fs & 1) + (fc & 31)] = st * FSC + fc < nb ? expand32_fp4(f.dw[k]) : zero;
+        }
     };
 
     // the maxDist gate's per-wave statistics (wave-uniform: scalar registers)
@@ -657,10 +676,14 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
 #pragma unroll
             for (int q = 0; q < 8; q++) r1[rt][q] = r2[rt][q] = NONE16;
         {
-            const uint32_t w0 = fetch(0), w1 = nstages > 1 ? fetch(1) : 0u;
+            Fetch w[FPF];
+#pragma unroll
+            for (int j = 0; j < FPF; j++)
+                if (j < nstages) w[j] = fetch(j);
             __syncthreads();  // B resident / column states ready; the previous pass is done with the stages
-            fill(0, 0, w0);
-            if (nstages > 1) fill(1, 1, w1);
+#pragma unroll
+            for (int j = 0; j < FPF; j++)
+                if (j < nstages) fill(j, j, w[j]);
             __syncthreads();
         }
         // global key of a local column key (code = 63 - row in the wave's 64 rows):
@@ -671,7 +694,8 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
         PendingCol16 pc{0, 0, 0, 0, false};
         for (int st = 0; st < nstages; st++) {
             const int buf = st % FBUF;
-            const uint32_t nxt = st + 2 < nstages ? fetch(st + 2) : 0u;
+            Fetch nxt{};
+            if (st + FPF < nstages) nxt = fetch(st + FPF);
             if (active) {
 #pragma unroll
                 for (int ct = 0; ct < FNT; ct++) {
@@ -745,7 +769,7 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                     pc.old = pc.live ? atomicMax(&colM1[pc.j], g1) : NONE;
                 }
             }
-            if (st + 2 < nstages) fill((st + 2) % FBUF, st + 2, nxt);
+            if (st + FPF < nstages) fill((st + FPF) % FBUF, st + FPF, nxt);
             __syncthreads();
         }
         if (pc.live) atomicMax(&colM2[pc.j], pc.old > pc.c1 ? pc.c1 : max(pc.old, pc.c2));
