@@ -1314,13 +1314,83 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
         }
         __syncthreads();  // fill cursors (aliasing keys) are dead now
         SEL_STAMP(8);
+        // Top-N preselection: keys order by minR2 first, so with t the largest minR2 such that at
+        // least N items have minR2 >= t, the N largest keys are among those items.  When they fit
+        // a smaller power of two, only they are sorted (C2: ~2035 of ~2625 -> 2048 keys instead
+        // of 4096); the histogram's last bin collects minR2 >= SEL_HB - 1, where the cut is then
+        // too coarse and the full sort runs.
+        int Psort = P;
+        {
+            constexpr int SEL_HB = 1024;
+            uint32_t* mhist = items;  // dead after the ring search
+            __shared__ int s_thr, s_sel, s_fill;
+            for (int i = tid; i < SEL_HB; i += SEL_THREADS) mhist[i] = 0;
+            if (tid == 0) s_fill = 0;
+            __syncthreads();
 #pragma unroll
-        for (int q = 0; q < KMAX / SEL_THREADS; q++) {
-            int i = tid + q * SEL_THREADS;
-            if (i < P) keys[i] = mykeys[q];
+            for (int q = 0; q < KMAX / SEL_THREADS; q++) {
+                const int i = tid + q * SEL_THREADS;
+                if (i < K) atomicAdd(&mhist[min((int)(mykeys[q] >> 40), SEL_HB - 1)], 1u);
+            }
+            __syncthreads();
+            if (tid < kWave) {  // lane l: bins 16 l .. 16 l + 15; suffix sums, largest bin reaching N
+                constexpr int BPL = SEL_HB / kWave;
+                int sfx[BPL];
+                int run = 0;
+#pragma unroll
+                for (int j = BPL - 1; j >= 0; j--) {
+                    run += (int)mhist[BPL * tid + j];
+                    sfx[j] = run;
+                }
+                int above = run;
+#pragma unroll
+                for (int off = 1; off < kWave; off <<= 1) {
+                    const int o = __shfl_down(above, off);
+                    if (tid + off < kWave) above += o;
+                }
+                above -= run;
+                int tb = -1, cnt = 0;
+#pragma unroll
+                for (int j = 0; j < BPL; j++)
+                    if (sfx[j] + above >= N) {
+                        tb = BPL * tid + j;
+                        cnt = sfx[j] + above;
+                    }
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) {
+                    const int otb = __shfl_xor(tb, m), ocnt = __shfl_xor(cnt, m);
+                    if (otb > tb) {
+                        tb = otb;
+                        cnt = ocnt;
+                    }
+                }
+                if (tid == 0) {
+                    s_thr = tb;
+                    s_sel = cnt;
+                }
+            }
+            __syncthreads();
+            const int tb = s_thr, csel = s_sel;
+            int Pp = SORT_THREADS;
+            while (Pp < csel) Pp <<= 1;
+            if (tb >= 0 && tb < SEL_HB - 1 && Pp < P) {
+#pragma unroll
+                for (int q = 0; q < KMAX / SEL_THREADS; q++) {
+                    const int i = tid + q * SEL_THREADS;
+                    if (i < K && (int)(mykeys[q] >> 40) >= tb) keys[atomicAdd(&s_fill, 1)] = mykeys[q];
+                }
+                for (int i = csel + tid; i < Pp; i += SEL_THREADS) keys[i] = 0ull;
+                Psort = Pp;
+            } else {
+#pragma unroll
+                for (int q = 0; q < KMAX / SEL_THREADS; q++) {
+                    int i = tid + q * SEL_THREADS;
+                    if (i < P) keys[i] = mykeys[q];
+                }
+            }
         }
         __syncthreads();
-        sort_desc(keys, P);
+        sort_desc(keys, Psort);
         SEL_STAMP(9);
     }
 
