@@ -1026,7 +1026,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
         s_maxX = s_maxY = -1;
     }
     // tile offsets: all counts fetched at once, exclusive scan by one wave (in `sorted`, free
-    // until the cell sort); candidate i then lives in tile tile_of(i)
+    // until the cell sort): the candidate count n0 and each tile's count
     const int T = p.tiles;
     uint32_t* tstart = sorted;
     for (int t = tid; t < T; t += SEL_THREADS) tstart[t] = min(CNT[t], (uint32_t)TCAP);
@@ -1051,16 +1051,16 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
     __syncthreads();
     SEL_STAMP(1);
     const int n0 = (int)tstart[T];
-    auto cand_at = [&](int i) {  // tstart[lo] <= i < tstart[hi]
-        int lo = 0, hi = T;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if ((int)tstart[mid] <= i) lo = mid;
-            else hi = mid;
+    // the candidates tile by tile (4 threads per tile slot: no binary search per candidate)
+    auto for_each_cand = [&](auto&& fn) {
+        for (int w = tid; w < 4 * T; w += SEL_THREADS) {
+            const int t = w >> 2;
+            const int e = (int)(tstart[t + 1] - tstart[t]);
+            const uint32_t* ct = C + (long long)t * TCAP;
+            for (int j = w & 3; j < e; j += 4) fn(ct[j]);
         }
-        return C[lo * TCAP + (i - (int)tstart[lo])];
     };
-    for (int i = tid; i < n0; i += SEL_THREADS) atomicAdd(&hist[cand_s(cand_at(i))], 1u);
+    for_each_cand([&](uint32_t c) { atomicAdd(&hist[cand_s(c)], 1u); });
     __syncthreads();
     SEL_STAMP(2);
 
@@ -1122,13 +1122,12 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
     SEL_STAMP(3);
     if (s_mode == 2) return;
     const int cut = s_cut;
-    for (int i = tid; i < n0; i += SEL_THREADS) {
-        const uint32_t c = cand_at(i);
+    for_each_cand([&](uint32_t c) {
         if (cand_s(c) >= cut) {
             int pos = atomicAdd(&s_K, 1);
             if (pos < KMAX) items[pos] = c;
         }
-    }
+    });
     __syncthreads();
     SEL_STAMP(4);
     int K = s_K;
