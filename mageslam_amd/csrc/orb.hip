@@ -348,29 +348,35 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
     }
     constexpr int RP = LW / 4;
     const uint32_t* w32 = reinterpret_cast<const uint32_t*>(&img[SR * chunk][0]) + gx;
-    const _Float16 g1 = (_Float16)(float)(G + 1);
-    const h2 gp1 = {g1, g1};
+    // Pixels as f16 denormals (byte b -> pattern 0x00bb = b * 2^-24; f16 denormals are preserved,
+    // .amdhsa_float_denorm_mode_16_64 3): every difference and comparison is exact as with the
+    // 1024 + b form, and the zero high byte is v_perm's constant selector 0x0C, so any two bytes of
+    // two dwords become a pair in one v_perm (no v_alignbyte for the x +- 3 pixels).
+    auto pr = [](uint32_t s0, uint32_t s1, uint32_t sel) { return as_h2(__builtin_amdgcn_perm(s0, s1, sel)); };
+    const uint32_t g1 = (uint32_t)(G + 1);
+    const h2 gp1 = as_h2(g1 | (g1 << 16));
     // the centre dwords of LDS rows SR*chunk .. +SR+5 as f16 pairs, once: a row is the centre of
     // one score row and the up / down compass pixels of the rows 3 below / above
     h2 cp[SR + 6][2];
 #pragma unroll
     for (int k = 0; k < SR + 6; k++) {
         const uint32_t c = w32[k * RP + 1];
-        cp[k][0] = pair_in(c, 0);
-        cp[k][1] = pair_in(c, 2);
+        cp[k][0] = pr(c, c, 0x0C010C00u);  // pixels x, x + 1
+        cp[k][1] = pr(c, c, 0x0C030C02u);  // x + 2, x + 3
     }
     uint32_t neg = 0;  // bit 8 q + r: pixel q of score row SR*chunk + r fails
 #pragma unroll
     for (int r = 0; r < SR; r++) {
         const uint32_t* rp = w32 + (r + 3) * RP;  // LDS row of score row SR*chunk + r
-        const uint32_t l = rp[0], c = rp[1], n = rp[2];
-        const uint32_t lf = __builtin_amdgcn_alignbyte(c, l, 1);  // x - 3
-        const uint32_t rt = __builtin_amdgcn_alignbyte(n, c, 3);  // x + 3
+        const uint32_t l = rp[0], c = rp[1], n = rp[2];  // bytes x - 4 .., x .., x + 4 ..
+        // x - 3 and x + 3 of pixel pairs (x, x + 1) and (x + 2, x + 3)
+        const h2 ep[2] = {pr(l, l, 0x0C020C01u), pr(c, l, 0x0C040C03u)};
+        const h2 dp[2] = {pr(n, c, 0x0C040C03u), pr(n, n, 0x0C020C01u)};
         uint32_t t2[2];
 #pragma unroll
         for (int P = 0; P < 2; P++) {
             const h2 v = cp[r + 3][P], a = cp[r][P], b = cp[r + 6][P];
-            const h2 e = pair_in(lf, 2 * P), d = pair_in(rt, 2 * P);
+            const h2 e = ep[P], d = dp[P];
 #if MAGE_GATE_ANTIPODAL
             // every 9-arc holds one of the antipodal pixels 0 / 8 (a, b) and one of 4 / 12 (d, e)
             const h2 hi = __builtin_elementwise_minimum(__builtin_elementwise_maximum(a, b), __builtin_elementwise_maximum(d, e));
