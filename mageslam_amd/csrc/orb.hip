@@ -391,9 +391,10 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
 #endif
         }
         sc[SR * chunk + r][gx] = 0u;
-        // the sign bytes of pixels 0..3 (bit 7 of each byte), moved to bits 8 q + r
-        const uint32_t sb = __builtin_amdgcn_perm(t2[1], t2[0], 0x07050301u);
-        neg |= (sb >> (7 - r)) & (0x01010101u << r);
+        // the signs of pixels 0..3 as 0xFF / 0x00 bytes (v_perm sign-extension selectors 8-11:
+        // bits 15 / 31 of each source), kept at bits 8 q + r (one v_bitop3)
+        const uint32_t sb = __builtin_amdgcn_perm(t2[1], t2[0], 0x0B0A0908u);
+        neg |= sb & (0x01010101u << r);
     }
     return ~neg & keep;
 }
