@@ -2278,8 +2278,20 @@ __global__ __launch_bounds__(256) void orient_rows_kernel(mage_keypoint* __restr
         // level for every keypoint (the oriented border ceil(h sqrt 2) >= h + 3 for h >= 5)
         const int qlast = (int)(sh + 2 * h) >> 2;
         uint32_t d[9];
+        if (qlast >= 7) {
+            // dwords 0..7 all hold window bytes: two 16-byte loads (dword aligned) instead of eight
+            // dword loads, a third of the address instructions through the TA
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 a0, a1;
+            __builtin_memcpy(&a0, al, 16);
+            __builtin_memcpy(&a1, al + 4, 16);
+            d[0] = a0[0], d[1] = a0[1], d[2] = a0[2], d[3] = a0[3];
+            d[4] = a1[0], d[5] = a1[1], d[6] = a1[2], d[7] = a1[3];
+            d[8] = qlast >= 8 ? al[8] : 0u;
+        } else {
 #pragma unroll
-        for (int q = 0; q < 9; q++) d[q] = q <= qlast ? al[q] : 0u;
+            for (int q = 0; q < 9; q++) d[q] = q <= qlast ? al[q] : 0u;
+        }
         const uint32_t* mrow = wmask[v < 0 ? -v : v];
 #pragma unroll
         for (int q = 0; q < 8; q++) {
