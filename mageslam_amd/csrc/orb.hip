@@ -222,7 +222,40 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const
 {
     const int gx0 = T.x * TW - 8, gy0 = T.y * TH - 4;
     if (p.qword_ok && gx0 >= 0 && gx0 + LW <= p.w && gy0 >= 0 && gy0 + LH <= p.h) {
-        // interior tile (most of them): 8-byte loads, no reflection, addresses by increment
+        // interior tile (most of them): no reflection, addresses by increment.  A row is 8
+        // sixteen-byte loads + one 8-byte tail (9 threads per row, 14 rows per pass; 16-byte global
+        // loads need only dword alignment), stored as 8-byte LDS writes (rows are 8-byte aligned)
+#ifndef MAGE_FAST_LOAD16
+#define MAGE_FAST_LOAD16 1
+#endif
+#if MAGE_FAST_LOAD16
+        static_assert(LW == 8 * 16 + 8, "row = 8 x 16 + 8 bytes");
+        constexpr int RSTEP = FAST_THREADS / 9, NPASS = (LH + RSTEP - 1) / RSTEP;  // 14 rows per pass, 3 passes
+        const int c = threadIdx.x % 9, r0 = threadIdx.x / 9;
+        if (r0 < RSTEP) {
+            // chunk 8 (the row's last 8 bytes) loads bytes 120..135 and keeps the upper half, so
+            // every load is 16 bytes and stays inside the tile row; all loads issue before the writes
+            const uint8_t* g = src + (long long)(gy0 + r0) * p.stride + gx0 + (c < 8 ? 16 * c : 120);
+            const long long gstep = (long long)RSTEP * p.stride;
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 v[NPASS];
+#pragma unroll
+            for (int k = 0; k < NPASS; k++)
+                if (r0 + k * RSTEP < LH) __builtin_memcpy(&v[k], g + k * gstep, 16);
+#pragma unroll
+            for (int k = 0; k < NPASS; k++) {
+                const int r = r0 + k * RSTEP;
+                if (r >= LH) break;
+                if (c < 8) {
+                    uint2* d = reinterpret_cast<uint2*>(&img[r][16 * c]);
+                    d[0] = make_uint2(v[k][0], v[k][1]);
+                    d[1] = make_uint2(v[k][2], v[k][3]);
+                } else {
+                    *reinterpret_cast<uint2*>(&img[r][128]) = make_uint2(v[k][2], v[k][3]);
+                }
+            }
+        }
+#else
         constexpr int QW = LW / 8, RSTEP = FAST_THREADS / QW;  // 17 qwords per row, 7 rows per pass
         const int c = threadIdx.x % QW, r0 = threadIdx.x / QW;
         if (r0 < RSTEP) {
@@ -232,6 +265,7 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const
             for (int r = r0; r < LH; r += RSTEP, g += gstep)
                 *reinterpret_cast<uint2*>(&img[r][8 * c]) = *reinterpret_cast<const uint2*>(g);
         }
+#endif
         return;
     }
     constexpr int DW = LW / 4;
