@@ -548,6 +548,9 @@ constexpr int FPF = FBUF - 1;        // stages filled ahead
 constexpr uint32_t K16_BASE = 0x2400u;  // low-16 mantissa offset of the accumulator start
 constexpr int K16_D = 272;           // key >> 6 = K16_D - d
 constexpr uint32_t NONE16 = 0x80008000u;
+#ifndef MAGE_FP4_MAX3
+#define MAGE_FP4_MAX3 1  // column top-2 by a tournament + v_pk_maximum3_f16 (17 instead of 20 ops per row tile)
+#endif
 #ifndef MAGE_FP4_GATE
 // 1: skip the fold of 32x32 tiles with no key within maxDist (a v_max3 tree + one ballot per
 // tile), adaptively: a wave stops gating once more than a quarter of its tiles (after 64) held a
@@ -566,6 +569,14 @@ __device__ __forceinline__ uint32_t pkmax(uint32_t a, uint32_t b)
 __device__ __forceinline__ uint32_t pkmin(uint32_t a, uint32_t b)
 {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
+}
+// Three-input max of packed keys on the f16 path (v_pk_maximum3_f16): keys are positive normal
+// f16 values and NONE16 is -0, so the f16 order is the i16 order on every value that occurs.
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pkmax3(uint32_t a, uint32_t b, uint32_t c)
+{
+    const h16x2 m = __builtin_elementwise_maximum(__builtin_bit_cast(h16x2, a), __builtin_bit_cast(h16x2, b));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(m, __builtin_bit_cast(h16x2, c)));
 }
 __device__ __forceinline__ int lo16s(uint32_t v) { return (int)(short)(v & 0xFFFFu); }
 __device__ __forceinline__ int hi16s(uint32_t v) { return (int)v >> 16; }
@@ -734,19 +745,34 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                             r1[rt][q] = pkmax(r1[rt][q], P[q]);
                         }
                         // column: the two best (distance, row) keys of the lane's 16 rows of this tile
+#if MAGE_FP4_MAX3
+                        // a knock-out tournament: every key but the winner loses exactly one
+                        // comparison, so the second best is the best of the 7 losers (3 max3s)
+                        uint32_t h[4], l[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            h[q] = pkmax(P[2 * q], P[2 * q + 1]);
+                            l[q] = pkmin(P[2 * q], P[2 * q + 1]);
+                        }
+                        const uint32_t hh0 = pkmax(h[0], h[1]), hl0 = pkmin(h[0], h[1]);
+                        const uint32_t hh1 = pkmax(h[2], h[3]), hl1 = pkmin(h[2], h[3]);
+                        uint32_t t1 = pkmax(hh0, hh1);
+                        uint32_t t2 = pkmax3(pkmax3(l[0], l[1], l[2]), pkmax3(l[3], hl0, hl1), pkmin(hh0, hh1));
+#else
                         uint32_t t1 = pkmax(P[0], P[1]), t2 = pkmin(P[0], P[1]);
 #pragma unroll
                         for (int q = 2; q < 8; q++) {
                             t2 = pkmax(t2, pkmin(t1, P[q]));
                             t1 = pkmax(t1, P[q]);
                         }
+#endif
                         if (rt > 0) {  // rows 32..63 of the wave: codes 32..63 -> 0..31 (bit 5 cleared)
                             t1 ^= 0x00200020u;
                             t2 ^= 0x00200020u;
                         }
                         const uint32_t lo = pkmin(c1, t1);
                         c1 = pkmax(c1, t1);
-                        c2 = pkmax(pkmax(lo, c2), t2);
+                        c2 = MAGE_FP4_MAX3 ? pkmax3(lo, c2, t2) : pkmax(pkmax(lo, c2), t2);
                     }
                     if (gating && g_tiles >= 64 && 4 * g_hits > g_tiles) gating = false;  // dense: fold all
                     if (!any) continue;  // no key of the column tile within maxDist: no flush
@@ -755,7 +781,7 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                         const uint32_t o1 = (uint32_t)xor32((int)c1, lane), o2 = (uint32_t)xor32((int)c2, lane);
                         const uint32_t lo = pkmin(c1, o1);
                         c1 = pkmax(c1, o1);
-                        c2 = pkmax(pkmax(lo, c2), o2);
+                        c2 = MAGE_FP4_MAX3 ? pkmax3(lo, c2, o2) : pkmax(pkmax(lo, c2), o2);
                     }
                     const int a1 = lo16s(c1), b1 = hi16s(c1);
                     const int m1 = max(a1, b1), m2 = max(min(a1, b1), max(lo16s(c2), hi16s(c2)));

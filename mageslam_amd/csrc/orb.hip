@@ -1649,6 +1649,9 @@ static_assert(MAGE_DESC_WP_PAD % 16 == 0, "window rows stay 16-byte aligned (b12
 #ifndef MAGE_DESC_COMPACT
 #define MAGE_DESC_COMPACT 1
 #endif
+#ifndef MAGE_DESC_HOIST
+#define MAGE_DESC_HOIST 1  // pattern rows loaded once per wave ahead of the windows, 8 LDS reads in flight per keypoint
+#endif
 // f(std::integral_constant<int, j>) for j = 0 .. N-1, unrolled at compile time
 template <int N, int J = 0, class F>
 __device__ __forceinline__ void static_for(F&& f)
@@ -1688,6 +1691,26 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     const int n = (int)n_in[f];
     if (k0 >= n) return;
     const int R = p.R;
+#if MAGE_DESC_HOIST
+    // the tests' pattern rows, issued ahead of the window loads so both round trips overlap
+    // (without orientation the wave's keypoints share one set; the per-keypoint loads of the
+    // loop below had left each of its 4 chunks waiting on an L2 round trip of its own)
+    constexpr int NE = MULTI ? KP : 1;
+    const char4* pat = reinterpret_cast<const char4*>(pattern);
+    char4 e[NE][4];
+    float ang[KP];
+#pragma unroll
+    for (int q = 0; q < NE; q++) {
+        const long long ki = (long long)f * p.out_cap + min(k0 + q, n - 1);
+        const int rot = MULTI ? (p.lvl[ki] & 0xFF) : 0;
+        const char4* pr = pat + (p.random ? 0 : rot * 256);  // cvRound(angle / 12) % 30 (:526)
+#pragma unroll
+        for (int c = 0; c < 4; c++) e[q][c] = pr[c * kWave + lane];  // (x0, y0, x1, y1) of bit 64*c + lane
+    }
+    if (p.random)
+#pragma unroll
+        for (int q = 0; q < KP; q++) ang[q] = p.kp_angle[7 * ((long long)f * p.out_cap + min(k0 + q, n - 1))];
+#endif
     // load slot j: keypoint q, item i = row i / NP, part i % NP; keypoints keep the pattern
     // radius from the border (RunByImageBorder), so the clamps only keep reads inside the level
     // (a native vector type: HIP's uint4 struct copies stayed memcpys through a private array,
@@ -1719,6 +1742,39 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
         if (i < NI) *reinterpret_cast<u32x4*>(&win[wave][q][r * WPC + 16 * pt]) = v[j];
     });
     wave_lds_sync();
+#if MAGE_DESC_HOIST
+#pragma unroll
+    for (int q = 0; q < KP; q++) {
+        const int k = k0 + q;
+        if (k >= n) break;
+        const long long ki = (long long)f * p.out_cap + k;
+        const uint32_t xy = xy_in[ki];
+        const uint8_t* wb = &win[wave][q][((int)(xy & 0xFFFFu) - R) & 15];  // (x0 & 15): the window's column phase
+        char4 eq[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) eq[c] = e[MULTI ? q : 0][c];
+        if (p.random) {  // random pattern: rotation by the keypoint angle
+            float ra, rb_;
+            pattern_rotation(ang[q], ra, rb_);
+#pragma unroll
+            for (int c = 0; c < 4; c++) eq[c] = rotate_test(eq[c], ra, rb_);
+        }
+        int t0[4], t1[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            t0[c] = wb[(R + eq[c].y) * WPC + R + eq[c].x];
+            t1[c] = wb[(R + eq[c].w) * WPC + R + eq[c].z];
+        }
+        // lane c stores the descriptor's 64-bit word c
+        unsigned long long mw = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const unsigned long long m = __ballot(t0[c] < t1[c]);
+            mw = lane == c ? m : mw;
+        }
+        if (lane < 4) reinterpret_cast<unsigned long long*>(desc_out + ki * 32)[lane] = mw;
+    }
+#else
     const char4* pat = reinterpret_cast<const char4*>(pattern);
 #pragma unroll
     for (int q = 0; q < KP; q++) {
@@ -1742,6 +1798,7 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
             if (lane == 0) dst[c] = m;
         }
     }
+#endif
 }
 #endif
 // Whole-brick windows (MAGE_DESC_COMPACT=0): MULTI = false (one level, no orientation: the
