@@ -1037,6 +1037,12 @@ __device__ unsigned long long g_sel_stamps[1024][16];
 #define SEL_STAMP(k)
 #endif
 
+#ifndef MAGE_SEL_CREG
+#define MAGE_SEL_CREG 1  // select's candidate passes from registers (one global read per candidate)
+#endif
+#ifndef MAGE_SEL_RUN4
+#define MAGE_SEL_RUN4 1  // the ANMS square search reads a row's run four items at a time
+#endif
 // Frame f; G is the candidate gate its FAST pass ran with (no gate when G <= fast_threshold).
 #ifndef MAGE_GATE_SHIFT
 #define MAGE_GATE_SHIFT 4  // next gate = lower - lower / 2^MAGE_GATE_SHIFT (15/16: tools/gate_probe.py)
@@ -1093,6 +1099,32 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
     SEL_STAMP(1);
     const int n0 = (int)tstart[T];
     // the candidates tile by tile (4 threads per tile slot: no binary search per candidate)
+#if MAGE_SEL_CREG
+    // the thread's first SEL_CR entries of its tile slot are loaded once, all in flight together,
+    // and kept in registers for both passes below
+    constexpr int SEL_CR = 4;
+    uint32_t creg[SEL_CR];
+    const int tt0 = tid >> 2;
+    const int e0 = tid < 4 * T ? (int)(tstart[tt0 + 1] - tstart[tt0]) : 0;
+    const uint32_t* ct0 = C + (long long)tt0 * TCAP;
+#pragma unroll
+    for (int j = 0; j < SEL_CR; j++) {
+        const int jj = (tid & 3) + 4 * j;
+        creg[j] = jj < e0 ? ct0[jj] : 0u;
+    }
+    auto for_each_cand = [&](auto&& fn) {
+#pragma unroll
+        for (int j = 0; j < SEL_CR; j++)
+            if ((tid & 3) + 4 * j < e0) fn(creg[j]);
+        for (int j = (tid & 3) + 4 * SEL_CR; j < e0; j += 4) fn(ct0[j]);
+        for (int w = tid + SEL_THREADS; w < 4 * T; w += SEL_THREADS) {
+            const int t = w >> 2;
+            const int e = (int)(tstart[t + 1] - tstart[t]);
+            const uint32_t* ct = C + (long long)t * TCAP;
+            for (int j = w & 3; j < e; j += 4) fn(ct[j]);
+        }
+    };
+#else
     auto for_each_cand = [&](auto&& fn) {
         for (int w = tid; w < 4 * T; w += SEL_THREADS) {
             const int t = w >> 2;
@@ -1101,6 +1133,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
             for (int j = w & 3; j < e; j += 4) fn(ct[j]);
         }
     };
+#endif
     for_each_cand([&](uint32_t c) { atomicAdd(&hist[cand_s(c)], 1u); });
     __syncthreads();
     SEL_STAMP(2);
@@ -1313,15 +1346,26 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
                 if (square) {
                     const int x0 = max(cx - (D - 1), 0), x1 = min(cx + (D - 1), numX - 1);
                     const int y0 = max(cy - (D - 1), 0), y1 = min(cy + (D - 1), numY - 1);
+                    auto visit = [&](uint32_t o) {
+                        if ((float)cand_s(o) > sth) {
+                            const int ddx = x - cand_x(o), ddy = y - cand_y(o);
+                            minR2 = min(minR2, ddx * ddx + ddy * ddy);
+                        }
+                    };
                     for (int cYY = y0; cYY <= y1; cYY++) {
                         const uint32_t e = cellStart[cYY * numX + x1 + 1];
-                        for (uint32_t qq = cellStart[cYY * numX + x0]; qq < e; qq++) {
-                            const uint32_t o = sorted[qq];
-                            if ((float)cand_s(o) > sth) {
-                                const int ddx = x - cand_x(o), ddy = y - cand_y(o);
-                                minR2 = min(minR2, ddx * ddx + ddy * ddy);
-                            }
+                        uint32_t qq = cellStart[cYY * numX + x0];
+#if MAGE_SEL_RUN4
+                        // four items of the row's run per step: their LDS reads in flight together
+                        for (; qq + 4 <= e; qq += 4) {
+                            const uint32_t o0 = sorted[qq], o1 = sorted[qq + 1], o2 = sorted[qq + 2], o3 = sorted[qq + 3];
+                            visit(o0);
+                            visit(o1);
+                            visit(o2);
+                            visit(o3);
                         }
+#endif
+                        for (; qq < e; qq++) visit(sorted[qq]);
                     }
                 } else {
                     for (int d = 0; max(0, d - 1) * max(0, d - 1) * mcd2 < minR2; d++) {
