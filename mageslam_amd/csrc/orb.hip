@@ -1685,6 +1685,11 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_kernel(
 #define MAGE_DESC_KPW 4
 #endif
 constexpr int KPW = MAGE_DESC_KPW;
+#ifndef MAGE_DESC_KPW7
+#define MAGE_DESC_KPW7 8  // one level, radius <= 7 (C2): describe 0.074 ms at 4, 0.069-0.071 at 8, 0.091 at 12 or 16,
+                          // 0.095 at 2 (tools/abl.py): more window loads in flight per wave
+#endif
+constexpr int KPW7 = MAGE_DESC_KPW7;
 #ifndef MAGE_DESC_WP_PAD
 #define MAGE_DESC_WP_PAD 0
 #endif
@@ -2981,15 +2986,16 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
                 launch("orb.describe", describe_win_kernel, g3, dim3(DESC_WAVES * kWave), 0, st, dp,
                        (const uint32_t*)o->xy.as<uint32_t>(), d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
             } else if (fused_blur) {
-                // keypoints per wave: 4, or 2 for the wide (rotated, radius > 13) windows, whose
-                // LDS (37 rows x 96 bytes each) otherwise left two workgroups per CU
-                const int kp = dp.R <= 13 ? KPW : MAGE_DESC_KP_WIDE;
+                // keypoints per wave: 8 for one level at radius <= 7, 4 up to radius 13, and
+                // MAGE_DESC_KP_WIDE for the wide (rotated, radius > 13) windows, whose LDS (37 rows
+                // x 96 bytes each) otherwise left two workgroups per CU
+                const int kp = !multi && dp.R <= 7 ? KPW7 : (dp.R <= 13 ? KPW : MAGE_DESC_KP_WIDE);
                 dp.chunks = (int)((cap + DESC_WAVES * kp - 1) / (DESC_WAVES * kp));
                 dp.frames = (int)batch;
                 const dim3 g3((unsigned)(dp.chunks * ((batch + 7) / 8) * 8), 1, 1);
                 auto kern = multi ? (dp.R <= 7 ? describe_blurred_kernel<7, true, KPW>
                                                : (dp.R <= 13 ? describe_blurred_kernel<13, true, KPW> : describe_blurred_kernel<RMAX, true, MAGE_DESC_KP_WIDE>))
-                                  : (dp.R <= 7 ? describe_blurred_kernel<7, false, KPW>
+                                  : (dp.R <= 7 ? describe_blurred_kernel<7, false, KPW7>
                                                : (dp.R <= 13 ? describe_blurred_kernel<13, false, KPW> : describe_blurred_kernel<RMAX, false, MAGE_DESC_KP_WIDE>));
                 launch("orb.describe", kern, g3, dim3(DESC_WAVES * kWave), 0, st, dp, (const uint32_t*)o->xy.as<uint32_t>(),
                        d_n, (const int8_t*)o->pattern.as<int8_t>(), d_desc);
