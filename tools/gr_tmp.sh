@@ -1,4 +1,3 @@
 set -eo pipefail
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/pytest.log 2>&1
 timeout -k 10 600 python3 bench.py > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err
