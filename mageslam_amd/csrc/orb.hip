@@ -2379,6 +2379,11 @@ __global__ __launch_bounds__(256) void orient_kernel(mage_keypoint* __restrict__
 // m_10 = sum (u + half_k) I - half_k sum I and m_01 = v sum I, summed over the rows by shuffles.
 // Integer sums: identical to orient_kernel's per-pixel loop.
 constexpr int OR_ROWS = 32;  // lanes per keypoint
+#ifndef MAGE_OR_KPL
+#define MAGE_OR_KPL 2  // rBRIEF-31 orient 0.188 ms at 1, 0.183 at 2, 0.187 at 4
+#endif
+constexpr int OR_KPL = MAGE_OR_KPL;          // keypoints per half-wave
+constexpr int ORIENT_PER_BLOCK = 8 * OR_KPL;  // keypoints per 256-thread workgroup
 __global__ __launch_bounds__(256) void orient_rows_kernel(mage_keypoint* __restrict__ kp,
                                                           const uint32_t* __restrict__ xy, uint16_t* __restrict__ lvl,
                                                           const uint32_t* __restrict__ n_in, OrientParams p)
@@ -2404,58 +2409,76 @@ __global__ __launch_bounds__(256) void orient_rows_kernel(mage_keypoint* __restr
     const int chunk = slot % p.chunks, f = (slot / p.chunks) * 8 + xcd;
     if (f >= p.frames) return;  // the whole workgroup
     const int lane = threadIdx.x & 63, j = lane & (OR_ROWS - 1);
-    const int k = chunk * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
     const int n = (int)n_in[f];
-    const long long i = (long long)f * p.out_cap + min(k, max(n - 1, 0));
-    const int l = lvl[i] >> 8;
-    const uint32_t c = xy[i];
-    const int cx = (int)(c & 0xFFFFu), cy = (int)(c >> 16);
+    if (n == 0 || chunk * ORIENT_PER_BLOCK >= n) return;  // the whole workgroup (no barrier follows)
     const int v = j - h;
-    uint32_t s1 = 0, sw = 0;  // sum I, sum (u + h) I over the row
-    if (k < n && j <= 2 * h) {
-        const uint8_t* row = p.lev.base[l] + (long long)f * p.lev.pitch[l] + (long long)(cy + v) * p.lev.stride[l] + cx - h;
+    const uint32_t* mrow = wmask[v < 0 ? -v : v];
+    // OR_KPL keypoints per half-wave (ORIENT_PER_BLOCK per workgroup): every load of all of them
+    // is issued before the first one is used
+    int kk[OR_KPL], ll[OR_KPL];
+    long long ii[OR_KPL];
+    uint32_t cc[OR_KPL];
+#pragma unroll
+    for (int t = 0; t < OR_KPL; t++) {
+        kk[t] = chunk * ORIENT_PER_BLOCK + t * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
+        ii[t] = (long long)f * p.out_cap + min(kk[t], max(n - 1, 0));
+        ll[t] = lvl[ii[t]] >> 8;
+        cc[t] = xy[ii[t]];
+    }
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint32_t d[OR_KPL][9], shv[OR_KPL];
+#pragma unroll
+    for (int t = 0; t < OR_KPL; t++) {
+        const int cx = (int)(cc[t] & 0xFFFFu), cy = (int)(cc[t] >> 16);
+        const int l = ll[t];
+        // rows past the window (j > 2h) read the window's last row; their sums are discarded
+        const int vv = min(v, h);
+        const uint8_t* row = p.lev.base[l] + (long long)f * p.lev.pitch[l] + (long long)(cy + vv) * p.lev.stride[l] + cx - h;
         const uintptr_t a = reinterpret_cast<uintptr_t>(row);
         const uint32_t* al = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
         const uint32_t sh = (uint32_t)(a & 3u);
+        shv[t] = sh;
         // only the dwords holding window bytes: the last read byte is x + h + 3 at most, inside the
         // level for every keypoint (the oriented border ceil(h sqrt 2) >= h + 3 for h >= 5)
         const int qlast = (int)(sh + 2 * h) >> 2;
-        uint32_t d[9];
         if (qlast >= 7) {
             // dwords 0..7 all hold window bytes: two 16-byte loads (dword aligned) instead of eight
             // dword loads, a third of the address instructions through the TA
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             u32x4 a0, a1;
             __builtin_memcpy(&a0, al, 16);
             __builtin_memcpy(&a1, al + 4, 16);
-            d[0] = a0[0], d[1] = a0[1], d[2] = a0[2], d[3] = a0[3];
-            d[4] = a1[0], d[5] = a1[1], d[6] = a1[2], d[7] = a1[3];
-            d[8] = qlast >= 8 ? al[8] : 0u;
+            d[t][0] = a0[0], d[t][1] = a0[1], d[t][2] = a0[2], d[t][3] = a0[3];
+            d[t][4] = a1[0], d[t][5] = a1[1], d[t][6] = a1[2], d[t][7] = a1[3];
+            d[t][8] = qlast >= 8 ? al[8] : 0u;
         } else {
 #pragma unroll
-            for (int q = 0; q < 9; q++) d[q] = q <= qlast ? al[q] : 0u;
+            for (int q = 0; q < 9; q++) d[t][q] = q <= qlast ? al[q] : 0u;
         }
-        const uint32_t* mrow = wmask[v < 0 ? -v : v];
+    }
+#pragma unroll
+    for (int t = 0; t < OR_KPL; t++) {
+        uint32_t s1 = 0, sw = 0;  // sum I, sum (u + h) I over the row
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            const uint32_t w = __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh);  // bytes 4q .. 4q+3 of the row
+            const uint32_t w = __builtin_amdgcn_alignbyte(d[t][q + 1], d[t][q], shv[t]);  // bytes 4q .. 4q+3 of the row
             const uint32_t m = mrow[q];
-            const uint32_t pos = 0x03020100u + 0x04040404u * (uint32_t)q;     // byte j = u + h
+            const uint32_t pos = 0x03020100u + 0x04040404u * (uint32_t)q;  // byte j = u + h
             s1 = __builtin_amdgcn_udot4(w, m, s1, false);
             sw = __builtin_amdgcn_udot4(w, pos & (m * 0xFFu), sw, false);
         }
-    }
-    int m10 = (int)sw - h * (int)s1, m01 = v * (int)s1;
+        if (j > 2 * h) s1 = sw = 0;
+        int m10 = (int)sw - h * (int)s1, m01 = v * (int)s1;
 #pragma unroll
-    for (int off = OR_ROWS / 2; off >= 1; off >>= 1) {
-        m10 += __shfl_xor(m10, off);
-        m01 += __shfl_xor(m01, off);
-    }
-    if (j == 0 && k < n) {
-        const float angle = fast_atan2_deg((float)m01, (float)m10);
-        kp[i].angle = angle;
-        const int rot = ((int)rintf(__fdiv_rn(angle, 12.0f))) % 30;  // (:526)
-        lvl[i] = (uint16_t)((l << 8) | rot);
+        for (int off = OR_ROWS / 2; off >= 1; off >>= 1) {
+            m10 += __shfl_xor(m10, off);
+            m01 += __shfl_xor(m01, off);
+        }
+        if (j == 0 && kk[t] < n) {
+            const float angle = fast_atan2_deg((float)m01, (float)m10);
+            kp[ii[t]].angle = angle;
+            const int rot = ((int)rintf(__fdiv_rn(angle, 12.0f))) % 30;  // (:526)
+            lvl[ii[t]] = (uint16_t)((ll[t] << 8) | rot);
+        }
     }
 }
 
@@ -2951,7 +2974,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         }
         if (half >= 5 && half <= 15)  // a disc row per lane, two keypoints per wave
         {
-            op.chunks = (int)((cap + 7) / 8);
+            op.chunks = (int)((cap + ORIENT_PER_BLOCK - 1) / ORIENT_PER_BLOCK);
             op.frames = (int)batch;
             launch("orb.orient", orient_rows_kernel, dim3((unsigned)(op.chunks * ((batch + 7) / 8) * 8)), dim3(256), 0, st,
                    d_kp, o->xy.as<uint32_t>(), o->lvl.as<uint16_t>(), d_n, op);
