@@ -2372,8 +2372,8 @@ __global__ __launch_bounds__(256) void orient_kernel(mage_keypoint* __restrict__
     }
 }
 
-// The same moments with a row per lane (5 <= half_k <= 15: two keypoints per wave, lanes 32 s + j hold
-// row v = j - half_k of keypoint s): the row's 2 half_k + 1 bytes come from 9 aligned dword loads
+// The same moments with a row per lane (5 <= half_k <= 15: lanes 32 s + j hold row v = j - half_k of
+// half-wave s's keypoints, OR_KPL of them per half-wave): the row's 2 half_k + 1 bytes come from 9 aligned dword loads
 // issued together, are realigned to the window start (v_alignbyte), and two v_dot4_u32_u8 per
 // dword against the row's disc mask give sum_u (u + half_k) I and sum_u I; then
 // m_10 = sum (u + half_k) I - half_k sum I and m_01 = v sum I, summed over the rows by shuffles.
@@ -2972,7 +2972,7 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
             op.umax[v] = v0;
             ++v0;
         }
-        if (half >= 5 && half <= 15)  // a disc row per lane, two keypoints per wave
+        if (half >= 5 && half <= 15)  // a disc row per lane, 2 x OR_KPL keypoints per wave
         {
             op.chunks = (int)((cap + ORIENT_PER_BLOCK - 1) / ORIENT_PER_BLOCK);
             op.frames = (int)batch;
