@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--track-warmup", type=int, default=16, help="C4 warm-up frames (untimed run before the timed one)")
     p.add_argument("--track-parity-frames", type=int, default=600, help="frames of the C4 oracle parity run (>= 6 local-BA windows)")
     p.add_argument("--no-local-ba", action="store_true", help="C4 without the local BA after each keyframe")
+    p.add_argument("--track-depth-noise", type=float, default=0.02,
+                   help="C4 depth-error leg: new map points' depth error (rms fraction; 0: leg off)")
     p.add_argument("--no-tracking", action="store_true")
     p.add_argument("--trajectory-csv", default="", help="rank 0 writes the gathered trajectories (ExportFossilCsv)")
     p.add_argument("--cpu-sample-s", type=float, default=12.0, help="budget per CPU baseline leg")
@@ -774,8 +776,10 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
            "local_ba_outliers": int(sum(n for _, n in res.ba_outliers)),
            "pose_rmse_vs_ground_truth": tracking.pose_rmse(res, gt),
            "local_map": f"TrackLocalMap local-map search over the last {ts.local_map_keyframes} keyframes",
-           "local_ba": ("one StepBundleAdjustment per new keyframe over the local map's keyframes (oldest fixed), "
-                        "persisted lambda (MappingWorker.cpp:228-371)") if ts.local_ba else "off",
+           "local_ba": ("one StepBundleAdjustment per new keyframe over the covisibility window of the local map's "
+                        "keyframes (GetMapPointsAndDistantKeyframes: the new keyframe and those sharing >= theta points "
+                        "free, other observers fixed, theta retuned to 1500-2000 associations, ThreadSafeMap.cpp:888-957), "
+                        "persisted lambda and theta (MappingWorker.cpp:228-371)") if ts.local_ba else "off",
            "config": {"workload": f"C4: {T}-frame {args.width}x{args.height} hand-held pan over a textured plane "
                                   f"(synthetic, {TRACK_STEP} units per frame), {args.features} features/frame"
                                   + (f"; C5: {world} independent sequences (seed + rank), one per GPU, RCCL "
@@ -810,7 +814,34 @@ def run_tracking(args, rank, world, local_rank, torch, dist):
                without_local_ba={"track_ms_per_frame": 1000 * (t5 - t4) / T, "keyframes": len(dev_nb.keyframes),
                                  "pose_rmse_vs_ground_truth": tracking.pose_rmse(dev_nb, gt)},
                host_loop_track_ms_per_frame=1000 * (t6 - t5) / T, host_loop_identical=bool(same(host, dev_nb)))
-    return out, (seq, frames, res, feats, ts)
+    # The regime the local BA exists for: new map points carry the depth error a triangulated point
+    # has (NewMapPointsCreation.cpp:254) instead of the plane back-projection's exact depth; the
+    # same frames and features, with and without the local BA (oracle parity in cpu_tracking_baseline)
+    dctx = None
+    if args.track_depth_noise > 0:
+        import dataclasses
+
+        tsd = dataclasses.replace(ts, local_ba=True, map_point_depth_noise=args.track_depth_noise)
+        t7 = time.perf_counter()
+        rd = tracking.track_native_device(d_kp, d_desc, N, d_n, T, K, p0, synth.SCENE_PLANE_Z, settings=tsd)
+        t8 = time.perf_counter()
+        rd_nb = tracking.track_native_device(d_kp, d_desc, N, d_n, T, K, p0, synth.SCENE_PLANE_Z,
+                                             settings=dataclasses.replace(tsd, local_ba=False))
+        out["depth_error"] = {
+            "map_point_depth_noise": tsd.map_point_depth_noise,
+            "what": "new map points' depth x (1 + sigma g), g a seeded unit-variance variate per (keyframe, keypoint) "
+                    "(tracking.depth_noise_factor): a triangulated point's depth error; the same frames and features",
+            "value": T / (t8 - t7 + (t1 - t0)), "unit": "frames/s (extraction of the main leg + this loop)",
+            "track_ms_per_frame": 1000 * (t8 - t7) / T, "keyframes": len(rd.keyframes),
+            "local_ba_windows": len(rd.ba_outliers), "local_ba_outliers": int(sum(n for _, n in rd.ba_outliers)),
+            "local_ba": "covisibility window (GetMapPointsAndDistantKeyframes, ThreadSafeMap.cpp:888-957)",
+            "pose_rmse_vs_ground_truth": tracking.pose_rmse(rd, gt),
+            "without_local_ba": {"keyframes": len(rd_nb.keyframes),
+                                 "pose_rmse_vs_ground_truth": tracking.pose_rmse(rd_nb, gt)}}
+        out["depth_error"]["local_ba_reduces_error"] = bool(
+            out["depth_error"]["pose_rmse_vs_ground_truth"][0] < out["depth_error"]["without_local_ba"]["pose_rmse_vs_ground_truth"][0])
+        dctx = (rd, tsd)
+    return out, (seq, frames, res, feats, ts, dctx)
 
 
 def cpu_tracking_baseline(args, ctx, budget_s):
@@ -821,7 +852,7 @@ def cpu_tracking_baseline(args, ctx, budget_s):
 
     from mageslam_amd import synth, tracking
 
-    seq, frames, gres, gfeats, ts = ctx
+    seq, frames, gres, gfeats, ts, dctx = ctx
     n = min(args.track_parity_frames, len(gres.poses))
     ob = OracleBackend(args.features)
     host = frames[:n].cpu().numpy()
@@ -831,15 +862,23 @@ def cpu_tracking_baseline(args, ctx, budget_s):
     p0 = tracking.Pose(seq.R[0], seq.t[0])
     ores = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, ob, ts)
     el = time.perf_counter() - t0
-    gsub = tracking.TrackResult(poses=gres.poses[:n])
     same = all(np.array_equal(a[0].view(np.uint8), b[0].view(np.uint8)) for a, b in zip(gfeats[:n], feats))
-    gba = [x for x in gres.ba_outliers if x[0] < n]
+    def parity(g, o):
+        gba = [x for x in g.ba_outliers if x[0] < n]
+        return {"frames": n, "keypoints_identical": bool(same),
+                "pose_rmse_gpu_vs_cpu": tracking.pose_rmse(tracking.TrackResult(poses=g.poses[:n]), o),
+                "matches_identical": g.matches[:n] == o.matches, "inliers_identical": g.inliers[:n] == o.inliers,
+                "keyframes_identical": [k for k in g.keyframes if k < n] == o.keyframes,
+                "ba_outliers_identical": gba == o.ba_outliers, "local_ba_windows": len(o.ba_outliers),
+                "local_ba_outliers": int(sum(c for _, c in o.ba_outliers))}
+
+    par = parity(gres, ores)
+    if dctx is not None:  # the depth-error leg: the same oracle features, its settings
+        rd, tsd = dctx
+        par["depth_error"] = parity(rd, tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, ob, tsd))
     return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port", "build": ORACLE_BUILD[0],
             "sample": f"first {n} frames of the same sequence, oracle extract + RadiusMatch + pose BA + local map + "
-                      f"local BA, single thread, {el:.1f} s"}, {
-        "frames": n, "keypoints_identical": bool(same), "pose_rmse_gpu_vs_cpu": tracking.pose_rmse(gsub, ores),
-        "matches_identical": gres.matches[:n] == ores.matches, "keyframes_identical": [k for k in gres.keyframes if k < n] == ores.keyframes,
-        "ba_outliers_identical": gba == ores.ba_outliers, "local_ba_windows": len(ores.ba_outliers)}
+                      f"local BA, single thread, {el:.1f} s"}, par
 
 
 def cpu_ba_baseline(g, budget_s):
@@ -1210,6 +1249,8 @@ def main():
                 track_res["cpu_baseline"] = ct
                 track_res["vs_cpu"] = track_res["value"] / ct["value"]
                 track_res["parity"] = parity
+                if "depth_error" in parity and "depth_error" in track_res:
+                    track_res["depth_error"]["parity"] = parity.pop("depth_error")
             if pose_res is not None:
                 cp = median_of(lambda b: cpu_pose_baseline(pb, b), min(args.cpu_sample_s, 6.0))
                 pose_res["cpu_baseline"] = cp

@@ -74,6 +74,13 @@ typedef void* mage_stream; /* a hipStream_t; NULL = the default stream */
 const char* mage_version(void);
 /* Last error message of the calling thread (empty string if none). */
 const char* mage_last_error(void);
+/* Frees the library's idle cached blocks (device, page-locked and mapped host memory retired by
+ * destroyed per-task objects such as mage_ba) on `device` (-1: every device); returns the bytes
+ * freed.  The cache keeps at most MAGE_POOL_CAP_MB (default 512) MB of idle device memory, a
+ * quarter of that page-locked and a sixteenth mapped, frees blocks no request could use over 256
+ * requests, and is trimmed automatically when an allocation fails.  No reference counterpart
+ * (the reference allocates per task through new / cv::Mat). */
+uint64_t mage_pool_trim(int32_t device);
 
 /* Per-kernel timing: when enabled, every launch is bracketed by HIP events recorded on the
  * stream it is launched on.  The report is one line per kernel: "<name> <launches> <total_ms>". */
@@ -467,7 +474,10 @@ typedef struct mage_track_settings {
     uint32_t final_steps;                                                /* 4 */
     float final_huber;                                                   /* 0.9 */
     double final_max_error;                                              /* 4.5 */
-    float refinement_info;                                               /* 1 - 1/1.5^2 */
+    /* FIXED (deprecated; kept for ABI layout): must equal MapPointRefinementConfidence(0) =
+     * 1 - 1/1.5^2, else MAGE_EINVAL.  Observation information now follows each map point's own
+     * refinement count (MappingMath.h:42-49); the field will be dropped at the next ABI bump. */
+    float refinement_info;
     double keyframe_ratio;                                               /* 0.5 */
     uint32_t keyframe_min;                                               /* 25 */
     /* TrackLocalMap's local-map search between the two pose passes (TrackLocalMap.cpp:114-265,
@@ -483,16 +493,31 @@ typedef struct mage_track_settings {
     uint32_t num_levels;                                                 /* pyramid levels 1 */
     int32_t width, height;                                               /* image size */
     /* Local bundle adjustment after every new keyframe (MappingWorker.cpp:228-371; device loop
-     * only, mage_track_sequence refuses it): the local map's keyframes (oldest fixed), the points
-     * they own that a free one observes, every alive association; one StepBundleAdjustment per
-     * keyframe at MaxOutlierError with the persisted lambda (tracking.py local_bundle_adjust). */
+     * only, mage_track_sequence refuses it): over the local map's keyframes, the free ones and the
+     * points they observe chosen as GetMapPointsAndDistantKeyframes does (ThreadSafeMap.cpp:
+     * 888-957, see ba_free_keyframes), every alive association of those points; one
+     * StepBundleAdjustment per keyframe at MaxOutlierError with the persisted lambda and
+     * covisibility threshold (tracking.py local_bundle_adjust). */
     uint32_t local_ba;                                                   /* 0: off */
     float ba_huber, ba_huber_scale, ba_max_outlier_error;                /* 1.8, 0.95, 7.25 */
     uint32_t ba_steps_per_run;                                           /* NumStepsPerRun 1 */
     float ba_low_connectivity_scale;                                     /* 1.5 */
     uint32_t ba_upper_connections;                                       /* UpperConnectionsForBA 2000 */
     float min_lambda;                                                    /* MappingSettings::MinLambda 1e-3 */
-    uint32_t ba_free_keyframes;  /* the newest keyframes of the window that move (older ones fixed, >= 1): 2 */
+    /* 0 (default): the new keyframe Ki and the keyframes sharing >= theta map points with it are
+     * free, every other observer and the sequence's first keyframe fixed; theta starts at
+     * covis_min_threshold, steps by covis_ba_step while the associations lie outside
+     * [ba_lower_connections, ba_upper_connections] (covis_max_steps + 1 rounds) and persists
+     * across windows.  N > 0: the newest N keyframes of the window free, the older ones fixed. */
+    uint32_t ba_free_keyframes;
+    uint32_t covis_min_threshold;                                        /* CovisMinThreshold 15 */
+    uint32_t covis_ba_step;                                              /* CovisBaStepThreshold 15 */
+    uint32_t ba_lower_connections;                                       /* LowerConnectionsForBA 1500 */
+    uint32_t covis_max_steps;                                            /* MaxSteps 1 */
+    /* New map points' depth x (1 + sigma g), g a seeded unit-variance variate per (keyframe frame,
+     * keypoint) (tracking.py depth_noise_factor): a triangulated point's depth error instead of the
+     * plane back-projection's exact depth.  0: exact. */
+    float map_point_depth_noise;
 } mage_track_settings;
 
 /* Features of `frames` frames (host): keypoints kp[frame_start[f] .. frame_start[f+1]) and their

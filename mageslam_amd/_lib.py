@@ -19,7 +19,7 @@ STATUS_NAMES = {0: "MAGE_OK", 1: "MAGE_EINVAL", 2: "MAGE_EDEVICE", 3: "MAGE_ENOM
 
 # Every entry point declared in include/mage_hot.h (checked by tests/test_capi.py).
 EXPORTS = [
-    "mage_version", "mage_last_error", "mage_profile_enable", "mage_profile_filter", "mage_profile_reset",
+    "mage_version", "mage_last_error", "mage_pool_trim", "mage_profile_enable", "mage_profile_filter", "mage_profile_reset",
     "mage_profile_report", "mage_orb_create", "mage_orb_destroy", "mage_orb_detect_and_compute",
     "mage_orb_detect_and_compute_batch_device", "mage_orb_status", "mage_orb_reset_status",
     "mage_orb_set_fast_gate", "mage_orb_fast_gate_stats",
@@ -103,7 +103,10 @@ class TrackSettingsC(C.Structure):
                 ("local_ba", C.c_uint32), ("ba_huber", C.c_float), ("ba_huber_scale", C.c_float),
                 ("ba_max_outlier_error", C.c_float), ("ba_steps_per_run", C.c_uint32),
                 ("ba_low_connectivity_scale", C.c_float), ("ba_upper_connections", C.c_uint32),
-                ("min_lambda", C.c_float), ("ba_free_keyframes", C.c_uint32)]
+                ("min_lambda", C.c_float), ("ba_free_keyframes", C.c_uint32),
+                ("covis_min_threshold", C.c_uint32), ("covis_ba_step", C.c_uint32),
+                ("ba_lower_connections", C.c_uint32), ("covis_max_steps", C.c_uint32),
+                ("map_point_depth_noise", C.c_float)]
 
 
 class BAStats(C.Structure):
@@ -168,6 +171,7 @@ def _declare(L: C.CDLL) -> None:
 
     sig("mage_version", C.c_char_p)
     sig("mage_last_error", C.c_char_p)
+    sig("mage_pool_trim", C.c_uint64, i32)
     sig("mage_profile_enable", None, i32)
     sig("mage_profile_filter", None, C.c_char_p)
     sig("mage_profile_reset", None)

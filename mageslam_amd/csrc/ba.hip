@@ -2526,6 +2526,7 @@ struct BundleAdjuster {
     // h_ctl on the host, h_ctl_dev in kernels; a trial's results need only the stream sync.
     double* h_ctl = nullptr;
     double* h_ctl_dev = nullptr;
+    size_t ctl_bytes = 0;  // the block's real size (a cached block may be larger than CTL_DOUBLES)
     OutlierCtl* d_octl() const { return reinterpret_cast<OutlierCtl*>(h_ctl_dev + CTL_OUTLIER); }
     const OutlierCtl& h_octl() const { return *reinterpret_cast<const OutlierCtl*>(h_ctl + CTL_OUTLIER); }
     LiveCtl* d_live() const { return reinterpret_cast<LiveCtl*>(d_livebuf.ptr); }
@@ -2602,7 +2603,9 @@ struct BundleAdjuster {
 
     void release()
     {
-        if (st) (void)hipStreamSynchronize(st);  // an eager linearisation may still be running
+        // an eager linearisation may still be running; only blocks of a synchronised stream are
+        // idle and go to the block cache, after a failed synchronisation everything is freed
+        const bool idle = !st || hipStreamSynchronize(st) == hipSuccess;
         for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
@@ -2610,20 +2613,43 @@ struct BundleAdjuster {
                         &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_chist, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf, &d_removed, &d_camflag,
                         &d_ikeys, &d_ivals, &d_isum, &d_iacc, &d_ctab, &d_csort_tmp})
-            b->retire();  // the stream is synchronised: the blocks are idle (common.hpp block cache)
-        h_olist.retire();
-        h_state.retire();
-        h_kb.retire();
-        h_isum.retire();
-        h_stage.retire();
-        h_dma.retire();
+            if (idle)
+                b->retire();  // the stream is synchronised: the blocks are idle (common.hpp block cache)
+            else
+                b->release();
+        if (idle) {
+            h_olist.retire();
+            h_state.retire();
+            h_kb.retire();
+            h_isum.retire();
+            h_stage.retire();
+            h_dma.retire();
+        } else {
+            h_olist.release();
+            h_state.release();
+            h_kb.release();
+            h_isum.release();
+            h_stage.release();
+            h_dma.release();
+        }
         iacc_clean = false;
         stage_off = dma_off = 0;
         pending.k = 0;
-        if (st) mage::stream_retire(st);  // idle (synchronised above)
+        if (st) {
+            if (idle)
+                mage::stream_retire(st);
+            else
+                (void)hipStreamDestroy(st);
+        }
         st = nullptr;
-        if (h_ctl) mage::pool_retire(2, h_ctl, CTL_DOUBLES * sizeof(double));
+        if (h_ctl) {
+            if (idle && ctl_bytes)
+                mage::pool_retire(2, h_ctl, ctl_bytes);
+            else
+                (void)hipHostFree(h_ctl);
+        }
         h_ctl = nullptr;
+        ctl_bytes = 0;
     }
 
     // Host-to-device copies are staged in pinned memory.  Large ones are DMA copies from a pinned
@@ -2767,12 +2793,13 @@ struct BundleAdjuster {
         };
         if (nkeys <= CS_MAX_KEYS) return pass(kin, vin, kout, vout, nkeys, kbits, 0, ~0u);
         const int npass = (kbits + CS_DIGIT_BITS - 1) / CS_DIGIT_BITS;
-        if ((r = d_csort_tmp.reserve((size_t)n * (sizeof(KeyT) + sizeof(ValT)) * 2 + 256)) != MAGE_OK) return r;
+        // two (keys, values) copies, each array starting 128-byte aligned
+        const size_t kb = ((size_t)n * sizeof(KeyT) + 127) / 128 * 128, vb = ((size_t)n * sizeof(ValT) + 127) / 128 * 128;
+        if ((r = d_csort_tmp.reserve(2 * (kb + vb))) != MAGE_OK) return r;
         KeyT* tk[2] = {d_csort_tmp.as<KeyT>(), nullptr};
         ValT* tv[2] = {nullptr, nullptr};
         {
             char* base = d_csort_tmp.as<char>();
-            const size_t kb = ((size_t)n * sizeof(KeyT) + 127) / 128 * 128, vb = ((size_t)n * sizeof(ValT) + 127) / 128 * 128;
             tk[0] = reinterpret_cast<KeyT*>(base);
             tv[0] = reinterpret_cast<ValT*>(base + kb);
             tk[1] = reinterpret_cast<KeyT*>(base + kb + vb);
@@ -3564,8 +3591,10 @@ mage_status mage_ba_create(int32_t points_fixed, int device, mage_ba** out)
     b->st = mage::stream_take();
     b->h_ctl = static_cast<double*>(mage::pool_take(2, mage::BundleAdjuster::CTL_DOUBLES * sizeof(double), &ctl_bytes));
     if ((!b->st && hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking) != hipSuccess) ||
-        (!b->h_ctl && hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), mage::BundleAdjuster::CTL_DOUBLES * sizeof(double),
-                                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) ||
+        (!b->h_ctl && (ctl_bytes = mage::BundleAdjuster::CTL_DOUBLES * sizeof(double),
+                       hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), ctl_bytes,
+                                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)) ||
+        (b->ctl_bytes = ctl_bytes, false) ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&b->h_ctl_dev), b->h_ctl, 0) != hipSuccess ||
         (std::memset(b->h_ctl, 0, mage::BundleAdjuster::CTL_DOUBLES * sizeof(double)), false)) {
         b->release();

@@ -21,10 +21,16 @@ thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 namespace {
+struct PoolBlock {
+    int dev;
+    void* p;
+    uint64_t stamp;  // pool_take requests of this kind when the block was retired
+};
 struct BlockPool {
     std::mutex mu;
-    std::multimap<size_t, std::pair<int, void*>> free[3];  // bytes -> (device, block)
+    std::multimap<size_t, PoolBlock> free[3];  // bytes -> block
     size_t held[3] = {0, 0, 0};
+    uint64_t takes[3] = {0, 0, 0};
     std::vector<std::pair<int, hipStream_t>> streams;
 };
 BlockPool& block_pool()
@@ -32,7 +38,45 @@ BlockPool& block_pool()
     static BlockPool* p = new BlockPool();  // never destroyed: blocks outlive static teardown order
     return *p;
 }
-constexpr size_t kPoolCap[3] = {size_t(2) << 30, size_t(512) << 20, size_t(64) << 20};  // retired bytes kept per kind
+// Retired bytes kept per kind (device / page-locked / mapped): 512 / 128 / 32 MB by default, or
+// MAGE_POOL_CAP_MB (one value for device memory; host kinds get a quarter and a sixteenth of it).
+size_t pool_cap(int kind)
+{
+    static const size_t dev_cap = [] {
+        const char* e = getenv("MAGE_POOL_CAP_MB");
+        const long long mb = e ? atoll(e) : 512;
+        return (size_t)(mb < 0 ? 0 : mb) << 20;
+    }();
+    return kind == 0 ? dev_cap : kind == 1 ? dev_cap / 4 : dev_cap / 16;
+}
+// A block no request could use over this many pool_take calls of its kind is freed for real.
+constexpr uint64_t kPoolMaxAge = 256;
+
+void free_block(int kind, void* p)
+{
+    if (kind == 0)
+        (void)hipFree(p);
+    else
+        (void)hipHostFree(p);  // page-locked (1) and mapped (2) host memory
+}
+// Frees (under P.mu) the idle blocks of `kind` on `dev` (all of them, or the ones older than
+// kPoolMaxAge requests); returns the bytes freed.
+size_t trim_locked(BlockPool& P, int kind, int dev, bool all)
+{
+    size_t freed = 0;
+    for (auto it = P.free[kind].begin(); it != P.free[kind].end();) {
+        const PoolBlock& b = it->second;
+        if ((dev < 0 || b.dev == dev) && (all || P.takes[kind] - b.stamp > kPoolMaxAge)) {
+            free_block(kind, b.p);
+            freed += it->first;
+            P.held[kind] -= it->first;
+            it = P.free[kind].erase(it);
+        } else {
+            ++it;
+        }
+    }
+    return freed;
+}
 }  // namespace
 
 void* pool_take(int kind, size_t n, size_t* got)
@@ -41,16 +85,29 @@ void* pool_take(int kind, size_t n, size_t* got)
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     BlockPool& P = block_pool();
     std::lock_guard<std::mutex> lk(P.mu);
+    P.takes[kind]++;
     // the smallest retired block that fits and wastes at most half of itself
     for (auto it = P.free[kind].lower_bound(n); it != P.free[kind].end() && it->first <= 2 * n + 4096; ++it)
-        if (it->second.first == dev) {
-            void* p = it->second.second;
+        if (it->second.dev == dev) {
+            void* p = it->second.p;
             *got = it->first;
             P.held[kind] -= it->first;
             P.free[kind].erase(it);
             return p;
         }
+    // a miss allocates anyway: free the blocks no request has been able to use for a while
+    trim_locked(P, kind, dev, false);
     return nullptr;
+}
+
+size_t pool_trim(int kind, int device)
+{
+    BlockPool& P = block_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    size_t freed = 0;
+    for (int k = 0; k < 3; k++)
+        if (kind < 0 || kind == k) freed += trim_locked(P, k, device, true);
+    return freed;
 }
 
 // Idle non-blocking streams of destroyed per-task objects (mage_ba), per device.
@@ -88,14 +145,11 @@ void pool_retire(int kind, void* p, size_t bytes)
     (void)hipGetDevice(&dev);
     BlockPool& P = block_pool();
     std::lock_guard<std::mutex> lk(P.mu);
-    if (P.held[kind] + bytes > kPoolCap[kind]) {  // over the cap: a real free
-        if (kind == 0)
-            (void)hipFree(p);
-        else
-            (void)hipHostFree(p);  // page-locked (1) and mapped (2) host memory
+    if (P.held[kind] + bytes > pool_cap(kind)) {  // over the cap: a real free
+        free_block(kind, p);
         return;
     }
-    P.free[kind].emplace(bytes, std::make_pair(dev, p));
+    P.free[kind].emplace(bytes, PoolBlock{dev, p, P.takes[kind]});
     P.held[kind] += bytes;
 }
 const char* last_error() { return g_last_error.c_str(); }
@@ -338,6 +392,7 @@ extern "C" {
 
 const char* mage_version(void) { return "mageslam_amd 0.1.0 (gfx950)"; }
 const char* mage_last_error(void) { return mage::last_error(); }
+uint64_t mage_pool_trim(int32_t device) { return (uint64_t)mage::pool_trim(-1, device); }
 
 void mage_profile_enable(int32_t enable) { mage::g_profiling.store(enable != 0); }
 

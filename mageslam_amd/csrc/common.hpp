@@ -47,6 +47,14 @@ mage_status bind_device(int device);
 // Kind 0: device memory, 1: page-locked host memory, 2: mapped (coherent) host memory.  Thread safe.
 void* pool_take(int kind, size_t n, size_t* got);
 void pool_retire(int kind, void* p, size_t bytes);
+// Frees the idle blocks of `kind` (-1: every kind) on `device` (-1: every device) for real;
+// returns the bytes freed.  The buffers below call it when an allocation fails and retry once.
+size_t pool_trim(int kind, int device);
+inline int current_device()
+{
+    int d = 0;
+    return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
 hipStream_t stream_take();  // an idle retired stream of the current device, or nullptr
 void stream_retire(hipStream_t s);
 
@@ -60,7 +68,9 @@ struct DeviceBuffer {
         ptr = nullptr;
         bytes = 0;
         if ((ptr = pool_take(0, n, &bytes)) != nullptr) return MAGE_OK;
-        if (hipMalloc(&ptr, n) != hipSuccess) {
+        if (hipMalloc(&ptr, n) != hipSuccess &&
+            (pool_trim(0, current_device()) == 0 || hipMalloc(&ptr, n) != hipSuccess)) {
+            ptr = nullptr;
             set_error("hipMalloc of " + std::to_string(n) + " bytes failed");
             return MAGE_ENOMEM;
         }
@@ -96,7 +106,9 @@ struct PinnedBuffer {
         ptr = nullptr;
         bytes = 0;
         if ((ptr = pool_take(1, n, &bytes)) != nullptr) return MAGE_OK;
-        if (hipHostMalloc(&ptr, n, hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc(&ptr, n, hipHostMallocDefault) != hipSuccess &&
+            (pool_trim(1, current_device()) == 0 || hipHostMalloc(&ptr, n, hipHostMallocDefault) != hipSuccess)) {
+            ptr = nullptr;
             set_error("hipHostMalloc of " + std::to_string(n) + " bytes failed");
             return MAGE_ENOMEM;
         }
@@ -134,8 +146,9 @@ struct MappedBuffer {
             ptr = nullptr;
             bytes = 0;
         }
-        if (hipHostMalloc(&ptr, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) {
+        auto alloc = [&] { return hipHostMalloc(&ptr, n, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess; };
+        if (!alloc() && (ptr = nullptr, pool_trim(2, current_device()) == 0 || !alloc())) ptr = nullptr;
+        if (!ptr || hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) {
             release();
             set_error("mapped hipHostMalloc of " + std::to_string(n) + " bytes failed");
             return MAGE_ENOMEM;

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "depth_noise.hpp"
 
 namespace {
 
@@ -112,9 +113,10 @@ void map_point_attributes(Keyframe& kf, const Pose& p, const float fmax[8], cons
     }
 }
 
-// keypoint rays of `pose` meet the plane Z = plane_z
+// keypoint rays of `pose` meet the plane Z = plane_z (the ray parameter scaled by the seeded
+// depth error of keyframe `fid` when sigma > 0, depth_noise.hpp)
 void backproject(const mage_keypoint* kp, uint32_t n, const Pose& p, const double K[4], double plane_z,
-                 std::vector<float>& out)
+                 std::vector<float>& out, uint32_t fid = 0, float sigma = 0.f)
 {
     const double fx = K[0], fy = K[1], cx = K[2], cy = K[3];
     const double* R = p.R;
@@ -125,7 +127,8 @@ void backproject(const mage_keypoint* kp, uint32_t n, const Pose& p, const doubl
         const double u = ((double)kp[i].x - cx) / fx, v = ((double)kp[i].y - cy) / fy;
         double d[3];
         for (int j = 0; j < 3; j++) d[j] = (u * R[j] + v * R[3 + j]) + R[6 + j];
-        const double lam = (plane_z - C[2]) / d[2];
+        double lam = (plane_z - C[2]) / d[2];
+        if (sigma != 0.f) lam = lam * mage::depth_noise_factor(fid, i, sigma);
         for (int j = 0; j < 3; j++) out[3 * i + j] = (float)(C[j] + lam * d[j]);
     }
 }
@@ -201,7 +204,7 @@ extern "C" mage_status mage_track_sequence(const mage_keypoint* kp, const uint8_
         k.id = f;
         k.kp.assign(frame_kp(f), frame_kp(f) + frame_n(f));
         k.desc.assign(frame_desc(f), frame_desc(f) + 32ull * frame_n(f));
-        backproject(k.kp.data(), frame_n(f), p, K, plane_z, k.pts);
+        backproject(k.kp.data(), frame_n(f), p, K, plane_z, k.pts, f, s->map_point_depth_noise);
         map_point_attributes(k, p, fmax, fmin);
         return k;
     };

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "depth_noise.hpp"
 
 namespace mage {
 namespace {
@@ -215,7 +216,7 @@ __device__ void world_position(const double* R, const double* t, float C[3])
 // plane and their MapPoint::UpdateMeanViewDirectionAndDistances attributes (track.cpp
 // map_point_attributes).
 __device__ void make_keyframe(const TrackBufs& b, const TrackConst& c, uint32_t slot, const mage_keypoint* fk,
-                              const uint8_t* fd, uint32_t nf, const DPose& P)
+                              const uint8_t* fd, uint32_t nf, const DPose& P, uint32_t fid)
 {
     const double fx = c.K[0], fy = c.K[1], cx = c.K[2], cy = c.K[3];
     const double* R = P.R;
@@ -236,7 +237,8 @@ __device__ void make_keyframe(const TrackBufs& b, const TrackConst& c, uint32_t 
         const double u = ((double)fk[i].x - cx) / fx, v = ((double)fk[i].y - cy) / fy;
         double dd[3];
         for (int j = 0; j < 3; j++) dd[j] = (u * R[j] + v * R[3 + j]) + R[6 + j];
-        const double lam = (c.plane_z - C[2]) / dd[2];
+        double lam = (c.plane_z - C[2]) / dd[2];
+        if (c.s.map_point_depth_noise != 0.f) lam = lam * depth_noise_factor(fid, i, c.s.map_point_depth_noise);
         float Pp[3];
         for (int j = 0; j < 3; j++) Pp[j] = (float)(C[j] + lam * dd[j]);
         for (int j = 0; j < 3; j++) b.kf_pts[3 * (o + i) + j] = Pp[j];
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(TT) void trk_init(TrackBufs b, TrackConst c, const 
                                                uint32_t* inliers, uint8_t* keyframe, uint32_t* status)
 {
     const uint32_t n = frame_count(c, nf, status);
-    make_keyframe(b, c, 0, fk, fd, n, load_pose(poses));
+    make_keyframe(b, c, 0, fk, fd, n, load_pose(poses), 0u);
     if (threadIdx.x == 0) {
         b.ctl->kf_first = 0;
         b.ctl->kf_count = 1;
@@ -615,7 +617,7 @@ __device__ void finish_frame(const TrackBufs& b, const TrackConst& c, int f, con
     __syncthreads();
     if (s_kf) {
         const uint32_t n = frame_count(c, nf, status);
-        make_keyframe(b, c, s_slot, fk, fd, n, load_pose(sP));
+        make_keyframe(b, c, s_slot, fk, fd, n, load_pose(sP), f);
         // its associations: the pass-2 inliers in observation order (ordered compaction)
         const uint32_t n2 = b.os2[1];
         int4* as = b.kf_assoc + (size_t)s_slot * c.acap;
@@ -761,9 +763,11 @@ struct HostRing {
     Pinned<uint32_t> zero;  // the halt word's clear value
 };
 
-struct LocalBA {  // MappingWorker's CurrentLambda, persisted across the windows
+struct LocalBA {  // MappingWorker's CurrentLambda and CosVisThreashold, persisted across the windows
     bool have_lambda = false;
     float lambda = 0.f;
+    bool have_theta = false;
+    uint32_t theta = 0;
 };
 
 struct BundlerHandle {  // a fresh BundlerLib per window (BundleAdjust.cpp MakeBundler)
@@ -852,12 +856,51 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
                 obs.push_back({r, (uint32_t)ow, (uint32_t)e.y, bits_float(e.z), bits_float(e.w), 1, a});
         }
     }
-    // points a free camera observes, ascending (owner, index): a dense (ring position, index) map
-    // instead of a sorted key list (the window build runs between frames, on the loop's critical path)
-    const uint32_t nfix = nr > c.s.ba_free_keyframes ? nr - c.s.ba_free_keyframes : 1u;  // the oldest are fixed
+    // the window's points, ascending (owner, index): a dense (ring position, index) map instead of
+    // a sorted key list (the window build runs between frames, on the loop's critical path)
     std::vector<int32_t> pmap((size_t)nr * R.cap, -1);
-    for (const Obs& ob : obs)
-        if (ob.cam >= nfix) pmap[(size_t)ob.owner * R.cap + ob.idx] = 0;
+    uint32_t freemask = 0;
+    if (c.s.ba_free_keyframes > 0) {
+        // the newest ba_free_keyframes free, the oldest fixed (at least one); the points they observe
+        const uint32_t nfix = nr > c.s.ba_free_keyframes ? nr - c.s.ba_free_keyframes : 1u;
+        for (uint32_t r = nfix; r < nr; r++) freemask |= 1u << r;
+        for (const Obs& ob : obs)
+            if (ob.cam >= nfix) pmap[(size_t)ob.owner * R.cap + ob.idx] = 0;
+    } else {
+        // GetMapPointsAndDistantKeyframes (ThreadSafeMap.cpp:888-957; tracking.py covisible_window):
+        // per point the mask of ring keyframes observing it; the covisibility weight of keyframe r
+        // to the newest one is the count of points both observe (CovisibilityGraph.cpp:131-170)
+        std::vector<uint8_t> seen((size_t)nr * R.cap, 0);
+        for (const Obs& ob : obs) seen[(size_t)ob.owner * R.cap + ob.idx] |= (uint8_t)(1u << ob.cam);
+        const uint32_t last = nr - 1;
+        uint32_t weight[NKMAX] = {};
+        for (uint8_t m : seen)
+            if (m >> last & 1u)
+                for (uint32_t r = 0; r < last; r++) weight[r] += m >> r & 1u;
+        uint32_t theta = L.have_theta ? L.theta : c.s.covis_min_threshold, kc = 0;
+        for (uint32_t step = 0; step <= c.s.covis_max_steps; step++) {
+            kc = 1u << last;
+            for (uint32_t r = 0; r < last; r++)
+                if (weight[r] >= theta) kc |= 1u << r;
+            size_t n_assoc = 0;
+            for (const Obs& ob : obs) n_assoc += (seen[(size_t)ob.owner * R.cap + ob.idx] & kc) != 0;
+            if (n_assoc > c.s.ba_upper_connections) {
+                theta += c.s.covis_ba_step;
+                continue;
+            }
+            if (n_assoc < c.s.ba_lower_connections && theta > c.s.covis_min_threshold) {
+                theta -= c.s.covis_ba_step;
+                continue;
+            }
+            break;
+        }
+        L.theta = theta;
+        L.have_theta = true;
+        for (size_t q = 0; q < seen.size(); q++)
+            if (seen[q] & kc) pmap[q] = 0;
+        for (uint32_t r = 0; r < nr; r++)  // the map's first keyframe stays fixed (ThreadSafeMap.cpp:89)
+            if ((kc >> r & 1u) && R.id[slot_of[r]] != 0) freemask |= 1u << r;
+    }
     std::vector<uint64_t> keys;
     for (uint32_t r = 0; r < nr; r++)
         for (uint32_t i = 0; i < R.cap; i++)
@@ -881,7 +924,7 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
         uv.push_back(ob.u);
         uv.push_back(ob.v);
     }
-    if (kept.empty()) return MAGE_OK;
+    if (kept.empty() || freemask == 0) return MAGE_OK;
     const uint32_t P = (uint32_t)keys.size(), E = (uint32_t)kept.size();
     std::vector<float> xyz(3ull * P);
     std::vector<uint32_t> pref(P);
@@ -895,7 +938,7 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
     // cameras: view-space t, Eigen column-major R, {cx, cy, fx, fy}; the oldest fixed
     std::vector<float> pos3(3 * nr), r9(9 * nr), intr(4 * nr);
     std::vector<uint8_t> fixed(nr, 0);
-    for (uint32_t r = 0; r < nfix; r++) fixed[r] = 1;
+    for (uint32_t r = 0; r < nr; r++) fixed[r] = (freemask >> r & 1u) ? 0 : 1;
     for (uint32_t r = 0; r < nr; r++) {
         const double* ps = &R.pose[12 * slot_of[r]];
         for (int i = 0; i < 3; i++) pos3[3 * r + i] = (float)ps[9 + i];
@@ -950,7 +993,8 @@ mage_status host_local_ba(HostRing& R, const TrackConst& c, LocalBA& L, int devi
             R.aalive[(size_t)sl * R.acap + ob.src] = 0;
         slot_changed[sl] = 1;
     }
-    for (uint32_t r = nfix; r < nr; r++) {
+    for (uint32_t r = 0; r < nr; r++) {
+        if (!(freemask >> r & 1u)) continue;
         double* ps = &R.pose[12 * slot_of[r]];
         for (int rr = 0; rr < 3; rr++)
             for (int cc = 0; cc < 3; cc++) ps[3 * rr + cc] = (double)r9_o[9 * r + 3 * cc + rr];

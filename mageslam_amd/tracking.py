@@ -38,6 +38,8 @@ class TrackerSettings:
     min_hamming_difference: int = 1        # OrbMatcherSettings::MinHammingDifference
     initial_ba: tuple = (3, 4.0, 6.0)      # steps, Huber width, MaxOutlierErrorPoseEstimation
     final_ba: tuple = (4, 0.9, 4.5)        # steps, Huber width, MaxOutlierError
+    # FIXED (deprecated): must stay MapPointRefinementConfidence(0) = 1 - 1/1.5^2 (ValueError
+    # otherwise); the information of an observation follows its point's refinement count
     refinement_info: float = float(np.float32(1.0) - np.float32(1.0) / np.float32(1.5) ** 2)  # count 0
     # NewKeyFrameDecision.cpp:196: a new keyframe when the frame tracks fewer than overlap x the
     # reference keyframe's map points + KeyframeDecisionMinTrackingPointCount; the overlap is the
@@ -71,7 +73,21 @@ class TrackerSettings:
     ba_low_connectivity_scale: float = 1.5  # ::LowConnectivityIterationsScale
     ba_upper_connections: int = 2000       # CovisibilitySettings::UpperConnectionsForBA
     min_lambda: float = 1e-3               # MappingSettings::MinLambda (PersistLambda on)
-    ba_free_keyframes: int = 2             # the newest keyframes of the window move, the older ones are fixed
+    # The window's free keyframes.  0 (default): GetMapPointsAndDistantKeyframes' rule
+    # (ThreadSafeMap.cpp:888-957) — the new keyframe Ki and the ring keyframes sharing at least
+    # theta map points with it are free, every other observer is fixed (as is the sequence's first
+    # keyframe, ThreadSafeMap.cpp:89), theta retuned until the associations lie in
+    # [ba_lower_connections, ba_upper_connections] and persisted across windows.  N > 0: the
+    # newest N ring keyframes free and the older ones fixed (the round-4/5 harness rule, studies).
+    ba_free_keyframes: int = 0
+    covis_min_threshold: int = 15          # CovisibilitySettings::CovisMinThreshold (theta's start and floor)
+    covis_ba_step: int = 15                # ::CovisBaStepThreshold
+    ba_lower_connections: int = 1500       # ::LowerConnectionsForBA
+    covis_max_steps: int = 1               # ::MaxSteps (the retune loop runs MaxSteps + 1 times)
+    # New map points' depth scaled by 1 + sigma g (g a seeded unit-variance variate per (keyframe
+    # frame, keypoint)): the depth error a triangulated point carries (NewMapPointsCreation.cpp:254),
+    # instead of the plane back-projection's exact depth; 0 = exact.
+    map_point_depth_noise: float = 0.0
 
     def __post_init__(self):
         # every loop takes an observation's information from MapPointRefinementConfidence of its
@@ -173,12 +189,33 @@ def world_position_f32(pose: Pose) -> np.ndarray:
     return C
 
 
+DEPTH_NOISE_SEED = 0xDE9785EED
+_DEPTH_INV_SD = 1.0 / (65536.0 * math.sqrt(1.0 / 3.0))  # 1 / sd of a sum of four uniform 16-bit draws
+
+
+def depth_noise_factor(fid: int, n: int, sigma: float) -> np.ndarray:
+    """Per keypoint i of keyframe `fid`: 1 + sigma g, g = (a + b + c + d - 131070) / sd with a..d
+    the 16-bit fields of splitmix64(seed ^ fid K1 ^ i K2) (a unit-variance, nearly normal variate);
+    float64, evaluated in this order by every loop (track.cpp, track.hip)."""
+    from .synth import splitmix64
+
+    i = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = splitmix64(np.uint64(DEPTH_NOISE_SEED) ^ (np.uint64(fid) * np.uint64(0x9E3779B97F4A7C15)) ^
+                       (i * np.uint64(0xC2B2AE3D27D4EB4F)))
+    m = np.uint64(0xFFFF)
+    q = (z & m) + ((z >> np.uint64(16)) & m) + ((z >> np.uint64(32)) & m) + (z >> np.uint64(48))
+    g = (q.astype(np.float64) - 131070.0) * _DEPTH_INV_SD
+    return 1.0 + float(np.float32(sigma)) * g
+
+
 def make_keyframe(fid: int, pose: Pose, kp, desc, K, plane_z: float, s: "TrackerSettings") -> Keyframe:
     """A keyframe and its map points: plane back-projection plus MapPoint::
     UpdateMeanViewDirectionAndDistances (Map/MapPoint.cpp:131-154) for a point seen by this keyframe
     alone: mean viewing direction = Normalize(Normalize(point - centre)) (cv::Vec / float scales by
     1.f / length), d = |centre - point|, dmax / dmin = d x the octave's ComputeDMax / DMin factor."""
-    pts = backproject_to_plane(kp, pose, K, plane_z)
+    factor = depth_noise_factor(fid, len(kp), s.map_point_depth_noise) if s.map_point_depth_noise else None
+    pts = backproject_to_plane(kp, pose, K, plane_z, factor)
     C = world_position_f32(pose)
     v = (pts - C).astype(np.float32)
     with np.errstate(divide="ignore", invalid="ignore"):
@@ -245,20 +282,12 @@ class BAWindow:
         return np.ascontiguousarray(np.transpose(self.rot, (0, 2, 1)).reshape(-1, 9))
 
 
-def build_ba_window(ring, K, s: "TrackerSettings") -> BAWindow | None:
-    """GetMapPointsAndDistantKeyframes + BuildDataForG2O (ThreadSafeMap.cpp:880-960; BundleAdjust.cpp:
-    25-193) over this loop's map: the keyframes of the local map (ascending id), the newest
-    ba_free_keyframes of them free and the older ones fixed, at least one (the reference fixes the
-    observing keyframes outside the covisible set; here the local map is the last keyframes, so its
-    oldest members anchor the window: position, orientation and scale); the points they own that a free keyframe
-    observes; every alive association of those points, per camera: its own points (ascending index),
-    then its associations in the order its frame made them.  info = MapPointRefinementConfidence of
-    the point's refinement count.  NumStepsPerRun and the Huber width scale with the connectivity
-    ratio UpperConnectionsForBA / associations (MappingWorker.cpp:254-263)."""
-    if len(ring) < 2:
-        return None
+def _ring_observations(ring):
+    """Every alive observation of the ring's map points, per camera: its own points (ascending
+    index), then its associations in the order its frame made them (owners outside the ring are
+    gone from this loop's map): (cam, owner ring position, point index, u, v, src)."""
     pos_of = {k.id: c for c, k in enumerate(ring)}
-    obs = []  # (cam, owner ring position, point index, u, v, src)
+    obs = []
     for c, k in enumerate(ring):
         for i in np.nonzero(k.own_alive)[0]:
             obs.append((c, c, int(i), k.kp["x"][i], k.kp["y"][i], ("own", c, int(i))))
@@ -266,13 +295,66 @@ def build_ba_window(ring, K, s: "TrackerSettings") -> BAWindow | None:
             o = pos_of.get(int(k.assoc_owner[a]))
             if k.assoc_alive[a] and o is not None:
                 obs.append((c, o, int(k.assoc_idx[a]), k.assoc_uv[a, 0], k.assoc_uv[a, 1], ("assoc", c, a)))
-    nfix = max(len(ring) - s.ba_free_keyframes, 1)  # the oldest keyframes are fixed, at least one
-    seen_free = {(o, i) for c, o, i, _, _, _ in obs if c >= nfix}
+    return obs
+
+
+def covisible_window(ring, obs, s: "TrackerSettings", theta: int):
+    """GetMapPointsAndDistantKeyframes (ThreadSafeMap.cpp:888-957) over the ring: Kc = the newest
+    keyframe Ki and the keyframes sharing >= theta map points with it (CovisibilityGraph::
+    GetConnectedKeyframes, CovisibilityGraph.cpp:131-170: the edge weight is the shared-point
+    count); the window's points are every point a Kc keyframe observes, its associations every
+    observation of those points; theta steps up while the associations exceed
+    UpperConnectionsForBA and down (not below CovisMinThreshold) while they are below
+    LowerConnectionsForBA, MaxSteps + 1 rounds.  Returns (free ring positions, point keys, theta)."""
+    last = len(ring) - 1
+    seen = [set() for _ in ring]
+    for c, o, i, _, _, _ in obs:
+        seen[c].add((o, i))
+    weight = [len(seen[c] & seen[last]) for c in range(len(ring))]
+    for _ in range(s.covis_max_steps + 1):
+        kc = {last} | {c for c in range(last) if weight[c] >= theta}
+        pts = set()
+        for c in kc:
+            pts |= seen[c]
+        n_assoc = sum(1 for c, o, i, _, _, _ in obs if (o, i) in pts)
+        if n_assoc > s.ba_upper_connections:
+            theta += s.covis_ba_step
+            continue
+        if n_assoc < s.ba_lower_connections and theta > s.covis_min_threshold:
+            theta -= s.covis_ba_step
+            continue
+        break
+    return kc, pts, theta
+
+
+def build_ba_window(ring, K, s: "TrackerSettings", theta: int | None = None):
+    """GetMapPointsAndDistantKeyframes + BuildDataForG2O (ThreadSafeMap.cpp:868-960; BundleAdjust.cpp:
+    25-193) over this loop's map (the local map's keyframes, ascending id) -> (window or None, the
+    covisibility threshold to persist).  Free keyframes: covisible_window's Kc (ba_free_keyframes =
+    0), fixed = every other observer and the sequence's first keyframe (ThreadSafeMap.cpp:89, 939);
+    or the newest ba_free_keyframes of the ring (at least one fixed).  Points: those a free
+    keyframe observes, ascending (owner, index); observations: every alive association of those
+    points, per camera: its own points (ascending index), then its associations in the order its
+    frame made them.  info = MapPointRefinementConfidence of the point's refinement count.
+    NumStepsPerRun and the Huber width scale with the connectivity ratio UpperConnectionsForBA /
+    associations (MappingWorker.cpp:254-263)."""
+    if theta is None:
+        theta = s.covis_min_threshold
+    if len(ring) < 2:
+        return None, theta
+    obs = _ring_observations(ring)
+    if s.ba_free_keyframes > 0:
+        nfix = max(len(ring) - s.ba_free_keyframes, 1)  # the oldest keyframes are fixed, at least one
+        free = set(range(nfix, len(ring)))
+        seen_free = {(o, i) for c, o, i, _, _, _ in obs if c in free}
+    else:
+        free, seen_free, theta = covisible_window(ring, obs, s, theta)
+        free = {c for c in free if ring[c].id != 0}  # the map's first keyframe stays fixed
     point_src = sorted(seen_free)
     pidx = {key: n for n, key in enumerate(point_src)}
     obs = [ob for ob in obs if (ob[1], ob[2]) in pidx]
-    if not obs:
-        return None
+    if not obs or not free:
+        return None, theta
     fx, fy, cx, cy = K
     npts = len(point_src)
     points = np.zeros((npts, 3), np.float32)
@@ -291,12 +373,11 @@ def build_ba_window(ring, K, s: "TrackerSettings") -> BAWindow | None:
     return BAWindow(pos=np.stack([k.pose.t for k in ring]).astype(np.float32),
                     rot=np.stack([k.pose.R for k in ring]).astype(np.float32),
                     intr=np.tile(np.float32([cx, cy, fx, fy]), (len(ring), 1)),
-                    fixed=np.array([1 if c < max(len(ring) - s.ba_free_keyframes, 1) else 0 for c in range(len(ring))],
-                                   np.uint8), points=points,
+                    fixed=np.array([0 if c in free else 1 for c in range(len(ring))], np.uint8), points=points,
                     uv=np.array([[ob[3], ob[4]] for ob in obs], np.float32),
                     cam=np.array([ob[0] for ob in obs], np.uint32), pt=pt, info=refinement_confidence(refine[pt]),
                     point_src=point_src, obs_src=[ob[5] for ob in obs], huber_widths=[float(huber)] * max(steps, 1),
-                    max_error_square=float(np.float32(s.ba_max_outlier_error)))
+                    max_error_square=float(np.float32(s.ba_max_outlier_error))), theta
 
 
 def apply_ba_window(ring, w: BAWindow, outliers, pos, r9, points, s: "TrackerSettings") -> None:
@@ -323,16 +404,17 @@ def apply_ba_window(ring, w: BAWindow, outliers, pos, r9, points, s: "TrackerSet
             point_attributes(k, s, np.asarray(moved[c], np.int64))
 
 
-def local_bundle_adjust(ring, K, s: "TrackerSettings", backend: "Backend", lam):
+def local_bundle_adjust(ring, K, s: "TrackerSettings", backend: "Backend", lam, theta=None):
     """One MappingWorker local BA after a new keyframe (NumSteps = 1: one StepBundleAdjustment at
-    MaxOutlierError, BundleAdjust.cpp:375-404, with the persisted lambda).  Returns (the next lambda,
-    the outlier observation count) or (lam, None) when there is no window."""
-    w = build_ba_window(ring, K, s)
+    MaxOutlierError, BundleAdjust.cpp:375-404, with the persisted lambda and covisibility threshold,
+    MappingWorker.cpp:237-293).  Returns (the next lambda, the outlier observation count or None when
+    there is no window, the next theta)."""
+    w, theta = build_ba_window(ring, K, s, theta)
     if w is None:
-        return lam, None
+        return lam, None, theta
     outl, pos, r9, pts, lam_out = backend.bundle_adjust(w, lam)
     apply_ba_window(ring, w, outl, pos, r9, pts, s)
-    return max(lam_out, s.min_lambda), len(outl)
+    return max(lam_out, s.min_lambda), len(outl), theta
 
 
 def local_map_queries(kfs, ref: Keyframe, visited_ref: np.ndarray, hide_ref: np.ndarray, pose: Pose, K,
@@ -410,8 +492,9 @@ class TrackResult:
         return np.stack([p.R for p in self.poses])
 
 
-def backproject_to_plane(kp: np.ndarray, pose: Pose, K, plane_z: float) -> np.ndarray:
-    """World points where the keypoints' rays meet the plane Z = plane_z (the scene's depth)."""
+def backproject_to_plane(kp: np.ndarray, pose: Pose, K, plane_z: float, factor=None) -> np.ndarray:
+    """World points where the keypoints' rays meet the plane Z = plane_z (the scene's depth), the
+    ray parameter scaled by `factor` (depth_noise_factor) when given."""
     fx, fy, cx, cy = K
     R = pose.R
     u = (kp["x"].astype(np.float64) - cx) / fx
@@ -419,6 +502,8 @@ def backproject_to_plane(kp: np.ndarray, pose: Pose, K, plane_z: float) -> np.nd
     d = [(u * R[0, j] + v * R[1, j]) + R[2, j] for j in range(3)]  # R^T (u, v, 1)
     C = [-((R[0, j] * pose.t[0] + R[1, j] * pose.t[1]) + R[2, j] * pose.t[2]) for j in range(3)]
     lam = (plane_z - C[2]) / d[2]
+    if factor is not None:
+        lam = lam * factor
     return np.stack([C[j] + lam * d[j] for j in range(3)], 1).astype(np.float32)
 
 
@@ -580,6 +665,7 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
     res.keyframes.append(0)
     res.local_matches.append(0)
     lam = None  # the persisted local-BA lambda (MappingWorker: CurrentLambda)
+    theta = s.covis_min_threshold  # the persisted covisibility threshold (MappingWorker: CosVisThreashold)
     for t in range(1, T):
         kp, desc = features[t]
         # motion model: constant velocity on SE3 (the tracker's predicted pose)
@@ -660,7 +746,7 @@ def track(features, K, first_pose: Pose, plane_z: float, backend: Backend,
             kfs = (kfs + [kf])[-max(s.local_map_keyframes, 1):]
             res.keyframes.append(t)
             if s.local_ba:
-                lam, n_out = local_bundle_adjust(kfs, K, s, backend, lam)
+                lam, n_out, theta = local_bundle_adjust(kfs, K, s, backend, lam, theta)
                 if n_out is not None:
                     res.ba_outliers.append((t, n_out))
                     res.poses[-1] = kf.pose  # this frame's pose as the BA left its keyframe
@@ -713,7 +799,8 @@ def _settings_c(s: TrackerSettings):
                                s.local_min_hamming_difference, float(s.min_view_cos()), s.image_border, s.min_tracked,
                                s.scale_factor, s.num_levels, s.width, s.height, int(s.local_ba), s.ba_huber,
                                s.ba_huber_scale, s.ba_max_outlier_error, s.ba_steps_per_run, s.ba_low_connectivity_scale,
-                               s.ba_upper_connections, s.min_lambda, s.ba_free_keyframes)
+                               s.ba_upper_connections, s.min_lambda, s.ba_free_keyframes, s.covis_min_threshold,
+                               s.covis_ba_step, s.ba_lower_connections, s.covis_max_steps, s.map_point_depth_noise)
 
 
 def track_native_device(d_kp, d_desc, pitch: int, d_counts, frames: int, K, first_pose: Pose, plane_z: float,

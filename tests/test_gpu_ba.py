@@ -418,3 +418,28 @@ def test_more_cameras_than_lds_sort_counters(gpu):
     assert len(g2.pos) > 12288
     gb, ob = run_pair(g2, 3)
     compare(gb, ob)
+
+
+def test_block_cache_trim_and_reuse(gpu):
+    """Destroyed BundlerLib instances retire their blocks into the library's cache (common.hpp);
+    mage_pool_trim frees them for real, and later instances allocate afresh with unchanged results."""
+    from mageslam_amd import _lib
+
+    g = synth.ba_graph(cameras=8, points=200, obs_per_point=6, fixed_cameras=2, seed=5)
+    first = None
+    for rnd in range(3):
+        gb, ob = run_pair(g, 2)
+        compare(gb, ob)
+        res = gb.state()
+        if first is None:
+            first = res
+        else:
+            assert np.array_equal(first[0], res[0]) and np.array_equal(first[1], res[1])
+        del gb
+        import gc
+
+        gc.collect()
+        freed = _lib.load().mage_pool_trim(-1)
+        if rnd == 0:
+            assert freed > 0  # the destroyed instance's device / host blocks were cached
+    assert _lib.load().mage_pool_trim(-1) == 0

@@ -149,6 +149,30 @@ def test_create_tree_empty_and_errors(gpu):
         bow.OnlineBowTree.CreateTree(np.zeros((10, 32), np.uint8), levels=0)
 
 
+@pytest.mark.parametrize("na,nb", [(2048, 2048), (2049, 2049), (1025, 2047), (3000, 1023), (1, 2049)])
+def test_indexed_match_stage_boundaries(gpu, oracle, na, nb):
+    """B sets at and around the 2048 descriptors indexed_match_kernel stages in LDS, and counts off
+    the 1024-thread stride (the stage hand-off audit): bit-exact, with and
+    without masks (the staged count is the masked count)."""
+    from mageslam_amd import orb
+
+    det = orb.OrbDetector(nfeatures=3200)
+    da = det.DetectAndCompute(synth.frame(0, 1280, 720))[1]
+    db = det.DetectAndCompute(synth.frame(1, 1280, 720))[1]
+    assert len(da) >= na and len(db) >= nb
+    da, db = da[:na], db[:nb]
+    tree = synth.bow_tree(np.concatenate([da[:1000], db[:1000]]))
+    t = bow.OnlineBowTree(*tree)
+    got = bow.IndexedMatch(t, da, db)
+    ref = oracle.indexed_match(tree, da, db)
+    assert np.array_equal(got.view(np.uint8), ref.view(np.uint8))
+    mb = np.ones(nb, bool)
+    mb[::7] = False  # a masked B count below the stage size
+    got = bow.IndexedMatch(t, da, db, None, mb)
+    ref = oracle.indexed_match(tree, da, db, None, mb.astype(np.uint8))
+    assert np.array_equal(got.view(np.uint8), ref.view(np.uint8))
+
+
 def test_indexed_and_radius_large_sets(gpu, oracle):
     """Sets above the 2048 entries staged in LDS (the kernels' global-memory path): 3000-feature
     frames through IndexedMatch and RadiusMatch, bit-exact vs the oracle."""

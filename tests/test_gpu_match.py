@@ -163,7 +163,9 @@ def test_radius_match_ties(gpu, oracle):
     rng = np.random.default_rng(11)
     from mageslam_amd._lib import KP_DTYPE
 
-    for nq, nt in ((500, 800), (1, 1), (3000, 4096)):
+    # set sizes around the 2048 targets staged in LDS and off the 1024-thread stride (the stage
+    # hand-off audit)
+    for nq, nt in ((500, 800), (1, 1), (3000, 4096), (1025, 2048), (2049, 2049), (64, 2047), (1023, 1025)):
         tk = np.zeros(nt, KP_DTYPE)
         tk["x"] = rng.integers(0, 60, nt).astype(np.float32)
         tk["y"] = rng.integers(0, 40, nt).astype(np.float32)

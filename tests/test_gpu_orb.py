@@ -395,3 +395,23 @@ def test_window_blur_descriptors_match_oracle(gpu):
     r = subprocess.run([sys.executable, "-c", WIN_BLUR_CHILD, root], capture_output=True, text=True, timeout=110,
                        env=dict(os.environ, MAGE_WIN_BLUR="1"), cwd=root)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(nlevels=4, patchSize=31, useOrientation=True), dict(patchSize=21),
+                                dict(gaussianKernelSize=5)])
+def test_describe_partial_waves(gpu, oracle, kw):
+    """describe_blurred_kernel / describe_kernel run KP keypoints per wave (8 for the default
+    windows, 2 for the rotated ones) and 4 waves per workgroup, each wave staging its keypoints'
+    windows in its own LDS region: keypoint counts that end inside a wave or a workgroup (the last
+    wave's loads clamp to the last keypoint, its tests stop at n) must stay bit-exact (the audit
+    after the matcher's stage-buffer race)."""
+    m = {"nlevels": "nlevels", "patchSize": "patch_size", "useOrientation": "use_orientation",
+         "gaussianKernelSize": "gaussian_kernel_size"}
+    img = synth.frame(4, 640, 480)
+    for nfeat in (1, 7, 9, 33, 257, 1001):
+        det = orb.OrbDetector(nfeatures=nfeat, **kw)
+        kp, d = det.DetectAndCompute(img)
+        st, okp, od = oracle.orb_detect(img, oracle.default_settings(nfeat, **{m[k]: v for k, v in kw.items()}))
+        assert st == 0 and len(kp) == len(okp) and len(kp) > 0, (kw, nfeat)
+        assert np.array_equal(kp_bytes(kp), kp_bytes(okp)), (kw, nfeat)
+        assert np.array_equal(d, od), (kw, nfeat)

@@ -89,13 +89,16 @@ def test_tracking_loop_720p_gpu_vs_oracle(gpu, oracle):
     assert rt <= 1e-4 and rr <= 1e-4, (rt, rr)
 
 
-def test_tracking_loop_local_ba_720p_device_vs_oracle(gpu, oracle):
+@pytest.mark.parametrize("noise,free", [(0.0, 0), (0.02, 0), (0.0, 2)])
+def test_tracking_loop_local_ba_720p_device_vs_oracle(gpu, oracle, noise, free):
     """C4 composed with the local BA MappingWorker runs after every new keyframe
-    (tracking.local_bundle_adjust: the local map's keyframes, oldest fixed, one StepBundleAdjustment
-    at MaxOutlierError with the persisted lambda, poses / points / refinement counts written back
-    before the next frame tracks): the device loop (mage_track_sequence_device, BundlerLib between
-    frames) and the Python loop on the GPU backend against the oracle loop at 1280 x 720 over 96
-    frames — identical matches, inliers, keyframes and BA outlier counts, pose RMSE <= 1e-4."""
+    (tracking.local_bundle_adjust: the covisibility window of GetMapPointsAndDistantKeyframes — or
+    the newest `free` keyframes — one StepBundleAdjustment at MaxOutlierError with the persisted
+    lambda and theta, poses / points / refinement counts written back before the next frame
+    tracks), with exact and with noisy map-point depth: the device loop (mage_track_sequence_device,
+    BundlerLib between frames) and the Python loop on the GPU backend against the oracle loop at
+    1280 x 720 over 96 frames — identical matches, inliers, keyframes and BA outlier counts, pose
+    RMSE <= 1e-4."""
     from oracle.tracking_backend import OracleBackend
 
     seq = synth.scene_sequence(96, 1280, 720, step=0.06)
@@ -106,7 +109,7 @@ def test_tracking_loop_local_ba_720p_device_vs_oracle(gpu, oracle):
     gf = gb.extract(frames)
     ob = OracleBackend(2000)
     of = ob.extract(frames)
-    s = tracking.TrackerSettings(local_ba=True)
+    s = tracking.TrackerSettings(local_ba=True, map_point_depth_noise=noise, ba_free_keyframes=free)
     o = tracking.track(of, K, p0, synth.SCENE_PLANE_Z, ob, s)
     g = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb, s)
     d = tracking.track_native_device(*tracking.features_to_device(gf), len(gf), K, p0, synth.SCENE_PLANE_Z,
@@ -119,8 +122,29 @@ def test_tracking_loop_local_ba_720p_device_vs_oracle(gpu, oracle):
         assert rt <= 1e-4 and rr <= 1e-4, (rt, rr)
     _same(d, g)  # the device loop and the Python loop over the same GPU kernels: bit-identical
     # the BA changed the map: without it the same frames give other poses
-    n = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb, tracking.TrackerSettings())
+    n = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb, tracking.TrackerSettings(map_point_depth_noise=noise))
     assert any(not np.array_equal(a.t, b.t) for a, b in zip(n.poses, g.poses))
+
+
+def test_native_tracking_loop_depth_noise(gpu):
+    """The seeded map-point depth error (depth_noise.hpp / tracking.depth_noise_factor) is the same
+    arithmetic in the host loop (mage_track_sequence), the device loop and the Python loop:
+    bit-identical poses, and different ones from the exact-depth map."""
+    seq = synth.scene_sequence(100, 1280, 720, step=0.06)
+    frames = synth.scene_frames(seq)
+    K = (seq.fx, seq.fy, seq.cx, seq.cy)
+    p0 = tracking.Pose(seq.R[0], seq.t[0])
+    gb = tracking.GpuBackend(2000)
+    gf = gb.extract(frames)
+    s = tracking.TrackerSettings(map_point_depth_noise=0.05)
+    g = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb, s)
+    n = tracking.track_native(gf, K, p0, synth.SCENE_PLANE_Z, settings=s)
+    d = tracking.track_native_device(*tracking.features_to_device(gf), len(gf), K, p0, synth.SCENE_PLANE_Z, settings=s)
+    assert len(g.keyframes) >= 2
+    _same(n, g)
+    _same(d, g)
+    e = tracking.track(gf, K, p0, synth.SCENE_PLANE_Z, gb, tracking.TrackerSettings())
+    assert any(not np.array_equal(a.t, b.t) for a, b in zip(e.poses, g.poses))
 
 
 def test_native_tracking_loop_720p_keyframes(gpu):

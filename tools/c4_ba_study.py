@@ -3,14 +3,18 @@
   python tools/c4_ba_study.py extract            # oracle ORB over the 1000-frame C4 sequence -> /tmp/c4_feats.npz
   python tools/c4_ba_study.py run MODE[,MODE...] # one oracle tracking run per mode (~60 s each), RMSE vs ground truth
 
-Modes (combine with '+'): noba (local BA off), ba (the C4 composition: ring of 4 keyframes, newest
-2 free), free1 / free3 (ba_free_keyframes), lm6 / lm8 (local_map_keyframes), minobs (only points
-with >= 2 observations in the window), anch (only points observed by a fixed keyframe), norefine
-(refinement counts not incremented after a window), steps3 / steps10 (3x / 10x the LM steps per
-window), nopoints (the window's poses written back, its points not), noposes (points written
-back, poses not), depth2 / depth5 (new map points at a depth off by 2 % / 5 % rms, seeded per
-keyframe: the error a triangulated point would carry instead of the exact plane depth).  Output: one line per mode, pose RMSE (translation, rotation) over the 1000
-frames against the synthetic ground truth; profiles/r5_c4_ba_study.md holds a run.
+Modes (combine with '+'): noba (local BA off), ba (the C4 composition: ring of 4 keyframes, the
+covisibility window of GetMapPointsAndDistantKeyframes — the new keyframe and the ring keyframes
+sharing >= theta points with it free, ThreadSafeMap.cpp:888-957), free1 / free2 / free3 (the newest
+N keyframes free instead: ba_free_keyframes; free2 was the round-4/5 rule), lm6 / lm8
+(local_map_keyframes), minobs (only points with >= 2 observations in the window), anch (only points
+observed by a fixed keyframe), norefine (refinement counts not incremented after a window), steps3 /
+steps10 (3x / 10x the LM steps per window), nopoints (the window's poses written back, its points
+not), noposes (points written back, poses not), depth2 / depth5 (new map points at a depth off by
+2 % / 5 % rms: TrackerSettings.map_point_depth_noise, the error a triangulated point would carry
+instead of the exact plane depth).  Output: one line per mode, pose RMSE (translation, rotation)
+over the 1000 frames against the synthetic ground truth; profiles/r5_c4_ba_study.md and
+profiles/r6_c4_ba_study.md hold runs.
 """
 import sys
 import time
@@ -70,20 +74,21 @@ def run(mode):
     p0 = tracking.Pose(seq.R[0], seq.t[0])
     gt = tracking.TrackResult(poses=[tracking.Pose(seq.R[i], seq.t[i]) for i in range(T)])
     kw = dict(width=1280, height=720, local_ba="noba" not in opts)
-    if "free1" in opts:
-        kw["ba_free_keyframes"] = 1
-    if "free3" in opts:
-        kw["ba_free_keyframes"] = 3
+    for n in (1, 2, 3):
+        if f"free{n}" in opts:
+            kw["ba_free_keyframes"] = n
+    if "depth2" in opts or "depth5" in opts:
+        kw["map_point_depth_noise"] = 0.02 if "depth2" in opts else 0.05
     if "lm6" in opts:
         kw["local_map_keyframes"] = 6
     if "lm8" in opts:
         kw["local_map_keyframes"] = 8
     build, apply = tracking.build_ba_window, tracking.apply_ba_window
 
-    def build_w(ring, K_, s):
-        w = build(ring, K_, s)
+    def build_w(ring, K_, s, theta=None):
+        w, theta = build(ring, K_, s, theta)
         if w is None:
-            return w
+            return w, theta
         keep = np.ones(len(w.points), bool)
         if "minobs" in opts:
             keep &= np.bincount(w.pt, minlength=len(w.points)) >= 2
@@ -95,7 +100,7 @@ def run(mode):
             w.huber_widths = w.huber_widths * 3
         if "steps10" in opts:
             w.huber_widths = w.huber_widths * 10
-        return _filter(w, keep)
+        return _filter(w, keep), theta
 
     def apply_w(ring, w, outl, pos, r9, pts, s):
         saved = [k.refine.copy() for k in ring] if "norefine" in opts else None
@@ -108,36 +113,24 @@ def run(mode):
             for k, r in zip(ring, saved):
                 k.refine[:] = r
 
-    backproject = tracking.backproject_to_plane
-    noise = 0.02 if "depth2" in opts else (0.05 if "depth5" in opts else 0.0)
-
-    def backproject_noisy(kp, pose, K_, plane_z):
-        pts = backproject(kp, pose, K_, plane_z).astype(np.float64)
-        if noise:
-            R, t = pose.R, pose.t
-            C = -(R.T @ t)
-            rng = np.random.default_rng(int(abs(hash((float(t[0]), float(t[1]), float(t[2])))) % 2**32))
-            pts = C + (pts - C) * (1.0 + noise * rng.standard_normal((len(pts), 1)))
-        return pts.astype(np.float32)
-
     tracking.build_ba_window, tracking.apply_ba_window = build_w, apply_w
-    tracking.backproject_to_plane = backproject_noisy
     try:
         t0 = time.time()
         r = tracking.track(feats, K, p0, synth.SCENE_PLANE_Z, OracleBackend(2000), tracking.TrackerSettings(**kw))
     finally:
         tracking.build_ba_window, tracking.apply_ba_window = build, apply
-        tracking.backproject_to_plane = backproject
     rt, rr = tracking.pose_rmse(r, gt)
-    print(f"| {mode} | {rt:.5f} | {rr:.6f} | {len(r.keyframes)} | {len(r.ba_outliers)} | {time.time() - t0:.0f} s |",
-          flush=True)
+    nout = sum(n for _, n in r.ba_outliers)
+    n600 = sum(n for f, n in r.ba_outliers if f < 600)
+    print(f"| {mode} | {rt:.5f} | {rr:.6f} | {len(r.keyframes)} | {len(r.ba_outliers)} | {nout} ({n600} in the first 600 "
+          f"frames) | {time.time() - t0:.0f} s |", flush=True)
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "extract":
         extract()
     else:
-        print("| mode | translation RMSE | rotation RMSE | keyframes | BA windows | time |")
-        print("|---|---|---|---|---|---|")
+        print("| mode | translation RMSE | rotation RMSE | keyframes | BA windows | BA outliers | time |")
+        print("|---|---|---|---|---|---|---|")
         for m in sys.argv[2].split(","):
             run(m)
