@@ -1074,19 +1074,7 @@ __global__ __launch_bounds__(CH_THREADS) void cholesky_solve(double* __restrict_
 // resident tiles'.  Measured at n = 240 (tools/ablate_ba.py): 95 us with 8 waves and the factor
 // after the SYRK barrier, 74 us now (16 waves, 4 per SIMD).  Nothing of S leaves the chip between
 // steps; the solves use the per-block inverses kept in LDS.
-#ifndef MAGE_CHOL_ABLATE  // timing experiments only (tools/ablate_ba.py); 0 in the product
-#define MAGE_CHOL_ABLATE 0
-#endif
-#ifndef MAGE_CHOL_WAVES
-#define MAGE_CHOL_WAVES 16
-#endif
-#ifndef MAGE_CHOL_LIGHT
-#define MAGE_CHOL_LIGHT 0  // tiles of each tile wave on the factor wave's SIMD (at least; chol_tile_table)
-#endif
-#ifndef MAGE_CHOL_LOOKAHEAD
-#define MAGE_CHOL_LOOKAHEAD 1  // the diagonal-block factor starts column j+1's pivot chain early
-#endif
-constexpr int CT_WAVES = MAGE_CHOL_WAVES;  // 16: 4 per SIMD (15 tile waves x 8 resident tiles + the factor wave)
+constexpr int CT_WAVES = 16;  // 4 per SIMD (15 tile waves x 8 resident tiles + the factor wave)
 constexpr int CT_THREADS = CT_WAVES * kWave;
 constexpr int CT_TW = CT_WAVES - 1;  // tile waves (wave CT_TW: the factor wave, which holds no tile)
 constexpr int CT_MAXT = 15;
@@ -1158,118 +1146,75 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         ti = tIJ[sl] & 0xFF;
         tj = tIJ[sl] >> 8;
     };
-    long long tm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0;  // MAGE_CHOL_ABLATE == 3: phase cycles of wave 0
-    auto tick = [&](int ph) {
-        if (MAGE_CHOL_ABLATE == 3) {
-            const long long t = __builtin_amdgcn_s_memtime();
-            if (ph >= 0) tm[ph] += t - t0;
-            t0 = t;
-        }
-    };
-#if MAGE_CHOL_ABLATE == 4  // per-step timestamps of every wave (rel. to the first barrier)
-    __shared__ long long ttr[CT_MAXT][CT_WAVES][4];
-    long long tbase = 0;
-#define CT_STAMP(k, ph)                                                                   \
-    do {                                                                                  \
-        if (lane == 0 && (k) < CT_MAXT) ttr[k][wave][ph] = __builtin_amdgcn_s_memtime() - tbase; \
-    } while (0)
-#else
-#define CT_STAMP(k, ph) \
-    do {                \
-    } while (0)
-#endif
     // --- the 16x16 diagonal block factor (the factor wave), from dsc ---
     auto factor_diag = [&](int k) {  // from dsc
         const int l = lane;
-        if (MAGE_CHOL_ABLATE == 2) {
-            if (l < 16)
-                for (int q = 0; q < 16; q++) invT[k][q][l] = (q == l) ? 1.0 / sqrt(dsc[l][l]) : 0.0;
-            if (l < 16) vb[16 * k + l] = 0;
-        } else {
-            // Right-looking Cholesky of the 16x16 block with the triangular inverse and the
-            // forward substitution fused into the same column loop, one register array v[] over
-            // three lane groups that all take the same update v[q] -= v[j] L[q][j]:
-            //   lanes 0-15:  row l of A -> row l of L (entries above the diagonal are never read)
-            //   lanes 16-31: column l-16 of I -> column l-16 of inv(L)
-            //   lane 32:     vb_k (final: every block above has updated it) -> y_k, in place
-            // Column j's L[q][j] are broadcast once with v_readlane (scalar registers).  Lane j's
-            // own v[j] is the pivot d, so v[j] *= 1/sqrt(d) yields sqrt(d) there with no select.
-            // (An LDS column broadcast instead measured 2x slower.)
-            double v[16];
-            const double* vbk = &vb[16 * k];
-            const int c = l - 16;
-            // one batch of unconditional 16-byte loads from a per-lane source (row l of A for
-            // lanes 0-15, vb_k for the others), then per-lane selects
-            double dq[16];
-            {
-                const double2* dr = reinterpret_cast<const double2*>(l < 16 ? &dsc[l][0] : vbk);
+        // Right-looking Cholesky of the 16x16 block with the triangular inverse and the
+        // forward substitution fused into the same column loop, one register array v[] over
+        // three lane groups that all take the same update v[q] -= v[j] L[q][j]:
+        //   lanes 0-15:  row l of A -> row l of L (entries above the diagonal are never read)
+        //   lanes 16-31: column l-16 of I -> column l-16 of inv(L)
+        //   lane 32:     vb_k (final: every block above has updated it) -> y_k, in place
+        // Column j's L[q][j] are broadcast once with v_readlane (scalar registers).  Lane j's
+        // own v[j] is the pivot d, so v[j] *= 1/sqrt(d) yields sqrt(d) there with no select.
+        // (An LDS column broadcast instead measured 2x slower.)
+        double v[16];
+        const double* vbk = &vb[16 * k];
+        const int c = l - 16;
+        // one batch of unconditional 16-byte loads from a per-lane source (row l of A for
+        // lanes 0-15, vb_k for the others), then per-lane selects
+        double dq[16];
+        {
+            const double2* dr = reinterpret_cast<const double2*>(l < 16 ? &dsc[l][0] : vbk);
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const double2 d2 = dr[q];
-                    dq[2 * q] = d2.x;
-                    dq[2 * q + 1] = d2.y;
-                }
+            for (int q = 0; q < 8; q++) {
+                const double2 d2 = dr[q];
+                dq[2 * q] = d2.x;
+                dq[2 * q + 1] = d2.y;
             }
+        }
 #pragma unroll
-            for (int q = 0; q < 16; q++)
-                v[q] = l < 16 ? (q <= l ? dq[q] : 0.0) : (l < 32 ? (q == c ? 1.0 : 0.0) : (l == 32 ? dq[q] : 0.0));
-            bool bad = false;
-            if (k == 0) tick(6);
-            // 1/sqrt by v_rsq_f64 + one Newton step (~1e-14 relative, no f64 sqrt / division
-            // sequence on the column's critical path)
-            auto rsq_newton = [&](double d) {
-                if (!(d > 0)) bad = true;
-                const double h = 0.5 * d;
-                double r = __builtin_amdgcn_rsq(d);
-                return r * __builtin_fma(-h * r, r, 1.5);
-            };
-#if MAGE_CHOL_LOOKAHEAD
-            // Look-ahead: column j + 1 is updated first and its pivot's 1/sqrt chain starts right
-            // away, so the chain (readlane -> rsq -> Newton -> scale, a run of dependent f64 ops)
-            // overlaps the rest of column j's update instead of following it in issue order.
-            double r = rsq_newton(readlane_f64(v[0], 0));
+        for (int q = 0; q < 16; q++)
+            v[q] = l < 16 ? (q <= l ? dq[q] : 0.0) : (l < 32 ? (q == c ? 1.0 : 0.0) : (l == 32 ? dq[q] : 0.0));
+        bool bad = false;
+        // 1/sqrt by v_rsq_f64 + one Newton step (~1e-14 relative, no f64 sqrt / division
+        // sequence on the column's critical path)
+        auto rsq_newton = [&](double d) {
+            if (!(d > 0)) bad = true;
+            const double h = 0.5 * d;
+            double r = __builtin_amdgcn_rsq(d);
+            return r * __builtin_fma(-h * r, r, 1.5);
+        };
+        // Look-ahead: column j + 1 is updated first and its pivot's 1/sqrt chain starts right
+        // away, so the chain (readlane -> rsq -> Newton -> scale, a run of dependent f64 ops)
+        // overlaps the rest of column j's update instead of following it in issue order.
+        double r = rsq_newton(readlane_f64(v[0], 0));
 #pragma unroll
-            for (int j = 0; j < 16; j++) {
-                v[j] *= r;
-                if (j < 15) {
-                    const double l1 = readlane_f64(v[j], j + 1);
-                    v[j + 1] = __builtin_fma(-v[j], l1, v[j + 1]);
-                    const double rn = rsq_newton(readlane_f64(v[j + 1], j + 1));
-                    double lq[16];
-#pragma unroll
-                    for (int q = j + 2; q < 16; q++) lq[q] = readlane_f64(v[j], q);
-#pragma unroll
-                    for (int q = j + 2; q < 16; q++) v[q] = __builtin_fma(-v[j], lq[q], v[q]);
-                    r = rn;
-                }
-                __builtin_amdgcn_sched_barrier(0);  // keep each column's broadcasts in its own window
-            }
-#else
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                v[j] *= rsq_newton(readlane_f64(v[j], j));
-                // all broadcasts of the column first (distinct scalar registers: the readlane ->
-                // VALU hazard is covered by the batch instead of an s_nop per element)
+        for (int j = 0; j < 16; j++) {
+            v[j] *= r;
+            if (j < 15) {
+                const double l1 = readlane_f64(v[j], j + 1);
+                v[j + 1] = __builtin_fma(-v[j], l1, v[j + 1]);
+                const double rn = rsq_newton(readlane_f64(v[j + 1], j + 1));
                 double lq[16];
 #pragma unroll
-                for (int q = j + 1; q < 16; q++) lq[q] = readlane_f64(v[j], q);
+                for (int q = j + 2; q < 16; q++) lq[q] = readlane_f64(v[j], q);
 #pragma unroll
-                for (int q = j + 1; q < 16; q++) v[q] = __builtin_fma(-v[j], lq[q], v[q]);
-                __builtin_amdgcn_sched_barrier(0);  // keep each column's broadcasts in its own window
+                for (int q = j + 2; q < 16; q++) v[q] = __builtin_fma(-v[j], lq[q], v[q]);
+                r = rn;
             }
-#endif
-            if (k == 0) tick(7);
-            if (l == 0 && bad) s_fail = 1;
-            if (l >= 16 && l < 32) {
-                double2* o = reinterpret_cast<double2*>(&invT[k][c][0]);
+            __builtin_amdgcn_sched_barrier(0);  // keep each column's broadcasts in its own window
+        }
+        if (l == 0 && bad) s_fail = 1;
+        if (l >= 16 && l < 32) {
+            double2* o = reinterpret_cast<double2*>(&invT[k][c][0]);
 #pragma unroll
-                for (int m = 0; m < 8; m++) o[m] = double2{v[2 * m], v[2 * m + 1]};
-            }
-            if (l == 32) {  // y_k replaces b_k in the solution vector
-                double2* o = reinterpret_cast<double2*>(&vb[16 * k]);
+            for (int m = 0; m < 8; m++) o[m] = double2{v[2 * m], v[2 * m + 1]};
+        }
+        if (l == 32) {  // y_k replaces b_k in the solution vector
+            double2* o = reinterpret_cast<double2*>(&vb[16 * k]);
 #pragma unroll
-                for (int m = 0; m < 8; m++) o[m] = double2{v[2 * m], v[2 * m + 1]};
-            }
+            for (int m = 0; m < 8; m++) o[m] = double2{v[2 * m], v[2 * m + 1]};
         }
     };
     auto solve_block = [&](int k) {  // by one wave: vb_k := inv(U_kk) vb_k, inv(U) = inv(L)^T
@@ -1325,9 +1270,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             factor_diag(0);
         }
         __syncthreads();  // tiles loaded, block 0 factored
-#if MAGE_CHOL_ABLATE == 4
-        tbase = __builtin_amdgcn_s_memtime();
-#endif
         for (int k = 0; k < mt; k++) {
             if (s_fail) break;
             const int kn = k + 1, buf = k & 1;
@@ -1339,7 +1281,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                         cD[r] = dst[lr + 4 * r][lc];
                     }
                 __builtin_amdgcn_s_setprio(3);  // the critical chain first on this SIMD
-                CT_STAMP(k, 0);
                 // TRSM U_{k,k+1} = inv(L_kk) A_{k,k+1} into the panel, y_{k+1} -= U^T y_k
                 dbl4 acc = {0, 0, 0, 0};
 #pragma unroll
@@ -1368,16 +1309,13 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                CT_STAMP(k, 1);
                 factor_diag(kn);
                 __builtin_amdgcn_s_setprio(0);
             } else {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == 0) __hip_atomic_fetch_add(&s_tile_bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            CT_STAMP(k, 2);
             __syncthreads();  // end of step k
-            CT_STAMP(k, 3);
         }
         if (s_fail) return;
         for (int k = 0; k < (mt > 0 ? mt : 1); k++) __syncthreads();  // the backward solve's barriers
@@ -1393,7 +1331,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
 #pragma unroll
                 for (int r = 0; r < 4; r++) dsc[lc][lr + 4 * r] = C[sl][r];
     };
-    tick(-1);
 #pragma unroll
     for (int sl = 0; sl < CT_TPW; sl++) {
         int ti, tj;
@@ -1413,10 +1350,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
     constexpr int TT = CT_TW * kWave;  // tile-wave threads
     for (int i = 16 + tid; i < np; i += TT) vb[i] = i < n ? b[i] : 0.0;
     __syncthreads();  // tiles loaded, block 0 factored
-#if MAGE_CHOL_ABLATE == 4
-    tbase = __builtin_amdgcn_s_memtime();
-#endif
-    tick(0);
     for (int k = 0; k < mt; k++) {
         const int buf = k & 1;
         if (s_fail) break;
@@ -1453,8 +1386,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
             const int ti = tIJ[sl] & 0xFF, tj = tIJ[sl] >> 8;
             if (ti == k && tj > kn) trsm(sl);
         }
-        tick(3);
-        CT_STAMP(k, 0);
         // the TRSM-phase barrier (an LDS counter: the factor wave arrives after its TRSM of
         // (k, k+1) and goes on to the factor): pan row-block k complete
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1462,8 +1393,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         while (__hip_atomic_load(&s_tile_bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)((CT_TW + 1) * kn))
             __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        CT_STAMP(k, 1);
-        tick(2);
 #pragma unroll
         for (int sl = 0; sl < CT_TPW; sl++)  // the owner of (k, k+1) keeps U for the backward solve
             if (tIJ[sl] == chain)
@@ -1491,11 +1420,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
                     for (int r = 0; r < 4; r++) dst[lr + 4 * r][lc] = C[sl][r];
             }
         }
-        tick(4);
-        CT_STAMP(k, 2);
         __syncthreads();  // block k+1 factored (invT, y_{k+1}), every SYRK of step k done
-        CT_STAMP(k, 3);
-        tick(2);
     }
     if (s_fail) {
         if (tid == 0) *fail = 1;
@@ -1532,22 +1457,7 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
         }
         __syncthreads();
     }
-    tick(5);
-#if MAGE_CHOL_ABLATE == 4
-    if (tid == 0) {
-        printf("chol_tiles np=%d backward end %lld\n", np, (long long)(__builtin_amdgcn_s_memtime() - tbase));
-        for (int k = 0; k < mt; k++) {
-            printf("step %2d:", k);
-            for (int w = 0; w < CT_WAVES; w++)
-                printf(" |%lld %lld %lld %lld", ttr[k][w][0], ttr[k][w][1], ttr[k][w][2], ttr[k][w][3]);
-            printf("\n");
-        }
-    }
-#endif
     for (int i = tid; i < np; i += TT) x[i] = i < n ? vb[i] : 0.0;
-    if (MAGE_CHOL_ABLATE == 3 && tid == 0)
-        printf("chol_tiles np=%d cycles: load %lld diag %lld barrier %lld trsm %lld syrk %lld backward %lld | factor0 stage %lld columns %lld\n", np, tm[0],
-               tm[1], tm[2], tm[3], tm[4], tm[5], tm[6], tm[7]);
 }
 
 // Back-substitution, the trial state and its evaluation in one launch.  Blocks [0, npb): a
@@ -2480,7 +2390,7 @@ static void chol_tile_table(int mt, const SchurPair* pairs, int npairs, std::vec
     for (int w = 0; w < CT_TW; w++) ((w & 3) == (CT_TW & 3) ? light : heavy).push_back(w);
     const int nheavy = (int)heavy.size() * CT_TPW;
     const int per_light = light.empty() ? 0
-                                        : std::min(CT_TPW, std::max(MAGE_CHOL_LIGHT, ((int)tiles.size() - nheavy +
+                                        : std::min(CT_TPW, std::max(0, ((int)tiles.size() - nheavy +
                                                                                       (int)light.size() - 1) /
                                                                                          (int)light.size()));
     size_t t = 0;

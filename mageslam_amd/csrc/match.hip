@@ -47,9 +47,6 @@ constexpr int NMAX = 4096;     // max descriptors per side (states in LDS)
 constexpr int NBUF = 3;        // B stage buffers
 constexpr int NONE = INT_MIN;  // empty key
 static_assert(SC * 8 == MT, "one stage-fill item per thread");
-#ifndef MAGE_MATCH_ABLATE  // timing experiments only (tools/ablate_match.py); 0 in the product
-#define MAGE_MATCH_ABLATE 0
-#endif
 
 struct MatchParams {
     int max_dist, min_diff;
@@ -249,18 +246,14 @@ struct Keys32 {
 #pragma unroll
         for (int g = 0; g < 16; g++) {
             const int D = acc[g];
-            if (MAGE_MATCH_ABLATE == 4) {
-                R.r1[rt][g] = max(R.r1[rt][g], D);
-                continue;
-            }
             int kr = (D << 15) | jc;
             int kc = (D << 6) | (63 - (rt * 32 + acc_row(g)));
             if (MASK) {
                 if (j >= nb) kr = NONE;
                 if (rowbase + rt * 32 + acc_row(g) + 4 * h >= na) kc = NONE;
             }
-            if (MAGE_MATCH_ABLATE != 2) push2(R.r1[rt][g], R.r2[rt][g], kr);
-            if (MAGE_MATCH_ABLATE != 1) push2(C.c1, C.c2, kc);
+            push2(R.r1[rt][g], R.r2[rt][g], kr);
+            push2(C.c1, C.c2, kc);
         }
     }
     // Padding rows and columns have zero operands, so D = 0 (d = 128) there: such a key can
@@ -277,7 +270,6 @@ struct Keys32 {
     static __device__ __forceinline__ PendingCol flush(const Part& C, int lane, int colbase, int nb, int rowbase,
                                                        int* colM1)
     {
-        if (MAGE_MATCH_ABLATE == 1 || MAGE_MATCH_ABLATE == 4) return PendingCol{0, 0, 0, 0, false};
         const int ib = rowbase + 4 * (lane >> 5) + 63;
         int c1 = C.c1, c2 = C.c2;
         if (c1 != NONE) c1 = ((c1 >> 6) << 15) | (0x7FFF - (ib - (c1 & 63)));
@@ -470,8 +462,8 @@ __device__ __forceinline__ void row_passes(const uint32_t* __restrict__ Aw, cons
                     cbp = colbase;
                 }
             }
-            if (MAGE_MATCH_ABLATE < 5 && st + 2 < nstages) fill((st + 2) % NBUF, st + 2, nxt);
-            if (MAGE_MATCH_ABLATE != 6) __syncthreads();
+            if (st + 2 < nstages) fill((st + 2) % NBUF, st + 2, nxt);
+            __syncthreads();
         }
         if (active) {
             if (cbp >= 0) {
@@ -548,9 +540,6 @@ constexpr int FPF = FBUF - 1;        // stages filled ahead
 constexpr uint32_t K16_BASE = 0x2400u;  // low-16 mantissa offset of the accumulator start
 constexpr int K16_D = 272;           // key >> 6 = K16_D - d
 constexpr uint32_t NONE16 = 0x80008000u;
-#ifndef MAGE_FP4_MAX3
-#define MAGE_FP4_MAX3 1  // column top-2 by a tournament + v_pk_maximum3_f16 (17 instead of 20 ops per row tile)
-#endif
 #ifndef MAGE_FP4_GATE
 // 1: skip the fold of 32x32 tiles with no key within maxDist (a v_max3 tree + one ballot per
 // tile), adaptively: a wave stops gating once more than a quarter of its tiles (after 64) held a
@@ -745,7 +734,6 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                             r1[rt][q] = pkmax(r1[rt][q], P[q]);
                         }
                         // column: the two best (distance, row) keys of the lane's 16 rows of this tile
-#if MAGE_FP4_MAX3
                         // a knock-out tournament: every key but the winner loses exactly one
                         // comparison, so the second best is the best of the 7 losers (3 max3s)
                         uint32_t h[4], l[4];
@@ -758,21 +746,13 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                         const uint32_t hh1 = pkmax(h[2], h[3]), hl1 = pkmin(h[2], h[3]);
                         uint32_t t1 = pkmax(hh0, hh1);
                         uint32_t t2 = pkmax3(pkmax3(l[0], l[1], l[2]), pkmax3(l[3], hl0, hl1), pkmin(hh0, hh1));
-#else
-                        uint32_t t1 = pkmax(P[0], P[1]), t2 = pkmin(P[0], P[1]);
-#pragma unroll
-                        for (int q = 2; q < 8; q++) {
-                            t2 = pkmax(t2, pkmin(t1, P[q]));
-                            t1 = pkmax(t1, P[q]);
-                        }
-#endif
                         if (rt > 0) {  // rows 32..63 of the wave: codes 32..63 -> 0..31 (bit 5 cleared)
                             t1 ^= 0x00200020u;
                             t2 ^= 0x00200020u;
                         }
                         const uint32_t lo = pkmin(c1, t1);
                         c1 = pkmax(c1, t1);
-                        c2 = MAGE_FP4_MAX3 ? pkmax3(lo, c2, t2) : pkmax(pkmax(lo, c2), t2);
+                        c2 = pkmax3(lo, c2, t2);
                     }
                     if (gating && g_tiles >= 64 && 4 * g_hits > g_tiles) gating = false;  // dense: fold all
                     if (!any) continue;  // no key of the column tile within maxDist: no flush
@@ -781,7 +761,7 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                         const uint32_t o1 = (uint32_t)xor32((int)c1, lane), o2 = (uint32_t)xor32((int)c2, lane);
                         const uint32_t lo = pkmin(c1, o1);
                         c1 = pkmax(c1, o1);
-                        c2 = MAGE_FP4_MAX3 ? pkmax3(lo, c2, o2) : pkmax(pkmax(lo, c2), o2);
+                        c2 = pkmax3(lo, c2, o2);
                     }
                     const int a1 = lo16s(c1), b1 = hi16s(c1);
                     const int m1 = max(a1, b1), m2 = max(min(a1, b1), max(lo16s(c2), hi16s(c2)));

@@ -74,9 +74,6 @@ struct Tile {
     int x, y;  // tile column / row in the frame
 };
 
-#ifndef MAGE_FAST_SCHED
-#define MAGE_FAST_SCHED 0  // 1: scheduling barriers between the ladders (register pressure experiment)
-#endif
 // Orders one wave's LDS writes before its other lanes' reads (when the waves of a workgroup
 // work on disjoint data no workgroup barrier is needed).
 __device__ __forceinline__ void wave_lds_sync()
@@ -225,10 +222,6 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const
         // interior tile (most of them): no reflection, addresses by increment.  A row is 8
         // sixteen-byte loads + one 8-byte tail (9 threads per row, 14 rows per pass; 16-byte global
         // loads need only dword alignment), stored as 8-byte LDS writes (rows are 8-byte aligned)
-#ifndef MAGE_FAST_LOAD16
-#define MAGE_FAST_LOAD16 1
-#endif
-#if MAGE_FAST_LOAD16
         static_assert(LW == 8 * 16 + 8, "row = 8 x 16 + 8 bytes");
         constexpr int RSTEP = FAST_THREADS / 9, NPASS = (LH + RSTEP - 1) / RSTEP;  // 14 rows per pass, 3 passes
         const int c = threadIdx.x % 9, r0 = threadIdx.x / 9;
@@ -255,17 +248,6 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ src, const
                 }
             }
         }
-#else
-        constexpr int QW = LW / 8, RSTEP = FAST_THREADS / QW;  // 17 qwords per row, 7 rows per pass
-        const int c = threadIdx.x % QW, r0 = threadIdx.x / QW;
-        if (r0 < RSTEP) {
-            const uint8_t* g = src + (long long)(gy0 + r0) * p.stride + gx0 + 8 * c;
-            const long long gstep = (long long)RSTEP * p.stride;
-#pragma unroll
-            for (int r = r0; r < LH; r += RSTEP, g += gstep)
-                *reinterpret_cast<uint2*>(&img[r][8 * c]) = *reinterpret_cast<const uint2*>(g);
-        }
-#endif
         return;
     }
     constexpr int DW = LW / 4;
@@ -330,9 +312,6 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
         const int Y = Y0 + r;
         if (Y < 3 || Y > p.h - 4) bytes = 0;
         sc[SR * chunk + r][gx] = bytes & colmask;
-#if MAGE_FAST_SCHED
-        __builtin_amdgcn_sched_barrier(0);
-#endif
     }
 }
 
@@ -359,9 +338,6 @@ __device__ __forceinline__ void score_strip(const uint8_t (*img)[LW], uint32_t (
 // holds at least one of the antipodal pixels 0 / 8 and one of 4 / 12, so "all darker" needs
 // max(min(x0, x8), min(x4, x12)) < v - G (and "all brighter" min(max(x0, x8), max(x4, x12)) > v + G):
 // two packed ops fewer per pixel pair, and never more pixels listed.
-#ifndef MAGE_GATE_ANTIPODAL
-#define MAGE_GATE_ANTIPODAL 1
-#endif
 __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_t (*sc)[GX], int G,
                                                const FastParams& p, Tile T)
 {
@@ -411,18 +387,10 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
         for (int P = 0; P < 2; P++) {
             const h2 v = cp[r + 3][P], a = cp[r][P], b = cp[r + 6][P];
             const h2 e = ep[P], d = dp[P];
-#if MAGE_GATE_ANTIPODAL
             // every 9-arc holds one of the antipodal pixels 0 / 8 (a, b) and one of 4 / 12 (d, e)
             const h2 hi = __builtin_elementwise_minimum(__builtin_elementwise_maximum(a, b), __builtin_elementwise_maximum(d, e));
             const h2 lo = __builtin_elementwise_maximum(__builtin_elementwise_minimum(a, b), __builtin_elementwise_minimum(d, e));
             t2[P] = as_u32(__builtin_elementwise_maximum(hi - v, v - lo) - gp1);  // >= 0: may reach G
-#else
-            const h2 pab = __builtin_elementwise_maximum(a, b), qab = __builtin_elementwise_minimum(a, b);
-            const h2 pde = __builtin_elementwise_maximum(d, e), qde = __builtin_elementwise_minimum(d, e);
-            const h2 x2l = max3h(__builtin_elementwise_minimum(pab, pde), qab, qde);  // second largest
-            const h2 x2s = min3h(__builtin_elementwise_maximum(qab, qde), pab, pde);  // second smallest
-            t2[P] = as_u32(__builtin_elementwise_maximum(x2l - v, v - x2s) - gp1);   // >= 0: may reach G
-#endif
         }
         sc[SR * chunk + r][gx] = 0u;
         // the signs of pixels 0..3 as 0xFF / 0x00 bytes (v_perm sign-extension selectors 8-11:
@@ -433,9 +401,6 @@ __device__ __forceinline__ uint32_t gate_strip(const uint8_t (*img)[LW], uint32_
     return ~neg & keep;
 }
 
-#ifndef MAGE_FAST_D16
-#define MAGE_FAST_D16 1  // ring bytes of a pixel pair by byte loads + one full-rate v_bitop3 per pair
-#endif
 // LDS byte offsets of the 16 ring pixels (and the centre, entry 16) from (centre - 3 LW - 3):
 // (dy + 3) LW + dx + 3 — every offset non-negative, as the DS offset field requires.
 static_assert(LW == 136, "ring_d16's immediate offsets assume LW = 136");
@@ -487,9 +452,6 @@ __device__ __forceinline__ uint32_t item_col(uint32_t it) { return __builtin_amd
 // Exact scores of two listed pixels (score row << 7 | score column) at once, one per f16 lane,
 // with threshold tf (listed pixels lie inside the FAST range, gate_strip).  Returns the two
 // score bytes (a in bits 0-7, b in bits 16-23).
-#ifndef MAGE_FAST_ONE_SIDE
-#define MAGE_FAST_ONE_SIDE 1
-#endif
 __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8_t* scb, uint32_t ia, uint32_t ib,
                                              h2 tf, h2 gp1)
 {
@@ -498,10 +460,8 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
     const uint8_t* ca = &img[ra_ + 3][ca_ + 4];
     const uint8_t* cb = &img[rb_ + 3][cb_ + 4];
     h2 x[16];
-#if MAGE_FAST_D16
     uint32_t ra[17], rb[17];
     ring_d16(lds_addr(ca - 3 * LW - 3), lds_addr(cb - 3 * LW - 3), ra, rb);
-#if MAGE_FAST_ONE_SIDE
     // One ladder per pixel.  A listed pixel passed gate_strip's dark or bright bound (antipodal
     // compass pixels 0 / 8 and 4 / 12, the same f16 arithmetic), and a side whose bound fails
     // scores <= G, i.e. 0 after the threshold G: so only the passing side needs its 9-arc
@@ -524,23 +484,6 @@ __device__ __forceinline__ uint32_t score_pixels(const uint8_t (*img)[LW], uint8
     if (__builtin_amdgcn_ballot_w64(((dk | br) & 0x80008000u) != 0x80008000u))
         raw = __builtin_elementwise_maximum(raw, fast_bright_hi(x) - v);
     const uint32_t sv = score2_clamp(raw, tf);
-#else
-    // [byte_a, 0x64, byte_b, 0x64]: 1024 + byte in both f16 lanes, one full-rate op per pair
-#pragma unroll
-    for (int k = 0; k < 16; k++) x[k] = as_h2(__builtin_amdgcn_bitop3_b32(ra[k], rb[k], 0x64006400u, 0xFE));
-    const h2 v = as_h2(__builtin_amdgcn_bitop3_b32(ra[16], rb[16], 0x64006400u, 0xFE));
-    const uint32_t sv = score2(fast_raw_ring(v, x), tf);
-#endif
-#else
-    auto pack = [](uint32_t a, uint32_t b) { return as_h2((a | (b << 16)) | 0x64006400u); };
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int off = ring_dy(k) * LW + ring_dx(k);
-        x[k] = pack(ca[off], cb[off]);
-    }
-    const h2 v = pack(ca[0], cb[0]);
-    const uint32_t sv = score2(fast_raw_ring(v, x), tf);
-#endif
     // (listed pixels lie inside the FAST range: gate_strip)
     const uint32_t sa = sv & 0xFFu, sb = (sv >> 16) & 0xFFu;
     scb[ra_ * (4 * GX) + ca_] = (uint8_t)sa;
@@ -688,117 +631,100 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[LH][LW];
     __shared__ uint32_t sc[SROWS][GX];  // scores; then the blurred tile
-#ifndef MAGE_FAST_DIRECT_OUT
-#define MAGE_FAST_DIRECT_OUT 1
-#endif
     // the tile's candidates (strict 3x3 maxima are never 8-adjacent: <= TCAP): written straight
     // into the tile's slot of the frame's candidate buffer (MAGE_FAST_DIRECT_OUT; no LDS list and
     // copy loop: 3.6 KB less LDS per workgroup), or staged in LDS
     const int tix = T.y * p.tiles_x + T.x;
     uint32_t* const tile_out = cand + (long long)f * p.cand_cap + (long long)tix * TCAP;
-#if MAGE_FAST_DIRECT_OUT
     uint32_t* const list = tile_out;
-#else
-    __shared__ uint32_t list[TCAP];
-#endif
     // gated pass: per wave, the pixels (score row << 7 | score column) that may reach the gate;
     // a wave with more than ICAP of them sends its tile through the exact strips (s_dense)
     constexpr uint32_t ICAP = 512;
     __shared__ __attribute__((aligned(4))) uint16_t items[FAST_THREADS / kWave][ICAP];
     __shared__ uint32_t s_cnt, s_dense;
-#ifndef MAGE_FAST_ABLATE
-#define MAGE_FAST_ABLATE 0  // tools/ablate_fast.py: 1 no blur, 2 no NMS / emission, 4 no score, 8 no tile load,
-                            // 64 gated: no exact scoring of the listed groups
-#endif
-    constexpr bool kBlur = !(MAGE_FAST_ABLATE & 1), kNms = !(MAGE_FAST_ABLATE & 2);
-    constexpr bool kScore = !(MAGE_FAST_ABLATE & 4), kLoad = !(MAGE_FAST_ABLATE & 8);
-    constexpr bool kEmit = !(MAGE_FAST_ABLATE & 16), kSink = (MAGE_FAST_ABLATE & 32) != 0;
-    uint32_t s_sink_acc = 0;
     FAST_STAMP(0);
-    if (kLoad) load_tile(frames + (long long)f * p.pitch, p, img, T);
+    load_tile(frames + (long long)f * p.pitch, p, img, T);
     if (threadIdx.x == 0) s_cnt = s_dense = 0;
     __syncthreads();
     FAST_STAMP(1);
-    const bool gated = kMayGate && kScore && G > p.threshold;
+    const bool gated = kMayGate && G > p.threshold;
     uint32_t total = 0;  // gated: the wave's listed pixels
-    if (kScore) {
-        if (gated) {
-            // gated: compass test per strip, then the wave's passing groups scored exactly,
-            // compacted over the wave's lanes
-            const uint32_t pix = gate_strip(img, sc, G, p, T);
-            FAST_STAMP(2);
-            const uint32_t cnt = __builtin_popcount(pix);
-            uint32_t pre = 0;
+    if (gated) {
+        // gated: compass test per strip, then the wave's passing groups scored exactly,
+        // compacted over the wave's lanes
+        const uint32_t pix = gate_strip(img, sc, G, p, T);
+        FAST_STAMP(2);
+        const uint32_t cnt = __builtin_popcount(pix);
+        uint32_t pre = 0;
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const uint64_t b = __ballot((cnt >> j) & 1u);
-                pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u)) << j;
-                total += (uint32_t)__builtin_popcountll(b) << j;
-            }
-            if (total > ICAP) {
-                if (__lane_id() == 0) s_dense = 1u;  // this tile goes through the exact strips
-            } else {
-                uint16_t* wl = items[threadIdx.x / kWave];
-                const uint32_t ibase = threadIdx.x << 5;  // item layout: item_row / item_col
-                uint32_t rb = pix;
-                while (rb) {
-                    const int b = __builtin_ctz(rb);
-                    rb &= rb - 1u;
-                    wl[pre++] = (uint16_t)(ibase | (uint32_t)b);
-                }
-            }
-            FAST_STAMP(3);
-            __syncthreads();  // s_dense is final
-            FAST_STAMP(4);
-            if (s_dense) {
-                score_strip(img, sc, p, T);
-            } else if (!(MAGE_FAST_ABLATE & 64)) {
-                // the wave's listed pixels, two per lane; the ones that reach G (the only
-                // possible maxima) are compacted in place to the front of the list for the NMS
-                uint16_t* wl = items[threadIdx.x / kWave];
-                const _Float16 gt = (_Float16)(float)G, gt1 = (_Float16)(float)(G + 1);
-                const h2 tg = {gt, gt}, tg1 = {gt1, gt1};
-                uint8_t* scb = reinterpret_cast<uint8_t*>(&sc[0][0]);
-                uint32_t nz = 0;
-                for (uint32_t i0 = 0; i0 < total; i0 += 2 * kWave) {
-                    const uint32_t i = i0 + 2 * __lane_id();
-                    uint32_t ia = 0, ib = 0;
-                    bool fa = false, fb = false;
-                    if (i < total) {
-                        const uint32_t pr = *reinterpret_cast<const uint32_t*>(&wl[i]);  // i even: one dword
-                        ia = pr & 0xFFFFu;
-                        ib = i + 1 < total ? pr >> 16 : ia;
-                        const uint32_t ss = score_pixels(img, scb, ia, ib, tg, tg1);
-                        fa = (ss & 0xFFu) != 0;
-                        fb = i + 1 < total && (ss >> 16) != 0;
-                    }
-                    // every lane read its items before any lane writes (writes land below i0 + 128)
-                    const uint64_t ba = __ballot(fa), bb = __ballot(fb);
-                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(ba >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ba, 0u)) +
-                                           __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
-                    const uint32_t pa = nz + below;
-                    if (fa) wl[pa] = (uint16_t)ia;
-                    if (fb) wl[pa + (fa ? 1u : 0u)] = (uint16_t)ib;
-                    nz += (uint32_t)(__builtin_popcountll(ba) + __builtin_popcountll(bb));
-                }
-                total = nz;
-                FAST_STAMP(5);
-            }
-        } else {
-            score_strip(img, sc, p, T);
+        for (int j = 0; j < 6; j++) {
+            const uint64_t b = __ballot((cnt >> j) & 1u);
+            pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u)) << j;
+            total += (uint32_t)__builtin_popcountll(b) << j;
         }
+        if (total > ICAP) {
+            if (__lane_id() == 0) s_dense = 1u;  // this tile goes through the exact strips
+        } else {
+            uint16_t* wl = items[threadIdx.x / kWave];
+            const uint32_t ibase = threadIdx.x << 5;  // item layout: item_row / item_col
+            uint32_t rb = pix;
+            while (rb) {
+                const int b = __builtin_ctz(rb);
+                rb &= rb - 1u;
+                wl[pre++] = (uint16_t)(ibase | (uint32_t)b);
+            }
+        }
+        FAST_STAMP(3);
+        __syncthreads();  // s_dense is final
+        FAST_STAMP(4);
+        if (s_dense) {
+            score_strip(img, sc, p, T);
+        } else {
+            // the wave's listed pixels, two per lane; the ones that reach G (the only
+            // possible maxima) are compacted in place to the front of the list for the NMS
+            uint16_t* wl = items[threadIdx.x / kWave];
+            const _Float16 gt = (_Float16)(float)G, gt1 = (_Float16)(float)(G + 1);
+            const h2 tg = {gt, gt}, tg1 = {gt1, gt1};
+            uint8_t* scb = reinterpret_cast<uint8_t*>(&sc[0][0]);
+            uint32_t nz = 0;
+            for (uint32_t i0 = 0; i0 < total; i0 += 2 * kWave) {
+                const uint32_t i = i0 + 2 * __lane_id();
+                uint32_t ia = 0, ib = 0;
+                bool fa = false, fb = false;
+                if (i < total) {
+                    const uint32_t pr = *reinterpret_cast<const uint32_t*>(&wl[i]);  // i even: one dword
+                    ia = pr & 0xFFFFu;
+                    ib = i + 1 < total ? pr >> 16 : ia;
+                    const uint32_t ss = score_pixels(img, scb, ia, ib, tg, tg1);
+                    fa = (ss & 0xFFu) != 0;
+                    fb = i + 1 < total && (ss >> 16) != 0;
+                }
+                // every lane read its items before any lane writes (writes land below i0 + 128)
+                const uint64_t ba = __ballot(fa), bb = __ballot(fb);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(ba >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ba, 0u)) +
+                                       __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
+                const uint32_t pa = nz + below;
+                if (fa) wl[pa] = (uint16_t)ia;
+                if (fb) wl[pa + (fa ? 1u : 0u)] = (uint16_t)ib;
+                nz += (uint32_t)(__builtin_popcountll(ba) + __builtin_popcountll(bb));
+            }
+            total = nz;
+            FAST_STAMP(5);
+        }
+    } else {
+        score_strip(img, sc, p, T);
     }
     __syncthreads();
     // the FAST passes are done with the image: bias it for the blur's i8 MFMA operands
     FAST_STAMP(6);
-    if (kBlur && blur) xor_tile(img);
+    if (blur) xor_tile(img);
     FAST_STAMP(7);
     // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter, four
     // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8).  Scores
     // are split into even / odd pixels as f16 lanes (1024 + s); per score row the left / right
     // neighbour-aligned copies and the 3-wide maximum are formed once and rolled down, so a
     // pixel's 8-neighbour maximum is max(H3(up), H3(down), left, right).
-    if (kNms && gated && !s_dense) {
+    if (gated && !s_dense) {
         // gated: every score outside the listed pixels is 0, so the strict 3x3 maxima are among
         // them; per listed output pixel (score rows 1..TH, columns 4..TW+3) the 8 neighbours
         const uint16_t* wl = items[threadIdx.x / kWave];
@@ -822,10 +748,6 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                     c = ((uint32_t)Y << 20) | ((uint32_t)X << 8) | v;
                 }
             }
-            if (!kEmit) {
-                s_sink_acc |= c;
-                continue;
-            }
             const uint64_t b = __ballot(m);
             if (b) {
                 uint32_t base = 0;
@@ -835,7 +757,7 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                 if (m) list[base + pre] = c;
             }
         }
-    } else if (kNms) {
+    } else {
         constexpr int OG = TW / 4;  // 30 output groups per row
         const int og = threadIdx.x % 32, chunk = threadIdx.x / 32;
         const int X0 = T.x * TW + 4 * og;
@@ -882,37 +804,33 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
                 M = D;
             }
         }
-        if (!kEmit) {
-            s_sink_acc |= bits;
-        } else {
-            // one LDS atomic per wave: exclusive prefix of the lanes' counts (<= 32) from the
-            // ballots of their bit planes, then each lane writes its maxima at base + prefix
-            const uint32_t cnt = __builtin_popcount(bits);
-            uint32_t pre = 0, total = 0;
+        // one LDS atomic per wave: exclusive prefix of the lanes' counts (<= 32) from the
+        // ballots of their bit planes, then each lane writes its maxima at base + prefix
+        const uint32_t cnt = __builtin_popcount(bits);
+        uint32_t pre = 0, total = 0;
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const uint64_t b = __ballot((cnt >> j) & 1u);
-                pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u)) << j;
-                total += (uint32_t)__builtin_popcountll(b) << j;
-            }
-            if (total) {
-                uint32_t base = 0;
-                if (__lane_id() == 0) base = atomicAdd(&s_cnt, total);
-                uint32_t idx = __builtin_amdgcn_readfirstlane(base) + pre;
-                const uint8_t* scb = reinterpret_cast<const uint8_t*>(&sc[0][0]);
-                while (bits) {
-                    const int b = __builtin_ctz(bits);
-                    bits &= bits - 1u;
-                    const int oy = oy0 + (b >> 2), q = b & 3;
-                    const uint32_t sv = scb[(oy + 1) * (4 * GX) + 4 * (og + 1) + q];
-                    list[idx++] = ((uint32_t)(T.y * TH + oy) << 20) | ((uint32_t)(X0 + q) << 8) | sv;
-                }
+        for (int j = 0; j < 6; j++) {
+            const uint64_t b = __ballot((cnt >> j) & 1u);
+            pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u)) << j;
+            total += (uint32_t)__builtin_popcountll(b) << j;
+        }
+        if (total) {
+            uint32_t base = 0;
+            if (__lane_id() == 0) base = atomicAdd(&s_cnt, total);
+            uint32_t idx = __builtin_amdgcn_readfirstlane(base) + pre;
+            const uint8_t* scb = reinterpret_cast<const uint8_t*>(&sc[0][0]);
+            while (bits) {
+                const int b = __builtin_ctz(bits);
+                bits &= bits - 1u;
+                const int oy = oy0 + (b >> 2), q = b & 3;
+                const uint32_t sv = scb[(oy + 1) * (4 * GX) + 4 * (og + 1) + q];
+                list[idx++] = ((uint32_t)(T.y * TH + oy) << 20) | ((uint32_t)(X0 + q) << 8) | sv;
             }
         }
     }
     FAST_STAMP(8);
     // the blur reads only the (biased) image tile and writes the frame directly
-    if (kBlur && blur) {
+    if (blur) {
         __syncthreads();  // xor_tile is complete
         FAST_STAMP(9);
         blur_mfma(img, p, f, T);
@@ -920,23 +838,11 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
     }
     __syncthreads();  // s_cnt and the tile's list are final
     FAST_STAMP(11);
-    if (kSink || !kEmit) {  // ablation: keep the skipped stages' inputs alive
-        if (kSink) {
-            const uint32_t* w = &sc[0][0];
-            for (int i = threadIdx.x; i < SROWS * GX; i += FAST_THREADS) s_sink_acc ^= w[i];
-            s_sink_acc ^= reinterpret_cast<const uint32_t*>(&img[0][0])[threadIdx.x];
-        }
-        if (s_sink_acc == 0x12345678u) counts[f] = s_sink_acc;
-        __syncthreads();
-    }
     // the tile's own slot of the frame's candidate buffer (TCAP entries) and count: no global
     // atomics (the 264 tiles of a 720p frame run at once, and one counter per frame serialised
     // them at the L2)
     const uint32_t n = s_cnt;
     if (threadIdx.x == 0) counts[(long long)f * p.tiles + tix] = n;
-#if !MAGE_FAST_DIRECT_OUT
-    for (uint32_t k = threadIdx.x; k < n; k += FAST_THREADS) tile_out[k] = list[k];
-#endif
     FAST_STAMP(12);
 }
 
@@ -1037,12 +943,6 @@ __device__ unsigned long long g_sel_stamps[1024][16];
 #define SEL_STAMP(k)
 #endif
 
-#ifndef MAGE_SEL_CREG
-#define MAGE_SEL_CREG 1  // select's candidate passes from registers (one global read per candidate)
-#endif
-#ifndef MAGE_SEL_RUN4
-#define MAGE_SEL_RUN4 1  // the ANMS square search reads a row's run four items at a time
-#endif
 // Frame f; G is the candidate gate its FAST pass ran with (no gate when G <= fast_threshold).
 #ifndef MAGE_GATE_SHIFT
 #define MAGE_GATE_SHIFT 4  // next gate = lower - lower / 2^MAGE_GATE_SHIFT (15/16: tools/gate_probe.py)
@@ -1099,7 +999,6 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
     SEL_STAMP(1);
     const int n0 = (int)tstart[T];
     // the candidates tile by tile (4 threads per tile slot: no binary search per candidate)
-#if MAGE_SEL_CREG
     // the thread's first SEL_CR entries of its tile slot are loaded once, all in flight together,
     // and kept in registers for both passes below
     constexpr int SEL_CR = 4;
@@ -1124,16 +1023,6 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
             for (int j = w & 3; j < e; j += 4) fn(ct[j]);
         }
     };
-#else
-    auto for_each_cand = [&](auto&& fn) {
-        for (int w = tid; w < 4 * T; w += SEL_THREADS) {
-            const int t = w >> 2;
-            const int e = (int)(tstart[t + 1] - tstart[t]);
-            const uint32_t* ct = C + (long long)t * TCAP;
-            for (int j = w & 3; j < e; j += 4) fn(ct[j]);
-        }
-    };
-#endif
     for_each_cand([&](uint32_t c) { atomicAdd(&hist[cand_s(c)], 1u); });
     __syncthreads();
     SEL_STAMP(2);
@@ -1358,7 +1247,6 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
                     for (int cYY = y0; cYY <= y1; cYY++) {
                         const uint32_t e = cellStart[cYY * numX + x1 + 1];
                         uint32_t qq = cellStart[cYY * numX + x0];
-#if MAGE_SEL_RUN4
                         // four items of the row's run per step: their LDS reads in flight together
                         for (; qq + 4 <= e; qq += 4) {
                             const uint32_t o0 = sorted[qq], o1 = sorted[qq + 1], o2 = sorted[qq + 2], o3 = sorted[qq + 3];
@@ -1367,7 +1255,6 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
                             visit(o2);
                             visit(o3);
                         }
-#endif
                         for (; qq < e; qq++) visit(sorted[qq]);
                     }
                 } else {
@@ -1690,20 +1577,10 @@ constexpr int KPW = MAGE_DESC_KPW;
                           // 0.095 at 2 (tools/abl.py): more window loads in flight per wave
 #endif
 constexpr int KPW7 = MAGE_DESC_KPW7;
-#ifndef MAGE_DESC_WP_PAD
-#define MAGE_DESC_WP_PAD 0
-#endif
-static_assert(MAGE_DESC_WP_PAD % 16 == 0, "window rows stay 16-byte aligned (b128 stores)");
 #ifndef MAGE_DESC_KP_WIDE
 #define MAGE_DESC_KP_WIDE 2  // keypoints per wave for the rotated (radius 18) windows: rBRIEF-31 describe 0.205 ms at 1, 0.192 at 2, 0.230 at 3 (pattern rows hoisted; before that 0.254 at 1, 0.306 at 2)
 #endif
 
-#ifndef MAGE_DESC_COMPACT
-#define MAGE_DESC_COMPACT 1
-#endif
-#ifndef MAGE_DESC_HOIST
-#define MAGE_DESC_HOIST 1  // pattern rows loaded once per wave ahead of the windows, 8 LDS reads in flight per keypoint
-#endif
 // f(std::integral_constant<int, j>) for j = 0 .. N-1, unrolled at compile time
 template <int N, int J = 0, class F>
 __device__ __forceinline__ void static_for(F&& f)
@@ -1720,7 +1597,6 @@ __device__ __forceinline__ void static_for(F&& f)
 // lines touched drop from 10 to 5 for the ~55 % of windows inside one 32-byte brick column.
 // LDS rows have an odd number of 16-byte parts, so the 4-5 dwords a row's tests read start 4
 // banks apart for 8 consecutive rows (tests bank as (a / 4) mod 32).
-#if MAGE_DESC_COMPACT
 template <int RB, bool MULTI, int KP>
 __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     DescParams p, const uint32_t* __restrict__ xy_in, const uint32_t* __restrict__ n_in,
@@ -1743,7 +1619,6 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     const int n = (int)n_in[f];
     if (k0 >= n) return;
     const int R = p.R;
-#if MAGE_DESC_HOIST
     // the tests' pattern rows, issued ahead of the window loads so both round trips overlap
     // (without orientation the wave's keypoints share one set; the per-keypoint loads of the
     // loop below had left each of its 4 chunks waiting on an L2 round trip of its own)
@@ -1762,7 +1637,6 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
     if (p.random)
 #pragma unroll
         for (int q = 0; q < KP; q++) ang[q] = p.kp_angle[7 * ((long long)f * p.out_cap + min(k0 + q, n - 1))];
-#endif
     // load slot j: keypoint q, item i = row i / NP, part i % NP; keypoints keep the pattern
     // radius from the border (RunByImageBorder), so the clamps only keep reads inside the level
     // (a native vector type: HIP's uint4 struct copies stayed memcpys through a private array,
@@ -1794,7 +1668,6 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
         if (i < NI) *reinterpret_cast<u32x4*>(&win[wave][q][r * WPC + 16 * pt]) = v[j];
     });
     wave_lds_sync();
-#if MAGE_DESC_HOIST
 #pragma unroll
     for (int q = 0; q < KP; q++) {
         const int k = k0 + q;
@@ -1826,118 +1699,9 @@ __global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
         }
         if (lane < 4) reinterpret_cast<unsigned long long*>(desc_out + ki * 32)[lane] = mw;
     }
-#else
-    const char4* pat = reinterpret_cast<const char4*>(pattern);
-#pragma unroll
-    for (int q = 0; q < KP; q++) {
-        const int k = k0 + q;
-        if (k >= n) break;
-        const long long ki = (long long)f * p.out_cap + k;
-        const uint32_t xy = xy_in[ki];
-        const int rot = MULTI ? (p.lvl[ki] & 0xFF) : 0;
-        const uint8_t* wb = &win[wave][q][((int)(xy & 0xFFFFu) - R) & 15];  // (x0 & 15): the window's column phase
-        const char4* pr = pat + (p.random ? 0 : rot * 256);  // cvRound(angle / 12) % 30 (:526)
-        float ra = 1.f, rb_ = 0.f;  // random pattern: rotation by the keypoint angle
-        if (p.random) pattern_rotation(p.kp_angle[7 * ki], ra, rb_);
-        unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ki * 32);
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            char4 e = pr[c * kWave + lane];  // (x0, y0, x1, y1) of bit 64*c + lane
-            if (p.random) e = rotate_test(e, ra, rb_);
-            const int t0 = wb[(R + e.y) * WPC + R + e.x];
-            const int t1 = wb[(R + e.w) * WPC + R + e.z];
-            const unsigned long long m = __ballot(t0 < t1);
-            if (lane == 0) dst[c] = m;
-        }
-    }
-#endif
 }
-#endif
 // Whole-brick windows (MAGE_DESC_COMPACT=0): MULTI = false (one level, no orientation: the
 // default configuration): level 0 and rotation 0 without the per-keypoint level lookups.
-#if !MAGE_DESC_COMPACT
-template <int RB, bool MULTI, int KP>
-__global__ __launch_bounds__(DESC_WAVES * kWave) void describe_blurred_kernel(
-    DescParams p, const uint32_t* __restrict__ xy_in, const uint32_t* __restrict__ n_in,
-    const int8_t* __restrict__ pattern, uint8_t* __restrict__ desc_out)
-{
-    constexpr int BDMAX = 2 * RB + 1;
-    // the window's bricks (BLUR_BRICK: 4 rows x 32 bytes): any row / column phase
-    constexpr int NBR = (BDMAX + 3 + 3) / 4, NBC = (BDMAX + 31 + 31) / 32;
-    constexpr int NIT = NBR * NBC * 8;  // 16-byte items, 8 per brick (one 128-byte line)
-    constexpr int NLD = (NIT + kWave - 1) / kWave;
-    // LDS window row pitch: 32 NBC bytes + MAGE_DESC_WP_PAD.  The tests' byte reads bank as
-    // (a / 4) mod 32 per 32-lane group; at a 64-byte pitch rows r and r + 2 share their banks
-    // (SQ_LDS_BANK_CONFLICT 43 % of the kernel's cycles).  A 16 / 32 / 48-byte pad spreads the
-    // rows over all banks but costs occupancy (8 -> 6 workgroups per CU): describe 0.138 ->
-    // 0.176 / 0.201 / 0.230 ms on C2 — the kernel is bound by its window gathers, not the LDS.
-    constexpr int WP = 32 * NBC + MAGE_DESC_WP_PAD;
-    __shared__ __attribute__((aligned(16))) uint8_t win[DESC_WAVES][KP][4 * NBR * WP];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave: scalar
-    // XCD-aware 1-D grid: workgroups are dispatched round-robin over the 8 XCDs, so block b runs
-    // on XCD b % 8; all keypoint chunks of frame f get blocks = f (mod 8) and consecutive slots,
-    // so the frame's blurred image is fetched into one XCD's L2 once (placement affects speed only)
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    const int chunk = slot % p.chunks, f = (slot / p.chunks) * 8 + xcd;
-    if (f >= p.frames) return;
-    const int k0 = (chunk * DESC_WAVES + wave) * KP;
-    const int n = (int)n_in[f];
-    if (k0 >= n) return;
-    const int R = p.R;
-    // lane item i -> brick i / 8 of the window, 16-byte part i % 8; keypoints keep the pattern
-    // radius from the border (RunByImageBorder), so the clamps are inert: they only keep reads
-    // inside the level
-    uint4 v[KP][NLD];
-    int off[KP], rot[KP];
-#pragma unroll
-    for (int q = 0; q < KP; q++) {
-        const long long ki = (long long)f * p.out_cap + min(k0 + q, n - 1);
-        const uint32_t xy = xy_in[ki];
-        const int lv = MULTI ? __builtin_amdgcn_readfirstlane(p.lvl[ki]) : 0, l = lv >> 8;  // wave-uniform
-        rot[q] = lv & 0xFF;
-        const uint8_t* src = p.lev.base[l] + (long long)f * p.lev.pitch[l];
-        const int bcols = p.lev.stride[l], brows = (p.lh[MULTI ? l : 0] + 3) >> 2;
-        const int x0 = (int)(xy & 0xFFFFu) - R, y0 = (int)(xy >> 16) - R;
-        const int bx0 = max(x0, 0) >> 5, by0 = max(y0, 0) >> 2;
-        off[q] = (y0 - 4 * by0) * WP + (x0 - 32 * bx0);
-#pragma unroll
-        for (int ld = 0; ld < NLD; ld++) {
-            const int i = min(lane + kWave * ld, NIT - 1), b = i >> 3, br = b / NBC, bc = b - br * NBC;
-            const int gbr = min(by0 + br, brows - 1), gbc = min(bx0 + bc, bcols - 1);
-            v[q][ld] = *reinterpret_cast<const uint4*>(src + ((long long)gbr * bcols + gbc) * 128 + 16 * (i & 7));
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < KP; q++)
-#pragma unroll
-        for (int ld = 0; ld < NLD; ld++) {
-            const int i = lane + kWave * ld, b = i >> 3, br = b / NBC, bc = b - br * NBC;
-            if (i < NIT)
-                *reinterpret_cast<uint4*>(&win[wave][q][(4 * br + ((i & 7) >> 1)) * WP + 32 * bc + 16 * (i & 1)]) = v[q][ld];
-        }
-    wave_lds_sync();
-    const char4* pat = reinterpret_cast<const char4*>(pattern);
-#pragma unroll
-    for (int q = 0; q < KP; q++) {
-        const int k = k0 + q;
-        if (k >= n) break;
-        const uint8_t* wb = &win[wave][q][off[q]];
-        const char4* pr = pat + (p.random ? 0 : rot[q] * 256);  // cvRound(angle / 12) % 30 (:526)
-        float ra = 1.f, rb_ = 0.f;  // random pattern: rotation by the keypoint angle
-        if (p.random) pattern_rotation(p.kp_angle[7 * ((long long)f * p.out_cap + k)], ra, rb_);
-        unsigned long long* dst = reinterpret_cast<unsigned long long*>(desc_out + ((long long)f * p.out_cap + k) * 32);
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            char4 e = pr[c * kWave + lane];  // (x0, y0, x1, y1) of bit 64*c + lane
-            if (p.random) e = rotate_test(e, ra, rb_);
-            const int t0 = wb[(R + e.y) * WP + R + e.x];
-            const int t1 = wb[(R + e.w) * WP + R + e.z];
-            const unsigned long long m = __ballot(t0 < t1);
-            if (lane == 0) dst[c] = m;
-        }
-    }
-}
-#endif
 
 
 // Descriptors with the 7-tap Gaussian computed per keypoint window on the matrix cores instead of

@@ -19,6 +19,23 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 
 
+def variant_source(stem):
+    """csrc/<stem> with tools/patches/<name>_variants.patch applied (the ablation / experiment
+    switches removed from the product sources in round 6) as csrc/.abl_variants_<stem>; the caller
+    deletes it.  Without a patch for the file: the product source itself."""
+    sys.path.insert(0, str(ROOT))
+    from mageslam_amd import build as B
+
+    patch = ROOT / "tools" / "patches" / (Path(stem).stem + "_variants.patch")
+    if not patch.exists():
+        return B.CSRC / stem, False
+    out = B.CSRC / f".abl_variants_{stem}"
+    out.write_bytes((B.CSRC / stem).read_bytes())
+    with open(patch, "rb") as f:
+        subprocess.run(["patch", "-s", str(out)], stdin=f, check=True)
+    return out, True
+
+
 def build(src, specs):
     sys.path.insert(0, str(ROOT))
     from mageslam_amd import build as B
@@ -33,14 +50,14 @@ def build(src, specs):
         out.mkdir(parents=True, exist_ok=True)
         obj = out / (stem + ".o")
         flags = [f"-D{d}" for d in defs.split("+") if d]
-        src_path = B.CSRC / stem
+        src_path, tmp = variant_source(stem)
         if rev:
             src_path = B.CSRC / f".abl_{name}_{stem}"
             src_path.write_bytes(subprocess.run(["git", "show", f"{rev}:mageslam_amd/csrc/{stem}"], cwd=ROOT,
                                                 check=True, capture_output=True).stdout)
         subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON, *flags,
                         "-c", str(src_path), "-o", str(obj)], check=True)
-        if rev:
+        if rev or tmp:
             src_path.unlink()
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
                         str(obj), *map(str, objs)], check=True)

@@ -27,16 +27,20 @@ def build():
     sys.path.insert(0, str(ROOT))
     from mageslam_amd import build as B
     B.build()
+    from abl import variant_source
+
+    src, _ = variant_source("ba.hip")  # the product source + tools/patches/ba_variants.patch
     objs = [p for p in B.OBJ.glob("*.o") if not p.name.startswith("ba.")]
     for i, v in enumerate(VARIANTS):
         out = ROOT / "abl" / f"ba_{i}"
         out.mkdir(parents=True, exist_ok=True)
         subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON,
-                        *defines(v), "-c", str(B.CSRC / "ba.hip"), "-o", str(out / "ba.o")], check=True)
+                        *defines(v), "-c", str(src), "-o", str(out / "ba.o")], check=True)
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
                         str(out / "ba.o"), *map(str, objs)], check=True)
         (out / "variant.txt").write_text(v)
         print("built", out, v)
+    src.unlink()
 
 
 def run():

@@ -23,6 +23,9 @@ def build():
     sys.path.insert(0, str(ROOT))
     from mageslam_amd import build as B
     B.build()
+    from abl import variant_source
+
+    src, _ = variant_source("orb.hip")  # the product source + tools/patches/orb_variants.patch
     objs = [p for p in (B.OBJ).glob("*.o") if not p.name.startswith("orb")]
     for v in VARIANTS:
         out = ROOT / "abl" / ("f" + v.replace(":", "w"))
@@ -31,11 +34,12 @@ def build():
         a, w, sch, kpw = (v.split(":") + ["", "", ""])[:4]
         subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON,
                         f"-DMAGE_FAST_ABLATE={a}", f"-DMAGE_FAST_WAVES_PER_EU={w or 5}", f"-DMAGE_FAST_SCHED={sch or 0}", f"-DMAGE_DESC_KPW={kpw or 4}",
-                        "-c", str(B.CSRC / "orb.hip"),
+                        "-c", str(src),
                         "-o", str(obj)], check=True)
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
                         str(obj), *map(str, objs)], check=True)
         print("built", out)
+    src.unlink()
 
 
 def run():

@@ -19,16 +19,20 @@ def build():
     sys.path.insert(0, str(ROOT))
     from mageslam_amd import build as B
     B.build()
+    from abl import variant_source
+
+    src, _ = variant_source("match.hip")  # the product source + tools/patches/match_variants.patch
     objs = [p for p in (B.OBJ).glob("*.o") if not p.name.startswith("match")]
     for v in VARIANTS:
         out = ROOT / "abl" / f"v{v}"
         out.mkdir(parents=True, exist_ok=True)
         obj = out / "match.o"
         subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON,
-                        f"-DMAGE_MATCH_ABLATE={v}", "-c", str(B.CSRC / "match.hip"), "-o", str(obj)], check=True)
+                        f"-DMAGE_MATCH_ABLATE={v}", "-c", str(src), "-o", str(obj)], check=True)
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
                         str(obj), *map(str, objs)], check=True)
         print("built", out)
+    src.unlink()
 
 
 def run():
