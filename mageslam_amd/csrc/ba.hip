@@ -724,6 +724,10 @@ __device__ __forceinline__ void schur_write(const SchurPair& pr, int k, double s
     const bool diag = pr.h1 == pr.h2;
     if (k < 36) {
         const int r = k / 6, c = k % 6;
+        // a diagonal block's (r, c) and (c, r) sums add the same products in another order: only
+        // the upper entry's value is written, to both triangles (one writer per address, so the
+        // result does not depend on which store lands last)
+        if (diag && r > c) return;
         double v = -sum;
         if (diag) v += cam + (r == c ? lambda : 0.0);
         // tether H12 blocks of this camera pair (code = 2 t + transposed)
@@ -842,23 +846,31 @@ __global__ __launch_bounds__(SC_THREADS) void schur_chunks(const SchurChunk* __r
     if (t < 42) schur_write(pr, t, red[0][t], 0.0, lambda, np, ptlist, tout, S, rhs);
 }
 
-// Diagonal pairs and pairs of more than one chunk: a 64-lane wave per pair adds its chunk partials
+// Diagonal pairs and pairs of more than one chunk: entry t < 42 of a pair adds its chunk partials
 // in chunk order.  A diagonal pair's camera block comes from the linearisation partials (chunk
 // order, then the tethers in set order: g2o's addEdge order), written to Hpp / bp as well
-// (update_state's computeScale reads bp).
-__global__ __launch_bounds__(64) void schur_finish(const int* __restrict__ flist, const SchurPair* __restrict__ pairs,
-                                                   const double* __restrict__ part, const double* __restrict__ campart,
-                                                   const Tether* __restrict__ teth, int nt,
-                                                   double* __restrict__ Hpp, double* __restrict__ bp,
-                                                   double lambda, int np, const int* __restrict__ ptlist,
-                                                   const double* __restrict__ tout, double* __restrict__ S,
-                                                   double* __restrict__ rhs)
+// (update_state's computeScale reads bp).  A 64-lane wave per pair.
+struct FinishArgs {
+    const int* flist;
+    int nf;  // pairs in flist (0: S and rhs are complete)
+    const SchurPair* pairs;
+    const double* part;
+    const double* campart;
+    const Tether* teth;
+    int nt;
+    double* Hpp;
+    double* bp;
+    double lambda;
+    const int* ptlist;
+    const double* tout;
+    double* S;
+    double* rhs;
+};
+
+__device__ __forceinline__ void finish_entry(const FinishArgs& a, const SchurPair& pr, int t, int np)
 {
-    const SchurPair pr = pairs[flist[blockIdx.x]];
-    const int t = threadIdx.x;
-    if (t >= 42) return;
     double v = 0;
-    for (int q = 0; q < pr.nslots; q++) v += part[(long long)(pr.slot0 + q) * 42 + t];
+    for (int q = 0; q < pr.nslots; q++) v += a.part[(long long)(pr.slot0 + q) * 42 + t];
     double cam = 0;
     if (pr.h1 == pr.h2) {
         const int h = pr.h1;
@@ -870,20 +882,26 @@ __global__ __launch_bounds__(64) void schur_finish(const int* __restrict__ flist
         } else {
             pk = 21 + (t - 36);
         }
-        for (int q = 0; q < CAM_CHUNKS; q++) cam += campart[((long long)h * CAM_CHUNKS + q) * 27 + pk];
-        for (int i = 0; i < nt; i++) {
-            const Tether& T = teth[i];
+        for (int q = 0; q < CAM_CHUNKS; q++) cam += a.campart[((long long)h * CAM_CHUNKS + q) * 27 + pk];
+        for (int i = 0; i < a.nt; i++) {
+            const Tether& T = a.teth[i];
             if (!T.active) continue;
             for (int vtx = 0; vtx < 2; vtx++) {
                 if ((vtx ? T.h2 : T.h1) != h) continue;
-                const double* o = tout + (long long)i * TETHER_OUT;
+                const double* o = a.tout + (long long)i * TETHER_OUT;
                 cam += t < 36 ? o[36 * vtx + r * 6 + c] : o[108 + 6 * vtx + (t - 36)];
             }
         }
-        if (t < 36) Hpp[36 * (long long)pr.c1 + t] = cam;
-        else bp[6 * pr.c1 + (t - 36)] = cam;
+        if (t < 36) a.Hpp[36 * (long long)pr.c1 + t] = cam;
+        else a.bp[6 * pr.c1 + (t - 36)] = cam;
     }
-    schur_write(pr, t, v, cam, lambda, np, ptlist, tout, S, rhs);
+    schur_write(pr, t, v, cam, a.lambda, np, a.ptlist, a.tout, a.S, a.rhs);
+}
+
+__global__ __launch_bounds__(64) void schur_finish(FinishArgs a, int np)
+{
+    const SchurPair pr = a.pairs[a.flist[blockIdx.x]];
+    if (threadIdx.x < 42) finish_entry(a, pr, threadIdx.x, np);
 }
 
 // Dense SPD solve S x = b in one workgroup, S of padded order np (multiple of 16, rows n..np-1
@@ -3255,11 +3273,14 @@ struct BundleAdjuster {
                    (const double*)d_camk.as<double>(), (const double*)d_bl.as<double>(), lam, np, n_entries,
                    (const int*)d_ptlist.as<int>(), (const double*)d_tout.as<double>(), d_spart.as<double>(), d_S.as<double>(),
                    d_rhs.as<double>());
-            launch("ba.schur_finish", schur_finish, dim3(n_sfinish), dim3(64), 0, st, (const int*)d_sfinish.as<int>(),
-                   (const SchurPair*)d_spairs.as<SchurPair>(), (const double*)d_spart.as<double>(),
-                   (const double*)d_campart.as<double>(), (const Tether*)d_teth.as<Tether>(), (int)teth.size(),
-                   d_Hpp.as<double>(), d_bp.as<double>(), lam, np, (const int*)d_ptlist.as<int>(),
-                   (const double*)d_tout.as<double>(), d_S.as<double>(), d_rhs.as<double>());
+            const FinishArgs fin{(const int*)d_sfinish.as<int>(), n_sfinish, (const SchurPair*)d_spairs.as<SchurPair>(),
+                                 (const double*)d_spart.as<double>(), (const double*)d_campart.as<double>(),
+                                 (const Tether*)d_teth.as<Tether>(), (int)teth.size(), d_Hpp.as<double>(),
+                                 d_bp.as<double>(), lam, (const int*)d_ptlist.as<int>(), (const double*)d_tout.as<double>(),
+                                 d_S.as<double>(), d_rhs.as<double>()};
+            // (finishing these pairs inside chol_tiles' one workgroup instead measured 65 -> 138 us:
+            // the ~14k entries' dependent partial loads serialise on one CU)
+            if (n_sfinish > 0) launch("ba.schur_finish", schur_finish, dim3(n_sfinish), dim3(64), 0, st, fin, np);
             if (np <= 16 * CT_MAXT)
                 launch("ba.cholesky_solve", chol_tiles, dim3(1), dim3(CT_THREADS), 0, st,
                        (const double*)d_S.as<double>(), np, n, (const double*)d_rhs.as<double>(), xp, d_failp(),
