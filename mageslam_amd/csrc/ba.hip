@@ -1342,13 +1342,6 @@ __global__ __launch_bounds__(CT_THREADS) void chol_tiles(const double* __restric
 
     // ===== the tile waves =====
     dbl4 C[CT_TPW];
-    auto stage_diag = [&](int slot) {  // the owner's tile (k, k) -> dsc, transposed
-#pragma unroll
-        for (int sl = 0; sl < CT_TPW; sl++)
-            if (sl == slot)
-#pragma unroll
-                for (int r = 0; r < 4; r++) dsc[lc][lr + 4 * r] = C[sl][r];
-    };
 #pragma unroll
     for (int sl = 0; sl < CT_TPW; sl++) {
         int ti, tj;

@@ -862,15 +862,19 @@ __global__ __launch_bounds__(FAST_THREADS, MAGE_FAST_WAVES_PER_EU) void fast_nms
 }
 
 // The exact (ungated) pass over the frames select_kernel listed in p.redo; no blur (the gated
-// pass wrote it).  blockIdx.z strides over the list.
+// pass wrote it).  A small 1-D grid strides over (listed frame, tile): the list is almost always
+// empty, and a grid of the frame's 264 tiles x 2 cost 4 us per batch just to dispatch.
+constexpr int REDO_BLOCKS = 64;
 __global__ __launch_bounds__(FAST_THREADS, 4) void fast_redo_kernel(const uint8_t* __restrict__ frames,
                                                                  FastParams p,
                                                                  uint32_t* __restrict__ cand,
                                                                  uint32_t* __restrict__ counts)
 {
-    const uint32_t n = p.redo[0];
-    for (uint32_t z = blockIdx.z; z < n; z += gridDim.z) {
-        fast_tile<false>(frames, p, (int)p.redo[1 + z], 0, false, cand, counts, Tile{(int)blockIdx.x, (int)blockIdx.y});
+    const uint32_t n = p.redo[0], tiles = (uint32_t)p.tiles;
+    for (uint32_t w = blockIdx.x; w < n * tiles; w += gridDim.x) {
+        const uint32_t z = w / tiles, t = w - z * tiles;
+        const int ty = (int)(t / (uint32_t)p.tiles_x), tx = (int)t - ty * p.tiles_x;
+        fast_tile<false>(frames, p, (int)p.redo[1 + z], 0, false, cand, counts, Tile{tx, ty});
         __syncthreads();
     }
 }
@@ -2716,9 +2720,9 @@ mage_status run_batch(OrbDetector* o, const uint8_t* d_frames, uint32_t batch, i
         MAGE_HIP(hipGetLastError());
         // frames whose gate was above their retain bound: the exact path (no-ops when none)
         // (small grids: a frame rarely takes this path, and an empty list should cost little)
-        launch("orb.fast_redo", fast_redo_kernel, dim3(fgrid.x, fgrid.y, std::min(batch, 2u)), dim3(FAST_THREADS), 0,
+        launch("orb.fast_redo", fast_redo_kernel, dim3(REDO_BLOCKS), dim3(FAST_THREADS), 0,
                st, raw.base[l], fp, cand, counts);
-        launch("orb.select_redo", select_redo_kernel, dim3(std::min(batch, 32u)), dim3(SEL_THREADS), 0, st, cand,
+        launch("orb.select_redo", select_redo_kernel, dim3(std::min(batch, 8u)), dim3(SEL_THREADS), 0, st, cand,
                counts, sp, d_kp, o->xy.as<uint32_t>(), d_n, o->status.as<uint32_t>());
         MAGE_HIP(hipGetLastError());
     }
