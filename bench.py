@@ -70,6 +70,9 @@ def parse():
     p.add_argument("--batch-parity", type=int, default=4,
                    help="frames of the last timed ORB batch checked against the oracle (0: off)")
     p.add_argument("--cpu-dry-run", action="store_true", help="gloo rehearsal of the multi-rank flow (tests)")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="multi-rank rehearsal on a one-GPU box: every rank on cuda:0, gloo collectives (the flow "
+                        "of the C5 configuration; times are not a scaling measurement)")
     return p.parse_args()
 
 
@@ -1122,8 +1125,10 @@ def main():
             dist.destroy_process_group()
         return
 
+    if args.rehearse_one_gpu:
+        local_rank = 0  # every rank on the one GPU; RCCL refuses duplicate devices, so gloo
     torch.cuda.set_device(local_rank)
-    dist = multigpu.init("nccl", local_rank)
+    dist = multigpu.init("gloo" if args.rehearse_one_gpu else "nccl", local_rank)
 
     orb_res = run_orb(args, rank, world, local_rank, torch, dist,
                       variant=None if args.orb_variant == "c2" else args.orb_variant)
@@ -1181,6 +1186,9 @@ def main():
             "mean_matches": orb_res["mean_matches"],
             "parity": orb_res.get("parity"),
         }
+        if args.rehearse_one_gpu and world > 1:
+            out["rehearsal"] = (f"{world} ranks sharing cuda:0 with gloo collectives (bench.py --rehearse-one-gpu): "
+                                "the C5 flow, not a scaling measurement")
         failed = [k for k, v in (("ba.many_windows", (ba_res or {}).get("many_windows")),) if v and v.get("status") == "failed"]
         if failed:
             out["failed_legs"] = failed

@@ -19,8 +19,14 @@ def sequence_seed(base: int, rank: int) -> int:
     return (base + rank) & 0xFFFFFFFFFFFFFFFF
 
 
+_cpu_collectives = False  # gloo: collectives on host copies (device tensors move through the CPU)
+
+
 def init(backend: str, local_rank: int):
-    """Initialise torch.distributed when WORLD_SIZE > 1; returns the module or None."""
+    """Initialise torch.distributed when WORLD_SIZE > 1; returns the module or None.  With gloo
+    (CPU tests, and bench.py --rehearse-one-gpu: several ranks sharing one GPU, which RCCL refuses)
+    the helpers below run the collectives on host copies."""
+    global _cpu_collectives
     _, world, _ = rank_env()
     if world <= 1:
         return None
@@ -32,13 +38,14 @@ def init(backend: str, local_rank: int):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         dist.init_process_group(backend)
+        _cpu_collectives = True
     return dist
 
 
 def max_over_ranks(value: float, device, dist) -> float:
     import torch
 
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device="cpu" if _cpu_collectives else device)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -50,9 +57,10 @@ def gather_rows(rows, dist):
 
     if dist is None:
         return [rows]
-    out = [torch.zeros_like(rows) for _ in range(dist.get_world_size())]
-    dist.all_gather(out, rows)
-    return out
+    src = rows.cpu() if _cpu_collectives else rows
+    out = [torch.zeros_like(src) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, src)
+    return [o.to(rows.device) for o in out] if _cpu_collectives else out
 
 
 def barrier(dist) -> None:
