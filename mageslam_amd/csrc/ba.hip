@@ -594,14 +594,25 @@ __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, in
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double v[7] = {0, 0, 0, 0, 0, 0, 0};  // a, b, c, osum[0] (sum, count), osum[1] (sum, count)
     double vm = 0;
-    for (int i = tid; i < na; i += 1024) v[0] += a[i];
-    for (int i = tid; i < nb; i += 1024) v[1] += b[i];
-    for (int i = tid; i < nc; i += 1024) v[2] += c[i];
-    for (int k = 0; k < ns; k++)
-        for (int i = tid; i < oblocks; i += 1024) {
-            v[3 + 2 * k] += opart[(2 * k) * oblocks + i];
-            v[4 + 2 * k] += opart[(2 * k + 1) * oblocks + i];
+    // strided sums with the loads of R consecutive strides issued together (a runtime-trip loop
+    // waited on each load in turn: ~15 dependent L2 round trips, 8.7 us for 15k doubles)
+    constexpr int R = 8;
+    auto strided = [&](const double* __restrict__ x, int n, double& acc) {
+        for (int i0 = tid; i0 < n; i0 += R * 1024) {
+            double t[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) t[r] = i0 + r * 1024 < n ? x[i0 + r * 1024] : 0.0;
+#pragma unroll
+            for (int r = 0; r < R; r++) acc += t[r];
         }
+    };
+    strided(a, na, v[0]);
+    strided(b, nb, v[1]);
+    strided(c, nc, v[2]);
+    for (int k = 0; k < ns; k++) {
+        strided(opart + (2 * k) * oblocks, oblocks, v[3 + 2 * k]);
+        strided(opart + (2 * k + 1) * oblocks, oblocks, v[4 + 2 * k]);
+    }
     for (int i = tid; i < nm; i += 1024) vm = fmax(vm, m[i]);
     const int e = reduce_scatter<7, kWave>(v, lane);
     if (e >= 0) red[wave][e] = v[0];
@@ -870,7 +881,14 @@ struct FinishArgs {
 __device__ __forceinline__ void finish_entry(const FinishArgs& a, const SchurPair& pr, int t, int np)
 {
     double v = 0;
-    for (int q = 0; q < pr.nslots; q++) v += a.part[(long long)(pr.slot0 + q) * 42 + t];
+    for (int q0 = 0; q0 < pr.nslots; q0 += 8) {  // chunk order, the loads of 8 partials in flight together
+        double x[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) x[q] = q0 + q < pr.nslots ? a.part[(long long)(pr.slot0 + q0 + q) * 42 + t] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (q0 + q < pr.nslots) v += x[q];
+    }
     double cam = 0;
     if (pr.h1 == pr.h2) {
         const int h = pr.h1;
