@@ -500,10 +500,13 @@ constexpr int NRES = 2560;  // B descriptors kept resident in LDS up to this cou
 // ------------------------------------------------------------------------------------------
 // fp4 matcher (nb <= 2048, maxDist < 128, minDiff >= 1: every practical call, C2 included).
 //
-// 12 waves (3 per SIMD, 162 VGPRs), two 32-row A tiles each per pass: one column flush (partner
-// half, LDS atomics) serves both tiles.  Measured on C2 (tools/abl.py, 256 pairs): 16 waves x 1
-// tile 0.277 ms, 8 x 2 0.261, 12 x 2 0.228; 16 x 2 spills.  Per 32x32 tile a lane folds 16
-// accumulator values:
+// 8 waves (2 per SIMD, 249 VGPRs), four 32-row A tiles each per pass; one column flush (partner
+// half, LDS atomics) per two tiles (64 rows: the 6-bit row code).  2000 rows are 63 row tiles:
+// 8 waves x 4 run them in 2 passes with one wave slot idle (98 % of the slots busy), 12 x 2 in 3
+// passes with 9 idle (88 %).  Measured on C2 (tools/abl.py, 256 pairs, one box): 12 x 2 0.234-0.240
+// ms, 8 x 4 0.227-0.229 (8 x 4 with 4 / 1 fill columns per thread 0.229 / 0.230, 16 x 2 0.288
+// (4 waves per SIMD: spills), 4 x 8 0.341); round 5: 16 x 1 0.277, 8 x 2 0.261.  Per 32x32 tile a
+// lane folds 16 accumulator values:
 //   * the accumulator starts at C = 1/8 + (0x2400 + code) ulp (per-lane constant registers, code =
 //     63 - the lane's row in the tile), so the result's low 16 bits are the packed key
 //     64 (272 - d) + code, a positive i16 (and positive normal f16), exact: see tile_mfma_fp4;
@@ -516,12 +519,12 @@ constexpr int NRES = 2560;  // B descriptors kept resident in LDS up to this cou
 //     radiusMatch calls + cross-check (FeatureMatcher.cpp:117-167) whenever ties are rejected.
 // ------------------------------------------------------------------------------------------
 #ifndef MAGE_FP4_WAVES
-#define MAGE_FP4_WAVES 12
+#define MAGE_FP4_WAVES 8
 #endif
 constexpr int FW = MAGE_FP4_WAVES;   // waves
-constexpr int FT = FW * kWave;       // 1024 threads
+constexpr int FT = FW * kWave;       // 512 threads
 #ifndef MAGE_FP4_RT
-#define MAGE_FP4_RT 2
+#define MAGE_FP4_RT 4
 #endif
 constexpr int FRT = MAGE_FP4_RT;     // 32-row A tiles per wave per pass (the column flush serves all)
 constexpr int FROWS = FW * 32 * FRT; // A rows per pass
@@ -704,75 +707,79 @@ __global__ __launch_bounds__(FT) void match_fp4_kernel(const uint8_t* __restrict
                     v4i bf[4];
 #pragma unroll
                     for (int s = 0; s < 4; s++) bf[s] = stage[buf][ct][s][lane];
-                    uint32_t c1 = NONE16, c2 = NONE16;
-                    bool any = false;
 #pragma unroll
-                    for (int rt = 0; rt < FRT; rt++) {
-                        const v16i acc = __builtin_bit_cast(v16i, tile_mfma_k16(a[rt], bf, cc));
-                        if (MAGE_FP4_GATE && gating) {
-                            // maxDist gate: radiusMatch keeps only d <= maxDist, and a top-2 state over
-                            // a superset of those values decides exactly as one over them alone, so a
-                            // tile whose 1024 keys all lie below the gate key (d > maxDist) is skipped
-                            uint32_t mx = (uint32_t)acc[15];  // v_max3_u32 tree (key order = bit order)
+                    for (int grp = 0; grp < FRT; grp += 2) {  // one column flush per 64 rows (6-bit codes)
+                        uint32_t c1 = NONE16, c2 = NONE16;
+                        bool any = false;
 #pragma unroll
-                            for (int g = 0; g < 15; g += 3)
-                                mx = max(mx, max(max((uint32_t)acc[g], (uint32_t)acc[g + 1]), (uint32_t)acc[g + 2]));
-                            const bool hit = __ballot(mx >= gate_bits) != 0;  // wave-uniform
-                            g_tiles++;
-                            g_hits += hit ? 1 : 0;
-                            if (!hit) continue;
+                        for (int rt = grp; rt < min(grp + 2, FRT); rt++) {
+                            const v16i acc = __builtin_bit_cast(v16i, tile_mfma_k16(a[rt], bf, cc));
+                            if (MAGE_FP4_GATE && gating) {
+                                // maxDist gate: radiusMatch keeps only d <= maxDist, and a top-2 state over
+                                // a superset of those values decides exactly as one over them alone, so a
+                                // tile whose 1024 keys all lie below the gate key (d > maxDist) is skipped
+                                uint32_t mx = (uint32_t)acc[15];  // v_max3_u32 tree (key order = bit order)
+#pragma unroll
+                                for (int g = 0; g < 15; g += 3)
+                                    mx = max(mx, max(max((uint32_t)acc[g], (uint32_t)acc[g + 1]), (uint32_t)acc[g + 2]));
+                                const bool hit = __ballot(mx >= gate_bits) != 0;  // wave-uniform
+                                g_tiles++;
+                                g_hits += hit ? 1 : 0;
+                                if (!hit) continue;
+                            }
+                            any = true;
+                            uint32_t P[8];
+#pragma unroll
+                            for (int q = 0; q < 8; q++)
+                                P[q] = __builtin_amdgcn_perm((uint32_t)acc[2 * q + 1], (uint32_t)acc[2 * q], 0x05040100u);
+                            // row states: the two best distances over the tiles (same code per register)
+#pragma unroll
+                            for (int q = 0; q < 8; q++) {
+                                r2[rt][q] = pkmax(r2[rt][q], pkmin(r1[rt][q], P[q]));
+                                r1[rt][q] = pkmax(r1[rt][q], P[q]);
+                            }
+                            // column: the two best (distance, row) keys of the lane's 16 rows of this tile
+                            // a knock-out tournament: every key but the winner loses exactly one
+                            // comparison, so the second best is the best of the 7 losers (3 max3s)
+                            uint32_t h[4], l[4];
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                h[q] = pkmax(P[2 * q], P[2 * q + 1]);
+                                l[q] = pkmin(P[2 * q], P[2 * q + 1]);
+                            }
+                            const uint32_t hh0 = pkmax(h[0], h[1]), hl0 = pkmin(h[0], h[1]);
+                            const uint32_t hh1 = pkmax(h[2], h[3]), hl1 = pkmin(h[2], h[3]);
+                            uint32_t t1 = pkmax(hh0, hh1);
+                            uint32_t t2 = pkmax3(pkmax3(l[0], l[1], l[2]), pkmax3(l[3], hl0, hl1), pkmin(hh0, hh1));
+                            if (rt & 1) {  // rows 32..63 of the group: codes 32..63 -> 0..31 (bit 5 cleared)
+                                t1 ^= 0x00200020u;
+                                t2 ^= 0x00200020u;
+                            }
+                            const uint32_t lo = pkmin(c1, t1);
+                            c1 = pkmax(c1, t1);
+                            c2 = pkmax3(lo, c2, t2);
                         }
-                        any = true;
-                        uint32_t P[8];
-#pragma unroll
-                        for (int q = 0; q < 8; q++)
-                            P[q] = __builtin_amdgcn_perm((uint32_t)acc[2 * q + 1], (uint32_t)acc[2 * q], 0x05040100u);
-                        // row states: the two best distances over the tiles (same code per register)
-#pragma unroll
-                        for (int q = 0; q < 8; q++) {
-                            r2[rt][q] = pkmax(r2[rt][q], pkmin(r1[rt][q], P[q]));
-                            r1[rt][q] = pkmax(r1[rt][q], P[q]);
+                        if (gating && g_tiles >= 64 && 4 * g_hits > g_tiles) gating = false;  // dense: fold all
+                        if (!any) continue;  // no key of the column tile within maxDist: no flush
+                        const int kg = kadd - 64 * (grp / 2);
+                        // the partner half-wave holds the same column (rows + 4)
+                        {
+                            const uint32_t o1 = (uint32_t)xor32((int)c1, lane), o2 = (uint32_t)xor32((int)c2, lane);
+                            const uint32_t lo = pkmin(c1, o1);
+                            c1 = pkmax(c1, o1);
+                            c2 = pkmax3(lo, c2, o2);
                         }
-                        // column: the two best (distance, row) keys of the lane's 16 rows of this tile
-                        // a knock-out tournament: every key but the winner loses exactly one
-                        // comparison, so the second best is the best of the 7 losers (3 max3s)
-                        uint32_t h[4], l[4];
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            h[q] = pkmax(P[2 * q], P[2 * q + 1]);
-                            l[q] = pkmin(P[2 * q], P[2 * q + 1]);
-                        }
-                        const uint32_t hh0 = pkmax(h[0], h[1]), hl0 = pkmin(h[0], h[1]);
-                        const uint32_t hh1 = pkmax(h[2], h[3]), hl1 = pkmin(h[2], h[3]);
-                        uint32_t t1 = pkmax(hh0, hh1);
-                        uint32_t t2 = pkmax3(pkmax3(l[0], l[1], l[2]), pkmax3(l[3], hl0, hl1), pkmin(hh0, hh1));
-                        if (rt > 0) {  // rows 32..63 of the wave: codes 32..63 -> 0..31 (bit 5 cleared)
-                            t1 ^= 0x00200020u;
-                            t2 ^= 0x00200020u;
-                        }
-                        const uint32_t lo = pkmin(c1, t1);
-                        c1 = pkmax(c1, t1);
-                        c2 = pkmax3(lo, c2, t2);
+                        const int a1 = lo16s(c1), b1 = hi16s(c1);
+                        const int m1 = max(a1, b1), m2 = max(min(a1, b1), max(lo16s(c2), hi16s(c2)));
+                        const int g1 = ((m1 >> 6) << 16) | ((m1 & 63) + kg);
+                        const int g2 = ((m2 >> 6) << 16) | ((m2 & 63) + kg);
+                        if (pc.live) atomicMax(&colM2[pc.j], pc.old > pc.c1 ? pc.c1 : max(pc.old, pc.c2));
+                        pc.j = colbase + (lane & 31);
+                        pc.c1 = g1;
+                        pc.c2 = g2;
+                        pc.live = lane < 32 && pc.j < nb;
+                        pc.old = pc.live ? atomicMax(&colM1[pc.j], g1) : NONE;
                     }
-                    if (gating && g_tiles >= 64 && 4 * g_hits > g_tiles) gating = false;  // dense: fold all
-                    if (!any) continue;  // no key of the column tile within maxDist: no flush
-                    // the partner half-wave holds the same column (rows + 4)
-                    {
-                        const uint32_t o1 = (uint32_t)xor32((int)c1, lane), o2 = (uint32_t)xor32((int)c2, lane);
-                        const uint32_t lo = pkmin(c1, o1);
-                        c1 = pkmax(c1, o1);
-                        c2 = pkmax3(lo, c2, o2);
-                    }
-                    const int a1 = lo16s(c1), b1 = hi16s(c1);
-                    const int m1 = max(a1, b1), m2 = max(min(a1, b1), max(lo16s(c2), hi16s(c2)));
-                    const int g1 = ((m1 >> 6) << 16) | ((m1 & 63) + kadd);
-                    const int g2 = ((m2 >> 6) << 16) | ((m2 & 63) + kadd);
-                    if (pc.live) atomicMax(&colM2[pc.j], pc.old > pc.c1 ? pc.c1 : max(pc.old, pc.c2));
-                    pc.j = colbase + (lane & 31);
-                    pc.c1 = g1;
-                    pc.c2 = g2;
-                    pc.live = lane < 32 && pc.j < nb;
-                    pc.old = pc.live ? atomicMax(&colM1[pc.j], g1) : NONE;
                 }
             }
             if (st + FPF < nstages) fill((st + FPF) % FBUF, st + FPF, nxt);

@@ -29,6 +29,11 @@ def variant_source(stem):
     patch = ROOT / "tools" / "patches" / (Path(stem).stem + "_variants.patch")
     if not patch.exists():
         return B.CSRC / stem, False
+    with open(patch, "rb") as f:
+        dry = subprocess.run(["patch", "-s", "--dry-run", str(B.CSRC / stem)], stdin=f, capture_output=True)
+    if dry.returncode != 0:  # the product source moved on: its own switches only
+        print(f"note: {patch.name} does not apply to the current {stem}; building the product source", flush=True)
+        return B.CSRC / stem, False
     out = B.CSRC / f".abl_variants_{stem}"
     out.write_bytes((B.CSRC / stem).read_bytes())
     with open(patch, "rb") as f:
