@@ -2,6 +2,7 @@
 
   python tools/ablate_ba.py build [V1 V2 ...]   # variants of ba.hip into abl/ba_<i>/ (CPU)
   python tools/ablate_ba.py run   [V1 V2 ...]   # per-kernel times of the C3 graph per variant (GPU)
+  python tools/ablate_ba.py libs  name[,name]   # the same for abl/<name>/libmage_hot.so (tools/abl.py build)
 
 A variant is a '+'-joined list of NAME=VALUE preprocessor definitions ("0" = the product build),
 e.g. MAGE_CHOL_ABLATE=3.  Switches in ba.hip:
@@ -43,14 +44,17 @@ def build():
     src.unlink()
 
 
-def run():
+def run(libs=None):
     import torch  # noqa: F401  (HIP runtime init through torch, as the bench does)
     sys.path.insert(0, str(ROOT))
     from mageslam_amd import _lib, bundler, synth
     g = synth.ba_graph()
-    for i, v in enumerate(VARIANTS):
-        d = ROOT / "abl" / f"ba_{i}"
-        assert (d / "variant.txt").read_text() == v, f"abl/ba_{i} was built for another variant"
+    for i, v in enumerate(libs or VARIANTS):
+        if libs:
+            d = ROOT / "abl" / v
+        else:
+            d = ROOT / "abl" / f"ba_{i}"
+            assert (d / "variant.txt").read_text() == v, f"abl/ba_{i} was built for another variant"
         lib = C.CDLL(str(d / "libmage_hot.so"))
         _lib._declare(lib)
         _lib._lib = lib  # this process only: route the mirror classes to the variant
@@ -71,4 +75,7 @@ def run():
 
 
 if __name__ == "__main__":
-    {"build": build, "run": run}[sys.argv[1]]()
+    if sys.argv[1] == "libs":
+        run(sys.argv[2].split(","))
+    else:
+        {"build": build, "run": run}[sys.argv[1]]()
