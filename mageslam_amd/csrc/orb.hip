@@ -1311,6 +1311,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
                 if (i < K) atomicAdd(&mhist[min((int)(mykeys[q] >> 40), SEL_HB - 1)], 1u);
             }
             __syncthreads();
+            SEL_STAMP(11);
             if (tid < kWave) {  // lane l: bins 16 l .. 16 l + 15; suffix sums, largest bin reaching N
                 constexpr int BPL = SEL_HB / kWave;
                 int sfx[BPL];
@@ -1348,6 +1349,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
                 }
             }
             __syncthreads();
+            SEL_STAMP(12);
             const int tb = s_thr, csel = s_sel;
             int Pp = SORT_THREADS;
             while (Pp < csel) Pp <<= 1;
@@ -1368,6 +1370,7 @@ __device__ __forceinline__ void select_frame(int f, int G, const uint32_t* __res
             }
         }
         __syncthreads();
+        SEL_STAMP(13);
         sort_desc(keys, Psort);
         SEL_STAMP(9);
     }

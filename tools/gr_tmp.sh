@@ -1,6 +1,5 @@
 set -eo pipefail
 export TMPDIR=/tmp
-# scratch GPU step (development): BA determinism + parity, then the BA leg
-timeout -k 10 120 python3 -u tools/ba_det_probe.py > gpurun_out/det.log 2>&1
-timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_ba.py tests/test_gpu_tracking.py tests/test_local_ba.py > gpurun_out/pytest.log 2>&1
-timeout -k 10 400 python3 -u bench.py --steps 5 --warmup 2 --no-pose --no-tracking --no-cpu-baseline --no-rbrief31 --pipelined-streams 0 > gpurun_out/b_ba.json 2> gpurun_out/b_ba.err
+# scratch GPU step (development): parity of the sort users, then variant timings
+timeout -k 10 500 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_orb.py tests/test_gpu_match.py tests/test_gpu_bow.py tests/test_gpu_tracking.py > gpurun_out/pytest.log 2>&1
+timeout -k 10 300 python3 tools/abl.py run head,sortu,head,sortu > gpurun_out/abl_run.log 2>&1

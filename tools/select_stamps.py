@@ -45,7 +45,7 @@ def run():
     orb.synth_frames_device(frames, B, W, H, 0, synth.FRAME_SEED)
     det = orb.OrbDetector(nfeatures=N)
     st = np.zeros((1024, 16), np.uint64)
-    acc = []
+    acc, sub = [], []
     for it in range(6):
         det.detect_and_compute_batch_device(frames, W, H, kp, desc, cnt, N)
         torch.cuda.synchronize()
@@ -53,12 +53,16 @@ def run():
         if it >= 2:
             s = st[:B, :11].astype(np.int64)
             acc.append(np.diff(s, axis=1))
+            x = st[:B].astype(np.int64)
+            sub.append(np.stack([x[:, 11] - x[:, 8], x[:, 12] - x[:, 11], x[:, 13] - x[:, 12], x[:, 9] - x[:, 13]], 1))
             print("start spread (cycles):", int(s[:, 0].max() - s[:, 0].min()), " end-start mean:",
                   int((s[:, 10] - s[:, 0]).mean()), flush=True)
     d = np.concatenate(acc).mean(0)
     tot = d.sum()
     for n, v in zip(NAMES, d):
         print(f"{n:>10}: {v:9.0f} cycles  {100 * v / tot:5.1f} %")
+    for n, v in zip(["mhist", "mscan", "compact", "bitonic"], np.concatenate(sub).mean(0)):
+        print(f"{n:>10}: {v:9.0f} cycles  (inside sort)")
     print(f"{'total':>10}: {tot:9.0f} cycles ({tot / 100e6 * 1e3:.3f} ms at the 100 MHz s_memtime? see note)")
 
 
