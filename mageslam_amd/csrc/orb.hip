@@ -516,21 +516,6 @@ __device__ __forceinline__ long long brick_offset(int y, int x, int bcols)
     return ((long long)(y >> 2) * bcols + (x >> 5)) * 128 + (y & 3) * 32 + (x & 31);
 }
 
-// The tile is biased in place before the blur (xor_tile: every byte b becomes b ^ 0x80, the
-// signed i8 b - 128), after the FAST passes have read it.
-__device__ __forceinline__ void xor_tile(uint8_t (*img)[LW])
-{
-    uint2* q = reinterpret_cast<uint2*>(&img[0][0]);
-    constexpr int NQ = LH * LW / 8;
-    static_assert(LH * LW % 8 == 0, "qword tile");
-    for (int i = threadIdx.x; i < NQ; i += FAST_THREADS) {
-        uint2 v = q[i];
-        v.x ^= 0x80808080u;
-        v.y ^= 0x80808080u;
-        q[i] = v;
-    }
-}
-
 __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastParams& p, int f, Tile T)
 {
     typedef int v4i __attribute__((ext_vector_type(4)));
@@ -541,7 +526,7 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
     const uint4 o0 = p.blur_ops[3 * lane], o1 = p.blur_ops[3 * lane + 1], o2 = p.blur_ops[3 * lane + 2];
     const v4i tb = {(int)o0.x, (int)o0.y, (int)o0.z, (int)o0.w};
     const v4i ta[2] = {{(int)o1.x, (int)o1.y, (int)o1.z, (int)o1.w}, {(int)o2.x, (int)o2.y, (int)o2.z, (int)o2.w}};
-    // row pass: H' = sum tap (b - 128) + 128 = H - 32768 in [-32768, 32767] (the tile holds
+    // row pass: H' = sum tap (b - 128) + 128 = H - 32768 in [-32768, 32767] (the operands hold
     // b ^ 0x80), so the high byte of H' is its signed i8 digit and only the low byte needs the
     // 0x80 bias.  Column pass with C = 0: the constants ride in each lane's spare K slots 12..15
     // (A dword 3 x B dword 3 = {-128, a1} . {-64, 1}, four K groups): hi 4 (8192 + 64) = 33024,
@@ -569,7 +554,10 @@ __device__ __forceinline__ void blur_mfma(const uint8_t (*img)[LW], const FastPa
             const int c0 = min(16 * s + 16 * g, LW - 8), c1 = min(16 * s + 16 * g + 8, LW - 8);
             const uint2 d0 = *reinterpret_cast<const uint2*>(&img[row][c0]);
             const uint2 d1 = *reinterpret_cast<const uint2*>(&img[row][c1]);
-            const v4i a = {(int)d0.x, (int)d0.y, (int)d1.x, (int)d1.y};
+            // bytes b enter as the signed i8 b - 128 = b ^ 0x80 (full-rate v_xor_b32 here instead of
+            // a biasing pass over the LDS tile and a barrier)
+            const v4i a = {(int)(d0.x ^ 0x80808080u), (int)(d0.y ^ 0x80808080u), (int)(d1.x ^ 0x80808080u),
+                           (int)(d1.y ^ 0x80808080u)};
             H[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, tb, c_row, 0, 0, 0);
         }
         // bytes of H': per block one dword of lo bytes (^ 0x80) and one of signed hi bytes
@@ -714,11 +702,12 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
     } else {
         score_strip(img, sc, p, T);
     }
-    __syncthreads();
-    // the FAST passes are done with the image: bias it for the blur's i8 MFMA operands
+    // the blur only reads the image tile (biased for the i8 MFMA operands in registers) and writes
+    // the frame directly: a wave runs it as soon as its own scoring is done, ahead of the barrier
     FAST_STAMP(6);
-    if (blur) xor_tile(img);
+    if (blur) blur_mfma(img, p, f, T);
     FAST_STAMP(7);
+    __syncthreads();
     // strict 3x3 non-maximum suppression (OpenCVModified.cpp:1499-1509) + border filter, four
     // pixels per dword: output group og (score dword og + 1), tile rows [8 * chunk, +8).  Scores
     // are split into even / odd pixels as f16 lanes (1024 + s); per score row the left / right
@@ -829,13 +818,6 @@ __device__ __forceinline__ void fast_tile(const uint8_t* __restrict__ frames, co
         }
     }
     FAST_STAMP(8);
-    // the blur reads only the (biased) image tile and writes the frame directly
-    if (blur) {
-        __syncthreads();  // xor_tile is complete
-        FAST_STAMP(9);
-        blur_mfma(img, p, f, T);
-        FAST_STAMP(10);
-    }
     __syncthreads();  // s_cnt and the tile's list are final
     FAST_STAMP(11);
     // the tile's own slot of the frame's candidate buffer (TCAP entries) and count: no global
