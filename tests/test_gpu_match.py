@@ -26,7 +26,8 @@ def test_hamming_distance_known_answers(gpu, oracle):
         assert matcher.GetDescriptorDistance(x, y) == oracle.hamming(x, y)
 
 
-@pytest.mark.parametrize("na,nb", [(1, 1), (5, 300), (300, 5), (640, 700), (2000, 2000), (4096, 100), (513, 64)])
+@pytest.mark.parametrize("na,nb", [(1, 1), (5, 300), (300, 5), (640, 700), (2000, 2000), (4096, 100), (513, 64),
+                                   (1024, 97), (1025, 2048), (96, 2000)])  # fp4 passes of 1024 rows: exact, ragged, 3 row tiles
 def test_match_random(gpu, oracle, na, nb):
     rng = np.random.default_rng(na * 7 + nb)
     base = rng.integers(0, 256, (max(na, nb), 32), dtype=np.uint8)

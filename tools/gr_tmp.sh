@@ -1,4 +1,4 @@
 set -eo pipefail
 export TMPDIR=/tmp
-# scratch GPU step (development): variant timings, alternating
-timeout -k 10 300 python3 tools/abl.py run head,xorreg,head,xorreg,head,xorreg,head,xorreg,head,xorreg > gpurun_out/abl_run.log 2>&1
+# scratch GPU step (development): the whole GPU suite + smoke
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests > gpurun_out/pytest_all.log 2>&1
