@@ -216,13 +216,20 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
     double& chi = acc[9];
     const long long es = pb.ecsr;
     const int e0 = pb.pstart[p], e1 = pb.pstart[p + 1];
+    // the lane's edge for the G pass below, kept in registers when the point has at most PG edges
+    // (one per lane): camera-CSR position (-1: none or a fixed camera) and W as stored in Q
+    int c_ap = -1;
+    double c_W[6] = {0, 0, 0, 0, 0, 0};
     for (int a = e0 + sub; a < e1; a += PG) {
         const int e = pb.pedges[a];
         if (!pb.active[e]) {
             // the Schur products read Q of every listed edge: a removed edge contributes zero
-            if (free_p && pb.camh[pb.ecam[e]] >= 0) {
-                double* q = o.Q + pb.epos[e];
-                for (int k = 0; k < EQ_N; k++) q[k * es] = 0;
+            if (LIN && pb.camh[pb.ecam[e]] >= 0) {
+                c_ap = pb.epos[e];
+                if (free_p) {
+                    double* q = o.Q + c_ap;
+                    for (int k = 0; k < EQ_N; k++) q[k * es] = 0;
+                }
             }
             continue;
         }
@@ -248,8 +255,10 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
             }
             continue;
         }
-        if (!free_p) continue;
         const int c = pb.ecam[e];
+        const bool cam_free = pb.camh[c] >= 0;
+        if (cam_free) c_ap = pb.epos[e];
+        if (!free_p) continue;
         const double f = pb.camk[3 * c];
         const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
         double R[9];
@@ -273,14 +282,17 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
         H[3] += (J[1] * J[1] + J[4] * J[4]) * w;
         H[4] += (J[1] * J[2] + J[4] * J[5]) * w;
         H[5] += (J[2] * J[2] + J[5] * J[5]) * w;
-        if (pb.camh[c] >= 0) {
+        if (cam_free) {
             // Hpl_e = Jp^T (w J): kept factored as (x/z, y/z, f/z) + W = w J (camera-major
             // component arrays; schur_chunks reads them coalesced)
-            double* qo = o.Q + pb.epos[e];
+            double* qo = o.Q + c_ap;
             qo[0] = xi;
             qo[es] = yi;
             qo[2 * es] = f * iz;
-            for (int k = 0; k < 6; k++) qo[(3 + k) * es] = J[k] * w;
+            for (int k = 0; k < 6; k++) {
+                c_W[k] = J[k] * w;
+                qo[(3 + k) * es] = c_W[k];
+            }
         }
     }
     // group sums by reduce-scatter: lane `sub` ends up with entry k of acc (H 00 01 02 11 12 22,
@@ -300,22 +312,31 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
             D[4] += lambda;
             D[8] += lambda;
             d_inv3(D, Di);
-            for (int a = e0 + sub; a < e1; a += PG) {
-                const int e = pb.pedges[a];
-                if (pb.camh[pb.ecam[e]] < 0) continue;
-                const int ap = pb.epos[e];
+            auto store_g = [&](int ap, const double (&W)[6]) {
                 if (!free_p) {
                     for (int j = 0; j < EG_N; j++) o.G[j * es + ap] = 0;
-                    continue;
+                    return;
                 }
-                double W[6];
-#pragma unroll
-                for (int j = 0; j < 6; j++) W[j] = o.Q[(3 + j) * es + ap];
 #pragma unroll
                 for (int i = 0; i < 2; i++)
 #pragma unroll
                     for (int kk = 0; kk < 3; kk++)
                         o.G[(i * 3 + kk) * es + ap] = W[i * 3] * Di[kk] + W[i * 3 + 1] * Di[3 + kk] + W[i * 3 + 2] * Di[6 + kk];
+            };
+            if (e1 - e0 <= PG) {
+                // the lane's one edge from registers (no dependent reload of pedges / ecam /
+                // camh / epos / Q after the group reduction)
+                if (c_ap >= 0) store_g(c_ap, c_W);
+            } else {
+                for (int a = e0 + sub; a < e1; a += PG) {
+                    const int e = pb.pedges[a];
+                    if (pb.camh[pb.ecam[e]] < 0) continue;
+                    const int ap = pb.epos[e];
+                    double W[6];
+#pragma unroll
+                    for (int j = 0; j < 6; j++) W[j] = o.Q[(3 + j) * es + ap];
+                    store_g(ap, W);
+                }
             }
         }
     }
@@ -1552,17 +1573,34 @@ __global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const 
         double sc = 0;
         const long long es = pb.ecsr;
         const int e0 = pb.pstart[p], e1 = pb.pstart[p + 1];
+        // With at most PG edges (one per lane) the lane keeps its edge (index, camera, block,
+        // camera update) from the first pass for the evaluation pass: no dependent reload of
+        // pedges / active / ecam / camh / xp after the group reduction.
+        const bool one = e1 - e0 <= PG;
+        int c_e = -1, c_c = 0, c_h = -1;
+        double c_u[6] = {0, 0, 0, 0, 0, 0};
+        if (one && e0 + sub < e1) {
+            c_e = pb.pedges[e0 + sub];
+            if (!pb.active[c_e]) c_e = -1;
+            else {
+                c_c = pb.ecam[c_e];
+                c_h = pb.camh[c_c];
+                if (c_h >= 0)
+#pragma unroll
+                    for (int k = 0; k < 6; k++) c_u[k] = xp[6 * c_h + k];
+            }
+        }
         if (pb.ptfree[p]) {
+            // Hll_p and bl_p are loaded ahead of the edge pass (independent of it)
+            double D[9], Di[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
+            const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
             double cl[3] = {0, 0, 0};
-            for (int a = e0 + sub; a < e1; a += PG) {
-                const int e = pb.pedges[a];
-                if (!pb.active[e]) continue;
-                const int h = pb.camh[pb.ecam[e]];
-                if (h < 0) continue;
+            auto add_edge = [&](int e, int c, int h, const double (&Xp)[6]) {
                 const int a2 = pb.epos[e];
                 double J[12];
-                jac_pose_q(Q[a2], Q[es + a2], Q[2 * es + a2], pb.camk[3 * pb.ecam[e]], J);
-                const double* Xp = xp + 6 * h;
+                jac_pose_q(Q[a2], Q[es + a2], Q[2 * es + a2], pb.camk[3 * c], J);
                 double u0 = 0, u1 = 0;
 #pragma unroll
                 for (int r = 0; r < 6; r++) {
@@ -1571,17 +1609,27 @@ __global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const 
                 }
 #pragma unroll
                 for (int k = 0; k < 3; k++) cl[k] += G[k * es + a2] * u0 + G[(3 + k) * es + a2] * u1;
+            };
+            if (one) {
+                if (c_e >= 0 && c_h >= 0) add_edge(c_e, c_c, c_h, c_u);
+            } else {
+                for (int a = e0 + sub; a < e1; a += PG) {
+                    const int e = pb.pedges[a];
+                    if (!pb.active[e]) continue;
+                    const int c = pb.ecam[e], h = pb.camh[c];
+                    if (h < 0) continue;
+                    double Xp[6];
+#pragma unroll
+                    for (int r = 0; r < 6; r++) Xp[r] = xp[6 * h + r];
+                    add_edge(e, c, h, Xp);
+                }
             }
             group_sum(cl);  // every lane of the group holds the sums
             // db_p = Dinv_p bl_p, Dinv_p = (Hll_p + lambda I)^-1 as in edge_schur
-            double D[9], Di[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
             D[0] += lambda;
             D[4] += lambda;
             D[8] += lambda;
             d_inv3(D, Di);
-            const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
             for (int r = 0; r < 3; r++) {
                 const double dbr = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
                 const double v = dbr - cl[r];
@@ -1595,17 +1643,27 @@ __global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const 
         }
         double chi = 0;
         for (int a = e0 + sub; a < e1; a += PG) {
-            const int e = pb.pedges[a];
-            if (!pb.active[e]) continue;
-            const int c = pb.ecam[e];
+            int e, c, h;
+            double u[6];
+            if (one) {
+                e = c_e;
+                if (e < 0) continue;
+                c = c_c;
+                h = c_h;
+#pragma unroll
+                for (int k = 0; k < 6; k++) u[k] = c_u[k];
+            } else {
+                e = pb.pedges[a];
+                if (!pb.active[e]) continue;
+                c = pb.ecam[e];
+                h = pb.camh[c];
+                if (h >= 0)
+#pragma unroll
+                    for (int k = 0; k < 6; k++) u[k] = xp[6 * h + k];
+            }
             double q[4] = {A.q[4 * c], A.q[4 * c + 1], A.q[4 * c + 2], A.q[4 * c + 3]};
             double t[3] = {A.t[3 * c], A.t[3 * c + 1], A.t[3 * c + 2]};
-            const int h = pb.camh[c];
-            if (h >= 0) {
-                double u[6];
-                for (int k = 0; k < 6; k++) u[k] = xp[6 * h + k];
-                d_oplus(q, t, u);
-            }
+            if (h >= 0) d_oplus(q, t, u);
             double ev[2], xc[3], rho0, rho1;
             edge_eval_at(pb, e, q, t, X, ev, xc, rho0, rho1);
             o.err[2 * e] = ev[0];
