@@ -220,6 +220,7 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
     // (one per lane): camera-CSR position (-1: none or a fixed camera) and W as stored in Q
     int c_ap = -1;
     double c_W[6] = {0, 0, 0, 0, 0, 0};
+    const double Xp3[3] = {s.p[3 * p], s.p[3 * p + 1], s.p[3 * p + 2]};  // the group's point (no ept reload)
     for (int a = e0 + sub; a < e1; a += PG) {
         const int e = pb.pedges[a];
         if (!pb.active[e]) {
@@ -234,14 +235,18 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
             continue;
         }
         double ev[2], xc[3], rho0, rho1;
-        edge_eval(pb, s, e, ev, xc, rho0, rho1);
+        const int c = pb.ecam[e];
+        {
+            const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
+            const double t[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
+            edge_eval_at(pb, e, c, q, t, Xp3, ev, xc, rho0, rho1);
+        }
         o.err[2 * e] = ev[0];
         o.err[2 * e + 1] = ev[1];
         chi += rho0;
         if (!LIN) {
             if (sp) {
                 const double sumSquares = ev[0] * ev[0] + ev[1] * ev[1];
-                const int c = pb.ecam[e];
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
                     const double dot = cheirality(k == 0 ? s : sp->cur, c, p);
@@ -255,7 +260,6 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
             }
             continue;
         }
-        const int c = pb.ecam[e];
         const bool cam_free = pb.camh[c] >= 0;
         if (cam_free) c_ap = pb.epos[e];
         if (!free_p) continue;
@@ -477,11 +481,15 @@ __device__ __forceinline__ void cam_chunk(const Problem& pb, const State& s, con
     double acc[27];
     for (int k = 0; k < 27; k++) acc[k] = 0;
     const double f = pb.camk[3 * c];
+    // the block's camera pose once; an entry's point from cpt (no ecam / ept reload per edge)
+    const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
+    const double t[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
     for (int a = pb.cstart[c] + chunk * BA_THREADS + threadIdx.x; a < pb.cstart[c + 1]; a += CAM_CHUNKS * BA_THREADS) {
-        const int e = pb.cedges[a];
+        const int e = pb.cedges[a], pt = pb.cpt[a];
         if (!pb.active[e]) continue;
         double ev[2], xc[3], rho0, rho1;
-        edge_eval(pb, s, e, ev, xc, rho0, rho1);  // the same error point_group computes for e
+        const double X[3] = {s.p[3 * pt], s.p[3 * pt + 1], s.p[3 * pt + 2]};
+        edge_eval_at(pb, e, c, q, t, X, ev, xc, rho0, rho1);  // the same error point_group computes for e
         double Jp[12];
         jac_pose(xc, f, Jp);
         const double inf = pb.info[e];
@@ -1665,7 +1673,7 @@ __global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const 
             double t[3] = {A.t[3 * c], A.t[3 * c + 1], A.t[3 * c + 2]};
             if (h >= 0) d_oplus(q, t, u);
             double ev[2], xc[3], rho0, rho1;
-            edge_eval_at(pb, e, q, t, X, ev, xc, rho0, rho1);
+            edge_eval_at(pb, e, c, q, t, X, ev, xc, rho0, rho1);
             o.err[2 * e] = ev[0];
             o.err[2 * e + 1] = ev[1];
             chi += rho0;

@@ -306,12 +306,12 @@ struct Problem {
     double huber;
 };
 
-// computeError + chi2 + robustify for edge e with its camera pose (q, t) and point X given
-__device__ __forceinline__ void edge_eval_at(const Problem& pb, int e, const double q[4], const double t[3],
+// computeError + chi2 + robustify for edge e of camera c with its camera pose (q, t) and point X
+// given (the callers know c and X, so the edge's own loads are uv and info only)
+__device__ __forceinline__ void edge_eval_at(const Problem& pb, int e, int c, const double q[4], const double t[3],
                                              const double X[3], double err[2], double xc[3], double& rho0,
                                              double& rho1)
 {
-    const int c = pb.ecam[e];
     d_qrot(q, X, xc);
     xc[0] += t[0];
     xc[1] += t[1];
@@ -332,7 +332,7 @@ __device__ __forceinline__ void edge_eval(const Problem& pb, const State& s, int
     const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
     const double X[3] = {s.p[3 * p], s.p[3 * p + 1], s.p[3 * p + 2]};
     const double t[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
-    edge_eval_at(pb, e, q, t, X, err, xc, rho0, rho1);
+    edge_eval_at(pb, e, c, q, t, X, err, xc, rho0, rho1);
 }
 
 // EdgeProjectXYZ2UV::linearizeOplus pose block (2x6, row-major).  One reciprocal of z instead of

@@ -56,13 +56,22 @@ def build(src, specs):
         obj = out / (stem + ".o")
         flags = [f"-D{d}" for d in defs.split("+") if d]
         src_path, tmp = variant_source(stem)
+        inc = []
         if rev:
-            src_path = B.CSRC / f".abl_{name}_{stem}"
-            src_path.write_bytes(subprocess.run(["git", "show", f"{rev}:mageslam_amd/csrc/{stem}"], cwd=ROOT,
-                                                check=True, capture_output=True).stdout)
-        subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *B.COMMON, *flags,
+            # the sources and headers as committed at REV (a same-box baseline), in a scratch tree
+            import shutil
+            import tempfile
+            tree = Path(tempfile.mkdtemp(prefix="abl_rev_"))
+            arch = subprocess.run(["git", "archive", rev, "mageslam_amd/csrc", "include"], cwd=ROOT, check=True,
+                                  capture_output=True).stdout
+            subprocess.run(["tar", "-x", "-C", str(tree)], input=arch, check=True)
+            src_path = tree / "mageslam_amd" / "csrc" / stem
+            inc = [f"-I{tree / 'include'}"]
+        subprocess.run([B.hipcc(), "-x", "hip", f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", *inc, *B.COMMON, *flags,
                         "-c", str(src_path), "-o", str(obj)], check=True)
-        if rev or tmp:
+        if rev:
+            shutil.rmtree(tree)
+        elif tmp:
             src_path.unlink()
         subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out / "libmage_hot.so"),
                         str(obj), *map(str, objs)], check=True)
