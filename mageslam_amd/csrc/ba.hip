@@ -222,11 +222,12 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
     double c_W[6] = {0, 0, 0, 0, 0, 0};
     const double Xp3[3] = {s.p[3 * p], s.p[3 * p + 1], s.p[3 * p + 2]};  // the group's point (no ept reload)
     for (int a = e0 + sub; a < e1; a += PG) {
-        const int e = pb.pedges[a];
+        const int4 ent = pb.pe[a];  // (edge, camera, camera block, camera-CSR position)
+        const int e = ent.x;
         if (!pb.active[e]) {
             // the Schur products read Q of every listed edge: a removed edge contributes zero
-            if (LIN && pb.camh[pb.ecam[e]] >= 0) {
-                c_ap = pb.epos[e];
+            if (LIN && ent.z >= 0) {
+                c_ap = ent.w;
                 if (free_p) {
                     double* q = o.Q + c_ap;
                     for (int k = 0; k < EQ_N; k++) q[k * es] = 0;
@@ -235,7 +236,7 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
             continue;
         }
         double ev[2], xc[3], rho0, rho1;
-        const int c = pb.ecam[e];
+        const int c = ent.y;
         {
             const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
             const double t[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
@@ -260,8 +261,8 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
             }
             continue;
         }
-        const bool cam_free = pb.camh[c] >= 0;
-        if (cam_free) c_ap = pb.epos[e];
+        const bool cam_free = ent.z >= 0;
+        if (cam_free) c_ap = ent.w;
         if (!free_p) continue;
         const double f = pb.camk[3 * c];
         const double q[4] = {s.q[4 * c], s.q[4 * c + 1], s.q[4 * c + 2], s.q[4 * c + 3]};
@@ -333,9 +334,9 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
                 if (c_ap >= 0) store_g(c_ap, c_W);
             } else {
                 for (int a = e0 + sub; a < e1; a += PG) {
-                    const int e = pb.pedges[a];
-                    if (pb.camh[pb.ecam[e]] < 0) continue;
-                    const int ap = pb.epos[e];
+                    const int4 ent = pb.pe[a];
+                    if (ent.z < 0) continue;
+                    const int ap = ent.w;
                     double W[6];
 #pragma unroll
                     for (int j = 0; j < 6; j++) W[j] = o.Q[(3 + j) * es + ap];
@@ -1587,16 +1588,17 @@ __global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const 
         const bool one = e1 - e0 <= PG;
         int c_e = -1, c_c = 0, c_h = -1;
         double c_u[6] = {0, 0, 0, 0, 0, 0};
+        int c_pos = 0;
         if (one && e0 + sub < e1) {
-            c_e = pb.pedges[e0 + sub];
-            if (!pb.active[c_e]) c_e = -1;
-            else {
-                c_c = pb.ecam[c_e];
-                c_h = pb.camh[c_c];
-                if (c_h >= 0)
+            const int4 ent = pb.pe[e0 + sub];
+            c_e = ent.x;
+            c_c = ent.y;
+            c_h = ent.z;
+            c_pos = ent.w;
+            if (c_h >= 0)
 #pragma unroll
-                    for (int k = 0; k < 6; k++) c_u[k] = xp[6 * c_h + k];
-            }
+                for (int k = 0; k < 6; k++) c_u[k] = xp[6 * c_h + k];
+            if (!pb.active[c_e]) c_e = -1;
         }
         if (pb.ptfree[p]) {
             // Hll_p and bl_p are loaded ahead of the edge pass (independent of it)
@@ -1605,8 +1607,7 @@ __global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const 
             for (int k = 0; k < 9; k++) D[k] = Hll[9 * (long long)p + k];
             const double b0 = bl[3 * p], b1 = bl[3 * p + 1], b2 = bl[3 * p + 2];
             double cl[3] = {0, 0, 0};
-            auto add_edge = [&](int e, int c, int h, const double (&Xp)[6]) {
-                const int a2 = pb.epos[e];
+            auto add_edge = [&](int a2, int c, const double (&Xp)[6]) {
                 double J[12];
                 jac_pose_q(Q[a2], Q[es + a2], Q[2 * es + a2], pb.camk[3 * c], J);
                 double u0 = 0, u1 = 0;
@@ -1619,17 +1620,15 @@ __global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const 
                 for (int k = 0; k < 3; k++) cl[k] += G[k * es + a2] * u0 + G[(3 + k) * es + a2] * u1;
             };
             if (one) {
-                if (c_e >= 0 && c_h >= 0) add_edge(c_e, c_c, c_h, c_u);
+                if (c_e >= 0 && c_h >= 0) add_edge(c_pos, c_c, c_u);
             } else {
                 for (int a = e0 + sub; a < e1; a += PG) {
-                    const int e = pb.pedges[a];
-                    if (!pb.active[e]) continue;
-                    const int c = pb.ecam[e], h = pb.camh[c];
-                    if (h < 0) continue;
+                    const int4 ent = pb.pe[a];
+                    if (!pb.active[ent.x] || ent.z < 0) continue;
                     double Xp[6];
 #pragma unroll
-                    for (int r = 0; r < 6; r++) Xp[r] = xp[6 * h + r];
-                    add_edge(e, c, h, Xp);
+                    for (int r = 0; r < 6; r++) Xp[r] = xp[6 * ent.z + r];
+                    add_edge(ent.w, ent.y, Xp);
                 }
             }
             group_sum(cl);  // every lane of the group holds the sums
@@ -1661,10 +1660,11 @@ __global__ __launch_bounds__(BA_THREADS) void update_evaluate(Problem pb, const 
 #pragma unroll
                 for (int k = 0; k < 6; k++) u[k] = c_u[k];
             } else {
-                e = pb.pedges[a];
+                const int4 ent = pb.pe[a];
+                e = ent.x;
                 if (!pb.active[e]) continue;
-                c = pb.ecam[e];
-                h = pb.camh[c];
+                c = ent.y;
+                h = ent.z;
                 if (h >= 0)
 #pragma unroll
                     for (int k = 0; k < 6; k++) u[k] = xp[6 * h + k];
@@ -2104,6 +2104,21 @@ template <typename KeyT>
 __device__ __forceinline__ int cs_digit(KeyT k, int shift, unsigned dmask)
 {
     return (int)(((unsigned long long)k >> shift) & dmask);
+}
+
+// The point CSR's entries with what the point passes read next, (edge, camera, camera block,
+// camera-CSR position), in one 16-byte record per entry: a point pass's loads are then pstart ->
+// record -> the edge's data, instead of pstart -> pedges -> ecam -> camh / epos.  Fixed until the
+// next initialisation (removed edges keep their records; `active` says which are live).
+__global__ __launch_bounds__(256) void init_pcache(int E, int P, const int* __restrict__ pstart,
+                                                   const int* __restrict__ pedges, const int* __restrict__ ecam,
+                                                   const int* __restrict__ camh, const int* __restrict__ epos,
+                                                   int4* __restrict__ pe)
+{
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= E || a >= pstart[P]) return;
+    const int e = pedges[a], c = ecam[e];
+    pe[a] = make_int4(e, c, camh[c], epos[e]);
 }
 
 template <typename KeyT>
@@ -2618,7 +2633,7 @@ struct BundleAdjuster {
     int cur = 0;  // which state buffer holds the current estimate
     // device buffers
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
-        d_pstart, d_pedges, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
+        d_pstart, d_pedges, d_pe, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
         d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
         d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_chist, d_kdst, d_rblk, d_sbits, d_srank, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
         d_sfinish, d_epos, d_chi_lin, d_livebuf, d_removed, d_camflag, d_ikeys, d_ivals, d_isum, d_iacc, d_ctab, d_csort_tmp;
@@ -2654,6 +2669,7 @@ struct BundleAdjuster {
         pb.cedges = d_cedges.as<int>();
         pb.cpt = d_cpt.as<int>();
         pb.epos = d_epos.as<int>();
+        pb.pe = d_pe.as<int4>();
         pb.ecsr = n_entries;
         pb.huber = huber;
         return pb;
@@ -2666,7 +2682,7 @@ struct BundleAdjuster {
         // idle and go to the block cache, after a failed synchronisation everything is freed
         const bool idle = !st || hipStreamSynchronize(st) == hipSuccess;
         for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
-                        &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_cstart, &d_cedges, &d_cpt,
+                        &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_pe, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
                         &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
                         &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_chist, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
@@ -2999,6 +3015,7 @@ struct BundleAdjuster {
                         std::make_pair(&d_pstart, (size_t)(Pm + 1) * 4), std::make_pair(&d_cstart, (size_t)(Cm + 1) * 4),
                         std::make_pair(&d_pedges, (size_t)Em * 4), std::make_pair(&d_cedges, (size_t)Em * 4),
                         std::make_pair(&d_cpt, (size_t)Em * 4), std::make_pair(&d_epos, (size_t)Em * 4),
+                        std::make_pair(&d_pe, (size_t)Em * 16),
                         std::make_pair(&d_active, (size_t)Em), std::make_pair(&d_ikeys, (size_t)Em * 8),
                         std::make_pair(&d_ivals, (size_t)Em * 4), std::make_pair(&d_isum, nsum * 4)})
             if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
@@ -3047,6 +3064,9 @@ struct BundleAdjuster {
             launch("ba.init_camcsr", init_camcsr, dim3(ge), dim3(256), 0, st, E, C, nbm, (const unsigned*)k1, (const int*)v0,
                    (const int*)d_ept.as<int>(), (const int*)d_camh.as<int>(), (const int*)d_ptfree.as<int>(),
                    d_cedges.as<int>(), d_cpt.as<int>(), d_epos.as<int>(), sum, s_rc);
+            launch("ba.init_pcache", init_pcache, dim3(ge), dim3(256), 0, st, E, P, (const int*)d_pstart.as<int>(),
+                   (const int*)d_pedges.as<int>(), (const int*)d_ecam.as<int>(), (const int*)d_camh.as<int>(),
+                   (const int*)d_epos.as<int>(), d_pe.as<int4>());
         }
         const bool bitmap_fits = PW <= SC_LDS_WORDS && nbm > 0 && P > 0;
         if (bitmap_fits) {

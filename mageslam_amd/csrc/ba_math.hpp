@@ -302,6 +302,8 @@ struct Problem {
     const int* cedges;            // edges by camera, sorted by point id, filtered by `active`
     const int* cpt;               // point id of each cedges entry (binary search key)
     const int* epos;              // E: position of the edge in the camera CSR (-1: not listed)
+    const int4* pe;               // per point-CSR entry: (edge, camera, camera block or -1, camera-CSR
+                                  // position) in one 16-byte load (init_pcache)
     int ecsr;                     // camera-CSR entries = row stride of the Hpl / Z component arrays
     double huber;
 };
