@@ -1,4 +1,4 @@
 set -eo pipefail
 export TMPDIR=/tmp
 # scratch GPU step (development): BA variant timings
-timeout -k 10 300 python3 tools/ablate_ba.py libs head,e2,e4,e6,head,e2,e4,e6 > gpurun_out/ab_ba.log 2>&1
+timeout -k 10 300 python3 tools/ablate_ba.py libs head,pre,head,pre,head,pre > gpurun_out/ab_ba.log 2>&1
