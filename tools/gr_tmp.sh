@@ -1,4 +1,4 @@
 set -eo pipefail
 export TMPDIR=/tmp
-# final GPU check: the whole GPU suite
-timeout -k 10 900 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests > gpurun_out/pytest_all.log 2>&1
+# scratch GPU step (development): BA variant timings
+timeout -k 10 300 python3 tools/ablate_ba.py libs head,w4,head,w4,head,w4 > gpurun_out/ab_ba.log 2>&1
