@@ -37,6 +37,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -72,6 +73,17 @@ struct OutlierCtl {
     int fail;
     uint32_t count[2];
     uint32_t ticket;
+};
+
+// The LM decision of a trial as reduce3 takes it on the device (OptimizationAlgorithmLevenberg::
+// solve: rho = (chi_current - chi_trial) / (scale + 1e-3), accept when rho > 0 and chi_trial is
+// finite; lambda *= max(1/3, min(2/3, 1 - (2 rho - 1)^3)) on accept, lambda *= ni on reject), so a
+// linearisation of the next state can be queued before the host has read the trial back.  The
+// host takes the same decision from the same doubles and adopts lam_next.
+struct LmDev {
+    double lam_next;
+    int cur_next;
+    int accept;
 };
 
 template <int N>
@@ -242,8 +254,10 @@ __device__ __forceinline__ void point_group(const Problem& pb, const State& s, i
             const double t[3] = {s.t[3 * c], s.t[3 * c + 1], s.t[3 * c + 2]};
             edge_eval_at(pb, e, c, q, t, Xp3, ev, xc, rho0, rho1);
         }
-        o.err[2 * e] = ev[0];
-        o.err[2 * e + 1] = ev[1];
+        if (o.err) {  // (a speculative linearisation after a rejected trial keeps the trial's errors)
+            o.err[2 * e] = ev[0];
+            o.err[2 * e + 1] = ev[1];
+        }
         chi += rho0;
         if (!LIN) {
             if (sp) {
@@ -510,8 +524,16 @@ __device__ __forceinline__ void cam_chunk(const Problem& pb, const State& s, con
 // added in chunk order by schur_finish / linearize_finish).
 __global__ __launch_bounds__(BA_THREADS) void linearize_kernel(Problem pb, State s, PointOut o, double lambda, int with_g,
                                                                int npb, const int* __restrict__ cam_of_block,
-                                                               double* __restrict__ campart)
+                                                               double* __restrict__ campart, State s1,
+                                                               const LmDev* __restrict__ lm)
 {
+    if (lm) {
+        // speculative: the state and lambda of the decision reduce3 just took (s = buffer 0, s1 =
+        // buffer 1); after a rejection the state is unchanged and the trial's errors stay
+        if (lm->cur_next == 1) s = s1;
+        lambda = lm->lam_next;
+        if (!lm->accept) o.err = nullptr;
+    }
     if ((int)blockIdx.x >= npb) {
         cam_chunk(pb, s, cam_of_block, campart, blockIdx.x - npb);
         return;
@@ -613,7 +635,9 @@ __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, in
                                                 const double* __restrict__ c, int nc, double* __restrict__ outc,
                                                 const double* __restrict__ opart, int oblocks, int ns,
                                                 OutlierCtl* __restrict__ ctl, LiveCtl* __restrict__ live,
-                                                unsigned* __restrict__ seq_out, unsigned seq)
+                                                unsigned* __restrict__ seq_out, unsigned seq,
+                                                LmDev* __restrict__ lm, double lam, double ni, int cur,
+                                                double cur_chi, double* __restrict__ lam_out)
 {
     // the seven sums in one pass (strided per thread, fixed order), one reduce-scatter per wave,
     // then the 16 wave partials in order; the max separately (only linearize_finish's callers
@@ -683,6 +707,28 @@ __global__ __launch_bounds__(1024) void reduce3(const double* __restrict__ a, in
         for (int k = 0; k < ns; k++) {
             ctl->osum[k][0] = red[0][3 + 2 * k];
             ctl->osum[k][1] = red[0][4 + 2 * k];
+        }
+        if (lm) {
+            // the trial's LM decision (see LmDev); the chi of the current state is the
+            // linearisation's (reduced here) unless the host passed it
+            const double tempChi = live->fail ? __DBL_MAX__ : red[0][0];
+            const double currentChi = isnan(cur_chi) ? red[0][2] : cur_chi;
+            double rho = currentChi - tempChi;
+            const double scale = red[0][1] + 1e-3;
+            rho /= scale;
+            const bool acc = rho > 0 && isfinite(tempChi);
+            double ln;
+            if (acc) {
+                double alpha = 1. - pow(2 * rho - 1, 3.0);
+                alpha = fmin(alpha, 2. / 3.);
+                ln = lam * fmax(1. / 3., alpha);
+            } else {
+                ln = lam * ni;
+            }
+            lm->lam_next = ln;
+            lm->cur_next = acc ? 1 - cur : cur;
+            lm->accept = acc ? 1 : 0;
+            lam_out[0] = ln;
         }
         // the trial's counters to the host block, and zero for the next trial
         ctl->fail = live->fail;
@@ -2594,7 +2640,7 @@ struct BundleAdjuster {
     // Control block read back at every host decision (one pinned copy per synchronisation):
     // doubles [0,3) linearisation chi2 / max diag, [3,6) trial, then the outlier pass's
     // OutlierCtl (sums, Cholesky failure flag, counts, ticket).
-    static constexpr int CTL_DOUBLES = 16, CTL_OUTLIER = 6, CTL_SCRATCH = 12, CTL_SEQ = 15;
+    static constexpr int CTL_DOUBLES = 16, CTL_OUTLIER = 6, CTL_SCRATCH = 12, CTL_LMNEXT = 13, CTL_SEQ = 15;
     static_assert(CTL_OUTLIER * 8 + sizeof(OutlierCtl) <= CTL_SCRATCH * 8, "control block layout");
     // The control block is host memory the kernels write directly (pinned, coherent, mapped):
     // h_ctl on the host, h_ctl_dev in kernels; a trial's results need only the stream sync.
@@ -2634,7 +2680,7 @@ struct BundleAdjuster {
     // device buffers
     DeviceBuffer d_q[2], d_t[2], d_p[2], d_camk, d_camh, d_ptfree, d_uv, d_ecam, d_ept, d_info,
         d_pstart, d_pedges, d_pe, d_cstart, d_cedges, d_cpt, d_active, d_err, d_Hll, d_bl, d_Hpl, d_Hpp,
-        d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_osum, d_camblk,
+        d_bp, d_S, d_rhs, d_x, d_chi, d_maxd, d_scale, d_red, d_lm, d_osum, d_camblk,
         d_ptcnt, d_plist, d_pcnt, d_skeys, d_svals, d_kb, d_chist, d_kdst, d_rblk, d_sbits, d_srank, d_Z, d_campart, d_teth, d_tout, d_ptlist, d_sentries, d_spairs, d_schunks, d_spart,
         d_sfinish, d_epos, d_chi_lin, d_livebuf, d_removed, d_camflag, d_ikeys, d_ivals, d_isum, d_iacc, d_ctab, d_csort_tmp;
     bool iacc_clean = false;  // d_iacc is all zero (see initialize())
@@ -2684,7 +2730,7 @@ struct BundleAdjuster {
         for (auto* b : {&d_q[0], &d_q[1], &d_t[0], &d_t[1], &d_p[0], &d_p[1], &d_camk, &d_camh, &d_ptfree,
                         &d_uv, &d_ecam, &d_ept, &d_info, &d_pstart, &d_pedges, &d_pe, &d_cstart, &d_cedges, &d_cpt,
                         &d_active, &d_err, &d_Hll, &d_bl, &d_Hpl, &d_Hpp, &d_bp, &d_S, &d_rhs,
-                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_osum, &d_camblk,
+                        &d_x, &d_chi, &d_maxd, &d_scale, &d_red, &d_lm, &d_osum, &d_camblk,
                         &d_ptcnt, &d_plist, &d_pcnt, &d_skeys, &d_svals, &d_kb, &d_chist, &d_kdst, &d_rblk, &d_sbits, &d_srank, &d_Z, &d_campart, &d_teth, &d_tout, &d_ptlist, &d_sentries, &d_spairs,
                         &d_schunks, &d_spart, &d_sfinish, &d_epos, &d_chi_lin, &d_livebuf, &d_removed, &d_camflag,
                         &d_ikeys, &d_ivals, &d_isum, &d_iacc, &d_ctab, &d_csort_tmp})
@@ -3125,7 +3171,7 @@ struct BundleAdjuster {
                             std::make_pair(&d_chi_lin, (Pm + teth.size()) * 8),
                             std::make_pair(&d_tout, std::max<size_t>(teth.size(), 1) * TETHER_OUT * 8),
                             std::make_pair(&d_maxd, (Pm + Cm) * 8), std::make_pair(&d_scale, (Pm + Cm) * 8),
-                            std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8),
+                            std::make_pair(&d_red, (size_t)CTL_DOUBLES * 8), std::make_pair(&d_lm, sizeof(LmDev)),
                             std::make_pair(&d_osum, ((size_t)std::max<int>((int)(Em / BA_THREADS), group_grid((int)Pm)) + 2) * 4 * 8)})
                 if ((r = pr.first->reserve(pr.second)) != MAGE_OK) return r;
             if ((r = d_livebuf.reserve(sizeof(LiveCtl))) != MAGE_OK) return r;
@@ -3389,7 +3435,7 @@ struct BundleAdjuster {
         if (npb + ncb > 0)
             launch("ba.linearize", linearize_kernel, dim3(npb + ncb), dim3(BA_THREADS), 0, st, pb, state(cur),
                    point_out(d_chi_lin.as<double>()), with_g ? lam_for_g : 0.0, with_g ? 1 : 0, npb,
-                   (const int*)d_camblk.as<int>(), d_campart.as<double>());
+                   (const int*)d_camblk.as<int>(), d_campart.as<double>(), state(1 - cur), (const LmDev*)nullptr);
         g_lambda = with_g ? lam_for_g : std::numeric_limits<double>::quiet_NaN();
         const int nt = (int)teth.size();
         if (nt > 0)
@@ -3406,7 +3452,16 @@ struct BundleAdjuster {
 
     // One trial: solve with lambda, build the trial state in the other buffer, evaluate it.
     // Reads back red[0..5] = {chi(current), -, -, chi(trial), scale, -} and the fail flag.
-    mage_status trial(double lam, bool* ok, double red[6], bool speculate)
+    // Speculative linearisation (MAGE_BA_SPEC_LIN, default on): queued behind each trial's reduce3,
+    // on the state and lambda of the decision reduce3 takes on the device, so the next trial (after
+    // a rejection) or the next call (after an acceptance) starts without the host round trip.
+    bool spec_lin = []() {
+        const char* v = std::getenv("MAGE_BA_SPEC_LIN");
+        return !(v && v[0] == '0');
+    }();
+    bool spec_lin_queued = false;  // set by trial(): the host adopts the device's lambda
+    bool last_call_removed = false;  // the previous StepBundleAdjustment removed outliers
+    mage_status trial(double lam, bool* ok, double red[6], bool speculate, double cur_chi = std::numeric_limits<double>::quiet_NaN())
     {
         Problem pb = problem();
         double* xp = d_x.as<double>();
@@ -3453,10 +3508,20 @@ struct BundleAdjuster {
         if (nt > 0)
             launch("ba.tether_eval", tether_eval, dim3((nt + 63) / 64), dim3(64), 0, st, (const Tether*)d_teth.as<Tether>(),
                    nt, state(1 - cur), 0, d_chi.as<double>() + P, d_tout.as<double>());
+        // (not on a call's last step when the previous call removed outliers: a removal invalidates
+        // the linearisation, and the reference's schedule removes some on most calls)
+        spec_lin_queued = spec_lin && !(speculate && last_call_removed) && nt == 0 && n > 0 && n_entries > 0 &&
+                          !points_fixed && npb + nb_free * CAM_CHUNKS > 0;
+        LmDev* lmd = spec_lin_queued ? d_lm.as<LmDev>() : nullptr;
         launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)d_chi.as<double>(), P + nt,
                (const double*)d_scale.as<double>(), P + C, (const double*)d_maxd.as<double>(), 0, h_ctl_dev + 3,
                (const double*)d_chi_lin.as<double>(), P + nt, h_ctl_dev + CTL_SCRATCH,
-               (const double*)d_osum.as<double>(), npb, spec ? 2 : 0, d_octl(), d_live(), seq_dev(), ++seq_counter);
+               (const double*)d_osum.as<double>(), npb, spec ? 2 : 0, d_octl(), d_live(), seq_dev(), ++seq_counter,
+               lmd, lam, (double)ni, cur, cur_chi, h_ctl_dev + CTL_LMNEXT);
+        if (spec_lin_queued)
+            launch("ba.linearize", linearize_kernel, dim3(npb + nb_free * CAM_CHUNKS), dim3(BA_THREADS), 0, st, pb,
+                   state(0), point_out(d_chi_lin.as<double>()), 0.0, 1, npb, (const int*)d_camblk.as<int>(),
+                   d_campart.as<double>(), state(1), (const LmDev*)lmd);
         MAGE_HIP(hipGetLastError());
         mage_status r = wait_seq(seq_counter);
         if (r != MAGE_OK) return r;
@@ -3494,7 +3559,12 @@ struct BundleAdjuster {
         do {
             bool ok2 = true;
             double red[6];
-            if ((r = trial(lambda, &ok2, red, speculate)) != MAGE_OK) return r;
+            if ((r = trial(lambda, &ok2, red, speculate, haveChi ? currentChi : std::numeric_limits<double>::quiet_NaN())) !=
+                MAGE_OK)
+                return r;
+            // the device's lambda for the next step when a speculative linearisation was queued (same
+            // decision from the same doubles; its pow may differ from the host's in the last bit)
+            const double lam_dev = spec_lin_queued ? h_ctl[CTL_LMNEXT] : 0.0;
             *spec_valid = speculate ? 1 : -1;  // rejected: the current state's result (list 1)
             if (!haveChi) {
                 currentChi = red[0];
@@ -3520,6 +3590,17 @@ struct BundleAdjuster {
                 lambda *= ni;
                 ni *= 2;
                 stats.rejected_trials++;  // pop: the current buffer is unchanged
+            }
+            if (spec_lin_queued) {
+                // the queued linearisation is of this state and lambda: the next trial's G (no
+                // edge_schur) or the next call's eager linearisation
+                lambda = lam_dev;
+                eager = true;
+                eager_init = false;
+                eager_huber = huber;
+                eager_lambda = lambda;
+                eager_cur = cur;
+                g_lambda = lambda;
             }
             qmax++;
         } while (rho < 0 && qmax < 10);
@@ -3596,13 +3677,14 @@ struct BundleAdjuster {
             launch("ba.reduce", reduce3, dim3(1), dim3(1024), 0, st, (const double*)nullptr, 0, (const double*)nullptr, 0,
                    (const double*)nullptr, 0, h_ctl_dev + CTL_SCRATCH, (const double*)nullptr, 0,
                    h_ctl_dev + CTL_SCRATCH, (const double*)d_osum.as<double>(), outlier_blocks(), 1, d_octl(), d_live(),
-                   seq_dev(), ++seq_counter);
+                   seq_dev(), ++seq_counter, (LmDev*)nullptr, 0.0, 0.0, 0, 0.0, (double*)nullptr);
             MAGE_HIP(hipGetLastError());
             if ((r = read_ctl()) != MAGE_OK) return r;
             k = 0;
         }
         const double h[2] = {h_octl().osum[k][0], h_octl().osum[k][1]};
         const uint32_t no = h_octl().count[k];
+        last_call_removed = no > 0;
         if (no > 0) {
             // the pass wrote the list into mapped host memory before the completion word
             const uint32_t* h_list = h_olist.host<uint32_t>() + (size_t)k * E;
@@ -3619,6 +3701,7 @@ struct BundleAdjuster {
             for (int c = 0; c < C; c++)
                 if (camh[c] >= 0 && camcnt[c] == 0 && cam_tethers[c] == 0) dirty = true;
             iteration = 0;  // removeEdge dirties the optimizer: next Step re-initialises (lambda init)
+            eager = false;  // a speculative linearisation ran before the removal
         }
         *nOut = std::min(no, cap);
         *meanSq = (float)(h[0] / h[1]);
