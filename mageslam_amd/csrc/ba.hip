@@ -3562,8 +3562,9 @@ struct BundleAdjuster {
             if ((r = trial(lambda, &ok2, red, speculate, haveChi ? currentChi : std::numeric_limits<double>::quiet_NaN())) !=
                 MAGE_OK)
                 return r;
-            // the device's lambda for the next step when a speculative linearisation was queued (same
-            // decision from the same doubles; its pow may differ from the host's in the last bit)
+            // the device's lambda for the next step when a speculative linearisation was queued (the
+            // same decision from the same doubles; its pow may differ from the host's in the last bit,
+            // and then the queued linearisation is not used)
             const double lam_dev = spec_lin_queued ? h_ctl[CTL_LMNEXT] : 0.0;
             *spec_valid = speculate ? 1 : -1;  // rejected: the current state's result (list 1)
             if (!haveChi) {
@@ -3592,15 +3593,22 @@ struct BundleAdjuster {
                 stats.rejected_trials++;  // pop: the current buffer is unchanged
             }
             if (spec_lin_queued) {
-                // the queued linearisation is of this state and lambda: the next trial's G (no
-                // edge_schur) or the next call's eager linearisation
-                lambda = lam_dev;
-                eager = true;
-                eager_init = false;
-                eager_huber = huber;
-                eager_lambda = lambda;
-                eager_cur = cur;
-                g_lambda = lambda;
+                if (lam_dev == lambda) {
+                    // the queued linearisation is of this state and lambda: the next trial's G (no
+                    // edge_schur) or the next call's eager linearisation
+                    eager = true;
+                    eager_init = false;
+                    eager_huber = huber;
+                    eager_lambda = lambda;
+                    eager_cur = cur;
+                    g_lambda = lambda;
+                } else {
+                    // lambda differs in the last bit: the host's (g2o's) lambda holds; the queued
+                    // linearisation's G is for the other value (its H and records are still this
+                    // state's, so only G is redone, by edge_schur, for the next trial)
+                    eager = false;
+                    g_lambda = lam_dev;
+                }
             }
             qmax++;
         } while (rho < 0 && qmax < 10);

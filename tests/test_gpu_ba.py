@@ -70,6 +70,25 @@ def test_c3_graph(gpu):
     compare(gb, ob)
 
 
+@pytest.mark.parametrize("spec", ["1", "0"])
+def test_rejected_trials(gpu, monkeypatch, spec):
+    """Small lambda + noisy observations: many LM trials are rejected (pop, lambda *= ni), which
+    exercises the device-side decision and the speculative linearisation after a rejection (the
+    unchanged state with the new lambda, the trial's errors kept) against the oracle; spec = 0 runs
+    the host-only path (MAGE_BA_SPEC_LIN=0)."""
+    monkeypatch.setenv("MAGE_BA_SPEC_LIN", spec)
+    # (seed 5, 8 px noise: chi2 stays far above roundoff, so every accept/reject is decisive; a graph
+    # that converges to chi2 ~ 1e-25 decides its late trials on roundoff and the counts differ)
+    g = synth.ba_graph(cameras=12, points=300, obs_per_point=8, fixed_cameras=3, seed=5, noise_px=8.0,
+                       outlier_frac=0.05)
+    gb, ob = run_pair(g, 5, lam=1e-6)
+    compare(gb, ob)
+    sg, so = gb.stats(), ob.stats()
+    assert sg["iterations"] == so["iterations"] and sg["trials"] == so["trials"]
+    assert so["trials"] > so["iterations"]  # rejections happened
+    assert abs(gb.GetCurrentLambda() - ob.get_lambda()) <= 1e-3 * abs(ob.get_lambda())
+
+
 def test_multi_step_and_user_lambda(gpu):
     g = synth.ba_graph(cameras=20, points=1500, obs_per_point=10, fixed_cameras=5, seed=7)
     gb, ob = run_pair(g, 3, nsteps=3, lam=0.01)

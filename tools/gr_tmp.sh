@@ -1,4 +1,4 @@
 set -eo pipefail
 export TMPDIR=/tmp
-# final GPU check: the whole GPU suite
-timeout -k 10 900 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests > gpurun_out/pytest_all.log 2>&1
+# scratch GPU step (development): BA parity incl. rejected trials
+timeout -k 10 400 python3 -u -m pytest -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_ba.py > gpurun_out/pytest.log 2>&1
